@@ -1,0 +1,29 @@
+"""Protocol messages and user I/O records (same names, fields and field order as the
+reference's `AllreduceMessage.scala:7-20` and `DataWrapper.scala:3-7`).
+
+All classes are native (C++) types so that messages cross the actor runtime without
+Python overhead; payload fields accept any float sequence / numpy array (host) or a
+torch tensor on the GPU (device payloads, see `parallel.device_plane`).
+"""
+from ._native import C
+
+InitWorkers = C.InitWorkers
+StartAllreduce = C.StartAllreduce
+ScatterBlock = C.ScatterBlock
+ReduceBlock = C.ReduceBlock
+CompleteAllreduce = C.CompleteAllreduce
+AllReduceInputRequest = C.AllReduceInputRequest
+AllReduceInput = C.AllReduceInput
+AllReduceOutput = C.AllReduceOutput
+MemberUp = C.MemberUp
+Terminated = C.Terminated
+AllreduceFinished = C.AllreduceFinished
+PoisonPill = C.PoisonPill
+TextMessage = C.TextMessage
+ActorRef = C.ActorRef
+
+__all__ = [
+    "InitWorkers", "StartAllreduce", "ScatterBlock", "ReduceBlock", "CompleteAllreduce",
+    "AllReduceInputRequest", "AllReduceInput", "AllReduceOutput", "MemberUp", "Terminated",
+    "AllreduceFinished", "PoisonPill", "TextMessage", "ActorRef",
+]

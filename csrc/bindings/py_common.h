@@ -1,0 +1,41 @@
+// Shared helpers for the Python bindings: payload <-> numpy conversion, message
+// <-> Python object conversion, and GIL-safe holders for Python callables.
+#pragma once
+
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../core/protocol.h"
+
+namespace py = pybind11;
+
+namespace mxar {
+
+// A Python callable that may be destroyed from a non-Python thread.
+struct PyCallable {
+  py::object fn;
+  explicit PyCallable(py::object f) : fn(std::move(f)) {}
+  ~PyCallable() {
+    if (!Py_IsInitialized()) {
+      fn.release();  // interpreter gone: leak rather than crash
+      return;
+    }
+    py::gil_scoped_acquire g;
+    fn = py::object();
+  }
+};
+
+Payload payload_from_py(const py::handle& obj);
+py::object payload_to_py(const Payload& p);
+py::object message_to_py(const Message& m);
+Message message_from_py(const py::handle& obj);
+
+// Hook so the HIP part of the module can turn device payloads into torch tensors
+// (DLPack) and accept torch CUDA tensors as payloads.
+using DevicePayloadToPy = py::object (*)(const Payload&);
+using PyToDevicePayload = Payload (*)(const py::handle&);  // returns nullptr if not a device tensor
+void register_device_payload_hooks(DevicePayloadToPy to_py, PyToDevicePayload from_py);
+
+}  // namespace mxar

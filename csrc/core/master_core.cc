@@ -1,0 +1,109 @@
+#include "master_core.h"
+
+#include <algorithm>
+
+#include "log.h"
+
+namespace mxar {
+
+// MemberUp -> register (AllreduceMaster.scala:38-48, 70-82)
+void MasterCore::on_member_up(int handle) {
+  for (auto& [id, h] : workers_)
+    if (h == handle) return;  // already registered
+  // id = workers.size in the reference (:75-76); after a removal that id can collide
+  // with a live worker, so take the first free id instead.
+  int id = 0;
+  while (workers_.count(id)) ++id;
+  workers_[id] = handle;
+  MXAR_LOG(INFO, "master", "----current size = " << workers_.size());
+  if (static_cast<int>(workers_.size()) >= f32_threshold_count(p_.thAllreduce, p_.totalWorkers)) {
+    MXAR_LOG(INFO, "master", "----" << workers_.size() << " (out of " << p_.totalWorkers << ") workers are up");
+    init_workers();
+    round_ = 0;
+    finished_ = false;
+    start_allreduce();
+  }
+}
+
+// Terminated (AllreduceMaster.scala:50-56)
+void MasterCore::on_terminated(int handle) {
+  for (auto it = workers_.begin(); it != workers_.end(); ++it) {
+    if (it->second == handle) {
+      MXAR_LOG(INFO, "master", "----worker " << it->first << " is terminated, removing it from the set");
+      workers_.erase(it);
+      stats_.removed++;
+      break;
+    }
+  }
+  // With liveBarrier the round may now be complete.
+  if (p_.liveBarrier && round_ >= 0 && !finished_ &&
+      static_cast<float>(numComplete_) >= barrier_base() * p_.thAllreduce && numComplete_ > 0) {
+    on_complete(-1, -1);
+  }
+}
+
+float MasterCore::barrier_base() const {
+  if (p_.liveBarrier) return static_cast<float>(std::min<int>(p_.totalWorkers, static_cast<int>(workers_.size())));
+  return static_cast<float>(p_.totalWorkers);
+}
+
+// CompleteAllreduce (AllreduceMaster.scala:58-67)
+void MasterCore::on_complete(int srcId, int round) {
+  if (srcId >= 0) {
+    MXAR_LOG(INFO, "master", "----Node " << srcId << " completes allreduce round " << round);
+    stats_.completes++;
+    if (round != round_) {
+      stats_.stale_completes++;
+      return;
+    }
+    numComplete_ += 1;
+  }
+  // numComplete >= totalWorkers * thAllreduce : float compare, not truncated (:62)
+  volatile float need = barrier_base() * p_.thAllreduce;
+  if (static_cast<float>(numComplete_) >= need) {
+    if (round_ < p_.maxRound) {
+      MXAR_LOG(INFO, "master", "----" << numComplete_ << " (out of " << p_.totalWorkers
+                                      << ") workers complete round " << round_);
+      round_ += 1;
+      start_allreduce();
+    } else if (!finished_) {
+      finished_ = true;
+      MXAR_LOG(INFO, "master", "----All " << (p_.maxRound + 1) << " rounds complete");
+      fx_->finished(p_.maxRound + 1);
+    }
+  }
+}
+
+// init_workers (AllreduceMaster.scala:84-89)
+void MasterCore::init_workers() {
+  // re-number densely 0..P-1 in id order
+  std::map<int, int> dense;
+  int k = 0;
+  for (auto& [id, h] : workers_) dense[k++] = h;
+  workers_.swap(dense);
+  ++epoch_;
+  stats_.inits++;
+  for (auto& [idx, h] : workers_) {
+    MXAR_LOG(INFO, "master", "----Init worker " << idx << " (epoch " << epoch_ << ")");
+    InitParams p;
+    p.destId = idx;
+    p.numPeers = static_cast<int>(workers_.size());
+    p.thReduce = p_.thReduce;
+    p.thComplete = p_.thComplete;
+    p.maxLag = p_.maxLag;
+    p.dataSize = p_.dataSize;
+    p.maxChunkSize = p_.maxChunkSize;
+    p.epoch = epoch_;
+    fx_->send_init(h, p, workers_);
+  }
+}
+
+// startAllreduce (AllreduceMaster.scala:91-97)
+void MasterCore::start_allreduce() {
+  MXAR_LOG(INFO, "master", "----Start allreduce round " << round_);
+  numComplete_ = 0;
+  stats_.rounds_started++;
+  for (auto& [idx, h] : workers_) fx_->send_start(h, round_);
+}
+
+}  // namespace mxar

@@ -1,0 +1,80 @@
+// Coordinator state machine: membership -> ids, InitWorkers broadcast, round barrier.
+//
+//   reference: src/main/scala/sample/cluster/allreduce/AllreduceMaster.scala:15-98
+//
+// Kept: init trigger at (totalWorkers * thAllreduce).toInt registered workers (truncated,
+// :42) and advance when numComplete >= totalWorkers * thAllreduce (float compare, NOT
+// truncated, :62) - the asymmetry is protocol-visible; rounds 0..maxRound
+// run (maxRound + 1 rounds); every MemberUp past the threshold re-initialises everyone
+// at round 0 (now epoch-tagged).
+// Fixed: all state changes happen on the coordinator's own turn; ids are
+// re-numbered densely 0..P-1 at every (re-)init so removals cannot collide (Q3);
+// optional barrier on live membership (Q4, `liveBarrier`); a finished notification
+// after maxRound (Q15).
+#pragma once
+
+#include <functional>
+#include <map>
+#include <vector>
+
+#include "worker_core.h"
+
+namespace mxar {
+
+struct MasterParams {
+  int totalWorkers = 2;
+  float thAllreduce = 1.f;
+  float thReduce = 0.9f;
+  float thComplete = 0.8f;
+  int maxLag = 1;
+  int dataSize = 10;
+  int maxRound = 100;
+  int maxChunkSize = 2;
+  bool liveBarrier = false;
+};
+
+class MasterEffects {
+ public:
+  virtual ~MasterEffects() = default;
+  // `ids` maps worker id -> handle for the whole membership (the InitWorkers.workers map).
+  virtual void send_init(int handle, const InitParams& p, const std::map<int, int>& ids) = 0;
+  virtual void send_start(int handle, int round) = 0;
+  virtual void finished(int rounds) = 0;
+};
+
+struct MasterStats {
+  uint64_t inits = 0, rounds_started = 0, completes = 0, stale_completes = 0, removed = 0;
+};
+
+class MasterCore {
+ public:
+  MasterCore(MasterEffects* fx, MasterParams p) : fx_(fx), p_(p) {}
+
+  void on_member_up(int handle);
+  void on_terminated(int handle);
+  void on_complete(int srcId, int round);
+
+  int round() const { return round_; }
+  int num_complete() const { return numComplete_; }
+  int64_t epoch() const { return epoch_; }
+  bool finished() const { return finished_; }
+  const std::map<int, int>& workers() const { return workers_; }  // id -> handle
+  const MasterParams& params() const { return p_; }
+  const MasterStats& stats() const { return stats_; }
+
+ private:
+  void init_workers();
+  void start_allreduce();
+  float barrier_base() const;
+
+  MasterEffects* fx_;
+  MasterParams p_;
+  std::map<int, int> workers_;  // id -> handle (AllreduceMaster.scala:26)
+  int round_ = -1;              // :29
+  int numComplete_ = 0;         // :30
+  int64_t epoch_ = 0;
+  bool finished_ = false;
+  MasterStats stats_;
+};
+
+}  // namespace mxar

@@ -1,0 +1,149 @@
+// Wire protocol of the threshold allreduce: the five actor messages and the three
+// user-I/O records of the reference, with identical fields and field order.
+//
+//   reference: src/main/scala/sample/cluster/allreduce/AllreduceMessage.scala:7-20
+//              src/main/scala/sample/cluster/allreduce/DataWrapper.scala:3-7
+//
+// Payloads (`value`, `data`) are reference-counted immutable float32 chunks. A payload
+// is host memory or device (HBM) memory; the protocol cores never touch the bytes
+// themselves, they hand payloads to a DataPlane (host loops or HIP kernels).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <string>
+#include <variant>
+#include <vector>
+
+namespace mxar {
+
+// ---------------------------------------------------------------------------------
+// Payload storage
+// ---------------------------------------------------------------------------------
+class PayloadStorage {
+ public:
+  virtual ~PayloadStorage() = default;
+  virtual bool on_device() const = 0;
+  // Pointer to the first float (host pointer, or device pointer when on_device()).
+  virtual const float* data() const = 0;
+  virtual size_t size() const = 0;
+  // Blocking copy to host (device payloads synchronise on their ready event).
+  virtual std::vector<float> to_host() const = 0;
+};
+using Payload = std::shared_ptr<const PayloadStorage>;
+
+class HostPayload final : public PayloadStorage {
+ public:
+  explicit HostPayload(std::vector<float> v) : v_(std::move(v)) {}
+  bool on_device() const override { return false; }
+  const float* data() const override { return v_.data(); }
+  size_t size() const override { return v_.size(); }
+  std::vector<float> to_host() const override { return v_; }
+  const std::vector<float>& vec() const { return v_; }
+
+ private:
+  std::vector<float> v_;
+};
+
+inline Payload make_host_payload(std::vector<float> v) {
+  return std::make_shared<HostPayload>(std::move(v));
+}
+inline size_t payload_size(const Payload& p) { return p ? p->size() : 0; }
+
+// ---------------------------------------------------------------------------------
+// Actor references (opaque to the protocol cores; implemented by the runtime)
+// ---------------------------------------------------------------------------------
+class ActorRefBase;
+using ActorRef = std::shared_ptr<ActorRefBase>;
+
+// ---------------------------------------------------------------------------------
+// Messages (AllreduceMessage.scala)
+// ---------------------------------------------------------------------------------
+struct InitWorkers {  // AllreduceMessage.scala:7-16
+  std::map<int, ActorRef> workers;
+  ActorRef master;
+  int destId = 0;
+  float thReduce = 1.f;
+  float thComplete = 1.f;
+  int maxLag = 0;
+  int dataSize = 0;
+  int maxChunkSize = 1024;
+  // Extension (not in the reference): membership epoch, bumped by the master on every
+  // (re-)initialisation so late messages of an older epoch can be told apart.
+  int64_t epoch = 0;
+};
+
+struct StartAllreduce {  // AllreduceMessage.scala:17
+  int round = 0;
+};
+
+struct ScatterBlock {  // AllreduceMessage.scala:18
+  Payload value;
+  int srcId = 0;
+  int destId = 0;
+  int chunkId = 0;
+  int round = 0;
+};
+
+struct ReduceBlock {  // AllreduceMessage.scala:19
+  Payload value;
+  int srcId = 0;
+  int destId = 0;
+  int chunkId = 0;
+  int round = 0;
+  int count = 0;
+};
+
+struct CompleteAllreduce {  // AllreduceMessage.scala:20
+  int srcId = 0;
+  int round = 0;
+};
+
+// ---------------------------------------------------------------------------------
+// User I/O records (DataWrapper.scala)
+// ---------------------------------------------------------------------------------
+struct AllReduceInputRequest {  // DataWrapper.scala:3
+  int iteration = 0;
+};
+struct AllReduceInput {  // DataWrapper.scala:5
+  Payload data;
+};
+struct AllReduceOutput {  // DataWrapper.scala:7
+  Payload data;
+  // The reference always reports Array(0) (AllreduceWorker.scala:191).
+  // We report the real per-chunk contribution counts of every block, concatenated in
+  // block order (a superset: element 0 is still a valid count).
+  std::vector<int> count;
+  int iteration = 0;
+};
+
+// ---------------------------------------------------------------------------------
+// Runtime / cluster control messages (Akka library messages in the reference)
+// ---------------------------------------------------------------------------------
+struct MemberUp {  // akka.cluster.ClusterEvent.MemberUp (AllreduceMaster.scala:38)
+  ActorRef ref;  // the member's "/user/worker" actor, already resolved
+  std::string role;
+  std::string address;
+};
+struct Terminated {  // akka.actor.Terminated (AllreduceMaster.scala:50)
+  ActorRef ref;
+};
+// Emitted by the master when maxRound has completed (the reference idles).
+struct AllreduceFinished {
+  int rounds = 0;
+};
+struct PoisonPill {};
+// Generic string message for tests and for the TCP control plane's tooling.
+struct TextMessage {
+  std::string text;
+};
+
+using Message = std::variant<InitWorkers, StartAllreduce, ScatterBlock, ReduceBlock,
+                             CompleteAllreduce, MemberUp, Terminated, AllreduceFinished,
+                             PoisonPill, TextMessage>;
+
+const char* message_name(const Message& m);
+
+}  // namespace mxar

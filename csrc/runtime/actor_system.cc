@@ -1,0 +1,474 @@
+#include "actor_system.h"
+
+#include <algorithm>
+
+#include "../core/log.h"
+
+namespace mxar {
+
+namespace {
+std::atomic<uint64_t> g_uid{1};
+}
+
+ActorRefBase::ActorRefBase() : uid_(g_uid.fetch_add(1)) {}
+
+const char* message_name(const Message& m) {
+  static const char* names[] = {"InitWorkers",    "StartAllreduce", "ScatterBlock",
+                                "ReduceBlock",    "CompleteAllreduce", "MemberUp",
+                                "Terminated",     "AllreduceFinished", "PoisonPill",
+                                "TextMessage"};
+  return names[m.index()];
+}
+
+// ------------------------------------------------------------------------ context
+ActorRef ActorContext::self() const { return cell_->ref(); }
+
+void ActorContext::watch(const ActorRef& ref) {
+  if (!ref) return;
+  auto* local = dynamic_cast<LocalActorRef*>(ref.get());
+  if (!local) return;  // remote refs: the cluster layer's failure detector reports them
+  auto c = local->cell();
+  ActorRef me = self();
+  if (!c || c->stopped()) {
+    me->tell(Terminated{ref}, nullptr);
+    return;
+  }
+  std::lock_guard<std::mutex> g(c->mu_);
+  c->watchers_.insert(me);
+}
+
+void ActorContext::unwatch(const ActorRef& ref) {
+  auto* local = dynamic_cast<LocalActorRef*>(ref.get());
+  if (!local) return;
+  auto c = local->cell();
+  if (!c) return;
+  std::lock_guard<std::mutex> g(c->mu_);
+  c->watchers_.erase(self());
+}
+
+void ActorContext::stash(Envelope env) {
+  std::lock_guard<std::mutex> g(cell_->mu_);
+  cell_->stash_.push_back(std::move(env));
+}
+
+void ActorContext::unstash_all() {
+  // Stashed messages go back to the FRONT of the mailbox, in their original order
+  // (Akka's Stash.unstashAll semantics).
+  std::lock_guard<std::mutex> g(cell_->mu_);
+  while (!cell_->stash_.empty()) {
+    cell_->mailbox_.push_front(std::move(cell_->stash_.back()));
+    cell_->stash_.pop_back();
+  }
+}
+
+void ActorContext::stop_self() { cell_->stop_requested_ = true; }
+
+// ------------------------------------------------------------------------ refs
+void LocalActorRef::tell(Message msg, ActorRef sender) {
+  auto c = cell_.lock();
+  if (!c || c->stopped()) {
+    sys_->dead_letters()->tell(std::move(msg), std::move(sender));
+    return;
+  }
+  c->enqueue(Envelope{std::move(msg), std::move(sender)});
+}
+
+void ProbeRef::tell(Message msg, ActorRef sender) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    q_.push_back(Envelope{std::move(msg), std::move(sender)});
+  }
+  cv_.notify_all();
+}
+
+std::optional<Envelope> ProbeRef::receive(std::chrono::milliseconds timeout) {
+  if (sys_->deterministic()) {
+    sys_->run_until_idle();
+    std::lock_guard<std::mutex> g(mu_);
+    if (q_.empty()) return std::nullopt;
+    Envelope e = std::move(q_.front());
+    q_.pop_front();
+    return e;
+  }
+  std::unique_lock<std::mutex> lk(mu_);
+  if (!cv_.wait_for(lk, timeout, [&] { return !q_.empty(); })) return std::nullopt;
+  Envelope e = std::move(q_.front());
+  q_.pop_front();
+  return e;
+}
+
+size_t ProbeRef::pending() {
+  if (sys_->deterministic()) sys_->run_until_idle();
+  std::lock_guard<std::mutex> g(mu_);
+  return q_.size();
+}
+
+void ProbeRef::clear() {
+  std::lock_guard<std::mutex> g(mu_);
+  q_.clear();
+}
+
+void DeadLetterRef::tell(Message msg, ActorRef sender) {
+  count_.fetch_add(1);
+  sys_->note_dead_letter(msg, sender);
+}
+
+// ------------------------------------------------------------------------ cell
+ActorCell::ActorCell(ActorSystem* sys, std::unique_ptr<Actor> actor, std::string path)
+    : sys_(sys), actor_(std::move(actor)), path_(std::move(path)) {}
+
+void ActorCell::enqueue(Envelope env) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    mailbox_.push_back(std::move(env));
+  }
+  sys_->schedule(shared_from_this());
+}
+
+bool ActorCell::has_mail() {
+  std::lock_guard<std::mutex> g(mu_);
+  return !mailbox_.empty();
+}
+
+size_t ActorCell::process(size_t n) {
+  ActorContext ctx(sys_, this);
+  if (!started_.exchange(true)) {
+    try {
+      actor_->pre_start(ctx);
+    } catch (...) {
+      sys_->record_exception(std::current_exception());
+    }
+  }
+  size_t done = 0;
+  while (done < n && !stopped_) {
+    Envelope env;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (mailbox_.empty()) break;
+      env = std::move(mailbox_.front());
+      mailbox_.pop_front();
+    }
+    ++done;
+    if (std::holds_alternative<PoisonPill>(env.msg)) {
+      do_stop();
+      break;
+    }
+    ctx.sender_ = env.sender;
+    try {
+      actor_->receive(env, ctx);
+    } catch (const std::exception& e) {
+      // Supervision: "resume" - the actor keeps its state (the reference's default
+      // restart would reset an initialised worker to id = -1).
+      sys_->note_failure(path_, e.what());
+      sys_->record_exception(std::current_exception());
+    } catch (...) {
+      sys_->note_failure(path_, "unknown exception");
+      sys_->record_exception(std::current_exception());
+    }
+    if (stop_requested_) {
+      do_stop();
+      break;
+    }
+  }
+  return done;
+}
+
+void ActorCell::do_stop() {
+  if (stopped_.exchange(true)) return;
+  ActorContext ctx(sys_, this);
+  try {
+    actor_->post_stop(ctx);
+  } catch (...) {
+  }
+  std::set<ActorRef> w;
+  std::deque<Envelope> rest;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    w.swap(watchers_);
+    rest.swap(mailbox_);
+  }
+  ActorRef me = ref();
+  for (auto& e : rest) sys_->dead_letters()->tell(std::move(e.msg), e.sender);
+  for (auto& watcher : w) watcher->tell(Terminated{me}, me);
+  sys_->remove_cell(path_);
+}
+
+// ------------------------------------------------------------------------ system
+ActorSystem::ActorSystem(std::string name, Mode mode, int threads, int throughput)
+    : name_(std::move(name)), mode_(mode), throughput_(std::max(1, throughput)) {
+  dead_letters_ = std::make_shared<DeadLetterRef>(this);
+  virtual_now_ = std::chrono::steady_clock::time_point{};
+  if (mode_ == Mode::Threaded) {
+    int n = threads > 0 ? threads : std::max(2u, std::min(8u, std::thread::hardware_concurrency()));
+    for (int i = 0; i < n; ++i) threads_.emplace_back([this] { worker_loop(); });
+    timer_thread_ = std::thread([this] { timer_loop(); });
+  }
+}
+
+ActorSystem::~ActorSystem() { shutdown(); }
+
+void ActorSystem::shutdown() {
+  if (shutdown_.exchange(true)) return;
+  rq_cv_.notify_all();
+  timer_cv_.notify_all();
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  if (timer_thread_.joinable()) timer_thread_.join();
+  std::map<std::string, std::shared_ptr<ActorCell>> cells;
+  {
+    std::lock_guard<std::mutex> g(reg_mu_);
+    cells.swap(cells_);
+    refs_.clear();
+  }
+  for (auto& [p, c] : cells) {
+    ActorContext ctx(this, c.get());
+    if (!c->stopped_.exchange(true)) {
+      try {
+        c->actor_->post_stop(ctx);
+      } catch (...) {
+      }
+    }
+  }
+  std::lock_guard<std::mutex> g(rq_mu_);
+  runq_.clear();
+}
+
+ActorRef ActorSystem::actor_of(std::unique_ptr<Actor> actor, std::string name) {
+  std::string path;
+  std::shared_ptr<ActorCell> cell;
+  ActorRef ref;
+  {
+    std::lock_guard<std::mutex> g(reg_mu_);
+    if (name.empty()) name = "$" + std::to_string(++name_counter_);
+    path = "/user/" + name;
+    if (cells_.count(path)) throw std::runtime_error("actor name [" + name + "] is not unique!");
+    cell = std::make_shared<ActorCell>(this, std::move(actor), path);
+    ref = std::make_shared<LocalActorRef>(cell, path, this);
+    cell->ref_ = ref;
+    cells_[path] = cell;
+    refs_[path] = ref;
+  }
+  // pre_start runs on the actor's first turn; schedule one so it happens promptly.
+  if (mode_ == Mode::Threaded) schedule(cell);
+  return ref;
+}
+
+std::shared_ptr<ProbeRef> ActorSystem::make_probe(std::string name) {
+  std::lock_guard<std::mutex> g(reg_mu_);
+  if (name.empty()) name = "testActor" + std::to_string(++name_counter_);
+  auto p = std::make_shared<ProbeRef>("/system/" + name, this);
+  refs_[p->path()] = p;
+  return p;
+}
+
+ActorRef ActorSystem::lookup(const std::string& path) {
+  std::lock_guard<std::mutex> g(reg_mu_);
+  auto it = refs_.find(path);
+  return it == refs_.end() ? nullptr : it->second;
+}
+
+void ActorSystem::stop(const ActorRef& ref) {
+  if (ref) ref->tell(PoisonPill{}, nullptr);
+}
+
+void ActorSystem::remove_cell(const std::string& path) {
+  std::lock_guard<std::mutex> g(reg_mu_);
+  cells_.erase(path);
+  refs_.erase(path);
+}
+
+void ActorSystem::schedule(const std::shared_ptr<ActorCell>& cell) {
+  if (cell->scheduled_.exchange(true)) return;
+  {
+    std::lock_guard<std::mutex> g(rq_mu_);
+    runq_.push_back(cell);
+  }
+  rq_cv_.notify_one();
+}
+
+void ActorSystem::record_exception(std::exception_ptr e) {
+  if (mode_ != Mode::Deterministic) return;
+  std::lock_guard<std::mutex> g(exc_mu_);
+  if (!pending_exc_) pending_exc_ = e;
+}
+
+size_t ActorSystem::run_until_idle(size_t max_messages) {
+  if (mode_ != Mode::Deterministic) throw std::runtime_error("run_until_idle needs a deterministic system");
+  size_t total = 0;
+  while (total < max_messages) {
+    std::shared_ptr<ActorCell> cell;
+    {
+      std::lock_guard<std::mutex> g(rq_mu_);
+      if (runq_.empty()) break;
+      cell = runq_.front();
+      runq_.pop_front();
+    }
+    cell->scheduled_.store(false);
+    total += cell->process(1);  // one message per turn: fair round-robin interleaving
+    if (!cell->stopped() && cell->has_mail()) schedule(cell);
+    std::exception_ptr e;
+    {
+      std::lock_guard<std::mutex> g(exc_mu_);
+      std::swap(e, pending_exc_);
+    }
+    if (e) std::rethrow_exception(e);
+  }
+  {
+    std::lock_guard<std::mutex> g(stats_mu_);
+    stats_.delivered += total;
+  }
+  return total;
+}
+
+void ActorSystem::worker_loop() {
+  while (true) {
+    std::shared_ptr<ActorCell> cell;
+    {
+      std::unique_lock<std::mutex> lk(rq_mu_);
+      rq_cv_.wait(lk, [&] { return shutdown_.load() || !runq_.empty(); });
+      if (shutdown_) return;
+      cell = runq_.front();
+      runq_.pop_front();
+      ++busy_;
+    }
+    size_t n = cell->process(static_cast<size_t>(throughput_));
+    cell->scheduled_.store(false);
+    // Re-check after clearing the flag: a message may have arrived in between.
+    if (!cell->stopped() && cell->has_mail()) schedule(cell);
+    {
+      std::lock_guard<std::mutex> g(stats_mu_);
+      stats_.delivered += n;
+    }
+    {
+      std::lock_guard<std::mutex> g(rq_mu_);
+      --busy_;
+      if (busy_ == 0 && runq_.empty()) idle_cv_.notify_all();
+    }
+  }
+}
+
+bool ActorSystem::await_idle(std::chrono::milliseconds timeout) {
+  if (mode_ == Mode::Deterministic) {
+    run_until_idle();
+    return true;
+  }
+  std::unique_lock<std::mutex> lk(rq_mu_);
+  return idle_cv_.wait_for(lk, timeout, [&] { return busy_ == 0 && runq_.empty(); });
+}
+
+// ------------------------------------------------------------------------ timers
+uint64_t ActorSystem::schedule_once(std::chrono::milliseconds delay, ActorRef target, Message msg) {
+  auto shared = std::make_shared<Message>(std::move(msg));
+  std::lock_guard<std::mutex> g(timer_mu_);
+  const auto now = mode_ == Mode::Deterministic ? virtual_now_ : std::chrono::steady_clock::now();
+  Timer t{++timer_seq_, now + delay, std::chrono::milliseconds(0), std::move(target),
+          [shared] { return *shared; }};
+  timers_.push_back(std::move(t));
+  timer_cv_.notify_all();
+  return timer_seq_;
+}
+
+uint64_t ActorSystem::schedule_repeated(std::chrono::milliseconds initial, std::chrono::milliseconds period,
+                                        ActorRef target, std::function<Message()> make) {
+  std::lock_guard<std::mutex> g(timer_mu_);
+  const auto now = mode_ == Mode::Deterministic ? virtual_now_ : std::chrono::steady_clock::now();
+  timers_.push_back(Timer{++timer_seq_, now + initial, period, std::move(target), std::move(make)});
+  timer_cv_.notify_all();
+  return timer_seq_;
+}
+
+void ActorSystem::cancel(uint64_t id) {
+  std::lock_guard<std::mutex> g(timer_mu_);
+  timers_.erase(std::remove_if(timers_.begin(), timers_.end(), [&](const Timer& t) { return t.id == id; }),
+                timers_.end());
+}
+
+void ActorSystem::fire_due_timers_locked(std::chrono::steady_clock::time_point now,
+                                         std::vector<std::pair<ActorRef, Message>>& out) {
+  std::sort(timers_.begin(), timers_.end(), [](const Timer& a, const Timer& b) {
+    return a.due < b.due || (a.due == b.due && a.id < b.id);
+  });
+  std::vector<Timer> keep;
+  for (auto& t : timers_) {
+    if (t.due <= now) {
+      out.emplace_back(t.target, t.make());
+      if (t.period.count() > 0) {
+        t.due += t.period;
+        keep.push_back(std::move(t));
+      }
+    } else {
+      keep.push_back(std::move(t));
+    }
+  }
+  timers_.swap(keep);
+}
+
+void ActorSystem::advance_time(std::chrono::milliseconds dt) {
+  if (mode_ != Mode::Deterministic) throw std::runtime_error("advance_time needs a deterministic system");
+  const auto target = virtual_now_ + dt;
+  while (true) {
+    std::vector<std::pair<ActorRef, Message>> fire;
+    {
+      std::lock_guard<std::mutex> g(timer_mu_);
+      // fire timers one due-instant at a time so periodic timers interleave correctly
+      std::chrono::steady_clock::time_point next = target;
+      for (auto& t : timers_) next = std::min(next, t.due);
+      if (next > target || timers_.empty()) {
+        virtual_now_ = target;
+        break;
+      }
+      virtual_now_ = next;
+      fire_due_timers_locked(virtual_now_, fire);
+      if (fire.empty()) {
+        virtual_now_ = target;
+        break;
+      }
+    }
+    for (auto& [ref, msg] : fire) ref->tell(std::move(msg), nullptr);
+    run_until_idle();
+  }
+}
+
+void ActorSystem::timer_loop() {
+  std::unique_lock<std::mutex> lk(timer_mu_);
+  while (!shutdown_) {
+    auto next = std::chrono::steady_clock::now() + std::chrono::milliseconds(200);
+    for (auto& t : timers_) next = std::min(next, t.due);
+    timer_cv_.wait_until(lk, next);
+    if (shutdown_) break;
+    std::vector<std::pair<ActorRef, Message>> fire;
+    fire_due_timers_locked(std::chrono::steady_clock::now(), fire);
+    lk.unlock();
+    for (auto& [ref, msg] : fire) ref->tell(std::move(msg), nullptr);
+    lk.lock();
+  }
+}
+
+// ------------------------------------------------------------------------ stats
+SystemStats ActorSystem::stats() {
+  std::lock_guard<std::mutex> g(stats_mu_);
+  SystemStats s = stats_;
+  s.dead_letters = dead_letters_->count();
+  return s;
+}
+
+void ActorSystem::note_dead_letter(const Message& m, const ActorRef& sender) {
+  uint64_t n;
+  {
+    std::lock_guard<std::mutex> g(stats_mu_);
+    n = ++dead_letters_logged_;
+  }
+  if (n <= 5)  // application.conf:23 log-dead-letters = 5
+    MXAR_LOG(INFO, name_, "Message [" << message_name(m) << "] from " << (sender ? sender->path() : "noSender")
+                                      << " was not delivered. [" << n << "] dead letters encountered.");
+}
+
+void ActorSystem::note_failure(const std::string& path, const std::string& what) {
+  {
+    std::lock_guard<std::mutex> g(stats_mu_);
+    stats_.actor_failures++;
+  }
+  MXAR_LOG(ERROR, name_, "actor " << path << " failed: " << what << " (resuming)");
+}
+
+}  // namespace mxar

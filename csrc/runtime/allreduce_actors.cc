@@ -1,0 +1,152 @@
+#include "allreduce_actors.h"
+
+#include "../core/log.h"
+
+namespace mxar {
+
+// ------------------------------------------------------------------------ worker
+WorkerActor::WorkerActor(DataSource source, DataSink sink, std::shared_ptr<DataPlane> plane)
+    : source_(std::move(source)), sink_(std::move(sink)), core_(this, std::move(plane)) {}
+
+void WorkerActor::receive(Envelope& env, ActorContext& ctx) {
+  ctx_ = &ctx;
+  struct Visitor {
+    WorkerActor* w;
+    Envelope& env;
+    ActorContext& ctx;
+    void operator()(InitWorkers& m) {
+      InitParams p;
+      p.destId = m.destId;
+      p.numPeers = static_cast<int>(m.workers.size());
+      p.thReduce = m.thReduce;
+      p.thComplete = m.thComplete;
+      p.maxLag = m.maxLag;
+      p.dataSize = m.dataSize;
+      p.maxChunkSize = m.maxChunkSize;
+      p.epoch = m.epoch;
+      w->peers_ = m.workers;
+      w->master_ = m.master;
+      w->core_.on_init(p);
+      ctx.unstash_all();  // replay what arrived before Init
+    }
+    void operator()(StartAllreduce& m) {
+      if (!w->core_.on_start(m)) {
+        MXAR_LOG(WARNING, "worker", "----Actor is not initialized (stashing StartAllreduce " << m.round << ")");
+        ctx.stash(std::move(env));
+      }
+    }
+    void operator()(ScatterBlock& m) {
+      if (!w->core_.on_scatter(m)) {
+        MXAR_LOG(WARNING, "worker", "----Have not initialized! (stashing ScatterBlock)");
+        ctx.stash(std::move(env));
+      }
+    }
+    void operator()(ReduceBlock& m) {
+      if (!w->core_.on_reduce(m)) {
+        MXAR_LOG(WARNING, "worker", "----Have not initialized! (stashing ReduceBlock)");
+        ctx.stash(std::move(env));
+      }
+    }
+    void operator()(Terminated& m) {
+      // AllreduceWorker.scala:153-158 (dead code there: the worker never watches)
+      for (auto it = w->peers_.begin(); it != w->peers_.end(); ++it) {
+        if (it->second == m.ref) {
+          MXAR_LOG(WARNING, "worker", "----peer " << it->first << " terminated");
+          it->second = ctx.system().dead_letters();
+        }
+      }
+    }
+    void operator()(CompleteAllreduce&) {}
+    void operator()(MemberUp&) {}
+    void operator()(AllreduceFinished&) {}
+    void operator()(PoisonPill&) {}
+    void operator()(TextMessage&) {}
+  };
+  std::visit(Visitor{this, env, ctx}, env.msg);
+  ctx_ = nullptr;
+}
+
+template <class M>
+void WorkerActor::send_peer(int peer, M&& m) {
+  auto it = peers_.find(peer);
+  ActorRef self = ctx_ ? ctx_->self() : nullptr;
+  if (it == peers_.end() || !it->second) {
+    MXAR_LOG(WARNING, "worker", "----no actor for peer " << peer << ", message dropped");
+    if (ctx_) ctx_->system().dead_letters()->tell(Message(std::forward<M>(m)), self);
+    return;
+  }
+  it->second->tell(Message(std::forward<M>(m)), self);
+}
+
+void WorkerActor::to_peer(int peer, ScatterBlock&& m) { send_peer(peer, std::move(m)); }
+void WorkerActor::to_peer(int peer, ReduceBlock&& m) { send_peer(peer, std::move(m)); }
+
+void WorkerActor::to_master(CompleteAllreduce&& m) {
+  ActorRef self = ctx_ ? ctx_->self() : nullptr;
+  if (master_) master_->tell(Message(std::move(m)), self);
+}
+
+void WorkerActor::to_self(WorkerMsg&& m) {
+  ActorRef self = ctx_->self();
+  std::visit([&](auto&& x) { self->tell(Message(std::move(x)), self); }, std::move(m));
+}
+
+AllReduceInput WorkerActor::fetch(const AllReduceInputRequest& req) { return source_(req); }
+
+void WorkerActor::sink(AllReduceOutput&& out) {
+  if (sink_) sink_(out);
+}
+
+// ------------------------------------------------------------------------ master
+MasterActor::MasterActor(MasterParams p, FinishedCallback on_finished)
+    : core_(this, p), on_finished_(std::move(on_finished)) {}
+
+int MasterActor::handle_of(const ActorRef& ref, bool create) {
+  for (size_t i = 0; i < handles_.size(); ++i)
+    if (handles_[i] == ref) return static_cast<int>(i);
+  if (!create) return -1;
+  handles_.push_back(ref);
+  return static_cast<int>(handles_.size() - 1);
+}
+
+void MasterActor::receive(Envelope& env, ActorContext& ctx) {
+  ctx_ = &ctx;
+  if (auto* up = std::get_if<MemberUp>(&env.msg)) {
+    MXAR_LOG(INFO, "master", "----Detect member " << (up->address.empty() ? up->ref->path() : up->address) << " up");
+    if (up->role == "worker" && up->ref) {
+      ctx.watch(up->ref);  // AllreduceMaster.scala:74
+      core_.on_member_up(handle_of(up->ref, true));
+    }
+  } else if (auto* t = std::get_if<Terminated>(&env.msg)) {
+    MXAR_LOG(INFO, "master", "----" << (t->ref ? t->ref->path() : "?") << " is terminated, removing it from the set");
+    int h = handle_of(t->ref, false);
+    if (h >= 0) core_.on_terminated(h);
+  } else if (auto* c = std::get_if<CompleteAllreduce>(&env.msg)) {
+    core_.on_complete(c->srcId, c->round);
+  }
+  ctx_ = nullptr;
+}
+
+void MasterActor::send_init(int handle, const InitParams& p, const std::map<int, int>& ids) {
+  InitWorkers m;
+  for (auto& [id, h] : ids) m.workers[id] = handles_[h];
+  m.master = ctx_->self();
+  m.destId = p.destId;
+  m.thReduce = p.thReduce;
+  m.thComplete = p.thComplete;
+  m.maxLag = p.maxLag;
+  m.dataSize = p.dataSize;
+  m.maxChunkSize = p.maxChunkSize;
+  m.epoch = p.epoch;
+  handles_[handle]->tell(Message(std::move(m)), ctx_->self());
+}
+
+void MasterActor::send_start(int handle, int round) {
+  handles_[handle]->tell(StartAllreduce{round}, ctx_->self());
+}
+
+void MasterActor::finished(int rounds) {
+  if (on_finished_) on_finished_(rounds);
+}
+
+}  // namespace mxar

@@ -1,0 +1,69 @@
+// Actor shells that host the protocol cores on the actor runtime.
+//   WorkerActor  <- class AllreduceWorker (AllreduceWorker.scala:9-270)
+//   MasterActor  <- class AllreduceMaster (AllreduceMaster.scala:15-98)
+// The shells only translate between ActorRefs and the cores' integer ids; all
+// protocol decisions live in WorkerCore / MasterCore.
+#pragma once
+
+#include <functional>
+#include <memory>
+
+#include "../core/master_core.h"
+#include "../core/worker_core.h"
+#include "actor_system.h"
+
+namespace mxar {
+
+using DataSource = std::function<AllReduceInput(const AllReduceInputRequest&)>;
+using DataSink = std::function<void(const AllReduceOutput&)>;
+
+class WorkerActor final : public Actor, public WorkerEffects {
+ public:
+  WorkerActor(DataSource source, DataSink sink, std::shared_ptr<DataPlane> plane = nullptr);
+  void receive(Envelope& env, ActorContext& ctx) override;
+  std::string kind() const override { return "worker"; }
+
+  // WorkerEffects
+  void to_peer(int peer, ScatterBlock&& m) override;
+  void to_peer(int peer, ReduceBlock&& m) override;
+  void to_master(CompleteAllreduce&& m) override;
+  void to_self(WorkerMsg&& m) override;
+  AllReduceInput fetch(const AllReduceInputRequest& req) override;
+  void sink(AllReduceOutput&& out) override;
+
+  const WorkerCore& core() const { return core_; }
+
+ private:
+  template <class M>
+  void send_peer(int peer, M&& m);
+  DataSource source_;
+  DataSink sink_;
+  WorkerCore core_;
+  std::map<int, ActorRef> peers_;
+  ActorRef master_;
+  ActorContext* ctx_ = nullptr;
+};
+
+class MasterActor final : public Actor, public MasterEffects {
+ public:
+  using FinishedCallback = std::function<void(int rounds)>;
+  MasterActor(MasterParams p, FinishedCallback on_finished = nullptr);
+  void receive(Envelope& env, ActorContext& ctx) override;
+  std::string kind() const override { return "master"; }
+
+  // MasterEffects
+  void send_init(int handle, const InitParams& p, const std::map<int, int>& ids) override;
+  void send_start(int handle, int round) override;
+  void finished(int rounds) override;
+
+  const MasterCore& core() const { return core_; }
+
+ private:
+  int handle_of(const ActorRef& ref, bool create);
+  MasterCore core_;
+  std::vector<ActorRef> handles_;
+  FinishedCallback on_finished_;
+  ActorContext* ctx_ = nullptr;
+};
+
+}  // namespace mxar

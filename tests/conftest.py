@@ -1,0 +1,41 @@
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+if str(ROOT) not in sys.path:
+    sys.path.insert(0, str(ROOT))
+
+os.environ.setdefault("MXAR_LOGLEVEL", "ERROR")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device); run via gpurun")
+    config.addinivalue_line("markers", "slow: multi-process or long-running test")
+
+
+def gpu_available() -> bool:
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def C():
+    from akka_allreduce_1_amd._native import C as _C
+
+    return _C
+
+
+@pytest.fixture
+def tk():
+    from akka_allreduce_1_amd.testkit import TestKit
+
+    kit = TestKit("MySpec", deterministic=True)
+    yield kit
+    kit.shutdown()
