@@ -1,0 +1,2 @@
+"""Distributed data plane: xGMI communicators, RCCL baseline, bucketed DP gradient reducer."""
+from .comm import CommError, LocalCluster, XgmiCommunicator, free_port, init_distributed  # noqa: F401

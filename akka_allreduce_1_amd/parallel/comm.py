@@ -1,0 +1,218 @@
+"""Communicators over the xGMI data plane (`csrc/hip/xgmi_comm.*`).
+
+`XgmiCommunicator` - one process per GPU (torchrun / torch.distributed). Rendezvous and the
+    exchange of IPC handles go over a CPU (gloo) group; the data moves in ONE fused HIP
+    launch per segment: direct push reduce-scatter + direct push all-gather over the xGMI
+    mesh (the reference's ScatterBlock/ReduceBlock pattern, AllreduceWorker.scala:194-238),
+    or a one-shot push + local reduce for small tensors. RCCL (`backend="nccl"`) stays
+    reachable as `algo="rccl"` for comparison and for dtypes the kernels do not cover.
+`LocalCluster` - P logical ranks inside ONE process (one or several GPUs): the same kernels,
+    consecutive ranks of one device in ONE launch. This is how the multi-rank protocol is run on a
+    single MI355X and what `tests/test_comm_gpu.py` checks.
+
+Reduction semantics: fp32 accumulation in rank order 0..P-1, one rounding to the output
+dtype (bf16 sums are never accumulated in bf16 - MI355X_MICROARCH.md, global float atomics).
+"""
+from __future__ import annotations
+
+import os
+import socket
+from typing import Sequence
+
+import torch
+
+from .._native import C
+
+_H = C.hip
+
+ALGOS = {"auto": _H.Algo.Auto, "twoshot": _H.Algo.TwoShot, "oneshot": _H.Algo.OneShot}
+DEFAULT_SLOT_BYTES = int(os.environ.get("MXAR_SLOT_BYTES", 64 << 20))
+
+
+class CommError(RuntimeError):
+    """A device-side wait timed out (a peer never delivered); the communicator is poisoned."""
+
+
+_ERR_NAMES = {1: "scatter wait timed out", 2: "reduce wait timed out", 4: "barrier timed out", 8: "bad arguments"}
+
+
+def _describe(err: int) -> str:
+    return ", ".join(v for k, v in _ERR_NAMES.items() if err & k) or f"code {err}"
+
+
+def _dtype_code(dt: torch.dtype):
+    from ..ops.kernels import dtype_code
+
+    return dtype_code(dt)
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def init_distributed(backend: str = "nccl") -> tuple[int, int, int]:
+    """Initialise torch.distributed from torchrun's env (or as a 1-rank job on 127.0.0.1).
+
+    Returns (rank, world_size, local_rank) and binds the process to cuda:local_rank.
+    """
+    import torch.distributed as dist
+
+    if "RANK" not in os.environ:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    if backend == "nccl" and torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    if not dist.is_initialized():
+        kw = {}
+        if backend == "nccl" and torch.cuda.is_available():
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+    return rank, world, local
+
+
+class XgmiCommunicator:
+    """Allreduce over directly mapped peer HBM for the ranks of a torch.distributed group."""
+
+    def __init__(self, group=None, *, device: torch.device | int | None = None, slot_bytes: int | None = None,
+                 grid: int = 0, timeout_s: float = 20.0, cpu_group=None):
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            raise RuntimeError("XgmiCommunicator needs torch.distributed (see init_distributed)")
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        self.slot_bytes = int(slot_bytes or DEFAULT_SLOT_BYTES)
+        self._c = _H.XgmiComm(self.rank, self.world, self.device.index, self.slot_bytes, grid, timeout_s)
+        if cpu_group is None:
+            backend = dist.get_backend(group)
+            cpu_group = group if backend == "gloo" else dist.new_group(
+                ranks=None if group is None else dist.get_process_group_ranks(group), backend="gloo")
+        self.cpu_group = cpu_group
+        handles: list = [None] * self.world
+        dist.all_gather_object(handles, self._c.ipc_handle(), group=cpu_group)
+        self._c.connect(handles)
+        dist.barrier(group=cpu_group)
+
+    # ------------------------------------------------------------------ collectives
+    def allreduce(self, inp: torch.Tensor, out: torch.Tensor | None = None, *, op: str = "sum",
+                  algo: str = "auto") -> torch.Tensor:
+        """out = sum (or mean) over ranks of inp. `out=inp` gives an in-place allreduce."""
+        if out is None:
+            out = torch.empty_like(inp)
+        if inp.device != self.device or out.device != self.device:
+            raise ValueError(f"tensors must live on {self.device}")
+        if not (inp.is_contiguous() and out.is_contiguous()) or inp.numel() != out.numel() or inp.dtype != out.dtype:
+            raise ValueError("inp/out must be contiguous with the same numel and dtype")
+        if algo == "rccl":
+            import torch.distributed as dist
+
+            if out.data_ptr() != inp.data_ptr():
+                out.copy_(inp)
+            dist.all_reduce(out, group=self.group)
+        else:
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            self._c.allreduce(inp.data_ptr(), out.data_ptr(), inp.numel(), _dtype_code(inp.dtype), stream, ALGOS[algo])
+        if op == "avg":
+            out.div_(self.world)
+        elif op != "sum":
+            raise ValueError(f"unsupported op {op!r}")
+        return out
+
+    def allreduce_(self, t: torch.Tensor, *, op: str = "sum", algo: str = "auto") -> torch.Tensor:
+        return self.allreduce(t, t, op=op, algo=algo)
+
+    def barrier(self) -> None:
+        self._c.barrier(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ------------------------------------------------------------------ health
+    def error(self) -> int:
+        return int(self._c.error())
+
+    def check(self) -> None:
+        """Synchronise and raise CommError if any device-side wait timed out."""
+        torch.cuda.synchronize(self.device)
+        e = self.error()
+        if e:
+            raise CommError(f"rank {self.rank}: {_describe(e)} (error word {e:#x})")
+
+    @property
+    def native(self):
+        return self._c
+
+    @property
+    def stats(self):
+        return self._c.stats
+
+    def __repr__(self) -> str:
+        return (f"XgmiCommunicator(rank={self.rank}, world={self.world}, device={self.device}, "
+                f"slot={self.slot_bytes >> 20} MiB, grid={self._c.grid})")
+
+
+class LocalCluster:
+    """P logical ranks in one process; rank k lives on `devices[k]`.
+
+    Consecutive ranks on the same device are served by ONE launch (blockIdx.y = rank), so
+    their spinning workgroups are co-resident by construction; different devices run
+    their launches concurrently. `grid` is the workgroup budget per device.
+    """
+
+    def __init__(self, world: int, devices: Sequence[int] | None = None, *, slot_bytes: int = 16 << 20,
+                 grid: int = 32, timeout_s: float = 10.0):
+        if devices is None:
+            devices = [torch.cuda.current_device()] * world
+        if len(devices) != world:
+            raise ValueError("need one device per logical rank")
+        self.world = world
+        self.devices = [torch.device("cuda", d) for d in devices]
+        self.comms = [_H.XgmiComm(k, world, self.devices[k].index, slot_bytes, grid, timeout_s) for k in range(world)]
+        for c in self.comms:
+            c.connect_local(self.comms)
+        self.groups: list[list[int]] = []
+        for k in range(world):
+            if self.groups and self.devices[self.groups[-1][-1]] == self.devices[k]:
+                self.groups[-1].append(k)
+            else:
+                self.groups.append([k])
+
+    def allreduce(self, inputs: Sequence[torch.Tensor], outputs: Sequence[torch.Tensor] | None = None, *,
+                  algo: str = "auto") -> list[torch.Tensor]:
+        if len(inputs) != self.world:
+            raise ValueError("one input per logical rank")
+        outputs = list(outputs) if outputs is not None else [torch.empty_like(x) for x in inputs]
+        n = inputs[0].numel()
+        for k in range(self.world):
+            x, y = inputs[k], outputs[k]
+            if x.numel() != n or y.numel() != n or x.dtype != inputs[0].dtype or y.dtype != x.dtype:
+                raise ValueError("all ranks must pass the same shape and dtype")
+            if x.device != self.devices[k] or y.device != self.devices[k]:
+                raise ValueError(f"rank {k} tensors must live on {self.devices[k]}")
+            if not (x.is_contiguous() and y.is_contiguous()):
+                raise ValueError("tensors must be contiguous")
+        code = _dtype_code(inputs[0].dtype)
+        for g in self.groups:
+            dev = self.devices[g[0]]
+            _H.XgmiComm.allreduce_local([self.comms[k] for k in g], [inputs[k].data_ptr() for k in g],
+                                        [outputs[k].data_ptr() for k in g], n, code,
+                                        torch.cuda.current_stream(dev).cuda_stream, ALGOS[algo])
+        return outputs
+
+    def barrier(self) -> None:
+        for g in self.groups:
+            dev = self.devices[g[0]]
+            _H.XgmiComm.barrier_local([self.comms[k] for k in g], torch.cuda.current_stream(dev).cuda_stream)
+
+    def check(self) -> None:
+        for d in set(self.devices):
+            torch.cuda.synchronize(d)
+        errs = [c.error() for c in self.comms]
+        if any(errs):
+            raise CommError("; ".join(f"rank {k}: {_describe(e)}" for k, e in enumerate(errs) if e))

@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""Headline benchmark: allreduce algbw (GB/s) + p50 latency of a 256 MiB bf16 gradient
+buffer per GPU (BASELINE.json metric; config "Ring allreduce of 256 MiB bf16 gradient
+buffer across 8xMI355X over xGMI"), one process per GPU.
+
+    python bench.py                                    # 1 GPU, defaults
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8 --steps 20 --warmup 5
+
+One "step" = one out-of-place allreduce of the buffer through the framework's engine
+(the fused xGMI two-shot kernel, csrc/hip/xgmi_comm.hip). The result is validated against
+an fp32 reference before timing. RCCL (`torch.distributed` nccl backend) is timed on the
+same buffer for comparison. Rank 0 prints ONE JSON line; `value` = algbw = bytes / time of
+the slowest rank (nccl-tests convention). Data: synthetic uniform(-1, 1) gradients.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from akka_allreduce_1_amd.ops import fill_uniform  # noqa: E402
+from akka_allreduce_1_amd.parallel.comm import CommError, XgmiCommunicator, init_distributed  # noqa: E402
+from akka_allreduce_1_amd.utils.timing import busbw, percentile  # noqa: E402
+
+BASELINE_VALUE = None  # the reference publishes no numbers
+
+
+def log(rank: int, msg: str) -> None:
+    if rank == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def timed(fn, steps: int, dev) -> tuple[float, list[float]]:
+    """Wall time of `steps` back-to-back calls (barrier + sync on both sides) and per-call
+    device times from event pairs."""
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        starts[i].record()
+        fn()
+        ends[i].record()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    per = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    return wall, per
+
+
+def max_over_ranks(x: float, dev) -> float:
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def validate(comm: XgmiCommunicator, n: int, dtype: torch.dtype, dev, rank: int, world: int) -> tuple[bool, float]:
+    """Engine result vs an fp32 reference sum (computed with RCCL on fp32 copies)."""
+    x = torch.empty(n, dtype=dtype, device=dev)
+    fill_uniform(x, seed=1000 + rank)
+    ref = x.float()
+    dist.all_reduce(ref)
+    y = comm.allreduce(x)
+    comm.check()
+    err = (y.float() - ref).abs().max().item()
+    tol = 1e-5 * world if dtype == torch.float32 else 2e-2 * world  # one bf16 rounding of |sum| <= world
+    ok = err <= tol
+    flag = torch.tensor([0 if ok else 1], device=dev)
+    dist.all_reduce(flag)
+    return flag.item() == 0, err
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--size-mib", type=int, default=256)
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--algo", choices=["auto", "twoshot", "oneshot"], default="auto")
+    ap.add_argument("--no-rccl", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true")
+    ap.add_argument("--sweep-steps", type=int, default=20)
+    args = ap.parse_args()
+
+    rank, world, local = init_distributed("nccl")
+    if world != args.gpus:
+        log(rank, f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
+    dev = torch.device("cuda", local)
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    es = 2 if dtype == torch.bfloat16 else 4
+    nbytes = args.size_mib << 20
+    n = nbytes // es
+    slot = max(64 << 20, -(-nbytes // world) + (1 << 20))
+    comm = XgmiCommunicator(slot_bytes=slot)
+    log(rank, f"{comm}  tensor={args.size_mib} MiB {args.dtype}")
+
+    ok, err = validate(comm, n, dtype, dev, rank, world)
+    ok_small, err_small = validate(comm, 12345, dtype, dev, rank, world)
+    engine = "xgmi"
+    if not (ok and ok_small):
+        log(rank, f"VALIDATION FAILED (max err {err:.3g} / {err_small:.3g}); reporting RCCL instead")
+        engine = "rccl-fallback"
+
+    x = torch.empty(n, dtype=dtype, device=dev)
+    fill_uniform(x, seed=rank)
+    y = torch.empty_like(x)
+
+    def step_engine():
+        comm.allreduce(x, y, algo=args.algo)
+
+    def step_rccl():
+        y.copy_(x)
+        dist.all_reduce(y)
+
+    step = step_engine if engine == "xgmi" else step_rccl
+    for _ in range(args.warmup):
+        step()
+    wall, per = timed(step, args.steps, dev)
+    if engine == "xgmi":
+        try:
+            comm.check()
+        except CommError as e:
+            log(rank, f"engine error during timing: {e}")
+            engine = "rccl-fallback"
+    wall = max_over_ranks(wall, dev)
+    ms = wall / args.steps * 1e3
+    algbw = nbytes / (ms / 1e3) / 1e9
+    p50 = max_over_ranks(percentile(per, 50), dev)
+
+    result = {
+        "metric": "allreduce_algbw",
+        "value": round(algbw, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None if BASELINE_VALUE is None else round(algbw / BASELINE_VALUE, 3),
+        "dtype": args.dtype,
+        "data": "synthetic uniform(-1,1) gradient buffer per rank",
+        "config": {
+            "model": f"flat {args.size_mib} MiB {args.dtype} gradient buffer (BASELINE config 3)",
+            "global_batch": world,
+            "seq_len": None,
+            "parallelism": f"dp{world}",
+            "tensor_bytes": nbytes,
+            "engine": engine,
+            "algo": args.algo,
+        },
+        "p50_ms": round(p50, 4),
+        "busbw": round(busbw(algbw, world), 2),
+        "validated_max_abs_err": err,
+    }
+
+    if not args.no_rccl:
+        for _ in range(args.warmup):
+            step_rccl()
+        rwall, rper = timed(step_rccl, args.steps, dev)
+        rms = max_over_ranks(rwall, dev) / args.steps * 1e3
+        r_alg = nbytes / (rms / 1e3) / 1e9
+        result["rccl"] = {"algbw": round(r_alg, 2), "ms_per_step": round(rms, 4),
+                          "p50_ms": round(max_over_ranks(percentile(rper, 50), dev), 4)}
+        result["speedup_vs_rccl"] = round(algbw / r_alg, 3)
+
+    if not args.no_sweep and engine == "xgmi":
+        sweep = []
+        for sz in [4 << 10, 64 << 10, 1 << 20, 16 << 20, 64 << 20]:
+            m = sz // es
+            a = x[:m]
+            b = y[:m]
+            row = {"bytes": sz}
+            for name, fn in [("xgmi", lambda: comm.allreduce(a, b)),
+                             ("rccl", lambda: dist.all_reduce(b))]:
+                if name == "rccl" and args.no_rccl:
+                    continue
+                for _ in range(3):
+                    fn()
+                w, p = timed(fn, args.sweep_steps, dev)
+                p50s = max_over_ranks(percentile(p, 50), dev)
+                row[f"{name}_p50_us"] = round(p50s * 1e3, 1)
+                row[f"{name}_algbw"] = round(sz / (p50s / 1e3) / 1e9, 2)
+            sweep.append(row)
+        comm.check()
+        result["sweep"] = sweep
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,197 @@
+// Device-side helpers shared by the gfx950 kernels of the data plane.
+//
+//   * 16-byte vector packs (one `global_load/store_dwordx4` per lane): every kernel in
+//     csrc/hip moves data 16 B per lane (cdna_hip_programming.md Guideline 13); bf16 is
+//     never loaded as scalars.
+//   * fp32 accumulation of bf16/fp32 packs (bf16 -> fp32 is a 16-bit shift; fp32 -> bf16
+//     goes through the hardware `v_cvt_pk_bf16_f32` round-to-nearest-even, NaN-safe).
+//   * Cross-GPU signalling over xGMI: flags live in uncached (MTYPE UC) device memory that
+//     peers map through IPC. Producer: payload stores -> every storing wave drains its
+//     `vmcnt` -> workgroup barrier -> ONE lane: system-scope release fence -> asm drain ->
+//     relaxed system-scope flag store. Consumer: ONE wave polls relaxed (with `s_sleep`),
+//     then ONE system-scope acquire, then a workgroup barrier before any payload load
+//     (MI355X_MICROARCH.md "Valid forms"; the asm drain after the fence is the ROCm 7.2
+//     compiler-hazard fix from the same section).
+//   * Every spin is bounded by a wall-clock deadline (`s_memrealtime`, 100 MHz): a wedged
+//     peer turns into an error word the host reads, never into a hung GPU.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mxar {
+namespace dev {
+
+struct alignas(16) Pack16 {
+  uint32_t w[4];
+};
+
+// ---------------------------------------------------------------------------------
+// dtype traits: E = element type tag, ELEMS = elements per 16-B pack
+// ---------------------------------------------------------------------------------
+struct F32 {
+  static constexpr int ELEMS = 4;
+  typedef float scalar;
+};
+struct BF16 {
+  static constexpr int ELEMS = 8;
+  typedef uint16_t scalar;
+};
+
+__device__ __forceinline__ float bf16_to_f32(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  // v_cvt_pk_bf16_f32: RNE, NaN stays NaN (MI355X_MICROARCH.md numerics table)
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 v = {lo, hi};
+  bf2 r = __builtin_convertvector(v, bf2);
+  return __builtin_bit_cast(uint32_t, r);
+}
+
+template <typename E>
+struct Acc;
+
+template <>
+struct Acc<F32> {
+  float v[4];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = 0.f;
+  }
+  __device__ __forceinline__ void add(const Pack16& p) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] += __uint_as_float(p.w[i]);
+  }
+  __device__ __forceinline__ void scale(float s) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] *= s;
+  }
+  __device__ __forceinline__ Pack16 pack() const {
+    Pack16 p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) p.w[i] = __float_as_uint(v[i]);
+    return p;
+  }
+};
+
+template <>
+struct Acc<BF16> {
+  float v[8];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.f;
+  }
+  __device__ __forceinline__ void add(const Pack16& p) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] += bf16_to_f32(p.w[i] & 0xFFFFu);
+      v[2 * i + 1] += bf16_to_f32(p.w[i] >> 16);
+    }
+  }
+  __device__ __forceinline__ void scale(float s) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] *= s;
+  }
+  __device__ __forceinline__ Pack16 pack() const {
+    Pack16 p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) p.w[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
+    return p;
+  }
+};
+
+// Scalar element access for ragged tails (< one pack).
+template <typename E>
+struct Scalar;
+template <>
+struct Scalar<F32> {
+  __device__ __forceinline__ static float load(const void* p, int64_t i) { return static_cast<const float*>(p)[i]; }
+  __device__ __forceinline__ static void store(void* p, int64_t i, float x) { static_cast<float*>(p)[i] = x; }
+  __device__ __forceinline__ static void copy(void* d, const void* s, int64_t i) {
+    static_cast<float*>(d)[i] = static_cast<const float*>(s)[i];
+  }
+};
+template <>
+struct Scalar<BF16> {
+  __device__ __forceinline__ static float load(const void* p, int64_t i) {
+    return bf16_to_f32(static_cast<const uint16_t*>(p)[i]);
+  }
+  __device__ __forceinline__ static void store(void* p, int64_t i, float x) {
+    static_cast<uint16_t*>(p)[i] = static_cast<uint16_t>(pack_bf16x2(x, 0.f) & 0xFFFFu);
+  }
+  __device__ __forceinline__ static void copy(void* d, const void* s, int64_t i) {
+    static_cast<uint16_t*>(d)[i] = static_cast<const uint16_t*>(s)[i];
+  }
+};
+
+__device__ __forceinline__ Pack16 ld16(const void* p) { return *static_cast<const Pack16*>(p); }
+__device__ __forceinline__ void st16(void* p, const Pack16& v) { *static_cast<Pack16*>(p) = v; }
+
+// ---------------------------------------------------------------------------------
+// Clock + bounded spin
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wall_ticks() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
+
+// Error codes written to the host-visible error word (bitwise OR).
+enum : uint32_t {
+  ERR_TIMEOUT_SCATTER = 1u,
+  ERR_TIMEOUT_REDUCE = 2u,
+  ERR_TIMEOUT_BARRIER = 4u,
+  ERR_BAD_ARGS = 8u,
+};
+
+__device__ __forceinline__ uint32_t ld_flag(const uint32_t* f) {
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_flag(uint32_t* f, uint32_t v) {
+  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool reached(uint32_t flag, uint32_t epoch) {
+  return static_cast<int32_t>(flag - epoch) >= 0;  // wrap-safe epoch compare
+}
+
+// Producer side: called by ALL threads of the workgroup after their payload stores.
+// Lane i < nflags of wave 0 stores flag `addr(i)` (skipped when it returns nullptr).
+template <typename FlagAddr>
+__device__ __forceinline__ void publish_flags(FlagAddr addr, int nflags, uint32_t epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+  __syncthreads();
+  if (threadIdx.x < static_cast<unsigned>(nflags)) {
+    uint32_t* f = addr(static_cast<int>(threadIdx.x));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope (xGMI peers)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (f) st_flag(f, epoch);
+  }
+}
+
+// Consumer side: called by ALL threads. Lane i < nflags of wave 0 polls flag `addr(i)`
+// (nullptr = nothing to wait for) until every flag has reached `epoch` or the deadline
+// passes. Returns false on timeout (uniform across the workgroup) after OR-ing `code`
+// into the error word. On success the payload may be read with plain loads.
+template <typename FlagAddr>
+__device__ __forceinline__ bool wait_flags(FlagAddr addr, int nflags, uint32_t epoch, uint64_t deadline,
+                                           uint32_t* err, uint32_t code) {
+  __shared__ int ok_s;
+  if (threadIdx.x < 64) {
+    const uint32_t* f = threadIdx.x < static_cast<unsigned>(nflags) ? addr(static_cast<int>(threadIdx.x)) : nullptr;
+    bool ok = (f == nullptr) || reached(ld_flag(f), epoch);
+    while (!__all(ok)) {
+      __builtin_amdgcn_s_sleep(1);
+      if (!ok) ok = reached(ld_flag(f), epoch);
+      if (wall_ticks() > deadline) break;
+    }
+    const bool all_ok = __all(ok);
+    if (threadIdx.x == 0) {
+      ok_s = all_ok ? 1 : 0;
+      if (!all_ok) __hip_atomic_fetch_or(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  return ok_s != 0;
+}
+
+}  // namespace dev
+}  // namespace mxar

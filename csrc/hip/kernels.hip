@@ -1,0 +1,198 @@
+// Standalone data-plane kernels (gfx950), all HBM-bound, 16 B per lane:
+//   reduce_slots  - K1 of SURVEY §2.4: out[i] = sum_p slot[p][i] (AllreduceWorker.scala:240-251),
+//                   fp32 accumulation in fixed peer order, optional scale (mean).
+//   fill_iota     - K9: reference data source data[i] = i + iteration (AllreduceWorker.scala:285-291)
+//   fill_uniform  - synthetic random gradients for the benchmarks (counter-based hash, no state)
+//   cast          - fp32 <-> bf16
+//   bucket_copy   - gather many gradient tensors into one flat bucket and scatter back
+//                   (bucket fusion for the data-parallel reducer)
+// Grids are grid-stride, capped at 8 workgroups per CU (cdna_hip_programming.md Guideline 11).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "device_common.h"
+#include "xgmi_comm.h"
+
+namespace mxar {
+using namespace dev;
+
+static constexpr int kThreads = 256;
+
+static int grid_for(int64_t packs) {
+  static int cap = 0;
+  if (cap == 0) {
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    cap = 8 * cus;
+  }
+  const int64_t g = (packs + kThreads - 1) / kThreads;
+  return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(g, cap)));
+}
+
+template <class E>
+__global__ __launch_bounds__(kThreads) void reduce_slots_kernel(const char* __restrict__ slots, int64_t stride_bytes,
+                                                                 int nslots, char* __restrict__ out, int64_t n,
+                                                                 float scale) {
+  const int64_t npk = n / E::ELEMS;
+  const int64_t step = static_cast<int64_t>(gridDim.x) * kThreads;
+  int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  for (; i + step < npk; i += 2 * step) {
+    Acc<E> a0, a1;
+    a0.zero();
+    a1.zero();
+    for (int p = 0; p < nslots; ++p) {
+      const char* s = slots + p * stride_bytes;
+      const Pack16 v0 = ld16(s + i * 16);
+      const Pack16 v1 = ld16(s + (i + step) * 16);
+      a0.add(v0);
+      a1.add(v1);
+    }
+    if (scale != 1.f) {
+      a0.scale(scale);
+      a1.scale(scale);
+    }
+    st16(out + i * 16, a0.pack());
+    st16(out + (i + step) * 16, a1.pack());
+  }
+  for (; i < npk; i += step) {
+    Acc<E> a0;
+    a0.zero();
+    for (int p = 0; p < nslots; ++p) a0.add(ld16(slots + p * stride_bytes + i * 16));
+    if (scale != 1.f) a0.scale(scale);
+    st16(out + i * 16, a0.pack());
+  }
+  const int64_t t = npk * E::ELEMS + static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (t < n) {
+    float acc = 0.f;
+    for (int p = 0; p < nslots; ++p) acc += Scalar<E>::load(slots + p * stride_bytes, t);
+    Scalar<E>::store(out, t, acc * scale);
+  }
+}
+
+void launch_reduce_slots(const void* slots, int64_t slot_stride_elems, int nslots, void* out, int64_t n, DType dt,
+                         float scale, hipStream_t stream) {
+  if (n <= 0) return;
+  const int64_t es = static_cast<int64_t>(dtype_size(dt));
+  if (((reinterpret_cast<uintptr_t>(slots) | reinterpret_cast<uintptr_t>(out)) & 15) || ((slot_stride_elems * es) & 15))
+    throw std::invalid_argument("reduce_slots: slots, out and slot stride must be 16-byte aligned");
+  const int64_t npk = n * es / 16;
+  const int g = grid_for(std::max<int64_t>(npk / 2, 1));
+  if (dt == DType::F32)
+    hipLaunchKernelGGL(reduce_slots_kernel<F32>, dim3(g), dim3(kThreads), 0, stream, static_cast<const char*>(slots),
+                       slot_stride_elems * es, nslots, static_cast<char*>(out), n, scale);
+  else
+    hipLaunchKernelGGL(reduce_slots_kernel<BF16>, dim3(g), dim3(kThreads), 0, stream, static_cast<const char*>(slots),
+                       slot_stride_elems * es, nslots, static_cast<char*>(out), n, scale);
+  hip_check(hipGetLastError(), "reduce_slots launch");
+}
+
+template <class E>
+__global__ __launch_bounds__(kThreads) void fill_iota_kernel(char* out, int64_t n, double offset) {
+  const int64_t step = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n; i += step)
+    Scalar<E>::store(out, i, static_cast<float>(static_cast<double>(i) + offset));
+}
+
+void launch_fill_iota(void* dst, int64_t n, double offset, DType dt, hipStream_t stream) {
+  if (n <= 0) return;
+  const int g = grid_for(n);
+  if (dt == DType::F32)
+    hipLaunchKernelGGL(fill_iota_kernel<F32>, dim3(g), dim3(kThreads), 0, stream, static_cast<char*>(dst), n, offset);
+  else
+    hipLaunchKernelGGL(fill_iota_kernel<BF16>, dim3(g), dim3(kThreads), 0, stream, static_cast<char*>(dst), n, offset);
+  hip_check(hipGetLastError(), "fill_iota launch");
+}
+
+__device__ __forceinline__ uint32_t hash32(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return static_cast<uint32_t>(x);
+}
+
+template <class E>
+__global__ __launch_bounds__(kThreads) void fill_uniform_kernel(char* out, int64_t n, uint64_t seed) {
+  const int64_t step = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n; i += step) {
+    const uint32_t h = hash32(seed * 0x9E3779B97F4A7C15ULL + static_cast<uint64_t>(i));
+    const float u = static_cast<float>(h >> 8) * (1.0f / 16777216.0f);  // [0, 1)
+    Scalar<E>::store(out, i, 2.f * u - 1.f);
+  }
+}
+
+void launch_fill_uniform(void* dst, int64_t n, uint64_t seed, DType dt, hipStream_t stream) {
+  if (n <= 0) return;
+  const int g = grid_for(n);
+  if (dt == DType::F32)
+    hipLaunchKernelGGL(fill_uniform_kernel<F32>, dim3(g), dim3(kThreads), 0, stream, static_cast<char*>(dst), n, seed);
+  else
+    hipLaunchKernelGGL(fill_uniform_kernel<BF16>, dim3(g), dim3(kThreads), 0, stream, static_cast<char*>(dst), n, seed);
+  hip_check(hipGetLastError(), "fill_uniform launch");
+}
+
+template <class Ei, class Eo>
+__global__ __launch_bounds__(kThreads) void cast_kernel(const char* in, char* out, int64_t n) {
+  const int64_t step = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n; i += step)
+    Scalar<Eo>::store(out, i, Scalar<Ei>::load(in, i));
+}
+
+void launch_cast(const void* src, DType dt_in, void* dst, DType dt_out, int64_t n, hipStream_t stream) {
+  if (n <= 0) return;
+  const int g = grid_for(n);
+  const char* s = static_cast<const char*>(src);
+  char* d = static_cast<char*>(dst);
+  if (dt_in == DType::F32 && dt_out == DType::BF16)
+    hipLaunchKernelGGL((cast_kernel<F32, BF16>), dim3(g), dim3(kThreads), 0, stream, s, d, n);
+  else if (dt_in == DType::BF16 && dt_out == DType::F32)
+    hipLaunchKernelGGL((cast_kernel<BF16, F32>), dim3(g), dim3(kThreads), 0, stream, s, d, n);
+  else if (dt_in == DType::F32)
+    hipLaunchKernelGGL((cast_kernel<F32, F32>), dim3(g), dim3(kThreads), 0, stream, s, d, n);
+  else
+    hipLaunchKernelGGL((cast_kernel<BF16, BF16>), dim3(g), dim3(kThreads), 0, stream, s, d, n);
+  hip_check(hipGetLastError(), "cast launch");
+}
+
+// table: count x {tensor ptr, numel, bucket offset (elements)} as 3 u64 each.
+// One workgroup row per tensor slice: blockIdx.y = tensor, blockIdx.x strides its elements.
+template <class E>
+__global__ __launch_bounds__(kThreads) void bucket_copy_kernel(const uint64_t* table, char* bucket, int pack) {
+  constexpr int es = 16 / E::ELEMS;
+  const uint64_t* t = table + 3 * blockIdx.y;
+  char* tp = reinterpret_cast<char*>(t[0]);
+  const int64_t numel = static_cast<int64_t>(t[1]);
+  char* bp = bucket + static_cast<int64_t>(t[2]) * es;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(tp) | reinterpret_cast<uintptr_t>(bp)) & 15) == 0;
+  const int64_t step = static_cast<int64_t>(gridDim.x) * kThreads;
+  const int64_t first = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  char* dst = pack ? bp : tp;
+  const char* src = pack ? tp : bp;
+  int64_t done = 0;
+  if (aligned) {
+    const int64_t npk = numel / E::ELEMS;
+    for (int64_t i = first; i < npk; i += step) st16(dst + i * 16, ld16(src + i * 16));
+    done = npk * E::ELEMS;
+  }
+  for (int64_t i = done + first; i < numel; i += step) Scalar<E>::copy(dst, src, i);
+}
+
+void launch_bucket_copy(const uint64_t* dev_table, int count, void* bucket, DType dt, bool pack, int64_t total,
+                        hipStream_t stream) {
+  if (count <= 0) return;
+  const int64_t avg_packs = std::max<int64_t>(1, total * static_cast<int64_t>(dtype_size(dt)) / 16 / count);
+  const int gx = static_cast<int>(std::min<int64_t>(64, (avg_packs + kThreads - 1) / kThreads));
+  dim3 g(std::max(gx, 1), count);
+  if (dt == DType::F32)
+    hipLaunchKernelGGL(bucket_copy_kernel<F32>, g, dim3(kThreads), 0, stream, dev_table, static_cast<char*>(bucket),
+                       pack ? 1 : 0);
+  else
+    hipLaunchKernelGGL(bucket_copy_kernel<BF16>, g, dim3(kThreads), 0, stream, dev_table, static_cast<char*>(bucket),
+                       pack ? 1 : 0);
+  hip_check(hipGetLastError(), "bucket_copy launch");
+}
+
+}  // namespace mxar

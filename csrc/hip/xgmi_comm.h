@@ -1,0 +1,127 @@
+// XgmiComm: one-process-per-GPU allreduce over directly mapped peer HBM (xGMI).
+//
+// This is the MI355X data plane of the reference's scatter/reduce/broadcast protocol
+// (AllreduceWorker.scala:194-209 scatter, :240-251 reduce, :230-238 broadcast): a
+// *direct* (one-hop, fully connected) reduce-scatter + all-gather, which on an 8-GPU
+// xGMI mesh drives all 7 links of every GPU at once, where a ring drives 2.
+//
+//   ScatterBlock(chunk c of block j)  == rank r stores input[j][c] straight into rank j's
+//                                        receive slot S_j[r][c] over xGMI, then sets
+//                                        flag F1_j[r][c] = epoch
+//   count == minRequired (th = 1)      == rank j sees F1_j[s][c] == epoch for every s
+//   reduce + ReduceBlock broadcast     == rank j sums the P contributions in fp32 and
+//                                        stores the result into every R_k[j][c], then
+//                                        sets F2_k[j][c]
+//   CompleteAllreduce / flush          == rank k waits on F2_k[*][c] and copies R_k into
+//                                        the output (its own block is written directly)
+//
+// All three phases run inside ONE persistent launch per segment (no host round trip per
+// chunk), every spin is bounded by a deadline, and epochs live in device memory so a
+// launch can be captured into a hipGraph. Slabs are uncached device memory exported
+// with hipIpcGetMemHandle; peers map them with hipIpcOpenMemHandle.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace mxar {
+
+enum class DType : int { F32 = 0, BF16 = 1 };
+inline size_t dtype_size(DType d) { return d == DType::F32 ? 4 : 2; }
+
+enum class Algo : int { Auto = 0, TwoShot = 1, OneShot = 2 };
+
+constexpr int kMaxRanks = 16;
+constexpr int kCommThreads = 256;
+
+struct CommStats {
+  uint64_t calls = 0, launches = 0, bytes = 0, oneshot = 0, twoshot = 0;
+};
+
+class XgmiComm {
+ public:
+  // slot_bytes: capacity of one receive slot (one block of one peer). A two-shot launch
+  // reduces up to world * slot_bytes bytes, a one-shot launch up to slot_bytes bytes;
+  // larger tensors are processed in segments. Memory per GPU ~ 2 * world * slot_bytes.
+  XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid = 0, double timeout_s = 20.0);
+  ~XgmiComm();
+  XgmiComm(const XgmiComm&) = delete;
+  XgmiComm& operator=(const XgmiComm&) = delete;
+
+  // 64-byte hipIpcMemHandle of this rank's slab.
+  std::string ipc_handle() const;
+  // handles[k] = ipc_handle() of rank k (own entry ignored).
+  void connect(const std::vector<std::string>& handles);
+  // Single-process mode: all "ranks" are this process (tests / P logical ranks).
+  void connect_local(const std::vector<XgmiComm*>& comms);
+
+  // out = sum over ranks of in (n elements of dtype); in == out allowed (in-place).
+  // Pointers must be 16-byte aligned. Enqueued on `stream`; returns immediately.
+  void allreduce(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, Algo algo = Algo::Auto);
+  // Device-side barrier over all ranks (enqueued on `stream`).
+  void barrier(hipStream_t stream);
+
+  // Single-process cluster: ONE launch on `stream` runs every rank of `comms` (all on
+  // one device, consecutive ranks, connected with connect_local); blockIdx.y = rank.
+  static void allreduce_local(const std::vector<XgmiComm*>& comms, const std::vector<const void*>& ins,
+                              const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream,
+                              Algo algo = Algo::Auto);
+  static void barrier_group(const std::vector<XgmiComm*>& comms, hipStream_t stream);
+
+  // Sticky device error word (ORed codes, see device_common.h); 0 = healthy.
+  uint32_t error() const;
+  void clear_error();
+
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  int device() const { return device_; }
+  int grid() const { return grid_; }
+  int64_t slot_bytes() const { return slot_bytes_; }
+  int64_t oneshot_max_bytes() const { return oneshot_max_; }
+  void set_oneshot_max_bytes(int64_t b) { oneshot_max_ = b; }
+  void set_grid(int g);
+  void set_timeout(double s) { timeout_s_ = s; }
+  bool connected() const { return connected_; }
+  const CommStats& stats() const { return stats_; }
+  char* slab() const { return slab_; }
+  int64_t slab_bytes() const { return slab_bytes_; }
+  static int64_t min_chunk_bytes() { return 1024; }
+
+ private:
+  static void run(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
+                  const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, Algo algo);
+  static void launch_segment(const std::vector<XgmiComm*>& group, const char* const* ins, char* const* outs,
+                             int64_t n, DType dt, hipStream_t stream, bool oneshot);
+
+  int rank_, world_, device_, grid_;
+  int64_t slot_bytes_, maxch_, off_S_, off_R_, off_B_, slab_bytes_;
+  int64_t oneshot_max_;
+  double timeout_s_;
+  char* slab_ = nullptr;            // own uncached slab (flags | S | R)
+  uint32_t* ctl_ = nullptr;         // [0] epoch, [1] ticket, [2] sticky error (device memory)
+  char* peers_[kMaxRanks] = {};     // slab base of every rank (own included)
+  bool ipc_opened_[kMaxRanks] = {};
+  bool connected_ = false;
+  CommStats stats_;
+};
+
+// Standalone data-plane kernels (csrc/hip/kernels.hip).
+// out[i] = sum_{p < nslots} slots[p * slot_stride + i], fp32 accumulate; i < n.
+void launch_reduce_slots(const void* slots, int64_t slot_stride_elems, int nslots, void* out, int64_t n, DType dt,
+                         float scale, hipStream_t stream);
+// dst[i] = (float)(i + offset) (reference data source AllreduceWorker.scala:285-291)
+void launch_fill_iota(void* dst, int64_t n, double offset, DType dt, hipStream_t stream);
+// dst[i] = uniform(-1, 1) from a counter-based hash of (seed, i)
+void launch_fill_uniform(void* dst, int64_t n, uint64_t seed, DType dt, hipStream_t stream);
+// dst (dt_out) = src (dt_in), n elements
+void launch_cast(const void* src, DType dt_in, void* dst, DType dt_out, int64_t n, hipStream_t stream);
+// flat bucket pack/unpack: copy `count` tensors (ptr, numel) into / out of a contiguous bucket
+void launch_bucket_copy(const uint64_t* dev_table, int count, void* bucket, DType dt, bool pack, int64_t total,
+                        hipStream_t stream);
+
+void hip_check(hipError_t e, const char* what);
+
+}  // namespace mxar

@@ -1,0 +1,530 @@
+// Fused push-based allreduce over xGMI (gfx950). See xgmi_comm.h for the protocol map to
+// the reference (AllreduceWorker.scala scatter/reduce/broadcast/complete).
+//
+// Slab layout (identical offsets on every rank, uncached device memory):
+//   [F1: P x maxch u32][F2: P x maxch u32][FB: P u32]  pad to 64 KiB
+//   [S : P slots x slot_bytes]   S_k[s] = contribution of rank s to rank k's block
+//   [R : P slots x slot_bytes]   R_k[j] = reduced block j, pushed by its owner j
+// Flags hold the epoch of the launch that wrote them; epochs come from a device counter
+// so launches replay correctly under hipGraph capture.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "device_common.h"
+#include "xgmi_comm.h"
+
+namespace mxar {
+using namespace dev;
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    throw std::runtime_error(std::string("HIP error in ") + what + ": " + hipGetErrorString(e));
+  }
+}
+
+// One launch serves one rank (one process per GPU: gridDim.y == 1, rank = rank0) or all
+// P logical ranks of a single-process cluster on one device (gridDim.y == P, rank =
+// rank0 + blockIdx.y): every rank's workgroups are then co-resident in ONE dispatch, so
+// no rank can be starved behind another on a shared hardware queue.
+struct CommArgs {
+  const char* in[kMaxRanks];
+  char* out[kMaxRanks];
+  uint32_t* ctl[kMaxRanks];  // per rank: [0] epoch [1] ticket [2] error
+  int64_t n;      // elements in this segment
+  int64_t block;  // elements per block (two-shot) / whole segment (one-shot)
+  int64_t chunk;  // elements per chunk (work unit)
+  int nch;        // chunks per block
+  int P;
+  int rank0;
+  int pad_;
+  int64_t maxch;
+  int64_t off_S, off_R, slot_bytes;
+  uint64_t timeout;
+  char* base[kMaxRanks];
+};
+
+__device__ __forceinline__ uint32_t* f1(const CommArgs& a, int k, int s, int c) {
+  return reinterpret_cast<uint32_t*>(a.base[k]) + static_cast<int64_t>(s) * a.maxch + c;
+}
+__device__ __forceinline__ uint32_t* f2(const CommArgs& a, int k, int s, int c) {
+  return reinterpret_cast<uint32_t*>(a.base[k]) + static_cast<int64_t>(a.P + s) * a.maxch + c;
+}
+__device__ __forceinline__ uint32_t* fb(const CommArgs& a, int k, int s) {
+  return reinterpret_cast<uint32_t*>(a.base[k]) + static_cast<int64_t>(2 * a.P) * a.maxch + s;
+}
+__device__ __forceinline__ int64_t clamp_len(int64_t avail, int64_t cap) {
+  return avail <= 0 ? 0 : (avail < cap ? avail : cap);
+}
+
+// Copy len elements, 16 B per lane, 4 packs in flight per lane.
+template <class E>
+__device__ __forceinline__ void copy_elems(char* dst, const char* src, int64_t len) {
+  const int64_t npk = len / E::ELEMS;
+  const Pack16* s = reinterpret_cast<const Pack16*>(src);
+  Pack16* d = reinterpret_cast<Pack16*>(dst);
+  int64_t i = threadIdx.x;
+  constexpr int U = 4;
+  for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
+    Pack16 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = s[i + u * kCommThreads];
+#pragma unroll
+    for (int u = 0; u < U; ++u) d[i + u * kCommThreads] = v[u];
+  }
+  for (; i < npk; i += kCommThreads) d[i] = s[i];
+  const int64_t t = npk * E::ELEMS + threadIdx.x;
+  if (t < len) Scalar<E>::copy(dst, src, t);
+}
+
+// Sum P sources (fixed order s = 0..P-1, fp32) and store the result to up to P
+// destinations. src(s) / dst(k) return byte pointers to element 0 of the chunk.
+template <class E, int PT, class SrcF, class DstF>
+__device__ __forceinline__ void reduce_to(int P, SrcF src, int ndst, DstF dst, int64_t len) {
+  constexpr int es = 16 / E::ELEMS;
+  const int64_t npk = len / E::ELEMS;
+  constexpr int U = 2;
+  int64_t i = threadIdx.x;
+  for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
+    Acc<E> acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u].zero();
+    if constexpr (PT > 0) {
+      Pack16 v[PT][U];
+#pragma unroll
+      for (int s = 0; s < PT; ++s)
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[s][u] = ld16(src(s) + (i + u * kCommThreads) * 16);
+#pragma unroll
+      for (int s = 0; s < PT; ++s)
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u].add(v[s][u]);
+    } else {
+      for (int s = 0; s < P; ++s) {
+        Pack16 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ld16(src(s) + (i + u * kCommThreads) * 16);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u].add(v[u]);
+      }
+    }
+    Pack16 o[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) o[u] = acc[u].pack();
+    for (int k = 0; k < ndst; ++k) {
+      char* d = dst(k);
+      if (d == nullptr) continue;
+#pragma unroll
+      for (int u = 0; u < U; ++u) st16(d + (i + u * kCommThreads) * 16, o[u]);
+    }
+  }
+  for (; i < npk; i += kCommThreads) {
+    Acc<E> acc;
+    acc.zero();
+    for (int s = 0; s < P; ++s) acc.add(ld16(src(s) + i * 16));
+    const Pack16 o = acc.pack();
+    for (int k = 0; k < ndst; ++k) {
+      char* d = dst(k);
+      if (d) st16(d + i * 16, o);
+    }
+  }
+  const int64_t t = npk * E::ELEMS + threadIdx.x;
+  if (t < len) {
+    float acc = 0.f;
+    for (int s = 0; s < P; ++s) acc += Scalar<E>::load(src(s), t);
+    for (int k = 0; k < ndst; ++k) {
+      char* d = dst(k);
+      if (d) Scalar<E>::store(d, t, acc);
+    }
+  }
+  (void)es;
+}
+
+// The rank's last workgroup to finish publishes the epoch for the next launch.
+__device__ __forceinline__ void finish_launch(uint32_t* ctl, uint32_t epoch) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == gridDim.x - 1) {
+      __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ctl[0], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t launch_epoch(const uint32_t* ctl) {
+  return __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+}
+
+// ---------------------------------------------------------------------------------
+// Two-shot: direct reduce-scatter (push) + direct all-gather (push), one launch.
+// ---------------------------------------------------------------------------------
+template <class E, int PT>
+__global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
+  constexpr int es = 16 / E::ELEMS;
+  const int P = PT > 0 ? PT : a.P;
+  const int y = blockIdx.y;
+  const int r = a.rank0 + y;
+  const char* const in = a.in[y];
+  char* const out = a.out[y];
+  uint32_t* const ctl = a.ctl[y];
+  const uint32_t epoch = launch_epoch(ctl);
+  const uint64_t deadline = wall_ticks() + a.timeout;
+  const int G = gridDim.x;
+  const int64_t slot = a.slot_bytes;
+  uint32_t* err = &ctl[2];
+  const int Pm1 = P > 1 ? P - 1 : 1;
+  const int nu = (P - 1) * a.nch;
+
+  // Phase 1 - ScatterBlock: push chunk c of block j to its owner j (rotated dest order,
+  // AllreduceWorker.scala:194-209), so concurrent workgroups load all links.
+  for (int u = blockIdx.x; u < nu; u += G) {
+    const int c = u / Pm1;
+    const int j = (r + 1 + u % Pm1) % P;
+    const int64_t bstart = static_cast<int64_t>(j) * a.block;
+    const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
+    const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
+    if (len > 0) copy_elems<E>(a.base[j] + a.off_S + r * slot + cstart * es, in + (bstart + cstart) * es, len);
+    publish_flags([&](int) { return f1(a, j, r, c); }, 1, epoch);
+  }
+
+  // Phase 2 - reduce own block chunk by chunk once all P contributions have arrived
+  // (thReduce = 1), then ReduceBlock-broadcast the sum into every rank's R slot.
+  const int64_t bstart_own = static_cast<int64_t>(r) * a.block;
+  const int64_t blen_own = clamp_len(a.n - bstart_own, a.block);
+  for (int c = blockIdx.x; c < a.nch; c += G) {
+    const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
+    const int64_t len = clamp_len(blen_own - cstart, a.chunk);
+    wait_flags([&](int s) -> const uint32_t* { return s == r ? nullptr : f1(a, r, s, c); }, P, epoch, deadline, err,
+               ERR_TIMEOUT_SCATTER);
+    if (len > 0) {
+      const char* own_in = in + (bstart_own + cstart) * es;
+      const char* S = a.base[r] + a.off_S + cstart * es;
+      char* own_out = out + (bstart_own + cstart) * es;
+      const int64_t roff = a.off_R + r * slot + cstart * es;
+      reduce_to<E, PT>(
+          P, [&](int s) -> const char* { return s == r ? own_in : S + s * slot; }, P,
+          [&](int k) -> char* { return k == r ? own_out : a.base[k] + roff; }, len);
+    }
+    publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : f2(a, k, r, c); }, P, epoch);
+  }
+
+  // Phase 3 - complete: gather the other owners' reduced chunks into the output.
+  for (int u = blockIdx.x; u < nu; u += G) {
+    const int c = u / Pm1;
+    const int j = (r + 1 + u % Pm1) % P;
+    const int64_t bstart = static_cast<int64_t>(j) * a.block;
+    const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
+    const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
+    wait_flags([&](int) -> const uint32_t* { return f2(a, r, j, c); }, 1, epoch, deadline, err, ERR_TIMEOUT_REDUCE);
+    if (len > 0) copy_elems<E>(out + (bstart + cstart) * es, a.base[r] + a.off_R + j * slot + cstart * es, len);
+  }
+  finish_launch(ctl, epoch);
+}
+
+// ---------------------------------------------------------------------------------
+// One-shot (latency path): every rank pushes its whole input into every rank's S slot
+// (own included, so the reduce never reads `in` and in-place is safe), then reduces
+// all P slots locally. One xGMI hop instead of two.
+// ---------------------------------------------------------------------------------
+template <class E, int PT>
+__global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
+  constexpr int es = 16 / E::ELEMS;
+  const int P = PT > 0 ? PT : a.P;
+  const int y = blockIdx.y;
+  const int r = a.rank0 + y;
+  const char* const in = a.in[y];
+  char* const out = a.out[y];
+  uint32_t* const ctl = a.ctl[y];
+  const uint32_t epoch = launch_epoch(ctl);
+  const uint64_t deadline = wall_ticks() + a.timeout;
+  const int G = gridDim.x;
+  const int64_t slot = a.slot_bytes;
+  uint32_t* err = &ctl[2];
+  const int nu = P * a.nch;
+  for (int u = blockIdx.x; u < nu; u += G) {
+    const int c = u / P;
+    const int j = (r + 1 + u % P) % P;
+    const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
+    const int64_t len = clamp_len(a.n - cstart, a.chunk);
+    if (len > 0) copy_elems<E>(a.base[j] + a.off_S + r * slot + cstart * es, in + cstart * es, len);
+    publish_flags([&](int) { return f1(a, j, r, c); }, 1, epoch);
+  }
+  for (int c = blockIdx.x; c < a.nch; c += G) {
+    const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
+    const int64_t len = clamp_len(a.n - cstart, a.chunk);
+    wait_flags([&](int s) -> const uint32_t* { return f1(a, r, s, c); }, P, epoch, deadline, err, ERR_TIMEOUT_SCATTER);
+    if (len > 0) {
+      const char* S = a.base[r] + a.off_S + cstart * es;
+      char* o = out + cstart * es;
+      reduce_to<E, PT>(
+          P, [&](int s) -> const char* { return S + s * slot; }, 1, [&](int) -> char* { return o; }, len);
+    }
+  }
+  finish_launch(ctl, epoch);
+}
+
+__global__ __launch_bounds__(kCommThreads) void barrier_kernel(CommArgs a) {
+  const int r = a.rank0 + blockIdx.y;
+  uint32_t* const ctl = a.ctl[blockIdx.y];
+  const uint32_t epoch = launch_epoch(ctl);
+  const uint64_t deadline = wall_ticks() + a.timeout;
+  publish_flags([&](int k) -> uint32_t* { return fb(a, k, r); }, a.P, epoch);
+  wait_flags([&](int s) -> const uint32_t* { return fb(a, r, s); }, a.P, epoch, deadline, &ctl[2],
+             ERR_TIMEOUT_BARRIER);
+  finish_launch(ctl, epoch);
+}
+
+// ---------------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------------
+static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+static int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+static int default_grid(int device) {
+  if (const char* g = std::getenv("MXAR_GRID")) return std::max(1, std::atoi(g));
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  return 2 * cus;  // every workgroup must stay resident (they spin): 2 x 256-thread WG per CU
+}
+
+XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid, double timeout_s)
+    : rank_(rank), world_(world), device_(device), grid_(grid), timeout_s_(timeout_s) {
+  if (world < 1 || world > kMaxRanks) throw std::invalid_argument("XgmiComm: world must be in [1, 16]");
+  if (rank < 0 || rank >= world) throw std::invalid_argument("XgmiComm: bad rank");
+  slot_bytes_ = round_up(std::max<int64_t>(slot_bytes, 64 * 1024), 64 * 1024);
+  maxch_ = slot_bytes_ / min_chunk_bytes();
+  const int64_t flag_bytes = (2 * world_ * maxch_ + world_) * 4;
+  off_S_ = round_up(flag_bytes, 64 * 1024);
+  off_R_ = off_S_ + world_ * slot_bytes_;
+  off_B_ = 2 * world_ * maxch_ * 4;
+  slab_bytes_ = off_R_ + world_ * slot_bytes_;
+  oneshot_max_ = std::min<int64_t>(slot_bytes_, 256 * 1024);
+  if (const char* e = std::getenv("MXAR_ONESHOT_MAX")) oneshot_max_ = std::min<int64_t>(slot_bytes_, std::atoll(e));
+  if (grid_ <= 0) grid_ = default_grid(device);
+
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  const char* mem = std::getenv("MXAR_SLAB_MEM");
+  const std::string kind = mem ? mem : "uncached";
+  if (kind == "coarse") {
+    hip_check(hipMalloc(reinterpret_cast<void**>(&slab_), slab_bytes_), "hipMalloc(slab)");
+  } else {
+    const unsigned flags = kind == "fine" ? hipDeviceMallocFinegrained : hipDeviceMallocUncached;
+    hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&slab_), slab_bytes_, flags), "hipExtMallocWithFlags(slab)");
+  }
+  // Flags start at 0 = "epoch 0 done"; the first launch uses epoch 1.
+  hip_check(hipMemset(slab_, 0, off_S_), "hipMemset(flags)");
+  hip_check(hipMalloc(reinterpret_cast<void**>(&ctl_), 256), "hipMalloc(ctl)");
+  hip_check(hipMemset(ctl_, 0, 256), "hipMemset(ctl)");
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  peers_[rank_] = slab_;
+}
+
+XgmiComm::~XgmiComm() {
+  (void)hipSetDevice(device_);
+  for (int k = 0; k < world_; ++k)
+    if (ipc_opened_[k] && peers_[k]) (void)hipIpcCloseMemHandle(peers_[k]);
+  if (slab_) (void)hipFree(slab_);
+  if (ctl_) (void)hipFree(ctl_);
+}
+
+std::string XgmiComm::ipc_handle() const {
+  hipIpcMemHandle_t h;
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipIpcGetMemHandle(&h, slab_), "hipIpcGetMemHandle");
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void XgmiComm::connect(const std::vector<std::string>& handles) {
+  if (static_cast<int>(handles.size()) != world_) throw std::invalid_argument("connect: need one handle per rank");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  for (int k = 0; k < world_; ++k) {
+    if (k == rank_) continue;
+    if (handles[k].size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("connect: bad handle size");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handles[k].data(), sizeof(h));
+    void* p = nullptr;
+    hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    peers_[k] = static_cast<char*>(p);
+    ipc_opened_[k] = true;
+  }
+  connected_ = true;
+}
+
+void XgmiComm::connect_local(const std::vector<XgmiComm*>& comms) {
+  if (static_cast<int>(comms.size()) != world_) throw std::invalid_argument("connect_local: need one comm per rank");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  for (int k = 0; k < world_; ++k) {
+    if (comms[k]->slab_bytes_ != slab_bytes_) throw std::invalid_argument("connect_local: slab geometry differs");
+    peers_[k] = comms[k]->slab_;
+    if (comms[k]->device_ != device_) {
+      int can = 0;
+      (void)hipDeviceCanAccessPeer(&can, device_, comms[k]->device_);
+      if (!can) throw std::runtime_error("connect_local: no peer access between devices");
+      hipError_t e = hipDeviceEnablePeerAccess(comms[k]->device_, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) hip_check(e, "hipDeviceEnablePeerAccess");
+      (void)hipGetLastError();
+    }
+  }
+  connected_ = true;
+}
+
+void XgmiComm::set_grid(int g) { grid_ = g > 0 ? g : default_grid(device_); }
+
+uint32_t XgmiComm::error() const {
+  uint32_t e = 0;
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipMemcpy(&e, ctl_ + 2, 4, hipMemcpyDeviceToHost), "hipMemcpy(err)");
+  return e;
+}
+
+void XgmiComm::clear_error() {
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipMemset(ctl_ + 2, 0, 4), "hipMemset(err)");
+}
+
+template <class E>
+static void launch_typed(const CommArgs& a, dim3 grid, hipStream_t s, bool oneshot) {
+  const dim3 b(kCommThreads);
+#define MXAR_LAUNCH(PT)                                                                         \
+  do {                                                                                          \
+    if (oneshot)                                                                                \
+      hipLaunchKernelGGL((oneshot_kernel<E, PT>), grid, b, 0, s, a);                            \
+    else                                                                                        \
+      hipLaunchKernelGGL((twoshot_kernel<E, PT>), grid, b, 0, s, a);                            \
+  } while (0)
+  switch (a.P) {
+    case 1: MXAR_LAUNCH(1); break;
+    case 2: MXAR_LAUNCH(2); break;
+    case 4: MXAR_LAUNCH(4); break;
+    case 8: MXAR_LAUNCH(8); break;
+    default: MXAR_LAUNCH(0); break;
+  }
+#undef MXAR_LAUNCH
+}
+
+// Common launch geometry + args for the ranks `group` (all on one device, consecutive
+// rank ids starting at group[0]->rank()).
+void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* const* ins, char* const* outs,
+                              int64_t n, DType dt, hipStream_t stream, bool oneshot) {
+  const XgmiComm& c0 = *group[0];
+  const int W = c0.world_;
+  const int64_t es = static_cast<int64_t>(dtype_size(dt));
+  const int64_t elems = 16 / es;
+  CommArgs a;
+  std::memset(&a, 0, sizeof(a));
+  for (size_t y = 0; y < group.size(); ++y) {
+    a.in[y] = ins[y];
+    a.out[y] = outs[y];
+    a.ctl[y] = group[y]->ctl_;
+  }
+  a.n = n;
+  a.P = W;
+  a.rank0 = c0.rank_;
+  a.maxch = c0.maxch_;
+  a.off_S = c0.off_S_;
+  a.off_R = c0.off_R_;
+  a.slot_bytes = c0.slot_bytes_;
+  a.timeout = static_cast<uint64_t>(c0.timeout_s_ * 1e8);
+  for (int k = 0; k < W; ++k) a.base[k] = c0.peers_[k];
+  const int64_t min_chunk = min_chunk_bytes() / es;
+  const int ranks_here = static_cast<int>(group.size());
+  const int gmax = std::max(1, c0.grid_ / ranks_here);  // all workgroups of the launch stay resident
+  int gx;
+  if (oneshot) {
+    a.block = n;
+    const int64_t target = std::max<int64_t>(1, gmax / W);
+    a.chunk = std::max(min_chunk, round_up(ceil_div(n, target), elems));
+    a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(n, a.chunk)));
+    gx = static_cast<int>(std::min<int64_t>(gmax, std::max<int64_t>(1, W * static_cast<int64_t>(a.nch))));
+  } else {
+    a.block = round_up(ceil_div(n, W), elems);
+    const int64_t target = W > 1 ? std::max<int64_t>(1, 2 * gmax / (W - 1)) : gmax;
+    a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, target), elems));
+    a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
+    const int64_t units = std::max<int64_t>((W - 1) * static_cast<int64_t>(a.nch), a.nch);
+    gx = static_cast<int>(std::min<int64_t>(gmax, std::max<int64_t>(1, units)));
+  }
+  if (a.nch > c0.maxch_ || a.block * es > c0.slot_bytes_ + 16)
+    throw std::logic_error("XgmiComm: segment geometry exceeds slab");
+  const dim3 grid(gx, ranks_here);
+  if (dt == DType::F32)
+    launch_typed<F32>(a, grid, stream, oneshot);
+  else
+    launch_typed<BF16>(a, grid, stream, oneshot);
+  hip_check(hipGetLastError(), "allreduce launch");
+  for (XgmiComm* c : group) {
+    ++c->stats_.launches;
+    ++(oneshot ? c->stats_.oneshot : c->stats_.twoshot);
+  }
+}
+
+void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
+                   const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, Algo algo) {
+  if (group.empty() || ins.size() != group.size() || outs.size() != group.size())
+    throw std::invalid_argument("XgmiComm: one input and one output per rank");
+  const XgmiComm& c0 = *group[0];
+  for (size_t y = 0; y < group.size(); ++y) {
+    const XgmiComm& c = *group[y];
+    if (!c.connected_) throw std::runtime_error("XgmiComm: connect() first");
+    if (c.device_ != c0.device_ || c.rank_ != c0.rank_ + static_cast<int>(y) || c.world_ != c0.world_)
+      throw std::invalid_argument("XgmiComm: a grouped launch needs consecutive ranks on one device");
+    if ((reinterpret_cast<uintptr_t>(ins[y]) | reinterpret_cast<uintptr_t>(outs[y])) & 15)
+      throw std::invalid_argument("XgmiComm: buffers must be 16-byte aligned");
+  }
+  if (n <= 0) return;
+  hip_check(hipSetDevice(c0.device_), "hipSetDevice");
+  const int64_t es = static_cast<int64_t>(dtype_size(dt));
+  for (XgmiComm* c : group) {
+    ++c->stats_.calls;
+    c->stats_.bytes += n * es;
+  }
+  const bool oneshot =
+      algo == Algo::OneShot ? (n * es <= c0.slot_bytes_) : (algo == Algo::Auto && n * es <= c0.oneshot_max_);
+  const int64_t seg = oneshot ? c0.slot_bytes_ / es : c0.world_ * (c0.slot_bytes_ / es);
+  std::vector<const char*> ip(group.size());
+  std::vector<char*> op(group.size());
+  for (int64_t off = 0; off < n; off += seg) {
+    const int64_t len = std::min(seg, n - off);
+    for (size_t y = 0; y < group.size(); ++y) {
+      ip[y] = static_cast<const char*>(ins[y]) + off * es;
+      op[y] = static_cast<char*>(outs[y]) + off * es;
+    }
+    launch_segment(group, ip.data(), op.data(), len, dt, stream, oneshot);
+  }
+}
+
+void XgmiComm::allreduce(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, Algo algo) {
+  run({this}, {in}, {out}, n, dt, stream, algo);
+}
+
+void XgmiComm::allreduce_local(const std::vector<XgmiComm*>& comms, const std::vector<const void*>& ins,
+                               const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, Algo algo) {
+  run(comms, ins, outs, n, dt, stream, algo);
+}
+
+void XgmiComm::barrier_group(const std::vector<XgmiComm*>& group, hipStream_t stream) {
+  const XgmiComm& c0 = *group[0];
+  for (XgmiComm* c : group)
+    if (!c->connected_) throw std::runtime_error("XgmiComm: connect() first");
+  hip_check(hipSetDevice(c0.device_), "hipSetDevice");
+  CommArgs a;
+  std::memset(&a, 0, sizeof(a));
+  for (size_t y = 0; y < group.size(); ++y) a.ctl[y] = group[y]->ctl_;
+  a.P = c0.world_;
+  a.rank0 = c0.rank_;
+  a.maxch = c0.maxch_;
+  a.timeout = static_cast<uint64_t>(c0.timeout_s_ * 1e8);
+  for (int k = 0; k < c0.world_; ++k) a.base[k] = c0.peers_[k];
+  hipLaunchKernelGGL(barrier_kernel, dim3(1, static_cast<unsigned>(group.size())), dim3(kCommThreads), 0, stream, a);
+  hip_check(hipGetLastError(), "barrier launch");
+}
+
+void XgmiComm::barrier(hipStream_t stream) { barrier_group({this}, stream); }
+
+}  // namespace mxar

@@ -1,0 +1,119 @@
+"""The fused xGMI allreduce kernels on one MI355X.
+
+* LocalCluster: P logical ranks in one process, one HIP stream each (connect_local).
+* Multi-process: P processes on the same GPU exchange hipIpcMemHandles over gloo and map
+  each other's slabs - the exact one-process-per-GPU path, minus the xGMI hop.
+Every result is compared with an fp32 torch reference summed in rank order.
+"""
+import os
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+from akka_allreduce_1_amd.ops import fill_uniform  # noqa: E402
+from akka_allreduce_1_amd.parallel import LocalCluster  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+
+
+def _ref(xs):
+    acc = torch.zeros(xs[0].numel(), device=xs[0].device)
+    for x in xs:
+        acc += x.float()
+    return acc
+
+
+def _tol(dtype, P):
+    return 0.0 if dtype == torch.float32 else 1e-2 * P
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("algo", ["twoshot", "oneshot"])
+@pytest.mark.parametrize("n", [1, 7, 1000, 65536 + 3, 1 << 20])
+def test_local_cluster_allreduce(P, dtype, algo, n):
+    cl = LocalCluster(P, slot_bytes=4 << 20, grid=32, timeout_s=10.0)
+    xs = [fill_uniform(torch.empty(n, dtype=dtype, device=DEV), seed=100 * P + k) for k in range(P)]
+    ys = cl.allreduce(xs, algo=algo)
+    cl.check()
+    ref = _ref(xs)
+    for y in ys:
+        err = (y.float() - ref).abs().max().item() if n else 0.0
+        assert err <= _tol(dtype, P) + (1e-6 if dtype == torch.float32 else 0), (P, dtype, algo, n, err)
+
+
+def test_local_cluster_inplace_and_repeated_epochs():
+    P = 4
+    cl = LocalCluster(P, slot_bytes=1 << 20, grid=8, timeout_s=10.0)
+    for it in range(6):
+        n = [4096, 300_000, 17][it % 3]
+        xs = [fill_uniform(torch.empty(n, device=DEV), seed=it * 10 + k) for k in range(P)]
+        ref = _ref(xs)
+        ys = cl.allreduce(xs, xs, algo="auto")  # in place
+        cl.check()
+        for y in ys:
+            assert torch.allclose(y, ref, atol=1e-5)
+
+
+def test_local_cluster_segments_larger_than_slab():
+    P = 2
+    cl = LocalCluster(P, slot_bytes=64 << 10, grid=8, timeout_s=10.0)
+    n = 100_000  # 400 KB fp32 > P * 64 KiB -> several launches
+    xs = [fill_uniform(torch.empty(n, device=DEV), seed=k) for k in range(P)]
+    ys = cl.allreduce(xs, algo="twoshot")
+    cl.check()
+    assert cl.comms[0].stats.launches > 1
+    for y in ys:
+        assert torch.allclose(y, _ref(xs), atol=1e-5)
+
+
+def _mp_worker(rank, world, port, results):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.parallel import XgmiCommunicator
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ok = True
+    msg = ""
+    try:
+        comm = XgmiCommunicator(device=0, slot_bytes=2 << 20, grid=8, timeout_s=15.0)
+        for dtype in (torch.float32, torch.bfloat16):
+            for n, algo in ((100_003, "twoshot"), (5_000, "oneshot"), (1 << 20, "auto")):
+                xs = [fill_uniform(torch.empty(n, dtype=dtype, device=DEV), seed=k) for k in range(world)]
+                y = comm.allreduce(xs[rank], algo=algo)
+                comm.check()
+                err = (y.float() - _ref(xs)).abs().max().item()
+                if err > _tol(dtype, world) + 1e-5:
+                    ok, msg = False, f"{dtype} {algo} n={n} err={err}"
+        comm.barrier()
+        comm.check()
+    except Exception as e:  # report, never hang the parent
+        ok, msg = False, repr(e)
+    results.put((rank, ok, msg))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_multiprocess_ipc_allreduce(world):
+    from akka_allreduce_1_amd.parallel import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_mp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = []
+    for _ in range(world):
+        res.append(q.get(timeout=240))
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    bad = [r for r in res if not r[1]]
+    assert not bad, bad
