@@ -22,9 +22,9 @@
 namespace mxar {
 namespace dev {
 
-struct alignas(16) Pack16 {
-  uint32_t w[4];
-};
+// 16-byte pack as a native 4 x u32 vector (a struct-of-array pack gets promoted to LDS
+// by the alloca promotion pass when several packs are in flight per lane).
+typedef unsigned int Pack16 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------------
 // dtype traits: E = element type tag, ELEMS = elements per 16-B pack
@@ -61,7 +61,7 @@ struct Acc<F32> {
   }
   __device__ __forceinline__ void add(const Pack16& p) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] += __uint_as_float(p.w[i]);
+    for (int i = 0; i < 4; ++i) v[i] += __uint_as_float(p[i]);
   }
   __device__ __forceinline__ void scale(float s) {
 #pragma unroll
@@ -70,7 +70,7 @@ struct Acc<F32> {
   __device__ __forceinline__ Pack16 pack() const {
     Pack16 p;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) p.w[i] = __float_as_uint(v[i]);
+    for (int i = 0; i < 4; ++i) p[i] = __float_as_uint(v[i]);
     return p;
   }
 };
@@ -85,8 +85,8 @@ struct Acc<BF16> {
   __device__ __forceinline__ void add(const Pack16& p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      v[2 * i] += bf16_to_f32(p.w[i] & 0xFFFFu);
-      v[2 * i + 1] += bf16_to_f32(p.w[i] >> 16);
+      v[2 * i] += bf16_to_f32(p[i] & 0xFFFFu);
+      v[2 * i + 1] += bf16_to_f32(p[i] >> 16);
     }
   }
   __device__ __forceinline__ void scale(float s) {
@@ -96,7 +96,7 @@ struct Acc<BF16> {
   __device__ __forceinline__ Pack16 pack() const {
     Pack16 p;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) p.w[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
+    for (int i = 0; i < 4; ++i) p[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
     return p;
   }
 };
@@ -129,6 +129,62 @@ __device__ __forceinline__ Pack16 ld16(const void* p) { return *static_cast<cons
 __device__ __forceinline__ void st16(void* p, const Pack16& v) { *static_cast<Pack16*>(p) = v; }
 
 // ---------------------------------------------------------------------------------
+// Slab reads: `buffer_load ... sc1` bypasses the reading CU's L1, and the slab itself is
+// uncached device memory (no L2 copy), so every slab load reads what the peers' xGMI
+// stores left in HBM - no acquire fence (L1/L2 invalidate) is needed before it.
+// Descriptor built from wave-uniform values only (cdna_hip_programming.md T8/T20).
+// ---------------------------------------------------------------------------------
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+constexpr int kAuxSc1 = 16;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), static_cast<short>(0), 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ Pack16 ld16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, kAuxSc1);
+}
+// Slab writes: `buffer_store ... sc0 sc1` = system-coherent write-through. A drained
+// (`s_waitcnt vmcnt(0)`) write-through store has reached memory, so the flag that follows
+// needs no `buffer_wbl2` release (which would also write back every unrelated dirty L2
+// line, e.g. the output) - the guide's R1 hand-off, at system scope for xGMI peers.
+constexpr int kAuxWt = 17;  // sc0 | sc1
+__device__ __forceinline__ void st16_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, const Pack16& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, static_cast<int>(off), 0, kAuxWt);
+}
+template <class E>
+__device__ __forceinline__ void st_scalar_wt(__amdgpu_buffer_rsrc_t r, int64_t i, float x);
+template <>
+__device__ __forceinline__ void st_scalar_wt<F32>(__amdgpu_buffer_rsrc_t r, int64_t i, float x) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, static_cast<int>(i * 4), 0, kAuxWt);
+}
+template <>
+__device__ __forceinline__ void st_scalar_wt<BF16>(__amdgpu_buffer_rsrc_t r, int64_t i, float x) {
+  __builtin_amdgcn_raw_buffer_store_b16(static_cast<unsigned short>(pack_bf16x2(x, 0.f) & 0xFFFFu), r,
+                                        static_cast<int>(i * 2), 0, kAuxWt);
+}
+template <class E>
+__device__ __forceinline__ void copy_scalar_wt(__amdgpu_buffer_rsrc_t r, const void* src, int64_t i);
+template <>
+__device__ __forceinline__ void copy_scalar_wt<F32>(__amdgpu_buffer_rsrc_t r, const void* src, int64_t i) {
+  __builtin_amdgcn_raw_buffer_store_b32(static_cast<const uint32_t*>(src)[i], r, static_cast<int>(i * 4), 0, kAuxWt);
+}
+template <>
+__device__ __forceinline__ void copy_scalar_wt<BF16>(__amdgpu_buffer_rsrc_t r, const void* src, int64_t i) {
+  __builtin_amdgcn_raw_buffer_store_b16(static_cast<const uint16_t*>(src)[i], r, static_cast<int>(i * 2), 0, kAuxWt);
+}
+
+template <class E>
+__device__ __forceinline__ float ld_scalar_sc1(__amdgpu_buffer_rsrc_t r, int64_t i);
+template <>
+__device__ __forceinline__ float ld_scalar_sc1<F32>(__amdgpu_buffer_rsrc_t r, int64_t i) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(i * 4), 0, kAuxSc1));
+}
+template <>
+__device__ __forceinline__ float ld_scalar_sc1<BF16>(__amdgpu_buffer_rsrc_t r, int64_t i) {
+  return bf16_to_f32(__builtin_amdgcn_raw_buffer_load_b16(r, static_cast<int>(i * 2), 0, kAuxSc1));
+}
+
+// ---------------------------------------------------------------------------------
 // Clock + bounded spin
 // ---------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t wall_ticks() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
@@ -153,13 +209,15 @@ __device__ __forceinline__ bool reached(uint32_t flag, uint32_t epoch) {
 
 // Producer side: called by ALL threads of the workgroup after their payload stores.
 // Lane i < nflags of wave 0 stores flag `addr(i)` (skipped when it returns nullptr).
+// `release` = false drops the system-scope release fence (measurement knob only: the
+// payload then relies on the vmcnt drain of stores to uncached memory).
 template <typename FlagAddr>
-__device__ __forceinline__ void publish_flags(FlagAddr addr, int nflags, uint32_t epoch) {
+__device__ __forceinline__ void publish_flags(FlagAddr addr, int nflags, uint32_t epoch, bool release = true) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
   __syncthreads();
   if (threadIdx.x < static_cast<unsigned>(nflags)) {
     uint32_t* f = addr(static_cast<int>(threadIdx.x));
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope (xGMI peers)
+    if (release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope (xGMI peers)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (f) st_flag(f, epoch);
   }
@@ -171,7 +229,7 @@ __device__ __forceinline__ void publish_flags(FlagAddr addr, int nflags, uint32_
 // into the error word. On success the payload may be read with plain loads.
 template <typename FlagAddr>
 __device__ __forceinline__ bool wait_flags(FlagAddr addr, int nflags, uint32_t epoch, uint64_t deadline,
-                                           uint32_t* err, uint32_t code) {
+                                           uint32_t* err, uint32_t code, bool acquire = true) {
   __shared__ int ok_s;
   if (threadIdx.x < 64) {
     const uint32_t* f = threadIdx.x < static_cast<unsigned>(nflags) ? addr(static_cast<int>(threadIdx.x)) : nullptr;
@@ -186,7 +244,7 @@ __device__ __forceinline__ bool wait_flags(FlagAddr addr, int nflags, uint32_t e
       ok_s = all_ok ? 1 : 0;
       if (!all_ok) __hip_atomic_fetch_or(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+    if (acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();

@@ -87,6 +87,7 @@ void bind_hip(py::module_& m) {
       .def_property_readonly("slab_bytes", &XgmiComm::slab_bytes)
       .def_property_readonly("connected", &XgmiComm::connected)
       .def_property_readonly("stats", &XgmiComm::stats)
+      .def_property("fence", &XgmiComm::fence, &XgmiComm::set_fence)
       .def("set_timeout", &XgmiComm::set_timeout);
 
   h.def(

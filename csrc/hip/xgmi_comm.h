@@ -84,6 +84,11 @@ class XgmiComm {
   void set_oneshot_max_bytes(int64_t b) { oneshot_max_ = b; }
   void set_grid(int g);
   void set_timeout(double s) { timeout_s_ = s; }
+  // bit0: system-scope release fence before each flag store, bit1: system-scope acquire
+  // after each wait. Default 2: payload stores are write-through (sc0 sc1) and drained
+  // before the flag, so the release's L2 write-back is not needed; 3 adds it anyway.
+  int fence() const { return fence_; }
+  void set_fence(int f) { fence_ = f & 3; }
   bool connected() const { return connected_; }
   const CommStats& stats() const { return stats_; }
   char* slab() const { return slab_; }
@@ -100,6 +105,7 @@ class XgmiComm {
   int64_t slot_bytes_, maxch_, off_S_, off_R_, off_B_, slab_bytes_;
   int64_t oneshot_max_;
   double timeout_s_;
+  int fence_ = 2;
   char* slab_ = nullptr;            // own uncached slab (flags | S | R)
   uint32_t* ctl_ = nullptr;         // [0] epoch, [1] ticket, [2] sticky error (device memory)
   char* peers_[kMaxRanks] = {};     // slab base of every rank (own included)

@@ -38,11 +38,13 @@ struct CommArgs {
   uint32_t* ctl[kMaxRanks];  // per rank: [0] epoch [1] ticket [2] error
   int64_t n;      // elements in this segment
   int64_t block;  // elements per block (two-shot) / whole segment (one-shot)
-  int64_t chunk;  // elements per chunk (work unit)
+  int64_t chunk;  // elements per chunk (scatter / gather work unit)
+  int64_t subchunk;  // elements per reduce work unit (chunk split `sub` ways)
   int nch;        // chunks per block
+  int sub;        // reduce units per chunk
   int P;
   int rank0;
-  int pad_;
+  int fence;      // bit0: system release before flags, bit1: system acquire after waits
   int64_t maxch;
   int64_t off_S, off_R, slot_bytes;
   uint64_t timeout;
@@ -62,12 +64,13 @@ __device__ __forceinline__ int64_t clamp_len(int64_t avail, int64_t cap) {
   return avail <= 0 ? 0 : (avail < cap ? avail : cap);
 }
 
-// Copy len elements, 16 B per lane, 4 packs in flight per lane.
+// Push len elements from ordinary memory into a (peer's) slab with write-through stores,
+// 16 B per lane, 4 packs in flight per lane.
 template <class E>
-__device__ __forceinline__ void copy_elems(char* dst, const char* src, int64_t len) {
+__device__ __forceinline__ void copy_to_slab(char* slab_dst, const char* src, int64_t len) {
   const int64_t npk = len / E::ELEMS;
   const Pack16* s = reinterpret_cast<const Pack16*>(src);
-  Pack16* d = reinterpret_cast<Pack16*>(dst);
+  const __amdgpu_buffer_rsrc_t rd = slab_rsrc(slab_dst);
   int64_t i = threadIdx.x;
   constexpr int U = 4;
   for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
@@ -75,74 +78,117 @@ __device__ __forceinline__ void copy_elems(char* dst, const char* src, int64_t l
 #pragma unroll
     for (int u = 0; u < U; ++u) v[u] = s[i + u * kCommThreads];
 #pragma unroll
+    for (int u = 0; u < U; ++u) st16_wt(rd, static_cast<uint32_t>((i + u * kCommThreads) * 16), v[u]);
+  }
+  for (; i < npk; i += kCommThreads) st16_wt(rd, static_cast<uint32_t>(i * 16), s[i]);
+  const int64_t t = npk * E::ELEMS + threadIdx.x;
+  if (t < len) copy_scalar_wt<E>(rd, src, t);
+}
+
+// Copy len elements out of an uncached slab (sc1 loads), 4 packs in flight per lane.
+template <class E>
+__device__ __forceinline__ void copy_from_slab(char* dst, const char* slab_src, int64_t len) {
+  const int64_t npk = len / E::ELEMS;
+  const __amdgpu_buffer_rsrc_t rs = slab_rsrc(slab_src);
+  Pack16* d = reinterpret_cast<Pack16*>(dst);
+  int64_t i = threadIdx.x;
+  constexpr int U = 4;
+  for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
+    Pack16 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld16_sc1(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
+#pragma unroll
     for (int u = 0; u < U; ++u) d[i + u * kCommThreads] = v[u];
   }
-  for (; i < npk; i += kCommThreads) d[i] = s[i];
+  for (; i < npk; i += kCommThreads) d[i] = ld16_sc1(rs, static_cast<uint32_t>(i * 16));
   const int64_t t = npk * E::ELEMS + threadIdx.x;
-  if (t < len) Scalar<E>::copy(dst, src, t);
+  if (t < len) Scalar<E>::store(dst, t, ld_scalar_sc1<E>(rs, t));
 }
+
+// Reduction sources: source s is at slab0 + s * stride, except source `own` (if >= 0),
+// which is the rank's own input. Every source is read with sc1 buffer loads through a
+// descriptor chosen by a scalar select, so the P loads of a pack issue back to back
+// with no per-source branch (and the own input is simply L1-bypassing).
+struct RedSrc {
+  const char* own_ptr;
+  const char* slab0;
+  int64_t stride;
+  int own;
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(int s) const {
+    return slab_rsrc(s == own ? own_ptr : slab0 + s * stride);
+  }
+};
 
 // Sum P sources (fixed order s = 0..P-1, fp32) and store the result to up to P
 // destinations. src(s) / dst(k) return byte pointers to element 0 of the chunk.
-template <class E, int PT, class SrcF, class DstF>
-__device__ __forceinline__ void reduce_to(int P, SrcF src, int ndst, DstF dst, int64_t len) {
-  constexpr int es = 16 / E::ELEMS;
+// Destinations of a reduced chunk: k == own is the rank's own output (plain stores),
+// every other k is a peer slab written through (sc0 sc1).
+template <class E, int PT, class DstF>
+__device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, int own_dst, DstF dst, int64_t len) {
   const int64_t npk = len / E::ELEMS;
   constexpr int U = 2;
   int64_t i = threadIdx.x;
-  for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
-    Acc<E> acc[U];
+  if constexpr (PT > 0) {
+    __amdgpu_buffer_rsrc_t rs[PT];
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc[u].zero();
-    if constexpr (PT > 0) {
+    for (int s = 0; s < PT; ++s) rs[s] = src.rsrc(s);
+    for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
       Pack16 v[PT][U];
 #pragma unroll
       for (int s = 0; s < PT; ++s)
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[s][u] = ld16(src(s) + (i + u * kCommThreads) * 16);
+        for (int u = 0; u < U; ++u) v[s][u] = ld16_sc1(rs[s], static_cast<uint32_t>((i + u * kCommThreads) * 16));
+      Acc<E> acc[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u].zero();
 #pragma unroll
       for (int s = 0; s < PT; ++s)
 #pragma unroll
         for (int u = 0; u < U; ++u) acc[u].add(v[s][u]);
-    } else {
-      for (int s = 0; s < P; ++s) {
-        Pack16 v[U];
+      Pack16 o[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = ld16(src(s) + (i + u * kCommThreads) * 16);
+      for (int u = 0; u < U; ++u) o[u] = acc[u].pack();
+      for (int k = 0; k < ndst; ++k) {
+        char* d = dst(k);
+        if (d == nullptr) continue;
+        if (k == own_dst) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) acc[u].add(v[u]);
+          for (int u = 0; u < U; ++u) st16(d + (i + u * kCommThreads) * 16, o[u]);
+        } else {
+          const __amdgpu_buffer_rsrc_t rd = slab_rsrc(d);
+#pragma unroll
+          for (int u = 0; u < U; ++u) st16_wt(rd, static_cast<uint32_t>((i + u * kCommThreads) * 16), o[u]);
+        }
       }
-    }
-    Pack16 o[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) o[u] = acc[u].pack();
-    for (int k = 0; k < ndst; ++k) {
-      char* d = dst(k);
-      if (d == nullptr) continue;
-#pragma unroll
-      for (int u = 0; u < U; ++u) st16(d + (i + u * kCommThreads) * 16, o[u]);
     }
   }
   for (; i < npk; i += kCommThreads) {
     Acc<E> acc;
     acc.zero();
-    for (int s = 0; s < P; ++s) acc.add(ld16(src(s) + i * 16));
+    for (int s = 0; s < P; ++s) acc.add(ld16_sc1(src.rsrc(s), static_cast<uint32_t>(i * 16)));
     const Pack16 o = acc.pack();
     for (int k = 0; k < ndst; ++k) {
       char* d = dst(k);
-      if (d) st16(d + i * 16, o);
+      if (d == nullptr) continue;
+      if (k == own_dst)
+        st16(d + i * 16, o);
+      else
+        st16_wt(slab_rsrc(d), static_cast<uint32_t>(i * 16), o);
     }
   }
   const int64_t t = npk * E::ELEMS + threadIdx.x;
   if (t < len) {
     float acc = 0.f;
-    for (int s = 0; s < P; ++s) acc += Scalar<E>::load(src(s), t);
+    for (int s = 0; s < P; ++s) acc += ld_scalar_sc1<E>(src.rsrc(s), t);
     for (int k = 0; k < ndst; ++k) {
       char* d = dst(k);
-      if (d) Scalar<E>::store(d, t, acc);
+      if (d == nullptr) continue;
+      if (k == own_dst)
+        Scalar<E>::store(d, t, acc);
+      else
+        st_scalar_wt<E>(slab_rsrc(d), t, acc);
     }
   }
-  (void)es;
 }
 
 // The rank's last workgroup to finish publishes the epoch for the next launch.
@@ -178,6 +224,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
   const int G = gridDim.x;
   const int64_t slot = a.slot_bytes;
   uint32_t* err = &ctl[2];
+  const bool rel = a.fence & 1, acq = a.fence & 2;
   const int Pm1 = P > 1 ? P - 1 : 1;
   const int nu = (P - 1) * a.nch;
 
@@ -189,29 +236,35 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
     const int64_t bstart = static_cast<int64_t>(j) * a.block;
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
-    if (len > 0) copy_elems<E>(a.base[j] + a.off_S + r * slot + cstart * es, in + (bstart + cstart) * es, len);
-    publish_flags([&](int) { return f1(a, j, r, c); }, 1, epoch);
+    if (len > 0) copy_to_slab<E>(a.base[j] + a.off_S + r * slot + cstart * es, in + (bstart + cstart) * es, len);
+    publish_flags([&](int) { return f1(a, j, r, c); }, 1, epoch, rel);
   }
 
-  // Phase 2 - reduce own block chunk by chunk once all P contributions have arrived
-  // (thReduce = 1), then ReduceBlock-broadcast the sum into every rank's R slot.
+  // Phase 2 - reduce own block once all P contributions of a chunk have arrived
+  // (thReduce = 1), then ReduceBlock-broadcast the sum into every rank's R slot. A chunk
+  // is reduced in `sub` pieces by different workgroups so that phase 2 has as many
+  // units as phases 1 and 3 (each piece pays one acquire and one release).
   const int64_t bstart_own = static_cast<int64_t>(r) * a.block;
   const int64_t blen_own = clamp_len(a.n - bstart_own, a.block);
-  for (int c = blockIdx.x; c < a.nch; c += G) {
-    const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
-    const int64_t len = clamp_len(blen_own - cstart, a.chunk);
+  const int nu2 = a.nch * a.sub;
+  for (int u = blockIdx.x; u < nu2; u += G) {
+    const int c = u / a.sub;
+    const int q = u % a.sub;
+    const int64_t cbeg = static_cast<int64_t>(c) * a.chunk;
+    const int64_t qbeg = static_cast<int64_t>(q) * a.subchunk;
+    const int64_t cstart = cbeg + qbeg;
+    const int64_t len = clamp_len(clamp_len(blen_own - cbeg, a.chunk) - qbeg, a.subchunk);
     wait_flags([&](int s) -> const uint32_t* { return s == r ? nullptr : f1(a, r, s, c); }, P, epoch, deadline, err,
-               ERR_TIMEOUT_SCATTER);
+               ERR_TIMEOUT_SCATTER, acq);
     if (len > 0) {
       const char* own_in = in + (bstart_own + cstart) * es;
       const char* S = a.base[r] + a.off_S + cstart * es;
       char* own_out = out + (bstart_own + cstart) * es;
       const int64_t roff = a.off_R + r * slot + cstart * es;
-      reduce_to<E, PT>(
-          P, [&](int s) -> const char* { return s == r ? own_in : S + s * slot; }, P,
-          [&](int k) -> char* { return k == r ? own_out : a.base[k] + roff; }, len);
+      const RedSrc src{own_in, S, slot, r};
+      reduce_to<E, PT>(P, src, P, r, [&](int k) -> char* { return k == r ? own_out : a.base[k] + roff; }, len);
     }
-    publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : f2(a, k, r, c); }, P, epoch);
+    publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : f2(a, k, r, u); }, P, epoch, rel);
   }
 
   // Phase 3 - complete: gather the other owners' reduced chunks into the output.
@@ -221,8 +274,9 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
     const int64_t bstart = static_cast<int64_t>(j) * a.block;
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
-    wait_flags([&](int) -> const uint32_t* { return f2(a, r, j, c); }, 1, epoch, deadline, err, ERR_TIMEOUT_REDUCE);
-    if (len > 0) copy_elems<E>(out + (bstart + cstart) * es, a.base[r] + a.off_R + j * slot + cstart * es, len);
+    wait_flags([&](int q) -> const uint32_t* { return f2(a, r, j, c * a.sub + q); }, a.sub, epoch, deadline, err,
+               ERR_TIMEOUT_REDUCE, acq);
+    if (len > 0) copy_from_slab<E>(out + (bstart + cstart) * es, a.base[r] + a.off_R + j * slot + cstart * es, len);
   }
   finish_launch(ctl, epoch);
 }
@@ -246,24 +300,26 @@ __global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
   const int G = gridDim.x;
   const int64_t slot = a.slot_bytes;
   uint32_t* err = &ctl[2];
+  const bool rel = a.fence & 1, acq = a.fence & 2;
   const int nu = P * a.nch;
   for (int u = blockIdx.x; u < nu; u += G) {
     const int c = u / P;
     const int j = (r + 1 + u % P) % P;
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     const int64_t len = clamp_len(a.n - cstart, a.chunk);
-    if (len > 0) copy_elems<E>(a.base[j] + a.off_S + r * slot + cstart * es, in + cstart * es, len);
-    publish_flags([&](int) { return f1(a, j, r, c); }, 1, epoch);
+    if (len > 0) copy_to_slab<E>(a.base[j] + a.off_S + r * slot + cstart * es, in + cstart * es, len);
+    publish_flags([&](int) { return f1(a, j, r, c); }, 1, epoch, rel);
   }
   for (int c = blockIdx.x; c < a.nch; c += G) {
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     const int64_t len = clamp_len(a.n - cstart, a.chunk);
-    wait_flags([&](int s) -> const uint32_t* { return f1(a, r, s, c); }, P, epoch, deadline, err, ERR_TIMEOUT_SCATTER);
+    wait_flags([&](int s) -> const uint32_t* { return f1(a, r, s, c); }, P, epoch, deadline, err, ERR_TIMEOUT_SCATTER,
+               acq);
     if (len > 0) {
       const char* S = a.base[r] + a.off_S + cstart * es;
       char* o = out + cstart * es;
-      reduce_to<E, PT>(
-          P, [&](int s) -> const char* { return S + s * slot; }, 1, [&](int) -> char* { return o; }, len);
+      const RedSrc src{nullptr, S, slot, -1};
+      reduce_to<E, PT>(P, src, 1, 0, [&](int) -> char* { return o; }, len);
     }
   }
   finish_launch(ctl, epoch);
@@ -307,6 +363,7 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   oneshot_max_ = std::min<int64_t>(slot_bytes_, 256 * 1024);
   if (const char* e = std::getenv("MXAR_ONESHOT_MAX")) oneshot_max_ = std::min<int64_t>(slot_bytes_, std::atoll(e));
   if (grid_ <= 0) grid_ = default_grid(device);
+  if (const char* f = std::getenv("MXAR_FENCE")) fence_ = std::atoi(f) & 3;
 
   hip_check(hipSetDevice(device_), "hipSetDevice");
   const char* mem = std::getenv("MXAR_SLAB_MEM");
@@ -436,21 +493,31 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   const int ranks_here = static_cast<int>(group.size());
   const int gmax = std::max(1, c0.grid_ / ranks_here);  // all workgroups of the launch stay resident
   int gx;
+  a.sub = 1;
   if (oneshot) {
     a.block = n;
     const int64_t target = std::max<int64_t>(1, gmax / W);
     a.chunk = std::max(min_chunk, round_up(ceil_div(n, target), elems));
     a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(n, a.chunk)));
+    a.subchunk = a.chunk;
     gx = static_cast<int>(std::min<int64_t>(gmax, std::max<int64_t>(1, W * static_cast<int64_t>(a.nch))));
   } else {
+    // ~one scatter unit and one gather unit per workgroup: every unit pays one fence, so
+    // units are as large as the parallelism allows. The reduce phase splits each chunk
+    // W-1 ways to keep the same unit count.
     a.block = round_up(ceil_div(n, W), elems);
-    const int64_t target = W > 1 ? std::max<int64_t>(1, 2 * gmax / (W - 1)) : gmax;
+    const int64_t target = W > 1 ? std::max<int64_t>(1, gmax / (W - 1)) : gmax;
     a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, target), elems));
     a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
-    const int64_t units = std::max<int64_t>((W - 1) * static_cast<int64_t>(a.nch), a.nch);
+    int64_t sub = std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(W - 1), a.chunk / min_chunk, 64,
+                                                          c0.maxch_ / a.nch}));
+    a.subchunk = round_up(ceil_div(a.chunk, sub), elems);
+    a.sub = static_cast<int>(ceil_div(a.chunk, a.subchunk));
+    const int64_t units = std::max<int64_t>((W - 1) * static_cast<int64_t>(a.nch), static_cast<int64_t>(a.nch) * a.sub);
     gx = static_cast<int>(std::min<int64_t>(gmax, std::max<int64_t>(1, units)));
   }
-  if (a.nch > c0.maxch_ || a.block * es > c0.slot_bytes_ + 16)
+  a.fence = c0.fence_;
+  if (static_cast<int64_t>(a.nch) * a.sub > c0.maxch_ || a.block * es > c0.slot_bytes_ + 16)
     throw std::logic_error("XgmiComm: segment geometry exceeds slab");
   const dim3 grid(gx, ranks_here);
   if (dt == DType::F32)
@@ -483,6 +550,12 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
   for (XgmiComm* c : group) {
     ++c->stats_.calls;
     c->stats_.bytes += n * es;
+  }
+  if (c0.world_ == 1) {  // a 1-rank allreduce is the identity: copy out-of-place, nothing in place
+    for (size_t y = 0; y < group.size(); ++y)
+      if (ins[y] != outs[y])
+        hip_check(hipMemcpyAsync(outs[y], ins[y], n * es, hipMemcpyDeviceToDevice, stream), "hipMemcpyAsync");
+    return;
   }
   const bool oneshot =
       algo == Algo::OneShot ? (n * es <= c0.slot_bytes_) : (algo == Algo::Auto && n * es <= c0.oneshot_max_);
@@ -520,6 +593,7 @@ void XgmiComm::barrier_group(const std::vector<XgmiComm*>& group, hipStream_t st
   a.rank0 = c0.rank_;
   a.maxch = c0.maxch_;
   a.timeout = static_cast<uint64_t>(c0.timeout_s_ * 1e8);
+  a.fence = 3;
   for (int k = 0; k < c0.world_; ++k) a.base[k] = c0.peers_[k];
   hipLaunchKernelGGL(barrier_kernel, dim3(1, static_cast<unsigned>(group.size())), dim3(kCommThreads), 0, stream, a);
   hip_check(hipGetLastError(), "barrier launch");

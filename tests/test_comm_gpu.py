@@ -30,6 +30,17 @@ def _tol(dtype, P):
     return 0.0 if dtype == torch.float32 else 1e-2 * P
 
 
+def _diag(y, ref, xs, rank):
+    """Where a wrong result differs (helps tell a stale read from a missing contribution)."""
+    bad = ((y.float() - ref).abs() > 1e-3).nonzero().flatten()
+    if bad.numel() == 0:
+        return "no bad elements"
+    i = int(bad[0])
+    own = xs[rank].float()[i].item()
+    return (f"{bad.numel()} bad, first idx {i} last {int(bad[-1])}, y={y[i].item():.4f} ref={ref[i].item():.4f} "
+            f"own={own:.4f}")
+
+
 @pytest.mark.parametrize("P", [1, 2, 3, 4])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("algo", ["twoshot", "oneshot"])
@@ -40,9 +51,10 @@ def test_local_cluster_allreduce(P, dtype, algo, n):
     ys = cl.allreduce(xs, algo=algo)
     cl.check()
     ref = _ref(xs)
-    for y in ys:
+    for k, y in enumerate(ys):
         err = (y.float() - ref).abs().max().item() if n else 0.0
-        assert err <= _tol(dtype, P) + (1e-6 if dtype == torch.float32 else 0), (P, dtype, algo, n, err)
+        assert err <= _tol(dtype, P) + (1e-6 if dtype == torch.float32 else 0), (P, dtype, algo, n, err, k,
+                                                                                _diag(y, ref, xs, k))
 
 
 def test_local_cluster_inplace_and_repeated_epochs():

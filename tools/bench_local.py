@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""Single-GPU analysis bench: P logical ranks of the fused allreduce on ONE MI355X.
+
+All ranks' traffic lands in one GPU's HBM (no xGMI hop), so this measures the kernel's
+own costs - fences, flag hand-offs, unit geometry, HBM efficiency - not link bandwidth.
+HBM bytes per rank for a two-shot of S bytes (bf16): read S + write S(P-1)/P (scatter),
+read S + write S (reduce + broadcast), read S(P-1)/P + write S(P-1)/P (gather).
+
+    python tools/bench_local.py --ranks 2 4 8 --sizes 1M 16M 256M --fence 3 0
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from akka_allreduce_1_amd.ops import fill_uniform  # noqa: E402
+from akka_allreduce_1_amd.parallel import LocalCluster  # noqa: E402
+from akka_allreduce_1_amd.utils.timing import percentile  # noqa: E402
+
+
+def parse_size(s: str) -> int:
+    m = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}
+    return int(float(s[:-1]) * m[s[-1].upper()]) if s[-1].upper() in m else int(s)
+
+
+def hbm_bytes(S: int, P: int, algo: str) -> float:
+    if algo == "oneshot":
+        return P * (S + S * P + S * P + S)  # read in, write P slots, read P slots, write out
+    return P * (S + S * (P - 1) / P + S + S + 2 * S * (P - 1) / P)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ranks", type=int, nargs="+", default=[2, 4, 8])
+    ap.add_argument("--sizes", nargs="+", default=["64K", "1M", "16M", "64M", "256M"])
+    ap.add_argument("--algos", nargs="+", default=["twoshot", "oneshot"])
+    ap.add_argument("--fence", type=int, nargs="+", default=[2])
+    ap.add_argument("--grid", type=int, default=512)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    es = 2 if dtype == torch.bfloat16 else 4
+    rows = []
+    # reference: device copy bandwidth
+    x = torch.empty(256 << 20, dtype=torch.uint8, device=dev)
+    y = torch.empty_like(x)
+    for _ in range(3):
+        y.copy_(x)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        y.copy_(x)
+    e1.record()
+    torch.cuda.synchronize()
+    copy_ms = e0.elapsed_time(e1) / 10
+    print(json.dumps({"copy_256MiB_ms": round(copy_ms, 4), "copy_TBps": round(2 * x.numel() / copy_ms / 1e9, 2)}))
+    del x, y
+    for P in args.ranks:
+        max_sz = max(parse_size(s) for s in args.sizes)
+        slot = max(1 << 20, -(-max_sz // P) + (1 << 16))
+        cl = LocalCluster(P, slot_bytes=slot, grid=args.grid, timeout_s=10.0)
+        for sz_s in args.sizes:
+            S = parse_size(sz_s)
+            n = S // es
+            xs = [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=k) for k in range(P)]
+            ys = [torch.empty_like(t) for t in xs]
+            ref = torch.zeros(n, device=dev)
+            for t in xs:
+                ref += t.float()
+            for algo in args.algos:
+                if algo == "oneshot" and S > slot:
+                    continue
+                for fence in args.fence:
+                    for c in cl.comms:
+                        c.fence = fence
+                    cl.allreduce(xs, ys, algo=algo)
+                    cl.check()
+                    err = max((t.float() - ref).abs().max().item() for t in ys)
+                    for _ in range(3):
+                        cl.allreduce(xs, ys, algo=algo)
+                    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                          for _ in range(args.iters)]
+                    for a, b in ev:
+                        a.record()
+                        cl.allreduce(xs, ys, algo=algo)
+                        b.record()
+                    cl.check()
+                    ts = [a.elapsed_time(b) for a, b in ev]
+                    p50 = percentile(ts, 50)
+                    row = {"P": P, "bytes": S, "algo": algo, "fence": fence, "p50_us": round(p50 * 1e3, 1),
+                           "min_us": round(min(ts) * 1e3, 1), "hbm_TBps": round(hbm_bytes(S, P, algo) / p50 / 1e9, 2),
+                           "max_err": err}
+                    rows.append(row)
+                    print(json.dumps(row), flush=True)
+            del xs, ys, ref
+        for c in cl.comms:
+            c.fence = 2
+        del cl
+        torch.cuda.empty_cache()
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump({"copy_ms": copy_ms, "rows": rows}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
