@@ -1,2 +1,3 @@
 """Distributed data plane: xGMI communicators, RCCL baseline, bucketed DP gradient reducer."""
 from .comm import CommError, LocalCluster, XgmiCommunicator, free_port, init_distributed  # noqa: F401
+from .ddp import BucketedGradReducer, TorchDistComm, bucket_sizes  # noqa: F401,E402

@@ -91,16 +91,98 @@ class XgmiCommunicator:
             device = torch.cuda.current_device()
         self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
         self.slot_bytes = int(slot_bytes or DEFAULT_SLOT_BYTES)
-        self._c = _H.XgmiComm(self.rank, self.world, self.device.index, self.slot_bytes, grid, timeout_s)
         if cpu_group is None:
             backend = dist.get_backend(group)
             cpu_group = group if backend == "gloo" else dist.new_group(
                 ranks=None if group is None else dist.get_process_group_ranks(group), backend="gloo")
         self.cpu_group = cpu_group
+        # Every step that can fail locally is followed by an all-gather of its status, so a
+        # failure on one rank raises on every rank instead of leaving the others blocked in
+        # the next collective.
+        self._c, handle, err = None, None, ""
+        try:
+            self._c = _H.XgmiComm(self.rank, self.world, self.device.index, self.slot_bytes, grid, timeout_s)
+            handle = self._c.ipc_handle()
+        except Exception as e:  # noqa: BLE001
+            err = f"rank {self.rank}: {e}"
         handles: list = [None] * self.world
-        dist.all_gather_object(handles, self._c.ipc_handle(), group=cpu_group)
-        self._c.connect(handles)
-        dist.barrier(group=cpu_group)
+        dist.all_gather_object(handles, (handle, err), group=cpu_group)
+        errs = [e for _, e in handles if e]
+        if errs:
+            raise CommError("XgmiCommunicator setup failed: " + "; ".join(errs))
+        try:
+            self._c.connect([h for h, _ in handles])
+        except Exception as e:  # noqa: BLE001
+            err = f"rank {self.rank}: {e}"
+        status: list = [None] * self.world
+        dist.all_gather_object(status, err, group=cpu_group)
+        errs = [e for e in status if e]
+        if errs:
+            raise CommError("XgmiCommunicator connect failed: " + "; ".join(errs))
+        self.table: list[tuple[int, str]] = []  # (max bytes, algo) from tune(); empty = built-in policy
+
+    # ------------------------------------------------------------------ tuning
+    def tune(self, max_bytes: int = 256 << 20, dtype: torch.dtype = torch.bfloat16, iters: int = 10,
+             candidates: Sequence[str] = ("oneshot", "twoshot", "rccl"), min_bytes: int = 4 << 10) -> list[dict]:
+        """Measure p50 latency of every algorithm per power-of-4 size class in
+        [min_bytes, max_bytes] and keep the fastest per class (the slowest rank's p50
+        decides; rank 0's choice is broadcast so every rank dispatches identically - a split
+        decision would deadlock). Returns one row per size: {bytes, <algo>_p50_us, choice}."""
+        import torch.distributed as dist
+
+        from ..ops import fill_uniform
+        from ..utils.timing import percentile
+
+        es = torch.empty(0, dtype=dtype).element_size()
+        x = fill_uniform(torch.empty(max_bytes // es, dtype=dtype, device=self.device), seed=self.rank)
+        y = torch.empty_like(x)
+        src0 = 0 if self.cpu_group is None else dist.get_global_rank(self.cpu_group, 0)
+        rows, table = [], []
+        sizes, size = [], min_bytes
+        while size < max_bytes:
+            sizes.append(size)
+            size *= 4
+        sizes.append(max_bytes)
+        for size in sizes:
+            n = size // es
+            best, best_t, row = None, float("inf"), {"bytes": size}
+            for algo in candidates:
+                if algo == "oneshot" and (size > self.slot_bytes or size > (8 << 20)):
+                    continue
+                if algo == "rccl" and dist.get_backend(self.group) != "nccl":
+                    continue
+                a, b = x[:n], y[:n]
+                for _ in range(2):
+                    self.allreduce(a, b, algo=algo)
+                evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                       for _ in range(iters)]
+                torch.cuda.synchronize(self.device)
+                for e0, e1 in evs:
+                    e0.record()
+                    self.allreduce(a, b, algo=algo)
+                    e1.record()
+                torch.cuda.synchronize(self.device)
+                p50 = percentile([e0.elapsed_time(e1) for e0, e1 in evs], 50)
+                t = torch.tensor([p50], device=self.device, dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+                row[f"{algo}_p50_us"] = round(t.item() * 1e3, 2)
+                row[f"{algo}_algbw"] = round(size / (t.item() / 1e3) / 1e9, 2)
+                if t.item() < best_t:
+                    best, best_t = algo, t.item()
+            choice = [best]
+            dist.broadcast_object_list(choice, src=src0, group=self.cpu_group)
+            row["choice"] = choice[0]
+            rows.append(row)
+            table.append((size, choice[0]))
+        self.check()
+        self.table = table
+        return rows
+
+    def _pick(self, nbytes: int) -> str:
+        for limit, algo in self.table:
+            if nbytes <= limit:
+                return algo
+        return self.table[-1][1] if self.table else "auto"
 
     # ------------------------------------------------------------------ collectives
     def allreduce(self, inp: torch.Tensor, out: torch.Tensor | None = None, *, op: str = "sum",
@@ -112,19 +194,23 @@ class XgmiCommunicator:
             raise ValueError(f"tensors must live on {self.device}")
         if not (inp.is_contiguous() and out.is_contiguous()) or inp.numel() != out.numel() or inp.dtype != out.dtype:
             raise ValueError("inp/out must be contiguous with the same numel and dtype")
-        if algo == "rccl":
+        if algo == "auto" and self.table:
+            algo = self._pick(inp.numel() * inp.element_size())
+        if op not in ("sum", "avg"):
+            raise ValueError(f"unsupported op {op!r}")
+        if algo == "rccl" or inp.dtype not in (torch.float32, torch.bfloat16):
             import torch.distributed as dist
 
             if out.data_ptr() != inp.data_ptr():
                 out.copy_(inp)
             dist.all_reduce(out, group=self.group)
-        else:
+            if op == "avg":
+                out.div_(self.world)
+        else:  # the mean is fused into the kernel (scale applied to the fp32 sum)
             stream = torch.cuda.current_stream(self.device).cuda_stream
-            self._c.allreduce(inp.data_ptr(), out.data_ptr(), inp.numel(), _dtype_code(inp.dtype), stream, ALGOS[algo])
-        if op == "avg":
-            out.div_(self.world)
-        elif op != "sum":
-            raise ValueError(f"unsupported op {op!r}")
+            scale = 1.0 / self.world if op == "avg" else 1.0
+            self._c.allreduce(inp.data_ptr(), out.data_ptr(), inp.numel(), _dtype_code(inp.dtype), stream, ALGOS[algo],
+                              scale)
         return out
 
     def allreduce_(self, t: torch.Tensor, *, op: str = "sum", algo: str = "auto") -> torch.Tensor:
@@ -184,7 +270,7 @@ class LocalCluster:
                 self.groups.append([k])
 
     def allreduce(self, inputs: Sequence[torch.Tensor], outputs: Sequence[torch.Tensor] | None = None, *,
-                  algo: str = "auto") -> list[torch.Tensor]:
+                  algo: str = "auto", op: str = "sum") -> list[torch.Tensor]:
         if len(inputs) != self.world:
             raise ValueError("one input per logical rank")
         outputs = list(outputs) if outputs is not None else [torch.empty_like(x) for x in inputs]
@@ -202,7 +288,8 @@ class LocalCluster:
             dev = self.devices[g[0]]
             _H.XgmiComm.allreduce_local([self.comms[k] for k in g], [inputs[k].data_ptr() for k in g],
                                         [outputs[k].data_ptr() for k in g], n, code,
-                                        torch.cuda.current_stream(dev).cuda_stream, ALGOS[algo])
+                                        torch.cuda.current_stream(dev).cuda_stream, ALGOS[algo],
+                                        1.0 / self.world if op == "avg" else 1.0)
         return outputs
 
     def barrier(self) -> None:

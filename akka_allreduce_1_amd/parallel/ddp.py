@@ -1,0 +1,208 @@
+"""Bucketed, backward-overlapped data-parallel gradient allreduce.
+
+The reference allreduces one flat vector per round, pulled from a `dataSource` and handed
+to a `dataSink` (AllreduceWorker.scala:171-192). A trainer's "vector" is its gradient set,
+so this module makes the gradients themselves the flat vectors:
+
+* Parameters are grouped into buckets of ~`bucket_bytes` (in reverse registration order,
+  which is roughly the order autograd produces gradients). Each bucket owns ONE contiguous
+  HBM buffer and every parameter's `.grad` is a view into it (members 16-byte aligned), so
+  backward accumulates straight into the buffer that is allreduced - no pack/unpack copy.
+* A post-accumulate-grad hook counts ready members; a full bucket is allreduced on a
+  dedicated HIP stream while backward keeps running. Buckets are launched strictly in
+  bucket order (a later bucket that is ready first waits), so every rank issues the same
+  collective sequence - the same "every rank must agree" rule the reference's round
+  protocol relies on.
+* `wait()` (end of backward) launches any bucket that never became ready (unused
+  parameters), then joins the comm stream into the compute stream.
+
+`comm` is anything with `allreduce_(tensor, op=...)` that runs on the current stream:
+`XgmiCommunicator` (fused xGMI kernels), or `TorchDistComm` (RCCL / gloo; CPU tests).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Iterable, Sequence
+
+import torch
+
+_ALIGN_BYTES = 16
+
+
+class TorchDistComm:
+    """Adapter: torch.distributed all_reduce (RCCL on GPU, gloo on CPU)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self.group = group
+        self.world = dist.get_world_size(group)
+
+    def allreduce_(self, t: torch.Tensor, *, op: str = "sum", algo: str | None = None) -> torch.Tensor:
+        import torch.distributed as dist
+
+        dist.all_reduce(t, group=self.group)
+        if op == "avg":
+            t.div_(self.world)
+        return t
+
+
+@dataclass
+class GradBucket:
+    index: int
+    dtype: torch.dtype
+    params: list = field(default_factory=list)
+    offsets: list = field(default_factory=list)
+    numel: int = 0
+    buffer: torch.Tensor | None = None
+    pending: int = 0
+    ready: bool = False
+    launched: bool = False
+    done: object = None  # torch.cuda.Event
+
+    @property
+    def nbytes(self) -> int:
+        return self.numel * torch.empty(0, dtype=self.dtype).element_size()
+
+
+class BucketedGradReducer:
+    def __init__(self, params: Iterable[torch.nn.Parameter] | torch.nn.Module, comm, *,
+                 bucket_bytes: int = 64 << 20, op: str = "avg", overlap: bool = True,
+                 first_bucket_bytes: int | None = None):
+        if isinstance(params, torch.nn.Module):
+            params = params.parameters()
+        self.params = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise ValueError("no trainable parameters")
+        self.comm = comm
+        self.op = op
+        self.device = self.params[0].device
+        self.on_gpu = self.device.type == "cuda"
+        self.overlap = overlap and self.on_gpu
+        self.stream = torch.cuda.Stream(device=self.device) if self.on_gpu else None
+        self.buckets = self._build(bucket_bytes, first_bucket_bytes)
+        self.slot_of: dict[int, tuple[GradBucket, int]] = {}
+        for b in self.buckets:
+            for p, off in zip(b.params, b.offsets):
+                self.slot_of[id(p)] = (b, off)
+        self._next = 0
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad_ready) for p in self.params]
+        self.stats = {"steps": 0, "buckets_launched": 0, "bytes": 0}
+
+    # ------------------------------------------------------------------ layout
+    def _build(self, bucket_bytes: int, first_bucket_bytes: int | None) -> list[GradBucket]:
+        buckets: list[GradBucket] = []
+        cur: dict[torch.dtype, GradBucket] = {}
+        limit_first = first_bucket_bytes or bucket_bytes
+        for p in reversed(self.params):  # backward produces late layers first
+            es = p.element_size()
+            align = max(1, _ALIGN_BYTES // es)
+            b = cur.get(p.dtype)
+            cap = limit_first if not buckets else bucket_bytes
+            if b is not None and b.numel > 0 and (b.numel + p.numel()) * es > cap:
+                b = None
+            if b is None:
+                b = GradBucket(index=len(buckets), dtype=p.dtype)
+                buckets.append(b)
+                cur[p.dtype] = b
+            off = (b.numel + align - 1) // align * align
+            b.params.append(p)
+            b.offsets.append(off)
+            b.numel = off + p.numel()
+        for b in buckets:
+            es = torch.empty(0, dtype=b.dtype).element_size()
+            align = max(1, _ALIGN_BYTES // es)
+            b.numel = (b.numel + align - 1) // align * align
+            b.buffer = torch.zeros(b.numel, dtype=b.dtype, device=self.device)
+            for p, off in zip(b.params, b.offsets):
+                g = b.buffer[off:off + p.numel()].view_as(p)
+                if p.grad is not None:
+                    g.copy_(p.grad)
+                p.grad = g  # gradient-as-bucket-view: autograd accumulates in place
+            b.pending = len(b.params)
+        return buckets
+
+    # ------------------------------------------------------------------ hooks
+    def _on_grad_ready(self, p: torch.Tensor) -> None:
+        b, off = self.slot_of[id(p)]
+        expect = b.buffer.data_ptr() + off * b.buffer.element_size()
+        if p.grad is not None and p.grad.data_ptr() != expect:
+            # .grad was replaced (e.g. zero_grad(set_to_none=True)): fold it back into the
+            # bucket view - one copy; use reducer.zero_grad() to avoid it
+            view = b.buffer[off:off + p.numel()].view_as(p)
+            view.copy_(p.grad)
+            p.grad = view
+        b.pending -= 1
+        if b.pending == 0:
+            b.ready = True
+            if self.overlap:
+                self._launch_ready()
+
+    def _launch_ready(self) -> None:
+        while self._next < len(self.buckets) and self.buckets[self._next].ready:
+            self._launch(self.buckets[self._next])
+            self._next += 1
+
+    def _launch(self, b: GradBucket) -> None:
+        if self.on_gpu:
+            compute = torch.cuda.current_stream(self.device)
+            self.stream.wait_stream(compute)
+            with torch.cuda.stream(self.stream):
+                self.comm.allreduce_(b.buffer, op=self.op)
+                b.done = torch.cuda.Event()
+                b.done.record(self.stream)
+            b.buffer.record_stream(self.stream)
+        else:
+            self.comm.allreduce_(b.buffer, op=self.op)
+        b.launched = True
+        self.stats["buckets_launched"] += 1
+        self.stats["bytes"] += b.nbytes
+
+    # ------------------------------------------------------------------ step API
+    def wait(self) -> None:
+        """Finish the gradient allreduce of this step (call after backward, before the
+        optimizer). Buckets whose parameters got no gradient are reduced too (as zeros)."""
+        for b in self.buckets:
+            b.ready = True
+        self._launch_ready()
+        if self.on_gpu:
+            compute = torch.cuda.current_stream(self.device)
+            for b in self.buckets:
+                if b.done is not None:
+                    compute.wait_event(b.done)
+        for b in self.buckets:
+            b.pending = len(b.params)
+            b.ready = b.launched = False
+            b.done = None
+        self._next = 0
+        self.stats["steps"] += 1
+
+    def zero_grad(self) -> None:
+        for b in self.buckets:
+            b.buffer.zero_()
+
+    def remove_hooks(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+    def describe(self) -> list[dict]:
+        return [{"bucket": b.index, "dtype": str(b.dtype), "params": len(b.params), "bytes": b.nbytes}
+                for b in self.buckets]
+
+
+def bucket_sizes(shapes: Sequence[tuple[int, ...]], elem_bytes: int, bucket_bytes: int) -> list[int]:
+    """Bucket byte sizes the reducer would build for parameter `shapes` (reverse order)."""
+    sizes, cur = [], 0
+    align = max(1, _ALIGN_BYTES // elem_bytes)
+    for shp in reversed(list(shapes)):
+        n = 1
+        for d in shp:
+            n *= d
+        if cur > 0 and (cur + n) * elem_bytes > bucket_bytes:
+            sizes.append((cur + align - 1) // align * align * elem_bytes)
+            cur = 0
+        cur = (cur + align - 1) // align * align + n
+    if cur:
+        sizes.append((cur + align - 1) // align * align * elem_bytes)
+    return sizes

@@ -87,10 +87,10 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--size-mib", type=int, default=256)
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
-    ap.add_argument("--algo", choices=["auto", "twoshot", "oneshot"], default="auto")
-    ap.add_argument("--no-rccl", action="store_true")
-    ap.add_argument("--no-sweep", action="store_true")
-    ap.add_argument("--sweep-steps", type=int, default=20)
+    ap.add_argument("--algo", choices=["auto", "twoshot", "oneshot", "rccl"], default="auto")
+    ap.add_argument("--no-rccl", action="store_true", help="skip the RCCL comparison timing")
+    ap.add_argument("--no-tune", action="store_true", help="skip the size sweep / algorithm tuner")
+    ap.add_argument("--sweep-steps", type=int, default=10)
     args = ap.parse_args()
 
     rank, world, local = init_distributed("nccl")
@@ -102,37 +102,58 @@ def main() -> None:
     nbytes = args.size_mib << 20
     n = nbytes // es
     slot = max(64 << 20, -(-nbytes // world) + (1 << 20))
-    comm = XgmiCommunicator(slot_bytes=slot)
-    log(rank, f"{comm}  tensor={args.size_mib} MiB {args.dtype}")
 
-    ok, err = validate(comm, n, dtype, dev, rank, world)
-    ok_small, err_small = validate(comm, 12345, dtype, dev, rank, world)
-    engine = "xgmi"
-    if not (ok and ok_small):
-        log(rank, f"VALIDATION FAILED (max err {err:.3g} / {err_small:.3g}); reporting RCCL instead")
-        engine = "rccl-fallback"
+    # ---- engine bring-up + validation; any failure degrades to RCCL (recorded) instead of
+    # losing the run
+    comm, reason, err = None, "", float("nan")
+    try:
+        comm = XgmiCommunicator(slot_bytes=slot)
+        log(rank, f"{comm}  tensor={args.size_mib} MiB {args.dtype}")
+        ok, err = validate(comm, n, dtype, dev, rank, world)
+        ok_small, err_small = validate(comm, 12345, dtype, dev, rank, world)
+        if not (ok and ok_small):
+            reason = f"validation failed (max err {err:.3g} / {err_small:.3g})"
+    except Exception as e:  # noqa: BLE001 - reported in the JSON
+        reason = f"engine unavailable: {e!r}"
+    healthy = torch.tensor([0 if reason else 1], device=dev)
+    dist.all_reduce(healthy, op=dist.ReduceOp.MIN)
+    if healthy.item() == 0 and not reason:
+        reason = "engine failed on another rank"
+    engine_ok = healthy.item() == 1
+    if not engine_ok:
+        log(rank, f"ENGINE DISABLED: {reason}; timing RCCL")
 
     x = torch.empty(n, dtype=dtype, device=dev)
     fill_uniform(x, seed=rank)
     y = torch.empty_like(x)
 
-    def step_engine():
-        comm.allreduce(x, y, algo=args.algo)
-
     def step_rccl():
         y.copy_(x)
         dist.all_reduce(y)
 
-    step = step_engine if engine == "xgmi" else step_rccl
+    sweep = None
+    if engine_ok and not args.no_tune:
+        sweep = comm.tune(max_bytes=nbytes, dtype=dtype, iters=args.sweep_steps,
+                          candidates=("oneshot", "twoshot") + (() if args.no_rccl else ("rccl",)))
+    if engine_ok and args.algo != "rccl":
+        algo = args.algo
+        chosen = comm._pick(nbytes) if algo == "auto" else algo
+
+        def step():
+            comm.allreduce(x, y, algo=algo)
+    else:
+        chosen = "rccl" if engine_ok else "rccl-fallback"
+        step = step_rccl
+
     for _ in range(args.warmup):
         step()
     wall, per = timed(step, args.steps, dev)
-    if engine == "xgmi":
+    if engine_ok:
         try:
             comm.check()
         except CommError as e:
             log(rank, f"engine error during timing: {e}")
-            engine = "rccl-fallback"
+            chosen += " (ERROR during timing)"
     wall = max_over_ranks(wall, dev)
     ms = wall / args.steps * 1e3
     algbw = nbytes / (ms / 1e3) / 1e9
@@ -157,43 +178,33 @@ def main() -> None:
             "seq_len": None,
             "parallelism": f"dp{world}",
             "tensor_bytes": nbytes,
-            "engine": engine,
-            "algo": args.algo,
+            "algo": chosen,
         },
         "p50_ms": round(p50, 4),
         "busbw": round(busbw(algbw, world), 2),
         "validated_max_abs_err": err,
+        "engine_ok": engine_ok,
     }
+    if reason:
+        result["engine_note"] = reason
 
-    if not args.no_rccl:
+    if engine_ok and chosen != "twoshot" and world > 1:
+        for _ in range(args.warmup):
+            comm.allreduce(x, y, algo="twoshot")
+        twall, _ = timed(lambda: comm.allreduce(x, y, algo="twoshot"), args.steps, dev)
+        tms = max_over_ranks(twall, dev) / args.steps * 1e3
+        result["xgmi_twoshot"] = {"algbw": round(nbytes / (tms / 1e3) / 1e9, 2), "ms_per_step": round(tms, 4)}
+    if not args.no_rccl and chosen not in ("rccl", "rccl-fallback"):
         for _ in range(args.warmup):
             step_rccl()
         rwall, rper = timed(step_rccl, args.steps, dev)
         rms = max_over_ranks(rwall, dev) / args.steps * 1e3
         r_alg = nbytes / (rms / 1e3) / 1e9
         result["rccl"] = {"algbw": round(r_alg, 2), "ms_per_step": round(rms, 4),
-                          "p50_ms": round(max_over_ranks(percentile(rper, 50), dev), 4)}
+                          "p50_ms": round(max_over_ranks(percentile(rper, 50), dev), 4),
+                          "note": "copy + in-place dist.all_reduce (nccl backend = RCCL)"}
         result["speedup_vs_rccl"] = round(algbw / r_alg, 3)
-
-    if not args.no_sweep and engine == "xgmi":
-        sweep = []
-        for sz in [4 << 10, 64 << 10, 1 << 20, 16 << 20, 64 << 20]:
-            m = sz // es
-            a = x[:m]
-            b = y[:m]
-            row = {"bytes": sz}
-            for name, fn in [("xgmi", lambda: comm.allreduce(a, b)),
-                             ("rccl", lambda: dist.all_reduce(b))]:
-                if name == "rccl" and args.no_rccl:
-                    continue
-                for _ in range(3):
-                    fn()
-                w, p = timed(fn, args.sweep_steps, dev)
-                p50s = max_over_ranks(percentile(p, 50), dev)
-                row[f"{name}_p50_us"] = round(p50s * 1e3, 1)
-                row[f"{name}_algbw"] = round(sz / (p50s / 1e3) / 1e9, 2)
-            sweep.append(row)
-        comm.check()
+    if sweep is not None:
         result["sweep"] = sweep
 
     if rank == 0:

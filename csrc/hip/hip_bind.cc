@@ -43,12 +43,13 @@ void bind_hip(py::module_& m) {
       .def("connect_local", &XgmiComm::connect_local)
       .def(
           "allreduce",
-          [](XgmiComm& c, uintptr_t in, uintptr_t out, int64_t n, DType dt, uintptr_t stream, Algo algo) {
+          [](XgmiComm& c, uintptr_t in, uintptr_t out, int64_t n, DType dt, uintptr_t stream, Algo algo,
+             float scale) {
             py::gil_scoped_release r;
-            c.allreduce(as_cptr(in), as_ptr(out), n, dt, as_stream(stream), algo);
+            c.allreduce(as_cptr(in), as_ptr(out), n, dt, as_stream(stream), algo, scale);
           },
           py::arg("inp"), py::arg("out"), py::arg("n"), py::arg("dtype"), py::arg("stream") = 0,
-          py::arg("algo") = Algo::Auto)
+          py::arg("algo") = Algo::Auto, py::arg("scale") = 1.0f)
       .def(
           "barrier",
           [](XgmiComm& c, uintptr_t stream) {
@@ -59,16 +60,16 @@ void bind_hip(py::module_& m) {
       .def_static(
           "allreduce_local",
           [](const std::vector<XgmiComm*>& comms, const std::vector<uintptr_t>& ins, const std::vector<uintptr_t>& outs,
-             int64_t n, DType dt, uintptr_t stream, Algo algo) {
+             int64_t n, DType dt, uintptr_t stream, Algo algo, float scale) {
             std::vector<const void*> i;
             std::vector<void*> o;
             for (auto p : ins) i.push_back(as_cptr(p));
             for (auto p : outs) o.push_back(as_ptr(p));
             py::gil_scoped_release r;
-            XgmiComm::allreduce_local(comms, i, o, n, dt, as_stream(stream), algo);
+            XgmiComm::allreduce_local(comms, i, o, n, dt, as_stream(stream), algo, scale);
           },
           py::arg("comms"), py::arg("inputs"), py::arg("outputs"), py::arg("n"), py::arg("dtype"),
-          py::arg("stream") = 0, py::arg("algo") = Algo::Auto)
+          py::arg("stream") = 0, py::arg("algo") = Algo::Auto, py::arg("scale") = 1.0f)
       .def_static(
           "barrier_local",
           [](const std::vector<XgmiComm*>& comms, uintptr_t stream) {

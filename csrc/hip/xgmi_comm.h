@@ -58,9 +58,11 @@ class XgmiComm {
   // Single-process mode: all "ranks" are this process (tests / P logical ranks).
   void connect_local(const std::vector<XgmiComm*>& comms);
 
-  // out = sum over ranks of in (n elements of dtype); in == out allowed (in-place).
+  // out = scale * sum over ranks of in (n elements of dtype); in == out allowed (in-place).
+  // The scale is applied to the fp32 sum before the single rounding (scale = 1/P: mean).
   // Pointers must be 16-byte aligned. Enqueued on `stream`; returns immediately.
-  void allreduce(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, Algo algo = Algo::Auto);
+  void allreduce(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, Algo algo = Algo::Auto,
+                 float scale = 1.f);
   // Device-side barrier over all ranks (enqueued on `stream`).
   void barrier(hipStream_t stream);
 
@@ -68,7 +70,7 @@ class XgmiComm {
   // one device, consecutive ranks, connected with connect_local); blockIdx.y = rank.
   static void allreduce_local(const std::vector<XgmiComm*>& comms, const std::vector<const void*>& ins,
                               const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream,
-                              Algo algo = Algo::Auto);
+                              Algo algo = Algo::Auto, float scale = 1.f);
   static void barrier_group(const std::vector<XgmiComm*>& comms, hipStream_t stream);
 
   // Sticky device error word (ORed codes, see device_common.h); 0 = healthy.
@@ -97,9 +99,9 @@ class XgmiComm {
 
  private:
   static void run(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
-                  const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, Algo algo);
+                  const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, Algo algo, float scale);
   static void launch_segment(const std::vector<XgmiComm*>& group, const char* const* ins, char* const* outs,
-                             int64_t n, DType dt, hipStream_t stream, bool oneshot);
+                             int64_t n, DType dt, hipStream_t stream, bool oneshot, float scale);
 
   int rank_, world_, device_, grid_;
   int64_t slot_bytes_, maxch_, off_S_, off_R_, off_B_, slab_bytes_;

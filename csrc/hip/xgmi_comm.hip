@@ -45,6 +45,7 @@ struct CommArgs {
   int P;
   int rank0;
   int fence;      // bit0: system release before flags, bit1: system acquire after waits
+  float scale;    // applied to the fp32 sum before rounding (1 = sum, 1/P = mean)
   int64_t maxch;
   int64_t off_S, off_R, slot_bytes;
   uint64_t timeout;
@@ -124,7 +125,8 @@ struct RedSrc {
 // Destinations of a reduced chunk: k == own is the rank's own output (plain stores),
 // every other k is a peer slab written through (sc0 sc1).
 template <class E, int PT, class DstF>
-__device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, int own_dst, DstF dst, int64_t len) {
+__device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, int own_dst, DstF dst, int64_t len,
+                                          float scale) {
   const int64_t npk = len / E::ELEMS;
   constexpr int U = 2;
   int64_t i = threadIdx.x;
@@ -145,6 +147,10 @@ __device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, in
       for (int s = 0; s < PT; ++s)
 #pragma unroll
         for (int u = 0; u < U; ++u) acc[u].add(v[s][u]);
+      if (scale != 1.f) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u].scale(scale);
+      }
       Pack16 o[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) o[u] = acc[u].pack();
@@ -166,6 +172,7 @@ __device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, in
     Acc<E> acc;
     acc.zero();
     for (int s = 0; s < P; ++s) acc.add(ld16_sc1(src.rsrc(s), static_cast<uint32_t>(i * 16)));
+    if (scale != 1.f) acc.scale(scale);
     const Pack16 o = acc.pack();
     for (int k = 0; k < ndst; ++k) {
       char* d = dst(k);
@@ -180,6 +187,7 @@ __device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, in
   if (t < len) {
     float acc = 0.f;
     for (int s = 0; s < P; ++s) acc += ld_scalar_sc1<E>(src.rsrc(s), t);
+    acc *= scale;
     for (int k = 0; k < ndst; ++k) {
       char* d = dst(k);
       if (d == nullptr) continue;
@@ -262,7 +270,8 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
       char* own_out = out + (bstart_own + cstart) * es;
       const int64_t roff = a.off_R + r * slot + cstart * es;
       const RedSrc src{own_in, S, slot, r};
-      reduce_to<E, PT>(P, src, P, r, [&](int k) -> char* { return k == r ? own_out : a.base[k] + roff; }, len);
+      reduce_to<E, PT>(P, src, P, r, [&](int k) -> char* { return k == r ? own_out : a.base[k] + roff; }, len,
+                       a.scale);
     }
     publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : f2(a, k, r, u); }, P, epoch, rel);
   }
@@ -319,7 +328,7 @@ __global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
       const char* S = a.base[r] + a.off_S + cstart * es;
       char* o = out + cstart * es;
       const RedSrc src{nullptr, S, slot, -1};
-      reduce_to<E, PT>(P, src, 1, 0, [&](int) -> char* { return o; }, len);
+      reduce_to<E, PT>(P, src, 1, 0, [&](int) -> char* { return o; }, len, a.scale);
     }
   }
   finish_launch(ctl, epoch);
@@ -468,7 +477,7 @@ static void launch_typed(const CommArgs& a, dim3 grid, hipStream_t s, bool onesh
 // Common launch geometry + args for the ranks `group` (all on one device, consecutive
 // rank ids starting at group[0]->rank()).
 void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* const* ins, char* const* outs,
-                              int64_t n, DType dt, hipStream_t stream, bool oneshot) {
+                              int64_t n, DType dt, hipStream_t stream, bool oneshot, float scale) {
   const XgmiComm& c0 = *group[0];
   const int W = c0.world_;
   const int64_t es = static_cast<int64_t>(dtype_size(dt));
@@ -517,6 +526,7 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
     gx = static_cast<int>(std::min<int64_t>(gmax, std::max<int64_t>(1, units)));
   }
   a.fence = c0.fence_;
+  a.scale = scale;
   if (static_cast<int64_t>(a.nch) * a.sub > c0.maxch_ || a.block * es > c0.slot_bytes_ + 16)
     throw std::logic_error("XgmiComm: segment geometry exceeds slab");
   const dim3 grid(gx, ranks_here);
@@ -532,7 +542,7 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
 }
 
 void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
-                   const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, Algo algo) {
+                   const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, Algo algo, float scale) {
   if (group.empty() || ins.size() != group.size() || outs.size() != group.size())
     throw std::invalid_argument("XgmiComm: one input and one output per rank");
   const XgmiComm& c0 = *group[0];
@@ -551,7 +561,7 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
     ++c->stats_.calls;
     c->stats_.bytes += n * es;
   }
-  if (c0.world_ == 1) {  // a 1-rank allreduce is the identity: copy out-of-place, nothing in place
+  if (c0.world_ == 1 && scale == 1.f) {  // a 1-rank sum is the identity: copy out-of-place, nothing in place
     for (size_t y = 0; y < group.size(); ++y)
       if (ins[y] != outs[y])
         hip_check(hipMemcpyAsync(outs[y], ins[y], n * es, hipMemcpyDeviceToDevice, stream), "hipMemcpyAsync");
@@ -568,17 +578,18 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
       ip[y] = static_cast<const char*>(ins[y]) + off * es;
       op[y] = static_cast<char*>(outs[y]) + off * es;
     }
-    launch_segment(group, ip.data(), op.data(), len, dt, stream, oneshot);
+    launch_segment(group, ip.data(), op.data(), len, dt, stream, oneshot, scale);
   }
 }
 
-void XgmiComm::allreduce(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, Algo algo) {
-  run({this}, {in}, {out}, n, dt, stream, algo);
+void XgmiComm::allreduce(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, Algo algo, float scale) {
+  run({this}, {in}, {out}, n, dt, stream, algo, scale);
 }
 
 void XgmiComm::allreduce_local(const std::vector<XgmiComm*>& comms, const std::vector<const void*>& ins,
-                               const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, Algo algo) {
-  run(comms, ins, outs, n, dt, stream, algo);
+                               const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, Algo algo,
+                               float scale) {
+  run(comms, ins, outs, n, dt, stream, algo, scale);
 }
 
 void XgmiComm::barrier_group(const std::vector<XgmiComm*>& group, hipStream_t stream) {

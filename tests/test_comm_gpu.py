@@ -129,3 +129,16 @@ def test_multiprocess_ipc_allreduce(world):
             p.kill()
     bad = [r for r in res if not r[1]]
     assert not bad, bad
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("P", [1, 2, 4])
+def test_local_cluster_mean_fused(dtype, P):
+    cl = LocalCluster(P, slot_bytes=1 << 20, grid=16)
+    n = 50_001
+    xs = [fill_uniform(torch.empty(n, dtype=dtype, device=DEV), seed=k) for k in range(P)]
+    ys = cl.allreduce(xs, op="avg")
+    cl.check()
+    ref = _ref(xs) / P
+    for y in ys:
+        assert (y.float() - ref).abs().max().item() <= (1e-6 if dtype == torch.float32 else 1e-2)
