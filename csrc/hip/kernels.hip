@@ -134,6 +134,34 @@ void launch_fill_uniform(void* dst, int64_t n, uint64_t seed, DType dt, hipStrea
   hip_check(hipGetLastError(), "fill_uniform launch");
 }
 
+// Plain device copy, 16 B per lane (used for the 1-rank allreduce: a kernel keeps the copy
+// in stream order with the kernels around it, with no DMA-engine hand-off).
+__global__ __launch_bounds__(kThreads) void copy16_kernel(const char* __restrict__ in, char* __restrict__ out,
+                                                           int64_t bytes) {
+  const int64_t npk = bytes / 16;
+  const int64_t step = static_cast<int64_t>(gridDim.x) * kThreads;
+  int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  for (; i + step < npk; i += 2 * step) {
+    const Pack16 a = ld16(in + i * 16);
+    const Pack16 b = ld16(in + (i + step) * 16);
+    st16(out + i * 16, a);
+    st16(out + (i + step) * 16, b);
+  }
+  for (; i < npk; i += step) st16(out + i * 16, ld16(in + i * 16));
+  const int64_t t = npk * 16 + static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (t < bytes) out[t] = in[t];
+}
+
+void launch_copy(const void* src, void* dst, int64_t bytes, hipStream_t stream) {
+  if (bytes <= 0) return;
+  if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15)
+    throw std::invalid_argument("copy: buffers must be 16-byte aligned");
+  const int g = grid_for(std::max<int64_t>(bytes / 32, 1));
+  hipLaunchKernelGGL(copy16_kernel, dim3(g), dim3(kThreads), 0, stream, static_cast<const char*>(src),
+                     static_cast<char*>(dst), bytes);
+  hip_check(hipGetLastError(), "copy launch");
+}
+
 template <class Ei, class Eo>
 __global__ __launch_bounds__(kThreads) void cast_kernel(const char* in, char* out, int64_t n) {
   const int64_t step = static_cast<int64_t>(gridDim.x) * kThreads;

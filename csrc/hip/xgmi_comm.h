@@ -124,6 +124,8 @@ void launch_reduce_slots(const void* slots, int64_t slot_stride_elems, int nslot
 void launch_fill_iota(void* dst, int64_t n, double offset, DType dt, hipStream_t stream);
 // dst[i] = uniform(-1, 1) from a counter-based hash of (seed, i)
 void launch_fill_uniform(void* dst, int64_t n, uint64_t seed, DType dt, hipStream_t stream);
+// dst[0:bytes) = src[0:bytes) as a kernel (16-B aligned)
+void launch_copy(const void* src, void* dst, int64_t bytes, hipStream_t stream);
 // dst (dt_out) = src (dt_in), n elements
 void launch_cast(const void* src, DType dt_in, void* dst, DType dt_out, int64_t n, hipStream_t stream);
 // flat bucket pack/unpack: copy `count` tensors (ptr, numel) into / out of a contiguous bucket

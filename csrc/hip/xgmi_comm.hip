@@ -291,10 +291,42 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
-// One-shot (latency path): every rank pushes its whole input into every rank's S slot
-// (own included, so the reduce never reads `in` and in-place is safe), then reduces
-// all P slots locally. One xGMI hop instead of two.
+// One-shot (latency path): every rank pushes its whole input into every peer's S slot,
+// then reduces all P contributions locally - one xGMI hop instead of two.
+// A push unit reads input chunk c ONCE and writes it to all P-1 peers, then publishes
+// F1_k[r][c] for every k INCLUDING itself: the own flag means "chunk c of my input has
+// been read", which the reduce of chunk c waits for before it may overwrite the input
+// (in-place). The reduce reads its own contribution straight from the input.
 // ---------------------------------------------------------------------------------
+template <class E>
+__device__ __forceinline__ void push_to_peers(const CommArgs& a, int P, int r, int64_t slot_off, const char* src,
+                                              int64_t len) {
+  const int64_t npk = len / E::ELEMS;
+  const Pack16* s = reinterpret_cast<const Pack16*>(src);
+  int64_t i = threadIdx.x;
+  constexpr int U = 2;
+  for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
+    Pack16 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = s[i + u * kCommThreads];
+    for (int k = 0; k < P; ++k) {
+      if (k == r) continue;
+      const __amdgpu_buffer_rsrc_t rd = slab_rsrc(a.base[k] + slot_off);
+#pragma unroll
+      for (int u = 0; u < U; ++u) st16_wt(rd, static_cast<uint32_t>((i + u * kCommThreads) * 16), v[u]);
+    }
+  }
+  for (; i < npk; i += kCommThreads) {
+    const Pack16 v = s[i];
+    for (int k = 0; k < P; ++k)
+      if (k != r) st16_wt(slab_rsrc(a.base[k] + slot_off), static_cast<uint32_t>(i * 16), v);
+  }
+  const int64_t t = npk * E::ELEMS + threadIdx.x;
+  if (t < len)
+    for (int k = 0; k < P; ++k)
+      if (k != r) copy_scalar_wt<E>(slab_rsrc(a.base[k] + slot_off), src, t);
+}
+
 template <class E, int PT>
 __global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
   constexpr int es = 16 / E::ELEMS;
@@ -310,14 +342,11 @@ __global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
   const int64_t slot = a.slot_bytes;
   uint32_t* err = &ctl[2];
   const bool rel = a.fence & 1, acq = a.fence & 2;
-  const int nu = P * a.nch;
-  for (int u = blockIdx.x; u < nu; u += G) {
-    const int c = u / P;
-    const int j = (r + 1 + u % P) % P;
+  for (int c = blockIdx.x; c < a.nch; c += G) {
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     const int64_t len = clamp_len(a.n - cstart, a.chunk);
-    if (len > 0) copy_to_slab<E>(a.base[j] + a.off_S + r * slot + cstart * es, in + cstart * es, len);
-    publish_flags([&](int) { return f1(a, j, r, c); }, 1, epoch, rel);
+    if (len > 0) push_to_peers<E>(a, P, r, a.off_S + r * slot + cstart * es, in + cstart * es, len);
+    publish_flags([&](int k) { return f1(a, k, r, c); }, P, epoch, rel);
   }
   for (int c = blockIdx.x; c < a.nch; c += G) {
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
@@ -325,9 +354,8 @@ __global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
     wait_flags([&](int s) -> const uint32_t* { return f1(a, r, s, c); }, P, epoch, deadline, err, ERR_TIMEOUT_SCATTER,
                acq);
     if (len > 0) {
-      const char* S = a.base[r] + a.off_S + cstart * es;
+      const RedSrc src{in + cstart * es, a.base[r] + a.off_S + cstart * es, slot, r};
       char* o = out + cstart * es;
-      const RedSrc src{nullptr, S, slot, -1};
       reduce_to<E, PT>(P, src, 1, 0, [&](int) -> char* { return o; }, len, a.scale);
     }
   }
@@ -505,11 +533,10 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   a.sub = 1;
   if (oneshot) {
     a.block = n;
-    const int64_t target = std::max<int64_t>(1, gmax / W);
-    a.chunk = std::max(min_chunk, round_up(ceil_div(n, target), elems));
+    a.chunk = std::max(min_chunk, round_up(ceil_div(n, gmax), elems));
     a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(n, a.chunk)));
     a.subchunk = a.chunk;
-    gx = static_cast<int>(std::min<int64_t>(gmax, std::max<int64_t>(1, W * static_cast<int64_t>(a.nch))));
+    gx = static_cast<int>(std::min<int64_t>(gmax, a.nch));
   } else {
     // ~one scatter unit and one gather unit per workgroup: every unit pays one fence, so
     // units are as large as the parallelism allows. The reduce phase splits each chunk
@@ -564,7 +591,7 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
   if (c0.world_ == 1 && scale == 1.f) {  // a 1-rank sum is the identity: copy out-of-place, nothing in place
     for (size_t y = 0; y < group.size(); ++y)
       if (ins[y] != outs[y])
-        hip_check(hipMemcpyAsync(outs[y], ins[y], n * es, hipMemcpyDeviceToDevice, stream), "hipMemcpyAsync");
+        launch_copy(ins[y], outs[y], n * es, stream);
     return;
   }
   const bool oneshot =

@@ -43,7 +43,8 @@ def _worker(rank, world, port, q, dtype):
                 grads.append([p.grad.float().clone() for p in ref.parameters()])
             for i, p in enumerate(m.parameters()):
                 exp = sum(gr[i] for gr in grads) / world
-                tol = 1e-5 if dtype == torch.float32 else 2e-2 * (exp.abs().max().item() + 1e-3)
+                scale = exp.abs().max().item() + 1e-3
+                tol = (1e-5 if dtype == torch.float32 else 2e-2) * scale
                 err = (p.grad.float() - exp).abs().max().item()
                 assert err <= tol, (step, i, err, tol)
         q.put((rank, True, ""))
