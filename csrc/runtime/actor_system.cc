@@ -26,7 +26,11 @@ ActorRef ActorContext::self() const { return cell_->ref(); }
 void ActorContext::watch(const ActorRef& ref) {
   if (!ref) return;
   auto* local = dynamic_cast<LocalActorRef*>(ref.get());
-  if (!local) return;  // remote refs: the cluster layer's failure detector reports them
+  if (!local) {  // remote refs: the cluster layer's failure detector reports them
+    if (ref->is_remote())
+      if (auto h = sys_->remote_watch_hook()) h(ref, self(), true);
+    return;
+  }
   auto c = local->cell();
   ActorRef me = self();
   if (!c || c->stopped()) {
@@ -39,7 +43,11 @@ void ActorContext::watch(const ActorRef& ref) {
 
 void ActorContext::unwatch(const ActorRef& ref) {
   auto* local = dynamic_cast<LocalActorRef*>(ref.get());
-  if (!local) return;
+  if (!local) {
+    if (ref && ref->is_remote())
+      if (auto h = sys_->remote_watch_hook()) h(ref, self(), false);
+    return;
+  }
   auto c = local->cell();
   if (!c) return;
   std::lock_guard<std::mutex> g(c->mu_);

@@ -210,6 +210,17 @@ class ActorSystem {
 
   SystemStats stats();
   void note_dead_letter(const Message& m, const ActorRef& sender);
+
+  // DeathWatch for remote refs is delegated to the cluster layer (csrc/cluster).
+  using RemoteWatchHook = std::function<void(const ActorRef& target, const ActorRef& watcher, bool watch)>;
+  void set_remote_watch_hook(RemoteWatchHook h) {
+    std::lock_guard<std::mutex> g(hook_mu_);
+    remote_watch_ = std::move(h);
+  }
+  RemoteWatchHook remote_watch_hook() {
+    std::lock_guard<std::mutex> g(hook_mu_);
+    return remote_watch_;
+  }
   void note_failure(const std::string& path, const std::string& what);
 
   // Called by cells/refs.
@@ -261,6 +272,8 @@ class ActorSystem {
 
   std::mutex stats_mu_;
   SystemStats stats_;
+  std::mutex hook_mu_;
+  RemoteWatchHook remote_watch_;
   uint64_t dead_letters_logged_ = 0;
 };
 
