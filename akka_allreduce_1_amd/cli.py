@@ -1,0 +1,173 @@
+"""Command-line entry points, argument-compatible with the reference's mains.
+
+    mxar-master [port totalWorkers dataSize maxChunkSize]      AllreduceMaster.scala:101-137
+    mxar-worker [port sourceDataSize]                           AllreduceWorker.scala:272-301
+
+Defaults are the reference's: master port 2551, 2 workers, dataSize = totalWorkers * 5,
+maxChunkSize 2, thresholds thAllreduce 1 / thReduce 0.9 / thComplete 0.8, maxLag 1,
+maxRound 100; worker port 2553, sourceDataSize 10, data source data[i] = i + iteration.
+Everything else comes from the layered config (conf/application.conf, MXAR_* env,
+--set key=value). Differences from the reference (documented fixes): the master exits
+after the last round and workers exit when the master leaves the cluster.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import signal
+import sys
+import threading
+import time
+
+import numpy as np
+
+from . import config as mconfig
+from ._native import C
+
+
+def _cluster_cfg(cfg: mconfig.Config, port: int, roles: list[str]) -> "C.ClusterConfig":
+    cc = C.ClusterConfig()
+    cc.host = str(cfg["mxar.remote.hostname"])
+    cc.port = int(port)
+    cc.roles = roles
+    cc.seed_nodes = cfg.seeds()
+    cc.heartbeat_interval_s = float(cfg["mxar.cluster.failure-detector.heartbeat-interval"])
+    cc.acceptable_heartbeat_pause_s = float(cfg["mxar.cluster.failure-detector.acceptable-heartbeat-pause"])
+    cc.auto_down_unreachable_after_s = float(cfg["mxar.cluster.auto-down-unreachable-after"])
+    cc.worker_path = str(cfg["mxar.cluster.worker-path"])
+    return cc
+
+
+def _common(ap: argparse.ArgumentParser) -> None:
+    ap.add_argument("--config", action="append", default=[], help="HOCON config file (repeatable)")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE", help="config override")
+    ap.add_argument("--metrics-json", default=None, help="write node/actor metrics here at exit")
+
+
+def _load(args) -> mconfig.Config:
+    cfg = mconfig.load(args.config, args.set)
+    C.set_log_level(str(cfg["mxar.loglevel"]))
+    return cfg
+
+
+def _install_signals(stop: threading.Event) -> None:
+    for s in (signal.SIGINT, signal.SIGTERM):
+        try:
+            signal.signal(s, lambda *_: stop.set())
+        except ValueError:  # not the main thread
+            pass
+
+
+def _write_metrics(path: str | None, node, extra: dict) -> None:
+    if not path:
+        return
+    st = node.stats()
+    doc = {k: getattr(st, k) for k in dir(st) if not k.startswith("_")}
+    doc.update(extra)
+    with open(path, "w") as f:
+        json.dump(doc, f, indent=1)
+
+
+def master_main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(prog="mxar-master", description=__doc__)
+    ap.add_argument("port", nargs="?", type=int, default=2551)
+    ap.add_argument("totalWorkers", nargs="?", type=int, default=None)
+    ap.add_argument("dataSize", nargs="?", type=int, default=None)
+    ap.add_argument("maxChunkSize", nargs="?", type=int, default=None)
+    ap.add_argument("--linger", action="store_true", help="keep running after the last round (reference behaviour)")
+    _common(ap)
+    args = ap.parse_args(argv)
+    cfg = _load(args)
+    total = args.totalWorkers if args.totalWorkers is not None else int(cfg["mxar.allreduce.total-workers"])
+    data_size = args.dataSize if args.dataSize is not None else (
+        total * 5 if cfg.origin.get("mxar.allreduce.data-size") == "default" else int(cfg["mxar.allreduce.data-size"]))
+    chunk = args.maxChunkSize if args.maxChunkSize is not None else int(cfg["mxar.allreduce.max-chunk-size"])
+    system = C.ActorSystem(str(cfg["mxar.system-name"]), False)
+    done = threading.Event()
+    stop = threading.Event()
+    rounds = {"n": 0}
+
+    def finished(r: int) -> None:
+        rounds["n"] = r
+        done.set()
+
+    master = system.master(total, float(cfg["mxar.allreduce.th-allreduce"]), float(cfg["mxar.allreduce.th-reduce"]),
+                           float(cfg["mxar.allreduce.th-complete"]), int(cfg["mxar.allreduce.max-lag"]), data_size,
+                           int(cfg["mxar.allreduce.max-round"]), chunk,
+                           liveBarrier=bool(cfg["mxar.allreduce.live-barrier"]), on_finished=finished, name="master")
+    node = C.ClusterNode.start(system, _cluster_cfg(cfg, args.port, ["master"]))
+    node.subscribe(master)
+    print(f"[mxar-master] {node.address} totalWorkers={total} dataSize={data_size} maxChunkSize={chunk}",
+          flush=True)
+    _install_signals(stop)
+    t0 = time.time()
+    while not stop.is_set() and not (done.is_set() and not args.linger):
+        stop.wait(0.1)
+    elapsed = time.time() - t0
+    if done.is_set():
+        print(f"[mxar-master] finished {rounds['n']} rounds in {elapsed:.2f}s", flush=True)
+    _write_metrics(args.metrics_json, node, {"rounds": rounds["n"], "elapsed_s": elapsed})
+    node.leave()
+    time.sleep(0.2)
+    node.shutdown()
+    system.shutdown()
+    return 0 if done.is_set() or stop.is_set() else 1
+
+
+def worker_main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(prog="mxar-worker", description=__doc__)
+    ap.add_argument("port", nargs="?", type=int, default=2553)
+    ap.add_argument("sourceDataSize", nargs="?", type=int, default=10)
+    ap.add_argument("--print-outputs", action="store_true", help="one JSON line per AllReduceOutput on stdout")
+    ap.add_argument("--max-outputs", type=int, default=0, help="exit after this many outputs (0 = never)")
+    _common(ap)
+    args = ap.parse_args(argv)
+    cfg = _load(args)
+    system = C.ActorSystem(str(cfg["mxar.system-name"]), False)
+    n = args.sourceDataSize
+    count = {"n": 0}
+    stop = threading.Event()
+    base = np.arange(n, dtype=np.float32)
+
+    def source(req):  # createDataSource: data[i] = i + iteration (AllreduceWorker.scala:285-291)
+        return C.AllReduceInput(base + np.float32(req.iteration))
+
+    def sink(out):  # logging sink (AllreduceWorker.scala:295-297)
+        count["n"] += 1
+        if args.print_outputs:
+            print(json.dumps({"iteration": out.iteration, "data": np.asarray(out.data).tolist(),
+                              "count": list(out.count)}), flush=True)
+        if args.max_outputs and count["n"] >= args.max_outputs:
+            stop.set()
+
+    system.worker(source, sink, "worker")
+    node = C.ClusterNode.start(system, _cluster_cfg(cfg, args.port, ["worker"]))
+    events = system.probe("membership")
+    node.subscribe(events)  # MemberUp events are queued: a short-lived master is never missed
+    print(f"[mxar-worker] {node.address} sourceDataSize={n}", file=sys.stderr, flush=True)
+    _install_signals(stop)
+    seen_master = False
+    while not stop.is_set():
+        ev = events.receive(0.1)
+        if ev is not None and isinstance(ev[0], C.MemberUp) and ev[0].role == "master":
+            seen_master = True
+        if seen_master and not any("master" in m["roles"] for m in node.members()):
+            break  # the master left / was downed: the job is over
+    _write_metrics(args.metrics_json, node, {"outputs": count["n"]})
+    node.leave()
+    time.sleep(0.1)
+    node.shutdown()
+    system.shutdown()
+    return 0
+
+
+def main(argv: list[str] | None = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv or argv[0] not in ("master", "worker"):
+        print("usage: python -m akka_allreduce_1_amd {master|worker} [args...]", file=sys.stderr)
+        return 2
+    return master_main(argv[1:]) if argv[0] == "master" else worker_main(argv[1:])
+
+
+if __name__ == "__main__":
+    sys.exit(main())

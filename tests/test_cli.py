@@ -1,0 +1,45 @@
+"""The reference's deployment (README.md:3-7): one master process + N worker processes
+joined through the seed node, over real TCP on 127.0.0.1, via the CLI entry points."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from akka_allreduce_1_amd.parallel.comm import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FAST = ["--set", "mxar.cluster.failure-detector.heartbeat-interval=100ms",
+        "--set", "mxar.cluster.failure-detector.acceptable-heartbeat-pause=1s",
+        "--set", "mxar.cluster.auto-down-unreachable-after=1s", "--set", "mxar.loglevel=WARNING"]
+
+
+@pytest.mark.slow
+def test_master_and_two_worker_processes():
+    port = free_port()
+    seed = ["--set", f"mxar.cluster.seed-nodes=mxar.tcp://ClusterSystem@127.0.0.1:{port}"]
+    exact = ["--set", "mxar.allreduce.th-reduce=1.0", "--set", "mxar.allreduce.th-complete=1.0",
+             "--set", "mxar.allreduce.max-round=4"]
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    py = [sys.executable, "-m", "akka_allreduce_1_amd"]
+    master = subprocess.Popen(py + ["master", str(port), "2", "10", "2"] + seed + exact + FAST, env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    workers = [subprocess.Popen(py + ["worker", "0", "10", "--print-outputs"] + seed + FAST, env=env,
+                                stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for _ in range(2)]
+    try:
+        mout, merr = master.communicate(timeout=60)
+        assert master.returncode == 0, merr
+        assert "finished 5 rounds" in mout, mout + merr  # rounds 0..maxRound (AllreduceMaster.scala:62)
+        for w in workers:
+            out, err = w.communicate(timeout=30)
+            assert w.returncode == 0, err
+            rows = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+            got = {r["iteration"]: r["data"] for r in rows}
+            for it in range(5):  # rounds 0..maxRound
+                np.testing.assert_array_equal(got[it], 2 * (np.arange(10) + it))
+    finally:
+        for p in [master] + workers:
+            if p.poll() is None:
+                p.kill()
