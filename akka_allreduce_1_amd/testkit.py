@@ -26,13 +26,21 @@ class ExpectationError(AssertionError):
     pass
 
 
+def to_host(v) -> np.ndarray:
+    """Payload -> numpy (device payloads arrive as torch tensors on the GPU)."""
+    if hasattr(v, "detach") and hasattr(v, "cpu"):
+        return v.detach().cpu().numpy()
+    return np.asarray(v)
+
+
 class TestKit:
     __test__ = False  # not a pytest class
 
-    def __init__(self, name: str = "MySpec", deterministic: bool = True, timeout: float = 3.0):
+    def __init__(self, name: str = "MySpec", deterministic: bool = True, timeout: float = 3.0, plane=None):
         self.system = C.ActorSystem(name, deterministic)
         self.test_actor = self.system.probe("testActor")
         self.timeout = timeout
+        self.plane = plane  # default DataPlane of created workers (None = host)
 
     # ImplicitSender: `self` in the Scala spec
     @property
@@ -52,7 +60,7 @@ class TestKit:
     def create_new_worker(self, source, sink=None, plane=None):
         """AllreduceSpec.scala:746-755 (random actor name)."""
         name = "".join(random.choice(string.ascii_letters + string.digits) for _ in range(10))
-        return self.system.worker(source, sink, name, plane)
+        return self.system.worker(source, sink, name, plane if plane is not None else self.plane)
 
     def initialize_workers_as_self(self, size: int) -> dict:
         """AllreduceSpec.scala:757-763: every peer id points at the probe."""
@@ -88,7 +96,7 @@ class TestKit:
         for f in ("srcId", "destId", "round", "chunkId"):
             if getattr(s, f) != getattr(expected, f):
                 raise ExpectationError(f"ScatterBlock.{f}: expected {expected!r}, found {s!r}")
-        if list(np.asarray(s.value)) != list(np.asarray(expected.value)):
+        if list(to_host(s.value)) != list(to_host(expected.value)):
             raise ExpectationError(f"ScatterBlock.value: expected {expected!r}, found {s!r}")
         return s
 
@@ -98,7 +106,7 @@ class TestKit:
         for f in ("srcId", "destId", "round", "chunkId", "count"):
             if getattr(r, f) != getattr(expected, f):
                 raise ExpectationError(f"ReduceBlock.{f}: expected {expected!r}, found {r!r}")
-        if list(np.asarray(r.value)) != list(np.asarray(expected.value)):
+        if list(to_host(r.value)) != list(to_host(expected.value)):
             raise ExpectationError(f"ReduceBlock.value: expected {expected!r}, found {r!r}")
         return r
 
@@ -139,7 +147,7 @@ def assertive_data_sink(expected: list[list[float]], iterations: Iterable[int], 
     def sink(r):
         assert r.iteration in iterations, f"unexpected iteration {r.iteration}"
         pos = iterations.index(r.iteration)
-        got = [float(x) for x in np.asarray(r.data)]
+        got = [float(x) for x in to_host(r.data)]
         assert got == list(expected[pos]), f"iteration {r.iteration}: {got} != {expected[pos]}"
         if seen is not None:
             seen.append(r.iteration)

@@ -126,6 +126,8 @@ class DataPlane {
   virtual Payload slice(const Payload& p, size_t start, size_t len) = 0;
   // Payload of n zeros (the reference initialises data with zeros).
   virtual Payload zeros(size_t n) = 0;
+  // Bring a payload into this plane's memory space (identity when it already lives there).
+  virtual Payload adopt(Payload p) { return p; }
 };
 
 class HostSlab final : public Slab {

@@ -199,7 +199,7 @@ void WorkerCore::fetch(int round) {
   if (payload_size(in.data) != static_cast<size_t>(params_.dataSize))
     throw ProtocolError("Input data size " + std::to_string(payload_size(in.data)) +
                         " is different from initialization time " + std::to_string(params_.dataSize) + "!");
-  data_ = std::move(in.data);
+  data_ = plane_->adopt(std::move(in.data));  // e.g. upload a host input to HBM once
 }
 
 // flush (AllreduceWorker.scala:180-192)

@@ -8,11 +8,107 @@
 
 #include <vector>
 
+#include "../bindings/py_common.h"
+#include "device_plane.h"
 #include "xgmi_comm.h"
 
 namespace py = pybind11;
 
 namespace mxar {
+
+// ---------------------------------------------------------------------------------
+// DLPack (ABI v0, "dltensor" capsules): zero-copy device payload <-> torch tensor
+// ---------------------------------------------------------------------------------
+namespace {
+struct DLDevice {
+  int32_t device_type;
+  int32_t device_id;
+};
+struct DLDataType {
+  uint8_t code;
+  uint8_t bits;
+  uint16_t lanes;
+};
+struct DLTensor {
+  void* data;
+  DLDevice device;
+  int32_t ndim;
+  DLDataType dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+};
+struct DLManagedTensor {
+  DLTensor dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(DLManagedTensor*);
+};
+constexpr int32_t kDLROCM = 10;
+constexpr uint8_t kDLFloat = 2;
+
+struct ExportCtx {
+  Payload keep;
+  int64_t shape[1];
+  int64_t strides[1];
+};
+
+void export_deleter(DLManagedTensor* m) {
+  delete static_cast<ExportCtx*>(m->manager_ctx);  // drops the payload ref (C++ only: no GIL)
+  delete m;
+}
+
+void capsule_destructor(PyObject* cap) {
+  if (PyCapsule_IsValid(cap, "dltensor")) {  // never consumed
+    auto* m = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap, "dltensor"));
+    if (m && m->deleter) m->deleter(m);
+  }
+}
+
+py::object device_payload_to_py(const Payload& p) {
+  auto* d = dynamic_cast<const DevicePayload*>(p.get());
+  if (!d) return py::none();
+  d->wait_host();  // torch consumes it on its own stream
+  auto* ctx = new ExportCtx{p, {static_cast<int64_t>(p->size())}, {1}};
+  auto* mt = new DLManagedTensor{};
+  mt->dl_tensor.data = const_cast<float*>(p->data());
+  mt->dl_tensor.device = DLDevice{kDLROCM, d->device()};
+  mt->dl_tensor.ndim = 1;
+  mt->dl_tensor.dtype = DLDataType{kDLFloat, 32, 1};
+  mt->dl_tensor.shape = ctx->shape;
+  mt->dl_tensor.strides = ctx->strides;
+  mt->dl_tensor.byte_offset = 0;
+  mt->manager_ctx = ctx;
+  mt->deleter = export_deleter;
+  py::capsule cap(mt, "dltensor", capsule_destructor);
+  return py::module_::import("torch.utils.dlpack").attr("from_dlpack")(cap);
+}
+
+Payload py_to_device_payload(const py::handle& obj) {
+  if (!py::hasattr(obj, "__dlpack__") || !py::hasattr(obj, "is_cuda")) return nullptr;
+  if (!obj.attr("is_cuda").cast<bool>()) return nullptr;  // CPU tensors take the numpy path
+  py::object t = obj.attr("detach")().attr("float")().attr("contiguous")().attr("reshape")(-1);
+  // order: the producer ran on torch's current stream; make it complete before the
+  // worker's plane stream (a different stream) reads the memory
+  py::module_::import("torch.cuda").attr("current_stream")(t.attr("device")).attr("synchronize")();
+  py::object cap = t.attr("__dlpack__")();
+  auto* mt = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap.ptr(), "dltensor"));
+  if (!mt) throw py::error_already_set();
+  PyCapsule_SetName(cap.ptr(), "used_dltensor");
+  const int64_t n = mt->dl_tensor.ndim > 0 ? mt->dl_tensor.shape[0] : 1;
+  char* data = static_cast<char*>(mt->dl_tensor.data) + mt->dl_tensor.byte_offset;
+  std::shared_ptr<void> mem(data, [mt](void*) {
+    if (!mt->deleter) return;
+    if (Py_IsInitialized()) {
+      py::gil_scoped_acquire g;
+      mt->deleter(mt);
+    } else {
+      mt->deleter(mt);
+    }
+  });
+  return std::make_shared<DevicePayload>(std::move(mem), 0, static_cast<size_t>(n), mt->dl_tensor.device.device_id,
+                                         nullptr, nullptr);
+}
+}  // namespace
 
 static hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 static const void* as_cptr(uintptr_t p) { return reinterpret_cast<const void*>(p); }
@@ -20,6 +116,21 @@ static void* as_ptr(uintptr_t p) { return reinterpret_cast<void*>(p); }
 
 void bind_hip(py::module_& m) {
   py::module_ h = m.def_submodule("hip", "HIP/CDNA4 data plane (gfx950)");
+  register_device_payload_hooks(&device_payload_to_py, &py_to_device_payload);
+
+  py::class_<DevicePlane, DataPlane, std::shared_ptr<DevicePlane>>(h, "DevicePlane")
+      .def_property_readonly("device", &DevicePlane::device)
+      .def("synchronize", [](DevicePlane& p) {
+        py::gil_scoped_release r;
+        p.synchronize();
+      })
+      .def_property_readonly("stream", [](DevicePlane& p) { return reinterpret_cast<uintptr_t>(p.stream()); })
+      .def_property_readonly("cached_bytes", [](DevicePlane& p) { return p.pool().cached_bytes(); })
+      .def_readonly("h2d_bytes", &DevicePlane::h2d_bytes)
+      .def_readonly("d2d_bytes", &DevicePlane::d2d_bytes)
+      .def_readonly("kernels", &DevicePlane::kernels);
+  h.def("device_plane", &make_device_plane, py::arg("device") = 0,
+        "DataPlane whose slabs and payloads live in HBM of `device` (worker protocol on the GPU)");
 
   py::enum_<DType>(h, "DType").value("F32", DType::F32).value("BF16", DType::BF16);
   py::enum_<Algo>(h, "Algo").value("Auto", Algo::Auto).value("TwoShot", Algo::TwoShot).value("OneShot", Algo::OneShot);

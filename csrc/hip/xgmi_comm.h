@@ -86,9 +86,12 @@ class XgmiComm {
   void set_oneshot_max_bytes(int64_t b) { oneshot_max_ = b; }
   void set_grid(int g);
   void set_timeout(double s) { timeout_s_ = s; }
-  // bit0: system-scope release fence before each flag store, bit1: system-scope acquire
-  // after each wait. Default 2: payload stores are write-through (sc0 sc1) and drained
-  // before the flag, so the release's L2 write-back is not needed; 3 adds it anyway.
+  // bit0: system-scope release fence (buffer_wbl2 sc0 sc1) before each flag store,
+  // bit1: system-scope acquire after each wait. Default 3 (memory-model correct). A
+  // drained write-through store is only known to have reached the producer's L2; without
+  // the release the flag can reach memory first through another L2 channel (observed on
+  // MI355X: stale slab reads). All kernel stores are write-through, so the release finds
+  // no dirty lines and stays cheap. 2 exists only to measure the fence's cost.
   int fence() const { return fence_; }
   void set_fence(int f) { fence_ = f & 3; }
   bool connected() const { return connected_; }
@@ -107,7 +110,7 @@ class XgmiComm {
   int64_t slot_bytes_, maxch_, off_S_, off_R_, off_B_, slab_bytes_;
   int64_t oneshot_max_;
   double timeout_s_;
-  int fence_ = 2;
+  int fence_ = 3;
   char* slab_ = nullptr;            // own uncached slab (flags | S | R)
   uint32_t* ctl_ = nullptr;         // [0] epoch, [1] ticket, [2] sticky error (device memory)
   char* peers_[kMaxRanks] = {};     // slab base of every rank (own included)

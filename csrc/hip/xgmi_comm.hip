@@ -1,7 +1,9 @@
 // Fused push-based allreduce over xGMI (gfx950). See xgmi_comm.h for the protocol map to
 // the reference (AllreduceWorker.scala scatter/reduce/broadcast/complete).
 //
-// Slab layout (identical offsets on every rank, uncached device memory):
+// Slab layout (identical offsets on every rank, fine-grained device memory - the kind HSA
+// makes coherent across agents during a kernel; MXAR_SLAB_MEM=uncached|coarse exist for
+// study only: uncached slabs showed stale reads on MI355X, tests/test_comm_gpu.py stress):
 //   [F1: P x maxch u32][F2: P x maxch u32][FB: P u32]  pad to 64 KiB
 //   [S : P slots x slot_bytes]   S_k[s] = contribution of rank s to rank k's block
 //   [R : P slots x slot_bytes]   R_k[j] = reduced block j, pushed by its owner j
@@ -91,7 +93,7 @@ template <class E>
 __device__ __forceinline__ void copy_from_slab(char* dst, const char* slab_src, int64_t len) {
   const int64_t npk = len / E::ELEMS;
   const __amdgpu_buffer_rsrc_t rs = slab_rsrc(slab_src);
-  Pack16* d = reinterpret_cast<Pack16*>(dst);
+  const __amdgpu_buffer_rsrc_t rd = slab_rsrc(dst);
   int64_t i = threadIdx.x;
   constexpr int U = 4;
   for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
@@ -99,11 +101,11 @@ __device__ __forceinline__ void copy_from_slab(char* dst, const char* slab_src, 
 #pragma unroll
     for (int u = 0; u < U; ++u) v[u] = ld16_sc1(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
 #pragma unroll
-    for (int u = 0; u < U; ++u) d[i + u * kCommThreads] = v[u];
+    for (int u = 0; u < U; ++u) st16_wt(rd, static_cast<uint32_t>((i + u * kCommThreads) * 16), v[u]);
   }
-  for (; i < npk; i += kCommThreads) d[i] = ld16_sc1(rs, static_cast<uint32_t>(i * 16));
+  for (; i < npk; i += kCommThreads) st16_wt(rd, static_cast<uint32_t>(i * 16), ld16_sc1(rs, static_cast<uint32_t>(i * 16)));
   const int64_t t = npk * E::ELEMS + threadIdx.x;
-  if (t < len) Scalar<E>::store(dst, t, ld_scalar_sc1<E>(rs, t));
+  if (t < len) st_scalar_wt<E>(rd, t, ld_scalar_sc1<E>(rs, t));
 }
 
 // Reduction sources: source s is at slab0 + s * stride, except source `own` (if >= 0),
@@ -122,11 +124,12 @@ struct RedSrc {
 
 // Sum P sources (fixed order s = 0..P-1, fp32) and store the result to up to P
 // destinations. src(s) / dst(k) return byte pointers to element 0 of the chunk.
-// Destinations of a reduced chunk: k == own is the rank's own output (plain stores),
-// every other k is a peer slab written through (sc0 sc1).
+// Destinations of a reduced chunk: every peer slab is written through (sc0 sc1); the
+// rank's own output (k == own) too when `wt_out`, so it leaves no dirty L2 lines for the
+// next release fence to write back.
 template <class E, int PT, class DstF>
 __device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, int own_dst, DstF dst, int64_t len,
-                                          float scale) {
+                                          float scale, bool wt_out) {
   const int64_t npk = len / E::ELEMS;
   constexpr int U = 2;
   int64_t i = threadIdx.x;
@@ -157,7 +160,7 @@ __device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, in
       for (int k = 0; k < ndst; ++k) {
         char* d = dst(k);
         if (d == nullptr) continue;
-        if (k == own_dst) {
+        if (k == own_dst && !wt_out) {
 #pragma unroll
           for (int u = 0; u < U; ++u) st16(d + (i + u * kCommThreads) * 16, o[u]);
         } else {
@@ -177,7 +180,7 @@ __device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, in
     for (int k = 0; k < ndst; ++k) {
       char* d = dst(k);
       if (d == nullptr) continue;
-      if (k == own_dst)
+      if (k == own_dst && !wt_out)
         st16(d + i * 16, o);
       else
         st16_wt(slab_rsrc(d), static_cast<uint32_t>(i * 16), o);
@@ -191,7 +194,7 @@ __device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, in
     for (int k = 0; k < ndst; ++k) {
       char* d = dst(k);
       if (d == nullptr) continue;
-      if (k == own_dst)
+      if (k == own_dst && !wt_out)
         Scalar<E>::store(d, t, acc);
       else
         st_scalar_wt<E>(slab_rsrc(d), t, acc);
@@ -271,7 +274,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
       const int64_t roff = a.off_R + r * slot + cstart * es;
       const RedSrc src{own_in, S, slot, r};
       reduce_to<E, PT>(P, src, P, r, [&](int k) -> char* { return k == r ? own_out : a.base[k] + roff; }, len,
-                       a.scale);
+                       a.scale, a.fence & 1);
     }
     publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : f2(a, k, r, u); }, P, epoch, rel);
   }
@@ -356,7 +359,7 @@ __global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
     if (len > 0) {
       const RedSrc src{in + cstart * es, a.base[r] + a.off_S + cstart * es, slot, r};
       char* o = out + cstart * es;
-      reduce_to<E, PT>(P, src, 1, 0, [&](int) -> char* { return o; }, len, a.scale);
+      reduce_to<E, PT>(P, src, 1, 0, [&](int) -> char* { return o; }, len, a.scale, a.fence & 1);
     }
   }
   finish_launch(ctl, epoch);
@@ -404,7 +407,7 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
 
   hip_check(hipSetDevice(device_), "hipSetDevice");
   const char* mem = std::getenv("MXAR_SLAB_MEM");
-  const std::string kind = mem ? mem : "uncached";
+  const std::string kind = mem ? mem : "fine";
   if (kind == "coarse") {
     hip_check(hipMalloc(reinterpret_cast<void**>(&slab_), slab_bytes_), "hipMalloc(slab)");
   } else {

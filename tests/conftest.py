@@ -32,10 +32,17 @@ def C():
     return _C
 
 
-@pytest.fixture
-def tk():
+@pytest.fixture(params=["host", pytest.param("device", marks=pytest.mark.gpu)])
+def tk(request):
+    """Deterministic TestKit; the `device` variant runs the same worker protocol with its
+    DataBuffers and payloads in MI355X HBM (DevicePlane)."""
     from akka_allreduce_1_amd.testkit import TestKit
 
-    kit = TestKit("MySpec", deterministic=True)
+    plane = None
+    if request.param == "device":
+        from akka_allreduce_1_amd._native import C
+
+        plane = C.hip.device_plane(0)
+    kit = TestKit("MySpec", deterministic=True, plane=plane)
     yield kit
     kit.shutdown()

@@ -160,3 +160,29 @@ def test_inplace_no_input_overwrite_race(algo, P):
             err = (y - ref).abs().max().item()
             if err > 1e-5:
                 pytest.fail(f"it {it} rank {k}: err {err}: {_diag(y, ref, xs, k)}")
+
+
+def test_stress_cluster_churn():
+    """Clusters created and destroyed with changing rank counts, slot sizes and lengths: new
+    slabs land on memory that old slabs (with other layouts) just used, the pattern that
+    exposes any flag-before-data ordering hole (a stale slab read shows as a wrong sum)."""
+    import random
+
+    rng = random.Random(1234)
+    for it in range(40):
+        P = rng.choice([2, 3, 4])
+        slot = rng.choice([1 << 20, 2 << 20, 4 << 20])
+        dtype = rng.choice([torch.float32, torch.bfloat16])
+        es = 4 if dtype == torch.float32 else 2
+        n = rng.randint(1, (slot * P) // es)
+        algo = rng.choice(["auto", "twoshot", "oneshot"]) if n * es <= slot else "twoshot"
+        cl = LocalCluster(P, slot_bytes=slot, grid=rng.choice([8, 32, 64]))
+        xs = [fill_uniform(torch.empty(n, dtype=dtype, device=DEV), seed=rng.randint(0, 1 << 30)) for _ in range(P)]
+        ref = _ref(xs)
+        ys = cl.allreduce(xs, algo=algo)
+        cl.check()
+        for k, y in enumerate(ys):
+            err = (y.float() - ref).abs().max().item()
+            if err > _tol(dtype, P) + (1e-5 if dtype == torch.float32 else 0):
+                pytest.fail(f"it {it} P={P} n={n} {dtype} {algo} rank {k}: err {err}: {_diag(y, ref, xs, k)}")
+        del cl, xs, ys
