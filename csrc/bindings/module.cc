@@ -14,6 +14,7 @@
 #include "../core/worker_core.h"
 #include "../runtime/actor_system.h"
 #include "../runtime/allreduce_actors.h"
+#include "../runtime/fault_injector.h"
 #include "py_common.h"
 
 namespace py = pybind11;
@@ -148,7 +149,7 @@ py::dict worker_stats_dict(const WorkerStats& s) {
 #define F(x) d[#x] = s.x
   F(scatter_in); F(reduce_in); F(start_in); F(scatter_out); F(reduce_out); F(complete_out);
   F(bytes_out); F(bytes_in); F(outdated_dropped); F(future_requeued); F(stashed);
-  F(forced_completions); F(rounds_completed); F(reductions); F(duplicate_arrivals); F(malformed_dropped);
+  F(forced_completions); F(rounds_completed); F(reductions); F(duplicate_arrivals); F(malformed_dropped); F(stale_epoch_dropped);
 #undef F
   return d;
 }
@@ -202,19 +203,25 @@ PYBIND11_MODULE(_C, m) {
       });
 
   py::class_<StartAllreduce>(m, "StartAllreduce")
-      .def(py::init([](int r) { return StartAllreduce{r}; }), py::arg("round"))
+      .def(py::init([](int r, int64_t epoch) { return StartAllreduce{r, epoch}; }), py::arg("round"),
+           py::arg("epoch") = 0)
       .def_readwrite("round", &StartAllreduce::round)
+      .def_readwrite("epoch", &StartAllreduce::epoch)
       .def("__eq__", [](const StartAllreduce& a, py::object b) {
-        return py::isinstance<StartAllreduce>(b) && a.round == b.cast<StartAllreduce>().round;
+        if (!py::isinstance<StartAllreduce>(b)) return false;
+        const auto& x = b.cast<const StartAllreduce&>();
+        return a.round == x.round && a.epoch == x.epoch;
       })
       .def("__hash__", [](const StartAllreduce& a) { return a.round; })
       .def("__repr__", [](const StartAllreduce& a) { return "StartAllreduce(" + std::to_string(a.round) + ")"; });
 
   py::class_<ScatterBlock>(m, "ScatterBlock")
-      .def(py::init([](py::object value, int srcId, int destId, int chunkId, int round) {
-             return ScatterBlock{payload_from_py(value), srcId, destId, chunkId, round};
+      .def(py::init([](py::object value, int srcId, int destId, int chunkId, int round, int64_t epoch) {
+             return ScatterBlock{payload_from_py(value), srcId, destId, chunkId, round, epoch};
            }),
-           py::arg("value"), py::arg("srcId"), py::arg("destId"), py::arg("chunkId"), py::arg("round"))
+           py::arg("value"), py::arg("srcId"), py::arg("destId"), py::arg("chunkId"), py::arg("round"),
+           py::arg("epoch") = 0)
+      .def_readwrite("epoch", &ScatterBlock::epoch)
       .def_property("value", [](const ScatterBlock& s) { return payload_to_py(s.value); },
                     [](ScatterBlock& s, py::object v) { s.value = payload_from_py(v); })
       .def_property_readonly("on_device", [](const ScatterBlock& s) { return s.value && s.value->on_device(); })
@@ -226,7 +233,7 @@ PYBIND11_MODULE(_C, m) {
         if (!py::isinstance<ScatterBlock>(o)) return false;
         const auto& b = o.cast<const ScatterBlock&>();
         return a.srcId == b.srcId && a.destId == b.destId && a.chunkId == b.chunkId && a.round == b.round &&
-               payload_eq(a.value, b.value);
+               a.epoch == b.epoch && payload_eq(a.value, b.value);
       })
       .def("__repr__", [](const ScatterBlock& s) {
         std::ostringstream os;
@@ -236,11 +243,12 @@ PYBIND11_MODULE(_C, m) {
       });
 
   py::class_<ReduceBlock>(m, "ReduceBlock")
-      .def(py::init([](py::object value, int srcId, int destId, int chunkId, int round, int count) {
-             return ReduceBlock{payload_from_py(value), srcId, destId, chunkId, round, count};
+      .def(py::init([](py::object value, int srcId, int destId, int chunkId, int round, int count, int64_t epoch) {
+             return ReduceBlock{payload_from_py(value), srcId, destId, chunkId, round, count, epoch};
            }),
            py::arg("value"), py::arg("srcId"), py::arg("destId"), py::arg("chunkId"), py::arg("round"),
-           py::arg("count"))
+           py::arg("count"), py::arg("epoch") = 0)
+      .def_readwrite("epoch", &ReduceBlock::epoch)
       .def_property("value", [](const ReduceBlock& s) { return payload_to_py(s.value); },
                     [](ReduceBlock& s, py::object v) { s.value = payload_from_py(v); })
       .def_property_readonly("on_device", [](const ReduceBlock& s) { return s.value && s.value->on_device(); })
@@ -253,7 +261,7 @@ PYBIND11_MODULE(_C, m) {
         if (!py::isinstance<ReduceBlock>(o)) return false;
         const auto& b = o.cast<const ReduceBlock&>();
         return a.srcId == b.srcId && a.destId == b.destId && a.chunkId == b.chunkId && a.round == b.round &&
-               a.count == b.count && payload_eq(a.value, b.value);
+               a.count == b.count && a.epoch == b.epoch && payload_eq(a.value, b.value);
       })
       .def("__repr__", [](const ReduceBlock& s) {
         std::ostringstream os;
@@ -263,13 +271,15 @@ PYBIND11_MODULE(_C, m) {
       });
 
   py::class_<CompleteAllreduce>(m, "CompleteAllreduce")
-      .def(py::init([](int src, int r) { return CompleteAllreduce{src, r}; }), py::arg("srcId"), py::arg("round"))
+      .def(py::init([](int src, int r, int64_t epoch) { return CompleteAllreduce{src, r, epoch}; }), py::arg("srcId"),
+           py::arg("round"), py::arg("epoch") = 0)
       .def_readwrite("srcId", &CompleteAllreduce::srcId)
       .def_readwrite("round", &CompleteAllreduce::round)
+      .def_readwrite("epoch", &CompleteAllreduce::epoch)
       .def("__eq__", [](const CompleteAllreduce& a, py::object o) {
         if (!py::isinstance<CompleteAllreduce>(o)) return false;
         const auto& b = o.cast<const CompleteAllreduce&>();
-        return a.srcId == b.srcId && a.round == b.round;
+        return a.srcId == b.srcId && a.round == b.round && a.epoch == b.epoch;
       })
       .def("__hash__", [](const CompleteAllreduce& a) { return a.srcId * 1000003 + a.round; })
       .def("__repr__", [](const CompleteAllreduce& c) {
@@ -486,6 +496,36 @@ PYBIND11_MODULE(_C, m) {
         d["stale_completes"] = c.stats().stale_completes;
         return d;
       });
+
+  py::class_<FaultStats>(m, "FaultStats")
+      .def_readonly("seen", &FaultStats::seen)
+      .def_readonly("forwarded", &FaultStats::forwarded)
+      .def_readonly("dropped", &FaultStats::dropped)
+      .def_readonly("duplicated", &FaultStats::duplicated)
+      .def_readonly("delayed", &FaultStats::delayed);
+  py::class_<FaultyRef, ActorRefBase, std::shared_ptr<FaultyRef>>(m, "FaultyRef")
+      .def("stats", &FaultyRef::stats)
+      .def("set_enabled", &FaultyRef::set_enabled)
+      .def_property_readonly("target", &FaultyRef::target);
+  m.def(
+      "faulty",
+      [](std::shared_ptr<ActorSystem> sys, ActorRef target, double drop, double duplicate, int delay_ms,
+         double delay_prob, std::vector<std::string> kinds, int round_lo, int round_hi, uint64_t seed) {
+        FaultPolicy p;
+        p.drop = drop;
+        p.duplicate = duplicate;
+        p.delay_ms = delay_ms;
+        p.delay_prob = delay_prob;
+        p.kinds = std::set<std::string>(kinds.begin(), kinds.end());
+        p.round_lo = round_lo;
+        p.round_hi = round_hi;
+        p.seed = seed;
+        return std::make_shared<FaultyRef>(sys.get(), std::move(target), std::move(p));
+      },
+      py::arg("system"), py::arg("target"), py::arg("drop") = 0.0, py::arg("duplicate") = 0.0,
+      py::arg("delay_ms") = 0, py::arg("delay_prob") = 1.0, py::arg("kinds") = std::vector<std::string>{},
+      py::arg("round_lo") = INT32_MIN, py::arg("round_hi") = INT32_MAX, py::arg("seed") = 1,
+      "Fault-injecting ActorRef decorator (drop / duplicate / delay selected messages)");
 
   py::class_<DataPlane, std::shared_ptr<DataPlane>>(m, "DataPlane").def_property_readonly("name", &DataPlane::name);
   m.def("host_plane", [] { return std::static_pointer_cast<DataPlane>(HostPlane::instance()); });

@@ -38,12 +38,14 @@ void encode_message(Writer& w, const Message& m, const RefCodec& rc) {
           w.i64(x.epoch);
         } else if constexpr (std::is_same_v<T, StartAllreduce>) {
           w.i32(x.round);
+          w.i64(x.epoch);
         } else if constexpr (std::is_same_v<T, ScatterBlock>) {
           put_payload(w, x.value);
           w.i32(x.srcId);
           w.i32(x.destId);
           w.i32(x.chunkId);
           w.i32(x.round);
+          w.i64(x.epoch);
         } else if constexpr (std::is_same_v<T, ReduceBlock>) {
           put_payload(w, x.value);
           w.i32(x.srcId);
@@ -51,9 +53,11 @@ void encode_message(Writer& w, const Message& m, const RefCodec& rc) {
           w.i32(x.chunkId);
           w.i32(x.round);
           w.i32(x.count);
+          w.i64(x.epoch);
         } else if constexpr (std::is_same_v<T, CompleteAllreduce>) {
           w.i32(x.srcId);
           w.i32(x.round);
+          w.i64(x.epoch);
         } else if constexpr (std::is_same_v<T, MemberUp>) {
           w.str(rc.encode_ref(x.ref));
           w.str(x.role);
@@ -90,8 +94,12 @@ Message decode_message(Reader& r, RefCodec& rc) {
       x.epoch = r.i64();
       return x;
     }
-    case 1:
-      return StartAllreduce{r.i32()};
+    case 1: {
+      StartAllreduce x;
+      x.round = r.i32();
+      x.epoch = r.i64();
+      return x;
+    }
     case 2: {
       ScatterBlock x;
       x.value = make_host_payload(r.floats());
@@ -99,6 +107,7 @@ Message decode_message(Reader& r, RefCodec& rc) {
       x.destId = r.i32();
       x.chunkId = r.i32();
       x.round = r.i32();
+      x.epoch = r.i64();
       return x;
     }
     case 3: {
@@ -109,12 +118,14 @@ Message decode_message(Reader& r, RefCodec& rc) {
       x.chunkId = r.i32();
       x.round = r.i32();
       x.count = r.i32();
+      x.epoch = r.i64();
       return x;
     }
     case 4: {
       CompleteAllreduce x;
       x.srcId = r.i32();
       x.round = r.i32();
+      x.epoch = r.i64();
       return x;
     }
     case 5: {

@@ -48,7 +48,11 @@ float MasterCore::barrier_base() const {
 }
 
 // CompleteAllreduce (AllreduceMaster.scala:58-67)
-void MasterCore::on_complete(int srcId, int round) {
+void MasterCore::on_complete(int srcId, int round, int64_t epoch) {
+  if (epoch >= 0 && epoch != epoch_ && round >= 0) {  // sent before the last re-init
+    stats_.stale_completes++;
+    return;
+  }
   if (srcId >= 0) {
     MXAR_LOG(INFO, "master", "----Node " << srcId << " completes allreduce round " << round);
     stats_.completes++;

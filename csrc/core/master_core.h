@@ -52,7 +52,8 @@ class MasterCore {
 
   void on_member_up(int handle);
   void on_terminated(int handle);
-  void on_complete(int srcId, int round);
+  // epoch < 0: untagged (accepted); otherwise completions of another epoch are stale
+  void on_complete(int srcId, int round, int64_t epoch = -1);
 
   int round() const { return round_; }
   int num_complete() const { return numComplete_; }

@@ -75,8 +75,14 @@ struct InitWorkers {  // AllreduceMessage.scala:7-16
   int64_t epoch = 0;
 };
 
+// Extension: the round messages carry the membership epoch of the
+// InitWorkers they belong to, as a trailing field (the reference's field order is kept).
+// A worker drops messages of an older epoch and stashes messages of a newer one until its
+// own re-init arrives, so traffic in flight across a re-initialisation can never land in
+// the new epoch's buffers.
 struct StartAllreduce {  // AllreduceMessage.scala:17
   int round = 0;
+  int64_t epoch = 0;
 };
 
 struct ScatterBlock {  // AllreduceMessage.scala:18
@@ -85,6 +91,7 @@ struct ScatterBlock {  // AllreduceMessage.scala:18
   int destId = 0;
   int chunkId = 0;
   int round = 0;
+  int64_t epoch = 0;
 };
 
 struct ReduceBlock {  // AllreduceMessage.scala:19
@@ -94,11 +101,13 @@ struct ReduceBlock {  // AllreduceMessage.scala:19
   int chunkId = 0;
   int round = 0;
   int count = 0;
+  int64_t epoch = 0;
 };
 
 struct CompleteAllreduce {  // AllreduceMessage.scala:20
   int srcId = 0;
   int round = 0;
+  int64_t epoch = 0;
 };
 
 // ---------------------------------------------------------------------------------

@@ -75,11 +75,24 @@ void WorkerCore::on_init(const InitParams& p) {
 }
 
 // StartAllreduce handler (AllreduceWorker.scala:84-104)
+// Membership-epoch gate: 1 = handle, 0 = drop (older epoch), -1 = stash
+// (newer epoch: this worker's own re-init is still in flight).
+int WorkerCore::epoch_gate(int64_t e) {
+  if (e == params_.epoch) return 1;
+  if (e > params_.epoch) {
+    stats_.stashed++;
+    return -1;
+  }
+  stats_.stale_epoch_dropped++;
+  return 0;
+}
+
 bool WorkerCore::on_start(const StartAllreduce& s) {
   if (!initialized()) {
     stats_.stashed++;
     return false;
   }
+  if (const int g = epoch_gate(s.epoch); g <= 0) return g == 0;
   stats_.start_in++;
   MXAR_LOG(INFO, "worker", "----Start allreduce round " << s.round);
   maxRound_ = std::max(maxRound_, s.round);
@@ -108,6 +121,7 @@ bool WorkerCore::on_scatter(const ScatterBlock& s) {
     stats_.stashed++;
     return false;
   }
+  if (const int g = epoch_gate(s.epoch); g <= 0) return g == 0;
   stats_.scatter_in++;
   stats_.bytes_in += payload_size(s.value) * sizeof(float);
   MXAR_LOG(TRACE, "worker", "----receive scattered data from round " << s.round << ": value = "
@@ -141,7 +155,7 @@ bool WorkerCore::on_scatter(const ScatterBlock& s) {
     }
   } else {
     stats_.future_requeued++;
-    fx_->to_self(StartAllreduce{s.round});
+    fx_->to_self(StartAllreduce{s.round, params_.epoch});
     fx_->to_self(ScatterBlock(s));
   }
   return true;
@@ -153,6 +167,7 @@ bool WorkerCore::on_reduce(const ReduceBlock& r) {
     stats_.stashed++;
     return false;
   }
+  if (const int g = epoch_gate(r.epoch); g <= 0) return g == 0;
   stats_.reduce_in++;
   stats_.bytes_in += payload_size(r.value) * sizeof(float);
   MXAR_LOG(TRACE, "worker", "----Receive reduced data from round " << r.round << ": value = " << dump(r.value)
@@ -186,7 +201,7 @@ bool WorkerCore::on_reduce(const ReduceBlock& r) {
     }
   } else {
     stats_.future_requeued++;
-    fx_->to_self(StartAllreduce{r.round});
+    fx_->to_self(StartAllreduce{r.round, params_.epoch});
     fx_->to_self(ReduceBlock(r));
   }
   return true;
@@ -233,7 +248,7 @@ void WorkerCore::scatter() {
                                     << ", chunkId: " << k);
       stats_.scatter_out++;
       stats_.bytes_out += payload_size(chunk) * sizeof(float);
-      fx_->to_peer(idx, ScatterBlock{std::move(chunk), id_, idx, k, r});
+      fx_->to_peer(idx, ScatterBlock{std::move(chunk), id_, idx, k, r, params_.epoch});
     }
   }
 }
@@ -247,7 +262,7 @@ void WorkerCore::broadcast(const Payload& v, int chunkId, int round, int count) 
                                   << ", chunkId: " << chunkId << ", round: " << round);
     stats_.reduce_out++;
     stats_.bytes_out += payload_size(v) * sizeof(float);
-    fx_->to_peer(idx, ReduceBlock{v, id_, idx, chunkId, round, count});
+    fx_->to_peer(idx, ReduceBlock{v, id_, idx, chunkId, round, count, params_.epoch});
   }
 }
 
@@ -269,13 +284,17 @@ void WorkerCore::complete(int completedRound, int row) {
   data_ = plane_->zeros(0);
   stats_.complete_out++;
   stats_.rounds_completed++;
-  fx_->to_master(CompleteAllreduce{id_, completedRound});
+  fx_->to_master(CompleteAllreduce{id_, completedRound, params_.epoch});
   completed_.insert(completedRound);
   if (round_ == completedRound) {
     do {
       round_ += 1;
+      const size_t recycled = static_cast<size_t>(reduceBuf_.counters.phys(0));
       scatterBuf_.up();
       reduceBuf_.up();
+      // the recycled row's reported contribution counts start over with its data
+      const size_t per_row = static_cast<size_t>(P_) * std::max(maxNumChunks_, 0);
+      std::fill(reduceCounts_.begin() + recycled * per_row, reduceCounts_.begin() + (recycled + 1) * per_row, 0);
     } while (completed_.count(round_));
   }
 }

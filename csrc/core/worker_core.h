@@ -61,7 +61,7 @@ struct WorkerStats {
   uint64_t bytes_out = 0, bytes_in = 0;
   uint64_t outdated_dropped = 0, future_requeued = 0, stashed = 0;
   uint64_t forced_completions = 0, rounds_completed = 0, reductions = 0;
-  uint64_t duplicate_arrivals = 0, malformed_dropped = 0;
+  uint64_t duplicate_arrivals = 0, malformed_dropped = 0, stale_epoch_dropped = 0;
 };
 
 class WorkerCore {
@@ -70,8 +70,9 @@ class WorkerCore {
 
   bool initialized() const { return id_ >= 0; }
   void on_init(const InitParams& p);
-  // The three handlers return false when the core is not initialised: the host must
-  // stash the message and replay it after Init.
+  // The three handlers return false when the core is not initialised, or when the message
+  // belongs to a newer membership epoch than the last Init: the host must stash it and
+  // replay it after the next Init. Messages of an older epoch are dropped.
   bool on_start(const StartAllreduce& m);
   bool on_scatter(const ScatterBlock& m);
   bool on_reduce(const ReduceBlock& m);
@@ -100,6 +101,7 @@ class WorkerCore {
   void complete(int completedRound, int row);
   void flush(int completedRound, int row);
   bool outdated(int r) const { return r < round_ || completed_.count(r) > 0; }
+  int epoch_gate(int64_t e);
 
   WorkerEffects* fx_;
   std::shared_ptr<DataPlane> plane_;

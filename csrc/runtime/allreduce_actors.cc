@@ -122,7 +122,7 @@ void MasterActor::receive(Envelope& env, ActorContext& ctx) {
     int h = handle_of(t->ref, false);
     if (h >= 0) core_.on_terminated(h);
   } else if (auto* c = std::get_if<CompleteAllreduce>(&env.msg)) {
-    core_.on_complete(c->srcId, c->round);
+    core_.on_complete(c->srcId, c->round, c->epoch);
   }
   ctx_ = nullptr;
 }
@@ -142,7 +142,7 @@ void MasterActor::send_init(int handle, const InitParams& p, const std::map<int,
 }
 
 void MasterActor::send_start(int handle, int round) {
-  handles_[handle]->tell(StartAllreduce{round}, ctx_->self());
+  handles_[handle]->tell(StartAllreduce{round, core_.epoch()}, ctx_->self());
 }
 
 void MasterActor::finished(int rounds) {

@@ -1,0 +1,135 @@
+"""Straggler tolerance end to end (the reference's reason to exist: thReduce / thComplete /
+thAllreduce / maxLag, AllreduceWorker.scala:15-17, AllreduceMaster.scala:17-20), driven by
+the fault-injection decorator on a threaded in-process cluster."""
+import threading
+
+import numpy as np
+import pytest
+
+from akka_allreduce_1_amd._native import C
+from akka_allreduce_1_amd.protocol import AllReduceInput, MemberUp
+
+
+def run_cluster(P, N, chunk, thA, thR, thC, lag, rounds, data=None, wrap=None, stop_after=None, timeout=30):
+    """Master + P workers; returns ({k: {iteration: (data, counts)}}, master_state, worker_states)."""
+    system = C.ActorSystem("ClusterSystem", False)
+    done = threading.Event()
+    master = system.master(P, thA, thR, thC, lag, N, rounds - 1, chunk, on_finished=lambda r: done.set())
+    outs = {k: {} for k in range(P)}
+    lock = threading.Lock()
+    data = data or (lambda k, it: (np.arange(N, dtype=np.float32) + it) * (k + 1))
+    workers = []
+
+    def make(k):
+        def src(req):
+            return AllReduceInput(data(k, req.iteration))
+
+        def sink(o):
+            with lock:
+                outs[k][o.iteration] = (np.asarray(o.data).copy(), list(o.count))
+            if stop_after and k == stop_after[0] and o.iteration == stop_after[1]:
+                threading.Thread(target=lambda: system.stop(workers[k])).start()
+
+        return src, sink
+
+    for k in range(P):
+        src, sink = make(k)
+        workers.append(system.worker(src, sink, f"worker{k}"))
+    refs = [wrap(k, w, system) if wrap else w for k, w in enumerate(workers)]
+    for r in refs:
+        master.tell(MemberUp(r, "worker", ""), None)
+    ok = done.wait(timeout)
+    system.await_idle(5.0)
+    mstate = system.master_state(master)
+    wstates = [system.worker_state(w) for w in workers]
+    system.shutdown()
+    assert ok, f"cluster did not finish: {mstate}"
+    return outs, mstate, wstates
+
+
+def counts_per_element(N, P, chunk, counts):
+    lay = C.BlockLayout(N, P, chunk)
+    maxc = max(lay.num_chunks(b) for b in range(P))
+    per = np.zeros(N, dtype=np.int64)
+    for b in range(P):
+        for i in range(lay.start[b], lay.end[b]):
+            per[i] = counts[b * maxc + (i - lay.start[b]) // chunk]
+    return per
+
+
+@pytest.mark.parametrize("P,N,chunk", [(4, 10, 2), (4, 6, 2), (3, 4, 2), (3, 7, 2)])
+def test_reference_crash_configs_now_exact(P, N, chunk):
+    """these (P, N, C) crash the reference (ArrayIndexOutOfBounds); here they run."""
+    outs, _, _ = run_cluster(P, N, chunk, 1.0, 1.0, 1.0, 1, 4)
+    for k in range(P):
+        for it in range(4):
+            exp = (np.arange(N) + it) * sum(range(1, P + 1))
+            np.testing.assert_array_equal(outs[k][it][0], exp)
+
+
+def test_lossy_scatter_partial_sums_are_consistent():
+    """25 % of the scatter traffic to worker 1 is lost; thresholds 0.75 let every round finish.
+    With all-ones inputs each output element equals the number of contributions summed into
+    its chunk, which must equal the count the worker reports for that chunk."""
+    P, N, chunk, rounds = 4, 64, 4, 12
+
+    def wrap(k, ref, system):
+        return C.faulty(system, ref, drop=0.25, kinds=["ScatterBlock"], seed=7) if k == 1 else ref
+
+    outs, mstate, ws = run_cluster(P, N, chunk, 0.75, 0.75, 0.75, 1, rounds, data=lambda k, it: np.ones(N, np.float32),
+                                   wrap=wrap)
+    assert mstate["finished"]
+    partial = 0
+    for k in range(P):
+        for it, (vals, counts) in outs[k].items():
+            per = counts_per_element(N, P, chunk, counts)
+            nz = per > 0
+            np.testing.assert_array_equal(vals[nz], per[nz].astype(np.float32))
+            assert np.all(vals[~nz] == 0)
+            partial += int((per[nz] < P).sum())
+    assert partial > 0, "expected some partial (threshold-fired) sums"
+
+
+def test_master_advances_without_a_silent_worker():
+    """thAllreduce = thReduce = thComplete = 0.75: from round 3 on worker 3 receives nothing
+    (a hung or partitioned node); the other three keep completing rounds with partial sums
+    and the master's barrier advances on 3 of 4 completions."""
+    P, N, chunk, rounds = 4, 16, 4, 10
+
+    def wrap(k, ref, system):
+        return C.faulty(system, ref, drop=1.0, round_lo=3, seed=5) if k == 3 else ref
+
+    outs, mstate, ws = run_cluster(P, N, chunk, 0.75, 0.75, 0.75, 1, rounds, wrap=wrap)
+    assert mstate["finished"]
+    assert max(outs[3]) <= 3
+    for k in range(3):
+        assert rounds - 1 in outs[k]
+        vals, counts = outs[k][rounds - 1]
+        assert max(counts) <= 3  # worker 3's contribution is missing from every late sum
+
+
+def test_delays_reorder_but_exact_sums_hold():
+    """Half of all scatters/reduces delayed by 5 ms (reordered across rounds): with exact
+    thresholds and maxLag 3 the future-round path absorbs the reordering and every sum is
+    exact."""
+    P, N, chunk, rounds = 3, 12, 2, 8
+
+    def wrap(k, ref, system):
+        return C.faulty(system, ref, delay_ms=5, delay_prob=0.5, kinds=["ScatterBlock", "ReduceBlock"], seed=k + 1)
+
+    outs, mstate, ws = run_cluster(P, N, chunk, 1.0, 1.0, 1.0, 3, rounds, wrap=wrap)
+    for k in range(P):
+        for it in range(rounds):
+            np.testing.assert_array_equal(outs[k][it][0], (np.arange(N) + it) * 6)
+
+
+def test_duplicates_are_detected():
+    """The reference double-counts a duplicated message (kept); the worker reports
+    it in its stats."""
+    P, N, chunk, rounds = 2, 8, 2, 4
+
+    def wrap(k, ref, system):
+        return C.faulty(system, ref, duplicate=1.0, kinds=["ReduceBlock"], seed=3) if k == 0 else ref
+
+    _, _, ws = run_cluster(P, N, chunk, 1.0, 1.0, 0.5, 1, rounds, wrap=wrap)
+    assert ws[0]["stats"]["duplicate_arrivals"] > 0
