@@ -23,6 +23,7 @@ import numpy as np
 
 from . import config as mconfig
 from ._native import C
+from .utils.metrics import MetricsRegistry, cluster_source, master_source, worker_source, write_trace
 
 
 def _cluster_cfg(cfg: mconfig.Config, port: int, roles: list[str]) -> "C.ClusterConfig":
@@ -41,7 +42,34 @@ def _cluster_cfg(cfg: mconfig.Config, port: int, roles: list[str]) -> "C.Cluster
 def _common(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--config", action="append", default=[], help="HOCON config file (repeatable)")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE", help="config override")
-    ap.add_argument("--metrics-json", default=None, help="write node/actor metrics here at exit")
+    ap.add_argument("--metrics-json", default=None, help="write the metrics snapshot here at exit")
+    ap.add_argument("--metrics-port", type=int, default=None, help="serve Prometheus /metrics on this port")
+    ap.add_argument("--trace-json", default=None, help="record a Chrome-trace timeline, written at exit")
+
+
+def _observe(args, cfg, labels: dict) -> MetricsRegistry:
+    reg = MetricsRegistry(labels)
+    trace = args.trace_json or cfg.get("mxar.trace.json")
+    if trace:
+        C.trace.enable(True)
+    if args.metrics_port is not None:
+        port = reg.serve(args.metrics_port)
+        print(f"[mxar] metrics on http://127.0.0.1:{port}/metrics", file=sys.stderr, flush=True)
+    return reg
+
+
+def _finish(args, cfg, reg: MetricsRegistry, extra: dict) -> None:
+    path = args.metrics_json or cfg.get("mxar.metrics.json")
+    if path:
+        snap = reg.snapshot()
+        snap.update(extra)
+        with open(path, "w") as f:
+            json.dump(snap, f, indent=1, default=str)
+    trace = args.trace_json or cfg.get("mxar.trace.json")
+    if trace:
+        n = write_trace(trace)
+        print(f"[mxar] wrote {n} trace events to {trace}", file=sys.stderr, flush=True)
+    reg.close()
 
 
 def _load(args) -> mconfig.Config:
@@ -56,16 +84,6 @@ def _install_signals(stop: threading.Event) -> None:
             signal.signal(s, lambda *_: stop.set())
         except ValueError:  # not the main thread
             pass
-
-
-def _write_metrics(path: str | None, node, extra: dict) -> None:
-    if not path:
-        return
-    st = node.stats()
-    doc = {k: getattr(st, k) for k in dir(st) if not k.startswith("_")}
-    doc.update(extra)
-    with open(path, "w") as f:
-        json.dump(doc, f, indent=1)
 
 
 def master_main(argv: list[str] | None = None) -> int:
@@ -97,6 +115,9 @@ def master_main(argv: list[str] | None = None) -> int:
                            liveBarrier=bool(cfg["mxar.allreduce.live-barrier"]), on_finished=finished, name="master")
     node = C.ClusterNode.start(system, _cluster_cfg(cfg, args.port, ["master"]))
     node.subscribe(master)
+    reg = _observe(args, cfg, {"role": "master", "address": node.address})
+    reg.register("master", master_source(system, master))
+    reg.register("cluster", cluster_source(node))
     print(f"[mxar-master] {node.address} totalWorkers={total} dataSize={data_size} maxChunkSize={chunk}",
           flush=True)
     _install_signals(stop)
@@ -106,7 +127,7 @@ def master_main(argv: list[str] | None = None) -> int:
     elapsed = time.time() - t0
     if done.is_set():
         print(f"[mxar-master] finished {rounds['n']} rounds in {elapsed:.2f}s", flush=True)
-    _write_metrics(args.metrics_json, node, {"rounds": rounds["n"], "elapsed_s": elapsed})
+    _finish(args, cfg, reg, {"rounds": rounds["n"], "elapsed_s": elapsed})
     node.leave()
     time.sleep(0.2)
     node.shutdown()
@@ -140,8 +161,11 @@ def worker_main(argv: list[str] | None = None) -> int:
         if args.max_outputs and count["n"] >= args.max_outputs:
             stop.set()
 
-    system.worker(source, sink, "worker")
+    wref = system.worker(source, sink, "worker")
     node = C.ClusterNode.start(system, _cluster_cfg(cfg, args.port, ["worker"]))
+    reg = _observe(args, cfg, {"role": "worker", "address": node.address})
+    reg.register("worker", worker_source(system, wref))
+    reg.register("cluster", cluster_source(node))
     events = system.probe("membership")
     node.subscribe(events)  # MemberUp events are queued: a short-lived master is never missed
     print(f"[mxar-worker] {node.address} sourceDataSize={n}", file=sys.stderr, flush=True)
@@ -153,7 +177,7 @@ def worker_main(argv: list[str] | None = None) -> int:
             seen_master = True
         if seen_master and not any("master" in m["roles"] for m in node.members()):
             break  # the master left / was downed: the job is over
-    _write_metrics(args.metrics_json, node, {"outputs": count["n"]})
+    _finish(args, cfg, reg, {"outputs": count["n"]})
     node.leave()
     time.sleep(0.1)
     node.shutdown()

@@ -10,6 +10,7 @@
 
 #include "../core/data_buffer.h"
 #include "../core/log.h"
+#include "../core/trace.h"
 #include "../core/master_core.h"
 #include "../core/worker_core.h"
 #include "../runtime/actor_system.h"
@@ -370,6 +371,16 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("min_chunks_required", &ArrivalCounters::min_chunks_required);
 
   // ---------------------------------------------------------------- logging
+  py::module_ tr = m.def_submodule("trace", "Chrome-trace timeline + roctx ranges (csrc/core/trace.h)");
+  tr.def("enable", [](bool on) { Tracer::get().enable(on); }, py::arg("on") = true);
+  tr.def("enabled", [] { return Tracer::get().enabled(); });
+  tr.def("set_roctx", [](bool on) { Tracer::get().set_roctx(on); });
+  tr.def("dump_json", [] { return Tracer::get().dump_json(); });
+  tr.def("size", [] { return Tracer::get().size(); });
+  tr.def("clear", [] { Tracer::get().clear(); });
+  tr.def("instant", [](const std::string& name, const std::string& args) { trace_instant("user", name, args); },
+         py::arg("name"), py::arg("args") = "");
+
   m.def("set_log_level", [](const std::string& l) { Logger::get().set_level(Logger::parse(l)); });
   m.def("get_log_level", [] { return std::string(Logger::level_name(Logger::get().level())); });
   m.def("set_log_sink", [](py::object fn) {
@@ -479,6 +490,14 @@ PYBIND11_MODULE(_C, m) {
         d["maxNumChunks"] = c.max_num_chunks();
         d["initialized"] = c.initialized();
         d["stats"] = worker_stats_dict(c.stats());
+        const RoundLatency lat = c.round_latency();
+        py::dict l;
+        l["count"] = lat.count;
+        l["p50_ms"] = lat.p50_ms;
+        l["p99_ms"] = lat.p99_ms;
+        l["mean_ms"] = lat.mean_ms;
+        l["max_ms"] = lat.max_ms;
+        d["round_latency"] = l;
         d["describe"] = c.describe();
         return d;
       })

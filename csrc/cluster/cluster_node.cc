@@ -14,6 +14,7 @@
 #include <random>
 
 #include "../core/log.h"
+#include "../core/trace.h"
 
 namespace mxar {
 
@@ -411,6 +412,7 @@ void ClusterNode::on_member_up(const MemberInfo& m) {
     ++stats_.members_up;
   }
   MXAR_LOG(INFO, "cluster", "Member is Up: " << m.address);
+  trace_instant("cluster", "MemberUp " + m.address);
   for (auto& s : subs) s->tell(member_up_event(m), nullptr);
 }
 
@@ -433,6 +435,7 @@ void ClusterNode::on_member_removed(const std::string& address) {
     ++stats_.members_removed;
   }
   MXAR_LOG(INFO, "cluster", "Member removed: " << address);
+  trace_instant("cluster", "MemberRemoved " + address);
   close_connection(address);
   for (auto& [target, watcher] : fire) watcher->tell(Terminated{target}, target);
   if (address == address_) joined_ = false;

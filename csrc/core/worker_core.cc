@@ -102,6 +102,7 @@ bool WorkerCore::on_start(const StartAllreduce& s) {
       broadcast(v, k, round_, c);
     }
     stats_.forced_completions++;
+    trace_instant("worker", "forced catch-up r" + std::to_string(round_), "{\"worker\":" + std::to_string(id_) + "}");
     MXAR_LOG(INFO, "worker", "----Catch up: force-completing round " << round_);
     complete(round_, 0);
   }
@@ -210,6 +211,8 @@ bool WorkerCore::on_reduce(const ReduceBlock& r) {
 // fetch (AllreduceWorker.scala:171-178)
 void WorkerCore::fetch(int round) {
   MXAR_LOG(INFO, "worker", "fetch " << round);
+  round_t0_[round] = Tracer::now_ns();
+  TraceScope span("worker", "fetch r" + std::to_string(round), "{\"worker\":" + std::to_string(id_) + "}");
   AllReduceInput in = fx_->fetch(AllReduceInputRequest{round});
   if (payload_size(in.data) != static_cast<size_t>(params_.dataSize))
     throw ProtocolError("Input data size " + std::to_string(payload_size(in.data)) +
@@ -230,6 +233,8 @@ void WorkerCore::flush(int completedRound, int row) {
 
 // scatter (AllreduceWorker.scala:194-209)
 void WorkerCore::scatter() {
+  TraceScope span("worker", "scatter r" + std::to_string(maxScattered_ + 1),
+                  "{\"worker\":" + std::to_string(id_) + "}");
   const int r = maxScattered_ + 1;
   const int C = params_.maxChunkSize;
   for (int i = 0; i < P_; ++i) {
@@ -280,6 +285,18 @@ std::pair<Payload, int> WorkerCore::reduce(int row, int chunkId) {
 // complete (AllreduceWorker.scala:253-268)
 void WorkerCore::complete(int completedRound, int row) {
   MXAR_LOG(DEBUG, "worker", "----Complete allreduce round " << completedRound);
+  TraceScope span("worker", "complete r" + std::to_string(completedRound),
+                  "{\"worker\":" + std::to_string(id_) + "}");
+  if (auto it = round_t0_.find(completedRound); it != round_t0_.end()) {
+    const double ms = (Tracer::now_ns() - it->second) / 1e6;
+    if (lat_ms_.size() < 4096)
+      lat_ms_.push_back(ms);
+    else
+      lat_ms_[lat_pos_] = ms;
+    lat_pos_ = (lat_pos_ + 1) % 4096;
+    ++lat_count_;
+    round_t0_.erase(it);
+  }
   flush(completedRound, row);
   data_ = plane_->zeros(0);
   stats_.complete_out++;
@@ -297,6 +314,22 @@ void WorkerCore::complete(int completedRound, int row) {
       std::fill(reduceCounts_.begin() + recycled * per_row, reduceCounts_.begin() + (recycled + 1) * per_row, 0);
     } while (completed_.count(round_));
   }
+}
+
+RoundLatency WorkerCore::round_latency() const {
+  RoundLatency r;
+  r.count = lat_count_;
+  if (lat_ms_.empty()) return r;
+  std::vector<double> v = lat_ms_;
+  std::sort(v.begin(), v.end());
+  auto q = [&](double p) { return v[std::min(v.size() - 1, static_cast<size_t>(p * (v.size() - 1) + 0.5))]; };
+  r.p50_ms = q(0.5);
+  r.p99_ms = q(0.99);
+  r.max_ms = v.back();
+  double s = 0;
+  for (double x : v) s += x;
+  r.mean_ms = s / v.size();
+  return r;
 }
 
 std::string WorkerCore::describe() const {

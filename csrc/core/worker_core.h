@@ -18,6 +18,7 @@
 #pragma once
 
 #include <functional>
+#include <map>
 #include <set>
 #include <string>
 #include <variant>
@@ -25,6 +26,7 @@
 
 #include "data_buffer.h"
 #include "protocol.h"
+#include "trace.h"
 
 namespace mxar {
 
@@ -53,6 +55,11 @@ class WorkerEffects {
   virtual void to_self(WorkerMsg&& m) = 0;
   virtual AllReduceInput fetch(const AllReduceInputRequest& req) = 0;  // dataSource
   virtual void sink(AllReduceOutput&& out) = 0;                        // dataSink
+};
+
+struct RoundLatency {  // fetch of round r -> its completion, over the last 4096 rounds
+  uint64_t count = 0;
+  double p50_ms = 0, p99_ms = 0, mean_ms = 0, max_ms = 0;
 };
 
 struct WorkerStats {
@@ -90,6 +97,7 @@ class WorkerCore {
   const DataBuffer& scatter_buf() const { return scatterBuf_; }
   const DataBuffer& reduce_buf() const { return reduceBuf_; }
   const WorkerStats& stats() const { return stats_; }
+  RoundLatency round_latency() const;
   const InitParams& params() const { return params_; }
   std::string describe() const;
 
@@ -117,6 +125,10 @@ class WorkerCore {
   // per physical row, per block owner: count carried by the ReduceBlock (for Output.count)
   std::vector<int> reduceCounts_;
   WorkerStats stats_;
+  std::map<int, uint64_t> round_t0_;
+  std::vector<double> lat_ms_;
+  size_t lat_pos_ = 0;
+  uint64_t lat_count_ = 0;
 };
 
 }  // namespace mxar

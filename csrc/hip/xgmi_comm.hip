@@ -18,6 +18,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "../core/trace.h"
 #include "device_common.h"
 #include "xgmi_comm.h"
 
@@ -599,6 +600,9 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
   }
   const bool oneshot =
       algo == Algo::OneShot ? (n * es <= c0.slot_bytes_) : (algo == Algo::Auto && n * es <= c0.oneshot_max_);
+  TraceScope span("xgmi", std::string(oneshot ? "oneshot " : "twoshot ") + std::to_string(n * es) + "B",
+                  "{\"rank\":" + std::to_string(c0.rank_) + ",\"ranks_in_launch\":" + std::to_string(group.size()) +
+                      "}");
   const int64_t seg = oneshot ? c0.slot_bytes_ / es : c0.world_ * (c0.slot_bytes_ / es);
   std::vector<const char*> ip(group.size());
   std::vector<char*> op(group.size());

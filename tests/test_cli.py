@@ -17,7 +17,7 @@ FAST = ["--set", "mxar.cluster.failure-detector.heartbeat-interval=100ms",
 
 
 @pytest.mark.slow
-def test_master_and_two_worker_processes():
+def test_master_and_two_worker_processes(tmp_path):
     port = free_port()
     seed = ["--set", f"mxar.cluster.seed-nodes=mxar.tcp://ClusterSystem@127.0.0.1:{port}"]
     exact = ["--set", "mxar.allreduce.th-reduce=1.0", "--set", "mxar.allreduce.th-complete=1.0",
@@ -26,8 +26,10 @@ def test_master_and_two_worker_processes():
     py = [sys.executable, "-m", "akka_allreduce_1_amd"]
     master = subprocess.Popen(py + ["master", str(port), "2", "10", "2"] + seed + exact + FAST, env=env,
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-    workers = [subprocess.Popen(py + ["worker", "0", "10", "--print-outputs"] + seed + FAST, env=env,
-                                stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for _ in range(2)]
+    workers = [subprocess.Popen(py + ["worker", "0", "10", "--print-outputs", "--metrics-json",
+                                      str(tmp_path / f"w{i}.json"), "--trace-json", str(tmp_path / f"t{i}.json")]
+                                + seed + FAST, env=env,
+                                stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for i in range(2)]
     try:
         mout, merr = master.communicate(timeout=60)
         assert master.returncode == 0, merr
@@ -39,6 +41,11 @@ def test_master_and_two_worker_processes():
             got = {r["iteration"]: r["data"] for r in rows}
             for it in range(5):  # rounds 0..maxRound
                 np.testing.assert_array_equal(got[it], 2 * (np.arange(10) + it))
+        for i in range(2):
+            m = json.loads((tmp_path / f"w{i}.json").read_text())
+            assert m["worker"]["rounds_completed"] == 5 and m["cluster"]["frames_in"] > 0
+            t = json.loads((tmp_path / f"t{i}.json").read_text())
+            assert any(e["name"].startswith("complete r") for e in t["traceEvents"])
     finally:
         for p in [master] + workers:
             if p.poll() is None:
