@@ -174,13 +174,15 @@ void ClusterNode::leave() {
 
 void ClusterNode::shutdown() {
   if (stopping_.exchange(true)) return;
+  // the accept loop polls with a short timeout and sees `stopping_`; only after it has
+  // exited is the listening socket closed (it reads listen_fd_)
+  if (accept_thread_.joinable()) accept_thread_.join();
+  if (ticker_thread_.joinable()) ticker_thread_.join();
   if (listen_fd_ >= 0) {
     ::shutdown(listen_fd_, SHUT_RDWR);
     ::close(listen_fd_);
     listen_fd_ = -1;
   }
-  if (accept_thread_.joinable()) accept_thread_.join();
-  if (ticker_thread_.joinable()) ticker_thread_.join();
   {
     std::lock_guard<std::mutex> g(readers_mu_);
     for (int fd : reader_fds_)

@@ -7,7 +7,12 @@
 #include <sstream>
 #include <thread>
 
+#ifndef MXAR_NO_ROCTX
 #include <rocprofiler-sdk-roctx/roctx.h>
+#else  // host-only sanitizer builds (tools/sanitize.py) do not link roctx
+static inline void roctxRangePushA(const char*) {}
+static inline void roctxRangePop() {}
+#endif
 
 namespace mxar {
 

@@ -8,6 +8,20 @@ namespace mxar {
 
 namespace {
 std::atomic<uint64_t> g_uid{1};
+
+// Timed condition-variable waits go through system_clock deadlines: libstdc++ implements
+// steady_clock waits with pthread_cond_clockwait, which ThreadSanitizer (GCC 11) does not
+// intercept - it would miss the unlock inside the wait and report phantom double locks.
+// A system_clock deadline uses pthread_cond_timedwait, which every sanitizer models.
+template <class Pred>
+bool cv_wait_for(std::condition_variable& cv, std::unique_lock<std::mutex>& lk, std::chrono::milliseconds d,
+                 Pred pred) {
+  const auto deadline = std::chrono::system_clock::now() + d;
+  while (!pred()) {
+    if (cv.wait_until(lk, deadline) == std::cv_status::timeout) return pred();
+  }
+  return true;
+}
 }
 
 ActorRefBase::ActorRefBase() : uid_(g_uid.fetch_add(1)) {}
@@ -99,7 +113,7 @@ std::optional<Envelope> ProbeRef::receive(std::chrono::milliseconds timeout) {
     return e;
   }
   std::unique_lock<std::mutex> lk(mu_);
-  if (!cv_.wait_for(lk, timeout, [&] { return !q_.empty(); })) return std::nullopt;
+  if (!cv_wait_for(cv_, lk, timeout, [&] { return !q_.empty(); })) return std::nullopt;
   Envelope e = std::move(q_.front());
   q_.pop_front();
   return e;
@@ -361,7 +375,7 @@ bool ActorSystem::await_idle(std::chrono::milliseconds timeout) {
     return true;
   }
   std::unique_lock<std::mutex> lk(rq_mu_);
-  return idle_cv_.wait_for(lk, timeout, [&] { return busy_ == 0 && runq_.empty(); });
+  return cv_wait_for(idle_cv_, lk, timeout, [&] { return busy_ == 0 && runq_.empty(); });
 }
 
 // ------------------------------------------------------------------------ timers
@@ -442,7 +456,8 @@ void ActorSystem::timer_loop() {
   while (!shutdown_) {
     auto next = std::chrono::steady_clock::now() + std::chrono::milliseconds(200);
     for (auto& t : timers_) next = std::min(next, t.due);
-    timer_cv_.wait_until(lk, next);
+    const auto wait = std::chrono::duration_cast<std::chrono::microseconds>(next - std::chrono::steady_clock::now());
+    if (wait.count() > 0) timer_cv_.wait_until(lk, std::chrono::system_clock::now() + wait);
     if (shutdown_) break;
     std::vector<std::pair<ActorRef, Message>> fire;
     fire_due_timers_locked(std::chrono::steady_clock::now(), fire);

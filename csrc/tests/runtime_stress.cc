@@ -1,0 +1,136 @@
+// Host-runtime stress program for sanitizer builds (ThreadSanitizer / AddressSanitizer):
+// the threaded actor system, the TCP cluster layer and the full master/worker protocol,
+// with fault injection, exactly as the CLIs run them - but in one process without Python,
+// so the sanitizer sees every thread. Exit 0 = all rounds exact and clean shutdown.
+//
+//   build + run: python tools/sanitize.py --sanitize thread
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../cluster/cluster_node.h"
+#include "../core/log.h"
+#include "../runtime/allreduce_actors.h"
+#include "../runtime/fault_injector.h"
+
+using namespace mxar;
+
+static bool wait_until(const std::function<bool()>& pred, double timeout_s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < timeout_s) {
+    if (pred()) return true;
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  }
+  return false;
+}
+
+// In-process threaded cluster with reordering faults; exact thresholds.
+static int run_local(int P, int N, int C, int rounds) {
+  auto sys = std::make_shared<ActorSystem>("ClusterSystem", ActorSystem::Mode::Threaded, 4);
+  std::atomic<bool> done{false};
+  MasterParams mp{P, 1.f, 1.f, 1.f, 3, N, rounds - 1, C, false};
+  ActorRef master = sys->actor_of(std::make_unique<MasterActor>(mp, [&](int) { done = true; }), "master");
+  std::mutex mu;
+  std::vector<std::vector<std::vector<float>>> outs(P);
+  std::vector<ActorRef> refs;
+  for (int k = 0; k < P; ++k) {
+    DataSource src = [N, k](const AllReduceInputRequest& r) {
+      std::vector<float> v(N);
+      for (int i = 0; i < N; ++i) v[i] = static_cast<float>((i + r.iteration) * (k + 1));
+      return AllReduceInput{make_host_payload(std::move(v))};
+    };
+    DataSink sink = [&, k](const AllReduceOutput& o) {
+      std::lock_guard<std::mutex> g(mu);
+      if (static_cast<int>(outs[k].size()) <= o.iteration) outs[k].resize(o.iteration + 1);
+      outs[k][o.iteration] = o.data->to_host();
+    };
+    ActorRef w = sys->actor_of(std::make_unique<WorkerActor>(src, sink), "worker" + std::to_string(k));
+    FaultPolicy fp;
+    fp.delay_ms = 2;
+    fp.delay_prob = 0.3;
+    fp.kinds = {"ScatterBlock", "ReduceBlock"};
+    fp.seed = 11 + k;
+    refs.push_back(std::make_shared<FaultyRef>(sys.get(), w, fp));
+  }
+  for (auto& r : refs) master->tell(MemberUp{r, "worker", ""}, nullptr);
+  const bool ok = wait_until([&] { return done.load(); }, 60);
+  sys->await_idle(std::chrono::milliseconds(5000));
+  sys->shutdown();
+  if (!ok) {
+    std::fprintf(stderr, "local cluster did not finish\n");
+    return 1;
+  }
+  const float tri = P * (P + 1) / 2.f;
+  for (int k = 0; k < P; ++k)
+    for (int r = 0; r < rounds; ++r)
+      for (int i = 0; i < N; ++i)
+        if (std::fabs(outs[k][r][i] - (i + r) * tri) > 1e-3f) {
+          std::fprintf(stderr, "bad sum worker %d round %d idx %d\n", k, r, i);
+          return 1;
+        }
+  return 0;
+}
+
+// Three nodes over TCP on 127.0.0.1: master node + two worker nodes.
+static int run_tcp(int rounds) {
+  const int N = 10, C = 2;
+  auto msys = std::make_shared<ActorSystem>("ClusterSystem", ActorSystem::Mode::Threaded, 2);
+  std::atomic<bool> done{false};
+  MasterParams mp{2, 1.f, 1.f, 1.f, 1, N, rounds - 1, C, false};
+  ActorRef master = msys->actor_of(std::make_unique<MasterActor>(mp, [&](int) { done = true; }), "master");
+  ClusterConfig mc;
+  mc.port = 0;
+  mc.roles = {"master"};
+  mc.heartbeat_interval_s = 0.05;
+  auto mnode = ClusterNode::start(msys, mc);
+  mnode->subscribe(master);
+  const std::string seed = mnode->address();
+  std::vector<std::shared_ptr<ActorSystem>> wsys;
+  std::vector<std::shared_ptr<ClusterNode>> wnodes;
+  std::atomic<int> outputs{0};
+  for (int k = 0; k < 2; ++k) {
+    auto s = std::make_shared<ActorSystem>("ClusterSystem", ActorSystem::Mode::Threaded, 2);
+    DataSource src = [N](const AllReduceInputRequest& r) {
+      std::vector<float> v(N);
+      for (int i = 0; i < N; ++i) v[i] = static_cast<float>(i + r.iteration);
+      return AllReduceInput{make_host_payload(std::move(v))};
+    };
+    DataSink sink = [&](const AllReduceOutput&) { outputs++; };
+    s->actor_of(std::make_unique<WorkerActor>(src, sink), "worker");
+    ClusterConfig wc;
+    wc.port = 0;
+    wc.roles = {"worker"};
+    wc.seed_nodes = {seed};
+    wc.heartbeat_interval_s = 0.05;
+    wnodes.push_back(ClusterNode::start(s, wc));
+    wsys.push_back(s);
+  }
+  const bool ok = wait_until([&] { return done.load() && outputs.load() >= 2 * rounds; }, 60);
+  for (auto& n : wnodes) n->leave();
+  for (auto& n : wnodes) n->shutdown();
+  mnode->shutdown();
+  for (auto& s : wsys) s->shutdown();
+  msys->shutdown();
+  if (!ok) {
+    std::fprintf(stderr, "tcp cluster did not finish (outputs %d)\n", outputs.load());
+    return 1;
+  }
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  Logger::get().set_level(LogLevel::ERROR);
+  const std::string only = argc > 1 ? argv[1] : "";
+  int rc = 0;
+  if (only.empty() || only == "local") rc = run_local(4, 37, 3, 30);
+  if (rc == 0 && (only.empty() || only == "local2")) rc = run_local(3, 9, 2, 30);
+  if (rc == 0 && (only.empty() || only == "tcp")) rc = run_tcp(20);
+  std::printf(rc == 0 ? "runtime_stress: OK\n" : "runtime_stress: FAILED\n");
+  return rc;
+}
