@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
 import signal
 import sys
 import threading
@@ -93,6 +94,8 @@ def master_main(argv: list[str] | None = None) -> int:
     ap.add_argument("dataSize", nargs="?", type=int, default=None)
     ap.add_argument("maxChunkSize", nargs="?", type=int, default=None)
     ap.add_argument("--linger", action="store_true", help="keep running after the last round (reference behaviour)")
+    ap.add_argument("--checkpoint", default=None, help="write {round, epoch} here after every completed round")
+    ap.add_argument("--resume", action="store_true", help="start at the round after the one in --checkpoint")
     _common(ap)
     args = ap.parse_args(argv)
     cfg = _load(args)
@@ -109,10 +112,24 @@ def master_main(argv: list[str] | None = None) -> int:
         rounds["n"] = r
         done.set()
 
+    start_round = 0
+    if args.resume and args.checkpoint and os.path.exists(args.checkpoint):
+        with open(args.checkpoint) as f:
+            start_round = int(json.load(f)["round"]) + 1
+        print(f"[mxar-master] resuming at round {start_round} from {args.checkpoint}", flush=True)
+
+    def on_round(r: int, epoch: int) -> None:
+        if args.checkpoint:  # atomic replace: a crash never leaves a torn checkpoint
+            tmp = args.checkpoint + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump({"round": r, "epoch": epoch, "dataSize": data_size, "totalWorkers": total}, f)
+            os.replace(tmp, args.checkpoint)
+
     master = system.master(total, float(cfg["mxar.allreduce.th-allreduce"]), float(cfg["mxar.allreduce.th-reduce"]),
                            float(cfg["mxar.allreduce.th-complete"]), int(cfg["mxar.allreduce.max-lag"]), data_size,
                            int(cfg["mxar.allreduce.max-round"]), chunk,
-                           liveBarrier=bool(cfg["mxar.allreduce.live-barrier"]), on_finished=finished, name="master")
+                           liveBarrier=bool(cfg["mxar.allreduce.live-barrier"]), on_finished=finished, name="master",
+                           startRound=start_round, on_round=on_round)
     node = C.ClusterNode.start(system, _cluster_cfg(cfg, args.port, ["master"]))
     node.subscribe(master)
     reg = _observe(args, cfg, {"role": "master", "address": node.address})

@@ -180,12 +180,14 @@ PYBIND11_MODULE(_C, m) {
   // ---------------------------------------------------------------- messages
   py::class_<InitWorkers>(m, "InitWorkers")
       .def(py::init([](std::map<int, ActorRef> workers, ActorRef master, int destId, float thReduce,
-                       float thComplete, int maxLag, int dataSize, int maxChunkSize, int64_t epoch) {
+                       float thComplete, int maxLag, int dataSize, int maxChunkSize, int64_t epoch, int startRound) {
              return InitWorkers{std::move(workers), std::move(master), destId, thReduce, thComplete,
-                                maxLag, dataSize, maxChunkSize, epoch};
+                                maxLag, dataSize, maxChunkSize, epoch, startRound};
            }),
            py::arg("workers"), py::arg("master"), py::arg("destId"), py::arg("thReduce"), py::arg("thComplete"),
-           py::arg("maxLag"), py::arg("dataSize"), py::arg("maxChunkSize"), py::arg("epoch") = 0)
+           py::arg("maxLag"), py::arg("dataSize"), py::arg("maxChunkSize"), py::arg("epoch") = 0,
+           py::arg("startRound") = 0)
+      .def_readwrite("startRound", &InitWorkers::startRound)
       .def_readwrite("workers", &InitWorkers::workers)
       .def_readwrite("master", &InitWorkers::master)
       .def_readwrite("destId", &InitWorkers::destId)
@@ -434,9 +436,17 @@ PYBIND11_MODULE(_C, m) {
           }, py::arg("source"), py::arg("sink") = py::none(), py::arg("name") = "", py::arg("plane") = nullptr)
       .def("master", [](ActorSystem& s, int totalWorkers, float thAllreduce, float thReduce, float thComplete,
                         int maxLag, int dataSize, int maxRound, int maxChunkSize, bool liveBarrier,
-                        py::object on_finished, std::string name) {
+                        py::object on_finished, std::string name, int startRound, py::object on_round) {
             MasterParams p{totalWorkers, thAllreduce, thReduce, thComplete, maxLag, dataSize, maxRound,
-                           maxChunkSize, liveBarrier};
+                           maxChunkSize, liveBarrier, startRound};
+            MasterActor::RoundCallback rcb;
+            if (!on_round.is_none()) {
+              auto h = std::make_shared<PyCallable>(std::move(on_round));
+              rcb = [h](int round, int64_t epoch) {
+                py::gil_scoped_acquire g;
+                h->fn(round, epoch);
+              };
+            }
             MasterActor::FinishedCallback cb;
             if (!on_finished.is_none()) {
               auto h = std::make_shared<PyCallable>(std::move(on_finished));
@@ -445,10 +455,11 @@ PYBIND11_MODULE(_C, m) {
                 h->fn(rounds);
               };
             }
-            return s.actor_of(std::make_unique<MasterActor>(p, cb), std::move(name));
+            return s.actor_of(std::make_unique<MasterActor>(p, cb, rcb), std::move(name));
           }, py::arg("totalWorkers"), py::arg("thAllreduce"), py::arg("thReduce"), py::arg("thComplete"),
           py::arg("maxLag"), py::arg("dataSize"), py::arg("maxRound"), py::arg("maxChunkSize"),
-          py::arg("liveBarrier") = false, py::arg("on_finished") = py::none(), py::arg("name") = "master")
+          py::arg("liveBarrier") = false, py::arg("on_finished") = py::none(), py::arg("name") = "master",
+          py::arg("startRound") = 0, py::arg("on_round") = py::none())
       .def("probe", &ActorSystem::make_probe, py::arg("name") = "")
       .def("lookup", &ActorSystem::lookup)
       .def("stop", &ActorSystem::stop)

@@ -36,6 +36,7 @@ void encode_message(Writer& w, const Message& m, const RefCodec& rc) {
           w.i32(x.dataSize);
           w.i32(x.maxChunkSize);
           w.i64(x.epoch);
+          w.i32(x.startRound);
         } else if constexpr (std::is_same_v<T, StartAllreduce>) {
           w.i32(x.round);
           w.i64(x.epoch);
@@ -92,6 +93,7 @@ Message decode_message(Reader& r, RefCodec& rc) {
       x.dataSize = r.i32();
       x.maxChunkSize = r.i32();
       x.epoch = r.i64();
+      x.startRound = r.i32();
       return x;
     }
     case 1: {

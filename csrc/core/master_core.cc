@@ -19,7 +19,8 @@ void MasterCore::on_member_up(int handle) {
   if (static_cast<int>(workers_.size()) >= f32_threshold_count(p_.thAllreduce, p_.totalWorkers)) {
     MXAR_LOG(INFO, "master", "----" << workers_.size() << " (out of " << p_.totalWorkers << ") workers are up");
     init_workers();
-    round_ = 0;
+    round_ = std::max(0, p_.startRound);
+    last_reported_ = round_ - 1;
     finished_ = false;
     start_allreduce();
   }
@@ -65,6 +66,10 @@ void MasterCore::on_complete(int srcId, int round, int64_t epoch) {
   // numComplete >= totalWorkers * thAllreduce : float compare, not truncated (:62)
   volatile float need = barrier_base() * p_.thAllreduce;
   if (static_cast<float>(numComplete_) >= need) {
+    if (last_reported_ < round_) {
+      last_reported_ = round_;
+      fx_->round_completed(round_, epoch_);
+    }
     if (round_ < p_.maxRound) {
       MXAR_LOG(INFO, "master", "----" << numComplete_ << " (out of " << p_.totalWorkers
                                       << ") workers complete round " << round_);
@@ -98,6 +103,7 @@ void MasterCore::init_workers() {
     p.dataSize = p_.dataSize;
     p.maxChunkSize = p_.maxChunkSize;
     p.epoch = epoch_;
+    p.startRound = std::max(0, p_.startRound);
     fx_->send_init(h, p, workers_);
   }
 }

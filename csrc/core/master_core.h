@@ -31,6 +31,7 @@ struct MasterParams {
   int maxRound = 100;
   int maxChunkSize = 2;
   bool liveBarrier = false;
+  int startRound = 0;  // resume point (checkpoint/resume)
 };
 
 class MasterEffects {
@@ -40,6 +41,8 @@ class MasterEffects {
   virtual void send_init(int handle, const InitParams& p, const std::map<int, int>& ids) = 0;
   virtual void send_start(int handle, int round) = 0;
   virtual void finished(int rounds) = 0;
+  // Called once per round that reached the barrier (the checkpoint hook).
+  virtual void round_completed(int /*round*/, int64_t /*epoch*/) {}
 };
 
 struct MasterStats {
@@ -74,6 +77,7 @@ class MasterCore {
   int round_ = -1;              // :29
   int numComplete_ = 0;         // :30
   int64_t epoch_ = 0;
+  int last_reported_ = -1;
   bool finished_ = false;
   MasterStats stats_;
 };

@@ -73,6 +73,9 @@ struct InitWorkers {  // AllreduceMessage.scala:7-16
   // Extension (not in the reference): membership epoch, bumped by the master on every
   // (re-)initialisation so late messages of an older epoch can be told apart.
   int64_t epoch = 0;
+  // Extension: first round of this epoch - 0 normally, the checkpointed
+  // round when a job resumes (workers start there instead of replaying earlier rounds).
+  int startRound = 0;
 };
 
 // Extension: the round messages carry the membership epoch of the

@@ -35,9 +35,9 @@ void WorkerCore::on_init(const InitParams& p) {
   params_ = p;
   id_ = p.destId;
   P_ = p.numPeers;
-  round_ = 0;  // clear round info to start over
-  maxRound_ = -1;
-  maxScattered_ = -1;
+  round_ = std::max(0, p.startRound);  // clear round info to start over (at the resume round)
+  maxRound_ = round_ - 1;
+  maxScattered_ = round_ - 1;
   completed_.clear();
   data_ = plane_->zeros(static_cast<size_t>(p.dataSize));
 

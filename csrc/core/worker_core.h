@@ -39,6 +39,7 @@ struct InitParams {
   int dataSize = 0;
   int maxChunkSize = 1024;
   int64_t epoch = 0;
+  int startRound = 0;
 };
 
 // Messages the worker core can emit to a peer or to itself.

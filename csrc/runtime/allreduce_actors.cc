@@ -24,6 +24,7 @@ void WorkerActor::receive(Envelope& env, ActorContext& ctx) {
       p.dataSize = m.dataSize;
       p.maxChunkSize = m.maxChunkSize;
       p.epoch = m.epoch;
+      p.startRound = m.startRound;
       w->peers_ = m.workers;
       w->master_ = m.master;
       w->core_.on_init(p);
@@ -98,8 +99,8 @@ void WorkerActor::sink(AllReduceOutput&& out) {
 }
 
 // ------------------------------------------------------------------------ master
-MasterActor::MasterActor(MasterParams p, FinishedCallback on_finished)
-    : core_(this, p), on_finished_(std::move(on_finished)) {}
+MasterActor::MasterActor(MasterParams p, FinishedCallback on_finished, RoundCallback on_round)
+    : core_(this, p), on_finished_(std::move(on_finished)), on_round_(std::move(on_round)) {}
 
 int MasterActor::handle_of(const ActorRef& ref, bool create) {
   for (size_t i = 0; i < handles_.size(); ++i)
@@ -138,6 +139,7 @@ void MasterActor::send_init(int handle, const InitParams& p, const std::map<int,
   m.dataSize = p.dataSize;
   m.maxChunkSize = p.maxChunkSize;
   m.epoch = p.epoch;
+  m.startRound = p.startRound;
   handles_[handle]->tell(Message(std::move(m)), ctx_->self());
 }
 
@@ -147,6 +149,10 @@ void MasterActor::send_start(int handle, int round) {
 
 void MasterActor::finished(int rounds) {
   if (on_finished_) on_finished_(rounds);
+}
+
+void MasterActor::round_completed(int round, int64_t epoch) {
+  if (on_round_) on_round_(round, epoch);
 }
 
 }  // namespace mxar

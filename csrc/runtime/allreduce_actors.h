@@ -47,7 +47,8 @@ class WorkerActor final : public Actor, public WorkerEffects {
 class MasterActor final : public Actor, public MasterEffects {
  public:
   using FinishedCallback = std::function<void(int rounds)>;
-  MasterActor(MasterParams p, FinishedCallback on_finished = nullptr);
+  using RoundCallback = std::function<void(int round, int64_t epoch)>;  // checkpoint hook
+  MasterActor(MasterParams p, FinishedCallback on_finished = nullptr, RoundCallback on_round = nullptr);
   void receive(Envelope& env, ActorContext& ctx) override;
   std::string kind() const override { return "master"; }
 
@@ -55,6 +56,7 @@ class MasterActor final : public Actor, public MasterEffects {
   void send_init(int handle, const InitParams& p, const std::map<int, int>& ids) override;
   void send_start(int handle, int round) override;
   void finished(int rounds) override;
+  void round_completed(int round, int64_t epoch) override;
 
   const MasterCore& core() const { return core_; }
 
@@ -63,6 +65,7 @@ class MasterActor final : public Actor, public MasterEffects {
   MasterCore core_;
   std::vector<ActorRef> handles_;
   FinishedCallback on_finished_;
+  RoundCallback on_round_;
   ActorContext* ctx_ = nullptr;
 };
 

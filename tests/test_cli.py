@@ -24,7 +24,9 @@ def test_master_and_two_worker_processes(tmp_path):
              "--set", "mxar.allreduce.max-round=4"]
     env = dict(os.environ, PYTHONPATH=ROOT)
     py = [sys.executable, "-m", "akka_allreduce_1_amd"]
-    master = subprocess.Popen(py + ["master", str(port), "2", "10", "2"] + seed + exact + FAST, env=env,
+    ckpt = tmp_path / "ckpt.json"
+    master = subprocess.Popen(py + ["master", str(port), "2", "10", "2", "--checkpoint", str(ckpt)] + seed + exact + FAST,
+                              env=env,
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     workers = [subprocess.Popen(py + ["worker", "0", "10", "--print-outputs", "--metrics-json",
                                       str(tmp_path / f"w{i}.json"), "--trace-json", str(tmp_path / f"t{i}.json")]
@@ -41,6 +43,7 @@ def test_master_and_two_worker_processes(tmp_path):
             got = {r["iteration"]: r["data"] for r in rows}
             for it in range(5):  # rounds 0..maxRound
                 np.testing.assert_array_equal(got[it], 2 * (np.arange(10) + it))
+        assert json.loads(ckpt.read_text())["round"] == 4  # last completed round (0..maxRound)
         for i in range(2):
             m = json.loads((tmp_path / f"w{i}.json").read_text())
             assert m["worker"]["rounds_completed"] == 5 and m["cluster"]["frames_in"] > 0

@@ -133,3 +133,34 @@ def test_duplicates_are_detected():
 
     _, _, ws = run_cluster(P, N, chunk, 1.0, 1.0, 0.5, 1, rounds, wrap=wrap)
     assert ws[0]["stats"]["duplicate_arrivals"] > 0
+
+
+def test_resume_from_checkpointed_round():
+    """Checkpoint/resume of the control state: the master reports every
+    completed round; a new job started at round R re-initialises workers there (InitWorkers
+    startRound) and they fetch round R first - no replay of rounds 0..R-1."""
+    P, N, chunk = 2, 8, 2
+    system = C.ActorSystem("ClusterSystem", False)
+    done = threading.Event()
+    seen_rounds, fetched = [], []
+    master = system.master(P, 1.0, 1.0, 1.0, 1, N, 9, chunk, on_finished=lambda r: done.set(), startRound=6,
+                           on_round=lambda r, e: seen_rounds.append(r))
+    outs = {}
+
+    def src(req):
+        fetched.append(req.iteration)
+        return AllReduceInput(np.arange(N, dtype=np.float32) + req.iteration)
+
+    def sink(o):
+        outs.setdefault(o.iteration, np.asarray(o.data).copy())
+
+    ws = [system.worker(src, sink, f"w{k}") for k in range(P)]
+    for w in ws:
+        master.tell(MemberUp(w, "worker", ""), None)
+    assert done.wait(20)
+    system.await_idle(5.0)
+    system.shutdown()
+    assert seen_rounds == [6, 7, 8, 9]
+    assert min(fetched) == 6
+    for r in range(6, 10):
+        np.testing.assert_array_equal(outs[r], 2 * (np.arange(N) + r))
