@@ -1,4 +1,5 @@
 #!/bin/bash
+# GPU CI: the MI355X test suite, smoke() and the 1-GPU bench (run via gpurun)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out

@@ -1,4 +1,5 @@
 #!/bin/bash
+# GPU tests + single-GPU multi-rank kernel bench with both fence modes (run via gpurun)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
