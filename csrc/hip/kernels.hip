@@ -31,32 +31,38 @@ static int grid_for(int64_t packs) {
   return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(g, cap)));
 }
 
+// Tiled like the fastest copy variant: each workgroup sweeps contiguous tiles of
+// 2 x 4 KiB per slot (one 1 KiB wave access per pack), tiles dealt grid-stride; all P
+// slot loads of a tile are in flight together.
 template <class E>
 __global__ __launch_bounds__(kThreads) void reduce_slots_kernel(const char* __restrict__ slots, int64_t stride_bytes,
                                                                  int nslots, char* __restrict__ out, int64_t n,
                                                                  float scale) {
+  constexpr int U = 2;
+  constexpr int64_t kTile = static_cast<int64_t>(U) * kThreads;
   const int64_t npk = n / E::ELEMS;
-  const int64_t step = static_cast<int64_t>(gridDim.x) * kThreads;
-  int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  for (; i + step < npk; i += 2 * step) {
-    Acc<E> a0, a1;
-    a0.zero();
-    a1.zero();
+  const int64_t ntiles = npk / kTile;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t base = t * kTile + threadIdx.x;
+    Acc<E> a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u].zero();
     for (int p = 0; p < nslots; ++p) {
       const char* s = slots + p * stride_bytes;
-      const Pack16 v0 = ld16(s + i * 16);
-      const Pack16 v1 = ld16(s + (i + step) * 16);
-      a0.add(v0);
-      a1.add(v1);
+      Pack16 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld16(s + (base + u * kThreads) * 16);
+#pragma unroll
+      for (int u = 0; u < U; ++u) a[u].add(v[u]);
     }
-    if (scale != 1.f) {
-      a0.scale(scale);
-      a1.scale(scale);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (scale != 1.f) a[u].scale(scale);
+      st16(out + (base + u * kThreads) * 16, a[u].pack());
     }
-    st16(out + i * 16, a0.pack());
-    st16(out + (i + step) * 16, a1.pack());
   }
-  for (; i < npk; i += step) {
+  for (int64_t i = ntiles * kTile + static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < npk;
+       i += static_cast<int64_t>(gridDim.x) * kThreads) {
     Acc<E> a0;
     a0.zero();
     for (int p = 0; p < nslots; ++p) a0.add(ld16(slots + p * stride_bytes + i * 16));
@@ -78,7 +84,7 @@ void launch_reduce_slots(const void* slots, int64_t slot_stride_elems, int nslot
   if (((reinterpret_cast<uintptr_t>(slots) | reinterpret_cast<uintptr_t>(out)) & 15) || ((slot_stride_elems * es) & 15))
     throw std::invalid_argument("reduce_slots: slots, out and slot stride must be 16-byte aligned");
   const int64_t npk = n * es / 16;
-  const int g = grid_for(std::max<int64_t>(npk / 2, 1));
+  const int g = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(npk / (2 * kThreads), 2048)));
   if (dt == DType::F32)
     hipLaunchKernelGGL(reduce_slots_kernel<F32>, dim3(g), dim3(kThreads), 0, stream, static_cast<const char*>(slots),
                        slot_stride_elems * es, nslots, static_cast<char*>(out), n, scale);
@@ -136,29 +142,93 @@ void launch_fill_uniform(void* dst, int64_t n, uint64_t seed, DType dt, hipStrea
 
 // Plain device copy, 16 B per lane (used for the 1-rank allreduce: a kernel keeps the copy
 // in stream order with the kernels around it, with no DMA-engine hand-off).
+// Variants (A/B study, tools/bench_copy.py): UNROLL packs in flight per lane, NT = nontemporal
+// loads/stores (streaming data that is not re-read soon should not displace cached lines).
+template <int UNROLL, bool NT>
 __global__ __launch_bounds__(kThreads) void copy16_kernel(const char* __restrict__ in, char* __restrict__ out,
                                                            int64_t bytes) {
   const int64_t npk = bytes / 16;
   const int64_t step = static_cast<int64_t>(gridDim.x) * kThreads;
+  const Pack16* src = reinterpret_cast<const Pack16*>(in);
+  Pack16* dst = reinterpret_cast<Pack16*>(out);
   int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  for (; i + step < npk; i += 2 * step) {
-    const Pack16 a = ld16(in + i * 16);
-    const Pack16 b = ld16(in + (i + step) * 16);
-    st16(out + i * 16, a);
-    st16(out + (i + step) * 16, b);
+  for (; i + (UNROLL - 1) * step < npk; i += UNROLL * step) {
+    Pack16 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) v[u] = NT ? __builtin_nontemporal_load(src + i + u * step) : src[i + u * step];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      if (NT)
+        __builtin_nontemporal_store(v[u], dst + i + u * step);
+      else
+        dst[i + u * step] = v[u];
+    }
   }
-  for (; i < npk; i += step) st16(out + i * 16, ld16(in + i * 16));
+  for (; i < npk; i += step) dst[i] = src[i];
   const int64_t t = npk * 16 + static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
   if (t < bytes) out[t] = in[t];
 }
+
+// Blocked variant: workgroup-contiguous tiles of UNROLL x 4 KiB (one 1 KiB wave access per
+// pack, all packs of a tile in one contiguous region), tiles dealt grid-stride.
+template <int UNROLL, bool NT>
+__global__ __launch_bounds__(kThreads) void copy_tiles_kernel(const char* __restrict__ in, char* __restrict__ out,
+                                                               int64_t bytes) {
+  constexpr int64_t kTile = static_cast<int64_t>(UNROLL) * kThreads;  // packs per tile
+  const int64_t npk = bytes / 16;
+  const int64_t ntiles = npk / kTile;
+  const Pack16* src = reinterpret_cast<const Pack16*>(in);
+  Pack16* dst = reinterpret_cast<Pack16*>(out);
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t base = t * kTile + threadIdx.x;
+    Pack16 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) v[u] = NT ? __builtin_nontemporal_load(src + base + u * kThreads) : src[base + u * kThreads];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      if (NT)
+        __builtin_nontemporal_store(v[u], dst + base + u * kThreads);
+      else
+        dst[base + u * kThreads] = v[u];
+    }
+  }
+  for (int64_t i = ntiles * kTile + static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < npk;
+       i += static_cast<int64_t>(gridDim.x) * kThreads)
+    dst[i] = src[i];
+  const int64_t t = npk * 16 + static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (t < bytes) out[t] = in[t];
+}
+
+static int g_copy_variant = -1;  // -1: default (see launch_copy)
+
+void set_copy_variant(int v) { g_copy_variant = v; }
 
 void launch_copy(const void* src, void* dst, int64_t bytes, hipStream_t stream) {
   if (bytes <= 0) return;
   if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15)
     throw std::invalid_argument("copy: buffers must be 16-byte aligned");
-  const int g = grid_for(std::max<int64_t>(bytes / 32, 1));
-  hipLaunchKernelGGL(copy16_kernel, dim3(g), dim3(kThreads), 0, stream, static_cast<const char*>(src),
-                     static_cast<char*>(dst), bytes);
+  const char* s = static_cast<const char*>(src);
+  char* d = static_cast<char*>(dst);
+  const int v = g_copy_variant < 0 ? 5 : g_copy_variant;  // 5: measured fastest (profiles/copy_variants.md)
+  // grid: ~4 packs per thread for the unrolled variants, capped at 8 WG/CU
+  const int unroll = (v == 0) ? 2 : 4;
+  const int g = grid_for(std::max<int64_t>(bytes / 16 / unroll, 1));
+  const int64_t tiles4 = std::max<int64_t>(1, bytes / (16LL * 4 * kThreads));
+  const int64_t tiles8 = std::max<int64_t>(1, bytes / (16LL * 8 * kThreads));
+  switch (v) {
+    case 0: hipLaunchKernelGGL((copy16_kernel<2, false>), dim3(g), dim3(kThreads), 0, stream, s, d, bytes); break;
+    case 1: hipLaunchKernelGGL((copy16_kernel<4, false>), dim3(g), dim3(kThreads), 0, stream, s, d, bytes); break;
+    case 2: hipLaunchKernelGGL((copy16_kernel<4, true>), dim3(g), dim3(kThreads), 0, stream, s, d, bytes); break;
+    case 3: hipLaunchKernelGGL((copy16_kernel<8, true>), dim3(g), dim3(kThreads), 0, stream, s, d, bytes); break;
+    case 4: hipLaunchKernelGGL((copy_tiles_kernel<4, false>), dim3(std::min<int64_t>(tiles4, 2048)), dim3(kThreads), 0,
+                               stream, s, d, bytes); break;
+    case 5: hipLaunchKernelGGL((copy_tiles_kernel<4, true>), dim3(std::min<int64_t>(tiles4, 2048)), dim3(kThreads), 0,
+                               stream, s, d, bytes); break;
+    case 6: hipLaunchKernelGGL((copy_tiles_kernel<8, false>), dim3(std::min<int64_t>(tiles8, 1024)), dim3(kThreads), 0,
+                               stream, s, d, bytes); break;
+    default: hipLaunchKernelGGL((copy_tiles_kernel<4, false>), dim3(tiles4), dim3(kThreads), 0, stream, s, d, bytes);
+      break;
+  }
   hip_check(hipGetLastError(), "copy launch");
 }
 
