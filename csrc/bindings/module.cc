@@ -436,9 +436,10 @@ PYBIND11_MODULE(_C, m) {
           }, py::arg("source"), py::arg("sink") = py::none(), py::arg("name") = "", py::arg("plane") = nullptr)
       .def("master", [](ActorSystem& s, int totalWorkers, float thAllreduce, float thReduce, float thComplete,
                         int maxLag, int dataSize, int maxRound, int maxChunkSize, bool liveBarrier,
-                        py::object on_finished, std::string name, int startRound, py::object on_round) {
+                        py::object on_finished, std::string name, int startRound, py::object on_round,
+                        int roundTimeoutMs) {
             MasterParams p{totalWorkers, thAllreduce, thReduce, thComplete, maxLag, dataSize, maxRound,
-                           maxChunkSize, liveBarrier, startRound};
+                           maxChunkSize, liveBarrier, startRound, roundTimeoutMs};
             MasterActor::RoundCallback rcb;
             if (!on_round.is_none()) {
               auto h = std::make_shared<PyCallable>(std::move(on_round));
@@ -459,7 +460,7 @@ PYBIND11_MODULE(_C, m) {
           }, py::arg("totalWorkers"), py::arg("thAllreduce"), py::arg("thReduce"), py::arg("thComplete"),
           py::arg("maxLag"), py::arg("dataSize"), py::arg("maxRound"), py::arg("maxChunkSize"),
           py::arg("liveBarrier") = false, py::arg("on_finished") = py::none(), py::arg("name") = "master",
-          py::arg("startRound") = 0, py::arg("on_round") = py::none())
+          py::arg("startRound") = 0, py::arg("on_round") = py::none(), py::arg("roundTimeoutMs") = 0)
       .def("probe", &ActorSystem::make_probe, py::arg("name") = "")
       .def("lookup", &ActorSystem::lookup)
       .def("stop", &ActorSystem::stop)
@@ -524,6 +525,7 @@ PYBIND11_MODULE(_C, m) {
         d["inits"] = c.stats().inits;
         d["rounds_started"] = c.stats().rounds_started;
         d["stale_completes"] = c.stats().stale_completes;
+        d["round_timeouts"] = c.stats().round_timeouts;
         return d;
       });
 

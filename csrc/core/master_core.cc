@@ -65,22 +65,35 @@ void MasterCore::on_complete(int srcId, int round, int64_t epoch) {
   }
   // numComplete >= totalWorkers * thAllreduce : float compare, not truncated (:62)
   volatile float need = barrier_base() * p_.thAllreduce;
-  if (static_cast<float>(numComplete_) >= need) {
-    if (last_reported_ < round_) {
-      last_reported_ = round_;
-      fx_->round_completed(round_, epoch_);
-    }
-    if (round_ < p_.maxRound) {
-      MXAR_LOG(INFO, "master", "----" << numComplete_ << " (out of " << p_.totalWorkers
-                                      << ") workers complete round " << round_);
-      round_ += 1;
-      start_allreduce();
-    } else if (!finished_) {
-      finished_ = true;
-      MXAR_LOG(INFO, "master", "----All " << (p_.maxRound + 1) << " rounds complete");
-      fx_->finished(p_.maxRound + 1);
-    }
+  if (static_cast<float>(numComplete_) >= need) advance();
+}
+
+void MasterCore::advance() {
+  if (last_reported_ < round_) {
+    last_reported_ = round_;
+    fx_->round_completed(round_, epoch_);
   }
+  if (round_ < p_.maxRound) {
+    MXAR_LOG(INFO, "master", "----" << numComplete_ << " (out of " << p_.totalWorkers
+                                    << ") workers complete round " << round_);
+    round_ += 1;
+    start_allreduce();
+  } else if (!finished_) {
+    finished_ = true;
+    MXAR_LOG(INFO, "master", "----All " << (p_.maxRound + 1) << " rounds complete");
+    fx_->finished(p_.maxRound + 1);
+  }
+}
+
+// Round deadline: a round that has not reached the barrier roundTimeoutMs after
+// its start is advanced anyway - the coordinator-level counterpart of the workers' maxLag
+// catch-up (stragglers then force-complete it when the next Start arrives).
+void MasterCore::on_round_timeout(int64_t epoch, int round) {
+  if (epoch != epoch_ || round != round_ || finished_ || round_ < 0) return;  // already advanced
+  stats_.round_timeouts++;
+  MXAR_LOG(WARNING, "master", "----Round " << round << " timed out with " << numComplete_ << " of "
+                                             << workers_.size() << " completions; advancing");
+  advance();
 }
 
 // init_workers (AllreduceMaster.scala:84-89)
@@ -114,6 +127,7 @@ void MasterCore::start_allreduce() {
   numComplete_ = 0;
   stats_.rounds_started++;
   for (auto& [idx, h] : workers_) fx_->send_start(h, round_);
+  if (p_.roundTimeoutMs > 0) fx_->arm_round_timer(epoch_, round_, p_.roundTimeoutMs);
 }
 
 }  // namespace mxar

@@ -32,6 +32,7 @@ struct MasterParams {
   int maxChunkSize = 2;
   bool liveBarrier = false;
   int startRound = 0;  // resume point (checkpoint/resume)
+  int roundTimeoutMs = 0;  // > 0: advance a round that misses the barrier this long
 };
 
 class MasterEffects {
@@ -43,10 +44,12 @@ class MasterEffects {
   virtual void finished(int rounds) = 0;
   // Called once per round that reached the barrier (the checkpoint hook).
   virtual void round_completed(int /*round*/, int64_t /*epoch*/) {}
+  // Ask the host to call MasterCore::on_round_timeout(epoch, round) after `ms`.
+  virtual void arm_round_timer(int64_t /*epoch*/, int /*round*/, int /*ms*/) {}
 };
 
 struct MasterStats {
-  uint64_t inits = 0, rounds_started = 0, completes = 0, stale_completes = 0, removed = 0;
+  uint64_t inits = 0, rounds_started = 0, completes = 0, stale_completes = 0, removed = 0, round_timeouts = 0;
 };
 
 class MasterCore {
@@ -57,6 +60,7 @@ class MasterCore {
   void on_terminated(int handle);
   // epoch < 0: untagged (accepted); otherwise completions of another epoch are stale
   void on_complete(int srcId, int round, int64_t epoch = -1);
+  void on_round_timeout(int64_t epoch, int round);
 
   int round() const { return round_; }
   int num_complete() const { return numComplete_; }
@@ -69,6 +73,7 @@ class MasterCore {
  private:
   void init_workers();
   void start_allreduce();
+  void advance();
   float barrier_base() const;
 
   MasterEffects* fx_;

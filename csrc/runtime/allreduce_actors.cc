@@ -1,5 +1,7 @@
 #include "allreduce_actors.h"
 
+#include <cstdio>
+
 #include "../core/log.h"
 
 namespace mxar {
@@ -124,8 +126,18 @@ void MasterActor::receive(Envelope& env, ActorContext& ctx) {
     if (h >= 0) core_.on_terminated(h);
   } else if (auto* c = std::get_if<CompleteAllreduce>(&env.msg)) {
     core_.on_complete(c->srcId, c->round, c->epoch);
+  } else if (auto* tm = std::get_if<TextMessage>(&env.msg)) {
+    long long epoch = 0;
+    int round = 0;
+    if (std::sscanf(tm->text.c_str(), "mxar.round-timeout %lld %d", &epoch, &round) == 2)
+      core_.on_round_timeout(epoch, round);
   }
   ctx_ = nullptr;
+}
+
+void MasterActor::arm_round_timer(int64_t epoch, int round, int ms) {
+  ctx_->system().schedule_once(std::chrono::milliseconds(ms), ctx_->self(),
+                               TextMessage{"mxar.round-timeout " + std::to_string(epoch) + " " + std::to_string(round)});
 }
 
 void MasterActor::send_init(int handle, const InitParams& p, const std::map<int, int>& ids) {

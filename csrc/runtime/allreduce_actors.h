@@ -57,6 +57,7 @@ class MasterActor final : public Actor, public MasterEffects {
   void send_start(int handle, int round) override;
   void finished(int rounds) override;
   void round_completed(int round, int64_t epoch) override;
+  void arm_round_timer(int64_t epoch, int round, int ms) override;
 
   const MasterCore& core() const { return core_; }
 

@@ -164,3 +164,27 @@ def test_resume_from_checkpointed_round():
     assert min(fetched) == 6
     for r in range(6, 10):
         np.testing.assert_array_equal(outs[r], 2 * (np.arange(N) + r))
+
+
+def test_master_round_deadline_advances_past_a_hung_worker():
+    """thAllreduce = 1 would stall forever on a worker that never completes; a
+    round deadline at the master advances such rounds, and the healthy workers still finish
+    every round (the hung worker's share is missing from their partial sums)."""
+    P, N, chunk, rounds = 3, 12, 2, 6
+    system = C.ActorSystem("ClusterSystem", False)
+    done = threading.Event()
+    master = system.master(P, 1.0, 0.6, 0.6, 1, N, rounds - 1, chunk, on_finished=lambda r: done.set(),
+                           roundTimeoutMs=100)
+    outs = {k: {} for k in range(P)}
+    ws = []
+    for k in range(P):
+        ws.append(system.worker(lambda req: AllReduceInput(np.ones(N, np.float32)),
+                                (lambda o, k=k: outs[k].setdefault(o.iteration, 1)), f"w{k}"))
+    hung = C.faulty(system, ws[2], drop=1.0, round_lo=2, seed=1)  # deaf from round 2 on
+    for r in [ws[0], ws[1], hung]:
+        master.tell(MemberUp(r, "worker", ""), None)
+    assert done.wait(20)
+    st = system.master_state(master)
+    system.shutdown()
+    assert st["round_timeouts"] >= 1
+    assert all(len(outs[k]) == rounds for k in (0, 1))
