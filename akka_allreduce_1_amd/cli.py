@@ -118,7 +118,10 @@ def master_main(argv: list[str] | None = None) -> int:
             start_round = int(json.load(f)["round"]) + 1
         print(f"[mxar-master] resuming at round {start_round} from {args.checkpoint}", flush=True)
 
+    stamps: list[float] = []  # completion time of every round: steady-state round rate
+
     def on_round(r: int, epoch: int) -> None:
+        stamps.append(time.perf_counter())
         if args.checkpoint:  # atomic replace: a crash never leaves a torn checkpoint
             tmp = args.checkpoint + ".tmp"
             with open(tmp, "w") as f:
@@ -145,7 +148,8 @@ def master_main(argv: list[str] | None = None) -> int:
     elapsed = time.time() - t0
     if done.is_set():
         print(f"[mxar-master] finished {rounds['n']} rounds in {elapsed:.2f}s", flush=True)
-    _finish(args, cfg, reg, {"rounds": rounds["n"], "elapsed_s": elapsed})
+    steady = (len(stamps) - 1) / (stamps[-1] - stamps[0]) if len(stamps) > 1 and stamps[-1] > stamps[0] else 0.0
+    _finish(args, cfg, reg, {"rounds": rounds["n"], "elapsed_s": elapsed, "steady_rounds_per_s": steady})
     node.leave()
     time.sleep(0.2)
     node.shutdown()

@@ -1,0 +1,137 @@
+#!/usr/bin/env python3
+"""BASELINE config 1: 2-actor float32[1024] allreduce on localhost, CPU only.
+
+Runs the reference's deployment shape - one master + 2 workers, source `data[i] = i + round`
+(AllreduceWorker.scala:285-291) - for `--rounds` rounds and reports correctness (exact sums
+at thReduce = thComplete = 1) plus the per-round latency distribution, in two transports:
+
+  inproc  master + 2 workers in one actor system (threaded dispatcher, shared-memory mailboxes)
+  tcp     master and 2 worker *processes* through the CLI (`python -m akka_allreduce_1_amd
+          master|worker`), joined via the seed node, messages over the binary TCP codec -
+          the reference's `sbt runMain ...AllreduceMaster 2551 2 ...` deployment
+
+Latency = worker round latency (fetch of round r -> its completion), p50/p99 from the native
+histogram (WorkerCore::round_latency); throughput = steady-state rounds/s at the master.
+The reference JVM cannot run here (no JVM in the image), so there is no side-by-side number:
+parity of the latency is unpinned; the protocol's message counts are pinned by the tests.
+
+    python benchmarks/bench_actors.py --rounds 2000 --chunk 256
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from akka_allreduce_1_amd._native import C  # noqa: E402
+from akka_allreduce_1_amd.parallel.comm import free_port  # noqa: E402
+from akka_allreduce_1_amd.protocol import AllReduceInput, MemberUp  # noqa: E402
+
+
+def run_inproc(P: int, N: int, chunk: int, rounds: int, th: float) -> dict:
+    system = C.ActorSystem("ClusterSystem", False)
+    done = threading.Event()
+    base = np.arange(N, dtype=np.float32)
+    bad = []
+    stamps: list[float] = []
+    master = system.master(P, 1.0, th, th, 1, N, rounds - 1, chunk, on_finished=lambda r: done.set(),
+                           on_round=lambda r, e: stamps.append(time.perf_counter()))
+
+    def sink(o):
+        if th >= 1.0 and not np.array_equal(np.asarray(o.data), P * (base + o.iteration)):
+            bad.append(o.iteration)
+
+    ws = [system.worker(lambda req: AllReduceInput(base + np.float32(req.iteration)), sink, f"worker{k}")
+          for k in range(P)]
+    t0 = time.perf_counter()
+    for w in ws:
+        master.tell(MemberUp(w, "worker", ""), None)
+    ok = done.wait(600)
+    wall = time.perf_counter() - t0
+    lat = [system.worker_state(w)["round_latency"] for w in ws]
+    system.shutdown()
+    return {"transport": "inproc", "finished": ok, "exact": ok and not bad, "rounds": rounds,
+            "wall_s": round(wall, 3), "steady_rounds_per_s": round((len(stamps) - 1) / (stamps[-1] - stamps[0]), 1),
+            "p50_ms": round(max(l["p50_ms"] for l in lat), 4), "p99_ms": round(max(l["p99_ms"] for l in lat), 4)}
+
+
+def run_tcp(P: int, N: int, chunk: int, rounds: int, th: float) -> dict:
+    port = free_port()
+    sets = [f"mxar.cluster.seed-nodes=mxar.tcp://ClusterSystem@127.0.0.1:{port}", f"mxar.allreduce.th-reduce={th}",
+            f"mxar.allreduce.th-complete={th}", f"mxar.allreduce.max-round={rounds - 1}", "mxar.loglevel=WARNING",
+            "mxar.cluster.failure-detector.heartbeat-interval=100ms", "mxar.cluster.auto-down-unreachable-after=2s"]
+    opts = [a for s in sets for a in ("--set", s)]
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    py = [sys.executable, "-m", "akka_allreduce_1_amd"]
+    with tempfile.TemporaryDirectory() as td:
+        mj = os.path.join(td, "m.json")
+        master = subprocess.Popen(py + ["master", str(port), str(P), str(N), str(chunk), "--metrics-json", mj] + opts,
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        # worker output goes to files: a pipe nobody drains while the master runs would block them
+        logs = [open(os.path.join(td, f"w{i}.out"), "w+") for i in range(P)]
+        workers = [subprocess.Popen(py + ["worker", "0", str(N), "--metrics-json", os.path.join(td, f"w{i}.json")]
+                                    + opts + (["--print-outputs"] if th >= 1.0 else []),
+                                    env=env, stdout=logs[i], stderr=subprocess.DEVNULL, text=True)
+                   for i in range(P)]
+        try:
+            mout, merr = master.communicate(timeout=900)
+            for w in workers:
+                w.wait(timeout=60)
+            outs = []
+            for f in logs:
+                f.seek(0)
+                outs.append(f.read())
+                f.close()
+        finally:
+            for p in [master] + workers:
+                if p.poll() is None:
+                    p.kill()
+        m = json.load(open(mj))
+        ws = [json.load(open(os.path.join(td, f"w{i}.json"))) for i in range(P)]
+    exact = True
+    if th >= 1.0:
+        base = np.arange(N, dtype=np.float32)
+        for out in outs:
+            rows = [json.loads(line) for line in out.splitlines() if line.startswith("{")]
+            exact &= len(rows) == rounds and all(
+                np.array_equal(np.asarray(r["data"], np.float32), P * (base + r["iteration"])) for r in rows)
+    return {"transport": "tcp", "finished": master.returncode == 0 and m.get("rounds") == rounds, "exact": exact,
+            "rounds": rounds, "wall_s": round(m["elapsed_s"], 3),
+            "steady_rounds_per_s": round(m["steady_rounds_per_s"], 1),
+            "p50_ms": round(max(w["worker"]["latency_p50_ms"] for w in ws), 4),
+            "p99_ms": round(max(w["worker"]["latency_p99_ms"] for w in ws), 4),
+            "frames_per_worker": ws[0]["cluster"]["frames_out"]}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workers", type=int, default=2)
+    ap.add_argument("--size", type=int, default=1024)
+    ap.add_argument("--chunk", type=int, default=256, help="maxChunkSize (floats per message)")
+    ap.add_argument("--rounds", type=int, default=1000)
+    ap.add_argument("--th", type=float, default=1.0, help="thReduce = thComplete")
+    ap.add_argument("--transport", choices=["inproc", "tcp", "both"], default="both")
+    args = ap.parse_args()
+    C.set_log_level("WARNING")
+    res = []
+    if args.transport in ("inproc", "both"):
+        res.append(run_inproc(args.workers, args.size, args.chunk, args.rounds, args.th))
+    if args.transport in ("tcp", "both"):
+        res.append(run_tcp(args.workers, args.size, args.chunk, args.rounds, args.th))
+    for r in res:
+        r.update(workers=args.workers, size=args.size, chunk=args.chunk, th=args.th)
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

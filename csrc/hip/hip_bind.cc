@@ -240,6 +240,7 @@ void bind_hip(py::module_& m) {
       [](uintptr_t src, uintptr_t dst, int64_t bytes, uintptr_t s) { launch_copy(as_cptr(src), as_ptr(dst), bytes, as_stream(s)); },
       py::arg("src"), py::arg("dst"), py::arg("bytes"), py::arg("stream") = 0);
   h.def("set_copy_variant", &set_copy_variant);
+  h.def("set_reduce_variant", &set_reduce_variant);
   h.def("device_count", [] {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) n = 0;

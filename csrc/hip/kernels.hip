@@ -32,12 +32,64 @@ static int grid_for(int64_t packs) {
 }
 
 // Tiled like the fastest copy variant: each workgroup sweeps contiguous tiles of
-// 2 x 4 KiB per slot (one 1 KiB wave access per pack), tiles dealt grid-stride; all P
-// slot loads of a tile are in flight together.
+// U x 4 KiB per slot (one 1 KiB wave access per pack), tiles dealt grid-stride.
+// P is a template parameter for 2..8 slots so every slot's loads of a tile are issued
+// before the first add (P*U*16 bytes in flight per lane); the sum still runs in peer
+// order 0..P-1. NT = nontemporal loads/stores (streaming data, no reuse).
+// out may alias one slot row (in-place reduce): every element is read and written by the
+// same lane, loads before the store.
+template <class E, int U, int P, bool NT>
+__global__ __launch_bounds__(kThreads) void reduce_slots_static(const char* __restrict__ slots, int64_t stride_bytes,
+                                                                char* out, int64_t n, float scale) {
+  constexpr int64_t kTile = static_cast<int64_t>(U) * kThreads;
+  const int64_t npk = n / E::ELEMS;
+  const int64_t ntiles = npk / kTile;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t base = t * kTile + threadIdx.x;
+    Pack16 v[P][U];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const Pack16* s = reinterpret_cast<const Pack16*>(slots + p * stride_bytes);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        v[p][u] = NT ? __builtin_nontemporal_load(s + base + u * kThreads) : s[base + u * kThreads];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      Acc<E> a;
+      a.zero();
+#pragma unroll
+      for (int p = 0; p < P; ++p) a.add(v[p][u]);
+      if (scale != 1.f) a.scale(scale);
+      Pack16* d = reinterpret_cast<Pack16*>(out) + base + u * kThreads;
+      if (NT)
+        __builtin_nontemporal_store(a.pack(), d);
+      else
+        *d = a.pack();
+    }
+  }
+  for (int64_t i = ntiles * kTile + static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < npk;
+       i += static_cast<int64_t>(gridDim.x) * kThreads) {
+    Acc<E> a0;
+    a0.zero();
+#pragma unroll
+    for (int p = 0; p < P; ++p) a0.add(ld16(slots + p * stride_bytes + i * 16));
+    if (scale != 1.f) a0.scale(scale);
+    st16(out + i * 16, a0.pack());
+  }
+  const int64_t t = npk * E::ELEMS + static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (t < n) {
+    float acc = 0.f;
+#pragma unroll
+    for (int p = 0; p < P; ++p) acc += Scalar<E>::load(slots + p * stride_bytes, t);
+    Scalar<E>::store(out, t, acc * scale);
+  }
+}
+
+// Any slot count: the runtime-P loop (loads of one slot in flight at a time).
 template <class E>
 __global__ __launch_bounds__(kThreads) void reduce_slots_kernel(const char* __restrict__ slots, int64_t stride_bytes,
-                                                                 int nslots, char* __restrict__ out, int64_t n,
-                                                                 float scale) {
+                                                                int nslots, char* out, int64_t n, float scale) {
   constexpr int U = 2;
   constexpr int64_t kTile = static_cast<int64_t>(U) * kThreads;
   const int64_t npk = n / E::ELEMS;
@@ -77,20 +129,55 @@ __global__ __launch_bounds__(kThreads) void reduce_slots_kernel(const char* __re
   }
 }
 
+static int g_reduce_variant = -1;  // -1: default (see launch_reduce_slots)
+
+void set_reduce_variant(int v) { g_reduce_variant = v; }
+
+template <class E, int U, bool NT>
+static void launch_static(int P, const char* s, int64_t stride, char* o, int64_t n, float scale, int g,
+                          hipStream_t st) {
+#define MXAR_RS(PP)                                                                                            \
+  case PP:                                                                                                     \
+    hipLaunchKernelGGL((reduce_slots_static<E, U, PP, NT>), dim3(g), dim3(kThreads), 0, st, s, stride, o, n, \
+                       scale);                                                                                 \
+    break;
+  switch (P) {
+    MXAR_RS(1) MXAR_RS(2) MXAR_RS(3) MXAR_RS(4) MXAR_RS(5) MXAR_RS(6) MXAR_RS(7) MXAR_RS(8)
+    default: hipLaunchKernelGGL(reduce_slots_kernel<E>, dim3(g), dim3(kThreads), 0, st, s, stride, P, o, n, scale);
+  }
+#undef MXAR_RS
+}
+
+template <class E>
+static void launch_reduce_typed(int v, int P, const char* s, int64_t stride, char* o, int64_t n, float scale,
+                                hipStream_t st) {
+  const int64_t npk = n / E::ELEMS;
+  auto grid = [&](int U) {
+    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(npk / (int64_t(U) * kThreads), 2048)));
+  };
+  switch (v) {
+    case 0: hipLaunchKernelGGL(reduce_slots_kernel<E>, dim3(grid(2)), dim3(kThreads), 0, st, s, stride, P, o, n, scale);
+      break;
+    case 1: launch_static<E, 2, false>(P, s, stride, o, n, scale, grid(2), st); break;
+    case 2: launch_static<E, 2, true>(P, s, stride, o, n, scale, grid(2), st); break;
+    case 3: launch_static<E, 4, true>(P, s, stride, o, n, scale, grid(4), st); break;
+    default: launch_static<E, 4, false>(P, s, stride, o, n, scale, grid(4), st); break;
+  }
+}
+
 void launch_reduce_slots(const void* slots, int64_t slot_stride_elems, int nslots, void* out, int64_t n, DType dt,
                          float scale, hipStream_t stream) {
   if (n <= 0) return;
   const int64_t es = static_cast<int64_t>(dtype_size(dt));
   if (((reinterpret_cast<uintptr_t>(slots) | reinterpret_cast<uintptr_t>(out)) & 15) || ((slot_stride_elems * es) & 15))
     throw std::invalid_argument("reduce_slots: slots, out and slot stride must be 16-byte aligned");
-  const int64_t npk = n * es / 16;
-  const int g = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(npk / (2 * kThreads), 2048)));
+  const int v = g_reduce_variant < 0 ? 1 : g_reduce_variant;
+  const char* s = static_cast<const char*>(slots);
+  char* o = static_cast<char*>(out);
   if (dt == DType::F32)
-    hipLaunchKernelGGL(reduce_slots_kernel<F32>, dim3(g), dim3(kThreads), 0, stream, static_cast<const char*>(slots),
-                       slot_stride_elems * es, nslots, static_cast<char*>(out), n, scale);
+    launch_reduce_typed<F32>(v, nslots, s, slot_stride_elems * es, o, n, scale, stream);
   else
-    hipLaunchKernelGGL(reduce_slots_kernel<BF16>, dim3(g), dim3(kThreads), 0, stream, static_cast<const char*>(slots),
-                       slot_stride_elems * es, nslots, static_cast<char*>(out), n, scale);
+    launch_reduce_typed<BF16>(v, nslots, s, slot_stride_elems * es, o, n, scale, stream);
   hip_check(hipGetLastError(), "reduce_slots launch");
 }
 

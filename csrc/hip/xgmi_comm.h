@@ -130,6 +130,7 @@ void launch_fill_uniform(void* dst, int64_t n, uint64_t seed, DType dt, hipStrea
 // dst[0:bytes) = src[0:bytes) as a kernel (16-B aligned)
 void launch_copy(const void* src, void* dst, int64_t bytes, hipStream_t stream);
 void set_copy_variant(int v);  // study knob: 0..3, -1 default
+void set_reduce_variant(int v);  // study knob: 0 runtime-P loop, 1..4 static-P (U, NT), -1 default
 // dst (dt_out) = src (dt_in), n elements
 void launch_cast(const void* src, DType dt_in, void* dst, DType dt_out, int64_t n, hipStream_t stream);
 // flat bucket pack/unpack: copy `count` tensors (ptr, numel) into / out of a contiguous bucket
