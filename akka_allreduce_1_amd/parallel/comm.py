@@ -25,7 +25,7 @@ from .._native import C
 
 _H = C.hip
 
-ALGOS = {"auto": _H.Algo.Auto, "twoshot": _H.Algo.TwoShot, "oneshot": _H.Algo.OneShot}
+ALGOS = {"auto": _H.Algo.Auto, "twoshot": _H.Algo.TwoShot, "oneshot": _H.Algo.OneShot, "ring": _H.Algo.Ring}
 DEFAULT_SLOT_BYTES = int(os.environ.get("MXAR_SLOT_BYTES", 64 << 20))
 
 

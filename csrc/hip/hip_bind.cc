@@ -133,14 +133,15 @@ void bind_hip(py::module_& m) {
         "DataPlane whose slabs and payloads live in HBM of `device` (worker protocol on the GPU)");
 
   py::enum_<DType>(h, "DType").value("F32", DType::F32).value("BF16", DType::BF16);
-  py::enum_<Algo>(h, "Algo").value("Auto", Algo::Auto).value("TwoShot", Algo::TwoShot).value("OneShot", Algo::OneShot);
+  py::enum_<Algo>(h, "Algo").value("Auto", Algo::Auto).value("TwoShot", Algo::TwoShot).value("OneShot", Algo::OneShot).value("Ring", Algo::Ring);
 
   py::class_<CommStats>(h, "CommStats")
       .def_readonly("calls", &CommStats::calls)
       .def_readonly("launches", &CommStats::launches)
       .def_readonly("bytes", &CommStats::bytes)
       .def_readonly("oneshot", &CommStats::oneshot)
-      .def_readonly("twoshot", &CommStats::twoshot);
+      .def_readonly("twoshot", &CommStats::twoshot)
+      .def_readonly("ring", &CommStats::ring);
 
   py::class_<XgmiComm>(h, "XgmiComm")
       .def(py::init<int, int, int, int64_t, int, double>(), py::arg("rank"), py::arg("world"), py::arg("device"),

@@ -171,7 +171,7 @@ void launch_reduce_slots(const void* slots, int64_t slot_stride_elems, int nslot
   const int64_t es = static_cast<int64_t>(dtype_size(dt));
   if (((reinterpret_cast<uintptr_t>(slots) | reinterpret_cast<uintptr_t>(out)) & 15) || ((slot_stride_elems * es) & 15))
     throw std::invalid_argument("reduce_slots: slots, out and slot stride must be 16-byte aligned");
-  const int v = g_reduce_variant < 0 ? 1 : g_reduce_variant;
+  const int v = g_reduce_variant < 0 ? 3 : g_reduce_variant;  // 3: measured fastest (profiles/reduce_kernel.md)
   const char* s = static_cast<const char*>(slots);
   char* o = static_cast<char*>(out);
   if (dt == DType::F32)

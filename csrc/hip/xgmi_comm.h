@@ -32,13 +32,13 @@ namespace mxar {
 enum class DType : int { F32 = 0, BF16 = 1 };
 inline size_t dtype_size(DType d) { return d == DType::F32 ? 4 : 2; }
 
-enum class Algo : int { Auto = 0, TwoShot = 1, OneShot = 2 };
+enum class Algo : int { Auto = 0, TwoShot = 1, OneShot = 2, Ring = 3 };
 
 constexpr int kMaxRanks = 16;
 constexpr int kCommThreads = 256;
 
 struct CommStats {
-  uint64_t calls = 0, launches = 0, bytes = 0, oneshot = 0, twoshot = 0;
+  uint64_t calls = 0, launches = 0, bytes = 0, oneshot = 0, twoshot = 0, ring = 0;
 };
 
 class XgmiComm {
@@ -104,7 +104,7 @@ class XgmiComm {
   static void run(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
                   const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, Algo algo, float scale);
   static void launch_segment(const std::vector<XgmiComm*>& group, const char* const* ins, char* const* outs,
-                             int64_t n, DType dt, hipStream_t stream, bool oneshot, float scale);
+                             int64_t n, DType dt, hipStream_t stream, Algo kind, float scale);
 
   int rank_, world_, device_, grid_;
   int64_t slot_bytes_, maxch_, off_S_, off_R_, off_B_, slab_bytes_;

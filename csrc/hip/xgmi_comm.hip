@@ -366,6 +366,112 @@ __global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
   finish_launch(ctl, epoch);
 }
 
+// ---------------------------------------------------------------------------------
+// Ring (BASELINE config 3's algorithm, kept for comparison and for topologies where only
+// neighbour links are fast): reduce-scatter in P-1 hops + all-gather in P-1 hops, every
+// hop a push into the next rank's slab. Each workgroup owns chunk c of every block and
+// carries it around the whole ring, so all chunks are pipelined around the ring at once.
+//   RS step s (0..P-2): send partial of block (r-s) into next's S[s][c], flag F1_next[s][c]
+//                       (step 0 sends the raw input; step s>0 first adds S_r[s-1][c]).
+//   final RS          : block (r+1) = S_r[P-2][c] + in[(r+1)][c], scaled once, to out and
+//                       into next's R[0][c], flag F2_next[0][c].
+//   AG step t (0..P-2): R_r[t][c] = block (r-t): copy to out, forward into next's R[t+1].
+// Slot reuse across launches is safe: rank r's predecessor can only start the next launch
+// after it received every block of this one, which transitively follows every read r
+// makes of its S/R slots. One xGMI link per direction per rank carries the traffic.
+// ---------------------------------------------------------------------------------
+template <class E>
+__device__ __forceinline__ void copy_slab_fwd(char* out, char* next_slab, const char* slab_src, int64_t len) {
+  const int64_t npk = len / E::ELEMS;
+  const __amdgpu_buffer_rsrc_t rs = slab_rsrc(slab_src);
+  const __amdgpu_buffer_rsrc_t ro = slab_rsrc(out);
+  const bool fwd = next_slab != nullptr;
+  const __amdgpu_buffer_rsrc_t rn = slab_rsrc(fwd ? next_slab : out);
+  int64_t i = threadIdx.x;
+  constexpr int U = 4;
+  for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
+    Pack16 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld16_sc1(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
+#pragma unroll
+    for (int u = 0; u < U; ++u) st16_wt(ro, static_cast<uint32_t>((i + u * kCommThreads) * 16), v[u]);
+    if (fwd) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) st16_wt(rn, static_cast<uint32_t>((i + u * kCommThreads) * 16), v[u]);
+    }
+  }
+  for (; i < npk; i += kCommThreads) {
+    const Pack16 v = ld16_sc1(rs, static_cast<uint32_t>(i * 16));
+    st16_wt(ro, static_cast<uint32_t>(i * 16), v);
+    if (fwd) st16_wt(rn, static_cast<uint32_t>(i * 16), v);
+  }
+  const int64_t t = npk * E::ELEMS + threadIdx.x;
+  if (t < len) {
+    const float x = ld_scalar_sc1<E>(rs, t);
+    st_scalar_wt<E>(ro, t, x);
+    if (fwd) st_scalar_wt<E>(rn, t, x);
+  }
+}
+
+template <class E>
+__global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
+  constexpr int es = 16 / E::ELEMS;
+  const int P = a.P;
+  const int y = blockIdx.y;
+  const int r = a.rank0 + y;
+  const int nxt = (r + 1) % P;
+  const char* const in = a.in[y];
+  char* const out = a.out[y];
+  uint32_t* const ctl = a.ctl[y];
+  const uint32_t epoch = launch_epoch(ctl);
+  const uint64_t deadline = wall_ticks() + a.timeout;
+  const int64_t slot = a.slot_bytes;
+  uint32_t* err = &ctl[2];
+  const bool rel = a.fence & 1, acq = a.fence & 2;
+  for (int c = blockIdx.x; c < a.nch; c += gridDim.x) {
+    const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
+    auto blen = [&](int b) { return clamp_len(clamp_len(a.n - static_cast<int64_t>(b) * a.block, a.block) - cstart, a.chunk); };
+    auto at = [&](int b) { return (static_cast<int64_t>(b) * a.block + cstart) * es; };
+    // RS step 0: raw own block r
+    {
+      const int64_t len = blen(r);
+      if (len > 0) copy_to_slab<E>(a.base[nxt] + a.off_S + cstart * es, in + at(r), len);
+      publish_flags([&](int) { return f1(a, nxt, 0, c); }, 1, epoch, rel);
+    }
+    // RS steps 1..P-1 (the last one completes block r+1)
+    for (int s = 1; s < P; ++s) {
+      const int b = (r - s + P) % P;
+      const int64_t len = blen(b);
+      wait_flags([&](int) -> const uint32_t* { return f1(a, r, s - 1, c); }, 1, epoch, deadline, err,
+                 ERR_TIMEOUT_SCATTER, acq);
+      const RedSrc src{in + at(b), a.base[r] + a.off_S + (s - 1) * slot + cstart * es, 0, 1};
+      if (s < P - 1) {
+        char* d = a.base[nxt] + a.off_S + s * slot + cstart * es;
+        if (len > 0) reduce_to<E, 2>(2, src, 1, -1, [&](int) -> char* { return d; }, len, 1.f, true);
+        publish_flags([&](int) { return f1(a, nxt, s, c); }, 1, epoch, rel);
+      } else {
+        char* o = out + at(b);
+        char* d = a.base[nxt] + a.off_R + cstart * es;
+        if (len > 0)
+          reduce_to<E, 2>(2, src, 2, 0, [&](int k) -> char* { return k == 0 ? o : d; }, len, a.scale, a.fence & 1);
+        publish_flags([&](int) { return f2(a, nxt, 0, c); }, 1, epoch, rel);
+      }
+    }
+    // AG steps: receive block (r - t), forward unless it is the last hop
+    for (int t = 0; t < P - 1; ++t) {
+      const int b = (r - t + P) % P;
+      const int64_t len = blen(b);
+      wait_flags([&](int) -> const uint32_t* { return f2(a, r, t, c); }, 1, epoch, deadline, err, ERR_TIMEOUT_REDUCE,
+                 acq);
+      const bool fwd = t < P - 2;
+      char* d = fwd ? a.base[nxt] + a.off_R + (t + 1) * slot + cstart * es : nullptr;
+      if (len > 0) copy_slab_fwd<E>(out + at(b), d, a.base[r] + a.off_R + t * slot + cstart * es, len);
+      if (fwd) publish_flags([&](int) { return f2(a, nxt, t + 1, c); }, 1, epoch, rel);
+    }
+  }
+  finish_launch(ctl, epoch);
+}
+
 __global__ __launch_bounds__(kCommThreads) void barrier_kernel(CommArgs a) {
   const int r = a.rank0 + blockIdx.y;
   uint32_t* const ctl = a.ctl[blockIdx.y];
@@ -487,8 +593,13 @@ void XgmiComm::clear_error() {
 }
 
 template <class E>
-static void launch_typed(const CommArgs& a, dim3 grid, hipStream_t s, bool oneshot) {
+static void launch_typed(const CommArgs& a, dim3 grid, hipStream_t s, Algo kind) {
   const dim3 b(kCommThreads);
+  if (kind == Algo::Ring) {
+    hipLaunchKernelGGL(ring_kernel<E>, grid, b, 0, s, a);
+    return;
+  }
+  const bool oneshot = kind == Algo::OneShot;
 #define MXAR_LAUNCH(PT)                                                                         \
   do {                                                                                          \
     if (oneshot)                                                                                \
@@ -509,7 +620,8 @@ static void launch_typed(const CommArgs& a, dim3 grid, hipStream_t s, bool onesh
 // Common launch geometry + args for the ranks `group` (all on one device, consecutive
 // rank ids starting at group[0]->rank()).
 void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* const* ins, char* const* outs,
-                              int64_t n, DType dt, hipStream_t stream, bool oneshot, float scale) {
+                              int64_t n, DType dt, hipStream_t stream, Algo kind, float scale) {
+  const bool oneshot = kind == Algo::OneShot;
   const XgmiComm& c0 = *group[0];
   const int W = c0.world_;
   const int64_t es = static_cast<int64_t>(dtype_size(dt));
@@ -541,6 +653,13 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
     a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(n, a.chunk)));
     a.subchunk = a.chunk;
     gx = static_cast<int>(std::min<int64_t>(gmax, a.nch));
+  } else if (kind == Algo::Ring) {
+    // one chunk per workgroup, carried around the whole ring by that workgroup
+    a.block = round_up(ceil_div(n, W), elems);
+    a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, gmax), elems));
+    a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
+    a.subchunk = a.chunk;
+    gx = static_cast<int>(std::min<int64_t>(gmax, a.nch));
   } else {
     // ~one scatter unit and one gather unit per workgroup: every unit pays one fence, so
     // units are as large as the parallelism allows. The reduce phase splits each chunk
@@ -562,13 +681,13 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
     throw std::logic_error("XgmiComm: segment geometry exceeds slab");
   const dim3 grid(gx, ranks_here);
   if (dt == DType::F32)
-    launch_typed<F32>(a, grid, stream, oneshot);
+    launch_typed<F32>(a, grid, stream, kind);
   else
-    launch_typed<BF16>(a, grid, stream, oneshot);
+    launch_typed<BF16>(a, grid, stream, kind);
   hip_check(hipGetLastError(), "allreduce launch");
   for (XgmiComm* c : group) {
     ++c->stats_.launches;
-    ++(oneshot ? c->stats_.oneshot : c->stats_.twoshot);
+    ++(oneshot ? c->stats_.oneshot : kind == Algo::Ring ? c->stats_.ring : c->stats_.twoshot);
   }
 }
 
@@ -600,7 +719,8 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
   }
   const bool oneshot =
       algo == Algo::OneShot ? (n * es <= c0.slot_bytes_) : (algo == Algo::Auto && n * es <= c0.oneshot_max_);
-  TraceScope span("xgmi", std::string(oneshot ? "oneshot " : "twoshot ") + std::to_string(n * es) + "B",
+  const Algo kind = oneshot ? Algo::OneShot : algo == Algo::Ring ? Algo::Ring : Algo::TwoShot;
+  TraceScope span("xgmi", std::string(oneshot ? "oneshot " : kind == Algo::Ring ? "ring " : "twoshot ") + std::to_string(n * es) + "B",
                   "{\"rank\":" + std::to_string(c0.rank_) + ",\"ranks_in_launch\":" + std::to_string(group.size()) +
                       "}");
   const int64_t seg = oneshot ? c0.slot_bytes_ / es : c0.world_ * (c0.slot_bytes_ / es);
@@ -612,7 +732,7 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
       ip[y] = static_cast<const char*>(ins[y]) + off * es;
       op[y] = static_cast<char*>(outs[y]) + off * es;
     }
-    launch_segment(group, ip.data(), op.data(), len, dt, stream, oneshot, scale);
+    launch_segment(group, ip.data(), op.data(), len, dt, stream, kind, scale);
   }
 }
 

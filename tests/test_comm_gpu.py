@@ -43,7 +43,7 @@ def _diag(y, ref, xs, rank):
 
 @pytest.mark.parametrize("P", [1, 2, 3, 4])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("algo", ["twoshot", "oneshot"])
+@pytest.mark.parametrize("algo", ["twoshot", "oneshot", "ring"])
 @pytest.mark.parametrize("n", [1, 7, 1000, 65536 + 3, 1 << 20])
 def test_local_cluster_allreduce(P, dtype, algo, n):
     cl = LocalCluster(P, slot_bytes=4 << 20, grid=32, timeout_s=10.0)
@@ -70,12 +70,13 @@ def test_local_cluster_inplace_and_repeated_epochs():
             assert torch.allclose(y, ref, atol=1e-5)
 
 
-def test_local_cluster_segments_larger_than_slab():
+@pytest.mark.parametrize("algo", ["twoshot", "ring"])
+def test_local_cluster_segments_larger_than_slab(algo):
     P = 2
     cl = LocalCluster(P, slot_bytes=64 << 10, grid=8, timeout_s=10.0)
     n = 100_000  # 400 KB fp32 > P * 64 KiB -> several launches
     xs = [fill_uniform(torch.empty(n, device=DEV), seed=k) for k in range(P)]
-    ys = cl.allreduce(xs, algo="twoshot")
+    ys = cl.allreduce(xs, algo=algo)
     cl.check()
     assert cl.comms[0].stats.launches > 1
     for y in ys:
@@ -144,14 +145,14 @@ def test_local_cluster_mean_fused(dtype, P):
         assert (y.float() - ref).abs().max().item() <= (1e-6 if dtype == torch.float32 else 1e-2)
 
 
-@pytest.mark.parametrize("algo", ["oneshot", "twoshot"])
+@pytest.mark.parametrize("algo", ["oneshot", "twoshot", "ring"])
 @pytest.mark.parametrize("P", [2, 4])
 def test_inplace_no_input_overwrite_race(algo, P):
     """In-place: a rank's reduced output must never leak into what a peer receives as that
     rank's contribution (the input may only be overwritten after every push read it)."""
     cl = LocalCluster(P, slot_bytes=2 << 20, grid=64)
     for it in range(8):
-        n = 200_003 if algo == "twoshot" else 60_001
+        n = 60_001 if algo == "oneshot" else 200_003
         xs = [fill_uniform(torch.empty(n, device=DEV), seed=1000 * it + k) for k in range(P)]
         ref = _ref(xs)
         cl.allreduce(xs, xs, algo=algo)
@@ -186,3 +187,21 @@ def test_stress_cluster_churn():
             if err > _tol(dtype, P) + (1e-5 if dtype == torch.float32 else 0):
                 pytest.fail(f"it {it} P={P} n={n} {dtype} {algo} rank {k}: err {err}: {_diag(y, ref, xs, k)}")
         del cl, xs, ys
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_ring_eight_ranks_mean_and_repeats(dtype):
+    """P = 8 ring (7 reduce-scatter + 7 all-gather hops per chunk), mean fused, repeated
+    launches reusing the same slots (the cross-launch slot-reuse argument of ring_kernel)."""
+    P = 8
+    cl = LocalCluster(P, slot_bytes=1 << 20, grid=64, timeout_s=10.0)
+    for it in range(5):
+        n = [1 << 20, 12_345, 3 * (1 << 18) + 5][it % 3]
+        xs = [fill_uniform(torch.empty(n, dtype=dtype, device=DEV), seed=50 * it + k) for k in range(P)]
+        ref = _ref(xs) / P
+        ys = cl.allreduce(xs, op="avg", algo="ring")
+        cl.check()
+        for k, y in enumerate(ys):
+            err = (y.float() - ref).abs().max().item()
+            assert err <= (1e-6 if dtype == torch.float32 else 1e-2), f"it {it} rank {k}: {err}"
+    assert cl.comms[0].stats.ring >= 5

@@ -30,6 +30,8 @@ def parse_size(s: str) -> int:
 
 
 def hbm_bytes(S: int, P: int, algo: str) -> float:
+    if algo == "ring":  # per rank, blocks of S/P: RS hops read in (+ slab) and push, AG hops copy out + forward
+        return P * (S / P) * (6 * (P - 2) + 8)
     if algo == "oneshot":
         return P * (S + S * P + S * P + S)  # read in, write P slots, read P slots, write out
     return P * (S + S * (P - 1) / P + S + S + 2 * S * (P - 1) / P)
