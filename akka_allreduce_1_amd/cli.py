@@ -209,9 +209,13 @@ def worker_main(argv: list[str] | None = None) -> int:
 
 def main(argv: list[str] | None = None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
-    if not argv or argv[0] not in ("master", "worker"):
-        print("usage: python -m akka_allreduce_1_amd {master|worker} [args...]", file=sys.stderr)
+    if not argv or argv[0] not in ("master", "worker", "bench"):
+        print("usage: python -m akka_allreduce_1_amd {master|worker|bench} [args...]", file=sys.stderr)
         return 2
+    if argv[0] == "bench":
+        from .bench_cli import main as bench_main
+
+        return bench_main(argv[1:])
     return master_main(argv[1:]) if argv[0] == "master" else worker_main(argv[1:])
 
 

@@ -68,7 +68,10 @@ class GradBucket:
 class BucketedGradReducer:
     def __init__(self, params: Iterable[torch.nn.Parameter] | torch.nn.Module, comm, *,
                  bucket_bytes: int = 64 << 20, op: str = "avg", overlap: bool = True,
-                 first_bucket_bytes: int | None = None):
+                 first_bucket_bytes: int | None = None, sync: str = "native", event_scope: int = 1):
+        """sync: how the comm stream is ordered after backward's gradient writes -
+        "native" = reusable HIP events created with `event_scope` (1: device-scope release,
+        enough within one GPU; 0: HIP default system-scope), "torch" = torch.cuda events."""
         if isinstance(params, torch.nn.Module):
             params = params.parameters()
         self.params = [p for p in params if p.requires_grad]
@@ -80,7 +83,15 @@ class BucketedGradReducer:
         self.on_gpu = self.device.type == "cuda"
         self.overlap = overlap and self.on_gpu
         self.stream = torch.cuda.Stream(device=self.device) if self.on_gpu else None
+        self.sync = sync if self.on_gpu else "none"
         self.buckets = self._build(bucket_bytes, first_bucket_bytes)
+        self._events: list[int] = []
+        if self.sync == "native":
+            from .._native import C
+
+            self._H = C.hip
+            # one compute->comm event per bucket + one comm->compute event
+            self._events = [self._H.event_create(event_scope) for _ in range(len(self.buckets) + 1)]
         self.slot_of: dict[int, tuple[GradBucket, int]] = {}
         for b in self.buckets:
             for p, off in zip(b.params, b.offsets):
@@ -144,14 +155,21 @@ class BucketedGradReducer:
             self._next += 1
 
     def _launch(self, b: GradBucket) -> None:
-        if self.on_gpu:
+        if self.sync == "native":
+            cs = torch.cuda.current_stream(self.device).cuda_stream
+            ev = self._events[b.index]
+            self._H.event_record(ev, cs)
+            self._H.stream_wait_event(self.stream.cuda_stream, ev)
+            with torch.cuda.stream(self.stream):
+                self.comm.allreduce_(b.buffer, op=self.op)
+            b.done = True
+        elif self.on_gpu:
             compute = torch.cuda.current_stream(self.device)
             self.stream.wait_stream(compute)
             with torch.cuda.stream(self.stream):
                 self.comm.allreduce_(b.buffer, op=self.op)
                 b.done = torch.cuda.Event()
                 b.done.record(self.stream)
-            b.buffer.record_stream(self.stream)
         else:
             self.comm.allreduce_(b.buffer, op=self.op)
         b.launched = True
@@ -165,11 +183,15 @@ class BucketedGradReducer:
         for b in self.buckets:
             b.ready = True
         self._launch_ready()
-        if self.on_gpu:
-            compute = torch.cuda.current_stream(self.device)
-            for b in self.buckets:
-                if b.done is not None:
-                    compute.wait_event(b.done)
+        # the comm stream runs the buckets in order: joining after the last one is enough
+        if self.sync == "native":
+            ev = self._events[-1]
+            self._H.event_record(ev, self.stream.cuda_stream)
+            self._H.stream_wait_event(torch.cuda.current_stream(self.device).cuda_stream, ev)
+        elif self.on_gpu:
+            last = [b for b in self.buckets if b.done is not None]
+            if last:
+                torch.cuda.current_stream(self.device).wait_event(last[-1].done)
         for b in self.buckets:
             b.pending = len(b.params)
             b.ready = b.launched = False
@@ -180,6 +202,14 @@ class BucketedGradReducer:
     def zero_grad(self) -> None:
         for b in self.buckets:
             b.buffer.zero_()
+
+    def __del__(self):
+        for e in getattr(self, "_events", []):
+            try:
+                self._H.event_destroy(e)
+            except Exception:  # noqa: BLE001 - interpreter shutdown
+                pass
+        self._events = []
 
     def remove_hooks(self) -> None:
         for h in self._hooks:

@@ -87,6 +87,9 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--layers", type=int, default=32, help="llama3_8b: transformer layers (32 = full model)")
+    ap.add_argument("--sync", choices=["native", "torch"], default="native", help="reducer stream ordering")
+    ap.add_argument("--event-scope", type=int, default=1, help="native events: 0 system, 1 device, 2 no fence")
+    ap.add_argument("--comm-grid", type=int, default=0, help="xgmi workgroups per launch (0 = engine default)")
     args = ap.parse_args()
     rank, world, local = init_distributed("nccl")
     dev = torch.device("cuda", local)
@@ -94,8 +97,9 @@ def main() -> None:
     shapes = gradient_shapes(args.model) if args.model != "llama3_8b" else \
         __import__("akka_allreduce_1_amd.models.grad_sets", fromlist=["x"]).llama3_8b_shapes(args.layers)
     params = [torch.nn.Parameter(torch.zeros(s, dtype=dtype, device=dev)) for _, s in shapes]
-    comm = XgmiCommunicator() if args.engine == "xgmi" else TorchDistComm()
-    reducer = BucketedGradReducer(params, comm, bucket_bytes=args.bucket_mib << 20, op="avg")
+    comm = XgmiCommunicator(grid=args.comm_grid) if args.engine == "xgmi" else TorchDistComm()
+    reducer = BucketedGradReducer(params, comm, bucket_bytes=args.bucket_mib << 20, op="avg", sync=args.sync,
+                                  event_scope=args.event_scope)
     reducer.remove_hooks()  # the synthetic backward calls the hook itself
     bwd = SyntheticBackward(params, args.tokens, dtype, dev)
     lr = 1e-3
@@ -131,7 +135,8 @@ def main() -> None:
     res = {
         "metric": "dp_step_ms", "model": args.model, "n_gpus": world, "engine": args.engine,
         "params": sum(numel(s) for _, s in shapes), "grad_bytes": nbytes, "buckets": len(reducer.buckets),
-        "tokens": args.tokens, "step_overlap_ms": round(t_overlap, 3), "step_serial_ms": round(t_serial, 3),
+        "tokens": args.tokens, "bucket_mib": args.bucket_mib, "sync": args.sync, "event_scope": args.event_scope,
+        "comm_grid": args.comm_grid, "step_overlap_ms": round(t_overlap, 3), "step_serial_ms": round(t_serial, 3),
         "compute_ms": round(t_compute, 3), "comm_ms": round(t_comm, 3),
         "exposed_comm_ms": round(t_overlap - t_compute, 3),
         "overlap_efficiency": round((t_serial - t_overlap) / max(min(t_comm, t_compute), 1e-9), 3),

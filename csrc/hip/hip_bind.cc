@@ -242,6 +242,26 @@ void bind_hip(py::module_& m) {
       py::arg("src"), py::arg("dst"), py::arg("bytes"), py::arg("stream") = 0);
   h.def("set_copy_variant", &set_copy_variant);
   h.def("set_reduce_variant", &set_reduce_variant);
+  // Stream-ordering events for the gradient reducer. scope: 0 = HIP default (system-scope
+  // release when recorded), 1 = device-scope release, 2 = no system fence. Timing disabled.
+  h.def(
+      "event_create",
+      [](int scope) {
+        unsigned flags = hipEventDisableTiming;
+        if (scope == 1) flags |= hipEventReleaseToDevice;
+        if (scope == 2) flags |= hipEventDisableSystemFence;
+        hipEvent_t e = nullptr;
+        hip_check(hipEventCreateWithFlags(&e, flags), "hipEventCreateWithFlags");
+        return reinterpret_cast<uintptr_t>(e);
+      },
+      py::arg("scope") = 1);
+  h.def("event_destroy", [](uintptr_t e) { (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(e)); });
+  h.def("event_record", [](uintptr_t e, uintptr_t s) {
+    hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(e), as_stream(s)), "hipEventRecord");
+  });
+  h.def("stream_wait_event", [](uintptr_t s, uintptr_t e) {
+    hip_check(hipStreamWaitEvent(as_stream(s), reinterpret_cast<hipEvent_t>(e), 0), "hipStreamWaitEvent");
+  });
   h.def("device_count", [] {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) n = 0;

@@ -53,3 +53,18 @@ def test_master_and_two_worker_processes(tmp_path):
         for p in [master] + workers:
             if p.poll() is None:
                 p.kill()
+
+
+def test_mxar_bench_gloo_two_ranks(tmp_path):
+    """mxar-bench under torchrun (2 gloo ranks on CPU): one JSON row per size, busbw = algbw."""
+    out = tmp_path / "rows.jsonl"
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), "-m", "akka_allreduce_1_amd", "bench", "--backend", "gloo",
+           "--algos", "torch", "--sizes", "4K..64K", "--dtype", "fp32", "--iters", "3", "--json", str(out)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    rows = [json.loads(l) for l in out.read_text().splitlines()]
+    assert [x["bytes"] for x in rows] == [4096, 16384, 65536]
+    for x in rows:
+        assert x["P"] == 2 and x["p50_us"] > 0 and x["busbw_GBps"] == x["algbw_GBps"]

@@ -205,3 +205,15 @@ def test_ring_eight_ranks_mean_and_repeats(dtype):
             err = (y.float() - ref).abs().max().item()
             assert err <= (1e-6 if dtype == torch.float32 else 1e-2), f"it {it} rank {k}: {err}"
     assert cl.comms[0].stats.ring >= 5
+
+
+def test_mxar_bench_local_cli(tmp_path):
+    from akka_allreduce_1_amd.bench_cli import main
+
+    out = tmp_path / "rows.jsonl"
+    assert main(["--local", "4", "--algos", "twoshot", "ring", "oneshot", "--sizes", "64K", "4M", "--iters", "3",
+                 "--json", str(out)]) == 0
+    import json
+
+    rows = [json.loads(l) for l in out.read_text().splitlines()]
+    assert {(r["bytes"], r["algo"]) for r in rows} >= {(65536, "twoshot"), (65536, "ring"), (4 << 20, "twoshot")}
