@@ -217,3 +217,30 @@ def test_mxar_bench_local_cli(tmp_path):
 
     rows = [json.loads(l) for l in out.read_text().splitlines()]
     assert {(r["bytes"], r["algo"]) for r in rows} >= {(65536, "twoshot"), (65536, "ring"), (4 << 20, "twoshot")}
+
+
+@pytest.mark.parametrize("algo", ["oneshot", "twoshot", "ring"])
+def test_hipgraph_capture_and_replay(algo):
+    """The allreduce launch is graph-safe: flags carry an epoch read from a device counter at
+    run time, so one captured launch replays correctly many times (new data each replay)."""
+    P, n = 4, 100_003
+    cl = LocalCluster(P, slot_bytes=1 << 20, grid=32, timeout_s=10.0)
+    xs = [torch.empty(n, device=DEV) for _ in range(P)]
+    ys = [torch.empty(n, device=DEV) for _ in range(P)]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        cl.allreduce(xs, ys, algo=algo)  # warm-up outside the capture
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        cl.allreduce(xs, ys, algo=algo, op="avg")
+    for it in range(6):
+        for k in range(P):
+            fill_uniform(xs[k], seed=700 + 10 * it + k)
+        g.replay()
+        cl.check()
+        ref = _ref(xs) / P
+        for k in range(P):
+            assert (ys[k] - ref).abs().max().item() <= 1e-6, f"replay {it} rank {k}"
