@@ -8,6 +8,7 @@ Per (size, algo): p50 and mean over `--iters` event-timed calls after `--warmup`
 slowest rank's numbers are reported (all-reduce MAX). algbw = bytes / p50, busbw =
 algbw * 2(P-1)/P (nccl-tests convention). Engines:
   twoshot / oneshot / ring  fused xGMI kernels (csrc/hip/xgmi_comm.hip)
+  threshold                 straggler-tolerant kernel at th = 1 (csrc/hip/xgmi_threshold.hip)
   rccl                      torch.distributed all_reduce on the nccl (= RCCL) backend
   torch                     torch.distributed all_reduce on whatever backend (gloo on CPU)
 Rank 0 prints a table to stderr and one JSON line per row to stdout (or --json FILE).
@@ -94,8 +95,13 @@ def main(argv: list[str] | None = None) -> int:
             for algo in args.algos:
                 if algo in ("rccl", "torch") or (algo == "oneshot" and size > cl.comms[0].slot_bytes):
                     continue
-                p50, mean = _time(lambda: cl.allreduce([x[:n] for x in xs], [y[:n] for y in ys], algo=algo, op=args.op),
-                                  args.iters, args.warmup, lambda: torch.cuda.synchronize(dev))
+                if algo == "threshold":
+                    def fn():
+                        cl.allreduce_threshold([x[:n] for x in xs], [y[:n] for y in ys])
+                else:
+                    def fn():
+                        cl.allreduce([x[:n] for x in xs], [y[:n] for y in ys], algo=algo, op=args.op)
+                p50, mean = _time(fn, args.iters, args.warmup, lambda: torch.cuda.synchronize(dev))
                 cl.check()
                 rows.append({"P": P, "mode": "local", "bytes": size, "algo": algo, "p50_us": round(p50 * 1e3, 2),
                              "mean_us": round(mean * 1e3, 2)})
@@ -109,7 +115,7 @@ def main(argv: list[str] | None = None) -> int:
         on_gpu = args.backend == "nccl"
         dev = torch.device("cuda", local) if on_gpu else torch.device("cpu")
         comm = None
-        if on_gpu and any(a in ("oneshot", "twoshot", "ring") for a in args.algos):
+        if on_gpu and any(a in ("oneshot", "twoshot", "ring", "threshold") for a in args.algos):
             from .parallel import XgmiCommunicator
 
             comm = XgmiCommunicator(slot_bytes=max(64 << 20, -(-max(sizes) // P) + (1 << 20)))
@@ -123,6 +129,10 @@ def main(argv: list[str] | None = None) -> int:
                     if comm is None or (algo == "oneshot" and size > comm.slot_bytes):
                         continue
                     fn = lambda: comm.allreduce(x[:n], y[:n], algo=algo, op=args.op)  # noqa: E731
+                elif algo == "threshold":
+                    if comm is None:
+                        continue
+                    fn = lambda: comm.allreduce_threshold(x[:n], y[:n])  # noqa: E731
                 elif algo in ("rccl", "torch"):
                     if algo == "rccl" and not on_gpu:
                         continue

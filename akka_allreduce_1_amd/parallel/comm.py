@@ -33,7 +33,8 @@ class CommError(RuntimeError):
     """A device-side wait timed out (a peer never delivered); the communicator is poisoned."""
 
 
-_ERR_NAMES = {1: "scatter wait timed out", 2: "reduce wait timed out", 4: "barrier timed out", 8: "bad arguments"}
+_ERR_NAMES = {1: "scatter wait timed out", 2: "reduce wait timed out", 4: "barrier timed out", 8: "bad arguments",
+              16: "a peer stayed more than maxLag rounds behind"}
 
 
 def _describe(err: int) -> str:
@@ -79,7 +80,9 @@ class XgmiCommunicator:
     """Allreduce over directly mapped peer HBM for the ranks of a torch.distributed group."""
 
     def __init__(self, group=None, *, device: torch.device | int | None = None, slot_bytes: int | None = None,
-                 grid: int = 0, timeout_s: float = 20.0, cpu_group=None):
+                 grid: int = 0, timeout_s: float = 20.0, cpu_group=None, max_lag: int = 0):
+        """max_lag: rounds a rank may run ahead of the slowest peer in `allreduce_threshold`
+        (lag-ring depth max_lag + 1; slab memory grows by that factor)."""
         import torch.distributed as dist
 
         if not dist.is_initialized():
@@ -101,7 +104,8 @@ class XgmiCommunicator:
         # the next collective.
         self._c, handle, err = None, None, ""
         try:
-            self._c = _H.XgmiComm(self.rank, self.world, self.device.index, self.slot_bytes, grid, timeout_s)
+            self._c = _H.XgmiComm(self.rank, self.world, self.device.index, self.slot_bytes, grid, timeout_s,
+                                  max_lag + 1)
             handle = self._c.ipc_handle()
         except Exception as e:  # noqa: BLE001
             err = f"rank {self.rank}: {e}"
@@ -216,6 +220,28 @@ class XgmiCommunicator:
     def allreduce_(self, t: torch.Tensor, *, op: str = "sum", algo: str = "auto") -> torch.Tensor:
         return self.allreduce(t, t, op=op, algo=algo)
 
+    def allreduce_threshold(self, inp: torch.Tensor, out: torch.Tensor | None = None, *, th_reduce: float = 1.0,
+                            th_complete: float = 1.0, counts: bool = False):
+        """Straggler-tolerant allreduce round (the reference's thReduce / thComplete / maxLag
+        semantics, csrc/hip/xgmi_threshold.hip). Returns `out`, or `(out, counts)` with
+        counts an int32 [world, nch] tensor: contributions summed per output chunk (0 = the
+        chunk was given up and is zero). The tensor must fit one launch (<= world * slot)."""
+        if out is None:
+            out = torch.empty_like(inp)
+        if inp.device != self.device or out.device != self.device or inp.numel() != out.numel():
+            raise ValueError(f"inp/out must live on {self.device} with the same numel")
+        if not (inp.is_contiguous() and out.is_contiguous()) or inp.dtype != out.dtype:
+            raise ValueError("inp/out must be contiguous with the same dtype")
+        code = _dtype_code(inp.dtype)
+        cnt = None
+        if counts:
+            cnt = torch.zeros(self.world, self._c.threshold_chunks(inp.numel(), code), dtype=torch.int32,
+                              device=self.device)
+        self._c.allreduce_threshold(inp.data_ptr(), out.data_ptr(), inp.numel(), code,
+                                    torch.cuda.current_stream(self.device).cuda_stream, th_reduce, th_complete,
+                                    0 if cnt is None else cnt.data_ptr())
+        return (out, cnt) if counts else out
+
     def barrier(self) -> None:
         self._c.barrier(torch.cuda.current_stream(self.device).cuda_stream)
 
@@ -252,14 +278,15 @@ class LocalCluster:
     """
 
     def __init__(self, world: int, devices: Sequence[int] | None = None, *, slot_bytes: int = 16 << 20,
-                 grid: int = 32, timeout_s: float = 10.0):
+                 grid: int = 32, timeout_s: float = 10.0, max_lag: int = 0):
         if devices is None:
             devices = [torch.cuda.current_device()] * world
         if len(devices) != world:
             raise ValueError("need one device per logical rank")
         self.world = world
         self.devices = [torch.device("cuda", d) for d in devices]
-        self.comms = [_H.XgmiComm(k, world, self.devices[k].index, slot_bytes, grid, timeout_s) for k in range(world)]
+        self.comms = [_H.XgmiComm(k, world, self.devices[k].index, slot_bytes, grid, timeout_s, max_lag + 1)
+                      for k in range(world)]
         for c in self.comms:
             c.connect_local(self.comms)
         self.groups: list[list[int]] = []
@@ -269,8 +296,7 @@ class LocalCluster:
             else:
                 self.groups.append([k])
 
-    def allreduce(self, inputs: Sequence[torch.Tensor], outputs: Sequence[torch.Tensor] | None = None, *,
-                  algo: str = "auto", op: str = "sum") -> list[torch.Tensor]:
+    def _check(self, inputs, outputs) -> list[torch.Tensor]:
         if len(inputs) != self.world:
             raise ValueError("one input per logical rank")
         outputs = list(outputs) if outputs is not None else [torch.empty_like(x) for x in inputs]
@@ -283,6 +309,12 @@ class LocalCluster:
                 raise ValueError(f"rank {k} tensors must live on {self.devices[k]}")
             if not (x.is_contiguous() and y.is_contiguous()):
                 raise ValueError("tensors must be contiguous")
+        return outputs
+
+    def allreduce(self, inputs: Sequence[torch.Tensor], outputs: Sequence[torch.Tensor] | None = None, *,
+                  algo: str = "auto", op: str = "sum") -> list[torch.Tensor]:
+        outputs = self._check(inputs, outputs)
+        n = inputs[0].numel()
         code = _dtype_code(inputs[0].dtype)
         for g in self.groups:
             dev = self.devices[g[0]]
@@ -291,6 +323,25 @@ class LocalCluster:
                                         torch.cuda.current_stream(dev).cuda_stream, ALGOS[algo],
                                         1.0 / self.world if op == "avg" else 1.0)
         return outputs
+
+    def allreduce_threshold(self, inputs: Sequence[torch.Tensor], outputs: Sequence[torch.Tensor] | None = None, *,
+                            th_reduce: float = 1.0, th_complete: float = 1.0):
+        """One straggler-tolerant round for every logical rank (see
+        XgmiCommunicator.allreduce_threshold). Returns (outputs, counts[world, world, nch])."""
+        outputs = self._check(inputs, outputs)
+        n = inputs[0].numel()
+        code = _dtype_code(inputs[0].dtype)
+        counts = []
+        for g in self.groups:
+            dev = self.devices[g[0]]
+            nch = self.comms[g[0]].threshold_chunks(n, code, len(g))
+            cnt = torch.zeros(len(g), self.world, nch, dtype=torch.int32, device=dev)
+            _H.XgmiComm.allreduce_threshold_local([self.comms[k] for k in g], [inputs[k].data_ptr() for k in g],
+                                                  [outputs[k].data_ptr() for k in g], n, code,
+                                                  torch.cuda.current_stream(dev).cuda_stream, th_reduce, th_complete,
+                                                  cnt.data_ptr())
+            counts.append(cnt)
+        return outputs, counts[0] if len(counts) == 1 else counts
 
     def barrier(self) -> None:
         for g in self.groups:

@@ -195,6 +195,7 @@ enum : uint32_t {
   ERR_TIMEOUT_REDUCE = 2u,
   ERR_TIMEOUT_BARRIER = 4u,
   ERR_BAD_ARGS = 8u,
+  ERR_TIMEOUT_LAG = 16u,  // threshold kernel: a peer stayed more than maxLag rounds behind
 };
 
 __device__ __forceinline__ uint32_t ld_flag(const uint32_t* f) {

@@ -141,11 +141,12 @@ void bind_hip(py::module_& m) {
       .def_readonly("bytes", &CommStats::bytes)
       .def_readonly("oneshot", &CommStats::oneshot)
       .def_readonly("twoshot", &CommStats::twoshot)
-      .def_readonly("ring", &CommStats::ring);
+      .def_readonly("ring", &CommStats::ring)
+      .def_readonly("threshold", &CommStats::threshold);
 
   py::class_<XgmiComm>(h, "XgmiComm")
-      .def(py::init<int, int, int, int64_t, int, double>(), py::arg("rank"), py::arg("world"), py::arg("device"),
-           py::arg("slot_bytes"), py::arg("grid") = 0, py::arg("timeout_s") = 20.0)
+      .def(py::init<int, int, int, int64_t, int, double, int>(), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::arg("slot_bytes"), py::arg("grid") = 0, py::arg("timeout_s") = 20.0, py::arg("rows") = 1)
       .def("ipc_handle", [](const XgmiComm& c) { return py::bytes(c.ipc_handle()); })
       .def("connect", [](XgmiComm& c, const std::vector<py::bytes>& hs) {
         std::vector<std::string> v;
@@ -162,6 +163,35 @@ void bind_hip(py::module_& m) {
           },
           py::arg("inp"), py::arg("out"), py::arg("n"), py::arg("dtype"), py::arg("stream") = 0,
           py::arg("algo") = Algo::Auto, py::arg("scale") = 1.0f)
+      .def(
+          "allreduce_threshold",
+          [](XgmiComm& c, uintptr_t in, uintptr_t out, int64_t n, DType dt, uintptr_t stream, float thr, float thc,
+             uintptr_t counts, float scale) {
+            py::gil_scoped_release r;
+            c.allreduce_threshold(as_cptr(in), as_ptr(out), n, dt, as_stream(stream), thr, thc,
+                                  reinterpret_cast<int32_t*>(counts), scale);
+          },
+          py::arg("inp"), py::arg("out"), py::arg("n"), py::arg("dtype"), py::arg("stream") = 0,
+          py::arg("th_reduce") = 1.0f, py::arg("th_complete") = 1.0f, py::arg("counts") = 0, py::arg("scale") = 1.0f)
+      .def_static(
+          "allreduce_threshold_local",
+          [](const std::vector<XgmiComm*>& comms, const std::vector<uintptr_t>& ins, const std::vector<uintptr_t>& outs,
+             int64_t n, DType dt, uintptr_t stream, float thr, float thc, uintptr_t counts, float scale) {
+            std::vector<const void*> i;
+            std::vector<void*> o;
+            for (auto p : ins) i.push_back(as_cptr(p));
+            for (auto p : outs) o.push_back(as_ptr(p));
+            py::gil_scoped_release r;
+            XgmiComm::allreduce_threshold_local(comms, i, o, n, dt, as_stream(stream), thr, thc,
+                                                reinterpret_cast<int32_t*>(counts), scale);
+          },
+          py::arg("comms"), py::arg("inputs"), py::arg("outputs"), py::arg("n"), py::arg("dtype"),
+          py::arg("stream") = 0, py::arg("th_reduce") = 1.0f, py::arg("th_complete") = 1.0f, py::arg("counts") = 0,
+          py::arg("scale") = 1.0f)
+      .def("threshold_chunks", &XgmiComm::threshold_chunks, py::arg("n"), py::arg("dtype"),
+           py::arg("ranks_in_launch") = 1)
+      .def("set_straggler", &XgmiComm::set_straggler, py::arg("rank"), py::arg("us"))
+      .def_property_readonly("rows", &XgmiComm::rows)
       .def(
           "barrier",
           [](XgmiComm& c, uintptr_t stream) {

@@ -38,7 +38,7 @@ constexpr int kMaxRanks = 16;
 constexpr int kCommThreads = 256;
 
 struct CommStats {
-  uint64_t calls = 0, launches = 0, bytes = 0, oneshot = 0, twoshot = 0, ring = 0;
+  uint64_t calls = 0, launches = 0, bytes = 0, oneshot = 0, twoshot = 0, ring = 0, threshold = 0;
 };
 
 class XgmiComm {
@@ -46,7 +46,9 @@ class XgmiComm {
   // slot_bytes: capacity of one receive slot (one block of one peer). A two-shot launch
   // reduces up to world * slot_bytes bytes, a one-shot launch up to slot_bytes bytes;
   // larger tensors are processed in segments. Memory per GPU ~ 2 * world * slot_bytes.
-  XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid = 0, double timeout_s = 20.0);
+  // rows: depth of the lag ring of S/R slots used by allreduce_threshold (maxLag + 1);
+  // the other algorithms use row 0. Memory per GPU ~ 2 * rows * world * slot_bytes.
+  XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid = 0, double timeout_s = 20.0, int rows = 1);
   ~XgmiComm();
   XgmiComm(const XgmiComm&) = delete;
   XgmiComm& operator=(const XgmiComm&) = delete;
@@ -63,6 +65,25 @@ class XgmiComm {
   // Pointers must be 16-byte aligned. Enqueued on `stream`; returns immediately.
   void allreduce(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, Algo algo = Algo::Auto,
                  float scale = 1.f);
+  // Straggler-tolerant round (xgmi_threshold.hip): a chunk is reduced once
+  // f32((th_reduce * P)) contributions are in, the round completes once
+  // f32(th_complete * P * nch) reduced chunks are in (missing ones -> zeros, count 0), and
+  // ranks run at most rows-1 rounds apart. counts (optional, int32 [P][nch], device) receives
+  // the number of contributions summed per output chunk. The tensor must fit one launch
+  // (n * dtype <= world * slot_bytes); nch = threshold_chunks(n, dt).
+  void allreduce_threshold(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, float th_reduce,
+                           float th_complete, int32_t* counts = nullptr, float scale = 1.f);
+  static void allreduce_threshold_local(const std::vector<XgmiComm*>& comms, const std::vector<const void*>& ins,
+                                        const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream,
+                                        float th_reduce, float th_complete, int32_t* counts = nullptr,
+                                        float scale = 1.f);
+  // Chunks per block the threshold kernel uses for n elements (size of `counts` = P * this).
+  int threshold_chunks(int64_t n, DType dt, int ranks_in_launch = 1) const;
+  // Test knob: rank `rank` idles `us` microseconds at the start of each threshold launch.
+  void set_straggler(int rank, double us) {
+    delay_rank_ = rank;
+    delay_us_ = us;
+  }
   // Device-side barrier over all ranks (enqueued on `stream`).
   void barrier(hipStream_t stream);
 
@@ -78,6 +99,7 @@ class XgmiComm {
   void clear_error();
 
   int rank() const { return rank_; }
+  int rows() const { return rows_; }
   int world() const { return world_; }
   int device() const { return device_; }
   int grid() const { return grid_; }
@@ -106,8 +128,16 @@ class XgmiComm {
   static void launch_segment(const std::vector<XgmiComm*>& group, const char* const* ins, char* const* outs,
                              int64_t n, DType dt, hipStream_t stream, Algo kind, float scale);
 
-  int rank_, world_, device_, grid_;
+  static void run_threshold(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
+                            const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, float thr,
+                            float thc, int32_t* counts, float scale);
+  void geometry_threshold(int64_t n, DType dt, int ranks_here, int64_t* block, int64_t* chunk, int* nch,
+                          int* gx) const;
+
+  int rank_, world_, device_, grid_, rows_;
   int64_t slot_bytes_, maxch_, off_S_, off_R_, off_B_, slab_bytes_;
+  int delay_rank_ = -1;
+  double delay_us_ = 0;
   int64_t oneshot_max_;
   double timeout_s_;
   int fence_ = 3;

@@ -18,205 +18,16 @@
 #include <stdexcept>
 #include <string>
 
+#include "../core/data_buffer.h"
 #include "../core/trace.h"
-#include "device_common.h"
-#include "xgmi_comm.h"
+#include "xgmi_device.h"
 
 namespace mxar {
-using namespace dev;
 
 void hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) {
     throw std::runtime_error(std::string("HIP error in ") + what + ": " + hipGetErrorString(e));
   }
-}
-
-// One launch serves one rank (one process per GPU: gridDim.y == 1, rank = rank0) or all
-// P logical ranks of a single-process cluster on one device (gridDim.y == P, rank =
-// rank0 + blockIdx.y): every rank's workgroups are then co-resident in ONE dispatch, so
-// no rank can be starved behind another on a shared hardware queue.
-struct CommArgs {
-  const char* in[kMaxRanks];
-  char* out[kMaxRanks];
-  uint32_t* ctl[kMaxRanks];  // per rank: [0] epoch [1] ticket [2] error
-  int64_t n;      // elements in this segment
-  int64_t block;  // elements per block (two-shot) / whole segment (one-shot)
-  int64_t chunk;  // elements per chunk (scatter / gather work unit)
-  int64_t subchunk;  // elements per reduce work unit (chunk split `sub` ways)
-  int nch;        // chunks per block
-  int sub;        // reduce units per chunk
-  int P;
-  int rank0;
-  int fence;      // bit0: system release before flags, bit1: system acquire after waits
-  float scale;    // applied to the fp32 sum before rounding (1 = sum, 1/P = mean)
-  int64_t maxch;
-  int64_t off_S, off_R, slot_bytes;
-  uint64_t timeout;
-  char* base[kMaxRanks];
-};
-
-__device__ __forceinline__ uint32_t* f1(const CommArgs& a, int k, int s, int c) {
-  return reinterpret_cast<uint32_t*>(a.base[k]) + static_cast<int64_t>(s) * a.maxch + c;
-}
-__device__ __forceinline__ uint32_t* f2(const CommArgs& a, int k, int s, int c) {
-  return reinterpret_cast<uint32_t*>(a.base[k]) + static_cast<int64_t>(a.P + s) * a.maxch + c;
-}
-__device__ __forceinline__ uint32_t* fb(const CommArgs& a, int k, int s) {
-  return reinterpret_cast<uint32_t*>(a.base[k]) + static_cast<int64_t>(2 * a.P) * a.maxch + s;
-}
-__device__ __forceinline__ int64_t clamp_len(int64_t avail, int64_t cap) {
-  return avail <= 0 ? 0 : (avail < cap ? avail : cap);
-}
-
-// Push len elements from ordinary memory into a (peer's) slab with write-through stores,
-// 16 B per lane, 4 packs in flight per lane.
-template <class E>
-__device__ __forceinline__ void copy_to_slab(char* slab_dst, const char* src, int64_t len) {
-  const int64_t npk = len / E::ELEMS;
-  const Pack16* s = reinterpret_cast<const Pack16*>(src);
-  const __amdgpu_buffer_rsrc_t rd = slab_rsrc(slab_dst);
-  int64_t i = threadIdx.x;
-  constexpr int U = 4;
-  for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
-    Pack16 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = s[i + u * kCommThreads];
-#pragma unroll
-    for (int u = 0; u < U; ++u) st16_wt(rd, static_cast<uint32_t>((i + u * kCommThreads) * 16), v[u]);
-  }
-  for (; i < npk; i += kCommThreads) st16_wt(rd, static_cast<uint32_t>(i * 16), s[i]);
-  const int64_t t = npk * E::ELEMS + threadIdx.x;
-  if (t < len) copy_scalar_wt<E>(rd, src, t);
-}
-
-// Copy len elements out of an uncached slab (sc1 loads), 4 packs in flight per lane.
-template <class E>
-__device__ __forceinline__ void copy_from_slab(char* dst, const char* slab_src, int64_t len) {
-  const int64_t npk = len / E::ELEMS;
-  const __amdgpu_buffer_rsrc_t rs = slab_rsrc(slab_src);
-  const __amdgpu_buffer_rsrc_t rd = slab_rsrc(dst);
-  int64_t i = threadIdx.x;
-  constexpr int U = 4;
-  for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
-    Pack16 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = ld16_sc1(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
-#pragma unroll
-    for (int u = 0; u < U; ++u) st16_wt(rd, static_cast<uint32_t>((i + u * kCommThreads) * 16), v[u]);
-  }
-  for (; i < npk; i += kCommThreads) st16_wt(rd, static_cast<uint32_t>(i * 16), ld16_sc1(rs, static_cast<uint32_t>(i * 16)));
-  const int64_t t = npk * E::ELEMS + threadIdx.x;
-  if (t < len) st_scalar_wt<E>(rd, t, ld_scalar_sc1<E>(rs, t));
-}
-
-// Reduction sources: source s is at slab0 + s * stride, except source `own` (if >= 0),
-// which is the rank's own input. Every source is read with sc1 buffer loads through a
-// descriptor chosen by a scalar select, so the P loads of a pack issue back to back
-// with no per-source branch (and the own input is simply L1-bypassing).
-struct RedSrc {
-  const char* own_ptr;
-  const char* slab0;
-  int64_t stride;
-  int own;
-  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(int s) const {
-    return slab_rsrc(s == own ? own_ptr : slab0 + s * stride);
-  }
-};
-
-// Sum P sources (fixed order s = 0..P-1, fp32) and store the result to up to P
-// destinations. src(s) / dst(k) return byte pointers to element 0 of the chunk.
-// Destinations of a reduced chunk: every peer slab is written through (sc0 sc1); the
-// rank's own output (k == own) too when `wt_out`, so it leaves no dirty L2 lines for the
-// next release fence to write back.
-template <class E, int PT, class DstF>
-__device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, int own_dst, DstF dst, int64_t len,
-                                          float scale, bool wt_out) {
-  const int64_t npk = len / E::ELEMS;
-  constexpr int U = 2;
-  int64_t i = threadIdx.x;
-  if constexpr (PT > 0) {
-    __amdgpu_buffer_rsrc_t rs[PT];
-#pragma unroll
-    for (int s = 0; s < PT; ++s) rs[s] = src.rsrc(s);
-    for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
-      Pack16 v[PT][U];
-#pragma unroll
-      for (int s = 0; s < PT; ++s)
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[s][u] = ld16_sc1(rs[s], static_cast<uint32_t>((i + u * kCommThreads) * 16));
-      Acc<E> acc[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) acc[u].zero();
-#pragma unroll
-      for (int s = 0; s < PT; ++s)
-#pragma unroll
-        for (int u = 0; u < U; ++u) acc[u].add(v[s][u]);
-      if (scale != 1.f) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) acc[u].scale(scale);
-      }
-      Pack16 o[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) o[u] = acc[u].pack();
-      for (int k = 0; k < ndst; ++k) {
-        char* d = dst(k);
-        if (d == nullptr) continue;
-        if (k == own_dst && !wt_out) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) st16(d + (i + u * kCommThreads) * 16, o[u]);
-        } else {
-          const __amdgpu_buffer_rsrc_t rd = slab_rsrc(d);
-#pragma unroll
-          for (int u = 0; u < U; ++u) st16_wt(rd, static_cast<uint32_t>((i + u * kCommThreads) * 16), o[u]);
-        }
-      }
-    }
-  }
-  for (; i < npk; i += kCommThreads) {
-    Acc<E> acc;
-    acc.zero();
-    for (int s = 0; s < P; ++s) acc.add(ld16_sc1(src.rsrc(s), static_cast<uint32_t>(i * 16)));
-    if (scale != 1.f) acc.scale(scale);
-    const Pack16 o = acc.pack();
-    for (int k = 0; k < ndst; ++k) {
-      char* d = dst(k);
-      if (d == nullptr) continue;
-      if (k == own_dst && !wt_out)
-        st16(d + i * 16, o);
-      else
-        st16_wt(slab_rsrc(d), static_cast<uint32_t>(i * 16), o);
-    }
-  }
-  const int64_t t = npk * E::ELEMS + threadIdx.x;
-  if (t < len) {
-    float acc = 0.f;
-    for (int s = 0; s < P; ++s) acc += ld_scalar_sc1<E>(src.rsrc(s), t);
-    acc *= scale;
-    for (int k = 0; k < ndst; ++k) {
-      char* d = dst(k);
-      if (d == nullptr) continue;
-      if (k == own_dst && !wt_out)
-        Scalar<E>::store(d, t, acc);
-      else
-        st_scalar_wt<E>(slab_rsrc(d), t, acc);
-    }
-  }
-}
-
-// The rank's last workgroup to finish publishes the epoch for the next launch.
-__device__ __forceinline__ void finish_launch(uint32_t* ctl, uint32_t epoch) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == gridDim.x - 1) {
-      __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ctl[0], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-__device__ __forceinline__ uint32_t launch_epoch(const uint32_t* ctl) {
-  return __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
 }
 
 // ---------------------------------------------------------------------------------
@@ -496,17 +307,19 @@ static int default_grid(int device) {
   return 2 * cus;  // every workgroup must stay resident (they spin): 2 x 256-thread WG per CU
 }
 
-XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid, double timeout_s)
-    : rank_(rank), world_(world), device_(device), grid_(grid), timeout_s_(timeout_s) {
+XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid, double timeout_s, int rows)
+    : rank_(rank), world_(world), device_(device), grid_(grid), rows_(rows), timeout_s_(timeout_s) {
+  if (rows < 1 || rows > 64) throw std::invalid_argument("XgmiComm: rows (maxLag + 1) must be in [1, 64]");
   if (world < 1 || world > kMaxRanks) throw std::invalid_argument("XgmiComm: world must be in [1, 16]");
   if (rank < 0 || rank >= world) throw std::invalid_argument("XgmiComm: bad rank");
   slot_bytes_ = round_up(std::max<int64_t>(slot_bytes, 64 * 1024), 64 * 1024);
   maxch_ = slot_bytes_ / min_chunk_bytes();
-  const int64_t flag_bytes = (2 * world_ * maxch_ + world_) * 4;
+  // [F1: rows x P x maxch][F2: rows x P x maxch][FB: P][PROG: P][F2C: rows x P x maxch]
+  const int64_t flag_bytes = (3 * rows_ * world_ * maxch_ + 2 * world_) * 4;
   off_S_ = round_up(flag_bytes, 64 * 1024);
-  off_R_ = off_S_ + world_ * slot_bytes_;
-  off_B_ = 2 * world_ * maxch_ * 4;
-  slab_bytes_ = off_R_ + world_ * slot_bytes_;
+  off_R_ = off_S_ + rows_ * world_ * slot_bytes_;
+  off_B_ = 2 * rows_ * world_ * maxch_ * 4;
+  slab_bytes_ = off_R_ + rows_ * world_ * slot_bytes_;
   oneshot_max_ = std::min<int64_t>(slot_bytes_, 256 * 1024);
   if (const char* e = std::getenv("MXAR_ONESHOT_MAX")) oneshot_max_ = std::min<int64_t>(slot_bytes_, std::atoll(e));
   if (grid_ <= 0) grid_ = default_grid(device);
@@ -635,6 +448,7 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   }
   a.n = n;
   a.P = W;
+  a.rows = c0.rows_;
   a.rank0 = c0.rank_;
   a.maxch = c0.maxch_;
   a.off_S = c0.off_S_;
@@ -746,6 +560,108 @@ void XgmiComm::allreduce_local(const std::vector<XgmiComm*>& comms, const std::v
   run(comms, ins, outs, n, dt, stream, algo, scale);
 }
 
+void XgmiComm::geometry_threshold(int64_t n, DType dt, int ranks_here, int64_t* block, int64_t* chunk, int* nch,
+                                  int* gx) const {
+  const int64_t es = static_cast<int64_t>(dtype_size(dt));
+  const int64_t elems = 16 / es;
+  const int64_t min_chunk = min_chunk_bytes() / es;
+  const int gmax = std::max(1, grid_ / std::max(1, ranks_here));
+  *block = round_up(ceil_div(n, world_), elems);
+  // one reduce unit (a chunk: one threshold decision) per workgroup; phase 1/3 get P-1 each
+  *chunk = std::max(min_chunk, round_up(ceil_div(*block, gmax), elems));
+  *nch = static_cast<int>(std::max<int64_t>(1, ceil_div(*block, *chunk)));
+  *gx = std::min(gmax, std::max(*nch, 1));
+}
+
+int XgmiComm::threshold_chunks(int64_t n, DType dt, int ranks_in_launch) const {
+  int64_t b, c;
+  int nch, gx;
+  geometry_threshold(n, dt, ranks_in_launch, &b, &c, &nch, &gx);
+  return nch;
+}
+
+void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
+                             const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, float thr,
+                             float thc, int32_t* counts, float scale) {
+  if (group.empty() || ins.size() != group.size() || outs.size() != group.size())
+    throw std::invalid_argument("XgmiComm: one input and one output per rank");
+  const XgmiComm& c0 = *group[0];
+  for (size_t y = 0; y < group.size(); ++y) {
+    const XgmiComm& c = *group[y];
+    if (!c.connected_) throw std::runtime_error("XgmiComm: connect() first");
+    if (c.device_ != c0.device_ || c.rank_ != c0.rank_ + static_cast<int>(y) || c.world_ != c0.world_ ||
+        c.rows_ != c0.rows_)
+      throw std::invalid_argument("XgmiComm: a grouped launch needs consecutive ranks on one device");
+    if ((reinterpret_cast<uintptr_t>(ins[y]) | reinterpret_cast<uintptr_t>(outs[y])) & 15)
+      throw std::invalid_argument("XgmiComm: buffers must be 16-byte aligned");
+  }
+  if (!(thr >= 0.f && thr <= 1.f && thc >= 0.f && thc <= 1.f))
+    throw std::invalid_argument("allreduce_threshold: thresholds must be in [0, 1]");
+  if (n <= 0) return;
+  const int W = c0.world_;
+  if (W > 32) throw std::invalid_argument("allreduce_threshold: at most 32 ranks");
+  const int64_t es = static_cast<int64_t>(dtype_size(dt));
+  const int ranks_here = static_cast<int>(group.size());
+  CommArgs a;
+  std::memset(&a, 0, sizeof(a));
+  for (size_t y = 0; y < group.size(); ++y) {
+    a.in[y] = static_cast<const char*>(ins[y]);
+    a.out[y] = static_cast<char*>(outs[y]);
+    a.ctl[y] = group[y]->ctl_;
+  }
+  int gx = 1;
+  c0.geometry_threshold(n, dt, ranks_here, &a.block, &a.chunk, &a.nch, &gx);
+  if (a.block * es > c0.slot_bytes_ || a.nch > c0.maxch_)
+    throw std::invalid_argument("allreduce_threshold: tensor exceeds one launch (n * dtype <= world * slot_bytes)");
+  if (ceil_div(static_cast<int64_t>(W - 1) * a.nch, gx) > 64)
+    throw std::logic_error("allreduce_threshold: more than 64 gather units per workgroup");
+  a.n = n;
+  a.P = W;
+  a.rows = c0.rows_;
+  a.rank0 = c0.rank_;
+  a.maxch = c0.maxch_;
+  a.off_S = c0.off_S_;
+  a.off_R = c0.off_R_;
+  a.slot_bytes = c0.slot_bytes_;
+  a.timeout = static_cast<uint64_t>(c0.timeout_s_ * 1e8);
+  a.fence = c0.fence_;
+  a.scale = scale;
+  a.subchunk = a.chunk;
+  a.sub = 1;
+  a.min_reduce = std::max(1, f32_threshold_count(thr, W));
+  a.min_complete = f32_threshold_chunks(thc, W, a.nch);
+  a.counts = counts;
+  a.delay_rank = -1;
+  for (XgmiComm* c : group)
+    if (c->delay_rank_ >= 0 && c->delay_us_ > 0) {
+      a.delay_rank = c->delay_rank_;
+      a.delay = static_cast<uint64_t>(c->delay_us_ * 100.0);  // s_memrealtime: 100 MHz
+    }
+  for (int k = 0; k < W; ++k) a.base[k] = c0.peers_[k];
+  hip_check(hipSetDevice(c0.device_), "hipSetDevice");
+  TraceScope span("xgmi", "threshold " + std::to_string(n * es) + "B",
+                  "{\"rank\":" + std::to_string(c0.rank_) + ",\"ranks_in_launch\":" + std::to_string(ranks_here) + "}");
+  launch_threshold(a, dim3(gx, ranks_here), stream, dt);
+  hip_check(hipGetLastError(), "threshold launch");
+  for (XgmiComm* c : group) {
+    ++c->stats_.calls;
+    ++c->stats_.launches;
+    ++c->stats_.threshold;
+    c->stats_.bytes += n * es;
+  }
+}
+
+void XgmiComm::allreduce_threshold(const void* in, void* out, int64_t n, DType dt, hipStream_t stream,
+                                   float th_reduce, float th_complete, int32_t* counts, float scale) {
+  run_threshold({this}, {in}, {out}, n, dt, stream, th_reduce, th_complete, counts, scale);
+}
+
+void XgmiComm::allreduce_threshold_local(const std::vector<XgmiComm*>& comms, const std::vector<const void*>& ins,
+                                         const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream,
+                                         float th_reduce, float th_complete, int32_t* counts, float scale) {
+  run_threshold(comms, ins, outs, n, dt, stream, th_reduce, th_complete, counts, scale);
+}
+
 void XgmiComm::barrier_group(const std::vector<XgmiComm*>& group, hipStream_t stream) {
   const XgmiComm& c0 = *group[0];
   for (XgmiComm* c : group)
@@ -755,6 +671,7 @@ void XgmiComm::barrier_group(const std::vector<XgmiComm*>& group, hipStream_t st
   std::memset(&a, 0, sizeof(a));
   for (size_t y = 0; y < group.size(); ++y) a.ctl[y] = group[y]->ctl_;
   a.P = c0.world_;
+  a.rows = c0.rows_;
   a.rank0 = c0.rank_;
   a.maxch = c0.maxch_;
   a.timeout = static_cast<uint64_t>(c0.timeout_s_ * 1e8);

@@ -1,0 +1,213 @@
+// Device-side pieces shared by the fused allreduce kernels (xgmi_comm.hip: two-shot,
+// one-shot, ring, barrier; xgmi_threshold.hip: threshold / bounded-staleness two-shot):
+// launch arguments, slab flag addressing, slab copy / reduce loops, launch epochs.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "device_common.h"
+#include "xgmi_comm.h"
+
+namespace mxar {
+using namespace dev;
+
+// One launch serves one rank (one process per GPU: gridDim.y == 1, rank = rank0) or all
+// P logical ranks of a single-process cluster on one device (gridDim.y == P, rank =
+// rank0 + blockIdx.y): every rank's workgroups are then co-resident in ONE dispatch, so
+// no rank can be starved behind another on a shared hardware queue.
+struct CommArgs {
+  const char* in[kMaxRanks];
+  char* out[kMaxRanks];
+  uint32_t* ctl[kMaxRanks];  // per rank: [0] epoch [1] ticket [2] error
+  int64_t n;      // elements in this segment
+  int64_t block;  // elements per block (two-shot) / whole segment (one-shot)
+  int64_t chunk;  // elements per chunk (scatter / gather work unit)
+  int64_t subchunk;  // elements per reduce work unit (chunk split `sub` ways)
+  int nch;        // chunks per block
+  int sub;        // reduce units per chunk
+  int P;
+  int rank0;
+  int fence;      // bit0: system release before flags, bit1: system acquire after waits
+  float scale;    // applied to the fp32 sum before rounding (1 = sum, 1/P = mean)
+  int64_t maxch;
+  int64_t off_S, off_R, slot_bytes;
+  uint64_t timeout;
+  char* base[kMaxRanks];
+  // threshold kernel (xgmi_threshold.hip); rows = 1 for the other kernels
+  int rows;            // lag-ring depth of the S/R slots and F1/F2 flags (maxLag + 1)
+  int min_reduce;      // contributions per chunk that complete a reduce (thReduce)
+  int64_t min_complete;  // reduced chunks that complete the round (thComplete)
+  int32_t* counts;     // optional [P][nch] contributions per output chunk (0 = missing)
+  uint64_t delay;      // test knob: ticks rank `delay_rank` idles before phase 1
+  int delay_rank;
+};
+
+__device__ __forceinline__ uint32_t* f1(const CommArgs& a, int k, int s, int c) {
+  return reinterpret_cast<uint32_t*>(a.base[k]) + static_cast<int64_t>(s) * a.maxch + c;
+}
+__device__ __forceinline__ uint32_t* f2(const CommArgs& a, int k, int s, int c) {
+  return reinterpret_cast<uint32_t*>(a.base[k]) + static_cast<int64_t>(a.rows * a.P + s) * a.maxch + c;
+}
+__device__ __forceinline__ uint32_t* fb(const CommArgs& a, int k, int s) {
+  return reinterpret_cast<uint32_t*>(a.base[k]) + static_cast<int64_t>(2 * a.rows * a.P) * a.maxch + s;
+}
+__device__ __forceinline__ int64_t clamp_len(int64_t avail, int64_t cap) {
+  return avail <= 0 ? 0 : (avail < cap ? avail : cap);
+}
+
+// Push len elements from ordinary memory into a (peer's) slab with write-through stores,
+// 16 B per lane, 4 packs in flight per lane.
+template <class E>
+__device__ __forceinline__ void copy_to_slab(char* slab_dst, const char* src, int64_t len) {
+  const int64_t npk = len / E::ELEMS;
+  const Pack16* s = reinterpret_cast<const Pack16*>(src);
+  const __amdgpu_buffer_rsrc_t rd = slab_rsrc(slab_dst);
+  int64_t i = threadIdx.x;
+  constexpr int U = 4;
+  for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
+    Pack16 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = s[i + u * kCommThreads];
+#pragma unroll
+    for (int u = 0; u < U; ++u) st16_wt(rd, static_cast<uint32_t>((i + u * kCommThreads) * 16), v[u]);
+  }
+  for (; i < npk; i += kCommThreads) st16_wt(rd, static_cast<uint32_t>(i * 16), s[i]);
+  const int64_t t = npk * E::ELEMS + threadIdx.x;
+  if (t < len) copy_scalar_wt<E>(rd, src, t);
+}
+
+// Copy len elements out of an uncached slab (sc1 loads), 4 packs in flight per lane.
+template <class E>
+__device__ __forceinline__ void copy_from_slab(char* dst, const char* slab_src, int64_t len) {
+  const int64_t npk = len / E::ELEMS;
+  const __amdgpu_buffer_rsrc_t rs = slab_rsrc(slab_src);
+  const __amdgpu_buffer_rsrc_t rd = slab_rsrc(dst);
+  int64_t i = threadIdx.x;
+  constexpr int U = 4;
+  for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
+    Pack16 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld16_sc1(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
+#pragma unroll
+    for (int u = 0; u < U; ++u) st16_wt(rd, static_cast<uint32_t>((i + u * kCommThreads) * 16), v[u]);
+  }
+  for (; i < npk; i += kCommThreads) st16_wt(rd, static_cast<uint32_t>(i * 16), ld16_sc1(rs, static_cast<uint32_t>(i * 16)));
+  const int64_t t = npk * E::ELEMS + threadIdx.x;
+  if (t < len) st_scalar_wt<E>(rd, t, ld_scalar_sc1<E>(rs, t));
+}
+
+// Reduction sources: source s is at slab0 + s * stride, except source `own` (if >= 0),
+// which is the rank's own input. Every source is read with sc1 buffer loads through a
+// descriptor chosen by a scalar select, so the P loads of a pack issue back to back
+// with no per-source branch (and the own input is simply L1-bypassing).
+struct RedSrc {
+  const char* own_ptr;
+  const char* slab0;
+  int64_t stride;
+  int own;
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(int s) const {
+    return slab_rsrc(s == own ? own_ptr : slab0 + s * stride);
+  }
+};
+
+// Sum P sources (fixed order s = 0..P-1, fp32) and store the result to up to P
+// destinations. src(s) / dst(k) return byte pointers to element 0 of the chunk.
+// Destinations of a reduced chunk: every peer slab is written through (sc0 sc1); the
+// rank's own output (k == own) too when `wt_out`, so it leaves no dirty L2 lines for the
+// next release fence to write back.
+template <class E, int PT, class DstF>
+__device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, int own_dst, DstF dst, int64_t len,
+                                          float scale, bool wt_out) {
+  const int64_t npk = len / E::ELEMS;
+  constexpr int U = 2;
+  int64_t i = threadIdx.x;
+  if constexpr (PT > 0) {
+    __amdgpu_buffer_rsrc_t rs[PT];
+#pragma unroll
+    for (int s = 0; s < PT; ++s) rs[s] = src.rsrc(s);
+    for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
+      Pack16 v[PT][U];
+#pragma unroll
+      for (int s = 0; s < PT; ++s)
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[s][u] = ld16_sc1(rs[s], static_cast<uint32_t>((i + u * kCommThreads) * 16));
+      Acc<E> acc[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u].zero();
+#pragma unroll
+      for (int s = 0; s < PT; ++s)
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u].add(v[s][u]);
+      if (scale != 1.f) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u].scale(scale);
+      }
+      Pack16 o[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) o[u] = acc[u].pack();
+      for (int k = 0; k < ndst; ++k) {
+        char* d = dst(k);
+        if (d == nullptr) continue;
+        if (k == own_dst && !wt_out) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) st16(d + (i + u * kCommThreads) * 16, o[u]);
+        } else {
+          const __amdgpu_buffer_rsrc_t rd = slab_rsrc(d);
+#pragma unroll
+          for (int u = 0; u < U; ++u) st16_wt(rd, static_cast<uint32_t>((i + u * kCommThreads) * 16), o[u]);
+        }
+      }
+    }
+  }
+  for (; i < npk; i += kCommThreads) {
+    Acc<E> acc;
+    acc.zero();
+    for (int s = 0; s < P; ++s) acc.add(ld16_sc1(src.rsrc(s), static_cast<uint32_t>(i * 16)));
+    if (scale != 1.f) acc.scale(scale);
+    const Pack16 o = acc.pack();
+    for (int k = 0; k < ndst; ++k) {
+      char* d = dst(k);
+      if (d == nullptr) continue;
+      if (k == own_dst && !wt_out)
+        st16(d + i * 16, o);
+      else
+        st16_wt(slab_rsrc(d), static_cast<uint32_t>(i * 16), o);
+    }
+  }
+  const int64_t t = npk * E::ELEMS + threadIdx.x;
+  if (t < len) {
+    float acc = 0.f;
+    for (int s = 0; s < P; ++s) acc += ld_scalar_sc1<E>(src.rsrc(s), t);
+    acc *= scale;
+    for (int k = 0; k < ndst; ++k) {
+      char* d = dst(k);
+      if (d == nullptr) continue;
+      if (k == own_dst && !wt_out)
+        Scalar<E>::store(d, t, acc);
+      else
+        st_scalar_wt<E>(slab_rsrc(d), t, acc);
+    }
+  }
+}
+
+// The rank's last workgroup to finish publishes the epoch for the next launch.
+__device__ __forceinline__ void finish_launch(uint32_t* ctl, uint32_t epoch) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == gridDim.x - 1) {
+      __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ctl[0], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t launch_epoch(const uint32_t* ctl) {
+  return __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+}
+
+
+// Host entry of the threshold kernel (xgmi_threshold.hip).
+void launch_threshold(const CommArgs& a, dim3 grid, hipStream_t s, DType dt);
+
+}  // namespace mxar
