@@ -86,7 +86,8 @@ def main(argv: list[str] | None = None) -> int:
         from .parallel import LocalCluster
 
         P = args.local
-        cl = LocalCluster(P, slot_bytes=max(16 << 20, -(-max(sizes) // P) + (1 << 20)), grid=max(8, 512 // P))
+        cl = LocalCluster(P, slot_bytes=max(16 << 20, -(-max(sizes) // P) + (1 << 20)), grid=512,  # workgroup budget of the device, shared by the P ranks
+                          max_lag=0 if "threshold" in args.algos else None)
         dev = cl.devices[0]
         xs = [fill_uniform(torch.empty(max(sizes) // es, dtype=dtype, device=dev), seed=k) for k in range(P)]
         ys = [torch.empty_like(x) for x in xs]
@@ -118,7 +119,8 @@ def main(argv: list[str] | None = None) -> int:
         if on_gpu and any(a in ("oneshot", "twoshot", "ring", "threshold") for a in args.algos):
             from .parallel import XgmiCommunicator
 
-            comm = XgmiCommunicator(slot_bytes=max(64 << 20, -(-max(sizes) // P) + (1 << 20)))
+            comm = XgmiCommunicator(slot_bytes=max(64 << 20, -(-max(sizes) // P) + (1 << 20)),
+                                    max_lag=0 if "threshold" in args.algos else None)
         x = torch.empty(max(sizes) // es, dtype=dtype, device=dev).uniform_(-1, 1)
         y = torch.empty_like(x)
         sync = (lambda: torch.cuda.synchronize(dev)) if on_gpu else (lambda: None)

@@ -80,9 +80,9 @@ class XgmiCommunicator:
     """Allreduce over directly mapped peer HBM for the ranks of a torch.distributed group."""
 
     def __init__(self, group=None, *, device: torch.device | int | None = None, slot_bytes: int | None = None,
-                 grid: int = 0, timeout_s: float = 20.0, cpu_group=None, max_lag: int = 0):
-        """max_lag: rounds a rank may run ahead of the slowest peer in `allreduce_threshold`
-        (lag-ring depth max_lag + 1; slab memory grows by that factor)."""
+                 grid: int = 0, timeout_s: float = 20.0, cpu_group=None, max_lag: int | None = None):
+        """max_lag: enables `allreduce_threshold`, whose ranks may run up to max_lag rounds
+        ahead of the slowest peer (a lag ring of max_lag + 1 extra slot rows in the slab)."""
         import torch.distributed as dist
 
         if not dist.is_initialized():
@@ -105,7 +105,7 @@ class XgmiCommunicator:
         self._c, handle, err = None, None, ""
         try:
             self._c = _H.XgmiComm(self.rank, self.world, self.device.index, self.slot_bytes, grid, timeout_s,
-                                  max_lag + 1)
+                                  0 if max_lag is None else max_lag + 1)
             handle = self._c.ipc_handle()
         except Exception as e:  # noqa: BLE001
             err = f"rank {self.rank}: {e}"
@@ -278,14 +278,15 @@ class LocalCluster:
     """
 
     def __init__(self, world: int, devices: Sequence[int] | None = None, *, slot_bytes: int = 16 << 20,
-                 grid: int = 32, timeout_s: float = 10.0, max_lag: int = 0):
+                 grid: int = 32, timeout_s: float = 10.0, max_lag: int | None = None):
         if devices is None:
             devices = [torch.cuda.current_device()] * world
         if len(devices) != world:
             raise ValueError("need one device per logical rank")
         self.world = world
         self.devices = [torch.device("cuda", d) for d in devices]
-        self.comms = [_H.XgmiComm(k, world, self.devices[k].index, slot_bytes, grid, timeout_s, max_lag + 1)
+        rows = 0 if max_lag is None else max_lag + 1  # threshold lag ring (allreduce_threshold)
+        self.comms = [_H.XgmiComm(k, world, self.devices[k].index, slot_bytes, grid, timeout_s, rows)
                       for k in range(world)]
         for c in self.comms:
             c.connect_local(self.comms)

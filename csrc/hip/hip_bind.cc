@@ -146,7 +146,7 @@ void bind_hip(py::module_& m) {
 
   py::class_<XgmiComm>(h, "XgmiComm")
       .def(py::init<int, int, int, int64_t, int, double, int>(), py::arg("rank"), py::arg("world"), py::arg("device"),
-           py::arg("slot_bytes"), py::arg("grid") = 0, py::arg("timeout_s") = 20.0, py::arg("rows") = 1)
+           py::arg("slot_bytes"), py::arg("grid") = 0, py::arg("timeout_s") = 20.0, py::arg("threshold_rows") = 0)
       .def("ipc_handle", [](const XgmiComm& c) { return py::bytes(c.ipc_handle()); })
       .def("connect", [](XgmiComm& c, const std::vector<py::bytes>& hs) {
         std::vector<std::string> v;
@@ -191,7 +191,7 @@ void bind_hip(py::module_& m) {
       .def("threshold_chunks", &XgmiComm::threshold_chunks, py::arg("n"), py::arg("dtype"),
            py::arg("ranks_in_launch") = 1)
       .def("set_straggler", &XgmiComm::set_straggler, py::arg("rank"), py::arg("us"))
-      .def_property_readonly("rows", &XgmiComm::rows)
+      .def_property_readonly("threshold_rows", &XgmiComm::threshold_rows)
       .def(
           "barrier",
           [](XgmiComm& c, uintptr_t stream) {

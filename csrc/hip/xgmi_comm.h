@@ -46,9 +46,11 @@ class XgmiComm {
   // slot_bytes: capacity of one receive slot (one block of one peer). A two-shot launch
   // reduces up to world * slot_bytes bytes, a one-shot launch up to slot_bytes bytes;
   // larger tensors are processed in segments. Memory per GPU ~ 2 * world * slot_bytes.
-  // rows: depth of the lag ring of S/R slots used by allreduce_threshold (maxLag + 1);
-  // the other algorithms use row 0. Memory per GPU ~ 2 * rows * world * slot_bytes.
-  XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid = 0, double timeout_s = 20.0, int rows = 1);
+  // threshold_rows: depth of the lag ring of S/R slots used by allreduce_threshold
+  // (maxLag + 1; 0 = threshold rounds disabled). The other algorithms use row 0.
+  // Memory per GPU ~ 2 * (1 + threshold_rows) * world * slot_bytes.
+  XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid = 0, double timeout_s = 20.0,
+           int threshold_rows = 0);
   ~XgmiComm();
   XgmiComm(const XgmiComm&) = delete;
   XgmiComm& operator=(const XgmiComm&) = delete;
@@ -99,7 +101,7 @@ class XgmiComm {
   void clear_error();
 
   int rank() const { return rank_; }
-  int rows() const { return rows_; }
+  int threshold_rows() const { return rows_ - 1; }
   int world() const { return world_; }
   int device() const { return device_; }
   int grid() const { return grid_; }

@@ -307,9 +307,11 @@ static int default_grid(int device) {
   return 2 * cus;  // every workgroup must stay resident (they spin): 2 x 256-thread WG per CU
 }
 
-XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid, double timeout_s, int rows)
-    : rank_(rank), world_(world), device_(device), grid_(grid), rows_(rows), timeout_s_(timeout_s) {
-  if (rows < 1 || rows > 64) throw std::invalid_argument("XgmiComm: rows (maxLag + 1) must be in [1, 64]");
+XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid, double timeout_s,
+                   int threshold_rows)
+    : rank_(rank), world_(world), device_(device), grid_(grid), rows_(1 + threshold_rows), timeout_s_(timeout_s) {
+  if (threshold_rows < 0 || threshold_rows > 64)
+    throw std::invalid_argument("XgmiComm: threshold_rows (maxLag + 1) must be in [0, 64]");
   if (world < 1 || world > kMaxRanks) throw std::invalid_argument("XgmiComm: world must be in [1, 16]");
   if (rank < 0 || rank >= world) throw std::invalid_argument("XgmiComm: bad rank");
   slot_bytes_ = round_up(std::max<int64_t>(slot_bytes, 64 * 1024), 64 * 1024);
@@ -595,6 +597,8 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
     if ((reinterpret_cast<uintptr_t>(ins[y]) | reinterpret_cast<uintptr_t>(outs[y])) & 15)
       throw std::invalid_argument("XgmiComm: buffers must be 16-byte aligned");
   }
+  if (c0.rows_ < 2)
+    throw std::invalid_argument("allreduce_threshold: construct the comm with threshold_rows = maxLag + 1 >= 1");
   if (!(thr >= 0.f && thr <= 1.f && thc >= 0.f && thc <= 1.f))
     throw std::invalid_argument("allreduce_threshold: thresholds must be in [0, 1]");
   if (n <= 0) return;
@@ -618,6 +622,7 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
   a.n = n;
   a.P = W;
   a.rows = c0.rows_;
+  a.trows = c0.rows_ - 1;
   a.rank0 = c0.rank_;
   a.maxch = c0.maxch_;
   a.off_S = c0.off_S_;

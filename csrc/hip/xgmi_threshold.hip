@@ -8,8 +8,11 @@
 //   thComplete - the round completes once `min_complete` of the P x nch reduced chunks are
 //                in; chunks still missing then are output as zeros with count 0
 //                (AllreduceWorker.scala:143-145, reachRoundThreshold DataBuffer.scala:69-75).
-//   maxLag     - the S/R slots and their flags form a ring of `rows` = maxLag + 1 rows
-//                indexed by epoch; a rank may run up to maxLag rounds ahead of the slowest
+//   maxLag     - the S/R slots and their flags form a ring of `trows` = maxLag + 1 rows
+//                (slab rows 1..trows; row 0 belongs to the lock-step kernels, so a fast
+//                rank that moves on to another algorithm never touches a row a lagging
+//                rank still reads), indexed by the threshold-round counter ctl[4]; a rank
+//                may run up to maxLag rounds ahead of the slowest
 //                peer (the worker's lag ring, AllreduceWorker.scala:59-73). Before
 //                writing row e % rows a rank waits until every peer has finished the
 //                round that last used it (progress words), so a row is never overwritten
@@ -128,8 +131,9 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   const char* const in = a.in[y];
   char* const out = a.out[y];
   uint32_t* const ctl = a.ctl[y];
-  const uint32_t epoch = launch_epoch(ctl);
-  const int row = static_cast<int>(epoch % static_cast<uint32_t>(a.rows));
+  // threshold rounds count separately (ctl[4]); flags and progress words carry this count
+  const uint32_t epoch = __hip_atomic_load(&ctl[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int row = 1 + static_cast<int>(epoch % static_cast<uint32_t>(a.trows));
   const int G = gridDim.x;
   const int64_t slot = a.slot_bytes;
   const int64_t rowS = a.off_S + static_cast<int64_t>(row) * P * slot;
@@ -148,7 +152,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   // Lag gate: every peer has finished the round that last used row `row` of its slab
   // (progress words live in OUR slab, written by the peers at the end of each round).
   wait_flags([&](int k) -> const uint32_t* { return k == r ? nullptr : prog(a, r, k); }, P,
-             epoch - static_cast<uint32_t>(a.rows), deadline, err, ERR_TIMEOUT_LAG, acq);
+             epoch - static_cast<uint32_t>(a.trows), deadline, err, ERR_TIMEOUT_LAG, acq);
 
   // Phase 1 - ScatterBlock into the owners' row slots
   const int nu = (P - 1) * a.nch;
@@ -268,7 +272,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
     }
   }
 
-  // Round end: the last workgroup resets the completion counter, advances the epoch and
+  // Round end: the last workgroup resets the completion counter, advances the round count and
   // tells every peer that this rank is done with row `row` (all its reads happened
   // before the workgroups' tickets).
   __syncthreads();
@@ -277,7 +281,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
     if (t == static_cast<uint32_t>(G) - 1) {
       __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&ctl[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ctl[0], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ctl[4], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       for (int k = 0; k < P; ++k)
         if (k != r) st_flag(prog(a, k, r), epoch);

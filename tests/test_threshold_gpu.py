@@ -62,7 +62,7 @@ def test_threshold_one_is_exact(P, dtype, max_lag):
 @pytest.mark.parametrize("P", [3, 4])
 def test_straggler_is_left_out_and_its_block_given_up(P):
     slow = P - 1
-    cl = LocalCluster(P, slot_bytes=1 << 20, grid=32, timeout_s=10.0)
+    cl = LocalCluster(P, slot_bytes=1 << 20, grid=32, timeout_s=10.0, max_lag=0)
     cl.comms[0].set_straggler(slow, 5000.0)  # 5 ms idle at the start of the slow rank
     th = (P - 1) / P
     n = 50_001
@@ -160,3 +160,28 @@ def test_lag_ring_two_processes():
             p.kill()
     bad = [r for r in res if not r[1]]
     assert not bad, bad
+
+
+def test_threshold_interleaved_with_lockstep_algorithms():
+    """Threshold rounds keep their own round count and slab rows: interleaving them with
+    two-shot / one-shot / ring launches on the same communicator stays correct."""
+    P, n = 4, 30_011
+    cl = LocalCluster(P, slot_bytes=1 << 20, grid=32, timeout_s=10.0, max_lag=1)
+    for it, algo in enumerate(["twoshot", "threshold", "oneshot", "ring", "threshold", "threshold", "twoshot"]):
+        xs = [fill_uniform(torch.empty(n, device=DEV), seed=77 * it + k) for k in range(P)]
+        if algo == "threshold":
+            ys, counts = cl.allreduce_threshold(xs)
+            assert bool((counts == P).all())
+        else:
+            ys = cl.allreduce(xs, algo=algo)
+        cl.check()
+        ref = _sum(xs, range(P))
+        for y in ys:
+            assert (y - ref).abs().max().item() <= 1e-6, algo
+
+
+def test_threshold_needs_a_lag_ring():
+    cl = LocalCluster(2, slot_bytes=1 << 20, grid=8)
+    xs = [torch.zeros(1024, device=DEV) for _ in range(2)]
+    with pytest.raises(Exception, match="threshold_rows"):
+        cl.allreduce_threshold(xs)
