@@ -124,14 +124,18 @@ class XgmiCommunicator:
         if errs:
             raise CommError("XgmiCommunicator connect failed: " + "; ".join(errs))
         self.table: list[tuple[int, str]] = []  # (max bytes, algo) from tune(); empty = built-in policy
+        self._default_grid = self._c.grid
 
     # ------------------------------------------------------------------ tuning
     def tune(self, max_bytes: int = 256 << 20, dtype: torch.dtype = torch.bfloat16, iters: int = 10,
-             candidates: Sequence[str] = ("oneshot", "twoshot", "rccl"), min_bytes: int = 4 << 10) -> list[dict]:
+             candidates: Sequence[str] = ("oneshot", "twoshot", "rccl"), min_bytes: int = 4 << 10,
+             grids: Sequence[int] = (), grid_min_bytes: int = 1 << 20) -> list[dict]:
         """Measure p50 latency of every algorithm per power-of-4 size class in
         [min_bytes, max_bytes] and keep the fastest per class (the slowest rank's p50
         decides; rank 0's choice is broadcast so every rank dispatches identically - a split
-        decision would deadlock). Returns one row per size: {bytes, <algo>_p50_us, choice}."""
+        decision would deadlock). `grids`: extra workgroup counts tried for twoshot / ring at
+        sizes >= grid_min_bytes (labels "twoshot@256"); only counts <= the default grid, so
+        every workgroup stays resident. Returns one row per size: {bytes, <algo>_p50_us, choice}."""
         import torch.distributed as dist
 
         from ..ops import fill_uniform
@@ -147,10 +151,16 @@ class XgmiCommunicator:
             sizes.append(size)
             size *= 4
         sizes.append(max_bytes)
+        extra = [g for g in grids if 0 < g < self._default_grid]
         for size in sizes:
             n = size // es
             best, best_t, row = None, float("inf"), {"bytes": size}
+            labels = []
             for algo in candidates:
+                labels.append(algo)
+                if algo in ("twoshot", "ring") and size >= grid_min_bytes:
+                    labels += [f"{algo}@{g}" for g in extra]
+            for algo in labels:
                 if algo == "oneshot" and (size > self.slot_bytes or size > (8 << 20)):
                     continue
                 if algo == "rccl" and dist.get_backend(self.group) != "nccl":
@@ -213,7 +223,11 @@ class XgmiCommunicator:
         else:  # the mean is fused into the kernel (scale applied to the fp32 sum)
             stream = torch.cuda.current_stream(self.device).cuda_stream
             scale = 1.0 / self.world if op == "avg" else 1.0
-            self._c.allreduce(inp.data_ptr(), out.data_ptr(), inp.numel(), _dtype_code(inp.dtype), stream, ALGOS[algo],
+            name, _, g = algo.partition("@")  # "twoshot@256": workgroup count chosen by tune()
+            grid = int(g) if g else self._default_grid
+            if self._c.grid != grid:
+                self._c.grid = grid
+            self._c.allreduce(inp.data_ptr(), out.data_ptr(), inp.numel(), _dtype_code(inp.dtype), stream, ALGOS[name],
                               scale)
         return out
 

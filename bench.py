@@ -137,7 +137,8 @@ def main() -> None:
     sweep = None
     if engine_ok and not args.no_tune:
         sweep = comm.tune(max_bytes=nbytes, dtype=dtype, iters=args.sweep_steps,
-                          candidates=("oneshot", "twoshot", "ring") + (() if args.no_rccl else ("rccl",)))
+                          candidates=("oneshot", "twoshot", "ring") + (() if args.no_rccl else ("rccl",)),
+                          grids=(128, 256))
     if engine_ok and args.algo != "rccl":
         algo = args.algo
         chosen = comm._pick(nbytes) if algo == "auto" else algo
@@ -193,7 +194,7 @@ def main() -> None:
     if reason:
         result["engine_note"] = reason
 
-    if engine_ok and chosen != "twoshot" and world > 1:
+    if engine_ok and chosen.partition("@")[0] != "twoshot" and world > 1:
         for _ in range(args.warmup):
             comm.allreduce(x, y, algo="twoshot")
         twall, _ = timed(lambda: comm.allreduce(x, y, algo="twoshot"), args.steps, dev)
