@@ -40,25 +40,32 @@ def log(rank: int, msg: str) -> None:
         print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def timed(fn, steps: int, dev) -> tuple[float, list[float]]:
-    """Wall time of `steps` back-to-back calls (barrier + sync on both sides) and per-call
-    device times from event pairs."""
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+def timed(fn, steps: int, dev) -> float:
+    """Wall time of `steps` back-to-back calls, barrier + sync on both sides. Nothing else
+    is enqueued in between (an event record per step would add a cache flush per step)."""
     torch.cuda.synchronize(dev)
     dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(steps):
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    return time.perf_counter() - t0
+
+
+def event_times(fn, iters: int, dev) -> list[float]:
+    """Per-call device times (ms) from event pairs - a separate, untimed pass for p50."""
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(iters)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(iters)]
+    torch.cuda.synchronize(dev)
+    for i in range(iters):
         starts[i].record()
         fn()
         ends[i].record()
     torch.cuda.synchronize(dev)
-    dist.barrier()
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
-    per = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    return wall, per
+    return [a.elapsed_time(b) for a, b in zip(starts, ends)]
 
 
 def max_over_ranks(x: float, dev) -> float:
@@ -151,7 +158,8 @@ def main() -> None:
 
     for _ in range(args.warmup):
         step()
-    wall, per = timed(step, args.steps, dev)
+    wall = timed(step, args.steps, dev)
+    per = event_times(step, args.steps, dev)
     if engine_ok:
         try:
             comm.check()
@@ -197,13 +205,14 @@ def main() -> None:
     if engine_ok and chosen.partition("@")[0] != "twoshot" and world > 1:
         for _ in range(args.warmup):
             comm.allreduce(x, y, algo="twoshot")
-        twall, _ = timed(lambda: comm.allreduce(x, y, algo="twoshot"), args.steps, dev)
+        twall = timed(lambda: comm.allreduce(x, y, algo="twoshot"), args.steps, dev)
         tms = max_over_ranks(twall, dev) / args.steps * 1e3
         result["xgmi_twoshot"] = {"algbw": round(nbytes / (tms / 1e3) / 1e9, 2), "ms_per_step": round(tms, 4)}
     if not args.no_rccl and chosen not in ("rccl", "rccl-fallback"):
         for _ in range(args.warmup):
             step_rccl()
-        rwall, rper = timed(step_rccl, args.steps, dev)
+        rwall = timed(step_rccl, args.steps, dev)
+        rper = event_times(step_rccl, args.steps, dev)
         rms = max_over_ranks(rwall, dev) / args.steps * 1e3
         r_alg = nbytes / (rms / 1e3) / 1e9
         result["rccl"] = {"algbw": round(r_alg, 2), "ms_per_step": round(rms, 4),
