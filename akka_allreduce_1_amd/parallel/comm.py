@@ -125,6 +125,16 @@ class XgmiCommunicator:
             raise CommError("XgmiCommunicator connect failed: " + "; ".join(errs))
         self.table: list[tuple[int, str]] = []  # (max bytes, algo) from tune(); empty = built-in policy
         self._default_grid = self._c.grid
+        self._p2p = None
+
+    @property
+    def p2p(self):
+        """The reference protocol over RCCL point-to-point (parallel/p2p.py), created lazily."""
+        if self._p2p is None:
+            from .p2p import P2PCommunicator
+
+            self._p2p = P2PCommunicator(self.group, chunk_bytes=self.slot_bytes)
+        return self._p2p
 
     # ------------------------------------------------------------------ tuning
     def tune(self, max_bytes: int = 256 << 20, dtype: torch.dtype = torch.bfloat16, iters: int = 10,
@@ -212,7 +222,9 @@ class XgmiCommunicator:
             algo = self._pick(inp.numel() * inp.element_size())
         if op not in ("sum", "avg"):
             raise ValueError(f"unsupported op {op!r}")
-        if algo == "rccl" or inp.dtype not in (torch.float32, torch.bfloat16):
+        if algo in ("p2p", "rsag"):  # the same protocol over RCCL point-to-point / RS+AG
+            self.p2p.allreduce(inp, out, op=op, algo=algo)
+        elif algo == "rccl" or inp.dtype not in (torch.float32, torch.bfloat16):
             import torch.distributed as dist
 
             if out.data_ptr() != inp.data_ptr():

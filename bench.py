@@ -42,7 +42,9 @@ def log(rank: int, msg: str) -> None:
 
 def timed(fn, steps: int, dev) -> float:
     """Wall time of `steps` back-to-back calls, barrier + sync on both sides. Nothing else
-    is enqueued in between (an event record per step would add a cache flush per step)."""
+    is enqueued in between (an event record per step would add a cache flush per step).
+    The clock stops once this rank's device has drained; the closing barrier runs after
+    it, and the caller takes the MAX over ranks, so the slowest rank decides."""
     torch.cuda.synchronize(dev)
     dist.barrier()
     torch.cuda.synchronize(dev)
@@ -50,9 +52,10 @@ def timed(fn, steps: int, dev) -> float:
     for _ in range(steps):
         fn()
     torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
     dist.barrier()
     torch.cuda.synchronize(dev)
-    return time.perf_counter() - t0
+    return t1 - t0
 
 
 def event_times(fn, iters: int, dev) -> list[float]:
@@ -97,7 +100,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--size-mib", type=int, default=256)
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
-    ap.add_argument("--algo", choices=["auto", "twoshot", "oneshot", "ring", "rccl"], default="auto")
+    ap.add_argument("--algo", choices=["auto", "twoshot", "oneshot", "ring", "rccl", "rsag", "p2p"], default="auto")
     ap.add_argument("--no-rccl", action="store_true", help="skip the RCCL comparison timing")
     ap.add_argument("--no-tune", action="store_true", help="skip the size sweep / algorithm tuner")
     ap.add_argument("--sweep-steps", type=int, default=10)
@@ -143,9 +146,9 @@ def main() -> None:
 
     sweep = None
     if engine_ok and not args.no_tune:
+        rccl_algos = () if args.no_rccl else ("rccl", "rsag", "p2p") if world > 1 else ("rccl",)
         sweep = comm.tune(max_bytes=nbytes, dtype=dtype, iters=args.sweep_steps,
-                          candidates=("oneshot", "twoshot", "ring") + (() if args.no_rccl else ("rccl",)),
-                          grids=(128, 256))
+                          candidates=("oneshot", "twoshot", "ring") + rccl_algos, grids=(128, 256))
     if engine_ok and args.algo != "rccl":
         algo = args.algo
         chosen = comm._pick(nbytes) if algo == "auto" else algo

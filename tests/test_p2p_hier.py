@@ -1,0 +1,131 @@
+"""P2PCommunicator (the reference's direct protocol over point-to-point sends) and the
+two-level HierarchicalCommunicator, multi-process on gloo (CPU). Expected values are fp32
+sums computed locally from every rank's deterministic input."""
+import os
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from akka_allreduce_1_amd.parallel.p2p import block_bounds, reduce_rows
+
+
+def _inputs(world, n, dtype, seed=0):
+    return [torch.randn(n, generator=torch.Generator().manual_seed(seed + r)).to(dtype) for r in range(world)]
+
+
+def _ref(xs, scale=1.0):
+    return sum(x.float() for x in xs) * scale
+
+
+def test_block_bounds_cover_and_match_reference_partition():
+    # stepSize = ceil(N / P); the last block ends at N (AllreduceWorker.scala:211-228)
+    assert block_bounds(8, 4) == [(0, 2), (2, 4), (4, 6), (6, 8)]
+    assert block_bounds(3, 2) == [(0, 2), (2, 3)]
+    # reference crash config (P=4, N=6): trailing blocks are empty, nothing is lost
+    b = block_bounds(6, 4)
+    assert b[0] == (0, 2) and b[-1] == (6, 6)
+    for m, p in ((1, 8), (7, 3), (100, 7)):
+        bb = block_bounds(m, p)
+        assert bb[0][0] == 0 and bb[-1][1] == m
+        assert all(bb[i][1] == bb[i + 1][0] for i in range(p - 1))
+
+
+def test_reduce_rows_cpu_accumulates_in_fp32():
+    slots = torch.tensor([[1.0, 2.0], [3.0, 4.0], [5.0, 6.0]]).to(torch.bfloat16)
+    out = torch.empty(2, dtype=torch.bfloat16)
+    reduce_rows(slots, out, scale=0.5)
+    assert out.tolist() == [4.5, 6.0]
+
+
+def _p2p_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.parallel import P2PCommunicator
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = P2PCommunicator(chunk_bytes=64)  # 16 fp32 per block per segment: many segments
+        for algo in ("p2p", "rsag"):
+            for n in (1, 5, 16 * world, 1000, 4099):
+                for dtype in (torch.float32, torch.bfloat16):
+                    xs = _inputs(world, n, dtype, seed=n)
+                    y = comm.allreduce(xs[rank], algo=algo)
+                    tol = 1e-5 if dtype == torch.float32 else 2e-2 * world
+                    err = (y.float() - _ref(xs)).abs().max().item()
+                    assert err <= tol, (algo, n, dtype, err)
+                # in place + mean
+                xs = _inputs(world, 333, torch.float32, seed=7)
+                t = xs[rank].clone()
+                comm.allreduce_(t, op="avg", algo=algo)
+                assert torch.allclose(t, _ref(xs, 1 / world), atol=1e-6), algo
+        assert comm.stats["segments"] > comm.stats["calls"]
+        q.put((rank, True, ""))
+    except Exception:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, False, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _hier_worker(rank, world, port, cols, q):
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.parallel import HierarchicalCommunicator, P2PCommunicator
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        h = HierarchicalCommunicator(cols)
+        for n in (1, 3, 64, 1001):
+            xs = _inputs(world, n, torch.float32, seed=100 + n)
+            y = h.allreduce(xs[rank])
+            assert torch.allclose(y, _ref(xs), atol=1e-5), n
+        xs = _inputs(world, 50, torch.float32, seed=3)
+        t = xs[rank].clone()
+        h.allreduce_(t, op="avg")
+        assert torch.allclose(t, _ref(xs, 1 / world), atol=1e-6)
+        # the column level can itself be the point-to-point protocol
+        h2 = HierarchicalCommunicator(cols)
+        if h2.rows > 1:
+            p = P2PCommunicator(h2.col_group)
+            h2.col_comm = type("C", (), {"allreduce_": lambda self, t, op="sum": p.allreduce_(t, op=op)})()
+        y = h2.allreduce(xs[rank])
+        assert torch.allclose(y, _ref(xs), atol=1e-5)
+        q.put((rank, True, ""))
+    except Exception:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, False, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(target, world, *extra):
+    from akka_allreduce_1_amd.parallel.comm import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, *extra, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    bad = [r for r in res if not r[1]]
+    assert not bad, bad[0][2]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_p2p_allreduce_gloo(world):
+    _run(_p2p_worker, world)
+
+
+@pytest.mark.parametrize("cols", [2, 4, 1])
+def test_hierarchical_allreduce_gloo(cols):
+    _run(_hier_worker, 4, cols)
