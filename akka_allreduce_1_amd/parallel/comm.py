@@ -247,11 +247,16 @@ class XgmiCommunicator:
         return self.allreduce(t, t, op=op, algo=algo)
 
     def allreduce_threshold(self, inp: torch.Tensor, out: torch.Tensor | None = None, *, th_reduce: float = 1.0,
-                            th_complete: float = 1.0, counts: bool = False):
+                            th_complete: float = 1.0, counts: bool = False, op: str = "sum", rescale: bool = False):
         """Straggler-tolerant allreduce round (the reference's thReduce / thComplete / maxLag
         semantics, csrc/hip/xgmi_threshold.hip). Returns `out`, or `(out, counts)` with
         counts an int32 [world, nch] tensor: contributions summed per output chunk (0 = the
-        chunk was given up and is zero). The tensor must fit one launch (<= world * slot)."""
+        chunk was given up and is zero). The tensor must fit one launch (<= world * slot).
+        op="avg" divides by world; rescale=True extrapolates a chunk summed from cnt < world
+        contributions by world / cnt inside the kernel (with avg: the mean over the ranks
+        that contributed) - the reference leaves partial sums unscaled."""
+        if op not in ("sum", "avg"):
+            raise ValueError(f"unsupported op {op!r}")
         if out is None:
             out = torch.empty_like(inp)
         if inp.device != self.device or out.device != self.device or inp.numel() != out.numel():
@@ -265,7 +270,8 @@ class XgmiCommunicator:
                               device=self.device)
         self._c.allreduce_threshold(inp.data_ptr(), out.data_ptr(), inp.numel(), code,
                                     torch.cuda.current_stream(self.device).cuda_stream, th_reduce, th_complete,
-                                    0 if cnt is None else cnt.data_ptr())
+                                    0 if cnt is None else cnt.data_ptr(), 1.0 / self.world if op == "avg" else 1.0,
+                                    rescale)
         return (out, cnt) if counts else out
 
     def barrier(self) -> None:
@@ -352,7 +358,7 @@ class LocalCluster:
         return outputs
 
     def allreduce_threshold(self, inputs: Sequence[torch.Tensor], outputs: Sequence[torch.Tensor] | None = None, *,
-                            th_reduce: float = 1.0, th_complete: float = 1.0):
+                            th_reduce: float = 1.0, th_complete: float = 1.0, op: str = "sum", rescale: bool = False):
         """One straggler-tolerant round for every logical rank (see
         XgmiCommunicator.allreduce_threshold). Returns (outputs, counts[world, world, nch])."""
         outputs = self._check(inputs, outputs)
@@ -366,7 +372,7 @@ class LocalCluster:
             _H.XgmiComm.allreduce_threshold_local([self.comms[k] for k in g], [inputs[k].data_ptr() for k in g],
                                                   [outputs[k].data_ptr() for k in g], n, code,
                                                   torch.cuda.current_stream(dev).cuda_stream, th_reduce, th_complete,
-                                                  cnt.data_ptr())
+                                                  cnt.data_ptr(), 1.0 / self.world if op == "avg" else 1.0, rescale)
             counts.append(cnt)
         return outputs, counts[0] if len(counts) == 1 else counts
 

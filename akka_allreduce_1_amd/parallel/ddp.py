@@ -18,6 +18,12 @@ so this module makes the gradients themselves the flat vectors:
 
 `comm` is anything with `allreduce_(tensor, op=...)` that runs on the current stream:
 `XgmiCommunicator` (fused xGMI kernels), or `TorchDistComm` (RCCL / gloo; CPU tests).
+
+Straggler-tolerant steps (`th_reduce` / `th_complete` < 1, the reference's thresholds,
+AllreduceWorker.scala:116-145): every bucket is reduced by the threshold kernel
+(`XgmiCommunicator.allreduce_threshold`, communicator built with `max_lag`), so a slow rank
+delays nobody: its late contributions are left out of this step's sums, and with
+`rescale=True` each partial chunk is extrapolated by world / contributors inside the kernel.
 """
 from __future__ import annotations
 
@@ -68,10 +74,16 @@ class GradBucket:
 class BucketedGradReducer:
     def __init__(self, params: Iterable[torch.nn.Parameter] | torch.nn.Module, comm, *,
                  bucket_bytes: int = 64 << 20, op: str = "avg", overlap: bool = True,
-                 first_bucket_bytes: int | None = None, sync: str = "native", event_scope: int = 1):
+                 first_bucket_bytes: int | None = None, sync: str = "native", event_scope: int = 1,
+                 th_reduce: float = 1.0, th_complete: float = 1.0, rescale: bool = False):
         """sync: how the comm stream is ordered after backward's gradient writes -
         "native" = reusable HIP events created with `event_scope` (1: device-scope release,
-        enough within one GPU; 0: HIP default system-scope), "torch" = torch.cuda events."""
+        enough within one GPU; 0: HIP default system-scope), "torch" = torch.cuda events.
+        th_reduce / th_complete < 1 (or rescale): threshold rounds per bucket (module doc)."""
+        self.threshold = th_reduce < 1.0 or th_complete < 1.0 or rescale
+        self.th = (float(th_reduce), float(th_complete), bool(rescale))
+        if self.threshold and not hasattr(comm, "allreduce_threshold"):
+            raise ValueError("threshold rounds need a communicator with allreduce_threshold (XgmiCommunicator)")
         if isinstance(params, torch.nn.Module):
             params = params.parameters()
         self.params = [p for p in params if p.requires_grad]
@@ -85,6 +97,11 @@ class BucketedGradReducer:
         self.stream = torch.cuda.Stream(device=self.device) if self.on_gpu else None
         self.sync = sync if self.on_gpu else "none"
         self.buckets = self._build(bucket_bytes, first_bucket_bytes)
+        if self.threshold:
+            cap = getattr(comm, "world", 1) * getattr(comm, "slot_bytes", 0)
+            big = [b.nbytes for b in self.buckets if b.nbytes > cap]
+            if big:
+                raise ValueError(f"threshold rounds need buckets <= world * slot_bytes = {cap} B (largest {max(big)})")
         self._events: list[int] = []
         if self.sync == "native":
             from .._native import C
@@ -154,6 +171,14 @@ class BucketedGradReducer:
             self._launch(self.buckets[self._next])
             self._next += 1
 
+    def _reduce(self, b: GradBucket) -> None:
+        if self.threshold:
+            thr, thc, rescale = self.th
+            self.comm.allreduce_threshold(b.buffer, b.buffer, th_reduce=thr, th_complete=thc, op=self.op,
+                                          rescale=rescale)
+        else:
+            self.comm.allreduce_(b.buffer, op=self.op)
+
     def _launch(self, b: GradBucket) -> None:
         if self.sync == "native":
             cs = torch.cuda.current_stream(self.device).cuda_stream
@@ -161,17 +186,17 @@ class BucketedGradReducer:
             self._H.event_record(ev, cs)
             self._H.stream_wait_event(self.stream.cuda_stream, ev)
             with torch.cuda.stream(self.stream):
-                self.comm.allreduce_(b.buffer, op=self.op)
+                self._reduce(b)
             b.done = True
         elif self.on_gpu:
             compute = torch.cuda.current_stream(self.device)
             self.stream.wait_stream(compute)
             with torch.cuda.stream(self.stream):
-                self.comm.allreduce_(b.buffer, op=self.op)
+                self._reduce(b)
                 b.done = torch.cuda.Event()
                 b.done.record(self.stream)
         else:
-            self.comm.allreduce_(b.buffer, op=self.op)
+            self._reduce(b)
         b.launched = True
         self.stats["buckets_launched"] += 1
         self.stats["bytes"] += b.nbytes

@@ -166,28 +166,30 @@ void bind_hip(py::module_& m) {
       .def(
           "allreduce_threshold",
           [](XgmiComm& c, uintptr_t in, uintptr_t out, int64_t n, DType dt, uintptr_t stream, float thr, float thc,
-             uintptr_t counts, float scale) {
+             uintptr_t counts, float scale, bool rescale) {
             py::gil_scoped_release r;
             c.allreduce_threshold(as_cptr(in), as_ptr(out), n, dt, as_stream(stream), thr, thc,
-                                  reinterpret_cast<int32_t*>(counts), scale);
+                                  reinterpret_cast<int32_t*>(counts), scale, rescale);
           },
           py::arg("inp"), py::arg("out"), py::arg("n"), py::arg("dtype"), py::arg("stream") = 0,
-          py::arg("th_reduce") = 1.0f, py::arg("th_complete") = 1.0f, py::arg("counts") = 0, py::arg("scale") = 1.0f)
+          py::arg("th_reduce") = 1.0f, py::arg("th_complete") = 1.0f, py::arg("counts") = 0, py::arg("scale") = 1.0f,
+          py::arg("rescale") = false)
       .def_static(
           "allreduce_threshold_local",
           [](const std::vector<XgmiComm*>& comms, const std::vector<uintptr_t>& ins, const std::vector<uintptr_t>& outs,
-             int64_t n, DType dt, uintptr_t stream, float thr, float thc, uintptr_t counts, float scale) {
+             int64_t n, DType dt, uintptr_t stream, float thr, float thc, uintptr_t counts, float scale,
+             bool rescale) {
             std::vector<const void*> i;
             std::vector<void*> o;
             for (auto p : ins) i.push_back(as_cptr(p));
             for (auto p : outs) o.push_back(as_ptr(p));
             py::gil_scoped_release r;
             XgmiComm::allreduce_threshold_local(comms, i, o, n, dt, as_stream(stream), thr, thc,
-                                                reinterpret_cast<int32_t*>(counts), scale);
+                                                reinterpret_cast<int32_t*>(counts), scale, rescale);
           },
           py::arg("comms"), py::arg("inputs"), py::arg("outputs"), py::arg("n"), py::arg("dtype"),
           py::arg("stream") = 0, py::arg("th_reduce") = 1.0f, py::arg("th_complete") = 1.0f, py::arg("counts") = 0,
-          py::arg("scale") = 1.0f)
+          py::arg("scale") = 1.0f, py::arg("rescale") = false)
       .def("threshold_chunks", &XgmiComm::threshold_chunks, py::arg("n"), py::arg("dtype"),
            py::arg("ranks_in_launch") = 1)
       .def("set_straggler", &XgmiComm::set_straggler, py::arg("rank"), py::arg("us"))

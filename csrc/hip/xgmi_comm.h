@@ -72,13 +72,16 @@ class XgmiComm {
   // f32(th_complete * P * nch) reduced chunks are in (missing ones -> zeros, count 0), and
   // ranks run at most rows-1 rounds apart. counts (optional, int32 [P][nch], device) receives
   // the number of contributions summed per output chunk. The tensor must fit one launch
-  // (n * dtype <= world * slot_bytes); nch = threshold_chunks(n, dt).
+  // (n * dtype <= world * slot_bytes); nch = threshold_chunks(n, dt). rescale: a chunk
+  // reduced from cnt < P contributions is multiplied by P / cnt before the rounding, i.e.
+  // the sum is extrapolated from the contributions that made it (with scale = 1/P: the mean
+  // over the contributors) - the reference leaves partial sums unscaled.
   void allreduce_threshold(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, float th_reduce,
-                           float th_complete, int32_t* counts = nullptr, float scale = 1.f);
+                           float th_complete, int32_t* counts = nullptr, float scale = 1.f, bool rescale = false);
   static void allreduce_threshold_local(const std::vector<XgmiComm*>& comms, const std::vector<const void*>& ins,
                                         const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream,
                                         float th_reduce, float th_complete, int32_t* counts = nullptr,
-                                        float scale = 1.f);
+                                        float scale = 1.f, bool rescale = false);
   // Chunks per block the threshold kernel uses for n elements (size of `counts` = P * this).
   int threshold_chunks(int64_t n, DType dt, int ranks_in_launch = 1) const;
   // Test knob: rank `rank` idles `us` microseconds at the start of each threshold launch.
@@ -132,7 +135,7 @@ class XgmiComm {
 
   static void run_threshold(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
                             const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, float thr,
-                            float thc, int32_t* counts, float scale);
+                            float thc, int32_t* counts, float scale, bool rescale);
   void geometry_threshold(int64_t n, DType dt, int ranks_here, int64_t* block, int64_t* chunk, int* nch,
                           int* gx) const;
 

@@ -584,7 +584,7 @@ int XgmiComm::threshold_chunks(int64_t n, DType dt, int ranks_in_launch) const {
 
 void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
                              const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, float thr,
-                             float thc, int32_t* counts, float scale) {
+                             float thc, int32_t* counts, float scale, bool rescale) {
   if (group.empty() || ins.size() != group.size() || outs.size() != group.size())
     throw std::invalid_argument("XgmiComm: one input and one output per rank");
   const XgmiComm& c0 = *group[0];
@@ -631,6 +631,7 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
   a.timeout = static_cast<uint64_t>(c0.timeout_s_ * 1e8);
   a.fence = c0.fence_;
   a.scale = scale;
+  a.rescale = rescale ? 1 : 0;
   a.subchunk = a.chunk;
   a.sub = 1;
   a.min_reduce = std::max(1, f32_threshold_count(thr, W));
@@ -657,14 +658,15 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
 }
 
 void XgmiComm::allreduce_threshold(const void* in, void* out, int64_t n, DType dt, hipStream_t stream,
-                                   float th_reduce, float th_complete, int32_t* counts, float scale) {
-  run_threshold({this}, {in}, {out}, n, dt, stream, th_reduce, th_complete, counts, scale);
+                                   float th_reduce, float th_complete, int32_t* counts, float scale, bool rescale) {
+  run_threshold({this}, {in}, {out}, n, dt, stream, th_reduce, th_complete, counts, scale, rescale);
 }
 
 void XgmiComm::allreduce_threshold_local(const std::vector<XgmiComm*>& comms, const std::vector<const void*>& ins,
                                          const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream,
-                                         float th_reduce, float th_complete, int32_t* counts, float scale) {
-  run_threshold(comms, ins, outs, n, dt, stream, th_reduce, th_complete, counts, scale);
+                                         float th_reduce, float th_complete, int32_t* counts, float scale,
+                                         bool rescale) {
+  run_threshold(comms, ins, outs, n, dt, stream, th_reduce, th_complete, counts, scale, rescale);
 }
 
 void XgmiComm::barrier_group(const std::vector<XgmiComm*>& group, hipStream_t stream) {

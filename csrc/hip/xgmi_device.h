@@ -39,6 +39,7 @@ struct CommArgs {
   int min_reduce;      // contributions per chunk that complete a reduce (thReduce)
   int64_t min_complete;  // reduced chunks that complete the round (thComplete)
   int32_t* counts;     // optional [P][nch] contributions per output chunk (0 = missing)
+  int rescale;         // scale a chunk reduced from cnt contributions by P / cnt
   uint64_t delay;      // test knob: ticks rank `delay_rank` idles before phase 1
   int delay_rank;
 };

@@ -42,7 +42,7 @@ __device__ __forceinline__ uint32_t* f2c(const CommArgs& a, int k, int rs, int c
 template <class E>
 __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, uint32_t mask, const char* own_in,
                                               const char* S, int64_t slot, char* own_out, int64_t roff,
-                                              int64_t len, bool wt_out) {
+                                              int64_t len, bool wt_out, float scale) {
   const int64_t npk = len / E::ELEMS;
   constexpr int U = 2;
   int64_t i = threadIdx.x;
@@ -62,7 +62,7 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
     Pack16 o[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (a.scale != 1.f) acc[u].scale(a.scale);
+      if (scale != 1.f) acc[u].scale(scale);
       o[u] = acc[u].pack();
     }
     for (int k = 0; k < P; ++k) {
@@ -82,7 +82,7 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
     acc.zero();
     for (int s = 0; s < P; ++s)
       if ((mask >> s) & 1u) acc.add(ld16_sc1(slab_rsrc(s == r ? own_in : S + s * slot), static_cast<uint32_t>(i * 16)));
-    if (a.scale != 1.f) acc.scale(a.scale);
+    if (scale != 1.f) acc.scale(scale);
     const Pack16 o = acc.pack();
     for (int k = 0; k < P; ++k) {
       char* d = k == r ? own_out : a.base[k] + roff;
@@ -97,7 +97,7 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
     float acc = 0.f;
     for (int s = 0; s < P; ++s)
       if ((mask >> s) & 1u) acc += ld_scalar_sc1<E>(slab_rsrc(s == r ? own_in : S + s * slot), t);
-    acc *= a.scale;
+    acc *= scale;
     for (int k = 0; k < P; ++k) {
       char* d = k == r ? own_out : a.base[k] + roff;
       if (k == r && !wt_out)
@@ -198,9 +198,10 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
     __syncthreads();
     const uint32_t mask = sh_mask;
     const int cnt = __popc(mask);
+    const float sc = (a.rescale && cnt > 0) ? a.scale * static_cast<float>(P) / static_cast<float>(cnt) : a.scale;
     if (len > 0)
       reduce_masked<E>(a, P, r, mask, in + (bstart_own + cstart) * es, a.base[r] + rowS + cstart * es, slot,
-                       out + (bstart_own + cstart) * es, rowR + r * slot + cstart * es, len, a.fence & 1);
+                       out + (bstart_own + cstart) * es, rowR + r * slot + cstart * es, len, a.fence & 1, sc);
     if (threadIdx.x < static_cast<unsigned>(P) && static_cast<int>(threadIdx.x) != r)
       st_flag(f2c(a, static_cast<int>(threadIdx.x), row * P + r, c), static_cast<uint32_t>(cnt));
     if (threadIdx.x == 0) {

@@ -1,5 +1,7 @@
 """BucketedGradReducer + XgmiCommunicator: 2 processes on one MI355X (IPC-mapped slabs),
-gradients overlapped with backward on the comm stream, checked against per-rank references."""
+gradients overlapped with backward on the comm stream, checked against per-rank references.
+mode "threshold": every bucket goes through the straggler-tolerant kernel (th = 1 with the
+fused rescale, so the result must still be the exact mean)."""
 import os
 
 import pytest
@@ -16,7 +18,7 @@ def _model(seed, dtype):
     return m.to(device="cuda:0", dtype=dtype)
 
 
-def _worker(rank, world, port, q, dtype):
+def _worker(rank, world, port, q, dtype, mode):
     import torch.distributed as dist
 
     from akka_allreduce_1_amd.parallel import BucketedGradReducer, XgmiCommunicator
@@ -25,9 +27,11 @@ def _worker(rank, world, port, q, dtype):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        comm = XgmiCommunicator(device=0, slot_bytes=1 << 20, grid=8, timeout_s=15.0)
+        thr = mode == "threshold"
+        comm = XgmiCommunicator(device=0, slot_bytes=1 << 20, grid=8, timeout_s=15.0, max_lag=1 if thr else None)
         m, ref = _model(0, dtype), _model(0, dtype)
-        red = BucketedGradReducer(m, comm, bucket_bytes=32 << 10, op="avg")
+        red = BucketedGradReducer(m, comm, bucket_bytes=32 << 10, op="avg", rescale=thr)
+        assert red.threshold == thr
         assert len(red.buckets) >= 3
         g = torch.Generator(device="cuda:0")
         data = [torch.randn(16, 64, device="cuda:0", generator=g.manual_seed(10 + r)).to(dtype) for r in range(world)]
@@ -56,14 +60,15 @@ def _worker(rank, world, port, q, dtype):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("mode", ["exact", "threshold"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_ddp_reducer_xgmi_two_processes(dtype):
+def test_ddp_reducer_xgmi_two_processes(dtype, mode):
     from akka_allreduce_1_amd.parallel import free_port
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, dtype)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, dtype, mode)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(2)]

@@ -92,6 +92,36 @@ def test_straggler_is_left_out_and_its_block_given_up(P):
                 torch.testing.assert_close(got, without[lo:hi], rtol=0, atol=1e-6)
 
 
+@pytest.mark.parametrize("P", [3, 4])
+def test_straggler_rescaled_mean_over_contributors(P):
+    """rescale=True + op="avg": a chunk summed from cnt contributions is divided by cnt
+    (the mean over the ranks that made it), fused into the kernel."""
+    slow = 0
+    cl = LocalCluster(P, slot_bytes=1 << 20, grid=32, timeout_s=10.0, max_lag=0)
+    cl.comms[0].set_straggler(slow, 5000.0)
+    th = (P - 1) / P
+    n = 20_011
+    xs = [fill_uniform(torch.empty(n, device=DEV), seed=300 + k) for k in range(P)]
+    ys, counts = cl.allreduce_threshold(xs, th_reduce=th, th_complete=th, op="avg", rescale=True)
+    cl.check()
+    block, _ = _blocks(n, P, counts.shape[2], torch.float32)
+    fast_mean = _sum(xs, [k for k in range(P) if k != slow]) / (P - 1)
+    full_mean = _sum(xs, range(P)) / P
+    for k in range(P):
+        for j in range(P):
+            lo, hi = j * block, min(n, (j + 1) * block)
+            if lo >= hi:
+                continue
+            got = ys[k][lo:hi]
+            if k == slow and j == slow:
+                torch.testing.assert_close(got, full_mean[lo:hi], rtol=0, atol=1e-6)
+            elif j == slow:
+                assert bool((got == 0).all())
+            else:
+                assert bool((counts[k, j] == P - 1).all())
+                torch.testing.assert_close(got, fast_mean[lo:hi], rtol=0, atol=1e-6)
+
+
 def _lag_worker(rank, world, port, results):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     import time
