@@ -104,11 +104,19 @@ def main() -> None:
     ap.add_argument("--no-rccl", action="store_true", help="skip the RCCL comparison timing")
     ap.add_argument("--no-tune", action="store_true", help="skip the size sweep / algorithm tuner")
     ap.add_argument("--sweep-steps", type=int, default=10)
+    ap.add_argument("--share-device", action="store_true",
+                    help="rehearsal: every rank on cuda:0 over gloo (RCCL refuses two ranks on one GPU), "
+                         "workgroup budget split between the ranks so all spinning workgroups stay resident")
     args = ap.parse_args()
 
-    rank, world, local = init_distributed("nccl")
+    rank, world, local = init_distributed("gloo" if args.share_device else "nccl")
     if world != args.gpus:
         log(rank, f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
+    grid = 0
+    if args.share_device:
+        local, args.no_rccl = 0, True
+        torch.cuda.set_device(0)
+        grid = max(8, 512 // world)
     dev = torch.device("cuda", local)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     es = 2 if dtype == torch.bfloat16 else 4
@@ -120,7 +128,7 @@ def main() -> None:
     # losing the run
     comm, reason, err = None, "", float("nan")
     try:
-        comm = XgmiCommunicator(slot_bytes=slot)
+        comm = XgmiCommunicator(slot_bytes=slot, grid=grid)
         log(rank, f"{comm}  tensor={args.size_mib} MiB {args.dtype}")
         ok, err = validate(comm, n, dtype, dev, rank, world)
         ok_small, err_small = validate(comm, 12345, dtype, dev, rank, world)
@@ -146,7 +154,7 @@ def main() -> None:
 
     sweep = None
     if engine_ok and not args.no_tune:
-        rccl_algos = () if args.no_rccl else ("rccl", "rsag", "p2p") if world > 1 else ("rccl",)
+        rccl_algos = () if args.no_rccl else ("rccl", "rsag") if world > 1 else ("rccl",)
         sweep = comm.tune(max_bytes=nbytes, dtype=dtype, iters=args.sweep_steps,
                           candidates=("oneshot", "twoshot", "ring") + rccl_algos, grids=(128, 256))
     if engine_ok and args.algo != "rccl":
@@ -193,7 +201,7 @@ def main() -> None:
             "model": f"flat {args.size_mib} MiB {args.dtype} gradient buffer (BASELINE config 3)",
             "global_batch": world,
             "seq_len": None,
-            "parallelism": f"dp{world}",
+            "parallelism": f"dp{world}" + (" (rehearsal: all ranks on one GPU)" if args.share_device else ""),
             "tensor_bytes": nbytes,
             "algo": chosen,
         },
