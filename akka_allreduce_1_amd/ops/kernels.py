@@ -16,14 +16,14 @@ import torch
 from .._native import C
 
 _H = C.hip
-_DT = {torch.float32: _H.DType.F32, torch.bfloat16: _H.DType.BF16}
+_DT = {torch.float32: _H.DType.F32, torch.bfloat16: _H.DType.BF16, torch.float16: _H.DType.F16}
 
 
 def dtype_code(dt: torch.dtype):
     try:
         return _DT[dt]
     except KeyError:
-        raise TypeError(f"unsupported dtype {dt}: the HIP data plane handles float32 and bfloat16") from None
+        raise TypeError(f"unsupported dtype {dt}: the HIP data plane handles float32, bfloat16 and float16") from None
 
 
 def _stream(t: torch.Tensor) -> int:

@@ -224,7 +224,7 @@ class XgmiCommunicator:
             raise ValueError(f"unsupported op {op!r}")
         if algo in ("p2p", "rsag"):  # the same protocol over RCCL point-to-point / RS+AG
             self.p2p.allreduce(inp, out, op=op, algo=algo)
-        elif algo == "rccl" or inp.dtype not in (torch.float32, torch.bfloat16):
+        elif algo == "rccl" or inp.dtype not in (torch.float32, torch.bfloat16, torch.float16):
             import torch.distributed as dist
 
             if out.data_ptr() != inp.data_ptr():

@@ -34,8 +34,8 @@ import torch.distributed as dist
 
 def reduce_rows(slots: torch.Tensor, out: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
     """out = scale * sum over the rows of `slots`, fp32 accumulation in row order, one
-    rounding. GPU float32/bfloat16 -> the HIP reduce_slots kernel; anything else -> torch."""
-    if slots.is_cuda and slots.dtype in (torch.float32, torch.bfloat16):
+    rounding. GPU float32/bfloat16/float16 -> the HIP reduce_slots kernel; anything else -> torch."""
+    if slots.is_cuda and slots.dtype in (torch.float32, torch.bfloat16, torch.float16):
         from ..ops import reduce_slots
 
         return reduce_slots(slots, out, scale=scale)
@@ -48,10 +48,12 @@ def reduce_rows(slots: torch.Tensor, out: torch.Tensor, scale: float = 1.0) -> t
     return out
 
 
-def block_bounds(m: int, world: int) -> list[tuple[int, int]]:
-    """Block j = [j*b, min((j+1)*b, m)) with b = ceil(m / P) (AllreduceWorker.scala:211-228),
-    trailing blocks empty instead of the reference's short range table."""
+def block_bounds(m: int, world: int, align: int = 1) -> list[tuple[int, int]]:
+    """Block j = [j*b, min((j+1)*b, m)) with b = ceil(m / P) (AllreduceWorker.scala:211-228)
+    rounded up to a multiple of `align` elements, trailing blocks empty instead of the
+    reference's short range table."""
     b = -(-m // world)
+    b = -(-b // align) * align
     return [(min(j * b, m), min((j + 1) * b, m)) for j in range(world)]
 
 
@@ -123,7 +125,8 @@ class P2PCommunicator:
 
     def _segment_p2p(self, x: torch.Tensor, y: torch.Tensor, scale: float) -> None:
         P, r = self.world, self.rank
-        bounds = block_bounds(x.numel(), P)
+        # GPU: 16-B aligned blocks, so the reduce kernel can write the output block in place
+        bounds = block_bounds(x.numel(), P, 16 // x.element_size() if x.is_cuda else 1)
         lo, hi = bounds[r]
         blen = hi - lo
         order = [(r + 1 + i) % P for i in range(P - 1)]  # rotated fan-out, AllreduceWorker.scala:197
@@ -141,7 +144,12 @@ class P2PCommunicator:
         # stride for the kernel, and an in-place call overwrites the input block)
         if blen > 0:
             slots[r, :blen].copy_(x[lo:hi])
-            reduce_rows(slots[:, :blen], y[lo:hi], scale)
+            dst = y[lo:hi]
+            if dst.is_cuda and dst.data_ptr() % 16:  # unaligned output tensor: reduce into the own row
+                reduce_rows(slots[:, :blen], slots[r, :blen], scale)
+                dst.copy_(slots[r, :blen])
+            else:
+                reduce_rows(slots[:, :blen], dst, scale)
         # 3. ReduceBlock broadcast: my reduced block to every peer, theirs into my output
         ops = []
         for j in order:

@@ -37,6 +37,21 @@ struct BF16 {
   static constexpr int ELEMS = 8;
   typedef uint16_t scalar;
 };
+struct F16 {
+  static constexpr int ELEMS = 8;
+  typedef uint16_t scalar;
+};
+
+// Host-side dtype dispatch: f(F32{}) / f(BF16{}) / f(F16{}) for DType codes 0 / 1 / 2.
+template <class Fn>
+inline void dispatch_dtype(int code, Fn&& f) {
+  if (code == 0)
+    f(F32{});
+  else if (code == 1)
+    f(BF16{});
+  else
+    f(F16{});
+}
 
 __device__ __forceinline__ float bf16_to_f32(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
 
@@ -46,6 +61,19 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   f2 v = {lo, hi};
   bf2 r = __builtin_convertvector(v, bf2);
+  return __builtin_bit_cast(uint32_t, r);
+}
+
+__device__ __forceinline__ float f16_to_f32(uint32_t bits16) {
+  return static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(bits16)));
+}
+
+__device__ __forceinline__ uint32_t pack_f16x2(float lo, float hi) {
+  // v_cvt_pk_f16_f32 family: RNE, overflow -> inf (IEEE half)
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 v = {lo, hi};
+  h2 r = __builtin_convertvector(v, h2);
   return __builtin_bit_cast(uint32_t, r);
 }
 
@@ -101,6 +129,32 @@ struct Acc<BF16> {
   }
 };
 
+template <>
+struct Acc<F16> {
+  float v[8];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.f;
+  }
+  __device__ __forceinline__ void add(const Pack16& p) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] += f16_to_f32(p[i] & 0xFFFFu);
+      v[2 * i + 1] += f16_to_f32(p[i] >> 16);
+    }
+  }
+  __device__ __forceinline__ void scale(float s) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] *= s;
+  }
+  __device__ __forceinline__ Pack16 pack() const {
+    Pack16 p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) p[i] = pack_f16x2(v[2 * i], v[2 * i + 1]);
+    return p;
+  }
+};
+
 // Scalar element access for ragged tails (< one pack).
 template <typename E>
 struct Scalar;
@@ -119,6 +173,19 @@ struct Scalar<BF16> {
   }
   __device__ __forceinline__ static void store(void* p, int64_t i, float x) {
     static_cast<uint16_t*>(p)[i] = static_cast<uint16_t>(pack_bf16x2(x, 0.f) & 0xFFFFu);
+  }
+  __device__ __forceinline__ static void copy(void* d, const void* s, int64_t i) {
+    static_cast<uint16_t*>(d)[i] = static_cast<const uint16_t*>(s)[i];
+  }
+};
+
+template <>
+struct Scalar<F16> {
+  __device__ __forceinline__ static float load(const void* p, int64_t i) {
+    return f16_to_f32(static_cast<const uint16_t*>(p)[i]);
+  }
+  __device__ __forceinline__ static void store(void* p, int64_t i, float x) {
+    static_cast<uint16_t*>(p)[i] = static_cast<uint16_t>(pack_f16x2(x, 0.f) & 0xFFFFu);
   }
   __device__ __forceinline__ static void copy(void* d, const void* s, int64_t i) {
     static_cast<uint16_t*>(d)[i] = static_cast<const uint16_t*>(s)[i];
@@ -162,6 +229,11 @@ __device__ __forceinline__ void st_scalar_wt<BF16>(__amdgpu_buffer_rsrc_t r, int
   __builtin_amdgcn_raw_buffer_store_b16(static_cast<unsigned short>(pack_bf16x2(x, 0.f) & 0xFFFFu), r,
                                         static_cast<int>(i * 2), 0, kAuxWt);
 }
+template <>
+__device__ __forceinline__ void st_scalar_wt<F16>(__amdgpu_buffer_rsrc_t r, int64_t i, float x) {
+  __builtin_amdgcn_raw_buffer_store_b16(static_cast<unsigned short>(pack_f16x2(x, 0.f) & 0xFFFFu), r,
+                                        static_cast<int>(i * 2), 0, kAuxWt);
+}
 template <class E>
 __device__ __forceinline__ void copy_scalar_wt(__amdgpu_buffer_rsrc_t r, const void* src, int64_t i);
 template <>
@@ -170,6 +242,11 @@ __device__ __forceinline__ void copy_scalar_wt<F32>(__amdgpu_buffer_rsrc_t r, co
 }
 template <>
 __device__ __forceinline__ void copy_scalar_wt<BF16>(__amdgpu_buffer_rsrc_t r, const void* src, int64_t i) {
+  __builtin_amdgcn_raw_buffer_store_b16(static_cast<const uint16_t*>(src)[i], r, static_cast<int>(i * 2), 0, kAuxWt);
+}
+
+template <>
+__device__ __forceinline__ void copy_scalar_wt<F16>(__amdgpu_buffer_rsrc_t r, const void* src, int64_t i) {
   __builtin_amdgcn_raw_buffer_store_b16(static_cast<const uint16_t*>(src)[i], r, static_cast<int>(i * 2), 0, kAuxWt);
 }
 
@@ -182,6 +259,10 @@ __device__ __forceinline__ float ld_scalar_sc1<F32>(__amdgpu_buffer_rsrc_t r, in
 template <>
 __device__ __forceinline__ float ld_scalar_sc1<BF16>(__amdgpu_buffer_rsrc_t r, int64_t i) {
   return bf16_to_f32(__builtin_amdgcn_raw_buffer_load_b16(r, static_cast<int>(i * 2), 0, kAuxSc1));
+}
+template <>
+__device__ __forceinline__ float ld_scalar_sc1<F16>(__amdgpu_buffer_rsrc_t r, int64_t i) {
+  return f16_to_f32(__builtin_amdgcn_raw_buffer_load_b16(r, static_cast<int>(i * 2), 0, kAuxSc1));
 }
 
 // ---------------------------------------------------------------------------------

@@ -132,7 +132,7 @@ void bind_hip(py::module_& m) {
   h.def("device_plane", &make_device_plane, py::arg("device") = 0,
         "DataPlane whose slabs and payloads live in HBM of `device` (worker protocol on the GPU)");
 
-  py::enum_<DType>(h, "DType").value("F32", DType::F32).value("BF16", DType::BF16);
+  py::enum_<DType>(h, "DType").value("F32", DType::F32).value("BF16", DType::BF16).value("F16", DType::F16);
   py::enum_<Algo>(h, "Algo").value("Auto", Algo::Auto).value("TwoShot", Algo::TwoShot).value("OneShot", Algo::OneShot).value("Ring", Algo::Ring);
 
   py::class_<CommStats>(h, "CommStats")

@@ -174,10 +174,9 @@ void launch_reduce_slots(const void* slots, int64_t slot_stride_elems, int nslot
   const int v = g_reduce_variant < 0 ? 3 : g_reduce_variant;  // 3: measured fastest (profiles/reduce_kernel.md)
   const char* s = static_cast<const char*>(slots);
   char* o = static_cast<char*>(out);
-  if (dt == DType::F32)
-    launch_reduce_typed<F32>(v, nslots, s, slot_stride_elems * es, o, n, scale, stream);
-  else
-    launch_reduce_typed<BF16>(v, nslots, s, slot_stride_elems * es, o, n, scale, stream);
+  dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
+    launch_reduce_typed<decltype(tag)>(v, nslots, s, slot_stride_elems * es, o, n, scale, stream);
+  });
   hip_check(hipGetLastError(), "reduce_slots launch");
 }
 
@@ -191,10 +190,10 @@ __global__ __launch_bounds__(kThreads) void fill_iota_kernel(char* out, int64_t 
 void launch_fill_iota(void* dst, int64_t n, double offset, DType dt, hipStream_t stream) {
   if (n <= 0) return;
   const int g = grid_for(n);
-  if (dt == DType::F32)
-    hipLaunchKernelGGL(fill_iota_kernel<F32>, dim3(g), dim3(kThreads), 0, stream, static_cast<char*>(dst), n, offset);
-  else
-    hipLaunchKernelGGL(fill_iota_kernel<BF16>, dim3(g), dim3(kThreads), 0, stream, static_cast<char*>(dst), n, offset);
+  dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
+    hipLaunchKernelGGL(fill_iota_kernel<decltype(tag)>, dim3(g), dim3(kThreads), 0, stream, static_cast<char*>(dst), n,
+                       offset);
+  });
   hip_check(hipGetLastError(), "fill_iota launch");
 }
 
@@ -220,10 +219,10 @@ __global__ __launch_bounds__(kThreads) void fill_uniform_kernel(char* out, int64
 void launch_fill_uniform(void* dst, int64_t n, uint64_t seed, DType dt, hipStream_t stream) {
   if (n <= 0) return;
   const int g = grid_for(n);
-  if (dt == DType::F32)
-    hipLaunchKernelGGL(fill_uniform_kernel<F32>, dim3(g), dim3(kThreads), 0, stream, static_cast<char*>(dst), n, seed);
-  else
-    hipLaunchKernelGGL(fill_uniform_kernel<BF16>, dim3(g), dim3(kThreads), 0, stream, static_cast<char*>(dst), n, seed);
+  dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
+    hipLaunchKernelGGL(fill_uniform_kernel<decltype(tag)>, dim3(g), dim3(kThreads), 0, stream, static_cast<char*>(dst),
+                       n, seed);
+  });
   hip_check(hipGetLastError(), "fill_uniform launch");
 }
 
@@ -331,14 +330,11 @@ void launch_cast(const void* src, DType dt_in, void* dst, DType dt_out, int64_t 
   const int g = grid_for(n);
   const char* s = static_cast<const char*>(src);
   char* d = static_cast<char*>(dst);
-  if (dt_in == DType::F32 && dt_out == DType::BF16)
-    hipLaunchKernelGGL((cast_kernel<F32, BF16>), dim3(g), dim3(kThreads), 0, stream, s, d, n);
-  else if (dt_in == DType::BF16 && dt_out == DType::F32)
-    hipLaunchKernelGGL((cast_kernel<BF16, F32>), dim3(g), dim3(kThreads), 0, stream, s, d, n);
-  else if (dt_in == DType::F32)
-    hipLaunchKernelGGL((cast_kernel<F32, F32>), dim3(g), dim3(kThreads), 0, stream, s, d, n);
-  else
-    hipLaunchKernelGGL((cast_kernel<BF16, BF16>), dim3(g), dim3(kThreads), 0, stream, s, d, n);
+  dispatch_dtype(static_cast<int>(dt_in), [&](auto ti) {
+    dispatch_dtype(static_cast<int>(dt_out), [&](auto to) {
+      hipLaunchKernelGGL((cast_kernel<decltype(ti), decltype(to)>), dim3(g), dim3(kThreads), 0, stream, s, d, n);
+    });
+  });
   hip_check(hipGetLastError(), "cast launch");
 }
 
@@ -371,12 +367,10 @@ void launch_bucket_copy(const uint64_t* dev_table, int count, void* bucket, DTyp
   const int64_t avg_packs = std::max<int64_t>(1, total * static_cast<int64_t>(dtype_size(dt)) / 16 / count);
   const int gx = static_cast<int>(std::min<int64_t>(64, (avg_packs + kThreads - 1) / kThreads));
   dim3 g(std::max(gx, 1), count);
-  if (dt == DType::F32)
-    hipLaunchKernelGGL(bucket_copy_kernel<F32>, g, dim3(kThreads), 0, stream, dev_table, static_cast<char*>(bucket),
-                       pack ? 1 : 0);
-  else
-    hipLaunchKernelGGL(bucket_copy_kernel<BF16>, g, dim3(kThreads), 0, stream, dev_table, static_cast<char*>(bucket),
-                       pack ? 1 : 0);
+  dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
+    hipLaunchKernelGGL(bucket_copy_kernel<decltype(tag)>, g, dim3(kThreads), 0, stream, dev_table,
+                       static_cast<char*>(bucket), pack ? 1 : 0);
+  });
   hip_check(hipGetLastError(), "bucket_copy launch");
 }
 

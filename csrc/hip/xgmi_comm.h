@@ -29,7 +29,7 @@
 
 namespace mxar {
 
-enum class DType : int { F32 = 0, BF16 = 1 };
+enum class DType : int { F32 = 0, BF16 = 1, F16 = 2 };
 inline size_t dtype_size(DType d) { return d == DType::F32 ? 4 : 2; }
 
 enum class Algo : int { Auto = 0, TwoShot = 1, OneShot = 2, Ring = 3 };

@@ -496,10 +496,7 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   if (static_cast<int64_t>(a.nch) * a.sub > c0.maxch_ || a.block * es > c0.slot_bytes_ + 16)
     throw std::logic_error("XgmiComm: segment geometry exceeds slab");
   const dim3 grid(gx, ranks_here);
-  if (dt == DType::F32)
-    launch_typed<F32>(a, grid, stream, kind);
-  else
-    launch_typed<BF16>(a, grid, stream, kind);
+  dispatch_dtype(static_cast<int>(dt), [&](auto tag) { launch_typed<decltype(tag)>(a, grid, stream, kind); });
   hip_check(hipGetLastError(), "allreduce launch");
   for (XgmiComm* c : group) {
     ++c->stats_.launches;

@@ -291,10 +291,9 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
 }
 
 void launch_threshold(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {
-  if (dt == DType::F32)
-    hipLaunchKernelGGL(threshold_kernel<F32>, grid, dim3(kCommThreads), 0, s, a);
-  else
-    hipLaunchKernelGGL(threshold_kernel<BF16>, grid, dim3(kCommThreads), 0, s, a);
+  dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
+    hipLaunchKernelGGL(threshold_kernel<decltype(tag)>, grid, dim3(kCommThreads), 0, s, a);
+  });
 }
 
 }  // namespace mxar

@@ -42,7 +42,7 @@ def _diag(y, ref, xs, rank):
 
 
 @pytest.mark.parametrize("P", [1, 2, 3, 4])
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("algo", ["twoshot", "oneshot", "ring"])
 @pytest.mark.parametrize("n", [1, 7, 1000, 65536 + 3, 1 << 20])
 def test_local_cluster_allreduce(P, dtype, algo, n):
@@ -132,7 +132,7 @@ def test_multiprocess_ipc_allreduce(world):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("P", [1, 2, 4])
 def test_local_cluster_mean_fused(dtype, P):
     cl = LocalCluster(P, slot_bytes=1 << 20, grid=16)

@@ -10,7 +10,7 @@ from akka_allreduce_1_amd.ops.kernels import BucketTable  # noqa: E402
 DEV = torch.device("cuda", 0)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("P,n", [(1, 1000), (2, 4096), (3, 12345), (8, 1 << 20), (5, 7)])
 def test_reduce_slots_matches_fp32_reference(dtype, P, n):
     padded = torch.randn(P, (n + 7) // 8 * 8, device=DEV).to(dtype)  # 16-B aligned rows
@@ -22,8 +22,8 @@ def test_reduce_slots_matches_fp32_reference(dtype, P, n):
     torch.cuda.synchronize()
     if dtype == torch.float32:
         assert torch.equal(out, ref)
-    else:
-        assert torch.equal(out, ref.to(torch.bfloat16))
+    else:  # one rounding of the fp32 sum (RNE), like torch's conversion
+        assert torch.equal(out, ref.to(dtype))
 
 
 def test_reduce_slots_scale_and_tail():
@@ -34,7 +34,7 @@ def test_reduce_slots_scale_and_tail():
     assert torch.allclose(out, ref, atol=1e-6)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_fill_iota_is_reference_data_source(dtype):
     t = fill_iota(torch.empty(1000, dtype=dtype, device=DEV), offset=3)
     ref = (torch.arange(1000, device=DEV, dtype=torch.float64) + 3).to(dtype)
@@ -49,15 +49,18 @@ def test_fill_uniform_range_and_determinism():
     assert a.min() >= -1 and a.max() < 1 and abs(a.mean().item()) < 0.02
 
 
-def test_cast_roundtrip_matches_torch():
+@pytest.mark.parametrize("low", [torch.bfloat16, torch.float16])
+def test_cast_roundtrip_matches_torch(low):
     x = torch.randn(100_003, device=DEV)
-    y = cast(x, torch.bfloat16)
-    assert torch.equal(y, x.to(torch.bfloat16))
+    y = cast(x, low)
+    assert torch.equal(y, x.to(low))
     z = cast(y, torch.float32)
     assert torch.equal(z, y.float())
+    other = torch.float16 if low == torch.bfloat16 else torch.bfloat16
+    assert torch.equal(cast(y, other), y.float().to(other))
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_bucket_copy_pack_unpack(dtype):
     ts = [torch.randn(s, device=DEV).to(dtype) for s in (17, 4096, 3, 1000, 64)]
     offs, o = [], 0

@@ -12,7 +12,7 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("P,n", [(2, 1), (3, 1001), (8, 65543)])
 def test_reduce_rows_on_padded_staging_rows(dtype, P, n):
     from akka_allreduce_1_amd.ops import fill_uniform

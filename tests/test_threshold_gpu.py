@@ -42,7 +42,7 @@ def _blocks(n, P, nch, dtype):
 
 
 @pytest.mark.parametrize("P", [2, 4, 8])
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("max_lag", [0, 2])
 def test_threshold_one_is_exact(P, dtype, max_lag):
     cl = LocalCluster(P, slot_bytes=1 << 20, grid=64, timeout_s=10.0, max_lag=max_lag)
