@@ -59,7 +59,8 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
     const int64_t bstart = static_cast<int64_t>(j) * a.block;
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
-    if (len > 0) copy_to_slab<E>(a.base[j] + a.off_S + r * slot + cstart * es, in + (bstart + cstart) * es, len);
+    if (len > 0 && unit_in_bounds(a, cstart * es, len * es, c, err))
+      copy_to_slab<E>(a.base[j] + a.off_S + r * slot + cstart * es, in + (bstart + cstart) * es, len);
     publish_flags([&](int) { return f1(a, j, r, c); }, 1, epoch, rel);
   }
 
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
     const int64_t len = clamp_len(clamp_len(blen_own - cbeg, a.chunk) - qbeg, a.subchunk);
     wait_flags([&](int s) -> const uint32_t* { return s == r ? nullptr : f1(a, r, s, c); }, P, epoch, deadline, err,
                ERR_TIMEOUT_SCATTER, acq);
-    if (len > 0) {
+    if (len > 0 && unit_in_bounds(a, cstart * es, len * es, u, err)) {
       const char* own_in = in + (bstart_own + cstart) * es;
       const char* S = a.base[r] + a.off_S + cstart * es;
       char* own_out = out + (bstart_own + cstart) * es;
@@ -100,7 +101,8 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
     const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
     wait_flags([&](int q) -> const uint32_t* { return f2(a, r, j, c * a.sub + q); }, a.sub, epoch, deadline, err,
                ERR_TIMEOUT_REDUCE, acq);
-    if (len > 0) copy_from_slab<E>(out + (bstart + cstart) * es, a.base[r] + a.off_R + j * slot + cstart * es, len);
+    if (len > 0 && unit_in_bounds(a, cstart * es, len * es, c, err))
+      copy_from_slab<E>(out + (bstart + cstart) * es, a.base[r] + a.off_R + j * slot + cstart * es, len);
   }
   finish_launch(ctl, epoch);
 }
@@ -160,7 +162,8 @@ __global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
   for (int c = blockIdx.x; c < a.nch; c += G) {
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     const int64_t len = clamp_len(a.n - cstart, a.chunk);
-    if (len > 0) push_to_peers<E>(a, P, r, a.off_S + r * slot + cstart * es, in + cstart * es, len);
+    if (len > 0 && unit_in_bounds(a, cstart * es, len * es, c, err))
+      push_to_peers<E>(a, P, r, a.off_S + r * slot + cstart * es, in + cstart * es, len);
     publish_flags([&](int k) { return f1(a, k, r, c); }, P, epoch, rel);
   }
   for (int c = blockIdx.x; c < a.nch; c += G) {
@@ -168,7 +171,7 @@ __global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
     const int64_t len = clamp_len(a.n - cstart, a.chunk);
     wait_flags([&](int s) -> const uint32_t* { return f1(a, r, s, c); }, P, epoch, deadline, err, ERR_TIMEOUT_SCATTER,
                acq);
-    if (len > 0) {
+    if (len > 0 && unit_in_bounds(a, cstart * es, len * es, c, err)) {
       const RedSrc src{in + cstart * es, a.base[r] + a.off_S + cstart * es, slot, r};
       char* o = out + cstart * es;
       reduce_to<E, PT>(P, src, 1, 0, [&](int) -> char* { return o; }, len, a.scale, a.fence & 1);
@@ -243,6 +246,12 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     auto blen = [&](int b) { return clamp_len(clamp_len(a.n - static_cast<int64_t>(b) * a.block, a.block) - cstart, a.chunk); };
     auto at = [&](int b) { return (static_cast<int64_t>(b) * a.block + cstart) * es; };
+    // every slot access of this chunk is [cstart, cstart + chunk) of a row; flags index c
+    const bool inb = unit_in_bounds(a, cstart * es, clamp_len(a.block - cstart, a.chunk) * es, c, err);
+    if (!inb) {  // publish every flag this workgroup owes, move no data
+      publish_flags([&](int) { return f1(a, nxt, 0, c); }, 1, epoch, rel);
+      continue;
+    }
     // RS step 0: raw own block r
     {
       const int64_t len = blen(r);

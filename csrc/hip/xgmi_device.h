@@ -57,6 +57,18 @@ __device__ __forceinline__ int64_t clamp_len(int64_t avail, int64_t cap) {
   return avail <= 0 ? 0 : (avail < cap ? avail : cap);
 }
 
+// Device-side bounds guard of one work unit: the bytes [off, off + bytes) of
+// a slot and the flag index `flag` must lie inside the slab geometry. The host derives the
+// geometry so this never fires; if it does (a geometry bug), the unit moves no data, the
+// error word gets ERR_BAD_ARGS (CommError on the host) and the flags are still published,
+// so no peer hangs and nothing is written out of bounds. Wave-uniform scalar compares.
+__device__ __forceinline__ bool unit_in_bounds(const CommArgs& a, int64_t off, int64_t bytes, int64_t flag,
+                                               uint32_t* err) {
+  const bool ok = off >= 0 && bytes >= 0 && off + bytes <= a.slot_bytes && flag >= 0 && flag < a.maxch;
+  if (!ok && threadIdx.x == 0) __hip_atomic_fetch_or(err, ERR_BAD_ARGS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return ok;
+}
+
 // Push len elements from ordinary memory into a (peer's) slab with write-through stores,
 // 16 B per lane, 4 packs in flight per lane.
 template <class E>

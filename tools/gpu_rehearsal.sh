@@ -6,7 +6,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-for N in 2 4; do
+for N in ${REHEARSAL_NS:-2 4 8}; do
   timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 \
     --master-port $((29600 + N)) bench.py --gpus $N --steps 10 --warmup 3 --share-device ${BENCH_ARGS:-} \
     > gpurun_out/rehearsal_n$N.json 2> gpurun_out/rehearsal_n$N.err || { echo "rehearsal N=$N failed"; tail -30 gpurun_out/rehearsal_n$N.err; exit 1; }
