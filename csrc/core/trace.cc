@@ -96,6 +96,10 @@ TraceScope::TraceScope(const char* cat, std::string name, std::string args)
   Tracer& t = Tracer::get();
   on_ = t.enabled();
   rx_ = t.roctx();
+  begin();
+}
+
+void TraceScope::begin() {
   if (rx_) roctxRangePushA(name_.c_str());
   if (on_) t0_ = Tracer::now_ns();
 }

@@ -11,6 +11,8 @@
 #include <cstdint>
 #include <mutex>
 #include <string>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 namespace mxar {
@@ -51,14 +53,29 @@ class Tracer {
 };
 
 // RAII span: records a complete event (and a roctx range) when the tracer is on.
+// The lazy form takes a callable returning {name, args_json}; it is only invoked when the
+// tracer or roctx is on, so a hot path pays no string building while tracing is off.
 class TraceScope {
  public:
   TraceScope(const char* cat, std::string name, std::string args = "");
+  template <class Fn, class = std::enable_if_t<std::is_invocable_v<Fn>>>
+  TraceScope(const char* cat, Fn&& make) : cat_(cat) {
+    Tracer& t = Tracer::get();
+    on_ = t.enabled();
+    rx_ = t.roctx();
+    if (on_ || rx_) {
+      auto na = make();
+      name_ = std::move(na.first);
+      args_ = std::move(na.second);
+      begin();
+    }
+  }
   ~TraceScope();
   TraceScope(const TraceScope&) = delete;
   TraceScope& operator=(const TraceScope&) = delete;
 
  private:
+  void begin();
   const char* cat_;
   std::string name_, args_;
   uint64_t t0_ = 0;

@@ -212,7 +212,10 @@ bool WorkerCore::on_reduce(const ReduceBlock& r) {
 void WorkerCore::fetch(int round) {
   MXAR_LOG(INFO, "worker", "fetch " << round);
   round_t0_[round] = Tracer::now_ns();
-  TraceScope span("worker", "fetch r" + std::to_string(round), "{\"worker\":" + std::to_string(id_) + "}");
+  TraceScope span("worker", [&] {
+    return std::make_pair(std::string("fetch r" + std::to_string(round)),
+                          std::string("{\"worker\":" + std::to_string(id_) + "}"));
+  });
   AllReduceInput in = fx_->fetch(AllReduceInputRequest{round});
   if (payload_size(in.data) != static_cast<size_t>(params_.dataSize))
     throw ProtocolError("Input data size " + std::to_string(payload_size(in.data)) +
@@ -233,8 +236,10 @@ void WorkerCore::flush(int completedRound, int row) {
 
 // scatter (AllreduceWorker.scala:194-209)
 void WorkerCore::scatter() {
-  TraceScope span("worker", "scatter r" + std::to_string(maxScattered_ + 1),
-                  "{\"worker\":" + std::to_string(id_) + "}");
+  TraceScope span("worker", [&] {
+    return std::make_pair(std::string("scatter r" + std::to_string(maxScattered_ + 1)),
+                          std::string("{\"worker\":" + std::to_string(id_) + "}"));
+  });
   const int r = maxScattered_ + 1;
   const int C = params_.maxChunkSize;
   for (int i = 0; i < P_; ++i) {
@@ -285,8 +290,10 @@ std::pair<Payload, int> WorkerCore::reduce(int row, int chunkId) {
 // complete (AllreduceWorker.scala:253-268)
 void WorkerCore::complete(int completedRound, int row) {
   MXAR_LOG(DEBUG, "worker", "----Complete allreduce round " << completedRound);
-  TraceScope span("worker", "complete r" + std::to_string(completedRound),
-                  "{\"worker\":" + std::to_string(id_) + "}");
+  TraceScope span("worker", [&] {
+    return std::make_pair(std::string("complete r" + std::to_string(completedRound)),
+                          std::string("{\"worker\":" + std::to_string(id_) + "}"));
+  });
   if (auto it = round_t0_.find(completedRound); it != round_t0_.end()) {
     const double ms = (Tracer::now_ns() - it->second) / 1e6;
     if (lat_ms_.size() < 4096)

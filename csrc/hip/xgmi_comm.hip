@@ -542,9 +542,11 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
   const bool oneshot =
       algo == Algo::OneShot ? (n * es <= c0.slot_bytes_) : (algo == Algo::Auto && n * es <= c0.oneshot_max_);
   const Algo kind = oneshot ? Algo::OneShot : algo == Algo::Ring ? Algo::Ring : Algo::TwoShot;
-  TraceScope span("xgmi", std::string(oneshot ? "oneshot " : kind == Algo::Ring ? "ring " : "twoshot ") + std::to_string(n * es) + "B",
-                  "{\"rank\":" + std::to_string(c0.rank_) + ",\"ranks_in_launch\":" + std::to_string(group.size()) +
-                      "}");
+  TraceScope span("xgmi", [&] {
+    return std::make_pair(
+        std::string(oneshot ? "oneshot " : kind == Algo::Ring ? "ring " : "twoshot ") + std::to_string(n * es) + "B",
+        "{\"rank\":" + std::to_string(c0.rank_) + ",\"ranks_in_launch\":" + std::to_string(group.size()) + "}");
+  });
   const int64_t seg = oneshot ? c0.slot_bytes_ / es : c0.world_ * (c0.slot_bytes_ / es);
   std::vector<const char*> ip(group.size());
   std::vector<char*> op(group.size());
@@ -651,8 +653,11 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
     }
   for (int k = 0; k < W; ++k) a.base[k] = c0.peers_[k];
   hip_check(hipSetDevice(c0.device_), "hipSetDevice");
-  TraceScope span("xgmi", "threshold " + std::to_string(n * es) + "B",
-                  "{\"rank\":" + std::to_string(c0.rank_) + ",\"ranks_in_launch\":" + std::to_string(ranks_here) + "}");
+  TraceScope span("xgmi", [&] {
+    return std::make_pair("threshold " + std::to_string(n * es) + "B",
+                          "{\"rank\":" + std::to_string(c0.rank_) + ",\"ranks_in_launch\":" +
+                              std::to_string(ranks_here) + "}");
+  });
   launch_threshold(a, dim3(gx, ranks_here), stream, dt);
   hip_check(hipGetLastError(), "threshold launch");
   for (XgmiComm* c : group) {
