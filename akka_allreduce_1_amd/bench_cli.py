@@ -8,6 +8,7 @@ Per (size, algo): p50 and mean over `--iters` event-timed calls after `--warmup`
 slowest rank's numbers are reported (all-reduce MAX). algbw = bytes / p50, busbw =
 algbw * 2(P-1)/P (nccl-tests convention). Engines:
   twoshot / oneshot / ring  fused xGMI kernels (csrc/hip/xgmi_comm.hip)
+  ll                        low-latency one-shot, flags inside the data (csrc/hip/xgmi_ll.hip)
   threshold                 straggler-tolerant kernel at th = 1 (csrc/hip/xgmi_threshold.hip)
   rccl                      torch.distributed all_reduce on the nccl (= RCCL) backend
   torch                     torch.distributed all_reduce on whatever backend (gloo on CPU)
@@ -67,7 +68,7 @@ def _time(fn, iters: int, warmup: int, sync) -> tuple[float, float]:
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(prog="mxar-bench", description=__doc__, formatter_class=argparse.RawTextHelpFormatter)
     ap.add_argument("--sizes", nargs="+", default=["4K..256M"], help="sizes (4K 1M ...) or a range lo..hi (x4 steps)")
-    ap.add_argument("--algos", nargs="+", default=["oneshot", "twoshot", "ring", "rccl"])
+    ap.add_argument("--algos", nargs="+", default=["ll", "oneshot", "twoshot", "ring", "rccl"])
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
@@ -94,7 +95,8 @@ def main(argv: list[str] | None = None) -> int:
         for size in sizes:
             n = size // es
             for algo in args.algos:
-                if algo in ("rccl", "torch") or (algo == "oneshot" and size > cl.comms[0].slot_bytes):
+                if algo in ("rccl", "torch") or (algo == "oneshot" and size > cl.comms[0].slot_bytes) or (
+                        algo == "ll" and size > cl.comms[0].ll_max_bytes):
                     continue
                 if algo == "threshold":
                     def fn():
@@ -116,7 +118,7 @@ def main(argv: list[str] | None = None) -> int:
         on_gpu = args.backend == "nccl"
         dev = torch.device("cuda", local) if on_gpu else torch.device("cpu")
         comm = None
-        if on_gpu and any(a in ("oneshot", "twoshot", "ring", "threshold") for a in args.algos):
+        if on_gpu and any(a in ("ll", "oneshot", "twoshot", "ring", "threshold") for a in args.algos):
             from .parallel import XgmiCommunicator
 
             comm = XgmiCommunicator(slot_bytes=max(64 << 20, -(-max(sizes) // P) + (1 << 20)),
@@ -127,8 +129,9 @@ def main(argv: list[str] | None = None) -> int:
         for size in sizes:
             n = size // es
             for algo in args.algos:
-                if algo in ("oneshot", "twoshot", "ring"):
-                    if comm is None or (algo == "oneshot" and size > comm.slot_bytes):
+                if algo in ("ll", "oneshot", "twoshot", "ring"):
+                    if comm is None or (algo == "oneshot" and size > comm.slot_bytes) or (
+                            algo == "ll" and size > comm.native.ll_max_bytes):
                         continue
                     fn = lambda: comm.allreduce(x[:n], y[:n], algo=algo, op=args.op)  # noqa: E731
                 elif algo == "threshold":

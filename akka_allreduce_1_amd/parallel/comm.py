@@ -25,7 +25,8 @@ from .._native import C
 
 _H = C.hip
 
-ALGOS = {"auto": _H.Algo.Auto, "twoshot": _H.Algo.TwoShot, "oneshot": _H.Algo.OneShot, "ring": _H.Algo.Ring}
+ALGOS = {"auto": _H.Algo.Auto, "twoshot": _H.Algo.TwoShot, "oneshot": _H.Algo.OneShot, "ring": _H.Algo.Ring,
+         "ll": _H.Algo.LL}
 DEFAULT_SLOT_BYTES = int(os.environ.get("MXAR_SLOT_BYTES", 64 << 20))
 
 
@@ -187,6 +188,8 @@ class XgmiCommunicator:
                     labels += [f"{algo}@{g}" for g in extra]
             for algo in labels:
                 if algo == "oneshot" and (size > self.slot_bytes or size > (8 << 20)):
+                    continue
+                if algo == "ll" and size > self._c.ll_max_bytes:
                     continue
                 if algo == "rccl" and dist.get_backend(self.group) != "nccl":
                     continue

@@ -133,7 +133,7 @@ void bind_hip(py::module_& m) {
         "DataPlane whose slabs and payloads live in HBM of `device` (worker protocol on the GPU)");
 
   py::enum_<DType>(h, "DType").value("F32", DType::F32).value("BF16", DType::BF16).value("F16", DType::F16);
-  py::enum_<Algo>(h, "Algo").value("Auto", Algo::Auto).value("TwoShot", Algo::TwoShot).value("OneShot", Algo::OneShot).value("Ring", Algo::Ring);
+  py::enum_<Algo>(h, "Algo").value("Auto", Algo::Auto).value("TwoShot", Algo::TwoShot).value("OneShot", Algo::OneShot).value("Ring", Algo::Ring).value("LL", Algo::LL);
 
   py::class_<CommStats>(h, "CommStats")
       .def_readonly("calls", &CommStats::calls)
@@ -142,7 +142,8 @@ void bind_hip(py::module_& m) {
       .def_readonly("oneshot", &CommStats::oneshot)
       .def_readonly("twoshot", &CommStats::twoshot)
       .def_readonly("ring", &CommStats::ring)
-      .def_readonly("threshold", &CommStats::threshold);
+      .def_readonly("threshold", &CommStats::threshold)
+      .def_readonly("ll", &CommStats::ll);
 
   py::class_<XgmiComm>(h, "XgmiComm")
       .def(py::init<int, int, int, int64_t, int, double, int>(), py::arg("rank"), py::arg("world"), py::arg("device"),
@@ -228,6 +229,7 @@ void bind_hip(py::module_& m) {
       .def_property_readonly("device", &XgmiComm::device)
       .def_property("grid", &XgmiComm::grid, &XgmiComm::set_grid)
       .def_property("oneshot_max_bytes", &XgmiComm::oneshot_max_bytes, &XgmiComm::set_oneshot_max_bytes)
+      .def_property_readonly("ll_max_bytes", &XgmiComm::ll_max_bytes)
       .def_property_readonly("slot_bytes", &XgmiComm::slot_bytes)
       .def_property_readonly("slab_bytes", &XgmiComm::slab_bytes)
       .def_property_readonly("connected", &XgmiComm::connected)

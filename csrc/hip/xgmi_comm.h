@@ -32,13 +32,13 @@ namespace mxar {
 enum class DType : int { F32 = 0, BF16 = 1, F16 = 2 };
 inline size_t dtype_size(DType d) { return d == DType::F32 ? 4 : 2; }
 
-enum class Algo : int { Auto = 0, TwoShot = 1, OneShot = 2, Ring = 3 };
+enum class Algo : int { Auto = 0, TwoShot = 1, OneShot = 2, Ring = 3, LL = 4 };
 
 constexpr int kMaxRanks = 16;
 constexpr int kCommThreads = 256;
 
 struct CommStats {
-  uint64_t calls = 0, launches = 0, bytes = 0, oneshot = 0, twoshot = 0, ring = 0, threshold = 0;
+  uint64_t calls = 0, launches = 0, bytes = 0, oneshot = 0, twoshot = 0, ring = 0, threshold = 0, ll = 0;
 };
 
 class XgmiComm {
@@ -111,6 +111,9 @@ class XgmiComm {
   int64_t slot_bytes() const { return slot_bytes_; }
   int64_t oneshot_max_bytes() const { return oneshot_max_; }
   void set_oneshot_max_bytes(int64_t b) { oneshot_max_ = b; }
+  // Largest tensor (bytes) one low-latency launch carries (Algo::LL; larger ones run in
+  // segments). Fixed at construction: the LL slots are sized for it (MXAR_LL_MAX).
+  int64_t ll_max_bytes() const { return ll_max_; }
   void set_grid(int g);
   void set_timeout(double s) { timeout_s_ = s; }
   // bit0: system-scope release fence (buffer_wbl2 sc0 sc1) before each flag store,
@@ -141,6 +144,7 @@ class XgmiComm {
 
   int rank_, world_, device_, grid_, rows_;
   int64_t slot_bytes_, maxch_, off_S_, off_R_, off_B_, slab_bytes_;
+  int64_t ll_max_ = 0, ll_slot_ = 0, off_LL_ = 0;
   int delay_rank_ = -1;
   double delay_us_ = 0;
   int64_t oneshot_max_;

@@ -330,7 +330,14 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   off_S_ = round_up(flag_bytes, 64 * 1024);
   off_R_ = off_S_ + rows_ * world_ * slot_bytes_;
   off_B_ = 2 * rows_ * world_ * maxch_ * 4;
-  slab_bytes_ = off_R_ + rows_ * world_ * slot_bytes_;
+  // low-latency one-shot slots: [2 parities][P sources] x ll_slot (two 8-B LL words per
+  // 16-B store: ll_slot = 2 x payload)
+  ll_max_ = 512 * 1024;
+  if (const char* e = std::getenv("MXAR_LL_MAX")) ll_max_ = std::max<int64_t>(0, std::atoll(e));
+  ll_max_ = round_up(ll_max_, 16);
+  ll_slot_ = round_up(std::max<int64_t>(2 * ll_max_, 16), 64 * 1024);
+  off_LL_ = off_R_ + rows_ * world_ * slot_bytes_;
+  slab_bytes_ = off_LL_ + 2 * world_ * ll_slot_;
   oneshot_max_ = std::min<int64_t>(slot_bytes_, 256 * 1024);
   if (const char* e = std::getenv("MXAR_ONESHOT_MAX")) oneshot_max_ = std::min<int64_t>(slot_bytes_, std::atoll(e));
   if (grid_ <= 0) grid_ = default_grid(device);
@@ -347,6 +354,7 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   }
   // Flags start at 0 = "epoch 0 done"; the first launch uses epoch 1.
   hip_check(hipMemset(slab_, 0, off_S_), "hipMemset(flags)");
+  hip_check(hipMemset(slab_ + off_LL_, 0, 2 * world_ * ll_slot_), "hipMemset(ll)");  // epoch 0 never occurs
   hip_check(hipMalloc(reinterpret_cast<void**>(&ctl_), 256), "hipMalloc(ctl)");
   hip_check(hipMemset(ctl_, 0, 256), "hipMemset(ctl)");
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
@@ -472,7 +480,14 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   const int gmax = std::max(1, c0.grid_ / ranks_here);  // all workgroups of the launch stay resident
   int gx;
   a.sub = 1;
-  if (oneshot) {
+  a.off_LL = c0.off_LL_;
+  a.ll_slot = c0.ll_slot_;
+  if (kind == Algo::LL) {
+    const int64_t units = ceil_div(n * es, 8);
+    a.block = a.chunk = a.subchunk = n;
+    a.nch = 1;
+    gx = static_cast<int>(std::min<int64_t>(gmax, std::max<int64_t>(1, ceil_div(units, kCommThreads))));
+  } else if (oneshot) {
     a.block = n;
     a.chunk = std::max(min_chunk, round_up(ceil_div(n, gmax), elems));
     a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(n, a.chunk)));
@@ -502,14 +517,20 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   }
   a.fence = c0.fence_;
   a.scale = scale;
-  if (static_cast<int64_t>(a.nch) * a.sub > c0.maxch_ || a.block * es > c0.slot_bytes_ + 16)
+  if (kind != Algo::LL && (static_cast<int64_t>(a.nch) * a.sub > c0.maxch_ || a.block * es > c0.slot_bytes_ + 16))
     throw std::logic_error("XgmiComm: segment geometry exceeds slab");
   const dim3 grid(gx, ranks_here);
-  dispatch_dtype(static_cast<int>(dt), [&](auto tag) { launch_typed<decltype(tag)>(a, grid, stream, kind); });
+  if (kind == Algo::LL) {
+    if (2 * ceil_div(n * es, 8) * 8 > c0.ll_slot_) throw std::logic_error("XgmiComm: LL segment exceeds its slot");
+    launch_ll(a, grid, stream, dt);
+  } else {
+    dispatch_dtype(static_cast<int>(dt), [&](auto tag) { launch_typed<decltype(tag)>(a, grid, stream, kind); });
+  }
   hip_check(hipGetLastError(), "allreduce launch");
   for (XgmiComm* c : group) {
     ++c->stats_.launches;
-    ++(oneshot ? c->stats_.oneshot : kind == Algo::Ring ? c->stats_.ring : c->stats_.twoshot);
+    ++(kind == Algo::LL ? c->stats_.ll
+                        : oneshot ? c->stats_.oneshot : kind == Algo::Ring ? c->stats_.ring : c->stats_.twoshot);
   }
 }
 
@@ -539,15 +560,20 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
         launch_copy(ins[y], outs[y], n * es, stream);
     return;
   }
-  const bool oneshot =
-      algo == Algo::OneShot ? (n * es <= c0.slot_bytes_) : (algo == Algo::Auto && n * es <= c0.oneshot_max_);
-  const Algo kind = oneshot ? Algo::OneShot : algo == Algo::Ring ? Algo::Ring : Algo::TwoShot;
+  const bool ll = algo == Algo::LL && c0.ll_max_ >= 16;
+  const bool oneshot = !ll && (algo == Algo::OneShot ? (n * es <= c0.slot_bytes_)
+                                                     : (algo == Algo::Auto && n * es <= c0.oneshot_max_));
+  const Algo kind = ll ? Algo::LL : oneshot ? Algo::OneShot : algo == Algo::Ring ? Algo::Ring : Algo::TwoShot;
   TraceScope span("xgmi", [&] {
-    return std::make_pair(
-        std::string(oneshot ? "oneshot " : kind == Algo::Ring ? "ring " : "twoshot ") + std::to_string(n * es) + "B",
-        "{\"rank\":" + std::to_string(c0.rank_) + ",\"ranks_in_launch\":" + std::to_string(group.size()) + "}");
+    return std::make_pair(std::string(ll        ? "ll "
+                                      : oneshot ? "oneshot "
+                                      : kind == Algo::Ring ? "ring "
+                                                           : "twoshot ") +
+                              std::to_string(n * es) + "B",
+                          "{\"rank\":" + std::to_string(c0.rank_) + ",\"ranks_in_launch\":" +
+                              std::to_string(group.size()) + "}");
   });
-  const int64_t seg = oneshot ? c0.slot_bytes_ / es : c0.world_ * (c0.slot_bytes_ / es);
+  const int64_t seg = ll ? c0.ll_max_ / es : oneshot ? c0.slot_bytes_ / es : c0.world_ * (c0.slot_bytes_ / es);
   std::vector<const char*> ip(group.size());
   std::vector<char*> op(group.size());
   for (int64_t off = 0; off < n; off += seg) {

@@ -40,6 +40,8 @@ struct CommArgs {
   int64_t min_complete;  // reduced chunks that complete the round (thComplete)
   int32_t* counts;     // optional [P][nch] contributions per output chunk (0 = missing)
   int rescale;         // scale a chunk reduced from cnt contributions by P / cnt
+  // low-latency one-shot (xgmi_ll.hip): slots [parity][src] of ll_slot bytes at off_LL
+  int64_t off_LL, ll_slot;
   uint64_t delay;      // test knob: ticks rank `delay_rank` idles before phase 1
   int delay_rank;
 };
@@ -223,5 +225,7 @@ __device__ __forceinline__ uint32_t launch_epoch(const uint32_t* ctl) {
 
 // Host entry of the threshold kernel (xgmi_threshold.hip).
 void launch_threshold(const CommArgs& a, dim3 grid, hipStream_t s, DType dt);
+// Host entry of the low-latency one-shot (xgmi_ll.hip).
+void launch_ll(const CommArgs& a, dim3 grid, hipStream_t s, DType dt);
 
 }  // namespace mxar

@@ -43,7 +43,7 @@ def _diag(y, ref, xs, rank):
 
 @pytest.mark.parametrize("P", [1, 2, 3, 4])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("algo", ["twoshot", "oneshot", "ring"])
+@pytest.mark.parametrize("algo", ["twoshot", "oneshot", "ring", "ll"])
 @pytest.mark.parametrize("n", [1, 7, 1000, 65536 + 3, 1 << 20])
 def test_local_cluster_allreduce(P, dtype, algo, n):
     cl = LocalCluster(P, slot_bytes=4 << 20, grid=32, timeout_s=10.0)
@@ -70,11 +70,11 @@ def test_local_cluster_inplace_and_repeated_epochs():
             assert torch.allclose(y, ref, atol=1e-5)
 
 
-@pytest.mark.parametrize("algo", ["twoshot", "ring"])
+@pytest.mark.parametrize("algo", ["twoshot", "ring", "ll"])
 def test_local_cluster_segments_larger_than_slab(algo):
     P = 2
     cl = LocalCluster(P, slot_bytes=64 << 10, grid=8, timeout_s=10.0)
-    n = 100_000  # 400 KB fp32 > P * 64 KiB -> several launches
+    n = 100_000 if algo != "ll" else 300_000  # > P * 64 KiB (> ll_max_bytes for ll) -> several launches
     xs = [fill_uniform(torch.empty(n, device=DEV), seed=k) for k in range(P)]
     ys = cl.allreduce(xs, algo=algo)
     cl.check()
@@ -96,7 +96,8 @@ def _mp_worker(rank, world, port, results):
     try:
         comm = XgmiCommunicator(device=0, slot_bytes=2 << 20, grid=8, timeout_s=15.0)
         for dtype in (torch.float32, torch.bfloat16):
-            for n, algo in ((100_003, "twoshot"), (5_000, "oneshot"), (1 << 20, "auto")):
+            for n, algo in ((100_003, "twoshot"), (5_000, "oneshot"), (1 << 20, "auto"), (3_333, "ll"),
+                            (300_001, "ll")):
                 xs = [fill_uniform(torch.empty(n, dtype=dtype, device=DEV), seed=k) for k in range(world)]
                 y = comm.allreduce(xs[rank], algo=algo)
                 comm.check()
@@ -145,14 +146,14 @@ def test_local_cluster_mean_fused(dtype, P):
         assert (y.float() - ref).abs().max().item() <= (1e-6 if dtype == torch.float32 else 1e-2)
 
 
-@pytest.mark.parametrize("algo", ["oneshot", "twoshot", "ring"])
+@pytest.mark.parametrize("algo", ["oneshot", "twoshot", "ring", "ll"])
 @pytest.mark.parametrize("P", [2, 4])
 def test_inplace_no_input_overwrite_race(algo, P):
     """In-place: a rank's reduced output must never leak into what a peer receives as that
     rank's contribution (the input may only be overwritten after every push read it)."""
     cl = LocalCluster(P, slot_bytes=2 << 20, grid=64)
     for it in range(8):
-        n = 60_001 if algo == "oneshot" else 200_003
+        n = 60_001 if algo in ("oneshot", "ll") else 200_003
         xs = [fill_uniform(torch.empty(n, device=DEV), seed=1000 * it + k) for k in range(P)]
         ref = _ref(xs)
         cl.allreduce(xs, xs, algo=algo)
@@ -176,7 +177,7 @@ def test_stress_cluster_churn():
         dtype = rng.choice([torch.float32, torch.bfloat16])
         es = 4 if dtype == torch.float32 else 2
         n = rng.randint(1, (slot * P) // es)
-        algo = rng.choice(["auto", "twoshot", "oneshot"]) if n * es <= slot else "twoshot"
+        algo = rng.choice(["auto", "twoshot", "oneshot", "ll"]) if n * es <= slot else rng.choice(["twoshot", "ll"])
         cl = LocalCluster(P, slot_bytes=slot, grid=rng.choice([8, 32, 64]))
         xs = [fill_uniform(torch.empty(n, dtype=dtype, device=DEV), seed=rng.randint(0, 1 << 30)) for _ in range(P)]
         ref = _ref(xs)
@@ -219,7 +220,7 @@ def test_mxar_bench_local_cli(tmp_path):
     assert {(r["bytes"], r["algo"]) for r in rows} >= {(65536, "twoshot"), (65536, "ring"), (4 << 20, "twoshot")}
 
 
-@pytest.mark.parametrize("algo", ["oneshot", "twoshot", "ring"])
+@pytest.mark.parametrize("algo", ["oneshot", "twoshot", "ring", "ll"])
 def test_hipgraph_capture_and_replay(algo):
     """The allreduce launch is graph-safe: flags carry an epoch read from a device counter at
     run time, so one captured launch replays correctly many times (new data each replay)."""

@@ -32,6 +32,8 @@ def parse_size(s: str) -> int:
 def hbm_bytes(S: int, P: int, algo: str) -> float:
     if algo == "ring":  # per rank, blocks of S/P: RS hops read in (+ slab) and push, AG hops copy out + forward
         return P * (S / P) * (6 * (P - 2) + 8)
+    if algo == "ll":  # read in, write P-1 LL slots (2x), read P-1 LL slots (2x), write out
+        return P * (S + 4 * S * (P - 1) + S)
     if algo == "oneshot":
         return P * (S + S * P + S * P + S)  # read in, write P slots, read P slots, write out
     return P * (S + S * (P - 1) / P + S + S + 2 * S * (P - 1) / P)
@@ -79,7 +81,7 @@ def main() -> None:
             for t in xs:
                 ref += t.float()
             for algo in args.algos:
-                if algo == "oneshot" and S > slot:
+                if (algo == "oneshot" and S > slot) or (algo == "ll" and S > cl.comms[0].ll_max_bytes):
                     continue
                 for fence in args.fence:
                     for c in cl.comms:
