@@ -112,6 +112,7 @@ def main() -> None:
     ap.add_argument("--no-rccl", action="store_true", help="skip the RCCL comparison timing")
     ap.add_argument("--no-tune", action="store_true", help="skip the size sweep / algorithm tuner")
     ap.add_argument("--sweep-steps", type=int, default=10)
+    ap.add_argument("--no-threshold", action="store_true", help="skip the straggler-tolerant kernel timing")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal: every rank on cuda:0 over gloo (RCCL refuses two ranks on one GPU), "
                          "workgroup budget split between the ranks so all spinning workgroups stay resident")
@@ -135,9 +136,13 @@ def main() -> None:
     # ---- engine bring-up + validation; any failure degrades to RCCL (recorded) instead of
     # losing the run
     comm, reason, err = None, "", float("nan")
+    t_setup = time.perf_counter()
+    log(rank, f"bring-up: world={world} slot={slot >> 20} MiB")
     try:
-        comm = XgmiCommunicator(slot_bytes=slot, grid=grid)
-        log(rank, f"{comm}  tensor={args.size_mib} MiB {args.dtype}")
+        # max_lag=1: a lag ring for the straggler-tolerant kernel, timed after the headline
+        # (the lock-step kernels use slab row 0 only; the extra rows cost HBM, not time)
+        comm = XgmiCommunicator(slot_bytes=slot, grid=grid, max_lag=1 if world > 1 else None)
+        log(rank, f"{comm}  tensor={args.size_mib} MiB {args.dtype}  (setup {time.perf_counter() - t_setup:.1f} s)")
         ok, err = validate(comm, n, dtype, dev, rank, world)
         ok_small, err_small = validate(comm, 12345, dtype, dev, rank, world)
         if not (ok and ok_small):
@@ -238,6 +243,25 @@ def main() -> None:
                           "p50_ms": round(max_over_ranks(percentile(rper, 50), dev), 4),
                           "note": "copy + in-place dist.all_reduce (nccl backend = RCCL)"}
         result["speedup_vs_rccl"] = round(algbw / r_alg, 3)
+    if engine_ok and world > 1 and not args.no_threshold:
+        # the reference's round semantics (thReduce / thComplete / maxLag) on the same buffer,
+        # at th = 1 so every rank must still deliver: the cost of straggler tolerance itself
+        try:
+            def step_th():
+                comm.allreduce_threshold(x, y, th_reduce=1.0, th_complete=1.0)
+
+            for _ in range(args.warmup):
+                step_th()
+            thw = max_over_ranks(timed(step_th, args.steps, dev), dev) / args.steps * 1e3
+            comm.check()
+            ref = x.float()
+            dist.all_reduce(ref)
+            step_th()
+            terr = max_over_ranks((y.float() - ref).abs().max().item(), dev)
+            result["xgmi_threshold"] = {"algbw": round(nbytes / (thw / 1e3) / 1e9, 2), "ms_per_step": round(thw, 4),
+                                        "max_abs_err": terr, "th_reduce": 1.0, "th_complete": 1.0, "max_lag": 1}
+        except Exception as e:  # noqa: BLE001 - reported, never loses the headline
+            result["xgmi_threshold"] = {"error": repr(e)}
     if sweep is not None:
         result["sweep"] = sweep
 

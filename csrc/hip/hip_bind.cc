@@ -232,6 +232,7 @@ void bind_hip(py::module_& m) {
       .def_property_readonly("ll_max_bytes", &XgmiComm::ll_max_bytes)
       .def_property_readonly("slot_bytes", &XgmiComm::slot_bytes)
       .def_property_readonly("slab_bytes", &XgmiComm::slab_bytes)
+      .def_property_readonly("alloc_bytes", &XgmiComm::alloc_bytes)
       .def_property_readonly("connected", &XgmiComm::connected)
       .def_property_readonly("stats", &XgmiComm::stats)
       .def_property("fence", &XgmiComm::fence, &XgmiComm::set_fence)

@@ -128,6 +128,7 @@ class XgmiComm {
   const CommStats& stats() const { return stats_; }
   char* slab() const { return slab_; }
   int64_t slab_bytes() const { return slab_bytes_; }
+  int64_t alloc_bytes() const { return alloc_bytes_; }
   static int64_t min_chunk_bytes() { return 1024; }
 
  private:
@@ -145,6 +146,7 @@ class XgmiComm {
   int rank_, world_, device_, grid_, rows_;
   int64_t slot_bytes_, maxch_, off_S_, off_R_, off_B_, slab_bytes_;
   int64_t ll_max_ = 0, ll_slot_ = 0, off_LL_ = 0;
+  int64_t alloc_bytes_ = 0;  // slab_bytes_ padded around the IPC size bug (constructor)
   int delay_rank_ = -1;
   double delay_us_ = 0;
   int64_t oneshot_max_;

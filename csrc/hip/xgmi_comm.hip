@@ -338,6 +338,14 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   ll_slot_ = round_up(std::max<int64_t>(2 * ll_max_, 16), 64 * 1024);
   off_LL_ = off_R_ + rows_ * world_ * slot_bytes_;
   slab_bytes_ = off_LL_ + 2 * world_ * ll_slot_;
+  // Allocation size: on this ROCm stack hipIpcOpenMemHandle of an allocation whose size has
+  // bit 31 set (2-4 GiB, 6-8 GiB, ...) never returns in the importing process, while the
+  // sizes around it map and reduce correctly (measured with tools/ipc_size_probe.py: 1.97,
+  // 4.05, 4.33 GiB fine; 2.03-3.9 GiB hang). Such slabs are padded up to the next multiple of
+  // 4 GiB - at most 2 GiB of the 288 GB of HBM. MXAR_IPC_NO_PAD=1 disables it (probing).
+  alloc_bytes_ = slab_bytes_;
+  if ((alloc_bytes_ & (int64_t{1} << 31)) && !std::getenv("MXAR_IPC_NO_PAD"))
+    alloc_bytes_ = round_up(alloc_bytes_, int64_t{1} << 32);
   oneshot_max_ = std::min<int64_t>(slot_bytes_, 256 * 1024);
   if (const char* e = std::getenv("MXAR_ONESHOT_MAX")) oneshot_max_ = std::min<int64_t>(slot_bytes_, std::atoll(e));
   if (grid_ <= 0) grid_ = default_grid(device);
@@ -347,10 +355,10 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   const char* mem = std::getenv("MXAR_SLAB_MEM");
   const std::string kind = mem ? mem : "fine";
   if (kind == "coarse") {
-    hip_check(hipMalloc(reinterpret_cast<void**>(&slab_), slab_bytes_), "hipMalloc(slab)");
+    hip_check(hipMalloc(reinterpret_cast<void**>(&slab_), alloc_bytes_), "hipMalloc(slab)");
   } else {
     const unsigned flags = kind == "fine" ? hipDeviceMallocFinegrained : hipDeviceMallocUncached;
-    hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&slab_), slab_bytes_, flags), "hipExtMallocWithFlags(slab)");
+    hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&slab_), alloc_bytes_, flags), "hipExtMallocWithFlags(slab)");
   }
   // Flags start at 0 = "epoch 0 done"; the first launch uses epoch 1.
   hip_check(hipMemset(slab_, 0, off_S_), "hipMemset(flags)");
@@ -385,7 +393,10 @@ void XgmiComm::connect(const std::vector<std::string>& handles) {
     hipIpcMemHandle_t h;
     std::memcpy(&h, handles[k].data(), sizeof(h));
     void* p = nullptr;
+    static const bool dbg = std::getenv("MXAR_DEBUG_IPC") != nullptr;
+    if (dbg) std::fprintf(stderr, "[mxar ipc] rank %d opening rank %d\n", rank_, k);
     hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    if (dbg) std::fprintf(stderr, "[mxar ipc] rank %d opened rank %d at %p\n", rank_, k, p);
     peers_[k] = static_cast<char*>(p);
     ipc_opened_[k] = true;
   }

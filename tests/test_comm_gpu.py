@@ -133,6 +133,54 @@ def test_multiprocess_ipc_allreduce(world):
     assert not bad, bad
 
 
+def _big_slab_worker(rank, world, port, slot, results):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.parallel import XgmiCommunicator
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ok, msg = True, ""
+    try:
+        comm = XgmiCommunicator(device=0, slot_bytes=slot, grid=16, timeout_s=15.0)
+        alloc, slab = comm.native.alloc_bytes, comm.native.slab_bytes
+        if not (alloc >= slab and not (alloc >> 31) & 1):
+            ok, msg = False, f"allocation {alloc} keeps bit 31 (slab {slab})"
+        n = world * slot // 4  # fill every slot of the slab
+        xs = [fill_uniform(torch.empty(n, device=DEV), seed=k) for k in range(world)]
+        y = comm.allreduce(xs[rank], algo="twoshot")
+        comm.check()
+        err = (y - _ref(xs)).abs().max().item()
+        if err > 1e-5:
+            ok, msg = False, f"err {err}"
+    except Exception as e:  # noqa: BLE001
+        ok, msg = False, repr(e)
+    results.put((rank, ok, msg))
+    dist.destroy_process_group()
+
+
+def test_multiprocess_slab_in_ipc_size_hole():
+    """A 2.3 GiB slab (size bit 31 set) hangs hipIpcOpenMemHandle on this stack unless the
+    allocation is padded to 4 GiB: the communicator must connect and reduce correctly."""
+    from akka_allreduce_1_amd.parallel import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    slot = 600 << 20
+    procs = [ctx.Process(target=_big_slab_worker, args=(r, 2, port, slot, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    bad = [r for r in res if not r[1]]
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("P", [1, 2, 4])
 def test_local_cluster_mean_fused(dtype, P):
