@@ -302,6 +302,70 @@ class XgmiCommunicator:
                                     rescale)
         return (out, cnt) if counts else out
 
+    # ------------------------------------------------------------------ other collectives
+    def _coll_ok(self, inp: torch.Tensor, out: torch.Tensor, m: int) -> bool:
+        if inp.get_device() != self._dev or out.get_device() != self._dev:
+            raise ValueError(f"tensors must live on {self.device}")
+        if not (inp.is_contiguous() and out.is_contiguous()) or inp.dtype != out.dtype:
+            raise ValueError("inp/out must be contiguous with the same dtype")
+        return inp.dtype in _KERNEL_DTYPES and (m * inp.element_size()) % 16 == 0
+
+    def all_to_all(self, inp: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """inp / out: world equal blocks; block s of out on rank r = block r of inp on rank s.
+        One xGMI launch (csrc/hip/xgmi_coll.hip); RCCL when the block is not 16-B sized."""
+        if out is None:
+            out = torch.empty_like(inp)
+        if inp.numel() % self.world or out.numel() != inp.numel():
+            raise ValueError("all_to_all needs world equal blocks and out.numel() == inp.numel()")
+        m = inp.numel() // self.world
+        if self._coll_ok(inp, out, m):
+            self._c.collective(_H.Coll.AllToAll, inp.data_ptr(), out.data_ptr(), m, _KERNEL_DTYPES[inp.dtype],
+                               _current_stream(self._dev))
+        else:
+            import torch.distributed as dist
+
+            dist.all_to_all_single(out.view(-1), inp.reshape(-1), group=self.group)
+        return out
+
+    def all_gather(self, inp: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """out = concatenation over ranks of inp (world x inp.numel())."""
+        m = inp.numel()
+        if out is None:
+            out = torch.empty(self.world * m, dtype=inp.dtype, device=inp.device)
+        if out.numel() != self.world * m:
+            raise ValueError("all_gather output must hold world x inp.numel() elements")
+        if self._coll_ok(inp, out, m):
+            self._c.collective(_H.Coll.AllGather, inp.data_ptr(), out.data_ptr(), m, _KERNEL_DTYPES[inp.dtype],
+                               _current_stream(self._dev))
+        else:
+            import torch.distributed as dist
+
+            dist.all_gather_into_tensor(out.view(-1), inp.reshape(-1), group=self.group)
+        return out
+
+    def reduce_scatter(self, inp: torch.Tensor, out: torch.Tensor | None = None, *, op: str = "sum") -> torch.Tensor:
+        """out (inp.numel() / world elements) on rank r = sum (or mean) over ranks of block r
+        of inp; fp32 accumulation in rank order, one rounding."""
+        if op not in ("sum", "avg"):
+            raise ValueError(f"unsupported op {op!r}")
+        if inp.numel() % self.world:
+            raise ValueError("reduce_scatter needs world equal blocks")
+        m = inp.numel() // self.world
+        if out is None:
+            out = torch.empty(m, dtype=inp.dtype, device=inp.device)
+        if out.numel() != m:
+            raise ValueError("reduce_scatter output must hold inp.numel() / world elements")
+        if self._coll_ok(inp, out, m):
+            self._c.collective(_H.Coll.ReduceScatter, inp.data_ptr(), out.data_ptr(), m, _KERNEL_DTYPES[inp.dtype],
+                               _current_stream(self._dev), 1.0 / self.world if op == "avg" else 1.0)
+        else:
+            import torch.distributed as dist
+
+            dist.reduce_scatter_tensor(out.view(-1), inp.reshape(-1), group=self.group)
+            if op == "avg":
+                out.div_(self.world)
+        return out
+
     def barrier(self) -> None:
         self._c.barrier(torch.cuda.current_stream(self.device).cuda_stream)
 
@@ -403,6 +467,27 @@ class LocalCluster:
                                                   cnt.data_ptr(), 1.0 / self.world if op == "avg" else 1.0, rescale)
             counts.append(cnt)
         return outputs, counts[0] if len(counts) == 1 else counts
+
+    def collective(self, op: str, inputs: Sequence[torch.Tensor], outputs: Sequence[torch.Tensor] | None = None, *,
+                   scale: float = 1.0) -> list[torch.Tensor]:
+        """op: "all_to_all" (in/out [world*m]), "all_gather" (in [m], out [world*m]) or
+        "reduce_scatter" (in [world*m], out [m]) for every logical rank (xgmi_coll.hip)."""
+        kind = {"all_to_all": _H.Coll.AllToAll, "all_gather": _H.Coll.AllGather,
+                "reduce_scatter": _H.Coll.ReduceScatter}[op]
+        if len(inputs) != self.world:
+            raise ValueError("one input per logical rank")
+        n = inputs[0].numel()
+        m = n if op == "all_gather" else n // self.world
+        out_n = self.world * m if op != "reduce_scatter" else m
+        if outputs is None:
+            outputs = [torch.empty(out_n, dtype=x.dtype, device=x.device) for x in inputs]
+        code = _dtype_code(inputs[0].dtype)
+        for g in self.groups:
+            dev = self.devices[g[0]]
+            _H.XgmiComm.collective_local([self.comms[k] for k in g], kind, [inputs[k].data_ptr() for k in g],
+                                         [outputs[k].data_ptr() for k in g], m, code,
+                                         torch.cuda.current_stream(dev).cuda_stream, scale)
+        return list(outputs)
 
     def barrier(self) -> None:
         for g in self.groups:

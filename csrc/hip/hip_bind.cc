@@ -134,6 +134,10 @@ void bind_hip(py::module_& m) {
 
   py::enum_<DType>(h, "DType").value("F32", DType::F32).value("BF16", DType::BF16).value("F16", DType::F16);
   py::enum_<Algo>(h, "Algo").value("Auto", Algo::Auto).value("TwoShot", Algo::TwoShot).value("OneShot", Algo::OneShot).value("Ring", Algo::Ring).value("LL", Algo::LL);
+  py::enum_<Coll>(h, "Coll")
+      .value("AllToAll", Coll::AllToAll)
+      .value("AllGather", Coll::AllGather)
+      .value("ReduceScatter", Coll::ReduceScatter);
 
   py::class_<CommStats>(h, "CommStats")
       .def_readonly("calls", &CommStats::calls)
@@ -143,7 +147,8 @@ void bind_hip(py::module_& m) {
       .def_readonly("twoshot", &CommStats::twoshot)
       .def_readonly("ring", &CommStats::ring)
       .def_readonly("threshold", &CommStats::threshold)
-      .def_readonly("ll", &CommStats::ll);
+      .def_readonly("ll", &CommStats::ll)
+      .def_readonly("coll", &CommStats::coll);
 
   py::class_<XgmiComm>(h, "XgmiComm")
       .def(py::init<int, int, int, int64_t, int, double, int>(), py::arg("rank"), py::arg("world"), py::arg("device"),
@@ -215,6 +220,27 @@ void bind_hip(py::module_& m) {
           },
           py::arg("comms"), py::arg("inputs"), py::arg("outputs"), py::arg("n"), py::arg("dtype"),
           py::arg("stream") = 0, py::arg("algo") = Algo::Auto, py::arg("scale") = 1.0f)
+      .def(
+          "collective",
+          [](XgmiComm& c, Coll op, uintptr_t in, uintptr_t out, int64_t m, DType dt, uintptr_t stream, float scale) {
+            py::gil_scoped_release r;
+            c.collective(op, as_cptr(in), as_ptr(out), m, dt, as_stream(stream), scale);
+          },
+          py::arg("op"), py::arg("inp"), py::arg("out"), py::arg("m"), py::arg("dtype"), py::arg("stream") = 0,
+          py::arg("scale") = 1.0f)
+      .def_static(
+          "collective_local",
+          [](const std::vector<XgmiComm*>& comms, Coll op, const std::vector<uintptr_t>& ins,
+             const std::vector<uintptr_t>& outs, int64_t m, DType dt, uintptr_t stream, float scale) {
+            std::vector<const void*> i;
+            std::vector<void*> o;
+            for (auto p : ins) i.push_back(as_cptr(p));
+            for (auto p : outs) o.push_back(as_ptr(p));
+            py::gil_scoped_release r;
+            XgmiComm::collective_local(comms, op, i, o, m, dt, as_stream(stream), scale);
+          },
+          py::arg("comms"), py::arg("op"), py::arg("inputs"), py::arg("outputs"), py::arg("m"), py::arg("dtype"),
+          py::arg("stream") = 0, py::arg("scale") = 1.0f)
       .def_static(
           "barrier_local",
           [](const std::vector<XgmiComm*>& comms, uintptr_t stream) {

@@ -34,11 +34,14 @@ inline size_t dtype_size(DType d) { return d == DType::F32 ? 4 : 2; }
 
 enum class Algo : int { Auto = 0, TwoShot = 1, OneShot = 2, Ring = 3, LL = 4 };
 
+// The reference's two allreduce phases as collectives of their own (xgmi_coll.hip).
+enum class Coll : int { AllToAll = 0, AllGather = 1, ReduceScatter = 2 };
+
 constexpr int kMaxRanks = 16;
 constexpr int kCommThreads = 256;
 
 struct CommStats {
-  uint64_t calls = 0, launches = 0, bytes = 0, oneshot = 0, twoshot = 0, ring = 0, threshold = 0, ll = 0;
+  uint64_t calls = 0, launches = 0, bytes = 0, oneshot = 0, twoshot = 0, ring = 0, threshold = 0, ll = 0, coll = 0;
 };
 
 class XgmiComm {
@@ -92,6 +95,16 @@ class XgmiComm {
   // Device-side barrier over all ranks (enqueued on `stream`).
   void barrier(hipStream_t stream);
 
+  // Collectives on [P][m] buffers (m elements per block, m * dtype a multiple of 16 B):
+  //   AllToAll      in[P][m] -> out[P][m]   out_r[s] = in_s[r]
+  //   AllGather     in[m]    -> out[P][m]   out_r[s] = in_s
+  //   ReduceScatter in[P][m] -> out[m]      out_r = scale * sum_s in_s[r]
+  // in and out must not overlap. One launch per segment of slot_bytes per block.
+  void collective(Coll op, const void* in, void* out, int64_t m, DType dt, hipStream_t stream, float scale = 1.f);
+  static void collective_local(const std::vector<XgmiComm*>& comms, Coll op, const std::vector<const void*>& ins,
+                               const std::vector<void*>& outs, int64_t m, DType dt, hipStream_t stream,
+                               float scale = 1.f);
+
   // Single-process cluster: ONE launch on `stream` runs every rank of `comms` (all on
   // one device, consecutive ranks, connected with connect_local); blockIdx.y = rank.
   static void allreduce_local(const std::vector<XgmiComm*>& comms, const std::vector<const void*>& ins,
@@ -137,6 +150,8 @@ class XgmiComm {
   static void launch_segment(const std::vector<XgmiComm*>& group, const char* const* ins, char* const* outs,
                              int64_t n, DType dt, hipStream_t stream, Algo kind, float scale);
 
+  static void run_coll(const std::vector<XgmiComm*>& group, Coll op, const std::vector<const void*>& ins,
+                       const std::vector<void*>& outs, int64_t m, DType dt, hipStream_t stream, float scale);
   static void run_threshold(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
                             const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, float thr,
                             float thc, int32_t* counts, float scale, bool rescale);

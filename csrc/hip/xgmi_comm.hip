@@ -738,4 +738,101 @@ void XgmiComm::barrier_group(const std::vector<XgmiComm*>& group, hipStream_t st
 
 void XgmiComm::barrier(hipStream_t stream) { barrier_group({this}, stream); }
 
+void XgmiComm::run_coll(const std::vector<XgmiComm*>& group, Coll op, const std::vector<const void*>& ins,
+                        const std::vector<void*>& outs, int64_t m, DType dt, hipStream_t stream, float scale) {
+  if (group.empty() || ins.size() != group.size() || outs.size() != group.size())
+    throw std::invalid_argument("XgmiComm: one input and one output per rank");
+  const XgmiComm& c0 = *group[0];
+  const int W = c0.world_;
+  const int64_t es = static_cast<int64_t>(dtype_size(dt));
+  const int64_t in_blocks = op == Coll::AllGather ? 1 : W, out_blocks = op == Coll::ReduceScatter ? 1 : W;
+  for (size_t y = 0; y < group.size(); ++y) {
+    const XgmiComm& c = *group[y];
+    if (!c.connected_) throw std::runtime_error("XgmiComm: connect() first");
+    if (c.device_ != c0.device_ || c.rank_ != c0.rank_ + static_cast<int>(y) || c.world_ != W)
+      throw std::invalid_argument("XgmiComm: a grouped launch needs consecutive ranks on one device");
+    const uintptr_t i0 = reinterpret_cast<uintptr_t>(ins[y]), o0 = reinterpret_cast<uintptr_t>(outs[y]);
+    if ((i0 | o0) & 15) throw std::invalid_argument("XgmiComm: buffers must be 16-byte aligned");
+    if (i0 < o0 + static_cast<uintptr_t>(out_blocks * m * es) && o0 < i0 + static_cast<uintptr_t>(in_blocks * m * es))
+      throw std::invalid_argument("XgmiComm: collective input and output must not overlap");
+  }
+  if ((m * es) & 15) throw std::invalid_argument("XgmiComm: block size (m x dtype) must be a multiple of 16 bytes");
+  if (m <= 0) return;
+  hip_check(hipSetDevice(c0.device_), "hipSetDevice");
+  for (XgmiComm* c : group) {
+    ++c->stats_.calls;
+    c->stats_.bytes += in_blocks * m * es;
+  }
+  if (W == 1) {  // one rank: a copy (scaled for reduce-scatter)
+    for (size_t y = 0; y < group.size(); ++y) {
+      if (op == Coll::ReduceScatter && scale != 1.f)
+        launch_reduce_slots(ins[y], m, 1, outs[y], m, dt, scale, stream);
+      else
+        launch_copy(ins[y], outs[y], m * es, stream);
+    }
+    return;
+  }
+  static const char* names[] = {"all_to_all ", "all_gather ", "reduce_scatter "};
+  TraceScope span("xgmi", [&] {
+    return std::make_pair(std::string(names[static_cast<int>(op)]) + std::to_string(in_blocks * m * es) + "B",
+                          "{\"rank\":" + std::to_string(c0.rank_) + ",\"ranks_in_launch\":" +
+                              std::to_string(group.size()) + "}");
+  });
+  const int ranks_here = static_cast<int>(group.size());
+  const int gmax = std::max(1, c0.grid_ / ranks_here);
+  const int64_t elems = 16 / es, min_chunk = min_chunk_bytes() / es;
+  const int64_t seg = c0.slot_bytes_ / es;  // per block per launch
+  for (int64_t off = 0; off < m; off += seg) {
+    const int64_t len = std::min(seg, m - off);
+    CommArgs a;
+    std::memset(&a, 0, sizeof(a));
+    for (size_t y = 0; y < group.size(); ++y) {
+      a.in[y] = static_cast<const char*>(ins[y]) + off * es;
+      a.out[y] = static_cast<char*>(outs[y]) + off * es;
+      a.ctl[y] = group[y]->ctl_;
+    }
+    a.n = len;
+    a.block = m;
+    a.P = W;
+    a.rows = c0.rows_;
+    a.rank0 = c0.rank_;
+    a.maxch = c0.maxch_;
+    a.off_S = c0.off_S_;
+    a.off_R = c0.off_R_;
+    a.slot_bytes = c0.slot_bytes_;
+    a.timeout = static_cast<uint64_t>(c0.timeout_s_ * 1e8);
+    a.fence = c0.fence_;
+    a.scale = scale;
+    for (int k = 0; k < W; ++k) a.base[k] = c0.peers_[k];
+    const int64_t target = std::max<int64_t>(1, gmax / (W - 1));
+    a.chunk = std::max(min_chunk, round_up(ceil_div(len, target), elems));
+    a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(len, a.chunk)));
+    a.subchunk = a.chunk;
+    a.sub = 1;
+    if (op == Coll::ReduceScatter) {  // reduce units = push units: split every chunk W-1 ways
+      const int64_t sub = std::max<int64_t>(1, std::min<int64_t>(W - 1, a.chunk / min_chunk));
+      a.subchunk = round_up(ceil_div(a.chunk, sub), elems);
+      a.sub = static_cast<int>(ceil_div(a.chunk, a.subchunk));
+    }
+    if (a.nch > c0.maxch_) throw std::logic_error("XgmiComm: collective geometry exceeds the flag table");
+    const int gx = static_cast<int>(std::min<int64_t>(gmax, std::max<int64_t>(1, (W - 1) * int64_t{a.nch})));
+    launch_coll(a, dim3(gx, ranks_here), stream, dt, static_cast<int>(op));
+    hip_check(hipGetLastError(), "collective launch");
+    for (XgmiComm* c : group) {
+      ++c->stats_.launches;
+      ++c->stats_.coll;
+    }
+  }
+}
+
+void XgmiComm::collective(Coll op, const void* in, void* out, int64_t m, DType dt, hipStream_t stream, float scale) {
+  run_coll({this}, op, {in}, {out}, m, dt, stream, scale);
+}
+
+void XgmiComm::collective_local(const std::vector<XgmiComm*>& comms, Coll op, const std::vector<const void*>& ins,
+                                const std::vector<void*>& outs, int64_t m, DType dt, hipStream_t stream,
+                                float scale) {
+  run_coll(comms, op, ins, outs, m, dt, stream, scale);
+}
+
 }  // namespace mxar

@@ -227,5 +227,7 @@ __device__ __forceinline__ uint32_t launch_epoch(const uint32_t* ctl) {
 void launch_threshold(const CommArgs& a, dim3 grid, hipStream_t s, DType dt);
 // Host entry of the low-latency one-shot (xgmi_ll.hip).
 void launch_ll(const CommArgs& a, dim3 grid, hipStream_t s, DType dt);
+// Host entry of all-to-all (mode 0) / all-gather (1) / reduce-scatter (2) (xgmi_coll.hip).
+void launch_coll(const CommArgs& a, dim3 grid, hipStream_t s, DType dt, int mode);
 
 }  // namespace mxar

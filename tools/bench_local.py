@@ -32,6 +32,13 @@ def parse_size(s: str) -> int:
 def hbm_bytes(S: int, P: int, algo: str) -> float:
     if algo == "ring":  # per rank, blocks of S/P: RS hops read in (+ slab) and push, AG hops copy out + forward
         return P * (S / P) * (6 * (P - 2) + 8)
+    if algo == "all_to_all":  # S = P blocks per rank: read in + write slab (P-1)/P + read slab + write out
+        return P * (2 * S + 2 * S * (P - 1) / P)
+    if algo == "reduce_scatter":
+        return P * (S + 2 * S * (P - 1) / P + S / P)
+    if algo == "all_gather":  # S = the gathered output per rank (input S/P)
+        m = S / P
+        return P * ((4 * P - 2) * m)
     if algo == "ll":  # read in, write P-1 LL slots (2x), read P-1 LL slots (2x), write out
         return P * (S + 4 * S * (P - 1) + S)
     if algo == "oneshot":
@@ -86,16 +93,27 @@ def main() -> None:
                 for fence in args.fence:
                     for c in cl.comms:
                         c.fence = fence
-                    cl.allreduce(xs, ys, algo=algo)
-                    cl.check()
-                    err = max((t.float() - ref).abs().max().item() for t in ys)
+                    if algo in ("all_to_all", "reduce_scatter", "all_gather"):
+                        ins = [t[:n // P].contiguous() for t in xs] if algo == "all_gather" else xs
+                        outs = [torch.empty(n // P if algo == "reduce_scatter" else n, dtype=dtype, device=dev)
+                                for _ in range(P)]
+
+                        def fn(ins=ins, outs=outs, algo=algo):
+                            cl.collective(algo, ins, outs)
+                        err = 0.0
+                    else:
+                        def fn(algo=algo):
+                            cl.allreduce(xs, ys, algo=algo)
+                        fn()
+                        cl.check()
+                        err = max((t.float() - ref).abs().max().item() for t in ys)
                     for _ in range(3):
-                        cl.allreduce(xs, ys, algo=algo)
+                        fn()
                     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                           for _ in range(args.iters)]
                     for a, b in ev:
                         a.record()
-                        cl.allreduce(xs, ys, algo=algo)
+                        fn()
                         b.record()
                     cl.check()
                     ts = [a.elapsed_time(b) for a, b in ev]
