@@ -13,7 +13,10 @@ the same local GPU across nodes (NIC). Each level runs the reference's two-shot 
 
 Intra-node traffic equals a flat allreduce's; inter-node traffic drops by `cols` against
 a flat ring across every rank. `col_comm` is anything with `allreduce_(t, op=...)`
-(default: torch.distributed all_reduce on the column group, i.e. RCCL or gloo).
+(default: torch.distributed all_reduce on the column group, i.e. RCCL or gloo). `row_comm`
+is anything with `reduce_scatter(inp, out)` / `all_gather(inp, out)` over the row group -
+an `XgmiCommunicator(group=h.row_group)` runs both row steps as single xGMI launches
+(csrc/hip/xgmi_coll.hip); default: torch.distributed on the row group.
 """
 from __future__ import annotations
 
@@ -35,7 +38,7 @@ class _GroupAllreduce:
 class HierarchicalCommunicator:
     """Allreduce over a rows x cols grid of ranks (rank = row * cols + col)."""
 
-    def __init__(self, cols: int, *, backend: str | None = None, col_comm=None):
+    def __init__(self, cols: int, *, backend: str | None = None, col_comm=None, row_comm=None):
         if not dist.is_initialized():
             raise RuntimeError("HierarchicalCommunicator needs torch.distributed")
         self.world = dist.get_world_size()
@@ -52,6 +55,7 @@ class HierarchicalCommunicator:
         self.row_group = row_groups[self.row]
         self.col_group = col_groups[self.col]
         self.col_comm = col_comm if col_comm is not None else _GroupAllreduce(self.col_group)
+        self.row_comm = row_comm
         self.stats = {"calls": 0, "row_bytes": 0, "col_bytes": 0}
 
     def allreduce(self, inp: torch.Tensor, out: torch.Tensor | None = None, *, op: str = "sum") -> torch.Tensor:
@@ -71,7 +75,9 @@ class HierarchicalCommunicator:
             src[:n].copy_(x)
         shard = torch.empty(b, dtype=x.dtype, device=x.device)
         # 1. intra-node reduce-scatter
-        if C > 1:
+        if C > 1 and self.row_comm is not None:
+            self.row_comm.reduce_scatter(src, shard)
+        elif C > 1:
             dist.reduce_scatter_tensor(shard, src, group=self.row_group)
         else:
             shard.copy_(src)
@@ -81,11 +87,13 @@ class HierarchicalCommunicator:
         if op == "avg":
             shard.div_(self.world)
         # 3. intra-node all-gather
+        gather = (self.row_comm.all_gather if self.row_comm is not None else
+                  lambda i, o: dist.all_gather_into_tensor(o, i, group=self.row_group))
         if C > 1 and n == C * b and y.data_ptr() != x.data_ptr():
-            dist.all_gather_into_tensor(y, shard, group=self.row_group)
+            gather(shard, y)
         elif C > 1:
             full = torch.empty(C * b, dtype=x.dtype, device=x.device)
-            dist.all_gather_into_tensor(full, shard, group=self.row_group)
+            gather(shard, full)
             y.copy_(full[:n])
         else:
             y.copy_(shard[:n])

@@ -128,3 +128,51 @@ def test_collectives_two_processes_ipc():
             p.kill()
     bad = [r for r in res if not r[1]]
     assert not bad, bad
+
+
+def _hier_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.parallel import HierarchicalCommunicator, XgmiCommunicator
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ok, msg = True, ""
+    try:
+        h = HierarchicalCommunicator(cols=2)
+        h.row_comm = XgmiCommunicator(h.row_group, device=0, slot_bytes=1 << 20, grid=16, timeout_s=15.0)
+        n = 2 * 40_000
+        xs = [fill_uniform(torch.empty(n, device=DEV), seed=900 + k) for k in range(world)]
+        y = h.allreduce(xs[rank], op="avg")
+        h.row_comm.check()
+        ref = sum(x for x in xs) / world
+        err = (y - ref).abs().max().item()
+        if err > 1e-5:
+            ok, msg = False, f"err {err}"
+        if h.row_comm.native.stats.coll < 2:
+            ok, msg = False, "row steps did not run on the xGMI kernels"
+    except Exception as e:  # noqa: BLE001
+        ok, msg = False, repr(e)
+    q.put((rank, ok, msg))
+    dist.destroy_process_group()
+
+
+def test_hierarchical_rows_on_xgmi_collectives():
+    """2 x 2 grid of processes: reduce-scatter / all-gather inside a row on the xGMI kernels,
+    the column allreduce on gloo."""
+    from akka_allreduce_1_amd.parallel import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_hier_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(4)]
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    bad = [r for r in res if not r[1]]
+    assert not bad, bad

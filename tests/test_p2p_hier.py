@@ -94,6 +94,18 @@ def _hier_worker(rank, world, port, cols, q):
             h2.col_comm = type("C", (), {"allreduce_": lambda self, t, op="sum": p.allreduce_(t, op=op)})()
         y = h2.allreduce(xs[rank])
         assert torch.allclose(y, _ref(xs), atol=1e-5)
+        # the row level through any reduce_scatter / all_gather provider (P2P-style object)
+        if cols > 1:
+            class RowComm:
+                def reduce_scatter(self, i, o):
+                    dist.reduce_scatter_tensor(o, i, group=h2.row_group)
+
+                def all_gather(self, i, o):
+                    dist.all_gather_into_tensor(o, i, group=h2.row_group)
+
+            h2.row_comm = RowComm()
+            y = h2.allreduce(xs[rank])
+            assert torch.allclose(y, _ref(xs), atol=1e-5)
         q.put((rank, True, ""))
     except Exception:  # noqa: BLE001
         import traceback
