@@ -262,6 +262,7 @@ void bind_hip(py::module_& m) {
       .def_property_readonly("connected", &XgmiComm::connected)
       .def_property_readonly("stats", &XgmiComm::stats)
       .def_property("fence", &XgmiComm::fence, &XgmiComm::set_fence)
+      .def_property("units_per_wg", &XgmiComm::units_per_wg, &XgmiComm::set_units_per_wg)
       .def("set_timeout", &XgmiComm::set_timeout);
 
   h.def(

@@ -350,6 +350,7 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   if (const char* e = std::getenv("MXAR_ONESHOT_MAX")) oneshot_max_ = std::min<int64_t>(slot_bytes_, std::atoll(e));
   if (grid_ <= 0) grid_ = default_grid(device);
   if (const char* f = std::getenv("MXAR_FENCE")) fence_ = std::atoi(f) & 3;
+  if (const char* u = std::getenv("MXAR_TWOSHOT_UNITS")) units_per_wg_ = std::max(1, std::atoi(u));
 
   hip_check(hipSetDevice(device_), "hipSetDevice");
   const char* mem = std::getenv("MXAR_SLAB_MEM");
@@ -516,7 +517,10 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
     // units are as large as the parallelism allows. The reduce phase splits each chunk
     // W-1 ways to keep the same unit count.
     a.block = round_up(ceil_div(n, W), elems);
-    const int64_t target = W > 1 ? std::max<int64_t>(1, gmax / (W - 1)) : gmax;
+    // units_per_wg_ > 1: finer chunks, so a chunk's reduce can start while other chunks
+    // are still in flight (more flag hand-offs, shorter pipeline fill / drain)
+    const int64_t target =
+        W > 1 ? std::max<int64_t>(1, int64_t{gmax} * c0.units_per_wg_ / (W - 1)) : int64_t{gmax} * c0.units_per_wg_;
     a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, target), elems));
     a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
     int64_t sub = std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(W - 1), a.chunk / min_chunk, 64,
