@@ -176,3 +176,78 @@ def test_hierarchical_rows_on_xgmi_collectives():
             p.kill()
     bad = [r for r in res if not r[1]]
     assert not bad, bad
+
+
+def _stress_worker(rank, world, port, q):
+    """The same random sequence of operations on every rank (shared seed): every allreduce
+    algorithm, the collectives and threshold rounds interleaved, random sizes and dtypes,
+    in place and out of place - every result checked against gloo on fp32 copies."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import random
+
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.parallel import XgmiCommunicator
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ok, msg = True, ""
+    try:
+        comm = XgmiCommunicator(device=0, slot_bytes=512 << 10, grid=16, timeout_s=15.0, max_lag=1)
+        rng = random.Random(1234)
+        for it in range(60):
+            op = rng.choice(["twoshot", "oneshot", "ll", "ring", "auto", "threshold", "a2a", "ag", "rs"])
+            dtype = rng.choice([torch.float32, torch.bfloat16, torch.float16])
+            el = 16 // torch.empty(0, dtype=dtype).element_size()
+            m = rng.choice([1, 3, 100, 4096, 50_000, 200_000]) * el
+            if op == "threshold":
+                m = min(m, (512 << 10) // 16)  # one launch: n * es <= world * slot
+            n = m * world if op in ("a2a", "rs") else m
+            x = fill_uniform(torch.empty(n, dtype=dtype, device=DEV), seed=it * 100 + rank)
+            xs = [fill_uniform(torch.empty(n, dtype=dtype, device=DEV), seed=it * 100 + k) for k in range(world)]
+            tol = 1e-5 if dtype == torch.float32 else 2e-2 * world
+            if op in ("twoshot", "oneshot", "ll", "ring", "auto", "threshold"):
+                inplace = rng.random() < 0.5
+                if op == "threshold":
+                    y = comm.allreduce_threshold(x, x if inplace else None)
+                else:
+                    y = comm.allreduce(x, x if inplace else None, algo=op)
+                ref = sum(t.float() for t in xs)
+            elif op == "a2a":
+                y = comm.all_to_all(x)
+                ref = torch.cat([xs[s][rank * m:(rank + 1) * m].float() for s in range(world)])
+                tol = 0
+            elif op == "ag":
+                y = comm.all_gather(x)
+                ref = torch.cat([t.float() for t in xs])
+                tol = 0
+            else:
+                y = comm.reduce_scatter(x)
+                ref = sum(t[rank * m:(rank + 1) * m].float() for t in xs)
+            comm.check()
+            err = (y.float() - ref).abs().max().item()
+            if err > tol:
+                ok, msg = False, f"it {it} {op} {dtype} m={m}: err {err}"
+                break
+    except Exception as e:  # noqa: BLE001
+        ok, msg = False, repr(e)
+    q.put((rank, ok, msg))
+    dist.destroy_process_group()
+
+
+def test_multiprocess_random_operation_stress():
+    from akka_allreduce_1_amd.parallel import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_stress_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=110) for _ in range(4)]
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    bad = [r for r in res if not r[1]]
+    assert not bad, bad
