@@ -3,3 +3,4 @@ from .comm import CommError, LocalCluster, XgmiCommunicator, free_port, init_dis
 from .ddp import BucketedGradReducer, TorchDistComm, bucket_sizes  # noqa: F401,E402
 from .hierarchical import HierarchicalCommunicator  # noqa: F401,E402
 from .p2p import P2PCommunicator, block_bounds, reduce_rows  # noqa: F401,E402
+from .zero import ShardedDataParallel  # noqa: F401,E402

@@ -43,6 +43,7 @@ class TorchDistComm:
 
         self.group = group
         self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
 
     def allreduce_(self, t: torch.Tensor, *, op: str = "sum", algo: str | None = None) -> torch.Tensor:
         import torch.distributed as dist
@@ -51,6 +52,20 @@ class TorchDistComm:
         if op == "avg":
             t.div_(self.world)
         return t
+
+    def reduce_scatter(self, inp: torch.Tensor, out: torch.Tensor, *, op: str = "sum") -> torch.Tensor:
+        import torch.distributed as dist
+
+        dist.reduce_scatter_tensor(out, inp, group=self.group)
+        if op == "avg":
+            out.div_(self.world)
+        return out
+
+    def all_gather(self, inp: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        import torch.distributed as dist
+
+        dist.all_gather_into_tensor(out, inp, group=self.group)
+        return out
 
 
 @dataclass

@@ -1,0 +1,165 @@
+"""Sharded data parallelism on the reference's two phases (ZeRO-2 style).
+
+An allreduce is a reduce-scatter followed by an all-gather (the reference's ScatterBlock +
+reduce, then ReduceBlock broadcast: AllreduceWorker.scala:194-251). Data-parallel training
+does not need the second half for gradients: after the reduce-scatter every rank owns the
+averaged gradient of 1/P of the parameters, so it can keep the optimizer state for that
+1/P only, update its parameter shard, and all-gather the updated parameters. Same bytes on
+the wire as an allreduce, 1/P of the optimizer memory and optimizer FLOPs per rank.
+
+`ShardedDataParallel(model, comm, optimizer_factory)`:
+
+* parameters are grouped into buckets of ~`bucket_bytes`; each bucket has ONE flat
+  parameter buffer and ONE flat gradient buffer, and every `param.data` / `param.grad` is a
+  view into them (sizes padded to a multiple of world x 16 B so shards stay aligned);
+* a post-accumulate-grad hook launches a bucket's reduce-scatter (mean) on a side stream as
+  soon as the bucket is complete - overlapped with the rest of backward;
+* `step()` joins the side stream, runs the optimizer on the local shard views (one flat
+  parameter per bucket: `optimizer_factory(list_of_shard_params)`), then all-gathers every
+  bucket's updated shard back into the full flat parameter buffer.
+
+`comm` needs `reduce_scatter(inp, out, op=)` and `all_gather(inp, out)` on the current stream:
+`XgmiCommunicator` (one xGMI launch each, csrc/hip/xgmi_coll.hip) or `TorchDistComm` (RCCL /
+gloo).
+"""
+from __future__ import annotations
+
+from typing import Callable, Iterable
+
+import torch
+
+_ALIGN_BYTES = 16
+
+
+class _Bucket:
+    def __init__(self, index: int, dtype: torch.dtype):
+        self.index = index
+        self.dtype = dtype
+        self.params: list[torch.nn.Parameter] = []
+        self.offsets: list[int] = []
+        self.numel = 0
+        self.flat_param: torch.Tensor | None = None
+        self.flat_grad: torch.Tensor | None = None
+        self.grad_shard: torch.Tensor | None = None
+        self.shard_param: torch.nn.Parameter | None = None
+        self.pending = 0
+        self.launched = False
+
+
+class ShardedDataParallel:
+    def __init__(self, module: torch.nn.Module | Iterable[torch.nn.Parameter], comm,
+                 optimizer_factory: Callable[[list[torch.nn.Parameter]], torch.optim.Optimizer], *,
+                 bucket_bytes: int = 64 << 20, overlap: bool = True):
+        params = module.parameters() if isinstance(module, torch.nn.Module) else module
+        self.params = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise ValueError("no trainable parameters")
+        self.comm = comm
+        self.world = int(getattr(comm, "world"))
+        self.rank = int(getattr(comm, "rank"))
+        self.device = self.params[0].device
+        self.on_gpu = self.device.type == "cuda"
+        self.overlap = overlap and self.on_gpu
+        self.stream = torch.cuda.Stream(device=self.device) if self.on_gpu else None
+        self.buckets = self._build(bucket_bytes)
+        self.slot_of = {id(p): (b, off) for b in self.buckets for p, off in zip(b.params, b.offsets)}
+        self.optimizer = optimizer_factory([b.shard_param for b in self.buckets])
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+        self._next = 0
+        self.stats = {"steps": 0, "reduce_scatter_bytes": 0, "all_gather_bytes": 0}
+
+    # ------------------------------------------------------------------ layout
+    def _build(self, bucket_bytes: int) -> list[_Bucket]:
+        buckets: list[_Bucket] = []
+        cur: dict[torch.dtype, _Bucket] = {}
+        for p in reversed(self.params):  # backward produces the last layers first
+            es = p.element_size()
+            align = max(1, _ALIGN_BYTES // es)
+            b = cur.get(p.dtype)
+            if b is not None and b.numel > 0 and (b.numel + p.numel()) * es > bucket_bytes:
+                b = None
+            if b is None:
+                b = _Bucket(len(buckets), p.dtype)
+                buckets.append(b)
+                cur[p.dtype] = b
+            off = (b.numel + align - 1) // align * align
+            b.params.append(p)
+            b.offsets.append(off)
+            b.numel = off + p.numel()
+        for b in buckets:
+            es = torch.empty(0, dtype=b.dtype).element_size()
+            unit = self.world * max(1, _ALIGN_BYTES // es)  # every shard 16-B sized and aligned
+            b.numel = (b.numel + unit - 1) // unit * unit
+            b.flat_param = torch.zeros(b.numel, dtype=b.dtype, device=self.device)
+            b.flat_grad = torch.zeros(b.numel, dtype=b.dtype, device=self.device)
+            for p, off in zip(b.params, b.offsets):
+                view = b.flat_param[off:off + p.numel()].view_as(p)
+                view.copy_(p.data)
+                p.data = view
+                p.grad = b.flat_grad[off:off + p.numel()].view_as(p)
+            s = b.numel // self.world
+            b.grad_shard = torch.zeros(s, dtype=b.dtype, device=self.device)
+            shard = torch.nn.Parameter(b.flat_param[self.rank * s:(self.rank + 1) * s], requires_grad=True)
+            shard.grad = b.grad_shard
+            b.shard_param = shard
+            b.pending = len(b.params)
+        return buckets
+
+    # ------------------------------------------------------------------ hooks
+    def _on_grad(self, p: torch.Tensor) -> None:
+        b, off = self.slot_of[id(p)]
+        expect = b.flat_grad.data_ptr() + off * b.flat_grad.element_size()
+        if p.grad is not None and p.grad.data_ptr() != expect:  # .grad was replaced: fold it back
+            view = b.flat_grad[off:off + p.numel()].view_as(p)
+            view.copy_(p.grad)
+            p.grad = view
+        b.pending -= 1
+        if b.pending == 0 and self.overlap:
+            self._launch_ready()
+
+    def _launch_ready(self, all_: bool = False) -> None:
+        while self._next < len(self.buckets) and (all_ or self.buckets[self._next].pending == 0):
+            self._reduce(self.buckets[self._next])
+            self._next += 1
+
+    def _reduce(self, b: _Bucket) -> None:
+        if self.on_gpu:
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.stream):
+                self.comm.reduce_scatter(b.flat_grad, b.grad_shard, op="avg")
+        else:
+            self.comm.reduce_scatter(b.flat_grad, b.grad_shard, op="avg")
+        b.launched = True
+        self.stats["reduce_scatter_bytes"] += b.flat_grad.numel() * b.flat_grad.element_size()
+
+    # ------------------------------------------------------------------ step API
+    def step(self) -> None:
+        """Finish the gradient reduce-scatter, update the local shards, all-gather the
+        parameters (call after backward)."""
+        self._launch_ready(all_=True)
+        if self.on_gpu:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        self.optimizer.step()
+        for b in self.buckets:
+            # the shard is part of the gather's output buffer: gather from a copy
+            src = b.shard_param.detach().clone()
+            self.comm.all_gather(src, b.flat_param)
+            self.stats["all_gather_bytes"] += b.flat_param.numel() * b.flat_param.element_size()
+        for b in self.buckets:
+            b.pending = len(b.params)
+            b.launched = False
+        self._next = 0
+        self.stats["steps"] += 1
+
+    def zero_grad(self) -> None:
+        for b in self.buckets:
+            b.flat_grad.zero_()
+
+    def remove_hooks(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+    def describe(self) -> list[dict]:
+        return [{"bucket": b.index, "dtype": str(b.dtype), "params": len(b.params), "numel": b.numel,
+                 "shard": b.numel // self.world} for b in self.buckets]

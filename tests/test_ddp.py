@@ -86,3 +86,66 @@ def test_reducer_gloo_world2():
         p.join(timeout=30)
     bad = [r for r in res if not r[1]]
     assert not bad, bad[0][2]
+
+
+def _zero_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.parallel import ShardedDataParallel
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        for opt_name in ("sgd", "adam"):
+            make = (lambda ps: torch.optim.SGD(ps, lr=0.05, momentum=0.9)) if opt_name == "sgd" else (
+                lambda ps: torch.optim.Adam(ps, lr=0.01))
+            m, ref = _model(0), _model(0)
+            zdp = ShardedDataParallel(m, TorchDistComm(), make, bucket_bytes=300)
+            assert len(zdp.buckets) > 1
+            ref_opt = make(list(ref.parameters()))
+            data = [torch.randn(4, 7, generator=torch.Generator().manual_seed(200 + r)) for r in range(world)]
+            for step in range(4):
+                zdp.zero_grad()
+                m(data[rank] * (step + 1)).pow(2).sum().backward()
+                zdp.step()
+                # reference: full optimizer on the averaged full gradient
+                ref_opt.zero_grad()
+                grads = []
+                for r in range(world):
+                    ref.zero_grad()
+                    ref(data[r] * (step + 1)).pow(2).sum().backward()
+                    grads.append([p.grad.clone() for p in ref.parameters()])
+                for i, p in enumerate(ref.parameters()):
+                    p.grad = sum(g[i] for g in grads) / world
+                ref_opt.step()
+                for p, rp in zip(m.parameters(), ref.parameters()):
+                    assert torch.allclose(p, rp, atol=1e-5), (opt_name, step)
+            # every rank holds optimizer state for its shard only
+            n_state = sum(t.numel() for st in zdp.optimizer.state.values() for t in st.values() if torch.is_tensor(t)
+                          and t.dim() > 0)
+            total = sum(b.numel for b in zdp.buckets)
+            assert n_state <= total * (2 if opt_name == "adam" else 1) // world
+            zdp.remove_hooks()
+        q.put((rank, True, ""))
+    except Exception:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, False, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_data_parallel_matches_full_optimizer_gloo():
+    from akka_allreduce_1_amd.parallel.comm import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_zero_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=30)
+    bad = [r for r in res if not r[1]]
+    assert not bad, bad[0][2]

@@ -78,3 +78,63 @@ def test_ddp_reducer_xgmi_two_processes(dtype, mode):
             p.kill()
     bad = [r for r in res if not r[1]]
     assert not bad, bad[0][2]
+
+
+def _zero_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.parallel import ShardedDataParallel, XgmiCommunicator
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = XgmiCommunicator(device=0, slot_bytes=1 << 20, grid=8, timeout_s=15.0)
+        make = lambda ps: torch.optim.Adam(ps, lr=1e-3)  # noqa: E731
+        m, ref = _model(0, torch.float32), _model(0, torch.float32)
+        zdp = ShardedDataParallel(m, comm, make, bucket_bytes=32 << 10)
+        ref_opt = make(list(ref.parameters()))
+        g = torch.Generator(device="cuda:0")
+        data = [torch.randn(16, 64, device="cuda:0", generator=g.manual_seed(30 + r)) for r in range(world)]
+        for step in range(3):
+            zdp.zero_grad()
+            m(data[rank]).pow(2).mean().backward()
+            zdp.step()
+            comm.check()
+            grads = []
+            for r in range(world):
+                ref.zero_grad()
+                ref(data[r]).pow(2).mean().backward()
+                grads.append([p.grad.clone() for p in ref.parameters()])
+            for i, p in enumerate(ref.parameters()):
+                p.grad = sum(gr[i] for gr in grads) / world
+            ref_opt.step()
+            for p, rp in zip(m.parameters(), ref.parameters()):
+                err = (p - rp).abs().max().item()
+                assert err <= 1e-5, (step, err)
+        assert comm.native.stats.coll >= 2 * 3 * len(zdp.buckets)  # RS + AG per bucket per step on xGMI
+        q.put((rank, True, ""))
+    except Exception:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, False, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_data_parallel_xgmi_two_processes():
+    from akka_allreduce_1_amd.parallel import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_zero_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    bad = [r for r in res if not r[1]]
+    assert not bad, bad[0][2]
