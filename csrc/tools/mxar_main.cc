@@ -1,0 +1,216 @@
+// mxar: native (Python-free) master / worker executables of the actor runtime - the
+// reference's AllreduceMaster.main (AllreduceMaster.scala:101-137) and AllreduceWorker.main
+// (AllreduceWorker.scala:272-301), same positional arguments and defaults, on the C++
+// actor system + TCP cluster layer (csrc/runtime, csrc/cluster).
+//
+//   mxar master [port totalWorkers dataSize maxChunkSize] [options]
+//       defaults 2551 2 totalWorkers*5 2; thAllreduce 1, thReduce 0.9, thComplete 0.8,
+//       maxLag 1, maxRound 100 (AllreduceMaster.scala:105-114). Exits once round maxRound
+//       completed (the reference idles forever).
+//   mxar worker [port sourceDataSize] [options]
+//       defaults 2553 10; data source data[i] = i + iteration (AllreduceWorker.scala:285-291);
+//       the sink logs every completed round; exits when the master leaves the cluster.
+//   options: --host H  --seeds addr[,addr]  --th-allreduce F --th-reduce F --th-complete F
+//            --max-lag N --max-round N --round-timeout-ms N --loglevel L --quiet
+//   seeds default to the reference's application.conf:14-16 (127.0.0.1:2551, :2552).
+#include <atomic>
+#include <chrono>
+#include <csignal>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../cluster/cluster_node.h"
+#include "../core/log.h"
+#include "../runtime/allreduce_actors.h"
+
+using namespace mxar;
+
+namespace {
+
+std::atomic<bool> g_stop{false};
+void on_signal(int) { g_stop = true; }
+
+// The node and the actor system were shut down explicitly; leave without running the
+// destructors of the objects still referenced from transport / actor state (the OS reclaims
+// sockets and memory), so a departed peer can never hold the exit.
+[[noreturn]] void exit_now(int rc) {
+  std::fflush(nullptr);
+  std::_Exit(rc);
+}
+
+struct Options {
+  std::vector<std::string> positional;
+  std::string host = "127.0.0.1";
+  std::vector<std::string> seeds;
+  float th_allreduce = 1.f, th_reduce = 0.9f, th_complete = 0.8f;  // AllreduceMaster.scala:105-107
+  int max_lag = 1, max_round = 100, round_timeout_ms = 0;          // :108-109
+  std::string loglevel = "INFO";
+  bool quiet = false;
+};
+
+[[noreturn]] void usage(const char* msg) {
+  std::fprintf(stderr,
+               "%s\nusage: mxar master [port totalWorkers dataSize maxChunkSize] [options]\n"
+               "       mxar worker [port sourceDataSize] [options]\n"
+               "options: --host H --seeds a[,b] --th-allreduce F --th-reduce F --th-complete F --max-lag N\n"
+               "         --max-round N --round-timeout-ms N --loglevel L --quiet\n",
+               msg);
+  std::exit(2);
+}
+
+Options parse(int argc, char** argv) {
+  Options o;
+  for (int i = 2; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto val = [&]() -> std::string {
+      if (i + 1 >= argc) usage(("missing value for " + a).c_str());
+      return argv[++i];
+    };
+    if (a == "--host") o.host = val();
+    else if (a == "--seeds") {
+      std::stringstream ss(val());
+      std::string s;
+      while (std::getline(ss, s, ',')) o.seeds.push_back(s);
+    } else if (a == "--th-allreduce") o.th_allreduce = std::stof(val());
+    else if (a == "--th-reduce") o.th_reduce = std::stof(val());
+    else if (a == "--th-complete") o.th_complete = std::stof(val());
+    else if (a == "--max-lag") o.max_lag = std::stoi(val());
+    else if (a == "--max-round") o.max_round = std::stoi(val());
+    else if (a == "--round-timeout-ms") o.round_timeout_ms = std::stoi(val());
+    else if (a == "--loglevel") o.loglevel = val();
+    else if (a == "--quiet") o.quiet = true;
+    else if (a.rfind("--", 0) == 0) usage(("unknown option " + a).c_str());
+    else o.positional.push_back(a);
+  }
+  if (o.seeds.empty())  // application.conf:14-16
+    o.seeds = {"mxar.tcp://ClusterSystem@127.0.0.1:2551", "mxar.tcp://ClusterSystem@127.0.0.1:2552"};
+  return o;
+}
+
+int pos_int(const Options& o, size_t k, int def) { return o.positional.size() > k ? std::stoi(o.positional[k]) : def; }
+
+void set_level(const std::string& l) {
+  static const char* names[] = {"TRACE", "DEBUG", "INFO", "WARNING", "ERROR", "OFF"};
+  for (int i = 0; i < 6; ++i)
+    if (l == names[i]) Logger::get().set_level(static_cast<LogLevel>(i));
+}
+
+[[noreturn]] void run_master(const Options& o) {
+  const int port = pos_int(o, 0, 2551);
+  const int total = pos_int(o, 1, 2);
+  const int data_size = pos_int(o, 2, total * 5);
+  const int chunk = pos_int(o, 3, 2);
+  MasterParams mp;
+  mp.totalWorkers = total;
+  mp.thAllreduce = o.th_allreduce;
+  mp.thReduce = o.th_reduce;
+  mp.thComplete = o.th_complete;
+  mp.maxLag = o.max_lag;
+  mp.dataSize = data_size;
+  mp.maxRound = o.max_round;
+  mp.maxChunkSize = chunk;
+  mp.roundTimeoutMs = o.round_timeout_ms;
+  auto sys = std::make_shared<ActorSystem>("ClusterSystem", ActorSystem::Mode::Threaded, 2);
+  std::atomic<int> finished{-1};
+  const auto t0 = std::chrono::steady_clock::now();
+  ActorRef master = sys->actor_of(std::make_unique<MasterActor>(mp, [&](int rounds) { finished = rounds; }), "master");
+  ClusterConfig cc;
+  cc.host = o.host;
+  cc.port = port;
+  cc.roles = {"master"};
+  cc.seed_nodes = o.seeds;
+  auto node = ClusterNode::start(sys, cc);
+  node->subscribe(master);
+  std::printf("[mxar master] %s totalWorkers=%d dataSize=%d maxChunkSize=%d th=(%.2f, %.2f, %.2f) maxLag=%d "
+              "maxRound=%d\n",
+              node->address().c_str(), total, data_size, chunk, o.th_allreduce, o.th_reduce, o.th_complete,
+              o.max_lag, o.max_round);
+  std::fflush(stdout);
+  while (!g_stop && finished.load() < 0) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (finished.load() >= 0)
+    std::printf("[mxar master] finished %d rounds in %.3f s\n", finished.load(), s);
+  std::fflush(stdout);
+  node->leave();
+  std::this_thread::sleep_for(std::chrono::milliseconds(200));  // let the Leave / Removed frames go out
+  node->shutdown();
+  sys->shutdown();
+  exit_now(finished.load() >= 0 ? 0 : 1);
+}
+
+[[noreturn]] void run_worker(const Options& o) {
+  const int port = pos_int(o, 0, 2553);
+  const int size = pos_int(o, 1, 10);
+  auto sys = std::make_shared<ActorSystem>("ClusterSystem", ActorSystem::Mode::Threaded, 2);
+  DataSource src = [size](const AllReduceInputRequest& r) {  // AllreduceWorker.scala:285-291
+    std::vector<float> v(size);
+    for (int i = 0; i < size; ++i) v[i] = static_cast<float>(i + r.iteration);
+    return AllReduceInput{make_host_payload(std::move(v))};
+  };
+  std::atomic<int> rounds{0};
+  const bool quiet = o.quiet;
+  DataSink sink = [&rounds, quiet](const AllReduceOutput& out) {  // AllreduceWorker.scala:295-297
+    const std::vector<float> d = out.data->to_host();
+    const double sum = std::accumulate(d.begin(), d.end(), 0.0);
+    rounds++;
+    if (!quiet) {
+      std::printf("[mxar worker] round %d sum %.1f head", out.iteration, sum);
+      for (size_t i = 0; i < d.size() && i < 6; ++i) std::printf(" %g", d[i]);
+      std::printf("\n");
+      std::fflush(stdout);
+    }
+  };
+  sys->actor_of(std::make_unique<WorkerActor>(src, sink), "worker");
+  ClusterConfig cc;
+  cc.host = o.host;
+  cc.port = port;
+  cc.roles = {"worker"};
+  cc.seed_nodes = o.seeds;
+  auto node = ClusterNode::start(sys, cc);
+  std::printf("[mxar worker] %s sourceDataSize=%d\n", node->address().c_str(), size);
+  std::fflush(stdout);
+  bool saw_master = false;
+  while (!g_stop) {
+    bool master_up = false;
+    for (const MemberInfo& m : node->members())
+      if (m.has_role("master") && m.status == MemberStatus::Up && !node->is_unreachable(m.address)) master_up = true;
+    // a short-lived master can join and leave between two polls: a completed round also
+    // proves it was there
+    if (master_up || rounds.load() > 0) saw_master = true;
+    if (saw_master && !master_up) break;  // the master left: the job is over
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  }
+  std::printf("[mxar worker] %d rounds completed\n", rounds.load());
+  std::fflush(stdout);
+  node->leave();
+  std::this_thread::sleep_for(std::chrono::milliseconds(100));  // let the Leave frame go out
+  node->shutdown();
+  sys->shutdown();
+  exit_now(0);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 2) usage("missing role");
+  std::signal(SIGINT, on_signal);
+  std::signal(SIGTERM, on_signal);
+  const std::string role = argv[1];
+  const Options o = parse(argc, argv);
+  set_level(o.loglevel);
+  try {
+    if (role == "master") run_master(o);
+    if (role == "worker") run_worker(o);
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "mxar %s: %s\n", role.c_str(), e.what());
+    exit_now(1);
+  }
+  usage(("unknown role " + role).c_str());
+}

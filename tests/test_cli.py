@@ -68,3 +68,37 @@ def test_mxar_bench_gloo_two_ranks(tmp_path):
     assert [x["bytes"] for x in rows] == [4096, 16384, 65536]
     for x in rows:
         assert x["P"] == 2 and x["p50_us"] > 0 and x["busbw_GBps"] == x["algbw_GBps"]
+
+
+def test_native_master_and_two_workers(tmp_path):
+    """The Python-free executables (csrc/tools/mxar_main.cc): the reference's deployment
+    (one master + 2 workers, positional args), exact sums at th = 1, every process exits."""
+    import socket
+    import subprocess
+
+    exe = os.path.join(ROOT, "akka_allreduce_1_amd", "mxar")
+    if not os.path.exists(exe):
+        pytest.skip("native executable not built (tools/build_native.py)")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    seed = f"mxar.tcp://ClusterSystem@127.0.0.1:{port}"
+    common = ["--seeds", seed, "--loglevel", "ERROR"]
+    master = subprocess.Popen([exe, "master", str(port), "2", "12", "2", "--th-reduce", "1", "--th-complete", "1",
+                               "--max-round", "15"] + common, stdout=subprocess.PIPE, text=True)
+    workers = [subprocess.Popen([exe, "worker", "0", "12"] + common, stdout=subprocess.PIPE, text=True)
+               for _ in range(2)]
+    try:
+        mout, _ = master.communicate(timeout=60)
+        wouts = [w.communicate(timeout=60)[0] for w in workers]
+    finally:
+        for p in [master] + workers:
+            if p.poll() is None:
+                p.kill()
+    assert master.returncode == 0 and "finished 16 rounds" in mout, mout
+    for out, w in zip(wouts, workers):
+        assert w.returncode == 0, out
+        sums = {int(line.split()[3]): float(line.split()[5]) for line in out.splitlines() if " sum " in line}
+        assert sorted(sums) == list(range(16)), out
+        for r, v in sums.items():  # data[i] = i + r on both workers: sum 2 * (66 + 12 r)
+            assert v == 2 * (66 + 12 * r), (r, v)

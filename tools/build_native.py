@@ -54,6 +54,11 @@ def output_path() -> Path:
     return PKG / ("_C" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
+def exe_path() -> Path:
+    """The native master/worker executable (csrc/tools/mxar_main.cc)."""
+    return PKG / "mxar"
+
+
 def _compile(src: Path, obj: Path, debug: bool, sanitize: str | None) -> tuple[Path, str]:
     opt = ["-O0", "-g"] if debug else ["-O3", "-DNDEBUG"]
     common = ["-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function"] + opt + _includes()
@@ -112,7 +117,30 @@ def build(jobs: int | None = None, clean: bool = False, debug: bool = False, san
             raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         if verbose:
             print(f"[build_native] linked {out.relative_to(ROOT)}", flush=True)
+    if not sanitize:
+        _build_exe(bdir, debug, verbose)
     return out
+
+
+def _build_exe(bdir: Path, debug: bool, verbose: bool) -> None:
+    """Link the Python-free `mxar` executable from the host runtime objects (core, runtime,
+    cluster) + csrc/tools/mxar_main.cc."""
+    main_src = CSRC / "tools" / "mxar_main.cc"
+    main_obj = bdir / "tools_mxar_main.cc.o"
+    if not main_obj.exists() or main_obj.stat().st_mtime < max(main_src.stat().st_mtime, _headers_mtime()):
+        _compile(main_src, main_obj, debug, None)
+    objs = [bdir / (p.parent.name + "_" + p.name + ".o") for sub in ("core", "runtime", "cluster")
+            for p in sorted((CSRC / sub).glob("*.cc"))] + [main_obj]
+    exe = exe_path()
+    if exe.exists() and exe.stat().st_mtime >= max(o.stat().st_mtime for o in objs):
+        return
+    cmd = [os.environ.get("CXX", "g++"), "-o", str(exe)] + [str(o) for o in objs]
+    cmd += [f"-L{ROCM / 'lib'}", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM / 'lib'}", "-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(f"[build_native] linked {exe.relative_to(ROOT)}", flush=True)
 
 
 def main() -> None:
