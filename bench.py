@@ -101,6 +101,40 @@ def validate(comm: XgmiCommunicator, n: int, dtype: torch.dtype, dev, rank: int,
     return flag.item() == 0, err
 
 
+def collectives(comm: XgmiCommunicator, x: torch.Tensor, world: int, args, dev) -> dict:
+    """ms per call of the xGMI all_to_all / all_gather / reduce_scatter vs RCCL on the bench
+    buffer (all_gather gathers 1/world of it per rank, so every op moves the same bytes)."""
+    n = x.numel()
+    m = n // world
+    a2a_out = torch.empty_like(x)
+    shard = x[:m].contiguous()
+    rs_out = torch.empty(m, dtype=x.dtype, device=dev)
+    ops = {
+        "all_to_all": (lambda: comm.all_to_all(x, a2a_out), lambda: dist.all_to_all_single(a2a_out, x)),
+        "all_gather": (lambda: comm.all_gather(shard, a2a_out), lambda: dist.all_gather_into_tensor(a2a_out, shard)),
+        "reduce_scatter": (lambda: comm.reduce_scatter(x, rs_out), lambda: dist.reduce_scatter_tensor(rs_out, x)),
+    }
+    out = {}
+    for name, (ours, rccl) in ops.items():
+        row = {}
+        try:
+            for label, fn in (("xgmi", ours), ("rccl", rccl)):
+                if label == "rccl" and args.no_rccl:
+                    continue
+                for _ in range(args.warmup):
+                    fn()
+                ms = max_over_ranks(timed(fn, args.steps, dev), dev) / args.steps * 1e3
+                row[f"{label}_ms"] = round(ms, 4)
+                row[f"{label}_algbw"] = round(x.numel() * x.element_size() / (ms / 1e3) / 1e9, 2)
+            comm.check()
+            if "rccl_ms" in row:
+                row["speedup_vs_rccl"] = round(row["rccl_ms"] / row["xgmi_ms"], 3)
+        except Exception as e:  # noqa: BLE001 - reported, never loses the headline
+            row["error"] = repr(e)
+        out[name] = row
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -113,6 +147,7 @@ def main() -> None:
     ap.add_argument("--no-tune", action="store_true", help="skip the size sweep / algorithm tuner")
     ap.add_argument("--sweep-steps", type=int, default=10)
     ap.add_argument("--no-threshold", action="store_true", help="skip the straggler-tolerant kernel timing")
+    ap.add_argument("--no-collectives", action="store_true", help="skip the all-to-all / all-gather / reduce-scatter timing")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal: every rank on cuda:0 over gloo (RCCL refuses two ranks on one GPU), "
                          "workgroup budget split between the ranks so all spinning workgroups stay resident")
@@ -262,6 +297,10 @@ def main() -> None:
                                         "max_abs_err": terr, "th_reduce": 1.0, "th_complete": 1.0, "max_lag": 1}
         except Exception as e:  # noqa: BLE001 - reported, never loses the headline
             result["xgmi_threshold"] = {"error": repr(e)}
+    if engine_ok and world > 1 and not args.no_collectives:
+        # the allreduce's two halves and the all-to-all as collectives of their own
+        # (csrc/hip/xgmi_coll.hip) on the same bytes, next to RCCL's equivalents
+        result["collectives"] = collectives(comm, x, world, args, dev)
     if sweep is not None:
         result["sweep"] = sweep
 
