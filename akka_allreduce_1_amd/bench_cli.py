@@ -9,6 +9,8 @@ slowest rank's numbers are reported (all-reduce MAX). algbw = bytes / p50, busbw
 algbw * 2(P-1)/P (nccl-tests convention). Engines:
   twoshot / oneshot / ring  fused xGMI kernels (csrc/hip/xgmi_comm.hip)
   ll                        low-latency one-shot, flags inside the data (csrc/hip/xgmi_ll.hip)
+  all_to_all / all_gather / reduce_scatter   xGMI collectives (csrc/hip/xgmi_coll.hip); SIZE =
+                            the full [world x m] buffer (all_gather: its output)
   threshold                 straggler-tolerant kernel at th = 1 (csrc/hip/xgmi_threshold.hip)
   rccl                      torch.distributed all_reduce on the nccl (= RCCL) backend
   torch                     torch.distributed all_reduce on whatever backend (gloo on CPU)
@@ -101,6 +103,15 @@ def main(argv: list[str] | None = None) -> int:
                 if algo == "threshold":
                     def fn():
                         cl.allreduce_threshold([x[:n] for x in xs], [y[:n] for y in ys])
+                elif algo in ("all_to_all", "all_gather", "reduce_scatter"):
+                    m = n // P // 8 * 8
+                    if m == 0:
+                        continue
+                    ins = [x[:m] for x in xs] if algo == "all_gather" else [x[:P * m] for x in xs]
+                    outs = [y[:m] for y in ys] if algo == "reduce_scatter" else [y[:P * m] for y in ys]
+
+                    def fn(algo=algo, ins=ins, outs=outs):
+                        cl.collective(algo, ins, outs)
                 else:
                     def fn():
                         cl.allreduce([x[:n] for x in xs], [y[:n] for y in ys], algo=algo, op=args.op)
@@ -118,7 +129,7 @@ def main(argv: list[str] | None = None) -> int:
         on_gpu = args.backend == "nccl"
         dev = torch.device("cuda", local) if on_gpu else torch.device("cpu")
         comm = None
-        if on_gpu and any(a in ("ll", "oneshot", "twoshot", "ring", "threshold") for a in args.algos):
+        if on_gpu and any(a in ("ll", "oneshot", "twoshot", "ring", "threshold") + ("all_to_all", "all_gather", "reduce_scatter") for a in args.algos):
             from .parallel import XgmiCommunicator
 
             comm = XgmiCommunicator(slot_bytes=max(64 << 20, -(-max(sizes) // P) + (1 << 20)),
@@ -138,6 +149,18 @@ def main(argv: list[str] | None = None) -> int:
                     if comm is None:
                         continue
                     fn = lambda: comm.allreduce_threshold(x[:n], y[:n])  # noqa: E731
+                elif algo in ("all_to_all", "all_gather", "reduce_scatter"):
+                    if comm is None:
+                        continue
+                    m = n // P // 8 * 8
+                    if m == 0:
+                        continue
+                    if algo == "all_gather":
+                        fn = lambda m=m: comm.all_gather(x[:m], y[:P * m])  # noqa: E731
+                    elif algo == "all_to_all":
+                        fn = lambda m=m: comm.all_to_all(x[:P * m], y[:P * m])  # noqa: E731
+                    else:
+                        fn = lambda m=m: comm.reduce_scatter(x[:P * m], y[:m])  # noqa: E731
                 elif algo in ("rccl", "torch"):
                     if algo == "rccl" and not on_gpu:
                         continue

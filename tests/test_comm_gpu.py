@@ -260,12 +260,14 @@ def test_mxar_bench_local_cli(tmp_path):
     from akka_allreduce_1_amd.bench_cli import main
 
     out = tmp_path / "rows.jsonl"
-    assert main(["--local", "4", "--algos", "twoshot", "ring", "oneshot", "--sizes", "64K", "4M", "--iters", "3",
-                 "--json", str(out)]) == 0
+    assert main(["--local", "4", "--algos", "twoshot", "ring", "oneshot", "ll", "all_to_all", "all_gather",
+                 "reduce_scatter", "--sizes", "64K", "4M", "--iters", "3", "--json", str(out)]) == 0
     import json
 
     rows = [json.loads(l) for l in out.read_text().splitlines()]
-    assert {(r["bytes"], r["algo"]) for r in rows} >= {(65536, "twoshot"), (65536, "ring"), (4 << 20, "twoshot")}
+    assert {(r["bytes"], r["algo"]) for r in rows} >= {(65536, "twoshot"), (65536, "ring"), (4 << 20, "twoshot"),
+                                                       (65536, "ll"), (4 << 20, "all_to_all"),
+                                                       (4 << 20, "reduce_scatter"), (65536, "all_gather")}
 
 
 @pytest.mark.parametrize("algo", ["oneshot", "twoshot", "ring", "ll"])
