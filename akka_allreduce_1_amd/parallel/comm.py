@@ -191,6 +191,8 @@ class XgmiCommunicator:
                     continue
                 if algo == "ll" and size > self._c.ll_max_bytes:
                     continue
+                if algo == "threshold" and not self._threshold_fits(x[:size // es]):
+                    continue
                 if algo == "rccl" and dist.get_backend(self.group) != "nccl":
                     continue
                 a, b = x[:n], y[:n]
@@ -253,6 +255,10 @@ class XgmiCommunicator:
                 self._grid = grid
             self._c.allreduce(inp.data_ptr(), out.data_ptr(), inp.numel(), code, _current_stream(self._dev), kind,
                               1.0 / self.world if op == "avg" else 1.0)
+        elif algo == "threshold" and self._threshold_fits(inp):
+            # the straggler-tolerant kernel at th = 1 is an exact allreduce with its own
+            # geometry (one chunk per workgroup, round-robin gather); a tune() candidate
+            self.allreduce_threshold(inp, out, op=op)
         elif algo in ("p2p", "rsag"):  # the same protocol over RCCL point-to-point / RS+AG
             self.p2p.allreduce(inp, out, op=op, algo=algo)
         elif algo == "rccl" or code is None:
@@ -265,6 +271,8 @@ class XgmiCommunicator:
                 out.div_(self.world)
         else:
             name, _, g = algo.partition("@")  # "twoshot@256": workgroup count chosen by tune()
+            if name == "threshold":  # no lag ring, or too large for one launch
+                return self.allreduce(inp, out, op=op, algo="twoshot")
             if name not in ALGOS:
                 raise ValueError(f"unknown algo {algo!r}")
             self._launch[algo] = (ALGOS[name], int(g) if g else self._default_grid)
@@ -273,6 +281,10 @@ class XgmiCommunicator:
 
     def allreduce_(self, t: torch.Tensor, *, op: str = "sum", algo: str = "auto") -> torch.Tensor:
         return self.allreduce(t, t, op=op, algo=algo)
+
+    def _threshold_fits(self, t: torch.Tensor) -> bool:
+        return (self.world > 1 and self._c.threshold_rows > 0 and t.dtype in _KERNEL_DTYPES
+                and t.numel() * t.element_size() <= self.world * self.slot_bytes)
 
     def allreduce_threshold(self, inp: torch.Tensor, out: torch.Tensor | None = None, *, th_reduce: float = 1.0,
                             th_complete: float = 1.0, counts: bool = False, op: str = "sum", rescale: bool = False):

@@ -142,7 +142,8 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--size-mib", type=int, default=256)
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
-    ap.add_argument("--algo", choices=["auto", "twoshot", "oneshot", "ll", "ring", "rccl", "rsag", "p2p"], default="auto")
+    ap.add_argument("--algo", choices=["auto", "twoshot", "oneshot", "ll", "ring", "threshold", "rccl", "rsag", "p2p"],
+                    default="auto")
     ap.add_argument("--no-rccl", action="store_true", help="skip the RCCL comparison timing")
     ap.add_argument("--no-tune", action="store_true", help="skip the size sweep / algorithm tuner")
     ap.add_argument("--sweep-steps", type=int, default=10)
@@ -204,7 +205,8 @@ def main() -> None:
     if engine_ok and not args.no_tune:
         rccl_algos = () if args.no_rccl else ("rccl", "rsag") if world > 1 else ("rccl",)
         sweep = comm.tune(max_bytes=nbytes, dtype=dtype, iters=args.sweep_steps,
-                          candidates=("ll", "oneshot", "twoshot", "ring") + rccl_algos, grids=(128, 256))
+                          candidates=("ll", "oneshot", "twoshot", "ring") + (("threshold",) if world > 1 else ())
+                          + rccl_algos, grids=(128, 256))
     if engine_ok and args.algo != "rccl":
         algo = args.algo
         chosen = comm._pick(nbytes) if algo == "auto" else algo

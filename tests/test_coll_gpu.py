@@ -195,8 +195,8 @@ def _stress_worker(rank, world, port, q):
     try:
         comm = XgmiCommunicator(device=0, slot_bytes=512 << 10, grid=16, timeout_s=15.0, max_lag=1)
         rng = random.Random(1234)
-        for it in range(60):
-            op = rng.choice(["twoshot", "oneshot", "ll", "ring", "auto", "threshold", "a2a", "ag", "rs"])
+        for it in range(120):
+            op = rng.choice(["twoshot", "oneshot", "ll", "ring", "auto", "threshold", "thr_algo", "a2a", "ag", "rs"])
             dtype = rng.choice([torch.float32, torch.bfloat16, torch.float16])
             el = 16 // torch.empty(0, dtype=dtype).element_size()
             m = rng.choice([1, 3, 100, 4096, 50_000, 200_000]) * el
@@ -206,9 +206,11 @@ def _stress_worker(rank, world, port, q):
             x = fill_uniform(torch.empty(n, dtype=dtype, device=DEV), seed=it * 100 + rank)
             xs = [fill_uniform(torch.empty(n, dtype=dtype, device=DEV), seed=it * 100 + k) for k in range(world)]
             tol = 1e-5 if dtype == torch.float32 else 2e-2 * world
-            if op in ("twoshot", "oneshot", "ll", "ring", "auto", "threshold"):
+            if op in ("twoshot", "oneshot", "ll", "ring", "auto", "threshold", "thr_algo"):
                 inplace = rng.random() < 0.5
-                if op == "threshold":
+                if op == "thr_algo":  # the threshold kernel as an exact allreduce algorithm (falls back if too big)
+                    y = comm.allreduce(x, x if inplace else None, algo="threshold")
+                elif op == "threshold":
                     y = comm.allreduce_threshold(x, x if inplace else None)
                 else:
                     y = comm.allreduce(x, x if inplace else None, algo=op)
