@@ -137,7 +137,7 @@ class XgmiComm {
   // no dirty lines and stays cheap. 2 exists only to measure the fence's cost.
   int fence() const { return fence_; }
   int units_per_wg() const { return units_per_wg_; }
-  void set_units_per_wg(int u) { units_per_wg_ = u > 0 ? u : 1; }
+  void set_units_per_wg(int u) { units_per_wg_ = u > 0 ? u : 0; }
   void set_fence(int f) { fence_ = f & 3; }
   bool connected() const { return connected_; }
   const CommStats& stats() const { return stats_; }
@@ -169,7 +169,8 @@ class XgmiComm {
   int64_t oneshot_max_;
   double timeout_s_;
   int fence_ = 3;
-  int units_per_wg_ = 1;  // two-shot scatter units per workgroup (chunk granularity)
+  int units_per_wg_ = 0;  // two-shot scatter units per workgroup; 0 = by block size (launch_segment)
+  int sub_max_ = 0;       // two-shot: most reduce pieces per chunk; 0 = by block size
   char* slab_ = nullptr;            // own uncached slab (flags | S | R)
   uint32_t* ctl_ = nullptr;         // [0] epoch, [1] ticket, [2] sticky error (device memory)
   char* peers_[kMaxRanks] = {};     // slab base of every rank (own included)

@@ -351,6 +351,7 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   if (grid_ <= 0) grid_ = default_grid(device);
   if (const char* f = std::getenv("MXAR_FENCE")) fence_ = std::atoi(f) & 3;
   if (const char* u = std::getenv("MXAR_TWOSHOT_UNITS")) units_per_wg_ = std::max(1, std::atoi(u));
+  if (const char* u = std::getenv("MXAR_TWOSHOT_SUB")) sub_max_ = std::max(1, std::atoi(u));
 
   hip_check(hipSetDevice(device_), "hipSetDevice");
   const char* mem = std::getenv("MXAR_SLAB_MEM");
@@ -517,14 +518,20 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
     // units are as large as the parallelism allows. The reduce phase splits each chunk
     // W-1 ways to keep the same unit count.
     a.block = round_up(ceil_div(n, W), elems);
-    // units_per_wg_ > 1: finer chunks, so a chunk's reduce can start while other chunks
-    // are still in flight (more flag hand-offs, shorter pipeline fill / drain)
-    const int64_t target =
-        W > 1 ? std::max<int64_t>(1, int64_t{gmax} * c0.units_per_wg_ / (W - 1)) : int64_t{gmax} * c0.units_per_wg_;
+    // Geometry by block size (measured, profiles/twoshot_granularity.md): small blocks want
+    // ~one scatter unit per workgroup (fewest flag hand-offs); large blocks (>= 32 MiB) want
+    // one chunk per workgroup (W-1 scatter units each) reduced in at most 2 pieces - chunks
+    // arrive in a finer stream, so reduces start earlier and the tail is shorter (4 / 8 ranks
+    // x 256 MiB: -6 % / -4 %; at 8-16 MiB blocks it loses 14-20 %). MXAR_TWOSHOT_UNITS /
+    // MXAR_TWOSHOT_SUB override.
+    const bool fine = a.block * es >= (int64_t{32} << 20);
+    const int upw = c0.units_per_wg_ > 0 ? c0.units_per_wg_ : fine ? std::max(1, W - 1) : 1;
+    const int sub_max = c0.sub_max_ > 0 ? c0.sub_max_ : fine ? 2 : 64;
+    const int64_t target = W > 1 ? std::max<int64_t>(1, int64_t{gmax} * upw / (W - 1)) : int64_t{gmax} * upw;
     a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, target), elems));
     a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
     int64_t sub = std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(W - 1), a.chunk / min_chunk, 64,
-                                                          c0.maxch_ / a.nch}));
+                                                          c0.maxch_ / a.nch, int64_t{sub_max}}));
     a.subchunk = round_up(ceil_div(a.chunk, sub), elems);
     a.sub = static_cast<int>(ceil_div(a.chunk, a.subchunk));
     const int64_t units = std::max<int64_t>((W - 1) * static_cast<int64_t>(a.nch), static_cast<int64_t>(a.nch) * a.sub);

@@ -295,3 +295,18 @@ def test_hipgraph_capture_and_replay(algo):
         ref = _ref(xs) / P
         for k in range(P):
             assert (ys[k] - ref).abs().max().item() <= 1e-6, f"replay {it} rank {k}"
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_local_cluster_large_blocks_fine_geometry(P):
+    """Blocks >= 32 MiB switch the two-shot to one chunk per workgroup, reduced in <= 2
+    pieces (launch_segment); odd sizes, in place, bf16."""
+    n = P * (20 << 20) + 12_345  # 40 MiB bf16 blocks
+    cl = LocalCluster(P, slot_bytes=48 << 20, grid=512, timeout_s=20.0)
+    xs = [fill_uniform(torch.empty(n, dtype=torch.bfloat16, device=DEV), seed=3000 + k) for k in range(P)]
+    ref = _ref(xs)
+    ys = cl.allreduce(xs, xs, algo="twoshot")  # in place
+    cl.check()
+    for k, y in enumerate(ys):
+        err = (y.float() - ref).abs().max().item()
+        assert err <= 1e-2 * P, (k, err)

@@ -1,11 +1,9 @@
 #!/bin/bash
-# two-shot chunk granularity study: MXAR_TWOSHOT_UNITS = scatter units per workgroup
+# two-shot geometry: automatic (by block size) vs the old fixed one-unit-per-workgroup geometry
 export HSA_ENABLE_IPC_MODE_LEGACY=0; mkdir -p gpurun_out
-for u in 1 2 4 8; do
-  MXAR_TWOSHOT_UNITS=$u timeout -k 10 120 python tools/bench_local.py --ranks 8 --sizes 16M 256M --algos twoshot --fence 3 > gpurun_out/units_local_$u.log 2>&1 || exit 1
-  echo "local u=$u: $(grep '"P"' gpurun_out/units_local_$u.log | python3 -c 'import sys,json; print([ (json.loads(l)["bytes"]>>20, json.loads(l)["p50_us"]) for l in sys.stdin])')"
-done
-for u in 1 4; do
-  MXAR_TWOSHOT_UNITS=$u timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port $((29650 + u)) bench.py --gpus 8 --steps 10 --warmup 3 --share-device --no-tune --no-threshold --algo twoshot > gpurun_out/units_reh_$u.json 2> gpurun_out/units_reh_$u.err || { tail -5 gpurun_out/units_reh_$u.err; exit 1; }
-  echo "rehearsal8 u=$u: $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/units_reh_$u.json | head -1)"
+for mode in auto fixed; do
+  if [ $mode = fixed ]; then export MXAR_TWOSHOT_UNITS=1 MXAR_TWOSHOT_SUB=64; fi
+  timeout -k 10 200 python -m akka_allreduce_1_amd bench --local 4 --algos twoshot threshold --sizes 16M 64M 256M --iters 10 > gpurun_out/geo4_$mode.txt 2>&1 || exit 1
+  timeout -k 10 200 python -m akka_allreduce_1_amd bench --local 8 --algos twoshot threshold --sizes 16M 64M 256M --iters 10 > gpurun_out/geo8_$mode.txt 2>&1 || exit 1
+  for P in 4 8; do echo "$mode P=$P: $(grep -E '^ +[0-9]+ +(twoshot|threshold)' gpurun_out/geo${P}_$mode.txt | awk '{printf "%s/%s=%sus ", $1/1048576, $2, $3}')"; done
 done
