@@ -90,11 +90,15 @@ class BucketedGradReducer:
     def __init__(self, params: Iterable[torch.nn.Parameter] | torch.nn.Module, comm, *,
                  bucket_bytes: int = 64 << 20, op: str = "avg", overlap: bool = True,
                  first_bucket_bytes: int | None = None, sync: str = "native", event_scope: int = 1,
-                 th_reduce: float = 1.0, th_complete: float = 1.0, rescale: bool = False):
+                 th_reduce: float = 1.0, th_complete: float = 1.0, rescale: bool = False, algo: str = "auto"):
         """sync: how the comm stream is ordered after backward's gradient writes -
         "native" = reusable HIP events created with `event_scope` (1: device-scope release,
         enough within one GPU; 0: HIP default system-scope), "torch" = torch.cuda events.
-        th_reduce / th_complete < 1 (or rescale): threshold rounds per bucket (module doc)."""
+        th_reduce / th_complete < 1 (or rescale): threshold rounds per bucket (module doc).
+        algo: the communicator's algorithm label per bucket, e.g. "twoshot@128": a bucket
+        reduced while backward still runs competes with it for CUs, and fewer persistent
+        workgroups leave more of the GPU to the GEMMs (default: the tuned / built-in choice)."""
+        self.algo = algo
         self.threshold = th_reduce < 1.0 or th_complete < 1.0 or rescale
         self.th = (float(th_reduce), float(th_complete), bool(rescale))
         if self.threshold and not hasattr(comm, "allreduce_threshold"):
@@ -191,6 +195,8 @@ class BucketedGradReducer:
             thr, thc, rescale = self.th
             self.comm.allreduce_threshold(b.buffer, b.buffer, th_reduce=thr, th_complete=thc, op=self.op,
                                           rescale=rescale)
+        elif self.algo != "auto":
+            self.comm.allreduce_(b.buffer, op=self.op, algo=self.algo)
         else:
             self.comm.allreduce_(b.buffer, op=self.op)
 

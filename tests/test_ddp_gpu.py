@@ -30,7 +30,8 @@ def _worker(rank, world, port, q, dtype, mode):
         thr = mode == "threshold"
         comm = XgmiCommunicator(device=0, slot_bytes=1 << 20, grid=8, timeout_s=15.0, max_lag=1 if thr else None)
         m, ref = _model(0, dtype), _model(0, dtype)
-        red = BucketedGradReducer(m, comm, bucket_bytes=32 << 10, op="avg", rescale=thr)
+        red = BucketedGradReducer(m, comm, bucket_bytes=32 << 10, op="avg", rescale=thr,
+                                  algo="auto" if thr else "twoshot@4")
         assert red.threshold == thr
         assert len(red.buckets) >= 3
         g = torch.Generator(device="cuda:0")
