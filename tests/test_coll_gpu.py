@@ -195,7 +195,7 @@ def _stress_worker(rank, world, port, q):
     try:
         comm = XgmiCommunicator(device=0, slot_bytes=512 << 10, grid=16, timeout_s=15.0, max_lag=1)
         rng = random.Random(1234)
-        for it in range(120):
+        for it in range(int(os.environ.get("MXAR_STRESS_ITERS", "120"))):
             op = rng.choice(["twoshot", "oneshot", "ll", "ring", "auto", "threshold", "thr_algo", "a2a", "ag", "rs"])
             dtype = rng.choice([torch.float32, torch.bfloat16, torch.float16])
             el = 16 // torch.empty(0, dtype=dtype).element_size()
@@ -238,15 +238,17 @@ def _stress_worker(rank, world, port, q):
 
 
 def test_multiprocess_random_operation_stress():
+    """4 ranks x 120 operations by default; MXAR_STRESS_RANKS / MXAR_STRESS_ITERS for a soak."""
     from akka_allreduce_1_amd.parallel import free_port
 
+    world = int(os.environ.get("MXAR_STRESS_RANKS", "4"))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_stress_worker, args=(r, 4, port, q)) for r in range(4)]
+    procs = [ctx.Process(target=_stress_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=110) for _ in range(4)]
+    res = [q.get(timeout=float(os.environ.get("MXAR_STRESS_TIMEOUT", "110"))) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         if p.is_alive():
