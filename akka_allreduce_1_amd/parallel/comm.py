@@ -392,6 +392,19 @@ class XgmiCommunicator:
         if e:
             raise CommError(f"rank {self.rank}: {_describe(e)} (error word {e:#x})")
 
+    def reset(self) -> None:
+        """Recover after a CommError (a peer missed a deadline): every rank calls this
+        collectively. Each rank drains its device, all ranks meet on the CPU group, every rank
+        zeroes its flags / LL slots / epoch counters, and all meet again - so no rank can see
+        a stale flag of the failed collective, and epochs restart from the same value on every
+        rank. The slabs' IPC mappings stay valid."""
+        import torch.distributed as dist
+
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=self.cpu_group)
+        self._c.reset_local()
+        dist.barrier(group=self.cpu_group)
+
     @property
     def native(self):
         return self._c

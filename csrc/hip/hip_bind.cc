@@ -250,6 +250,10 @@ void bind_hip(py::module_& m) {
           py::arg("comms"), py::arg("stream") = 0)
       .def("error", &XgmiComm::error)
       .def("clear_error", &XgmiComm::clear_error)
+      .def("reset_local", [](XgmiComm& c) {
+        py::gil_scoped_release r;
+        c.reset_local();
+      })
       .def_property_readonly("rank", &XgmiComm::rank)
       .def_property_readonly("world", &XgmiComm::world)
       .def_property_readonly("device", &XgmiComm::device)

@@ -115,6 +115,9 @@ class XgmiComm {
   // Sticky device error word (ORed codes, see device_common.h); 0 = healthy.
   uint32_t error() const;
   void clear_error();
+  // Zero this rank's flags, LL slots and counters (recovery after CommError; collective use
+  // only, with every rank idle - see XgmiCommunicator.reset).
+  void reset_local();
 
   int rank() const { return rank_; }
   int threshold_rows() const { return rows_ - 1; }

@@ -437,6 +437,19 @@ void XgmiComm::clear_error() {
   hip_check(hipMemset(ctl_ + 2, 0, 4), "hipMemset(err)");
 }
 
+void XgmiComm::reset_local() {
+  // Back to the state right after construction: every flag, progress word and LL slot 0
+  // (= "epoch 0 done"), epoch / ticket / error / threshold-round counters 0. Only valid when
+  // no launch of this communicator is in flight on any rank (XgmiCommunicator.reset
+  // brackets it with device synchronisation and host barriers).
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  hip_check(hipMemset(slab_, 0, off_S_), "hipMemset(flags)");
+  hip_check(hipMemset(slab_ + off_LL_, 0, 2 * world_ * ll_slot_), "hipMemset(ll)");
+  hip_check(hipMemset(ctl_, 0, 256), "hipMemset(ctl)");
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+}
+
 template <class E>
 static void launch_typed(const CommArgs& a, dim3 grid, hipStream_t s, Algo kind) {
   const dim3 b(kCommThreads);

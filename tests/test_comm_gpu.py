@@ -310,3 +310,62 @@ def test_local_cluster_large_blocks_fine_geometry(P):
     for k, y in enumerate(ys):
         err = (y.float() - ref).abs().max().item()
         assert err <= 1e-2 * P, (k, err)
+
+
+def _recover_worker(rank, world, port, results):
+    """Rank 1 skips one collective: rank 0 times out (CommError). After a collective reset()
+    both ranks reduce exactly again, with every algorithm."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.parallel import CommError, XgmiCommunicator
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ok, msg = True, ""
+    try:
+        comm = XgmiCommunicator(device=0, slot_bytes=1 << 20, grid=8, timeout_s=2.0, max_lag=1)
+        x = fill_uniform(torch.empty(50_000, device=DEV), seed=rank)
+        if rank == 0:
+            comm.allreduce(x, algo="twoshot")
+            try:
+                comm.check()
+                ok, msg = False, "expected a CommError"
+            except CommError:
+                pass
+        dist.barrier()
+        comm.reset()
+        assert comm.error() == 0
+        xs = [fill_uniform(torch.empty(50_000, device=DEV), seed=10 + k) for k in range(world)]
+        for algo in ("twoshot", "oneshot", "ll", "ring", "threshold", "twoshot"):
+            y = comm.allreduce(xs[rank], algo=algo)
+            comm.check()
+            err = (y - _ref(xs)).abs().max().item()
+            if err > 1e-5:
+                ok, msg = False, f"{algo} after reset: err {err}"
+        g = comm.all_gather(xs[rank][:1024].contiguous())
+        comm.check()
+        if not torch.equal(g[1024:2048] if rank == 0 else g[:1024], xs[1 - rank][:1024]):
+            ok, msg = False, "all_gather after reset"
+    except Exception as e:  # noqa: BLE001
+        ok, msg = False, repr(e)
+    results.put((rank, ok, msg))
+    dist.destroy_process_group()
+
+
+def test_reset_recovers_after_a_missed_collective():
+    from akka_allreduce_1_amd.parallel import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_recover_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    bad = [r for r in res if not r[1]]
+    assert not bad, bad
