@@ -392,6 +392,35 @@ class XgmiCommunicator:
         if e:
             raise CommError(f"rank {self.rank}: {_describe(e)} (error word {e:#x})")
 
+    def step_adamw(self, grads: torch.Tensor, params: torch.Tensor, state: dict, *, lr: float,
+                   betas: tuple[float, float] = (0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                   step: int, op: str = "avg") -> torch.Tensor:
+        """One fused sharded-DP step (csrc/hip/xgmi_adam.hip): reduce-scatter `grads` (mean by
+        default), AdamW on this rank's shard state, all-gather the new `params` (in place,
+        identical on every rank) - one launch. `state` = {"master", "exp_avg", "exp_avg_sq"}:
+        fp32 tensors of `shard_len(n)` elements holding block `rank` (see `adamw_state`)."""
+        if grads.numel() != params.numel() or grads.dtype != params.dtype:
+            raise ValueError("grads and params must match in size and dtype")
+        h = _H.AdamW()
+        h.lr, (h.beta1, h.beta2), h.eps, h.weight_decay, h.step = lr, betas, eps, weight_decay, step
+        self._c.step_adamw(grads.data_ptr(), params.data_ptr(), params.numel(), _dtype_code(params.dtype),
+                           _current_stream(self._dev), state["master"].data_ptr(), state["exp_avg"].data_ptr(),
+                           state["exp_avg_sq"].data_ptr(), h, 1.0 / self.world if op == "avg" else 1.0)
+        return params
+
+    def shard_len(self, n: int, dtype: torch.dtype) -> int:
+        """Elements of the block a rank owns in a fused step over n elements."""
+        return self._c.block_elems(n, _dtype_code(dtype))
+
+    def adamw_state(self, params: torch.Tensor) -> dict:
+        """Fresh fp32 shard state for `step_adamw`: master = this rank's block of params."""
+        b = self.shard_len(params.numel(), params.dtype)
+        lo, hi = self.rank * b, min(params.numel(), (self.rank + 1) * b)
+        master = torch.zeros(b, dtype=torch.float32, device=self.device)
+        if hi > lo:
+            master[:hi - lo].copy_(params.view(-1)[lo:hi].float())
+        return {"master": master, "exp_avg": torch.zeros_like(master), "exp_avg_sq": torch.zeros_like(master)}
+
     def reset(self) -> None:
         """Recover after a CommError (a peer missed a deadline): every rank calls this
         collectively. Each rank drains its device, all ranks meet on the CPU group, every rank
@@ -513,6 +542,22 @@ class LocalCluster:
                                          [outputs[k].data_ptr() for k in g], m, code,
                                          torch.cuda.current_stream(dev).cuda_stream, scale)
         return list(outputs)
+
+    def step_adamw(self, grads: Sequence[torch.Tensor], params: Sequence[torch.Tensor], states: Sequence[dict], *,
+                   lr: float, betas: tuple[float, float] = (0.9, 0.999), eps: float = 1e-8,
+                   weight_decay: float = 0.0, step: int, op: str = "avg") -> None:
+        """The fused reduce-scatter + AdamW + all-gather for every logical rank."""
+        h = _H.AdamW()
+        h.lr, (h.beta1, h.beta2), h.eps, h.weight_decay, h.step = lr, betas, eps, weight_decay, step
+        n = params[0].numel()
+        code = _dtype_code(params[0].dtype)
+        for g in self.groups:
+            dev = self.devices[g[0]]
+            _H.XgmiComm.step_adamw_local(
+                [self.comms[k] for k in g], [grads[k].data_ptr() for k in g], [params[k].data_ptr() for k in g], n,
+                code, torch.cuda.current_stream(dev).cuda_stream,
+                [(states[k]["master"].data_ptr(), states[k]["exp_avg"].data_ptr(), states[k]["exp_avg_sq"].data_ptr())
+                 for k in g], h, 1.0 / self.world if op == "avg" else 1.0)
 
     def barrier(self) -> None:
         for g in self.groups:

@@ -21,6 +21,11 @@ the wire as an allreduce, 1/P of the optimizer memory and optimizer FLOPs per ra
 `comm` needs `reduce_scatter(inp, out, op=)` and `all_gather(inp, out)` on the current stream:
 `XgmiCommunicator` (one xGMI launch each, csrc/hip/xgmi_coll.hip) or `TorchDistComm` (RCCL /
 gloo).
+
+`fused_adamw={"lr": ..., "betas": ..., "eps": ..., "weight_decay": ...}` (XgmiCommunicator
+only): every bucket's reduce-scatter, AdamW on the fp32 shard state and parameter all-gather
+run as ONE launch per bucket at `step()` (csrc/hip/xgmi_adam.hip); `optimizer_factory` is
+then unused (pass None) and the optimizer state is `self.adamw_states`.
 """
 from __future__ import annotations
 
@@ -48,8 +53,8 @@ class _Bucket:
 
 class ShardedDataParallel:
     def __init__(self, module: torch.nn.Module | Iterable[torch.nn.Parameter], comm,
-                 optimizer_factory: Callable[[list[torch.nn.Parameter]], torch.optim.Optimizer], *,
-                 bucket_bytes: int = 64 << 20, overlap: bool = True):
+                 optimizer_factory: Callable[[list[torch.nn.Parameter]], torch.optim.Optimizer] | None, *,
+                 bucket_bytes: int = 64 << 20, overlap: bool = True, fused_adamw: dict | None = None):
         params = module.parameters() if isinstance(module, torch.nn.Module) else module
         self.params = [p for p in params if p.requires_grad]
         if not self.params:
@@ -63,7 +68,21 @@ class ShardedDataParallel:
         self.stream = torch.cuda.Stream(device=self.device) if self.on_gpu else None
         self.buckets = self._build(bucket_bytes)
         self.slot_of = {id(p): (b, off) for b in self.buckets for p, off in zip(b.params, b.offsets)}
-        self.optimizer = optimizer_factory([b.shard_param for b in self.buckets])
+        self.fused = dict(fused_adamw) if fused_adamw is not None else None
+        self.adamw_states: list[dict] = []
+        self._t = 0
+        if self.fused is not None:
+            if not hasattr(comm, "step_adamw"):
+                raise ValueError("fused_adamw needs a communicator with step_adamw (XgmiCommunicator)")
+            cap = comm.world * comm.slot_bytes
+            for b in self.buckets:
+                if b.numel * b.flat_param.element_size() > cap:
+                    raise ValueError(f"fused_adamw: bucket of {b.numel} elements exceeds world * slot_bytes = {cap} B")
+            self.adamw_states = [comm.adamw_state(b.flat_param) for b in self.buckets]
+            self.overlap = False  # the fused launch needs the step's hyper-parameters: it runs in step()
+            self.optimizer = None
+        else:
+            self.optimizer = optimizer_factory([b.shard_param for b in self.buckets])
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
         self._next = 0
         self.stats = {"steps": 0, "reduce_scatter_bytes": 0, "all_gather_bytes": 0}
@@ -136,6 +155,16 @@ class ShardedDataParallel:
     def step(self) -> None:
         """Finish the gradient reduce-scatter, update the local shards, all-gather the
         parameters (call after backward)."""
+        if self.fused is not None:
+            self._t += 1
+            for b, st in zip(self.buckets, self.adamw_states):
+                self.comm.step_adamw(b.flat_grad, b.flat_param, st, step=self._t, **self.fused)
+                self.stats["reduce_scatter_bytes"] += b.flat_grad.numel() * b.flat_grad.element_size()
+                self.stats["all_gather_bytes"] += b.flat_param.numel() * b.flat_param.element_size()
+            for b in self.buckets:
+                b.pending = len(b.params)
+            self.stats["steps"] += 1
+            return
         self._launch_ready(all_=True)
         if self.on_gpu:
             torch.cuda.current_stream(self.device).wait_stream(self.stream)

@@ -6,6 +6,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <tuple>
 #include <vector>
 
 #include "../bindings/py_common.h"
@@ -148,7 +149,17 @@ void bind_hip(py::module_& m) {
       .def_readonly("ring", &CommStats::ring)
       .def_readonly("threshold", &CommStats::threshold)
       .def_readonly("ll", &CommStats::ll)
-      .def_readonly("coll", &CommStats::coll);
+      .def_readonly("coll", &CommStats::coll)
+      .def_readonly("adamw", &CommStats::adamw);
+
+  py::class_<AdamW>(h, "AdamW")
+      .def(py::init<>())
+      .def_readwrite("lr", &AdamW::lr)
+      .def_readwrite("beta1", &AdamW::beta1)
+      .def_readwrite("beta2", &AdamW::beta2)
+      .def_readwrite("eps", &AdamW::eps)
+      .def_readwrite("weight_decay", &AdamW::weight_decay)
+      .def_readwrite("step", &AdamW::step);
 
   py::class_<XgmiComm>(h, "XgmiComm")
       .def(py::init<int, int, int, int64_t, int, double, int>(), py::arg("rank"), py::arg("world"), py::arg("device"),
@@ -220,6 +231,34 @@ void bind_hip(py::module_& m) {
           },
           py::arg("comms"), py::arg("inputs"), py::arg("outputs"), py::arg("n"), py::arg("dtype"),
           py::arg("stream") = 0, py::arg("algo") = Algo::Auto, py::arg("scale") = 1.0f)
+      .def(
+          "step_adamw",
+          [](XgmiComm& c, uintptr_t grads, uintptr_t params, int64_t n, DType dt, uintptr_t stream, uintptr_t mp,
+             uintptr_t m1, uintptr_t m2, const AdamW& hp, float scale) {
+            AdamShard st{reinterpret_cast<float*>(mp), reinterpret_cast<float*>(m1), reinterpret_cast<float*>(m2)};
+            py::gil_scoped_release r;
+            c.step_adamw(as_cptr(grads), as_ptr(params), n, dt, as_stream(stream), st, hp, scale);
+          },
+          py::arg("grads"), py::arg("params"), py::arg("n"), py::arg("dtype"), py::arg("stream"), py::arg("master"),
+          py::arg("exp_avg"), py::arg("exp_avg_sq"), py::arg("hyper"), py::arg("scale") = 1.0f)
+      .def_static(
+          "step_adamw_local",
+          [](const std::vector<XgmiComm*>& comms, const std::vector<uintptr_t>& grads,
+             const std::vector<uintptr_t>& params, int64_t n, DType dt, uintptr_t stream,
+             const std::vector<std::tuple<uintptr_t, uintptr_t, uintptr_t>>& states, const AdamW& hp, float scale) {
+            std::vector<const void*> g;
+            std::vector<void*> p;
+            std::vector<AdamShard> st;
+            for (auto x : grads) g.push_back(as_cptr(x));
+            for (auto x : params) p.push_back(as_ptr(x));
+            for (auto& [a, b, c] : states)
+              st.push_back({reinterpret_cast<float*>(a), reinterpret_cast<float*>(b), reinterpret_cast<float*>(c)});
+            py::gil_scoped_release r;
+            XgmiComm::step_adamw_local(comms, g, p, n, dt, as_stream(stream), st, hp, scale);
+          },
+          py::arg("comms"), py::arg("grads"), py::arg("params"), py::arg("n"), py::arg("dtype"), py::arg("stream"),
+          py::arg("states"), py::arg("hyper"), py::arg("scale") = 1.0f)
+      .def("block_elems", &XgmiComm::block_elems, py::arg("n"), py::arg("dtype"))
       .def(
           "collective",
           [](XgmiComm& c, Coll op, uintptr_t in, uintptr_t out, int64_t m, DType dt, uintptr_t stream, float scale) {

@@ -37,11 +37,25 @@ enum class Algo : int { Auto = 0, TwoShot = 1, OneShot = 2, Ring = 3, LL = 4 };
 // The reference's two allreduce phases as collectives of their own (xgmi_coll.hip).
 enum class Coll : int { AllToAll = 0, AllGather = 1, ReduceScatter = 2 };
 
+// AdamW hyper-parameters of one fused step (PyTorch AdamW semantics; step counts from 1).
+struct AdamW {
+  float lr = 1e-3f, beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, weight_decay = 0.f;
+  int step = 1;
+};
+// Per-rank fp32 shard state for the fused step: master params, exp_avg, exp_avg_sq, each
+// holding the rank's own block (block r of the flat tensor, ceil(n / P) rounded to 16 B).
+struct AdamShard {
+  float* param = nullptr;
+  float* exp_avg = nullptr;
+  float* exp_avg_sq = nullptr;
+};
+
 constexpr int kMaxRanks = 16;
 constexpr int kCommThreads = 256;
 
 struct CommStats {
-  uint64_t calls = 0, launches = 0, bytes = 0, oneshot = 0, twoshot = 0, ring = 0, threshold = 0, ll = 0, coll = 0;
+  uint64_t calls = 0, launches = 0, bytes = 0, oneshot = 0, twoshot = 0, ring = 0, threshold = 0, ll = 0, coll = 0,
+           adamw = 0;
 };
 
 class XgmiComm {
@@ -94,6 +108,17 @@ class XgmiComm {
   }
   // Device-side barrier over all ranks (enqueued on `stream`).
   void barrier(hipStream_t stream);
+
+  // Fused data-parallel step (xgmi_adam.hip): grads [n] of every rank are reduce-scattered
+  // (x scale, fp32), the owner applies AdamW to its shard state, and the updated parameters
+  // are all-gathered into `params` [n] (identical on every rank). One launch; n * dtype must
+  // fit one segment (<= world * slot_bytes). shard_len() = elements of this rank's block.
+  void step_adamw(const void* grads, void* params, int64_t n, DType dt, hipStream_t stream, const AdamShard& st,
+                  const AdamW& h, float scale);
+  static void step_adamw_local(const std::vector<XgmiComm*>& comms, const std::vector<const void*>& grads,
+                               const std::vector<void*>& params, int64_t n, DType dt, hipStream_t stream,
+                               const std::vector<AdamShard>& st, const AdamW& h, float scale);
+  int64_t block_elems(int64_t n, DType dt) const;
 
   // Collectives on [P][m] buffers (m elements per block, m * dtype a multiple of 16 B):
   //   AllToAll      in[P][m] -> out[P][m]   out_r[s] = in_s[r]
@@ -153,7 +178,8 @@ class XgmiComm {
   static void run(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
                   const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, Algo algo, float scale);
   static void launch_segment(const std::vector<XgmiComm*>& group, const char* const* ins, char* const* outs,
-                             int64_t n, DType dt, hipStream_t stream, Algo kind, float scale);
+                             int64_t n, DType dt, hipStream_t stream, Algo kind, float scale,
+                             const std::vector<AdamShard>* adam_state = nullptr, const AdamW* adam = nullptr);
 
   static void run_coll(const std::vector<XgmiComm*>& group, Coll op, const std::vector<const void*>& ins,
                        const std::vector<void*>& outs, int64_t m, DType dt, hipStream_t stream, float scale);

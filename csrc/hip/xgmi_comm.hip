@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -478,7 +479,8 @@ static void launch_typed(const CommArgs& a, dim3 grid, hipStream_t s, Algo kind)
 // Common launch geometry + args for the ranks `group` (all on one device, consecutive
 // rank ids starting at group[0]->rank()).
 void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* const* ins, char* const* outs,
-                              int64_t n, DType dt, hipStream_t stream, Algo kind, float scale) {
+                              int64_t n, DType dt, hipStream_t stream, Algo kind, float scale,
+                              const std::vector<AdamShard>* adam_state, const AdamW* adam) {
   const bool oneshot = kind == Algo::OneShot;
   const XgmiComm& c0 = *group[0];
   const int W = c0.world_;
@@ -555,6 +557,27 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   if (kind != Algo::LL && (static_cast<int64_t>(a.nch) * a.sub > c0.maxch_ || a.block * es > c0.slot_bytes_ + 16))
     throw std::logic_error("XgmiComm: segment geometry exceeds slab");
   const dim3 grid(gx, ranks_here);
+  if (adam != nullptr) {
+    for (size_t y = 0; y < group.size(); ++y) {
+      a.opt_p[y] = (*adam_state)[y].param;
+      a.opt_m[y] = (*adam_state)[y].exp_avg;
+      a.opt_v[y] = (*adam_state)[y].exp_avg_sq;
+    }
+    a.lr = adam->lr;
+    a.beta1 = adam->beta1;
+    a.beta2 = adam->beta2;
+    a.eps = adam->eps;
+    a.wd = adam->weight_decay;
+    a.c1 = 1.f - std::pow(adam->beta1, static_cast<float>(adam->step));
+    a.c2_sqrt = std::sqrt(1.f - std::pow(adam->beta2, static_cast<float>(adam->step)));
+    launch_adamw(a, grid, stream, dt);
+    hip_check(hipGetLastError(), "adamw launch");
+    for (XgmiComm* c : group) {
+      ++c->stats_.launches;
+      ++c->stats_.adamw;
+    }
+    return;
+  }
   if (kind == Algo::LL) {
     if (2 * ceil_div(n * es, 8) * 8 > c0.ll_slot_) throw std::logic_error("XgmiComm: LL segment exceeds its slot");
     launch_ll(a, grid, stream, dt);
@@ -619,6 +642,56 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
     }
     launch_segment(group, ip.data(), op.data(), len, dt, stream, kind, scale);
   }
+}
+
+int64_t XgmiComm::block_elems(int64_t n, DType dt) const {
+  const int64_t elems = 16 / static_cast<int64_t>(dtype_size(dt));
+  return round_up(ceil_div(n, world_), elems);
+}
+
+void XgmiComm::step_adamw_local(const std::vector<XgmiComm*>& group, const std::vector<const void*>& grads,
+                                const std::vector<void*>& params, int64_t n, DType dt, hipStream_t stream,
+                                const std::vector<AdamShard>& st, const AdamW& h, float scale) {
+  if (group.empty() || grads.size() != group.size() || params.size() != group.size() || st.size() != group.size())
+    throw std::invalid_argument("step_adamw: one grads / params / shard state per rank");
+  const XgmiComm& c0 = *group[0];
+  const int64_t es = static_cast<int64_t>(dtype_size(dt));
+  for (size_t y = 0; y < group.size(); ++y) {
+    const XgmiComm& c = *group[y];
+    if (!c.connected_) throw std::runtime_error("XgmiComm: connect() first");
+    if (c.device_ != c0.device_ || c.rank_ != c0.rank_ + static_cast<int>(y) || c.world_ != c0.world_)
+      throw std::invalid_argument("XgmiComm: a grouped launch needs consecutive ranks on one device");
+    const uintptr_t g = reinterpret_cast<uintptr_t>(grads[y]), p = reinterpret_cast<uintptr_t>(params[y]);
+    if ((g | p | reinterpret_cast<uintptr_t>(st[y].param) | reinterpret_cast<uintptr_t>(st[y].exp_avg) |
+         reinterpret_cast<uintptr_t>(st[y].exp_avg_sq)) & 15)
+      throw std::invalid_argument("step_adamw: buffers must be 16-byte aligned");
+    if (g < p + static_cast<uintptr_t>(n * es) && p < g + static_cast<uintptr_t>(n * es))
+      throw std::invalid_argument("step_adamw: grads and params must not overlap");
+  }
+  if (n <= 0) return;
+  if (n * es > c0.world_ * c0.slot_bytes_)
+    throw std::invalid_argument("step_adamw: tensor exceeds one launch (n * dtype <= world * slot_bytes)");
+  if (h.step < 1) throw std::invalid_argument("step_adamw: step counts from 1");
+  hip_check(hipSetDevice(c0.device_), "hipSetDevice");
+  for (XgmiComm* c : group) {
+    ++c->stats_.calls;
+    c->stats_.bytes += n * es;
+  }
+  TraceScope span("xgmi", [&] {
+    return std::make_pair("adamw " + std::to_string(n * es) + "B", "{\"rank\":" + std::to_string(c0.rank_) + "}");
+  });
+  std::vector<const char*> ip(group.size());
+  std::vector<char*> op(group.size());
+  for (size_t y = 0; y < group.size(); ++y) {
+    ip[y] = static_cast<const char*>(grads[y]);
+    op[y] = static_cast<char*>(params[y]);
+  }
+  launch_segment(group, ip.data(), op.data(), n, dt, stream, Algo::TwoShot, scale, &st, &h);
+}
+
+void XgmiComm::step_adamw(const void* grads, void* params, int64_t n, DType dt, hipStream_t stream,
+                          const AdamShard& st, const AdamW& h, float scale) {
+  step_adamw_local({this}, {grads}, {params}, n, dt, stream, {st}, h, scale);
 }
 
 void XgmiComm::allreduce(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, Algo algo, float scale) {

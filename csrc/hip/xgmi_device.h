@@ -42,6 +42,11 @@ struct CommArgs {
   int rescale;         // scale a chunk reduced from cnt contributions by P / cnt
   // low-latency one-shot (xgmi_ll.hip): slots [parity][src] of ll_slot bytes at off_LL
   int64_t off_LL, ll_slot;
+  // fused reduce-scatter + AdamW + all-gather (xgmi_adam.hip): per rank fp32 shard state
+  float* opt_p[kMaxRanks];
+  float* opt_m[kMaxRanks];
+  float* opt_v[kMaxRanks];
+  float lr, beta1, beta2, eps, wd, c1, c2_sqrt;  // c1 = 1 - beta1^t, c2_sqrt = sqrt(1 - beta2^t)
   uint64_t delay;      // test knob: ticks rank `delay_rank` idles before phase 1
   int delay_rank;
 };
@@ -227,6 +232,8 @@ __device__ __forceinline__ uint32_t launch_epoch(const uint32_t* ctl) {
 void launch_threshold(const CommArgs& a, dim3 grid, hipStream_t s, DType dt);
 // Host entry of the low-latency one-shot (xgmi_ll.hip).
 void launch_ll(const CommArgs& a, dim3 grid, hipStream_t s, DType dt);
+// Host entry of the fused reduce-scatter + AdamW + all-gather (xgmi_adam.hip).
+void launch_adamw(const CommArgs& a, dim3 grid, hipStream_t s, DType dt);
 // Host entry of all-to-all (mode 0) / all-gather (1) / reduce-scatter (2) (xgmi_coll.hip).
 void launch_coll(const CommArgs& a, dim3 grid, hipStream_t s, DType dt, int mode);
 

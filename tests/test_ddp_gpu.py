@@ -81,7 +81,7 @@ def test_ddp_reducer_xgmi_two_processes(dtype, mode):
     assert not bad, bad[0][2]
 
 
-def _zero_worker(rank, world, port, q):
+def _zero_worker(rank, world, port, q, fused=False):
     import torch.distributed as dist
 
     from akka_allreduce_1_amd.parallel import ShardedDataParallel, XgmiCommunicator
@@ -93,7 +93,12 @@ def _zero_worker(rank, world, port, q):
         comm = XgmiCommunicator(device=0, slot_bytes=1 << 20, grid=8, timeout_s=15.0)
         make = lambda ps: torch.optim.Adam(ps, lr=1e-3)  # noqa: E731
         m, ref = _model(0, torch.float32), _model(0, torch.float32)
-        zdp = ShardedDataParallel(m, comm, make, bucket_bytes=32 << 10)
+        if fused:  # one fused reduce-scatter + AdamW + all-gather launch per bucket
+            zdp = ShardedDataParallel(m, comm, None, bucket_bytes=32 << 10,
+                                      fused_adamw={"lr": 1e-3, "betas": (0.9, 0.999), "eps": 1e-8,
+                                                   "weight_decay": 0.0})
+        else:
+            zdp = ShardedDataParallel(m, comm, make, bucket_bytes=32 << 10)
         ref_opt = make(list(ref.parameters()))
         g = torch.Generator(device="cuda:0")
         data = [torch.randn(16, 64, device="cuda:0", generator=g.manual_seed(30 + r)) for r in range(world)]
@@ -113,7 +118,10 @@ def _zero_worker(rank, world, port, q):
             for p, rp in zip(m.parameters(), ref.parameters()):
                 err = (p - rp).abs().max().item()
                 assert err <= 1e-5, (step, err)
-        assert comm.native.stats.coll >= 2 * 3 * len(zdp.buckets)  # RS + AG per bucket per step on xGMI
+        if fused:
+            assert comm.native.stats.adamw == 3 * len(zdp.buckets)
+        else:
+            assert comm.native.stats.coll >= 2 * 3 * len(zdp.buckets)  # RS + AG per bucket per step on xGMI
         q.put((rank, True, ""))
     except Exception:  # noqa: BLE001
         import traceback
@@ -123,13 +131,14 @@ def _zero_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_sharded_data_parallel_xgmi_two_processes():
+@pytest.mark.parametrize("fused", [False, True])
+def test_sharded_data_parallel_xgmi_two_processes(fused):
     from akka_allreduce_1_amd.parallel import free_port
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_zero_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_zero_worker, args=(r, 2, port, q, fused)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(2)]
