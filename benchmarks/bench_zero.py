@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Sharded data-parallel optimizer step at model scale (Llama-3-8B parameter set).
+
+Parameters live in flat bf16 buckets (`--bucket-mib`), every rank keeps fp32 master /
+exp_avg / exp_avg_sq for its 1/P shard (12 B per owned parameter: the whole 8.03 B-parameter
+model's state is 96 GB at P = 1, which an MI355X's 288 GB holds next to the bf16 params and
+grads). One step per bucket:
+
+  fused    one xGMI launch: reduce-scatter (mean) + AdamW on the fp32 shard + all-gather of
+           the new bf16 parameters (csrc/hip/xgmi_adam.hip)
+  unfused  xGMI reduce-scatter -> cast to fp32 -> torch AdamW(fused=True) on the fp32 master
+           shard -> cast to bf16 -> xGMI all-gather (the same math, five steps)
+
+    python benchmarks/bench_zero.py --layers 32 --mode fused          # full model, 1 GPU
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 benchmarks/bench_zero.py
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from akka_allreduce_1_amd.models.grad_sets import llama3_8b_shapes, numel  # noqa: E402
+from akka_allreduce_1_amd.ops import fill_uniform  # noqa: E402
+from akka_allreduce_1_amd.parallel import XgmiCommunicator  # noqa: E402
+from akka_allreduce_1_amd.parallel.comm import init_distributed  # noqa: E402
+
+
+def timed(fn, steps: int, dev) -> float:
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / steps
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item() * 1e3
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layers", type=int, default=32, help="transformer layers (32 = the full 8.03 B model)")
+    ap.add_argument("--bucket-mib", type=int, default=256)
+    ap.add_argument("--mode", choices=["fused", "unfused", "both"], default="both")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    args = ap.parse_args()
+    rank, world, local = init_distributed("nccl")
+    dev = torch.device("cuda", local)
+    dt = torch.bfloat16
+    shapes = llama3_8b_shapes(args.layers)
+    total = sum(numel(s) for _, s in shapes)
+    per_bucket = (args.bucket_mib << 20) // 2
+    unit = world * 8
+    sizes = []
+    left = total
+    while left > 0:
+        m = min(per_bucket, left)
+        sizes.append(-(-m // unit) * unit)
+        left -= m
+    comm = XgmiCommunicator(slot_bytes=-(-(args.bucket_mib << 20) // world) + (1 << 20))
+    params = [fill_uniform(torch.empty(n, dtype=dt, device=dev), seed=1000 + i) for i, n in enumerate(sizes)]
+    grads = [fill_uniform(torch.empty(n, dtype=dt, device=dev), seed=2000 + i + rank) for i, n in enumerate(sizes)]
+    hp = dict(lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    res = {"metric": "sharded_dp_optimizer_step_ms", "model": f"llama3_8b ({args.layers} layers)", "params": total,
+           "n_gpus": world, "buckets": len(sizes), "bucket_mib": args.bucket_mib, "dtype": "bf16 params, fp32 state"}
+
+    if args.mode in ("fused", "both"):
+        states = [comm.adamw_state(p) for p in params]
+        t = {"step": 0}
+
+        def fused():
+            t["step"] += 1
+            for p, g, st in zip(params, grads, states):
+                comm.step_adamw(g, p, st, step=t["step"], **hp)
+
+        for _ in range(args.warmup):
+            fused()
+        res["fused_ms"] = round(timed(fused, args.steps, dev), 2)
+        comm.check()
+        res["state_GB_per_rank"] = round(sum(3 * s["master"].numel() * 4 for s in states) / 1e9, 1)
+        del states
+        torch.cuda.empty_cache()
+
+    if args.mode in ("unfused", "both"):
+        shards, masters, opts, pshards = [], [], [], []
+        for p in params:
+            b = comm.shard_len(p.numel(), dt)
+            shards.append(torch.empty(b, dtype=dt, device=dev))
+            mst = torch.nn.Parameter(p[rank * b:(rank + 1) * b].float())
+            masters.append(mst)
+            opts.append(torch.optim.AdamW([mst], fused=True, **hp))
+            pshards.append(torch.empty(b, dtype=dt, device=dev))
+
+        def unfused():
+            for i, (p, g) in enumerate(zip(params, grads)):
+                comm.reduce_scatter(g, shards[i], op="avg")
+                masters[i].grad = shards[i].float()
+                opts[i].step()
+                pshards[i].copy_(masters[i].detach())
+                comm.all_gather(pshards[i], p)
+
+        for _ in range(args.warmup):
+            unfused()
+        res["unfused_ms"] = round(timed(unfused, args.steps, dev), 2)
+        comm.check()
+    if "fused_ms" in res and "unfused_ms" in res:
+        res["speedup"] = round(res["unfused_ms"] / res["fused_ms"], 2)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
