@@ -135,6 +135,46 @@ def collectives(comm: XgmiCommunicator, x: torch.Tensor, world: int, args, dev) 
     return out
 
 
+def fused_step(comm: XgmiCommunicator, grads: torch.Tensor, params: torch.Tensor, world: int, rank: int, args,
+               dev) -> dict:
+    """Sharded-DP optimizer step on the bench buffer (bf16 params, fp32 AdamW shard state):
+    the fused launch (csrc/hip/xgmi_adam.hip) vs reduce-scatter + torch fused AdamW + casts +
+    all-gather."""
+    row = {}
+    try:
+        hp = dict(lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+        st = comm.adamw_state(params)
+        t = {"step": 0}
+
+        def fused():
+            t["step"] += 1
+            comm.step_adamw(grads, params, st, step=t["step"], **hp)
+
+        b = comm.shard_len(params.numel(), params.dtype)
+        shard = torch.empty(b, dtype=params.dtype, device=dev)
+        pshard = torch.empty(b, dtype=params.dtype, device=dev)
+        master = torch.nn.Parameter(st["master"].clone())
+        opt = torch.optim.AdamW([master], fused=True, **hp)
+
+        def unfused():
+            comm.reduce_scatter(grads, shard, op="avg")
+            master.grad = shard.float()
+            opt.step()
+            pshard.copy_(master.detach())
+            comm.all_gather(pshard, params)
+
+        for label, fn in (("fused", fused), ("unfused", unfused)):
+            for _ in range(args.warmup):
+                fn()
+            row[f"{label}_ms"] = round(max_over_ranks(timed(fn, args.steps, dev), dev) / args.steps * 1e3, 4)
+        comm.check()
+        row["speedup"] = round(row["unfused_ms"] / row["fused_ms"], 3)
+        row["params"] = params.numel()
+    except Exception as e:  # noqa: BLE001 - reported, never loses the headline
+        row["error"] = repr(e)
+    return row
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -149,6 +189,7 @@ def main() -> None:
     ap.add_argument("--sweep-steps", type=int, default=10)
     ap.add_argument("--no-threshold", action="store_true", help="skip the straggler-tolerant kernel timing")
     ap.add_argument("--no-collectives", action="store_true", help="skip the all-to-all / all-gather / reduce-scatter timing")
+    ap.add_argument("--no-fused-step", action="store_true", help="skip the fused reduce-scatter + AdamW + all-gather timing")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal: every rank on cuda:0 over gloo (RCCL refuses two ranks on one GPU), "
                          "workgroup budget split between the ranks so all spinning workgroups stay resident")
@@ -303,6 +344,8 @@ def main() -> None:
         # the allreduce's two halves and the all-to-all as collectives of their own
         # (csrc/hip/xgmi_coll.hip) on the same bytes, next to RCCL's equivalents
         result["collectives"] = collectives(comm, x, world, args, dev)
+    if engine_ok and not args.no_fused_step:
+        result["fused_adamw_step"] = fused_step(comm, x, y, world, rank, args, dev)
     if sweep is not None:
         result["sweep"] = sweep
 
