@@ -321,6 +321,14 @@ def main() -> None:
                           "p50_ms": round(max_over_ranks(percentile(rper, 50), dev), 4),
                           "note": "copy + in-place dist.all_reduce (nccl backend = RCCL)"}
         result["speedup_vs_rccl"] = round(algbw / r_alg, 3)
+    # the optional sections below only run on a healthy engine (every rank's error word 0),
+    # so one timed-out launch can never cascade into a chain of 20-s device deadlines
+    if engine_ok:
+        e = torch.tensor([1 if comm.error() == 0 else 0], device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MIN)
+        if e.item() == 0:
+            log(rank, "engine error word set: optional sections skipped")
+            engine_ok = False
     if engine_ok and world > 1 and not args.no_threshold:
         # the reference's round semantics (thReduce / thComplete / maxLag) on the same buffer,
         # at th = 1 so every rank must still deliver: the cost of straggler tolerance itself
