@@ -113,6 +113,43 @@ def run_tcp(P: int, N: int, chunk: int, rounds: int, th: float) -> dict:
             "frames_per_worker": ws[0]["cluster"]["frames_out"]}
 
 
+def run_native(P: int, N: int, chunk: int, rounds: int, th: float) -> dict:
+    """The same deployment with the Python-free executables (csrc/tools/mxar_main.cc)."""
+    exe = os.path.join(ROOT, "akka_allreduce_1_amd", "mxar")
+    port = free_port()
+    seed = ["--seeds", f"mxar.tcp://ClusterSystem@127.0.0.1:{port}", "--loglevel", "ERROR"]
+    master = subprocess.Popen([exe, "master", str(port), str(P), str(N), str(chunk), "--th-reduce", str(th),
+                               "--th-complete", str(th), "--max-round", str(rounds - 1)] + seed,
+                              stdout=subprocess.PIPE, text=True)
+    with tempfile.TemporaryDirectory() as td:
+        # worker output goes to files: a pipe nobody drains while the master runs would block them
+        logs = [open(os.path.join(td, f"w{i}.out"), "w+") for i in range(P)]
+        workers = [subprocess.Popen([exe, "worker", "0", str(N)] + seed, stdout=logs[i], text=True) for i in range(P)]
+        try:
+            mout, _ = master.communicate(timeout=900)
+            for w in workers:
+                w.wait(timeout=60)
+            wouts = []
+            for f in logs:
+                f.seek(0)
+                wouts.append(f.read())
+                f.close()
+        finally:
+            for q in [master] + workers:
+                if q.poll() is None:
+                    q.kill()
+    stats = next(json.loads(line) for line in mout.splitlines() if line.startswith("{"))
+    exact = True
+    if th >= 1.0:  # worker sink lines: "round r sum S ..." with data[i] = i + r on every worker
+        for out in wouts:
+            sums = {int(line.split()[3]): float(line.split()[5]) for line in out.splitlines() if " sum " in line}
+            exact &= len(sums) == rounds and all(v == P * (N * (N - 1) / 2 + N * r) for r, v in sums.items())
+    return {"transport": "tcp-native", "finished": master.returncode == 0 and stats["rounds"] == rounds,
+            "exact": exact, "rounds": rounds, "steady_rounds_per_s": stats["steady_rounds_per_s"],
+            "round_interval_p50_ms": round(stats["round_interval_p50_us"] / 1e3, 4),
+            "round_interval_p99_ms": round(stats["round_interval_p99_us"] / 1e3, 4)}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--workers", type=int, default=2)
@@ -120,14 +157,16 @@ def main() -> None:
     ap.add_argument("--chunk", type=int, default=256, help="maxChunkSize (floats per message)")
     ap.add_argument("--rounds", type=int, default=1000)
     ap.add_argument("--th", type=float, default=1.0, help="thReduce = thComplete")
-    ap.add_argument("--transport", choices=["inproc", "tcp", "both"], default="both")
+    ap.add_argument("--transport", choices=["inproc", "tcp", "native", "both", "all"], default="all")
     args = ap.parse_args()
     C.set_log_level("WARNING")
     res = []
-    if args.transport in ("inproc", "both"):
+    if args.transport in ("inproc", "both", "all"):
         res.append(run_inproc(args.workers, args.size, args.chunk, args.rounds, args.th))
-    if args.transport in ("tcp", "both"):
+    if args.transport in ("tcp", "both", "all"):
         res.append(run_tcp(args.workers, args.size, args.chunk, args.rounds, args.th))
+    if args.transport in ("native", "all"):
+        res.append(run_native(args.workers, args.size, args.chunk, args.rounds, args.th))
     for r in res:
         r.update(workers=args.workers, size=args.size, chunk=args.chunk, th=args.th)
         print(json.dumps(r), flush=True)

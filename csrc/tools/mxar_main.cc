@@ -13,6 +13,7 @@
 //   options: --host H  --seeds addr[,addr]  --th-allreduce F --th-reduce F --th-complete F
 //            --max-lag N --max-round N --round-timeout-ms N --loglevel L --quiet
 //   seeds default to the reference's application.conf:14-16 (127.0.0.1:2551, :2552).
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <csignal>
@@ -120,7 +121,13 @@ void set_level(const std::string& l) {
   auto sys = std::make_shared<ActorSystem>("ClusterSystem", ActorSystem::Mode::Threaded, 2);
   std::atomic<int> finished{-1};
   const auto t0 = std::chrono::steady_clock::now();
-  ActorRef master = sys->actor_of(std::make_unique<MasterActor>(mp, [&](int rounds) { finished = rounds; }), "master");
+  std::vector<double> stamps;  // completion time of every round (master thread only)
+  stamps.reserve(static_cast<size_t>(o.max_round) + 1);
+  auto on_round = [&stamps](int, int64_t) {
+    stamps.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count());
+  };
+  ActorRef master =
+      sys->actor_of(std::make_unique<MasterActor>(mp, [&](int rounds) { finished = rounds; }, on_round), "master");
   ClusterConfig cc;
   cc.host = o.host;
   cc.port = port;
@@ -135,8 +142,18 @@ void set_level(const std::string& l) {
   std::fflush(stdout);
   while (!g_stop && finished.load() < 0) std::this_thread::sleep_for(std::chrono::milliseconds(10));
   const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  if (finished.load() >= 0)
+  if (finished.load() >= 0) {
     std::printf("[mxar master] finished %d rounds in %.3f s\n", finished.load(), s);
+    if (stamps.size() > 2) {  // steady state: the intervals between consecutive round completions
+      std::vector<double> iv;
+      for (size_t i = 1; i < stamps.size(); ++i) iv.push_back((stamps[i] - stamps[i - 1]) * 1e6);
+      std::sort(iv.begin(), iv.end());
+      const double rate = static_cast<double>(stamps.size() - 1) / (stamps.back() - stamps.front());
+      std::printf("{\"rounds\": %zu, \"steady_rounds_per_s\": %.1f, \"round_interval_p50_us\": %.1f, "
+                  "\"round_interval_p99_us\": %.1f}\n",
+                  stamps.size(), rate, iv[iv.size() / 2], iv[std::min(iv.size() - 1, iv.size() * 99 / 100)]);
+    }
+  }
   std::fflush(stdout);
   node->leave();
   std::this_thread::sleep_for(std::chrono::milliseconds(200));  // let the Leave / Removed frames go out
