@@ -26,6 +26,12 @@ gloo).
 only): every bucket's reduce-scatter, AdamW on the fp32 shard state and parameter all-gather
 run as ONE launch per bucket at `step()` (csrc/hip/xgmi_adam.hip); `optimizer_factory` is
 then unused (pass None) and the optimizer state is `self.adamw_states`.
+
+`step_in_backward=True` (with `fused_adamw`, GPU): a bucket's fused step is launched on the
+side stream the moment its last gradient is accumulated, so communication AND the optimizer
+overlap the rest of backward ("optimizer in backward"). Valid because a parameter's
+AccumulateGrad hook fires after its autograd node has used it; parameters shared between
+layers (tied weights) must not be used with this mode.
 """
 from __future__ import annotations
 
@@ -54,7 +60,8 @@ class _Bucket:
 class ShardedDataParallel:
     def __init__(self, module: torch.nn.Module | Iterable[torch.nn.Parameter], comm,
                  optimizer_factory: Callable[[list[torch.nn.Parameter]], torch.optim.Optimizer] | None, *,
-                 bucket_bytes: int = 64 << 20, overlap: bool = True, fused_adamw: dict | None = None):
+                 bucket_bytes: int = 64 << 20, overlap: bool = True, fused_adamw: dict | None = None,
+                 step_in_backward: bool = False):
         params = module.parameters() if isinstance(module, torch.nn.Module) else module
         self.params = [p for p in params if p.requires_grad]
         if not self.params:
@@ -79,10 +86,15 @@ class ShardedDataParallel:
                 if b.numel * b.flat_param.element_size() > cap:
                     raise ValueError(f"fused_adamw: bucket of {b.numel} elements exceeds world * slot_bytes = {cap} B")
             self.adamw_states = [comm.adamw_state(b.flat_param) for b in self.buckets]
-            self.overlap = False  # the fused launch needs the step's hyper-parameters: it runs in step()
+            # without step_in_backward the fused launch runs in step(); with it, from the hooks
+            self.overlap = bool(step_in_backward) and self.on_gpu
             self.optimizer = None
         else:
+            if step_in_backward:
+                raise ValueError("step_in_backward needs fused_adamw")
             self.optimizer = optimizer_factory([b.shard_param for b in self.buckets])
+        self.step_in_backward = self.fused is not None and self.overlap
+        self._t_started = False
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
         self._next = 0
         self.stats = {"steps": 0, "reduce_scatter_bytes": 0, "all_gather_bytes": 0}
@@ -141,7 +153,22 @@ class ShardedDataParallel:
             self._reduce(self.buckets[self._next])
             self._next += 1
 
+    def _fused_bucket(self, b: _Bucket) -> None:
+        if not self._t_started:  # first bucket of this backward: a new optimizer step
+            self._t += 1
+            self._t_started = True
+        st = self.adamw_states[b.index]
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            self.comm.step_adamw(b.flat_grad, b.flat_param, st, step=self._t, **self.fused)
+        b.launched = True
+        self.stats["reduce_scatter_bytes"] += b.flat_grad.numel() * b.flat_grad.element_size()
+        self.stats["all_gather_bytes"] += b.flat_param.numel() * b.flat_param.element_size()
+
     def _reduce(self, b: _Bucket) -> None:
+        if self.fused is not None:
+            self._fused_bucket(b)
+            return
         if self.on_gpu:
             self.stream.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self.stream):
@@ -155,6 +182,16 @@ class ShardedDataParallel:
     def step(self) -> None:
         """Finish the gradient reduce-scatter, update the local shards, all-gather the
         parameters (call after backward)."""
+        if self.step_in_backward:
+            self._launch_ready(all_=True)  # buckets whose parameters got no gradient
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+            for b in self.buckets:
+                b.pending = len(b.params)
+                b.launched = False
+            self._next = 0
+            self._t_started = False
+            self.stats["steps"] += 1
+            return
         if self.fused is not None:
             self._t += 1
             for b, st in zip(self.buckets, self.adamw_states):

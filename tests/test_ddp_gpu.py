@@ -96,7 +96,7 @@ def _zero_worker(rank, world, port, q, fused=False):
         if fused:  # one fused reduce-scatter + AdamW + all-gather launch per bucket
             zdp = ShardedDataParallel(m, comm, None, bucket_bytes=32 << 10,
                                       fused_adamw={"lr": 1e-3, "betas": (0.9, 0.999), "eps": 1e-8,
-                                                   "weight_decay": 0.0})
+                                                   "weight_decay": 0.0}, step_in_backward=fused == "backward")
         else:
             zdp = ShardedDataParallel(m, comm, make, bucket_bytes=32 << 10)
         ref_opt = make(list(ref.parameters()))
@@ -131,7 +131,7 @@ def _zero_worker(rank, world, port, q, fused=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("fused", [False, "step", "backward"])
 def test_sharded_data_parallel_xgmi_two_processes(fused):
     from akka_allreduce_1_amd.parallel import free_port
 
