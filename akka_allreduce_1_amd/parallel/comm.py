@@ -60,6 +60,17 @@ def _current_stream(device_index: int) -> int:
     return torch.cuda.current_stream(device_index).cuda_stream
 
 
+def comm_stream(device) -> "torch.cuda.Stream":
+    """Side stream for collectives overlapped with compute (gradient buckets, fused optimizer
+    steps). High priority on purpose: HIP hands out hardware queues to streams round-robin
+    within a priority level (GPU_MAX_HW_QUEUES per process), so a normal-priority side stream
+    can share the compute stream's queue - its kernels then run strictly in order with the
+    GEMMs and nothing overlaps (seen in a rocprofv3 kernel trace: both streams on one
+    Queue_Id). A high-priority stream is served from a queue of its own, and the dispatcher
+    favours it, so a persistent collective's workgroups become resident next to the GEMMs."""
+    return torch.cuda.Stream(device=device, priority=-1)
+
+
 def free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -394,13 +405,18 @@ class XgmiCommunicator:
 
     def step_adamw(self, grads: torch.Tensor, params: torch.Tensor, state: dict, *, lr: float,
                    betas: tuple[float, float] = (0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                   step: int, op: str = "avg") -> torch.Tensor:
+                   step: int, op: str = "avg", grid: int = 0) -> torch.Tensor:
         """One fused sharded-DP step (csrc/hip/xgmi_adam.hip): reduce-scatter `grads` (mean by
         default), AdamW on this rank's shard state, all-gather the new `params` (in place,
         identical on every rank) - one launch. `state` = {"master", "exp_avg", "exp_avg_sq"}:
-        fp32 tensors of `shard_len(n)` elements holding block `rank` (see `adamw_state`)."""
+        fp32 tensors of `shard_len(n)` elements holding block `rank` (see `adamw_state`).
+        `grid` > 0 overrides the workgroup count (fewer leave CUs to overlapped GEMMs)."""
         if grads.numel() != params.numel() or grads.dtype != params.dtype:
             raise ValueError("grads and params must match in size and dtype")
+        g = grid if grid > 0 else self._default_grid
+        if self._grid != g:
+            self._c.grid = g
+            self._grid = g
         h = _H.AdamW()
         h.lr, (h.beta1, h.beta2), h.eps, h.weight_decay, h.step = lr, betas, eps, weight_decay, step
         self._c.step_adamw(grads.data_ptr(), params.data_ptr(), params.numel(), _dtype_code(params.dtype),

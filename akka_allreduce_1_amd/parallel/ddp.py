@@ -32,6 +32,8 @@ from typing import Iterable, Sequence
 
 import torch
 
+from .comm import comm_stream
+
 _ALIGN_BYTES = 16
 
 
@@ -113,7 +115,7 @@ class BucketedGradReducer:
         self.device = self.params[0].device
         self.on_gpu = self.device.type == "cuda"
         self.overlap = overlap and self.on_gpu
-        self.stream = torch.cuda.Stream(device=self.device) if self.on_gpu else None
+        self.stream = comm_stream(self.device) if self.on_gpu else None
         self.sync = sync if self.on_gpu else "none"
         self.buckets = self._build(bucket_bytes, first_bucket_bytes)
         if self.threshold:

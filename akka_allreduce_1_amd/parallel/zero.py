@@ -31,13 +31,16 @@ then unused (pass None) and the optimizer state is `self.adamw_states`.
 side stream the moment its last gradient is accumulated, so communication AND the optimizer
 overlap the rest of backward ("optimizer in backward"). Valid because a parameter's
 AccumulateGrad hook fires after its autograd node has used it; parameters shared between
-layers (tied weights) must not be used with this mode.
+layers (tied weights) must not be used with this mode. `comm_grid` sets the workgroup count
+of the fused launches (0 = engine default).
 """
 from __future__ import annotations
 
 from typing import Callable, Iterable
 
 import torch
+
+from .comm import comm_stream
 
 _ALIGN_BYTES = 16
 
@@ -61,7 +64,7 @@ class ShardedDataParallel:
     def __init__(self, module: torch.nn.Module | Iterable[torch.nn.Parameter], comm,
                  optimizer_factory: Callable[[list[torch.nn.Parameter]], torch.optim.Optimizer] | None, *,
                  bucket_bytes: int = 64 << 20, overlap: bool = True, fused_adamw: dict | None = None,
-                 step_in_backward: bool = False):
+                 step_in_backward: bool = False, comm_grid: int = 0):
         params = module.parameters() if isinstance(module, torch.nn.Module) else module
         self.params = [p for p in params if p.requires_grad]
         if not self.params:
@@ -72,10 +75,12 @@ class ShardedDataParallel:
         self.device = self.params[0].device
         self.on_gpu = self.device.type == "cuda"
         self.overlap = overlap and self.on_gpu
-        self.stream = torch.cuda.Stream(device=self.device) if self.on_gpu else None
+        self.stream = comm_stream(self.device) if self.on_gpu else None
         self.buckets = self._build(bucket_bytes)
         self.slot_of = {id(p): (b, off) for b in self.buckets for p, off in zip(b.params, b.offsets)}
         self.fused = dict(fused_adamw) if fused_adamw is not None else None
+        if self.fused is not None:
+            self.fused["grid"] = int(comm_grid)
         self.adamw_states: list[dict] = []
         self._t = 0
         if self.fused is not None:

@@ -52,7 +52,8 @@ class SyntheticBackward:
     def flops(self) -> float:
         return sum(2.0 * self.tokens * numel(tuple(p.shape)) for p in self.params if p.dim() > 1)
 
-    def run(self, reducer: BucketedGradReducer | None) -> None:
+    def run(self, reducer: BucketedGradReducer | None, hook=None) -> None:
+        hook = hook if hook is not None else (reducer._on_grad_ready if reducer is not None else None)
         for p in reversed(self.params):  # autograd order
             o, i = gemm_shape(tuple(p.shape))
             g = p.grad.view(o, i)
@@ -60,8 +61,8 @@ class SyntheticBackward:
                 torch.matmul(self.dy[:, :o].t(), self.x[:, :i], out=g)
             else:
                 g.copy_(self.dy[0, :o].view(o, 1))
-            if reducer is not None:
-                reducer._on_grad_ready(p)  # what the post-accumulate-grad hook does
+            if hook is not None:
+                hook(p)  # what the post-accumulate-grad hook does
 
 
 def timed(fn, steps: int, dev) -> float:

@@ -11,7 +11,13 @@ grads). One step per bucket:
   unfused  xGMI reduce-scatter -> cast to fp32 -> torch AdamW(fused=True) on the fp32 master
            shard -> cast to bf16 -> xGMI all-gather (the same math, five steps)
 
+  train    ShardedDataParallel(fused_adamw=...) behind a synthetic backward (one GEMM per
+           gradient, benchmarks/bench_dp.py): the fused step after backward (`serial`) vs
+           launched per bucket from the gradient hooks (`step_in_backward=True`), where the
+           HBM-bound optimizer overlaps the GEMM-bound backward
+
     python benchmarks/bench_zero.py --layers 32 --mode fused          # full model, 1 GPU
+    python benchmarks/bench_zero.py --layers 32 --mode train
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 benchmarks/bench_zero.py
 """
 from __future__ import annotations
@@ -26,10 +32,11 @@ import torch
 import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from akka_allreduce_1_amd.models.grad_sets import llama3_8b_shapes, numel  # noqa: E402
 from akka_allreduce_1_amd.ops import fill_uniform  # noqa: E402
-from akka_allreduce_1_amd.parallel import XgmiCommunicator  # noqa: E402
+from akka_allreduce_1_amd.parallel import ShardedDataParallel, XgmiCommunicator  # noqa: E402
 from akka_allreduce_1_amd.parallel.comm import init_distributed  # noqa: E402
 
 
@@ -46,17 +53,71 @@ def timed(fn, steps: int, dev) -> float:
     return t.item() * 1e3
 
 
+def train(args, rank: int, world: int, dev, dt, hp) -> None:
+    from bench_dp import SyntheticBackward
+
+    shapes = llama3_8b_shapes(args.layers)
+    params = [torch.nn.Parameter(fill_uniform(torch.empty(s, dtype=dt, device=dev), seed=7 + i))
+              for i, (_, s) in enumerate(shapes)]
+    biggest = max(args.bucket_mib << 20, max(p.numel() * p.element_size() for p in params))
+    comm = XgmiCommunicator(slot_bytes=-(-biggest // world) + (1 << 20))
+    zdp = ShardedDataParallel(params, comm, None, bucket_bytes=args.bucket_mib << 20, fused_adamw=hp)
+    zdp.remove_hooks()  # the synthetic backward calls the hook itself
+    bwd = SyntheticBackward(params, args.tokens, dt, dev)
+
+    def mode(in_backward: bool) -> None:  # same buckets and optimizer state, launch site toggled
+        zdp.overlap = zdp.step_in_backward = in_backward
+
+    def step() -> None:
+        bwd.run(None, hook=zdp._on_grad)
+        zdp.step()
+
+    res = {"metric": "sharded_dp_train_step_ms", "model": f"llama3_8b ({args.layers} layers)",
+           "params": sum(p.numel() for p in params), "n_gpus": world, "buckets": len(zdp.buckets),
+           "bucket_mib": args.bucket_mib, "tokens": args.tokens, "dtype": "bf16 params, fp32 state"}
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            bwd.run(None)
+        res["backward_ms"] = round(timed(lambda: bwd.run(None), args.steps, dev), 2)
+        runs = [("serial_ms", False, 0)] + [("step_in_backward_ms" + (f"@{g}" if g else ""), True, g)
+                                            for g in args.grids]
+        for name, flag, g in runs:
+            mode(flag)
+            zdp.fused["grid"] = g
+            for _ in range(args.warmup):
+                step()
+            res[name] = round(timed(step, args.steps, dev), 2)
+    comm.check()
+    best = min((k for k in res if k.startswith("step_in_backward_ms")), key=lambda k: res[k])
+    res["step_in_backward_ms"] = res[best]
+    res["best_grid"] = best.partition("@")[2] or "default"
+    res["optimizer_exposed_ms"] = round(res["step_in_backward_ms"] - res["backward_ms"], 2)
+    res["serial_optimizer_ms"] = round(res["serial_ms"] - res["backward_ms"], 2)
+    res["speedup"] = round(res["serial_ms"] / res["step_in_backward_ms"], 2)
+    res["backward_tflops"] = round(bwd.flops() / (res["backward_ms"] / 1e3) / 1e12, 1)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--layers", type=int, default=32, help="transformer layers (32 = the full 8.03 B model)")
     ap.add_argument("--bucket-mib", type=int, default=256)
-    ap.add_argument("--mode", choices=["fused", "unfused", "both"], default="both")
+    ap.add_argument("--mode", choices=["fused", "unfused", "both", "train"], default="both")
+    ap.add_argument("--tokens", type=int, default=1024, help="train: rows of the synthetic backward GEMMs")
+    ap.add_argument("--grids", type=int, nargs="+", default=[0], help="train: fused-launch workgroups to try (0 = default)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     args = ap.parse_args()
     rank, world, local = init_distributed("nccl")
     dev = torch.device("cuda", local)
     dt = torch.bfloat16
+    hp = dict(lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    if args.mode == "train":
+        train(args, rank, world, dev, dt, hp)
+        return
     shapes = llama3_8b_shapes(args.layers)
     total = sum(numel(s) for _, s in shapes)
     per_bucket = (args.bucket_mib << 20) // 2
@@ -70,7 +131,6 @@ def main() -> None:
     comm = XgmiCommunicator(slot_bytes=-(-(args.bucket_mib << 20) // world) + (1 << 20))
     params = [fill_uniform(torch.empty(n, dtype=dt, device=dev), seed=1000 + i) for i, n in enumerate(sizes)]
     grads = [fill_uniform(torch.empty(n, dtype=dt, device=dev), seed=2000 + i + rank) for i, n in enumerate(sizes)]
-    hp = dict(lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
     res = {"metric": "sharded_dp_optimizer_step_ms", "model": f"llama3_8b ({args.layers} layers)", "params": total,
            "n_gpus": world, "buckets": len(sizes), "bucket_mib": args.bucket_mib, "dtype": "bf16 params, fp32 state"}
 
