@@ -19,7 +19,7 @@ from typing import Callable, Iterable
 import numpy as np
 
 from ._native import C
-from .protocol import AllReduceInput, CompleteAllreduce, ReduceBlock, ScatterBlock
+from .protocol import AllReduceInput, ReduceBlock, ScatterBlock
 
 
 class ExpectationError(AssertionError):

@@ -158,11 +158,18 @@ void ClusterNode::listen() {
 }
 
 void ClusterNode::leave() {
-  if (!joined_.load() || stopping_.load()) return;
-  const std::string lead = leader();
+  if (stopping_.load() || leaving_.exchange(true)) return;
   Writer w;
   w.u8(static_cast<uint8_t>(FrameKind::Leave));
   w.str(address_);
+  if (!joined_.load()) {
+    // a seed may already list this node while its Welcome is still in flight: every seed that
+    // admitted it removes it, the others ignore the frame (unknown member)
+    for (auto& s : cfg_.seed_nodes)
+      if (s != address_) send_frame(s, w.bytes());
+    return;
+  }
+  const std::string lead = leader();
   if (!lead.empty() && lead != address_) {
     send_frame(lead, w.bytes());
   } else {
@@ -549,6 +556,7 @@ void ClusterNode::handle_frame(const uint8_t* p, size_t n) {
       break;
     }
     case FrameKind::Welcome: {
+      if (leaving_.load()) break;  // admitted after leave(): the Leave sent to the seeds undoes it
       const uint32_t cnt = r.u32();
       std::vector<MemberInfo> fresh;
       {
@@ -617,6 +625,7 @@ void ClusterNode::ticker_loop() {
     while (!stopping_.load() && Clock::now() < until) std::this_thread::sleep_for(std::chrono::milliseconds(20));
     if (stopping_.load()) break;
     if (!joined_.load()) {
+      if (leaving_.load()) continue;
       Writer w;
       w.u8(static_cast<uint8_t>(FrameKind::Join));
       encode_member(w, MemberInfo{address_, cfg_.roles, uid_, MemberStatus::Joining});

@@ -132,6 +132,7 @@ class ClusterNode : public std::enable_shared_from_this<ClusterNode>, public Ref
   uint64_t uid_ = 0;
   std::atomic<bool> stopping_{false};
   std::atomic<bool> joined_{false};
+  std::atomic<bool> leaving_{false};  // leave() was called: never (re-)join
   std::thread accept_thread_, ticker_thread_;
   std::mutex readers_mu_;
   std::vector<std::thread> readers_;

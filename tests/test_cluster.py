@@ -5,7 +5,6 @@ import threading
 import time
 
 import numpy as np
-import pytest
 
 from akka_allreduce_1_amd._native import C
 from akka_allreduce_1_amd.parallel.comm import free_port

@@ -4,7 +4,6 @@ native WorkerCore through the deterministic TestKit. The probe impersonates ever
 and the master; the test injects the other peers' traffic by hand.
 """
 import numpy as np
-import pytest
 
 from akka_allreduce_1_amd.protocol import (CompleteAllreduce, InitWorkers, ReduceBlock, ScatterBlock,
                                            StartAllreduce)
