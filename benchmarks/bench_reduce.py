@@ -49,6 +49,8 @@ def main() -> None:
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--variants", type=int, nargs="*", default=[],
                     help="also time these reduce_slots kernel variants (kernels.hip launch_reduce_typed)")
+    ap.add_argument("--pad-kib", type=int, default=0,
+                    help="pad every slot row by this much (slot stride not a power of two)")
     args = ap.parse_args()
     dt = torch.float32 if args.dtype == "fp32" else torch.bfloat16
     es = 4 if dt == torch.float32 else 2
@@ -65,12 +67,13 @@ def main() -> None:
     del src, dst
     rows = []
     for P in args.slots:
-        slots = torch.empty(P, n, dtype=dt, device=dev)
+        pad = (args.pad_kib << 10) // es
+        slots = torch.empty(P, n + pad, dtype=dt, device=dev)[:, :n]
         for p in range(P):
             fill_uniform(slots[p], seed=p)
         # correctness: one in-place launch vs an fp32 torch reference
         ref = slots.float().sum(0)
-        work = slots.clone()
+        work = slots.contiguous().clone()
         reduce_slots(work, out=work[0])
         err = (work[0].float() - ref).abs().max().item()
         del work, ref
@@ -88,7 +91,7 @@ def main() -> None:
         for name, fn in cases.items():
             t = time_ms(fn, args.iters)
             hbm = (P + 1) * nbytes / (t / 1e3) / 1e12
-            rows.append({"case": name, "P": P, "dtype": args.dtype, "bytes_per_slot": nbytes, "ms": round(t, 4),
+            rows.append({"case": name, "P": P, "pad_kib": args.pad_kib, "dtype": args.dtype, "bytes_per_slot": nbytes, "ms": round(t, 4),
                          "algbw_GBps": round(nbytes / (t / 1e3) / 1e9, 1), "hbm_TBps": round(hbm, 3),
                          "frac_of_copy_roofline": round(hbm / copy_rate, 3),
                          **({"max_abs_err_vs_fp32": err} if name == "mxar_inplace" else {})})

@@ -161,6 +161,12 @@ static void launch_reduce_typed(int v, int P, const char* s, int64_t stride, cha
     case 1: launch_static<E, 2, false>(P, s, stride, o, n, scale, grid(2), st); break;
     case 2: launch_static<E, 2, true>(P, s, stride, o, n, scale, grid(2), st); break;
     case 3: launch_static<E, 4, true>(P, s, stride, o, n, scale, grid(4), st); break;
+    case 5: launch_static<E, 2, true>(P, s, stride, o, n, scale, grid(2), st); break;
+    case 6: launch_static<E, 8, true>(P, s, stride, o, n, scale, grid(8), st); break;
+    case 7:  // U by slot count: ~ the same bytes in flight per lane for every P
+      if (P > 4) launch_static<E, 2, true>(P, s, stride, o, n, scale, grid(2), st);
+      else launch_static<E, 4, true>(P, s, stride, o, n, scale, grid(4), st);
+      break;
     default: launch_static<E, 4, false>(P, s, stride, o, n, scale, grid(4), st); break;
   }
 }

@@ -190,7 +190,7 @@ class XgmiComm {
                           int* gx) const;
 
   int rank_, world_, device_, grid_, rows_;
-  int64_t slot_bytes_, maxch_, off_S_, off_R_, off_B_, slab_bytes_;
+  int64_t slot_bytes_, slot_stride_, maxch_, off_S_, off_R_, off_B_, slab_bytes_;
   int64_t ll_max_ = 0, ll_slot_ = 0, off_LL_ = 0;
   int64_t alloc_bytes_ = 0;  // slab_bytes_ padded around the IPC size bug (constructor)
   int delay_rank_ = -1;

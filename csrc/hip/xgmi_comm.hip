@@ -329,7 +329,14 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   // [F1: rows x P x maxch][F2: rows x P x maxch][FB: P][PROG: P][F2C: rows x P x maxch]
   const int64_t flag_bytes = (3 * rows_ * world_ * maxch_ + 2 * world_) * 4;
   off_S_ = round_up(flag_bytes, 64 * 1024);
-  off_R_ = off_S_ + rows_ * world_ * slot_bytes_;
+  // Slots sit slot_stride_ apart: capacity + a 64 KiB pad, so the P slots a reduce reads at
+  // the same offset are not a power of two apart. At a power-of-two stride they map onto the
+  // same HBM channels: 8-slot fp32 reduce 5.49 TB/s unpadded vs 6.02 TB/s with the pad
+  // (benchmarks/bench_reduce.py --pad-kib, profiles/reduce_kernel.md).
+  int64_t pad = 64 * 1024;
+  if (const char* e = std::getenv("MXAR_SLOT_PAD")) pad = round_up(std::max<int64_t>(0, std::atoll(e)), 4096);
+  slot_stride_ = slot_bytes_ + pad;
+  off_R_ = off_S_ + rows_ * world_ * slot_stride_;
   off_B_ = 2 * rows_ * world_ * maxch_ * 4;
   // low-latency one-shot slots: [2 parities][P sources] x ll_slot (two 8-B LL words per
   // 16-B store: ll_slot = 2 x payload)
@@ -337,7 +344,7 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   if (const char* e = std::getenv("MXAR_LL_MAX")) ll_max_ = std::max<int64_t>(0, std::atoll(e));
   ll_max_ = round_up(ll_max_, 16);
   ll_slot_ = round_up(std::max<int64_t>(2 * ll_max_, 16), 64 * 1024);
-  off_LL_ = off_R_ + rows_ * world_ * slot_bytes_;
+  off_LL_ = off_R_ + rows_ * world_ * slot_stride_;
   slab_bytes_ = off_LL_ + 2 * world_ * ll_slot_;
   // Allocation size: on this ROCm stack hipIpcOpenMemHandle of an allocation whose size has
   // bit 31 set (2-4 GiB, 6-8 GiB, ...) never returns in the importing process, while the
@@ -500,7 +507,8 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   a.maxch = c0.maxch_;
   a.off_S = c0.off_S_;
   a.off_R = c0.off_R_;
-  a.slot_bytes = c0.slot_bytes_;
+  a.slot_bytes = c0.slot_stride_;
+  a.slot_cap = c0.slot_bytes_;
   a.timeout = static_cast<uint64_t>(c0.timeout_s_ * 1e8);
   for (int k = 0; k < W; ++k) a.base[k] = c0.peers_[k];
   const int64_t min_chunk = min_chunk_bytes() / es;
@@ -769,7 +777,8 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
   a.maxch = c0.maxch_;
   a.off_S = c0.off_S_;
   a.off_R = c0.off_R_;
-  a.slot_bytes = c0.slot_bytes_;
+  a.slot_bytes = c0.slot_stride_;
+  a.slot_cap = c0.slot_bytes_;
   a.timeout = static_cast<uint64_t>(c0.timeout_s_ * 1e8);
   a.fence = c0.fence_;
   a.scale = scale;
@@ -896,7 +905,8 @@ void XgmiComm::run_coll(const std::vector<XgmiComm*>& group, Coll op, const std:
     a.maxch = c0.maxch_;
     a.off_S = c0.off_S_;
     a.off_R = c0.off_R_;
-    a.slot_bytes = c0.slot_bytes_;
+    a.slot_bytes = c0.slot_stride_;
+    a.slot_cap = c0.slot_bytes_;
     a.timeout = static_cast<uint64_t>(c0.timeout_s_ * 1e8);
     a.fence = c0.fence_;
     a.scale = scale;

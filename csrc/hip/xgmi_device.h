@@ -30,7 +30,8 @@ struct CommArgs {
   int fence;      // bit0: system release before flags, bit1: system acquire after waits
   float scale;    // applied to the fp32 sum before rounding (1 = sum, 1/P = mean)
   int64_t maxch;
-  int64_t off_S, off_R, slot_bytes;
+  int64_t off_S, off_R, slot_bytes;  // slot_bytes: the slot STRIDE in the slab (capacity + pad)
+  int64_t slot_cap;                   // usable bytes per slot
   uint64_t timeout;
   char* base[kMaxRanks];
   // threshold kernel (xgmi_threshold.hip); rows = 1 for the other kernels
@@ -71,7 +72,7 @@ __device__ __forceinline__ int64_t clamp_len(int64_t avail, int64_t cap) {
 // so no peer hangs and nothing is written out of bounds. Wave-uniform scalar compares.
 __device__ __forceinline__ bool unit_in_bounds(const CommArgs& a, int64_t off, int64_t bytes, int64_t flag,
                                                uint32_t* err) {
-  const bool ok = off >= 0 && bytes >= 0 && off + bytes <= a.slot_bytes && flag >= 0 && flag < a.maxch;
+  const bool ok = off >= 0 && bytes >= 0 && off + bytes <= a.slot_cap && flag >= 0 && flag < a.maxch;
   if (!ok && threadIdx.x == 0) __hip_atomic_fetch_or(err, ERR_BAD_ARGS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   return ok;
 }
