@@ -364,6 +364,12 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   hip_check(hipSetDevice(device_), "hipSetDevice");
   const char* mem = std::getenv("MXAR_SLAB_MEM");
   const std::string kind = mem ? mem : "fine";
+  // study knobs that trade away correctness guarantees: say so once per communicator
+  if (fence_ != 3 || kind != "fine" || std::getenv("MXAR_IPC_NO_PAD"))
+    std::fprintf(stderr,
+                 "[mxar] WARNING rank %d: study settings active (MXAR_FENCE=%d, MXAR_SLAB_MEM=%s%s); "
+                 "results may be wrong - use the defaults in production\n",
+                 rank_, fence_, kind.c_str(), std::getenv("MXAR_IPC_NO_PAD") ? ", MXAR_IPC_NO_PAD" : "");
   if (kind == "coarse") {
     hip_check(hipMalloc(reinterpret_cast<void**>(&slab_), alloc_bytes_), "hipMalloc(slab)");
   } else {
