@@ -60,9 +60,6 @@ def _current_stream(device_index: int) -> int:
     return torch.cuda.current_stream(device_index).cuda_stream
 
 
-_STATE_PAD_ELEMS = 16384  # 64 KiB of fp32 between the fused-AdamW state streams
-
-
 def comm_stream(device) -> "torch.cuda.Stream":
     """Side stream for collectives overlapped with compute (gradient buckets, fused optimizer
     steps). High priority on purpose: HIP hands out hardware queues to streams round-robin
@@ -435,16 +432,10 @@ class XgmiCommunicator:
         """Fresh fp32 shard state for `step_adamw`: master = this rank's block of params."""
         b = self.shard_len(params.numel(), params.dtype)
         lo, hi = self.rank * b, min(params.numel(), (self.rank + 1) * b)
-        # one allocation, the three streams 64 KiB off a power-of-two spacing: the kernel reads
-        # and writes all three at the same index, and equal-sized separate allocations tend to
-        # sit a power of two apart, on the same HBM channels (profiles/reduce_kernel.md). A
-        # precaution: Llama-3-8B fused step 47.1 -> 46.7 ms on one GPU, within noise
-        pad = _STATE_PAD_ELEMS
-        buf = torch.zeros(3 * (b + pad), dtype=torch.float32, device=self.device)
-        master, exp_avg, exp_avg_sq = (buf[k * (b + pad):k * (b + pad) + b] for k in range(3))
+        master = torch.zeros(b, dtype=torch.float32, device=self.device)
         if hi > lo:
             master[:hi - lo].copy_(params.view(-1)[lo:hi].float())
-        return {"master": master, "exp_avg": exp_avg, "exp_avg_sq": exp_avg_sq}
+        return {"master": master, "exp_avg": torch.zeros_like(master), "exp_avg_sq": torch.zeros_like(master)}
 
     def reset(self) -> None:
         """Recover after a CommError (a peer missed a deadline): every rank calls this

@@ -88,6 +88,11 @@ def main() -> None:
                 C.hip.set_reduce_variant(v)
                 reduce_slots(slots, out=out)
             cases[f"variant{v}_outofplace"] = run_v
+
+            def run_vi(v=v):
+                C.hip.set_reduce_variant(v)
+                reduce_slots(slots, out=slots[0])
+            cases[f"variant{v}_inplace"] = run_vi
         for name, fn in cases.items():
             t = time_ms(fn, args.iters)
             hbm = (P + 1) * nbytes / (t / 1e3) / 1e12

@@ -35,10 +35,11 @@ static int grid_for(int64_t packs) {
 // U x 4 KiB per slot (one 1 KiB wave access per pack), tiles dealt grid-stride.
 // P is a template parameter for 2..8 slots so every slot's loads of a tile are issued
 // before the first add (P*U*16 bytes in flight per lane); the sum still runs in peer
-// order 0..P-1. NT = nontemporal loads/stores (streaming data, no reuse).
+// order 0..P-1. NT bit 0 = nontemporal loads, bit 1 = nontemporal stores (streaming data,
+// no reuse).
 // out may alias one slot row (in-place reduce): every element is read and written by the
 // same lane, loads before the store.
-template <class E, int U, int P, bool NT>
+template <class E, int U, int P, int NT>
 __global__ __launch_bounds__(kThreads) void reduce_slots_static(const char* __restrict__ slots, int64_t stride_bytes,
                                                                 char* out, int64_t n, float scale) {
   constexpr int64_t kTile = static_cast<int64_t>(U) * kThreads;
@@ -52,7 +53,7 @@ __global__ __launch_bounds__(kThreads) void reduce_slots_static(const char* __re
       const Pack16* s = reinterpret_cast<const Pack16*>(slots + p * stride_bytes);
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        v[p][u] = NT ? __builtin_nontemporal_load(s + base + u * kThreads) : s[base + u * kThreads];
+        v[p][u] = (NT & 1) ? __builtin_nontemporal_load(s + base + u * kThreads) : s[base + u * kThreads];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -62,7 +63,7 @@ __global__ __launch_bounds__(kThreads) void reduce_slots_static(const char* __re
       for (int p = 0; p < P; ++p) a.add(v[p][u]);
       if (scale != 1.f) a.scale(scale);
       Pack16* d = reinterpret_cast<Pack16*>(out) + base + u * kThreads;
-      if (NT)
+      if (NT & 2)
         __builtin_nontemporal_store(a.pack(), d);
       else
         *d = a.pack();
@@ -133,7 +134,7 @@ static int g_reduce_variant = -1;  // -1: default (see launch_reduce_slots)
 
 void set_reduce_variant(int v) { g_reduce_variant = v; }
 
-template <class E, int U, bool NT>
+template <class E, int U, int NT>
 static void launch_static(int P, const char* s, int64_t stride, char* o, int64_t n, float scale, int g,
                           hipStream_t st) {
 #define MXAR_RS(PP)                                                                                            \
@@ -158,16 +159,18 @@ static void launch_reduce_typed(int v, int P, const char* s, int64_t stride, cha
   switch (v) {
     case 0: hipLaunchKernelGGL(reduce_slots_kernel<E>, dim3(grid(2)), dim3(kThreads), 0, st, s, stride, P, o, n, scale);
       break;
-    case 1: launch_static<E, 2, false>(P, s, stride, o, n, scale, grid(2), st); break;
-    case 2: launch_static<E, 2, true>(P, s, stride, o, n, scale, grid(2), st); break;
-    case 3: launch_static<E, 4, true>(P, s, stride, o, n, scale, grid(4), st); break;
-    case 5: launch_static<E, 2, true>(P, s, stride, o, n, scale, grid(2), st); break;
-    case 6: launch_static<E, 8, true>(P, s, stride, o, n, scale, grid(8), st); break;
+    case 1: launch_static<E, 2, 0>(P, s, stride, o, n, scale, grid(2), st); break;
+    case 2: launch_static<E, 2, 3>(P, s, stride, o, n, scale, grid(2), st); break;
+    case 3: launch_static<E, 4, 3>(P, s, stride, o, n, scale, grid(4), st); break;
+    case 5: launch_static<E, 2, 3>(P, s, stride, o, n, scale, grid(2), st); break;
+    case 6: launch_static<E, 8, 3>(P, s, stride, o, n, scale, grid(8), st); break;
     case 7:  // U by slot count: ~ the same bytes in flight per lane for every P
-      if (P > 4) launch_static<E, 2, true>(P, s, stride, o, n, scale, grid(2), st);
-      else launch_static<E, 4, true>(P, s, stride, o, n, scale, grid(4), st);
+      if (P > 4) launch_static<E, 2, 3>(P, s, stride, o, n, scale, grid(2), st);
+      else launch_static<E, 4, 3>(P, s, stride, o, n, scale, grid(4), st);
       break;
-    default: launch_static<E, 4, false>(P, s, stride, o, n, scale, grid(4), st); break;
+    case 8: launch_static<E, 4, 1>(P, s, stride, o, n, scale, grid(4), st); break;  // NT loads only
+    case 9: launch_static<E, 4, 2>(P, s, stride, o, n, scale, grid(4), st); break;  // NT stores only
+    default: launch_static<E, 4, 0>(P, s, stride, o, n, scale, grid(4), st); break;
   }
 }
 

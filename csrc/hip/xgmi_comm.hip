@@ -329,11 +329,11 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   // [F1: rows x P x maxch][F2: rows x P x maxch][FB: P][PROG: P][F2C: rows x P x maxch]
   const int64_t flag_bytes = (3 * rows_ * world_ * maxch_ + 2 * world_) * 4;
   off_S_ = round_up(flag_bytes, 64 * 1024);
-  // Slots sit slot_stride_ apart: capacity + a 64 KiB pad, so the P slots a reduce reads at
-  // the same offset are not a power of two apart. At a power-of-two stride they map onto the
-  // same HBM channels: 8-slot fp32 reduce 5.49 TB/s unpadded vs 6.02 TB/s with the pad
-  // (benchmarks/bench_reduce.py --pad-kib, profiles/reduce_kernel.md).
-  int64_t pad = 64 * 1024;
+  // Slots sit slot_stride_ = capacity + MXAR_SLOT_PAD bytes apart (default 0). A pad takes the
+  // P slots a reduce reads at one offset off a power-of-two spacing; an A/B on one box showed
+  // no gain for the reduce kernel (benchmarks/bench_reduce.py --pad-kib, profiles/reduce_kernel.md),
+  // so the knob stays for study.
+  int64_t pad = 0;
   if (const char* e = std::getenv("MXAR_SLOT_PAD")) pad = round_up(std::max<int64_t>(0, std::atoll(e)), 4096);
   slot_stride_ = slot_bytes_ + pad;
   off_R_ = off_S_ + rows_ * world_ * slot_stride_;
