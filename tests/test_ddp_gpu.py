@@ -148,3 +148,13 @@ def test_sharded_data_parallel_xgmi_two_processes(fused):
             p.kill()
     bad = [r for r in res if not r[1]]
     assert not bad, bad[0][2]
+
+
+def test_comm_stream_has_priority_over_compute():
+    """Side streams for overlapped collectives are high priority: a normal-priority stream can
+    share the compute stream's hardware queue and then serialises with it
+    (profiles/zero_step_in_backward.md)."""
+    from akka_allreduce_1_amd.parallel.comm import comm_stream
+
+    s = comm_stream(torch.device("cuda", 0))
+    assert s.priority < torch.cuda.current_stream(0).priority
