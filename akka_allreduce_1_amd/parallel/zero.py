@@ -222,6 +222,44 @@ class ShardedDataParallel:
         self._next = 0
         self.stats["steps"] += 1
 
+    # ------------------------------------------------------------------ checkpoint / resume
+    def state_dict(self) -> dict:
+        """This rank's shard of the optimizer state, for resume (the reference
+        checkpoints nothing; its master restarts at round 0). Parameters are not included -
+        every rank holds them in full, so save `module.state_dict()` once. Tensors are
+        references, as in `torch.optim.Optimizer.state_dict`; `torch.save` one file per rank
+        and reload with `torch.load(..., weights_only=True)`."""
+        sd = {"world": self.world, "rank": self.rank, "step": self._t, "steps": self.stats["steps"],
+              "layout": [[b.numel, str(b.dtype), len(b.params)] for b in self.buckets]}
+        if self.fused is not None:
+            sd["adamw"] = [{k: st[k] for k in ("master", "exp_avg", "exp_avg_sq")} for st in self.adamw_states]
+        else:
+            sd["optimizer"] = self.optimizer.state_dict()
+        return sd
+
+    def load_state_dict(self, sd: dict) -> None:
+        """Resume from `state_dict()` of the same rank of a run with the same parameters,
+        bucket_bytes, world size and optimizer kind."""
+        layout = [[b.numel, str(b.dtype), len(b.params)] for b in self.buckets]
+        if (sd.get("world"), sd.get("rank")) != (self.world, self.rank):
+            raise ValueError(f"checkpoint of rank {sd.get('rank')}/{sd.get('world')}, this is {self.rank}/{self.world}")
+        if [list(x) for x in sd.get("layout", [])] != layout:
+            raise ValueError("checkpoint bucket layout differs (parameters or bucket_bytes changed)")
+        if self.fused is not None:
+            if "adamw" not in sd:
+                raise ValueError("checkpoint has no fused AdamW state")
+            for st, saved in zip(self.adamw_states, sd["adamw"]):
+                for k in ("master", "exp_avg", "exp_avg_sq"):
+                    if saved[k].shape != st[k].shape:
+                        raise ValueError(f"{k}: shape {tuple(saved[k].shape)} != {tuple(st[k].shape)}")
+                    st[k].copy_(saved[k])
+        else:
+            if "optimizer" not in sd:
+                raise ValueError("checkpoint has no optimizer state")
+            self.optimizer.load_state_dict(sd["optimizer"])
+        self._t = int(sd["step"])
+        self.stats["steps"] = int(sd["steps"])
+
     def zero_grad(self) -> None:
         for b in self.buckets:
             b.flat_grad.zero_()

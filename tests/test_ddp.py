@@ -149,3 +149,73 @@ def test_sharded_data_parallel_matches_full_optimizer_gloo():
         p.join(timeout=30)
     bad = [r for r in res if not r[1]]
     assert not bad, bad[0][2]
+
+
+def _resume_worker(rank, world, port, q, path):
+    """Train 3 steps, checkpoint (model once + one optimizer shard per rank), train 2 more;
+    a fresh model + ShardedDataParallel loaded from the checkpoint must reproduce those 2."""
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.parallel import ShardedDataParallel
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def make(ps):
+            return torch.optim.Adam(ps, lr=0.01)
+        data = [torch.randn(4, 7, generator=torch.Generator().manual_seed(300 + s)) for s in range(5)]
+
+        def train(m, zdp, steps):
+            for s in steps:
+                zdp.zero_grad()
+                m(data[s] * (rank + 1)).pow(2).sum().backward()
+                zdp.step()
+
+        m = _model(0)
+        zdp = ShardedDataParallel(m, TorchDistComm(), make, bucket_bytes=300)
+        train(m, zdp, range(3))
+        if rank == 0:
+            torch.save(m.state_dict(), os.path.join(path, "model.pt"))
+        torch.save(zdp.state_dict(), os.path.join(path, f"optim_rank{rank}.pt"))
+        dist.barrier()
+        train(m, zdp, range(3, 5))
+
+        m2 = _model(1)  # different init: everything must come from the checkpoint
+        m2.load_state_dict(torch.load(os.path.join(path, "model.pt"), weights_only=True))
+        zdp2 = ShardedDataParallel(m2, TorchDistComm(), make, bucket_bytes=300)
+        zdp2.load_state_dict(torch.load(os.path.join(path, f"optim_rank{rank}.pt"), weights_only=True))
+        assert zdp2.stats["steps"] == 3
+        train(m2, zdp2, range(3, 5))
+        for p, p2 in zip(m.parameters(), m2.parameters()):
+            assert torch.equal(p, p2)
+        bad = dict(zdp2.state_dict(), rank=(rank + 1) % world)
+        try:
+            zdp.load_state_dict(bad)
+            raise AssertionError("a checkpoint of another rank must be refused")
+        except ValueError:
+            pass
+        zdp.remove_hooks()
+        zdp2.remove_hooks()
+        q.put((rank, True, ""))
+    except Exception:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, False, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_checkpoint_resume_gloo(tmp_path):
+    from akka_allreduce_1_amd.parallel.comm import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_resume_worker, args=(r, 2, port, q, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=30)
+    bad = [r for r in res if not r[1]]
+    assert not bad, bad[0][2]

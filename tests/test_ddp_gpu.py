@@ -120,6 +120,28 @@ def _zero_worker(rank, world, port, q, fused=False):
                 assert err <= 1e-5, (step, err)
         if fused:
             assert comm.native.stats.adamw == 3 * len(zdp.buckets)
+            # resume: a fresh model + ShardedDataParallel loaded from a checkpoint of this state
+            # takes the same next step as the original
+            import copy
+
+            saved, msaved = copy.deepcopy(zdp.state_dict()), copy.deepcopy(m.state_dict())
+
+            def one(mm, zz):
+                zz.zero_grad()
+                mm(data[rank] * 2).pow(2).mean().backward()
+                zz.step()
+                comm.check()
+
+            one(m, zdp)
+            m2 = _model(1, torch.float32)
+            m2.load_state_dict(msaved)
+            zdp2 = ShardedDataParallel(m2, comm, None, bucket_bytes=32 << 10,
+                                       fused_adamw={"lr": 1e-3, "betas": (0.9, 0.999), "eps": 1e-8,
+                                                    "weight_decay": 0.0}, step_in_backward=fused == "backward")
+            zdp2.load_state_dict(saved)
+            one(m2, zdp2)
+            for p, p2 in zip(m.parameters(), m2.parameters()):
+                assert (p - p2).abs().max().item() <= 1e-6
         else:
             assert comm.native.stats.coll >= 2 * 3 * len(zdp.buckets)  # RS + AG per bucket per step on xGMI
         q.put((rank, True, ""))
