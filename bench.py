@@ -31,8 +31,15 @@ if "--share-device" in sys.argv:
     # process keeps every rank's kernel on the device at once. Set before HIP initialises.
     os.environ["GPU_MAX_HW_QUEUES"] = "1"
 
-import torch
-import torch.distributed as dist
+# Library banners (RCCL's version block, gloo's "connected to N peer ranks") are written to
+# fd 1 from native code; keep stdout for the ONE result line: fd 1 -> stderr for the whole
+# run, the result goes to a private copy of the original stdout.
+sys.stdout.flush()
+_RESULT_FD = os.dup(1)
+os.dup2(2, 1)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -358,7 +365,9 @@ def main() -> None:
         result["sweep"] = sweep
 
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        sys.stdout.flush()
+        with os.fdopen(_RESULT_FD, "w") as out:
+            out.write(json.dumps(result) + "\n")
     dist.barrier()
     dist.destroy_process_group()
 
