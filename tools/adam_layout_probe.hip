@@ -12,6 +12,8 @@
 #include <cstdlib>
 #include <vector>
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 #define CK(x)                                                                        \
   do {                                                                               \
     hipError_t e = (x);                                                              \
@@ -40,12 +42,19 @@ __device__ __forceinline__ uint16_t tobf(float f) {
 }
 
 // 8 params per lane per iteration (one 16-byte bf16 grad pack), workgroup-contiguous tiles
+template <bool NT>
 __global__ __launch_bounds__(kThreads) void soa(const uint4* g, float4* p, float4* m, float4* v, uint4* out,
                                                 int64_t npk) {
   const int64_t per = (npk + gridDim.x - 1) / gridDim.x;
   const int64_t beg = blockIdx.x * per, end = beg + per < npk ? beg + per : npk;
   for (int64_t i = beg + threadIdx.x; i < end; i += kThreads) {
-    const uint4 gg = g[i];
+    uint4 gg;
+    if (NT) {
+      const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(g) + i);
+      gg = make_uint4(t.x, t.y, t.z, t.w);
+    } else {
+      gg = g[i];
+    }
     float4 P[2] = {p[2 * i], p[2 * i + 1]}, M[2] = {m[2 * i], m[2 * i + 1]}, V[2] = {v[2 * i], v[2 * i + 1]};
     const uint32_t w[4] = {gg.x, gg.y, gg.z, gg.w};
     float* pp = reinterpret_cast<float*>(P);
@@ -56,8 +65,12 @@ __global__ __launch_bounds__(kThreads) void soa(const uint4* g, float4* p, float
     for (int e = 0; e < 8; ++e)
       o[e] = tobf(adamw(bf(static_cast<uint16_t>(w[e / 2] >> (16 * (e & 1)))), pp[e], mm[e], vv[e]));
     p[2 * i] = P[0], p[2 * i + 1] = P[1], m[2 * i] = M[0], m[2 * i + 1] = M[1], v[2 * i] = V[0], v[2 * i + 1] = V[1];
-    out[i] = make_uint4(o[0] | (uint32_t(o[1]) << 16), o[2] | (uint32_t(o[3]) << 16), o[4] | (uint32_t(o[5]) << 16),
-                        o[6] | (uint32_t(o[7]) << 16));
+    const uint4 ov = make_uint4(o[0] | (uint32_t(o[1]) << 16), o[2] | (uint32_t(o[3]) << 16),
+                                o[4] | (uint32_t(o[5]) << 16), o[6] | (uint32_t(o[7]) << 16));
+    if (NT)
+      __builtin_nontemporal_store(u32x4{ov.x, ov.y, ov.z, ov.w}, reinterpret_cast<u32x4*>(out) + i);
+    else
+      out[i] = ov;
   }
 }
 
@@ -110,12 +123,14 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   const double bytes = 28.0 * n;
-  for (int grid : {512, 1024, 2048, 4096}) {
+  for (int grid : {256, 512, 1024}) {
     for (int rep = 0; rep < 2; ++rep) {
-      for (int layout = 0; layout < 2; ++layout) {
+      for (int layout = 0; layout < 3; ++layout) {
         auto run = [&] {
           if (layout == 0)
-            hipLaunchKernelGGL(soa, dim3(grid), dim3(kThreads), 0, 0, g, p, m, v, out, npk);
+            hipLaunchKernelGGL(soa<false>, dim3(grid), dim3(kThreads), 0, 0, g, p, m, v, out, npk);
+          else if (layout == 2)
+            hipLaunchKernelGGL(soa<true>, dim3(grid), dim3(kThreads), 0, 0, g, p, m, v, out, npk);
           else
             hipLaunchKernelGGL(aos, dim3(grid), dim3(kThreads), 0, 0, g, st, out, npk);
         };
@@ -134,7 +149,7 @@ int main(int argc, char** argv) {
         std::sort(ts.begin(), ts.end());
         const float med = ts[ts.size() / 2];
         std::printf("{\"layout\": \"%s\", \"grid\": %d, \"rep\": %d, \"params\": %lld, \"ms\": %.3f, \"TBps\": %.2f}\n",
-                    layout ? "aos" : "soa", grid, rep, static_cast<long long>(n), med, bytes / med / 1e9);
+                    layout == 2 ? "soa_nt_grad_out" : layout ? "aos" : "soa", grid, rep, static_cast<long long>(n), med, bytes / med / 1e9);
         std::fflush(stdout);
       }
     }
