@@ -14,6 +14,12 @@ of the slowest rank (nccl-tests convention, reported as `algbw_per_rank`); `valu
 whole-job aggregate the driver contract asks for = N x per-rank algbw (gradient bytes reduced
 per second by the job). At N=1 an allreduce is an out-of-place copy, so the N=1 point is an
 HBM copy rate, not a communication rate. Data: synthetic uniform(-1, 1) gradients.
+
+After the headline, side sections on the same engine (in the JSON, not in `value`): the
+tuner's size sweep vs RCCL, the straggler-tolerant kernel, all-to-all / all-gather /
+reduce-scatter, the fused sharded AdamW step, and `dp` = BASELINE configs 4 and 5 (one
+data-parallel step of the ResNet-50 and full Llama-3-8B gradient sets with a GEMM-backed
+synthetic backward overlapped with the bucketed reducer).
 """
 from __future__ import annotations
 
@@ -21,6 +27,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 if "--share-device" in sys.argv:
@@ -182,6 +189,64 @@ def fused_step(comm: XgmiCommunicator, grads: torch.Tensor, params: torch.Tensor
     return row
 
 
+def dp_step(comm: XgmiCommunicator, model: str, dev) -> dict:
+    """BASELINE configs 4 / 5 on the same engine: one data-parallel step of a gradient set
+    (ResNet-50: 25.6 M params in 161 tensors; Llama-3-8B: 8.03 B params, 16.06 GB bf16),
+    every gradient produced by a real GEMM in autograd order while the bucketed reducer
+    allreduces full buckets on its own stream, then an SGD update (benchmarks/bench_dp.py has
+    the full breakdown). exposed = step - compute-only step; comm_only = every bucket's
+    allreduce back to back."""
+    from akka_allreduce_1_amd.models.grad_sets import gradient_shapes, numel
+    from akka_allreduce_1_amd.parallel import BucketedGradReducer
+    from benchmarks.bench_dp import SyntheticBackward
+
+    row: dict = {}
+    params = reducer = bwd = grads = None
+    try:
+        shapes = gradient_shapes(model)
+        params = [torch.nn.Parameter(torch.zeros(sh, dtype=torch.bfloat16, device=dev)) for _, sh in shapes]
+        big = model == "llama3_8b"
+        # 64 MiB buckets for the 16 GB set; torch DDP's 25 MiB for ResNet-50 (2 buckets: the
+        # first one overlaps the rest of backward)
+        reducer = BucketedGradReducer(params, comm, bucket_bytes=(64 if big else 25) << 20, op="avg")
+        reducer.remove_hooks()  # the synthetic backward calls the hook itself
+        bwd = SyntheticBackward(params, 1024, torch.bfloat16, dev)
+        grads = [q.grad for q in params]
+        steps, warm = (3, 1) if big else (10, 3)
+
+        def overlap():
+            bwd.run(reducer)
+            reducer.wait()
+            torch._foreach_add_(params, grads, alpha=-1e-3)
+
+        def compute():
+            bwd.run(None)
+            torch._foreach_add_(params, grads, alpha=-1e-3)
+
+        def comm_only():
+            for b in reducer.buckets:
+                comm.allreduce_(b.buffer, op="avg")
+
+        with torch.no_grad():
+            t = {}
+            for name, fn in (("step", overlap), ("compute", compute), ("comm", comm_only)):
+                for _ in range(warm):
+                    fn()
+                t[name] = max_over_ranks(timed(fn, steps, dev), dev) / steps * 1e3
+        comm.check()
+        nbytes = sum(b.nbytes for b in reducer.buckets)
+        row = {"params": sum(numel(sh) for _, sh in shapes), "grad_bytes": nbytes, "buckets": len(reducer.buckets),
+               "step_ms": round(t["step"], 3), "compute_ms": round(t["compute"], 3),
+               "comm_only_ms": round(t["comm"], 3), "exposed_comm_ms": round(t["step"] - t["compute"], 3),
+               "comm_algbw_per_rank": round(nbytes / (t["comm"] / 1e3) / 1e9, 2), "steps": steps}
+    except Exception as e:  # noqa: BLE001 - reported, never loses the headline
+        row["error"] = repr(e)
+    finally:
+        del params, reducer, bwd, grads
+        torch.cuda.empty_cache()
+    return row
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -197,6 +262,9 @@ def main() -> None:
     ap.add_argument("--no-threshold", action="store_true", help="skip the straggler-tolerant kernel timing")
     ap.add_argument("--no-collectives", action="store_true", help="skip the all-to-all / all-gather / reduce-scatter timing")
     ap.add_argument("--no-fused-step", action="store_true", help="skip the fused reduce-scatter + AdamW + all-gather timing")
+    ap.add_argument("--no-dp", action="store_true", help="skip the ResNet-50 / Llama-3-8B DP-step sections")
+    ap.add_argument("--dp-timeout", type=float, default=240.0,
+                    help="seconds for the DP-step sections; past it the result line is written without them")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal: every rank on cuda:0 over gloo (RCCL refuses two ranks on one GPU), "
                          "workgroup budget split between the ranks so all spinning workgroups stay resident")
@@ -363,6 +431,25 @@ def main() -> None:
         result["fused_adamw_step"] = fused_step(comm, x, y, world, rank, args, dev)
     if sweep is not None:
         result["sweep"] = sweep
+    if engine_ok and not args.no_dp and not args.share_device:
+        # configs 4 / 5 (full Llama-3-8B: 32 GB of params + grads per rank). Not in the
+        # one-GPU rehearsal: there every rank's spinning comm kernel shares the device with the
+        # other ranks' GEMMs (8 ranks: 953 ms per overlapped ResNet-50 step vs 5.9 ms compute +
+        # 0.8 ms comm), which says nothing about one GPU per rank. A watchdog keeps a stuck
+        # section from costing the result line.
+        def give_up() -> None:
+            if rank == 0:
+                result["dp"] = {"error": f"timed out after {args.dp_timeout:.0f} s"}
+                with os.fdopen(_RESULT_FD, "w") as out:
+                    out.write(json.dumps(result) + "\n")
+            os._exit(0)
+
+        dog = threading.Timer(args.dp_timeout, give_up)
+        dog.daemon = True
+        dog.start()
+        result["dp"] = {m: dp_step(comm, m, dev)
+                        for m in ("resnet50", "llama3_8b")}
+        dog.cancel()
 
     if rank == 0:
         sys.stdout.flush()
