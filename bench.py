@@ -439,7 +439,7 @@ def main() -> None:
         # section from costing the result line.
         def give_up() -> None:
             if rank == 0:
-                result["dp"] = {"error": f"timed out after {args.dp_timeout:.0f} s"}
+                result["dp"] = {"error": f"timed out after {args.dp_timeout:g} s"}
                 with os.fdopen(_RESULT_FD, "w") as out:
                     out.write(json.dumps(result) + "\n")
             os._exit(0)
