@@ -233,12 +233,22 @@ def dp_step(comm: XgmiCommunicator, model: str, dev) -> dict:
                 for _ in range(warm):
                     fn()
                 t[name] = max_over_ranks(timed(fn, steps, dev), dev) / steps * 1e3
+            if comm.world > 1:
+                # the same step with the bucket launches capped at 128 workgroups: a reduce
+                # running beside backward's GEMMs competes for CUs (ddp.py `algo`)
+                reducer.algo = "twoshot@128"
+                for _ in range(warm):
+                    overlap()
+                t["step_g128"] = max_over_ranks(timed(overlap, steps, dev), dev) / steps * 1e3
+                reducer.algo = "auto"
         comm.check()
         nbytes = sum(b.nbytes for b in reducer.buckets)
         row = {"params": sum(numel(sh) for _, sh in shapes), "grad_bytes": nbytes, "buckets": len(reducer.buckets),
                "step_ms": round(t["step"], 3), "compute_ms": round(t["compute"], 3),
                "comm_only_ms": round(t["comm"], 3), "exposed_comm_ms": round(t["step"] - t["compute"], 3),
                "comm_algbw_per_rank": round(nbytes / (t["comm"] / 1e3) / 1e9, 2), "steps": steps}
+        if "step_g128" in t:
+            row["step_ms_twoshot_128wg"] = round(t["step_g128"], 3)
     except Exception as e:  # noqa: BLE001 - reported, never loses the headline
         row["error"] = repr(e)
     finally:
@@ -263,6 +273,7 @@ def main() -> None:
     ap.add_argument("--no-collectives", action="store_true", help="skip the all-to-all / all-gather / reduce-scatter timing")
     ap.add_argument("--no-fused-step", action="store_true", help="skip the fused reduce-scatter + AdamW + all-gather timing")
     ap.add_argument("--no-dp", action="store_true", help="skip the ResNet-50 / Llama-3-8B DP-step sections")
+    ap.add_argument("--dp-rehearsal", action="store_true", help="with --share-device: run the ResNet-50 DP step too")
     ap.add_argument("--dp-timeout", type=float, default=240.0,
                     help="seconds for the DP-step sections; past it the result line is written without them")
     ap.add_argument("--share-device", action="store_true",
@@ -431,7 +442,7 @@ def main() -> None:
         result["fused_adamw_step"] = fused_step(comm, x, y, world, rank, args, dev)
     if sweep is not None:
         result["sweep"] = sweep
-    if engine_ok and not args.no_dp and not args.share_device:
+    if engine_ok and not args.no_dp and (not args.share_device or args.dp_rehearsal):
         # configs 4 / 5 (full Llama-3-8B: 32 GB of params + grads per rank). Not in the
         # one-GPU rehearsal: there every rank's spinning comm kernel shares the device with the
         # other ranks' GEMMs (8 ranks: 953 ms per overlapped ResNet-50 step vs 5.9 ms compute +
@@ -448,7 +459,7 @@ def main() -> None:
         dog.daemon = True
         dog.start()
         result["dp"] = {m: dp_step(comm, m, dev)
-                        for m in ("resnet50", "llama3_8b")}
+                        for m in (("resnet50",) if args.share_device else ("resnet50", "llama3_8b"))}
         dog.cancel()
 
     if rank == 0:
