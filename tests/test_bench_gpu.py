@@ -1,0 +1,37 @@
+"""bench.py output contract (the driver parses it): stdout is exactly one JSON line with the
+metric / value / config fields, the engine validated, and the DP-step section (BASELINE
+configs 4 / 5) present without errors."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+pytestmark = pytest.mark.gpu
+
+
+def test_bench_prints_one_json_line_with_contract_fields():
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1", "--no-tune",
+                        "--no-rccl", "--no-threshold", "--no-collectives", "--no-fused-step", "--dp-timeout", "90"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout[:2000]
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["warmup"] == 1 and d["dtype"] == "bf16"
+    assert d["engine_ok"] is True and d["validated_max_abs_err"] == 0.0
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    for k in ("model", "global_batch", "seq_len", "parallelism"):
+        assert k in d["config"], k
+    for model in ("resnet50", "llama3_8b"):
+        row = d["dp"][model]
+        assert "error" not in row, row
+        assert row["step_ms"] > 0 and row["compute_ms"] > 0
