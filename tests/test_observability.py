@@ -68,3 +68,47 @@ def test_node_sampler():
     time.sleep(0.3)
     s.stop()
     assert len(s.history) >= 2 and "pid" in s.latest()
+
+
+def _collect_logs(level):
+    """Run a small in-process cluster with the native logger at `level`, sink -> list."""
+    records = []
+    lock = threading.Lock()
+
+    def sink(lvl, src, msg):
+        with lock:
+            records.append((lvl, src, msg))
+
+    prev = C.get_log_level()
+    C.set_log_level(level)
+    C.set_log_sink(sink)
+    try:
+        system, _, _ = _cluster(P=2, N=8, rounds=2)
+        system.shutdown()
+    finally:
+        C.set_log_sink(None)
+        C.set_log_level(prev)
+    return records
+
+
+def test_logger_levels_vocabulary_and_trace_only_payloads():
+    """C15: levelled logger with the reference's event vocabulary
+    (AllreduceMaster.scala / AllreduceWorker.scala log.info sites); full-array payload
+    dumps are emitted at TRACE only, never at INFO."""
+    order = ["TRACE", "DEBUG", "INFO", "WARNING", "ERROR", "OFF"]
+    info = _collect_logs("INFO")
+    assert info, "no log records at INFO"
+    assert all(order.index(lvl) >= order.index("INFO") for lvl, _, _ in info)
+    msgs = [m for _, _, m in info]
+    assert any("Start allreduce round" in m for m in msgs)
+    assert any("Number of peers = 2" in m for m in msgs)
+    assert any("completes allreduce round" in m for m in msgs)
+    assert any("rounds complete" in m for m in msgs)
+    assert {src for _, src, _ in info} >= {"master", "worker"}
+    assert not any("value =" in m or "Broadcast data:" in m for m in msgs)
+
+    trace = _collect_logs("TRACE")
+    assert any(lvl == "TRACE" and "Broadcast data:" in m for lvl, _, m in trace)
+    assert len(trace) > len(info)
+
+    assert _collect_logs("OFF") == []
