@@ -74,6 +74,43 @@ __global__ __launch_bounds__(kThreads) void soa(const uint4* g, float4* p, float
   }
 }
 
+// lane-contiguous: 4 params per lane per access (8-byte bf16 grad, one float4 per state
+// array), adjacent lanes adjacent, so every store instruction writes a full 1 KiB span;
+// two accesses in flight per lane (loads of both issued before the first update)
+__global__ __launch_bounds__(kThreads) void soa_lc(const uint2* g, float4* p, float4* m, float4* v, uint2* out,
+                                                   int64_t nq) {
+  const int64_t per = (nq + gridDim.x - 1) / gridDim.x;
+  const int64_t beg = blockIdx.x * per, end = beg + per < nq ? beg + per : nq;
+  for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += 2 * kThreads) {
+    uint2 gg[2];
+    float4 P[2], M[2], V[2];
+    bool live[2];
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      const int64_t i = i0 + w * kThreads;
+      live[w] = i < end;
+      if (!live[w]) continue;
+      gg[w] = g[i];
+      P[w] = p[i], M[w] = m[i], V[w] = v[i];
+    }
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      if (!live[w]) continue;
+      const int64_t i = i0 + w * kThreads;
+      const uint32_t wd2[2] = {gg[w].x, gg[w].y};
+      float* pp = reinterpret_cast<float*>(&P[w]);
+      float* mm = reinterpret_cast<float*>(&M[w]);
+      float* vv = reinterpret_cast<float*>(&V[w]);
+      uint16_t o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        o[e] = tobf(adamw(bf(static_cast<uint16_t>(wd2[e / 2] >> (16 * (e & 1)))), pp[e], mm[e], vv[e]));
+      p[i] = P[w], m[i] = M[w], v[i] = V[w];
+      out[i] = make_uint2(o[0] | (uint32_t(o[1]) << 16), o[2] | (uint32_t(o[3]) << 16));
+    }
+  }
+}
+
 // state interleaved: per 4 params {p4, m4, v4} = 48 bytes; 8 params = 6 float4
 __global__ __launch_bounds__(kThreads) void aos(const uint4* g, float4* st, uint4* out, int64_t npk) {
   const int64_t per = (npk + gridDim.x - 1) / gridDim.x;
@@ -125,12 +162,15 @@ int main(int argc, char** argv) {
   const double bytes = 28.0 * n;
   for (int grid : {256, 512, 1024}) {
     for (int rep = 0; rep < 2; ++rep) {
-      for (int layout = 0; layout < 3; ++layout) {
+      for (int layout = 0; layout < 4; ++layout) {
         auto run = [&] {
           if (layout == 0)
             hipLaunchKernelGGL(soa<false>, dim3(grid), dim3(kThreads), 0, 0, g, p, m, v, out, npk);
           else if (layout == 2)
             hipLaunchKernelGGL(soa<true>, dim3(grid), dim3(kThreads), 0, 0, g, p, m, v, out, npk);
+          else if (layout == 3)
+            hipLaunchKernelGGL(soa_lc, dim3(grid), dim3(kThreads), 0, 0, reinterpret_cast<const uint2*>(g), p, m, v,
+                               reinterpret_cast<uint2*>(out), 2 * npk);
           else
             hipLaunchKernelGGL(aos, dim3(grid), dim3(kThreads), 0, 0, g, st, out, npk);
         };
@@ -149,7 +189,7 @@ int main(int argc, char** argv) {
         std::sort(ts.begin(), ts.end());
         const float med = ts[ts.size() / 2];
         std::printf("{\"layout\": \"%s\", \"grid\": %d, \"rep\": %d, \"params\": %lld, \"ms\": %.3f, \"TBps\": %.2f}\n",
-                    layout == 2 ? "soa_nt_grad_out" : layout ? "aos" : "soa", grid, rep, static_cast<long long>(n), med, bytes / med / 1e9);
+                    layout == 3 ? "soa_lc" : layout == 2 ? "soa_nt_grad_out" : layout ? "aos" : "soa", grid, rep, static_cast<long long>(n), med, bytes / med / 1e9);
         std::fflush(stdout);
       }
     }
