@@ -293,15 +293,20 @@ __device__ __forceinline__ bool reached(uint32_t flag, uint32_t epoch) {
 // Lane i < nflags of wave 0 stores flag `addr(i)` (skipped when it returns nullptr).
 // `release` = false drops the system-scope release fence (measurement knob only: the
 // payload then relies on the vmcnt drain of stores to uncached memory).
+// Lanes with no flag (nullptr: the own rank, or a 1-rank launch) skip the fence: its
+// `buffer_wbl2` would write back every dirty L2 line of the kernel (e.g. half-updated
+// AdamW state lines of other workgroups, which are then written again) and order nothing.
 template <typename FlagAddr>
 __device__ __forceinline__ void publish_flags(FlagAddr addr, int nflags, uint32_t epoch, bool release = true) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
   __syncthreads();
   if (threadIdx.x < static_cast<unsigned>(nflags)) {
     uint32_t* f = addr(static_cast<int>(threadIdx.x));
-    if (release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope (xGMI peers)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (f) st_flag(f, epoch);
+    if (f) {
+      if (release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope (xGMI peers)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      st_flag(f, epoch);
+    }
   }
 }
 
