@@ -216,7 +216,10 @@ __device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, in
 __device__ __forceinline__ void finish_launch(uint32_t* ctl, uint32_t epoch) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    // relaxed: only the count matters (the next launch is stream-ordered after this one and
+    // kernel end publishes ctl[0]); an acq_rel at agent scope is a `buffer_wbl2` per
+    // workgroup, writing back the XCD's dirty L2 lines mid-kernel (e.g. AdamW state)
+    const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == gridDim.x - 1) {
       __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&ctl[0], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
