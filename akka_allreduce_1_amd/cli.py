@@ -24,7 +24,8 @@ import numpy as np
 
 from . import config as mconfig
 from ._native import C
-from .utils.metrics import MetricsRegistry, cluster_source, master_source, worker_source, write_trace
+from .utils.metrics import (MetricsRegistry, cluster_source, master_source, plane_worker_source, worker_source,
+                            write_trace)
 
 
 def _cluster_cfg(cfg: mconfig.Config, port: int, roles: list[str]) -> "C.ClusterConfig":
@@ -163,6 +164,10 @@ def worker_main(argv: list[str] | None = None) -> int:
     ap.add_argument("sourceDataSize", nargs="?", type=int, default=10)
     ap.add_argument("--print-outputs", action="store_true", help="one JSON line per AllReduceOutput on stdout")
     ap.add_argument("--max-outputs", type=int, default=0, help="exit after this many outputs (0 = never)")
+    ap.add_argument("--device", type=int, default=None,
+                    help="run the worker on this GPU: an xGMI round plane (one kernel launch per round, peers' "
+                         "HBM mapped over IPC; csrc/hip/xgmi_plane.h) instead of ScatterBlock/ReduceBlock messages")
+    ap.add_argument("--dtype", choices=["fp32", "bf16", "fp16"], default=None, help="GPU worker element type")
     _common(ap)
     args = ap.parse_args(argv)
     cfg = _load(args)
@@ -170,27 +175,42 @@ def worker_main(argv: list[str] | None = None) -> int:
     n = args.sourceDataSize
     count = {"n": 0}
     stop = threading.Event()
-    base = np.arange(n, dtype=np.float32)
-
-    def source(req):  # createDataSource: data[i] = i + iteration (AllreduceWorker.scala:285-291)
-        return C.AllReduceInput(base + np.float32(req.iteration))
+    plane = None
 
     def sink(out):  # logging sink (AllreduceWorker.scala:295-297)
         count["n"] += 1
         if args.print_outputs:
-            print(json.dumps({"iteration": out.iteration, "data": np.asarray(out.data).tolist(),
-                              "count": list(out.count)}), flush=True)
+            data = out.data
+            data = data.float().cpu().tolist() if hasattr(data, "cpu") else np.asarray(data).tolist()
+            print(json.dumps({"iteration": out.iteration, "data": data, "count": list(out.count)}), flush=True)
         if args.max_outputs and count["n"] >= args.max_outputs:
             stop.set()
 
-    wref = system.worker(source, sink, "worker")
-    node = C.ClusterNode.start(system, _cluster_cfg(cfg, args.port, ["worker"]))
+    meta = ""
+    if args.device is None:
+        base = np.arange(n, dtype=np.float32)
+
+        def source(req):  # createDataSource: data[i] = i + iteration (AllreduceWorker.scala:285-291)
+            return C.AllReduceInput(base + np.float32(req.iteration))
+
+        wref = system.worker(source, sink, "worker")
+    else:
+        plane, source = _gpu_worker_plane(args, cfg, n)
+        wref = system.plane_worker(source, sink, plane, "worker")
+        meta = plane.descriptor  # the master relays it to every peer in InitWorkers.planes
+    cc = _cluster_cfg(cfg, args.port, ["worker"])
+    cc.meta = meta
+    node = C.ClusterNode.start(system, cc)
     reg = _observe(args, cfg, {"role": "worker", "address": node.address})
-    reg.register("worker", worker_source(system, wref))
+    if plane is None:
+        reg.register("worker", worker_source(system, wref))
+    else:
+        reg.register("worker", plane_worker_source(system, wref, plane))
     reg.register("cluster", cluster_source(node))
     events = system.probe("membership")
     node.subscribe(events)  # MemberUp events are queued: a short-lived master is never missed
-    print(f"[mxar-worker] {node.address} sourceDataSize={n}", file=sys.stderr, flush=True)
+    where = f" device=cuda:{args.device} plane={plane.name}" if plane is not None else ""
+    print(f"[mxar-worker] {node.address} sourceDataSize={n}{where}", file=sys.stderr, flush=True)
     _install_signals(stop)
     seen_master = False
     while not stop.is_set():
@@ -205,6 +225,31 @@ def worker_main(argv: list[str] | None = None) -> int:
     node.shutdown()
     system.shutdown()
     return 0
+
+
+def _gpu_worker_plane(args, cfg: mconfig.Config, n: int):
+    """The GPU worker: an xGMI round plane on cuda:<device> and the reference's demo data
+    source, data[i] = i + iteration (AllreduceWorker.scala:285-291), produced on the GPU by
+    the fill_iota kernel in the plane's element type."""
+    import torch
+
+    from .ops.kernels import dtype_code
+
+    dt = args.dtype or str(cfg["mxar.plane.dtype"])
+    tdt = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[dt]
+    dev = torch.device("cuda", args.device)
+    torch.cuda.set_device(dev)
+    plane = C.hip.xgmi_plane(args.device, dtype_code(tdt), n, max_peers=int(cfg["mxar.plane.max-peers"]),
+                             max_lag=int(cfg["mxar.plane.max-lag"]), grid=int(cfg["mxar.plane.grid"]),
+                             timeout_s=float(cfg["mxar.plane.timeout"]))
+
+    def source(req):
+        x = torch.empty(n, dtype=tdt, device=dev)
+        C.hip.fill_iota(x.data_ptr(), n, float(req.iteration), dtype_code(tdt),
+                        torch.cuda.current_stream(dev).cuda_stream)
+        return x
+
+    return plane, source
 
 
 def main(argv: list[str] | None = None) -> int:

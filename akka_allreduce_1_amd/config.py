@@ -48,6 +48,12 @@ DEFAULTS: dict[str, Any] = {
     "mxar.engine.grid": 0,
     "mxar.engine.dtype": "bf16",
     "mxar.engine.bucket-bytes": 64 << 20,
+    # GPU workers (mxar-worker --device k): the xGMI round plane (csrc/hip/xgmi_plane.h)
+    "mxar.plane.dtype": "fp32",                                # fp32 | bf16 | fp16
+    "mxar.plane.max-peers": 8,                                 # arena sized for <= this many workers
+    "mxar.plane.max-lag": 4,                                   # ... and maxLag <= this
+    "mxar.plane.grid": 0,                                      # workgroups per round launch (0: 2 per CU)
+    "mxar.plane.timeout": 60.0,                                # seconds a kernel waits for a dead peer
     "mxar.metrics.json": "",
     "mxar.trace.json": "",
 }

@@ -64,6 +64,21 @@ def worker_source(system, ref) -> Source:
     return f
 
 
+def plane_worker_source(system, ref, plane=None) -> Source:
+    """A round-plane worker (csrc/runtime/plane_worker.h): protocol counters, round latency
+    (fetch -> completion), and the plane's own counters (launches, cold rounds, forces)."""
+    def f() -> dict:
+        st = system.plane_worker_state(ref)
+        d = dict(st["stats"])
+        d.update({f"latency_{k}": v for k, v in st["round_latency"].items()})
+        d.update(round=st["round"], max_round=st["maxRound"], launched=st["launched"])
+        if plane is not None and hasattr(plane, "stats"):
+            d.update({f"plane_{k}": v for k, v in _obj_fields(plane.stats).items()})
+        return d
+
+    return f
+
+
 def master_source(system, ref) -> Source:
     return lambda: {k: v for k, v in system.master_state(ref).items() if isinstance(v, (int, float, bool))}
 

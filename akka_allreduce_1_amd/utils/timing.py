@@ -19,6 +19,28 @@ def busbw(algbw: float, world: int) -> float:
     return algbw * 2.0 * (world - 1) / world if world > 1 else 0.0
 
 
+def hbm_bytes(S: int, P: int, algo: str) -> float:
+    """HBM bytes the kernels move when P logical ranks of ONE GPU allreduce S bytes each
+    (every rank's traffic lands in the same HBM; counts checked against rocprofv3 PMC
+    FETCH_SIZE / WRITE_SIZE in profiles/pmc_counters.md)."""
+    if algo == "ring":  # per rank, blocks of S/P: RS hops read in (+ slab) and push, AG hops copy out + forward
+        return P * (S / P) * (6 * (P - 2) + 8)
+    if algo == "all_to_all":  # S = P blocks per rank: read in + write slab (P-1)/P + read slab + write out
+        return P * (2 * S + 2 * S * (P - 1) / P)
+    if algo == "reduce_scatter":
+        return P * (S + 2 * S * (P - 1) / P + S / P)
+    if algo == "all_gather":  # S = the gathered output per rank (input S/P)
+        m = S / P
+        return P * ((4 * P - 2) * m)
+    if algo == "ll":  # read in, write P-1 LL slots (2x), read P-1 LL slots (2x), write out
+        return P * (S + 4 * S * (P - 1) + S)
+    if algo == "oneshot":
+        return P * (S + S * P + S * P + S)  # read in, write P slots, read P slots, write out
+    # two-shot: read in + push (P-1)/P, reduce reads S (own input + P-1 slots) and writes S
+    # (own output + P-1 peers' R slots), gather reads + writes (P-1)/P
+    return P * (S + S * (P - 1) / P + S + S + 2 * S * (P - 1) / P)
+
+
 def summarize(times_ms: Sequence[float]) -> dict:
     return {
         "p50_ms": percentile(times_ms, 50),

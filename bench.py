@@ -13,7 +13,13 @@ same buffer for comparison. Rank 0 prints ONE JSON line. Per-rank algbw = buffer
 of the slowest rank (nccl-tests convention, reported as `algbw_per_rank`); `value` is the
 whole-job aggregate the driver contract asks for = N x per-rank algbw (gradient bytes reduced
 per second by the job). At N=1 an allreduce is an out-of-place copy, so the N=1 point is an
-HBM copy rate, not a communication rate. Data: synthetic uniform(-1, 1) gradients.
+HBM copy rate, not a communication rate (`algo` says "copy (world=1)" and the tuner is
+skipped); the `local_ranks` section then times the allreduce kernels themselves with 8
+logical ranks in one launch on the GPU. Data: synthetic uniform(-1, 1) gradients.
+
+Before anything is timed, every algorithm a section may pick (ll, one-shot, two-shot, ring,
+threshold, all-to-all, all-gather, reduce-scatter) is checked against fp32 (`validated`),
+and rank 0 records the peer-access / link-type / hop matrix (`topology`).
 
 After the headline, side sections on the same engine (in the JSON, not in `value`): the
 tuner's size sweep vs RCCL, the straggler-tolerant kernel, all-to-all / all-gather /
@@ -115,6 +121,158 @@ def validate(comm: XgmiCommunicator, n: int, dtype: torch.dtype, dev, rank: int,
     return flag.item() == 0, err
 
 
+_LINK_NAMES = {0: "hypertransport", 1: "qpi", 2: "pcie", 3: "infiniband", 4: "xgmi"}
+
+
+def topology(world: int) -> dict:
+    """Peer access, link type and hop count of every pair of visible devices (rank 0's view):
+    the first multi-GPU run records what its cross-GPU stores actually went over."""
+    from akka_allreduce_1_amd._native import C
+
+    n = C.hip.device_count()
+    peer, link, hops = [], [], []
+    for a in range(n):
+        pr, lr, hr = [], [], []
+        for b in range(n):
+            can, t, h = C.hip.link_info(a, b)
+            pr.append(int(can))
+            lr.append("self" if a == b else _LINK_NAMES.get(t, str(t)))
+            hr.append(0 if a == b else h)
+        peer.append(pr)
+        link.append(lr)
+        hops.append(hr)
+    return {"devices_visible": n, "ranks": world, "peer_access": peer, "link_type": link, "hops": hops}
+
+
+def validate_algos(comm: XgmiCommunicator, dtype: torch.dtype, dev, rank: int, world: int) -> dict:
+    """Every algorithm the tuner or a section may pick, checked against an fp32 reference
+    BEFORE anything is timed, so a first-run failure on new hardware is loud and attributed.
+    Every rank regenerates all ranks' inputs from their seeds: the reference needs no
+    collective of its own."""
+    tol_el = 1e-5 * world if dtype == torch.float32 else 2e-2 * world
+    out: dict = {}
+
+    def inputs(n, seed):
+        return [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=seed + k) for k in range(world)]
+
+    cases = [("ll", 100_003), ("oneshot", 300_007), ("twoshot", 5_000_011), ("ring", 5_000_011)]
+    if world > 1 and comm._c.threshold_rows > 0:
+        cases.append(("threshold", 2_000_003))
+    for algo, n in cases:
+        if algo == "ll" and n * torch.empty(0, dtype=dtype).element_size() > comm._c.ll_max_bytes:
+            n = comm._c.ll_max_bytes // torch.empty(0, dtype=dtype).element_size() - 5
+        xs = inputs(n, 7000 + len(out) * 31)
+        ref = torch.zeros(n, device=dev)
+        for t in xs:
+            ref += t.float()
+        try:
+            if algo == "threshold":
+                y = comm.allreduce_threshold(xs[rank])
+            else:
+                y = comm.allreduce(xs[rank], algo=algo)
+            comm.check()
+            err = (y.float() - ref).abs().max().item()
+            out[algo] = {"ok": err <= tol_el, "max_abs_err": err, "n": n}
+        except Exception as e:  # noqa: BLE001 - reported per algorithm
+            out[algo] = {"ok": False, "error": repr(e)}
+    m = 65_536
+    for name in ("all_to_all", "all_gather", "reduce_scatter"):
+        try:
+            if name == "all_gather":
+                xs = inputs(m, 8100)
+                y = comm.all_gather(xs[rank])
+                ref = torch.cat([t.float() for t in xs])
+            else:
+                xs = inputs(world * m, 8200 if name == "all_to_all" else 8300)
+                if name == "all_to_all":
+                    y = comm.all_to_all(xs[rank])
+                    ref = torch.cat([t[rank * m:(rank + 1) * m].float() for t in xs])
+                else:
+                    y = comm.reduce_scatter(xs[rank])
+                    ref = sum(t[rank * m:(rank + 1) * m].float() for t in xs)
+            comm.check()
+            err = (y.float() - ref).abs().max().item()
+            out[name] = {"ok": err <= tol_el, "max_abs_err": err}
+        except Exception as e:  # noqa: BLE001
+            out[name] = {"ok": False, "error": repr(e)}
+    flags = torch.tensor([1 if out[k]["ok"] else 0 for k in out], device=dev)
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+    for k, f in zip(out, flags.tolist()):
+        out[k]["validated"] = bool(f)
+    return out
+
+
+def local_ranks(dev, args, P: int = 8) -> dict:
+    """P logical ranks in ONE launch on this GPU (LocalCluster), the bench buffer per rank:
+    the allreduce kernels themselves at N = 1, where the one-rank headline is only a copy.
+    All traffic lands in one HBM, so the yardstick is the copy roofline measured in this
+    process: hbm_TBps = protocol bytes (utils.timing.hbm_bytes, PMC-checked) / time."""
+    from akka_allreduce_1_amd._native import C
+    from akka_allreduce_1_amd.parallel import LocalCluster
+    from akka_allreduce_1_amd.utils.timing import hbm_bytes
+
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    es = 2 if dtype == torch.bfloat16 else 4
+    S = args.size_mib << 20
+    n = S // es
+    row: dict = {"ranks": P, "bytes_per_rank": S, "dtype": args.dtype}
+    cl = xs = ys = ref = a = b = None
+    try:
+        # copy roofline: the engine's own copy kernel, 2 x 256 MiB of traffic per call
+        a = torch.empty(S, dtype=torch.uint8, device=dev)
+        b = torch.empty_like(a)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+
+        def cp():
+            C.hip.copy(a.data_ptr(), b.data_ptr(), S, stream)
+
+        for _ in range(args.warmup):
+            cp()
+        cms = percentile(event_times(cp, args.steps, dev), 50)
+        copy_tbps = 2 * S / (cms / 1e3) / 1e12
+        row["copy_roofline_TBps"] = round(copy_tbps, 3)
+        del a, b
+        a = b = None
+        cl = LocalCluster(P, slot_bytes=-(-S // P) + (1 << 20), grid=512, timeout_s=10.0)
+        xs = [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=500 + k) for k in range(P)]
+        ys = [torch.empty_like(t) for t in xs]
+        ref = torch.zeros(n, device=dev)
+        for t in xs:
+            ref += t.float()
+        for algo in ("twoshot", "ring"):
+            def fn(algo=algo):
+                cl.allreduce(xs, ys, algo=algo)
+
+            fn()
+            cl.check()
+            err = max((t.float() - ref).abs().max().item() for t in ys)
+            for _ in range(args.warmup):
+                fn()
+            wall = timed_local(fn, args.steps, dev) / args.steps * 1e3
+            p50 = percentile(event_times(fn, args.steps, dev), 50)
+            cl.check()
+            tbps = hbm_bytes(S, P, algo) / (p50 / 1e3) / 1e12
+            row[algo] = {"p50_ms": round(p50, 4), "ms_per_step": round(wall, 4), "max_abs_err": err,
+                         "validated": err <= 2e-2 * P if dtype == torch.bfloat16 else err <= 1e-5 * P,
+                         "hbm_bytes": int(hbm_bytes(S, P, algo)), "hbm_TBps": round(tbps, 3),
+                         "frac_copy_roofline": round(tbps / copy_tbps, 3)}
+    except Exception as e:  # noqa: BLE001 - reported, never loses the headline
+        row["error"] = repr(e)
+    finally:
+        del cl, xs, ys, ref, a, b
+        torch.cuda.empty_cache()
+    return row
+
+
+def timed_local(fn, steps: int, dev) -> float:
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize(dev)
+    return time.perf_counter() - t0
+
+
 def collectives(comm: XgmiCommunicator, x: torch.Tensor, world: int, args, dev) -> dict:
     """ms per call of the xGMI all_to_all / all_gather / reduce_scatter vs RCCL on the bench
     buffer (all_gather gathers 1/world of it per rank, so every op moves the same bytes)."""
@@ -206,9 +364,15 @@ def dp_step(comm: XgmiCommunicator, model: str, dev) -> dict:
         shapes = gradient_shapes(model)
         params = [torch.nn.Parameter(torch.zeros(sh, dtype=torch.bfloat16, device=dev)) for _, sh in shapes]
         big = model == "llama3_8b"
-        # 64 MiB buckets for the 16 GB set; torch DDP's 25 MiB for ResNet-50 (2 buckets: the
-        # first one overlaps the rest of backward)
-        reducer = BucketedGradReducer(params, comm, bucket_bytes=(64 if big else 25) << 20, op="avg")
+        # Llama-3-8B (16 GB): size-graded buckets - a 32 MiB first bucket starts the overlap
+        # early, 256 MiB buckets after it keep the per-bucket hand-off count low (each costs a
+        # few us of host time and a compute-stream drain: 163 x 64 MiB buckets exposed 1.1 ms
+        # at N = 1, profiles/dp_llama_n1_sync_sweep.jsonl). ResNet-50: torch DDP's 25 MiB.
+        if big:
+            reducer = BucketedGradReducer(params, comm, bucket_bytes=256 << 20, first_bucket_bytes=32 << 20,
+                                          op="avg")
+        else:
+            reducer = BucketedGradReducer(params, comm, bucket_bytes=25 << 20, op="avg")
         reducer.remove_hooks()  # the synthetic backward calls the hook itself
         bwd = SyntheticBackward(params, 1024, torch.bfloat16, dev)
         grads = [q.grad for q in params]
@@ -244,9 +408,15 @@ def dp_step(comm: XgmiCommunicator, model: str, dev) -> dict:
         comm.check()
         nbytes = sum(b.nbytes for b in reducer.buckets)
         row = {"params": sum(numel(sh) for _, sh in shapes), "grad_bytes": nbytes, "buckets": len(reducer.buckets),
+               "bucket_bytes": [reducer.buckets[0].nbytes, max(b.nbytes for b in reducer.buckets)],
                "step_ms": round(t["step"], 3), "compute_ms": round(t["compute"], 3),
-               "comm_only_ms": round(t["comm"], 3), "exposed_comm_ms": round(t["step"] - t["compute"], 3),
-               "comm_algbw_per_rank": round(nbytes / (t["comm"] / 1e3) / 1e9, 2), "steps": steps}
+               "exposed_comm_ms": round(t["step"] - t["compute"], 3), "steps": steps}
+        if comm.world > 1:
+            row["comm_only_ms"] = round(t["comm"], 3)
+            row["comm_algbw_per_rank"] = round(nbytes / (t["comm"] / 1e3) / 1e9, 2)
+        else:  # an average over one rank is the identity: no kernel runs, nothing to rate
+            row["note"] = ("world=1: the allreduce is the identity (no launch), so exposed_comm_ms is the "
+                           "reducer's host overhead; comm-only time / bandwidth are not measured")
         if "step_g128" in t:
             row["step_ms_twoshot_128wg"] = round(t["step_g128"], 3)
     except Exception as e:  # noqa: BLE001 - reported, never loses the headline
@@ -255,6 +425,24 @@ def dp_step(comm: XgmiCommunicator, model: str, dev) -> dict:
         del params, reducer, bwd, grads
         torch.cuda.empty_cache()
     return row
+
+
+_EMIT_LOCK = threading.Lock()
+_EMITTED = [False]
+
+
+def emit(rank: int, result: dict) -> bool:
+    """Write the ONE result line (rank 0), at most once per process: the dp watchdog and the
+    main path may both get here. Returns True for the caller that wrote it."""
+    with _EMIT_LOCK:
+        if _EMITTED[0]:
+            return False
+        _EMITTED[0] = True
+        if rank == 0:
+            sys.stdout.flush()
+            with os.fdopen(_RESULT_FD, "w") as out:
+                out.write(json.dumps(result) + "\n")
+        return True
 
 
 def main() -> None:
@@ -273,6 +461,7 @@ def main() -> None:
     ap.add_argument("--no-collectives", action="store_true", help="skip the all-to-all / all-gather / reduce-scatter timing")
     ap.add_argument("--no-fused-step", action="store_true", help="skip the fused reduce-scatter + AdamW + all-gather timing")
     ap.add_argument("--no-dp", action="store_true", help="skip the ResNet-50 / Llama-3-8B DP-step sections")
+    ap.add_argument("--no-local", action="store_true", help="skip the 8-logical-rank section at N = 1")
     ap.add_argument("--dp-rehearsal", action="store_true", help="with --share-device: run the ResNet-50 DP step too")
     ap.add_argument("--dp-timeout", type=float, default=240.0,
                     help="seconds for the DP-step sections; past it the result line is written without them")
@@ -328,8 +517,15 @@ def main() -> None:
         y.copy_(x)
         dist.all_reduce(y)
 
+    validated = None
+    if engine_ok:
+        # every algorithm a section or the tuner may pick, against fp32, before any timing
+        validated = validate_algos(comm, dtype, dev, rank, world)
+        bad = [k for k, v in validated.items() if not v["validated"]]
+        if bad:
+            log(rank, f"VALIDATION FAILED for {bad}: {[validated[k] for k in bad]}")
     sweep = None
-    if engine_ok and not args.no_tune:
+    if engine_ok and not args.no_tune and world > 1:  # at world = 1 every candidate is the same copy
         rccl_algos = () if args.no_rccl else ("rccl", "rsag") if world > 1 else ("rccl",)
         sweep = comm.tune(max_bytes=nbytes, dtype=dtype, iters=args.sweep_steps,
                           candidates=("ll", "oneshot", "twoshot", "ring") + (("threshold",) if world > 1 else ())
@@ -337,6 +533,8 @@ def main() -> None:
     if engine_ok and args.algo != "rccl":
         algo = args.algo
         chosen = comm._pick(nbytes) if algo == "auto" else algo
+        if world == 1:  # XgmiComm::run: a 1-rank sum is an out-of-place copy, whatever the algorithm
+            chosen = "copy (world=1)"
 
         def step():
             comm.allreduce(x, y, algo=algo)
@@ -386,7 +584,19 @@ def main() -> None:
         "busbw": round(busbw(algbw, world), 2),
         "validated_max_abs_err": err,
         "engine_ok": engine_ok,
+        "status": "ok",
     }
+    if world == 1:
+        result["value_note"] += ("; world=1: the allreduce is an out-of-place HBM copy (no communication) - "
+                                 "see local_ranks for the allreduce kernels on this GPU")
+    if validated is not None:
+        result["validated"] = {k: v["validated"] for k, v in validated.items()}
+        result["validation"] = validated
+    if rank == 0:
+        try:
+            result["topology"] = topology(world)
+        except Exception as e:  # noqa: BLE001
+            result["topology"] = {"error": repr(e)}
     if reason:
         result["engine_note"] = reason
 
@@ -442,6 +652,9 @@ def main() -> None:
         result["fused_adamw_step"] = fused_step(comm, x, y, world, rank, args, dev)
     if sweep is not None:
         result["sweep"] = sweep
+    if engine_ok and world == 1 and not args.share_device and not args.no_local:
+        # the allreduce kernels at N = 1: 8 logical ranks in one launch on this GPU
+        result["local_ranks"] = local_ranks(dev, args, P=8)
     if engine_ok and not args.no_dp and (not args.share_device or args.dp_rehearsal):
         # configs 4 / 5 (full Llama-3-8B: 32 GB of params + grads per rank). Not in the
         # one-GPU rehearsal: there every rank's spinning comm kernel shares the device with the
@@ -449,23 +662,25 @@ def main() -> None:
         # 0.8 ms comm), which says nothing about one GPU per rank. A watchdog keeps a stuck
         # section from costing the result line.
         def give_up() -> None:
-            if rank == 0:
-                result["dp"] = {"error": f"timed out after {args.dp_timeout:g} s"}
-                with os.fdopen(_RESULT_FD, "w") as out:
-                    out.write(json.dumps(result) + "\n")
-            os._exit(0)
+            # the result line is written exactly once (emit's lock + flag); the explicit
+            # status says the dp section did not finish, the process exits at once because
+            # a persistent kernel of the stuck section may still spin
+            result["dp"] = {"error": f"timed out after {args.dp_timeout:g} s"}
+            result["status"] = "dp_timeout"
+            if emit(rank, result):
+                os._exit(0)
 
         dog = threading.Timer(args.dp_timeout, give_up)
         dog.daemon = True
         dog.start()
-        result["dp"] = {m: dp_step(comm, m, dev)
-                        for m in (("resnet50",) if args.share_device else ("resnet50", "llama3_8b"))}
+        dp = {m: dp_step(comm, m, dev) for m in (("resnet50",) if args.share_device else ("resnet50", "llama3_8b"))}
         dog.cancel()
+        with _EMIT_LOCK:
+            if _EMITTED[0]:  # the watchdog won the race and has already written the line
+                return
+            result["dp"] = dp
 
-    if rank == 0:
-        sys.stdout.flush()
-        with os.fdopen(_RESULT_FD, "w") as out:
-            out.write(json.dumps(result) + "\n")
+    emit(rank, result)
     dist.barrier()
     dist.destroy_process_group()
 

@@ -14,6 +14,7 @@ static py::dict member_dict(const MemberInfo& m) {
   d["roles"] = m.roles;
   d["uid"] = m.uid;
   d["status"] = static_cast<int>(m.status);
+  d["meta"] = m.meta;
   return d;
 }
 
@@ -28,7 +29,8 @@ void bind_cluster(py::module_& m) {
       .def_readwrite("acceptable_heartbeat_pause_s", &ClusterConfig::acceptable_heartbeat_pause_s)
       .def_readwrite("auto_down_unreachable_after_s", &ClusterConfig::auto_down_unreachable_after_s)
       .def_readwrite("connect_timeout_s", &ClusterConfig::connect_timeout_s)
-      .def_readwrite("worker_path", &ClusterConfig::worker_path);
+      .def_readwrite("worker_path", &ClusterConfig::worker_path)
+      .def_readwrite("meta", &ClusterConfig::meta);
 
   py::class_<ClusterStats>(m, "ClusterStats")
       .def_readonly("frames_out", &ClusterStats::frames_out)

@@ -16,6 +16,7 @@
 #include "../runtime/actor_system.h"
 #include "../runtime/allreduce_actors.h"
 #include "../runtime/fault_injector.h"
+#include "../runtime/plane_worker.h"
 #include "py_common.h"
 
 namespace py = pybind11;
@@ -34,6 +35,17 @@ static PyToDevicePayload g_py_to_dev = nullptr;
 void register_device_payload_hooks(DevicePayloadToPy to_py, PyToDevicePayload from_py) {
   g_dev_to_py = to_py;
   g_py_to_dev = from_py;
+}
+
+static PyToDevicePayload g_py_to_dev_typed = nullptr;
+void register_typed_payload_hook(PyToDevicePayload from_py) { g_py_to_dev_typed = from_py; }
+
+Payload typed_payload_from_py(const py::handle& obj) {
+  if (g_py_to_dev_typed) {
+    Payload d = g_py_to_dev_typed(obj);
+    if (d) return d;
+  }
+  return payload_from_py(obj);
 }
 
 Payload payload_from_py(const py::handle& obj) {
@@ -78,6 +90,7 @@ Message message_from_py(const py::handle& obj) {
   if (py::isinstance<AllreduceFinished>(obj)) return obj.cast<AllreduceFinished>();
   if (py::isinstance<PoisonPill>(obj)) return obj.cast<PoisonPill>();
   if (py::isinstance<TextMessage>(obj)) return obj.cast<TextMessage>();
+  if (py::isinstance<RoundTimeout>(obj)) return obj.cast<RoundTimeout>();
   if (py::isinstance<py::str>(obj)) return TextMessage{obj.cast<std::string>()};
   throw py::type_error("not a protocol message: " + std::string(py::str(py::type::of(obj))));
 }
@@ -123,6 +136,27 @@ DataSink make_sink(py::object fn) {
     py::gil_scoped_acquire g;
     holder->fn(out);
   };
+}
+
+// dataSource of a plane worker: a device tensor keeps its dtype and is ordered by event
+DataSource make_plane_source(py::object fn) {
+  auto holder = std::make_shared<PyCallable>(std::move(fn));
+  return [holder](const AllReduceInputRequest& req) -> AllReduceInput {
+    py::gil_scoped_acquire g;
+    py::object r = holder->fn(req);
+    if (py::isinstance<AllReduceInput>(r)) return r.cast<AllReduceInput>();
+    return AllReduceInput{typed_payload_from_py(r)};
+  };
+}
+
+PlaneWorkerActor* plane_worker_of(const ActorRef& ref) {
+  auto* l = dynamic_cast<LocalActorRef*>(ref.get());
+  if (!l) throw py::value_error("not a local actor");
+  auto c = l->cell();
+  if (!c) throw py::value_error("actor is stopped");
+  auto* w = dynamic_cast<PlaneWorkerActor*>(c->actor());
+  if (!w) throw py::value_error("not a plane worker actor");
+  return w;
 }
 
 WorkerActor* worker_of(const ActorRef& ref) {
@@ -188,6 +222,8 @@ PYBIND11_MODULE(_C, m) {
            py::arg("maxLag"), py::arg("dataSize"), py::arg("maxChunkSize"), py::arg("epoch") = 0,
            py::arg("startRound") = 0)
       .def_readwrite("startRound", &InitWorkers::startRound)
+      .def_readwrite("planes", &InitWorkers::planes)
+      .def_readwrite("roundBase", &InitWorkers::roundBase)
       .def_readwrite("workers", &InitWorkers::workers)
       .def_readwrite("master", &InitWorkers::master)
       .def_readwrite("destId", &InitWorkers::destId)
@@ -290,13 +326,14 @@ PYBIND11_MODULE(_C, m) {
       });
 
   py::class_<MemberUp>(m, "MemberUp")
-      .def(py::init([](ActorRef ref, std::string role, std::string address) {
-             return MemberUp{std::move(ref), std::move(role), std::move(address)};
+      .def(py::init([](ActorRef ref, std::string role, std::string address, std::string meta) {
+             return MemberUp{std::move(ref), std::move(role), std::move(address), std::move(meta)};
            }),
-           py::arg("ref"), py::arg("role") = "worker", py::arg("address") = "")
+           py::arg("ref"), py::arg("role") = "worker", py::arg("address") = "", py::arg("meta") = "")
       .def_readwrite("ref", &MemberUp::ref)
       .def_readwrite("role", &MemberUp::role)
       .def_readwrite("address", &MemberUp::address)
+      .def_readwrite("meta", &MemberUp::meta)
       .def("__repr__", [](const MemberUp& u) { return "MemberUp(" + (u.ref ? u.ref->path() : "?") + ", " + u.role + ")"; });
 
   py::class_<Terminated>(m, "Terminated")
@@ -320,6 +357,20 @@ PYBIND11_MODULE(_C, m) {
         return py::isinstance<TextMessage>(o) && a.text == o.cast<TextMessage>().text;
       })
       .def("__repr__", [](const TextMessage& t) { return "TextMessage(" + t.text + ")"; });
+
+  py::class_<RoundTimeout>(m, "RoundTimeout")
+      .def(py::init([](int64_t epoch, int round) { return RoundTimeout{epoch, round}; }), py::arg("epoch"),
+           py::arg("round"))
+      .def_readwrite("epoch", &RoundTimeout::epoch)
+      .def_readwrite("round", &RoundTimeout::round)
+      .def("__repr__", [](const RoundTimeout& t) {
+        return "RoundTimeout(epoch=" + std::to_string(t.epoch) + ", round=" + std::to_string(t.round) + ")";
+      });
+  py::class_<PlaneRoundDone>(m, "PlaneRoundDone")
+      .def_readonly("epoch", &PlaneRoundDone::epoch)
+      .def_readonly("error", &PlaneRoundDone::error)
+      .def_readonly("cold", &PlaneRoundDone::cold)
+      .def_property_readonly("iteration", [](const PlaneRoundDone& d) { return d.output.iteration; });
 
   py::class_<AllReduceInputRequest>(m, "AllReduceInputRequest")
       .def(py::init([](int it) { return AllReduceInputRequest{it}; }), py::arg("iteration"))
@@ -461,6 +512,40 @@ PYBIND11_MODULE(_C, m) {
           py::arg("maxLag"), py::arg("dataSize"), py::arg("maxRound"), py::arg("maxChunkSize"),
           py::arg("liveBarrier") = false, py::arg("on_finished") = py::none(), py::arg("name") = "master",
           py::arg("startRound") = 0, py::arg("on_round") = py::none(), py::arg("roundTimeoutMs") = 0)
+      .def("plane_worker", [](ActorSystem& s, py::object source, py::object sink, std::shared_ptr<RoundPlane> plane,
+                              std::string name) {
+            auto a = std::make_unique<PlaneWorkerActor>(make_plane_source(std::move(source)),
+                                                        make_sink(std::move(sink)), std::move(plane));
+            return s.actor_of(std::move(a), std::move(name));
+          }, py::arg("source"), py::arg("sink") = py::none(), py::arg("plane"), py::arg("name") = "",
+          "Round-granular worker (csrc/runtime/plane_worker.h): the reference protocol with one plane launch "
+          "per round; announce plane.descriptor as the member's meta (MemberUp / ClusterConfig.meta)")
+      .def("plane_worker_state", [](ActorSystem&, ActorRef ref) {
+        auto* w = plane_worker_of(ref);
+        py::dict d;
+        d["id"] = w->id();
+        d["round"] = w->round();
+        d["maxRound"] = w->max_round();
+        d["launched"] = w->launched();
+        d["epoch"] = w->epoch();
+        d["initialized"] = w->initialized();
+        const PlaneWorkerStats& s = w->stats();
+        py::dict st;
+#define F(x) st[#x] = s.x
+        F(start_in); F(rounds_launched); F(cold_rounds); F(forced_completions); F(rounds_completed);
+        F(complete_out); F(stale_dropped); F(stashed); F(plane_errors); F(inits);
+#undef F
+        d["stats"] = st;
+        const RoundLatency lat = w->round_latency();
+        py::dict l;
+        l["count"] = lat.count;
+        l["p50_ms"] = lat.p50_ms;
+        l["p99_ms"] = lat.p99_ms;
+        l["mean_ms"] = lat.mean_ms;
+        l["max_ms"] = lat.max_ms;
+        d["round_latency"] = l;
+        return d;
+      })
       .def("probe", &ActorSystem::make_probe, py::arg("name") = "")
       .def("lookup", &ActorSystem::lookup)
       .def("stop", &ActorSystem::stop)
@@ -560,6 +645,10 @@ PYBIND11_MODULE(_C, m) {
       "Fault-injecting ActorRef decorator (drop / duplicate / delay selected messages)");
 
   py::class_<DataPlane, std::shared_ptr<DataPlane>>(m, "DataPlane").def_property_readonly("name", &DataPlane::name);
+  py::class_<RoundPlane, std::shared_ptr<RoundPlane>>(m, "RoundPlane")
+      .def_property_readonly("name", &RoundPlane::name)
+      .def_property_readonly("descriptor", &RoundPlane::descriptor)
+      .def_property_readonly("chunks", &RoundPlane::chunks);
   m.def("host_plane", [] { return std::static_pointer_cast<DataPlane>(HostPlane::instance()); });
 
   bind_cluster(m);

@@ -37,5 +37,10 @@ Message message_from_py(const py::handle& obj);
 using DevicePayloadToPy = py::object (*)(const Payload&);
 using PyToDevicePayload = Payload (*)(const py::handle&);  // returns nullptr if not a device tensor
 void register_device_payload_hooks(DevicePayloadToPy to_py, PyToDevicePayload from_py);
+// Plane workers: a device tensor of ANY supported dtype (float32 / bfloat16 / float16),
+// zero-copy, ordered after its producer by an event on torch's current stream (no host
+// synchronisation). nullptr if `obj` is not a device tensor.
+void register_typed_payload_hook(PyToDevicePayload from_py);
+Payload typed_payload_from_py(const py::handle& obj);
 
 }  // namespace mxar

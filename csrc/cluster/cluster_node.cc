@@ -118,7 +118,7 @@ std::shared_ptr<ClusterNode> ClusterNode::start(std::shared_ptr<ActorSystem> sys
   });
   const bool first_seed = n->cfg_.seed_nodes.empty() || n->cfg_.seed_nodes.front() == n->address_;
   if (first_seed) {  // the first seed joins itself and starts the cluster
-    MemberInfo me{n->address_, n->cfg_.roles, n->uid_, MemberStatus::Up};
+    MemberInfo me{n->address_, n->cfg_.roles, n->uid_, MemberStatus::Up, n->cfg_.meta};
     {
       std::lock_guard<std::mutex> g(n->mem_mu_);
       n->members_[n->address_] = me;
@@ -173,7 +173,7 @@ void ClusterNode::leave() {
   if (!lead.empty() && lead != address_) {
     send_frame(lead, w.bytes());
   } else {
-    MemberInfo me{address_, cfg_.roles, uid_, MemberStatus::Removed};
+    MemberInfo me{address_, cfg_.roles, uid_, MemberStatus::Removed, cfg_.meta};
     broadcast(frame_member_event(MemberEventKind::Removed, me), address_);
   }
   joined_ = false;
@@ -406,6 +406,7 @@ MemberUp ClusterNode::member_up_event(const MemberInfo& m) {
   MemberUp up;
   up.role = m.roles.empty() ? "" : m.roles.front();
   up.address = m.address;
+  up.meta = m.meta;
   up.ref = resolve(m.address + (m.has_role("worker") ? cfg_.worker_path : std::string("/user")));
   return up;
 }
@@ -628,7 +629,7 @@ void ClusterNode::ticker_loop() {
       if (leaving_.load()) continue;
       Writer w;
       w.u8(static_cast<uint8_t>(FrameKind::Join));
-      encode_member(w, MemberInfo{address_, cfg_.roles, uid_, MemberStatus::Joining});
+      encode_member(w, MemberInfo{address_, cfg_.roles, uid_, MemberStatus::Joining, cfg_.meta});
       for (auto& s : cfg_.seed_nodes)
         if (s != address_) send_frame(s, w.bytes());
       continue;

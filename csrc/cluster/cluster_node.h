@@ -47,6 +47,9 @@ struct ClusterConfig {
   double auto_down_unreachable_after_s = 10.0;  // < 0 disables auto-down
   double connect_timeout_s = 2.0;
   std::string worker_path = "/user/worker";
+  // Announced with the join and delivered in every MemberUp of this member (a GPU worker's
+  // plane descriptor: the master relays it to the peers in InitWorkers.planes).
+  std::string meta;
 };
 
 struct ClusterStats {

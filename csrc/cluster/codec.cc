@@ -37,6 +37,12 @@ void encode_message(Writer& w, const Message& m, const RefCodec& rc) {
           w.i32(x.maxChunkSize);
           w.i64(x.epoch);
           w.i32(x.startRound);
+          w.u32(static_cast<uint32_t>(x.planes.size()));
+          for (auto& [id, d] : x.planes) {
+            w.i32(id);
+            w.str(d);
+          }
+          w.u32(x.roundBase);
         } else if constexpr (std::is_same_v<T, StartAllreduce>) {
           w.i32(x.round);
           w.i64(x.epoch);
@@ -63,6 +69,7 @@ void encode_message(Writer& w, const Message& m, const RefCodec& rc) {
           w.str(rc.encode_ref(x.ref));
           w.str(x.role);
           w.str(x.address);
+          w.str(x.meta);
         } else if constexpr (std::is_same_v<T, Terminated>) {
           w.str(rc.encode_ref(x.ref));
         } else if constexpr (std::is_same_v<T, AllreduceFinished>) {
@@ -70,6 +77,12 @@ void encode_message(Writer& w, const Message& m, const RefCodec& rc) {
         } else if constexpr (std::is_same_v<T, PoisonPill>) {
         } else if constexpr (std::is_same_v<T, TextMessage>) {
           w.str(x.text);
+        } else if constexpr (std::is_same_v<T, RoundTimeout>) {
+          w.i64(x.epoch);
+          w.i32(x.round);
+        } else if constexpr (std::is_same_v<T, PlaneRoundDone>) {
+          // process-local (a plane's completion to its own worker); never crosses a node
+          throw CodecError("PlaneRoundDone is local to a node");
         }
       },
       m);
@@ -94,6 +107,12 @@ Message decode_message(Reader& r, RefCodec& rc) {
       x.maxChunkSize = r.i32();
       x.epoch = r.i64();
       x.startRound = r.i32();
+      const uint32_t np = r.u32();
+      for (uint32_t i = 0; i < np; ++i) {
+        const int id = r.i32();
+        x.planes[id] = r.str();
+      }
+      x.roundBase = r.u32();
       return x;
     }
     case 1: {
@@ -135,6 +154,7 @@ Message decode_message(Reader& r, RefCodec& rc) {
       x.ref = rc.decode_ref(r.str());
       x.role = r.str();
       x.address = r.str();
+      x.meta = r.str();
       return x;
     }
     case 6:
@@ -145,6 +165,12 @@ Message decode_message(Reader& r, RefCodec& rc) {
       return PoisonPill{};
     case 9:
       return TextMessage{r.str()};
+    case 10: {
+      RoundTimeout x;
+      x.epoch = r.i64();
+      x.round = r.i32();
+      return x;
+    }
     default:
       throw CodecError("unknown message kind " + std::to_string(kind));
   }
@@ -156,6 +182,7 @@ void encode_member(Writer& w, const MemberInfo& m) {
   for (auto& s : m.roles) w.str(s);
   w.u64(m.uid);
   w.u8(static_cast<uint8_t>(m.status));
+  w.str(m.meta);
 }
 
 MemberInfo decode_member(Reader& r) {
@@ -165,6 +192,7 @@ MemberInfo decode_member(Reader& r) {
   for (uint32_t i = 0; i < n; ++i) m.roles.push_back(r.str());
   m.uid = r.u64();
   m.status = static_cast<MemberStatus>(r.u8());
+  m.meta = r.str();
   return m;
 }
 

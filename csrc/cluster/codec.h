@@ -36,6 +36,7 @@ struct MemberInfo {
   std::vector<std::string> roles;
   uint64_t uid = 0;
   MemberStatus status = MemberStatus::Up;
+  std::string meta;  // ClusterConfig.meta of the member (e.g. a GPU worker's plane descriptor)
   bool has_role(const std::string& r) const {
     for (auto& x : roles)
       if (x == r) return true;

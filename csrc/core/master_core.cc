@@ -103,6 +103,9 @@ void MasterCore::init_workers() {
   int k = 0;
   for (auto& [id, h] : workers_) dense[k++] = h;
   workers_.swap(dense);
+  if (epoch_ > 0)  // skip past every device round epoch the previous membership epoch could use
+    round_base_ += static_cast<uint32_t>(std::max(0, round_ - epoch_start_round_ + 1)) + 1u;
+  epoch_start_round_ = std::max(0, p_.startRound);
   ++epoch_;
   stats_.inits++;
   for (auto& [idx, h] : workers_) {
@@ -117,6 +120,7 @@ void MasterCore::init_workers() {
     p.maxChunkSize = p_.maxChunkSize;
     p.epoch = epoch_;
     p.startRound = std::max(0, p_.startRound);
+    p.roundBase = round_base_;
     fx_->send_init(h, p, workers_);
   }
 }

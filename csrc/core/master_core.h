@@ -65,6 +65,7 @@ class MasterCore {
   int round() const { return round_; }
   int num_complete() const { return numComplete_; }
   int64_t epoch() const { return epoch_; }
+  uint32_t round_base() const { return round_base_; }
   bool finished() const { return finished_; }
   const std::map<int, int>& workers() const { return workers_; }  // id -> handle
   const MasterParams& params() const { return p_; }
@@ -82,6 +83,10 @@ class MasterCore {
   int round_ = -1;              // :29
   int numComplete_ = 0;         // :30
   int64_t epoch_ = 0;
+  // Device round epochs of plane workers (InitWorkers.roundBase): every epoch's rounds map
+  // above all rounds any earlier epoch started, so flags left in a reused arena are stale.
+  uint32_t round_base_ = 0;
+  int epoch_start_round_ = 0;
   int last_reported_ = -1;
   bool finished_ = false;
   MasterStats stats_;

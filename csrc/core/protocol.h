@@ -31,6 +31,10 @@ class PayloadStorage {
   virtual size_t size() const = 0;
   // Blocking copy to host (device payloads synchronise on their ready event).
   virtual std::vector<float> to_host() const = 0;
+  // Element type: 0 = float32 (every host payload, the reference's Array[Float]),
+  // 1 = bfloat16, 2 = float16 (device payloads of the xGMI round engine). size() counts
+  // elements of this type; to_host() converts to float32.
+  virtual int dtype() const { return 0; }
 };
 using Payload = std::shared_ptr<const PayloadStorage>;
 
@@ -76,6 +80,16 @@ struct InitWorkers {  // AllreduceMessage.scala:7-16
   // Extension: first round of this epoch - 0 normally, the checkpointed
   // round when a job resumes (workers start there instead of replaying earlier rounds).
   int startRound = 0;
+  // Extension (data plane A): every worker's plane descriptor as it announced
+  // it at registration (MemberUp.meta) - for the xGMI round engine the IPC handle of its
+  // HBM arena - so each worker maps its peers' slabs from InitWorkers alone. Empty when the
+  // workers use the actor data path (ScatterBlock / ReduceBlock messages).
+  std::map<int, std::string> planes;
+  // Extension: device round-epoch base of this membership epoch. Round r of the epoch is
+  // device epoch roundBase + (r - startRound) + 1; the master keeps the bases increasing
+  // across re-initialisations, so flags an older epoch left in a reused arena are never
+  // mistaken for this epoch's.
+  uint32_t roundBase = 0;
 };
 
 // Extension: the round messages carry the membership epoch of the
@@ -138,6 +152,9 @@ struct MemberUp {  // akka.cluster.ClusterEvent.MemberUp (AllreduceMaster.scala:
   ActorRef ref;  // the member's "/user/worker" actor, already resolved
   std::string role;
   std::string address;
+  // Extension: metadata the member announced when it joined (ClusterConfig.meta); a GPU
+  // worker's plane descriptor, relayed by the master in InitWorkers.planes.
+  std::string meta;
 };
 struct Terminated {  // akka.actor.Terminated (AllreduceMaster.scala:50)
   ActorRef ref;
@@ -151,10 +168,26 @@ struct PoisonPill {};
 struct TextMessage {
   std::string text;
 };
+// The master's round deadline (scheduled to itself, mxar.allreduce.round-timeout): the
+// round `round` of membership epoch `epoch` has not reached the barrier in time.
+struct RoundTimeout {
+  int64_t epoch = 0;
+  int round = 0;
+};
+// A round of a plane worker (csrc/runtime/plane_worker.h) finished on its data plane; posted
+// by the plane's completion thread to the worker's own mailbox. `output` is the reference's
+// AllReduceOutput (dataSink), `error` the plane's error word (0 = healthy), `cold` marks a
+// round force-completed before it ever started.
+struct PlaneRoundDone {
+  int64_t epoch = 0;
+  AllReduceOutput output;
+  uint32_t error = 0;
+  bool cold = false;
+};
 
 using Message = std::variant<InitWorkers, StartAllreduce, ScatterBlock, ReduceBlock,
                              CompleteAllreduce, MemberUp, Terminated, AllreduceFinished,
-                             PoisonPill, TextMessage>;
+                             PoisonPill, TextMessage, RoundTimeout, PlaneRoundDone>;
 
 const char* message_name(const Message& m);
 

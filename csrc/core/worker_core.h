@@ -40,6 +40,7 @@ struct InitParams {
   int maxChunkSize = 1024;
   int64_t epoch = 0;
   int startRound = 0;
+  uint32_t roundBase = 0;  // device round-epoch base (InitWorkers.roundBase; plane workers)
 };
 
 // Messages the worker core can emit to a peer or to itself.

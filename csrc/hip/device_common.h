@@ -5,11 +5,20 @@
 //     never loaded as scalars.
 //   * fp32 accumulation of bf16/fp32 packs (bf16 -> fp32 is a 16-bit shift; fp32 -> bf16
 //     goes through the hardware `v_cvt_pk_bf16_f32` round-to-nearest-even, NaN-safe).
-//   * Cross-GPU signalling over xGMI: flags live in uncached (MTYPE UC) device memory that
-//     peers map through IPC. Producer: payload stores -> every storing wave drains its
+//   * Cross-GPU signalling over xGMI, as shipped: flags AND payload slots live in
+//     fine-grained device memory (hipDeviceMallocFinegrained, the default of XgmiComm;
+//     `MXAR_SLAB_MEM=uncached|coarse` exist for study only - uncached slabs showed stale
+//     reads, profiles/memory_ordering_study.md) that peers map through IPC, and the
+//     communicator runs with release AND acquire on (`fence = 3`).
+//     Producer: write-through payload stores (`sc0 sc1`) -> every storing wave drains its
 //     `vmcnt` -> workgroup barrier -> ONE lane: system-scope release fence -> asm drain ->
-//     relaxed system-scope flag store. Consumer: ONE wave polls relaxed (with `s_sleep`),
-//     then ONE system-scope acquire, then a workgroup barrier before any payload load
+//     relaxed system-scope flag store. The release is required: a drained write-through
+//     store is only known to have reached the producer's L2 channel, and without the
+//     fence the flag was seen to arrive first (stale slab reads). Because every kernel
+//     store is write-through, the release's L2 writeback finds (almost) nothing dirty.
+//     Consumer: ONE wave polls relaxed (with `s_sleep`), then ONE system-scope acquire
+//     (invalidates this CU's L1 and the non-coherent L2 lines), then a workgroup barrier
+//     before any payload load; payload loads additionally use `sc1` (L1 bypass)
 //     (MI355X_MICROARCH.md "Valid forms"; the asm drain after the fence is the ROCm 7.2
 //     compiler-hazard fix from the same section).
 //   * Every spin is bounded by a wall-clock deadline (`s_memrealtime`, 100 MHz): a wedged
@@ -196,9 +205,10 @@ __device__ __forceinline__ Pack16 ld16(const void* p) { return *static_cast<cons
 __device__ __forceinline__ void st16(void* p, const Pack16& v) { *static_cast<Pack16*>(p) = v; }
 
 // ---------------------------------------------------------------------------------
-// Slab reads: `buffer_load ... sc1` bypasses the reading CU's L1, and the slab itself is
-// uncached device memory (no L2 copy), so every slab load reads what the peers' xGMI
-// stores left in HBM - no acquire fence (L1/L2 invalidate) is needed before it.
+// Slab reads: `buffer_load ... sc1` bypasses the reading CU's L1. The slab is fine-grained
+// device memory, so its lines may still be held in L2: the consumer's system-scope
+// acquire after the flag poll (wait_flags, fence bit 1, on by default) is what makes the
+// peers' xGMI stores visible - the sc1 load alone is not a substitute for it.
 // Descriptor built from wave-uniform values only (cdna_hip_programming.md T8/T20).
 // ---------------------------------------------------------------------------------
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -291,8 +301,9 @@ __device__ __forceinline__ bool reached(uint32_t flag, uint32_t epoch) {
 
 // Producer side: called by ALL threads of the workgroup after their payload stores.
 // Lane i < nflags of wave 0 stores flag `addr(i)` (skipped when it returns nullptr).
-// `release` = false drops the system-scope release fence (measurement knob only: the
-// payload then relies on the vmcnt drain of stores to uncached memory).
+// `release` = false drops the system-scope release fence (measurement knob only, fence
+// bit 0 cleared: the payload then relies on the vmcnt drain alone, which is NOT enough on
+// fine-grained memory - see the header comment).
 // Lanes with no flag (nullptr: the own rank, or a 1-rank launch) skip the fence: its
 // `buffer_wbl2` would write back every dirty L2 line of the kernel (e.g. half-updated
 // AdamW state lines of other workgroups, which are then written again) and order nothing.

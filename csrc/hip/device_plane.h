@@ -48,12 +48,20 @@ ReadyEvent record_ready(hipStream_t s);
 // Device payload: a float view [offset, offset + n) of a refcounted device allocation.
 class DevicePayload final : public PayloadStorage {
  public:
+  // offset and n in elements of `dtype` (0 = float32, 1 = bfloat16, 2 = float16)
   DevicePayload(std::shared_ptr<void> mem, size_t offset, size_t n, int device, hipStream_t stream,
-                ReadyEvent ready = nullptr)
-      : mem_(std::move(mem)), off_(offset), n_(n), device_(device), stream_(stream), ready_(std::move(ready)) {}
+                ReadyEvent ready = nullptr, int dtype = 0)
+      : mem_(std::move(mem)), off_(offset), n_(n), device_(device), stream_(stream), ready_(std::move(ready)),
+        dtype_(dtype) {}
   bool on_device() const override { return true; }
-  const float* data() const override { return static_cast<const float*>(mem_.get()) + off_; }
+  // first element (typed as float for the protocol's float32 payloads; see dtype())
+  const float* data() const override {
+    return reinterpret_cast<const float*>(static_cast<const char*>(mem_.get()) + off_ * elem_bytes());
+  }
+  const void* bytes() const { return static_cast<const char*>(mem_.get()) + off_ * elem_bytes(); }
   size_t size() const override { return n_; }
+  int dtype() const override { return dtype_; }
+  size_t elem_bytes() const { return dtype_ == 0 ? 4 : 2; }
   std::vector<float> to_host() const override;
   int device() const { return device_; }
   const std::shared_ptr<void>& memory() const { return mem_; }
@@ -69,6 +77,7 @@ class DevicePayload final : public PayloadStorage {
   int device_;
   hipStream_t stream_;
   ReadyEvent ready_;
+  int dtype_ = 0;
 };
 
 class DevicePlane;

@@ -30,7 +30,20 @@ std::vector<float> DevicePayload::to_host() const {
   if (n_ == 0) return h;
   wait_host();
   hip_check(hipSetDevice(device_), "hipSetDevice");
-  hip_check(hipMemcpy(h.data(), data(), n_ * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy D2H");
+  if (dtype_ == 0) {
+    hip_check(hipMemcpy(h.data(), data(), n_ * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy D2H");
+    return h;
+  }
+  std::vector<uint16_t> raw(n_);
+  hip_check(hipMemcpy(raw.data(), bytes(), n_ * 2, hipMemcpyDeviceToHost), "hipMemcpy D2H");
+  for (size_t i = 0; i < n_; ++i) {
+    if (dtype_ == 1) {  // bfloat16: the high half of a float32
+      const uint32_t b = static_cast<uint32_t>(raw[i]) << 16;
+      std::memcpy(&h[i], &b, 4);
+    } else {  // float16
+      h[i] = static_cast<float>(__builtin_bit_cast(_Float16, raw[i]));
+    }
+  }
   return h;
 }
 

@@ -12,6 +12,7 @@
 #include "../bindings/py_common.h"
 #include "device_plane.h"
 #include "xgmi_comm.h"
+#include "xgmi_plane.h"
 
 namespace py = pybind11;
 
@@ -46,6 +47,7 @@ struct DLManagedTensor {
 };
 constexpr int32_t kDLROCM = 10;
 constexpr uint8_t kDLFloat = 2;
+constexpr uint8_t kDLBfloat = 4;
 
 struct ExportCtx {
   Payload keep;
@@ -71,10 +73,12 @@ py::object device_payload_to_py(const Payload& p) {
   d->wait_host();  // torch consumes it on its own stream
   auto* ctx = new ExportCtx{p, {static_cast<int64_t>(p->size())}, {1}};
   auto* mt = new DLManagedTensor{};
-  mt->dl_tensor.data = const_cast<float*>(p->data());
+  mt->dl_tensor.data = const_cast<void*>(d->bytes());
   mt->dl_tensor.device = DLDevice{kDLROCM, d->device()};
   mt->dl_tensor.ndim = 1;
-  mt->dl_tensor.dtype = DLDataType{kDLFloat, 32, 1};
+  mt->dl_tensor.dtype = d->dtype() == 1   ? DLDataType{kDLBfloat, 16, 1}
+                        : d->dtype() == 2 ? DLDataType{kDLFloat, 16, 1}
+                                          : DLDataType{kDLFloat, 32, 1};
   mt->dl_tensor.shape = ctx->shape;
   mt->dl_tensor.strides = ctx->strides;
   mt->dl_tensor.byte_offset = 0;
@@ -109,6 +113,40 @@ Payload py_to_device_payload(const py::handle& obj) {
   return std::make_shared<DevicePayload>(std::move(mem), 0, static_cast<size_t>(n), mt->dl_tensor.device.device_id,
                                          nullptr, nullptr);
 }
+// Plane-worker inputs: the tensor's own dtype, zero copy, and an event recorded on torch's
+// current stream of its device - the plane's stream waits on it (no host synchronisation).
+Payload py_to_device_payload_typed(const py::handle& obj) {
+  if (!py::hasattr(obj, "__dlpack__") || !py::hasattr(obj, "is_cuda")) return nullptr;
+  if (!obj.attr("is_cuda").cast<bool>()) return nullptr;
+  py::module_ torch = py::module_::import("torch");
+  py::object dt = obj.attr("dtype");
+  int code = -1;
+  if (dt.equal(torch.attr("float32"))) code = 0;
+  else if (dt.equal(torch.attr("bfloat16"))) code = 1;
+  else if (dt.equal(torch.attr("float16"))) code = 2;
+  if (code < 0) throw py::type_error("plane input must be float32, bfloat16 or float16");
+  py::object t = obj.attr("detach")().attr("contiguous")().attr("reshape")(-1);
+  const uintptr_t cs = torch.attr("cuda").attr("current_stream")(t.attr("device")).attr("cuda_stream").cast<uintptr_t>();
+  py::object cap = t.attr("__dlpack__")();
+  auto* mt = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap.ptr(), "dltensor"));
+  if (!mt) throw py::error_already_set();
+  PyCapsule_SetName(cap.ptr(), "used_dltensor");
+  const int64_t n = mt->dl_tensor.ndim > 0 ? mt->dl_tensor.shape[0] : 1;
+  char* data = static_cast<char*>(mt->dl_tensor.data) + mt->dl_tensor.byte_offset;
+  const int dev = mt->dl_tensor.device.device_id;
+  std::shared_ptr<void> mem(data, [mt](void*) {
+    if (!mt->deleter) return;
+    if (Py_IsInitialized()) {
+      py::gil_scoped_acquire g;
+      mt->deleter(mt);
+    } else {
+      mt->deleter(mt);
+    }
+  });
+  ReadyEvent ready = record_ready(reinterpret_cast<hipStream_t>(cs));
+  return std::make_shared<DevicePayload>(std::move(mem), 0, static_cast<size_t>(n), dev, nullptr, std::move(ready),
+                                         code);
+}
 }  // namespace
 
 static hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
@@ -118,6 +156,7 @@ static void* as_ptr(uintptr_t p) { return reinterpret_cast<void*>(p); }
 void bind_hip(py::module_& m) {
   py::module_ h = m.def_submodule("hip", "HIP/CDNA4 data plane (gfx950)");
   register_device_payload_hooks(&device_payload_to_py, &py_to_device_payload);
+  register_typed_payload_hook(&py_to_device_payload_typed);
 
   py::class_<DevicePlane, DataPlane, std::shared_ptr<DevicePlane>>(h, "DevicePlane")
       .def_property_readonly("device", &DevicePlane::device)
@@ -134,6 +173,46 @@ void bind_hip(py::module_& m) {
         "DataPlane whose slabs and payloads live in HBM of `device` (worker protocol on the GPU)");
 
   py::enum_<DType>(h, "DType").value("F32", DType::F32).value("BF16", DType::BF16).value("F16", DType::F16);
+
+  py::class_<XgmiPlaneStats>(h, "XgmiPlaneStats")
+      .def_readonly("launches", &XgmiPlaneStats::launches)
+      .def_readonly("cold", &XgmiPlaneStats::cold)
+      .def_readonly("forced", &XgmiPlaneStats::forced)
+      .def_readonly("bytes", &XgmiPlaneStats::bytes)
+      .def_readonly("completed", &XgmiPlaneStats::completed)
+      .def_readonly("coarsened", &XgmiPlaneStats::coarsened)
+      .def_readonly("peer_maps", &XgmiPlaneStats::peer_maps);
+  py::class_<XgmiRoundPlane, RoundPlane, std::shared_ptr<XgmiRoundPlane>>(h, "XgmiRoundPlane")
+      .def_property_readonly("stats", &XgmiRoundPlane::stats)
+      .def_property_readonly("arena_bytes", &XgmiRoundPlane::arena_bytes)
+      .def_property_readonly("chunk_elems", &XgmiRoundPlane::chunk_elems)
+      .def_property_readonly("block_elems", &XgmiRoundPlane::block_elems)
+      .def_property_readonly("device", [](const XgmiRoundPlane& p) { return p.options().device; })
+      .def_property_readonly("stream", [](const XgmiRoundPlane& p) { return reinterpret_cast<uintptr_t>(p.stream()); })
+      .def("drain", [](XgmiRoundPlane& p) {
+        py::gil_scoped_release r;
+        p.drain();
+      });
+  h.def(
+      "xgmi_plane",
+      [](int device, DType dtype, int64_t capacity, int max_peers, int max_lag, int grid, double timeout_s,
+         bool order_ref) {
+        XgmiPlaneOptions o;
+        o.device = device;
+        o.dtype = dtype;
+        o.capacity = capacity;
+        o.max_peers = max_peers;
+        o.max_lag = max_lag;
+        o.grid = grid;
+        o.timeout_s = timeout_s;
+        o.order_ref = order_ref;
+        py::gil_scoped_release r;
+        return make_xgmi_plane(o);
+      },
+      py::arg("device") = 0, py::arg("dtype") = DType::F32, py::arg("capacity"), py::arg("max_peers") = 8,
+      py::arg("max_lag") = 4, py::arg("grid") = 0, py::arg("timeout_s") = 60.0, py::arg("order_ref") = true,
+      "RoundPlane of the protocol engine on MI355X: an HBM arena exported over IPC, one threshold-kernel launch "
+      "per round (csrc/hip/xgmi_plane.h)");
   py::enum_<Algo>(h, "Algo").value("Auto", Algo::Auto).value("TwoShot", Algo::TwoShot).value("OneShot", Algo::OneShot).value("Ring", Algo::Ring).value("LL", Algo::LL);
   py::enum_<Coll>(h, "Coll")
       .value("AllToAll", Coll::AllToAll)
@@ -150,7 +229,8 @@ void bind_hip(py::module_& m) {
       .def_readonly("threshold", &CommStats::threshold)
       .def_readonly("ll", &CommStats::ll)
       .def_readonly("coll", &CommStats::coll)
-      .def_readonly("adamw", &CommStats::adamw);
+      .def_readonly("adamw", &CommStats::adamw)
+      .def_readonly("stream_switches", &CommStats::stream_switches);
 
   py::class_<AdamW>(h, "AdamW")
       .def(py::init<>())
@@ -372,6 +452,20 @@ void bind_hip(py::module_& m) {
     if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
     return n;
   });
+  // Topology of a device pair: (can_access_peer, link type, hop count). Link types are
+  // HSA_AMD_LINK_INFO_TYPE_* (4 = xGMI, 2 = PCIe); (-1, -1) when the runtime does not say.
+  h.def(
+      "link_info",
+      [](int a, int b) {
+        int can = 0;
+        if (a != b) (void)hipDeviceCanAccessPeer(&can, a, b);
+        uint32_t type = 0, hops = 0;
+        const bool ok = a != b && hipExtGetLinkTypeAndHopCount(a, b, &type, &hops) == hipSuccess;
+        (void)hipGetLastError();
+        return py::make_tuple(a == b ? true : can != 0, ok ? static_cast<int>(type) : -1,
+                              ok ? static_cast<int>(hops) : -1);
+      },
+      py::arg("a"), py::arg("b"));
   h.attr("MAX_RANKS") = kMaxRanks;
 }
 

@@ -37,6 +37,9 @@ __device__ __forceinline__ void finish_with_barrier(const CommArgs& a, uint32_t*
   __shared__ int last;
   __syncthreads();
   if (threadIdx.x == 0) {
+    // acq_rel (unlike finish_launch's relaxed ticket): the last workgroup's FB flags tell the
+    // peers that EVERY workgroup's slab reads of this launch are done, so each ticket must
+    // be ordered after its workgroup's loads and the last one must see all of them.
     const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     last = t == gridDim.x - 1 ? 1 : 0;
   }

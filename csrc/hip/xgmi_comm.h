@@ -17,7 +17,7 @@
 //
 // All three phases run inside ONE persistent launch per segment (no host round trip per
 // chunk), every spin is bounded by a deadline, and epochs live in device memory so a
-// launch can be captured into a hipGraph. Slabs are uncached device memory exported
+// launch can be captured into a hipGraph. Slabs are fine-grained device memory exported
 // with hipIpcGetMemHandle; peers map them with hipIpcOpenMemHandle.
 #pragma once
 
@@ -55,7 +55,7 @@ constexpr int kCommThreads = 256;
 
 struct CommStats {
   uint64_t calls = 0, launches = 0, bytes = 0, oneshot = 0, twoshot = 0, ring = 0, threshold = 0, ll = 0, coll = 0,
-           adamw = 0;
+           adamw = 0, stream_switches = 0;
 };
 
 class XgmiComm {
@@ -66,8 +66,13 @@ class XgmiComm {
   // threshold_rows: depth of the lag ring of S/R slots used by allreduce_threshold
   // (maxLag + 1; 0 = threshold rounds disabled). The other algorithms use row 0.
   // Memory per GPU ~ 2 * (1 + threshold_rows) * world * slot_bytes.
+  // external_slab: lay the communicator out over an arena the caller allocated (fine-grained,
+  // zeroed once, >= layout(...).slab_bytes; xgmi_plane.cc) instead of allocating one.
+  // min_flag_bytes: reserve at least this much for the flag table (an arena reused by
+  // layouts of different sizes keeps its flags at the same place: data never lands on a flag).
   XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid = 0, double timeout_s = 20.0,
-           int threshold_rows = 0);
+           int threshold_rows = 0, char* external_slab = nullptr, int64_t external_bytes = 0,
+           int64_t min_flag_bytes = 0);
   ~XgmiComm();
   XgmiComm(const XgmiComm&) = delete;
   XgmiComm& operator=(const XgmiComm&) = delete;
@@ -78,6 +83,25 @@ class XgmiComm {
   void connect(const std::vector<std::string>& handles);
   // Single-process mode: all "ranks" are this process (tests / P logical ranks).
   void connect_local(const std::vector<XgmiComm*>& comms);
+  // Peer slab bases already mapped by the caller (the protocol plane keeps its own IPC
+  // mappings across re-initialisations); own entry ignored.
+  void connect_ptrs(const std::vector<char*>& bases);
+
+  // Slab geometry for (world, slot_bytes, threshold_rows), without allocating.
+  struct Layout {
+    int64_t slot_bytes = 0, slot_stride = 0, maxch = 0, off_S = 0, off_R = 0, off_LL = 0, ll_max = 0, ll_slot = 0;
+    int64_t slab_bytes = 0, alloc_bytes = 0;
+  };
+  static Layout layout(int world, int64_t slot_bytes, int threshold_rows, int64_t min_flag_bytes = 0);
+  // Bytes of the flag table alone (the part of off_S before its 64 KiB rounding).
+  static int64_t flag_bytes(int world, int64_t slot_bytes, int threshold_rows);
+  // Tell every peer that this rank has finished every threshold round up to `value`
+  // (progress words; enqueued on `stream`). The protocol plane publishes its round base
+  // after draining an old membership epoch, which opens the peers' lag gates for the new
+  // epoch's first rounds only once no old-epoch round of this rank can still write.
+  void publish_progress(uint32_t value, hipStream_t stream);
+  // An allocation size hipIpcOpenMemHandle can map on this ROCm stack (see the constructor).
+  static int64_t ipc_safe_bytes(int64_t bytes);
 
   // out = scale * sum over ranks of in (n elements of dtype); in == out allowed (in-place).
   // The scale is applied to the fp32 sum before the single rounding (scale = 1/P: mean).
@@ -99,6 +123,21 @@ class XgmiComm {
                                         const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream,
                                         float th_reduce, float th_complete, int32_t* counts = nullptr,
                                         float scale = 1.f, bool rescale = false);
+  // One round of the protocol engine (xgmi_plane.cc) on the threshold kernel: explicit round
+  // epoch and geometry (the reference's block ranges and maxChunkSize), the reference's
+  // arrival-order accounting, a cold (force-completed, never started) round, and the pinned
+  // host word the engine raises to force-complete rounds on a catch-up.
+  struct RoundSpec {
+    uint32_t epoch = 0;            // 0: this communicator's own threshold-round count + 1
+    int64_t block = 0, chunk = 0;  // elements; 0: the kernel's own geometry
+    bool cold = false;
+    bool order_ref = false;
+    const uint32_t* host_force = nullptr;  // device-visible pinned host word (may be null)
+  };
+  void round(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, float th_reduce, float th_complete,
+             int32_t* counts, const RoundSpec& spec, float scale = 1.f);
+  // Workgroups a round launch of `nch` chunks per block uses (counts / geometry checks).
+  int round_grid(int nch) const;
   // Chunks per block the threshold kernel uses for n elements (size of `counts` = P * this).
   int threshold_chunks(int64_t n, DType dt, int ranks_in_launch = 1) const;
   // Test knob: rank `rank` idles `us` microseconds at the start of each threshold launch.
@@ -170,11 +209,21 @@ class XgmiComm {
   bool connected() const { return connected_; }
   const CommStats& stats() const { return stats_; }
   char* slab() const { return slab_; }
+  uint32_t* ctl_ptr() const { return ctl_; }  // device control words ([2] = error word)
   int64_t slab_bytes() const { return slab_bytes_; }
   int64_t alloc_bytes() const { return alloc_bytes_; }
   static int64_t min_chunk_bytes() { return 1024; }
 
  private:
+  // Stream safety: every launch of a communicator reads its epoch / slab rows from device
+  // state the previous launch left behind, so launches must run one after the other even
+  // when callers use different streams (e.g. the DP reducer's comm stream and user code on
+  // the default stream). When `s` differs from the stream of this communicator's previous
+  // launch, an event recorded on that stream NOW (it covers the previous launch) is waited
+  // on by `s`. Same stream: nothing to do, no per-call event.
+  static void order_group(const std::vector<XgmiComm*>& group, hipStream_t s);
+  void order_after_last(hipStream_t s);
+
   static void run(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
                   const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, Algo algo, float scale);
   static void launch_segment(const std::vector<XgmiComm*>& group, const char* const* ins, char* const* outs,
@@ -185,7 +234,7 @@ class XgmiComm {
                        const std::vector<void*>& outs, int64_t m, DType dt, hipStream_t stream, float scale);
   static void run_threshold(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
                             const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, float thr,
-                            float thc, int32_t* counts, float scale, bool rescale);
+                            float thc, int32_t* counts, float scale, bool rescale, const RoundSpec* spec = nullptr);
   void geometry_threshold(int64_t n, DType dt, int ranks_here, int64_t* block, int64_t* chunk, int* nch,
                           int* gx) const;
 
@@ -200,11 +249,15 @@ class XgmiComm {
   int fence_ = 3;
   int units_per_wg_ = 0;  // two-shot scatter units per workgroup; 0 = by block size (launch_segment)
   int sub_max_ = 0;       // two-shot: most reduce pieces per chunk; 0 = by block size
-  char* slab_ = nullptr;            // own uncached slab (flags | S | R)
+  char* slab_ = nullptr;            // own fine-grained slab (flags | S | R | LL)
   uint32_t* ctl_ = nullptr;         // [0] epoch, [1] ticket, [2] sticky error (device memory)
   char* peers_[kMaxRanks] = {};     // slab base of every rank (own included)
   bool ipc_opened_[kMaxRanks] = {};
   bool connected_ = false;
+  bool own_slab_ = true;           // false: laid out over a caller's arena
+  bool launched_ = false;          // a launch has been enqueued (last_stream_ valid)
+  hipStream_t last_stream_ = nullptr;
+  hipEvent_t switch_ev_ = nullptr;  // recorded on last_stream_ when the stream changes
   CommStats stats_;
 };
 

@@ -317,43 +317,68 @@ static int default_grid(int device) {
   return 2 * cus;  // every workgroup must stay resident (they spin): 2 x 256-thread WG per CU
 }
 
-XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid, double timeout_s,
-                   int threshold_rows)
-    : rank_(rank), world_(world), device_(device), grid_(grid), rows_(1 + threshold_rows), timeout_s_(timeout_s) {
-  if (threshold_rows < 0 || threshold_rows > 64)
-    throw std::invalid_argument("XgmiComm: threshold_rows (maxLag + 1) must be in [0, 64]");
-  if (world < 1 || world > kMaxRanks) throw std::invalid_argument("XgmiComm: world must be in [1, 16]");
-  if (rank < 0 || rank >= world) throw std::invalid_argument("XgmiComm: bad rank");
-  slot_bytes_ = round_up(std::max<int64_t>(slot_bytes, 64 * 1024), 64 * 1024);
-  maxch_ = slot_bytes_ / min_chunk_bytes();
-  // [F1: rows x P x maxch][F2: rows x P x maxch][FB: P][PROG: P][F2C: rows x P x maxch]
-  const int64_t flag_bytes = (3 * rows_ * world_ * maxch_ + 2 * world_) * 4;
-  off_S_ = round_up(flag_bytes, 64 * 1024);
-  // Slots sit slot_stride_ = capacity + MXAR_SLOT_PAD bytes apart (default 0). A pad takes the
+int64_t XgmiComm::flag_bytes(int world, int64_t slot_bytes, int threshold_rows) {
+  const int rows = 1 + threshold_rows;
+  const int64_t maxch = round_up(std::max<int64_t>(slot_bytes, 64 * 1024), 64 * 1024) / min_chunk_bytes();
+  // [F1: rows x P x maxch][F2: rows x P x maxch][FB: P][PROG: P][F2C: rows x P x maxch][FORCE: P]
+  return (3 * rows * world * maxch + 3 * world) * 4;
+}
+
+XgmiComm::Layout XgmiComm::layout(int world, int64_t slot_bytes, int threshold_rows, int64_t min_flag_bytes) {
+  Layout L;
+  const int rows = 1 + threshold_rows;
+  L.slot_bytes = round_up(std::max<int64_t>(slot_bytes, 64 * 1024), 64 * 1024);
+  L.maxch = L.slot_bytes / min_chunk_bytes();
+  L.off_S = round_up(std::max(flag_bytes(world, slot_bytes, threshold_rows), min_flag_bytes), 64 * 1024);
+  // Slots sit slot_stride = capacity + MXAR_SLOT_PAD bytes apart (default 0). A pad takes the
   // P slots a reduce reads at one offset off a power-of-two spacing; an A/B on one box showed
   // no gain for the reduce kernel (benchmarks/bench_reduce.py --pad-kib, profiles/reduce_kernel.md),
   // so the knob stays for study.
   int64_t pad = 0;
   if (const char* e = std::getenv("MXAR_SLOT_PAD")) pad = round_up(std::max<int64_t>(0, std::atoll(e)), 4096);
-  slot_stride_ = slot_bytes_ + pad;
-  off_R_ = off_S_ + rows_ * world_ * slot_stride_;
-  off_B_ = 2 * rows_ * world_ * maxch_ * 4;
+  L.slot_stride = L.slot_bytes + pad;
+  L.off_R = L.off_S + rows * world * L.slot_stride;
   // low-latency one-shot slots: [2 parities][P sources] x ll_slot (two 8-B LL words per
   // 16-B store: ll_slot = 2 x payload)
-  ll_max_ = 512 * 1024;
-  if (const char* e = std::getenv("MXAR_LL_MAX")) ll_max_ = std::max<int64_t>(0, std::atoll(e));
-  ll_max_ = round_up(ll_max_, 16);
-  ll_slot_ = round_up(std::max<int64_t>(2 * ll_max_, 16), 64 * 1024);
-  off_LL_ = off_R_ + rows_ * world_ * slot_stride_;
-  slab_bytes_ = off_LL_ + 2 * world_ * ll_slot_;
+  L.ll_max = 512 * 1024;
+  if (const char* e = std::getenv("MXAR_LL_MAX")) L.ll_max = std::max<int64_t>(0, std::atoll(e));
+  L.ll_max = round_up(L.ll_max, 16);
+  L.ll_slot = round_up(std::max<int64_t>(2 * L.ll_max, 16), 64 * 1024);
+  L.off_LL = L.off_R + rows * world * L.slot_stride;
+  L.slab_bytes = L.off_LL + 2 * world * L.ll_slot;
   // Allocation size: on this ROCm stack hipIpcOpenMemHandle of an allocation whose size has
   // bit 31 set (2-4 GiB, 6-8 GiB, ...) never returns in the importing process, while the
   // sizes around it map and reduce correctly (measured with tools/ipc_size_probe.py: 1.97,
   // 4.05, 4.33 GiB fine; 2.03-3.9 GiB hang). Such slabs are padded up to the next multiple of
   // 4 GiB - at most 2 GiB of the 288 GB of HBM. MXAR_IPC_NO_PAD=1 disables it (probing).
-  alloc_bytes_ = slab_bytes_;
-  if ((alloc_bytes_ & (int64_t{1} << 31)) && !std::getenv("MXAR_IPC_NO_PAD"))
-    alloc_bytes_ = round_up(alloc_bytes_, int64_t{1} << 32);
+  L.alloc_bytes = ipc_safe_bytes(L.slab_bytes);
+  return L;
+}
+
+int64_t XgmiComm::ipc_safe_bytes(int64_t bytes) {
+  if ((bytes & (int64_t{1} << 31)) && !std::getenv("MXAR_IPC_NO_PAD")) return round_up(bytes, int64_t{1} << 32);
+  return bytes;
+}
+
+XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid, double timeout_s,
+                   int threshold_rows, char* external_slab, int64_t external_bytes, int64_t min_flag_bytes)
+    : rank_(rank), world_(world), device_(device), grid_(grid), rows_(1 + threshold_rows), timeout_s_(timeout_s) {
+  if (threshold_rows < 0 || threshold_rows > 64)
+    throw std::invalid_argument("XgmiComm: threshold_rows (maxLag + 1) must be in [0, 64]");
+  if (world < 1 || world > kMaxRanks) throw std::invalid_argument("XgmiComm: world must be in [1, 16]");
+  if (rank < 0 || rank >= world) throw std::invalid_argument("XgmiComm: bad rank");
+  const Layout L = layout(world, slot_bytes, threshold_rows, min_flag_bytes);
+  slot_bytes_ = L.slot_bytes;
+  maxch_ = L.maxch;
+  off_S_ = L.off_S;
+  slot_stride_ = L.slot_stride;
+  off_R_ = L.off_R;
+  off_B_ = 2 * rows_ * world_ * maxch_ * 4;
+  ll_max_ = L.ll_max;
+  ll_slot_ = L.ll_slot;
+  off_LL_ = L.off_LL;
+  slab_bytes_ = L.slab_bytes;
+  alloc_bytes_ = L.alloc_bytes;
   oneshot_max_ = std::min<int64_t>(slot_bytes_, 256 * 1024);
   if (const char* e = std::getenv("MXAR_ONESHOT_MAX")) oneshot_max_ = std::min<int64_t>(slot_bytes_, std::atoll(e));
   if (grid_ <= 0) grid_ = default_grid(device);
@@ -370,15 +395,26 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
                  "[mxar] WARNING rank %d: study settings active (MXAR_FENCE=%d, MXAR_SLAB_MEM=%s%s); "
                  "results may be wrong - use the defaults in production\n",
                  rank_, fence_, kind.c_str(), std::getenv("MXAR_IPC_NO_PAD") ? ", MXAR_IPC_NO_PAD" : "");
-  if (kind == "coarse") {
+  if (external_slab != nullptr) {
+    // An arena owned by the caller (xgmi_plane.cc): allocated fine-grained and zeroed ONCE,
+    // exported before any peer knew it, and laid out again on every re-initialisation. Its
+    // flags are never zeroed here - a peer may already be writing this epoch's flags; stale
+    // flags of an older layout are older epochs, which no wait accepts.
+    if (external_bytes < slab_bytes_) throw std::invalid_argument("XgmiComm: external slab too small for the layout");
+    slab_ = external_slab;
+    own_slab_ = false;
+    alloc_bytes_ = external_bytes;
+  } else if (kind == "coarse") {
     hip_check(hipMalloc(reinterpret_cast<void**>(&slab_), alloc_bytes_), "hipMalloc(slab)");
   } else {
     const unsigned flags = kind == "fine" ? hipDeviceMallocFinegrained : hipDeviceMallocUncached;
     hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&slab_), alloc_bytes_, flags), "hipExtMallocWithFlags(slab)");
   }
-  // Flags start at 0 = "epoch 0 done"; the first launch uses epoch 1.
-  hip_check(hipMemset(slab_, 0, off_S_), "hipMemset(flags)");
-  hip_check(hipMemset(slab_ + off_LL_, 0, 2 * world_ * ll_slot_), "hipMemset(ll)");  // epoch 0 never occurs
+  if (own_slab_) {
+    // Flags start at 0 = "epoch 0 done"; the first launch uses epoch 1.
+    hip_check(hipMemset(slab_, 0, off_S_), "hipMemset(flags)");
+    hip_check(hipMemset(slab_ + off_LL_, 0, 2 * world_ * ll_slot_), "hipMemset(ll)");  // epoch 0 never occurs
+  }
   hip_check(hipMalloc(reinterpret_cast<void**>(&ctl_), 256), "hipMalloc(ctl)");
   hip_check(hipMemset(ctl_, 0, 256), "hipMemset(ctl)");
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
@@ -387,9 +423,10 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
 
 XgmiComm::~XgmiComm() {
   (void)hipSetDevice(device_);
+  if (switch_ev_) (void)hipEventDestroy(switch_ev_);
   for (int k = 0; k < world_; ++k)
     if (ipc_opened_[k] && peers_[k]) (void)hipIpcCloseMemHandle(peers_[k]);
-  if (slab_) (void)hipFree(slab_);
+  if (slab_ && own_slab_) (void)hipFree(slab_);
   if (ctl_) (void)hipFree(ctl_);
 }
 
@@ -437,7 +474,42 @@ void XgmiComm::connect_local(const std::vector<XgmiComm*>& comms) {
   connected_ = true;
 }
 
+void XgmiComm::connect_ptrs(const std::vector<char*>& bases) {
+  if (static_cast<int>(bases.size()) != world_) throw std::invalid_argument("connect_ptrs: need one base per rank");
+  for (int k = 0; k < world_; ++k) {
+    if (k == rank_) continue;
+    if (bases[k] == nullptr) throw std::invalid_argument("connect_ptrs: null peer slab");
+    peers_[k] = bases[k];
+  }
+  connected_ = true;
+}
+
 void XgmiComm::set_grid(int g) { grid_ = g > 0 ? g : default_grid(device_); }
+
+static bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
+void XgmiComm::order_after_last(hipStream_t s) {
+  if (launched_ && s != last_stream_) {
+    // Graph capture: a captured stream cannot wait on work outside its graph; the caller
+    // orders the graph launch (documented in xgmi_comm.h).
+    if (!capturing(s) && !capturing(last_stream_)) {
+      if (!switch_ev_)
+        hip_check(hipEventCreateWithFlags(&switch_ev_, hipEventDisableTiming), "hipEventCreateWithFlags");
+      hip_check(hipEventRecord(switch_ev_, last_stream_), "hipEventRecord(stream switch)");
+      hip_check(hipStreamWaitEvent(s, switch_ev_, 0), "hipStreamWaitEvent(stream switch)");
+      ++stats_.stream_switches;
+    }
+  }
+  launched_ = true;
+  last_stream_ = s;
+}
+
+void XgmiComm::order_group(const std::vector<XgmiComm*>& group, hipStream_t s) {
+  for (XgmiComm* c : group) c->order_after_last(s);
+}
 
 uint32_t XgmiComm::error() const {
   uint32_t e = 0;
@@ -626,6 +698,7 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
     ++c->stats_.calls;
     c->stats_.bytes += n * es;
   }
+  order_group(group, stream);
   if (c0.world_ == 1 && scale == 1.f) {  // a 1-rank sum is the identity: copy out-of-place, nothing in place
     for (size_t y = 0; y < group.size(); ++y)
       if (ins[y] != outs[y])
@@ -691,6 +764,7 @@ void XgmiComm::step_adamw_local(const std::vector<XgmiComm*>& group, const std::
     ++c->stats_.calls;
     c->stats_.bytes += n * es;
   }
+  order_group(group, stream);
   TraceScope span("xgmi", [&] {
     return std::make_pair("adamw " + std::to_string(n * es) + "B", "{\"rank\":" + std::to_string(c0.rank_) + "}");
   });
@@ -731,6 +805,13 @@ void XgmiComm::geometry_threshold(int64_t n, DType dt, int ranks_here, int64_t* 
   *gx = std::min(gmax, std::max(*nch, 1));
 }
 
+int XgmiComm::round_grid(int nch) const {
+  // one reduce unit per workgroup where possible; at most 1024 gather units per workgroup
+  // (the kernel's pending bitmap)
+  const int64_t units = static_cast<int64_t>(std::max(world_ - 1, 1)) * std::max(nch, 1);
+  return static_cast<int>(std::min<int64_t>(grid_, std::max<int64_t>({1, nch, ceil_div(units, 1024)})));
+}
+
 int XgmiComm::threshold_chunks(int64_t n, DType dt, int ranks_in_launch) const {
   int64_t b, c;
   int nch, gx;
@@ -740,7 +821,7 @@ int XgmiComm::threshold_chunks(int64_t n, DType dt, int ranks_in_launch) const {
 
 void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
                              const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, float thr,
-                             float thc, int32_t* counts, float scale, bool rescale) {
+                             float thc, int32_t* counts, float scale, bool rescale, const RoundSpec* spec) {
   if (group.empty() || ins.size() != group.size() || outs.size() != group.size())
     throw std::invalid_argument("XgmiComm: one input and one output per rank");
   const XgmiComm& c0 = *group[0];
@@ -770,11 +851,20 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
     a.ctl[y] = group[y]->ctl_;
   }
   int gx = 1;
-  c0.geometry_threshold(n, dt, ranks_here, &a.block, &a.chunk, &a.nch, &gx);
+  if (spec != nullptr && spec->block > 0) {  // the protocol's geometry (reference block ranges, maxChunkSize)
+    if (spec->chunk <= 0) throw std::invalid_argument("round: chunk must be > 0");
+    a.block = spec->block;
+    a.chunk = spec->chunk;
+    a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
+    if (ranks_here != 1) throw std::invalid_argument("round: one rank per launch");
+    gx = c0.round_grid(a.nch);
+  } else {
+    c0.geometry_threshold(n, dt, ranks_here, &a.block, &a.chunk, &a.nch, &gx);
+  }
   if (a.block * es > c0.slot_bytes_ || a.nch > c0.maxch_)
     throw std::invalid_argument("allreduce_threshold: tensor exceeds one launch (n * dtype <= world * slot_bytes)");
-  if (ceil_div(static_cast<int64_t>(W - 1) * a.nch, gx) > 64)
-    throw std::logic_error("allreduce_threshold: more than 64 gather units per workgroup");
+  if (ceil_div(static_cast<int64_t>(W - 1) * a.nch, gx) > 1024)
+    throw std::logic_error("allreduce_threshold: more than 1024 gather units per workgroup");
   a.n = n;
   a.P = W;
   a.rows = c0.rows_;
@@ -794,6 +884,12 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
   a.min_reduce = std::max(1, f32_threshold_count(thr, W));
   a.min_complete = f32_threshold_chunks(thc, W, a.nch);
   a.counts = counts;
+  if (spec != nullptr) {
+    a.epoch_set = spec->epoch;
+    a.cold = spec->cold ? 1 : 0;
+    a.order_ref = spec->order_ref ? 1 : 0;
+    a.hforce = spec->host_force;
+  }
   a.delay_rank = -1;
   for (XgmiComm* c : group)
     if (c->delay_rank_ >= 0 && c->delay_us_ > 0) {
@@ -807,6 +903,7 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
                           "{\"rank\":" + std::to_string(c0.rank_) + ",\"ranks_in_launch\":" +
                               std::to_string(ranks_here) + "}");
   });
+  order_group(group, stream);
   launch_threshold(a, dim3(gx, ranks_here), stream, dt);
   hip_check(hipGetLastError(), "threshold launch");
   for (XgmiComm* c : group) {
@@ -815,6 +912,27 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
     ++c->stats_.threshold;
     c->stats_.bytes += n * es;
   }
+}
+
+void XgmiComm::publish_progress(uint32_t value, hipStream_t stream) {
+  if (!connected_) throw std::runtime_error("XgmiComm: connect() first");
+  if (rows_ < 2) throw std::invalid_argument("publish_progress: no threshold rows");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  CommArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.P = world_;
+  a.rows = rows_;
+  a.rank0 = rank_;
+  a.maxch = maxch_;
+  for (int k = 0; k < world_; ++k) a.base[k] = peers_[k];
+  order_after_last(stream);
+  launch_publish_progress(a, value, stream);
+  hip_check(hipGetLastError(), "publish_progress launch");
+}
+
+void XgmiComm::round(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, float th_reduce,
+                     float th_complete, int32_t* counts, const RoundSpec& spec, float scale) {
+  run_threshold({this}, {in}, {out}, n, dt, stream, th_reduce, th_complete, counts, scale, false, &spec);
 }
 
 void XgmiComm::allreduce_threshold(const void* in, void* out, int64_t n, DType dt, hipStream_t stream,
@@ -844,6 +962,7 @@ void XgmiComm::barrier_group(const std::vector<XgmiComm*>& group, hipStream_t st
   a.timeout = static_cast<uint64_t>(c0.timeout_s_ * 1e8);
   a.fence = 3;
   for (int k = 0; k < c0.world_; ++k) a.base[k] = c0.peers_[k];
+  order_group(group, stream);
   hipLaunchKernelGGL(barrier_kernel, dim3(1, static_cast<unsigned>(group.size())), dim3(kCommThreads), 0, stream, a);
   hip_check(hipGetLastError(), "barrier launch");
 }
@@ -875,6 +994,7 @@ void XgmiComm::run_coll(const std::vector<XgmiComm*>& group, Coll op, const std:
     ++c->stats_.calls;
     c->stats_.bytes += in_blocks * m * es;
   }
+  order_group(group, stream);
   if (W == 1) {  // one rank: a copy (scaled for reduce-scatter)
     for (size_t y = 0; y < group.size(); ++y) {
       if (op == Coll::ReduceScatter && scale != 1.f)

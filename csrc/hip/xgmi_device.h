@@ -18,7 +18,9 @@ using namespace dev;
 struct CommArgs {
   const char* in[kMaxRanks];
   char* out[kMaxRanks];
-  uint32_t* ctl[kMaxRanks];  // per rank: [0] epoch [1] ticket [2] error
+  // per rank: [0] epoch [1] ticket [2] error; threshold rounds: [3] completion / late-ticket
+  // counter [4] round count [5] early arrivals [6] snapshot barrier [7] early tickets
+  uint32_t* ctl[kMaxRanks];
   int64_t n;      // elements in this segment
   int64_t block;  // elements per block (two-shot) / whole segment (one-shot)
   int64_t chunk;  // elements per chunk (scatter / gather work unit)
@@ -41,6 +43,13 @@ struct CommArgs {
   int64_t min_complete;  // reduced chunks that complete the round (thComplete)
   int32_t* counts;     // optional [P][nch] contributions per output chunk (0 = missing)
   int rescale;         // scale a chunk reduced from cnt contributions by P / cnt
+  // protocol-engine rounds (xgmi_plane.cc, RoundSpec): explicit round epoch (0 = ctl[4] + 1),
+  // forced-cold round (no own contribution, nothing waited for), the reference's
+  // arrival-order accounting, and the pinned host word the engine raises on a catch-up
+  uint32_t epoch_set;
+  int cold;
+  int order_ref;
+  const uint32_t* hforce;
   // low-latency one-shot (xgmi_ll.hip): slots [parity][src] of ll_slot bytes at off_LL
   int64_t off_LL, ll_slot;
   // fused reduce-scatter + AdamW + all-gather (xgmi_adam.hip): per rank fp32 shard state
@@ -98,7 +107,8 @@ __device__ __forceinline__ void copy_to_slab(char* slab_dst, const char* src, in
   if (t < len) copy_scalar_wt<E>(rd, src, t);
 }
 
-// Copy len elements out of an uncached slab (sc1 loads), 4 packs in flight per lane.
+// Copy len elements out of a (fine-grained) slab with sc1 loads - after the caller's
+// acquire - 4 packs in flight per lane.
 template <class E>
 __device__ __forceinline__ void copy_from_slab(char* dst, const char* slab_src, int64_t len) {
   const int64_t npk = len / E::ELEMS;
@@ -216,9 +226,14 @@ __device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, in
 __device__ __forceinline__ void finish_launch(uint32_t* ctl, uint32_t epoch) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    // relaxed: only the count matters (the next launch is stream-ordered after this one and
-    // kernel end publishes ctl[0]); an acq_rel at agent scope is a `buffer_wbl2` per
-    // workgroup, writing back the XCD's dirty L2 lines mid-kernel (e.g. AdamW state)
+    // relaxed: only the count matters. The next launch of this communicator is ordered
+    // after this one - same stream, or XgmiComm::order_after_last makes the new stream
+    // wait - and kernel end publishes ctl[0]; no peer learns anything from this ticket
+    // (slot reuse is guarded by the kernels' own phase flags). An acq_rel at agent scope
+    // would be a `buffer_wbl2` per workgroup, writing back the XCD's dirty L2 lines
+    // mid-kernel (e.g. AdamW state). Kernels whose last workgroup DOES tell peers that all
+    // reads are done (xgmi_coll.hip FB barrier, xgmi_threshold.hip progress words) keep
+    // an acq_rel ticket.
     const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == gridDim.x - 1) {
       __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -234,6 +249,8 @@ __device__ __forceinline__ uint32_t launch_epoch(const uint32_t* ctl) {
 
 // Host entry of the threshold kernel (xgmi_threshold.hip).
 void launch_threshold(const CommArgs& a, dim3 grid, hipStream_t s, DType dt);
+// Progress words = value in every peer's slab (xgmi_threshold.hip; XgmiComm::publish_progress).
+void launch_publish_progress(const CommArgs& a, uint32_t value, hipStream_t s);
 // Host entry of the low-latency one-shot (xgmi_ll.hip).
 void launch_ll(const CommArgs& a, dim3 grid, hipStream_t s, DType dt);
 // Host entry of the fused reduce-scatter + AdamW + all-gather (xgmi_adam.hip).

@@ -1,0 +1,406 @@
+#include "xgmi_plane.h"
+
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <sstream>
+#include <stdexcept>
+
+#include "../core/data_buffer.h"
+#include "../core/log.h"
+#include "../core/trace.h"
+
+namespace mxar {
+
+namespace {
+
+// Arenas of this process by id: a worker cannot open its own process's IPC handles, so
+// in-process peers (several workers of one process on one GPU) are found here.
+std::mutex g_arena_mu;
+std::map<uint64_t, char*> g_arenas;
+
+std::string to_hex(const std::string& b) {
+  static const char* d = "0123456789abcdef";
+  std::string s;
+  for (unsigned char c : b) {
+    s += d[c >> 4];
+    s += d[c & 15];
+  }
+  return s;
+}
+
+std::string from_hex(const std::string& h) {
+  if (h.size() % 2) throw ProtocolError("plane descriptor: odd hex length");
+  std::string b(h.size() / 2, '\0');
+  for (size_t i = 0; i < b.size(); ++i) b[i] = static_cast<char>(std::stoi(h.substr(2 * i, 2), nullptr, 16));
+  return b;
+}
+
+struct Desc {
+  long pid = 0;
+  int device = 0;
+  int64_t bytes = 0;
+  uint64_t id = 0;
+  std::string handle;
+};
+
+// "xgmi1 pid=<pid> dev=<device> bytes=<arena bytes> id=<arena id> h=<hex IPC handle>"
+Desc parse_desc(const std::string& s) {
+  std::istringstream is(s);
+  std::string tag;
+  is >> tag;
+  if (tag != "xgmi1") throw ProtocolError("not an xGMI plane descriptor: '" + s.substr(0, 40) + "'");
+  Desc d;
+  std::string kv;
+  while (is >> kv) {
+    const size_t eq = kv.find('=');
+    if (eq == std::string::npos) continue;
+    const std::string k = kv.substr(0, eq), v = kv.substr(eq + 1);
+    if (k == "pid") d.pid = std::stol(v);
+    else if (k == "dev") d.device = std::stoi(v);
+    else if (k == "bytes") d.bytes = std::stoll(v);
+    else if (k == "id") d.id = std::stoull(v);
+    else if (k == "h") d.handle = from_hex(v);
+  }
+  if (d.handle.size() != sizeof(hipIpcMemHandle_t)) throw ProtocolError("plane descriptor without an IPC handle");
+  return d;
+}
+
+int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace
+
+XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o), pool_(o.device) {
+  if (o_.capacity <= 0) throw std::invalid_argument("xgmi plane: capacity (elements per round) must be > 0");
+  if (o_.max_peers < 1 || o_.max_peers > 32 || o_.max_peers > kMaxRanks)
+    throw std::invalid_argument("xgmi plane: max_peers must be in [1, 16]");
+  if (o_.max_lag < 0 || o_.max_lag > 62) throw std::invalid_argument("xgmi plane: max_lag must be in [0, 62]");
+  o_.ring = std::max(4, o_.ring);
+  const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
+  // The flag table is reserved at its largest size over every membership of <= max_peers
+  // workers and maxLag <= max_lag, so it sits at the same place in every layout: a late
+  // store of an older layout can only hit a flag word (holding an older, smaller epoch),
+  // never turn data into a flag. Then the largest layout any such membership needs.
+  for (int P = 1; P <= o_.max_peers; ++P) {
+    const int64_t block = static_cast<int64_t>(f32_ceil_div(o_.capacity, P));
+    for (int lag = 0; lag <= o_.max_lag; ++lag)
+      flag_bytes_ = std::max(flag_bytes_, XgmiComm::flag_bytes(P, std::max<int64_t>(block * es, 16), lag + 1));
+  }
+  for (int P = 1; P <= o_.max_peers; ++P) {
+    const int64_t block = static_cast<int64_t>(f32_ceil_div(o_.capacity, P));
+    const XgmiComm::Layout L = XgmiComm::layout(P, std::max<int64_t>(block * es, 16), o_.max_lag + 1, flag_bytes_);
+    arena_bytes_ = std::max(arena_bytes_, L.slab_bytes);
+  }
+  arena_bytes_ = XgmiComm::ipc_safe_bytes(arena_bytes_);
+  hip_check(hipSetDevice(o_.device), "hipSetDevice");
+  hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&arena_), arena_bytes_, hipDeviceMallocFinegrained),
+            "hipExtMallocWithFlags(plane arena)");
+  // zeroed ONCE, before anyone can know the handle: every flag reads "epoch 0 done"
+  hip_check(hipMemset(arena_, 0, arena_bytes_), "hipMemset(plane arena)");
+  hip_check(hipHostMalloc(reinterpret_cast<void**>(&hforce_), 64, hipHostMallocCoherent | hipHostMallocMapped),
+            "hipHostMalloc(force word)");
+  std::memset(hforce_, 0, 64);
+  hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&hforce_dev_), hforce_, 0), "hipHostGetDevicePointer");
+  hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate(plane)");
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  hipIpcMemHandle_t h;
+  hip_check(hipIpcGetMemHandle(&h, arena_), "hipIpcGetMemHandle(plane arena)");
+  std::random_device rd;
+  arena_id_ = (static_cast<uint64_t>(rd()) << 32) ^ rd() ^ reinterpret_cast<uintptr_t>(arena_);
+  {
+    std::lock_guard<std::mutex> g(g_arena_mu);
+    g_arenas[arena_id_] = arena_;
+  }
+  std::ostringstream os;
+  os << "xgmi1 pid=" << static_cast<long>(getpid()) << " dev=" << o_.device << " bytes=" << arena_bytes_
+     << " id=" << arena_id_ << " h=" << to_hex(std::string(reinterpret_cast<const char*>(&h), sizeof(h)));
+  desc_ = os.str();
+  th_ = std::thread([this] { completion_loop(); });
+  MXAR_LOG(INFO, "plane", "xgmi plane on device " << o_.device << ": arena " << (arena_bytes_ >> 20) << " MiB for <= "
+                                                  << o_.max_peers << " workers, maxLag <= " << o_.max_lag);
+}
+
+XgmiRoundPlane::~XgmiRoundPlane() {
+  try {
+    force(0x7fffffff);
+    drain();
+  } catch (...) {
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (th_.joinable()) th_.join();
+  (void)hipSetDevice(o_.device);
+  (void)hipStreamSynchronize(stream_);
+  comm_.reset();
+  for (auto& [h, p] : mapped_) (void)hipIpcCloseMemHandle(p);
+  {
+    std::lock_guard<std::mutex> g(g_arena_mu);
+    g_arenas.erase(arena_id_);
+  }
+  for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+  if (ring_) (void)hipHostFree(ring_);
+  if (hforce_) (void)hipHostFree(hforce_);
+  if (stream_) (void)hipStreamDestroy(stream_);
+  if (arena_) (void)hipFree(arena_);
+}
+
+void XgmiRoundPlane::set_done(DoneFn fn) {
+  std::lock_guard<std::mutex> g(done_mu_);
+  done_ = std::move(fn);
+}
+
+char* XgmiRoundPlane::map_peer(const std::string& desc) {
+  const Desc d = parse_desc(desc);
+  if (d.pid == static_cast<long>(getpid())) {  // a worker of this process: no IPC
+    std::lock_guard<std::mutex> g(g_arena_mu);
+    auto it = g_arenas.find(d.id);
+    if (it == g_arenas.end()) throw ProtocolError("plane descriptor names an arena of this process that is gone");
+    if (d.device != o_.device) {
+      int can = 0;
+      (void)hipDeviceCanAccessPeer(&can, o_.device, d.device);
+      if (!can) throw ProtocolError("no peer access from device " + std::to_string(o_.device) + " to " +
+                                    std::to_string(d.device));
+      const hipError_t e = hipDeviceEnablePeerAccess(d.device, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) hip_check(e, "hipDeviceEnablePeerAccess");
+      (void)hipGetLastError();
+    }
+    return it->second;
+  }
+  auto it = mapped_.find(d.handle);
+  if (it != mapped_.end()) return it->second;
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, d.handle.data(), sizeof(h));
+  void* p = nullptr;
+  hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(peer arena)");
+  mapped_[d.handle] = static_cast<char*>(p);
+  st_.peer_maps++;
+  return static_cast<char*>(p);
+}
+
+void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
+  if (cfg.peers < 1 || cfg.peers > o_.max_peers)
+    throw ProtocolError("xgmi plane sized for <= " + std::to_string(o_.max_peers) + " workers, InitWorkers has " +
+                        std::to_string(cfg.peers));
+  if (cfg.maxLag > o_.max_lag)
+    throw ProtocolError("xgmi plane sized for maxLag <= " + std::to_string(o_.max_lag) + ", InitWorkers has " +
+                        std::to_string(cfg.maxLag));
+  if (cfg.dataSize <= 0 || cfg.dataSize > o_.capacity)
+    throw ProtocolError("xgmi plane holds <= " + std::to_string(o_.capacity) + " elements per round, dataSize " +
+                        std::to_string(cfg.dataSize));
+  if (cfg.maxChunkSize <= 0) throw ProtocolError("maxChunkSize must be > 0");
+  if (static_cast<int>(cfg.descriptors.size()) != cfg.peers)
+    throw ProtocolError("InitWorkers.planes must hold one descriptor per worker");
+  // the previous epoch's rounds finish (forced) before the arena is laid out again
+  if (configured_) {
+    force(last_round_);
+    drain();
+  }
+  hip_check(hipSetDevice(o_.device), "hipSetDevice");
+  const int P = cfg.peers;
+  const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
+  // the reference's geometry: blocks of step = ceil(N / P) (float32 division,
+  // AllreduceWorker.scala:211-214), chunks of maxChunkSize elements (:56-57)
+  block_ = static_cast<int64_t>(f32_ceil_div(cfg.dataSize, P));
+  chunk_ = cfg.maxChunkSize;
+  int64_t nch = std::max<int64_t>(1, ceil_div(block_, chunk_));
+  const int64_t slot = std::max<int64_t>(block_ * es, 16);
+  const XgmiComm::Layout L = XgmiComm::layout(P, slot, cfg.maxLag + 1, flag_bytes_);
+  if (L.slab_bytes > arena_bytes_) throw ProtocolError("xgmi plane arena too small for this membership");
+  if (nch > L.maxch) {
+    // more chunks than the flag table holds (maxChunkSize far below 1 KiB on a big vector):
+    // chunks become whole multiples of maxChunkSize; counts are per such chunk
+    const int64_t m = ceil_div(nch, L.maxch);
+    chunk_ *= m;
+    nch = ceil_div(block_, chunk_);
+    st_.coarsened++;
+    MXAR_LOG(WARNING, "plane", "maxChunkSize " << cfg.maxChunkSize << " gives more chunks than the flag table; "
+                                               << "chunks of " << chunk_ << " elements");
+  }
+  nch_ = static_cast<int>(nch);
+  std::vector<char*> bases(P, nullptr);
+  for (int k = 0; k < P; ++k) {
+    auto it = cfg.descriptors.find(k);
+    if (it == cfg.descriptors.end() || it->second.empty()) throw ProtocolError("InitWorkers.planes misses worker " + std::to_string(k));
+    bases[k] = k == cfg.id ? arena_ : map_peer(it->second);
+  }
+  comm_.reset();
+  comm_ = std::make_unique<XgmiComm>(cfg.id, P, o_.device, slot, o_.grid, o_.timeout_s, cfg.maxLag + 1, arena_,
+                                     arena_bytes_, flag_bytes_);
+  comm_->connect_ptrs(bases);
+  // Every round of the previous epoch has finished here (drained): say so to the peers. Their
+  // lag gates for this epoch's first maxLag + 1 rounds wait for exactly this value, so no
+  // worker writes new-epoch data while any worker may still run an old-epoch round.
+  comm_->publish_progress(cfg.roundBase, stream_);
+  hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize(publish progress)");
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (ring_) (void)hipHostFree(ring_);
+    ring_stride_ = static_cast<size_t>(P) * nch_ + 4;
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&ring_), ring_stride_ * 4 * o_.ring, hipHostMallocDefault),
+              "hipHostMalloc(plane ring)");
+    free_slots_.clear();
+    for (int i = o_.ring - 1; i >= 0; --i) free_slots_.push_back(i);
+    while (static_cast<int>(events_.size()) < o_.ring) {
+      hipEvent_t e = nullptr;
+      hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+      events_.push_back(e);
+    }
+  }
+  cfg_ = cfg;
+  configured_ = true;
+  last_round_ = cfg.startRound - 1;
+  err_seen_ = 0;
+  MXAR_LOG(INFO, "plane", "xgmi plane: worker " << cfg.id << " of " << P << ", block " << block_ << ", chunk "
+                                                << chunk_ << " x " << nch_ << ", rows " << cfg.maxLag + 1
+                                                << ", round epochs from " << cfg.roundBase + 1);
+}
+
+int XgmiRoundPlane::take_slot(std::unique_lock<std::mutex>& lk) {
+  cv_idle_.wait(lk, [&] { return !free_slots_.empty(); });
+  const int s = free_slots_.back();
+  free_slots_.pop_back();
+  return s;
+}
+
+void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
+  if (!configured_) throw ProtocolError("xgmi plane: launch before configure (InitWorkers)");
+  if (round != last_round_ + 1) throw ProtocolError("xgmi plane: rounds must be launched in order");
+  hip_check(hipSetDevice(o_.device), "hipSetDevice");
+  const int64_t n = cfg_.dataSize;
+  const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
+  const int dcode = static_cast<int>(o_.dtype);
+  Rec rec;
+  rec.round = round;
+  rec.epoch = cfg_.epoch;
+  rec.cold = cold;
+  rec.out = pool_.get(static_cast<size_t>(n * es));
+  rec.cnt_dev = pool_.get(static_cast<size_t>(cfg_.peers) * nch_ * 4);
+  const void* in_ptr = rec.out.get();  // a cold round reads no input
+  if (!cold) {
+    if (!input || static_cast<int64_t>(input->size()) != n) throw ProtocolError("xgmi plane: input must hold dataSize elements");
+    auto* dp = dynamic_cast<const DevicePayload*>(input.get());
+    if (dp != nullptr && dp->device() == o_.device) {
+      if (dp->ready()) hip_check(hipStreamWaitEvent(stream_, static_cast<hipEvent_t>(dp->ready().get()), 0), "hipStreamWaitEvent");
+      else if (dp->stream() && dp->stream() != stream_) hip_check(hipStreamSynchronize(dp->stream()), "hipStreamSynchronize");
+      in_ptr = dp->bytes();  // any element alignment: the kernel takes unaligned units element-wise
+      if (dp->dtype() != dcode) {  // cast into the plane's dtype on the device
+        rec.staging = pool_.get(static_cast<size_t>(n * es));
+        launch_cast(dp->bytes(), static_cast<DType>(dp->dtype()), rec.staging.get(), o_.dtype, n, stream_);
+        in_ptr = rec.staging.get();
+      }
+      rec.input = input;  // held until the round completed
+    } else {  // host (or other-device) float32 payload: upload, cast into the plane's dtype
+      const std::vector<float> h = input->to_host();
+      auto up = pool_.get(static_cast<size_t>(n * 4));
+      hip_check(hipMemcpyAsync(up.get(), h.data(), n * 4, hipMemcpyHostToDevice, stream_), "hipMemcpyAsync H2D");
+      hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");  // h is pageable and local
+      if (o_.dtype == DType::F32) {
+        rec.staging = up;
+      } else {
+        rec.staging = pool_.get(static_cast<size_t>(n * es));
+        launch_cast(up.get(), DType::F32, rec.staging.get(), o_.dtype, n, stream_);
+        rec.input = std::make_shared<DevicePayload>(up, 0, static_cast<size_t>(n), o_.device, nullptr);  // keep alive
+      }
+      in_ptr = rec.staging.get();
+    }
+  }
+  XgmiComm::RoundSpec spec;
+  spec.epoch = epoch_of(round);
+  spec.block = block_;
+  spec.chunk = chunk_;
+  spec.cold = cold;
+  spec.order_ref = o_.order_ref;
+  spec.host_force = hforce_dev_;
+  {
+    TraceScope span("plane", [&] {
+      return std::make_pair(std::string(cold ? "cold round " : "round ") + std::to_string(round),
+                            "{\"worker\":" + std::to_string(cfg_.id) + ",\"bytes\":" + std::to_string(n * es) + "}");
+    });
+    comm_->round(in_ptr, rec.out.get(), n, o_.dtype, stream_, cfg_.thReduce, cfg_.thComplete,
+                 static_cast<int32_t*>(rec.cnt_dev.get()), spec, 1.f);
+  }
+  std::unique_lock<std::mutex> lk(mu_);
+  rec.slot = take_slot(lk);
+  int32_t* host = ring_ + static_cast<size_t>(rec.slot) * ring_stride_;
+  hip_check(hipMemcpyAsync(host, rec.cnt_dev.get(), static_cast<size_t>(cfg_.peers) * nch_ * 4, hipMemcpyDeviceToHost,
+                           stream_),
+            "hipMemcpyAsync(counts)");
+  hip_check(hipMemcpyAsync(host + ring_stride_ - 1, comm_->ctl_ptr() + 2, 4, hipMemcpyDeviceToHost, stream_),
+            "hipMemcpyAsync(error word)");
+  rec.ev = events_[rec.slot];
+  hip_check(hipEventRecord(rec.ev, stream_), "hipEventRecord(round)");
+  last_round_ = round;
+  st_.launches++;
+  if (cold) st_.cold++;
+  st_.bytes += static_cast<uint64_t>(n * es);
+  q_.push_back(std::move(rec));
+  lk.unlock();
+  cv_.notify_all();
+}
+
+void XgmiRoundPlane::force(int round) {
+  if (!configured_ || round < cfg_.startRound) return;
+  const int r = std::min(round, std::max(last_round_, cfg_.startRound));
+  const uint32_t e = epoch_of(r);
+  volatile uint32_t* w = hforce_;
+  if (static_cast<int32_t>(e - *w) > 0) {
+    *w = e;  // the kernel polls it (system-scope loads of coherent pinned memory)
+    st_.forced++;
+  }
+}
+
+void XgmiRoundPlane::drain() {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_idle_.wait(lk, [&] { return q_.empty(); });
+}
+
+void XgmiRoundPlane::completion_loop() {
+  for (;;) {
+    Rec rec;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;
+      rec = q_.front();  // stays queued until its callback ran (drain waits for that)
+    }
+    const hipError_t e = hipEventSynchronize(rec.ev);
+    RoundResult res;
+    res.epoch = rec.epoch;
+    res.round = rec.round;
+    res.cold = rec.cold;
+    const int32_t* host = ring_ + static_cast<size_t>(rec.slot) * ring_stride_;
+    const size_t nc = ring_stride_ - 4;
+    res.count.assign(host, host + nc);
+    const uint32_t err = static_cast<uint32_t>(host[ring_stride_ - 1]);
+    res.error = (err & ~err_seen_) | (e != hipSuccess ? 0x80000000u : 0u);
+    err_seen_ |= err;
+    res.data = std::make_shared<DevicePayload>(rec.out, 0, static_cast<size_t>(cfg_.dataSize), o_.device, nullptr,
+                                               nullptr, static_cast<int>(o_.dtype));
+    rec.input.reset();
+    rec.staging.reset();
+    {
+      std::lock_guard<std::mutex> g(done_mu_);
+      if (done_) done_(std::move(res));
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      free_slots_.push_back(rec.slot);
+      q_.pop_front();
+      st_.completed++;
+    }
+    cv_idle_.notify_all();
+  }
+}
+
+std::shared_ptr<XgmiRoundPlane> make_xgmi_plane(const XgmiPlaneOptions& o) {
+  return std::make_shared<XgmiRoundPlane>(o);
+}
+
+}  // namespace mxar

@@ -1,0 +1,133 @@
+// XgmiRoundPlane: the MI355X data plane of the round-granular protocol engine
+// (PlaneWorkerActor, csrc/runtime/plane_worker.h). One persistent threshold-kernel launch
+// per allreduce round (csrc/hip/xgmi_threshold.hip) replaces the reference's per-chunk
+// ScatterBlock / ReduceBlock messages (AllreduceWorker.scala:194-251) with direct xGMI
+// peer stores into the owners' HBM slots.
+//
+//   * Arena: at construction the worker allocates ONE fine-grained HBM arena big enough for
+//     any membership up to `max_peers` workers and `max_lag` (the largest slab layout of
+//     XgmiComm over those), zeroes it once and exports it with hipIpcGetMemHandle. The
+//     handle travels in the worker's registration (MemberUp.meta -> the master ->
+//     InitWorkers.planes), so a worker maps its peers from InitWorkers alone.
+//     Workers of one process find each other's arenas through a process-local registry
+//     (IPC handles cannot be opened by their own process).
+//   * configure (InitWorkers): the reference's block ranges (step = ceil(N / P), float32)
+//     and maxChunkSize chunks; an XgmiComm is laid out over the arena (rows = maxLag + 1)
+//     and connected to the peers' mapped arenas (mappings are kept across epochs).
+//   * launch (StartAllreduce): input ordered after its producer (ready event, no host
+//     sync), one threshold launch with the round's explicit epoch
+//     (roundBase + r - startRound + 1), per-chunk counts and the error word copied to
+//     pinned host memory, a completion event; a completion thread hands each finished
+//     round to the worker in launch order.
+//   * force (catch-up): raises a pinned host word the kernel polls; rounds <= it complete
+//     with what has arrived. Peers ahead by more than maxLag force us through our slab.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../runtime/round_plane.h"
+#include "device_plane.h"
+#include "xgmi_comm.h"
+
+namespace mxar {
+
+struct XgmiPlaneOptions {
+  int device = 0;
+  DType dtype = DType::F32;
+  int64_t capacity = 0;  // elements per round (>= the job's dataSize)
+  int max_peers = 8;     // largest membership the arena is sized for
+  int max_lag = 4;       // largest maxLag the arena is sized for
+  int grid = 0;          // workgroups per launch (0: 2 per CU; split when planes share a GPU)
+  double timeout_s = 60.0;
+  bool order_ref = true;  // the reference's arrival-order accounting (threshold kernel doc)
+  int ring = 64;          // rounds in flight at most (pinned count / error slots)
+};
+
+struct XgmiPlaneStats {
+  uint64_t launches = 0, cold = 0, forced = 0, bytes = 0, completed = 0, coarsened = 0, peer_maps = 0;
+};
+
+class XgmiRoundPlane final : public RoundPlane {
+ public:
+  explicit XgmiRoundPlane(const XgmiPlaneOptions& o);
+  ~XgmiRoundPlane() override;
+  const char* name() const override { return "xgmi"; }
+  std::string descriptor() const override { return desc_; }
+  void set_done(DoneFn fn) override;
+  void configure(const PlaneConfig& cfg) override;
+  void launch(int round, const Payload& input, bool cold) override;
+  void force(int round) override;
+  void drain() override;
+  int chunks() const override { return nch_; }
+
+  const XgmiPlaneOptions& options() const { return o_; }
+  const XgmiPlaneStats& stats() const { return st_; }
+  hipStream_t stream() const { return stream_; }
+  int64_t arena_bytes() const { return arena_bytes_; }
+  int64_t chunk_elems() const { return chunk_; }
+  int64_t block_elems() const { return block_; }
+  XgmiComm* comm() const { return comm_.get(); }
+
+ private:
+  struct Rec {
+    int round = 0;
+    int64_t epoch = 0;
+    std::shared_ptr<void> out, cnt_dev, staging;
+    Payload input;
+    hipEvent_t ev = nullptr;
+    int slot = 0;
+    bool cold = false;
+  };
+  uint32_t epoch_of(int round) const {
+    return cfg_.roundBase + static_cast<uint32_t>(round - cfg_.startRound) + 1u;
+  }
+  char* map_peer(const std::string& desc);
+  int take_slot(std::unique_lock<std::mutex>& lk);
+  void completion_loop();
+
+  XgmiPlaneOptions o_;
+  char* arena_ = nullptr;
+  int64_t arena_bytes_ = 0;
+  int64_t flag_bytes_ = 0;  // flag table reserved at its largest size (every layout the same)
+  uint64_t arena_id_ = 0;
+  std::string desc_;
+  uint32_t* hforce_ = nullptr;      // pinned host word the engine raises (force)
+  uint32_t* hforce_dev_ = nullptr;  // its device-visible address
+  hipStream_t stream_ = nullptr;
+  DevicePool pool_;
+  std::unique_ptr<XgmiComm> comm_;
+  std::map<std::string, char*> mapped_;  // peer IPC handle -> mapping (kept across epochs)
+  PlaneConfig cfg_;
+  bool configured_ = false;
+  int64_t block_ = 0, chunk_ = 0;
+  int nch_ = 0;
+  int last_round_ = -1;  // last launched round of this epoch
+  // pinned ring: per slot P x nch counts + the error word
+  int32_t* ring_ = nullptr;
+  size_t ring_stride_ = 0;  // int32 per slot
+  std::vector<int> free_slots_;
+  uint32_t err_seen_ = 0;
+
+  std::mutex mu_;
+  std::condition_variable cv_, cv_idle_;
+  std::deque<Rec> q_;
+  bool stop_ = false;
+  std::vector<hipEvent_t> events_;
+  std::mutex done_mu_;
+  DoneFn done_;
+  std::thread th_;
+  XgmiPlaneStats st_;
+};
+
+std::shared_ptr<XgmiRoundPlane> make_xgmi_plane(const XgmiPlaneOptions& o);
+
+}  // namespace mxar

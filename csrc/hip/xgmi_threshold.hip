@@ -2,25 +2,43 @@
 //
 // The reference's round semantics on the GPU hot path, in one persistent launch per round:
 //   thReduce   - a chunk of rank r's block is reduced as soon as `min_reduce` of the P
-//                contributions (own included) have arrived; contributions that arrive
-//                later are not waited for (AllreduceWorker.scala:116-121, DataBuffer
-//                reachThreshold :31-33). Missing contributions count as zeros.
+//                contributions (own included) have arrived (AllreduceWorker.scala:116-121,
+//                DataBuffer reachThreshold :31-33). Missing contributions count as zeros.
 //   thComplete - the round completes once `min_complete` of the P x nch reduced chunks are
 //                in; chunks still missing then are output as zeros with count 0
 //                (AllreduceWorker.scala:143-145, reachRoundThreshold DataBuffer.scala:69-75).
 //   maxLag     - the S/R slots and their flags form a ring of `trows` = maxLag + 1 rows
-//                (slab rows 1..trows; row 0 belongs to the lock-step kernels, so a fast
-//                rank that moves on to another algorithm never touches a row a lagging
-//                rank still reads), indexed by the threshold-round counter ctl[4]; a rank
-//                may run up to maxLag rounds ahead of the slowest
-//                peer (the worker's lag ring, AllreduceWorker.scala:59-73). Before
-//                writing row e % rows a rank waits until every peer has finished the
-//                round that last used it (progress words), so a row is never overwritten
-//                while a lagging peer still reads it.
+//                (slab rows 1..trows; row 0 belongs to the lock-step kernels), indexed by
+//                the round epoch (the worker's lag ring, AllreduceWorker.scala:59-73).
+//                Before writing row e % rows a rank waits until every peer has finished
+//                the round that last used it (progress words), so a row is never
+//                overwritten while a lagging peer still reads it.
+//   catch-up   - a rank held at that gate by a laggard does not just wait: it writes a
+//                FORCE request (the round the laggard must finish) into the laggard's slab,
+//                and the laggard's round stops waiting for contributions and reduced chunks
+//                and completes with what has arrived (zeros, count 0 elsewhere) - the
+//                reference's forced catch-up (AllreduceWorker.scala:91-97), triggered by
+//                the fast rank's traffic as in the reference (a future-round message makes
+//                the laggard StartAllreduce, :123-126). The protocol engine raises the same
+//                condition from the host (pinned `hforce` word) when StartAllreduce(r)
+//                arrives with r - maxLag > round; a `cold` round (never started before it
+//                became stale) contributes nothing and waits for nothing.
 //   count      - per output chunk, how many contributions were summed (ReduceBlock.count,
 //                AllreduceMessage.scala:19); 0 marks a chunk that was not completed.
-// Decisions are made per chunk from a snapshot of the arrival flags taken when the count
-// first reaches the threshold (all contributions present at that instant are summed).
+//
+// Two accountings of "what arrived first":
+//   greedy (DP communicator) - a chunk's reduce sums everything present when the count
+//                first reaches min_reduce (own input always present); the round keeps every
+//                reduced chunk that arrived before it gave up. Most data per round.
+//   reference (protocol engine, order_ref) - the reference's actor order: what was already
+//                queued when StartAllreduce was processed comes first (snapshot at launch,
+//                S0 per chunk / R0 for the round), then the worker's own scatter (it sends
+//                to itself first, :194-209, but behind the queued messages), then later
+//                arrivals. A reduce sums exactly the first min_reduce contributions of that
+//                order, and the round output holds exactly the first min_complete reduced
+//                chunks (tickets); own chunks reduced under a forced completion are flushed
+//                after it (outdated), as in the reference. Same outputs and counts as the
+//                host WorkerCore for the same arrival order.
 #include <hip/hip_runtime.h>
 
 #include "xgmi_device.h"
@@ -29,6 +47,10 @@ namespace mxar {
 
 namespace {
 
+constexpr int kMaxGatherUnits = 1024;  // gather units per workgroup (host geometry guarantees)
+constexpr int kGatherWords = kMaxGatherUnits / 64;
+constexpr int kMaxSnapChunks = 64;     // reduce chunks per workgroup with an S0 snapshot
+
 __device__ __forceinline__ uint32_t* prog(const CommArgs& a, int k, int s) {
   return reinterpret_cast<uint32_t*>(a.base[k]) + static_cast<int64_t>(2 * a.rows * a.P) * a.maxch + a.P + s;
 }
@@ -36,13 +58,111 @@ __device__ __forceinline__ uint32_t* f2c(const CommArgs& a, int k, int rs, int c
   return reinterpret_cast<uint32_t*>(a.base[k]) + static_cast<int64_t>(2 * a.rows * a.P) * a.maxch + 2 * a.P +
          static_cast<int64_t>(rs) * a.maxch + c;
 }
+// FORCE[s] in rank k's slab: rank s asks k to complete every round <= this epoch now.
+__device__ __forceinline__ uint32_t* forcew(const CommArgs& a, int k, int s) {
+  return reinterpret_cast<uint32_t*>(a.base[k]) + static_cast<int64_t>(3 * a.rows * a.P) * a.maxch + 2 * a.P + s;
+}
 
-// Sum the sources in `mask` (fixed order s = 0..P-1, fp32), store to own output and to
-// every peer's R slot. Source r is the rank's own input. The mask is wave-uniform.
+// Wave 0 only: is round `epoch` forced? Lane s < P reads FORCE[s] of the own slab (peer s
+// waits at its lag gate for this rank); lane 63 reads the engine's pinned host word when
+// `host` (a PCIe read: callers rate-limit it). Wave-uniform.
+__device__ __forceinline__ bool wave_forced(const CommArgs& a, int r, uint32_t epoch, bool host) {
+  const int s = static_cast<int>(threadIdx.x);
+  bool f = false;
+  if (s < a.P && s != r) f = reached(ld_flag(forcew(a, r, s)), epoch);
+  if (host && s == 63 && a.hforce != nullptr)
+    f = reached(__hip_atomic_load(const_cast<uint32_t*>(a.hforce), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                epoch);
+  return __any(f);
+}
+
+// Host-word polls at most every 20 us per workgroup.
+struct HostPoll {
+  uint64_t next = 0;
+  __device__ __forceinline__ bool due() {
+    const uint64_t t = wall_ticks();
+    if (t < next) return false;
+    next = t + 2000;
+    return true;
+  }
+};
+
+// The first k set bits of `mask` in the order start, start+1, ... (mod P): the reference's
+// rotated peer order (AllreduceWorker.scala:196) as the tie-break among simultaneous arrivals.
+__device__ __forceinline__ uint32_t first_k(uint32_t mask, int k, int start, int P) {
+  uint32_t out = 0;
+  for (int i = 0; i < P && k > 0; ++i) {
+    const int s = (start + i) % P;
+    if ((mask >> s) & 1u) {
+      out |= 1u << s;
+      --k;
+    }
+  }
+  return out;
+}
+
+__device__ __forceinline__ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// Protocol geometry (maxChunkSize elements, reference block ranges) need not be 16-B
+// aligned: such a unit takes an element-wise path (wave-uniform branch).
+template <class E>
+__device__ __forceinline__ void copy_in(char* slab_dst, const char* src, int64_t len) {
+  if (al16(slab_dst) && al16(src)) {
+    copy_to_slab<E>(slab_dst, src, len);
+    return;
+  }
+  const __amdgpu_buffer_rsrc_t rd = slab_rsrc(slab_dst);
+  for (int64_t t = threadIdx.x; t < len; t += kCommThreads) copy_scalar_wt<E>(rd, src, t);
+}
+
+template <class E>
+__device__ __forceinline__ void copy_out(char* dst, const char* slab_src, int64_t len) {
+  if (al16(dst) && al16(slab_src)) {
+    copy_from_slab<E>(dst, slab_src, len);
+    return;
+  }
+  const __amdgpu_buffer_rsrc_t rs = slab_rsrc(slab_src);
+  const __amdgpu_buffer_rsrc_t rd = slab_rsrc(dst);
+  for (int64_t t = threadIdx.x; t < len; t += kCommThreads) st_scalar_wt<E>(rd, t, ld_scalar_sc1<E>(rs, t));
+}
+
+template <class E>
+__device__ __forceinline__ void zero_fill(char* dst, int64_t len) {
+  if (al16(dst)) {
+    const int64_t npk = len / E::ELEMS;
+    Pack16 z;
+    z[0] = z[1] = z[2] = z[3] = 0u;
+    for (int64_t i = threadIdx.x; i < npk; i += kCommThreads) st16(dst + i * 16, z);
+    const int64_t t = npk * E::ELEMS + threadIdx.x;
+    if (t < len) Scalar<E>::store(dst, t, 0.f);
+    return;
+  }
+  for (int64_t t = threadIdx.x; t < len; t += kCommThreads) Scalar<E>::store(dst, t, 0.f);
+}
+
+// Sum the sources in `mask` (fixed order s = 0..P-1, fp32), store to the own output (when
+// own_out != nullptr) and to every peer's R slot. Source r is the rank's own input.
 template <class E>
 __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, uint32_t mask, const char* own_in,
                                               const char* S, int64_t slot, char* own_out, int64_t roff,
                                               int64_t len, bool wt_out, float scale) {
+  const bool vec = al16(own_in) && al16(S) && (own_out == nullptr || al16(own_out)) && (roff & 15) == 0;
+  if (!vec) {
+    for (int64_t t = threadIdx.x; t < len; t += kCommThreads) {
+      float acc = 0.f;
+      for (int s = 0; s < P; ++s)
+        if ((mask >> s) & 1u) acc += ld_scalar_sc1<E>(slab_rsrc(s == r ? own_in : S + s * slot), t);
+      acc *= scale;
+      for (int k = 0; k < P; ++k) {
+        if (k == r) {
+          if (own_out != nullptr) st_scalar_wt<E>(slab_rsrc(own_out), t, acc);
+        } else {
+          st_scalar_wt<E>(slab_rsrc(a.base[k] + roff), t, acc);
+        }
+      }
+    }
+    return;
+  }
   const int64_t npk = len / E::ELEMS;
   constexpr int U = 2;
   int64_t i = threadIdx.x;
@@ -67,6 +187,7 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
     }
     for (int k = 0; k < P; ++k) {
       char* d = k == r ? own_out : a.base[k] + roff;
+      if (d == nullptr) continue;
       if (k == r && !wt_out) {
 #pragma unroll
         for (int u = 0; u < U; ++u) st16(d + (i + u * kCommThreads) * 16, o[u]);
@@ -86,6 +207,7 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
     const Pack16 o = acc.pack();
     for (int k = 0; k < P; ++k) {
       char* d = k == r ? own_out : a.base[k] + roff;
+      if (d == nullptr) continue;
       if (k == r && !wt_out)
         st16(d + i * 16, o);
       else
@@ -100,6 +222,7 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
     acc *= scale;
     for (int k = 0; k < P; ++k) {
       char* d = k == r ? own_out : a.base[k] + roff;
+      if (d == nullptr) continue;
       if (k == r && !wt_out)
         Scalar<E>::store(d, t, acc);
       else
@@ -108,14 +231,11 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
   }
 }
 
-template <class E>
-__device__ __forceinline__ void zero_fill(char* dst, int64_t len) {
-  const int64_t npk = len / E::ELEMS;
-  Pack16 z;
-  z[0] = z[1] = z[2] = z[3] = 0u;
-  for (int64_t i = threadIdx.x; i < npk; i += kCommThreads) st16(dst + i * 16, z);
-  const int64_t t = npk * E::ELEMS + threadIdx.x;
-  if (t < len) Scalar<E>::store(dst, t, 0.f);
+__device__ __forceinline__ uint32_t ld_ctl(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t add_ctl(uint32_t* p, uint32_t v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace
@@ -125,14 +245,19 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   constexpr int es = 16 / E::ELEMS;
   __shared__ uint32_t sh_mask;
   __shared__ int sh_flag;
+  __shared__ uint32_t sh_u32;
+  __shared__ uint64_t sh_arr;
+  __shared__ uint64_t pend[kGatherWords];
+  __shared__ uint64_t early[kGatherWords];
+  __shared__ uint32_t s0[kMaxSnapChunks];
   const int P = a.P;
   const int y = blockIdx.y;
   const int r = a.rank0 + y;
   const char* const in = a.in[y];
   char* const out = a.out[y];
   uint32_t* const ctl = a.ctl[y];
-  // threshold rounds count separately (ctl[4]); flags and progress words carry this count
-  const uint32_t epoch = __hip_atomic_load(&ctl[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  // threshold rounds count separately (ctl[4]); the protocol engine passes its round epochs
+  const uint32_t epoch = a.epoch_set ? a.epoch_set : ld_ctl(&ctl[4]) + 1u;
   const int row = 1 + static_cast<int>(epoch % static_cast<uint32_t>(a.trows));
   const int G = gridDim.x;
   const int64_t slot = a.slot_bytes;
@@ -142,6 +267,13 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   const bool rel = a.fence & 1, acq = a.fence & 2;
   const int Pm1 = P > 1 ? P - 1 : 1;
   int32_t* const counts = a.counts ? a.counts + static_cast<int64_t>(y) * P * a.nch : nullptr;
+  const bool cold = a.cold != 0;
+  const bool ref = a.order_ref != 0;
+  const bool snap = ref && !cold;  // cold rounds are forced from the start: no snapshot
+  const int nu = (P - 1) * a.nch;
+  const int mine = blockIdx.x < static_cast<unsigned>(nu) ? (nu - 1 - static_cast<int>(blockIdx.x)) / G + 1 : 0;
+  const int nwords = (mine + 63) / 64;
+  HostPoll hp;
 
   if (a.delay && r == a.delay_rank) {  // straggler simulation (tests)
     const uint64_t until = wall_ticks() + a.delay;
@@ -149,109 +281,270 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   }
   const uint64_t deadline = wall_ticks() + a.timeout;
 
-  // Lag gate: every peer has finished the round that last used row `row` of its slab
-  // (progress words live in OUR slab, written by the peers at the end of each round).
-  wait_flags([&](int k) -> const uint32_t* { return k == r ? nullptr : prog(a, r, k); }, P,
-             epoch - static_cast<uint32_t>(a.trows), deadline, err, ERR_TIMEOUT_LAG, acq);
-
-  // Phase 1 - ScatterBlock into the owners' row slots
-  const int nu = (P - 1) * a.nch;
-  for (int u = blockIdx.x; u < nu; u += G) {
-    const int c = u / Pm1;
-    const int j = (r + 1 + u % Pm1) % P;
-    const int64_t bstart = static_cast<int64_t>(j) * a.block;
-    const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
-    const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
-    if (len > 0) copy_to_slab<E>(a.base[j] + rowS + r * slot + cstart * es, in + (bstart + cstart) * es, len);
-    publish_flags([&](int) { return f1(a, j, row * P + r, c); }, 1, epoch, rel);
+  // Reference order: what had arrived when the round started (S0 per own chunk, R0 for the
+  // round) comes before the own scatter. One grid-wide count of R0 (every workgroup is
+  // resident) decides how many later arrivals the round still takes.
+  uint32_t etotal = 0;
+  if (snap) {
+    if (threadIdx.x < 64) {
+      const int lane = static_cast<int>(threadIdx.x);
+      int k = 0;
+      for (int c = blockIdx.x; c < a.nch && k < kMaxSnapChunks; c += G, ++k) {
+        const bool in_ = lane < P && lane != r && reached(ld_flag(f1(a, r, row * P + lane, c)), epoch);
+        const uint32_t m = static_cast<uint32_t>(__ballot(in_));
+        if (lane == 0) s0[k] = m;
+      }
+      uint32_t cnt = 0;
+      for (int w = 0; w < nwords; ++w) {
+        const int idx = w * 64 + lane;
+        bool arr = false;
+        if (idx < mine) {
+          const int u = blockIdx.x + idx * G;
+          const int c = u / Pm1;
+          const int j = (r + 1 + u % Pm1) % P;
+          arr = reached(ld_flag(f2(a, r, row * P + j, c)), epoch);
+        }
+        const uint64_t m = __ballot(arr);
+        if (lane == 0) early[w] = m;
+        cnt += static_cast<uint32_t>(__popcll(m));
+      }
+      if (lane == 0) {
+        if (cnt) add_ctl(&ctl[5], cnt);
+        __hip_atomic_fetch_add(&ctl[6], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        while (__hip_atomic_load(&ctl[6], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < static_cast<uint32_t>(G)) {
+          __builtin_amdgcn_s_sleep(1);
+          if (wall_ticks() > deadline) {
+            __hip_atomic_fetch_or(err, ERR_TIMEOUT_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+        }
+        sh_u32 = ld_ctl(&ctl[5]);
+      }
+    }
+    __syncthreads();
+    etotal = sh_u32;
+  } else {
+    for (int w = static_cast<int>(threadIdx.x); w < nwords; w += kCommThreads) early[w] = 0;
   }
 
-  // Phase 2 - reduce own chunk c once min_reduce contributions are in (own one included)
+  // Lag gate: every peer has finished the round that last used row `row` of its slab
+  // (progress words live in OUR slab, written by the peers at the end of each round). A
+  // peer that is not there yet gets a FORCE request: it completes that round with what
+  // has arrived instead of waiting (catch-up), so this wait ends as soon as the laggard
+  // runs. Only a laggard that never runs again (a dead process) turns into ERR_TIMEOUT_LAG.
+  if (threadIdx.x < 64) {
+    const int k = static_cast<int>(threadIdx.x);
+    const uint32_t target = epoch - static_cast<uint32_t>(a.trows);
+    const uint32_t* f = (k < P && k != r) ? prog(a, r, k) : nullptr;
+    bool ok = f == nullptr || reached(ld_flag(f), target);
+    bool asked = false;
+    while (!__all(ok)) {
+      if (!ok && !asked && blockIdx.x == 0) {
+        st_flag(forcew(a, k, r), target);
+        asked = true;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      if (!ok) ok = reached(ld_flag(f), target);
+      if (wall_ticks() > deadline) {
+        if (k == 0) __hip_atomic_fetch_or(err, ERR_TIMEOUT_LAG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    if (acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+
+  // Phase 1 - ScatterBlock into the owners' row slots (a cold round sends nothing)
+  if (!cold) {
+    for (int u = blockIdx.x; u < nu; u += G) {
+      const int c = u / Pm1;
+      const int j = (r + 1 + u % Pm1) % P;
+      const int64_t bstart = static_cast<int64_t>(j) * a.block;
+      const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
+      const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
+      if (len > 0) copy_in<E>(a.base[j] + rowS + r * slot + cstart * es, in + (bstart + cstart) * es, len);
+      publish_flags([&](int) { return f1(a, j, row * P + r, c); }, 1, epoch, rel);
+    }
+  }
+
+  // Phase 2 - reduce own chunk c once min_reduce contributions are in
   const int64_t bstart_own = static_cast<int64_t>(r) * a.block;
   const int64_t blen_own = clamp_len(a.n - bstart_own, a.block);
   const uint32_t all = P >= 32 ? 0xffffffffu : ((1u << P) - 1u);
-  for (int c = blockIdx.x; c < a.nch; c += G) {
+  const uint32_t others = all & ~(1u << r);
+  const uint32_t own = cold ? 0u : (1u << r);
+  int kk = 0;
+  for (int c = blockIdx.x; c < a.nch; c += G, ++kk) {
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     const int64_t len = clamp_len(blen_own - cstart, a.chunk);
     if (threadIdx.x < 64) {
       const int s = static_cast<int>(threadIdx.x);
       const uint32_t* f = (s < P && s != r) ? f1(a, r, row * P + s, c) : nullptr;
-      bool in_ = (s == r) || (f != nullptr && reached(ld_flag(f), epoch));
-      uint32_t m = static_cast<uint32_t>(__ballot(in_)) & all;
-      bool timed_out = false;
-      while (__popc(m) < a.min_reduce && m != all) {
-        __builtin_amdgcn_s_sleep(1);
-        if (!in_ && f != nullptr) in_ = reached(ld_flag(f), epoch);
-        m = static_cast<uint32_t>(__ballot(in_)) & all;
-        if (wall_ticks() > deadline) {
-          timed_out = true;
-          break;
+      bool in_ = f != nullptr && reached(ld_flag(f), epoch);
+      uint32_t present = static_cast<uint32_t>(__ballot(in_)) & others;
+      bool forced = cold, timed_out = false;
+      uint32_t mask = 0;
+      const bool use_snap = snap && kk < kMaxSnapChunks;
+      const uint32_t s0c = use_snap ? s0[kk] : present;
+      if (snap && __popc(s0c) >= a.min_reduce) {
+        mask = first_k(s0c, a.min_reduce, r + 1, P);  // fired while draining the queue: no own
+      } else {
+        mask = (snap ? s0c : 0u) | own;
+        while (!forced) {
+          const uint32_t fresh = present & ~mask;
+          if (snap) {
+            if (fresh && __popc(mask) < a.min_reduce) mask |= first_k(fresh, a.min_reduce - __popc(mask), r + 1, P);
+          } else {
+            mask |= fresh;  // greedy: everything present
+          }
+          if (__popc(mask) >= a.min_reduce || (mask | own) == (own | others)) break;
+          if (wave_forced(a, r, epoch, hp.due())) {
+            forced = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          if (!in_ && f != nullptr) in_ = reached(ld_flag(f), epoch);
+          present = static_cast<uint32_t>(__ballot(in_)) & others;
+          if (wall_ticks() > deadline) {
+            timed_out = true;
+            break;
+          }
+        }
+        if (forced) {  // the reference's forced reduce sums whatever the buffer holds
+          if (!in_ && f != nullptr) in_ = reached(ld_flag(f), epoch);
+          mask = (static_cast<uint32_t>(__ballot(in_)) & others) | own;
         }
       }
       if (threadIdx.x == 0) {
-        sh_mask = m;
+        sh_mask = mask;
         if (timed_out) __hip_atomic_fetch_or(err, ERR_TIMEOUT_SCATTER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // reference order: does the own reduced chunk make this round's output? (forced
+        // reduces are flushed after the completion; a round complete at launch takes none)
+        int take = 1;
+        if (ref) {
+          if (forced || etotal >= static_cast<uint32_t>(a.min_complete))
+            take = 0;
+          else
+            take = etotal + add_ctl(&ctl[3], 1u) < static_cast<uint32_t>(a.min_complete) ? 1 : 0;
+        }
+        sh_flag = take;
       }
       if (acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     const uint32_t mask = sh_mask;
+    const bool take = sh_flag != 0;
     const int cnt = __popc(mask);
     const float sc = (a.rescale && cnt > 0) ? a.scale * static_cast<float>(P) / static_cast<float>(cnt) : a.scale;
-    if (len > 0)
+    char* own_out = out + (bstart_own + cstart) * es;
+    if (len > 0) {
       reduce_masked<E>(a, P, r, mask, in + (bstart_own + cstart) * es, a.base[r] + rowS + cstart * es, slot,
-                       out + (bstart_own + cstart) * es, rowR + r * slot + cstart * es, len, a.fence & 1, sc);
+                       take ? own_out : nullptr, rowR + r * slot + cstart * es, len, a.fence & 1, sc);
+      if (!take) zero_fill<E>(own_out, len);
+    }
     if (threadIdx.x < static_cast<unsigned>(P) && static_cast<int>(threadIdx.x) != r)
       st_flag(f2c(a, static_cast<int>(threadIdx.x), row * P + r, c), static_cast<uint32_t>(cnt));
     if (threadIdx.x == 0) {
-      if (counts) counts[static_cast<int64_t>(r) * a.nch + c] = cnt;
-      __hip_atomic_fetch_add(&ctl[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (counts) counts[static_cast<int64_t>(r) * a.nch + c] = take ? cnt : 0;
+      if (!ref) add_ctl(&ctl[3], 1u);
     }
     publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : f2(a, k, row * P + r, c); }, P, epoch, rel);
   }
 
-  // Phase 3 - gather the other owners' chunks; once min_complete chunks of the round are
-  // in, chunks still missing are given up (zeros, count 0). Units of this workgroup are
-  // polled round-robin so a late chunk never blocks the count of an early one.
-  int mine = 0;
-  for (int u = blockIdx.x; u < nu; u += G) ++mine;
-  uint64_t pending = mine >= 64 ? ~0ull : ((1ull << mine) - 1ull);
+  // Phase 3 - gather the other owners' chunks. Units of this workgroup are polled 64 at a
+  // time by wave 0 and round-robin over passes, so a late chunk never blocks the count of
+  // an early one. The round gives the rest up (zeros, count 0) once it has completed
+  // (greedy: min_complete chunks in; reference: the ticket count reached) or is forced.
+  for (int w = static_cast<int>(threadIdx.x); w < nwords; w += kCommThreads) {
+    const int left = mine - w * 64;
+    pend[w] = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+  }
+  __syncthreads();
   bool gave_up = false;
-  while (pending) {
-    bool progressed = false;
-    for (int i = 0; i < mine; ++i) {
-      if (!((pending >> i) & 1ull)) continue;
-      const int u = blockIdx.x + i * G;
-      const int c = u / Pm1;
-      const int j = (r + 1 + u % Pm1) % P;
-      if (threadIdx.x == 0) sh_flag = reached(ld_flag(f2(a, r, row * P + j, c)), epoch) ? 1 : 0;
-      __syncthreads();
-      const bool arrived = sh_flag != 0;
-      __syncthreads();
-      if (!arrived) continue;
-      if (acq && threadIdx.x < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-      __syncthreads();
-      const int64_t bstart = static_cast<int64_t>(j) * a.block;
-      const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
-      const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
-      if (len > 0) copy_from_slab<E>(out + (bstart + cstart) * es, a.base[r] + rowR + j * slot + cstart * es, len);
-      if (threadIdx.x == 0) {
-        if (counts) counts[static_cast<int64_t>(j) * a.nch + c] = static_cast<int32_t>(ld_flag(f2c(a, r, row * P + j, c)));
-        __hip_atomic_fetch_add(&ctl[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    bool any = false, progressed = false;
+    for (int w = 0; w < nwords; ++w) {
+      if (pend[w] == 0) continue;
+      any = true;
+      if (threadIdx.x < 64) {
+        const int idx = w * 64 + static_cast<int>(threadIdx.x);
+        bool arr = false;
+        if ((pend[w] >> threadIdx.x) & 1ull) {
+          const int u = blockIdx.x + idx * G;
+          const int c = u / Pm1;
+          const int j = (r + 1 + u % Pm1) % P;
+          arr = reached(ld_flag(f2(a, r, row * P + j, c)), epoch);
+        }
+        const uint64_t m = __ballot(arr);
+        if (threadIdx.x == 0) sh_arr = m;
+        if (m && acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      pending &= ~(1ull << i);
-      progressed = true;
+      __syncthreads();
+      uint64_t m = sh_arr;
+      __syncthreads();
+      while (m) {
+        const int i = __ffsll(static_cast<long long>(m)) - 1;
+        m &= m - 1;
+        const int idx = w * 64 + i;
+        const int u = blockIdx.x + idx * G;
+        const int c = u / Pm1;
+        const int j = (r + 1 + u % Pm1) % P;
+        if (threadIdx.x == 0) {
+          int take = 1;
+          if (ref) {
+            if ((early[w] >> i) & 1ull)
+              take = add_ctl(&ctl[7], 1u) < static_cast<uint32_t>(a.min_complete) ? 1 : 0;
+            else
+              take = etotal < static_cast<uint32_t>(a.min_complete) &&
+                             etotal + add_ctl(&ctl[3], 1u) < static_cast<uint32_t>(a.min_complete)
+                         ? 1
+                         : 0;
+          } else {
+            add_ctl(&ctl[3], 1u);
+          }
+          sh_flag = take;
+          pend[w] &= ~(1ull << i);
+        }
+        __syncthreads();
+        const bool take = sh_flag != 0;
+        const int64_t bstart = static_cast<int64_t>(j) * a.block;
+        const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
+        const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
+        if (len > 0) {
+          if (take)
+            copy_out<E>(out + (bstart + cstart) * es, a.base[r] + rowR + j * slot + cstart * es, len);
+          else
+            zero_fill<E>(out + (bstart + cstart) * es, len);
+        }
+        if (threadIdx.x == 0 && counts)
+          counts[static_cast<int64_t>(j) * a.nch + c] =
+              take ? static_cast<int32_t>(ld_flag(f2c(a, r, row * P + j, c))) : 0;
+        progressed = true;
+        __syncthreads();
+      }
     }
-    if (!pending || progressed) continue;
-    if (threadIdx.x == 0) {
-      const int64_t done = __hip_atomic_load(&ctl[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int give = done >= a.min_complete ? 1 : 0;
+    if (!any) break;
+    if (progressed) continue;
+    if (threadIdx.x < 64) {
+      int give = 0;
+      const uint32_t done = ld_ctl(&ctl[3]);
+      if (ref)
+        give = (etotal >= static_cast<uint32_t>(a.min_complete) ||
+                etotal + done >= static_cast<uint32_t>(a.min_complete))
+                   ? 1
+                   : 0;
+      else
+        give = done >= static_cast<uint32_t>(a.min_complete) ? 1 : 0;
+      if (!give && (cold || wave_forced(a, r, epoch, hp.due()))) give = 1;
       if (!give && wall_ticks() > deadline) {
-        __hip_atomic_fetch_or(err, ERR_TIMEOUT_REDUCE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (threadIdx.x == 0)
+          __hip_atomic_fetch_or(err, ERR_TIMEOUT_REDUCE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         give = 1;
       }
-      sh_flag = give;
+      if (threadIdx.x == 0) sh_flag = give;
     }
     __syncthreads();
     gave_up = sh_flag != 0;
@@ -260,34 +553,57 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
     __builtin_amdgcn_s_sleep(2);
   }
   if (gave_up) {
-    for (int i = 0; i < mine; ++i) {
-      if (!((pending >> i) & 1ull)) continue;
-      const int u = blockIdx.x + i * G;
-      const int c = u / Pm1;
-      const int j = (r + 1 + u % Pm1) % P;
-      const int64_t bstart = static_cast<int64_t>(j) * a.block;
-      const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
-      const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
-      if (len > 0) zero_fill<E>(out + (bstart + cstart) * es, len);
-      if (threadIdx.x == 0 && counts) counts[static_cast<int64_t>(j) * a.nch + c] = 0;
+    for (int w = 0; w < nwords; ++w) {
+      uint64_t m = pend[w];
+      while (m) {
+        const int i = __ffsll(static_cast<long long>(m)) - 1;
+        m &= m - 1;
+        const int u = blockIdx.x + (w * 64 + i) * G;
+        const int c = u / Pm1;
+        const int j = (r + 1 + u % Pm1) % P;
+        const int64_t bstart = static_cast<int64_t>(j) * a.block;
+        const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
+        const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
+        if (len > 0) zero_fill<E>(out + (bstart + cstart) * es, len);
+        if (threadIdx.x == 0 && counts) counts[static_cast<int64_t>(j) * a.nch + c] = 0;
+      }
     }
   }
 
-  // Round end: the last workgroup resets the completion counter, advances the round count and
-  // tells every peer that this rank is done with row `row` (all its reads happened
-  // before the workgroups' tickets).
+  // Round end: the last workgroup resets the per-round counters, records the round and
+  // tells every peer that this rank is done with row `row`. acq_rel ticket (unlike
+  // finish_launch): the progress word promises peers that EVERY workgroup's reads of the
+  // row are done, so each ticket is ordered after its workgroup's loads.
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (t == static_cast<uint32_t>(G) - 1) {
       __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&ctl[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ctl[5], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ctl[6], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ctl[7], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&ctl[4], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       for (int k = 0; k < P; ++k)
         if (k != r) st_flag(prog(a, k, r), epoch);
     }
   }
+}
+
+// One wave: lane k < P stores this rank's progress word into peer k's slab, after a
+// system-scope release (everything this rank did before is visible first).
+__global__ __launch_bounds__(64) void publish_progress_kernel(CommArgs a, uint32_t value) {
+  const int k = static_cast<int>(threadIdx.x);
+  if (k < a.P && k != a.rank0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st_flag(prog(a, k, a.rank0), value);
+  }
+}
+
+void launch_publish_progress(const CommArgs& a, uint32_t value, hipStream_t s) {
+  hipLaunchKernelGGL(publish_progress_kernel, dim3(1), dim3(64), 0, s, a, value);
 }
 
 void launch_threshold(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {

@@ -1,6 +1,5 @@
 #include "allreduce_actors.h"
 
-#include <cstdio>
 
 #include "../core/log.h"
 
@@ -64,6 +63,8 @@ void WorkerActor::receive(Envelope& env, ActorContext& ctx) {
     void operator()(AllreduceFinished&) {}
     void operator()(PoisonPill&) {}
     void operator()(TextMessage&) {}
+    void operator()(RoundTimeout&) {}
+    void operator()(PlaneRoundDone&) {}
   };
   std::visit(Visitor{this, env, ctx}, env.msg);
   ctx_ = nullptr;
@@ -109,6 +110,7 @@ int MasterActor::handle_of(const ActorRef& ref, bool create) {
     if (handles_[i] == ref) return static_cast<int>(i);
   if (!create) return -1;
   handles_.push_back(ref);
+  metas_.emplace_back();
   return static_cast<int>(handles_.size() - 1);
 }
 
@@ -118,7 +120,9 @@ void MasterActor::receive(Envelope& env, ActorContext& ctx) {
     MXAR_LOG(INFO, "master", "----Detect member " << (up->address.empty() ? up->ref->path() : up->address) << " up");
     if (up->role == "worker" && up->ref) {
       ctx.watch(up->ref);  // AllreduceMaster.scala:74
-      core_.on_member_up(handle_of(up->ref, true));
+      const int h = handle_of(up->ref, true);
+      if (!up->meta.empty()) metas_[h] = up->meta;
+      core_.on_member_up(h);
     }
   } else if (auto* t = std::get_if<Terminated>(&env.msg)) {
     MXAR_LOG(INFO, "master", "----" << (t->ref ? t->ref->path() : "?") << " is terminated, removing it from the set");
@@ -126,18 +130,14 @@ void MasterActor::receive(Envelope& env, ActorContext& ctx) {
     if (h >= 0) core_.on_terminated(h);
   } else if (auto* c = std::get_if<CompleteAllreduce>(&env.msg)) {
     core_.on_complete(c->srcId, c->round, c->epoch);
-  } else if (auto* tm = std::get_if<TextMessage>(&env.msg)) {
-    long long epoch = 0;
-    int round = 0;
-    if (std::sscanf(tm->text.c_str(), "mxar.round-timeout %lld %d", &epoch, &round) == 2)
-      core_.on_round_timeout(epoch, round);
+  } else if (auto* rt = std::get_if<RoundTimeout>(&env.msg)) {
+    core_.on_round_timeout(rt->epoch, rt->round);
   }
   ctx_ = nullptr;
 }
 
 void MasterActor::arm_round_timer(int64_t epoch, int round, int ms) {
-  ctx_->system().schedule_once(std::chrono::milliseconds(ms), ctx_->self(),
-                               TextMessage{"mxar.round-timeout " + std::to_string(epoch) + " " + std::to_string(round)});
+  ctx_->system().schedule_once(std::chrono::milliseconds(ms), ctx_->self(), RoundTimeout{epoch, round});
 }
 
 void MasterActor::send_init(int handle, const InitParams& p, const std::map<int, int>& ids) {
@@ -152,6 +152,11 @@ void MasterActor::send_init(int handle, const InitParams& p, const std::map<int,
   m.maxChunkSize = p.maxChunkSize;
   m.epoch = p.epoch;
   m.startRound = p.startRound;
+  m.roundBase = p.roundBase;
+  bool any_plane = false;
+  for (auto& [id, h] : ids) any_plane = any_plane || !metas_[h].empty();
+  if (any_plane)
+    for (auto& [id, h] : ids) m.planes[id] = metas_[h];
   handles_[handle]->tell(Message(std::move(m)), ctx_->self());
 }
 

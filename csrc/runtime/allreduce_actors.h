@@ -65,6 +65,7 @@ class MasterActor final : public Actor, public MasterEffects {
   int handle_of(const ActorRef& ref, bool create);
   MasterCore core_;
   std::vector<ActorRef> handles_;
+  std::vector<std::string> metas_;  // per handle: MemberUp.meta (plane descriptor or "")
   FinishedCallback on_finished_;
   RoundCallback on_round_;
   ActorContext* ctx_ = nullptr;

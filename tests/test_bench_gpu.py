@@ -14,11 +14,12 @@ ROOT = Path(__file__).resolve().parents[1]
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.timeout(300)
 def test_bench_prints_one_json_line_with_contract_fields():
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1", "--no-tune",
                         "--no-rccl", "--no-threshold", "--no-collectives", "--no-fused-step", "--dp-timeout", "90"],
-                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, p.stdout[:2000]
@@ -31,7 +32,16 @@ def test_bench_prints_one_json_line_with_contract_fields():
     assert d["value"] > 0 and d["ms_per_step"] > 0
     for k in ("model", "global_batch", "seq_len", "parallelism"):
         assert k in d["config"], k
+    assert d["status"] == "ok" and d["config"]["algo"] == "copy (world=1)"
+    assert d["validated"] and all(d["validated"].values()), d.get("validation")
+    assert d["topology"]["devices_visible"] >= 1
+    loc = d["local_ranks"]
+    assert "error" not in loc, loc
+    for algo in ("twoshot", "ring"):
+        assert loc[algo]["validated"] and 0 < loc[algo]["frac_copy_roofline"] < 1.5, loc
     for model in ("resnet50", "llama3_8b"):
         row = d["dp"][model]
         assert "error" not in row, row
         assert row["step_ms"] > 0 and row["compute_ms"] > 0
+        # world = 1: no bandwidth figure for an allreduce that launches nothing
+        assert "comm_algbw_per_rank" not in row and "note" in row

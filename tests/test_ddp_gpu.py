@@ -81,6 +81,70 @@ def test_ddp_reducer_xgmi_two_processes(dtype, mode):
     assert not bad, bad[0][2]
 
 
+def _mixed_stream_worker(rank, world, port, q):
+    """The reducer's buckets are still queued on its comm stream when user code calls the SAME
+    communicator on the default stream: the communicator orders the second stream after its
+    previous launch (XgmiComm::order_after_last), so both results are exact."""
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.ops import fill_uniform
+    from akka_allreduce_1_amd.parallel import BucketedGradReducer, XgmiCommunicator
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = XgmiCommunicator(device=0, slot_bytes=1 << 20, grid=8, timeout_s=15.0)
+        m, ref = _model(0, torch.float32), _model(0, torch.float32)
+        red = BucketedGradReducer(m, comm, bucket_bytes=32 << 10, op="avg", algo="twoshot@4")
+        g = torch.Generator(device="cuda:0")
+        data = [torch.randn(16, 64, device="cuda:0", generator=g.manual_seed(50 + r)) for r in range(world)]
+        for step in range(4):
+            xs = [fill_uniform(torch.empty(300_001, device="cuda:0"), seed=100 * step + r) for r in range(world)]
+            red.zero_grad()
+            m(data[rank] * (step + 1)).pow(2).mean().backward()  # buckets enqueued on the comm stream
+            y = comm.allreduce(xs[rank], algo="twoshot")  # default stream, same communicator
+            red.wait()
+            comm.check()
+            exp_y = xs[0] + xs[1]
+            assert (y - exp_y).abs().max().item() <= 1e-5, ("user allreduce", step)
+            grads = []
+            for r in range(world):
+                ref.zero_grad()
+                ref(data[r] * (step + 1)).pow(2).mean().backward()
+                grads.append([p.grad.clone() for p in ref.parameters()])
+            for i, p in enumerate(m.parameters()):
+                exp = sum(gr[i] for gr in grads) / world
+                err = (p.grad - exp).abs().max().item()
+                assert err <= 1e-5 * (exp.abs().max().item() + 1e-3), ("reducer", step, i, err)
+        assert comm.native.stats.stream_switches >= 4, comm.native.stats.stream_switches
+        q.put((rank, True, ""))
+    except Exception:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, False, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_reducer_and_default_stream_share_a_communicator():
+    from akka_allreduce_1_amd.parallel import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_mixed_stream_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    bad = [r for r in res if not r[1]]
+    assert not bad, bad[0][2]
+
+
 def _zero_worker(rank, world, port, q, fused=False):
     import torch.distributed as dist
 

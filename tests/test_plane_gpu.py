@@ -1,0 +1,361 @@
+"""The protocol-driven GPU round engine (csrc/runtime/plane_worker.*, csrc/hip/xgmi_plane.*,
+csrc/hip/xgmi_threshold.hip) on one MI355X.
+
+* exact rounds: master + P plane workers, thresholds 1, the reference's (unaligned) block
+  ranges and maxChunkSize chunks: every round's output is the exact sum, every count is P;
+* a deterministic straggler at th < 1 gives the SAME outputs and counts as the host
+  WorkerCore (the reference's state machine) in the same scenario - including the
+  reference's own-block-missing output of the straggler (its own ReduceBlocks are queued
+  behind the completion);
+* catch-up, GPU analogues of AllreduceSpec T13 (simple) and T14 (cold): rounds complete
+  with what arrived when StartAllreduce runs more than maxLag ahead, no error word, no
+  reset;
+* the reference deployment: mxar-master + P `mxar-worker --device 0` processes, 101 rounds.
+Worker k's data is i + iteration + 1000 k, so a chunk's sum identifies its contributors.
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from akka_allreduce_1_amd._native import C  # noqa: E402
+from akka_allreduce_1_amd.engine import PlaneJob, iota_source  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEV = torch.device("cuda", 0)
+F = np.float32
+
+
+def layout(n, P, C_):
+    step = -(-n // P)
+    return step, -(-step // C_)
+
+
+def expected(n, it, ranks):
+    i = np.arange(n, dtype=np.float64)
+    return sum(i + it + 1000.0 * k for k in ranks)
+
+
+def subset_of(vals, lo, hi, it, cnt, P):
+    """Which contributor subset (by sum of ids) produced vals[lo:hi] of round `it`; None if no
+    subset of size cnt fits every element."""
+    i = np.arange(lo, hi, dtype=np.float64)
+    s = (vals[lo:hi].astype(np.float64) - cnt * (i + it)) / 1000.0
+    if not np.allclose(s, s[0], atol=1e-3) or abs(s[0] - round(s[0])) > 1e-3:
+        return None
+    return int(round(s[0]))
+
+
+@pytest.mark.parametrize("P,n,chunk,dtype", [(2, 10, 2, torch.float32), (2, 10007, 333, torch.float32),
+                                             (3, 30000, 1000, torch.float32), (3, 4096, 512, torch.bfloat16)])
+def test_plane_rounds_exact_at_threshold_one(P, n, chunk, dtype):
+    job = PlaneJob(P, n, max_chunk_size=chunk, th_reduce=1.0, th_complete=1.0, max_lag=1, max_round=12, dtype=dtype,
+                   timeout_s=20.0)
+    try:
+        job.run(timeout=120)
+        assert job.rounds["n"] == 13
+        step, nch = layout(n, P, chunk)
+        for k in range(P):
+            st = job.system.plane_worker_state(job.workers[k])
+            assert st["stats"]["plane_errors"] == 0 and st["stats"]["rounds_completed"] == 13, st
+            for it in range(13):
+                data, counts = job.outputs[k][it]
+                assert data.dtype == dtype and data.numel() == n
+                got = data.float().cpu().numpy()
+                if dtype == torch.float32:
+                    np.testing.assert_array_equal(got, expected(n, it, range(P)), err_msg=f"worker {k} round {it}")
+                else:  # fp32 sum of the bf16 inputs, one rounding
+                    ar = torch.arange(n, dtype=torch.float64)
+                    ref = sum((ar + it + 1000.0 * j).to(dtype).double() for j in range(P)).numpy()
+                    assert np.all(np.abs(got - ref) <= np.abs(ref) * 2.0 ** -8 + 1e-6), (k, it)
+                assert len(counts) == P * job.planes[k].chunks
+                assert all(c == P for c in counts), counts
+        assert job.planes[0].stats.launches == 13
+    finally:
+        job.shutdown()
+
+
+def _host_outputs(P, n, chunk, th, straggler, delay, rounds):
+    """The same scenario on the host WorkerCore (the reference's state machine)."""
+    system = C.ActorSystem("Host", False)
+    done = {}
+    fin = __import__("threading").Event()
+    outs = [dict() for _ in range(P)]
+
+    def src(k):
+        base = np.arange(n, dtype=F) + F(1000 * k)
+
+        def f(req):
+            if k == straggler:
+                time.sleep(delay)
+            return C.AllReduceInput(base + F(req.iteration))
+        return f
+
+    def sink(k):
+        def f(out):
+            outs[k][out.iteration] = (np.asarray(out.data).copy(), list(out.count))
+        return f
+
+    master = system.master(P, 1.0, th, th, 1, n, rounds - 1, chunk, on_finished=lambda r: fin.set())
+    ws = [system.worker(src(k), sink(k), f"w{k}") for k in range(P)]
+    for w in ws:
+        master.tell(C.MemberUp(w, "worker", ""), None)
+    assert fin.wait(60)
+    system.await_idle(5.0)
+    system.shutdown()
+    del done
+    return outs
+
+
+def test_straggler_matches_host_worker_core():
+    P, n, chunk, rounds = 3, 3000, 250, 4
+    th = 2.0 / 3.0
+    straggler, delay = 2, 0.3
+    host = _host_outputs(P, n, chunk, th, straggler, delay, rounds)
+
+    def slow(source):
+        def f(req):
+            time.sleep(delay)
+            return source(req)
+        return f
+
+    srcs = [iota_source(n, DEV, torch.float32, 1000.0 * k) for k in range(P)]
+    srcs[straggler] = slow(srcs[straggler])
+    job = PlaneJob(P, n, max_chunk_size=chunk, th_reduce=th, th_complete=th, max_lag=1, max_round=rounds - 1,
+                   sources=srcs, timeout_s=20.0)
+    try:
+        job.run(timeout=120)
+        for k in range(P):
+            for it in range(rounds):
+                g, gc = job.outputs[k][it]
+                h, hc = host[k][it]
+                assert gc == hc, (k, it, gc, hc)
+                np.testing.assert_array_equal(g.float().cpu().numpy(), h, err_msg=f"worker {k} round {it}")
+        # the shape of the result, as the reference defines it
+        step, nch = layout(n, P, chunk)
+        g, gc = job.outputs[straggler][1]
+        assert gc[straggler * nch:(straggler + 1) * nch] == [0] * nch  # own block missing (queued behind)
+        assert not g[straggler * step:].float().abs().sum().item()
+        assert gc[:2 * nch] == [2] * (2 * nch)
+    finally:
+        job.shutdown()
+
+
+def _consistent(job, P, n, chunk, counts_ok):
+    """Every chunk of every output is the sum of `count` distinct workers (0 -> zeros)."""
+    step, nch = layout(n, P, chunk)
+    for k in range(P):
+        for it, (data, counts) in job.outputs[k].items():
+            v = data.float().cpu().numpy()
+            for j in range(P):
+                for c in range(nch):
+                    lo, hi = j * step + c * chunk, min(n, j * step + min(step, (c + 1) * chunk))
+                    if lo >= hi:
+                        continue
+                    cnt = counts[j * nch + c]
+                    assert cnt in counts_ok, (k, it, j, c, cnt)
+                    if cnt == 0:
+                        assert not np.any(v[lo:hi]), (k, it, j, c)
+                    else:
+                        assert subset_of(v, lo, hi, it, cnt, P) is not None, (k, it, j, c, cnt)
+
+
+def test_simple_catchup_forces_rounds_without_errors():
+    """T13 analogue (AllreduceSpec.scala:535-559): the straggler stalls, the fast workers'
+    reduces fire (thReduce 2/3) but their rounds cannot complete (thComplete 1); the master's
+    round deadline keeps starting rounds, StartAllreduce(r) with r - maxLag > round forces the
+    stuck round to complete with what arrived (the straggler's block: zeros, count 0). When
+    the straggler wakes, the fast workers' FORCE requests complete its stale round at once."""
+    P, n, chunk = 3, 6000, 500
+    srcs = [iota_source(n, DEV, torch.float32, 1000.0 * k) for k in range(P)]
+    base = srcs[2]
+
+    def stall(req):
+        if req.iteration == 0:
+            time.sleep(2.0)
+        return base(req)
+
+    srcs[2] = stall
+    job = PlaneJob(P, n, max_chunk_size=chunk, th_reduce=2.0 / 3.0, th_complete=1.0, max_lag=1, max_round=8,
+                   sources=srcs, round_timeout_ms=250, timeout_s=30.0)
+    try:
+        job.run(timeout=180)
+        st = job.state()
+        for k, w in enumerate(st["workers"]):
+            assert w["stats"]["plane_errors"] == 0, (k, w)  # no ERR_TIMEOUT_LAG, no timeouts
+            assert w["round"] == 9, (k, w)  # every round 0..maxRound completed
+        assert sum(w["stats"]["forced_completions"] for w in st["workers"][:2]) > 0, st
+        _consistent(job, P, n, chunk, {0, 2, 3})
+        step, nch = layout(n, P, chunk)
+        # round 0 of a fast worker: forced; the fast blocks made it (count 2), the straggler's not
+        data, counts = job.outputs[0][0]
+        assert counts[:2 * nch] == [2] * (2 * nch) and counts[2 * nch:] == [0] * nch, counts
+    finally:
+        job.shutdown()
+
+
+def test_cold_catchup():
+    """T14 analogue (AllreduceSpec.scala:561-584): worker 2 first hears of the job at
+    StartAllreduce(4) (maxLag 1): rounds 0..2 are completed cold - nothing of its own, what
+    the peers delivered - and 3..4 run normally; the fast workers, held at their lag gate,
+    resume as soon as the cold rounds publish progress."""
+    P, n, chunk = 3, 6000, 500
+    th = 2.0 / 3.0
+    system = C.ActorSystem("Cold", False)
+    probe = system.probe("master")
+    planes = [C.hip.xgmi_plane(0, C.hip.DType.F32, n, max_peers=P, max_lag=1, grid=64, timeout_s=30.0)
+              for _ in range(P)]
+    outs = [dict() for _ in range(P)]
+
+    def sink(k):
+        return lambda out: outs[k].__setitem__(out.iteration, (out.data, list(out.count)))
+
+    ws = [system.plane_worker(iota_source(n, DEV, torch.float32, 1000.0 * k), sink(k), planes[k], f"w{k}")
+          for k in range(P)]
+    try:
+        wmap = {k: ws[k] for k in range(P)}
+        descs = {k: planes[k].descriptor for k in range(P)}
+        for k in range(P):
+            m = C.InitWorkers(wmap, probe, k, th, th, 1, n, chunk, epoch=1)
+            m.planes = descs
+            ws[k].tell(m, None)
+        got = set()
+
+        def collect(want, limit):
+            t0 = time.time()
+            while not want <= got and time.time() - t0 < limit:
+                e = probe.receive(1.0)
+                if e is not None and isinstance(e[0], C.CompleteAllreduce):
+                    got.add((e[0].srcId, e[0].round))
+            return want <= got
+
+        # the fast workers run rounds 0 and 1 one at a time, as the master would start them (a
+        # StartAllreduce(r) that arrives while round r - maxLag - 1 is still open forces it -
+        # the reference's catch-up rule); round 2 then waits at its lag gate for worker 2
+        for r in (0, 1):
+            for k in (0, 1):
+                ws[k].tell(C.StartAllreduce(r, 1), None)
+            assert collect({(0, r), (1, r)}, 30), sorted(got)
+        for r in (2, 3, 4):
+            for k in (0, 1):
+                ws[k].tell(C.StartAllreduce(r, 1), None)
+        time.sleep(0.3)
+        ws[2].tell(C.StartAllreduce(4, 1), None)  # worker 2's first StartAllreduce
+        collect({(k, r) for k in range(P) for r in range(5)}, 60)
+        assert got == {(k, r) for k in range(P) for r in range(5)}, sorted(got)
+        st = system.plane_worker_state(ws[2])
+        assert st["stats"]["cold_rounds"] == 3 and st["stats"]["plane_errors"] == 0, st
+        for k in (0, 1):
+            assert system.plane_worker_state(ws[k])["stats"]["plane_errors"] == 0
+        step, nch = layout(n, P, chunk)
+        for it in (0, 1):  # cold rounds whose fast blocks were reduced before worker 2 started
+            data, counts = outs[2][it]
+            assert counts[:2 * nch] == [2] * (2 * nch), (it, counts)
+            assert counts[2 * nch:] == [0] * nch, (it, counts)  # nothing of its own in a cold round
+            v = data.float().cpu().numpy()
+            np.testing.assert_array_equal(v[:2 * step], expected(n, it, (0, 1))[:2 * step])
+            assert not np.any(v[2 * step:])
+
+        class J:
+            outputs = outs
+        _consistent(J, P, n, chunk, {0, 2, 3})
+    finally:
+        system.shutdown()
+
+
+def test_plane_stale_epoch_and_reinit():
+    """A re-initialisation (new membership epoch, startRound) lays the same arenas out again:
+    the new epoch's round epochs start above the old ones (InitWorkers.roundBase), so flags
+    the old epoch left behind are never taken for new arrivals."""
+    P, n, chunk = 2, 5000, 700
+    job = PlaneJob(P, n, max_chunk_size=chunk, max_round=3, timeout_s=20.0)
+    try:
+        job.run(timeout=60)
+        # second epoch by hand: same planes, resume at round 7, round base above epoch 1
+        probe = job.system.probe("m2")
+        wmap = {k: job.workers[k] for k in range(P)}
+        for k in range(P):
+            m = C.InitWorkers(wmap, probe, k, 1.0, 1.0, 1, n, chunk, epoch=2, startRound=7)
+            m.planes = {j: job.planes[j].descriptor for j in range(P)}
+            m.roundBase = 100
+            job.workers[k].tell(m, None)
+        for r in (7, 8, 9):
+            for k in range(P):
+                job.workers[k].tell(C.StartAllreduce(r, 2), None)
+        got = set()
+        t0 = time.time()
+        while len(got) < 6 and time.time() - t0 < 30:
+            e = probe.receive(5.0)
+            if e is not None and isinstance(e[0], C.CompleteAllreduce):
+                assert e[0].epoch == 2
+                got.add((e[0].srcId, e[0].round))
+        assert got == {(k, r) for k in range(P) for r in (7, 8, 9)}
+        for it in (7, 8, 9):
+            data, counts = job.outputs[0][it]
+            np.testing.assert_array_equal(data.cpu().numpy(), expected(n, it, range(P)))
+    finally:
+        job.shutdown()
+
+
+@pytest.mark.parametrize("P,n,chunk", [(2, 10, 2), (3, 3000, 100)])
+def test_cli_master_and_gpu_worker_processes(tmp_path, P, n, chunk):
+    """The reference's deployment (README.md:3-7) on the GPU: mxar-master + P
+    `mxar-worker --device 0` processes (plane descriptors in the cluster join, relayed in
+    InitWorkers), 101 rounds at th = 1, exact sums on every worker."""
+    from akka_allreduce_1_amd.parallel.comm import free_port
+
+    port = free_port()
+    fast = ["--set", "mxar.cluster.failure-detector.heartbeat-interval=100ms",
+            "--set", "mxar.cluster.failure-detector.acceptable-heartbeat-pause=3s",
+            "--set", "mxar.cluster.auto-down-unreachable-after=5s", "--set", "mxar.loglevel=WARNING"]
+    seed = ["--set", f"mxar.cluster.seed-nodes=mxar.tcp://ClusterSystem@127.0.0.1:{port}"]
+    exact = ["--set", "mxar.allreduce.th-reduce=1.0", "--set", "mxar.allreduce.th-complete=1.0"]
+    gpu = ["--device", "0", "--set", "mxar.plane.grid=32", "--set", f"mxar.plane.max-peers={P}",
+           "--set", "mxar.plane.timeout=20"]
+    env = dict(os.environ, PYTHONPATH=ROOT, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    py = [sys.executable, "-m", "akka_allreduce_1_amd"]
+    master = subprocess.Popen(py + ["master", str(port), str(P), str(n), str(chunk), "--metrics-json",
+                                    str(tmp_path / "m.json")] + seed + exact + fast,
+                              env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    # worker output goes to files: ~P x 101 JSON rows of n floats would fill a pipe nobody reads
+    wout = [open(tmp_path / f"w{i}.out", "w") for i in range(P)]
+    werr = [open(tmp_path / f"w{i}.err", "w") for i in range(P)]
+    workers = [subprocess.Popen(py + ["worker", "0", str(n), "--print-outputs", "--metrics-json",
+                                      str(tmp_path / f"w{i}.json")] + gpu + seed + fast, env=env,
+                                stdout=wout[i], stderr=werr[i], text=True) for i in range(P)]
+    try:
+        try:
+            mout, merr = master.communicate(timeout=150)
+        except subprocess.TimeoutExpired:
+            for p in [master] + workers:
+                p.kill()
+            logs = [master.communicate()[1][-2500:]] + [(tmp_path / f"w{i}.err").read_text()[-2500:] for i in range(P)]
+            pytest.fail("job did not finish; stderr tails:\n" + "\n----\n".join(logs))
+        assert master.returncode == 0, merr[-3000:]
+        assert "finished 101 rounds" in mout, mout + merr[-3000:]
+        for i, w in enumerate(workers):
+            w.wait(timeout=60)
+            out, err = (tmp_path / f"w{i}.out").read_text(), (tmp_path / f"w{i}.err").read_text()
+            assert w.returncode == 0, err[-3000:]
+            rows = [json.loads(line) for line in out.splitlines() if line.startswith("{")]
+            got = {r["iteration"]: r for r in rows}
+            assert sorted(got) == list(range(101)), sorted(got)[:5]
+            for it in range(101):  # every worker: data[i] = i + iteration
+                np.testing.assert_array_equal(got[it]["data"], P * (np.arange(n) + it))
+                assert set(got[it]["count"]) == {P}
+            m = json.loads((tmp_path / f"w{i}.json").read_text())
+            assert m["worker"]["rounds_completed"] == 101 and m["worker"]["plane_errors"] == 0, m["worker"]
+            assert m["worker"]["plane_launches"] == 101
+    finally:
+        for p in [master] + workers:
+            if p.poll() is None:
+                p.kill()
+        for f in wout + werr:
+            f.close()

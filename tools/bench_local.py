@@ -21,29 +21,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from akka_allreduce_1_amd.ops import fill_uniform  # noqa: E402
 from akka_allreduce_1_amd.parallel import LocalCluster  # noqa: E402
-from akka_allreduce_1_amd.utils.timing import percentile  # noqa: E402
+from akka_allreduce_1_amd.utils.timing import hbm_bytes, percentile  # noqa: E402
 
 
 def parse_size(s: str) -> int:
     m = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}
     return int(float(s[:-1]) * m[s[-1].upper()]) if s[-1].upper() in m else int(s)
-
-
-def hbm_bytes(S: int, P: int, algo: str) -> float:
-    if algo == "ring":  # per rank, blocks of S/P: RS hops read in (+ slab) and push, AG hops copy out + forward
-        return P * (S / P) * (6 * (P - 2) + 8)
-    if algo == "all_to_all":  # S = P blocks per rank: read in + write slab (P-1)/P + read slab + write out
-        return P * (2 * S + 2 * S * (P - 1) / P)
-    if algo == "reduce_scatter":
-        return P * (S + 2 * S * (P - 1) / P + S / P)
-    if algo == "all_gather":  # S = the gathered output per rank (input S/P)
-        m = S / P
-        return P * ((4 * P - 2) * m)
-    if algo == "ll":  # read in, write P-1 LL slots (2x), read P-1 LL slots (2x), write out
-        return P * (S + 4 * S * (P - 1) + S)
-    if algo == "oneshot":
-        return P * (S + S * P + S * P + S)  # read in, write P slots, read P slots, write out
-    return P * (S + S * (P - 1) / P + S + S + 2 * S * (P - 1) / P)
 
 
 def main() -> None:
