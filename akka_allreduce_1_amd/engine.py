@@ -48,7 +48,8 @@ class PlaneJob:
                  th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 1, max_round: int = 10,
                  devices: Sequence[int] | None = None, dtype: torch.dtype = torch.float32, grid: int = 0,
                  sources: Sequence[Callable] | None = None, keep_outputs: bool = True, round_timeout_ms: int = 0,
-                 timeout_s: float = 60.0, order_ref: bool = True, on_output: Callable | None = None):
+                 timeout_s: float = 60.0, order_ref: bool = True, on_output: Callable | None = None,
+                 max_peers: int | None = None):
         self.P = P
         self.n = data_size
         self.dtype = dtype
@@ -64,7 +65,8 @@ class PlaneJob:
         self.outputs: list[dict[int, tuple]] = [dict() for _ in range(P)]
         self.keep = keep_outputs
         self.on_output = on_output
-        self.planes = [C.hip.xgmi_plane(d, dtype_code(dtype), data_size, max_peers=max(P, 1), max_lag=max_lag,
+        self.stamps: list[float] = []  # perf_counter() when each round reached the master's barrier
+        self.planes = [C.hip.xgmi_plane(d, dtype_code(dtype), data_size, max_peers=max_peers or P, max_lag=max_lag,
                                         grid=grid, timeout_s=timeout_s, order_ref=order_ref) for d in self.devices]
         if sources is None:
             sources = [iota_source(data_size, torch.device("cuda", d), dtype, 1000.0 * k)
@@ -76,7 +78,8 @@ class PlaneJob:
             self.finished.set()
 
         self.master = self.system.master(P, th_allreduce, th_reduce, th_complete, max_lag, data_size, max_round,
-                                         max_chunk_size, on_finished=fin, roundTimeoutMs=round_timeout_ms)
+                                         max_chunk_size, on_finished=fin, roundTimeoutMs=round_timeout_ms,
+                                         on_round=lambda r, e: self.stamps.append(time.perf_counter()))
         self.workers = [self.system.plane_worker(self.sources[k], self._sink(k), self.planes[k], f"worker{k}")
                         for k in range(P)]
 
@@ -112,3 +115,61 @@ class PlaneJob:
     def shutdown(self) -> None:
         self.system.shutdown()
         self.planes = []
+
+
+def distributed_plane_job(n: int, source: Callable, *, max_chunk_size: int, dtype: torch.dtype, rounds: int,
+                          th: float = 1.0, max_lag: int = 1, grid: int = 0, timeout_s: float = 300.0,
+                          on_output: Callable | None = None) -> dict:
+    """One plane worker per torch.distributed rank (one process per GPU), the master on rank 0,
+    the reference's cluster shape: workers join rank 0's seed over TCP (127.0.0.1) and
+    announce their plane descriptors in the join; the master relays them in InitWorkers and
+    drives `rounds` rounds; the data moves over xGMI inside the planes. torch.distributed is
+    used only to agree on the seed port and to hold the ranks until the master is done.
+    Returns (rank 0) {"stamps": round completion times, "state": worker state}."""
+    import torch.distributed as dist
+
+    from .parallel.comm import free_port
+
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = torch.cuda.current_device()
+    system = C.ActorSystem("ClusterSystem", False)
+    plane = C.hip.xgmi_plane(dev, dtype_code(dtype), n, max_peers=world, max_lag=max_lag, grid=grid,
+                             timeout_s=min(60.0, timeout_s))
+    sink = (lambda out: on_output(out)) if on_output is not None else None
+    worker = system.plane_worker(source, sink, plane, "worker")
+    port = [free_port() if rank == 0 else 0]
+    dist.broadcast_object_list(port, src=0)
+    cc = C.ClusterConfig()
+    cc.host = "127.0.0.1"
+    cc.port = port[0] if rank == 0 else 0
+    cc.roles = ["worker"]
+    cc.seed_nodes = [f"mxar.tcp://ClusterSystem@127.0.0.1:{port[0]}"]
+    cc.heartbeat_interval_s = 0.2
+    cc.acceptable_heartbeat_pause_s = 10.0
+    cc.auto_down_unreachable_after_s = -1.0
+    cc.meta = plane.descriptor
+    stamps: list[float] = []
+    fin = threading.Event()
+    master = None
+    if rank == 0:
+        master = system.master(world, 1.0, th, th, max_lag, n, rounds - 1, max_chunk_size,
+                               on_finished=lambda r: fin.set(),
+                               on_round=lambda r, e: stamps.append(time.perf_counter()))
+    node = C.ClusterNode.start(system, cc)
+    if master is not None:
+        node.subscribe(master)
+    ok = [True]
+    if rank == 0:
+        ok = [fin.wait(timeout_s)]
+    dist.broadcast_object_list(ok, src=0)
+    plane.drain()
+    system.await_idle(5.0)
+    out = {"ok": bool(ok[0]), "stamps": stamps, "state": system.plane_worker_state(worker),
+           "plane": {"launches": plane.stats.launches, "chunk_elems": plane.chunk_elems, "chunks": plane.chunks}}
+    dist.barrier()
+    node.leave()
+    time.sleep(0.3)
+    node.shutdown()
+    system.shutdown()
+    del plane
+    return out

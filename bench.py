@@ -43,6 +43,11 @@ if "--share-device" in sys.argv:
     # co-resident (measured: 46.7 ms vs 3.1 ms per 256 MiB step at 8 ranks). One queue per
     # process keeps every rank's kernel on the device at once. Set before HIP initialises.
     os.environ["GPU_MAX_HW_QUEUES"] = "1"
+else:
+    # The N = 1 protocol section hosts two plane workers in this process; with RCCL's and
+    # torch's streams, 4 hardware queues (HIP's default) make streams share queues, and work
+    # queued behind a spinning round kernel in a shared queue stalls until its timeout.
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 # Library banners (RCCL's version block, gloo's "connected to N peer ranks") are written to
 # fd 1 from native code; keep stdout for the ONE result line: fd 1 -> stderr for the whole
@@ -364,12 +369,13 @@ def dp_step(comm: XgmiCommunicator, model: str, dev) -> dict:
         shapes = gradient_shapes(model)
         params = [torch.nn.Parameter(torch.zeros(sh, dtype=torch.bfloat16, device=dev)) for _, sh in shapes]
         big = model == "llama3_8b"
-        # Llama-3-8B (16 GB): size-graded buckets - a 32 MiB first bucket starts the overlap
-        # early, 256 MiB buckets after it keep the per-bucket hand-off count low (each costs a
+        # Llama-3-8B (16 GB): size-graded buckets - a 64 MiB first bucket starts the overlap
+        # early, 1 GiB buckets after it keep the per-bucket hand-off count low (each costs a
         # few us of host time and a compute-stream drain: 163 x 64 MiB buckets exposed 1.1 ms
-        # at N = 1, profiles/dp_llama_n1_sync_sweep.jsonl). ResNet-50: torch DDP's 25 MiB.
+        # at N = 1, 66 x 256 MiB 0.57 ms). The tail bucket is the 1.05 GB embedding whatever
+        # the cap (the last gradient backward produces). ResNet-50: torch DDP's 25 MiB.
         if big:
-            reducer = BucketedGradReducer(params, comm, bucket_bytes=256 << 20, first_bucket_bytes=32 << 20,
+            reducer = BucketedGradReducer(params, comm, bucket_bytes=1 << 30, first_bucket_bytes=64 << 20,
                                           op="avg")
         else:
             reducer = BucketedGradReducer(params, comm, bucket_bytes=25 << 20, op="avg")
@@ -427,6 +433,84 @@ def dp_step(comm: XgmiCommunicator, model: str, dev) -> dict:
     return row
 
 
+def protocol_rounds(args, rank: int, world: int, dev) -> dict:
+    """The reference's protocol driving the GPU engine: the master's
+    StartAllreduce(r) becomes one threshold-kernel round per worker on the xGMI round plane
+    (csrc/runtime/plane_worker.h, csrc/hip/xgmi_plane.h), CompleteAllreduce goes back, the
+    master starts r + 1 at the barrier - the bench buffer per worker, th = 1, maxLag 1.
+    N = 1: two workers in this process share the GPU (all traffic in one HBM). N > 1: one
+    worker per GPU process, master on rank 0, control over TCP, data over xGMI.
+    rounds_per_s / ms_per_round come from the master's round-barrier stamps after the
+    warm-up rounds; algbw = buffer bytes / ms_per_round."""
+    from akka_allreduce_1_amd.engine import PlaneJob, distributed_plane_job
+
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    es = 2 if dtype == torch.bfloat16 else 4
+    nbytes = args.size_mib << 20
+    n = nbytes // es
+    warm = max(1, args.warmup)
+    rounds = warm + max(args.steps, 10)
+    P = 2 if world == 1 else world
+    block = -(-n // P)
+    chunk = max(1024, -(-block // 256))  # ~256 reduce units per worker: one per workgroup pair of CUs
+    row: dict = {"workers": P, "bytes_per_worker": nbytes, "dtype": args.dtype, "rounds": rounds,
+                 "warmup_rounds": warm, "th_reduce": 1.0, "th_complete": 1.0, "max_lag": 1,
+                 "max_chunk_size": chunk, "engine": "PlaneWorkerActor + XgmiRoundPlane (threshold kernel)"}
+    try:
+        if world == 1:
+            xs = [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=700 + k) for k in range(P)]
+            last = {}
+
+            def on_output(k, out):
+                if out.iteration == rounds - 1 and k == 0:
+                    last["y"] = out.data.clone()
+
+            log(rank, f"protocol: {P} plane workers on this GPU, {rounds} rounds of {args.size_mib} MiB")
+            job = PlaneJob(P, n, max_chunk_size=chunk, dtype=dtype, max_round=rounds - 1,
+                           sources=[(lambda req, x=x: x) for x in xs], keep_outputs=False, on_output=on_output,
+                           timeout_s=20.0)
+            try:
+                job.run(timeout=300)
+                stamps = job.stamps
+                lat = job.system.plane_worker_state(job.workers[0])["round_latency"]
+                row["note"] = "N=1: 2 workers share one GPU (one HBM, no xGMI)"
+            finally:
+                job.shutdown()
+            ref = (xs[0].float() + xs[1].float()).to(dtype)
+            row["validated"] = bool(torch.equal(last["y"], ref))
+        else:
+            x = fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=700 + rank)
+            last = {}
+
+            def on_output(out):
+                if out.iteration == rounds - 1:
+                    last["y"] = out.data.clone()
+
+            grid = max(8, 512 // world) if args.share_device else 0
+            log(rank, f"protocol: one plane worker per rank, {rounds} rounds of {args.size_mib} MiB")
+            res = distributed_plane_job(n, lambda req: x, max_chunk_size=chunk, dtype=dtype, rounds=rounds,
+                                        grid=grid, on_output=on_output, timeout_s=120.0)
+            stamps = res["stamps"]
+            lat = res["state"]["round_latency"]
+            ref = torch.zeros(n, device=dev)
+            for k in range(world):
+                ref += fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=700 + k).float()
+            good = torch.tensor([1 if ("y" in last and torch.equal(last["y"], ref.to(dtype))) else 0], device=dev)
+            dist.all_reduce(good, op=dist.ReduceOp.MIN)
+            row["validated"] = bool(good.item())
+            row["note"] = "one worker per GPU process; master on rank 0; control over TCP, data over xGMI"
+        if len(stamps) > warm + 1:
+            per = (stamps[-1] - stamps[warm - 1]) / (len(stamps) - warm)
+            row["ms_per_round"] = round(per * 1e3, 4)
+            row["rounds_per_s"] = round(1.0 / per, 2)
+            row["algbw_per_worker"] = round(nbytes / per / 1e9, 2)
+        row["worker_round_latency_p50_ms"] = round(lat["p50_ms"], 4)
+        row["worker_round_latency_p99_ms"] = round(lat["p99_ms"], 4)
+    except Exception as e:  # noqa: BLE001 - reported, never loses the headline
+        row["error"] = repr(e)
+    return row
+
+
 _EMIT_LOCK = threading.Lock()
 _EMITTED = [False]
 
@@ -462,6 +546,7 @@ def main() -> None:
     ap.add_argument("--no-fused-step", action="store_true", help="skip the fused reduce-scatter + AdamW + all-gather timing")
     ap.add_argument("--no-dp", action="store_true", help="skip the ResNet-50 / Llama-3-8B DP-step sections")
     ap.add_argument("--no-local", action="store_true", help="skip the 8-logical-rank section at N = 1")
+    ap.add_argument("--no-protocol", action="store_true", help="skip the master/worker protocol-engine section")
     ap.add_argument("--dp-rehearsal", action="store_true", help="with --share-device: run the ResNet-50 DP step too")
     ap.add_argument("--dp-timeout", type=float, default=240.0,
                     help="seconds for the DP-step sections; past it the result line is written without them")
@@ -519,6 +604,7 @@ def main() -> None:
 
     validated = None
     if engine_ok:
+        log(rank, "validating every algorithm against fp32")
         # every algorithm a section or the tuner may pick, against fp32, before any timing
         validated = validate_algos(comm, dtype, dev, rank, world)
         bad = [k for k, v in validated.items() if not v["validated"]]
@@ -542,6 +628,7 @@ def main() -> None:
         chosen = "rccl" if engine_ok else "rccl-fallback"
         step = step_rccl
 
+    log(rank, f"headline: {chosen}, {args.warmup} + {args.steps} steps")
     for _ in range(args.warmup):
         step()
     wall = timed(step, args.steps, dev)
@@ -647,14 +734,20 @@ def main() -> None:
     if engine_ok and world > 1 and not args.no_collectives:
         # the allreduce's two halves and the all-to-all as collectives of their own
         # (csrc/hip/xgmi_coll.hip) on the same bytes, next to RCCL's equivalents
+        log(rank, "collectives")
         result["collectives"] = collectives(comm, x, world, args, dev)
     if engine_ok and not args.no_fused_step:
+        log(rank, "fused AdamW step")
         result["fused_adamw_step"] = fused_step(comm, x, y, world, rank, args, dev)
     if sweep is not None:
         result["sweep"] = sweep
     if engine_ok and world == 1 and not args.share_device and not args.no_local:
         # the allreduce kernels at N = 1: 8 logical ranks in one launch on this GPU
+        log(rank, "local_ranks: 8 logical ranks in one launch")
         result["local_ranks"] = local_ranks(dev, args, P=8)
+    if engine_ok and not args.no_protocol:
+        # the reference's master/worker round protocol driving the GPU engine
+        result["protocol"] = protocol_rounds(args, rank, world, dev)
     if engine_ok and not args.no_dp and (not args.share_device or args.dp_rehearsal):
         # configs 4 / 5 (full Llama-3-8B: 32 GB of params + grads per rank). Not in the
         # one-GPU rehearsal: there every rank's spinning comm kernel shares the device with the
@@ -673,6 +766,7 @@ def main() -> None:
         dog = threading.Timer(args.dp_timeout, give_up)
         dog.daemon = True
         dog.start()
+        log(rank, "dp: ResNet-50 / Llama-3-8B data-parallel steps")
         dp = {m: dp_step(comm, m, dev) for m in (("resnet50",) if args.share_device else ("resnet50", "llama3_8b"))}
         dog.cancel()
         with _EMIT_LOCK:

@@ -143,7 +143,11 @@ Payload py_to_device_payload_typed(const py::handle& obj) {
       mt->deleter(mt);
     }
   });
-  ReadyEvent ready = record_ready(reinterpret_cast<hipStream_t>(cs));
+  // the producer's stream idle: nothing to order after (and no marker that could queue behind
+  // another worker's spinning round in a shared hardware queue)
+  const hipStream_t ps = reinterpret_cast<hipStream_t>(cs);
+  ReadyEvent ready = hipStreamQuery(ps) == hipSuccess ? nullptr : record_ready(ps);
+  (void)hipGetLastError();
   return std::make_shared<DevicePayload>(std::move(mem), 0, static_cast<size_t>(n), dev, nullptr, std::move(ready),
                                          code);
 }

@@ -74,7 +74,7 @@ int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 }  // namespace
 
-XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o), pool_(o.device) {
+XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   if (o_.capacity <= 0) throw std::invalid_argument("xgmi plane: capacity (elements per round) must be > 0");
   if (o_.max_peers < 1 || o_.max_peers > 32 || o_.max_peers > kMaxRanks)
     throw std::invalid_argument("xgmi plane: max_peers must be in [1, 16]");
@@ -105,7 +105,22 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o), pool_(o.devic
             "hipHostMalloc(force word)");
   std::memset(hforce_, 0, 64);
   hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&hforce_dev_), hforce_, 0), "hipHostGetDevicePointer");
-  hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate(plane)");
+  // High priority: HIP serves each priority level from its own hardware-queue pool, so the
+  // plane's persistent round kernels never sit in the same hardware queue as the default
+  // stream (a marker or kernel queued behind a spinning round in a shared queue would wait
+  // for that round - a deadlock when the round waits for a peer fed by that work; seen in
+  // a kernel trace with two workers in one process).
+  int lo = 0, hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+  hip_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "hipStreamCreate(plane)");
+  // keep freed round buffers in the device's default pool instead of returning them to the
+  // driver at every synchronisation (the next round reuses them)
+  hipMemPool_t mp = nullptr;
+  if (hipDeviceGetDefaultMemPool(&mp, o_.device) == hipSuccess && mp != nullptr) {
+    uint64_t keep = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(mp, hipMemPoolAttrReleaseThreshold, &keep);
+  }
+  (void)hipGetLastError();
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
   hipIpcMemHandle_t h;
   hip_check(hipIpcGetMemHandle(&h, arena_), "hipIpcGetMemHandle(plane arena)");
@@ -125,6 +140,7 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o), pool_(o.devic
 }
 
 XgmiRoundPlane::~XgmiRoundPlane() {
+  *alive_ = false;
   try {
     force(0x7fffffff);
     drain();
@@ -149,6 +165,22 @@ XgmiRoundPlane::~XgmiRoundPlane() {
   if (hforce_) (void)hipHostFree(hforce_);
   if (stream_) (void)hipStreamDestroy(stream_);
   if (arena_) (void)hipFree(arena_);
+}
+
+std::shared_ptr<void> XgmiRoundPlane::buffer(size_t bytes) {
+  void* p = nullptr;
+  hip_check(hipMallocAsync(&p, std::max<size_t>(bytes, 256), stream_), "hipMallocAsync(plane)");
+  const hipStream_t s = stream_;
+  std::weak_ptr<bool> alive = alive_;
+  // released on the plane stream (ordered after every round that may still read it); an
+  // output the user keeps past the plane's lifetime is freed synchronously instead
+  return std::shared_ptr<void>(p, [s, alive](void* q) {
+    auto a = alive.lock();
+    if (a && *a)
+      (void)hipFreeAsync(q, s);
+    else
+      (void)hipFree(q);
+  });
 }
 
 void XgmiRoundPlane::set_done(DoneFn fn) {
@@ -280,8 +312,8 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   rec.round = round;
   rec.epoch = cfg_.epoch;
   rec.cold = cold;
-  rec.out = pool_.get(static_cast<size_t>(n * es));
-  rec.cnt_dev = pool_.get(static_cast<size_t>(cfg_.peers) * nch_ * 4);
+  rec.out = buffer(static_cast<size_t>(n * es));
+  rec.cnt_dev = buffer(static_cast<size_t>(cfg_.peers) * nch_ * 4);
   const void* in_ptr = rec.out.get();  // a cold round reads no input
   if (!cold) {
     if (!input || static_cast<int64_t>(input->size()) != n) throw ProtocolError("xgmi plane: input must hold dataSize elements");
@@ -291,20 +323,20 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
       else if (dp->stream() && dp->stream() != stream_) hip_check(hipStreamSynchronize(dp->stream()), "hipStreamSynchronize");
       in_ptr = dp->bytes();  // any element alignment: the kernel takes unaligned units element-wise
       if (dp->dtype() != dcode) {  // cast into the plane's dtype on the device
-        rec.staging = pool_.get(static_cast<size_t>(n * es));
+        rec.staging = buffer(static_cast<size_t>(n * es));
         launch_cast(dp->bytes(), static_cast<DType>(dp->dtype()), rec.staging.get(), o_.dtype, n, stream_);
         in_ptr = rec.staging.get();
       }
       rec.input = input;  // held until the round completed
     } else {  // host (or other-device) float32 payload: upload, cast into the plane's dtype
       const std::vector<float> h = input->to_host();
-      auto up = pool_.get(static_cast<size_t>(n * 4));
+      auto up = buffer(static_cast<size_t>(n * 4));
       hip_check(hipMemcpyAsync(up.get(), h.data(), n * 4, hipMemcpyHostToDevice, stream_), "hipMemcpyAsync H2D");
       hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");  // h is pageable and local
       if (o_.dtype == DType::F32) {
         rec.staging = up;
       } else {
-        rec.staging = pool_.get(static_cast<size_t>(n * es));
+        rec.staging = buffer(static_cast<size_t>(n * es));
         launch_cast(up.get(), DType::F32, rec.staging.get(), o_.dtype, n, stream_);
         rec.input = std::make_shared<DevicePayload>(up, 0, static_cast<size_t>(n), o_.device, nullptr);  // keep alive
       }

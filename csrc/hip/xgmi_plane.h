@@ -91,6 +91,10 @@ class XgmiRoundPlane final : public RoundPlane {
     return cfg_.roundBase + static_cast<uint32_t>(round - cfg_.startRound) + 1u;
   }
   char* map_peer(const std::string& desc);
+  // Stream-ordered device buffer (hipMallocAsync on the plane stream, hipFreeAsync when the
+  // last holder drops it): the launch path never calls a device-synchronising allocator
+  // while a peer's kernel may be spinning on this worker's next launch.
+  std::shared_ptr<void> buffer(size_t bytes);
   int take_slot(std::unique_lock<std::mutex>& lk);
   void completion_loop();
 
@@ -103,7 +107,6 @@ class XgmiRoundPlane final : public RoundPlane {
   uint32_t* hforce_ = nullptr;      // pinned host word the engine raises (force)
   uint32_t* hforce_dev_ = nullptr;  // its device-visible address
   hipStream_t stream_ = nullptr;
-  DevicePool pool_;
   std::unique_ptr<XgmiComm> comm_;
   std::map<std::string, char*> mapped_;  // peer IPC handle -> mapping (kept across epochs)
   PlaneConfig cfg_;
@@ -126,6 +129,7 @@ class XgmiRoundPlane final : public RoundPlane {
   DoneFn done_;
   std::thread th_;
   XgmiPlaneStats st_;
+  std::shared_ptr<bool> alive_ = std::make_shared<bool>(true);
 };
 
 std::shared_ptr<XgmiRoundPlane> make_xgmi_plane(const XgmiPlaneOptions& o);

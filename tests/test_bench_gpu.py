@@ -39,6 +39,8 @@ def test_bench_prints_one_json_line_with_contract_fields():
     assert "error" not in loc, loc
     for algo in ("twoshot", "ring"):
         assert loc[algo]["validated"] and 0 < loc[algo]["frac_copy_roofline"] < 1.5, loc
+    proto = d["protocol"]  # the reference's master/worker protocol driving the GPU round engine
+    assert "error" not in proto and proto["validated"] and proto["rounds_per_s"] > 0, proto
     for model in ("resnet50", "llama3_8b"):
         row = d["dp"][model]
         assert "error" not in row, row

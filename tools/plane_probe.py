@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""GPU probe of the protocol engine in one process: P plane workers on one GPU, fixed
+synthetic inputs, sizes from small to the bench's 256 MiB; prints one JSON row per size
+(round time at the master's barrier, validation) as it goes.
+
+    python tools/plane_probe.py --P 2 --sizes 1M 16M 64M 256M --rounds 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from akka_allreduce_1_amd.engine import PlaneJob  # noqa: E402
+from akka_allreduce_1_amd.ops import fill_uniform  # noqa: E402
+
+
+def parse_size(s: str) -> int:
+    m = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}
+    return int(float(s[:-1]) * m[s[-1].upper()]) if s[-1].upper() in m else int(s)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--P", type=int, default=2)
+    ap.add_argument("--sizes", nargs="+", default=["1M", "16M", "64M", "256M"])
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--units", type=int, default=256, help="reduce units (chunks) per block")
+    ap.add_argument("--timeout", type=float, default=10.0)
+    ap.add_argument("--dtype", default="bf16")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    es = 2 if dtype == torch.bfloat16 else 4
+    for sz in a.sizes:
+        S = parse_size(sz)
+        n = S // es
+        xs = [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=k) for k in range(a.P)]
+        ref = sum(x.float() for x in xs).to(dtype)
+        chunk = max(1024, -(-(-(-n // a.P)) // a.units))
+        last = {}
+
+        def on_output(k, out, rounds=a.rounds):
+            if out.iteration == rounds - 1:
+                last[k] = out.data.clone()
+
+        job = PlaneJob(a.P, n, max_chunk_size=chunk, dtype=dtype, max_round=a.rounds - 1,
+                       sources=[(lambda req, x=x: x) for x in xs], keep_outputs=False, on_output=on_output,
+                       timeout_s=a.timeout)
+        row = {"P": a.P, "bytes": S, "chunk": chunk}
+        t0 = time.perf_counter()
+        try:
+            job.run(timeout=max(60.0, 4 * a.timeout))
+            st = job.state()
+            row["wall_s"] = round(time.perf_counter() - t0, 3)
+            s = job.stamps
+            if len(s) > 2:
+                per = (s[-1] - s[1]) / (len(s) - 2)
+                row["ms_per_round"] = round(per * 1e3, 4)
+                row["algbw_GBps"] = round(S / per / 1e9, 2)
+            row["errors"] = [w["stats"]["plane_errors"] for w in st["workers"]]
+            row["validated"] = all(torch.equal(last.get(k, torch.empty(0)), ref) for k in range(a.P))
+            row["lat_p50_ms"] = [round(w["round_latency"]["p50_ms"], 3) for w in st["workers"]]
+        except Exception as e:  # noqa: BLE001
+            row["error"] = repr(e)[:400]
+        finally:
+            job.shutdown()
+        print(json.dumps(row), flush=True)
+        del xs, ref
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
