@@ -3,6 +3,7 @@
 #include <algorithm>
 
 #include "log.h"
+#include "trace.h"
 
 namespace mxar {
 
@@ -128,6 +129,7 @@ void MasterCore::init_workers() {
 // startAllreduce (AllreduceMaster.scala:91-97)
 void MasterCore::start_allreduce() {
   MXAR_LOG(INFO, "master", "----Start allreduce round " << round_);
+  trace_instant("master", "start r" + std::to_string(round_));
   numComplete_ = 0;
   stats_.rounds_started++;
   for (auto& [idx, h] : workers_) fx_->send_start(h, round_);

@@ -4,6 +4,7 @@
 
 #include <cstdlib>
 #include <functional>
+#include <iomanip>
 #include <sstream>
 #include <thread>
 
@@ -60,6 +61,9 @@ void Tracer::record(const char* cat, const std::string& name, uint64_t ts_ns, ui
 std::string Tracer::dump_json() {
   std::lock_guard<std::mutex> g(mu_);
   std::ostringstream os;
+  // microseconds with ns resolution: the default 6 significant digits would collapse every
+  // event of a process that has been up for more than a second onto one timestamp
+  os << std::fixed << std::setprecision(3);
   const int pid = static_cast<int>(getpid());
   os << "{\"displayTimeUnit\":\"ms\",\"otherData\":{\"dropped\":" << dropped_ << "},\"traceEvents\":[";
   bool first = true;

@@ -113,34 +113,53 @@ Payload py_to_device_payload(const py::handle& obj) {
   return std::make_shared<DevicePayload>(std::move(mem), 0, static_cast<size_t>(n), mt->dl_tensor.device.device_id,
                                          nullptr, nullptr);
 }
-// Plane-worker inputs: the tensor's own dtype, zero copy, and an event recorded on torch's
-// current stream of its device - the plane's stream waits on it (no host synchronisation).
+// Plane-worker inputs: the tensor's own dtype, zero copy (the payload keeps a reference to
+// the tensor), ordered after its producer by an event on torch's current stream when that
+// stream still has work in flight. This runs once per round on the dataSource path, so the
+// torch objects it needs are looked up once.
+struct TorchRefs {
+  py::object tensor_type, f32, bf16, f16, raw_stream;
+};
+const TorchRefs& torch_refs() {
+  static TorchRefs* r = [] {
+    py::module_ torch = py::module_::import("torch");
+    auto* t = new TorchRefs{torch.attr("Tensor"), torch.attr("float32"), torch.attr("bfloat16"),
+                            torch.attr("float16"), py::none()};
+    py::object c = torch.attr("_C");
+    if (py::hasattr(c, "_cuda_getCurrentRawStream")) t->raw_stream = c.attr("_cuda_getCurrentRawStream");
+    return t;
+  }();
+  return *r;
+}
+
 Payload py_to_device_payload_typed(const py::handle& obj) {
-  if (!py::hasattr(obj, "__dlpack__") || !py::hasattr(obj, "is_cuda")) return nullptr;
-  if (!obj.attr("is_cuda").cast<bool>()) return nullptr;
-  py::module_ torch = py::module_::import("torch");
-  py::object dt = obj.attr("dtype");
+  const TorchRefs& T = torch_refs();
+  if (!py::isinstance(obj, T.tensor_type)) return nullptr;
+  py::object t = py::reinterpret_borrow<py::object>(obj);
+  if (!t.attr("is_cuda").cast<bool>()) return nullptr;
+  const py::object dt = t.attr("dtype");
   int code = -1;
-  if (dt.equal(torch.attr("float32"))) code = 0;
-  else if (dt.equal(torch.attr("bfloat16"))) code = 1;
-  else if (dt.equal(torch.attr("float16"))) code = 2;
+  if (dt.is(T.f32)) code = 0;
+  else if (dt.is(T.bf16)) code = 1;
+  else if (dt.is(T.f16)) code = 2;
   if (code < 0) throw py::type_error("plane input must be float32, bfloat16 or float16");
-  py::object t = obj.attr("detach")().attr("contiguous")().attr("reshape")(-1);
-  const uintptr_t cs = torch.attr("cuda").attr("current_stream")(t.attr("device")).attr("cuda_stream").cast<uintptr_t>();
-  py::object cap = t.attr("__dlpack__")();
-  auto* mt = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap.ptr(), "dltensor"));
-  if (!mt) throw py::error_already_set();
-  PyCapsule_SetName(cap.ptr(), "used_dltensor");
-  const int64_t n = mt->dl_tensor.ndim > 0 ? mt->dl_tensor.shape[0] : 1;
-  char* data = static_cast<char*>(mt->dl_tensor.data) + mt->dl_tensor.byte_offset;
-  const int dev = mt->dl_tensor.device.device_id;
-  std::shared_ptr<void> mem(data, [mt](void*) {
-    if (!mt->deleter) return;
+  if (!t.attr("is_contiguous")().cast<bool>()) t = t.attr("contiguous")();
+  const uintptr_t ptr = t.attr("data_ptr")().cast<uintptr_t>();
+  const int64_t n = t.attr("numel")().cast<int64_t>();
+  const int dev = t.attr("get_device")().cast<int>();
+  uintptr_t cs = 0;
+  if (!T.raw_stream.is_none())
+    cs = T.raw_stream(dev).cast<uintptr_t>();
+  else
+    cs = py::module_::import("torch").attr("cuda").attr("current_stream")(dev).attr("cuda_stream").cast<uintptr_t>();
+  auto* hold = new py::object(std::move(t));  // released with the GIL when the plane drops the input
+  std::shared_ptr<void> mem(reinterpret_cast<void*>(ptr), [hold](void*) {
     if (Py_IsInitialized()) {
       py::gil_scoped_acquire g;
-      mt->deleter(mt);
+      delete hold;
     } else {
-      mt->deleter(mt);
+      hold->release();
+      delete hold;
     }
   });
   // the producer's stream idle: nothing to order after (and no marker that could queue behind
@@ -390,7 +409,12 @@ void bind_hip(py::module_& m) {
       .def_property_readonly("stats", &XgmiComm::stats)
       .def_property("fence", &XgmiComm::fence, &XgmiComm::set_fence)
       .def_property("units_per_wg", &XgmiComm::units_per_wg, &XgmiComm::set_units_per_wg)
-      .def("set_timeout", &XgmiComm::set_timeout);
+      .def("set_timeout", &XgmiComm::set_timeout)
+      .def(
+          "set_phase_stamps",
+          [](XgmiComm& c, uintptr_t buf, int64_t slots) { c.set_phase_stamps(reinterpret_cast<uint64_t*>(buf), slots); },
+          py::arg("buf"), py::arg("slots"),
+          "study knob: per-workgroup phase stamps of the two-shot / ring kernels (0 = off)");
 
   h.def(
       "reduce_slots",

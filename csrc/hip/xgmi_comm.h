@@ -133,6 +133,7 @@ class XgmiComm {
     bool cold = false;
     bool order_ref = false;
     const uint32_t* host_force = nullptr;  // device-visible pinned host word (may be null)
+    uint32_t* err_out = nullptr;           // device-visible word the round's error word is copied to
   };
   void round(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, float th_reduce, float th_complete,
              int32_t* counts, const RoundSpec& spec, float scale = 1.f);
@@ -206,6 +207,13 @@ class XgmiComm {
   int units_per_wg() const { return units_per_wg_; }
   void set_units_per_wg(int u) { units_per_wg_ = u > 0 ? u : 0; }
   void set_fence(int f) { fence_ = f & 3; }
+  // Study knob: per-workgroup phase stamps of the two-shot / ring kernels (xgmi_device.h
+  // PhaseStamps) into `buf` (device, >= slots x 8 u64; slots = workgroups x ranks in the
+  // launch); nullptr turns it off. Only the first rank of a grouped launch's buffer counts.
+  void set_phase_stamps(uint64_t* buf, int64_t slots) {
+    stamps_ = buf;
+    stamp_slots_ = buf ? slots : 0;
+  }
   bool connected() const { return connected_; }
   const CommStats& stats() const { return stats_; }
   char* slab() const { return slab_; }
@@ -247,6 +255,8 @@ class XgmiComm {
   int64_t oneshot_max_;
   double timeout_s_;
   int fence_ = 3;
+  uint64_t* stamps_ = nullptr;  // phase-stamp buffer (study knob, set_phase_stamps)
+  int64_t stamp_slots_ = 0;
   int units_per_wg_ = 0;  // two-shot scatter units per workgroup; 0 = by block size (launch_segment)
   int sub_max_ = 0;       // two-shot: most reduce pieces per chunk; 0 = by block size
   char* slab_ = nullptr;            // own fine-grained slab (flags | S | R | LL)

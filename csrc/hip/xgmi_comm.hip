@@ -51,6 +51,8 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
   const bool rel = a.fence & 1, acq = a.fence & 2;
   const int Pm1 = P > 1 ? P - 1 : 1;
   const int nu = (P - 1) * a.nch;
+  __shared__ uint64_t ps_lds[kPhaseSlots];
+  PhaseStamps ps(a, ps_lds);
 
   // Phase 1 - ScatterBlock: push chunk c of block j to its owner j (rotated dest order,
   // AllreduceWorker.scala:194-209), so concurrent workgroups load all links.
@@ -65,6 +67,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
     publish_flags([&](int) { return f1(a, j, r, c); }, 1, epoch, rel);
   }
 
+  ps.mark(1);
   // Phase 2 - reduce own block once all P contributions of a chunk have arrived
   // (thReduce = 1), then ReduceBlock-broadcast the sum into every rank's R slot. A chunk
   // is reduced in `sub` pieces by different workgroups so that phase 2 has as many
@@ -79,8 +82,11 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
     const int64_t qbeg = static_cast<int64_t>(q) * a.subchunk;
     const int64_t cstart = cbeg + qbeg;
     const int64_t len = clamp_len(clamp_len(blen_own - cbeg, a.chunk) - qbeg, a.subchunk);
+    const uint64_t tw = ps.now();
     wait_flags([&](int s) -> const uint32_t* { return s == r ? nullptr : f1(a, r, s, c); }, P, epoch, deadline, err,
                ERR_TIMEOUT_SCATTER, acq);
+    ps.add(2, tw);
+    ps.count(6);
     if (len > 0 && unit_in_bounds(a, cstart * es, len * es, u, err)) {
       const char* own_in = in + (bstart_own + cstart) * es;
       const char* S = a.base[r] + a.off_S + cstart * es;
@@ -93,6 +99,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
     publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : f2(a, k, r, u); }, P, epoch, rel);
   }
 
+  ps.mark(3);
   // Phase 3 - complete: gather the other owners' reduced chunks into the output.
   for (int u = blockIdx.x; u < nu; u += G) {
     const int c = u / Pm1;
@@ -100,11 +107,16 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
     const int64_t bstart = static_cast<int64_t>(j) * a.block;
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
+    const uint64_t tw = ps.now();
     wait_flags([&](int q) -> const uint32_t* { return f2(a, r, j, c * a.sub + q); }, a.sub, epoch, deadline, err,
                ERR_TIMEOUT_REDUCE, acq);
+    ps.add(4, tw);
+    ps.count(7);
     if (len > 0 && unit_in_bounds(a, cstart * es, len * es, c, err))
       copy_from_slab<E>(out + (bstart + cstart) * es, a.base[r] + a.off_R + j * slot + cstart * es, len);
   }
+  ps.mark(5);
+  ps.flush();
   finish_launch(ctl, epoch);
 }
 
@@ -243,6 +255,8 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
   const int64_t slot = a.slot_bytes;
   uint32_t* err = &ctl[2];
   const bool rel = a.fence & 1, acq = a.fence & 2;
+  __shared__ uint64_t ps_lds[kPhaseSlots];
+  PhaseStamps ps(a, ps_lds);  // ring: [1] = end of the reduce-scatter hops, [2]/[4] = waits in RS / AG
   for (int c = blockIdx.x; c < a.nch; c += gridDim.x) {
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     auto blen = [&](int b) { return clamp_len(clamp_len(a.n - static_cast<int64_t>(b) * a.block, a.block) - cstart, a.chunk); };
@@ -263,8 +277,11 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
     for (int s = 1; s < P; ++s) {
       const int b = (r - s + P) % P;
       const int64_t len = blen(b);
+      const uint64_t tw = ps.now();
       wait_flags([&](int) -> const uint32_t* { return f1(a, r, s - 1, c); }, 1, epoch, deadline, err,
                  ERR_TIMEOUT_SCATTER, acq);
+      ps.add(2, tw);
+      ps.count(6);
       const RedSrc src{in + at(b), a.base[r] + a.off_S + (s - 1) * slot + cstart * es, 0, 1};
       if (s < P - 1) {
         char* d = a.base[nxt] + a.off_S + s * slot + cstart * es;
@@ -279,17 +296,24 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
       }
     }
     // AG steps: receive block (r - t), forward unless it is the last hop
+    ps.mark(1);
     for (int t = 0; t < P - 1; ++t) {
       const int b = (r - t + P) % P;
       const int64_t len = blen(b);
+      const uint64_t tw = ps.now();
       wait_flags([&](int) -> const uint32_t* { return f2(a, r, t, c); }, 1, epoch, deadline, err, ERR_TIMEOUT_REDUCE,
                  acq);
+      ps.add(4, tw);
+      ps.count(7);
       const bool fwd = t < P - 2;
       char* d = fwd ? a.base[nxt] + a.off_R + (t + 1) * slot + cstart * es : nullptr;
       if (len > 0) copy_slab_fwd<E>(out + at(b), d, a.base[r] + a.off_R + t * slot + cstart * es, len);
       if (fwd) publish_flags([&](int) { return f2(a, nxt, t + 1, c); }, 1, epoch, rel);
     }
   }
+  ps.mark(3);
+  ps.mark(5);
+  ps.flush();
   finish_launch(ctl, epoch);
 }
 
@@ -640,6 +664,8 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   }
   a.fence = c0.fence_;
   a.scale = scale;
+  a.stamps = c0.stamps_;
+  if (a.stamps != nullptr && gx * ranks_here > c0.stamp_slots_) a.stamps = nullptr;  // buffer too small: off
   if (kind != Algo::LL && (static_cast<int64_t>(a.nch) * a.sub > c0.maxch_ || a.block * es > c0.slot_bytes_ + 16))
     throw std::logic_error("XgmiComm: segment geometry exceeds slab");
   const dim3 grid(gx, ranks_here);
@@ -889,6 +915,7 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
     a.cold = spec->cold ? 1 : 0;
     a.order_ref = spec->order_ref ? 1 : 0;
     a.hforce = spec->host_force;
+    a.err_out = spec->err_out;
   }
   a.delay_rank = -1;
   for (XgmiComm* c : group)

@@ -50,6 +50,7 @@ struct CommArgs {
   int cold;
   int order_ref;
   const uint32_t* hforce;
+  uint32_t* err_out;  // optional: the round's error word, written by the last workgroup (pinned host)
   // low-latency one-shot (xgmi_ll.hip): slots [parity][src] of ll_slot bytes at off_LL
   int64_t off_LL, ll_slot;
   // fused reduce-scatter + AdamW + all-gather (xgmi_adam.hip): per rank fp32 shard state
@@ -57,8 +58,43 @@ struct CommArgs {
   float* opt_m[kMaxRanks];
   float* opt_v[kMaxRanks];
   float lr, beta1, beta2, eps, wd, c1, c2_sqrt;  // c1 = 1 - beta1^t, c2_sqrt = sqrt(1 - beta2^t)
+  // phase profile (MXAR study knob, XgmiComm::set_phase_stamps): per (rank y, workgroup x)
+  // kPhaseSlots s_memrealtime values - see PhaseStamps below
+  uint64_t* stamps;
   uint64_t delay;      // test knob: ticks rank `delay_rank` idles before phase 1
   int delay_rank;
+};
+
+// Phase stamps of one workgroup (100 MHz s_memrealtime ticks): [0] start, [1] scatter done,
+// [2] ticks spent waiting in the reduce phase, [3] reduce phase done, [4] ticks spent
+// waiting in the gather phase, [5] end, [6] units reduced, [7] units gathered. Thread 0
+// writes them; a null buffer (the default) costs one scalar compare per phase.
+constexpr int kPhaseSlots = 8;
+struct PhaseStamps {
+  uint64_t* out;  // this workgroup's slots in the buffer, or null (uniform)
+  uint64_t* lds;  // kPhaseSlots u64 of LDS (thread 0 updates them)
+  __device__ __forceinline__ PhaseStamps(const CommArgs& a, uint64_t* sh) : lds(sh) {
+    out = a.stamps == nullptr ? nullptr
+                              : a.stamps + (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * kPhaseSlots;
+    if (out != nullptr && threadIdx.x == 0) {
+      for (int i = 0; i < kPhaseSlots; ++i) lds[i] = 0;
+      lds[0] = wall_ticks();
+    }
+  }
+  __device__ __forceinline__ void mark(int i) {
+    if (out != nullptr && threadIdx.x == 0) lds[i] = wall_ticks();
+  }
+  __device__ __forceinline__ uint64_t now() const { return out != nullptr ? wall_ticks() : 0; }
+  __device__ __forceinline__ void add(int i, uint64_t t0) {
+    if (out != nullptr && threadIdx.x == 0) lds[i] += wall_ticks() - t0;
+  }
+  __device__ __forceinline__ void count(int i) {
+    if (out != nullptr && threadIdx.x == 0) lds[i] += 1;
+  }
+  __device__ __forceinline__ void flush() {
+    if (out != nullptr && threadIdx.x == 0)
+      for (int i = 0; i < kPhaseSlots; ++i) out[i] = lds[i];
+  }
 };
 
 __device__ __forceinline__ uint32_t* f1(const CommArgs& a, int k, int s, int c) {

@@ -275,8 +275,12 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
     std::lock_guard<std::mutex> g(mu_);
     if (ring_) (void)hipHostFree(ring_);
     ring_stride_ = static_cast<size_t>(P) * nch_ + 4;
-    hip_check(hipHostMalloc(reinterpret_cast<void**>(&ring_), ring_stride_ * 4 * o_.ring, hipHostMallocDefault),
+    // the kernel writes each round's counts and error word straight into its slot (no
+    // per-round D2H copies); coherent + mapped, read after the round's completion event
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&ring_), ring_stride_ * 4 * o_.ring,
+                            hipHostMallocMapped | hipHostMallocCoherent),
               "hipHostMalloc(plane ring)");
+    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&ring_dev_), ring_, 0), "hipHostGetDevicePointer(ring)");
     free_slots_.clear();
     for (int i = o_.ring - 1; i >= 0; --i) free_slots_.push_back(i);
     while (static_cast<int>(events_.size()) < o_.ring) {
@@ -313,7 +317,11 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   rec.epoch = cfg_.epoch;
   rec.cold = cold;
   rec.out = buffer(static_cast<size_t>(n * es));
-  rec.cnt_dev = buffer(static_cast<size_t>(cfg_.peers) * nch_ * 4);
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    rec.slot = take_slot(lk);
+  }
+  int32_t* slot_dev = ring_dev_ + static_cast<size_t>(rec.slot) * ring_stride_;
   const void* in_ptr = rec.out.get();  // a cold round reads no input
   if (!cold) {
     if (!input || static_cast<int64_t>(input->size()) != n) throw ProtocolError("xgmi plane: input must hold dataSize elements");
@@ -350,22 +358,22 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   spec.cold = cold;
   spec.order_ref = o_.order_ref;
   spec.host_force = hforce_dev_;
+  spec.err_out = reinterpret_cast<uint32_t*>(slot_dev + ring_stride_ - 1);
   {
     TraceScope span("plane", [&] {
       return std::make_pair(std::string(cold ? "cold round " : "round ") + std::to_string(round),
                             "{\"worker\":" + std::to_string(cfg_.id) + ",\"bytes\":" + std::to_string(n * es) + "}");
     });
-    comm_->round(in_ptr, rec.out.get(), n, o_.dtype, stream_, cfg_.thReduce, cfg_.thComplete,
-                 static_cast<int32_t*>(rec.cnt_dev.get()), spec, 1.f);
+    try {
+      comm_->round(in_ptr, rec.out.get(), n, o_.dtype, stream_, cfg_.thReduce, cfg_.thComplete, slot_dev, spec,
+                   1.f);
+    } catch (...) {
+      std::lock_guard<std::mutex> g(mu_);
+      free_slots_.push_back(rec.slot);
+      throw;
+    }
   }
   std::unique_lock<std::mutex> lk(mu_);
-  rec.slot = take_slot(lk);
-  int32_t* host = ring_ + static_cast<size_t>(rec.slot) * ring_stride_;
-  hip_check(hipMemcpyAsync(host, rec.cnt_dev.get(), static_cast<size_t>(cfg_.peers) * nch_ * 4, hipMemcpyDeviceToHost,
-                           stream_),
-            "hipMemcpyAsync(counts)");
-  hip_check(hipMemcpyAsync(host + ring_stride_ - 1, comm_->ctl_ptr() + 2, 4, hipMemcpyDeviceToHost, stream_),
-            "hipMemcpyAsync(error word)");
   rec.ev = events_[rec.slot];
   hip_check(hipEventRecord(rec.ev, stream_), "hipEventRecord(round)");
   last_round_ = round;
@@ -402,7 +410,12 @@ void XgmiRoundPlane::completion_loop() {
       if (q_.empty()) return;
       rec = q_.front();  // stays queued until its callback ran (drain waits for that)
     }
-    const hipError_t e = hipEventSynchronize(rec.ev);
+    hipError_t e;
+    {
+      TraceScope span("plane", [&] { return std::make_pair("wait r" + std::to_string(rec.round), std::string()); });
+      e = hipEventSynchronize(rec.ev);
+    }
+    trace_instant("plane", "done r" + std::to_string(rec.round));
     RoundResult res;
     res.epoch = rec.epoch;
     res.round = rec.round;

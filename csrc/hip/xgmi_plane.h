@@ -81,7 +81,7 @@ class XgmiRoundPlane final : public RoundPlane {
   struct Rec {
     int round = 0;
     int64_t epoch = 0;
-    std::shared_ptr<void> out, cnt_dev, staging;
+    std::shared_ptr<void> out, staging;
     Payload input;
     hipEvent_t ev = nullptr;
     int slot = 0;
@@ -116,6 +116,7 @@ class XgmiRoundPlane final : public RoundPlane {
   int last_round_ = -1;  // last launched round of this epoch
   // pinned ring: per slot P x nch counts + the error word
   int32_t* ring_ = nullptr;
+  int32_t* ring_dev_ = nullptr;  // the ring's device-visible address
   size_t ring_stride_ = 0;  // int32 per slot
   std::vector<int> free_slots_;
   uint32_t err_seen_ = 0;

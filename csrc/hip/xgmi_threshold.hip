@@ -584,6 +584,8 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
       __hip_atomic_store(&ctl[6], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&ctl[7], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&ctl[4], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a.err_out)  // the protocol plane reads it from pinned memory after the round's event
+        __hip_atomic_store(a.err_out, ld_ctl(err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       for (int k = 0; k < P; ++k)
         if (k != r) st_flag(prog(a, k, r), epoch);

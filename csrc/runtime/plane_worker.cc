@@ -133,7 +133,13 @@ void PlaneWorkerActor::on_start(const StartAllreduce& m) {
     if (payload_size(in.data) != static_cast<size_t>(cfg_.dataSize))  // AllreduceWorker.scala:174-176
       throw ProtocolError("Input data size " + std::to_string(payload_size(in.data)) +
                           " is different from initialization time " + std::to_string(cfg_.dataSize) + "!");
-    plane_->launch(r, in.data, false);
+    {
+      TraceScope span("worker", [&] {
+        return std::make_pair(std::string("launch r" + std::to_string(r)),
+                              std::string("{\"worker\":" + std::to_string(id_) + "}"));
+      });
+      plane_->launch(r, in.data, false);
+    }
     launched_ = r;
     stats_.rounds_launched++;
   }
@@ -161,7 +167,13 @@ void PlaneWorkerActor::on_done(PlaneRoundDone& d) {
     t0_.erase(it);
   }
   MXAR_LOG(INFO, "worker", "----Flushing round " << r << " (" << payload_size(d.output.data) << " elements)");
-  if (sink_) sink_(d.output);
+  {
+    TraceScope span("worker", [&] {
+      return std::make_pair(std::string("sink r" + std::to_string(r)),
+                            std::string("{\"worker\":" + std::to_string(id_) + "}"));
+    });
+    if (sink_) sink_(d.output);
+  }
   stats_.rounds_completed++;
   stats_.complete_out++;
   if (master_) master_->tell(CompleteAllreduce{id_, r, cfg_.epoch}, self_);

@@ -132,3 +132,81 @@ def test_graceful_leave():
         mnode.shutdown()
         wsys.shutdown()
         msys.shutdown()
+
+
+def _recv(probe, kind, timeout=5.0):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        e = probe.receive(0.2)
+        if e is not None and isinstance(e[0], kind):
+            return e[0]
+    return None
+
+
+def test_plane_descriptors_ride_the_join_and_init_workers():
+    """a GPU worker announces its plane descriptor (the IPC handle of its HBM
+    arena) in the cluster join (ClusterConfig.meta); the master relays every worker's
+    descriptor in InitWorkers.planes, over the TCP codec."""
+    mport = free_port()
+    seed = f"mxar.tcp://ClusterSystem@127.0.0.1:{mport}"
+    msys = C.ActorSystem("ClusterSystem", False)
+    master = msys.master(2, 1.0, 1.0, 1.0, 1, 10, 3, 2)
+    mcfg = _cfg(mport, ["master"], [seed])
+    mcfg.worker_path = "/system/worker"  # the workers below are probes
+    mnode = C.ClusterNode.start(msys, mcfg)
+    mnode.subscribe(master)
+    systems, nodes, probes, metas = [], [], [], []
+    for k in range(2):
+        s = C.ActorSystem("ClusterSystem", False)
+        probes.append(s.probe("worker"))
+        cfg = _cfg(0, ["worker"], [seed])
+        cfg.meta = f"xgmi1 pid={1000 + k} dev=0 bytes=1 id={k} h=" + "ab" * 64
+        metas.append(cfg.meta)
+        systems.append(s)
+        nodes.append(C.ClusterNode.start(s, cfg))
+    try:
+        for k, p in enumerate(probes):
+            init = _recv(p, C.InitWorkers)
+            assert init is not None, k
+            assert sorted(init.planes.values()) == sorted(metas)
+            assert init.planes[init.destId] == metas[k]  # the own arena is the one it announced
+            assert init.roundBase == 0 and init.epoch == 1
+            assert _recv(p, C.StartAllreduce) is not None
+        assert sorted(m["meta"] for m in mnode.members() if "worker" in m["roles"]) == sorted(metas)
+    finally:
+        for n in nodes:
+            n.shutdown()
+        mnode.shutdown()
+        for s in systems + [msys]:
+            s.shutdown()
+
+
+def test_master_round_base_grows_across_reinit_and_typed_round_timer():
+    """InitWorkers.roundBase: a re-initialisation maps the new epoch's rounds above every
+    device round epoch the old one could have used. The round deadline is a typed
+    RoundTimeout message: a TextMessage with the old timer's text no longer advances."""
+    sys_ = C.ActorSystem("S", False)
+    master = sys_.master(2, 1.0, 1.0, 1.0, 1, 10, 100, 2, roundTimeoutMs=0)
+    probes = [sys_.probe(f"w{k}") for k in range(3)]
+    for k in range(2):
+        master.tell(C.MemberUp(probes[k], "worker", "", f"plane-{k}"), None)
+    for k in range(2):
+        init = _recv(probes[k], C.InitWorkers)
+        assert init.roundBase == 0 and init.planes == {0: "plane-0", 1: "plane-1"}
+    for r in range(3):  # rounds 0..2 complete, round 3 is started
+        for k in range(2):
+            assert _recv(probes[k], C.StartAllreduce).round == r
+        for k in range(2):
+            master.tell(C.CompleteAllreduce(k, r, 1), None)
+    master.tell(C.TextMessage("mxar.round-timeout 1 3"), None)  # not a timer any more
+    time.sleep(0.2)
+    assert sys_.master_state(master)["round"] == 3 and sys_.master_state(master)["round_timeouts"] == 0
+    master.tell(C.RoundTimeout(1, 3), None)  # the typed deadline advances the round
+    assert _wait(lambda: sys_.master_state(master)["round"] == 4)
+    master.tell(C.MemberUp(probes[2], "worker", "", "plane-2"), None)  # late joiner: re-init
+    inits = [_recv(p, C.InitWorkers) for p in probes]
+    assert all(i is not None and i.epoch == 2 for i in inits)
+    # epoch 1 started rounds 0..4 (device epochs 1..5): epoch 2 starts above them
+    assert {i.roundBase for i in inits} == {6}
+    assert sorted(inits[0].planes.values()) == ["plane-0", "plane-1", "plane-2"]
+    sys_.shutdown()

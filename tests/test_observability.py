@@ -36,6 +36,10 @@ def test_tracer_records_protocol_timeline():
     assert any(n.startswith("complete r") for n in names)
     spans = [e for e in doc["traceEvents"] if e["ph"] == "X"]
     assert spans and all(e["dur"] >= 0 for e in spans)
+    # timestamps keep sub-microsecond resolution however long the process has been up (a
+    # 6-significant-digit print once collapsed every event onto one instant)
+    ts = sorted(e["ts"] for e in doc["traceEvents"])
+    assert len(set(ts)) > len(ts) // 2, ts[:5]
     C.trace.clear()
 
 

@@ -34,7 +34,11 @@ def main() -> None:
     ap.add_argument("--units", type=int, default=256, help="reduce units (chunks) per block")
     ap.add_argument("--timeout", type=float, default=10.0)
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--trace", default=None, help="write a Chrome trace of the last size here")
     a = ap.parse_args()
+    from akka_allreduce_1_amd._native import C
+    if a.trace:
+        C.trace.enable(True)
     dev = torch.device("cuda", 0)
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     es = 2 if dtype == torch.bfloat16 else 4
@@ -72,6 +76,10 @@ def main() -> None:
         finally:
             job.shutdown()
         print(json.dumps(row), flush=True)
+        if a.trace:
+            with open(a.trace, "w") as f:
+                f.write(C.trace.dump_json())
+            C.trace.clear()
         del xs, ref
         torch.cuda.empty_cache()
 
