@@ -241,8 +241,10 @@ class XgmiCommunicator:
 
     # ------------------------------------------------------------------ collectives
     def allreduce(self, inp: torch.Tensor, out: torch.Tensor | None = None, *, op: str = "sum",
-                  algo: str = "auto") -> torch.Tensor:
+                  algo: str = "auto", stream: int | None = None) -> torch.Tensor:
         """out = sum (or mean) over ranks of inp. `out=inp` gives an in-place allreduce.
+        `stream`: raw HIP stream handle to enqueue on (default: torch's current stream) - the
+        DP reducer passes its comm stream without entering a torch stream context.
 
         The kernel path costs a few microseconds of host time per call (tools/host_overhead.py):
         integer device checks, a cached (Algo, grid) per algorithm label, the raw current-stream
@@ -264,7 +266,8 @@ class XgmiCommunicator:
             if self._grid != grid:
                 self._c.grid = grid
                 self._grid = grid
-            self._c.allreduce(inp.data_ptr(), out.data_ptr(), inp.numel(), code, _current_stream(self._dev), kind,
+            self._c.allreduce(inp.data_ptr(), out.data_ptr(), inp.numel(), code,
+                              _current_stream(self._dev) if stream is None else stream, kind,
                               1.0 / self.world if op == "avg" else 1.0)
         elif algo == "threshold" and self._threshold_fits(inp):
             # the straggler-tolerant kernel at th = 1 is an exact allreduce with its own
@@ -287,11 +290,12 @@ class XgmiCommunicator:
             if name not in ALGOS:
                 raise ValueError(f"unknown algo {algo!r}")
             self._launch[algo] = (ALGOS[name], int(g) if g else self._default_grid)
-            return self.allreduce(inp, out, op=op, algo=algo)
+            return self.allreduce(inp, out, op=op, algo=algo, stream=stream)
         return out
 
-    def allreduce_(self, t: torch.Tensor, *, op: str = "sum", algo: str = "auto") -> torch.Tensor:
-        return self.allreduce(t, t, op=op, algo=algo)
+    def allreduce_(self, t: torch.Tensor, *, op: str = "sum", algo: str = "auto",
+                   stream: int | None = None) -> torch.Tensor:
+        return self.allreduce(t, t, op=op, algo=algo, stream=stream)
 
     def _threshold_fits(self, t: torch.Tensor) -> bool:
         return (self.world > 1 and self._c.threshold_rows > 0 and t.dtype in _KERNEL_DTYPES

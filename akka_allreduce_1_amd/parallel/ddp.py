@@ -130,10 +130,21 @@ class BucketedGradReducer:
             self._H = C.hip
             # one compute->comm event per bucket + one comm->compute event
             self._events = [self._H.event_create(event_scope) for _ in range(len(self.buckets) + 1)]
-        self.slot_of: dict[int, tuple[GradBucket, int]] = {}
+        # per parameter: (bucket, offset, address its .grad view must have) - the hook runs
+        # once per parameter per step, so it does one data_ptr() call and no arithmetic
+        self.slot_of: dict[int, tuple[GradBucket, int, int]] = {}
         for b in self.buckets:
+            es = b.buffer.element_size()
             for p, off in zip(b.params, b.offsets):
-                self.slot_of[id(p)] = (b, off)
+                self.slot_of[id(p)] = (b, off, b.buffer.data_ptr() + off * es)
+        # raw stream handles: a bucket hand-off enters no torch stream context
+        from .comm import _current_stream
+
+        self._cur_stream = _current_stream
+        self._dev_index = self.device.index if self.on_gpu else -1
+        self._comm_raw = self.stream.cuda_stream if self.stream is not None else None
+        self._raw_ok = self.on_gpu and "stream" in getattr(getattr(comm, "allreduce_", None), "__code__",
+                                                              type("", (), {"co_varnames": ()})).co_varnames
         self._next = 0
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad_ready) for p in self.params]
         self.stats = {"steps": 0, "buckets_launched": 0, "bytes": 0}
@@ -173,9 +184,9 @@ class BucketedGradReducer:
 
     # ------------------------------------------------------------------ hooks
     def _on_grad_ready(self, p: torch.Tensor) -> None:
-        b, off = self.slot_of[id(p)]
-        expect = b.buffer.data_ptr() + off * b.buffer.element_size()
-        if p.grad is not None and p.grad.data_ptr() != expect:
+        b, off, expect = self.slot_of[id(p)]
+        g = p.grad
+        if g is not None and g.data_ptr() != expect:
             # .grad was replaced (e.g. zero_grad(set_to_none=True)): fold it back into the
             # bucket view - one copy; use reducer.zero_grad() to avoid it
             view = b.buffer[off:off + p.numel()].view_as(p)
@@ -204,12 +215,15 @@ class BucketedGradReducer:
 
     def _launch(self, b: GradBucket) -> None:
         if self.sync == "native":
-            cs = torch.cuda.current_stream(self.device).cuda_stream
+            cs = self._cur_stream(self._dev_index)
             ev = self._events[b.index]
             self._H.event_record(ev, cs)
-            self._H.stream_wait_event(self.stream.cuda_stream, ev)
-            with torch.cuda.stream(self.stream):
-                self._reduce(b)
+            self._H.stream_wait_event(self._comm_raw, ev)
+            if self._raw_ok and not self.threshold:  # straight onto the comm stream
+                self.comm.allreduce_(b.buffer, op=self.op, algo=self.algo, stream=self._comm_raw)
+            else:
+                with torch.cuda.stream(self.stream):
+                    self._reduce(b)
             b.done = True
         elif self.on_gpu:
             compute = torch.cuda.current_stream(self.device)
@@ -234,8 +248,8 @@ class BucketedGradReducer:
         # the comm stream runs the buckets in order: joining after the last one is enough
         if self.sync == "native":
             ev = self._events[-1]
-            self._H.event_record(ev, self.stream.cuda_stream)
-            self._H.stream_wait_event(torch.cuda.current_stream(self.device).cuda_stream, ev)
+            self._H.event_record(ev, self._comm_raw)
+            self._H.stream_wait_event(self._cur_stream(self._dev_index), ev)
         elif self.on_gpu:
             last = [b for b in self.buckets if b.done is not None]
             if last:
