@@ -103,6 +103,8 @@ def init_distributed(backend: str = "nccl") -> tuple[int, int, int]:
 class XgmiCommunicator:
     """Allreduce over directly mapped peer HBM for the ranks of a torch.distributed group."""
 
+    accepts_stream = True  # allreduce(..., stream=<raw hipStream_t>) (the DP reducer uses it)
+
     def __init__(self, group=None, *, device: torch.device | int | None = None, slot_bytes: int | None = None,
                  grid: int = 0, timeout_s: float = 20.0, cpu_group=None, max_lag: int | None = None):
         """max_lag: enables `allreduce_threshold`, whose ranks may run up to max_lag rounds

@@ -143,8 +143,8 @@ class BucketedGradReducer:
         self._cur_stream = _current_stream
         self._dev_index = self.device.index if self.on_gpu else -1
         self._comm_raw = self.stream.cuda_stream if self.stream is not None else None
-        self._raw_ok = self.on_gpu and "stream" in getattr(getattr(comm, "allreduce_", None), "__code__",
-                                                              type("", (), {"co_varnames": ()})).co_varnames
+        # communicators that take a raw `stream=` argument (XgmiCommunicator) skip the context
+        self._raw_ok = self.on_gpu and bool(getattr(comm, "accepts_stream", False))
         self._next = 0
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad_ready) for p in self.params]
         self.stats = {"steps": 0, "buckets_launched": 0, "bytes": 0}

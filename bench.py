@@ -33,6 +33,7 @@ import argparse
 import json
 import os
 import sys
+import statistics
 import threading
 import time
 
@@ -382,7 +383,7 @@ def dp_step(comm: XgmiCommunicator, model: str, dev) -> dict:
         reducer.remove_hooks()  # the synthetic backward calls the hook itself
         bwd = SyntheticBackward(params, 1024, torch.bfloat16, dev)
         grads = [q.grad for q in params]
-        steps, warm = (3, 1) if big else (10, 3)
+        steps, warm = (6, 1) if big else (20, 3)
 
         def overlap():
             bwd.run(reducer)
@@ -399,10 +400,19 @@ def dp_step(comm: XgmiCommunicator, model: str, dev) -> dict:
 
         with torch.no_grad():
             t = {}
-            for name, fn in (("step", overlap), ("compute", compute), ("comm", comm_only)):
+            for fn in (overlap, compute, comm_only):
                 for _ in range(warm):
                     fn()
-                t[name] = max_over_ranks(timed(fn, steps, dev), dev) / steps * 1e3
+            # step and compute-only alternate one step at a time and each takes its median:
+            # the exposed time is a ~1 % difference of two 30 ms steps, which clock drift
+            # between two back-to-back blocks of steps swamps (tools/reducer_overhead.py)
+            per = {"step": [], "compute": []}
+            for _ in range(steps):
+                per["step"].append(timed(overlap, 1, dev))
+                per["compute"].append(timed(compute, 1, dev))
+            for name, v in per.items():
+                t[name] = max_over_ranks(statistics.median(v), dev) * 1e3
+            t["comm"] = max_over_ranks(timed(comm_only, steps, dev), dev) / steps * 1e3
             if comm.world > 1:
                 # the same step with the bucket launches capped at 128 workgroups: a reduce
                 # running beside backward's GEMMs competes for CUs (ddp.py `algo`)

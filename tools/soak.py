@@ -11,8 +11,14 @@ calls on the same slabs and epoch counters (what `tune()` and a training step do
     # P processes on ONE GPU (rehearsal; gloo for the CPU group):
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/soak.py \
         --share-device --seconds 240
-    # one process per GPU:
+    # one process per GPU (rank k on local device k, cross-GPU stores over xGMI):
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/soak.py --seconds 600
+    # an explicit rank -> device map (rank k on devices[k % len]), e.g. 4 ranks on 2 GPUs:
+    torchrun --nproc-per-node 4 --master-addr 127.0.0.1 tools/soak.py --devices 0,1
+
+The control plane (stop flags, error counts, the communicator's handle exchange) is a gloo
+group in every mode, so the soak needs nothing from RCCL and the data moves only through
+the engine's kernels.
 """
 from __future__ import annotations
 
@@ -44,16 +50,22 @@ def main() -> None:
     ap.add_argument("--seconds", type=float, default=120.0)
     ap.add_argument("--max-mib", type=float, default=32.0, help="largest tensor per rank")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--share-device", action="store_true", help="every rank on cuda:0 (gloo CPU group)")
+    ap.add_argument("--share-device", action="store_true", help="every rank on cuda:0")
+    ap.add_argument("--devices", default="",
+                    help="comma-separated device ids, rank k runs on devices[k %% len] (default: local rank)")
     args = ap.parse_args()
-    rank, world, local = init_distributed("gloo" if args.share_device else "nccl")
+    rank, world, local = init_distributed("gloo")
+    devices = [int(d) for d in args.devices.split(",") if d.strip()] if args.devices else []
     if args.share_device:
-        local = 0
+        devices = [0]
+    local = devices[rank % len(devices)] if devices else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # ranks sharing a GPU split its workgroups so every persistent kernel stays resident
+    share = sum(1 for r in range(world) if (devices[r % len(devices)] if devices else r) == local)
     max_bytes = int(args.max_mib * (1 << 20))
     comm = XgmiCommunicator(device=local, slot_bytes=-(-max_bytes // world) + (1 << 20),
-                            grid=max(8, 512 // world) if args.share_device else 0, timeout_s=30.0, max_lag=1)
+                            grid=max(8, 512 // share) if share > 1 else 0, timeout_s=30.0, max_lag=1)
     rng = random.Random(args.seed)  # same stream on every rank
     counts: dict[str, int] = {}
     errors: list[str] = []
@@ -124,7 +136,8 @@ def main() -> None:
     if errors:
         print(f"[soak rank {rank}] " + "; ".join(errors[:5]), file=sys.stderr, flush=True)
     if rank == 0:
-        print(json.dumps({"metric": "soak", "world": world, "seconds": round(time.time() - t0, 1), "steps": step,
+        print(json.dumps({"metric": "soak", "world": world, "devices": devices or list(range(world)),
+                          "seconds": round(time.time() - t0, 1), "steps": step,
                           "errors_all_ranks": int(bad.item()), "ops": counts, "max_bytes": max_bytes}), flush=True)
     dist.barrier()
     dist.destroy_process_group()
