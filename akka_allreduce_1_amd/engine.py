@@ -42,14 +42,20 @@ def iota_source(n: int, device: torch.device, dtype: torch.dtype, offset: float 
 
 
 class PlaneJob:
-    """Master + P plane workers in one process (threaded actor system)."""
+    """Master + P plane workers in one process (threaded actor system).
+
+    Workers sharing a GPU run their round kernels concurrently on separate high-priority
+    streams; HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by
+    default), and a kernel queued behind a peer's spinning round kernel in the same queue
+    never starts. Set GPU_MAX_HW_QUEUES >= 2 * (workers per GPU) + 4 before HIP initialises
+    (bench.py and tools/plane_probe.py do) when several workers share one GPU."""
 
     def __init__(self, P: int, data_size: int, *, max_chunk_size: int, th_allreduce: float = 1.0,
                  th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 1, max_round: int = 10,
                  devices: Sequence[int] | None = None, dtype: torch.dtype = torch.float32, grid: int = 0,
                  sources: Sequence[Callable] | None = None, keep_outputs: bool = True, round_timeout_ms: int = 0,
                  timeout_s: float = 60.0, order_ref: bool = True, on_output: Callable | None = None,
-                 max_peers: int | None = None):
+                 max_peers: int | None = None, high_priority: bool = True):
         self.P = P
         self.n = data_size
         self.dtype = dtype
@@ -67,7 +73,8 @@ class PlaneJob:
         self.on_output = on_output
         self.stamps: list[float] = []  # perf_counter() when each round reached the master's barrier
         self.planes = [C.hip.xgmi_plane(d, dtype_code(dtype), data_size, max_peers=max_peers or P, max_lag=max_lag,
-                                        grid=grid, timeout_s=timeout_s, order_ref=order_ref) for d in self.devices]
+                                        grid=grid, timeout_s=timeout_s, order_ref=order_ref,
+                                        high_priority=high_priority) for d in self.devices]
         if sources is None:
             sources = [iota_source(data_size, torch.device("cuda", d), dtype, 1000.0 * k)
                        for k, d in enumerate(self.devices)]

@@ -48,7 +48,8 @@ else:
     # The N = 1 protocol section hosts two plane workers in this process; with RCCL's and
     # torch's streams, 4 hardware queues (HIP's default) make streams share queues, and work
     # queued behind a spinning round kernel in a shared queue stalls until its timeout.
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:  # raise, never lower (GPU boxes export 4)
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 # Library banners (RCCL's version block, gloo's "connected to N peer ranks") are written to
 # fd 1 from native code; keep stdout for the ONE result line: fd 1 -> stderr for the whole
@@ -502,12 +503,34 @@ def protocol_rounds(args, rank: int, world: int, dev) -> dict:
                                         grid=grid, on_output=on_output, timeout_s=120.0)
             stamps = res["stamps"]
             lat = res["state"]["round_latency"]
+            # the kernel sums in WORKER-id order (ids are dense in the master's join order, not
+            # torch ranks): the fp32 reference must add the ranks' inputs in that order
+            ids = [None] * world
+            dist.all_gather_object(ids, res["state"]["id"])
             ref = torch.zeros(n, device=dev)
-            for k in range(world):
+            for k in sorted(range(world), key=lambda q: ids[q]):
                 ref += fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=700 + k).float()
-            good = torch.tensor([1 if ("y" in last and torch.equal(last["y"], ref.to(dtype))) else 0], device=dev)
+            row["worker_ids"] = ids
+            st = res["state"]["stats"]
+            mine = {"rank": rank, "output": "y" in last, "plane_errors": st["plane_errors"],
+                    "forced": st["forced_completions"], "cold": st["cold_rounds"]}
+            if "y" in last:
+                diff = (last["y"].float() - ref.to(dtype).float()).abs()
+                mine["bad"] = int((diff > 0).sum().item())
+                mine["max_abs_err"] = float(diff.max().item())
+                if mine["bad"]:  # the first few mismatches with every rank's input (bf16 bits as floats)
+                    idx = torch.nonzero(diff > 0).flatten()[:3].tolist()
+                    xs_all = [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=700 + k) for k in range(world)]
+                    mine["first_bad"] = [{"i": i, "got": float(last["y"][i].float()), "ref_f32": float(ref[i]),
+                                          "inputs": [float(xk[i].float()) for xk in xs_all]} for i in idx]
+                    del xs_all
+            good = torch.tensor([1 if (mine.get("bad", 1) == 0 and not mine["plane_errors"]) else 0], device=dev)
             dist.all_reduce(good, op=dist.ReduceOp.MIN)
             row["validated"] = bool(good.item())
+            if not row["validated"]:  # which rank, how many elements, kernel error words
+                detail = [None] * world
+                dist.all_gather_object(detail, mine)
+                row["validation_detail"] = detail
             row["note"] = "one worker per GPU process; master on rank 0; control over TCP, data over xGMI"
         if len(stamps) > warm + 1:
             per = (stamps[-1] - stamps[warm - 1]) / (len(stamps) - warm)

@@ -112,7 +112,10 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   // a kernel trace with two workers in one process).
   int lo = 0, hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-  hip_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "hipStreamCreate(plane)");
+  // Many planes in one process (workers sharing a GPU) may instead want normal priority:
+  // normal-priority streams are dealt round-robin over GPU_MAX_HW_QUEUES queues.
+  hip_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, o_.high_priority ? hi : lo),
+            "hipStreamCreate(plane)");
   // keep freed round buffers in the device's default pool instead of returning them to the
   // driver at every synchronisation (the next round reuses them)
   hipMemPool_t mp = nullptr;

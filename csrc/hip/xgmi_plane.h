@@ -50,6 +50,7 @@ struct XgmiPlaneOptions {
   double timeout_s = 60.0;
   bool order_ref = true;  // the reference's arrival-order accounting (threshold kernel doc)
   int ring = 64;          // rounds in flight at most (pinned count / error slots)
+  bool high_priority = true;  // plane stream priority (see XgmiRoundPlane ctor)
 };
 
 struct XgmiPlaneStats {

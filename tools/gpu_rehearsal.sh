@@ -1,14 +1,13 @@
 #!/bin/bash
-# Multi-rank rehearsal of bench.py on ONE GPU: 2 and 4 ranks (torch.distributed.run, gloo,
-# every rank on cuda:0, IPC-mapped slabs, split workgroup budget). Same code path as the
-# driver's N-GPU run minus xGMI and RCCL. (run via gpurun)
+# Multi-process rehearsal of the whole N>1 bench path on ONE GPU (--share-device: gloo for the
+# CPU group, IPC-mapped slabs and plane arenas, split workgroup budget): N = 4, then N = 8.
 set -o pipefail
-cd "$GRAFT_REPO_ROOT" || exit 1
-mkdir -p gpurun_out
+mkdir -p gpurun_out/rehearsal
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-for N in ${REHEARSAL_NS:-2 4 8}; do
-  timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 \
-    --master-port $((29600 + N)) bench.py --gpus $N --steps 10 --warmup 3 --share-device ${BENCH_ARGS:-} \
-    > gpurun_out/rehearsal_n$N.json 2> gpurun_out/rehearsal_n$N.err || { echo "rehearsal N=$N failed"; tail -30 gpurun_out/rehearsal_n$N.err; exit 1; }
-  cut -c1-600 gpurun_out/rehearsal_n$N.json
+O=gpurun_out/rehearsal
+for n in 4 8; do
+  timeout -k 10 420 python -u -m torch.distributed.run --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29540 + n)) \
+      bench.py --gpus $n --share-device --steps 10 --warmup 3 --dp-rehearsal > $O/bench_share_n$n.json 2> $O/bench_share_n$n.err
+  rc=$?; echo "n=$n rc=$rc"; cat $O/bench_share_n$n.json; if [ $rc -ne 0 ]; then tail -20 $O/bench_share_n$n.err; exit $rc; fi
 done
+echo done

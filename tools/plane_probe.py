@@ -13,7 +13,22 @@ import os
 import sys
 import time
 
-import torch
+
+def _workers_from_argv() -> int:
+    for i, t in enumerate(sys.argv):
+        if t == "--P" and i + 1 < len(sys.argv):
+            return int(sys.argv[i + 1])
+    return 2
+
+
+# P workers in ONE process each spin a persistent kernel on its own plane stream; streams
+# that share a hardware queue serialise, so the queue count must cover every worker (plus
+# torch's own streams) or a round kernel waits behind a peer's spinning one. Before HIP init.
+_need = min(32, max(8, 2 * _workers_from_argv() + 4))
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _need:  # raise, never lower (the box sets 4)
+    os.environ["GPU_MAX_HW_QUEUES"] = str(_need)
+
+import torch  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -35,6 +50,7 @@ def main() -> None:
     ap.add_argument("--timeout", type=float, default=10.0)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--trace", default=None, help="write a Chrome trace of the last size here")
+    ap.add_argument("--priority", choices=["high", "normal"], default="high", help="plane stream priority")
     a = ap.parse_args()
     from akka_allreduce_1_amd._native import C
     if a.trace:
@@ -56,8 +72,9 @@ def main() -> None:
 
         job = PlaneJob(a.P, n, max_chunk_size=chunk, dtype=dtype, max_round=a.rounds - 1,
                        sources=[(lambda req, x=x: x) for x in xs], keep_outputs=False, on_output=on_output,
-                       timeout_s=a.timeout)
-        row = {"P": a.P, "bytes": S, "chunk": chunk}
+                       timeout_s=a.timeout, high_priority=a.priority == "high")
+        row = {"P": a.P, "bytes": S, "chunk": chunk, "priority": a.priority,
+               "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}
         t0 = time.perf_counter()
         try:
             job.run(timeout=max(60.0, 4 * a.timeout))
