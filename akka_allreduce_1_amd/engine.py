@@ -55,7 +55,7 @@ class PlaneJob:
                  devices: Sequence[int] | None = None, dtype: torch.dtype = torch.float32, grid: int = 0,
                  sources: Sequence[Callable] | None = None, keep_outputs: bool = True, round_timeout_ms: int = 0,
                  timeout_s: float = 60.0, order_ref: bool = True, on_output: Callable | None = None,
-                 max_peers: int | None = None, high_priority: bool = True):
+                 max_peers: int | None = None, high_priority: bool = True, order_release: bool = True):
         self.P = P
         self.n = data_size
         self.dtype = dtype
@@ -65,6 +65,7 @@ class PlaneJob:
         if grid <= 0:  # workers sharing a GPU split its workgroups so every kernel stays resident
             share = max(self.devices.count(d) for d in set(self.devices))
             grid = max(8, 512 // share)
+        self.grid = grid
         self.system = C.ActorSystem("ClusterSystem", False)
         self.finished = threading.Event()
         self.rounds = {"n": 0}
@@ -74,7 +75,8 @@ class PlaneJob:
         self.stamps: list[float] = []  # perf_counter() when each round reached the master's barrier
         self.planes = [C.hip.xgmi_plane(d, dtype_code(dtype), data_size, max_peers=max_peers or P, max_lag=max_lag,
                                         grid=grid, timeout_s=timeout_s, order_ref=order_ref,
-                                        high_priority=high_priority) for d in self.devices]
+                                        high_priority=high_priority, order_release=order_release)
+                       for d in self.devices]
         if sources is None:
             sources = [iota_source(data_size, torch.device("cuda", d), dtype, 1000.0 * k)
                        for k, d in enumerate(self.devices)]

@@ -6,6 +6,7 @@
 #include <pybind11/stl.h>
 
 #include <chrono>
+#include <optional>
 #include <sstream>
 
 #include "../core/data_buffer.h"
@@ -142,9 +143,18 @@ DataSink make_sink(py::object fn) {
 DataSource make_plane_source(py::object fn) {
   auto holder = std::make_shared<PyCallable>(std::move(fn));
   return [holder](const AllReduceInputRequest& req) -> AllReduceInput {
-    py::gil_scoped_acquire g;
-    py::object r = holder->fn(req);
+    std::optional<py::gil_scoped_acquire> g;
+    {
+      TraceScope span("worker", [] { return std::make_pair(std::string("gil"), std::string()); });
+      g.emplace();
+    }
+    py::object r;
+    {
+      TraceScope span("worker", [] { return std::make_pair(std::string("py source"), std::string()); });
+      r = holder->fn(req);
+    }
     if (py::isinstance<AllReduceInput>(r)) return r.cast<AllReduceInput>();
+    TraceScope span("worker", [] { return std::make_pair(std::string("import"), std::string()); });
     return AllReduceInput{typed_payload_from_py(r)};
   };
 }

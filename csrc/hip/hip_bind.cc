@@ -212,6 +212,11 @@ void bind_hip(py::module_& m) {
       .def_property_readonly("block_elems", &XgmiRoundPlane::block_elems)
       .def_property_readonly("device", [](const XgmiRoundPlane& p) { return p.options().device; })
       .def_property_readonly("stream", [](const XgmiRoundPlane& p) { return reinterpret_cast<uintptr_t>(p.stream()); })
+      .def(
+          "set_phase_stamps",
+          [](XgmiRoundPlane& p, uintptr_t buf, int64_t slots) { p.set_phase_stamps(reinterpret_cast<uint64_t*>(buf), slots); },
+          py::arg("buf"), py::arg("slots"),
+          "per-workgroup phase stamps of this plane's round kernels (kPhaseSlots u64 each; 0 = off)")
       .def("drain", [](XgmiRoundPlane& p) {
         py::gil_scoped_release r;
         p.drain();
@@ -219,7 +224,7 @@ void bind_hip(py::module_& m) {
   h.def(
       "xgmi_plane",
       [](int device, DType dtype, int64_t capacity, int max_peers, int max_lag, int grid, double timeout_s,
-         bool order_ref, bool high_priority) {
+         bool order_ref, bool high_priority, bool order_release) {
         XgmiPlaneOptions o;
         o.device = device;
         o.dtype = dtype;
@@ -230,12 +235,13 @@ void bind_hip(py::module_& m) {
         o.timeout_s = timeout_s;
         o.order_ref = order_ref;
         o.high_priority = high_priority;
+        o.order_release = order_release;
         py::gil_scoped_release r;
         return make_xgmi_plane(o);
       },
       py::arg("device") = 0, py::arg("dtype") = DType::F32, py::arg("capacity"), py::arg("max_peers") = 8,
       py::arg("max_lag") = 4, py::arg("grid") = 0, py::arg("timeout_s") = 60.0, py::arg("order_ref") = true,
-      py::arg("high_priority") = true,
+      py::arg("high_priority") = true, py::arg("order_release") = true,
       "RoundPlane of the protocol engine on MI355X: an HBM arena exported over IPC, one threshold-kernel launch "
       "per round (csrc/hip/xgmi_plane.h)");
   py::enum_<Algo>(h, "Algo").value("Auto", Algo::Auto).value("TwoShot", Algo::TwoShot).value("OneShot", Algo::OneShot).value("Ring", Algo::Ring).value("LL", Algo::LL);

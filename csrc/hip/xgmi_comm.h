@@ -134,6 +134,7 @@ class XgmiComm {
     bool order_ref = false;
     const uint32_t* host_force = nullptr;  // device-visible pinned host word (may be null)
     uint32_t* err_out = nullptr;           // device-visible word the round's error word is copied to
+    int32_t* counts_host = nullptr;        // device-visible pinned copy of `counts`, written at round end
   };
   void round(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, float th_reduce, float th_complete,
              int32_t* counts, const RoundSpec& spec, float scale = 1.f);

@@ -916,6 +916,7 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
     a.order_ref = spec->order_ref ? 1 : 0;
     a.hforce = spec->host_force;
     a.err_out = spec->err_out;
+    a.counts_host = counts != nullptr ? spec->counts_host : nullptr;
   }
   a.delay_rank = -1;
   for (XgmiComm* c : group)
@@ -924,6 +925,8 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
       a.delay = static_cast<uint64_t>(c->delay_us_ * 100.0);  // s_memrealtime: 100 MHz
     }
   for (int k = 0; k < W; ++k) a.base[k] = c0.peers_[k];
+  a.stamps = c0.stamps_;
+  if (a.stamps != nullptr && gx * ranks_here > c0.stamp_slots_) a.stamps = nullptr;  // buffer too small: off
   hip_check(hipSetDevice(c0.device_), "hipSetDevice");
   TraceScope span("xgmi", [&] {
     return std::make_pair("threshold " + std::to_string(n * es) + "B",

@@ -51,6 +51,10 @@ struct CommArgs {
   int order_ref;
   const uint32_t* hforce;
   uint32_t* err_out;  // optional: the round's error word, written by the last workgroup (pinned host)
+  // optional: where the last workgroup copies `counts` (P x nch int32, pinned host) once the
+  // round is done - every workgroup writes its counts to device memory (`counts`), so no
+  // unit waits on a PCIe write acknowledgement
+  int32_t* counts_host;
   // low-latency one-shot (xgmi_ll.hip): slots [parity][src] of ll_slot bytes at off_LL
   int64_t off_LL, ll_slot;
   // fused reduce-scatter + AdamW + all-gather (xgmi_adam.hip): per rank fp32 shard state

@@ -90,10 +90,15 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
     for (int lag = 0; lag <= o_.max_lag; ++lag)
       flag_bytes_ = std::max(flag_bytes_, XgmiComm::flag_bytes(P, std::max<int64_t>(block * es, 16), lag + 1));
   }
+  int64_t max_counts = 1;  // P x chunks per round, over every membership this plane may see
   for (int P = 1; P <= o_.max_peers; ++P) {
     const int64_t block = static_cast<int64_t>(f32_ceil_div(o_.capacity, P));
     const XgmiComm::Layout L = XgmiComm::layout(P, std::max<int64_t>(block * es, 16), o_.max_lag + 1, flag_bytes_);
     arena_bytes_ = std::max(arena_bytes_, L.slab_bytes);
+    for (int lag = 0; lag <= o_.max_lag; ++lag)
+      max_counts = std::max<int64_t>(
+          max_counts, static_cast<int64_t>(P) * XgmiComm::layout(P, std::max<int64_t>(block * es, 16), lag + 1,
+                                                                 flag_bytes_).maxch);
   }
   arena_bytes_ = XgmiComm::ipc_safe_bytes(arena_bytes_);
   hip_check(hipSetDevice(o_.device), "hipSetDevice");
@@ -105,6 +110,23 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
             "hipHostMalloc(force word)");
   std::memset(hforce_, 0, 64);
   hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&hforce_dev_), hforce_, 0), "hipHostGetDevicePointer");
+  // Per-round counts + error word: a pinned ring the host reads and its HBM twin the
+  // workgroups write, both sized here for the largest membership. Never reallocated:
+  // hipFree / hipHostFree in configure() could synchronise the device while a peer's round
+  // kernel spins waiting for this worker's re-initialisation.
+  ring_stride_ = static_cast<size_t>(max_counts) + 4;
+  hip_check(hipHostMalloc(reinterpret_cast<void**>(&ring_), ring_stride_ * 4 * o_.ring,
+                          hipHostMallocMapped | hipHostMallocCoherent),
+            "hipHostMalloc(plane ring)");
+  std::memset(ring_, 0, ring_stride_ * 4 * o_.ring);
+  hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&ring_dev_), ring_, 0), "hipHostGetDevicePointer(ring)");
+  hip_check(hipMalloc(reinterpret_cast<void**>(&cnt_vram_), ring_stride_ * 4 * o_.ring), "hipMalloc(plane counts)");
+  hip_check(hipEventCreateWithFlags(&rel_ev_, hipEventDisableTiming), "hipEventCreate(release)");
+  for (int i = 0; i < o_.ring; ++i) {
+    hipEvent_t e = nullptr;
+    hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    events_.push_back(e);
+  }
   // High priority: HIP serves each priority level from its own hardware-queue pool, so the
   // plane's persistent round kernels never sit in the same hardware queue as the default
   // stream (a marker or kernel queued behind a spinning round in a shared queue would wait
@@ -157,6 +179,13 @@ XgmiRoundPlane::~XgmiRoundPlane() {
   if (th_.joinable()) th_.join();
   (void)hipSetDevice(o_.device);
   (void)hipStreamSynchronize(stream_);
+  {
+    std::lock_guard<std::mutex> g(rel_->mu);
+    if (!rel_->ptrs.empty()) (void)hipStreamSynchronize(nullptr);
+    for (void* q : rel_->ptrs) (void)hipFree(q);
+    rel_->ptrs.clear();
+  }
+  if (rel_ev_) (void)hipEventDestroy(rel_ev_);
   comm_.reset();
   for (auto& [h, p] : mapped_) (void)hipIpcCloseMemHandle(p);
   {
@@ -165,25 +194,54 @@ XgmiRoundPlane::~XgmiRoundPlane() {
   }
   for (hipEvent_t e : events_) (void)hipEventDestroy(e);
   if (ring_) (void)hipHostFree(ring_);
+  if (cnt_vram_) (void)hipFree(cnt_vram_);
   if (hforce_) (void)hipHostFree(hforce_);
   if (stream_) (void)hipStreamDestroy(stream_);
   if (arena_) (void)hipFree(arena_);
 }
 
-std::shared_ptr<void> XgmiRoundPlane::buffer(size_t bytes) {
+std::shared_ptr<void> XgmiRoundPlane::buffer(size_t bytes, bool user_visible) {
   void* p = nullptr;
   hip_check(hipMallocAsync(&p, std::max<size_t>(bytes, 256), stream_), "hipMallocAsync(plane)");
   const hipStream_t s = stream_;
   std::weak_ptr<bool> alive = alive_;
   // released on the plane stream (ordered after every round that may still read it); an
-  // output the user keeps past the plane's lifetime is freed synchronously instead
-  return std::shared_ptr<void>(p, [s, alive](void* q) {
+  // output the user keeps past the plane's lifetime is freed synchronously instead.
+  // A round output went to the dataSink as a tensor: work the sink queued on the default
+  // stream (torch's, e.g. a clone) may still read it when the last reference drops, so its
+  // release is also ordered after the default stream - otherwise the next round could get
+  // the same block from the pool and overwrite it under that work.
+  std::weak_ptr<ReleaseQ> rq = rel_;
+  return std::shared_ptr<void>(p, [s, alive, user_visible, rq](void* q) {
     auto a = alive.lock();
-    if (a && *a)
+    if (a && *a) {
+      if (user_visible) {
+        if (auto r = rq.lock()) {  // freed by the next launch, behind the default stream
+          std::lock_guard<std::mutex> g(r->mu);
+          r->ptrs.push_back(q);
+          return;
+        }
+      }
       (void)hipFreeAsync(q, s);
-    else
+    } else {
       (void)hipFree(q);
+    }
   });
+}
+
+void XgmiRoundPlane::flush_releases() {
+  std::vector<void*> ptrs;
+  {
+    std::lock_guard<std::mutex> g(rel_->mu);
+    ptrs.swap(rel_->ptrs);
+  }
+  if (ptrs.empty()) return;
+  // one event for every output released since the last launch: the frees (and so the reuse
+  // of those blocks by this launch's allocations) come after everything the default stream
+  // held at this point - e.g. a sink's clone of the round output
+  hip_check(hipEventRecord(rel_ev_, nullptr), "hipEventRecord(release)");
+  hip_check(hipStreamWaitEvent(stream_, rel_ev_, 0), "hipStreamWaitEvent(release)");
+  for (void* q : ptrs) (void)hipFreeAsync(q, stream_);
 }
 
 void XgmiRoundPlane::set_done(DoneFn fn) {
@@ -269,28 +327,19 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
   comm_ = std::make_unique<XgmiComm>(cfg.id, P, o_.device, slot, o_.grid, o_.timeout_s, cfg.maxLag + 1, arena_,
                                      arena_bytes_, flag_bytes_);
   comm_->connect_ptrs(bases);
+  comm_->set_phase_stamps(stamps_, stamp_slots_);
   // Every round of the previous epoch has finished here (drained): say so to the peers. Their
   // lag gates for this epoch's first maxLag + 1 rounds wait for exactly this value, so no
   // worker writes new-epoch data while any worker may still run an old-epoch round.
   comm_->publish_progress(cfg.roundBase, stream_);
   hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize(publish progress)");
+  if (static_cast<size_t>(P) * nch_ + 4 > ring_stride_) throw ProtocolError("xgmi plane: counts ring too small");
   {
+    // the kernel counts into the slot's HBM twin and copies them, with the error word, into
+    // the pinned slot at round end (no per-round D2H copy); read after the completion event
     std::lock_guard<std::mutex> g(mu_);
-    if (ring_) (void)hipHostFree(ring_);
-    ring_stride_ = static_cast<size_t>(P) * nch_ + 4;
-    // the kernel writes each round's counts and error word straight into its slot (no
-    // per-round D2H copies); coherent + mapped, read after the round's completion event
-    hip_check(hipHostMalloc(reinterpret_cast<void**>(&ring_), ring_stride_ * 4 * o_.ring,
-                            hipHostMallocMapped | hipHostMallocCoherent),
-              "hipHostMalloc(plane ring)");
-    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&ring_dev_), ring_, 0), "hipHostGetDevicePointer(ring)");
     free_slots_.clear();
     for (int i = o_.ring - 1; i >= 0; --i) free_slots_.push_back(i);
-    while (static_cast<int>(events_.size()) < o_.ring) {
-      hipEvent_t e = nullptr;
-      hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
-      events_.push_back(e);
-    }
   }
   cfg_ = cfg;
   configured_ = true;
@@ -319,7 +368,8 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   rec.round = round;
   rec.epoch = cfg_.epoch;
   rec.cold = cold;
-  rec.out = buffer(static_cast<size_t>(n * es));
+  flush_releases();
+  rec.out = buffer(static_cast<size_t>(n * es), o_.order_release);
   {
     std::unique_lock<std::mutex> lk(mu_);
     rec.slot = take_slot(lk);
@@ -362,13 +412,15 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   spec.order_ref = o_.order_ref;
   spec.host_force = hforce_dev_;
   spec.err_out = reinterpret_cast<uint32_t*>(slot_dev + ring_stride_ - 1);
+  spec.counts_host = slot_dev;  // the kernel counts into HBM and copies once, at round end
+  int32_t* cnt_dev = cnt_vram_ + static_cast<size_t>(rec.slot) * ring_stride_;
   {
     TraceScope span("plane", [&] {
       return std::make_pair(std::string(cold ? "cold round " : "round ") + std::to_string(round),
                             "{\"worker\":" + std::to_string(cfg_.id) + ",\"bytes\":" + std::to_string(n * es) + "}");
     });
     try {
-      comm_->round(in_ptr, rec.out.get(), n, o_.dtype, stream_, cfg_.thReduce, cfg_.thComplete, slot_dev, spec,
+      comm_->round(in_ptr, rec.out.get(), n, o_.dtype, stream_, cfg_.thReduce, cfg_.thComplete, cnt_dev, spec,
                    1.f);
     } catch (...) {
       std::lock_guard<std::mutex> g(mu_);
@@ -424,7 +476,7 @@ void XgmiRoundPlane::completion_loop() {
     res.round = rec.round;
     res.cold = rec.cold;
     const int32_t* host = ring_ + static_cast<size_t>(rec.slot) * ring_stride_;
-    const size_t nc = ring_stride_ - 4;
+    const size_t nc = static_cast<size_t>(cfg_.peers) * nch_;
     res.count.assign(host, host + nc);
     const uint32_t err = static_cast<uint32_t>(host[ring_stride_ - 1]);
     res.error = (err & ~err_seen_) | (e != hipSuccess ? 0x80000000u : 0u);

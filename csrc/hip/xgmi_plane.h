@@ -51,6 +51,7 @@ struct XgmiPlaneOptions {
   bool order_ref = true;  // the reference's arrival-order accounting (threshold kernel doc)
   int ring = 64;          // rounds in flight at most (pinned count / error slots)
   bool high_priority = true;  // plane stream priority (see XgmiRoundPlane ctor)
+  bool order_release = true;  // a round output's release waits for the default stream (buffer())
 };
 
 struct XgmiPlaneStats {
@@ -77,6 +78,13 @@ class XgmiRoundPlane final : public RoundPlane {
   int64_t chunk_elems() const { return chunk_; }
   int64_t block_elems() const { return block_; }
   XgmiComm* comm() const { return comm_.get(); }
+  // Phase-stamp buffer for this plane's round kernels (study knob, XgmiComm::set_phase_stamps);
+  // kept across re-initialisations. Call between rounds.
+  void set_phase_stamps(uint64_t* buf, int64_t slots) {
+    stamps_ = buf;
+    stamp_slots_ = buf ? slots : 0;
+    if (comm_) comm_->set_phase_stamps(stamps_, stamp_slots_);
+  }
 
  private:
   struct Rec {
@@ -95,7 +103,7 @@ class XgmiRoundPlane final : public RoundPlane {
   // Stream-ordered device buffer (hipMallocAsync on the plane stream, hipFreeAsync when the
   // last holder drops it): the launch path never calls a device-synchronising allocator
   // while a peer's kernel may be spinning on this worker's next launch.
-  std::shared_ptr<void> buffer(size_t bytes);
+  std::shared_ptr<void> buffer(size_t bytes, bool user_visible = false);
   int take_slot(std::unique_lock<std::mutex>& lk);
   void completion_loop();
 
@@ -118,6 +126,7 @@ class XgmiRoundPlane final : public RoundPlane {
   // pinned ring: per slot P x nch counts + the error word
   int32_t* ring_ = nullptr;
   int32_t* ring_dev_ = nullptr;  // the ring's device-visible address
+  int32_t* cnt_vram_ = nullptr;  // per-slot counts the workgroups write (HBM); copied into the ring at round end
   size_t ring_stride_ = 0;  // int32 per slot
   std::vector<int> free_slots_;
   uint32_t err_seen_ = 0;
@@ -131,6 +140,17 @@ class XgmiRoundPlane final : public RoundPlane {
   DoneFn done_;
   std::thread th_;
   XgmiPlaneStats st_;
+  uint64_t* stamps_ = nullptr;
+  int64_t stamp_slots_ = 0;
+  // Round outputs the sinks dropped, freed at the next launch behind one default-stream event
+  // (work a sink queued on torch's default stream may still read them; see buffer()).
+  struct ReleaseQ {
+    std::mutex mu;
+    std::vector<void*> ptrs;
+  };
+  std::shared_ptr<ReleaseQ> rel_ = std::make_shared<ReleaseQ>();
+  hipEvent_t rel_ev_ = nullptr;
+  void flush_releases();
   std::shared_ptr<bool> alive_ = std::make_shared<bool>(true);
 };
 

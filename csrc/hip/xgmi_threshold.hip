@@ -76,9 +76,11 @@ __device__ __forceinline__ bool wave_forced(const CommArgs& a, int r, uint32_t e
   return __any(f);
 }
 
-// Host-word polls at most every 20 us per workgroup.
+// Host-word polls at most every 20 us per workgroup, the first one 20 us after the kernel
+// started: a PCIe read stalls the polling wave for microseconds, and a round that finishes
+// within 20 us does not need to learn that it was forced.
 struct HostPoll {
-  uint64_t next = 0;
+  uint64_t next = wall_ticks() + 2000;
   __device__ __forceinline__ bool due() {
     const uint64_t t = wall_ticks();
     if (t < next) return false;
@@ -250,6 +252,11 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   __shared__ uint64_t pend[kGatherWords];
   __shared__ uint64_t early[kGatherWords];
   __shared__ uint32_t s0[kMaxSnapChunks];
+  __shared__ uint64_t ps_lds[kPhaseSlots];
+  // phase stamps (threshold layout): [0] start, [1] snapshot + lag gate done, [2] ticks
+  // waiting for contributions, [3] scatter + reduce done, [4] ticks waiting in the gather,
+  // [5] end, [6] scatter done, [7] units gathered
+  PhaseStamps ps(a, ps_lds);
   const int P = a.P;
   const int y = blockIdx.y;
   const int r = a.rank0 + y;
@@ -269,7 +276,13 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   int32_t* const counts = a.counts ? a.counts + static_cast<int64_t>(y) * P * a.nch : nullptr;
   const bool cold = a.cold != 0;
   const bool ref = a.order_ref != 0;
-  const bool snap = ref && !cold;  // cold rounds are forced from the start: no snapshot
+  // Full thresholds (thReduce = thComplete = 1): every contribution and every chunk is taken
+  // whatever the arrival order, so neither the launch snapshot (a grid-wide barrier) nor the
+  // output tickets (one device-scope atomic per unit) change the result: both are skipped.
+  // Forced rounds still exclude their own force-reduced chunks (reference order).
+  const bool full = a.min_reduce >= P && a.min_complete >= P * a.nch;
+  const bool snap = ref && !cold && !full;  // cold rounds are forced from the start: no snapshot
+  const bool tickets = !full;
   const int nu = (P - 1) * a.nch;
   const int mine = blockIdx.x < static_cast<unsigned>(nu) ? (nu - 1 - static_cast<int>(blockIdx.x)) / G + 1 : 0;
   const int nwords = (mine + 63) / 64;
@@ -311,13 +324,16 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
       if (lane == 0) {
         if (cnt) add_ctl(&ctl[5], cnt);
         __hip_atomic_fetch_add(&ctl[6], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        while (__hip_atomic_load(&ctl[6], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < static_cast<uint32_t>(G)) {
+        // relaxed spin, ONE acquire after it: an acquire per poll would invalidate this
+        // XCD's L2 on every iteration of every workgroup
+        while (ld_ctl(&ctl[6]) < static_cast<uint32_t>(G)) {
           __builtin_amdgcn_s_sleep(1);
           if (wall_ticks() > deadline) {
             __hip_atomic_fetch_or(err, ERR_TIMEOUT_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             break;
           }
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         sh_u32 = ld_ctl(&ctl[5]);
       }
     }
@@ -354,6 +370,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  ps.mark(1);
 
   // Phase 1 - ScatterBlock into the owners' row slots (a cold round sends nothing)
   if (!cold) {
@@ -367,6 +384,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
       publish_flags([&](int) { return f1(a, j, row * P + r, c); }, 1, epoch, rel);
     }
   }
+  ps.mark(6);
 
   // Phase 2 - reduce own chunk c once min_reduce contributions are in
   const int64_t bstart_own = static_cast<int64_t>(r) * a.block;
@@ -391,6 +409,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
         mask = first_k(s0c, a.min_reduce, r + 1, P);  // fired while draining the queue: no own
       } else {
         mask = (snap ? s0c : 0u) | own;
+        const uint64_t tw = ps.now();
         while (!forced) {
           const uint32_t fresh = present & ~mask;
           if (snap) {
@@ -411,6 +430,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
             break;
           }
         }
+        ps.add(2, tw);
         if (forced) {  // the reference's forced reduce sums whatever the buffer holds
           if (!in_ && f != nullptr) in_ = reached(ld_flag(f), epoch);
           mask = (static_cast<uint32_t>(__ballot(in_)) & others) | own;
@@ -425,7 +445,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
         if (ref) {
           if (forced || etotal >= static_cast<uint32_t>(a.min_complete))
             take = 0;
-          else
+          else if (tickets)
             take = etotal + add_ctl(&ctl[3], 1u) < static_cast<uint32_t>(a.min_complete) ? 1 : 0;
         }
         sh_flag = take;
@@ -448,10 +468,12 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
       st_flag(f2c(a, static_cast<int>(threadIdx.x), row * P + r, c), static_cast<uint32_t>(cnt));
     if (threadIdx.x == 0) {
       if (counts) counts[static_cast<int64_t>(r) * a.nch + c] = take ? cnt : 0;
-      if (!ref) add_ctl(&ctl[3], 1u);
+      if (!ref && tickets) add_ctl(&ctl[3], 1u);
     }
     publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : f2(a, k, row * P + r, c); }, P, epoch, rel);
   }
+
+  ps.mark(3);
 
   // Phase 3 - gather the other owners' chunks. Units of this workgroup are polled 64 at a
   // time by wave 0 and round-robin over passes, so a late chunk never blocks the count of
@@ -494,7 +516,9 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
         const int j = (r + 1 + u % Pm1) % P;
         if (threadIdx.x == 0) {
           int take = 1;
-          if (ref) {
+          if (!tickets) {
+            // full thresholds: every reduced chunk that arrives before a force is taken
+          } else if (ref) {
             if ((early[w] >> i) & 1ull)
               take = add_ctl(&ctl[7], 1u) < static_cast<uint32_t>(a.min_complete) ? 1 : 0;
             else
@@ -523,6 +547,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
           counts[static_cast<int64_t>(j) * a.nch + c] =
               take ? static_cast<int32_t>(ld_flag(f2c(a, r, row * P + j, c))) : 0;
         progressed = true;
+        ps.count(7);
         __syncthreads();
       }
     }
@@ -550,7 +575,9 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
     gave_up = sh_flag != 0;
     __syncthreads();
     if (gave_up) break;
+    const uint64_t tw = ps.now();
     __builtin_amdgcn_s_sleep(2);
+    ps.add(4, tw);
   }
   if (gave_up) {
     for (int w = 0; w < nwords; ++w) {
@@ -570,6 +597,9 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
     }
   }
 
+  ps.mark(5);
+  ps.flush();
+
   // Round end: the last workgroup resets the per-round counters, records the round and
   // tells every peer that this rank is done with row `row`. acq_rel ticket (unlike
   // finish_launch): the progress word promises peers that EVERY workgroup's reads of the
@@ -577,7 +607,20 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == static_cast<uint32_t>(G) - 1) {
+    sh_flag = t == static_cast<uint32_t>(G) - 1 ? 1 : 0;
+  }
+  __syncthreads();
+  const bool last = sh_flag != 0;
+  if (last && counts != nullptr && a.counts_host != nullptr) {
+    // every workgroup's counts are visible here (their tickets released them, ours acquired)
+    int32_t* dst = a.counts_host + static_cast<int64_t>(y) * P * a.nch;
+    for (int64_t i = threadIdx.x; i < static_cast<int64_t>(P) * a.nch; i += kCommThreads)
+      __hip_atomic_store(dst + i, __hip_atomic_load(counts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (last) {
       __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&ctl[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&ctl[5], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

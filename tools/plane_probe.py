@@ -41,6 +41,31 @@ def parse_size(s: str) -> int:
     return int(float(s[:-1]) * m[s[-1].upper()]) if s[-1].upper() in m else int(s)
 
 
+def phase_summary(per_worker) -> list[dict]:
+    """Threshold-kernel stamps (xgmi_threshold.hip layout) of one round per worker, in us
+    from the earliest workgroup start of ANY worker: when each worker's kernel started, got
+    through the snapshot / lag gate, finished scatter / reduce / gather, and how long its
+    workgroups waited."""
+    used = [st[st[:, 0] > 0] for st in per_worker]
+    t0 = min(int(u[:, 0].min()) for u in used if len(u))
+
+    def us(v):
+        return round(float(v) / 100.0, 1)
+
+    out = []
+    for k, u in enumerate(used):
+        if not len(u):
+            out.append({"worker": k})
+            continue
+        med = lambda col: int(u[:, col].median().item())  # noqa: E731 - int64: ticks exceed float32
+        out.append({"worker": k, "wgs": int(u.shape[0]), "start_first": us(int(u[:, 0].min()) - t0),
+                    "start_last": us(int(u[:, 0].max()) - t0), "gate_p50": us(med(1) - t0),
+                    "scatter_p50": us(med(6) - t0), "reduce_wait_mean": us(float(u[:, 2].float().mean())),
+                    "reduce_p50": us(med(3) - t0), "gather_wait_mean": us(float(u[:, 4].float().mean())),
+                    "end_p50": us(med(5) - t0), "end_max": us(int(u[:, 5].max()) - t0)})
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--P", type=int, default=2)
@@ -51,6 +76,10 @@ def main() -> None:
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--trace", default=None, help="write a Chrome trace of the last size here")
     ap.add_argument("--priority", choices=["high", "normal"], default="high", help="plane stream priority")
+    ap.add_argument("--no-order-release", action="store_true",
+                    help="release round outputs without waiting for the default stream (A/B knob)")
+    ap.add_argument("--stamps", action="store_true",
+                    help="phase stamps of every worker's LAST round kernel (same GPU clock for all workers)")
     a = ap.parse_args()
     from akka_allreduce_1_amd._native import C
     if a.trace:
@@ -72,9 +101,15 @@ def main() -> None:
 
         job = PlaneJob(a.P, n, max_chunk_size=chunk, dtype=dtype, max_round=a.rounds - 1,
                        sources=[(lambda req, x=x: x) for x in xs], keep_outputs=False, on_output=on_output,
-                       timeout_s=a.timeout, high_priority=a.priority == "high")
-        row = {"P": a.P, "bytes": S, "chunk": chunk, "priority": a.priority,
+                       timeout_s=a.timeout, high_priority=a.priority == "high",
+                       order_release=not a.no_order_release)
+        row = {"P": a.P, "bytes": S, "chunk": chunk, "priority": a.priority, "order_release": not a.no_order_release,
                "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}
+        bufs = []
+        if a.stamps:
+            bufs = [torch.zeros(job.grid * 8, dtype=torch.int64, device=dev) for _ in job.planes]
+            for p, b in zip(job.planes, bufs):
+                p.set_phase_stamps(b.data_ptr(), job.grid)
         t0 = time.perf_counter()
         try:
             job.run(timeout=max(60.0, 4 * a.timeout))
@@ -88,6 +123,8 @@ def main() -> None:
             row["errors"] = [w["stats"]["plane_errors"] for w in st["workers"]]
             row["validated"] = all(torch.equal(last.get(k, torch.empty(0)), ref) for k in range(a.P))
             row["lat_p50_ms"] = [round(w["round_latency"]["p50_ms"], 3) for w in st["workers"]]
+            if bufs:
+                row["phases_last_round"] = phase_summary([b.view(-1, 8).cpu() for b in bufs])
         except Exception as e:  # noqa: BLE001
             row["error"] = repr(e)[:400]
         finally:
