@@ -18,14 +18,18 @@ the plane descriptor then travels in the cluster join (ClusterConfig.meta).
 """
 from __future__ import annotations
 
+import itertools
 import threading
 import time
 from typing import Callable, Sequence
 
+import numpy as np
 import torch
 
 from ._native import C
 from .ops.kernels import dtype_code
+
+_HUBS = itertools.count()
 
 
 def iota_source(n: int, device: torch.device, dtype: torch.dtype, offset: float = 0.0) -> Callable:
@@ -37,6 +41,16 @@ def iota_source(n: int, device: torch.device, dtype: torch.dtype, offset: float 
         x = torch.empty(n, dtype=dtype, device=device)
         C.hip.fill_iota(x.data_ptr(), n, float(req.iteration) + offset, code, torch.cuda.current_stream(device).cuda_stream)
         return x
+
+    return source
+
+
+def host_iota_source(n: int, offset: float = 0.0) -> Callable:
+    """The reference's demo dataSource on the host (float32 data[i] = i + iteration + offset)."""
+    base = np.arange(n, dtype=np.float32)
+
+    def source(req):
+        return base + np.float32(req.iteration + offset)
 
     return source
 
@@ -55,14 +69,25 @@ class PlaneJob:
                  devices: Sequence[int] | None = None, dtype: torch.dtype = torch.float32, grid: int = 0,
                  sources: Sequence[Callable] | None = None, keep_outputs: bool = True, round_timeout_ms: int = 0,
                  timeout_s: float = 60.0, order_ref: bool = True, on_output: Callable | None = None,
-                 max_peers: int | None = None, high_priority: bool = True, order_release: bool = True):
+                 max_peers: int | None = None, high_priority: bool = True, order_release: bool = True,
+                 plane: str = "xgmi", hub: str | None = None):
+        """plane: "xgmi" (one threshold-kernel launch per round on the GPUs in `devices`) or
+        "loopback" (host memory, no GPU: csrc/runtime/loopback_plane.h; `hub` names the
+        workers' shared hub, default a fresh one; dtype float32, devices ignored)."""
         self.P = P
         self.n = data_size
         self.dtype = dtype
-        self.devices = list(devices) if devices is not None else [torch.cuda.current_device()] * P
+        if plane not in ("xgmi", "loopback"):
+            raise ValueError(f"unknown plane {plane!r}")
+        self.plane_kind = plane
+        if plane == "loopback":
+            self.devices = [None] * P
+            grid = 0
+        else:
+            self.devices = list(devices) if devices is not None else [torch.cuda.current_device()] * P
         if len(self.devices) != P:
             raise ValueError("one device per worker")
-        if grid <= 0:  # workers sharing a GPU split its workgroups so every kernel stays resident
+        if grid <= 0 and plane == "xgmi":  # workers sharing a GPU split its workgroups so every kernel stays resident
             share = max(self.devices.count(d) for d in set(self.devices))
             grid = max(8, 512 // share)
         self.grid = grid
@@ -73,13 +98,19 @@ class PlaneJob:
         self.keep = keep_outputs
         self.on_output = on_output
         self.stamps: list[float] = []  # perf_counter() when each round reached the master's barrier
-        self.planes = [C.hip.xgmi_plane(d, dtype_code(dtype), data_size, max_peers=max_peers or P, max_lag=max_lag,
-                                        grid=grid, timeout_s=timeout_s, order_ref=order_ref,
-                                        high_priority=high_priority, order_release=order_release)
-                       for d in self.devices]
-        if sources is None:
-            sources = [iota_source(data_size, torch.device("cuda", d), dtype, 1000.0 * k)
-                       for k, d in enumerate(self.devices)]
+        if plane == "loopback":
+            hub = hub or f"planejob{next(_HUBS)}"
+            self.planes = [C.loopback_plane(hub) for _ in range(P)]
+            if sources is None:
+                sources = [host_iota_source(data_size, 1000.0 * k) for k in range(P)]
+        else:
+            self.planes = [C.hip.xgmi_plane(d, dtype_code(dtype), data_size, max_peers=max_peers or P,
+                                            max_lag=max_lag, grid=grid, timeout_s=timeout_s, order_ref=order_ref,
+                                            high_priority=high_priority, order_release=order_release)
+                           for d in self.devices]
+            if sources is None:
+                sources = [iota_source(data_size, torch.device("cuda", d), dtype, 1000.0 * k)
+                           for k, d in enumerate(self.devices)]
         self.sources = list(sources)
 
         def fin(r):

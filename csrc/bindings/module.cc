@@ -17,6 +17,7 @@
 #include "../runtime/actor_system.h"
 #include "../runtime/allreduce_actors.h"
 #include "../runtime/fault_injector.h"
+#include "../runtime/loopback_plane.h"
 #include "../runtime/plane_worker.h"
 #include "py_common.h"
 
@@ -659,6 +660,29 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("name", &RoundPlane::name)
       .def_property_readonly("descriptor", &RoundPlane::descriptor)
       .def_property_readonly("chunks", &RoundPlane::chunks);
+  py::class_<LoopbackRoundPlane, RoundPlane, std::shared_ptr<LoopbackRoundPlane>>(m, "LoopbackRoundPlane")
+      .def_property_readonly("stats",
+                             [](LoopbackRoundPlane& p) {
+                               const LoopbackPlaneStats s = p.stats();
+                               py::dict d;
+                               d["launches"] = s.launches;
+                               d["cold"] = s.cold;
+                               d["forced_rounds"] = s.forced_rounds;
+                               d["peer_forces"] = s.peer_forces;
+                               d["completed"] = s.completed;
+                               return d;
+                             })
+      .def("force", [](LoopbackRoundPlane& p, int round) {
+        py::gil_scoped_release r;
+        p.force(round);
+      })
+      .def("drain", [](LoopbackRoundPlane& p) {
+        py::gil_scoped_release r;
+        p.drain();
+      });
+  m.def("loopback_plane", &make_loopback_plane, py::arg("hub"),
+        "RoundPlane in host memory (csrc/runtime/loopback_plane.h): the round engine's semantics for the "
+        "workers of one process, no GPU; every worker of a job names the same hub");
   m.def("host_plane", [] { return std::static_pointer_cast<DataPlane>(HostPlane::instance()); });
 
   bind_cluster(m);

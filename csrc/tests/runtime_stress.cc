@@ -18,6 +18,8 @@
 #include "../core/log.h"
 #include "../runtime/allreduce_actors.h"
 #include "../runtime/fault_injector.h"
+#include "../runtime/loopback_plane.h"
+#include "../runtime/plane_worker.h"
 
 using namespace mxar;
 
@@ -77,6 +79,51 @@ static int run_local(int P, int N, int C, int rounds) {
   return 0;
 }
 
+// The round engine on host memory: master + P PlaneWorkerActors over LoopbackRoundPlanes
+// (plane completion threads, hub mutex, actor mailboxes all live under the sanitizer).
+static int run_plane(int P, int N, int C, int rounds) {
+  auto sys = std::make_shared<ActorSystem>("ClusterSystem", ActorSystem::Mode::Threaded, 4);
+  std::atomic<bool> done{false};
+  MasterParams mp{P, 1.f, 1.f, 1.f, 1, N, rounds - 1, C, false};
+  ActorRef master = sys->actor_of(std::make_unique<MasterActor>(mp, [&](int) { done = true; }), "master");
+  std::mutex mu;
+  std::vector<std::vector<std::vector<float>>> outs(P);
+  std::vector<std::shared_ptr<LoopbackRoundPlane>> planes;
+  std::vector<ActorRef> refs;
+  for (int k = 0; k < P; ++k) {
+    DataSource src = [N, k](const AllReduceInputRequest& r) {
+      std::vector<float> v(N);
+      for (int i = 0; i < N; ++i) v[i] = static_cast<float>((i + r.iteration) * (k + 1));
+      return AllReduceInput{make_host_payload(std::move(v))};
+    };
+    DataSink sink = [&, k](const AllReduceOutput& o) {
+      std::lock_guard<std::mutex> g(mu);
+      if (static_cast<int>(outs[k].size()) <= o.iteration) outs[k].resize(o.iteration + 1);
+      outs[k][o.iteration] = o.data->to_host();
+    };
+    planes.push_back(make_loopback_plane("stress"));
+    refs.push_back(sys->actor_of(std::make_unique<PlaneWorkerActor>(src, sink, planes.back()), "pw" + std::to_string(k)));
+  }
+  for (int k = 0; k < P; ++k) master->tell(MemberUp{refs[k], "worker", "", planes[k]->descriptor()}, nullptr);
+  const bool ok = wait_until([&] { return done.load(); }, 60);
+  for (auto& p : planes) p->drain();
+  sys->await_idle(std::chrono::milliseconds(5000));
+  sys->shutdown();
+  if (!ok) {
+    std::fprintf(stderr, "plane cluster did not finish\n");
+    return 1;
+  }
+  const float tri = P * (P + 1) / 2.f;
+  for (int k = 0; k < P; ++k)
+    for (int r = 0; r < rounds; ++r)
+      for (int i = 0; i < N; ++i)
+        if (std::fabs(outs[k][r][i] - (i + r) * tri) > 1e-3f) {
+          std::fprintf(stderr, "plane: bad sum worker %d round %d idx %d\n", k, r, i);
+          return 1;
+        }
+  return 0;
+}
+
 // Three nodes over TCP on 127.0.0.1: master node + two worker nodes.
 static int run_tcp(int rounds) {
   const int N = 10, C = 2;
@@ -131,6 +178,7 @@ int main(int argc, char** argv) {
   if (only.empty() || only == "local") rc = run_local(4, 37, 3, 30);
   if (rc == 0 && (only.empty() || only == "local2")) rc = run_local(3, 9, 2, 30);
   if (rc == 0 && (only.empty() || only == "tcp")) rc = run_tcp(20);
+  if (rc == 0 && (only.empty() || only == "plane")) rc = run_plane(3, 41, 4, 40);
   std::printf(rc == 0 ? "runtime_stress: OK\n" : "runtime_stress: FAILED\n");
   return rc;
 }
