@@ -70,7 +70,7 @@ class PlaneJob:
                  sources: Sequence[Callable] | None = None, keep_outputs: bool = True, round_timeout_ms: int = 0,
                  timeout_s: float = 60.0, order_ref: bool = True, on_output: Callable | None = None,
                  max_peers: int | None = None, high_priority: bool = True, order_release: bool = True,
-                 plane: str = "xgmi", hub: str | None = None):
+                 plane: str = "xgmi", hub: str | None = None, spin_us: int = 1000):
         """plane: "xgmi" (one threshold-kernel launch per round on the GPUs in `devices`) or
         "loopback" (host memory, no GPU: csrc/runtime/loopback_plane.h; `hub` names the
         workers' shared hub, default a fresh one; dtype float32, devices ignored)."""
@@ -106,7 +106,8 @@ class PlaneJob:
         else:
             self.planes = [C.hip.xgmi_plane(d, dtype_code(dtype), data_size, max_peers=max_peers or P,
                                             max_lag=max_lag, grid=grid, timeout_s=timeout_s, order_ref=order_ref,
-                                            high_priority=high_priority, order_release=order_release)
+                                            high_priority=high_priority, order_release=order_release,
+                                            spin_us=spin_us)
                            for d in self.devices]
             if sources is None:
                 sources = [iota_source(data_size, torch.device("cuda", d), dtype, 1000.0 * k)

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <chrono>
 #include <cstring>
 #include <random>
 #include <sstream>
@@ -468,7 +469,18 @@ void XgmiRoundPlane::completion_loop() {
     hipError_t e;
     {
       TraceScope span("plane", [&] { return std::make_pair("wait r" + std::to_string(rec.round), std::string()); });
-      e = hipEventSynchronize(rec.ev);
+      // poll first: a blocking wait sleeps on an interrupt, whose wake-up adds tens of
+      // microseconds to every round; this thread has nothing else to do meanwhile
+      const auto t0 = std::chrono::steady_clock::now();
+      for (;;) {
+        e = hipEventQuery(rec.ev);
+        if (e != hipErrorNotReady) break;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(o_.spin_us)) {
+          e = hipEventSynchronize(rec.ev);
+          break;
+        }
+        std::this_thread::yield();
+      }
     }
     trace_instant("plane", "done r" + std::to_string(rec.round));
     RoundResult res;

@@ -52,6 +52,7 @@ struct XgmiPlaneOptions {
   int ring = 64;          // rounds in flight at most (pinned count / error slots)
   bool high_priority = true;  // plane stream priority (see XgmiRoundPlane ctor)
   bool order_release = true;  // a round output's release waits for the default stream (buffer())
+  int spin_us = 1000;         // completion thread polls a round's event this long before blocking
 };
 
 struct XgmiPlaneStats {

@@ -1,6 +1,7 @@
 #include "actor_system.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "../core/log.h"
 
@@ -222,6 +223,12 @@ ActorSystem::ActorSystem(std::string name, Mode mode, int threads, int throughpu
   dead_letters_ = std::make_shared<DeadLetterRef>(this);
   virtual_now_ = std::chrono::steady_clock::time_point{};
   if (mode_ == Mode::Threaded) {
+    // A dispatcher thread that ran out of work polls the run queue for MXAR_DISPATCH_SPIN_US
+    // (default 50 us) before it sleeps on the condition variable: a protocol round is a chain
+    // of actor hops (Start -> worker, plane done -> worker, Complete -> master), and a futex
+    // wake-up per hop costs more than the hop itself.
+    spin_us_ = 50;
+    if (const char* e = std::getenv("MXAR_DISPATCH_SPIN_US")) spin_us_ = std::max(0, std::atoi(e));
     int n = threads > 0 ? threads : std::max(2u, std::min(8u, std::thread::hardware_concurrency()));
     for (int i = 0; i < n; ++i) threads_.emplace_back([this] { worker_loop(); });
     timer_thread_ = std::thread([this] { timer_loop(); });
@@ -305,6 +312,7 @@ void ActorSystem::schedule(const std::shared_ptr<ActorCell>& cell) {
   {
     std::lock_guard<std::mutex> g(rq_mu_);
     runq_.push_back(cell);
+    runq_len_.store(runq_.size(), std::memory_order_release);
   }
   rq_cv_.notify_one();
 }
@@ -325,6 +333,7 @@ size_t ActorSystem::run_until_idle(size_t max_messages) {
       if (runq_.empty()) break;
       cell = runq_.front();
       runq_.pop_front();
+      runq_len_.store(runq_.size(), std::memory_order_release);
     }
     cell->scheduled_.store(false);
     total += cell->process(1);  // one message per turn: fair round-robin interleaving
@@ -346,12 +355,19 @@ size_t ActorSystem::run_until_idle(size_t max_messages) {
 void ActorSystem::worker_loop() {
   while (true) {
     std::shared_ptr<ActorCell> cell;
+    if (spin_us_ > 0 && runq_len_.load(std::memory_order_acquire) == 0) {
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us_);
+      while (runq_len_.load(std::memory_order_acquire) == 0 && !shutdown_.load() &&
+             std::chrono::steady_clock::now() < until)
+        std::this_thread::yield();
+    }
     {
       std::unique_lock<std::mutex> lk(rq_mu_);
       rq_cv_.wait(lk, [&] { return shutdown_.load() || !runq_.empty(); });
       if (shutdown_) return;
       cell = runq_.front();
       runq_.pop_front();
+      runq_len_.store(runq_.size(), std::memory_order_release);
       ++busy_;
     }
     size_t n = cell->process(static_cast<size_t>(throughput_));

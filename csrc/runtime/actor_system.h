@@ -256,6 +256,8 @@ class ActorSystem {
   std::condition_variable rq_cv_;
   std::condition_variable idle_cv_;
   std::deque<std::shared_ptr<ActorCell>> runq_;
+  std::atomic<size_t> runq_len_{0};  // runq_.size(), readable without rq_mu_ (idle spin)
+  int spin_us_ = 0;                  // idle dispatcher threads poll this long before sleeping
   int busy_ = 0;
   std::vector<std::thread> threads_;
   std::atomic<bool> shutdown_{false};

@@ -192,7 +192,7 @@ def test_simple_catchup_forces_rounds_without_errors():
             assert w["stats"]["plane_errors"] == 0, (k, w)  # no ERR_TIMEOUT_LAG, no timeouts
             assert w["round"] == 9, (k, w)  # every round 0..maxRound completed
         assert sum(w["stats"]["forced_completions"] for w in st["workers"][:2]) > 0, st
-        _consistent(job, P, n, chunk, {0, 2, 3})
+        _consistent(job, P, n, chunk, {0, 1, 2, 3})  # 1: a forced reduce of what had arrived
         step, nch = layout(n, P, chunk)
         # round 0 of a fast worker: forced; the fast blocks made it (count 2), the straggler's not
         data, counts = job.outputs[0][0]
@@ -265,7 +265,7 @@ def test_cold_catchup():
 
         class J:
             outputs = outs
-        _consistent(J, P, n, chunk, {0, 2, 3})
+        _consistent(J, P, n, chunk, {0, 1, 2, 3})  # 1: a forced reduce of what had arrived
     finally:
         system.shutdown()
 

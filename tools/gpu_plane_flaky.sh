@@ -10,3 +10,5 @@ for i in 1 2 3; do
   rc=$?; echo "run $i rc=$rc $(tail -1 $O/full$i.log)"; grep -h "error word\|PASSED\|FAILED" $O/full$i.log | cut -c1-120
   if [ $rc -gt 1 ]; then exit $rc; fi
 done
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -20 $O/smoke.log; exit 1; }
+tail -2 $O/smoke.log

@@ -76,6 +76,7 @@ def main() -> None:
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--trace", default=None, help="write a Chrome trace of the last size here")
     ap.add_argument("--priority", choices=["high", "normal"], default="high", help="plane stream priority")
+    ap.add_argument("--spin-us", type=int, default=1000, help="completion-thread polling before blocking")
     ap.add_argument("--no-order-release", action="store_true",
                     help="release round outputs without waiting for the default stream (A/B knob)")
     ap.add_argument("--stamps", action="store_true",
@@ -102,8 +103,8 @@ def main() -> None:
         job = PlaneJob(a.P, n, max_chunk_size=chunk, dtype=dtype, max_round=a.rounds - 1,
                        sources=[(lambda req, x=x: x) for x in xs], keep_outputs=False, on_output=on_output,
                        timeout_s=a.timeout, high_priority=a.priority == "high",
-                       order_release=not a.no_order_release)
-        row = {"P": a.P, "bytes": S, "chunk": chunk, "priority": a.priority, "order_release": not a.no_order_release,
+                       order_release=not a.no_order_release, spin_us=a.spin_us)
+        row = {"P": a.P, "bytes": S, "chunk": chunk, "priority": a.priority, "order_release": not a.no_order_release, "spin_us": a.spin_us,
                "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}
         bufs = []
         if a.stamps:
