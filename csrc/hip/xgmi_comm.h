@@ -70,9 +70,14 @@ class XgmiComm {
   // zeroed once, >= layout(...).slab_bytes; xgmi_plane.cc) instead of allocating one.
   // min_flag_bytes: reserve at least this much for the flag table (an arena reused by
   // layouts of different sizes keeps its flags at the same place: data never lands on a flag).
+  // external_slab / external_ctl: an arena and 256 B of control words owned by the caller
+  // (xgmi_plane.cc). With both, construction and destruction make NO device-synchronising
+  // call (no hipMalloc / hipFree / hipMemset / hipDeviceSynchronize): a plane re-lays its
+  // arena out while a peer's round kernel may be spinning on this worker; the caller
+  // resets the control words stream-ordered (hipMemsetAsync) before the first launch.
   XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid = 0, double timeout_s = 20.0,
            int threshold_rows = 0, char* external_slab = nullptr, int64_t external_bytes = 0,
-           int64_t min_flag_bytes = 0);
+           int64_t min_flag_bytes = 0, uint32_t* external_ctl = nullptr);
   ~XgmiComm();
   XgmiComm(const XgmiComm&) = delete;
   XgmiComm& operator=(const XgmiComm&) = delete;
@@ -266,6 +271,7 @@ class XgmiComm {
   bool ipc_opened_[kMaxRanks] = {};
   bool connected_ = false;
   bool own_slab_ = true;           // false: laid out over a caller's arena
+  bool own_ctl_ = true;            // false: control words owned by the caller
   bool launched_ = false;          // a launch has been enqueued (last_stream_ valid)
   hipStream_t last_stream_ = nullptr;
   hipEvent_t switch_ev_ = nullptr;  // recorded on last_stream_ when the stream changes

@@ -385,7 +385,8 @@ int64_t XgmiComm::ipc_safe_bytes(int64_t bytes) {
 }
 
 XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid, double timeout_s,
-                   int threshold_rows, char* external_slab, int64_t external_bytes, int64_t min_flag_bytes)
+                   int threshold_rows, char* external_slab, int64_t external_bytes, int64_t min_flag_bytes,
+                   uint32_t* external_ctl)
     : rank_(rank), world_(world), device_(device), grid_(grid), rows_(1 + threshold_rows), timeout_s_(timeout_s) {
   if (threshold_rows < 0 || threshold_rows > 64)
     throw std::invalid_argument("XgmiComm: threshold_rows (maxLag + 1) must be in [0, 64]");
@@ -439,9 +440,14 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
     hip_check(hipMemset(slab_, 0, off_S_), "hipMemset(flags)");
     hip_check(hipMemset(slab_ + off_LL_, 0, 2 * world_ * ll_slot_), "hipMemset(ll)");  // epoch 0 never occurs
   }
-  hip_check(hipMalloc(reinterpret_cast<void**>(&ctl_), 256), "hipMalloc(ctl)");
-  hip_check(hipMemset(ctl_, 0, 256), "hipMemset(ctl)");
-  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  if (external_ctl != nullptr && !own_slab_) {
+    ctl_ = external_ctl;  // reset by the caller, stream-ordered
+    own_ctl_ = false;
+  } else {
+    hip_check(hipMalloc(reinterpret_cast<void**>(&ctl_), 256), "hipMalloc(ctl)");
+    hip_check(hipMemset(ctl_, 0, 256), "hipMemset(ctl)");
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  }
   peers_[rank_] = slab_;
 }
 
@@ -451,7 +457,7 @@ XgmiComm::~XgmiComm() {
   for (int k = 0; k < world_; ++k)
     if (ipc_opened_[k] && peers_[k]) (void)hipIpcCloseMemHandle(peers_[k]);
   if (slab_ && own_slab_) (void)hipFree(slab_);
-  if (ctl_) (void)hipFree(ctl_);
+  if (ctl_ && own_ctl_) (void)hipFree(ctl_);
 }
 
 std::string XgmiComm::ipc_handle() const {

@@ -122,6 +122,8 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   std::memset(ring_, 0, ring_stride_ * 4 * o_.ring);
   hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&ring_dev_), ring_, 0), "hipHostGetDevicePointer(ring)");
   hip_check(hipMalloc(reinterpret_cast<void**>(&cnt_vram_), ring_stride_ * 4 * o_.ring), "hipMalloc(plane counts)");
+  hip_check(hipMalloc(reinterpret_cast<void**>(&ctl_mem_), 256), "hipMalloc(plane ctl)");
+  hip_check(hipMemset(ctl_mem_, 0, 256), "hipMemset(plane ctl)");
   hip_check(hipEventCreateWithFlags(&rel_ev_, hipEventDisableTiming), "hipEventCreate(release)");
   for (int i = 0; i < o_.ring; ++i) {
     hipEvent_t e = nullptr;
@@ -196,6 +198,7 @@ XgmiRoundPlane::~XgmiRoundPlane() {
   for (hipEvent_t e : events_) (void)hipEventDestroy(e);
   if (ring_) (void)hipHostFree(ring_);
   if (cnt_vram_) (void)hipFree(cnt_vram_);
+  if (ctl_mem_) (void)hipFree(ctl_mem_);
   if (hforce_) (void)hipHostFree(hforce_);
   if (stream_) (void)hipStreamDestroy(stream_);
   if (arena_) (void)hipFree(arena_);
@@ -325,8 +328,13 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
     bases[k] = k == cfg.id ? arena_ : map_peer(it->second);
   }
   comm_.reset();
+  // No device-synchronising call from here on: a peer's round kernel of the new epoch may
+  // already spin waiting for this worker (its lag gate opens on the progress published
+  // below). The communicator reuses the plane's arena and control words; the control words
+  // are reset stream-ordered, after the drained old epoch.
+  hip_check(hipMemsetAsync(ctl_mem_, 0, 256, stream_), "hipMemsetAsync(plane ctl)");
   comm_ = std::make_unique<XgmiComm>(cfg.id, P, o_.device, slot, o_.grid, o_.timeout_s, cfg.maxLag + 1, arena_,
-                                     arena_bytes_, flag_bytes_);
+                                     arena_bytes_, flag_bytes_, ctl_mem_);
   comm_->connect_ptrs(bases);
   comm_->set_phase_stamps(stamps_, stamp_slots_);
   // Every round of the previous epoch has finished here (drained): say so to the peers. Their

@@ -127,6 +127,7 @@ class XgmiRoundPlane final : public RoundPlane {
   // pinned ring: per slot P x nch counts + the error word
   int32_t* ring_ = nullptr;
   int32_t* ring_dev_ = nullptr;  // the ring's device-visible address
+  uint32_t* ctl_mem_ = nullptr;  // the communicator's control words, kept across epochs
   int32_t* cnt_vram_ = nullptr;  // per-slot counts the workgroups write (HBM); copied into the ring at round end
   size_t ring_stride_ = 0;  // int32 per slot
   std::vector<int> free_slots_;
