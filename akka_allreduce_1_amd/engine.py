@@ -154,8 +154,16 @@ class PlaneJob:
                 "workers": [self.system.plane_worker_state(w) for w in self.workers]}
 
     def shutdown(self) -> None:
+        """Stop the actors and destroy the planes NOW. A plane's destructor frees device
+        memory (hipFree synchronises the whole device); left to a later garbage collection it
+        could run while another job's round kernels spin on a worker whose thread is stuck in
+        that free - a deadlock until the kernels' deadline."""
+        import gc
+
         self.system.shutdown()
         self.planes = []
+        self.workers = []
+        gc.collect()
 
 
 def distributed_plane_job(n: int, source: Callable, *, max_chunk_size: int, dtype: torch.dtype, rounds: int,
