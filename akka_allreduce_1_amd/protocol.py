@@ -21,9 +21,12 @@ AllreduceFinished = C.AllreduceFinished
 PoisonPill = C.PoisonPill
 TextMessage = C.TextMessage
 ActorRef = C.ActorRef
+# extensions: the master's typed round deadline, and a plane's round completion (local only)
+RoundTimeout = C.RoundTimeout
+PlaneRoundDone = C.PlaneRoundDone
 
 __all__ = [
     "InitWorkers", "StartAllreduce", "ScatterBlock", "ReduceBlock", "CompleteAllreduce",
     "AllReduceInputRequest", "AllReduceInput", "AllReduceOutput", "MemberUp", "Terminated",
-    "AllreduceFinished", "PoisonPill", "TextMessage", "ActorRef",
+    "AllreduceFinished", "PoisonPill", "TextMessage", "ActorRef", "RoundTimeout", "PlaneRoundDone",
 ]

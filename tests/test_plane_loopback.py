@@ -264,3 +264,31 @@ def test_loopback_planes_are_independent_across_hubs():
     finally:
         for j in jobs:
             j.shutdown()
+
+
+def test_make_plane_worker_with_a_loopback_hub():
+    """actors.make_plane_worker builds the worker + plane; the master relays the descriptors
+    announced in MemberUp.meta."""
+    from akka_allreduce_1_amd.actors import make_master, make_plane_worker
+    from akka_allreduce_1_amd.protocol import MemberUp
+
+    n, P = 12, 3
+    system = C.ActorSystem("Api", False)
+    fin = threading.Event()
+    outs = [dict() for _ in range(P)]
+    try:
+        pairs = [make_plane_worker(system, host_iota_source(n, 1000.0 * k),
+                                   (lambda k: lambda o: outs[k].__setitem__(o.iteration, np.asarray(o.data).copy()))(k),
+                                   data_size=n, name=f"w{k}", hub="api-hub") for k in range(P)]
+        master = make_master(system, P, 1.0, 1.0, 1.0, 1, n, 5, 2, on_finished=lambda r: fin.set())
+        for w, plane in pairs:
+            master.tell(MemberUp(w, "worker", "", plane.descriptor), None)
+        assert fin.wait(30)
+        for p in (pl for _, pl in pairs):
+            p.drain()
+        for k in range(P):
+            np.testing.assert_array_equal(outs[k][5], expected(n, 5, range(P)).astype(F))
+        with pytest.raises(ValueError):
+            make_plane_worker(system, host_iota_source(n), data_size=n)
+    finally:
+        system.shutdown()
