@@ -142,7 +142,8 @@ void DevicePlane::wait_for(const Payload& p) {
 
 void DevicePlane::hold(const Payload& p) {
   auto* d = dynamic_cast<const DevicePayload*>(p.get());
-  if (!d || d->stream() == stream_) return;  // own memory is stream-ordered already
+  if (d && d->stream() == stream_) return;  // own memory is stream-ordered already
+  // host payloads too: an asynchronous H2D copy reads them after this call returns
   ReadyEvent e = record_ready(stream_);
   std::lock_guard<std::mutex> g(pending_mu_);
   pending_.emplace_back(p, std::move(e));
@@ -179,10 +180,11 @@ Payload DevicePlane::to_device(const Payload& p) {
       hold(p);
       d2d_bytes += n * sizeof(float);
     } else {
-      // pageable host source: synchronous w.r.t. the host buffer, ordered on our stream
+      // host payloads are immutable: keep this one alive until the stream has copied it
+      // instead of draining the stream (the old per-store hipStreamSynchronize)
       hip_check(hipMemcpyAsync(mem.get(), p->data(), n * sizeof(float), hipMemcpyHostToDevice, stream_),
                 "hipMemcpyAsync H2D");
-      hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+      hold(p);
       h2d_bytes += n * sizeof(float);
     }
   }
@@ -236,7 +238,7 @@ void DeviceSlab::store(const Payload& v, int physRow, int src, size_t offset) {
   } else {
     hip_check(hipMemcpyAsync(dst, v->data(), n * sizeof(float), hipMemcpyHostToDevice, plane_->stream()),
               "hipMemcpyAsync(store H2D)");
-    hip_check(hipStreamSynchronize(plane_->stream()), "hipStreamSynchronize");
+    plane_->hold(v);  // immutable host payload, alive until the copy ran (no stream drain)
     plane_->h2d_bytes += n * sizeof(float);
   }
 }
