@@ -1,0 +1,50 @@
+"""The examples run end to end (examples/README.md)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, timeout=240, env=None):
+    e = dict(os.environ, **(env or {}))
+    return subprocess.run([sys.executable] + args, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=e)
+
+
+@pytest.mark.parametrize("plane", ["host", "loopback"])
+def test_reference_demo(plane):
+    extra = ["--th-reduce", "1", "--th-complete", "1"] if plane == "loopback" else []
+    r = _run(["examples/reference_demo.py", "--plane", plane, "--rounds", "4"] + extra)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "finished" in r.stdout
+    if plane == "loopback":  # exact: worker k's data is i + round + 1000 k
+        assert "worker 0 round 3: [1006.0, 1008.0" in r.stdout, r.stdout
+
+
+def test_train_dp_two_ranks_on_gloo():
+    from akka_allreduce_1_amd.parallel.comm import free_port
+
+    r = _run(["-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+              "--master-port", str(free_port()), "examples/train_dp.py", "--cpu", "--steps", "20", "--width", "64"],
+             timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "replica max diff 0" in r.stdout, r.stdout
+
+
+@pytest.mark.gpu
+def test_reference_demo_on_the_gpu_round_engine():
+    r = _run(["examples/reference_demo.py", "--plane", "gpu", "--rounds", "4", "--th-reduce", "1", "--th-complete", "1"])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "worker 1 round 3: [1006.0, 1008.0" in r.stdout, r.stdout
+
+
+@pytest.mark.gpu
+def test_train_dp_one_gpu():
+    from akka_allreduce_1_amd.parallel.comm import free_port
+
+    r = _run(["-m", "torch.distributed.run", "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
+              "--master-port", str(free_port()), "examples/train_dp.py", "--steps", "30"], timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "replica max diff 0" in r.stdout, r.stdout
