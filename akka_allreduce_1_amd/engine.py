@@ -70,7 +70,7 @@ class PlaneJob:
                  sources: Sequence[Callable] | None = None, keep_outputs: bool = True, round_timeout_ms: int = 0,
                  timeout_s: float = 60.0, order_ref: bool = True, on_output: Callable | None = None,
                  max_peers: int | None = None, high_priority: bool = True, order_release: bool = True,
-                 plane: str = "xgmi", hub: str | None = None, spin_us: int = 1000):
+                 plane: str = "xgmi", hub: str | None = None, spin_us: int = 1000, reinit_on_loss: bool = False):
         """plane: "xgmi" (one threshold-kernel launch per round on the GPUs in `devices`) or
         "loopback" (host memory, no GPU: csrc/runtime/loopback_plane.h; `hub` names the
         workers' shared hub, default a fresh one; dtype float32, devices ignored)."""
@@ -120,7 +120,8 @@ class PlaneJob:
 
         self.master = self.system.master(P, th_allreduce, th_reduce, th_complete, max_lag, data_size, max_round,
                                          max_chunk_size, on_finished=fin, roundTimeoutMs=round_timeout_ms,
-                                         on_round=lambda r, e: self.stamps.append(time.perf_counter()))
+                                         on_round=lambda r, e: self.stamps.append(time.perf_counter()),
+                                         reinitOnLoss=reinit_on_loss)
         self.workers = [self.system.plane_worker(self.sources[k], self._sink(k), self.planes[k], f"worker{k}")
                         for k in range(P)]
 

@@ -499,9 +499,9 @@ PYBIND11_MODULE(_C, m) {
       .def("master", [](ActorSystem& s, int totalWorkers, float thAllreduce, float thReduce, float thComplete,
                         int maxLag, int dataSize, int maxRound, int maxChunkSize, bool liveBarrier,
                         py::object on_finished, std::string name, int startRound, py::object on_round,
-                        int roundTimeoutMs) {
+                        int roundTimeoutMs, bool reinitOnLoss) {
             MasterParams p{totalWorkers, thAllreduce, thReduce, thComplete, maxLag, dataSize, maxRound,
-                           maxChunkSize, liveBarrier, startRound, roundTimeoutMs};
+                           maxChunkSize, liveBarrier, startRound, roundTimeoutMs, reinitOnLoss};
             MasterActor::RoundCallback rcb;
             if (!on_round.is_none()) {
               auto h = std::make_shared<PyCallable>(std::move(on_round));
@@ -522,7 +522,8 @@ PYBIND11_MODULE(_C, m) {
           }, py::arg("totalWorkers"), py::arg("thAllreduce"), py::arg("thReduce"), py::arg("thComplete"),
           py::arg("maxLag"), py::arg("dataSize"), py::arg("maxRound"), py::arg("maxChunkSize"),
           py::arg("liveBarrier") = false, py::arg("on_finished") = py::none(), py::arg("name") = "master",
-          py::arg("startRound") = 0, py::arg("on_round") = py::none(), py::arg("roundTimeoutMs") = 0)
+          py::arg("startRound") = 0, py::arg("on_round") = py::none(), py::arg("roundTimeoutMs") = 0,
+          py::arg("reinitOnLoss") = false)
       .def("plane_worker", [](ActorSystem& s, py::object source, py::object sink, std::shared_ptr<RoundPlane> plane,
                               std::string name) {
             auto a = std::make_unique<PlaneWorkerActor>(make_plane_source(std::move(source)),
@@ -622,6 +623,7 @@ PYBIND11_MODULE(_C, m) {
         d["rounds_started"] = c.stats().rounds_started;
         d["stale_completes"] = c.stats().stale_completes;
         d["round_timeouts"] = c.stats().round_timeouts;
+        d["loss_reinits"] = c.stats().loss_reinits;
         return d;
       });
 

@@ -29,13 +29,25 @@ void MasterCore::on_member_up(int handle) {
 
 // Terminated (AllreduceMaster.scala:50-56)
 void MasterCore::on_terminated(int handle) {
+  bool removed = false;
   for (auto it = workers_.begin(); it != workers_.end(); ++it) {
     if (it->second == handle) {
       MXAR_LOG(INFO, "master", "----worker " << it->first << " is terminated, removing it from the set");
       workers_.erase(it);
       stats_.removed++;
+      removed = true;
       break;
     }
+  }
+  if (removed && p_.reinitOnLoss && round_ >= 0 && !finished_ && !workers_.empty()) {
+    // the survivors become a new epoch that resumes at the current round (its partial
+    // completions belong to the old epoch and are discarded)
+    MXAR_LOG(WARNING, "master", "----re-initialising the " << workers_.size() << " surviving workers at round "
+                                                             << round_);
+    stats_.loss_reinits++;
+    init_workers(round_);
+    start_allreduce();
+    return;
   }
   // With liveBarrier the round may now be complete.
   if (p_.liveBarrier && round_ >= 0 && !finished_ &&
@@ -45,7 +57,8 @@ void MasterCore::on_terminated(int handle) {
 }
 
 float MasterCore::barrier_base() const {
-  if (p_.liveBarrier) return static_cast<float>(std::min<int>(p_.totalWorkers, static_cast<int>(workers_.size())));
+  if (p_.liveBarrier || p_.reinitOnLoss)
+    return static_cast<float>(std::min<int>(p_.totalWorkers, static_cast<int>(workers_.size())));
   return static_cast<float>(p_.totalWorkers);
 }
 
@@ -98,7 +111,7 @@ void MasterCore::on_round_timeout(int64_t epoch, int round) {
 }
 
 // init_workers (AllreduceMaster.scala:84-89)
-void MasterCore::init_workers() {
+void MasterCore::init_workers(int startRound) {
   // re-number densely 0..P-1 in id order
   std::map<int, int> dense;
   int k = 0;
@@ -106,7 +119,7 @@ void MasterCore::init_workers() {
   workers_.swap(dense);
   if (epoch_ > 0)  // skip past every device round epoch the previous membership epoch could use
     round_base_ += static_cast<uint32_t>(std::max(0, round_ - epoch_start_round_ + 1)) + 1u;
-  epoch_start_round_ = std::max(0, p_.startRound);
+  epoch_start_round_ = startRound;
   ++epoch_;
   stats_.inits++;
   for (auto& [idx, h] : workers_) {
@@ -120,7 +133,7 @@ void MasterCore::init_workers() {
     p.dataSize = p_.dataSize;
     p.maxChunkSize = p_.maxChunkSize;
     p.epoch = epoch_;
-    p.startRound = std::max(0, p_.startRound);
+    p.startRound = startRound;
     p.roundBase = round_base_;
     fx_->send_init(h, p, workers_);
   }

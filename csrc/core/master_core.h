@@ -13,6 +13,8 @@
 // after maxRound (Q15).
 #pragma once
 
+#include <algorithm>
+
 #include <functional>
 #include <map>
 #include <vector>
@@ -33,6 +35,11 @@ struct MasterParams {
   bool liveBarrier = false;
   int startRound = 0;  // resume point (checkpoint/resume)
   int roundTimeoutMs = 0;  // > 0: advance a round that misses the barrier this long
+  // Extension: when a registered worker terminates, re-initialise the
+  // survivors as a new membership epoch that resumes at the current round, and count the
+  // barrier over live workers. The reference only re-initialises on MemberUp, so a lost
+  // worker leaves its peers waiting on rounds that can never complete (Q4).
+  bool reinitOnLoss = false;
 };
 
 class MasterEffects {
@@ -49,7 +56,8 @@ class MasterEffects {
 };
 
 struct MasterStats {
-  uint64_t inits = 0, rounds_started = 0, completes = 0, stale_completes = 0, removed = 0, round_timeouts = 0;
+  uint64_t inits = 0, rounds_started = 0, completes = 0, stale_completes = 0, removed = 0, round_timeouts = 0,
+           loss_reinits = 0;
 };
 
 class MasterCore {
@@ -72,7 +80,8 @@ class MasterCore {
   const MasterStats& stats() const { return stats_; }
 
  private:
-  void init_workers();
+  void init_workers() { init_workers(std::max(0, p_.startRound)); }
+  void init_workers(int startRound);
   void start_allreduce();
   void advance();
   float barrier_base() const;

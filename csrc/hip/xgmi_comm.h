@@ -138,6 +138,7 @@ class XgmiComm {
     bool cold = false;
     bool order_ref = false;
     const uint32_t* host_force = nullptr;  // device-visible pinned host word (may be null)
+    const uint32_t* host_abort = nullptr;  // rounds <= this epoch are abandoned (may be null)
     uint32_t* err_out = nullptr;           // device-visible word the round's error word is copied to
     int32_t* counts_host = nullptr;        // device-visible pinned copy of `counts`, written at round end
   };

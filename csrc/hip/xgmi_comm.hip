@@ -921,6 +921,7 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
     a.cold = spec->cold ? 1 : 0;
     a.order_ref = spec->order_ref ? 1 : 0;
     a.hforce = spec->host_force;
+    a.habort = spec->host_abort;
     a.err_out = spec->err_out;
     a.counts_host = counts != nullptr ? spec->counts_host : nullptr;
   }

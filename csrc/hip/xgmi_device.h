@@ -50,6 +50,7 @@ struct CommArgs {
   int cold;
   int order_ref;
   const uint32_t* hforce;
+  const uint32_t* habort;  // pinned host word: rounds <= this epoch are abandoned (threshold kernel)
   uint32_t* err_out;  // optional: the round's error word, written by the last workgroup (pinned host)
   // optional: where the last workgroup copies `counts` (P x nch int32, pinned host) once the
   // round is done - every workgroup writes its counts to device memory (`counts`), so no

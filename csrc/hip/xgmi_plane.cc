@@ -170,7 +170,7 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
 XgmiRoundPlane::~XgmiRoundPlane() {
   *alive_ = false;
   try {
-    force(0x7fffffff);
+    abort(0x7fffffff);
     drain();
   } catch (...) {
   }
@@ -294,9 +294,11 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
   if (cfg.maxChunkSize <= 0) throw ProtocolError("maxChunkSize must be > 0");
   if (static_cast<int>(cfg.descriptors.size()) != cfg.peers)
     throw ProtocolError("InitWorkers.planes must hold one descriptor per worker");
-  // the previous epoch's rounds finish (forced) before the arena is laid out again
+  // the previous epoch's rounds are abandoned before the arena is laid out again (their
+  // results would be dropped as an older epoch; a round still at its lag gate must not
+  // wait for a peer that left the membership)
   if (configured_) {
-    force(last_round_);
+    abort(last_round_);
     drain();
   }
   hip_check(hipSetDevice(o_.device), "hipSetDevice");
@@ -420,6 +422,7 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   spec.cold = cold;
   spec.order_ref = o_.order_ref;
   spec.host_force = hforce_dev_;
+  spec.host_abort = hforce_dev_ + 1;
   spec.err_out = reinterpret_cast<uint32_t*>(slot_dev + ring_stride_ - 1);
   spec.counts_host = slot_dev;  // the kernel counts into HBM and copies once, at round end
   int32_t* cnt_dev = cnt_vram_ + static_cast<size_t>(rec.slot) * ring_stride_;
@@ -458,6 +461,15 @@ void XgmiRoundPlane::force(int round) {
     *w = e;  // the kernel polls it (system-scope loads of coherent pinned memory)
     st_.forced++;
   }
+}
+
+void XgmiRoundPlane::abort(int round) {
+  force(round);
+  if (!configured_ || round < cfg_.startRound) return;
+  const int r = std::min(round, std::max(last_round_, cfg_.startRound));
+  const uint32_t e = epoch_of(r);
+  volatile uint32_t* w = hforce_ + 1;
+  if (static_cast<int32_t>(e - *w) > 0) *w = e;  // the kernel polls it at its lag gate
 }
 
 void XgmiRoundPlane::drain() {

@@ -69,6 +69,7 @@ class XgmiRoundPlane final : public RoundPlane {
   void configure(const PlaneConfig& cfg) override;
   void launch(int round, const Payload& input, bool cold) override;
   void force(int round) override;
+  void abort(int round) override;
   void drain() override;
   int chunks() const override { return nch_; }
 
@@ -114,8 +115,8 @@ class XgmiRoundPlane final : public RoundPlane {
   int64_t flag_bytes_ = 0;  // flag table reserved at its largest size (every layout the same)
   uint64_t arena_id_ = 0;
   std::string desc_;
-  uint32_t* hforce_ = nullptr;      // pinned host word the engine raises (force)
-  uint32_t* hforce_dev_ = nullptr;  // its device-visible address
+  uint32_t* hforce_ = nullptr;      // pinned host words the engine raises: [0] force, [1] abort
+  uint32_t* hforce_dev_ = nullptr;  // their device-visible address
   hipStream_t stream_ = nullptr;
   std::unique_ptr<XgmiComm> comm_;
   std::map<std::string, char*> mapped_;  // peer IPC handle -> mapping (kept across epochs)

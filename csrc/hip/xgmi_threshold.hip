@@ -73,6 +73,9 @@ __device__ __forceinline__ bool wave_forced(const CommArgs& a, int r, uint32_t e
   if (host && s == 63 && a.hforce != nullptr)
     f = reached(__hip_atomic_load(const_cast<uint32_t*>(a.hforce), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
                 epoch);
+  if (host && s == 62 && a.habort != nullptr)  // an abandoned round is forced too
+    f = reached(__hip_atomic_load(const_cast<uint32_t*>(a.habort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                epoch);
   return __any(f);
 }
 
@@ -347,13 +350,15 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   // (progress words live in OUR slab, written by the peers at the end of each round). A
   // peer that is not there yet gets a FORCE request: it completes that round with what
   // has arrived instead of waiting (catch-up), so this wait ends as soon as the laggard
-  // runs. Only a laggard that never runs again (a dead process) turns into ERR_TIMEOUT_LAG.
+  // runs. Only a laggard that never runs again (a dead process) turns into ERR_TIMEOUT_LAG -
+  // unless the engine abandons the round meanwhile (host abort word: re-initialisation or
+  // shutdown): an abandoned round that has not passed its gate writes nothing anywhere.
   if (threadIdx.x < 64) {
     const int k = static_cast<int>(threadIdx.x);
     const uint32_t target = epoch - static_cast<uint32_t>(a.trows);
     const uint32_t* f = (k < P && k != r) ? prog(a, r, k) : nullptr;
     bool ok = f == nullptr || reached(ld_flag(f), target);
-    bool asked = false;
+    bool asked = false, aborted = false;
     while (!__all(ok)) {
       if (!ok && !asked && blockIdx.x == 0) {
         st_flag(forcew(a, k, r), target);
@@ -361,19 +366,30 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
       }
       __builtin_amdgcn_s_sleep(2);
       if (!ok) ok = reached(ld_flag(f), target);
+      if (a.habort != nullptr && hp.due()) {
+        const bool ab = k == 0 && reached(__hip_atomic_load(const_cast<uint32_t*>(a.habort), __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_SYSTEM),
+                                          epoch);
+        if (__any(ab)) {
+          aborted = true;
+          break;
+        }
+      }
       if (wall_ticks() > deadline) {
         if (k == 0) __hip_atomic_fetch_or(err, ERR_TIMEOUT_LAG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
     }
+    if (k == 0) sh_flag = aborted ? 1 : 0;
     if (acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  const bool void_round = sh_flag != 0;  // abandoned before the exchange: no peer writes
   ps.mark(1);
 
-  // Phase 1 - ScatterBlock into the owners' row slots (a cold round sends nothing)
-  if (!cold) {
+  // Phase 1 - ScatterBlock into the owners' row slots (a cold or void round sends nothing)
+  if (!cold && !void_round) {
     for (int u = blockIdx.x; u < nu; u += G) {
       const int c = u / Pm1;
       const int j = (r + 1 + u % Pm1) % P;
@@ -396,6 +412,11 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   for (int c = blockIdx.x; c < a.nch; c += G, ++kk) {
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     const int64_t len = clamp_len(blen_own - cstart, a.chunk);
+    if (void_round) {  // nothing reduced, nothing sent
+      if (len > 0) zero_fill<E>(out + (bstart_own + cstart) * es, len);
+      if (threadIdx.x == 0 && counts) counts[static_cast<int64_t>(r) * a.nch + c] = 0;
+      continue;
+    }
     if (threadIdx.x < 64) {
       const int s = static_cast<int>(threadIdx.x);
       const uint32_t* f = (s < P && s != r) ? f1(a, r, row * P + s, c) : nullptr;
@@ -563,7 +584,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
                    : 0;
       else
         give = done >= static_cast<uint32_t>(a.min_complete) ? 1 : 0;
-      if (!give && (cold || wave_forced(a, r, epoch, hp.due()))) give = 1;
+      if (!give && (cold || void_round || wave_forced(a, r, epoch, hp.due()))) give = 1;
       if (!give && wall_ticks() > deadline) {
         if (threadIdx.x == 0)
           __hip_atomic_fetch_or(err, ERR_TIMEOUT_REDUCE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

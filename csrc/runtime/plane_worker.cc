@@ -13,9 +13,9 @@ PlaneWorkerActor::PlaneWorkerActor(DataSource source, DataSink sink, std::shared
 }
 
 PlaneWorkerActor::~PlaneWorkerActor() {
-  // rounds still in flight complete (forced) before the plane may call back into nothing
+  // rounds still in flight are abandoned before the plane may call back into nothing
   try {
-    plane_->force(0x7fffffff);
+    plane_->abort(0x7fffffff);
     plane_->drain();
   } catch (const std::exception& e) {
     MXAR_LOG(ERROR, "worker", "----plane drain at shutdown failed: " << e.what());

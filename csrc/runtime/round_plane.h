@@ -70,6 +70,10 @@ class RoundPlane {
   virtual void launch(int round, const Payload& input, bool cold) = 0;
   // Rounds <= `round` stop waiting and complete with what has arrived.
   virtual void force(int round) = 0;
+  // Rounds <= `round` are abandoned (re-initialisation, shutdown): like force(), and a
+  // round that has not started exchanging yet delivers nothing instead of waiting for a
+  // peer that may never come back (its result is dropped as an older epoch anyway).
+  virtual void abort(int round) { force(round); }
   // Block until every launched round has completed (and its done callback ran).
   virtual void drain() = 0;
   // Chunks per block of the current configuration (AllReduceOutput.count has peers x this).

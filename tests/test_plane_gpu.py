@@ -361,3 +361,45 @@ def test_cli_master_and_gpu_worker_processes(tmp_path, P, n, chunk):
                 p.kill()
         for f in wout + werr:
             f.close()
+
+
+def test_worker_loss_reinitialises_the_survivors():
+    """A plane worker dies mid-job (its actor stops; its plane abandons its rounds). With
+    reinitOnLoss the master re-initialises the two survivors at the current round: their
+    planes abandon the old epoch's rounds (a round still at its lag gate, waiting for the
+    lost worker, delivers nothing instead of waiting out the kernel deadline), lay the
+    arena out for P = 2 and finish every round exactly."""
+    P, n, chunk, rounds, victim = 3, 3000, 250, 30, 2
+    started = __import__("threading").Event()
+
+    def slow(k):
+        base = iota_source(n, DEV, torch.float32, 1000.0 * k)
+
+        def f(req):
+            time.sleep(0.01)
+            if req.iteration >= 5:
+                started.set()
+            return base(req)
+        return f
+
+    job = PlaneJob(P, n, max_chunk_size=chunk, max_round=rounds - 1, sources=[slow(k) for k in range(P)],
+                   timeout_s=20.0, reinit_on_loss=True)
+    try:
+        t0 = time.time()
+        job.start()
+        assert started.wait(30)
+        job.workers[victim].tell(C.PoisonPill(), None)
+        assert job.finished.wait(60), job.state()
+        assert time.time() - t0 < 20, "a round waited for the lost worker until its kernel deadline"
+        for p in job.planes[:2]:
+            p.drain()
+        st = job.system.master_state(job.master)
+        assert st["loss_reinits"] == 1 and st["numWorkers"] == 2, st
+        for k in (0, 1):
+            w = job.system.plane_worker_state(job.workers[k])
+            assert w["stats"]["plane_errors"] == 0, w
+            data, counts = job.outputs[k][rounds - 1]
+            np.testing.assert_array_equal(data.cpu().numpy(), expected(n, rounds - 1, (0, 1)))
+            assert all(c == 2 for c in counts), counts
+    finally:
+        job.shutdown()
