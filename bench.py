@@ -787,25 +787,20 @@ def main() -> None:
         # other ranks' GEMMs (8 ranks: 953 ms per overlapped ResNet-50 step vs 5.9 ms compute +
         # 0.8 ms comm), which says nothing about one GPU per rank. A watchdog keeps a stuck
         # section from costing the result line.
-        def give_up() -> None:
-            # the result line is written exactly once (emit's lock + flag); the explicit
-            # status says the dp section did not finish, the process exits at once because
-            # a persistent kernel of the stuck section may still spin
-            result["dp"] = {"error": f"timed out after {args.dp_timeout:g} s"}
-            result["status"] = "dp_timeout"
-            if emit(rank, result):
-                os._exit(0)
+        # The watchdog is native: it writes the prepared line (explicit status "dp_timeout")
+        # and exits even while this thread is blocked in a C call holding the GIL - a
+        # Python Timer could not run then (seen in the 8-process one-GPU rehearsal). It
+        # exits at once because a persistent kernel of the stuck section may still spin.
+        from akka_allreduce_1_amd._native import C
 
-        dog = threading.Timer(args.dp_timeout, give_up)
-        dog.daemon = True
-        dog.start()
+        timed_out = dict(result, dp={"error": f"timed out after {args.dp_timeout:g} s"}, status="dp_timeout")
+        sys.stdout.flush()
+        cancel = C.watchdog_arm(args.dp_timeout, _RESULT_FD if rank == 0 else -1, json.dumps(timed_out) + "\n", 0)
         log(rank, "dp: ResNet-50 / Llama-3-8B data-parallel steps")
         dp = {m: dp_step(comm, m, dev) for m in (("resnet50",) if args.share_device else ("resnet50", "llama3_8b"))}
-        dog.cancel()
-        with _EMIT_LOCK:
-            if _EMITTED[0]:  # the watchdog won the race and has already written the line
-                return
-            result["dp"] = dp
+        if not cancel():  # the watchdog fired and wrote the line; the process is exiting
+            return
+        result["dp"] = dp
 
     emit(rank, result)
     dist.barrier()

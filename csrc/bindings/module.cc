@@ -6,6 +6,11 @@
 #include <pybind11/stl.h>
 
 #include <chrono>
+#include <mutex>
+#include <atomic>
+#include <condition_variable>
+#include <thread>
+#include <unistd.h>
 #include <optional>
 #include <sstream>
 
@@ -686,6 +691,46 @@ PYBIND11_MODULE(_C, m) {
         "RoundPlane in host memory (csrc/runtime/loopback_plane.h): the round engine's semantics for the "
         "workers of one process, no GPU; every worker of a job names the same hub");
   m.def("host_plane", [] { return std::static_pointer_cast<DataPlane>(HostPlane::instance()); });
+  // A process watchdog that needs no GIL (bench.py's dp section): a Python Timer cannot run
+  // while the main thread blocks inside a C call holding the GIL (e.g. a kernel launch into a
+  // full hardware queue behind a spinning kernel). Returns cancel() -> True if it disarmed
+  // the watchdog, False if it had already fired.
+  m.def(
+      "watchdog_arm",
+      [](double seconds, int fd, std::string line, int code) {
+        auto state = std::make_shared<std::atomic<int>>(0);  // 0 armed, 1 cancelled, 2 fired
+        auto mu = std::make_shared<std::mutex>();
+        auto cv = std::make_shared<std::condition_variable>();
+        std::thread([state, mu, cv, seconds, fd, line, code] {
+          {
+            std::unique_lock<std::mutex> lk(*mu);
+            cv->wait_for(lk, std::chrono::duration<double>(seconds), [&] { return state->load() != 0; });
+          }
+          int armed = 0;
+          if (!state->compare_exchange_strong(armed, 2)) return;
+          if (fd >= 0 && !line.empty()) {
+            const char* p = line.data();
+            size_t left = line.size();
+            while (left > 0) {
+              const ssize_t w = ::write(fd, p, left);
+              if (w <= 0) break;
+              p += w;
+              left -= static_cast<size_t>(w);
+            }
+          }
+          ::_exit(code);
+        }).detach();
+        return py::cpp_function([state, mu, cv] {
+          int armed = 0;
+          const bool won = state->compare_exchange_strong(armed, 1);
+          {
+            std::lock_guard<std::mutex> g(*mu);
+          }
+          cv->notify_all();
+          return won;
+        });
+      },
+      py::arg("seconds"), py::arg("fd"), py::arg("line"), py::arg("code") = 0);
 
   bind_cluster(m);
   bind_hip(m);

@@ -116,3 +116,28 @@ def test_logger_levels_vocabulary_and_trace_only_payloads():
     assert len(trace) > len(info)
 
     assert _collect_logs("OFF") == []
+
+
+def test_native_watchdog_fires_without_the_gil_and_can_be_cancelled():
+    """bench.py's dp watchdog: the line is written and the process exits even while the main
+    thread holds the GIL in a blocking call (time.sleep in C would release it; a busy loop in
+    a C extension would not - here the main thread spins in pure Python while the native
+    thread fires); cancel() before the deadline disarms it."""
+    import subprocess
+    import sys
+
+    code = ("from akka_allreduce_1_amd._native import C\n"
+            "import time\n"
+            "C.watchdog_arm(0.3, 1, 'FIRED\\n', 3)\n"
+            "t = time.time()\n"
+            "while time.time() - t < 10: pass\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3 and "FIRED" in r.stdout, (r.returncode, r.stdout, r.stderr[-500:])
+    code2 = ("from akka_allreduce_1_amd._native import C\n"
+             "import time\n"
+             "cancel = C.watchdog_arm(0.5, 1, 'FIRED\\n', 3)\n"
+             "assert cancel() is True\n"
+             "time.sleep(1.0)\n"
+             "print('survived')\n")
+    r = subprocess.run([sys.executable, "-c", code2], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "survived" in r.stdout and "FIRED" not in r.stdout, (r.stdout, r.stderr[-500:])
