@@ -169,6 +169,8 @@ def worker_main(argv: list[str] | None = None) -> int:
                     help="run the worker on this GPU: an xGMI round plane (one kernel launch per round, peers' "
                          "HBM mapped over IPC; csrc/hip/xgmi_plane.h) instead of ScatterBlock/ReduceBlock messages")
     ap.add_argument("--dtype", choices=["fp32", "bf16", "fp16"], default=None, help="GPU worker element type")
+    ap.add_argument("--source-delay-ms", type=float, default=0.0,
+                    help="sleep this long in the data source every round (demos / failure tests: slow rounds)")
     _common(ap)
     args = ap.parse_args(argv)
     cfg = _load(args)
@@ -192,6 +194,8 @@ def worker_main(argv: list[str] | None = None) -> int:
         base = np.arange(n, dtype=np.float32)
 
         def source(req):  # createDataSource: data[i] = i + iteration (AllreduceWorker.scala:285-291)
+            if args.source_delay_ms > 0:
+                time.sleep(args.source_delay_ms / 1e3)
             return C.AllReduceInput(base + np.float32(req.iteration))
 
         wref = system.worker(source, sink, "worker")

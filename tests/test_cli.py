@@ -4,6 +4,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -102,3 +103,44 @@ def test_native_master_and_two_workers(tmp_path):
         assert sorted(sums) == list(range(16)), out
         for r, v in sums.items():  # data[i] = i + r on both workers: sum 2 * (66 + 12 r)
             assert v == 2 * (66 + 12 * r), (r, v)
+
+
+@pytest.mark.slow
+def test_worker_process_killed_survivors_reinitialised(tmp_path):
+    """The reference's deployment over TCP, and one worker PROCESS is killed mid-job. The
+    failure detector marks it unreachable and auto-downs it; the master's remote DeathWatch
+    fires. With mxar.allreduce.reinit-on-loss the master re-initialises the two survivors
+    at the current round, and they finish every round with sums of exactly two workers."""
+    port = free_port()
+    seed = ["--set", f"mxar.cluster.seed-nodes=mxar.tcp://ClusterSystem@127.0.0.1:{port}"]
+    conf = ["--set", "mxar.allreduce.th-reduce=1.0", "--set", "mxar.allreduce.th-complete=1.0",
+            "--set", "mxar.allreduce.max-round=120", "--set", "mxar.allreduce.reinit-on-loss=true"]
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    py = [sys.executable, "-m", "akka_allreduce_1_amd"]
+    master = subprocess.Popen(py + ["master", str(port), "3", "10", "2"] + seed + conf + FAST, env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    outs = [open(tmp_path / f"w{i}.out", "w") for i in range(3)]
+    workers = [subprocess.Popen(py + ["worker", "0", "10", "--print-outputs", "--source-delay-ms", "20"] + seed + FAST,
+                                env=env, stdout=outs[i], stderr=subprocess.DEVNULL, text=True) for i in range(3)]
+    try:
+        t0 = time.time()
+        while time.time() - t0 < 30:  # wait until rounds are flowing
+            if sum(1 for _ in open(tmp_path / "w0.out")) >= 10:
+                break
+            time.sleep(0.1)
+        workers[2].kill()
+        mout, merr = master.communicate(timeout=90)
+        assert master.returncode == 0, merr[-3000:]
+        assert "finished 121 rounds" in mout, mout + merr[-3000:]
+        for i in (0, 1):
+            workers[i].wait(timeout=30)
+            rows = [json.loads(l) for l in open(tmp_path / f"w{i}.out") if l.startswith("{")]
+            got = {r["iteration"]: r["data"] for r in rows}
+            np.testing.assert_array_equal(got[120], 2 * (np.arange(10) + 120))  # the two survivors
+            np.testing.assert_array_equal(got[0], 3 * np.arange(10))            # all three before the loss
+    finally:
+        for p in [master] + workers:
+            if p.poll() is None:
+                p.kill()
+        for f in outs:
+            f.close()
