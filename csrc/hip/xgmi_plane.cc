@@ -228,7 +228,10 @@ std::shared_ptr<void> XgmiRoundPlane::buffer(size_t bytes, bool user_visible) {
       }
       (void)hipFreeAsync(q, s);
     } else {
-      (void)hipFree(q);
+      // the plane is gone: stream-ordered on the default stream - hipFree would wait for
+      // every kernel on the device, e.g. another plane's round spinning on its peers
+      // (profiles/round2/sync_probe.md)
+      (void)hipFreeAsync(q, nullptr);
     }
   });
 }
