@@ -426,7 +426,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
       uint32_t mask = 0;
       const bool use_snap = snap && kk < kMaxSnapChunks;
       const uint32_t s0c = use_snap ? s0[kk] : present;
-      if (snap && __popc(s0c) >= a.min_reduce) {
+      if (snap && static_cast<int>(__popc(s0c)) >= a.min_reduce) {
         mask = first_k(s0c, a.min_reduce, r + 1, P);  // fired while draining the queue: no own
       } else {
         mask = (snap ? s0c : 0u) | own;
@@ -434,11 +434,12 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
         while (!forced) {
           const uint32_t fresh = present & ~mask;
           if (snap) {
-            if (fresh && __popc(mask) < a.min_reduce) mask |= first_k(fresh, a.min_reduce - __popc(mask), r + 1, P);
+            if (fresh && static_cast<int>(__popc(mask)) < a.min_reduce)
+              mask |= first_k(fresh, a.min_reduce - static_cast<int>(__popc(mask)), r + 1, P);
           } else {
             mask |= fresh;  // greedy: everything present
           }
-          if (__popc(mask) >= a.min_reduce || (mask | own) == (own | others)) break;
+          if (static_cast<int>(__popc(mask)) >= a.min_reduce || (mask | own) == (own | others)) break;
           if (wave_forced(a, r, epoch, hp.due())) {
             forced = true;
             break;
