@@ -273,6 +273,7 @@ class XgmiComm {
   bool connected_ = false;
   bool own_slab_ = true;           // false: laid out over a caller's arena
   bool own_ctl_ = true;            // false: control words owned by the caller
+  bool dynamic_ = false;           // two-shot units from a counter (MXAR_TWOSHOT_DYNAMIC)
   bool launched_ = false;          // a launch has been enqueued (last_stream_ valid)
   hipStream_t last_stream_ = nullptr;
   hipEvent_t switch_ev_ = nullptr;  // recorded on last_stream_ when the stream changes

@@ -72,10 +72,23 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
   // (thReduce = 1), then ReduceBlock-broadcast the sum into every rank's R slot. A chunk
   // is reduced in `sub` pieces by different workgroups so that phase 2 has as many
   // units as phases 1 and 3 (each piece pays one acquire and one release).
+  // `dynamic`: units are taken in order from a per-rank counter instead of the static
+  // blockIdx stride, so a workgroup whose units' contributions arrive late does not hold
+  // back units another workgroup could already reduce (the counters are reset by the
+  // last workgroup of the launch).
   const int64_t bstart_own = static_cast<int64_t>(r) * a.block;
   const int64_t blen_own = clamp_len(a.n - bstart_own, a.block);
   const int nu2 = a.nch * a.sub;
-  for (int u = blockIdx.x; u < nu2; u += G) {
+  __shared__ int next_unit;
+  auto take = [&](int slot, int u_static) -> int {
+    if (!a.dynamic) return u_static;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      next_unit = static_cast<int>(__hip_atomic_fetch_add(&ctl[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    __syncthreads();
+    return next_unit;
+  };
+  for (int u = take(8, blockIdx.x), k2 = 1; u < nu2; u = take(8, blockIdx.x + k2 * G), ++k2) {
     const int c = u / a.sub;
     const int q = u % a.sub;
     const int64_t cbeg = static_cast<int64_t>(c) * a.chunk;
@@ -101,7 +114,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
 
   ps.mark(3);
   // Phase 3 - complete: gather the other owners' reduced chunks into the output.
-  for (int u = blockIdx.x; u < nu; u += G) {
+  for (int u = take(9, blockIdx.x), k3 = 1; u < nu; u = take(9, blockIdx.x + k3 * G), ++k3) {
     const int c = u / Pm1;
     const int j = (r + 1 + u % Pm1) % P;
     const int64_t bstart = static_cast<int64_t>(j) * a.block;
@@ -117,6 +130,17 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
   }
   ps.mark(5);
   ps.flush();
+  if (a.dynamic) {  // the last workgroup resets the unit counters for the next launch
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t t = __hip_atomic_fetch_add(&ctl[10], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == gridDim.x - 1) {
+        __hip_atomic_store(&ctl[8], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctl[9], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctl[10], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
   finish_launch(ctl, epoch);
 }
 
@@ -410,6 +434,7 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   if (const char* f = std::getenv("MXAR_FENCE")) fence_ = std::atoi(f) & 3;
   if (const char* u = std::getenv("MXAR_TWOSHOT_UNITS")) units_per_wg_ = std::max(1, std::atoi(u));
   if (const char* u = std::getenv("MXAR_TWOSHOT_SUB")) sub_max_ = std::max(1, std::atoi(u));
+  if (const char* d = std::getenv("MXAR_TWOSHOT_DYNAMIC")) dynamic_ = std::atoi(d) != 0;
 
   hip_check(hipSetDevice(device_), "hipSetDevice");
   const char* mem = std::getenv("MXAR_SLAB_MEM");
@@ -670,6 +695,7 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   }
   a.fence = c0.fence_;
   a.scale = scale;
+  a.dynamic = c0.dynamic_ ? 1 : 0;
   a.stamps = c0.stamps_;
   if (a.stamps != nullptr && gx * ranks_here > c0.stamp_slots_) a.stamps = nullptr;  // buffer too small: off
   if (kind != Algo::LL && (static_cast<int64_t>(a.nch) * a.sub > c0.maxch_ || a.block * es > c0.slot_bytes_ + 16))

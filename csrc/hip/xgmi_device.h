@@ -68,6 +68,7 @@ struct CommArgs {
   uint64_t* stamps;
   uint64_t delay;      // test knob: ticks rank `delay_rank` idles before phase 1
   int delay_rank;
+  int dynamic;  // two-shot: workgroups take reduce / gather units from a counter (ctl[8], ctl[9])
 };
 
 // Phase stamps of one workgroup (100 MHz s_memrealtime ticks): [0] start, [1] scatter done,
