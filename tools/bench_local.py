@@ -61,7 +61,8 @@ def main() -> None:
     for P in args.ranks:
         max_sz = max(parse_size(s) for s in args.sizes)
         slot = max(1 << 20, -(-max_sz // P) + (1 << 16))
-        cl = LocalCluster(P, slot_bytes=slot, grid=args.grid, timeout_s=10.0)
+        cl = LocalCluster(P, slot_bytes=slot, grid=args.grid, timeout_s=10.0,
+                          max_lag=1 if "threshold" in args.algos else None)
         for sz_s in args.sizes:
             S = parse_size(sz_s)
             n = S // es
@@ -84,6 +85,12 @@ def main() -> None:
                         def fn(ins=ins, outs=outs, algo=algo):
                             cl.collective(algo, ins, outs)
                         err = 0.0
+                    elif algo == "threshold":  # the round engine's kernel at th = 1 (same bytes as two-shot)
+                        def fn():
+                            cl.allreduce_threshold(xs, ys)
+                        fn()
+                        cl.check()
+                        err = max((t.float() - ref).abs().max().item() for t in ys)
                     else:
                         def fn(algo=algo):
                             cl.allreduce(xs, ys, algo=algo)
