@@ -345,6 +345,15 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
   // Every round of the previous epoch has finished here (drained): say so to the peers. Their
   // lag gates for this epoch's first maxLag + 1 rounds wait for exactly this value, so no
   // worker writes new-epoch data while any worker may still run an old-epoch round.
+  // Grow the stream-ordered pool now for the rounds' output buffers (an output is released
+  // one launch after its sink dropped it, so ~3 are live at once): growing it in the round
+  // path costs ~8 ms per 256 MiB buffer (profiles/round2/sync_probe.md) - paid here instead.
+  {
+    const size_t bytes = static_cast<size_t>(cfg.dataSize) * static_cast<size_t>(dtype_size(o_.dtype));
+    void* warm[3] = {nullptr, nullptr, nullptr};
+    for (void*& w : warm) hip_check(hipMallocAsync(&w, std::max<size_t>(bytes, 256), stream_), "hipMallocAsync(warm)");
+    for (void* w : warm) hip_check(hipFreeAsync(w, stream_), "hipFreeAsync(warm)");
+  }
   comm_->publish_progress(cfg.roundBase, stream_);
   hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize(publish progress)");
   if (static_cast<size_t>(P) * nch_ + 4 > ring_stride_) throw ProtocolError("xgmi plane: counts ring too small");

@@ -63,31 +63,52 @@ __device__ __forceinline__ uint32_t* forcew(const CommArgs& a, int k, int s) {
   return reinterpret_cast<uint32_t*>(a.base[k]) + static_cast<int64_t>(3 * a.rows * a.P) * a.maxch + 2 * a.P + s;
 }
 
+// The engine's pinned host words, [0] force and [1] abort: ONE PCIe read when they are
+// adjacent (the plane's layout). Returns "forced" (an abandoned round is forced too) and
+// sets *aborted.
+__device__ __forceinline__ bool host_forced(const CommArgs& a, uint32_t epoch, bool* aborted) {
+  *aborted = false;
+  if (a.hforce == nullptr) return false;
+  uint32_t fw, aw = epoch - 1u;
+  if (a.habort == a.hforce + 1) {
+    const uint64_t w = __hip_atomic_load(reinterpret_cast<const uint64_t*>(a.hforce), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
+    fw = static_cast<uint32_t>(w);
+    aw = static_cast<uint32_t>(w >> 32);
+  } else {
+    fw = __hip_atomic_load(const_cast<uint32_t*>(a.hforce), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (a.habort != nullptr)
+      aw = __hip_atomic_load(const_cast<uint32_t*>(a.habort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  *aborted = reached(aw, epoch);
+  return *aborted || reached(fw, epoch);
+}
+
 // Wave 0 only: is round `epoch` forced? Lane s < P reads FORCE[s] of the own slab (peer s
-// waits at its lag gate for this rank); lane 63 reads the engine's pinned host word when
+// waits at its lag gate for this rank); lane 63 reads the engine's pinned host words when
 // `host` (a PCIe read: callers rate-limit it). Wave-uniform.
 __device__ __forceinline__ bool wave_forced(const CommArgs& a, int r, uint32_t epoch, bool host) {
   const int s = static_cast<int>(threadIdx.x);
   bool f = false;
   if (s < a.P && s != r) f = reached(ld_flag(forcew(a, r, s)), epoch);
-  if (host && s == 63 && a.hforce != nullptr)
-    f = reached(__hip_atomic_load(const_cast<uint32_t*>(a.hforce), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                epoch);
-  if (host && s == 62 && a.habort != nullptr)  // an abandoned round is forced too
-    f = reached(__hip_atomic_load(const_cast<uint32_t*>(a.habort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                epoch);
+  if (host && s == 63) {
+    bool ab;
+    f = host_forced(a, epoch, &ab);
+  }
   return __any(f);
 }
 
-// Host-word polls at most every 20 us per workgroup, the first one 20 us after the kernel
-// started: a PCIe read stalls the polling wave for microseconds, and a round that finishes
-// within 20 us does not need to learn that it was forced.
+// Host-word polls at most every 100 us per workgroup, the first one 100 us after the kernel
+// started: every poll is a PCIe read that stalls the polling wave for microseconds, and at
+// 512 workgroups x 2 planes a 20 us interval put ~50 M reads/s on the link, slowing the
+// rounds themselves (same-box A/B, profiles/round2/README.md). A forced round is exceptional;
+// learning of it within 100 us is enough.
 struct HostPoll {
-  uint64_t next = wall_ticks() + 2000;
+  uint64_t next = wall_ticks() + 10000;
   __device__ __forceinline__ bool due() {
     const uint64_t t = wall_ticks();
     if (t < next) return false;
-    next = t + 2000;
+    next = t + 10000;
     return true;
   }
 };
@@ -367,9 +388,8 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
       __builtin_amdgcn_s_sleep(2);
       if (!ok) ok = reached(ld_flag(f), target);
       if (a.habort != nullptr && hp.due()) {
-        const bool ab = k == 0 && reached(__hip_atomic_load(const_cast<uint32_t*>(a.habort), __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_SYSTEM),
-                                          epoch);
+        bool ab = false;
+        if (k == 0) (void)host_forced(a, epoch, &ab);
         if (__any(ab)) {
           aborted = true;
           break;
