@@ -5,10 +5,12 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <chrono>
 #include <cstring>
 #include <random>
 #include <sstream>
+#include <string>
 #include <stdexcept>
 
 #include "../core/data_buffer.h"
@@ -216,11 +218,22 @@ std::shared_ptr<void> XgmiRoundPlane::buffer(size_t bytes, bool user_visible) {
   // release is also ordered after the default stream - otherwise the next round could get
   // the same block from the pool and overwrite it under that work.
   std::weak_ptr<ReleaseQ> rq = rel_;
+  static const bool via_event = [] {
+    const char* e = std::getenv("MXAR_PLANE_RELEASE");
+    return e != nullptr && std::string(e) == "event";
+  }();
   return std::shared_ptr<void>(p, [s, alive, user_visible, rq](void* q) {
     auto a = alive.lock();
     if (a && *a) {
       if (user_visible) {
-        if (auto r = rq.lock()) {  // freed by the next launch, behind the default stream
+        if (!via_event) {
+          // freed on the default stream itself: ordered after whatever the sink queued
+          // there, and the stream-ordered pool orders a later reuse by the plane stream
+          // after that free - no event or stream wait on the launch path
+          (void)hipFreeAsync(q, nullptr);
+          return;
+        }
+        if (auto r = rq.lock()) {  // MXAR_PLANE_RELEASE=event: freed by the next launch, behind an event
           std::lock_guard<std::mutex> g(r->mu);
           r->ptrs.push_back(q);
           return;
