@@ -133,7 +133,8 @@ def master_main(argv: list[str] | None = None) -> int:
                            float(cfg["mxar.allreduce.th-complete"]), int(cfg["mxar.allreduce.max-lag"]), data_size,
                            int(cfg["mxar.allreduce.max-round"]), chunk,
                            liveBarrier=bool(cfg["mxar.allreduce.live-barrier"]),
-                           reinitOnLoss=bool(cfg["mxar.allreduce.reinit-on-loss"]), on_finished=finished, name="master",
+                           reinitOnLoss=bool(cfg["mxar.allreduce.reinit-on-loss"]),
+                           resumeOnJoin=bool(cfg["mxar.allreduce.resume-on-join"]), on_finished=finished, name="master",
                            startRound=start_round, on_round=on_round,
                            roundTimeoutMs=int(float(cfg["mxar.allreduce.round-timeout"]) * 1000))
     node = C.ClusterNode.start(system, _cluster_cfg(cfg, args.port, ["master"]))

@@ -42,6 +42,7 @@ DEFAULTS: dict[str, Any] = {
     "mxar.allreduce.max-round": 100,                           # :109
     "mxar.allreduce.live-barrier": False,
     "mxar.allreduce.reinit-on-loss": False,                    # re-init the survivors when a worker dies
+    "mxar.allreduce.resume-on-join": False,                    # a mid-job join resumes everyone at the current round
     "mxar.allreduce.round-timeout": 0.0,                       # seconds; 0 = off
     "mxar.engine.device": "cpu",                               # cpu | cuda[:i]
     "mxar.engine.algo": "auto",                                # auto | twoshot | oneshot | rccl

@@ -504,9 +504,9 @@ PYBIND11_MODULE(_C, m) {
       .def("master", [](ActorSystem& s, int totalWorkers, float thAllreduce, float thReduce, float thComplete,
                         int maxLag, int dataSize, int maxRound, int maxChunkSize, bool liveBarrier,
                         py::object on_finished, std::string name, int startRound, py::object on_round,
-                        int roundTimeoutMs, bool reinitOnLoss) {
+                        int roundTimeoutMs, bool reinitOnLoss, bool resumeOnJoin) {
             MasterParams p{totalWorkers, thAllreduce, thReduce, thComplete, maxLag, dataSize, maxRound,
-                           maxChunkSize, liveBarrier, startRound, roundTimeoutMs, reinitOnLoss};
+                           maxChunkSize, liveBarrier, startRound, roundTimeoutMs, reinitOnLoss, resumeOnJoin};
             MasterActor::RoundCallback rcb;
             if (!on_round.is_none()) {
               auto h = std::make_shared<PyCallable>(std::move(on_round));
@@ -528,7 +528,7 @@ PYBIND11_MODULE(_C, m) {
           py::arg("maxLag"), py::arg("dataSize"), py::arg("maxRound"), py::arg("maxChunkSize"),
           py::arg("liveBarrier") = false, py::arg("on_finished") = py::none(), py::arg("name") = "master",
           py::arg("startRound") = 0, py::arg("on_round") = py::none(), py::arg("roundTimeoutMs") = 0,
-          py::arg("reinitOnLoss") = false)
+          py::arg("reinitOnLoss") = false, py::arg("resumeOnJoin") = false)
       .def("plane_worker", [](ActorSystem& s, py::object source, py::object sink, std::shared_ptr<RoundPlane> plane,
                               std::string name) {
             auto a = std::make_unique<PlaneWorkerActor>(make_plane_source(std::move(source)),
@@ -629,6 +629,7 @@ PYBIND11_MODULE(_C, m) {
         d["stale_completes"] = c.stats().stale_completes;
         d["round_timeouts"] = c.stats().round_timeouts;
         d["loss_reinits"] = c.stats().loss_reinits;
+        d["join_reinits"] = c.stats().join_reinits;
         return d;
       });
 

@@ -17,6 +17,14 @@ void MasterCore::on_member_up(int handle) {
   while (workers_.count(id)) ++id;
   workers_[id] = handle;
   MXAR_LOG(INFO, "master", "----current size = " << workers_.size());
+  if (p_.resumeOnJoin && round_ >= 0 && !finished_) {  // a join mid-job: everyone resumes here
+    MXAR_LOG(INFO, "master", "----worker joined at round " << round_ << ": re-initialising "
+                                                           << workers_.size() << " workers there");
+    stats_.join_reinits++;
+    init_workers(round_);
+    start_allreduce();
+    return;
+  }
   if (static_cast<int>(workers_.size()) >= f32_threshold_count(p_.thAllreduce, p_.totalWorkers)) {
     MXAR_LOG(INFO, "master", "----" << workers_.size() << " (out of " << p_.totalWorkers << ") workers are up");
     init_workers();

@@ -40,6 +40,10 @@ struct MasterParams {
   // barrier over live workers. The reference only re-initialises on MemberUp, so a lost
   // worker leaves its peers waiting on rounds that can never complete (Q4).
   bool reinitOnLoss = false;
+  // Extension: a worker that joins while rounds are running (e.g. a restarted one) is taken
+  // in by re-initialising everyone at the CURRENT round. The reference restarts the whole
+  // job at round 0 on every MemberUp past the threshold (Q2).
+  bool resumeOnJoin = false;
 };
 
 class MasterEffects {
@@ -57,7 +61,7 @@ class MasterEffects {
 
 struct MasterStats {
   uint64_t inits = 0, rounds_started = 0, completes = 0, stale_completes = 0, removed = 0, round_timeouts = 0,
-           loss_reinits = 0;
+           loss_reinits = 0, join_reinits = 0;
 };
 
 class MasterCore {

@@ -73,3 +73,67 @@ def test_survivors_are_reinitialised_and_finish(kind):
             assert all(c == 2 for c in counts), counts
     finally:
         system.shutdown()
+
+
+@pytest.mark.parametrize("kind", ["host", "loopback"])
+def test_lost_worker_replaced_mid_job(kind):
+    """Elastic membership: worker 2 dies (the survivors are re-initialised, reinitOnLoss), then
+    a replacement joins (resumeOnJoin). Everyone is re-initialised at the CURRENT round, not
+    restarted at round 0 as in the reference (Q2), and the job finishes with three workers."""
+    P, n, chunk, rounds = 3, 24, 4, 60
+    system = C.ActorSystem("Elastic", False)
+    fin = threading.Event()
+    outs = [dict() for _ in range(P + 1)]
+    lock = threading.Lock()
+    progressed = {"r": -1}
+
+    def src(k):
+        base = host_iota_source(n, 1000.0 * min(k, 2))  # the replacement contributes as worker 2 did
+
+        def f(req):
+            time.sleep(0.01)
+            progressed["r"] = max(progressed["r"], req.iteration)
+            v = base(req)
+            return AllReduceInput(v) if kind == "host" else v
+        return f
+
+    def sink(k):
+        def f(out):
+            with lock:
+                outs[k][out.iteration] = (np.asarray(out.data).copy(), list(out.count))
+        return f
+
+    master = system.master(P, 1.0, 1.0, 1.0, 1, n, rounds - 1, chunk, on_finished=lambda r: fin.set(),
+                           reinitOnLoss=True, resumeOnJoin=True)
+    planes = []
+
+    def join(k):
+        if kind == "host":
+            w = system.worker(src(k), sink(k), f"w{k}")
+            master.tell(MemberUp(w, "worker", ""), None)
+        else:
+            planes.append(C.loopback_plane("elastic-hub"))
+            w = system.plane_worker(src(k), sink(k), planes[-1], f"w{k}")
+            master.tell(MemberUp(w, "worker", "", planes[-1].descriptor), None)
+        return w
+
+    try:
+        ws = [join(k) for k in range(P)]
+        t0 = time.time()
+        while progressed["r"] < 5 and time.time() - t0 < 20:
+            time.sleep(0.01)
+        ws[2].tell(PoisonPill(), None)
+        while system.master_state(master)["loss_reinits"] < 1 and time.time() - t0 < 20:
+            time.sleep(0.01)
+        resumed_at = progressed["r"]
+        join(3)  # the replacement
+        assert fin.wait(30), system.master_state(master)
+        st = system.master_state(master)
+        assert st["loss_reinits"] == 1 and st["join_reinits"] == 1 and st["numWorkers"] == 3, st
+        assert st["inits"] == 3, st  # start, loss, join - never a restart from round 0
+        last, counts = outs[0][rounds - 1]
+        np.testing.assert_array_equal(last, expected(n, rounds - 1, (0, 1, 2)).astype(F))
+        assert all(c == 3 for c in counts), counts
+        assert min(outs[3]) >= resumed_at  # the replacement started at the current round
+    finally:
+        system.shutdown()
