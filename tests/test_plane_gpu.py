@@ -403,3 +403,57 @@ def test_worker_loss_reinitialises_the_survivors():
             assert all(c == 2 for c in counts), counts
     finally:
         job.shutdown()
+
+
+def test_lost_worker_replaced_by_a_new_plane_worker():
+    """Elastic membership on the GPU round engine: worker 2 dies, the survivors continue
+    (reinitOnLoss), a replacement worker with a NEW plane (arena) joins and everyone is
+    re-initialised at the current round (resumeOnJoin); the job finishes exactly with three."""
+    P, n, chunk, rounds = 3, 3000, 250, 40
+    system = C.ActorSystem("ElasticGpu", False)
+    fin = __import__("threading").Event()
+    outs = [dict() for _ in range(P + 1)]
+    progressed = {"r": -1}
+
+    def src(k):
+        base = iota_source(n, DEV, torch.float32, 1000.0 * min(k, 2))
+
+        def f(req):
+            time.sleep(0.01)
+            progressed["r"] = max(progressed["r"], req.iteration)
+            return base(req)
+        return f
+
+    planes = []
+    master = system.master(P, 1.0, 1.0, 1.0, 1, n, rounds - 1, chunk, on_finished=lambda r: fin.set(),
+                           reinitOnLoss=True, resumeOnJoin=True)
+
+    def join(k):
+        planes.append(C.hip.xgmi_plane(0, C.hip.DType.F32, n, max_peers=4, max_lag=1, grid=64, timeout_s=20.0))
+        w = system.plane_worker(src(k), (lambda k: lambda out: outs[k].__setitem__(out.iteration, (out.data, list(out.count))))(k),
+                                planes[-1], f"w{k}")
+        master.tell(C.MemberUp(w, "worker", "", planes[-1].descriptor), None)
+        return w
+
+    try:
+        ws = [join(k) for k in range(P)]
+        t0 = time.time()
+        while progressed["r"] < 5 and time.time() - t0 < 30:
+            time.sleep(0.01)
+        ws[2].tell(C.PoisonPill(), None)
+        while system.master_state(master)["loss_reinits"] < 1 and time.time() - t0 < 30:
+            time.sleep(0.01)
+        join(3)
+        assert fin.wait(60), system.master_state(master)
+        assert time.time() - t0 < 30, "a round waited out a kernel deadline"
+        for p in planes:
+            p.drain()
+        st = system.master_state(master)
+        assert st["loss_reinits"] == 1 and st["join_reinits"] == 1 and st["numWorkers"] == 3, st
+        data, counts = outs[0][rounds - 1]
+        np.testing.assert_array_equal(data.cpu().numpy(), expected(n, rounds - 1, (0, 1, 2)))
+        assert all(c == 3 for c in counts), counts
+    finally:
+        system.shutdown()
+        planes.clear()
+        __import__("gc").collect()
