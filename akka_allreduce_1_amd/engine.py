@@ -70,10 +70,13 @@ class PlaneJob:
                  sources: Sequence[Callable] | None = None, keep_outputs: bool = True, round_timeout_ms: int = 0,
                  timeout_s: float = 60.0, order_ref: bool = True, on_output: Callable | None = None,
                  max_peers: int | None = None, high_priority: bool = True, order_release: bool = True,
-                 plane: str = "xgmi", hub: str | None = None, spin_us: int = 1000, reinit_on_loss: bool = False):
+                 plane: str = "xgmi", hub: str | None = None, spin_us: int = 1000, reinit_on_loss: bool = False,
+                 split: bool = True):
         """plane: "xgmi" (one threshold-kernel launch per round on the GPUs in `devices`) or
         "loopback" (host memory, no GPU: csrc/runtime/loopback_plane.h; `hub` names the
-        workers' shared hub, default a fresh one; dtype float32, devices ignored)."""
+        workers' shared hub, default a fresh one; dtype float32, devices ignored).
+        split: chunks fewer than the plane's workgroups are split into slices over several
+        workgroups, each chunk still one threshold decision (csrc/hip/xgmi_threshold.hip)."""
         self.P = P
         self.n = data_size
         self.dtype = dtype
@@ -107,7 +110,7 @@ class PlaneJob:
             self.planes = [C.hip.xgmi_plane(d, dtype_code(dtype), data_size, max_peers=max_peers or P,
                                             max_lag=max_lag, grid=grid, timeout_s=timeout_s, order_ref=order_ref,
                                             high_priority=high_priority, order_release=order_release,
-                                            spin_us=spin_us)
+                                            spin_us=spin_us, split=split)
                            for d in self.devices]
             if sources is None:
                 sources = [iota_source(data_size, torch.device("cuda", d), dtype, 1000.0 * k)

@@ -224,7 +224,7 @@ void bind_hip(py::module_& m) {
   h.def(
       "xgmi_plane",
       [](int device, DType dtype, int64_t capacity, int max_peers, int max_lag, int grid, double timeout_s,
-         bool order_ref, bool high_priority, bool order_release, int spin_us) {
+         bool order_ref, bool high_priority, bool order_release, int spin_us, bool split) {
         XgmiPlaneOptions o;
         o.device = device;
         o.dtype = dtype;
@@ -237,12 +237,13 @@ void bind_hip(py::module_& m) {
         o.high_priority = high_priority;
         o.order_release = order_release;
         o.spin_us = spin_us;
+        o.split = split;
         py::gil_scoped_release r;
         return make_xgmi_plane(o);
       },
       py::arg("device") = 0, py::arg("dtype") = DType::F32, py::arg("capacity"), py::arg("max_peers") = 8,
       py::arg("max_lag") = 4, py::arg("grid") = 0, py::arg("timeout_s") = 60.0, py::arg("order_ref") = true,
-      py::arg("high_priority") = true, py::arg("order_release") = true, py::arg("spin_us") = 1000,
+      py::arg("high_priority") = true, py::arg("order_release") = true, py::arg("spin_us") = 1000, py::arg("split") = true,
       "RoundPlane of the protocol engine on MI355X: an HBM arena exported over IPC, one threshold-kernel launch "
       "per round (csrc/hip/xgmi_plane.h)");
   py::enum_<Algo>(h, "Algo").value("Auto", Algo::Auto).value("TwoShot", Algo::TwoShot).value("OneShot", Algo::OneShot).value("Ring", Algo::Ring).value("LL", Algo::LL);

@@ -141,7 +141,16 @@ class XgmiComm {
     const uint32_t* host_abort = nullptr;  // rounds <= this epoch are abandoned (may be null)
     uint32_t* err_out = nullptr;           // device-visible word the round's error word is copied to
     int32_t* counts_host = nullptr;        // device-visible pinned copy of `counts`, written at round end
+    // the rank's scratch for split chunks (zeroed per membership; split_scratch_bytes(P));
+    // null: one workgroup per chunk
+    void* split_scratch = nullptr;
+    size_t split_bytes = 0;
   };
+  // Scratch a round of P ranks needs to split its chunks over several workgroups.
+  static size_t split_scratch_bytes(int P, int64_t maxch) {
+    return static_cast<size_t>(maxch) * (static_cast<size_t>(P + 1) * 12 + static_cast<size_t>(P) * 4);
+  }
+  int64_t max_chunks() const { return maxch_; }
   void round(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, float th_reduce, float th_complete,
              int32_t* counts, const RoundSpec& spec, float scale = 1.f);
   // Workgroups a round launch of `nch` chunks per block uses (counts / geometry checks).

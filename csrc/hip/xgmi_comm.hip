@@ -916,12 +916,35 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
     a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
     if (ranks_here != 1) throw std::invalid_argument("round: one rank per launch");
     gx = c0.round_grid(a.nch);
+    // Fewer chunks than workgroups (big maxChunkSize): split each chunk into slices of at
+    // least 64 KiB, one workgroup each, until the reduce phase covers the grid. A chunk stays
+    // ONE threshold decision (xgmi_threshold.hip, split chunks).
+    const int64_t min_slice = std::max<int64_t>(64, (int64_t{64} << 10) / es);
+    if (spec->split_scratch != nullptr && W <= 30 && a.nch < c0.grid_ && a.chunk >= 2 * min_slice &&
+        spec->split_bytes >= split_scratch_bytes(W, c0.maxch_)) {
+      const int64_t S = std::min<int64_t>(ceil_div(c0.grid_, a.nch), a.chunk / min_slice);
+      if (S > 1) {
+        a.subchunk = round_up(ceil_div(a.chunk, S), 64);
+        a.sub = static_cast<int>(ceil_div(a.chunk, a.subchunk));
+        const int64_t units = static_cast<int64_t>(a.nch) * a.sub;
+        gx = static_cast<int>(std::min<int64_t>(
+            c0.grid_, std::max<int64_t>(units, ceil_div(static_cast<int64_t>(W - 1) * units, 1024))));
+        char* sp = static_cast<char*>(spec->split_scratch);
+        a.split_dec = reinterpret_cast<uint64_t*>(sp);
+        a.split_ctr = reinterpret_cast<uint32_t*>(sp + static_cast<size_t>(W + 1) * c0.maxch_ * 8);
+        a.split_early = reinterpret_cast<uint32_t*>(sp + static_cast<size_t>(W + 1) * c0.maxch_ * 12);
+      }
+    }
   } else {
     c0.geometry_threshold(n, dt, ranks_here, &a.block, &a.chunk, &a.nch, &gx);
   }
   if (a.block * es > c0.slot_bytes_ || a.nch > c0.maxch_)
     throw std::invalid_argument("allreduce_threshold: tensor exceeds one launch (n * dtype <= world * slot_bytes)");
-  if (ceil_div(static_cast<int64_t>(W - 1) * a.nch, gx) > 1024)
+  if (a.sub < 1) {  // unsplit: one workgroup per chunk
+    a.sub = 1;
+    a.subchunk = a.chunk;
+  }
+  if (ceil_div(static_cast<int64_t>(W - 1) * a.nch * a.sub, gx) > 1024)
     throw std::logic_error("allreduce_threshold: more than 1024 gather units per workgroup");
   a.n = n;
   a.P = W;
@@ -937,8 +960,6 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
   a.fence = c0.fence_;
   a.scale = scale;
   a.rescale = rescale ? 1 : 0;
-  a.subchunk = a.chunk;
-  a.sub = 1;
   a.min_reduce = std::max(1, f32_threshold_count(thr, W));
   a.min_complete = f32_threshold_chunks(thc, W, a.nch);
   a.counts = counts;

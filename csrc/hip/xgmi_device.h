@@ -69,6 +69,14 @@ struct CommArgs {
   uint64_t delay;      // test knob: ticks rank `delay_rank` idles before phase 1
   int delay_rank;
   int dynamic;  // two-shot: workgroups take reduce / gather units from a counter (ctl[8], ctl[9])
+  // threshold kernel with sub > 1 (chunks split into `sub` slices of `subchunk` elements,
+  // one workgroup each): the rank's own scratch, zeroed when the membership is configured.
+  // split_dec: 64-bit decision words, [c] own reduce chunk c, [maxch + j * maxch + c] gather
+  // unit (j, c); split_ctr: slice counters, [c] reduce, [maxch + j * maxch + c] scatter;
+  // split_early: [j * maxch + c] = epoch when gather unit (j, c) was in at launch
+  uint64_t* split_dec;
+  uint32_t* split_ctr;
+  uint32_t* split_early;
 };
 
 // Phase stamps of one workgroup (100 MHz s_memrealtime ticks): [0] start, [1] scatter done,

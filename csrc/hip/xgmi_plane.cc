@@ -83,6 +83,7 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
     throw std::invalid_argument("xgmi plane: max_peers must be in [1, 16]");
   if (o_.max_lag < 0 || o_.max_lag > 62) throw std::invalid_argument("xgmi plane: max_lag must be in [0, 62]");
   o_.ring = std::max(4, o_.ring);
+  if (const char* e = std::getenv("MXAR_PLANE_SPLIT")) o_.split = std::atoi(e) != 0;  // A/B knob
   const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
   // The flag table is reserved at its largest size over every membership of <= max_peers
   // workers and maxLag <= max_lag, so it sits at the same place in every layout: a late
@@ -98,10 +99,11 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
     const int64_t block = static_cast<int64_t>(f32_ceil_div(o_.capacity, P));
     const XgmiComm::Layout L = XgmiComm::layout(P, std::max<int64_t>(block * es, 16), o_.max_lag + 1, flag_bytes_);
     arena_bytes_ = std::max(arena_bytes_, L.slab_bytes);
-    for (int lag = 0; lag <= o_.max_lag; ++lag)
-      max_counts = std::max<int64_t>(
-          max_counts, static_cast<int64_t>(P) * XgmiComm::layout(P, std::max<int64_t>(block * es, 16), lag + 1,
-                                                                 flag_bytes_).maxch);
+    for (int lag = 0; lag <= o_.max_lag; ++lag) {
+      const int64_t maxch = XgmiComm::layout(P, std::max<int64_t>(block * es, 16), lag + 1, flag_bytes_).maxch;
+      max_counts = std::max<int64_t>(max_counts, static_cast<int64_t>(P) * maxch);
+      split_bytes_ = std::max(split_bytes_, XgmiComm::split_scratch_bytes(P, maxch));
+    }
   }
   arena_bytes_ = XgmiComm::ipc_safe_bytes(arena_bytes_);
   hip_check(hipSetDevice(o_.device), "hipSetDevice");
@@ -126,6 +128,9 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   hip_check(hipMalloc(reinterpret_cast<void**>(&cnt_vram_), ring_stride_ * 4 * o_.ring), "hipMalloc(plane counts)");
   hip_check(hipMalloc(reinterpret_cast<void**>(&ctl_mem_), 256), "hipMalloc(plane ctl)");
   hip_check(hipMemset(ctl_mem_, 0, 256), "hipMemset(plane ctl)");
+  // split-chunk scratch (decision words, slice counters; XgmiComm::RoundSpec::split_scratch)
+  hip_check(hipMalloc(&split_mem_, split_bytes_), "hipMalloc(plane split scratch)");
+  hip_check(hipMemset(split_mem_, 0, split_bytes_), "hipMemset(plane split scratch)");
   hip_check(hipEventCreateWithFlags(&rel_ev_, hipEventDisableTiming), "hipEventCreate(release)");
   for (int i = 0; i < o_.ring; ++i) {
     hipEvent_t e = nullptr;
@@ -201,6 +206,7 @@ XgmiRoundPlane::~XgmiRoundPlane() {
   if (ring_) (void)hipHostFree(ring_);
   if (cnt_vram_) (void)hipFree(cnt_vram_);
   if (ctl_mem_) (void)hipFree(ctl_mem_);
+  if (split_mem_) (void)hipFree(split_mem_);
   if (hforce_) (void)hipHostFree(hforce_);
   if (stream_) (void)hipStreamDestroy(stream_);
   if (arena_) (void)hipFree(arena_);
@@ -351,6 +357,8 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
   // below). The communicator reuses the plane's arena and control words; the control words
   // are reset stream-ordered, after the drained old epoch.
   hip_check(hipMemsetAsync(ctl_mem_, 0, 256, stream_), "hipMemsetAsync(plane ctl)");
+  // a new membership may reuse round epochs of the abandoned one: no stale decision survives
+  hip_check(hipMemsetAsync(split_mem_, 0, split_bytes_, stream_), "hipMemsetAsync(plane split scratch)");
   comm_ = std::make_unique<XgmiComm>(cfg.id, P, o_.device, slot, o_.grid, o_.timeout_s, cfg.maxLag + 1, arena_,
                                      arena_bytes_, flag_bytes_, ctl_mem_);
   comm_->connect_ptrs(bases);
@@ -450,6 +458,10 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   spec.host_abort = hforce_dev_ + 1;
   spec.err_out = reinterpret_cast<uint32_t*>(slot_dev + ring_stride_ - 1);
   spec.counts_host = slot_dev;  // the kernel counts into HBM and copies once, at round end
+  if (o_.split) {
+    spec.split_scratch = split_mem_;
+    spec.split_bytes = split_bytes_;
+  }
   int32_t* cnt_dev = cnt_vram_ + static_cast<size_t>(rec.slot) * ring_stride_;
   {
     TraceScope span("plane", [&] {

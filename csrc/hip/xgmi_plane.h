@@ -53,6 +53,7 @@ struct XgmiPlaneOptions {
   bool high_priority = true;  // plane stream priority (see XgmiRoundPlane ctor)
   bool order_release = true;  // a round output's release waits for the default stream (buffer())
   int spin_us = 1000;         // completion thread polls a round's event this long before blocking
+  bool split = true;          // chunks fewer than workgroups are split over several (threshold kernel)
 };
 
 struct XgmiPlaneStats {
@@ -129,6 +130,8 @@ class XgmiRoundPlane final : public RoundPlane {
   int32_t* ring_ = nullptr;
   int32_t* ring_dev_ = nullptr;  // the ring's device-visible address
   uint32_t* ctl_mem_ = nullptr;  // the communicator's control words, kept across epochs
+  void* split_mem_ = nullptr;    // split-chunk scratch, zeroed per membership
+  size_t split_bytes_ = 16;
   int32_t* cnt_vram_ = nullptr;  // per-slot counts the workgroups write (HBM); copied into the ring at round end
   size_t ring_stride_ = 0;  // int32 per slot
   std::vector<int> free_slots_;

@@ -264,6 +264,66 @@ __device__ __forceinline__ uint32_t add_ctl(uint32_t* p, uint32_t v) {
   return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Split chunks (a.sub = S > 1). A protocol chunk is ONE decision (which contributions its
+// reduce sums, whether the round takes it, its count) but S workgroups move its data, one
+// slice each, so a few big chunks still spread over the whole grid. The slices agree on the
+// decision through one epoch-tagged word per unit: the first slice ready to decide claims
+// it (CAS), decides exactly as an unsplit unit would (tickets included) and publishes;
+// every other slice adopts that decision. The decider never waits for anything after its
+// claim, so a slice waiting for a decision always gets one.
+constexpr uint64_t kDecided = 1ull << 31, kDecTake = 1ull << 30, kDecVal = (1ull << 30) - 1;
+
+__device__ __forceinline__ uint64_t dec_load(uint64_t* w) {
+  return __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool dec_this_epoch(uint64_t d, uint32_t epoch) {
+  return static_cast<uint32_t>(d >> 32) == epoch;
+}
+// One lane. True: the caller decides and must dec_publish. False: *out is the decision of
+// this epoch (0 with ERR_TIMEOUT_REDUCE if the decider never published before the deadline).
+__device__ __forceinline__ bool dec_claim(uint64_t* w, uint32_t epoch, uint64_t deadline, uint32_t* err,
+                                          uint64_t* out) {
+  uint64_t d = dec_load(w);
+  if (!dec_this_epoch(d, epoch)) {
+    if (__hip_atomic_compare_exchange_strong(w, &d, static_cast<uint64_t>(epoch) << 32, __ATOMIC_ACQ_REL,
+                                             __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT))
+      return true;
+  }
+  while (!(d & kDecided)) {  // claimed by another slice: its decision is instructions away
+    __builtin_amdgcn_s_sleep(1);
+    d = dec_load(w);
+    if (wall_ticks() > deadline) {
+      __hip_atomic_fetch_or(err, ERR_TIMEOUT_REDUCE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      d = 0;
+      break;
+    }
+  }
+  *out = d;
+  return false;
+}
+__device__ __forceinline__ void dec_publish(uint64_t* w, uint32_t epoch, bool take, uint32_t val) {
+  __hip_atomic_store(w, (static_cast<uint64_t>(epoch) << 32) | kDecided | (take ? kDecTake : 0ull) | val,
+                     __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// All threads. Every slice of a unit counts once per round; true (uniform) in the workgroup
+// that counted last, which then publishes the unit's flags. Each slice releases its stores
+// (system scope: they went to peer slabs) before it counts, so the last one's flags follow
+// every slice's data. The last one resets the counter for the next round of this unit.
+__device__ __forceinline__ bool last_slice(uint32_t* ctr, int S, int* sh) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    const uint32_t t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = t == static_cast<uint32_t>(S) - 1u;
+    if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *sh = last ? 1 : 0;
+  }
+  __syncthreads();
+  return *sh != 0;
+}
+
 }  // namespace
 
 template <class E>
@@ -271,6 +331,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   constexpr int es = 16 / E::ELEMS;
   __shared__ uint32_t sh_mask;
   __shared__ int sh_flag;
+  __shared__ int sh_last;
   __shared__ uint32_t sh_u32;
   __shared__ uint64_t sh_arr;
   __shared__ uint64_t pend[kGatherWords];
@@ -307,7 +368,13 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   const bool full = a.min_reduce >= P && a.min_complete >= P * a.nch;
   const bool snap = ref && !cold && !full;  // cold rounds are forced from the start: no snapshot
   const bool tickets = !full;
-  const int nu = (P - 1) * a.nch;
+  // work units: S slices per chunk (S = 1: a unit is a chunk). Scatter / gather unit
+  // u = ((c * (P-1) + peer) * S + slice); reduce unit v = c * S + slice.
+  const int S = a.sub > 1 ? a.sub : 1;
+  const bool split = S > 1;
+  const int nu = (P - 1) * a.nch * S;
+  const int nr = a.nch * S;
+  const int64_t sub = split ? a.subchunk : a.chunk;
   const int mine = blockIdx.x < static_cast<unsigned>(nu) ? (nu - 1 - static_cast<int>(blockIdx.x)) / G + 1 : 0;
   const int nwords = (mine + 63) / 64;
   HostPoll hp;
@@ -326,7 +393,8 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
     if (threadIdx.x < 64) {
       const int lane = static_cast<int>(threadIdx.x);
       int k = 0;
-      for (int c = blockIdx.x; c < a.nch && k < kMaxSnapChunks; c += G, ++k) {
+      for (int v = blockIdx.x; v < nr && k < kMaxSnapChunks; v += G, ++k) {
+        const int c = v / S;
         const bool in_ = lane < P && lane != r && reached(ld_flag(f1(a, r, row * P + lane, c)), epoch);
         const uint32_t m = static_cast<uint32_t>(__ballot(in_));
         if (lane == 0) s0[k] = m;
@@ -334,16 +402,21 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
       uint32_t cnt = 0;
       for (int w = 0; w < nwords; ++w) {
         const int idx = w * 64 + lane;
-        bool arr = false;
+        bool arr = false, first = false;
         if (idx < mine) {
           const int u = blockIdx.x + idx * G;
-          const int c = u / Pm1;
-          const int j = (r + 1 + u % Pm1) % P;
+          const int b = u / S;
+          const int c = b / Pm1;
+          const int j = (r + 1 + b % Pm1) % P;
           arr = reached(ld_flag(f2(a, r, row * P + j, c)), epoch);
+          first = u - b * S == 0;  // a split chunk's early arrival is decided by its slice 0
+          if (split && first && arr)
+            __hip_atomic_store(&a.split_early[static_cast<int64_t>(j) * a.maxch + c], epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
         const uint64_t m = __ballot(arr);
         if (lane == 0) early[w] = m;
-        cnt += static_cast<uint32_t>(__popcll(m));
+        cnt += static_cast<uint32_t>(__popcll(__ballot(arr && first)));
       }
       if (lane == 0) {
         if (cnt) add_ctl(&ctl[5], cnt);
@@ -363,6 +436,24 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
     }
     __syncthreads();
     etotal = sh_u32;
+    if (split) {  // every slice of a chunk takes slice 0's early bit (written before the barrier)
+      if (threadIdx.x < 64) {
+        const int lane = static_cast<int>(threadIdx.x);
+        for (int w = 0; w < nwords; ++w) {
+          const int idx = w * 64 + lane;
+          bool arr = false;
+          if (idx < mine) {
+            const int b = (static_cast<int>(blockIdx.x) + idx * G) / S;
+            const int c = b / Pm1;
+            const int j = (r + 1 + b % Pm1) % P;
+            arr = ld_ctl(&a.split_early[static_cast<int64_t>(j) * a.maxch + c]) == epoch;
+          }
+          const uint64_t m = __ballot(arr);
+          if (lane == 0) early[w] = m;
+        }
+      }
+      __syncthreads();
+    }
   } else {
     for (int w = static_cast<int>(threadIdx.x); w < nwords; w += kCommThreads) early[w] = 0;
   }
@@ -411,12 +502,16 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   // Phase 1 - ScatterBlock into the owners' row slots (a cold or void round sends nothing)
   if (!cold && !void_round) {
     for (int u = blockIdx.x; u < nu; u += G) {
-      const int c = u / Pm1;
-      const int j = (r + 1 + u % Pm1) % P;
+      const int b = u / S;
+      const int c = b / Pm1;
+      const int j = (r + 1 + b % Pm1) % P;
       const int64_t bstart = static_cast<int64_t>(j) * a.block;
-      const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
-      const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
+      const int64_t cstart = static_cast<int64_t>(c) * a.chunk + static_cast<int64_t>(u - b * S) * sub;
+      const int64_t len = clamp_len(clamp_len(clamp_len(a.n - bstart, a.block) - c * a.chunk, a.chunk) -
+                                        (cstart - c * a.chunk),
+                                    sub);
       if (len > 0) copy_in<E>(a.base[j] + rowS + r * slot + cstart * es, in + (bstart + cstart) * es, len);
+      if (split && !last_slice(&a.split_ctr[a.maxch + static_cast<int64_t>(j) * a.maxch + c], S, &sh_last)) continue;
       publish_flags([&](int) { return f1(a, j, row * P + r, c); }, 1, epoch, rel);
     }
   }
@@ -429,9 +524,12 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   const uint32_t others = all & ~(1u << r);
   const uint32_t own = cold ? 0u : (1u << r);
   int kk = 0;
-  for (int c = blockIdx.x; c < a.nch; c += G, ++kk) {
-    const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
-    const int64_t len = clamp_len(blen_own - cstart, a.chunk);
+  for (int v = blockIdx.x; v < nr; v += G, ++kk) {
+    const int c = v / S;
+    // this workgroup's slice of chunk c (the whole chunk when S = 1)
+    const int64_t cstart = static_cast<int64_t>(c) * a.chunk + static_cast<int64_t>(v - c * S) * sub;
+    const int64_t len = clamp_len(clamp_len(blen_own - c * a.chunk, a.chunk) - (cstart - c * a.chunk), sub);
+    uint64_t* const dec = split ? &a.split_dec[c] : nullptr;
     if (void_round) {  // nothing reduced, nothing sent
       if (len > 0) zero_fill<E>(out + (bstart_own + cstart) * es, len);
       if (threadIdx.x == 0 && counts) counts[static_cast<int64_t>(r) * a.nch + c] = 0;
@@ -460,6 +558,8 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
             mask |= fresh;  // greedy: everything present
           }
           if (static_cast<int>(__popc(mask)) >= a.min_reduce || (mask | own) == (own | others)) break;
+          // another slice of this chunk decided (or is deciding): adopt its decision
+          if (split && __any(s == 0 && dec_this_epoch(dec_load(dec), epoch))) break;
           if (wave_forced(a, r, epoch, hp.due())) {
             forced = true;
             break;
@@ -479,18 +579,28 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
         }
       }
       if (threadIdx.x == 0) {
-        sh_mask = mask;
         if (timed_out) __hip_atomic_fetch_or(err, ERR_TIMEOUT_SCATTER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        // reference order: does the own reduced chunk make this round's output? (forced
-        // reduces are flushed after the completion; a round complete at launch takes none)
-        int take = 1;
-        if (ref) {
-          if (forced || etotal >= static_cast<uint32_t>(a.min_complete))
-            take = 0;
-          else if (tickets)
-            take = etotal + add_ctl(&ctl[3], 1u) < static_cast<uint32_t>(a.min_complete) ? 1 : 0;
+        uint64_t d = 0;
+        if (split && !dec_claim(dec, epoch, deadline, err, &d)) {  // adopt the chunk's decision
+          sh_mask = static_cast<uint32_t>(d & kDecVal);
+          sh_flag = (d & kDecTake) ? 1 : 0;
+        } else {
+          sh_mask = mask;
+          // reference order: does the own reduced chunk make this round's output? (forced
+          // reduces are flushed after the completion; a round complete at launch takes none)
+          int take = 1;
+          if (ref) {
+            if (forced || etotal >= static_cast<uint32_t>(a.min_complete))
+              take = 0;
+            else if (tickets)
+              take = etotal + add_ctl(&ctl[3], 1u) < static_cast<uint32_t>(a.min_complete) ? 1 : 0;
+          }
+          sh_flag = take;
+          if (split) {
+            if (acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the flags it decided on
+            dec_publish(dec, epoch, take != 0, mask);
+          }
         }
-        sh_flag = take;
       }
       if (acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -506,6 +616,8 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
                        take ? own_out : nullptr, rowR + r * slot + cstart * es, len, a.fence & 1, sc);
       if (!take) zero_fill<E>(own_out, len);
     }
+    // a split chunk is reduced once its last slice is: that workgroup publishes it
+    if (split && !last_slice(&a.split_ctr[c], S, &sh_last)) continue;
     if (threadIdx.x < static_cast<unsigned>(P) && static_cast<int>(threadIdx.x) != r)
       st_flag(f2c(a, static_cast<int>(threadIdx.x), row * P + r, c), static_cast<uint32_t>(cnt));
     if (threadIdx.x == 0) {
@@ -536,9 +648,9 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
         const int idx = w * 64 + static_cast<int>(threadIdx.x);
         bool arr = false;
         if ((pend[w] >> threadIdx.x) & 1ull) {
-          const int u = blockIdx.x + idx * G;
-          const int c = u / Pm1;
-          const int j = (r + 1 + u % Pm1) % P;
+          const int b = (static_cast<int>(blockIdx.x) + idx * G) / S;
+          const int c = b / Pm1;
+          const int j = (r + 1 + b % Pm1) % P;
           arr = reached(ld_flag(f2(a, r, row * P + j, c)), epoch);
         }
         const uint64_t m = __ballot(arr);
@@ -554,11 +666,17 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
         m &= m - 1;
         const int idx = w * 64 + i;
         const int u = blockIdx.x + idx * G;
-        const int c = u / Pm1;
-        const int j = (r + 1 + u % Pm1) % P;
+        const int b = u / S;
+        const int c = b / Pm1;
+        const int j = (r + 1 + b % Pm1) % P;
+        uint64_t* const dec = split ? &a.split_dec[a.maxch + static_cast<int64_t>(j) * a.maxch + c] : nullptr;
         if (threadIdx.x == 0) {
           int take = 1;
-          if (!tickets) {
+          uint64_t d = 0;
+          const bool adopt = split && !dec_claim(dec, epoch, deadline, err, &d);
+          if (adopt) {  // another slice of this unit decided
+            take = (d & kDecTake) ? 1 : 0;
+          } else if (!tickets) {
             // full thresholds: every reduced chunk that arrives before a force is taken
           } else if (ref) {
             if ((early[w] >> i) & 1ull)
@@ -571,23 +689,28 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
           } else {
             add_ctl(&ctl[3], 1u);
           }
+          if (!adopt) {
+            if (counts)
+              counts[static_cast<int64_t>(j) * a.nch + c] =
+                  take ? static_cast<int32_t>(ld_flag(f2c(a, r, row * P + j, c))) : 0;
+            if (split) dec_publish(dec, epoch, take != 0, 0u);
+          }
           sh_flag = take;
           pend[w] &= ~(1ull << i);
         }
         __syncthreads();
         const bool take = sh_flag != 0;
         const int64_t bstart = static_cast<int64_t>(j) * a.block;
-        const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
-        const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
+        const int64_t cstart = static_cast<int64_t>(c) * a.chunk + static_cast<int64_t>(u - b * S) * sub;
+        const int64_t len = clamp_len(clamp_len(clamp_len(a.n - bstart, a.block) - c * a.chunk, a.chunk) -
+                                          (cstart - c * a.chunk),
+                                      sub);
         if (len > 0) {
           if (take)
             copy_out<E>(out + (bstart + cstart) * es, a.base[r] + rowR + j * slot + cstart * es, len);
           else
             zero_fill<E>(out + (bstart + cstart) * es, len);
         }
-        if (threadIdx.x == 0 && counts)
-          counts[static_cast<int64_t>(j) * a.nch + c] =
-              take ? static_cast<int32_t>(ld_flag(f2c(a, r, row * P + j, c))) : 0;
         progressed = true;
         ps.count(7);
         __syncthreads();
@@ -628,13 +751,40 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
         const int i = __ffsll(static_cast<long long>(m)) - 1;
         m &= m - 1;
         const int u = blockIdx.x + (w * 64 + i) * G;
-        const int c = u / Pm1;
-        const int j = (r + 1 + u % Pm1) % P;
+        const int b = u / S;
+        const int c = b / Pm1;
+        const int j = (r + 1 + b % Pm1) % P;
         const int64_t bstart = static_cast<int64_t>(j) * a.block;
-        const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
-        const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
-        if (len > 0) zero_fill<E>(out + (bstart + cstart) * es, len);
-        if (threadIdx.x == 0 && counts) counts[static_cast<int64_t>(j) * a.nch + c] = 0;
+        const int64_t cstart = static_cast<int64_t>(c) * a.chunk + static_cast<int64_t>(u - b * S) * sub;
+        const int64_t len = clamp_len(clamp_len(clamp_len(a.n - bstart, a.block) - c * a.chunk, a.chunk) -
+                                          (cstart - c * a.chunk),
+                                      sub);
+        bool take = false;
+        if (split) {  // give the unit up, unless another slice of it already took it
+          uint64_t* const dec = &a.split_dec[a.maxch + static_cast<int64_t>(j) * a.maxch + c];
+          if (threadIdx.x == 0) {
+            uint64_t d = 0;
+            if (dec_claim(dec, epoch, deadline, err, &d)) {
+              if (counts) counts[static_cast<int64_t>(j) * a.nch + c] = 0;
+              dec_publish(dec, epoch, false, 0u);
+              sh_flag = 0;
+            } else {
+              sh_flag = (d & kDecTake) ? 1 : 0;
+              if (sh_flag && acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the chunk it saw arrive
+            }
+          }
+          __syncthreads();
+          take = sh_flag != 0;
+          __syncthreads();
+        } else if (threadIdx.x == 0 && counts) {
+          counts[static_cast<int64_t>(j) * a.nch + c] = 0;
+        }
+        if (len > 0) {
+          if (take)
+            copy_out<E>(out + (bstart + cstart) * es, a.base[r] + rowR + j * slot + cstart * es, len);
+          else
+            zero_fill<E>(out + (bstart + cstart) * es, len);
+        }
       }
     }
   }

@@ -13,6 +13,9 @@
 //   options: --host H  --seeds addr[,addr]  --th-allreduce F --th-reduce F --th-complete F
 //            --max-lag N --max-round N --round-timeout-ms N --loglevel L --quiet
 //   seeds default to the reference's application.conf:14-16 (127.0.0.1:2551, :2552).
+//   mxar-gpu worker ... --device K   (the same executable linked with csrc/tools/mxar_gpu.cc)
+//       the worker's rounds run on GPU K: an XgmiRoundPlane under a PlaneWorkerActor, the
+//       source filled on the device. Workers on one node exchange through the xGMI arena.
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -30,8 +33,11 @@
 #include "../cluster/cluster_node.h"
 #include "../core/log.h"
 #include "../runtime/allreduce_actors.h"
+#include "../runtime/plane_worker.h"
+#include "gpu_worker.h"
 
 using namespace mxar;
+
 
 namespace {
 
@@ -54,6 +60,9 @@ struct Options {
   int max_lag = 1, max_round = 100, round_timeout_ms = 0;          // :108-109
   std::string loglevel = "INFO";
   bool quiet = false;
+  int device = -1;  // worker: >= 0 runs the rounds on this GPU (mxar-gpu)
+  int max_peers = 8, plane_max_lag = 4, grid = 0;
+  double plane_timeout_s = 60.0;
 };
 
 [[noreturn]] void usage(const char* msg) {
@@ -61,7 +70,8 @@ struct Options {
                "%s\nusage: mxar master [port totalWorkers dataSize maxChunkSize] [options]\n"
                "       mxar worker [port sourceDataSize] [options]\n"
                "options: --host H --seeds a[,b] --th-allreduce F --th-reduce F --th-complete F --max-lag N\n"
-               "         --max-round N --round-timeout-ms N --loglevel L --quiet\n",
+               "         --max-round N --round-timeout-ms N --loglevel L --quiet\n"
+               "worker on a GPU (mxar-gpu): --device K [--max-peers N --plane-max-lag N --grid N --plane-timeout S]\n",
                msg);
   std::exit(2);
 }
@@ -87,6 +97,11 @@ Options parse(int argc, char** argv) {
     else if (a == "--round-timeout-ms") o.round_timeout_ms = std::stoi(val());
     else if (a == "--loglevel") o.loglevel = val();
     else if (a == "--quiet") o.quiet = true;
+    else if (a == "--device") o.device = std::stoi(val());
+    else if (a == "--max-peers") o.max_peers = std::stoi(val());
+    else if (a == "--plane-max-lag") o.plane_max_lag = std::stoi(val());
+    else if (a == "--grid") o.grid = std::stoi(val());
+    else if (a == "--plane-timeout") o.plane_timeout_s = std::stod(val());
     else if (a.rfind("--", 0) == 0) usage(("unknown option " + a).c_str());
     else o.positional.push_back(a);
   }
@@ -174,18 +189,25 @@ void set_level(const std::string& l) {
   std::atomic<int> rounds{0};
   const bool quiet = o.quiet;
   DataSink sink = [&rounds, quiet](const AllReduceOutput& out) {  // AllreduceWorker.scala:295-297
-    const std::vector<float> d = out.data->to_host();
-    const double sum = std::accumulate(d.begin(), d.end(), 0.0);
     rounds++;
-    if (!quiet) {
+    if (!quiet) {  // quiet: no copy back of a device output either
+      const std::vector<float> d = out.data->to_host();
+      const double sum = std::accumulate(d.begin(), d.end(), 0.0);
       std::printf("[mxar worker] round %d sum %.1f head", out.iteration, sum);
       for (size_t i = 0; i < d.size() && i < 6; ++i) std::printf(" %g", d[i]);
       std::printf("\n");
       std::fflush(stdout);
     }
   };
-  sys->actor_of(std::make_unique<WorkerActor>(src, sink), "worker");
   ClusterConfig cc;
+  if (o.device >= 0) {  // the round engine on a GPU: one threshold-kernel launch per round
+    if (make_gpu_worker == nullptr) usage("--device needs the GPU build of this executable: mxar-gpu");
+    GpuWorkerParts g = make_gpu_worker(o.device, size, o.max_peers, o.plane_max_lag, o.grid, o.plane_timeout_s);
+    cc.meta = g.plane->descriptor();  // relayed by the master in InitWorkers.planes
+    sys->actor_of(std::make_unique<PlaneWorkerActor>(g.source, sink, g.plane), "worker");
+  } else {
+    sys->actor_of(std::make_unique<WorkerActor>(src, sink), "worker");
+  }
   cc.host = o.host;
   cc.port = port;
   cc.roles = {"worker"};
@@ -209,7 +231,11 @@ void set_level(const std::string& l) {
   node->leave();
   std::this_thread::sleep_for(std::chrono::milliseconds(100));  // let the Leave frame go out
   node->shutdown();
-  sys->shutdown();
+  sys->shutdown();  // destroys the plane worker: its plane aborts and drains, the GPU is idle
+  if (o.device >= 0) {  // run the atexit handlers: the HIP runtime and a profiler flush there
+    std::fflush(nullptr);
+    std::exit(0);
+  }
   exit_now(0);
 }
 

@@ -457,3 +457,108 @@ def test_lost_worker_replaced_by_a_new_plane_worker():
         system.shutdown()
         planes.clear()
         __import__("gc").collect()
+
+
+# ---- split chunks: fewer protocol chunks than workgroups (csrc/hip/xgmi_threshold.hip) ----
+# A chunk of >= 2 x 64 KiB is cut into slices, one workgroup each; it stays ONE threshold
+# decision (contributor set, take, count), so every property below is per whole chunk.
+
+@pytest.mark.parametrize("P,n,chunk,dtype", [(2, (1 << 20) + 7, (1 << 19) + 9, torch.float32),
+                                             (3, 600001, 100000, torch.float32),
+                                             (2, 1 << 20, 1 << 18, torch.bfloat16)])
+def test_split_chunks_exact_at_threshold_one(P, n, chunk, dtype):
+    job = PlaneJob(P, n, max_chunk_size=chunk, th_reduce=1.0, th_complete=1.0, max_lag=1, max_round=7, dtype=dtype,
+                   timeout_s=20.0)
+    try:
+        job.run(timeout=120)
+        assert job.rounds["n"] == 8
+        for k in range(P):
+            st = job.system.plane_worker_state(job.workers[k])
+            assert st["stats"]["plane_errors"] == 0, st
+            for it in range(8):
+                data, counts = job.outputs[k][it]
+                got = data.float().cpu().numpy()
+                if dtype == torch.float32:
+                    np.testing.assert_array_equal(got, expected(n, it, range(P)), err_msg=f"worker {k} round {it}")
+                else:
+                    ar = torch.arange(n, dtype=torch.float64)
+                    ref = sum((ar + it + 1000.0 * j).to(dtype).double() for j in range(P)).numpy()
+                    assert np.all(np.abs(got - ref) <= np.abs(ref) * 2.0 ** -8 + 1e-6), (k, it)
+                assert all(c == P for c in counts), counts
+    finally:
+        job.shutdown()
+
+
+def test_split_straggler_matches_host_worker_core():
+    """The reference-order accounting (snapshot, tickets) with split chunks: the same outputs
+    and counts as the host WorkerCore for a deterministic straggler."""
+    P, n, chunk, rounds = 3, 300000, 50000, 4
+    th = 2.0 / 3.0
+    straggler, delay = 2, 0.3
+    host = _host_outputs(P, n, chunk, th, straggler, delay, rounds)
+
+    def slow(source):
+        def f(req):
+            time.sleep(delay)
+            return source(req)
+        return f
+
+    srcs = [iota_source(n, DEV, torch.float32, 1000.0 * k) for k in range(P)]
+    srcs[straggler] = slow(srcs[straggler])
+    job = PlaneJob(P, n, max_chunk_size=chunk, th_reduce=th, th_complete=th, max_lag=1, max_round=rounds - 1,
+                   sources=srcs, timeout_s=20.0)
+    try:
+        job.run(timeout=120)
+        for k in range(P):
+            for it in range(rounds):
+                g, gc = job.outputs[k][it]
+                h, hc = host[k][it]
+                assert gc == hc, (k, it, gc, hc)
+                np.testing.assert_array_equal(g.float().cpu().numpy(), h, err_msg=f"worker {k} round {it}")
+    finally:
+        job.shutdown()
+
+
+def test_split_catchup_keeps_chunks_whole():
+    """Forced completions race the slices of a chunk: whatever each round ends with, every
+    chunk is the sum of ONE contributor subset of size `count` over all its slices (or zeros
+    with count 0) - never half one decision and half another."""
+    P, n, chunk = 3, 600000, 50000
+    srcs = [iota_source(n, DEV, torch.float32, 1000.0 * k) for k in range(P)]
+    base = srcs[2]
+
+    def stall(req):
+        if req.iteration in (0, 3):
+            time.sleep(1.0)
+        return base(req)
+
+    srcs[2] = stall
+    job = PlaneJob(P, n, max_chunk_size=chunk, th_reduce=2.0 / 3.0, th_complete=2.0 / 3.0, max_lag=1, max_round=8,
+                   sources=srcs, round_timeout_ms=250, timeout_s=30.0)
+    try:
+        job.run(timeout=180)
+        st = job.state()
+        for k, w in enumerate(st["workers"]):
+            assert w["stats"]["plane_errors"] == 0, (k, w)
+            assert w["round"] == 9, (k, w)
+        _consistent(job, P, n, chunk, {0, 1, 2, 3})
+    finally:
+        job.shutdown()
+
+
+def test_split_matches_unsplit_outputs():
+    """Same job, split on and off: identical outputs and counts at thresholds 1."""
+    P, n, chunk = 2, 1 << 20, 1 << 18
+    res = []
+    for split in (True, False):
+        job = PlaneJob(P, n, max_chunk_size=chunk, max_lag=1, max_round=3, timeout_s=20.0, split=split)
+        try:
+            job.run(timeout=120)
+            res.append({(k, it): (d.cpu().numpy().copy(), list(c)) for k in range(P)
+                        for it, (d, c) in job.outputs[k].items()})
+        finally:
+            job.shutdown()
+    assert res[0].keys() == res[1].keys()
+    for key in res[0]:
+        np.testing.assert_array_equal(res[0][key][0], res[1][key][0], err_msg=str(key))
+        assert res[0][key][1] == res[1][key][1]

@@ -119,6 +119,7 @@ def build(jobs: int | None = None, clean: bool = False, debug: bool = False, san
             print(f"[build_native] linked {out.relative_to(ROOT)}", flush=True)
     if not sanitize:
         _build_exe(bdir, debug, verbose)
+        _build_gpu_exe(bdir, debug, verbose)
     return out
 
 
@@ -136,6 +137,34 @@ def _build_exe(bdir: Path, debug: bool, verbose: bool) -> None:
         return
     cmd = [os.environ.get("CXX", "g++"), "-o", str(exe)] + [str(o) for o in objs]
     cmd += [f"-L{ROCM / 'lib'}", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM / 'lib'}", "-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(f"[build_native] linked {exe.relative_to(ROOT)}", flush=True)
+
+
+def gpu_exe_path() -> Path:
+    """The native worker with the round engine on a GPU (csrc/tools/mxar_gpu.cc)."""
+    return PKG / "mxar-gpu"
+
+
+def _build_gpu_exe(bdir: Path, debug: bool, verbose: bool) -> None:
+    """Link `mxar-gpu`: the `mxar` objects + the HIP plane (every csrc/hip object except the
+    Python bindings) + csrc/tools/mxar_gpu.cc, which resolves mxar_main's weak make_gpu_worker."""
+    gpu_src = CSRC / "tools" / "mxar_gpu.cc"
+    gpu_obj = bdir / "tools_mxar_gpu.cc.o"
+    if not gpu_obj.exists() or gpu_obj.stat().st_mtime < max(gpu_src.stat().st_mtime, _headers_mtime()):
+        _compile(gpu_src, gpu_obj, debug, None)
+    hip = [bdir / ("hip_" + p.name + ".o") for p in sorted((CSRC / "hip").iterdir())
+           if p.suffix in (".cc", ".hip") and not p.name.endswith("_bind.cc")]
+    objs = [bdir / (p.parent.name + "_" + p.name + ".o") for sub in ("core", "runtime", "cluster")
+            for p in sorted((CSRC / sub).glob("*.cc"))] + hip + [gpu_obj, bdir / "tools_mxar_main.cc.o"]
+    exe = gpu_exe_path()
+    if exe.exists() and exe.stat().st_mtime >= max(o.stat().st_mtime for o in objs):
+        return
+    cmd = [str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-o", str(exe)] + [str(o) for o in objs]
+    cmd += [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM / 'lib'}", "-lpthread"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
