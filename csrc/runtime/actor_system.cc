@@ -70,17 +70,17 @@ void ActorContext::unwatch(const ActorRef& ref) {
   c->watchers_.erase(self());
 }
 
-void ActorContext::stash(Envelope env) {
-  std::lock_guard<std::mutex> g(cell_->mu_);
-  cell_->stash_.push_back(std::move(env));
-}
+// stash / unstash run inside the actor's own turn: the cell's consumer-private queues
+void ActorContext::stash(Envelope env) { cell_->stash_.push_back(std::move(env)); }
 
 void ActorContext::unstash_all() {
   // Stashed messages go back to the FRONT of the mailbox, in their original order
   // (Akka's Stash.unstashAll semantics).
-  std::lock_guard<std::mutex> g(cell_->mu_);
+  const auto n = static_cast<int64_t>(cell_->stash_.size());
+  if (n == 0) return;
+  cell_->pending_.fetch_add(n);
   while (!cell_->stash_.empty()) {
-    cell_->mailbox_.push_front(std::move(cell_->stash_.back()));
+    cell_->front_.push_front(std::move(cell_->stash_.back()));
     cell_->stash_.pop_back();
   }
 }
@@ -137,22 +137,49 @@ void DeadLetterRef::tell(Message msg, ActorRef sender) {
   sys_->note_dead_letter(msg, sender);
 }
 
+// ------------------------------------------------------------------------ mailbox
+MpscMailbox::MpscMailbox() {
+  head_ = new Node;
+  tail_.store(head_, std::memory_order_relaxed);
+}
+
+MpscMailbox::~MpscMailbox() {
+  Envelope e;
+  while (pop(e)) {
+  }
+  delete head_;
+}
+
+void MpscMailbox::push(Envelope&& e) {
+  Node* n = new Node;
+  n->env = std::move(e);
+  Node* prev = tail_.exchange(n, std::memory_order_acq_rel);
+  prev->next.store(n, std::memory_order_release);  // the consumer may now reach n
+}
+
+bool MpscMailbox::pop(Envelope& out) {
+  Node* h = head_;
+  Node* next = h->next.load(std::memory_order_acquire);
+  if (next == nullptr) return false;  // empty, or a push between its exchange and its link
+  out = std::move(next->env);
+  head_ = next;  // next becomes the stub
+  delete h;
+  return true;
+}
+
 // ------------------------------------------------------------------------ cell
 ActorCell::ActorCell(ActorSystem* sys, std::unique_ptr<Actor> actor, std::string path)
     : sys_(sys), actor_(std::move(actor)), path_(std::move(path)) {}
 
 void ActorCell::enqueue(Envelope env) {
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    mailbox_.push_back(std::move(env));
-  }
+  // count first (seq_cst), then push, then try to schedule: a dispatcher that clears
+  // scheduled_ and then reads pending_ sees this message whenever our schedule() lost
+  pending_.fetch_add(1);
+  mailbox_.push(std::move(env));
   sys_->schedule(shared_from_this());
 }
 
-bool ActorCell::has_mail() {
-  std::lock_guard<std::mutex> g(mu_);
-  return !mailbox_.empty();
-}
+bool ActorCell::has_mail() { return pending_.load() > 0; }
 
 size_t ActorCell::process(size_t n) {
   ActorContext ctx(sys_, this);
@@ -166,12 +193,13 @@ size_t ActorCell::process(size_t n) {
   size_t done = 0;
   while (done < n && !stopped_) {
     Envelope env;
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      if (mailbox_.empty()) break;
-      env = std::move(mailbox_.front());
-      mailbox_.pop_front();
+    if (!front_.empty()) {
+      env = std::move(front_.front());
+      front_.pop_front();
+    } else if (!mailbox_.pop(env)) {
+      break;  // empty (or a push not linked yet: pending_ keeps the cell scheduled)
     }
+    pending_.fetch_sub(1);
     ++done;
     if (std::holds_alternative<PoisonPill>(env.msg)) {
       do_stop();
@@ -205,12 +233,14 @@ void ActorCell::do_stop() {
   } catch (...) {
   }
   std::set<ActorRef> w;
-  std::deque<Envelope> rest;
   {
     std::lock_guard<std::mutex> g(mu_);
     w.swap(watchers_);
-    rest.swap(mailbox_);
   }
+  std::deque<Envelope> rest;
+  rest.swap(front_);
+  for (Envelope e; mailbox_.pop(e);) rest.push_back(std::move(e));
+  pending_.fetch_sub(static_cast<int64_t>(rest.size()));
   ActorRef me = ref();
   for (auto& e : rest) sys_->dead_letters()->tell(std::move(e.msg), e.sender);
   for (auto& watcher : w) watcher->tell(Terminated{me}, me);
@@ -345,10 +375,7 @@ size_t ActorSystem::run_until_idle(size_t max_messages) {
     }
     if (e) std::rethrow_exception(e);
   }
-  {
-    std::lock_guard<std::mutex> g(stats_mu_);
-    stats_.delivered += total;
-  }
+  delivered_.fetch_add(total, std::memory_order_relaxed);
   return total;
 }
 
@@ -374,10 +401,7 @@ void ActorSystem::worker_loop() {
     cell->scheduled_.store(false);
     // Re-check after clearing the flag: a message may have arrived in between.
     if (!cell->stopped() && cell->has_mail()) schedule(cell);
-    {
-      std::lock_guard<std::mutex> g(stats_mu_);
-      stats_.delivered += n;
-    }
+    delivered_.fetch_add(n, std::memory_order_relaxed);
     {
       std::lock_guard<std::mutex> g(rq_mu_);
       --busy_;
@@ -488,6 +512,7 @@ void ActorSystem::timer_loop() {
 SystemStats ActorSystem::stats() {
   std::lock_guard<std::mutex> g(stats_mu_);
   SystemStats s = stats_;
+  s.delivered = delivered_.load(std::memory_order_relaxed);
   s.dead_letters = dead_letters_->count();
   return s;
 }

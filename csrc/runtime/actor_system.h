@@ -11,8 +11,10 @@
 //                     stepped round-robin one message at a time. Message order is then
 //                     a pure function of the program, which the conformance tests need
 //                     (test T1 only passes under "batch then drain").
-// Per (sender, receiver) FIFO holds in both modes: one mailbox per actor, appended
-// under one lock.
+// Per (sender, receiver) FIFO holds in both modes: one mailbox per actor, a lock-free
+// multi-producer / single-consumer queue (MpscMailbox): a tell() is one atomic exchange
+// plus one release store, never a lock, and the dispatcher thread that holds the actor's
+// turn is the only consumer.
 #pragma once
 
 #include <atomic>
@@ -135,6 +137,28 @@ class DeadLetterRef final : public ActorRefBase {
   std::atomic<uint64_t> count_{0};
 };
 
+// Unbounded MPSC queue (D. Vyukov's stub-node list). Producers swap the tail and link the
+// previous node; the single consumer walks from the stub. A push whose link is not yet
+// visible reads as "empty" for a moment - the cell's `pending_` count (raised before the
+// push) keeps such a cell scheduled, so no message is ever stranded.
+class MpscMailbox {
+ public:
+  MpscMailbox();
+  ~MpscMailbox();
+  MpscMailbox(const MpscMailbox&) = delete;
+  MpscMailbox& operator=(const MpscMailbox&) = delete;
+  void push(Envelope&& e);  // any thread
+  bool pop(Envelope& out);  // the consumer only
+
+ private:
+  struct Node {
+    std::atomic<Node*> next{nullptr};
+    Envelope env;
+  };
+  alignas(64) std::atomic<Node*> tail_;
+  alignas(64) Node* head_;
+};
+
 class ActorCell : public std::enable_shared_from_this<ActorCell> {
  public:
   ActorCell(ActorSystem* sys, std::unique_ptr<Actor> actor, std::string path);
@@ -155,9 +179,15 @@ class ActorCell : public std::enable_shared_from_this<ActorCell> {
   std::unique_ptr<Actor> actor_;
   std::string path_;
   std::weak_ptr<ActorRefBase> ref_;
-  std::mutex mu_;
-  std::deque<Envelope> mailbox_;
+  std::mutex mu_;  // watchers_ only (the mail path takes no lock)
+  MpscMailbox mailbox_;
+  // Consumer-private (the actor's own turn): unstashed messages, delivered before the
+  // mailbox (Akka's Stash.unstashAll prepends), and the stash itself.
+  std::deque<Envelope> front_;
   std::deque<Envelope> stash_;
+  // Messages pushed or unstashed and not yet taken; raised BEFORE a push, so a dispatcher
+  // that releases the cell and then reads it cannot miss a concurrent tell().
+  std::atomic<int64_t> pending_{0};
   std::set<ActorRef> watchers_;
   std::atomic<bool> scheduled_{false};
   std::atomic<bool> stopped_{false};
@@ -274,6 +304,7 @@ class ActorSystem {
 
   std::mutex stats_mu_;
   SystemStats stats_;
+  std::atomic<uint64_t> delivered_{0};  // per-turn count without stats_mu_
   std::mutex hook_mu_;
   RemoteWatchHook remote_watch_;
   uint64_t dead_letters_logged_ = 0;
