@@ -643,15 +643,27 @@ def main() -> None:
         bad = [k for k, v in validated.items() if not v["validated"]]
         if bad:
             log(rank, f"VALIDATION FAILED for {bad}: {[validated[k] for k in bad]}")
+            # a timed-out wait poisons the communicator: every rank saw the same `bad` list
+            # (the flags were all-reduced), so all of them take part in the collective reset
+            try:
+                comm.reset()
+            except Exception as e:  # noqa: BLE001 - recorded, the run degrades to RCCL
+                engine_ok, reason = False, f"reset after failed validation: {e!r}"
+    ok_algos = {k for k, v in (validated or {}).items() if v["validated"]} | {"rccl", "rsag"}
     sweep = None
     if engine_ok and not args.no_tune and world > 1:  # at world = 1 every candidate is the same copy
         rccl_algos = () if args.no_rccl else ("rccl", "rsag") if world > 1 else ("rccl",)
+        cands = ("ll", "oneshot", "twoshot", "ring") + (("threshold",) if world > 1 else ()) + rccl_algos
         sweep = comm.tune(max_bytes=nbytes, dtype=dtype, iters=args.sweep_steps,
-                          candidates=("ll", "oneshot", "twoshot", "ring") + (("threshold",) if world > 1 else ())
-                          + rccl_algos, grids=(128, 256))
+                          candidates=tuple(c for c in cands if c in ok_algos), grids=(128, 256))
     if engine_ok and args.algo != "rccl":
         algo = args.algo
         chosen = comm._pick(nbytes) if algo == "auto" else algo
+        # never time an unvalidated kernel ("auto" without a tuned table is the size-default
+        # dispatch, checked by validate() above)
+        if world > 1 and chosen.split("@")[0] not in ok_algos | {"auto"}:
+            log(rank, f"headline algorithm {chosen} failed validation: timing RCCL instead")
+            algo = chosen = "rccl"
         if world == 1:  # XgmiComm::run: a 1-rank sum is an out-of-place copy, whatever the algorithm
             chosen = "copy (world=1)"
 
