@@ -7,6 +7,7 @@
 #include <netinet/tcp.h>
 #include <poll.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -23,34 +24,78 @@ using Clock = std::chrono::steady_clock;
 
 std::chrono::milliseconds ms_of(double s) { return std::chrono::milliseconds(static_cast<int64_t>(s * 1000.0)); }
 
-bool write_all(int fd, const void* p, size_t n) {
-  const char* b = static_cast<const char*>(p);
-  while (n > 0) {
-    const ssize_t k = ::send(fd, b, n, MSG_NOSIGNAL);
+// One frame = u32 length + payload in ONE gather write: one syscall and (TCP_NODELAY) one
+// segment per message instead of two - a protocol round is a chain of such messages.
+bool write_frame(int fd, const void* p, uint32_t n) {
+  uint32_t len = n;
+  iovec iov[2] = {{&len, 4}, {const_cast<void*>(p), n}};
+  int first = 0;
+  size_t left = 4 + static_cast<size_t>(n);
+  while (left > 0) {
+    msghdr mh{};
+    mh.msg_iov = iov + first;
+    mh.msg_iovlen = static_cast<size_t>(2 - first);
+    const ssize_t k = ::sendmsg(fd, &mh, MSG_NOSIGNAL);
     if (k < 0) {
       if (errno == EINTR) continue;
       return false;
     }
-    b += k;
-    n -= static_cast<size_t>(k);
+    left -= static_cast<size_t>(k);
+    size_t adv = static_cast<size_t>(k);
+    while (first < 2 && adv >= iov[first].iov_len) {
+      adv -= iov[first].iov_len;
+      iov[first].iov_len = 0;
+      ++first;
+    }
+    if (first < 2) {
+      iov[first].iov_base = static_cast<char*>(iov[first].iov_base) + adv;
+      iov[first].iov_len -= adv;
+    }
   }
   return true;
 }
 
-bool read_all(int fd, void* p, size_t n) {
-  char* b = static_cast<char*>(p);
-  while (n > 0) {
-    const ssize_t k = ::recv(fd, b, n, 0);
-    if (k == 0) return false;
-    if (k < 0) {
-      if (errno == EINTR) continue;
-      return false;
-    }
-    b += k;
-    n -= static_cast<size_t>(k);
+// Buffered frame reader: one recv() takes every frame the peer has queued (a round's
+// Scatter/Reduce burst arrives together), instead of two recv() calls per frame.
+class FrameReader {
+ public:
+  explicit FrameReader(int fd) : fd_(fd), buf_(64 << 10) {}
+  // Next frame's payload (valid until the next call); false at EOF / error / bad length.
+  bool next(const uint8_t** p, uint32_t* n) {
+    if (!fill(4)) return false;
+    uint32_t len;
+    std::memcpy(&len, buf_.data() + head_, 4);
+    if (len == 0 || len > (1u << 30)) return false;
+    if (!fill(4 + static_cast<size_t>(len))) return false;
+    *p = buf_.data() + head_ + 4;
+    *n = len;
+    head_ += 4 + static_cast<size_t>(len);
+    return true;
   }
-  return true;
-}
+
+ private:
+  bool fill(size_t need) {
+    while (tail_ - head_ < need) {
+      if (head_ > 0 && (buf_.size() - head_ < need || head_ == tail_)) {  // compact
+        std::memmove(buf_.data(), buf_.data() + head_, tail_ - head_);
+        tail_ -= head_;
+        head_ = 0;
+      }
+      if (buf_.size() < need) buf_.resize(need);
+      const ssize_t k = ::recv(fd_, buf_.data() + tail_, buf_.size() - tail_, 0);
+      if (k == 0) return false;
+      if (k < 0) {
+        if (errno == EINTR) continue;
+        return false;
+      }
+      tail_ += static_cast<size_t>(k);
+    }
+    return true;
+  }
+  int fd_;
+  std::vector<uint8_t> buf_;
+  size_t head_ = 0, tail_ = 0;
+};
 
 int connect_with_timeout(const std::string& host, int port, double timeout_s) {
   addrinfo hints{}, *res = nullptr;
@@ -229,20 +274,18 @@ void ClusterNode::accept_loop() {
 }
 
 void ClusterNode::reader_loop(int fd) {
-  std::vector<uint8_t> buf;
+  FrameReader in(fd);
   while (!stopping_.load()) {
+    const uint8_t* data = nullptr;
     uint32_t len = 0;
-    if (!read_all(fd, &len, 4)) break;
-    if (len == 0 || len > (1u << 30)) break;
-    buf.resize(len);
-    if (!read_all(fd, buf.data(), len)) break;
+    if (!in.next(&data, &len)) break;
     {
       std::lock_guard<std::mutex> g(stats_mu_);
       ++stats_.frames_in;
       stats_.bytes_in += len + 4;
     }
     try {
-      handle_frame(buf.data(), len);
+      handle_frame(data, len);
     } catch (const std::exception& e) {
       std::lock_guard<std::mutex> g(stats_mu_);
       ++stats_.decode_errors;
@@ -282,8 +325,7 @@ bool ClusterNode::send_frame(const std::string& address, const std::vector<uint8
       Writer hello;
       hello.u8(static_cast<uint8_t>(FrameKind::Hello));
       hello.str(address_);
-      const uint32_t hl = static_cast<uint32_t>(hello.bytes().size());
-      if (!write_all(c->fd, &hl, 4) || !write_all(c->fd, hello.bytes().data(), hl)) {
+      if (!write_frame(c->fd, hello.bytes().data(), static_cast<uint32_t>(hello.bytes().size()))) {
         ::close(c->fd);
         c->fd = -1;
         continue;
@@ -292,7 +334,7 @@ bool ClusterNode::send_frame(const std::string& address, const std::vector<uint8
       ++stats_.connects;
     }
     const uint32_t len = static_cast<uint32_t>(payload.size());
-    if (write_all(c->fd, &len, 4) && write_all(c->fd, payload.data(), payload.size())) {
+    if (write_frame(c->fd, payload.data(), len)) {
       std::lock_guard<std::mutex> gs(stats_mu_);
       ++stats_.frames_out;
       stats_.bytes_out += len + 4;
