@@ -19,8 +19,10 @@ the plane descriptor then travels in the cluster join (ClusterConfig.meta).
 from __future__ import annotations
 
 import itertools
+import os
 import threading
 import time
+import warnings
 from typing import Callable, Sequence
 
 import numpy as np
@@ -90,9 +92,16 @@ class PlaneJob:
             self.devices = list(devices) if devices is not None else [torch.cuda.current_device()] * P
         if len(self.devices) != P:
             raise ValueError("one device per worker")
-        if grid <= 0 and plane == "xgmi":  # workers sharing a GPU split its workgroups so every kernel stays resident
+        if plane == "xgmi":
             share = max(self.devices.count(d) for d in set(self.devices))
-            grid = max(8, 512 // share)
+            if grid <= 0:  # workers sharing a GPU split its workgroups so every kernel stays resident
+                grid = max(8, 512 // share)
+            queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+            if share > 1 and queues < 2 * share + 4:
+                warnings.warn(f"{share} plane workers share a GPU in this process with GPU_MAX_HW_QUEUES={queues}: "
+                              f"a round kernel queued behind a peer's in a shared hardware queue waits out its "
+                              f"deadline; set GPU_MAX_HW_QUEUES >= {2 * share + 4} before HIP initialises",
+                              RuntimeWarning, stacklevel=2)
         self.grid = grid
         self.system = C.ActorSystem("ClusterSystem", False)
         self.finished = threading.Event()
