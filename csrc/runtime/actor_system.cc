@@ -150,8 +150,42 @@ MpscMailbox::~MpscMailbox() {
   delete head_;
 }
 
+// Per-thread node cache: a dispatcher thread frees the nodes of the mail it consumes and
+// allocates nodes for the mail its actors send, so nodes cycle within a thread without
+// touching the allocator (glibc's per-thread cache holds only 7 blocks per size; a round's
+// burst of Scatter/Reduce messages overflowed it into the locked arena bins).
+struct MpscMailbox::NodeCache {
+  std::vector<Node*> free;
+  ~NodeCache() {
+    for (Node* n : free) delete n;
+  }
+  static NodeCache& local() {
+    thread_local NodeCache c;
+    return c;
+  }
+};
+
+MpscMailbox::Node* MpscMailbox::alloc_node() {
+  auto& c = NodeCache::local().free;
+  if (c.empty()) return new Node;
+  Node* n = c.back();
+  c.pop_back();
+  n->next.store(nullptr, std::memory_order_relaxed);
+  return n;
+}
+
+void MpscMailbox::free_node(Node* n) {
+  auto& c = NodeCache::local().free;
+  if (c.size() >= 1024) {
+    delete n;
+    return;
+  }
+  n->env = Envelope{};  // drop the payload / sender references now
+  c.push_back(n);
+}
+
 void MpscMailbox::push(Envelope&& e) {
-  Node* n = new Node;
+  Node* n = alloc_node();
   n->env = std::move(e);
   Node* prev = tail_.exchange(n, std::memory_order_acq_rel);
   prev->next.store(n, std::memory_order_release);  // the consumer may now reach n
@@ -163,7 +197,7 @@ bool MpscMailbox::pop(Envelope& out) {
   if (next == nullptr) return false;  // empty, or a push between its exchange and its link
   out = std::move(next->env);
   head_ = next;  // next becomes the stub
-  delete h;
+  free_node(h);
   return true;
 }
 

@@ -155,6 +155,9 @@ class MpscMailbox {
     std::atomic<Node*> next{nullptr};
     Envelope env;
   };
+  struct NodeCache;
+  static Node* alloc_node();
+  static void free_node(Node* n);
   alignas(64) std::atomic<Node*> tail_;
   alignas(64) Node* head_;
 };
