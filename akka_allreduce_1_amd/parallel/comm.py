@@ -152,6 +152,7 @@ class XgmiCommunicator:
         self.table: list[tuple[int, str]] = []  # (max bytes, algo) from tune(); empty = built-in policy
         self._default_grid = self._c.grid
         self._grid = self._c.grid
+        self._default_units = self._units = self._c.units_per_wg  # MXAR_TWOSHOT_UNITS or 0 (by size)
         self._dev = self.device.index
         self._launch: dict[str, tuple] = {}  # algo label -> (native Algo, grid)
         self._p2p = None
@@ -174,7 +175,10 @@ class XgmiCommunicator:
         decides; rank 0's choice is broadcast so every rank dispatches identically - a split
         decision would deadlock). `grids`: extra workgroup counts tried for twoshot / ring at
         sizes >= grid_min_bytes (labels "twoshot@256"); only counts <= the default grid, so
-        every workgroup stays resident. Returns one row per size: {bytes, <algo>_p50_us, choice}."""
+        every workgroup stays resident. Where the two-shot picks its fine geometry (blocks of
+        >= 32 MiB: world - 1 scatter units per workgroup), the coarse one is tried too
+        ("twoshot~1", "twoshot@256~1"): on one GPU fine wins by 4-6 %, over xGMI links the
+        measured choice decides. Returns one row per size: {bytes, <algo>_p50_us, choice}."""
         import torch.distributed as dist
 
         from ..ops import fill_uniform
@@ -199,6 +203,8 @@ class XgmiCommunicator:
                 labels.append(algo)
                 if algo in ("twoshot", "ring") and size >= grid_min_bytes:
                     labels += [f"{algo}@{g}" for g in extra]
+                if algo == "twoshot" and self.world > 2 and self._default_units == 0 and size // self.world >= (32 << 20):
+                    labels += ["twoshot~1"] + [f"twoshot@{g}~1" for g in extra]
             for algo in labels:
                 if algo == "oneshot" and (size > self.slot_bytes or size > (8 << 20)):
                     continue
@@ -264,10 +270,13 @@ class XgmiCommunicator:
         code = _KERNEL_DTYPES.get(inp.dtype)
         launch = self._launch.get(algo) if code is not None else None
         if launch is not None:  # the mean is fused into the kernel (scale applied to the fp32 sum)
-            kind, grid = launch
+            kind, grid, units = launch
             if self._grid != grid:
                 self._c.grid = grid
                 self._grid = grid
+            if self._units != units:  # two-shot geometry: scatter units per workgroup (0 = by size)
+                self._c.units_per_wg = units
+                self._units = units
             self._c.allreduce(inp.data_ptr(), out.data_ptr(), inp.numel(), code,
                               _current_stream(self._dev) if stream is None else stream, kind,
                               1.0 / self.world if op == "avg" else 1.0)
@@ -286,12 +295,15 @@ class XgmiCommunicator:
             if op == "avg":
                 out.div_(self.world)
         else:
-            name, _, g = algo.partition("@")  # "twoshot@256": workgroup count chosen by tune()
+            # "twoshot@256": workgroup count chosen by tune(); "twoshot@256~1": and one scatter
+            # unit per workgroup (coarse chunks) instead of the size-based geometry
+            label, _, u = algo.partition("~")
+            name, _, g = label.partition("@")
             if name == "threshold":  # no lag ring, or too large for one launch
                 return self.allreduce(inp, out, op=op, algo="twoshot")
             if name not in ALGOS:
                 raise ValueError(f"unknown algo {algo!r}")
-            self._launch[algo] = (ALGOS[name], int(g) if g else self._default_grid)
+            self._launch[algo] = (ALGOS[name], int(g) if g else self._default_grid, int(u) if u else self._default_units)
             return self.allreduce(inp, out, op=op, algo=algo, stream=stream)
         return out
 
@@ -423,6 +435,9 @@ class XgmiCommunicator:
         if self._grid != g:
             self._c.grid = g
             self._grid = g
+        if self._units != self._default_units:  # a tuned "~1" two-shot label must not leak in here
+            self._c.units_per_wg = self._default_units
+            self._units = self._default_units
         h = _H.AdamW()
         h.lr, (h.beta1, h.beta2), h.eps, h.weight_decay, h.step = lr, betas, eps, weight_decay, step
         self._c.step_adamw(grads.data_ptr(), params.data_ptr(), params.numel(), _dtype_code(params.dtype),

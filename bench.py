@@ -118,9 +118,12 @@ def validate(comm: XgmiCommunicator, n: int, dtype: torch.dtype, dev, rank: int,
     fill_uniform(x, seed=1000 + rank)
     ref = x.float()
     dist.all_reduce(ref)
-    y = comm.allreduce(x)
-    comm.check()
-    err = (y.float() - ref).abs().max().item()
+    try:  # a timed-out wait must still reach the flag all-reduce below (no rank left blocked)
+        y = comm.allreduce(x)
+        comm.check()
+        err = (y.float() - ref).abs().max().item()
+    except CommError:
+        err = float("inf")
     tol = 1e-5 * world if dtype == torch.float32 else 2e-2 * world  # one bf16 rounding of |sum| <= world
     ok = err <= tol
     flag = torch.tensor([0 if ok else 1], device=dev)
@@ -661,9 +664,16 @@ def main() -> None:
         chosen = comm._pick(nbytes) if algo == "auto" else algo
         # never time an unvalidated kernel ("auto" without a tuned table is the size-default
         # dispatch, checked by validate() above)
-        if world > 1 and chosen.split("@")[0] not in ok_algos | {"auto"}:
+        if world > 1 and chosen.split("@")[0].split("~")[0] not in ok_algos | {"auto"}:
             log(rank, f"headline algorithm {chosen} failed validation: timing RCCL instead")
             algo = chosen = "rccl"
+        elif world > 1 and sweep is not None:
+            # the tuned headline configuration (algorithm, grid, geometry) at the full size
+            ok_tuned, err_tuned = validate(comm, n, dtype, dev, rank, world)
+            if not ok_tuned:
+                log(rank, f"tuned headline {chosen} failed validation (max err {err_tuned:.3g}): timing RCCL")
+                comm.reset()
+                algo = chosen = "rccl"
         if world == 1:  # XgmiComm::run: a 1-rank sum is an out-of-place copy, whatever the algorithm
             chosen = "copy (world=1)"
 
