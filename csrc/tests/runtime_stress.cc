@@ -171,11 +171,72 @@ static int run_tcp(int rounds) {
   return 0;
 }
 
+// Lock-free mailbox under contention: producer threads tell numbered messages to one actor
+// that stashes everything while "closed" and unstashes when a TextMessage opens it; every
+// message must arrive exactly once and in order per producer (Akka's per-pair FIFO).
+namespace {
+class SeqActor final : public Actor {
+ public:
+  SeqActor(int producers, std::atomic<int>* total, std::atomic<int>* bad)
+      : next_(producers, 0), total_(total), bad_(bad) {}
+  void receive(Envelope& env, ActorContext& ctx) override {
+    if (auto* t = std::get_if<TextMessage>(&env.msg)) {
+      closed_ = t->text == "close";
+      if (!closed_) ctx.unstash_all();
+      return;
+    }
+    auto* c = std::get_if<CompleteAllreduce>(&env.msg);
+    if (c == nullptr) return;
+    if (closed_) {
+      ctx.stash(std::move(env));
+      return;
+    }
+    if (c->round != next_[c->srcId]) bad_->fetch_add(1);
+    next_[c->srcId] = c->round + 1;
+    total_->fetch_add(1);
+  }
+
+ private:
+  std::vector<int> next_;
+  bool closed_ = false;
+  std::atomic<int>* total_;
+  std::atomic<int>* bad_;
+};
+}  // namespace
+
+static int run_mailbox(int producers, int per) {
+  auto sys = std::make_shared<ActorSystem>("MailboxStress", ActorSystem::Mode::Threaded, 4);
+  std::atomic<int> total{0}, bad{0};
+  ActorRef a = sys->actor_of(std::make_unique<SeqActor>(producers, &total, &bad), "seq");
+  std::vector<std::thread> ts;
+  for (int k = 0; k < producers; ++k)
+    ts.emplace_back([&, k] {
+      for (int i = 0; i < per; ++i) a->tell(CompleteAllreduce{k, i, 0}, nullptr);
+    });
+  std::thread toggler([&] {  // close / open the actor while the producers run
+    for (int i = 0; i < 200; ++i) {
+      a->tell(TextMessage{i % 2 == 0 ? "close" : "open"}, nullptr);
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+    a->tell(TextMessage{"open"}, nullptr);
+  });
+  for (auto& t : ts) t.join();
+  toggler.join();
+  const bool ok = wait_until([&] { return total.load() == producers * per; }, 60.0);
+  sys->shutdown();
+  if (!ok || bad.load() != 0) {
+    std::fprintf(stderr, "mailbox: %d of %d delivered, %d out of order\n", total.load(), producers * per, bad.load());
+    return 1;
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   Logger::get().set_level(LogLevel::ERROR);
   const std::string only = argc > 1 ? argv[1] : "";
   int rc = 0;
-  if (only.empty() || only == "local") rc = run_local(4, 37, 3, 30);
+  if (only.empty() || only == "mailbox") rc = run_mailbox(6, 20000);
+  if (rc == 0 && (only.empty() || only == "local")) rc = run_local(4, 37, 3, 30);
   if (rc == 0 && (only.empty() || only == "local2")) rc = run_local(3, 9, 2, 30);
   if (rc == 0 && (only.empty() || only == "tcp")) rc = run_tcp(20);
   if (rc == 0 && (only.empty() || only == "plane")) rc = run_plane(3, 41, 4, 40);
