@@ -73,12 +73,16 @@ class PlaneJob:
                  timeout_s: float = 60.0, order_ref: bool = True, on_output: Callable | None = None,
                  max_peers: int | None = None, high_priority: bool = True, order_release: bool = True,
                  plane: str = "xgmi", hub: str | None = None, spin_us: int = 1000, reinit_on_loss: bool = False,
-                 split: bool = True):
+                 split: bool = True, keep_last: bool = False):
         """plane: "xgmi" (one threshold-kernel launch per round on the GPUs in `devices`) or
         "loopback" (host memory, no GPU: csrc/runtime/loopback_plane.h; `hub` names the
         workers' shared hub, default a fresh one; dtype float32, devices ignored).
         split: chunks fewer than the plane's workgroups are split into slices over several
-        workgroups, each chunk still one threshold decision (csrc/hip/xgmi_threshold.hip)."""
+        workgroups, each chunk still one threshold decision (csrc/hip/xgmi_threshold.hip).
+        sources: callables (AllReduceInputRequest -> tensor / array) or GPU tensors; a tensor is
+        fetched natively every round (no Python, no GIL).
+        keep_last: each worker keeps only its newest round output, natively (`last_output(k)`);
+        replaces keep_outputs / on_output, so no Python runs on the round path."""
         self.P = P
         self.n = data_size
         self.dtype = dtype
@@ -109,7 +113,6 @@ class PlaneJob:
         self.outputs: list[dict[int, tuple]] = [dict() for _ in range(P)]
         self.keep = keep_outputs
         self.on_output = on_output
-        self.stamps: list[float] = []  # perf_counter() when each round reached the master's barrier
         if plane == "loopback":
             hub = hub or f"planejob{next(_HUBS)}"
             self.planes = [C.loopback_plane(hub) for _ in range(P)]
@@ -124,7 +127,12 @@ class PlaneJob:
             if sources is None:
                 sources = [iota_source(data_size, torch.device("cuda", d), dtype, 1000.0 * k)
                            for k, d in enumerate(self.devices)]
-        self.sources = list(sources)
+        # a GPU tensor as a source: the same buffer every round, fetched without Python
+        # (hip.tensor_source) - no GIL on the round path for persistent gradient buffers
+        self.sources = [C.hip.tensor_source(src) if isinstance(src, torch.Tensor) else src for src in sources]
+        self.keep_last = keep_last
+        self._final_stamps: list[float] | None = None
+        self._last = [C.last_output_sink() for _ in range(P)] if keep_last else None
 
         def fin(r):
             self.rounds["n"] = r
@@ -132,12 +140,16 @@ class PlaneJob:
 
         self.master = self.system.master(P, th_allreduce, th_reduce, th_complete, max_lag, data_size, max_round,
                                          max_chunk_size, on_finished=fin, roundTimeoutMs=round_timeout_ms,
-                                         on_round=lambda r, e: self.stamps.append(time.perf_counter()),
                                          reinitOnLoss=reinit_on_loss)
         self.workers = [self.system.plane_worker(self.sources[k], self._sink(k), self.planes[k], f"worker{k}")
                         for k in range(P)]
 
-    def _sink(self, k: int) -> Callable:
+    def _sink(self, k: int):
+        if self._last is not None:  # keep_last: a native sink, no Python per round
+            return self._last[k]
+        if not self.keep and self.on_output is None:
+            return None
+
         def sink(out):
             if self.keep:
                 self.outputs[k][out.iteration] = (out.data, list(out.count))
@@ -162,6 +174,20 @@ class PlaneJob:
         self.system.await_idle(10.0)
         return time.perf_counter() - t0
 
+    @property
+    def stamps(self) -> list[float]:
+        """perf_counter() seconds at which each round reached the master's barrier (recorded
+        natively by the master: no Python callback on the round path)."""
+        if self._final_stamps is not None:
+            return self._final_stamps
+        return self.system.master_round_stamps(self.master)
+
+    def last_output(self, k: int):
+        """keep_last: worker k's newest AllReduceOutput (None before its first round)."""
+        if self._last is None:
+            raise RuntimeError("PlaneJob(keep_last=True) keeps the last output")
+        return self._last[k].last()
+
     def state(self) -> dict:
         return {"master": self.system.master_state(self.master),
                 "workers": [self.system.plane_worker_state(w) for w in self.workers]}
@@ -173,20 +199,24 @@ class PlaneJob:
         that free - a deadlock until the kernels' deadline."""
         import gc
 
+        if self._final_stamps is None:
+            self._final_stamps = self.system.master_round_stamps(self.master)
         self.system.shutdown()
         self.planes = []
         self.workers = []
         gc.collect()
 
 
-def distributed_plane_job(n: int, source: Callable, *, max_chunk_size: int, dtype: torch.dtype, rounds: int,
+def distributed_plane_job(n: int, source, *, max_chunk_size: int, dtype: torch.dtype, rounds: int,
                           th: float = 1.0, max_lag: int = 1, grid: int = 0, timeout_s: float = 300.0,
-                          on_output: Callable | None = None) -> dict:
+                          on_output: Callable | None = None, keep_last: bool = False) -> dict:
     """One plane worker per torch.distributed rank (one process per GPU), the master on rank 0,
     the reference's cluster shape: workers join rank 0's seed over TCP (127.0.0.1) and
     announce their plane descriptors in the join; the master relays them in InitWorkers and
     drives `rounds` rounds; the data moves over xGMI inside the planes. torch.distributed is
     used only to agree on the seed port and to hold the ranks until the master is done.
+    `source`: a callable or a GPU tensor (fetched natively every round); keep_last: a native
+    sink keeps the newest output (returned as "last") instead of calling `on_output`.
     Returns (rank 0) {"stamps": round completion times, "state": worker state}."""
     import torch.distributed as dist
 
@@ -197,7 +227,10 @@ def distributed_plane_job(n: int, source: Callable, *, max_chunk_size: int, dtyp
     system = C.ActorSystem("ClusterSystem", False)
     plane = C.hip.xgmi_plane(dev, dtype_code(dtype), n, max_peers=world, max_lag=max_lag, grid=grid,
                              timeout_s=min(60.0, timeout_s))
-    sink = (lambda out: on_output(out)) if on_output is not None else None
+    if isinstance(source, torch.Tensor):  # fetched natively every round (no GIL)
+        source = C.hip.tensor_source(source)
+    last = C.last_output_sink() if keep_last else None
+    sink = last if keep_last else (lambda out: on_output(out)) if on_output is not None else None
     worker = system.plane_worker(source, sink, plane, "worker")
     port = [free_port() if rank == 0 else 0]
     dist.broadcast_object_list(port, src=0)
@@ -210,13 +243,11 @@ def distributed_plane_job(n: int, source: Callable, *, max_chunk_size: int, dtyp
     cc.acceptable_heartbeat_pause_s = 10.0
     cc.auto_down_unreachable_after_s = -1.0
     cc.meta = plane.descriptor
-    stamps: list[float] = []
     fin = threading.Event()
     master = None
     if rank == 0:
         master = system.master(world, 1.0, th, th, max_lag, n, rounds - 1, max_chunk_size,
-                               on_finished=lambda r: fin.set(),
-                               on_round=lambda r, e: stamps.append(time.perf_counter()))
+                               on_finished=lambda r: fin.set())
     node = C.ClusterNode.start(system, cc)
     if master is not None:
         node.subscribe(master)
@@ -226,8 +257,10 @@ def distributed_plane_job(n: int, source: Callable, *, max_chunk_size: int, dtyp
     dist.broadcast_object_list(ok, src=0)
     plane.drain()
     system.await_idle(5.0)
+    stamps = system.master_round_stamps(master) if master is not None else []
     out = {"ok": bool(ok[0]), "stamps": stamps, "state": system.plane_worker_state(worker),
-           "plane": {"launches": plane.stats.launches, "chunk_elems": plane.chunk_elems, "chunks": plane.chunks}}
+           "plane": {"launches": plane.stats.launches, "chunk_elems": plane.chunk_elems, "chunks": plane.chunks},
+           "last": last.last() if last is not None else None}
     dist.barrier()
     node.leave()
     time.sleep(0.3)

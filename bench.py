@@ -469,24 +469,24 @@ def protocol_rounds(args, rank: int, world: int, dev) -> dict:
     chunk = max(1024, -(-block // 256))  # ~256 reduce units per worker: one per workgroup pair of CUs
     row: dict = {"workers": P, "bytes_per_worker": nbytes, "dtype": args.dtype, "rounds": rounds,
                  "warmup_rounds": warm, "th_reduce": 1.0, "th_complete": 1.0, "max_lag": 1,
-                 "max_chunk_size": chunk, "engine": "PlaneWorkerActor + XgmiRoundPlane (threshold kernel)"}
+                 "max_chunk_size": chunk, "engine": "PlaneWorkerActor + XgmiRoundPlane (threshold kernel)",
+                 "io": "tensor dataSource + native keep-last dataSink (no Python per round)"}
     try:
         if world == 1:
             xs = [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=700 + k) for k in range(P)]
             last = {}
-
-            def on_output(k, out):
-                if out.iteration == rounds - 1 and k == 0:
-                    last["y"] = out.data.clone()
-
             log(rank, f"protocol: {P} plane workers on this GPU, {rounds} rounds of {args.size_mib} MiB")
-            job = PlaneJob(P, n, max_chunk_size=chunk, dtype=dtype, max_round=rounds - 1,
-                           sources=[(lambda req, x=x: x) for x in xs], keep_outputs=False, on_output=on_output,
-                           timeout_s=20.0)
+            # the gradient buffers themselves are the dataSources and a native sink keeps the
+            # newest output: no Python (GIL) on the round path (engine.PlaneJob)
+            job = PlaneJob(P, n, max_chunk_size=chunk, dtype=dtype, max_round=rounds - 1, sources=xs,
+                           keep_outputs=False, keep_last=True, timeout_s=20.0)
             try:
                 job.run(timeout=300)
                 stamps = job.stamps
                 lat = job.system.plane_worker_state(job.workers[0])["round_latency"]
+                o = job.last_output(0)
+                if o is not None and o.iteration == rounds - 1:
+                    last["y"] = o.data.clone()
                 row["note"] = "N=1: 2 workers share one GPU (one HBM, no xGMI)"
             finally:
                 job.shutdown()
@@ -495,15 +495,12 @@ def protocol_rounds(args, rank: int, world: int, dev) -> dict:
         else:
             x = fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=700 + rank)
             last = {}
-
-            def on_output(out):
-                if out.iteration == rounds - 1:
-                    last["y"] = out.data.clone()
-
             grid = max(8, 512 // world) if args.share_device else 0
             log(rank, f"protocol: one plane worker per rank, {rounds} rounds of {args.size_mib} MiB")
-            res = distributed_plane_job(n, lambda req: x, max_chunk_size=chunk, dtype=dtype, rounds=rounds,
-                                        grid=grid, on_output=on_output, timeout_s=120.0)
+            res = distributed_plane_job(n, x, max_chunk_size=chunk, dtype=dtype, rounds=rounds,
+                                        grid=grid, keep_last=True, timeout_s=120.0)
+            if res["last"] is not None and res["last"].iteration == rounds - 1:
+                last["y"] = res["last"].data.clone()
             stamps = res["stamps"]
             lat = res["state"]["round_latency"]
             # the kernel sums in WORKER-id order (ids are dense in the master's join order, not

@@ -412,6 +412,28 @@ PYBIND11_MODULE(_C, m) {
         return "AllReduceOutput(" + vec_str(o.data) + ", iteration=" + std::to_string(o.iteration) + ")";
       });
 
+  py::class_<NativeSource>(m, "NativeSource",
+                           "A dataSource that runs without Python (hip.tensor_source); pass it to plane_worker");
+  py::class_<NativeSink>(m, "NativeSink", "A dataSink that runs without Python (last_output_sink)")
+      .def("last", [](NativeSink& k) -> py::object {
+        std::lock_guard<std::mutex> g(k.keep->mu);
+        if (!k.keep->out) return py::none();
+        return py::cast(*k.keep->out);
+      }, "the newest AllReduceOutput (None before the first round)")
+      .def_property_readonly("rounds", [](NativeSink& k) {
+        std::lock_guard<std::mutex> g(k.keep->mu);
+        return k.keep->rounds;
+      });
+  m.def("last_output_sink", [] {
+    auto keep = std::make_shared<LastOutput>();
+    return NativeSink{[keep](const AllReduceOutput& o) {
+                        std::lock_guard<std::mutex> g(keep->mu);
+                        keep->out = o;  // holds the round output's buffer until the next round
+                        keep->rounds++;
+                      },
+                      keep};
+  }, "dataSink keeping only the newest round output, without the GIL (plane workers)");
+
   // ---------------------------------------------------------------- core helpers
   m.def("f32_threshold_count", &f32_threshold_count, py::arg("threshold"), py::arg("peers"));
   m.def("f32_threshold_chunks", &f32_threshold_chunks, py::arg("threshold"), py::arg("peers"), py::arg("numChunks"));
@@ -531,8 +553,10 @@ PYBIND11_MODULE(_C, m) {
           py::arg("reinitOnLoss") = false, py::arg("resumeOnJoin") = false)
       .def("plane_worker", [](ActorSystem& s, py::object source, py::object sink, std::shared_ptr<RoundPlane> plane,
                               std::string name) {
-            auto a = std::make_unique<PlaneWorkerActor>(make_plane_source(std::move(source)),
-                                                        make_sink(std::move(sink)), std::move(plane));
+            DataSource src = py::isinstance<NativeSource>(source) ? source.cast<NativeSource&>().fn
+                                                                  : make_plane_source(std::move(source));
+            DataSink snk = py::isinstance<NativeSink>(sink) ? sink.cast<NativeSink&>().fn : make_sink(std::move(sink));
+            auto a = std::make_unique<PlaneWorkerActor>(std::move(src), std::move(snk), std::move(plane));
             return s.actor_of(std::move(a), std::move(name));
           }, py::arg("source"), py::arg("sink") = py::none(), py::arg("plane"), py::arg("name") = "",
           "Round-granular worker (csrc/runtime/plane_worker.h): the reference protocol with one plane launch "
@@ -615,6 +639,8 @@ PYBIND11_MODULE(_C, m) {
         d["describe"] = c.describe();
         return d;
       })
+      .def("master_round_stamps", [](ActorSystem&, ActorRef ref) { return master_of(ref)->round_stamps(); },
+           "perf_counter()-compatible seconds at which each round reached the master's barrier")
       .def("master_state", [](ActorSystem&, ActorRef ref) {
         auto* ma = master_of(ref);
         const MasterCore& c = ma->core();

@@ -7,7 +7,11 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <mutex>
+#include <optional>
+
 #include "../core/protocol.h"
+#include "../runtime/allreduce_actors.h"
 
 namespace py = pybind11;
 
@@ -42,5 +46,21 @@ void register_device_payload_hooks(DevicePayloadToPy to_py, PyToDevicePayload fr
 // synchronisation). nullptr if `obj` is not a device tensor.
 void register_typed_payload_hook(PyToDevicePayload from_py);
 Payload typed_payload_from_py(const py::handle& obj);
+
+// dataSource / dataSink that run without Python: plane_worker() takes them as they are, so a
+// round's fetch and flush take no GIL (hip.tensor_source: a persistent device buffer;
+// last_output_sink: keeps the newest AllReduceOutput for the caller to read).
+struct NativeSource {
+  DataSource fn;
+};
+struct LastOutput {
+  std::mutex mu;
+  std::optional<AllReduceOutput> out;
+  uint64_t rounds = 0;
+};
+struct NativeSink {
+  DataSink fn;
+  std::shared_ptr<LastOutput> keep;
+};
 
 }  // namespace mxar

@@ -172,6 +172,33 @@ Payload py_to_device_payload_typed(const py::handle& obj) {
 }
 }  // namespace
 
+// dataSource over one persistent device tensor, without Python per round: each fetch returns
+// the same buffer, ordered after the work queued on the stream that was torch's current
+// stream at creation (an event only if that stream is busy, as the per-round import does).
+NativeSource tensor_source(py::object obj) {
+  const TorchRefs& T = torch_refs();
+  if (!py::isinstance(obj, T.tensor_type) || !obj.attr("is_cuda").cast<bool>())
+    throw py::type_error("tensor_source needs a GPU tensor");
+  if (!obj.attr("is_contiguous")().cast<bool>()) throw py::value_error("tensor_source needs a contiguous tensor");
+  const py::object dt = obj.attr("dtype");
+  const int code = dt.is(T.f32) ? 0 : dt.is(T.bf16) ? 1 : dt.is(T.f16) ? 2 : -1;
+  if (code < 0) throw py::type_error("plane input must be float32, bfloat16 or float16");
+  const uintptr_t ptr = obj.attr("data_ptr")().cast<uintptr_t>();
+  const size_t n = obj.attr("numel")().cast<size_t>();
+  const int dev = obj.attr("get_device")().cast<int>();
+  const uintptr_t cs = !T.raw_stream.is_none()
+                           ? T.raw_stream(dev).cast<uintptr_t>()
+                           : py::module_::import("torch").attr("cuda").attr("current_stream")(dev).attr("cuda_stream").cast<uintptr_t>();
+  auto holder = std::make_shared<PyCallable>(obj);  // keeps the tensor alive; released with the GIL
+  std::shared_ptr<void> mem(holder, reinterpret_cast<void*>(ptr));
+  const hipStream_t ps = reinterpret_cast<hipStream_t>(cs);
+  return NativeSource{[mem, n, dev, code, ps](const AllReduceInputRequest&) -> AllReduceInput {
+    ReadyEvent ready = hipStreamQuery(ps) == hipSuccess ? nullptr : record_ready(ps);
+    (void)hipGetLastError();
+    return AllReduceInput{std::make_shared<DevicePayload>(mem, 0, n, dev, nullptr, std::move(ready), code)};
+  }};
+}
+
 static hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 static const void* as_cptr(uintptr_t p) { return reinterpret_cast<const void*>(p); }
 static void* as_ptr(uintptr_t p) { return reinterpret_cast<void*>(p); }
@@ -180,6 +207,8 @@ void bind_hip(py::module_& m) {
   py::module_ h = m.def_submodule("hip", "HIP/CDNA4 data plane (gfx950)");
   register_device_payload_hooks(&device_payload_to_py, &py_to_device_payload);
   register_typed_payload_hook(&py_to_device_payload_typed);
+  h.def("tensor_source", &tensor_source, py::arg("tensor"),
+        "dataSource for a plane worker: the same GPU tensor every round, no Python (GIL) per round");
 
   py::class_<DevicePlane, DataPlane, std::shared_ptr<DevicePlane>>(h, "DevicePlane")
       .def_property_readonly("device", &DevicePlane::device)

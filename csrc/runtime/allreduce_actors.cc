@@ -1,5 +1,6 @@
 #include "allreduce_actors.h"
 
+#include <chrono>
 
 #include "../core/log.h"
 
@@ -169,7 +170,17 @@ void MasterActor::finished(int rounds) {
 }
 
 void MasterActor::round_completed(int round, int64_t epoch) {
+  {
+    std::lock_guard<std::mutex> g(stamp_mu_);
+    if (stamps_.size() < (size_t{1} << 22))
+      stamps_.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count());
+  }
   if (on_round_) on_round_(round, epoch);
+}
+
+std::vector<double> MasterActor::round_stamps() const {
+  std::lock_guard<std::mutex> g(stamp_mu_);
+  return stamps_;
 }
 
 }  // namespace mxar

@@ -5,6 +5,8 @@
 // protocol decisions live in WorkerCore / MasterCore.
 #pragma once
 
+#include <mutex>
+
 #include <functional>
 #include <memory>
 
@@ -60,6 +62,9 @@ class MasterActor final : public Actor, public MasterEffects {
   void arm_round_timer(int64_t epoch, int round, int ms) override;
 
   const MasterCore& core() const { return core_; }
+  // steady_clock (CLOCK_MONOTONIC = Python's perf_counter) seconds at which each round
+  // reached the barrier - recorded natively, so timing a job needs no callback per round
+  std::vector<double> round_stamps() const;
 
  private:
   int handle_of(const ActorRef& ref, bool create);
@@ -69,6 +74,8 @@ class MasterActor final : public Actor, public MasterEffects {
   FinishedCallback on_finished_;
   RoundCallback on_round_;
   ActorContext* ctx_ = nullptr;
+  mutable std::mutex stamp_mu_;
+  std::vector<double> stamps_;
 };
 
 }  // namespace mxar

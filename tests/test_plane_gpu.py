@@ -562,3 +562,27 @@ def test_split_matches_unsplit_outputs():
     for key in res[0]:
         np.testing.assert_array_equal(res[0][key][0], res[1][key][0], err_msg=str(key))
         assert res[0][key][1] == res[1][key][1]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_tensor_sources_and_native_keep_last_sink(dtype):
+    """GPU tensors as dataSources (hip.tensor_source: fetched natively, ordered after torch's
+    stream) and the native keep-last sink: no Python per round, outputs exact."""
+    P, n, rounds = 2, (1 << 20) + 3, 7
+    xs = [torch.empty(n, dtype=dtype, device=DEV) for _ in range(P)]
+    job = PlaneJob(P, n, max_chunk_size=4096, max_lag=1, max_round=rounds - 1, dtype=dtype, sources=xs,
+                   keep_outputs=False, keep_last=True, timeout_s=20.0)
+    try:
+        for k, x in enumerate(xs):  # queued on torch's stream, no sync: the source's event orders it
+            x.copy_(torch.arange(n, device=DEV, dtype=torch.float32).remainder_(97).add_(k).to(dtype))
+        job.run(timeout=120)
+        ref = (xs[0].float() + xs[1].float()).to(dtype)
+        for k in range(P):
+            o = job.last_output(k)
+            assert o.iteration == rounds - 1 and all(c == P for c in o.count)
+            assert torch.equal(o.data, ref), k
+            st = job.system.plane_worker_state(job.workers[k])
+            assert st["stats"]["plane_errors"] == 0 and st["stats"]["rounds_completed"] == rounds, st
+        assert len(job.stamps) == rounds
+    finally:
+        job.shutdown()

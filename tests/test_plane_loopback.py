@@ -292,3 +292,24 @@ def test_make_plane_worker_with_a_loopback_hub():
             make_plane_worker(system, host_iota_source(n), data_size=n)
     finally:
         system.shutdown()
+
+
+def test_loopback_native_keep_last_sink_and_master_stamps():
+    """keep_last: a native dataSink per worker keeps only the newest round output (no Python
+    on the round path); the master stamps every round barrier natively."""
+    P, n, chunk, rounds = 3, 1001, 50, 9
+    job = PlaneJob(P, n, max_chunk_size=chunk, max_lag=1, max_round=rounds - 1, plane="loopback",
+                   keep_outputs=False, keep_last=True)
+    try:
+        job.run(timeout=60)
+        st = job.stamps
+        assert len(st) == rounds and all(b >= a for a, b in zip(st, st[1:])), st
+        assert abs(st[-1] - __import__("time").perf_counter()) < 60  # perf_counter timebase
+        for k in range(P):
+            o = job.last_output(k)
+            assert o.iteration == rounds - 1 and all(c == P for c in o.count)
+            np.testing.assert_array_equal(np.asarray(o.data), expected(n, rounds - 1, range(P)).astype(F))
+        assert not any(job.outputs[k] for k in range(P))  # nothing kept by Python
+    finally:
+        job.shutdown()
+    assert len(job.stamps) == rounds  # still readable after shutdown

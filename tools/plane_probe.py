@@ -79,6 +79,8 @@ def main() -> None:
     ap.add_argument("--spin-us", type=int, default=1000, help="completion-thread polling before blocking")
     ap.add_argument("--no-order-release", action="store_true",
                     help="release round outputs without waiting for the default stream (A/B knob)")
+    ap.add_argument("--python-io", action="store_true",
+                    help="Python dataSource / dataSink callables (default: tensor sources + native keep-last sink)")
     ap.add_argument("--stamps", action="store_true",
                     help="phase stamps of every worker's LAST round kernel (same GPU clock for all workers)")
     a = ap.parse_args()
@@ -100,12 +102,15 @@ def main() -> None:
             if out.iteration == rounds - 1:
                 last[k] = out.data.clone()
 
-        job = PlaneJob(a.P, n, max_chunk_size=chunk, dtype=dtype, max_round=a.rounds - 1,
-                       sources=[(lambda req, x=x: x) for x in xs], keep_outputs=False, on_output=on_output,
-                       timeout_s=a.timeout, high_priority=a.priority == "high",
-                       order_release=not a.no_order_release, spin_us=a.spin_us)
+        if a.python_io:  # Python dataSource / dataSink every round (GIL on the round path)
+            io = dict(sources=[(lambda req, x=x: x) for x in xs], keep_outputs=False, on_output=on_output)
+        else:  # native: the tensors as sources, a native keep-last sink
+            io = dict(sources=xs, keep_outputs=False, keep_last=True)
+        job = PlaneJob(a.P, n, max_chunk_size=chunk, dtype=dtype, max_round=a.rounds - 1, timeout_s=a.timeout,
+                       high_priority=a.priority == "high", order_release=not a.no_order_release, spin_us=a.spin_us,
+                       **io)
         row = {"P": a.P, "bytes": S, "chunk": chunk, "priority": a.priority, "order_release": not a.no_order_release, "spin_us": a.spin_us,
-               "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}
+               "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "io": "python" if a.python_io else "native"}
         bufs = []
         if a.stamps:
             bufs = [torch.zeros(job.grid * 8, dtype=torch.int64, device=dev) for _ in job.planes]
@@ -122,6 +127,11 @@ def main() -> None:
                 row["ms_per_round"] = round(per * 1e3, 4)
                 row["algbw_GBps"] = round(S / per / 1e9, 2)
             row["errors"] = [w["stats"]["plane_errors"] for w in st["workers"]]
+            if not a.python_io:
+                for k in range(a.P):
+                    o = job.last_output(k)
+                    if o is not None and o.iteration == a.rounds - 1:
+                        last[k] = o.data.clone()
             row["validated"] = all(torch.equal(last.get(k, torch.empty(0)), ref) for k in range(a.P))
             row["lat_p50_ms"] = [round(w["round_latency"]["p50_ms"], 3) for w in st["workers"]]
             if bufs:
