@@ -129,7 +129,8 @@ class PlaneJob:
                            for k, d in enumerate(self.devices)]
         # a GPU tensor as a source: the same buffer every round, fetched without Python
         # (hip.tensor_source) - no GIL on the round path for persistent gradient buffers
-        self.sources = [C.hip.tensor_source(src) if isinstance(src, torch.Tensor) else src for src in sources]
+        self.sources = [C.hip.tensor_source(src) if isinstance(src, torch.Tensor) and plane == "xgmi" else src
+                        for src in sources]
         self.keep_last = keep_last
         self._final_stamps: list[float] | None = None
         self._last = [C.last_output_sink() for _ in range(P)] if keep_last else None
