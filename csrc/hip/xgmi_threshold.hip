@@ -492,7 +492,12 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
       }
     }
     if (k == 0) sh_flag = aborted ? 1 : 0;
-    if (acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    // No acquire here: the gate orders this round's STORES into the peers' rows after the
+    // peers' reads of those rows (write-after-read - the progress word was published after
+    // them, and our stores issue only once the poll has returned: the wait below + the
+    // barrier). Nothing peer-written is LOADED before phase 2's and phase 3's own acquires
+    // (flag / force / decision words are sc1 loads). A system-scope acquire here cost every
+    // workgroup an L1 + L2 invalidate on the round's critical path.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
