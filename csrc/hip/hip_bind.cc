@@ -175,6 +175,7 @@ Payload py_to_device_payload_typed(const py::handle& obj) {
 // dataSource over one persistent device tensor, without Python per round: each fetch returns
 // the same buffer, ordered after the work queued on the stream that was torch's current
 // stream at creation (an event only if that stream is busy, as the per-round import does).
+// That stream must outlive the source (torch's default / current streams do).
 NativeSource tensor_source(py::object obj) {
   const TorchRefs& T = torch_refs();
   if (!py::isinstance(obj, T.tensor_type) || !obj.attr("is_cuda").cast<bool>())
