@@ -173,7 +173,11 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a)
 void launch_adamw(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {
   dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
     using E = decltype(tag);
+    // P is a template constant wherever it can be: the reduce then issues every source's
+    // load before the first add (the PT = 0 loop waits on each load in turn) - P = 1 is the
+    // single-GPU optimizer step
     switch (a.P) {
+      case 1: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 1>), grid, dim3(kCommThreads), 0, s, a); break;
       case 2: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 2>), grid, dim3(kCommThreads), 0, s, a); break;
       case 4: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 4>), grid, dim3(kCommThreads), 0, s, a); break;
       case 8: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 8>), grid, dim3(kCommThreads), 0, s, a); break;
