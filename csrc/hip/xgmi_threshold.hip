@@ -326,6 +326,12 @@ __device__ __forceinline__ bool last_slice(uint32_t* ctr, int S, int* sh) {
 
 }  // namespace
 
+// A per-chunk count: a `sc1` store (leaves this XCD's L2), read back by the round's last
+// workgroup with `sc1` loads after the ticket count - no release / acquire needed.
+__device__ __forceinline__ void put_count(int32_t* p, int32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <class E>
 __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   constexpr int es = 16 / E::ELEMS;
@@ -537,7 +543,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
     uint64_t* const dec = split ? &a.split_dec[c] : nullptr;
     if (void_round) {  // nothing reduced, nothing sent
       if (len > 0) zero_fill<E>(out + (bstart_own + cstart) * es, len);
-      if (threadIdx.x == 0 && counts) counts[static_cast<int64_t>(r) * a.nch + c] = 0;
+      if (threadIdx.x == 0 && counts) put_count(counts + static_cast<int64_t>(r) * a.nch + c, 0);
       continue;
     }
     if (threadIdx.x < 64) {
@@ -626,7 +632,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
     if (threadIdx.x < static_cast<unsigned>(P) && static_cast<int>(threadIdx.x) != r)
       st_flag(f2c(a, static_cast<int>(threadIdx.x), row * P + r, c), static_cast<uint32_t>(cnt));
     if (threadIdx.x == 0) {
-      if (counts) counts[static_cast<int64_t>(r) * a.nch + c] = take ? cnt : 0;
+      if (counts) put_count(counts + static_cast<int64_t>(r) * a.nch + c, take ? cnt : 0);
       if (!ref && tickets) add_ctl(&ctl[3], 1u);
     }
     publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : f2(a, k, row * P + r, c); }, P, epoch, rel);
@@ -696,8 +702,8 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
           }
           if (!adopt) {
             if (counts)
-              counts[static_cast<int64_t>(j) * a.nch + c] =
-                  take ? static_cast<int32_t>(ld_flag(f2c(a, r, row * P + j, c))) : 0;
+              put_count(counts + static_cast<int64_t>(j) * a.nch + c,
+                        take ? static_cast<int32_t>(ld_flag(f2c(a, r, row * P + j, c))) : 0);
             if (split) dec_publish(dec, epoch, take != 0, 0u);
           }
           sh_flag = take;
@@ -770,7 +776,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
           if (threadIdx.x == 0) {
             uint64_t d = 0;
             if (dec_claim(dec, epoch, deadline, err, &d)) {
-              if (counts) counts[static_cast<int64_t>(j) * a.nch + c] = 0;
+              if (counts) put_count(counts + static_cast<int64_t>(j) * a.nch + c, 0);
               dec_publish(dec, epoch, false, 0u);
               sh_flag = 0;
             } else {
@@ -782,7 +788,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
           take = sh_flag != 0;
           __syncthreads();
         } else if (threadIdx.x == 0 && counts) {
-          counts[static_cast<int64_t>(j) * a.nch + c] = 0;
+          put_count(counts + static_cast<int64_t>(j) * a.nch + c, 0);
         }
         if (len > 0) {
           if (take)
@@ -798,18 +804,22 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   ps.flush();
 
   // Round end: the last workgroup resets the per-round counters, records the round and
-  // tells every peer that this rank is done with row `row`. acq_rel ticket (unlike
-  // finish_launch): the progress word promises peers that EVERY workgroup's reads of the
-  // row are done, so each ticket is ordered after its workgroup's loads.
+  // tells every peer that this rank is done with row `row`. The progress word promises the
+  // peers that EVERY workgroup's reads of the row are done: every wave drains its memory
+  // operations before the workgroup barrier, so the ticket follows them. The ticket itself
+  // is relaxed (an acq_rel one was an L2 writeback + invalidate per workgroup on the round's
+  // tail): the only data the last workgroup reads back are the counts, stored `sc1`
+  // (put_count) before the drain and loaded `sc1` - the guide's fence-free hand-off form.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sh_flag = t == static_cast<uint32_t>(G) - 1 ? 1 : 0;
   }
   __syncthreads();
   const bool last = sh_flag != 0;
   if (last && counts != nullptr && a.counts_host != nullptr) {
-    // every workgroup's counts are visible here (their tickets released them, ours acquired)
+    // every workgroup's counts are visible here (sc1 stores drained before their tickets)
     int32_t* dst = a.counts_host + static_cast<int64_t>(y) * P * a.nch;
     for (int64_t i = threadIdx.x; i < static_cast<int64_t>(P) * a.nch; i += kCommThreads)
       __hip_atomic_store(dst + i, __hip_atomic_load(counts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
