@@ -35,12 +35,15 @@ __device__ __forceinline__ void copy_plain(char* dst, const char* src, int64_t l
 __device__ __forceinline__ void finish_with_barrier(const CommArgs& a, uint32_t* ctl, uint32_t epoch, int r,
                                                     uint64_t deadline, uint32_t* err) {
   __shared__ int last;
+  // The last workgroup's FB flags tell the peers that EVERY workgroup's slab reads of this
+  // launch are done: every wave drains its memory operations before the barrier, so each
+  // ticket follows its workgroup's loads. The ticket is relaxed - nothing is read back after
+  // it, and an acq_rel one was an L2 writeback + invalidate per workgroup (the threshold
+  // kernel's round end measured -5 % at 64-256 MiB without it, profiles/round2/README.md).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    // acq_rel (unlike finish_launch's relaxed ticket): the last workgroup's FB flags tell the
-    // peers that EVERY workgroup's slab reads of this launch are done, so each ticket must
-    // be ordered after its workgroup's loads and the last one must see all of them.
-    const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = t == gridDim.x - 1 ? 1 : 0;
   }
   __syncthreads();
