@@ -315,7 +315,9 @@ __device__ __forceinline__ bool last_slice(uint32_t* ctr, int S, int* sh) {
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    const uint32_t t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    // relaxed: the system release above already ordered this slice's stores, and the last
+    // slice reads nothing of the others' (it only publishes flags, behind its own release)
+    const uint32_t t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool last = t == static_cast<uint32_t>(S) - 1u;
     if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *sh = last ? 1 : 0;

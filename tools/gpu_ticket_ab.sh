@@ -9,7 +9,7 @@ export HSA_ENABLE_IPC_MODE_LEGACY=0
 for i in 1 2 3; do
   for b in prev head; do
     s=tools/plane_probe.py; [ $b = prev ] && s=abtest/prev/tools/plane_probe.py
-    timeout -k 10 200 python -u $s --P 2 --sizes 1M 64M 256M --rounds 300 2>> $O/ab.err | sed "s/^{/{\"build\": \"$b\", /" >> $O/ab.jsonl || exit $?
+    timeout -k 10 200 python -u $s --P 2 --sizes 1M 64M 256M --rounds 300 --units 64 2>> $O/ab.err | sed "s/^{/{\"build\": \"$b\", /" >> $O/ab.jsonl || exit $?
   done
 done
 python - <<'PY'
