@@ -282,8 +282,9 @@ __device__ __forceinline__ void finish_launch(uint32_t* ctl, uint32_t epoch) {
     // (slot reuse is guarded by the kernels' own phase flags). An acq_rel at agent scope
     // would be a `buffer_wbl2` per workgroup, writing back the XCD's dirty L2 lines
     // mid-kernel (e.g. AdamW state). Kernels whose last workgroup DOES tell peers that all
-    // reads are done (xgmi_coll.hip FB barrier, xgmi_threshold.hip progress words) keep
-    // an acq_rel ticket.
+    // reads are done (xgmi_coll.hip FB barrier, xgmi_threshold.hip progress words) drain
+    // every wave (s_waitcnt vmcnt(0)) before their barrier and then take a relaxed ticket
+    // too.
     const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == gridDim.x - 1) {
       __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
