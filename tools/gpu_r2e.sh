@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out/r2e
 O=gpurun_out/r2e
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-for n in 2 8; do
+for n in ${NS:-2 8}; do
   timeout -k 10 500 python -u -m torch.distributed.run --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29550 + n)) \
       bench.py --gpus $n --share-device --steps 10 --warmup 3 --no-dp > $O/bench_share_n$n.json 2> $O/bench_share_n$n.err
   rc=$?; echo "n=$n rc=$rc"; [ $rc -eq 0 ] || { tail -20 $O/bench_share_n$n.err; exit $rc; }
