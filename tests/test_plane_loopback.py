@@ -313,3 +313,22 @@ def test_loopback_native_keep_last_sink_and_master_stamps():
     finally:
         job.shutdown()
     assert len(job.stamps) == rounds  # still readable after shutdown
+
+
+def test_tensor_source_rejects_host_tensors_and_loopback_keeps_callables():
+    """hip.tensor_source takes GPU tensors only (checked before any HIP call); on the
+    loopback plane PlaneJob leaves sources as they are."""
+    import torch
+
+    with pytest.raises(TypeError):
+        C.hip.tensor_source(torch.zeros(8))
+    with pytest.raises(TypeError):
+        C.hip.tensor_source([1.0, 2.0])
+    src = host_iota_source(16, 0.0)
+    job = PlaneJob(2, 16, max_chunk_size=4, max_round=1, plane="loopback", sources=[src, src], keep_last=True)
+    try:
+        assert job.sources[0] is src
+        job.run(timeout=30)
+        assert job.last_output(1).iteration == 1
+    finally:
+        job.shutdown()
