@@ -138,13 +138,20 @@ __device__ __forceinline__ bool unit_in_bounds(const CommArgs& a, int64_t off, i
 
 // Push len elements from ordinary memory into a (peer's) slab with write-through stores,
 // 16 B per lane, 4 packs in flight per lane.
+// Packs in flight per lane in the slab copies (scatter / gather phases). The persistent
+// grids run 2 workgroups per CU, so bytes in flight come from this unroll.
+#ifndef MXAR_COPY_U
+#define MXAR_COPY_U 8
+#endif
+constexpr int kCopyU = MXAR_COPY_U;
+
 template <class E>
 __device__ __forceinline__ void copy_to_slab(char* slab_dst, const char* src, int64_t len) {
   const int64_t npk = len / E::ELEMS;
   const Pack16* s = reinterpret_cast<const Pack16*>(src);
   const __amdgpu_buffer_rsrc_t rd = slab_rsrc(slab_dst);
   int64_t i = threadIdx.x;
-  constexpr int U = 4;
+  constexpr int U = kCopyU;
   for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
     Pack16 v[U];
 #pragma unroll
@@ -165,7 +172,7 @@ __device__ __forceinline__ void copy_from_slab(char* dst, const char* slab_src, 
   const __amdgpu_buffer_rsrc_t rs = slab_rsrc(slab_src);
   const __amdgpu_buffer_rsrc_t rd = slab_rsrc(dst);
   int64_t i = threadIdx.x;
-  constexpr int U = 4;
+  constexpr int U = kCopyU;
   for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
     Pack16 v[U];
 #pragma unroll
