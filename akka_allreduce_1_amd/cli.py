@@ -97,8 +97,16 @@ def master_main(argv: list[str] | None = None) -> int:
     ap.add_argument("--linger", action="store_true", help="keep running after the last round (reference behaviour)")
     ap.add_argument("--checkpoint", default=None, help="write {round, epoch} here after every completed round")
     ap.add_argument("--resume", action="store_true", help="start at the round after the one in --checkpoint")
+    ap.add_argument("--bridge", type=int, default=None, metavar="PORT",
+                    help="serve the control bridge (JSON lines, docs/BRIDGE.md) on PORT (0 = any free port)")
+    ap.add_argument("--external-rounds", action="store_true",
+                    help="bridge clients drive the rounds with StartAllreduce (the master only inits workers)")
     _common(ap)
     args = ap.parse_args(argv)
+    if args.bridge is not None:
+        args.set.append(f"mxar.bridge.port={args.bridge}")
+    if args.external_rounds:
+        args.set.append("mxar.bridge.external-rounds=true")
     cfg = _load(args)
     total = args.totalWorkers if args.totalWorkers is not None else int(cfg["mxar.allreduce.total-workers"])
     data_size = args.dataSize if args.dataSize is not None else (
@@ -136,7 +144,13 @@ def master_main(argv: list[str] | None = None) -> int:
                            reinitOnLoss=bool(cfg["mxar.allreduce.reinit-on-loss"]),
                            resumeOnJoin=bool(cfg["mxar.allreduce.resume-on-join"]), on_finished=finished, name="master",
                            startRound=start_round, on_round=on_round,
-                           roundTimeoutMs=int(float(cfg["mxar.allreduce.round-timeout"]) * 1000))
+                           roundTimeoutMs=int(float(cfg["mxar.allreduce.round-timeout"]) * 1000),
+                           externalRounds=bool(cfg["mxar.bridge.external-rounds"]),
+                           bridgePort=int(cfg["mxar.bridge.port"]), bridgeHost=str(cfg["mxar.bridge.host"]))
+    bridge_port = system.master_bridge_port(master)
+    if bridge_port >= 0:
+        print(f"[mxar-master] control bridge on {cfg['mxar.bridge.host']}:{bridge_port}"
+              f"{' (external rounds)' if cfg['mxar.bridge.external-rounds'] else ''}", flush=True)
     node = C.ClusterNode.start(system, _cluster_cfg(cfg, args.port, ["master"]))
     node.subscribe(master)
     reg = _observe(args, cfg, {"role": "master", "address": node.address})

@@ -43,6 +43,9 @@ DEFAULTS: dict[str, Any] = {
     "mxar.allreduce.live-barrier": False,
     "mxar.allreduce.reinit-on-loss": False,                    # re-init the survivors when a worker dies
     "mxar.allreduce.resume-on-join": False,                    # a mid-job join resumes everyone at the current round
+    "mxar.bridge.port": -1,                                    # control bridge TCP port (-1 off, 0 any free port)
+    "mxar.bridge.host": "127.0.0.1",                           # control bridge listen address
+    "mxar.bridge.external-rounds": False,                      # bridge clients drive the rounds (StartAllreduce)
     "mxar.allreduce.round-timeout": 0.0,                       # seconds; 0 = off
     "mxar.engine.device": "cpu",                               # cpu | cuda[:i]
     "mxar.engine.algo": "auto",                                # auto | twoshot | oneshot | rccl

@@ -382,6 +382,17 @@ PYBIND11_MODULE(_C, m) {
       .def("__repr__", [](const RoundTimeout& t) {
         return "RoundTimeout(epoch=" + std::to_string(t.epoch) + ", round=" + std::to_string(t.round) + ")";
       });
+  py::class_<BridgeCommand>(m, "BridgeCommand")
+      .def_readonly("round", &BridgeCommand::round)
+      .def_readonly("client", &BridgeCommand::client)
+      .def_property_readonly("kind", [](const BridgeCommand& b) {
+        return b.kind == BridgeCommand::Start ? "StartAllreduce" : "Status";
+      });
+  m.def("parse_flat_json", [](const std::string& line) -> py::object {
+    std::map<std::string, std::string> kv;
+    if (!parse_flat_json(line, kv)) return py::none();
+    return py::cast(kv);
+  }, "The bridge's line parser (flat JSON object -> {key: raw value}); None when malformed");
   py::class_<PlaneRoundDone>(m, "PlaneRoundDone")
       .def_readonly("epoch", &PlaneRoundDone::epoch)
       .def_readonly("error", &PlaneRoundDone::error)
@@ -526,9 +537,11 @@ PYBIND11_MODULE(_C, m) {
       .def("master", [](ActorSystem& s, int totalWorkers, float thAllreduce, float thReduce, float thComplete,
                         int maxLag, int dataSize, int maxRound, int maxChunkSize, bool liveBarrier,
                         py::object on_finished, std::string name, int startRound, py::object on_round,
-                        int roundTimeoutMs, bool reinitOnLoss, bool resumeOnJoin) {
+                        int roundTimeoutMs, bool reinitOnLoss, bool resumeOnJoin, bool externalRounds,
+                        int bridgePort, std::string bridgeHost) {
             MasterParams p{totalWorkers, thAllreduce, thReduce, thComplete, maxLag, dataSize, maxRound,
-                           maxChunkSize, liveBarrier, startRound, roundTimeoutMs, reinitOnLoss, resumeOnJoin};
+                           maxChunkSize, liveBarrier, startRound, roundTimeoutMs, reinitOnLoss, resumeOnJoin,
+                           externalRounds};
             MasterActor::RoundCallback rcb;
             if (!on_round.is_none()) {
               auto h = std::make_shared<PyCallable>(std::move(on_round));
@@ -545,12 +558,27 @@ PYBIND11_MODULE(_C, m) {
                 h->fn(rounds);
               };
             }
-            return s.actor_of(std::make_unique<MasterActor>(p, cb, rcb), std::move(name));
+            auto actor = std::make_unique<MasterActor>(p, cb, rcb);
+            std::shared_ptr<ControlBridge> bridge;
+            if (bridgePort >= 0) {
+              bridge = ControlBridge::start(bridgeHost, bridgePort);
+              actor->set_bridge(bridge);
+            }
+            ActorRef ref = s.actor_of(std::move(actor), std::move(name));
+            if (bridge) bridge->attach(ref, ref->path());
+            return ref;
           }, py::arg("totalWorkers"), py::arg("thAllreduce"), py::arg("thReduce"), py::arg("thComplete"),
           py::arg("maxLag"), py::arg("dataSize"), py::arg("maxRound"), py::arg("maxChunkSize"),
           py::arg("liveBarrier") = false, py::arg("on_finished") = py::none(), py::arg("name") = "master",
           py::arg("startRound") = 0, py::arg("on_round") = py::none(), py::arg("roundTimeoutMs") = 0,
-          py::arg("reinitOnLoss") = false, py::arg("resumeOnJoin") = false)
+          py::arg("reinitOnLoss") = false, py::arg("resumeOnJoin") = false, py::arg("externalRounds") = false,
+          py::arg("bridgePort") = -1, py::arg("bridgeHost") = "127.0.0.1",
+          "bridgePort >= 0 starts a control bridge (csrc/runtime/control_bridge.h; 0 = any free port, see "
+          "master_bridge_port); externalRounds makes its clients drive the rounds")
+      .def("master_bridge_port", [](ActorSystem&, ActorRef ref) {
+        auto* m = master_of(ref);
+        return m->bridge() ? m->bridge()->port() : -1;
+      })
       .def("plane_worker", [](ActorSystem& s, py::object source, py::object sink, std::shared_ptr<RoundPlane> plane,
                               std::string name) {
             DataSource src = py::isinstance<NativeSource>(source) ? source.cast<NativeSource&>().fn

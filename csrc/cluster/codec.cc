@@ -83,6 +83,8 @@ void encode_message(Writer& w, const Message& m, const RefCodec& rc) {
         } else if constexpr (std::is_same_v<T, PlaneRoundDone>) {
           // process-local (a plane's completion to its own worker); never crosses a node
           throw CodecError("PlaneRoundDone is local to a node");
+        } else if constexpr (std::is_same_v<T, BridgeCommand>) {
+          throw CodecError("BridgeCommand is local to a node");  // bridge client -> its own master
         }
       },
       m);

@@ -22,7 +22,7 @@ void MasterCore::on_member_up(int handle) {
                                                            << workers_.size() << " workers there");
     stats_.join_reinits++;
     init_workers(round_);
-    start_allreduce();
+    if (!external_idle()) start_allreduce();
     return;
   }
   if (static_cast<int>(workers_.size()) >= f32_threshold_count(p_.thAllreduce, p_.totalWorkers)) {
@@ -31,8 +31,28 @@ void MasterCore::on_member_up(int handle) {
     round_ = std::max(0, p_.startRound);
     last_reported_ = round_ - 1;
     finished_ = false;
+    if (p_.externalRounds) {  // the client starts the first round
+      awaiting_ = true;
+      started_ = false;
+      return;
+    }
     start_allreduce();
   }
+}
+
+std::string MasterCore::on_external_start(int round) {
+  if (!p_.externalRounds) return "master is not in externalRounds mode";
+  if (round_ < 0 || workers_.empty()) return "workers are not initialised";
+  if (finished_) return "job finished";
+  if (!awaiting_) return "round " + std::to_string(round_) + " has not reached its barrier";
+  if (round > p_.maxRound) return "round beyond maxRound " + std::to_string(p_.maxRound);
+  if (started_ ? round <= round_ : round < round_)
+    return "round " + std::to_string(round) + " is not after round " + std::to_string(round_);
+  round_ = round;
+  awaiting_ = false;
+  started_ = true;
+  start_allreduce();
+  return "";
 }
 
 // Terminated (AllreduceMaster.scala:50-56)
@@ -54,7 +74,7 @@ void MasterCore::on_terminated(int handle) {
                                                              << round_);
     stats_.loss_reinits++;
     init_workers(round_);
-    start_allreduce();
+    if (!external_idle()) start_allreduce();
     return;
   }
   // With liveBarrier the round may now be complete.
@@ -79,21 +99,27 @@ void MasterCore::on_complete(int srcId, int round, int64_t epoch) {
   if (srcId >= 0) {
     MXAR_LOG(INFO, "master", "----Node " << srcId << " completes allreduce round " << round);
     stats_.completes++;
-    if (round != round_) {
+    if (round != round_ || (p_.externalRounds && (awaiting_ || !started_))) {
       stats_.stale_completes++;
+      fx_->complete_seen(srcId, round, false);
       return;
     }
     numComplete_ += 1;
+    fx_->complete_seen(srcId, round, true);
   }
   // numComplete >= totalWorkers * thAllreduce : float compare, not truncated (:62)
   volatile float need = barrier_base() * p_.thAllreduce;
-  if (static_cast<float>(numComplete_) >= need) advance();
+  if (static_cast<float>(numComplete_) >= need && !(p_.externalRounds && awaiting_)) advance();
 }
 
 void MasterCore::advance() {
   if (last_reported_ < round_) {
     last_reported_ = round_;
     fx_->round_completed(round_, epoch_);
+  }
+  if (p_.externalRounds && round_ < p_.maxRound) {  // wait for the client's next start
+    awaiting_ = true;
+    return;
   }
   if (round_ < p_.maxRound) {
     MXAR_LOG(INFO, "master", "----" << numComplete_ << " (out of " << p_.totalWorkers
@@ -111,7 +137,7 @@ void MasterCore::advance() {
 // its start is advanced anyway - the coordinator-level counterpart of the workers' maxLag
 // catch-up (stragglers then force-complete it when the next Start arrives).
 void MasterCore::on_round_timeout(int64_t epoch, int round) {
-  if (epoch != epoch_ || round != round_ || finished_ || round_ < 0) return;  // already advanced
+  if (epoch != epoch_ || round != round_ || finished_ || round_ < 0 || awaiting_) return;  // already advanced
   stats_.round_timeouts++;
   MXAR_LOG(WARNING, "master", "----Round " << round << " timed out with " << numComplete_ << " of "
                                              << workers_.size() << " completions; advancing");
@@ -145,6 +171,17 @@ void MasterCore::init_workers(int startRound) {
     p.roundBase = round_base_;
     fx_->send_init(h, p, workers_);
   }
+  InitParams p;
+  p.numPeers = static_cast<int>(workers_.size());
+  p.thReduce = p_.thReduce;
+  p.thComplete = p_.thComplete;
+  p.maxLag = p_.maxLag;
+  p.dataSize = p_.dataSize;
+  p.maxChunkSize = p_.maxChunkSize;
+  p.epoch = epoch_;
+  p.startRound = startRound;
+  p.roundBase = round_base_;
+  fx_->workers_initialized(p, workers_);
 }
 
 // startAllreduce (AllreduceMaster.scala:91-97)

@@ -17,6 +17,7 @@
 
 #include <functional>
 #include <map>
+#include <string>
 #include <vector>
 
 #include "worker_core.h"
@@ -44,6 +45,12 @@ struct MasterParams {
   // in by re-initialising everyone at the CURRENT round. The reference restarts the whole
   // job at round 0 on every MemberUp past the threshold (Q2).
   bool resumeOnJoin = false;
+  // Extension: rounds are driven from outside (the control bridge,
+  // csrc/runtime/control_bridge.h). After init and after every barrier the master waits
+  // for an external StartAllreduce(r) instead of starting round + 1 itself, i.e. the
+  // client plays AllreduceMaster.scala:58-67,91-97 while this master keeps membership,
+  // ids and InitWorkers.
+  bool externalRounds = false;
 };
 
 class MasterEffects {
@@ -57,6 +64,10 @@ class MasterEffects {
   virtual void round_completed(int /*round*/, int64_t /*epoch*/) {}
   // Ask the host to call MasterCore::on_round_timeout(epoch, round) after `ms`.
   virtual void arm_round_timer(int64_t /*epoch*/, int /*round*/, int /*ms*/) {}
+  // Called once per (re-)initialisation, after every worker got its InitWorkers.
+  virtual void workers_initialized(const InitParams& /*p*/, const std::map<int, int>& /*ids*/) {}
+  // Called for every CompleteAllreduce the barrier counted (counted = round matched).
+  virtual void complete_seen(int /*srcId*/, int /*round*/, bool /*counted*/) {}
 };
 
 struct MasterStats {
@@ -73,6 +84,12 @@ class MasterCore {
   // epoch < 0: untagged (accepted); otherwise completions of another epoch are stale
   void on_complete(int srcId, int round, int64_t epoch = -1);
   void on_round_timeout(int64_t epoch, int round);
+  // externalRounds: start round `round` now. Accepted only while the master is waiting
+  // (workers initialised, previous round at its barrier or none started yet) and when
+  // round > the last round started (== startRound allowed first) and round <= maxRound.
+  // Returns "" when accepted, otherwise the reason.
+  std::string on_external_start(int round);
+  bool awaiting_start() const { return awaiting_; }
 
   int round() const { return round_; }
   int num_complete() const { return numComplete_; }
@@ -89,6 +106,8 @@ class MasterCore {
   void start_allreduce();
   void advance();
   float barrier_base() const;
+  // externalRounds and no round in flight: a re-init must not start a round by itself
+  bool external_idle() const { return p_.externalRounds && (awaiting_ || !started_); }
 
   MasterEffects* fx_;
   MasterParams p_;
@@ -102,6 +121,8 @@ class MasterCore {
   int epoch_start_round_ = 0;
   int last_reported_ = -1;
   bool finished_ = false;
+  bool awaiting_ = false;  // externalRounds: waiting for the client's next StartAllreduce
+  bool started_ = false;   // externalRounds: round_ has been started in this epoch
   MasterStats stats_;
 };
 

@@ -185,9 +185,18 @@ struct PlaneRoundDone {
   bool cold = false;
 };
 
+// A command from a control-bridge client (csrc/runtime/control_bridge.h) to the master:
+// Start = the reference's StartAllreduce(round) issued by an external round driver,
+// Status = one Status reply. Local to a node (never encoded).
+struct BridgeCommand {
+  enum Kind { Start, Status } kind = Status;
+  int round = 0;
+  uint64_t client = 0;  // bridge client that receives the reply
+};
+
 using Message = std::variant<InitWorkers, StartAllreduce, ScatterBlock, ReduceBlock,
                              CompleteAllreduce, MemberUp, Terminated, AllreduceFinished,
-                             PoisonPill, TextMessage, RoundTimeout, PlaneRoundDone>;
+                             PoisonPill, TextMessage, RoundTimeout, PlaneRoundDone, BridgeCommand>;
 
 const char* message_name(const Message& m);
 

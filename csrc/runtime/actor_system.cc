@@ -31,7 +31,8 @@ const char* message_name(const Message& m) {
   static const char* names[] = {"InitWorkers",    "StartAllreduce", "ScatterBlock",
                                 "ReduceBlock",    "CompleteAllreduce", "MemberUp",
                                 "Terminated",     "AllreduceFinished", "PoisonPill",
-                                "TextMessage",    "RoundTimeout",      "PlaneRoundDone"};
+                                "TextMessage",    "RoundTimeout",      "PlaneRoundDone",
+                                "BridgeCommand"};
   static_assert(sizeof(names) / sizeof(names[0]) == std::variant_size_v<Message>, "one name per message");
   return names[m.index()];
 }

@@ -1,5 +1,7 @@
 #include "allreduce_actors.h"
 
+#include <sstream>
+
 #include <chrono>
 
 #include "../core/log.h"
@@ -66,6 +68,7 @@ void WorkerActor::receive(Envelope& env, ActorContext& ctx) {
     void operator()(TextMessage&) {}
     void operator()(RoundTimeout&) {}
     void operator()(PlaneRoundDone&) {}
+    void operator()(BridgeCommand&) {}
   };
   std::visit(Visitor{this, env, ctx}, env.msg);
   ctx_ = nullptr;
@@ -133,8 +136,47 @@ void MasterActor::receive(Envelope& env, ActorContext& ctx) {
     core_.on_complete(c->srcId, c->round, c->epoch);
   } else if (auto* rt = std::get_if<RoundTimeout>(&env.msg)) {
     core_.on_round_timeout(rt->epoch, rt->round);
+  } else if (auto* bc = std::get_if<BridgeCommand>(&env.msg)) {
+    if (bridge_ && bc->kind == BridgeCommand::Start) {
+      const std::string why = core_.on_external_start(bc->round);
+      bridge_->reply(bc->client, why.empty()
+                                     ? "{\"type\":\"Accepted\",\"cmd\":\"StartAllreduce\",\"round\":" +
+                                           std::to_string(bc->round) + "}"
+                                     : "{\"type\":\"Error\",\"cmd\":\"StartAllreduce\",\"round\":" +
+                                           std::to_string(bc->round) + ",\"reason\":\"" + json_escape(why) + "\"}");
+    } else if (bridge_) {
+      std::ostringstream o;
+      o << "{\"type\":\"Status\",\"round\":" << core_.round() << ",\"epoch\":" << core_.epoch()
+        << ",\"workers\":" << core_.workers().size() << ",\"numComplete\":" << core_.num_complete()
+        << ",\"awaiting\":" << (core_.awaiting_start() ? "true" : "false")
+        << ",\"finished\":" << (core_.finished() ? "true" : "false") << "}";
+      bridge_->reply(bc->client, o.str());
+    }
   }
   ctx_ = nullptr;
+}
+
+void MasterActor::workers_initialized(const InitParams& p, const std::map<int, int>& ids) {
+  if (!bridge_) return;
+  std::ostringstream o;
+  o << "{\"type\":\"InitWorkers\",\"epoch\":" << p.epoch << ",\"workers\":[";
+  bool first = true;
+  for (auto& [id, h] : ids) {
+    o << (first ? "" : ",") << id;
+    first = false;
+  }
+  o << "],\"thReduce\":" << p.thReduce << ",\"thComplete\":" << p.thComplete << ",\"maxLag\":" << p.maxLag
+    << ",\"dataSize\":" << p.dataSize << ",\"maxChunkSize\":" << p.maxChunkSize
+    << ",\"startRound\":" << p.startRound << ",\"externalRounds\":"
+    << (core_.params().externalRounds ? "true" : "false") << "}";
+  bridge_->set_init_line(o.str());
+  bridge_->publish(o.str());
+}
+
+void MasterActor::complete_seen(int srcId, int round, bool counted) {
+  if (!bridge_) return;
+  bridge_->publish("{\"type\":\"CompleteAllreduce\",\"srcId\":" + std::to_string(srcId) +
+                   ",\"round\":" + std::to_string(round) + ",\"counted\":" + (counted ? "true" : "false") + "}");
 }
 
 void MasterActor::arm_round_timer(int64_t epoch, int round, int ms) {
@@ -166,6 +208,7 @@ void MasterActor::send_start(int handle, int round) {
 }
 
 void MasterActor::finished(int rounds) {
+  if (bridge_) bridge_->publish("{\"type\":\"AllreduceFinished\",\"rounds\":" + std::to_string(rounds) + "}");
   if (on_finished_) on_finished_(rounds);
 }
 
@@ -175,6 +218,10 @@ void MasterActor::round_completed(int round, int64_t epoch) {
     if (stamps_.size() < (size_t{1} << 22))
       stamps_.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count());
   }
+  if (bridge_)
+    bridge_->publish("{\"type\":\"RoundComplete\",\"round\":" + std::to_string(round) +
+                     ",\"epoch\":" + std::to_string(epoch) + ",\"numComplete\":" +
+                     std::to_string(core_.num_complete()) + "}");
   if (on_round_) on_round_(round, epoch);
 }
 

@@ -13,6 +13,7 @@
 #include "../core/master_core.h"
 #include "../core/worker_core.h"
 #include "actor_system.h"
+#include "control_bridge.h"
 
 namespace mxar {
 
@@ -60,6 +61,13 @@ class MasterActor final : public Actor, public MasterEffects {
   void finished(int rounds) override;
   void round_completed(int round, int64_t epoch) override;
   void arm_round_timer(int64_t epoch, int round, int ms) override;
+  void workers_initialized(const InitParams& p, const std::map<int, int>& ids) override;
+  void complete_seen(int srcId, int round, bool counted) override;
+
+  // Control bridge (csrc/runtime/control_bridge.h): events go out to its clients, its
+  // BridgeCommands come in. Set before the master receives its first message.
+  void set_bridge(std::shared_ptr<ControlBridge> b) { bridge_ = std::move(b); }
+  const std::shared_ptr<ControlBridge>& bridge() const { return bridge_; }
 
   const MasterCore& core() const { return core_; }
   // steady_clock (CLOCK_MONOTONIC = Python's perf_counter) seconds at which each round
@@ -74,6 +82,7 @@ class MasterActor final : public Actor, public MasterEffects {
   FinishedCallback on_finished_;
   RoundCallback on_round_;
   ActorContext* ctx_ = nullptr;
+  std::shared_ptr<ControlBridge> bridge_;
   mutable std::mutex stamp_mu_;
   std::vector<double> stamps_;
 };

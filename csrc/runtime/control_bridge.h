@@ -1,0 +1,94 @@
+// Control bridge: the master's round protocol over a language-neutral line protocol.
+//
+// SURVEY §7.5 item 3 ("existing Akka client can drive it"): real Akka wire compatibility
+// would mean Akka classic remoting plus Java serialization, i.e. a JVM on
+// the control path. Instead the bridge carries the reference's CONTROL messages with the
+// reference's names and field names as JSON lines over TCP, so a JVM client needs only a
+// socket and a JSON printer (examples/akka_bridge/BridgeDriver.scala). Payloads never
+// cross it: data stays on the workers' planes (HBM / xGMI).
+//
+// The client plays the round driver of AllreduceMaster.scala:58-67,91-97; the master
+// (MasterParams.externalRounds) keeps membership, dense ids and InitWorkers (:38-56,84-89).
+//
+//   client -> bridge   {"type":"StartAllreduce","round":r}      start round r
+//                      {"type":"Status"}                         one Status reply
+//   bridge -> client   {"type":"Hello","protocol":"mxar-bridge/1",...}         on connect
+//                      {"type":"InitWorkers","epoch":e,"workers":[0,..],"thReduce":..,
+//                       "thComplete":..,"maxLag":..,"dataSize":..,"maxChunkSize":..,
+//                       "startRound":..}                          every (re-)init
+//                      {"type":"CompleteAllreduce","srcId":i,"round":r,"counted":b}
+//                      {"type":"RoundComplete","round":r,"epoch":e,"numComplete":n}
+//                      {"type":"AllreduceFinished","rounds":n}
+//                      {"type":"Accepted","cmd":"StartAllreduce","round":r}
+//                      {"type":"Error","cmd":...,"reason":"..."}  (to the sender only)
+//                      {"type":"Status","round":..,"epoch":..,"workers":..,
+//                       "numComplete":..,"awaiting":b,"finished":b}
+//
+// Events go to every connected client; Accepted / Error / Status only to the sender.
+// A client that connects late first gets Hello, then the last InitWorkers line.
+#pragma once
+
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "actor_system.h"
+
+namespace mxar {
+
+// Flat JSON object -> key/value strings (strings unescaped, numbers/bools/null verbatim).
+// Nested values are rejected. Returns false on malformed input.
+bool parse_flat_json(const std::string& line, std::map<std::string, std::string>& out);
+std::string json_escape(const std::string& s);
+
+class ControlBridge : public std::enable_shared_from_this<ControlBridge> {
+ public:
+  // Listen on host:port (port 0 = any free port; see port()).
+  static std::shared_ptr<ControlBridge> start(const std::string& host, int port);
+  ~ControlBridge();
+  ControlBridge(const ControlBridge&) = delete;
+  ControlBridge& operator=(const ControlBridge&) = delete;
+
+  // Commands from clients go to `master` as BridgeCommand messages.
+  void attach(ActorRef master, std::string master_path);
+  int port() const { return port_; }
+  // Send one line to every client (events) / to one client (replies).
+  void publish(const std::string& line);
+  void reply(uint64_t client, const std::string& line);
+  // Remember the latest InitWorkers line for clients that connect later.
+  void set_init_line(std::string line);
+  size_t clients() const;
+  void stop();
+
+ private:
+  struct Client {
+    uint64_t id;
+    int fd;
+    std::mutex wmu;
+    std::thread reader;
+    std::atomic<bool> dead{false};
+  };
+  ControlBridge() = default;
+  void accept_loop();
+  void read_loop(std::shared_ptr<Client> c);
+  bool write_line(Client& c, const std::string& line);
+  void reap();
+
+  int lfd_ = -1;
+  int wake_[2] = {-1, -1};
+  int port_ = 0;
+  std::atomic<bool> stop_{false};
+  std::thread acceptor_;
+  mutable std::mutex mu_;
+  std::vector<std::shared_ptr<Client>> clients_;
+  uint64_t next_id_ = 1;
+  ActorRef master_;
+  std::string master_path_;
+  std::string init_line_;
+};
+
+}  // namespace mxar

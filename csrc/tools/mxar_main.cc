@@ -57,6 +57,8 @@ struct Options {
   std::string host = "127.0.0.1";
   std::vector<std::string> seeds;
   float th_allreduce = 1.f, th_reduce = 0.9f, th_complete = 0.8f;  // AllreduceMaster.scala:105-107
+  int bridge_port = -1;                 // --bridge PORT (control bridge, docs/BRIDGE.md)
+  bool external_rounds = false;         // --external-rounds
   int max_lag = 1, max_round = 100, round_timeout_ms = 0;          // :108-109
   std::string loglevel = "INFO";
   bool quiet = false;
@@ -71,6 +73,7 @@ struct Options {
                "       mxar worker [port sourceDataSize] [options]\n"
                "options: --host H --seeds a[,b] --th-allreduce F --th-reduce F --th-complete F --max-lag N\n"
                "         --max-round N --round-timeout-ms N --loglevel L --quiet\n"
+               "master control bridge (docs/BRIDGE.md): --bridge PORT [--external-rounds]\n"
                "worker on a GPU (mxar-gpu): --device K [--max-peers N --plane-max-lag N --grid N --plane-timeout S]\n",
                msg);
   std::exit(2);
@@ -95,6 +98,8 @@ Options parse(int argc, char** argv) {
     else if (a == "--max-lag") o.max_lag = std::stoi(val());
     else if (a == "--max-round") o.max_round = std::stoi(val());
     else if (a == "--round-timeout-ms") o.round_timeout_ms = std::stoi(val());
+    else if (a == "--bridge") o.bridge_port = std::stoi(val());
+    else if (a == "--external-rounds") o.external_rounds = true;
     else if (a == "--loglevel") o.loglevel = val();
     else if (a == "--quiet") o.quiet = true;
     else if (a == "--device") o.device = std::stoi(val());
@@ -133,6 +138,7 @@ void set_level(const std::string& l) {
   mp.maxRound = o.max_round;
   mp.maxChunkSize = chunk;
   mp.roundTimeoutMs = o.round_timeout_ms;
+  mp.externalRounds = o.external_rounds;
   auto sys = std::make_shared<ActorSystem>("ClusterSystem", ActorSystem::Mode::Threaded, 2);
   std::atomic<int> finished{-1};
   const auto t0 = std::chrono::steady_clock::now();
@@ -141,8 +147,18 @@ void set_level(const std::string& l) {
   auto on_round = [&stamps](int, int64_t) {
     stamps.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count());
   };
-  ActorRef master =
-      sys->actor_of(std::make_unique<MasterActor>(mp, [&](int rounds) { finished = rounds; }, on_round), "master");
+  auto master_actor = std::make_unique<MasterActor>(mp, [&](int rounds) { finished = rounds; }, on_round);
+  std::shared_ptr<ControlBridge> bridge;
+  if (o.bridge_port >= 0) {
+    bridge = ControlBridge::start(o.host, o.bridge_port);
+    master_actor->set_bridge(bridge);
+  }
+  ActorRef master = sys->actor_of(std::move(master_actor), "master");
+  if (bridge) {
+    bridge->attach(master, master->path());
+    std::printf("[mxar master] control bridge on %s:%d%s\n", o.host.c_str(), bridge->port(),
+                o.external_rounds ? " (external rounds)" : "");
+  }
   ClusterConfig cc;
   cc.host = o.host;
   cc.port = port;

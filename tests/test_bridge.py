@@ -1,0 +1,257 @@
+"""Control bridge (csrc/runtime/control_bridge.h, docs/BRIDGE.md): the reference's control
+messages as JSON lines over TCP, so a non-native client (e.g. a JVM Akka actor with a socket)
+can watch a job or drive its rounds.
+
+Driving mode mirrors AllreduceMaster.scala:58-67,91-97 from outside: the client sends
+StartAllreduce(r), the master forwards it to the workers and reports the barrier.
+"""
+import os
+import subprocess
+import sys
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from akka_allreduce_1_amd._native import C
+from akka_allreduce_1_amd.bridge import BridgeClient, BridgeError
+from akka_allreduce_1_amd.engine import host_iota_source
+from akka_allreduce_1_amd.protocol import AllReduceInput, MemberUp
+
+F = np.float32
+
+
+def expected(n, it, P):
+    i = np.arange(n, dtype=np.float64)
+    return sum(i + it + 1000.0 * k for k in range(P))
+
+
+def _job(P, n, chunk, rounds, kind="host", external=True, name="Bridge"):
+    system = C.ActorSystem(name, False)
+    fin = threading.Event()
+    outs = [dict() for _ in range(P)]
+    lock = threading.Lock()
+
+    def src(k):
+        base = host_iota_source(n, 1000.0 * k)
+
+        def f(req):
+            v = base(req)
+            return AllReduceInput(v) if kind == "host" else v
+        return f
+
+    def sink(k):
+        def f(out):
+            with lock:
+                outs[k][out.iteration] = (np.asarray(out.data).copy(), list(out.count))
+        return f
+
+    master = system.master(P, 1.0, 1.0, 1.0, 1, n, rounds - 1, chunk, on_finished=lambda r: fin.set(),
+                           externalRounds=external, bridgePort=0)
+    port = system.master_bridge_port(master)
+    assert port > 0
+    ws = []
+    for k in range(P):
+        if kind == "host":
+            ws.append(system.worker(src(k), sink(k), f"w{k}"))
+            master.tell(MemberUp(ws[k], "worker", ""), None)
+        else:
+            plane = C.loopback_plane(name + "-hub")
+            ws.append(system.plane_worker(src(k), sink(k), plane, f"w{k}"))
+            master.tell(MemberUp(ws[k], "worker", "", plane.descriptor), None)
+    return system, master, port, outs, fin
+
+
+@pytest.mark.parametrize("kind", ["host", "loopback"])
+def test_client_drives_every_round(kind):
+    P, n, chunk, rounds = 2, 40, 6, 12
+    system, master, port, outs, fin = _job(P, n, chunk, rounds, kind, name=f"Drive{kind}")
+    try:
+        with BridgeClient("127.0.0.1", port) as b:
+            assert b.hello["protocol"] == "mxar-bridge/1"
+            init = b.wait_for("InitWorkers")
+            assert init["workers"] == [0, 1] and init["dataSize"] == n and init["maxChunkSize"] == chunk
+            assert init["externalRounds"] is True
+            # nothing runs until the client starts a round
+            time.sleep(0.2)
+            assert all(not o for o in outs)
+            st = b.status()
+            assert st["awaiting"] is True and st["workers"] == P
+            done = b.drive(range(rounds))
+            assert [d["round"] for d in done] == list(range(rounds))
+            assert fin.wait(10)
+            b.wait_for("AllreduceFinished", rounds=rounds)
+            completes = [e for e in b.events if e["type"] == "CompleteAllreduce" and e["counted"]]
+            assert sorted((e["round"], e["srcId"]) for e in completes) == [(r, i) for r in range(rounds) for i in range(P)]
+        deadline = time.time() + 5
+        while time.time() < deadline and any(len(o) < rounds for o in outs):
+            time.sleep(0.01)
+        for k in range(P):
+            for it in range(rounds):
+                data, counts = outs[k][it]
+                np.testing.assert_array_equal(data, expected(n, it, P).astype(F))
+    finally:
+        system.shutdown()
+
+
+def test_refused_commands_and_malformed_lines():
+    P, n, chunk, rounds = 2, 12, 3, 6
+    system, master, port, outs, fin = _job(P, n, chunk, rounds, name="Refuse")
+    try:
+        with BridgeClient("127.0.0.1", port) as b:
+            b.wait_for("InitWorkers")
+            b.send_raw("not json")
+            assert "malformed" in b.wait_for("Error")["reason"]
+            b.send_raw('{"type": "StartAllreduce", "round": {"nested": 1}}')
+            b.wait_for("Error")
+            b.send_raw('{"type":"StartAllreduce","round":-3}')
+            assert "non-negative" in b.wait_for("Error")["reason"]
+            b.send({"type": "Reboot"})
+            assert b.wait_for("Error")["reason"] == "unknown command"
+            with pytest.raises(BridgeError, match="maxRound"):
+                b.start(rounds + 5)
+            b.start(2)  # skipping ahead is allowed (the client owns the round numbering)
+            b.wait_for("RoundComplete", round=2)
+            with pytest.raises(BridgeError, match="not after"):
+                b.start(1)  # never backwards
+            with pytest.raises(BridgeError, match="not after"):
+                b.start(2)
+            # the connection survived all of it
+            assert b.status()["round"] == 2
+    finally:
+        system.shutdown()
+
+
+def test_second_start_before_barrier_is_refused():
+    """A start while a round is in flight is refused, not queued: the reference master never
+    overlaps its own rounds (AllreduceMaster.scala:62-66)."""
+    P, n, chunk, rounds = 2, 8, 2, 4
+    system = C.ActorSystem("Inflight", False)
+    gate = threading.Event()
+
+    def src(k):
+        base = host_iota_source(n, 0.0)
+
+        def f(req):
+            gate.wait(10)  # hold round 0 in flight
+            return AllReduceInput(base(req))
+        return f
+
+    master = system.master(P, 1.0, 1.0, 1.0, 1, n, rounds - 1, chunk, externalRounds=True, bridgePort=0)
+    port = system.master_bridge_port(master)
+    for k in range(P):
+        w = system.worker(src(k), None, f"w{k}")
+        master.tell(MemberUp(w, "worker", ""), None)
+    try:
+        with BridgeClient("127.0.0.1", port) as b:
+            b.wait_for("InitWorkers")
+            b.start(0)
+            with pytest.raises(BridgeError, match="barrier"):
+                b.start(1)
+            gate.set()
+            b.wait_for("RoundComplete", round=0)
+            b.start(1)
+            b.wait_for("RoundComplete", round=1)
+    finally:
+        gate.set()
+        system.shutdown()
+
+
+def test_observer_mode_and_late_client():
+    """Without externalRounds the master drives itself; a client only watches. A client that
+    connects after the init still gets the InitWorkers line first."""
+    P, n, chunk, rounds = 2, 10, 5, 30
+    system, master, port, outs, fin = _job(P, n, chunk, rounds, external=False, name="Observe")
+    try:
+        assert fin.wait(20)
+        with BridgeClient("127.0.0.1", port) as b:
+            init = b.wait_for("InitWorkers")
+            assert init["externalRounds"] is False and init["workers"] == [0, 1]
+            with pytest.raises(BridgeError, match="externalRounds"):
+                b.start(0)
+            assert b.status()["finished"] is True
+    finally:
+        system.shutdown()
+
+
+def test_two_clients_see_the_same_events():
+    P, n, chunk, rounds = 2, 16, 4, 5
+    system, master, port, outs, fin = _job(P, n, chunk, rounds, name="TwoClients")
+    try:
+        with BridgeClient("127.0.0.1", port) as a, BridgeClient("127.0.0.1", port) as w:
+            a.wait_for("InitWorkers")
+            w.wait_for("InitWorkers")
+            a.drive(range(rounds))
+            w.wait_for("AllreduceFinished")
+            seen = [e["round"] for e in w.events if e["type"] == "RoundComplete"]
+            assert seen == list(range(rounds))
+            # replies go only to the sender
+            assert not any(e["type"] == "Accepted" for e in w.events)
+    finally:
+        system.shutdown()
+
+
+def test_flat_json_parser():
+    p = C.parse_flat_json
+    assert p('{"type":"StartAllreduce","round":7}') == {"type": "StartAllreduce", "round": "7"}
+    assert p(' { "a" : "x\\"y\\\\z\\n" , "b" : true } ') == {"a": 'x"y\\z\n', "b": "true"}
+    assert p("{}") == {}
+    assert p('{"a":"\\u0041"}') == {"a": "A"}
+    for bad in ["", "[]", '{"a":1', '{"a":1}x', '{"a":[1]}', '{"a":{"b":1}}', '{a:1}', '{"a":"x}', '{"a":1,}']:
+        assert p(bad) is None, bad
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("kind", ["python", "native"])
+def test_master_cli_bridge_external_rounds(kind):
+    """mxar-master --bridge PORT --external-rounds + 2 worker processes over TCP (Python CLIs,
+    or the Python-free `mxar` executable): the bridge client is the only round driver."""
+    from akka_allreduce_1_amd.parallel.comm import free_port
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    mport, bport = free_port(), free_port()
+    rounds = 8
+    if kind == "python":
+        seed = ["--set", f"mxar.cluster.seed-nodes=mxar.tcp://ClusterSystem@127.0.0.1:{mport}",
+                "--set", "mxar.loglevel=WARNING"]
+        py = [sys.executable, "-m", "akka_allreduce_1_amd"]
+        mcmd = py + ["master", str(mport), "2", "10", "2", "--bridge", str(bport), "--external-rounds",
+                     "--set", f"mxar.allreduce.max-round={rounds - 1}"] + seed
+    else:
+        exe = os.path.join(root, "akka_allreduce_1_amd", "mxar")
+        if not os.path.exists(exe):
+            pytest.skip("native executable not built (tools/build_native.py)")
+        seed = ["--seeds", f"mxar.tcp://ClusterSystem@127.0.0.1:{mport}", "--loglevel", "ERROR"]
+        py = [exe]
+        mcmd = [exe, "master", str(mport), "2", "10", "2", "--bridge", str(bport), "--external-rounds",
+                "--max-round", str(rounds - 1)] + seed
+    master = subprocess.Popen(mcmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    workers = []
+    try:
+        deadline = time.time() + 60
+        b = None
+        while b is None and time.time() < deadline:
+            try:
+                b = BridgeClient("127.0.0.1", bport, timeout=60)
+            except OSError:
+                time.sleep(0.2)
+        assert b is not None, "bridge did not come up"
+        workers = [subprocess.Popen(py + ["worker", "0", "10"] + seed, env=env, stdout=subprocess.PIPE,
+                                    stderr=subprocess.STDOUT, text=True) for _ in range(2)]
+        with b:
+            init = b.wait_for("InitWorkers", timeout=60)
+            assert init["workers"] == [0, 1]
+            done = b.drive(range(rounds), timeout=30)
+            assert len(done) == rounds
+            b.wait_for("AllreduceFinished", timeout=30)
+        assert master.wait(30) == 0
+    finally:
+        for p in workers + [master]:
+            if p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(10)
+                except subprocess.TimeoutExpired:
+                    p.kill()
