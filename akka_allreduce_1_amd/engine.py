@@ -73,7 +73,8 @@ class PlaneJob:
                  timeout_s: float = 60.0, order_ref: bool = True, on_output: Callable | None = None,
                  max_peers: int | None = None, high_priority: bool = True, order_release: bool = True,
                  plane: str = "xgmi", hub: str | None = None, spin_us: int = 1000, reinit_on_loss: bool = False,
-                 split: bool = True, keep_last: bool = False):
+                 split: bool = True, keep_last: bool = False, bridge_port: int | None = None,
+                 external_rounds: bool = False):
         """plane: "xgmi" (one threshold-kernel launch per round on the GPUs in `devices`) or
         "loopback" (host memory, no GPU: csrc/runtime/loopback_plane.h; `hub` names the
         workers' shared hub, default a fresh one; dtype float32, devices ignored).
@@ -82,7 +83,9 @@ class PlaneJob:
         sources: callables (AllReduceInputRequest -> tensor / array) or GPU tensors; a tensor is
         fetched natively every round (no Python, no GIL).
         keep_last: each worker keeps only its newest round output, natively (`last_output(k)`);
-        replaces keep_outputs / on_output, so no Python runs on the round path."""
+        replaces keep_outputs / on_output, so no Python runs on the round path.
+        bridge_port: serve the master's control bridge there (0 = any free port, see
+        `bridge_port`; docs/BRIDGE.md). external_rounds: bridge clients drive the rounds."""
         self.P = P
         self.n = data_size
         self.dtype = dtype
@@ -141,7 +144,8 @@ class PlaneJob:
 
         self.master = self.system.master(P, th_allreduce, th_reduce, th_complete, max_lag, data_size, max_round,
                                          max_chunk_size, on_finished=fin, roundTimeoutMs=round_timeout_ms,
-                                         reinitOnLoss=reinit_on_loss)
+                                         reinitOnLoss=reinit_on_loss, externalRounds=external_rounds,
+                                         bridgePort=-1 if bridge_port is None else bridge_port)
         self.workers = [self.system.plane_worker(self.sources[k], self._sink(k), self.planes[k], f"worker{k}")
                         for k in range(P)]
 
@@ -182,6 +186,11 @@ class PlaneJob:
         if self._final_stamps is not None:
             return self._final_stamps
         return self.system.master_round_stamps(self.master)
+
+    @property
+    def bridge_port(self) -> int:
+        """The master's control-bridge port (-1 without a bridge)."""
+        return self.system.master_bridge_port(self.master)
 
     def last_output(self, k: int):
         """keep_last: worker k's newest AllReduceOutput (None before its first round)."""

@@ -21,7 +21,7 @@ void MasterCore::on_member_up(int handle) {
     MXAR_LOG(INFO, "master", "----worker joined at round " << round_ << ": re-initialising "
                                                            << workers_.size() << " workers there");
     stats_.join_reinits++;
-    init_workers(round_);
+    init_workers(resume_round());
     if (!external_idle()) start_allreduce();
     return;
   }
@@ -73,7 +73,7 @@ void MasterCore::on_terminated(int handle) {
     MXAR_LOG(WARNING, "master", "----re-initialising the " << workers_.size() << " surviving workers at round "
                                                              << round_);
     stats_.loss_reinits++;
-    init_workers(round_);
+    init_workers(resume_round());
     if (!external_idle()) start_allreduce();
     return;
   }

@@ -108,6 +108,10 @@ class MasterCore {
   float barrier_base() const;
   // externalRounds and no round in flight: a re-init must not start a round by itself
   bool external_idle() const { return p_.externalRounds && (awaiting_ || !started_); }
+  // Where a mid-job re-init resumes: the current round, unless it already passed its barrier
+  // while the client has not started the next one (then workers begin at the next round, so a
+  // completed round is never force-completed a second time).
+  int resume_round() const { return p_.externalRounds && awaiting_ && started_ ? round_ + 1 : round_; }
 
   MasterEffects* fx_;
   MasterParams p_;

@@ -255,3 +255,84 @@ def test_master_cli_bridge_external_rounds(kind):
                     p.wait(10)
                 except subprocess.TimeoutExpired:
                     p.kill()
+
+
+def test_planejob_loopback_driven_through_the_bridge():
+    """PlaneJob(bridge_port=0, external_rounds=True) on the loopback round engine: the same
+    job shape the GPU test drives on the xGMI plane."""
+    from akka_allreduce_1_amd.engine import PlaneJob
+
+    P, n, chunk, rounds = 3, 301, 17, 10
+    job = PlaneJob(P, n, max_chunk_size=chunk, max_round=rounds - 1, plane="loopback", bridge_port=0,
+                   external_rounds=True)
+    try:
+        job.start()
+        with BridgeClient("127.0.0.1", job.bridge_port) as b:
+            assert b.wait_for("InitWorkers")["workers"] == list(range(P))
+            b.drive(range(rounds))
+            b.wait_for("AllreduceFinished", rounds=rounds)
+        assert job.finished.wait(10)
+        for p in job.planes:
+            p.drain()
+        job.system.await_idle(10.0)
+        for k in range(P):
+            for it in range(rounds):
+                data, counts = job.outputs[k][it]
+                np.testing.assert_array_equal(np.asarray(data), expected(n, it, P).astype(F))
+                assert all(c == P for c in counts)
+    finally:
+        job.shutdown()
+
+
+def test_worker_loss_while_the_client_drives():
+    """externalRounds + reinitOnLoss: a worker dies between two client-driven rounds. The
+    master re-initialises the survivors (a new InitWorkers epoch) WITHOUT starting a round by
+    itself; the client's next StartAllreduce runs on the survivors only."""
+    from akka_allreduce_1_amd.protocol import PoisonPill
+
+    P, n, chunk, rounds = 3, 30, 4, 10
+    system = C.ActorSystem("LossDrive", False)
+    outs = [dict() for _ in range(P)]
+    delivered = [[] for _ in range(P)]
+    lock = threading.Lock()
+
+    def src(k):
+        base = host_iota_source(n, 1000.0 * k)
+        return lambda req: AllReduceInput(base(req))
+
+    def sink(k):
+        def f(out):
+            with lock:
+                outs[k][out.iteration] = (np.asarray(out.data).copy(), list(out.count))
+                delivered[k].append(out.iteration)
+        return f
+
+    master = system.master(P, 1.0, 1.0, 1.0, 1, n, rounds - 1, chunk, reinitOnLoss=True, externalRounds=True,
+                           bridgePort=0)
+    ws = [system.worker(src(k), sink(k), f"w{k}") for k in range(P)]
+    for w in ws:
+        master.tell(MemberUp(w, "worker", ""), None)
+    try:
+        with BridgeClient("127.0.0.1", system.master_bridge_port(master)) as b:
+            e1 = b.wait_for("InitWorkers", workers=[0, 1, 2])
+            b.drive(range(3))
+            ws[2].tell(PoisonPill(), None)
+            e2 = b.wait_for("InitWorkers", workers=[0, 1])
+            assert e2["epoch"] > e1["epoch"]
+            time.sleep(0.2)
+            st = b.status()
+            assert st["awaiting"] is True and st["round"] == 2, st  # no round started by the re-init
+            b.drive(range(3, rounds))
+            b.wait_for("AllreduceFinished", rounds=rounds)
+        deadline = time.time() + 5
+        while time.time() < deadline and any(len(outs[k]) < rounds for k in (0, 1)):
+            time.sleep(0.01)
+        for k in (0, 1):
+            assert delivered[k] == list(range(rounds)), delivered[k]  # every round exactly once
+            np.testing.assert_array_equal(outs[k][2][0], expected(n, 2, 3).astype(F))
+            data, counts = outs[k][rounds - 1]
+            i = np.arange(n, dtype=np.float64)
+            np.testing.assert_array_equal(data, sum(i + rounds - 1 + 1000.0 * j for j in (0, 1)).astype(F))
+            assert all(c == 2 for c in counts)
+    finally:
+        system.shutdown()

@@ -586,3 +586,34 @@ def test_tensor_sources_and_native_keep_last_sink(dtype):
         assert len(job.stamps) == rounds
     finally:
         job.shutdown()
+
+
+def test_bridge_client_drives_gpu_rounds():
+    """The control bridge (docs/BRIDGE.md) drives the xGMI round engine: a socket client plays
+    AllreduceMaster's round loop (StartAllreduce -> barrier -> next), the plane workers run one
+    threshold-kernel launch per round on the GPU, every output exact."""
+    from akka_allreduce_1_amd.bridge import BridgeClient
+
+    P, n, chunk, rounds = 2, 10007, 333, 12
+    job = PlaneJob(P, n, max_chunk_size=chunk, max_round=rounds - 1, timeout_s=20.0, bridge_port=0,
+                   external_rounds=True)
+    try:
+        job.start()
+        with BridgeClient("127.0.0.1", job.bridge_port) as b:
+            assert b.wait_for("InitWorkers")["workers"] == [0, 1]
+            time.sleep(0.1)
+            assert job.planes[0].stats.launches == 0  # nothing launches before the client starts a round
+            b.drive(range(rounds), timeout=30)
+            b.wait_for("AllreduceFinished", rounds=rounds)
+        assert job.finished.wait(10)
+        for p in job.planes:
+            p.drain()
+        job.system.await_idle(10.0)
+        for k in range(P):
+            for it in range(rounds):
+                data, counts = job.outputs[k][it]
+                np.testing.assert_array_equal(data.float().cpu().numpy(), expected(n, it, range(P)))
+                assert all(c == P for c in counts)
+        assert job.planes[0].stats.launches == rounds
+    finally:
+        job.shutdown()
