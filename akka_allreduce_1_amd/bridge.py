@@ -31,6 +31,7 @@ class BridgeClient:
         self.timeout = timeout
         self._buf = b""
         self.events: list[dict] = []  # every event line received, in order
+        self._inbox: list[dict] = []  # received but not yet matched by a wait
         self.hello = self.wait_for("Hello")
 
     # ------------------------------------------------------------------ wire
@@ -56,33 +57,66 @@ class BridgeClient:
         self.events.append(msg)
         return msg
 
-    def wait_for(self, type_: str, timeout: float | None = None, **fields) -> dict:
-        """Next message of ``type_`` whose fields match; Error replies raise."""
+    def _next(self, pred, timeout: float | None) -> dict:
+        """First unmatched message satisfying pred (an Error raises); unmatched lines stay
+        in the inbox for later waits, so interleaved replies and events are never lost."""
+        for i, m in enumerate(self._inbox):
+            if m.get("type") == "Error" or pred(m):
+                del self._inbox[i]
+                if m.get("type") == "Error" and not pred(m):
+                    raise BridgeError(f"{m.get('cmd')}: {m.get('reason')}")
+                return m
         deadline = time.monotonic() + (self.timeout if timeout is None else timeout)
         while True:
             m = self.recv(max(0.0, deadline - time.monotonic()))
-            if m.get("type") == "Error" and type_ != "Error":
-                raise BridgeError(f"{m.get('cmd')}: {m.get('reason')}")
-            if m.get("type") == type_ and all(m.get(k) == v for k, v in fields.items()):
+            if pred(m):
                 return m
+            if m.get("type") == "Error":
+                raise BridgeError(f"{m.get('cmd')}: {m.get('reason')}")
+            self._inbox.append(m)
+            if len(self._inbox) > 100000:  # a watcher that never waits: keep the newest
+                del self._inbox[:50000]
+
+    def wait_for(self, type_: str, timeout: float | None = None, **fields) -> dict:
+        """Next message of ``type_`` whose fields match; Error replies raise."""
+        return self._next(lambda m: m.get("type") == type_ and all(m.get(k) == v for k, v in fields.items()),
+                          timeout)
+
+    def wait_for_any(self, types, timeout: float | None = None, **fields) -> dict:
+        return self._next(lambda m: m.get("type") in types and all(m.get(k) == v for k, v in fields.items()),
+                          timeout)
 
     # -------------------------------------------------------------- commands
     def start(self, round_: int) -> dict:
-        """StartAllreduce(round) -> the Accepted reply (BridgeError when refused)."""
+        """StartAllreduce(round) -> the reply: Accepted (started now) or Queued (runs when the
+        round in flight reaches its barrier; its Accepted follows then). BridgeError when refused."""
         self.send({"type": "StartAllreduce", "round": int(round_)})
-        return self.wait_for("Accepted", round=int(round_))
+        return self._start_reply(int(round_))
+
+    def _start_reply(self, r: int) -> dict:
+        return self.wait_for_any(("Accepted", "Queued"), round=r)
 
     def status(self) -> dict:
         self.send({"type": "Status"})
         return self.wait_for("Status")
 
-    def drive(self, rounds: Iterable[int], timeout: float | None = None) -> list[dict]:
+    def drive(self, rounds: Iterable[int], timeout: float | None = None, pipeline: bool = True) -> list[dict]:
         """The reference master's round loop (AllreduceMaster.scala:58-67,91-97) from outside:
-        start each round, wait for its barrier. Returns the RoundComplete events."""
-        done = []
-        for r in rounds:
-            self.start(r)
-            done.append(self.wait_for("RoundComplete", timeout=timeout, round=int(r)))
+        start each round, wait for its barrier. Returns the RoundComplete events.
+        pipeline: the next round's start is sent as soon as the current one is running, so
+        the master starts it at the barrier without waiting for this client (one start is
+        queued at a time; rounds never overlap)."""
+        rs = [int(r) for r in rounds]
+        done: list[dict] = []
+        if not rs:
+            return done
+        self.start(rs[0])
+        for i, r in enumerate(rs):
+            if pipeline and i + 1 < len(rs):
+                self.start(rs[i + 1])  # Queued behind r (or Accepted if r already finished)
+            done.append(self.wait_for("RoundComplete", timeout=timeout, round=r))
+            if not pipeline and i + 1 < len(rs):
+                self.start(rs[i + 1])
         return done
 
     def close(self) -> None:

@@ -40,19 +40,27 @@ void MasterCore::on_member_up(int handle) {
   }
 }
 
-std::string MasterCore::on_external_start(int round) {
-  if (!p_.externalRounds) return "master is not in externalRounds mode";
-  if (round_ < 0 || workers_.empty()) return "workers are not initialised";
-  if (finished_) return "job finished";
-  if (!awaiting_) return "round " + std::to_string(round_) + " has not reached its barrier";
-  if (round > p_.maxRound) return "round beyond maxRound " + std::to_string(p_.maxRound);
+MasterCore::StartResult MasterCore::on_external_start(int round, std::string* why) {
+  auto refuse = [&](std::string r) {
+    if (why) *why = std::move(r);
+    return StartResult::Refused;
+  };
+  if (!p_.externalRounds) return refuse("master is not in externalRounds mode");
+  if (round_ < 0 || workers_.empty()) return refuse("workers are not initialised");
+  if (finished_) return refuse("job finished");
+  if (round > p_.maxRound) return refuse("round beyond maxRound " + std::to_string(p_.maxRound));
   if (started_ ? round <= round_ : round < round_)
-    return "round " + std::to_string(round) + " is not after round " + std::to_string(round_);
+    return refuse("round " + std::to_string(round) + " is not after round " + std::to_string(round_));
+  if (!awaiting_) {  // round_ in flight: queue one start behind its barrier
+    if (queued_ >= 0) return refuse("round " + std::to_string(queued_) + " is already queued");
+    queued_ = round;
+    return StartResult::Queued;
+  }
   round_ = round;
   awaiting_ = false;
   started_ = true;
   start_allreduce();
-  return "";
+  return StartResult::Started;
 }
 
 // Terminated (AllreduceMaster.scala:50-56)
@@ -117,9 +125,21 @@ void MasterCore::advance() {
     last_reported_ = round_;
     fx_->round_completed(round_, epoch_);
   }
-  if (p_.externalRounds && round_ < p_.maxRound) {  // wait for the client's next start
+  if (p_.externalRounds && round_ < p_.maxRound) {  // the client's next start, or wait for it
+    if (queued_ > round_) {
+      const int r = queued_;
+      queued_ = -1;
+      round_ = r;
+      start_allreduce();
+      fx_->queued_start_done(r, true, "");
+      return;
+    }
     awaiting_ = true;
     return;
+  }
+  if (p_.externalRounds && queued_ >= 0) {  // cannot happen (queued <= maxRound), kept safe
+    fx_->queued_start_done(queued_, false, "job finished");
+    queued_ = -1;
   }
   if (round_ < p_.maxRound) {
     MXAR_LOG(INFO, "master", "----" << numComplete_ << " (out of " << p_.totalWorkers
@@ -146,6 +166,10 @@ void MasterCore::on_round_timeout(int64_t epoch, int round) {
 
 // init_workers (AllreduceMaster.scala:84-89)
 void MasterCore::init_workers(int startRound) {
+  if (queued_ >= 0) {  // a new membership epoch: the client re-drives from its InitWorkers
+    fx_->queued_start_done(queued_, false, "workers re-initialised");
+    queued_ = -1;
+  }
   // re-number densely 0..P-1 in id order
   std::map<int, int> dense;
   int k = 0;

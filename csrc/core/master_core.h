@@ -68,6 +68,9 @@ class MasterEffects {
   virtual void workers_initialized(const InitParams& /*p*/, const std::map<int, int>& /*ids*/) {}
   // Called for every CompleteAllreduce the barrier counted (counted = round matched).
   virtual void complete_seen(int /*srcId*/, int /*round*/, bool /*counted*/) {}
+  // externalRounds: a queued start ran at the barrier (started) or was dropped (a re-init or
+  // the end of the job made it invalid; `why` says which).
+  virtual void queued_start_done(int /*round*/, bool /*started*/, const std::string& /*why*/) {}
 };
 
 struct MasterStats {
@@ -84,12 +87,15 @@ class MasterCore {
   // epoch < 0: untagged (accepted); otherwise completions of another epoch are stale
   void on_complete(int srcId, int round, int64_t epoch = -1);
   void on_round_timeout(int64_t epoch, int round);
-  // externalRounds: start round `round` now. Accepted only while the master is waiting
-  // (workers initialised, previous round at its barrier or none started yet) and when
+  // externalRounds: start round `round`. Started now while the master is waiting (workers
+  // initialised, previous round at its barrier or none started yet); while a round is in
+  // flight ONE later start is queued and runs the moment the barrier is reached (the client
+  // keeps its round trip off the critical path; rounds still never overlap). Needs
   // round > the last round started (== startRound allowed first) and round <= maxRound.
-  // Returns "" when accepted, otherwise the reason.
-  std::string on_external_start(int round);
+  enum class StartResult { Started, Queued, Refused };
+  StartResult on_external_start(int round, std::string* why);
   bool awaiting_start() const { return awaiting_; }
+  int queued_start() const { return queued_; }
 
   int round() const { return round_; }
   int num_complete() const { return numComplete_; }
@@ -127,6 +133,7 @@ class MasterCore {
   bool finished_ = false;
   bool awaiting_ = false;  // externalRounds: waiting for the client's next StartAllreduce
   bool started_ = false;   // externalRounds: round_ has been started in this epoch
+  int queued_ = -1;        // externalRounds: start queued behind the round in flight (-1 none)
   MasterStats stats_;
 };
 

@@ -138,17 +138,26 @@ void MasterActor::receive(Envelope& env, ActorContext& ctx) {
     core_.on_round_timeout(rt->epoch, rt->round);
   } else if (auto* bc = std::get_if<BridgeCommand>(&env.msg)) {
     if (bridge_ && bc->kind == BridgeCommand::Start) {
-      const std::string why = core_.on_external_start(bc->round);
-      bridge_->reply(bc->client, why.empty()
-                                     ? "{\"type\":\"Accepted\",\"cmd\":\"StartAllreduce\",\"round\":" +
-                                           std::to_string(bc->round) + "}"
-                                     : "{\"type\":\"Error\",\"cmd\":\"StartAllreduce\",\"round\":" +
-                                           std::to_string(bc->round) + ",\"reason\":\"" + json_escape(why) + "\"}");
+      std::string why;
+      const std::string r = std::to_string(bc->round);
+      switch (core_.on_external_start(bc->round, &why)) {
+        case MasterCore::StartResult::Started:
+          bridge_->reply(bc->client, "{\"type\":\"Accepted\",\"cmd\":\"StartAllreduce\",\"round\":" + r + "}");
+          break;
+        case MasterCore::StartResult::Queued:
+          queued_client_ = bc->client;
+          bridge_->reply(bc->client, "{\"type\":\"Queued\",\"cmd\":\"StartAllreduce\",\"round\":" + r + "}");
+          break;
+        case MasterCore::StartResult::Refused:
+          bridge_->reply(bc->client, "{\"type\":\"Error\",\"cmd\":\"StartAllreduce\",\"round\":" + r +
+                                         ",\"reason\":\"" + json_escape(why) + "\"}");
+          break;
+      }
     } else if (bridge_) {
       std::ostringstream o;
       o << "{\"type\":\"Status\",\"round\":" << core_.round() << ",\"epoch\":" << core_.epoch()
         << ",\"workers\":" << core_.workers().size() << ",\"numComplete\":" << core_.num_complete()
-        << ",\"awaiting\":" << (core_.awaiting_start() ? "true" : "false")
+        << ",\"awaiting\":" << (core_.awaiting_start() ? "true" : "false") << ",\"queued\":" << core_.queued_start()
         << ",\"finished\":" << (core_.finished() ? "true" : "false") << "}";
       bridge_->reply(bc->client, o.str());
     }
@@ -171,6 +180,15 @@ void MasterActor::workers_initialized(const InitParams& p, const std::map<int, i
     << (core_.params().externalRounds ? "true" : "false") << "}";
   bridge_->set_init_line(o.str());
   bridge_->publish(o.str());
+}
+
+void MasterActor::queued_start_done(int round, bool started, const std::string& why) {
+  if (!bridge_) return;
+  const std::string r = std::to_string(round);
+  bridge_->reply(queued_client_,
+                 started ? "{\"type\":\"Accepted\",\"cmd\":\"StartAllreduce\",\"round\":" + r + "}"
+                         : "{\"type\":\"Error\",\"cmd\":\"StartAllreduce\",\"round\":" + r +
+                               ",\"reason\":\"queued start dropped: " + json_escape(why) + "\"}");
 }
 
 void MasterActor::complete_seen(int srcId, int round, bool counted) {

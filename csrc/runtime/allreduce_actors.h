@@ -63,6 +63,7 @@ class MasterActor final : public Actor, public MasterEffects {
   void arm_round_timer(int64_t epoch, int round, int ms) override;
   void workers_initialized(const InitParams& p, const std::map<int, int>& ids) override;
   void complete_seen(int srcId, int round, bool counted) override;
+  void queued_start_done(int round, bool started, const std::string& why) override;
 
   // Control bridge (csrc/runtime/control_bridge.h): events go out to its clients, its
   // BridgeCommands come in. Set before the master receives its first message.
@@ -83,6 +84,7 @@ class MasterActor final : public Actor, public MasterEffects {
   RoundCallback on_round_;
   ActorContext* ctx_ = nullptr;
   std::shared_ptr<ControlBridge> bridge_;
+  uint64_t queued_client_ = 0;  // bridge client whose StartAllreduce is queued
   mutable std::mutex stamp_mu_;
   std::vector<double> stamps_;
 };

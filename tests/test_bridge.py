@@ -123,9 +123,10 @@ def test_refused_commands_and_malformed_lines():
         system.shutdown()
 
 
-def test_second_start_before_barrier_is_refused():
-    """A start while a round is in flight is refused, not queued: the reference master never
-    overlaps its own rounds (AllreduceMaster.scala:62-66)."""
+def test_start_during_a_round_is_queued_once():
+    """A start while a round is in flight is queued (ONE at a time) and runs the moment the
+    barrier is reached; rounds never overlap, as with the reference master
+    (AllreduceMaster.scala:62-66)."""
     P, n, chunk, rounds = 2, 8, 2, 4
     system = C.ActorSystem("Inflight", False)
     gate = threading.Event()
@@ -146,15 +147,43 @@ def test_second_start_before_barrier_is_refused():
     try:
         with BridgeClient("127.0.0.1", port) as b:
             b.wait_for("InitWorkers")
-            b.start(0)
-            with pytest.raises(BridgeError, match="barrier"):
-                b.start(1)
+            assert b.start(0)["type"] == "Accepted"
+            assert b.start(1)["type"] == "Queued"
+            with pytest.raises(BridgeError, match="already queued"):
+                b.start(2)
+            st = b.status()
+            assert st["round"] == 0 and st["queued"] == 1, st
             gate.set()
             b.wait_for("RoundComplete", round=0)
-            b.start(1)
+            b.wait_for("Accepted", round=1)  # started at round 0's barrier
             b.wait_for("RoundComplete", round=1)
+            assert b.status()["awaiting"] is True
     finally:
         gate.set()
+        system.shutdown()
+
+
+@pytest.mark.parametrize("pipeline", [True, False])
+def test_drive_pipelined_and_lockstep(pipeline):
+    P, n, chunk, rounds = 3, 50, 7, 20
+    system, master, port, outs, fin = _job(P, n, chunk, rounds, name=f"Pipe{int(pipeline)}")
+    try:
+        with BridgeClient("127.0.0.1", port) as b:
+            b.wait_for("InitWorkers")
+            done = b.drive(range(rounds), pipeline=pipeline)
+            assert [d["round"] for d in done] == list(range(rounds))
+            b.wait_for("AllreduceFinished", rounds=rounds)
+            if pipeline:
+                assert any(e["type"] == "Queued" for e in b.events)
+            else:
+                assert not any(e["type"] == "Queued" for e in b.events)
+        deadline = time.time() + 5
+        while time.time() < deadline and any(len(o) < rounds for o in outs):
+            time.sleep(0.01)
+        for k in range(P):
+            for it in range(rounds):
+                np.testing.assert_array_equal(outs[k][it][0], expected(n, it, P).astype(F))
+    finally:
         system.shutdown()
 
 
