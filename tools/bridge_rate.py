@@ -20,7 +20,7 @@ from akka_allreduce_1_amd.bridge import BridgeClient  # noqa: E402
 from akka_allreduce_1_amd.engine import PlaneJob  # noqa: E402
 
 
-def run(plane, n, rounds, warm, external, chunk):
+def run(plane, n, rounds, warm, external, chunk, pipeline=False):
     P = 2
     if plane == "xgmi":
         dev = torch.device("cuda", 0)
@@ -39,10 +39,18 @@ def run(plane, n, rounds, warm, external, chunk):
             st = []
             with BridgeClient("127.0.0.1", job.bridge_port, timeout=60) as b:
                 b.wait_for("InitWorkers")
-                for r in range(rounds):
-                    b.send({"type": "StartAllreduce", "round": r})
-                    b.wait_for("RoundComplete", round=r)
-                    st.append(time.perf_counter())
+                if pipeline:  # the next start is queued while the round runs (BridgeClient.drive)
+                    b.start(0)
+                    for r in range(rounds):
+                        if r + 1 < rounds:
+                            b.start(r + 1)
+                        b.wait_for("RoundComplete", round=r)
+                        st.append(time.perf_counter())
+                else:  # lock-step: start, wait for the barrier, start the next
+                    for r in range(rounds):
+                        b.send({"type": "StartAllreduce", "round": r})
+                        b.wait_for("RoundComplete", round=r)
+                        st.append(time.perf_counter())
             assert job.finished.wait(30)
             for p in job.planes:
                 p.drain()
@@ -63,9 +71,9 @@ def main():
     for mib in a.mib:
         n = int(mib * 2 ** 20) // (2 if a.plane == "xgmi" else 4)
         chunk = max(1, -(-n // 2) // 128)  # 128 chunks per block (the bench's geometry)
-        for external in (False, True, False, True):
-            ms = run(a.plane, n, a.rounds, a.warmup, external, chunk)
-            print(json.dumps({"plane": a.plane, "MiB_per_worker": mib, "driver": "bridge client" if external else "master",
+        for mode in ("master", "bridge lock-step", "bridge pipelined") * 2:
+            ms = run(a.plane, n, a.rounds, a.warmup, mode != "master", chunk, pipeline=mode == "bridge pipelined")
+            print(json.dumps({"plane": a.plane, "MiB_per_worker": mib, "driver": mode,
                               "rounds": a.rounds, "ms_per_round": round(ms, 4)}), flush=True)
 
 
