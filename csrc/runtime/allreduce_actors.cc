@@ -176,7 +176,8 @@ void MasterActor::workers_initialized(const InitParams& p, const std::map<int, i
   }
   o << "],\"thReduce\":" << p.thReduce << ",\"thComplete\":" << p.thComplete << ",\"maxLag\":" << p.maxLag
     << ",\"dataSize\":" << p.dataSize << ",\"maxChunkSize\":" << p.maxChunkSize
-    << ",\"startRound\":" << p.startRound << ",\"externalRounds\":"
+    << ",\"startRound\":" << p.startRound << ",\"maxRound\":" << core_.params().maxRound
+    << ",\"externalRounds\":"
     << (core_.params().externalRounds ? "true" : "false") << "}";
   bridge_->set_init_line(o.str());
   bridge_->publish(o.str());

@@ -16,6 +16,12 @@
 //   mxar-gpu worker ... --device K   (the same executable linked with csrc/tools/mxar_gpu.cc)
 //       the worker's rounds run on GPU K: an XgmiRoundPlane under a PlaneWorkerActor, the
 //       source filled on the device. Workers on one node exchange through the xGMI arena.
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+#include <map>
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -59,6 +65,7 @@ struct Options {
   float th_allreduce = 1.f, th_reduce = 0.9f, th_complete = 0.8f;  // AllreduceMaster.scala:105-107
   int bridge_port = -1;                 // --bridge PORT (control bridge, docs/BRIDGE.md)
   bool external_rounds = false;         // --external-rounds
+  bool lockstep = false;                // drive: start the next round only after the barrier
   int max_lag = 1, max_round = 100, round_timeout_ms = 0;          // :108-109
   std::string loglevel = "INFO";
   bool quiet = false;
@@ -74,6 +81,7 @@ struct Options {
                "options: --host H --seeds a[,b] --th-allreduce F --th-reduce F --th-complete F --max-lag N\n"
                "         --max-round N --round-timeout-ms N --loglevel L --quiet\n"
                "master control bridge (docs/BRIDGE.md): --bridge PORT [--external-rounds]\n"
+               "       mxar drive [host:]bridgePort [rounds] [--lockstep]   (bridge client)\n"
                "worker on a GPU (mxar-gpu): --device K [--max-peers N --plane-max-lag N --grid N --plane-timeout S]\n",
                msg);
   std::exit(2);
@@ -100,6 +108,7 @@ Options parse(int argc, char** argv) {
     else if (a == "--round-timeout-ms") o.round_timeout_ms = std::stoi(val());
     else if (a == "--bridge") o.bridge_port = std::stoi(val());
     else if (a == "--external-rounds") o.external_rounds = true;
+    else if (a == "--lockstep") o.lockstep = true;
     else if (a == "--loglevel") o.loglevel = val();
     else if (a == "--quiet") o.quiet = true;
     else if (a == "--device") o.device = std::stoi(val());
@@ -257,6 +266,109 @@ void set_level(const std::string& l) {
 
 }  // namespace
 
+// `mxar drive [host:]port [rounds] [--lockstep]`: a Python-free control-bridge client
+// (docs/BRIDGE.md) that plays AllreduceMaster's round loop (AllreduceMaster.scala:58-67,
+// 91-97) against a master started with --bridge PORT --external-rounds. Pipelined by default
+// (the next start is queued while a round runs). Prints one JSON summary line.
+[[noreturn]] void run_drive(const Options& o) {
+  if (o.positional.empty()) usage("drive: missing [host:]port");
+  std::string host = o.host, hp = o.positional[0];
+  if (auto c = hp.rfind(':'); c != std::string::npos) {
+    host = hp.substr(0, c);
+    hp = hp.substr(c + 1);
+  }
+  const int port = std::stoi(hp);
+  const int want = pos_int(o, 1, -1);  // -1: through maxRound (from InitWorkers' job)
+  int fd = -1;
+  for (int attempt = 0; attempt < 300 && fd < 0 && !g_stop; ++attempt) {  // the master may still be starting
+    fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons(static_cast<uint16_t>(port));
+    ::inet_pton(AF_INET, host.c_str(), &a.sin_addr);
+    if (::connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0) {
+      ::close(fd);
+      fd = -1;
+      std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    }
+  }
+  if (fd < 0) throw std::runtime_error("drive: cannot connect to " + host + ":" + hp);
+  int one = 1;
+  ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  std::string buf;
+  auto next_line = [&]() -> std::map<std::string, std::string> {
+    for (;;) {
+      if (auto nl = buf.find('\n'); nl != std::string::npos) {
+        std::string line = buf.substr(0, nl);
+        buf.erase(0, nl + 1);
+        std::map<std::string, std::string> kv;
+        if (!parse_flat_json(line, kv)) {  // InitWorkers carries an array: pull its scalars by hand
+          kv.clear();
+          for (const char* k : {"type", "startRound", "maxRound", "epoch"}) {
+            auto at = line.find(std::string("\"") + k + "\":");
+            if (at == std::string::npos) continue;
+            at += std::strlen(k) + 3;
+            auto end = line.find_first_of(",}", at);
+            std::string v = line.substr(at, end - at);
+            if (!v.empty() && v.front() == '"') v = v.substr(1, v.size() - 2);
+            kv[k] = v;
+          }
+        }
+        if (kv["type"] == "Error") throw std::runtime_error("drive: bridge refused: " + line);
+        return kv;
+      }
+      char tmp[65536];
+      ssize_t n = ::recv(fd, tmp, sizeof(tmp), 0);
+      if (n <= 0) throw std::runtime_error("drive: bridge closed the connection");
+      buf.append(tmp, static_cast<size_t>(n));
+    }
+  };
+  auto send_start = [&](int r) {
+    const std::string l = "{\"type\":\"StartAllreduce\",\"round\":" + std::to_string(r) + "}\n";
+    if (::send(fd, l.data(), l.size(), MSG_NOSIGNAL) != static_cast<ssize_t>(l.size()))
+      throw std::runtime_error("drive: send failed");
+  };
+  std::map<std::string, std::string> m;
+  do m = next_line(); while (m["type"] != "InitWorkers");
+  const int first = std::stoi(m["startRound"]);
+  const int max_round = std::stoi(m["maxRound"]);
+  const int last = want > 0 ? std::min(max_round, first + want - 1) : max_round;
+  std::vector<double> stamps;
+  int completed = 0, next = first;
+  bool finished = false;
+  send_start(next++);
+  if (!o.lockstep && next <= last) send_start(next++);  // one queued behind the first
+  while (!finished && !g_stop) {
+    m = next_line();
+    const std::string& t = m["type"];
+    if (t == "RoundComplete") {
+      stamps.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count());
+      ++completed;
+      if (completed >= last - first + 1) break;
+      if (o.lockstep) send_start(next++);
+    } else if (t == "Accepted" && !o.lockstep) {  // round r started: queue r + 1 behind it
+      if (std::stoi(m["round"]) == next - 1 && next <= last) send_start(next++);
+    } else if (t == "AllreduceFinished") {
+      finished = true;
+    } else if (t == "InitWorkers") {
+      throw std::runtime_error("drive: workers re-initialised (epoch " + m["epoch"] + ")");
+    }
+  }
+  ::close(fd);
+  double rate = 0, p50 = 0;
+  if (stamps.size() > 2) {
+    std::vector<double> iv;
+    for (size_t i = 1; i < stamps.size(); ++i) iv.push_back((stamps[i] - stamps[i - 1]) * 1e6);
+    std::sort(iv.begin(), iv.end());
+    rate = static_cast<double>(stamps.size() - 1) / (stamps.back() - stamps.front());
+    p50 = iv[iv.size() / 2];
+  }
+  std::printf("{\"driver\": \"%s\", \"rounds\": %d, \"rounds_per_s\": %.1f, \"round_interval_p50_us\": %.1f}\n",
+              o.lockstep ? "bridge lock-step" : "bridge pipelined", completed, rate, p50);
+  std::fflush(stdout);
+  exit_now(completed > 0 ? 0 : 1);
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) usage("missing role");
   std::signal(SIGINT, on_signal);
@@ -267,6 +379,7 @@ int main(int argc, char** argv) {
   try {
     if (role == "master") run_master(o);
     if (role == "worker") run_worker(o);
+    if (role == "drive") run_drive(o);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "mxar %s: %s\n", role.c_str(), e.what());
     exit_now(1);

@@ -5,6 +5,7 @@ can watch a job or drive its rounds.
 Driving mode mirrors AllreduceMaster.scala:58-67,91-97 from outside: the client sends
 StartAllreduce(r), the master forwards it to the workers and reports the barrier.
 """
+import json
 import os
 import subprocess
 import sys
@@ -365,3 +366,41 @@ def test_worker_loss_while_the_client_drives():
             assert all(c == 2 for c in counts)
     finally:
         system.shutdown()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("lockstep", [False, True])
+def test_native_drive_client(lockstep):
+    """No Python anywhere: `mxar master --bridge --external-rounds`, two `mxar worker`s and the
+    `mxar drive` bridge client (pipelined, or lock-step) run the whole job."""
+    from akka_allreduce_1_amd.parallel.comm import free_port
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "akka_allreduce_1_amd", "mxar")
+    if not os.path.exists(exe):
+        pytest.skip("native executable not built (tools/build_native.py)")
+    mport, bport = free_port(), free_port()
+    seed = ["--seeds", f"mxar.tcp://ClusterSystem@127.0.0.1:{mport}", "--loglevel", "ERROR"]
+    rounds = 40
+    procs = [subprocess.Popen([exe, "master", str(mport), "2", "12", "2", "--th-reduce", "1", "--th-complete", "1",
+                               "--bridge", str(bport), "--external-rounds", "--max-round", str(rounds - 1)] + seed,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)]
+    try:
+        procs += [subprocess.Popen([exe, "worker", "0", "12"] + seed, stdout=subprocess.DEVNULL,
+                                   stderr=subprocess.DEVNULL) for _ in range(2)]
+        drive = subprocess.run([exe, "drive", f"127.0.0.1:{bport}"] + (["--lockstep"] if lockstep else []),
+                               capture_output=True, text=True, timeout=120)
+        assert drive.returncode == 0, (drive.stdout, drive.stderr)
+        line = json.loads(drive.stdout.strip().splitlines()[-1])
+        assert line["rounds"] == rounds and line["rounds_per_s"] > 0, line
+        assert line["driver"] == ("bridge lock-step" if lockstep else "bridge pipelined")
+        out, _ = procs[0].communicate(timeout=30)
+        assert procs[0].returncode == 0 and f"finished {rounds} rounds" in out, out
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(10)
+                except subprocess.TimeoutExpired:
+                    p.kill()
