@@ -447,6 +447,44 @@ def dp_step(comm: XgmiCommunicator, model: str, dev) -> dict:
     return row
 
 
+def bridge_driven_rounds(P, n, chunk, dtype, rounds, warm, xs, ref) -> dict:
+    """The same job with the rounds driven from OUTSIDE the engine: a control-bridge client
+    (docs/BRIDGE.md, JSON lines over TCP, the way a JVM Akka client would) sends each
+    StartAllreduce, pipelined (the next start queued while a round runs); timed by the
+    client's RoundComplete arrivals."""
+    from akka_allreduce_1_amd.bridge import BridgeClient
+    from akka_allreduce_1_amd.engine import PlaneJob
+
+    row: dict = {"driver": "control-bridge client, pipelined StartAllreduce (JSON lines over TCP)"}
+    job = PlaneJob(P, n, max_chunk_size=chunk, dtype=dtype, max_round=rounds - 1, sources=xs,
+                   keep_outputs=False, keep_last=True, timeout_s=20.0, bridge_port=0, external_rounds=True)
+    try:
+        job.start()
+        stamps = []
+        with BridgeClient("127.0.0.1", job.bridge_port, timeout=60) as b:
+            b.wait_for("InitWorkers")
+            b.start(0)
+            for r in range(rounds):
+                if r + 1 < rounds:
+                    b.start(r + 1)
+                b.wait_for("RoundComplete", round=r)
+                stamps.append(time.perf_counter())
+        if not job.finished.wait(30):
+            raise TimeoutError("bridge-driven job did not finish")
+        for p in job.planes:
+            p.drain()
+        o = job.last_output(0)
+        row["validated"] = bool(o is not None and o.iteration == rounds - 1 and torch.equal(o.data, ref))
+        per = (stamps[-1] - stamps[warm - 1]) / (len(stamps) - warm)
+        row["ms_per_round"] = round(per * 1e3, 4)
+        row["rounds_per_s"] = round(1.0 / per, 2)
+    except Exception as e:  # noqa: BLE001 - reported, never loses the protocol row
+        row["error"] = repr(e)
+    finally:
+        job.shutdown()
+    return row
+
+
 def protocol_rounds(args, rank: int, world: int, dev) -> dict:
     """The reference's protocol driving the GPU engine: the master's
     StartAllreduce(r) becomes one threshold-kernel round per worker on the xGMI round plane
@@ -492,6 +530,7 @@ def protocol_rounds(args, rank: int, world: int, dev) -> dict:
                 job.shutdown()
             ref = (xs[0].float() + xs[1].float()).to(dtype)
             row["validated"] = bool(torch.equal(last["y"], ref))
+            row["bridge"] = bridge_driven_rounds(P, n, chunk, dtype, rounds, warm, xs, ref)
         else:
             x = fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=700 + rank)
             last = {}
