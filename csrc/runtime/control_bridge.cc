@@ -210,10 +210,13 @@ void ControlBridge::reap() {  // join readers of clients that went away (mu_ not
       }
     }
   }
-  for (auto& c : dead) {
-    if (c->reader.joinable()) c->reader.join();
-    ::close(c->fd);
-  }
+  for (auto& c : dead)
+    if (c->reader.joinable()) c->reader.join();  // the fd closes with the last reference
+}
+
+ControlBridge::Client::~Client() {
+  if (reader.joinable()) reader.detach();  // only reachable from the reader itself at shutdown
+  if (fd >= 0) ::close(fd);
 }
 
 void ControlBridge::accept_loop() {
@@ -304,7 +307,14 @@ void ControlBridge::stop() {
     char x = 1;
     (void)!::write(wake_[1], &x, 1);
   }
-  if (acceptor_.joinable()) acceptor_.join();
+  // stop() can run on one of our own threads: a reader's tell() briefly owns the master's
+  // cell, and if the system dropped it meanwhile the master (and this bridge) die there.
+  auto join = [](std::thread& t) {
+    if (!t.joinable()) return;
+    if (t.get_id() == std::this_thread::get_id()) t.detach();
+    else t.join();
+  };
+  join(acceptor_);
   std::vector<std::shared_ptr<Client>> cs;
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -314,8 +324,7 @@ void ControlBridge::stop() {
   for (auto& c : cs) {
     c->dead = true;
     ::shutdown(c->fd, SHUT_RDWR);
-    if (c->reader.joinable()) c->reader.join();
-    ::close(c->fd);
+    join(c->reader);
   }
   if (lfd_ >= 0) ::close(lfd_);
   for (int& f : wake_)

@@ -66,8 +66,9 @@ class ControlBridge : public std::enable_shared_from_this<ControlBridge> {
 
  private:
   struct Client {
+    ~Client();  // closes fd: only once no publisher can still be writing to it
     uint64_t id;
-    int fd;
+    int fd = -1;
     std::mutex wmu;
     std::thread reader;
     std::atomic<bool> dead{false};

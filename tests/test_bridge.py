@@ -404,3 +404,32 @@ def test_native_drive_client(lockstep):
                     p.wait(10)
                 except subprocess.TimeoutExpired:
                     p.kill()
+
+
+def test_client_churn_while_rounds_publish():
+    """Observers connect, read a little and vanish (some mid-line) while the master publishes
+    every CompleteAllreduce / RoundComplete: the job is unaffected and the bridge keeps
+    serving (reap / close / publish never race on a reused fd)."""
+    import socket as pysock
+
+    P, n, chunk, rounds = 2, 64, 8, 400
+    system, master, port, outs, fin = _job(P, n, chunk, rounds, external=False, name="Churn")
+    try:
+        t_end = time.time() + 20
+        churned = 0
+        while not fin.is_set() and time.time() < t_end:
+            s = pysock.create_connection(("127.0.0.1", port), timeout=5)
+            s.recv(64)  # part of Hello / InitWorkers / events
+            if churned % 3 == 0:
+                s.sendall(b'{"type":"Sta')  # half a command, then gone
+            s.close()
+            churned += 1
+        assert fin.wait(30)
+        assert churned > 5
+        with BridgeClient("127.0.0.1", port) as b:
+            st = b.status()
+            assert st["finished"] is True
+        for k in range(P):
+            np.testing.assert_array_equal(outs[k][rounds - 1][0], expected(n, rounds - 1, P).astype(F))
+    finally:
+        system.shutdown()
