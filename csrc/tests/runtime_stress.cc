@@ -4,7 +4,13 @@
 // so the sanitizer sees every thread. Exit 0 = all rounds exact and clean shutdown.
 //
 //   build + run: python tools/sanitize.py --sanitize thread
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
 #include <atomic>
+#include <map>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -17,6 +23,7 @@
 #include "../cluster/cluster_node.h"
 #include "../core/log.h"
 #include "../runtime/allreduce_actors.h"
+#include "../runtime/control_bridge.h"
 #include "../runtime/fault_injector.h"
 #include "../runtime/loopback_plane.h"
 #include "../runtime/plane_worker.h"
@@ -76,6 +83,115 @@ static int run_local(int P, int N, int C, int rounds) {
           std::fprintf(stderr, "bad sum worker %d round %d idx %d\n", k, r, i);
           return 1;
         }
+  return 0;
+}
+
+// The control bridge (csrc/runtime/control_bridge.h): an external driver thread runs every
+// round through a socket, pipelined (one StartAllreduce queued behind the round in flight),
+// while churn threads connect, half-send and vanish - bridge reader / acceptor / reaper
+// threads, the master's publishes and client fds all under the sanitizer.
+static int connect_to(int port) {
+  int fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(static_cast<uint16_t>(port));
+  ::inet_pton(AF_INET, "127.0.0.1", &a.sin_addr);
+  if (::connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0) {
+    ::close(fd);
+    return -1;
+  }
+  return fd;
+}
+
+static int run_bridge(int P, int N, int C, int rounds) {
+  auto sys = std::make_shared<ActorSystem>("ClusterSystem", ActorSystem::Mode::Threaded, 4);
+  std::atomic<bool> done{false};
+  MasterParams mp{P, 1.f, 1.f, 1.f, 1, N, rounds - 1, C, false};
+  mp.externalRounds = true;
+  auto actor = std::make_unique<MasterActor>(mp, [&](int) { done = true; });
+  auto bridge = ControlBridge::start("127.0.0.1", 0);
+  actor->set_bridge(bridge);
+  ActorRef master = sys->actor_of(std::move(actor), "master");
+  bridge->attach(master, master->path());
+  const int port = bridge->port();
+  std::atomic<int> sinks{0};
+  for (int k = 0; k < P; ++k) {
+    DataSource src = [N](const AllReduceInputRequest& r) {
+      std::vector<float> v(N, static_cast<float>(r.iteration));
+      return AllReduceInput{make_host_payload(std::move(v))};
+    };
+    DataSink sink = [&](const AllReduceOutput&) { sinks++; };
+    ActorRef w = sys->actor_of(std::make_unique<WorkerActor>(src, sink), "worker" + std::to_string(k));
+    master->tell(MemberUp{w, "worker", ""}, nullptr);
+  }
+  std::atomic<bool> stop_churn{false};
+  std::vector<std::thread> churn;
+  for (int t = 0; t < 3; ++t)
+    churn.emplace_back([&, t] {
+      for (int i = 0; !stop_churn.load(); ++i) {
+        int fd = connect_to(port);
+        if (fd < 0) continue;
+        char b[32];
+        (void)!::recv(fd, b, sizeof(b), 0);
+        if ((i + t) % 2) (void)!::send(fd, "{\"type\":\"Sta", 12, MSG_NOSIGNAL);
+        ::close(fd);
+      }
+    });
+  int completed = 0;
+  std::string err;
+  {
+    int fd = -1;
+    for (int i = 0; i < 100 && fd < 0; ++i) fd = connect_to(port);
+    std::string buf;
+    auto line = [&]() -> std::map<std::string, std::string> {
+      for (;;) {
+        if (auto nl = buf.find('\n'); nl != std::string::npos) {
+          std::string l = buf.substr(0, nl);
+          buf.erase(0, nl + 1);
+          std::map<std::string, std::string> kv;
+          if (!parse_flat_json(l, kv)) kv["type"] = l.find("InitWorkers") != std::string::npos ? "InitWorkers" : "?";
+          return kv;
+        }
+        char tmp[4096];
+        ssize_t n = ::recv(fd, tmp, sizeof(tmp), 0);
+        if (n <= 0) return {{"type", "EOF"}};
+        buf.append(tmp, static_cast<size_t>(n));
+      }
+    };
+    auto start = [&](int r) {
+      std::string l = "{\"type\":\"StartAllreduce\",\"round\":" + std::to_string(r) + "}\n";
+      (void)!::send(fd, l.data(), l.size(), MSG_NOSIGNAL);
+    };
+    std::map<std::string, std::string> m;
+    do m = line(); while (m["type"] != "InitWorkers" && m["type"] != "EOF");
+    int next = 0;
+    start(next++);
+    start(next++);
+    while (completed < rounds) {
+      m = line();
+      if (m["type"] == "EOF" || m["type"] == "Error") {
+        err = "bridge driver got " + m["type"] + " " + m["reason"];
+        break;
+      }
+      if (m["type"] == "RoundComplete") ++completed;
+      if (m["type"] == "Accepted" && std::stoi(m["round"]) == next - 1 && next < rounds) start(next++);
+    }
+    ::close(fd);
+  }
+  stop_churn = true;
+  for (auto& t : churn) t.join();
+  const bool ok = err.empty() && wait_until([&] { return done.load(); }, 30);
+  sys->await_idle(std::chrono::milliseconds(5000));
+  sys->shutdown();
+  bridge.reset();
+  if (!ok) {
+    std::fprintf(stderr, "bridge-driven job failed: %s (rounds %d)\n", err.c_str(), completed);
+    return 1;
+  }
+  if (sinks.load() != P * rounds) {
+    std::fprintf(stderr, "bridge-driven job: %d outputs, want %d\n", sinks.load(), P * rounds);
+    return 1;
+  }
   return 0;
 }
 
@@ -240,6 +356,7 @@ int main(int argc, char** argv) {
   if (rc == 0 && (only.empty() || only == "local2")) rc = run_local(3, 9, 2, 30);
   if (rc == 0 && (only.empty() || only == "tcp")) rc = run_tcp(20);
   if (rc == 0 && (only.empty() || only == "plane")) rc = run_plane(3, 41, 4, 40);
+  if (rc == 0 && (only.empty() || only == "bridge")) rc = run_bridge(3, 23, 4, 60);
   std::printf(rc == 0 ? "runtime_stress: OK\n" : "runtime_stress: FAILED\n");
   return rc;
 }
