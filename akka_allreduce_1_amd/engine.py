@@ -219,7 +219,8 @@ class PlaneJob:
 
 def distributed_plane_job(n: int, source, *, max_chunk_size: int, dtype: torch.dtype, rounds: int,
                           th: float = 1.0, max_lag: int = 1, grid: int = 0, timeout_s: float = 300.0,
-                          on_output: Callable | None = None, keep_last: bool = False) -> dict:
+                          on_output: Callable | None = None, keep_last: bool = False,
+                          external_client: bool = False) -> dict:
     """One plane worker per torch.distributed rank (one process per GPU), the master on rank 0,
     the reference's cluster shape: workers join rank 0's seed over TCP (127.0.0.1) and
     announce their plane descriptors in the join; the master relays them in InitWorkers and
@@ -227,6 +228,9 @@ def distributed_plane_job(n: int, source, *, max_chunk_size: int, dtype: torch.d
     used only to agree on the seed port and to hold the ranks until the master is done.
     `source`: a callable or a GPU tensor (fetched natively every round); keep_last: a native
     sink keeps the newest output (returned as "last") instead of calling `on_output`.
+    external_client: the master runs in externalRounds mode with a control bridge and rank 0
+    drives the rounds through it as an outside client would (docs/BRIDGE.md, pipelined
+    StartAllreduce); "stamps" are then the client's RoundComplete arrival times.
     Returns (rank 0) {"stamps": round completion times, "state": worker state}."""
     import torch.distributed as dist
 
@@ -257,17 +261,37 @@ def distributed_plane_job(n: int, source, *, max_chunk_size: int, dtype: torch.d
     master = None
     if rank == 0:
         master = system.master(world, 1.0, th, th, max_lag, n, rounds - 1, max_chunk_size,
-                               on_finished=lambda r: fin.set())
+                               on_finished=lambda r: fin.set(), externalRounds=external_client,
+                               bridgePort=0 if external_client else -1)
     node = C.ClusterNode.start(system, cc)
     if master is not None:
         node.subscribe(master)
     ok = [True]
-    if rank == 0:
+    client_stamps: list[float] = []
+    if rank == 0 and external_client:
+        from .bridge import BridgeClient
+
+        try:
+            with BridgeClient("127.0.0.1", system.master_bridge_port(master), timeout=min(120.0, timeout_s)) as b:
+                b.wait_for("InitWorkers")
+                b.start(0)
+                for r in range(rounds):
+                    if r + 1 < rounds:
+                        b.start(r + 1)  # queued behind round r
+                    b.wait_for("RoundComplete", round=r)
+                    client_stamps.append(time.perf_counter())
+        except Exception as e:  # noqa: BLE001 - the ranks must still leave together
+            ok = [False]
+            client_stamps = []
+            import warnings
+
+            warnings.warn(f"bridge-driven job failed: {e!r}", RuntimeWarning, stacklevel=2)
+    if rank == 0 and ok[0]:
         ok = [fin.wait(timeout_s)]
     dist.broadcast_object_list(ok, src=0)
     plane.drain()
     system.await_idle(5.0)
-    stamps = system.master_round_stamps(master) if master is not None else []
+    stamps = (client_stamps if external_client else system.master_round_stamps(master)) if master is not None else []
     out = {"ok": bool(ok[0]), "stamps": stamps, "state": system.plane_worker_state(worker),
            "plane": {"launches": plane.stats.launches, "chunk_elems": plane.chunk_elems, "chunks": plane.chunks},
            "last": last.last() if last is not None else None}

@@ -571,6 +571,28 @@ def protocol_rounds(args, rank: int, world: int, dev) -> dict:
                 dist.all_gather_object(detail, mine)
                 row["validation_detail"] = detail
             row["note"] = "one worker per GPU process; master on rank 0; control over TCP, data over xGMI"
+            if row["validated"]:  # the same job with rounds driven by a control-bridge client on rank 0
+                b: dict = {"driver": "control-bridge client on rank 0, pipelined StartAllreduce (JSON lines over TCP)"}
+                res2 = distributed_plane_job(n, x, max_chunk_size=chunk, dtype=dtype, rounds=rounds, grid=grid,
+                                             keep_last=True, timeout_s=120.0, external_client=True)
+                ids2 = [None] * world
+                dist.all_gather_object(ids2, res2["state"]["id"])
+                ref2 = torch.zeros(n, device=dev)
+                for k in sorted(range(world), key=lambda q: ids2[q]):
+                    ref2 += fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=700 + k).float()
+                y2 = res2["last"]
+                ok2 = bool(res2["ok"] and y2 is not None and y2.iteration == rounds - 1
+                           and torch.equal(y2.data, ref2.to(dtype)))
+                del ref2
+                good2 = torch.tensor([1 if ok2 else 0], device=dev)
+                dist.all_reduce(good2, op=dist.ReduceOp.MIN)
+                b["validated"] = bool(good2.item())
+                st2 = res2["stamps"]
+                if len(st2) > warm + 1:
+                    per2 = (st2[-1] - st2[warm - 1]) / (len(st2) - warm)
+                    b["ms_per_round"] = round(per2 * 1e3, 4)
+                    b["rounds_per_s"] = round(1.0 / per2, 2)
+                row["bridge"] = b
         if len(stamps) > warm + 1:
             per = (stamps[-1] - stamps[warm - 1]) / (len(stamps) - warm)
             row["ms_per_round"] = round(per * 1e3, 4)
