@@ -617,3 +617,55 @@ def test_bridge_client_drives_gpu_rounds():
         assert job.planes[0].stats.launches == rounds
     finally:
         job.shutdown()
+
+
+def _dist_job_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.engine import distributed_plane_job
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = []
+    try:
+        n, rounds = 100_003, 8
+        x = torch.arange(n, dtype=torch.float32, device=DEV) + 1000.0 * rank  # exact in fp32
+        want = sum(torch.arange(n, dtype=torch.float64) + 1000.0 * k for k in range(world)).float()
+        for external in (False, True):
+            res = distributed_plane_job(n, x, max_chunk_size=4001, dtype=torch.float32, rounds=rounds,
+                                        grid=max(8, 512 // world), keep_last=True, timeout_s=60.0,
+                                        external_client=external)
+            y = res["last"]
+            ok = bool(res["ok"] and y is not None and y.iteration == rounds - 1
+                      and torch.equal(y.data.cpu(), want))
+            out.append((external, ok, len(res["stamps"]) if rank == 0 else rounds))
+    except Exception as e:  # report, never hang the parent
+        out.append(("error", False, repr(e)))
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_distributed_plane_job_master_and_bridge_driven():
+    """One plane worker per process (the N > 1 bench's protocol shape, here 2 processes on one
+    GPU): the master on rank 0 drives the rounds, then a control-bridge client on rank 0 does
+    (docs/BRIDGE.md); every rank's last output is the exact sum both times."""
+    import multiprocessing as mp
+
+    from akka_allreduce_1_amd.parallel import free_port
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_dist_job_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    for rank, out in res:
+        assert [o[:2] for o in out] == [(False, True), (True, True)], (rank, out)
+        assert all(o[2] == 8 for o in out), (rank, out)
