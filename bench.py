@@ -574,7 +574,7 @@ def protocol_rounds(args, rank: int, world: int, dev) -> dict:
             if row["validated"]:  # the same job with rounds driven by a control-bridge client on rank 0
                 b: dict = {"driver": "control-bridge client on rank 0, pipelined StartAllreduce (JSON lines over TCP)"}
                 res2 = distributed_plane_job(n, x, max_chunk_size=chunk, dtype=dtype, rounds=rounds, grid=grid,
-                                             keep_last=True, timeout_s=120.0, external_client=True)
+                                             keep_last=True, timeout_s=45.0, external_client=True)
                 ids2 = [None] * world
                 dist.all_gather_object(ids2, res2["state"]["id"])
                 ref2 = torch.zeros(n, device=dev)
@@ -641,6 +641,8 @@ def main() -> None:
     ap.add_argument("--no-dp", action="store_true", help="skip the ResNet-50 / Llama-3-8B DP-step sections")
     ap.add_argument("--no-local", action="store_true", help="skip the 8-logical-rank section at N = 1")
     ap.add_argument("--no-protocol", action="store_true", help="skip the master/worker protocol-engine section")
+    ap.add_argument("--protocol-timeout", type=float, default=240.0,
+                    help="native watchdog over the protocol section (s); the result line is written either way")
     ap.add_argument("--dp-rehearsal", action="store_true", help="with --share-device: run the ResNet-50 DP step too")
     ap.add_argument("--dp-timeout", type=float, default=240.0,
                     help="seconds for the DP-step sections; past it the result line is written without them")
@@ -859,8 +861,19 @@ def main() -> None:
         log(rank, "local_ranks: 8 logical ranks in one launch")
         result["local_ranks"] = local_ranks(dev, args, P=8)
     if engine_ok and not args.no_protocol:
-        # the reference's master/worker round protocol driving the GPU engine
-        result["protocol"] = protocol_rounds(args, rank, world, dev)
+        # the reference's master/worker round protocol driving the GPU engine, under the same
+        # native watchdog as the dp section: a stuck round never costs the result line
+        from akka_allreduce_1_amd._native import C
+
+        timed_out = dict(result, protocol={"error": f"timed out after {args.protocol_timeout:g} s"},
+                         status="protocol_timeout")
+        sys.stdout.flush()
+        cancel = C.watchdog_arm(args.protocol_timeout, _RESULT_FD if rank == 0 else -1,
+                                json.dumps(timed_out) + "\n", 0)
+        prot = protocol_rounds(args, rank, world, dev)
+        if not cancel():  # the watchdog fired and wrote the line; the process is exiting
+            return
+        result["protocol"] = prot
     if engine_ok and not args.no_dp and (not args.share_device or args.dp_rehearsal):
         # configs 4 / 5 (full Llama-3-8B: 32 GB of params + grads per rank). Not in the
         # one-GPU rehearsal: there every rank's spinning comm kernel shares the device with the
