@@ -40,10 +40,10 @@ class BridgeDriver(host: String, port: Int, maxRound: Int) extends Actor with Ac
   reader.setDaemon(true)
   reader.start()
 
-  private var round = -1
+  private var lastSent = -1  // newest StartAllreduce sent (at most one queued behind the round in flight)
 
   private def startAllreduce(r: Int): Unit = {  // AllreduceMaster.scala:91-97
-    round = r
+    lastSent = r
     log.info(s"----Start allreduce round $r")
     out.println(s"""{"type":"StartAllreduce","round":$r}""")
   }
@@ -53,12 +53,16 @@ class BridgeDriver(host: String, port: Int, maxRound: Int) extends Actor with Ac
       field(json, "type") match {
         case Some("InitWorkers") =>
           log.info(s"----workers initialised: $json")
-          if (round < 0) startAllreduce(field(json, "startRound").map(_.toInt).getOrElse(0))
+          if (lastSent < 0) startAllreduce(field(json, "startRound").map(_.toInt).getOrElse(0))
+        case Some("Accepted") =>
+          // round r is running: queue r + 1 now, so the master starts it at r's barrier
+          // without waiting for this actor (docs/BRIDGE.md "Queued starts")
+          val r = field(json, "round").map(_.toInt).getOrElse(-1)
+          if (r == lastSent && r < maxRound) startAllreduce(r + 1)
         case Some("CompleteAllreduce") =>  // AllreduceMaster.scala:58-61
           log.info(s"----Node ${field(json, "srcId").getOrElse("?")} completes allreduce round ${field(json, "round").getOrElse("?")}")
         case Some("RoundComplete") =>  // the barrier of AllreduceMaster.scala:62-66
-          val r = field(json, "round").map(_.toInt).getOrElse(-1)
-          if (r == round && r < maxRound) startAllreduce(r + 1)
+          log.info(s"----round ${field(json, "round").getOrElse("?")} complete")
         case Some("AllreduceFinished") =>
           log.info("----All rounds complete"); context.stop(self)
         case Some("Error") => log.warning(s"bridge refused: $json")
