@@ -283,29 +283,41 @@ class XgmiCommunicator:
         elif algo == "threshold" and self._threshold_fits(inp):
             # the straggler-tolerant kernel at th = 1 is an exact allreduce with its own
             # geometry (one chunk per workgroup, round-robin gather); a tune() candidate
-            self.allreduce_threshold(inp, out, op=op)
-        elif algo in ("p2p", "rsag"):  # the same protocol over RCCL point-to-point / RS+AG
-            self.p2p.allreduce(inp, out, op=op, algo=algo)
-        elif algo == "rccl" or code is None:
-            import torch.distributed as dist
+            self.allreduce_threshold(inp, out, op=op, stream=stream)
+        elif algo in ("p2p", "rsag", "rccl") or code is None:
+            # library paths enqueue on torch's current stream: make it the caller's stream,
+            # so a DP reducer's bucket still overlaps with compute (no raw-stream argument)
+            with self._on_stream(stream):
+                if algo in ("p2p", "rsag"):  # the same protocol over RCCL point-to-point / RS+AG
+                    self.p2p.allreduce(inp, out, op=op, algo=algo)
+                else:
+                    import torch.distributed as dist
 
-            if out.data_ptr() != inp.data_ptr():
-                out.copy_(inp)
-            dist.all_reduce(out, group=self.group)
-            if op == "avg":
-                out.div_(self.world)
+                    if out.data_ptr() != inp.data_ptr():
+                        out.copy_(inp)
+                    dist.all_reduce(out, group=self.group)
+                    if op == "avg":
+                        out.div_(self.world)
         else:
             # "twoshot@256": workgroup count chosen by tune(); "twoshot@256~1": and one scatter
             # unit per workgroup (coarse chunks) instead of the size-based geometry
             label, _, u = algo.partition("~")
             name, _, g = label.partition("@")
             if name == "threshold":  # no lag ring, or too large for one launch
-                return self.allreduce(inp, out, op=op, algo="twoshot")
+                return self.allreduce(inp, out, op=op, algo="twoshot", stream=stream)
             if name not in ALGOS:
                 raise ValueError(f"unknown algo {algo!r}")
             self._launch[algo] = (ALGOS[name], int(g) if g else self._default_grid, int(u) if u else self._default_units)
             return self.allreduce(inp, out, op=op, algo=algo, stream=stream)
         return out
+
+    def _on_stream(self, stream: int | None):
+        """Context making the raw HIP stream `stream` torch's current stream (no-op for None)."""
+        import contextlib
+
+        if stream is None:
+            return contextlib.nullcontext()
+        return torch.cuda.stream(torch.cuda.ExternalStream(stream, device=self.device))
 
     def allreduce_(self, t: torch.Tensor, *, op: str = "sum", algo: str = "auto",
                    stream: int | None = None) -> torch.Tensor:
@@ -316,7 +328,8 @@ class XgmiCommunicator:
                 and t.numel() * t.element_size() <= self.world * self.slot_bytes)
 
     def allreduce_threshold(self, inp: torch.Tensor, out: torch.Tensor | None = None, *, th_reduce: float = 1.0,
-                            th_complete: float = 1.0, counts: bool = False, op: str = "sum", rescale: bool = False):
+                            th_complete: float = 1.0, counts: bool = False, op: str = "sum", rescale: bool = False,
+                            stream: int | None = None):
         """Straggler-tolerant allreduce round (the reference's thReduce / thComplete / maxLag
         semantics, csrc/hip/xgmi_threshold.hip). Returns `out`, or `(out, counts)` with
         counts an int32 [world, nch] tensor: contributions summed per output chunk (0 = the
@@ -338,7 +351,7 @@ class XgmiCommunicator:
             cnt = torch.zeros(self.world, self._c.threshold_chunks(inp.numel(), code), dtype=torch.int32,
                               device=self.device)
         self._c.allreduce_threshold(inp.data_ptr(), out.data_ptr(), inp.numel(), code,
-                                    torch.cuda.current_stream(self.device).cuda_stream, th_reduce, th_complete,
+                                    _current_stream(self._dev) if stream is None else stream, th_reduce, th_complete,
                                     0 if cnt is None else cnt.data_ptr(), 1.0 / self.world if op == "avg" else 1.0,
                                     rescale)
         return (out, cnt) if counts else out

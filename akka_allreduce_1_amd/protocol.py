@@ -3,7 +3,8 @@ reference's `AllreduceMessage.scala:7-20` and `DataWrapper.scala:3-7`).
 
 All classes are native (C++) types so that messages cross the actor runtime without
 Python overhead; payload fields accept any float sequence / numpy array (host) or a
-torch tensor on the GPU (device payloads, see `parallel.device_plane`).
+torch tensor on the GPU (device payloads: the HIP device plane in
+`csrc/hip/device_plane.hip`; tensor dataSources for the round engine: `engine.PlaneJob`).
 """
 from ._native import C
 

@@ -869,7 +869,7 @@ def main() -> None:
                          status="protocol_timeout")
         sys.stdout.flush()
         cancel = C.watchdog_arm(args.protocol_timeout, _RESULT_FD if rank == 0 else -1,
-                                json.dumps(timed_out) + "\n", 0)
+                                json.dumps(timed_out) + "\n", 3)
         prot = protocol_rounds(args, rank, world, dev)
         if not cancel():  # the watchdog fired and wrote the line; the process is exiting
             return
@@ -888,7 +888,7 @@ def main() -> None:
 
         timed_out = dict(result, dp={"error": f"timed out after {args.dp_timeout:g} s"}, status="dp_timeout")
         sys.stdout.flush()
-        cancel = C.watchdog_arm(args.dp_timeout, _RESULT_FD if rank == 0 else -1, json.dumps(timed_out) + "\n", 0)
+        cancel = C.watchdog_arm(args.dp_timeout, _RESULT_FD if rank == 0 else -1, json.dumps(timed_out) + "\n", 3)
         log(rank, "dp: ResNet-50 / Llama-3-8B data-parallel steps")
         dp = {m: dp_step(comm, m, dev) for m in (("resnet50",) if args.share_device else ("resnet50", "llama3_8b"))}
         if not cancel():  # the watchdog fired and wrote the line; the process is exiting

@@ -106,6 +106,10 @@ void WorkerActor::sink(AllReduceOutput&& out) {
 }
 
 // ------------------------------------------------------------------------ master
+MasterActor::~MasterActor() {
+  if (bridge_) bridge_->stop();
+}
+
 MasterActor::MasterActor(MasterParams p, FinishedCallback on_finished, RoundCallback on_round)
     : core_(this, p), on_finished_(std::move(on_finished)), on_round_(std::move(on_round)) {}
 

@@ -52,6 +52,9 @@ class MasterActor final : public Actor, public MasterEffects {
   using FinishedCallback = std::function<void(int rounds)>;
   using RoundCallback = std::function<void(int round, int64_t epoch)>;  // checkpoint hook
   MasterActor(MasterParams p, FinishedCallback on_finished = nullptr, RoundCallback on_round = nullptr);
+  // Stops the control bridge: its threads hold references to it, so without an explicit
+  // stop it would outlive the master (control_bridge.h, "Threads and lifetime").
+  ~MasterActor() override;
   void receive(Envelope& env, ActorContext& ctx) override;
   std::string kind() const override { return "master"; }
 

@@ -134,7 +134,7 @@ std::shared_ptr<ControlBridge> ControlBridge::start(const std::string& host, int
   ::getsockname(b->lfd_, reinterpret_cast<sockaddr*>(&a), &len);
   b->port_ = ntohs(a.sin_port);
   if (::pipe2(b->wake_, O_CLOEXEC) != 0) throw std::runtime_error("bridge: pipe failed");
-  b->acceptor_ = std::thread([raw = b.get()] { raw->accept_loop(); });
+  b->acceptor_ = std::thread([b] { b->accept_loop(b); });
   MXAR_LOG(INFO, "bridge", "----control bridge listening on " << host << ":" << b->port_);
   return b;
 }
@@ -159,23 +159,65 @@ size_t ControlBridge::clients() const {
   return n;
 }
 
+void ControlBridge::Client::kill() {
+  if (dead.exchange(true)) return;
+  {
+    std::lock_guard<std::mutex> g(wmu);
+    out.clear();
+    queued = 0;
+  }
+  wcv.notify_all();
+  ::shutdown(fd, SHUT_RDWR);  // the reader sees EOF, a blocked send returns
+}
+
 bool ControlBridge::write_line(Client& c, const std::string& line) {
   if (c.dead.load()) return false;
-  std::lock_guard<std::mutex> g(c.wmu);
-  std::string buf = line;
-  buf.push_back('\n');
-  size_t off = 0;
-  while (off < buf.size()) {
-    ssize_t n = ::send(c.fd, buf.data() + off, buf.size() - off, MSG_NOSIGNAL);
-    if (n < 0 && errno == EINTR) continue;
-    if (n <= 0) {
-      c.dead = true;
-      ::shutdown(c.fd, SHUT_RDWR);  // the reader sees EOF and exits
-      return false;
+  bool overflow = false;
+  {
+    std::lock_guard<std::mutex> g(c.wmu);
+    if (c.queued + line.size() + 1 > max_queued_.load()) {
+      overflow = true;
+    } else {
+      c.out.push_back(line + "\n");
+      c.queued += line.size() + 1;
     }
-    off += static_cast<size_t>(n);
   }
+  if (overflow) {
+    MXAR_LOG(WARNING, "bridge", "client " << c.id << " stopped reading (" << max_queued_.load()
+                                           << " bytes of events queued): disconnecting it");
+    c.kill();
+    return false;
+  }
+  c.wcv.notify_one();
   return true;
+}
+
+void ControlBridge::write_loop(std::shared_ptr<ControlBridge> self, std::shared_ptr<Client> c) {
+  (void)self;  // keeps the bridge alive while this thread runs
+  std::string buf;
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> g(c->wmu);
+      c->wcv.wait(g, [&] { return !c->out.empty() || c->dead.load(); });
+      if (c->dead.load()) return;
+      buf.clear();
+      while (!c->out.empty()) {  // coalesce: one send for everything queued
+        buf += c->out.front();
+        c->out.pop_front();
+      }
+      c->queued = 0;
+    }
+    size_t off = 0;
+    while (off < buf.size()) {
+      ssize_t n = ::send(c->fd, buf.data() + off, buf.size() - off, MSG_NOSIGNAL);
+      if (n < 0 && errno == EINTR) continue;
+      if (n <= 0) {
+        c->kill();
+        return;
+      }
+      off += static_cast<size_t>(n);
+    }
+  }
 }
 
 void ControlBridge::publish(const std::string& line) {
@@ -210,16 +252,20 @@ void ControlBridge::reap() {  // join readers of clients that went away (mu_ not
       }
     }
   }
-  for (auto& c : dead)
-    if (c->reader.joinable()) c->reader.join();  // the fd closes with the last reference
+  for (auto& c : dead) {  // the fd closes with the last reference
+    if (c->reader.joinable()) c->reader.join();
+    if (c->writer.joinable()) c->writer.join();
+  }
 }
 
 ControlBridge::Client::~Client() {
-  if (reader.joinable()) reader.detach();  // only reachable from the reader itself at shutdown
+  // only reachable with a joinable thread from that thread itself at shutdown
+  if (reader.joinable()) reader.detach();
+  if (writer.joinable()) writer.detach();
   if (fd >= 0) ::close(fd);
 }
 
-void ControlBridge::accept_loop() {
+void ControlBridge::accept_loop(std::shared_ptr<ControlBridge> self) {
   while (!stop_.load()) {
     pollfd p[2] = {{lfd_, POLLIN, 0}, {wake_[0], POLLIN, 0}};
     int r = ::poll(p, 2, 200);
@@ -242,11 +288,13 @@ void ControlBridge::accept_loop() {
     write_line(*c, "{\"type\":\"Hello\",\"protocol\":\"mxar-bridge/1\",\"client\":" + std::to_string(c->id) +
                        ",\"master\":\"" + json_escape(master_path_) + "\"}");
     if (!init.empty()) write_line(*c, init);
-    c->reader = std::thread([this, c] { read_loop(c); });
+    c->writer = std::thread([self, c] { self->write_loop(self, c); });
+    c->reader = std::thread([self, c] { self->read_loop(self, c); });
   }
 }
 
-void ControlBridge::read_loop(std::shared_ptr<Client> c) {
+void ControlBridge::read_loop(std::shared_ptr<ControlBridge> self, std::shared_ptr<Client> c) {
+  (void)self;  // keeps the bridge alive while this thread runs (tell() may drop the master)
   std::string buf;
   char tmp[4096];
   while (!stop_.load() && !c->dead.load()) {
@@ -298,7 +346,7 @@ void ControlBridge::read_loop(std::shared_ptr<Client> c) {
       m->tell(Message(cmd), nullptr);
     }
   }
-  c->dead = true;
+  c->kill();
 }
 
 void ControlBridge::stop() {
@@ -308,7 +356,8 @@ void ControlBridge::stop() {
     (void)!::write(wake_[1], &x, 1);
   }
   // stop() can run on one of our own threads: a reader's tell() briefly owns the master's
-  // cell, and if the system dropped it meanwhile the master (and this bridge) die there.
+  // cell, and if the system dropped it meanwhile ~MasterActor stops the bridge there (the
+  // reader's own reference keeps the object alive until that thread returns).
   auto join = [](std::thread& t) {
     if (!t.joinable()) return;
     if (t.get_id() == std::this_thread::get_id()) t.detach();
@@ -322,9 +371,9 @@ void ControlBridge::stop() {
     master_ = nullptr;
   }
   for (auto& c : cs) {
-    c->dead = true;
-    ::shutdown(c->fd, SHUT_RDWR);
+    c->kill();
     join(c->reader);
+    join(c->writer);
   }
   if (lfd_ >= 0) ::close(lfd_);
   for (int& f : wake_)

@@ -26,9 +26,20 @@
 //
 // Events go to every connected client; Accepted / Error / Status only to the sender.
 // A client that connects late first gets Hello, then the last InitWorkers line.
+//
+// Threads and lifetime: one acceptor thread, and per client a reader and a writer thread.
+// Every thread holds a strong reference to the bridge, so the bridge is never destroyed
+// while one of its own threads still runs (a reader's tell() may be the call that drops
+// the master - and with it the master's reference). Whoever owns the bridge calls stop()
+// (MasterActor's destructor does): threads then exit and release their references.
+// publish() / reply() never block on a socket: each client has a bounded outbound queue
+// drained by its writer thread; a client whose queue overflows (it stopped reading) is
+// disconnected instead of stalling the master actor that publishes round events.
 #pragma once
 
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -62,20 +73,32 @@ class ControlBridge : public std::enable_shared_from_this<ControlBridge> {
   // Remember the latest InitWorkers line for clients that connect later.
   void set_init_line(std::string line);
   size_t clients() const;
+  // Outbound queue cap per client (bytes, default kMaxQueuedBytes); tests lower it.
+  void set_max_queued_bytes(size_t b) { max_queued_.store(b); }
   void stop();
 
  private:
+  // Outbound bytes a client may have queued before it is dropped (a control line is < 1 KiB,
+  // so this is thousands of rounds of events a client has not read).
+  static constexpr size_t kMaxQueuedBytes = 4u << 20;
+
   struct Client {
     ~Client();  // closes fd: only once no publisher can still be writing to it
     uint64_t id;
     int fd = -1;
-    std::mutex wmu;
-    std::thread reader;
+    std::mutex wmu;               // guards out / queued
+    std::condition_variable wcv;  // writer wake-up
+    std::deque<std::string> out;  // lines waiting for the writer
+    size_t queued = 0;            // bytes in `out`
+    std::thread reader, writer;
     std::atomic<bool> dead{false};
+    void kill();  // mark dead, wake the writer, unblock the reader (idempotent)
   };
   ControlBridge() = default;
-  void accept_loop();
-  void read_loop(std::shared_ptr<Client> c);
+  void accept_loop(std::shared_ptr<ControlBridge> self);
+  void read_loop(std::shared_ptr<ControlBridge> self, std::shared_ptr<Client> c);
+  void write_loop(std::shared_ptr<ControlBridge> self, std::shared_ptr<Client> c);
+  // Queue one line for a client (never blocks on the socket); false if the client is gone.
   bool write_line(Client& c, const std::string& line);
   void reap();
 
@@ -83,6 +106,7 @@ class ControlBridge : public std::enable_shared_from_this<ControlBridge> {
   int wake_[2] = {-1, -1};
   int port_ = 0;
   std::atomic<bool> stop_{false};
+  std::atomic<size_t> max_queued_{kMaxQueuedBytes};
   std::thread acceptor_;
   mutable std::mutex mu_;
   std::vector<std::shared_ptr<Client>> clients_;

@@ -195,6 +195,63 @@ static int run_bridge(int P, int N, int C, int rounds) {
   return 0;
 }
 
+// Bridge teardown: (1) a client that connects and never reads while the master
+// runs rounds on its own - its queue overflows and it is dropped, the rounds never stall on
+// its socket; (2) the system shuts down while another client floods StartAllreduce, with
+// the master holding the ONLY reference to the bridge, so the master (and the bridge's
+// owner reference) can die inside a reader's tell().
+static int run_bridge_teardown(int P, int N, int C, int rounds) {
+  auto sys = std::make_shared<ActorSystem>("ClusterSystem", ActorSystem::Mode::Threaded, 4);
+  std::atomic<bool> done{false};
+  MasterParams mp{P, 1.f, 1.f, 1.f, 1, N, rounds - 1, C, false};
+  auto actor = std::make_unique<MasterActor>(mp, [&](int) { done = true; });
+  int port = 0;
+  {
+    auto bridge = ControlBridge::start("127.0.0.1", 0);
+    bridge->set_max_queued_bytes(4096);
+    actor->set_bridge(bridge);
+    port = bridge->port();
+    ActorRef master = sys->actor_of(std::move(actor), "master");
+    bridge->attach(master, master->path());
+    int lazy = connect_to(port);  // connects, never reads
+    if (lazy >= 0) {
+      int small = 4096;
+      ::setsockopt(lazy, SOL_SOCKET, SO_RCVBUF, &small, sizeof(small));
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    for (int k = 0; k < P; ++k) {
+      DataSource src = [N](const AllReduceInputRequest& r) {
+        std::vector<float> v(N, static_cast<float>(r.iteration));
+        return AllReduceInput{make_host_payload(std::move(v))};
+      };
+      ActorRef w = sys->actor_of(std::make_unique<WorkerActor>(src, [](const AllReduceOutput&) {}),
+                                 "worker" + std::to_string(k));
+      master->tell(MemberUp{w, "worker", ""}, nullptr);
+    }
+    const bool ok = wait_until([&] { return done.load(); }, 60);
+    if (lazy >= 0) ::close(lazy);
+    if (!ok) {
+      std::fprintf(stderr, "bridge teardown: rounds stalled behind a client that never reads\n");
+      sys->shutdown();
+      return 1;
+    }
+  }  // from here the master actor owns the only reference to the bridge
+  std::atomic<bool> stop_flood{false};
+  std::thread flood([&] {
+    int fd = connect_to(port);
+    if (fd < 0) return;
+    const std::string l = "{\"type\":\"StartAllreduce\",\"round\":1}\n{\"type\":\"Status\"}\n";
+    while (!stop_flood.load())
+      if (::send(fd, l.data(), l.size(), MSG_NOSIGNAL) <= 0) break;
+    ::close(fd);
+  });
+  std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  sys->shutdown();  // drops the master -> ~MasterActor stops the bridge mid-flood
+  stop_flood = true;
+  flood.join();
+  return 0;
+}
+
 // The round engine on host memory: master + P PlaneWorkerActors over LoopbackRoundPlanes
 // (plane completion threads, hub mutex, actor mailboxes all live under the sanitizer).
 static int run_plane(int P, int N, int C, int rounds) {
@@ -357,6 +414,7 @@ int main(int argc, char** argv) {
   if (rc == 0 && (only.empty() || only == "tcp")) rc = run_tcp(20);
   if (rc == 0 && (only.empty() || only == "plane")) rc = run_plane(3, 41, 4, 40);
   if (rc == 0 && (only.empty() || only == "bridge")) rc = run_bridge(3, 23, 4, 60);
+  if (rc == 0 && (only.empty() || only == "bridge_teardown")) rc = run_bridge_teardown(3, 23, 4, 400);
   std::printf(rc == 0 ? "runtime_stress: OK\n" : "runtime_stress: FAILED\n");
   return rc;
 }
