@@ -261,7 +261,8 @@ def _gpu_worker_plane(args, cfg: mconfig.Config, n: int):
     torch.cuda.set_device(dev)
     plane = C.hip.xgmi_plane(args.device, dtype_code(tdt), n, max_peers=int(cfg["mxar.plane.max-peers"]),
                              max_lag=int(cfg["mxar.plane.max-lag"]), grid=int(cfg["mxar.plane.grid"]),
-                             timeout_s=float(cfg["mxar.plane.timeout"]), spin_us=int(cfg["mxar.plane.spin-us"]))
+                             timeout_s=float(cfg["mxar.plane.timeout"]), spin_us=int(cfg["mxar.plane.spin-us"]),
+                             min_chunk=int(cfg["mxar.plane.min-chunk"]))
 
     def source(req):
         x = torch.empty(n, dtype=tdt, device=dev)

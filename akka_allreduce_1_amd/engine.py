@@ -74,7 +74,7 @@ class PlaneJob:
                  max_peers: int | None = None, high_priority: bool = True, order_release: bool = True,
                  plane: str = "xgmi", hub: str | None = None, spin_us: int = 1000, reinit_on_loss: bool = False,
                  split: bool = True, keep_last: bool = False, bridge_port: int | None = None,
-                 external_rounds: bool = False):
+                 external_rounds: bool = False, min_chunk: int | None = None):
         """plane: "xgmi" (one threshold-kernel launch per round on the GPUs in `devices`) or
         "loopback" (host memory, no GPU: csrc/runtime/loopback_plane.h; `hub` names the
         workers' shared hub, default a fresh one; dtype float32, devices ignored).
@@ -85,7 +85,11 @@ class PlaneJob:
         keep_last: each worker keeps only its newest round output, natively (`last_output(k)`);
         replaces keep_outputs / on_output, so no Python runs on the round path.
         bridge_port: serve the master's control bridge there (0 = any free port, see
-        `bridge_port`; docs/BRIDGE.md). external_rounds: bridge clients drive the rounds."""
+        `bridge_port`; docs/BRIDGE.md). external_rounds: bridge clients drive the rounds.
+        min_chunk: the planes keep one flag / count / threshold decision per chunk of at least
+        this many elements (xgmi_plane.h); default: max_chunk_size whenever it is finer than the
+        1 KiB flag granularity, so every reference chunk is decided on its own (the reference's
+        DataBuffer semantics at any maxChunkSize)."""
         self.P = P
         self.n = data_size
         self.dtype = dtype
@@ -122,10 +126,13 @@ class PlaneJob:
             if sources is None:
                 sources = [host_iota_source(data_size, 1000.0 * k) for k in range(P)]
         else:
+            es = torch.empty(0, dtype=dtype).element_size()
+            if min_chunk is None:
+                min_chunk = max_chunk_size if max_chunk_size * es < 1024 else 0
             self.planes = [C.hip.xgmi_plane(d, dtype_code(dtype), data_size, max_peers=max_peers or P,
                                             max_lag=max_lag, grid=grid, timeout_s=timeout_s, order_ref=order_ref,
                                             high_priority=high_priority, order_release=order_release,
-                                            spin_us=spin_us, split=split)
+                                            spin_us=spin_us, split=split, min_chunk=min_chunk)
                            for d in self.devices]
             if sources is None:
                 sources = [iota_source(data_size, torch.device("cuda", d), dtype, 1000.0 * k)
@@ -220,7 +227,7 @@ class PlaneJob:
 def distributed_plane_job(n: int, source, *, max_chunk_size: int, dtype: torch.dtype, rounds: int,
                           th: float = 1.0, max_lag: int = 1, grid: int = 0, timeout_s: float = 300.0,
                           on_output: Callable | None = None, keep_last: bool = False,
-                          external_client: bool = False) -> dict:
+                          external_client: bool = False, min_chunk: int | None = None) -> dict:
     """One plane worker per torch.distributed rank (one process per GPU), the master on rank 0,
     the reference's cluster shape: workers join rank 0's seed over TCP (127.0.0.1) and
     announce their plane descriptors in the join; the master relays them in InitWorkers and
@@ -239,8 +246,10 @@ def distributed_plane_job(n: int, source, *, max_chunk_size: int, dtype: torch.d
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = torch.cuda.current_device()
     system = C.ActorSystem("ClusterSystem", False)
+    if min_chunk is None:  # one flag per reference chunk when maxChunkSize is finer than 1 KiB
+        min_chunk = max_chunk_size if max_chunk_size * torch.empty(0, dtype=dtype).element_size() < 1024 else 0
     plane = C.hip.xgmi_plane(dev, dtype_code(dtype), n, max_peers=world, max_lag=max_lag, grid=grid,
-                             timeout_s=min(60.0, timeout_s))
+                             timeout_s=min(60.0, timeout_s), min_chunk=min_chunk)
     if isinstance(source, torch.Tensor):  # fetched natively every round (no GIL)
         source = C.hip.tensor_source(source)
     last = C.last_output_sink() if keep_last else None

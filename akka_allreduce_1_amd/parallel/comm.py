@@ -549,28 +549,35 @@ class LocalCluster:
             dev = self.devices[g[0]]
             _H.XgmiComm.allreduce_local([self.comms[k] for k in g], [inputs[k].data_ptr() for k in g],
                                         [outputs[k].data_ptr() for k in g], n, code,
-                                        torch.cuda.current_stream(dev).cuda_stream, ALGOS[algo],
+                                        _current_stream(dev.index), ALGOS[algo],
                                         1.0 / self.world if op == "avg" else 1.0)
         return outputs
 
     def allreduce_threshold(self, inputs: Sequence[torch.Tensor], outputs: Sequence[torch.Tensor] | None = None, *,
-                            th_reduce: float = 1.0, th_complete: float = 1.0, op: str = "sum", rescale: bool = False):
+                            th_reduce: float = 1.0, th_complete: float = 1.0, op: str = "sum", rescale: bool = False,
+                            counts: bool = True):
         """One straggler-tolerant round for every logical rank (see
-        XgmiCommunicator.allreduce_threshold). Returns (outputs, counts[world, world, nch])."""
+        XgmiCommunicator.allreduce_threshold). Returns (outputs, counts[world, world, nch]);
+        counts=False skips the counts tensor (no allocation per call) and returns (outputs, None)."""
         outputs = self._check(inputs, outputs)
         n = inputs[0].numel()
         code = _dtype_code(inputs[0].dtype)
-        counts = []
+        cnts = []
         for g in self.groups:
             dev = self.devices[g[0]]
-            nch = self.comms[g[0]].threshold_chunks(n, code, len(g))
-            cnt = torch.zeros(len(g), self.world, nch, dtype=torch.int32, device=dev)
+            cnt = None
+            if counts:
+                nch = self.comms[g[0]].threshold_chunks(n, code, len(g))
+                cnt = torch.zeros(len(g), self.world, nch, dtype=torch.int32, device=dev)
             _H.XgmiComm.allreduce_threshold_local([self.comms[k] for k in g], [inputs[k].data_ptr() for k in g],
                                                   [outputs[k].data_ptr() for k in g], n, code,
-                                                  torch.cuda.current_stream(dev).cuda_stream, th_reduce, th_complete,
-                                                  cnt.data_ptr(), 1.0 / self.world if op == "avg" else 1.0, rescale)
-            counts.append(cnt)
-        return outputs, counts[0] if len(counts) == 1 else counts
+                                                  _current_stream(dev.index), th_reduce, th_complete,
+                                                  0 if cnt is None else cnt.data_ptr(),
+                                                  1.0 / self.world if op == "avg" else 1.0, rescale)
+            cnts.append(cnt)
+        if not counts:
+            return outputs, None
+        return outputs, cnts[0] if len(cnts) == 1 else cnts
 
     def collective(self, op: str, inputs: Sequence[torch.Tensor], outputs: Sequence[torch.Tensor] | None = None, *,
                    scale: float = 1.0) -> list[torch.Tensor]:

@@ -19,12 +19,16 @@ def busbw(algbw: float, world: int) -> float:
     return algbw * 2.0 * (world - 1) / world if world > 1 else 0.0
 
 
-def hbm_bytes(S: int, P: int, algo: str) -> float:
-    """HBM bytes the kernels move when P logical ranks of ONE GPU allreduce S bytes each
-    (every rank's traffic lands in the same HBM; counts checked against rocprofv3 PMC
-    FETCH_SIZE / WRITE_SIZE in profiles/pmc_counters.md)."""
-    if algo == "ring":  # per rank, blocks of S/P: RS hops read in (+ slab) and push, AG hops copy out + forward
-        return P * (S / P) * (6 * (P - 2) + 8)
+def hbm_bytes(S: int, P: int, algo: str, es: int = 4) -> float:
+    """HBM bytes the kernels move when P logical ranks of ONE GPU allreduce S bytes each of an
+    `es`-byte element type (every rank's traffic lands in the same HBM; counts checked against
+    rocprofv3 PMC FETCH_SIZE / WRITE_SIZE in profiles/pmc_counters.md)."""
+    if algo == "ring":
+        # per rank, blocks B = S/P: RS hops read in (+ an fp32 partial) and push an fp32 partial
+        # (Bp = B * 4 / es: 2 (P - 1) partial transfers), the final hop and the AG hops move
+        # E-typed blocks (4 P - 2 of them)
+        B = S / P
+        return P * (B * (4 * P - 2) + B * 4 / es * (2 * P - 2))
     if algo == "all_to_all":  # S = P blocks per rank: read in + write slab (P-1)/P + read slab + write out
         return P * (2 * S + 2 * S * (P - 1) / P)
     if algo == "reduce_scatter":

@@ -261,10 +261,10 @@ def local_ranks(dev, args, P: int = 8) -> dict:
             wall = timed_local(fn, args.steps, dev) / args.steps * 1e3
             p50 = percentile(event_times(fn, args.steps, dev), 50)
             cl.check()
-            tbps = hbm_bytes(S, P, algo) / (p50 / 1e3) / 1e12
+            tbps = hbm_bytes(S, P, algo, es) / (p50 / 1e3) / 1e12
             row[algo] = {"p50_ms": round(p50, 4), "ms_per_step": round(wall, 4), "max_abs_err": err,
                          "validated": err <= 2e-2 * P if dtype == torch.bfloat16 else err <= 1e-5 * P,
-                         "hbm_bytes": int(hbm_bytes(S, P, algo)), "hbm_TBps": round(tbps, 3),
+                         "hbm_bytes": int(hbm_bytes(S, P, algo, es)), "hbm_TBps": round(tbps, 3),
                          "frac_copy_roofline": round(tbps / copy_tbps, 3)}
     except Exception as e:  # noqa: BLE001 - reported, never loses the headline
         row["error"] = repr(e)
@@ -641,6 +641,8 @@ def main() -> None:
     ap.add_argument("--no-dp", action="store_true", help="skip the ResNet-50 / Llama-3-8B DP-step sections")
     ap.add_argument("--no-local", action="store_true", help="skip the 8-logical-rank section at N = 1")
     ap.add_argument("--no-protocol", action="store_true", help="skip the master/worker protocol-engine section")
+    ap.add_argument("--no-sizes", action="store_true",
+                    help="skip the N = 1 size-axis sections (latency_vs_size, reduce_kernel, protocol sizes)")
     ap.add_argument("--protocol-timeout", type=float, default=240.0,
                     help="native watchdog over the protocol section (s); the result line is written either way")
     ap.add_argument("--dp-rehearsal", action="store_true", help="with --share-device: run the ResNet-50 DP step too")
@@ -808,7 +810,8 @@ def main() -> None:
         twall = timed(lambda: comm.allreduce(x, y, algo="twoshot"), args.steps, dev)
         tms = max_over_ranks(twall, dev) / args.steps * 1e3
         result["xgmi_twoshot"] = {"algbw": round(nbytes / (tms / 1e3) / 1e9, 2), "ms_per_step": round(tms, 4)}
-    if not args.no_rccl and chosen not in ("rccl", "rccl-fallback"):
+    if not args.no_rccl and chosen not in ("rccl", "rccl-fallback") and world > 1:
+        # (at world = 1 RCCL's allreduce is a no-op after a copy: nothing to compare)
         for _ in range(args.warmup):
             step_rccl()
         rwall = timed(step_rccl, args.steps, dev)
@@ -860,6 +863,14 @@ def main() -> None:
         # the allreduce kernels at N = 1: 8 logical ranks in one launch on this GPU
         log(rank, "local_ranks: 8 logical ranks in one launch")
         result["local_ranks"] = local_ranks(dev, args, P=8)
+        if not args.no_sizes:
+            from benchmarks.sections import latency_vs_size, reduce_kernel
+
+            # the headline metric's size axis: p50 latency + algbw per kernel, 4 KiB .. 256 MiB
+            log(rank, "latency_vs_size: 8 and 2 logical ranks, 4 KiB .. 256 MiB")
+            result["latency_vs_size"] = latency_vs_size(dev, dtype, max_bytes=nbytes)
+            log(rank, "reduce_kernel: BASELINE config 2 (1 GiB fp32, P = 2 / 4 / 8)")
+            result["reduce_kernel"] = reduce_kernel(dev)
     if engine_ok and not args.no_protocol:
         # the reference's master/worker round protocol driving the GPU engine, under the same
         # native watchdog as the dp section: a stuck round never costs the result line
@@ -871,6 +882,11 @@ def main() -> None:
         cancel = C.watchdog_arm(args.protocol_timeout, _RESULT_FD if rank == 0 else -1,
                                 json.dumps(timed_out) + "\n", 3)
         prot = protocol_rounds(args, rank, world, dev)
+        if world == 1 and not args.no_sizes:
+            from benchmarks.sections import protocol_sizes
+
+            log(rank, "protocol: 40 B / 1 MiB / 64 MiB rounds")
+            prot["sizes"] = protocol_sizes(dev)
         if not cancel():  # the watchdog fired and wrote the line; the process is exiting
             return
         result["protocol"] = prot

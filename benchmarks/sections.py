@@ -1,0 +1,293 @@
+"""Side sections of the N = 1 bench line (bench.py) that put the headline metric's SIZE axis in
+front of the driver: "allreduce algbw + p50 latency vs tensor size" (BASELINE.json).
+
+At N = 1 the one-rank allreduce is a copy, so the allreduce kernels themselves are timed with
+P logical ranks in ONE launch on the GPU (LocalCluster: every rank's traffic lands in the
+same HBM, no xGMI):
+
+  latency_vs_size  P = 8 and P = 2, 4 KiB .. 256 MiB per rank in x4 steps; every cell holds
+                   p50 device latency and algbw of ll / oneshot / twoshot / ring / threshold
+                   and of `auto` (plus the kernel auto resolves to), each cell validated
+                   against an fp32 reference (rounded once: within 1 bf16 ulp) BEFORE it is
+                   timed. `auto_vs_best` = auto's p50 / the best kernel's p50 per size.
+  reduce_kernel    BASELINE config 2: the reduce_slots kernel over P = 2 / 4 / 8 slots of a
+                   1 GiB fp32 buffer (the worker's `reduce`, AllreduceWorker.scala:240-251),
+                   TB/s of HBM traffic and the fraction of the same-run copy roofline.
+  protocol_sizes   the reference's master / worker round protocol driving the GPU round
+                   engine (PlaneJob: StartAllreduce -> one threshold-kernel launch per worker)
+                   at 40 B (the reference's default job: 10 floats, maxChunkSize 2, 101
+                   rounds - AllreduceMaster.scala:105-114), 1 MiB and 64 MiB per worker.
+
+Latency method: the host is put ahead of the GPU (a sleep kernel first), then every call is
+bracketed by device events - so p50 is the device time of one call (kernel launch to kernel
+end, as seen by the GPU's command processor), not the Python enqueue rate; the host-bound
+rate of back-to-back calls is reported next to it (`wall_us`).
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from akka_allreduce_1_amd._native import C
+from akka_allreduce_1_amd.ops import fill_uniform
+from akka_allreduce_1_amd.utils.timing import percentile
+
+_SLEEP_CYCLES_PER_MS: list[float] = []
+
+
+def _sleep_cycles_per_ms(dev) -> float:
+    """torch.cuda._sleep spins on the shader clock: calibrate cycles per ms once."""
+    if not _SLEEP_CYCLES_PER_MS:
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        a.record()
+        torch.cuda._sleep(1_000_000)
+        b.record()
+        torch.cuda.synchronize(dev)
+        _SLEEP_CYCLES_PER_MS.append(1_000_000 / max(a.elapsed_time(b), 1e-3))
+    return _SLEEP_CYCLES_PER_MS[0]
+
+
+def device_times(fn, iters: int, dev, lead_ms: float = 4.0) -> list[float]:
+    """Per-call device time (ms) of `fn` with the host AHEAD of the GPU: a sleep kernel of
+    `lead_ms` is queued first, so the calls behind it run back to back on the device and each
+    event pair brackets exactly one call's device work."""
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    cyc = _sleep_cycles_per_ms(dev)
+    torch.cuda.synchronize(dev)
+    torch.cuda._sleep(int(cyc * lead_ms))
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize(dev)
+    return [a.elapsed_time(b) for a, b in ev]
+
+
+def wall_per_call(fn, iters: int, dev) -> float:
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize(dev)
+    return (time.perf_counter() - t0) / iters
+
+
+def _bf16_ulp(x: torch.Tensor) -> torch.Tensor:
+    _, e = torch.frexp(x.abs().clamp_min(1e-30))
+    return torch.ldexp(torch.ones_like(x), e - 8)
+
+
+def rounding_check(ys, ref: torch.Tensor, dtype: torch.dtype, P: int) -> tuple[bool, float, float]:
+    """(ok, max_abs_err, max_err_in_ulps): every output within ONE ulp of the fp32 reference
+    (bf16: the fp32 sum rounded once; the ordering of fp32 additions may move a value across a
+    rounding boundary, never further), plus an absolute slack for fp32 reassociation."""
+    worst_abs, worst_ulp, ok = 0.0, 0.0, True
+    slack = 4e-7 * P
+    for y in ys:
+        d = (y.float() - ref).abs()
+        worst_abs = max(worst_abs, d.max().item())
+        if dtype == torch.bfloat16:
+            u = _bf16_ulp(ref)
+            worst_ulp = max(worst_ulp, (d / (u + slack)).max().item())
+            ok = ok and bool((d <= u + slack).all().item())
+        else:
+            ok = ok and bool((d <= 1e-6 * P * ref.abs().clamp_min(1.0)).all().item())
+    return ok, worst_abs, worst_ulp
+
+
+def _sizes(lo: int, hi: int) -> list[int]:
+    out, s = [], lo
+    while s <= hi:
+        out.append(s)
+        s *= 4
+    return out
+
+
+def latency_vs_size(dev, dtype: torch.dtype = torch.bfloat16, ranks=(8, 4, 2), min_bytes: int = 4 << 10,
+                    max_bytes: int = 256 << 20, iters: int = 20, warmup: int = 3) -> dict:
+    from akka_allreduce_1_amd.parallel import LocalCluster
+
+    es = torch.empty(0, dtype=dtype).element_size()
+    out: dict = {"dtype": str(dtype).replace("torch.", ""), "method": "p50 of per-call device time (host ahead "
+                 "of the GPU), P logical ranks in one launch on one GPU; algbw = bytes per rank / p50",
+                 "sizes": _sizes(min_bytes, max_bytes)}
+    names = {0: "auto", 1: "twoshot", 2: "oneshot", 3: "ring", 4: "ll"}
+    for P in ranks:
+        rows = []
+        cl = xs = ys = None
+        try:
+            slot = -(-max_bytes // P) + (1 << 20)
+            cl = LocalCluster(P, slot_bytes=slot, grid=512, timeout_s=10.0, max_lag=1)
+            n_max = max_bytes // es
+            xs = [fill_uniform(torch.empty(n_max, dtype=dtype, device=dev), seed=900 + k) for k in range(P)]
+            ys = [torch.empty_like(t) for t in xs]
+            ll_max = cl.comms[0].ll_max_bytes
+            for size in out["sizes"]:
+                n = size // es
+                xv = [t[:n] for t in xs]
+                yv = [t[:n] for t in ys]
+                ref = torch.zeros(n, device=dev)
+                for t in xv:
+                    ref += t.float()
+                row: dict = {"bytes": size}
+                algos = ["ll", "oneshot", "twoshot", "ring", "threshold", "auto"]
+                for algo in algos:
+                    if algo == "ll" and size > 4 * ll_max:
+                        continue
+                    if algo == "oneshot" and size > min(slot - (1 << 20), 64 << 20):
+                        continue
+                    if algo == "threshold":
+                        def fn(xv=xv, yv=yv):
+                            cl.allreduce_threshold(xv, yv, counts=False)
+                    else:
+                        def fn(xv=xv, yv=yv, algo=algo):
+                            cl.allreduce(xv, yv, algo=algo)
+                    cell: dict = {}
+                    try:
+                        for y in yv:
+                            y.fill_(float("nan"))  # a kernel that writes nothing cannot pass
+                        fn()
+                        cl.check()
+                        ok, err, ulps = rounding_check(yv, ref, dtype, P)
+                        cell.update(validated=ok, max_abs_err=err, max_err_ulp=round(ulps, 3))
+                        if not ok:
+                            row[algo] = cell
+                            continue
+                        for _ in range(warmup):
+                            fn()
+                        t = device_times(fn, iters, dev)
+                        p50 = percentile(t, 50)
+                        cell.update(p50_us=round(p50 * 1e3, 2), algbw_GBps=round(size / (p50 / 1e3) / 1e9, 2),
+                                    wall_us=round(wall_per_call(fn, iters, dev) * 1e6, 2))
+                        cl.check()
+                    except Exception as e:  # noqa: BLE001 - reported per cell
+                        cell["error"] = repr(e)
+                    row[algo] = cell
+                code = _H_dtype(dtype)
+                row["auto_picks"] = names[int(cl.comms[0].resolve(n, code, C.hip.Algo.Auto, P))]
+                timed_ = {a: c["p50_us"] for a, c in row.items() if isinstance(c, dict) and "p50_us" in c
+                          and a != "auto"}
+                if timed_:
+                    best = min(timed_, key=timed_.get)
+                    row["best"] = best
+                    if "p50_us" in row.get("auto", {}):
+                        row["auto_vs_best"] = round(row["auto"]["p50_us"] / timed_[best], 3)
+                rows.append(row)
+                del ref
+        except Exception as e:  # noqa: BLE001 - reported, never loses the headline
+            out[f"P{P}_error"] = repr(e)
+        finally:
+            del cl, xs, ys
+            torch.cuda.empty_cache()
+        out[f"P{P}"] = rows
+        ratios = [r["auto_vs_best"] for r in rows if "auto_vs_best" in r]
+        if ratios:
+            out[f"P{P}_auto_worst_vs_best"] = max(ratios)
+        out[f"P{P}_all_validated"] = all(c.get("validated", False) for r in rows for c in r.values()
+                                         if isinstance(c, dict))
+    return out
+
+
+def _H_dtype(dtype: torch.dtype):
+    return {torch.float32: C.hip.DType.F32, torch.bfloat16: C.hip.DType.BF16, torch.float16: C.hip.DType.F16}[dtype]
+
+
+def reduce_kernel(dev, mib: int = 1024, slots=(2, 4, 8), iters: int = 10) -> dict:
+    """BASELINE config 2: in-place-style reduce of P fp32 slots of `mib` MiB each into an
+    output (out = sum of slots, fp32), the reduce_slots HIP kernel (csrc/hip/kernels.hip)."""
+    from akka_allreduce_1_amd.ops import reduce_slots
+
+    nbytes = mib << 20
+    n = nbytes // 4
+    res: dict = {"bytes_per_slot": nbytes, "dtype": "fp32"}
+    s = torch.cuda.current_stream(dev).cuda_stream
+    try:
+        a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        b = torch.empty_like(a)
+        for _ in range(3):
+            C.hip.copy(a.data_ptr(), b.data_ptr(), nbytes, s)
+        tc = percentile(device_times(lambda: C.hip.copy(a.data_ptr(), b.data_ptr(), nbytes, s), iters, dev), 50)
+        roof = 2 * nbytes / (tc / 1e3) / 1e12
+        res["copy_roofline_TBps"] = round(roof, 3)
+        del a, b
+        for P in slots:
+            row: dict = {}
+            sl = out = ref = None
+            try:
+                sl = torch.empty(P, n, device=dev)
+                for p in range(P):
+                    fill_uniform(sl[p], seed=40 + p)
+                out = torch.empty(n, device=dev)
+                reduce_slots(sl, out=out)
+                ref = sl[0].clone()
+                for p in range(1, P):
+                    ref += sl[p]
+                err = (out - ref).abs().max().item()
+                row["max_abs_err"] = err
+                row["validated"] = err <= 1e-6 * P
+                del ref
+                ref = None
+                for _ in range(3):
+                    reduce_slots(sl, out=out)
+                t = percentile(device_times(lambda: reduce_slots(sl, out=out), iters, dev), 50)
+                tb = (P + 1) * nbytes / (t / 1e3) / 1e12
+                row.update(ms=round(t, 4), hbm_TBps=round(tb, 3), frac_copy_roofline=round(tb / roof, 3),
+                           algbw_GBps=round(nbytes / (t / 1e3) / 1e9, 1))
+            except Exception as e:  # noqa: BLE001
+                row["error"] = repr(e)
+            finally:
+                del sl, out, ref
+                torch.cuda.empty_cache()
+            res[f"P{P}"] = row
+    except Exception as e:  # noqa: BLE001
+        res["error"] = repr(e)
+    return res
+
+
+def protocol_sizes(dev, cases=((40, torch.float32, 2, 101), (1 << 20, torch.bfloat16, 0, 200),
+                               (64 << 20, torch.bfloat16, 0, 60))) -> dict:
+    """The master / worker protocol on the GPU round engine at several per-worker sizes, two
+    workers sharing the GPU (th = 1, maxLag 1). chunk 0 = the bench geometry (about 256 reduce
+    units per worker). ms_per_round from the master's native round-barrier stamps after 10
+    warm-up rounds; validated = the last round's output equals the fp32-ordered sum."""
+    from akka_allreduce_1_amd.engine import PlaneJob
+
+    res: dict = {"workers": 2, "th_reduce": 1.0, "th_complete": 1.0, "max_lag": 1,
+                 "note": "2 plane workers share one GPU; StartAllreduce -> one threshold-kernel launch per worker"}
+    P = 2
+    for nbytes, dtype, chunk, rounds in cases:
+        es = torch.empty(0, dtype=dtype).element_size()
+        n = max(1, nbytes // es)
+        if chunk <= 0:
+            block = -(-n // P)
+            chunk = max(1024, -(-block // 256))
+        row: dict = {"bytes": nbytes, "dtype": str(dtype).replace("torch.", ""), "max_chunk_size": chunk,
+                     "rounds": rounds}
+        job = None
+        try:
+            xs = [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=70 + k) for k in range(P)]
+            ref = (xs[0].float() + xs[1].float()).to(dtype)
+            job = PlaneJob(P, n, max_chunk_size=chunk, dtype=dtype, max_round=rounds - 1, sources=xs,
+                           keep_outputs=False, keep_last=True, timeout_s=20.0)
+            job.run(timeout=120)
+            st = job.stamps
+            warm = 10
+            if len(st) > warm + 1:
+                per = (st[-1] - st[warm - 1]) / (len(st) - warm)
+                row["ms_per_round"] = round(per * 1e3, 4)
+                row["us_per_round"] = round(per * 1e6, 1)
+                row["rounds_per_s"] = round(1.0 / per, 1)
+                row["algbw_per_worker_GBps"] = round(nbytes / per / 1e9, 3)
+            lat = job.system.plane_worker_state(job.workers[0])["round_latency"]
+            row["worker_round_latency_p50_us"] = round(lat["p50_ms"] * 1e3, 1)
+            o = job.last_output(0)
+            row["validated"] = bool(o is not None and o.iteration == rounds - 1 and torch.equal(o.data, ref))
+        except Exception as e:  # noqa: BLE001
+            row["error"] = repr(e)
+        finally:
+            if job is not None:
+                job.shutdown()
+        res[f"{nbytes}B"] = row
+    return res

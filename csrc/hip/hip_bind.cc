@@ -254,7 +254,7 @@ void bind_hip(py::module_& m) {
   h.def(
       "xgmi_plane",
       [](int device, DType dtype, int64_t capacity, int max_peers, int max_lag, int grid, double timeout_s,
-         bool order_ref, bool high_priority, bool order_release, int spin_us, bool split) {
+         bool order_ref, bool high_priority, bool order_release, int spin_us, bool split, int64_t min_chunk) {
         XgmiPlaneOptions o;
         o.device = device;
         o.dtype = dtype;
@@ -268,12 +268,14 @@ void bind_hip(py::module_& m) {
         o.order_release = order_release;
         o.spin_us = spin_us;
         o.split = split;
+        o.min_chunk = min_chunk;
         py::gil_scoped_release r;
         return make_xgmi_plane(o);
       },
       py::arg("device") = 0, py::arg("dtype") = DType::F32, py::arg("capacity"), py::arg("max_peers") = 8,
       py::arg("max_lag") = 4, py::arg("grid") = 0, py::arg("timeout_s") = 60.0, py::arg("order_ref") = true,
       py::arg("high_priority") = true, py::arg("order_release") = true, py::arg("spin_us") = 1000, py::arg("split") = true,
+      py::arg("min_chunk") = 0,
       "RoundPlane of the protocol engine on MI355X: an HBM arena exported over IPC, one threshold-kernel launch "
       "per round (csrc/hip/xgmi_plane.h)");
   py::enum_<Algo>(h, "Algo").value("Auto", Algo::Auto).value("TwoShot", Algo::TwoShot).value("OneShot", Algo::OneShot).value("Ring", Algo::Ring).value("LL", Algo::LL);
@@ -350,6 +352,8 @@ void bind_hip(py::module_& m) {
           py::arg("comms"), py::arg("inputs"), py::arg("outputs"), py::arg("n"), py::arg("dtype"),
           py::arg("stream") = 0, py::arg("th_reduce") = 1.0f, py::arg("th_complete") = 1.0f, py::arg("counts") = 0,
           py::arg("scale") = 1.0f, py::arg("rescale") = false)
+      .def("resolve", &XgmiComm::resolve, py::arg("n"), py::arg("dtype"), py::arg("algo") = Algo::Auto,
+           py::arg("ranks_in_launch") = 1, "the kernel a call of `algo` over n elements runs (Auto resolved)")
       .def("threshold_chunks", &XgmiComm::threshold_chunks, py::arg("n"), py::arg("dtype"),
            py::arg("ranks_in_launch") = 1)
       .def("set_straggler", &XgmiComm::set_straggler, py::arg("rank"), py::arg("us"))
@@ -441,6 +445,7 @@ void bind_hip(py::module_& m) {
       .def_property_readonly("device", &XgmiComm::device)
       .def_property("grid", &XgmiComm::grid, &XgmiComm::set_grid)
       .def_property("oneshot_max_bytes", &XgmiComm::oneshot_max_bytes, &XgmiComm::set_oneshot_max_bytes)
+      .def_property("ll_auto_max_bytes", &XgmiComm::ll_auto_max_bytes, &XgmiComm::set_ll_auto_max_bytes)
       .def_property_readonly("ll_max_bytes", &XgmiComm::ll_max_bytes)
       .def_property_readonly("slot_bytes", &XgmiComm::slot_bytes)
       .def_property_readonly("slab_bytes", &XgmiComm::slab_bytes)

@@ -51,6 +51,10 @@ struct AdamShard {
 };
 
 constexpr int kMaxRanks = 16;
+// Threshold kernel: gather units (chunk x peer) one workgroup may own (its pending bitmap in
+// LDS), and reduce chunks per workgroup with a launch snapshot (reference arrival order).
+constexpr int kThresholdGatherUnits = 4096;
+constexpr int kThresholdSnapChunks = 2048;
 constexpr int kCommThreads = 256;
 
 struct CommStats {
@@ -75,9 +79,12 @@ class XgmiComm {
   // call (no hipMalloc / hipFree / hipMemset / hipDeviceSynchronize): a plane re-lays its
   // arena out while a peer's round kernel may be spinning on this worker; the caller
   // resets the control words stream-ordered (hipMemsetAsync) before the first launch.
+  // flag_gran: slot bytes per flag word (0 = min_chunk_bytes(), 1 KiB). The protocol plane
+  // passes its maxChunkSize in bytes when chunks are finer, so that every reference chunk
+  // keeps a flag, a count and a threshold decision of its own (xgmi_plane.cc).
   XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid = 0, double timeout_s = 20.0,
            int threshold_rows = 0, char* external_slab = nullptr, int64_t external_bytes = 0,
-           int64_t min_flag_bytes = 0, uint32_t* external_ctl = nullptr);
+           int64_t min_flag_bytes = 0, uint32_t* external_ctl = nullptr, int64_t flag_gran = 0);
   ~XgmiComm();
   XgmiComm(const XgmiComm&) = delete;
   XgmiComm& operator=(const XgmiComm&) = delete;
@@ -97,9 +104,10 @@ class XgmiComm {
     int64_t slot_bytes = 0, slot_stride = 0, maxch = 0, off_S = 0, off_R = 0, off_LL = 0, ll_max = 0, ll_slot = 0;
     int64_t slab_bytes = 0, alloc_bytes = 0;
   };
-  static Layout layout(int world, int64_t slot_bytes, int threshold_rows, int64_t min_flag_bytes = 0);
+  static Layout layout(int world, int64_t slot_bytes, int threshold_rows, int64_t min_flag_bytes = 0,
+                       int64_t flag_gran = 0);
   // Bytes of the flag table alone (the part of off_S before its 64 KiB rounding).
-  static int64_t flag_bytes(int world, int64_t slot_bytes, int threshold_rows);
+  static int64_t flag_bytes(int world, int64_t slot_bytes, int threshold_rows, int64_t flag_gran = 0);
   // Tell every peer that this rank has finished every threshold round up to `value`
   // (progress words; enqueued on `stream`). The protocol plane publishes its round base
   // after draining an old membership epoch, which opens the peers' lag gates for the new
@@ -113,6 +121,10 @@ class XgmiComm {
   // Pointers must be 16-byte aligned. Enqueued on `stream`; returns immediately.
   void allreduce(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, Algo algo = Algo::Auto,
                  float scale = 1.f);
+  // The kernel a call of `algo` (Auto included) over n elements runs - the one place the
+  // automatic dispatch is decided (allreduce() and the bench's latency table both use it).
+  // ranks_in_launch: logical ranks of this device served by one launch (LocalCluster).
+  Algo resolve(int64_t n, DType dt, Algo algo, int ranks_in_launch = 1) const;
   // Straggler-tolerant round (xgmi_threshold.hip): a chunk is reduced once
   // f32((th_reduce * P)) contributions are in, the round completes once
   // f32(th_complete * P * nch) reduced chunks are in (missing ones -> zeros, count 0), and
@@ -208,6 +220,8 @@ class XgmiComm {
   int64_t slot_bytes() const { return slot_bytes_; }
   int64_t oneshot_max_bytes() const { return oneshot_max_; }
   void set_oneshot_max_bytes(int64_t b) { oneshot_max_ = b; }
+  int64_t ll_auto_max_bytes() const { return ll_auto_max_; }
+  void set_ll_auto_max_bytes(int64_t b) { ll_auto_max_ = b; }
   // Largest tensor (bytes) one low-latency launch carries (Algo::LL; larger ones run in
   // segments). Fixed at construction: the LL slots are sized for it (MXAR_LL_MAX).
   int64_t ll_max_bytes() const { return ll_max_; }
@@ -269,6 +283,7 @@ class XgmiComm {
   int delay_rank_ = -1;
   double delay_us_ = 0;
   int64_t oneshot_max_;
+  int64_t ll_auto_max_ = 0;  // Auto picks the low-latency one-shot up to this many bytes
   double timeout_s_;
   int fence_ = 3;
   uint64_t* stamps_ = nullptr;  // phase-stamp buffer (study knob, set_phase_stamps)

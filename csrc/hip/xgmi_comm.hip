@@ -227,6 +227,10 @@ __global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
 //   final RS          : block (r+1) = S_r[P-2][c] + in[(r+1)][c], scaled once, to out and
 //                       into next's R[0][c], flag F2_next[0][c].
 //   AG step t (0..P-2): R_r[t][c] = block (r-t): copy to out, forward into next's R[t+1].
+// Partial sums travel in fp32 whatever the element type (S slots hold fp32; a bf16 input is
+// widened on the first hop), so a bf16 ring is rounded ONCE, at the final RS hop - as the
+// two-shot is. For 16-bit types that costs 2x bytes on the RS hops and halves
+// the elements one launch carries (XgmiComm::run segments by slot_bytes / 4 per block).
 // Slot reuse across launches is safe: rank r's predecessor can only start the next launch
 // after it received every block of this one, which transitively follows every read r
 // makes of its S/R slots. One xGMI link per direction per rank carries the traffic.
@@ -264,6 +268,82 @@ __device__ __forceinline__ void copy_slab_fwd(char* out, char* next_slab, const 
   }
 }
 
+// One ring hop on fp32 partials. `partial` (fp32 slab, null on the first hop) + `in` (element
+// type E) -> either the next fp32 partial (`fwd_f32`, write-through into the next rank's S
+// slot) or, on the final hop, scale x sum rounded once to E into `out` and the next rank's R
+// slot (`fwd_e`). One E pack (16 B) of input per lane per step, E::ELEMS / 4 fp32 packs of
+// partial; two steps in flight per lane.
+template <class E>
+__device__ __forceinline__ void ring_hop(const char* partial, const char* in, char* fwd_f32, char* out, char* fwd_e,
+                                         int64_t len, float scale) {
+  constexpr int NP = E::ELEMS / 4;  // fp32 packs per E pack
+  const int64_t npk = len / E::ELEMS;
+  const bool has_p = partial != nullptr;
+  const __amdgpu_buffer_rsrc_t rp = slab_rsrc(has_p ? partial : in);
+  const __amdgpu_buffer_rsrc_t ri = slab_rsrc(in);
+  const __amdgpu_buffer_rsrc_t rf = slab_rsrc(fwd_f32 != nullptr ? fwd_f32 : in);
+  const __amdgpu_buffer_rsrc_t ro = slab_rsrc(out != nullptr ? out : in);
+  const __amdgpu_buffer_rsrc_t re = slab_rsrc(fwd_e != nullptr ? fwd_e : in);
+  constexpr int U = 2;
+  auto step = [&](int64_t i0, int nu) {
+    Pack16 xv[U], pv[U][NP];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u >= nu) break;
+      const int64_t i = i0 + u * kCommThreads;
+      xv[u] = ld16_sc1(ri, static_cast<uint32_t>(i * 16));
+      if (has_p) {
+#pragma unroll
+        for (int h = 0; h < NP; ++h) pv[u][h] = ld16_sc1(rp, static_cast<uint32_t>((i * NP + h) * 16));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u >= nu) break;
+      const int64_t i = i0 + u * kCommThreads;
+      Acc<E> acc;
+      acc.zero();
+      if (has_p) {
+#pragma unroll
+        for (int h = 0; h < NP; ++h)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc.v[4 * h + q] = __uint_as_float(pv[u][h][q]);
+      }
+      acc.add(xv[u]);
+      if (fwd_f32 != nullptr) {
+#pragma unroll
+        for (int h = 0; h < NP; ++h) {
+          Pack16 o;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = __float_as_uint(acc.v[4 * h + q]);
+          st16_wt(rf, static_cast<uint32_t>((i * NP + h) * 16), o);
+        }
+      } else {
+        if (scale != 1.f) acc.scale(scale);
+        const Pack16 o = acc.pack();
+        st16_wt(ro, static_cast<uint32_t>(i * 16), o);
+        if (fwd_e != nullptr) st16_wt(re, static_cast<uint32_t>(i * 16), o);
+      }
+    }
+  };
+  int64_t i = threadIdx.x;
+  for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) step(i, U);
+  for (; i < npk; i += kCommThreads) step(i, 1);
+  const int64_t t = npk * E::ELEMS + threadIdx.x;
+  if (t < len) {  // ragged tail: one element per lane
+    float acc = (has_p ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rp, static_cast<int>(t * 4), 0, kAuxSc1))
+                       : 0.f) +
+                ld_scalar_sc1<E>(ri, t);
+    if (fwd_f32 != nullptr) {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc), rf, static_cast<int>(t * 4), 0, kAuxWt);
+    } else {
+      acc *= scale;
+      st_scalar_wt<E>(ro, t, acc);
+      if (fwd_e != nullptr) st_scalar_wt<E>(re, t, acc);
+    }
+  }
+}
+
 template <class E>
 __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
   constexpr int es = 16 / E::ELEMS;
@@ -285,16 +365,17 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     auto blen = [&](int b) { return clamp_len(clamp_len(a.n - static_cast<int64_t>(b) * a.block, a.block) - cstart, a.chunk); };
     auto at = [&](int b) { return (static_cast<int64_t>(b) * a.block + cstart) * es; };
-    // every slot access of this chunk is [cstart, cstart + chunk) of a row; flags index c
-    const bool inb = unit_in_bounds(a, cstart * es, clamp_len(a.block - cstart, a.chunk) * es, c, err);
+    const int64_t pofs = cstart * 4;  // fp32 partial slots
+    // every S access of this chunk is fp32 [cstart, cstart + chunk), every R access E-typed
+    const bool inb = unit_in_bounds(a, pofs, clamp_len(a.block - cstart, a.chunk) * 4, c, err);
     if (!inb) {  // publish every flag this workgroup owes, move no data
       publish_flags([&](int) { return f1(a, nxt, 0, c); }, 1, epoch, rel);
       continue;
     }
-    // RS step 0: raw own block r
+    // RS step 0: raw own block r, widened to fp32
     {
       const int64_t len = blen(r);
-      if (len > 0) copy_to_slab<E>(a.base[nxt] + a.off_S + cstart * es, in + at(r), len);
+      if (len > 0) ring_hop<E>(nullptr, in + at(r), a.base[nxt] + a.off_S + pofs, nullptr, nullptr, len, 1.f);
       publish_flags([&](int) { return f1(a, nxt, 0, c); }, 1, epoch, rel);
     }
     // RS steps 1..P-1 (the last one completes block r+1)
@@ -306,16 +387,13 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
                  ERR_TIMEOUT_SCATTER, acq);
       ps.add(2, tw);
       ps.count(6);
-      const RedSrc src{in + at(b), a.base[r] + a.off_S + (s - 1) * slot + cstart * es, 0, 1};
+      const char* part = a.base[r] + a.off_S + (s - 1) * slot + pofs;
       if (s < P - 1) {
-        char* d = a.base[nxt] + a.off_S + s * slot + cstart * es;
-        if (len > 0) reduce_to<E, 2>(2, src, 1, -1, [&](int) -> char* { return d; }, len, 1.f, true);
+        if (len > 0) ring_hop<E>(part, in + at(b), a.base[nxt] + a.off_S + s * slot + pofs, nullptr, nullptr, len, 1.f);
         publish_flags([&](int) { return f1(a, nxt, s, c); }, 1, epoch, rel);
       } else {
-        char* o = out + at(b);
-        char* d = a.base[nxt] + a.off_R + cstart * es;
         if (len > 0)
-          reduce_to<E, 2>(2, src, 2, 0, [&](int k) -> char* { return k == 0 ? o : d; }, len, a.scale, a.fence & 1);
+          ring_hop<E>(part, in + at(b), nullptr, out + at(b), a.base[nxt] + a.off_R + cstart * es, len, a.scale);
         publish_flags([&](int) { return f2(a, nxt, 0, c); }, 1, epoch, rel);
       }
     }
@@ -365,19 +443,22 @@ static int default_grid(int device) {
   return 2 * cus;  // every workgroup must stay resident (they spin): 2 x 256-thread WG per CU
 }
 
-int64_t XgmiComm::flag_bytes(int world, int64_t slot_bytes, int threshold_rows) {
+int64_t XgmiComm::flag_bytes(int world, int64_t slot_bytes, int threshold_rows, int64_t flag_gran) {
   const int rows = 1 + threshold_rows;
-  const int64_t maxch = round_up(std::max<int64_t>(slot_bytes, 64 * 1024), 64 * 1024) / min_chunk_bytes();
+  if (flag_gran <= 0) flag_gran = min_chunk_bytes();
+  const int64_t maxch = ceil_div(round_up(std::max<int64_t>(slot_bytes, 64 * 1024), 64 * 1024), flag_gran);
   // [F1: rows x P x maxch][F2: rows x P x maxch][FB: P][PROG: P][F2C: rows x P x maxch][FORCE: P]
   return (3 * rows * world * maxch + 3 * world) * 4;
 }
 
-XgmiComm::Layout XgmiComm::layout(int world, int64_t slot_bytes, int threshold_rows, int64_t min_flag_bytes) {
+XgmiComm::Layout XgmiComm::layout(int world, int64_t slot_bytes, int threshold_rows, int64_t min_flag_bytes,
+                                  int64_t flag_gran) {
   Layout L;
   const int rows = 1 + threshold_rows;
+  if (flag_gran <= 0) flag_gran = min_chunk_bytes();
   L.slot_bytes = round_up(std::max<int64_t>(slot_bytes, 64 * 1024), 64 * 1024);
-  L.maxch = L.slot_bytes / min_chunk_bytes();
-  L.off_S = round_up(std::max(flag_bytes(world, slot_bytes, threshold_rows), min_flag_bytes), 64 * 1024);
+  L.maxch = ceil_div(L.slot_bytes, flag_gran);
+  L.off_S = round_up(std::max(flag_bytes(world, slot_bytes, threshold_rows, flag_gran), min_flag_bytes), 64 * 1024);
   // Slots sit slot_stride = capacity + MXAR_SLOT_PAD bytes apart (default 0). A pad takes the
   // P slots a reduce reads at one offset off a power-of-two spacing; an A/B on one box showed
   // no gain for the reduce kernel (benchmarks/bench_reduce.py --pad-kib, profiles/reduce_kernel.md),
@@ -410,13 +491,13 @@ int64_t XgmiComm::ipc_safe_bytes(int64_t bytes) {
 
 XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid, double timeout_s,
                    int threshold_rows, char* external_slab, int64_t external_bytes, int64_t min_flag_bytes,
-                   uint32_t* external_ctl)
+                   uint32_t* external_ctl, int64_t flag_gran)
     : rank_(rank), world_(world), device_(device), grid_(grid), rows_(1 + threshold_rows), timeout_s_(timeout_s) {
   if (threshold_rows < 0 || threshold_rows > 64)
     throw std::invalid_argument("XgmiComm: threshold_rows (maxLag + 1) must be in [0, 64]");
   if (world < 1 || world > kMaxRanks) throw std::invalid_argument("XgmiComm: world must be in [1, 16]");
   if (rank < 0 || rank >= world) throw std::invalid_argument("XgmiComm: bad rank");
-  const Layout L = layout(world, slot_bytes, threshold_rows, min_flag_bytes);
+  const Layout L = layout(world, slot_bytes, threshold_rows, min_flag_bytes, flag_gran);
   slot_bytes_ = L.slot_bytes;
   maxch_ = L.maxch;
   off_S_ = L.off_S;
@@ -428,7 +509,18 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   off_LL_ = L.off_LL;
   slab_bytes_ = L.slab_bytes;
   alloc_bytes_ = L.alloc_bytes;
-  oneshot_max_ = std::min<int64_t>(slot_bytes_, 256 * 1024);
+  // Automatic dispatch limits (resolve()), measured with P logical ranks in one launch on one
+  // MI355X (bench.py latency_vs_size, profiles/round3/README.md): the low-latency one-shot
+  // wins up to 1 MiB at 2 ranks and 256 KiB at 8 (it moves 2x bytes as flag-carrying LL
+  // words, so it loses to the plain kernels as soon as they are bandwidth bound); the
+  // one-shot (one hop, every rank reads all P inputs) wins up to 16 MiB at 2 ranks, where it
+  // moves the same bytes as the two-shot with one hand-off less; at 8 ranks the two-shot
+  // takes over from the low-latency kernel directly. MXAR_LL_AUTO_MAX / MXAR_ONESHOT_MAX
+  // override (bytes).
+  const int64_t mib = int64_t{1} << 20;
+  ll_auto_max_ = world_ <= 2 ? mib : world_ <= 4 ? mib / 2 : mib / 4;
+  if (const char* e = std::getenv("MXAR_LL_AUTO_MAX")) ll_auto_max_ = std::max<int64_t>(0, std::atoll(e));
+  oneshot_max_ = std::min<int64_t>(slot_bytes_, world_ <= 2 ? 16 * mib : world_ <= 4 ? 2 * mib : mib / 4);
   if (const char* e = std::getenv("MXAR_ONESHOT_MAX")) oneshot_max_ = std::min<int64_t>(slot_bytes_, std::atoll(e));
   if (grid_ <= 0) grid_ = default_grid(device);
   if (const char* f = std::getenv("MXAR_FENCE")) fence_ = std::atoi(f) & 3;
@@ -698,7 +790,8 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   a.dynamic = c0.dynamic_ ? 1 : 0;
   a.stamps = c0.stamps_;
   if (a.stamps != nullptr && gx * ranks_here > c0.stamp_slots_) a.stamps = nullptr;  // buffer too small: off
-  if (kind != Algo::LL && (static_cast<int64_t>(a.nch) * a.sub > c0.maxch_ || a.block * es > c0.slot_bytes_ + 16))
+  const int64_t block_bytes = a.block * (kind == Algo::Ring ? 4 : es);  // ring: fp32 partial slots
+  if (kind != Algo::LL && (static_cast<int64_t>(a.nch) * a.sub > c0.maxch_ || block_bytes > c0.slot_bytes_ + 16))
     throw std::logic_error("XgmiComm: segment geometry exceeds slab");
   const dim3 grid(gx, ranks_here);
   if (adam != nullptr) {
@@ -763,10 +856,9 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
         launch_copy(ins[y], outs[y], n * es, stream);
     return;
   }
-  const bool ll = algo == Algo::LL && c0.ll_max_ >= 16;
-  const bool oneshot = !ll && (algo == Algo::OneShot ? (n * es <= c0.slot_bytes_)
-                                                     : (algo == Algo::Auto && n * es <= c0.oneshot_max_));
-  const Algo kind = ll ? Algo::LL : oneshot ? Algo::OneShot : algo == Algo::Ring ? Algo::Ring : Algo::TwoShot;
+  const Algo kind = c0.resolve(n, dt, algo, static_cast<int>(group.size()));
+  const bool ll = kind == Algo::LL;
+  const bool oneshot = kind == Algo::OneShot;
   TraceScope span("xgmi", [&] {
     return std::make_pair(std::string(ll        ? "ll "
                                       : oneshot ? "oneshot "
@@ -776,7 +868,10 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
                           "{\"rank\":" + std::to_string(c0.rank_) + ",\"ranks_in_launch\":" +
                               std::to_string(group.size()) + "}");
   });
-  const int64_t seg = ll ? c0.ll_max_ / es : oneshot ? c0.slot_bytes_ / es : c0.world_ * (c0.slot_bytes_ / es);
+  // ring: S slots carry fp32 partials, so a block holds slot_bytes / 4 elements
+  const int64_t seg = ll ? c0.ll_max_ / es
+                      : oneshot ? c0.slot_bytes_ / es
+                      : kind == Algo::Ring ? c0.world_ * (c0.slot_bytes_ / 4) : c0.world_ * (c0.slot_bytes_ / es);
   std::vector<const char*> ip(group.size());
   std::vector<char*> op(group.size());
   for (int64_t off = 0; off < n; off += seg) {
@@ -787,6 +882,19 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
     }
     launch_segment(group, ip.data(), op.data(), len, dt, stream, kind, scale);
   }
+}
+
+Algo XgmiComm::resolve(int64_t n, DType dt, Algo algo, int ranks_in_launch) const {
+  (void)ranks_in_launch;
+  const int64_t bytes = n * static_cast<int64_t>(dtype_size(dt));
+  if (algo == Algo::LL) return ll_max_ >= 16 ? Algo::LL : Algo::TwoShot;
+  if (algo == Algo::OneShot) return bytes <= slot_bytes_ ? Algo::OneShot : Algo::TwoShot;
+  if (algo == Algo::Ring) return Algo::Ring;
+  if (algo == Algo::TwoShot) return Algo::TwoShot;
+  // Auto: low-latency one-shot, then one-shot, then two-shot, with size limits per rank count
+  // set in the constructor from the bench's latency table (profiles/round3/README.md)
+  if (ll_max_ >= 16 && bytes <= ll_auto_max_) return Algo::LL;
+  return bytes <= oneshot_max_ ? Algo::OneShot : Algo::TwoShot;
 }
 
 int64_t XgmiComm::block_elems(int64_t n, DType dt) const {
@@ -857,17 +965,19 @@ void XgmiComm::geometry_threshold(int64_t n, DType dt, int ranks_here, int64_t* 
   const int64_t min_chunk = min_chunk_bytes() / es;
   const int gmax = std::max(1, grid_ / std::max(1, ranks_here));
   *block = round_up(ceil_div(n, world_), elems);
-  // one reduce unit (a chunk: one threshold decision) per workgroup; phase 1/3 get P-1 each
+  // one reduce unit (a chunk: one threshold decision) per workgroup; phase 1/3 get P-1 each,
+  // spread over up to (P - 1) x nch workgroups when the chunks are few (small tensors)
   *chunk = std::max(min_chunk, round_up(ceil_div(*block, gmax), elems));
   *nch = static_cast<int>(std::max<int64_t>(1, ceil_div(*block, *chunk)));
-  *gx = std::min(gmax, std::max(*nch, 1));
+  *gx = static_cast<int>(std::min<int64_t>(gmax, std::max<int64_t>(1, static_cast<int64_t>(std::max(world_ - 1, 1)) * *nch)));
 }
 
 int XgmiComm::round_grid(int nch) const {
-  // one reduce unit per workgroup where possible; at most 1024 gather units per workgroup
-  // (the kernel's pending bitmap)
+  // one reduce unit per workgroup where possible, and the scatter / gather units (P - 1 per
+  // chunk) spread over as many workgroups as there are, up to the grid: a round of few
+  // chunks otherwise serialises its hand-offs in one workgroup
   const int64_t units = static_cast<int64_t>(std::max(world_ - 1, 1)) * std::max(nch, 1);
-  return static_cast<int>(std::min<int64_t>(grid_, std::max<int64_t>({1, nch, ceil_div(units, 1024)})));
+  return static_cast<int>(std::min<int64_t>(grid_, std::max<int64_t>({1, nch, units})));
 }
 
 int XgmiComm::threshold_chunks(int64_t n, DType dt, int ranks_in_launch) const {
@@ -944,8 +1054,15 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
     a.sub = 1;
     a.subchunk = a.chunk;
   }
-  if (ceil_div(static_cast<int64_t>(W - 1) * a.nch * a.sub, gx) > 1024)
-    throw std::logic_error("allreduce_threshold: more than 1024 gather units per workgroup");
+  // The reference's arrival order needs every reduce chunk of a workgroup in its launch
+  // snapshot (xgmi_threshold.hip, S0); at thresholds 1 the order cannot change the result.
+  if (spec != nullptr && spec->order_ref && !(thr >= 1.f && thc >= 1.f) &&
+      ceil_div(static_cast<int64_t>(a.nch) * a.sub, gx) > kThresholdSnapChunks)
+    throw std::invalid_argument("round: more than " + std::to_string(kThresholdSnapChunks) +
+                                " chunks per workgroup at thresholds < 1 (the arrival-order snapshot)");
+  if (ceil_div(static_cast<int64_t>(W - 1) * a.nch * a.sub, gx) > kThresholdGatherUnits)
+    throw std::invalid_argument("allreduce_threshold: more than " + std::to_string(kThresholdGatherUnits) +
+                                " gather units per workgroup (too many chunks for the grid)");
   a.n = n;
   a.P = W;
   a.rows = c0.rows_;

@@ -85,6 +85,8 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   o_.ring = std::max(4, o_.ring);
   if (const char* e = std::getenv("MXAR_PLANE_SPLIT")) o_.split = std::atoi(e) != 0;  // A/B knob
   const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
+  flag_gran_ = o_.min_chunk > 0 ? std::min<int64_t>(XgmiComm::min_chunk_bytes(), o_.min_chunk * es)
+                                : XgmiComm::min_chunk_bytes();
   // The flag table is reserved at its largest size over every membership of <= max_peers
   // workers and maxLag <= max_lag, so it sits at the same place in every layout: a late
   // store of an older layout can only hit a flag word (holding an older, smaller epoch),
@@ -92,15 +94,18 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   for (int P = 1; P <= o_.max_peers; ++P) {
     const int64_t block = static_cast<int64_t>(f32_ceil_div(o_.capacity, P));
     for (int lag = 0; lag <= o_.max_lag; ++lag)
-      flag_bytes_ = std::max(flag_bytes_, XgmiComm::flag_bytes(P, std::max<int64_t>(block * es, 16), lag + 1));
+      flag_bytes_ =
+          std::max(flag_bytes_, XgmiComm::flag_bytes(P, std::max<int64_t>(block * es, 16), lag + 1, flag_gran_));
   }
   int64_t max_counts = 1;  // P x chunks per round, over every membership this plane may see
   for (int P = 1; P <= o_.max_peers; ++P) {
     const int64_t block = static_cast<int64_t>(f32_ceil_div(o_.capacity, P));
-    const XgmiComm::Layout L = XgmiComm::layout(P, std::max<int64_t>(block * es, 16), o_.max_lag + 1, flag_bytes_);
+    const XgmiComm::Layout L =
+        XgmiComm::layout(P, std::max<int64_t>(block * es, 16), o_.max_lag + 1, flag_bytes_, flag_gran_);
     arena_bytes_ = std::max(arena_bytes_, L.slab_bytes);
     for (int lag = 0; lag <= o_.max_lag; ++lag) {
-      const int64_t maxch = XgmiComm::layout(P, std::max<int64_t>(block * es, 16), lag + 1, flag_bytes_).maxch;
+      const int64_t maxch =
+          XgmiComm::layout(P, std::max<int64_t>(block * es, 16), lag + 1, flag_bytes_, flag_gran_).maxch;
       max_counts = std::max<int64_t>(max_counts, static_cast<int64_t>(P) * maxch);
       split_bytes_ = std::max(split_bytes_, XgmiComm::split_scratch_bytes(P, maxch));
     }
@@ -332,17 +337,28 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
   chunk_ = cfg.maxChunkSize;
   int64_t nch = std::max<int64_t>(1, ceil_div(block_, chunk_));
   const int64_t slot = std::max<int64_t>(block_ * es, 16);
-  const XgmiComm::Layout L = XgmiComm::layout(P, slot, cfg.maxLag + 1, flag_bytes_);
+  const XgmiComm::Layout L = XgmiComm::layout(P, slot, cfg.maxLag + 1, flag_bytes_, flag_gran_);
   if (L.slab_bytes > arena_bytes_) throw ProtocolError("xgmi plane arena too small for this membership");
+  nch_ref_ = static_cast<int>(nch);
+  coarse_ = 1;
   if (nch > L.maxch) {
-    // more chunks than the flag table holds (maxChunkSize far below 1 KiB on a big vector):
-    // chunks become whole multiples of maxChunkSize; counts are per such chunk
+    // More reference chunks than the flag table holds (maxChunkSize below the plane's flag
+    // granularity). At thresholds 1 every contribution and every chunk is taken whatever the
+    // granularity, so the kernel runs whole multiples of maxChunkSize and the counts are
+    // reported per reference chunk. Below 1 the threshold decisions ARE per reference chunk
+    // (DataBuffer.scala:28-29,69-75): coarser units would change which data a round keeps.
+    if (cfg.thReduce < 1.f || cfg.thComplete < 1.f)
+      throw ProtocolError("maxChunkSize " + std::to_string(cfg.maxChunkSize) + " at thReduce " +
+                          std::to_string(cfg.thReduce) + " / thComplete " + std::to_string(cfg.thComplete) +
+                          " needs one flag per chunk: build the plane with min_chunk <= " +
+                          std::to_string(cfg.maxChunkSize) + " (PlaneJob(min_chunk=...), mxar.plane.min_chunk)");
     const int64_t m = ceil_div(nch, L.maxch);
     chunk_ *= m;
+    coarse_ = static_cast<int>(m);
     nch = ceil_div(block_, chunk_);
     st_.coarsened++;
-    MXAR_LOG(WARNING, "plane", "maxChunkSize " << cfg.maxChunkSize << " gives more chunks than the flag table; "
-                                               << "chunks of " << chunk_ << " elements");
+    MXAR_LOG(INFO, "plane", "maxChunkSize " << cfg.maxChunkSize << " is finer than the flag table at thresholds 1: "
+                                            << "kernel chunks of " << chunk_ << " elements, counts per reference chunk");
   }
   nch_ = static_cast<int>(nch);
   std::vector<char*> bases(P, nullptr);
@@ -360,7 +376,7 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
   // a new membership may reuse round epochs of the abandoned one: no stale decision survives
   hip_check(hipMemsetAsync(split_mem_, 0, split_bytes_, stream_), "hipMemsetAsync(plane split scratch)");
   comm_ = std::make_unique<XgmiComm>(cfg.id, P, o_.device, slot, o_.grid, o_.timeout_s, cfg.maxLag + 1, arena_,
-                                     arena_bytes_, flag_bytes_, ctl_mem_);
+                                     arena_bytes_, flag_bytes_, ctl_mem_, flag_gran_);
   comm_->connect_ptrs(bases);
   comm_->set_phase_stamps(stamps_, stamp_slots_);
   // Every round of the previous epoch has finished here (drained): say so to the peers. Their
@@ -390,7 +406,8 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
   last_round_ = cfg.startRound - 1;
   err_seen_ = 0;
   MXAR_LOG(INFO, "plane", "xgmi plane: worker " << cfg.id << " of " << P << ", block " << block_ << ", chunk "
-                                                << chunk_ << " x " << nch_ << ", rows " << cfg.maxLag + 1
+                                                << chunk_ << " x " << nch_ << " (" << nch_ref_
+                                                << " reference chunks), rows " << cfg.maxLag + 1
                                                 << ", round epochs from " << cfg.roundBase + 1);
 }
 
@@ -546,7 +563,14 @@ void XgmiRoundPlane::completion_loop() {
     res.cold = rec.cold;
     const int32_t* host = ring_ + static_cast<size_t>(rec.slot) * ring_stride_;
     const size_t nc = static_cast<size_t>(cfg_.peers) * nch_;
-    res.count.assign(host, host + nc);
+    if (coarse_ == 1) {
+      res.count.assign(host, host + nc);
+    } else {  // coarsened at thresholds 1: every reference chunk of a kernel chunk shares its count
+      res.count.resize(static_cast<size_t>(cfg_.peers) * nch_ref_);
+      for (int j = 0; j < cfg_.peers; ++j)
+        for (int c = 0; c < nch_ref_; ++c)
+          res.count[static_cast<size_t>(j) * nch_ref_ + c] = host[static_cast<size_t>(j) * nch_ + c / coarse_];
+    }
     const uint32_t err = static_cast<uint32_t>(host[ring_stride_ - 1]);
     res.error = (err & ~err_seen_) | (e != hipSuccess ? 0x80000000u : 0u);
     err_seen_ |= err;

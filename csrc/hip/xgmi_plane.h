@@ -54,6 +54,12 @@ struct XgmiPlaneOptions {
   bool order_release = true;  // a round output's release waits for the default stream (buffer())
   int spin_us = 1000;         // completion thread polls a round's event this long before blocking
   bool split = true;          // chunks fewer than workgroups are split over several (threshold kernel)
+  // Smallest maxChunkSize (elements) that keeps one flag word, count and threshold decision
+  // per reference chunk (DataBuffer.scala:12,28-29,69-75); 0 = 1 KiB of data per flag. Finer
+  // chunks cost flag-table memory (3 x rows x P words per chunk). A job with a finer
+  // maxChunkSize runs at thresholds 1 with chunks coarsened to the flag granularity (counts
+  // reported per reference chunk), and is refused at thresholds < 1 (ProtocolError).
+  int64_t min_chunk = 0;
 };
 
 struct XgmiPlaneStats {
@@ -72,7 +78,9 @@ class XgmiRoundPlane final : public RoundPlane {
   void force(int round) override;
   void abort(int round) override;
   void drain() override;
-  int chunks() const override { return nch_; }
+  // chunks per block as the reference counts them (ceil(block / maxChunkSize)): the length of
+  // an output's counts is peers x chunks()
+  int chunks() const override { return nch_ref_; }
 
   const XgmiPlaneOptions& options() const { return o_; }
   const XgmiPlaneStats& stats() const { return st_; }
@@ -114,6 +122,7 @@ class XgmiRoundPlane final : public RoundPlane {
   char* arena_ = nullptr;
   int64_t arena_bytes_ = 0;
   int64_t flag_bytes_ = 0;  // flag table reserved at its largest size (every layout the same)
+  int64_t flag_gran_ = 0;   // slot bytes per flag word (XgmiComm flag_gran)
   uint64_t arena_id_ = 0;
   std::string desc_;
   uint32_t* hforce_ = nullptr;      // pinned host words the engine raises: [0] force, [1] abort
@@ -124,7 +133,9 @@ class XgmiRoundPlane final : public RoundPlane {
   PlaneConfig cfg_;
   bool configured_ = false;
   int64_t block_ = 0, chunk_ = 0;
-  int nch_ = 0;
+  int nch_ = 0;       // chunks per block the kernel runs
+  int nch_ref_ = 0;   // reference chunks per block (= nch_ unless coarsened at thresholds 1)
+  int coarse_ = 1;    // reference chunks per kernel chunk
   int last_round_ = -1;  // last launched round of this epoch
   // pinned ring: per slot P x nch counts + the error word
   int32_t* ring_ = nullptr;

@@ -47,9 +47,9 @@ namespace mxar {
 
 namespace {
 
-constexpr int kMaxGatherUnits = 1024;  // gather units per workgroup (host geometry guarantees)
+constexpr int kMaxGatherUnits = kThresholdGatherUnits;  // gather units per workgroup (host geometry guarantees)
 constexpr int kGatherWords = kMaxGatherUnits / 64;
-constexpr int kMaxSnapChunks = 64;     // reduce chunks per workgroup with an S0 snapshot
+constexpr int kMaxSnapChunks = kThresholdSnapChunks;    // reduce chunks per workgroup with an S0 snapshot
 
 __device__ __forceinline__ uint32_t* prog(const CommArgs& a, int k, int s) {
   return reinterpret_cast<uint32_t*>(a.base[k]) + static_cast<int64_t>(2 * a.rows * a.P) * a.maxch + a.P + s;

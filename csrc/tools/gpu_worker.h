@@ -13,7 +13,8 @@ struct GpuWorkerParts {
   DataSource source;                  // data[i] = i + iteration, produced on the device
 };
 
-GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag, int grid, double timeout_s)
+GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag, int grid, double timeout_s,
+                               int64_t min_chunk)
     __attribute__((weak));
 
 }  // namespace mxar

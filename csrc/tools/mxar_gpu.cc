@@ -19,7 +19,8 @@
 namespace mxar {
 
 
-GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag, int grid, double timeout_s) {
+GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag, int grid, double timeout_s,
+                               int64_t min_chunk) {
   XgmiPlaneOptions o;
   o.device = device;
   o.dtype = DType::F32;
@@ -28,6 +29,7 @@ GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag,
   o.max_lag = max_lag;
   o.grid = grid;
   o.timeout_s = timeout_s;
+  o.min_chunk = min_chunk;
   GpuWorkerParts p;
   p.plane = make_xgmi_plane(o);
   hipStream_t s = nullptr;

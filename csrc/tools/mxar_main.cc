@@ -72,6 +72,7 @@ struct Options {
   int device = -1;  // worker: >= 0 runs the rounds on this GPU (mxar-gpu)
   int max_peers = 8, plane_max_lag = 4, grid = 0;
   double plane_timeout_s = 60.0;
+  int64_t min_chunk = 0;  // --min-chunk N: one flag per chunk of >= N elements (0: 1 KiB)
 };
 
 [[noreturn]] void usage(const char* msg) {
@@ -82,7 +83,8 @@ struct Options {
                "         --max-round N --round-timeout-ms N --loglevel L --quiet\n"
                "master control bridge (docs/BRIDGE.md): --bridge PORT [--external-rounds]\n"
                "       mxar drive [host:]bridgePort [rounds] [--lockstep]   (bridge client)\n"
-               "worker on a GPU (mxar-gpu): --device K [--max-peers N --plane-max-lag N --grid N --plane-timeout S]\n",
+               "worker on a GPU (mxar-gpu): --device K [--max-peers N --plane-max-lag N --grid N --plane-timeout S\n"
+               "                              --min-chunk N]\n",
                msg);
   std::exit(2);
 }
@@ -116,6 +118,7 @@ Options parse(int argc, char** argv) {
     else if (a == "--plane-max-lag") o.plane_max_lag = std::stoi(val());
     else if (a == "--grid") o.grid = std::stoi(val());
     else if (a == "--plane-timeout") o.plane_timeout_s = std::stod(val());
+    else if (a == "--min-chunk") o.min_chunk = std::stoll(val());
     else if (a.rfind("--", 0) == 0) usage(("unknown option " + a).c_str());
     else o.positional.push_back(a);
   }
@@ -227,7 +230,8 @@ void set_level(const std::string& l) {
   ClusterConfig cc;
   if (o.device >= 0) {  // the round engine on a GPU: one threshold-kernel launch per round
     if (make_gpu_worker == nullptr) usage("--device needs the GPU build of this executable: mxar-gpu");
-    GpuWorkerParts g = make_gpu_worker(o.device, size, o.max_peers, o.plane_max_lag, o.grid, o.plane_timeout_s);
+    GpuWorkerParts g = make_gpu_worker(o.device, size, o.max_peers, o.plane_max_lag, o.grid, o.plane_timeout_s,
+                                         o.min_chunk);
     cc.meta = g.plane->descriptor();  // relayed by the master in InitWorkers.planes
     sys->actor_of(std::make_unique<PlaneWorkerActor>(g.source, sink, g.plane), "worker");
   } else {

@@ -148,6 +148,66 @@ def test_straggler_matches_host_worker_core():
         job.shutdown()
 
 
+def test_fine_chunks_keep_reference_semantics():
+    """maxChunkSize below the 1 KiB flag granularity (the reference's default 2-float chunk on
+    a 1 M-float vector: 174 763 chunks per block): the plane keeps one flag, count and
+    threshold decision per reference chunk (min_chunk), so a deterministic straggler at
+    th = 2/3 gives bit-identical outputs and counts to the host WorkerCore
+    (DataBuffer.scala:12,28-29,69-75; AllreduceWorker.scala:56-57)."""
+    P, n, chunk, rounds = 3, 1 << 20, 2, 3
+    th = 2.0 / 3.0
+    straggler, delay = 2, 0.3
+    lvl = C.get_log_level()
+    C.set_log_level("ERROR")  # the host run logs every outdated 2-float ReduceBlock
+    try:
+        host = _host_outputs(P, n, chunk, th, straggler, delay, rounds)
+    finally:
+        C.set_log_level(lvl)
+
+    def slow(source):
+        def f(req):
+            time.sleep(delay)
+            return source(req)
+        return f
+
+    srcs = [iota_source(n, DEV, torch.float32, 1000.0 * k) for k in range(P)]
+    srcs[straggler] = slow(srcs[straggler])
+    job = PlaneJob(P, n, max_chunk_size=chunk, th_reduce=th, th_complete=th, max_lag=1, max_round=rounds - 1,
+                   sources=srcs, timeout_s=30.0)
+    try:
+        job.run(timeout=180)
+        step, nch = layout(n, P, chunk)
+        assert job.planes[0].chunks == nch and job.planes[0].stats.coarsened == 0
+        for k in range(P):
+            for it in range(rounds):
+                g, gc = job.outputs[k][it]
+                h, hc = host[k][it]
+                assert len(gc) == P * nch
+                assert gc == hc, (k, it, [i for i in range(len(gc)) if gc[i] != hc[i]][:8])
+                np.testing.assert_array_equal(g.float().cpu().numpy(), h, err_msg=f"worker {k} round {it}")
+    finally:
+        job.shutdown()
+
+
+def test_fine_chunks_coarsen_at_threshold_one():
+    """Without a fine flag table (min_chunk=0) a 2-float maxChunkSize runs at thresholds 1 in
+    coarse kernel chunks - the sums cannot change - with the counts still reported per
+    reference chunk."""
+    P, n, chunk = 2, 1 << 20, 2
+    job = PlaneJob(P, n, max_chunk_size=chunk, th_reduce=1.0, th_complete=1.0, max_lag=1, max_round=2,
+                   timeout_s=20.0, min_chunk=0)
+    try:
+        job.run(timeout=120)
+        step, nch = layout(n, P, chunk)
+        assert job.planes[0].chunks == nch and job.planes[0].stats.coarsened == 1
+        for k in range(P):
+            data, counts = job.outputs[k][2]
+            np.testing.assert_array_equal(data.float().cpu().numpy(), expected(n, 2, range(P)))
+            assert len(counts) == P * nch and all(c == P for c in counts)
+    finally:
+        job.shutdown()
+
+
 def _consistent(job, P, n, chunk, counts_ok):
     """Every chunk of every output is the sum of `count` distinct workers (0 -> zeros)."""
     step, nch = layout(n, P, chunk)

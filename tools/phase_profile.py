@@ -43,19 +43,28 @@ def main() -> None:
     dtype = torch.bfloat16
     S = a.mib << 20
     n = S // 2
-    cl = LocalCluster(a.P, slot_bytes=-(-S // a.P) + (1 << 20), grid=a.grid, timeout_s=10.0)
+    # a lag ring for the threshold kernel (its stamps: [1] lag gate done, [3] reduce done,
+    # [6] scatter done - see xgmi_threshold.hip)
+    cl = LocalCluster(a.P, slot_bytes=-(-S // a.P) + (1 << 20), grid=a.grid, timeout_s=10.0,
+                      max_lag=1 if "threshold" in a.algos else None)
     xs = [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=k) for k in range(a.P)]
     ys = [torch.empty_like(t) for t in xs]
     buf = torch.zeros(a.grid * a.P * SLOTS, dtype=torch.int64, device=dev)
     out = {"P": a.P, "bytes_per_rank": S, "grid": a.grid, "algos": {}}
     for algo in a.algos:
+        def run(algo=algo):
+            if algo == "threshold":
+                cl.allreduce_threshold(xs, ys, counts=False)
+            else:
+                cl.allreduce(xs, ys, algo=algo)
+
         for _ in range(3):
-            cl.allreduce(xs, ys, algo=algo)
+            run()
         rows = []
         for _ in range(a.iters):
             buf.zero_()
             cl.comms[0].set_phase_stamps(buf.data_ptr(), a.grid * a.P)
-            cl.allreduce(xs, ys, algo=algo)
+            run()
             torch.cuda.synchronize()
             cl.comms[0].set_phase_stamps(0, 0)
             st = buf.view(-1, SLOTS).cpu()
@@ -69,6 +78,7 @@ def main() -> None:
                 "reduce_wait_us": [us(x) for x in used[:, 2]],
                 "reduce_end_us": [us(int(x) - t0) for x in used[:, 3]],
                 "gather_wait_us": [us(x) for x in used[:, 4]],
+                "stamp6": [us(int(x) - t0) if algo == "threshold" else float(x) for x in used[:, 6]],
                 "end_us": [us(int(x) - t0) for x in used[:, 5]],
                 "workgroups": int(used.shape[0]),
             })
@@ -76,9 +86,9 @@ def main() -> None:
         span = [r["span_us"] for r in rows]
         best = rows[span.index(sorted(span)[len(span) // 2])]  # the median launch
         summ = {"span_us": stats(span), "start_skew_us": best["start_skew_us"], "workgroups": best["workgroups"]}
-        for k in ("scatter_end_us", "reduce_wait_us", "reduce_end_us", "gather_wait_us", "end_us"):
+        for k in ("scatter_end_us", "reduce_wait_us", "reduce_end_us", "gather_wait_us", "end_us", "stamp6"):
             summ[k] = stats(best[k])
-        summ["hbm_TBps_at_span_p50"] = round(hbm_bytes(S, a.P, algo) / (summ["span_us"]["p50"] * 1e-6) / 1e12, 3)
+        summ["hbm_TBps_at_span_p50"] = round(hbm_bytes(S, a.P, "twoshot" if algo == "threshold" else algo, 2) / (summ["span_us"]["p50"] * 1e-6) / 1e12, 3)
         out["algos"][algo] = summ
         print(json.dumps({algo: summ}), flush=True)
     if a.json:
