@@ -541,7 +541,8 @@ class LocalCluster:
         return outputs
 
     def allreduce(self, inputs: Sequence[torch.Tensor], outputs: Sequence[torch.Tensor] | None = None, *,
-                  algo: str = "auto", op: str = "sum") -> list[torch.Tensor]:
+                  algo: str = "auto", op: str = "sum", stream: int | None = None) -> list[torch.Tensor]:
+        """`stream`: raw HIP stream for a single-device cluster (default: the current one)."""
         outputs = self._check(inputs, outputs)
         n = inputs[0].numel()
         code = _dtype_code(inputs[0].dtype)
@@ -549,7 +550,7 @@ class LocalCluster:
             dev = self.devices[g[0]]
             _H.XgmiComm.allreduce_local([self.comms[k] for k in g], [inputs[k].data_ptr() for k in g],
                                         [outputs[k].data_ptr() for k in g], n, code,
-                                        _current_stream(dev.index), ALGOS[algo],
+                                        _current_stream(dev.index) if stream is None else stream, ALGOS[algo],
                                         1.0 / self.world if op == "avg" else 1.0)
         return outputs
 

@@ -26,6 +26,13 @@ tuner's size sweep vs RCCL, the straggler-tolerant kernel, all-to-all / all-gath
 reduce-scatter, the fused sharded AdamW step, and `dp` = BASELINE configs 4 and 5 (one
 data-parallel step of the ResNet-50 and full Llama-3-8B gradient sets with a GEMM-backed
 synthetic backward overlapped with the bucketed reducer).
+
+At N = 1 the metric's size axis is timed too (benchmarks/sections.py): `latency_vs_size`
+(p50 latency + algbw of every kernel and of `auto`, 8 / 4 / 2 logical ranks in one launch,
+4 KiB .. 256 MiB, each cell validated to one rounding first), `reduce_kernel` (BASELINE
+config 2: 1 GiB fp32 reduce of 2 / 4 / 8 slots vs the copy roofline), `protocol.sizes` (the
+reference's round protocol on the GPU at 40 B / 1 MiB / 64 MiB) and `dp.overlap_rehearsal`
+(config 5 with real 2-rank comm kernels beside the GEMMs, swept over the reducer grid).
 """
 from __future__ import annotations
 
@@ -907,6 +914,13 @@ def main() -> None:
         cancel = C.watchdog_arm(args.dp_timeout, _RESULT_FD if rank == 0 else -1, json.dumps(timed_out) + "\n", 3)
         log(rank, "dp: ResNet-50 / Llama-3-8B data-parallel steps")
         dp = {m: dp_step(comm, m, dev) for m in (("resnet50",) if args.share_device else ("resnet50", "llama3_8b"))}
+        if world == 1 and not args.share_device and not args.no_sizes:
+            # the same steps with REAL comm kernels beside the GEMMs (2 logical ranks per
+            # bucket launch), swept over the reducer's workgroup budget
+            from benchmarks.sections import dp_overlap
+
+            log(rank, "dp.overlap_rehearsal: 2-logical-rank bucket allreduces beside backward")
+            dp["overlap_rehearsal"] = dp_overlap(dev)
         if not cancel():  # the watchdog fired and wrote the line; the process is exiting
             return
         result["dp"] = dp

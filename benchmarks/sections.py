@@ -13,6 +13,11 @@ same HBM, no xGMI):
   reduce_kernel    BASELINE config 2: the reduce_slots kernel over P = 2 / 4 / 8 slots of a
                    1 GiB fp32 buffer (the worker's `reduce`, AllreduceWorker.scala:240-251),
                    TB/s of HBM traffic and the fraction of the same-run copy roofline.
+  dp_overlap       BASELINE config 5's overlap on one GPU with REAL communication: the
+                   bucketed reducer's buckets go through a 2-logical-rank allreduce (this
+                   rank's bucket + a synthetic peer gradient, one launch, on the comm stream)
+                   while the synthetic backward's GEMMs run; swept over the reducer's
+                   workgroup budget, reporting the GEMMs' slowdown and the exposed time.
   protocol_sizes   the reference's master / worker round protocol driving the GPU round
                    engine (PlaneJob: StartAllreduce -> one threshold-kernel launch per worker)
                    at 40 B (the reference's default job: 10 floats, maxChunkSize 2, 101
@@ -25,6 +30,7 @@ rate of back-to-back calls is reported next to it (`wall_us`).
 """
 from __future__ import annotations
 
+import statistics
 import time
 
 import torch
@@ -291,3 +297,141 @@ def protocol_sizes(dev, cases=((40, torch.float32, 2, 101), (1 << 20, torch.bflo
                 job.shutdown()
         res[f"{nbytes}B"] = row
     return res
+
+
+class PairRehearsalComm:
+    """A 2-rank data-parallel communicator on ONE GPU for overlap rehearsals: every bucket
+    allreduce runs the real 2-rank kernel (LocalCluster, both ranks in one launch) over the
+    bucket and a synthetic peer gradient of the same size, on the stream the reducer passes.
+    Both ranks' kernel traffic lands on this GPU, so it contends with compute at about twice
+    one rank's HBM traffic of a real 2-GPU job (and none of it crosses xGMI): an upper bound
+    on the CU / HBM contention a real rank sees."""
+
+    accepts_stream = True
+    world = 2
+
+    def __init__(self, buckets, grid: int, algo: str = "twoshot"):
+        from akka_allreduce_1_amd.parallel import LocalCluster
+
+        big = max(b.nbytes for b in buckets)
+        self.cl = LocalCluster(2, slot_bytes=-(-big // 2) + (1 << 20), grid=grid, timeout_s=20.0)
+        self.algo = algo
+        self.peer = {}
+        for b in buckets:
+            t = b.buffer
+            self.peer[t.data_ptr()] = (fill_uniform(torch.empty_like(t), seed=3 + b.index), torch.empty_like(t))
+
+    def allreduce_(self, t: torch.Tensor, *, op: str = "sum", algo: str = "auto", stream: int | None = None):
+        x1, y1 = self.peer[t.data_ptr()]
+        self.cl.allreduce([t, x1], [t, y1], algo=self.algo if algo == "auto" else algo, op=op, stream=stream)
+        return t
+
+    def check(self):
+        self.cl.check()
+
+
+def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(64, 128, 256, 512)) -> dict:
+    """BASELINE config 5 (and 4) rehearsed on one GPU with real comm kernels beside the GEMMs:
+    per reducer grid (workgroups of one bucket launch, both logical ranks), the step
+    (backward + overlapped bucket allreduces + SGD update), the compute-only step, the
+    backward's own time with comm running beside it (up to the last GEMM on the compute
+    stream) vs without it (gemm_slowdown), and the comm-only time of every bucket."""
+    from akka_allreduce_1_amd.models.grad_sets import gradient_shapes
+    from akka_allreduce_1_amd.parallel import BucketedGradReducer
+    from benchmarks.bench_dp import SyntheticBackward
+
+    out: dict = {"method": "2 logical ranks in one launch per bucket (this rank's bucket + a synthetic peer) "
+                           "on the reducer's comm stream; medians of interleaved steps",
+                 "note": "both ranks' comm traffic lands on this GPU: about 2x the HBM traffic of one rank "
+                         "of a real 2-GPU job (upper bound on contention); no xGMI"}
+    for model in models:
+        row: dict = {}
+        params = bwd = reducer = comm = None
+        try:
+            shapes = gradient_shapes(model)
+            params = [torch.nn.Parameter(torch.zeros(sh, dtype=torch.bfloat16, device=dev)) for _, sh in shapes]
+            big = model == "llama3_8b"
+            steps, warm = (5, 1) if big else (15, 3)
+            kw = dict(bucket_bytes=1 << 30, first_bucket_bytes=64 << 20) if big else dict(bucket_bytes=25 << 20)
+            reducer = BucketedGradReducer(params, _Placeholder(), op="avg", **kw)
+            reducer.remove_hooks()  # the synthetic backward calls the hook itself
+            comm = PairRehearsalComm(reducer.buckets, max(grids))
+            reducer.comm = comm
+            reducer._raw_ok = True
+            bwd = SyntheticBackward(params, 1024, torch.bfloat16, dev)
+            grads = [q.grad for q in params]
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+
+            def overlap():
+                ev[0].record()
+                bwd.run(reducer)
+                ev[1].record()
+                reducer.wait()
+                torch._foreach_add_(params, grads, alpha=-1e-3)
+
+            def compute():
+                ev[0].record()
+                bwd.run(None)
+                ev[1].record()
+                torch._foreach_add_(params, grads, alpha=-1e-3)
+
+            def comm_only():
+                for b in reducer.buckets:
+                    comm.allreduce_(b.buffer, op="avg", stream=reducer._comm_raw)
+                torch.cuda.current_stream(dev).wait_stream(reducer.stream)
+
+            for grid in grids:
+                cell: dict = {}
+                try:
+                    for c in comm.cl.comms:
+                        c.grid = grid
+                    with torch.no_grad():
+                        for fn in (overlap, compute, comm_only):
+                            for _ in range(warm):
+                                fn()
+                        per = {"step": [], "compute": [], "bwd_with_comm": [], "bwd_alone": []}
+                        for _ in range(steps):  # interleaved: clock drift hits both alike
+                            for name, fn, bkey in (("step", overlap, "bwd_with_comm"), ("compute", compute, "bwd_alone")):
+                                torch.cuda.synchronize(dev)
+                                t0 = time.perf_counter()
+                                fn()
+                                torch.cuda.synchronize(dev)
+                                per[name].append((time.perf_counter() - t0) * 1e3)
+                                per[bkey].append(ev[0].elapsed_time(ev[1]))
+                        torch.cuda.synchronize(dev)
+                        t0 = time.perf_counter()
+                        for _ in range(steps):
+                            comm_only()
+                        torch.cuda.synchronize(dev)
+                        comm_ms = (time.perf_counter() - t0) / steps * 1e3
+                    comm.check()
+                    med = {k: statistics.median(v) for k, v in per.items()}
+                    exposed = med["step"] - med["compute"]
+                    cell = {"step_ms": round(med["step"], 3), "compute_ms": round(med["compute"], 3),
+                            "exposed_comm_ms": round(exposed, 3), "comm_only_ms": round(comm_ms, 3),
+                            "bwd_ms_with_comm": round(med["bwd_with_comm"], 3),
+                            "bwd_ms_alone": round(med["bwd_alone"], 3),
+                            "gemm_slowdown": round(med["bwd_with_comm"] / med["bwd_alone"], 3),
+                            "hidden_frac": round(max(0.0, 1 - exposed / comm_ms), 3)}
+                except Exception as e:  # noqa: BLE001
+                    cell["error"] = repr(e)
+                row[f"grid{grid}"] = cell
+            ok = {g: c for g, c in row.items() if "step_ms" in c}
+            if ok:
+                row["best_grid"] = min(ok, key=lambda g: ok[g]["step_ms"])
+            row["buckets"] = f"{len(reducer.buckets)} ({'64 MiB first, 1 GiB after' if big else '25 MiB'})"
+        except Exception as e:  # noqa: BLE001
+            row["error"] = repr(e)
+        finally:
+            del params, bwd, reducer, comm
+            torch.cuda.empty_cache()
+        out[model] = row
+    return out
+
+
+class _Placeholder:
+    """Stands in for the communicator while the reducer lays out its buckets (the rehearsal
+    communicator needs the bucket buffers to build its peer gradients)."""
+
+    world = 2
+    accepts_stream = True

@@ -1078,7 +1078,22 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
   a.scale = scale;
   a.rescale = rescale ? 1 : 0;
   a.min_reduce = std::max(1, f32_threshold_count(thr, W));
-  a.min_complete = f32_threshold_chunks(thc, W, a.nch);
+  // thComplete: the reference's (th * P * nch) when every block has nch chunks; with a short
+  // last block (uneven blocks) the chunks that exist, as the host WorkerCore
+  // counts them (worker_core.cc) - the kernel never counts a chunk past a block's end
+  {
+    int64_t total = 0;
+    bool uniform = true;
+    for (int j = 0; j < W; ++j) {
+      const int64_t bl = std::max<int64_t>(0, std::min<int64_t>(a.block, n - static_cast<int64_t>(j) * a.block));
+      const int64_t nc = ceil_div(bl, a.chunk);
+      total += nc;
+      uniform = uniform && nc == a.nch;
+    }
+    a.min_complete = uniform ? f32_threshold_chunks(thc, W, a.nch)
+                             : std::max(1, f32_threshold_count(thc, static_cast<int>(total)));
+  }
+  a.full = (a.min_reduce >= W && thc >= 1.f) ? 1 : 0;
   a.counts = counts;
   if (spec != nullptr) {
     a.epoch_set = spec->epoch;

@@ -39,6 +39,7 @@ struct CommArgs {
   // threshold kernel (xgmi_threshold.hip); rows = 1 for the other kernels
   int rows;            // S/R slot rows in the slab: row 0 (lock-step kernels) + trows
   int trows;           // threshold lag ring: rows 1..trows (maxLag + 1; 0 = not allocated)
+  int full;            // thReduce = thComplete = 1: every contribution and chunk is taken
   int min_reduce;      // contributions per chunk that complete a reduce (thReduce)
   int64_t min_complete;  // reduced chunks that complete the round (thComplete)
   int32_t* counts;     // optional [P][nch] contributions per output chunk (0 = missing)

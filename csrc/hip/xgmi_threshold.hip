@@ -373,7 +373,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   // whatever the arrival order, so neither the launch snapshot (a grid-wide barrier) nor the
   // output tickets (one device-scope atomic per unit) change the result: both are skipped.
   // Forced rounds still exclude their own force-reduced chunks (reference order).
-  const bool full = a.min_reduce >= P && a.min_complete >= P * a.nch;
+  const bool full = a.full != 0;
   const bool snap = ref && !cold && !full;  // cold rounds are forced from the start: no snapshot
   const bool tickets = !full;
   // work units: S slices per chunk (S = 1: a unit is a chunk). Scatter / gather unit
@@ -384,6 +384,13 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   const int nr = a.nch * S;
   const int64_t sub = split ? a.subchunk : a.chunk;
   const int mine = blockIdx.x < static_cast<unsigned>(nu) ? (nu - 1 - static_cast<int>(blockIdx.x)) / G + 1 : 0;
+  // Chunk c of block j exists: the last block may have fewer chunks than nch (uneven blocks,
+  // SURVEY Q9). A chunk that does not exist is never a reduced chunk of the round: no ticket,
+  // count 0 - the host WorkerCore counts only the chunks that exist.
+  auto exists = [&](int j, int c) -> bool {
+    return clamp_len(clamp_len(a.n - static_cast<int64_t>(j) * a.block, a.block) - static_cast<int64_t>(c) * a.chunk,
+                     a.chunk) > 0;
+  };
   const int nwords = (mine + 63) / 64;
   HostPoll hp;
 
@@ -416,7 +423,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
           const int b = u / S;
           const int c = b / Pm1;
           const int j = (r + 1 + b % Pm1) % P;
-          arr = reached(ld_flag(f2(a, r, row * P + j, c)), epoch);
+          arr = exists(j, c) && reached(ld_flag(f2(a, r, row * P + j, c)), epoch);
           first = u - b * S == 0;  // a split chunk's early arrival is decided by its slice 0
           if (split && first && arr)
             __hip_atomic_store(&a.split_early[static_cast<int64_t>(j) * a.maxch + c], epoch, __ATOMIC_RELAXED,
@@ -601,8 +608,9 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
           sh_mask = mask;
           // reference order: does the own reduced chunk make this round's output? (forced
           // reduces are flushed after the completion; a round complete at launch takes none)
-          int take = 1;
-          if (ref) {
+          const bool real = blen_own - static_cast<int64_t>(c) * a.chunk > 0;
+          int take = real ? 1 : 0;
+          if (ref && real) {
             if (forced || etotal >= static_cast<uint32_t>(a.min_complete))
               take = 0;
             else if (tickets)
@@ -635,7 +643,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
       st_flag(f2c(a, static_cast<int>(threadIdx.x), row * P + r, c), static_cast<uint32_t>(cnt));
     if (threadIdx.x == 0) {
       if (counts) put_count(counts + static_cast<int64_t>(r) * a.nch + c, take ? cnt : 0);
-      if (!ref && tickets) add_ctl(&ctl[3], 1u);
+      if (!ref && tickets && blen_own - static_cast<int64_t>(c) * a.chunk > 0) add_ctl(&ctl[3], 1u);
     }
     publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : f2(a, k, row * P + r, c); }, P, epoch, rel);
   }
@@ -689,6 +697,8 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
           const bool adopt = split && !dec_claim(dec, epoch, deadline, err, &d);
           if (adopt) {  // another slice of this unit decided
             take = (d & kDecTake) ? 1 : 0;
+          } else if (!exists(j, c)) {
+            take = 0;  // past the end of a short last block: not a chunk of the round
           } else if (!tickets) {
             // full thresholds: every reduced chunk that arrives before a force is taken
           } else if (ref) {

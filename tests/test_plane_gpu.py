@@ -148,34 +148,92 @@ def test_straggler_matches_host_worker_core():
         job.shutdown()
 
 
+class _Gate:
+    """A causal straggler: its fetch of round r waits until every other worker's sink has
+    received round r. Its data then arrives strictly after the others completed the round,
+    whatever the host or device speed - a deterministic scenario for both engines."""
+
+    def __init__(self, others: int):
+        import threading
+
+        self.others = others
+        self.cv = threading.Condition()
+        self.seen: dict[int, int] = {}
+
+    def sink(self, it: int) -> None:
+        with self.cv:
+            self.seen[it] = self.seen.get(it, 0) + 1
+            self.cv.notify_all()
+
+    def wait(self, it: int) -> None:
+        with self.cv:
+            assert self.cv.wait_for(lambda: self.seen.get(it, 0) >= self.others, timeout=300), it
+
+
+def _host_outputs_gated(P, n, chunk, th, straggler, rounds):
+    import threading
+
+    system = C.ActorSystem("Host", False)
+    fin = threading.Event()
+    outs = [dict() for _ in range(P)]
+    gate = _Gate(P - 1)
+
+    def src(k):
+        base = np.arange(n, dtype=F) + F(1000 * k)
+
+        def f(req):
+            if k == straggler:
+                gate.wait(req.iteration)
+            return C.AllReduceInput(base + F(req.iteration))
+        return f
+
+    def sink(k):
+        def f(out):
+            outs[k][out.iteration] = (np.asarray(out.data).copy(), list(out.count))
+            if k != straggler:
+                gate.sink(out.iteration)
+        return f
+
+    master = system.master(P, 1.0, th, th, 1, n, rounds - 1, chunk, on_finished=lambda r: fin.set())
+    ws = [system.worker(src(k), sink(k), f"w{k}") for k in range(P)]
+    for w in ws:
+        master.tell(C.MemberUp(w, "worker", ""), None)
+    assert fin.wait(600)
+    system.await_idle(5.0)
+    system.shutdown()
+    return outs
+
+
 def test_fine_chunks_keep_reference_semantics():
     """maxChunkSize below the 1 KiB flag granularity (the reference's default 2-float chunk on
     a 1 M-float vector: 174 763 chunks per block): the plane keeps one flag, count and
-    threshold decision per reference chunk (min_chunk), so a deterministic straggler at
-    th = 2/3 gives bit-identical outputs and counts to the host WorkerCore
+    threshold decision per reference chunk (min_chunk), so a causal straggler at th = 2/3
+    gives bit-identical outputs and counts to the host WorkerCore
     (DataBuffer.scala:12,28-29,69-75; AllreduceWorker.scala:56-57)."""
-    P, n, chunk, rounds = 3, 1 << 20, 2, 3
+    P, n, chunk, rounds = 3, 1 << 20, 2, 2
     th = 2.0 / 3.0
-    straggler, delay = 2, 0.3
+    straggler = 2
     lvl = C.get_log_level()
     C.set_log_level("ERROR")  # the host run logs every outdated 2-float ReduceBlock
     try:
-        host = _host_outputs(P, n, chunk, th, straggler, delay, rounds)
+        host = _host_outputs_gated(P, n, chunk, th, straggler, rounds)
     finally:
         C.set_log_level(lvl)
+    gate = _Gate(P - 1)
 
-    def slow(source):
+    def gated(source):
         def f(req):
-            time.sleep(delay)
+            gate.wait(req.iteration)
             return source(req)
         return f
 
     srcs = [iota_source(n, DEV, torch.float32, 1000.0 * k) for k in range(P)]
-    srcs[straggler] = slow(srcs[straggler])
+    srcs[straggler] = gated(srcs[straggler])
     job = PlaneJob(P, n, max_chunk_size=chunk, th_reduce=th, th_complete=th, max_lag=1, max_round=rounds - 1,
-                   sources=srcs, timeout_s=30.0)
+                   sources=srcs, timeout_s=60.0,
+                   on_output=lambda k, out: gate.sink(out.iteration) if k != straggler else None)
     try:
-        job.run(timeout=180)
+        job.run(timeout=300)
         step, nch = layout(n, P, chunk)
         assert job.planes[0].chunks == nch and job.planes[0].stats.coarsened == 0
         for k in range(P):
@@ -185,6 +243,9 @@ def test_fine_chunks_keep_reference_semantics():
                 assert len(gc) == P * nch
                 assert gc == hc, (k, it, [i for i in range(len(gc)) if gc[i] != hc[i]][:8])
                 np.testing.assert_array_equal(g.float().cpu().numpy(), h, err_msg=f"worker {k} round {it}")
+        # the fast workers completed each round with exactly the two fast blocks
+        g, gc = job.outputs[0][0]
+        assert gc[:2 * nch] == [2] * (2 * nch) and not any(gc[2 * nch:])
     finally:
         job.shutdown()
 
