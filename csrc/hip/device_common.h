@@ -205,20 +205,24 @@ __device__ __forceinline__ Pack16 ld16(const void* p) { return *static_cast<cons
 __device__ __forceinline__ void st16(void* p, const Pack16& v) { *static_cast<Pack16*>(p) = v; }
 
 // ---------------------------------------------------------------------------------
-// Slab reads: `buffer_load ... sc1` bypasses the reading CU's L1. The slab is fine-grained
-// device memory, so its lines may still be held in L2: the consumer's system-scope
-// acquire after the flag poll (wait_flags, fence bit 1, on by default) is what makes the
-// peers' xGMI stores visible - the sc1 load alone is not a substitute for it.
+// Data-plane reads: `buffer_load ... nt` (non-temporal). Like `sc1` it bypasses the reading
+// CU's L1 (MI355X_MICROARCH.md, load flavours), so after the consumer's acquire it reads
+// what the peers' write-through stores left in memory - the acquire (wait_flags, fence bit
+// 1, on by default) is what makes the peers' xGMI stores visible, not the load flavour. As a
+// streaming hint it also keeps one-pass streams from displacing each other in L2: a copy of
+// 256 MiB with nt loads + write-through stores runs 6.77 TB/s vs 5.18 with sc1 or plain loads
+// (tools/store_probe.hip, profiles/round3/store_probe.json), into fine-grained and coarse
+// memory alike. Every slab read AND every read of a kernel's own input stream uses it.
 // Descriptor built from wave-uniform values only (cdna_hip_programming.md T8/T20).
 // ---------------------------------------------------------------------------------
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-constexpr int kAuxSc1 = 16;
+constexpr int kAuxNt = 2;  // CPol NT (slc)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), static_cast<short>(0), 0x7fffffff, 0x00020000);
 }
-__device__ __forceinline__ Pack16 ld16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, kAuxSc1);
+__device__ __forceinline__ Pack16 ld16_nt(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, kAuxNt);
 }
 // Slab writes: `buffer_store ... sc0 sc1` = system-coherent write-through. A drained
 // (`s_waitcnt vmcnt(0)`) write-through store has reached memory, so the flag that follows
@@ -261,18 +265,18 @@ __device__ __forceinline__ void copy_scalar_wt<F16>(__amdgpu_buffer_rsrc_t r, co
 }
 
 template <class E>
-__device__ __forceinline__ float ld_scalar_sc1(__amdgpu_buffer_rsrc_t r, int64_t i);
+__device__ __forceinline__ float ld_scalar_nt(__amdgpu_buffer_rsrc_t r, int64_t i);
 template <>
-__device__ __forceinline__ float ld_scalar_sc1<F32>(__amdgpu_buffer_rsrc_t r, int64_t i) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(i * 4), 0, kAuxSc1));
+__device__ __forceinline__ float ld_scalar_nt<F32>(__amdgpu_buffer_rsrc_t r, int64_t i) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(i * 4), 0, kAuxNt));
 }
 template <>
-__device__ __forceinline__ float ld_scalar_sc1<BF16>(__amdgpu_buffer_rsrc_t r, int64_t i) {
-  return bf16_to_f32(__builtin_amdgcn_raw_buffer_load_b16(r, static_cast<int>(i * 2), 0, kAuxSc1));
+__device__ __forceinline__ float ld_scalar_nt<BF16>(__amdgpu_buffer_rsrc_t r, int64_t i) {
+  return bf16_to_f32(__builtin_amdgcn_raw_buffer_load_b16(r, static_cast<int>(i * 2), 0, kAuxNt));
 }
 template <>
-__device__ __forceinline__ float ld_scalar_sc1<F16>(__amdgpu_buffer_rsrc_t r, int64_t i) {
-  return f16_to_f32(__builtin_amdgcn_raw_buffer_load_b16(r, static_cast<int>(i * 2), 0, kAuxSc1));
+__device__ __forceinline__ float ld_scalar_nt<F16>(__amdgpu_buffer_rsrc_t r, int64_t i) {
+  return f16_to_f32(__builtin_amdgcn_raw_buffer_load_b16(r, static_cast<int>(i * 2), 0, kAuxNt));
 }
 
 // ---------------------------------------------------------------------------------

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <map>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -70,8 +71,17 @@ class DevicePayload final : public PayloadStorage {
   const ReadyEvent& ready() const { return ready_; }
   // Block the host until the producing operation finished.
   void wait_host() const;
+  // Pooled round outputs (xgmi_plane.cc): a buffer whose memory was handed to another stream
+  // (a torch tensor view, or a native consumer enqueuing GPU work on its own stream) is
+  // returned to the pool only behind the default stream; one never exported is reused at
+  // once on the producer's stream. to_py marks it; native consumers call mark_exported().
+  void set_export_flag(std::shared_ptr<std::atomic<bool>> f) { exported_ = std::move(f); }
+  void mark_exported() const {
+    if (exported_) exported_->store(true, std::memory_order_relaxed);
+  }
 
  private:
+  std::shared_ptr<std::atomic<bool>> exported_;
   std::shared_ptr<void> mem_;
   size_t off_, n_;
   int device_;

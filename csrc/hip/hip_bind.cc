@@ -71,6 +71,7 @@ py::object device_payload_to_py(const Payload& p) {
   auto* d = dynamic_cast<const DevicePayload*>(p.get());
   if (!d) return py::none();
   d->wait_host();  // torch consumes it on its own stream
+  d->mark_exported();  // a pooled round output returns to its pool behind torch's stream
   auto* ctx = new ExportCtx{p, {static_cast<int64_t>(p->size())}, {1}};
   auto* mt = new DLManagedTensor{};
   mt->dl_tensor.data = const_cast<void*>(d->bytes());
@@ -234,6 +235,7 @@ void bind_hip(py::module_& m) {
       .def_readonly("bytes", &XgmiPlaneStats::bytes)
       .def_readonly("completed", &XgmiPlaneStats::completed)
       .def_readonly("coarsened", &XgmiPlaneStats::coarsened)
+      .def_readonly("pool_grown", &XgmiPlaneStats::pool_grown)
       .def_readonly("peer_maps", &XgmiPlaneStats::peer_maps);
   py::class_<XgmiRoundPlane, RoundPlane, std::shared_ptr<XgmiRoundPlane>>(h, "XgmiRoundPlane")
       .def_property_readonly("stats", &XgmiRoundPlane::stats)

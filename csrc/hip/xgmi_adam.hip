@@ -109,11 +109,11 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a)
           if constexpr (PT > 0) {
             Pack16 g[PT];
 #pragma unroll
-            for (int s = 0; s < PT; ++s) g[s] = ld16_sc1(src.rsrc(s), static_cast<uint32_t>(i * 16));
+            for (int s = 0; s < PT; ++s) g[s] = ld16_nt(src.rsrc(s), static_cast<uint32_t>(i * 16));
 #pragma unroll
             for (int s = 0; s < PT; ++s) acc[w].add(g[s]);
           } else {
-            for (int s = 0; s < P; ++s) acc[w].add(ld16_sc1(src.rsrc(s), static_cast<uint32_t>(i * 16)));
+            for (int s = 0; s < P; ++s) acc[w].add(ld16_nt(src.rsrc(s), static_cast<uint32_t>(i * 16)));
           }
 #pragma unroll
           for (int e = 0; e < EL / 4; ++e) {
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a)
       const int64_t t = npk * EL + threadIdx.x;
       if (t < len) {
         float g = 0.f;
-        for (int s = 0; s < P; ++s) g += ld_scalar_sc1<E>(src.rsrc(s), t);
+        for (int s = 0; s < P; ++s) g += ld_scalar_nt<E>(src.rsrc(s), t);
         const float pv = adamw(g * a.scale, sp + t, sm + t, sv + t, a);
         Scalar<E>::store(own_out, t, pv);
         for (int k = 0; k < P; ++k)

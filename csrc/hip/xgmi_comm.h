@@ -152,6 +152,9 @@ class XgmiComm {
     const uint32_t* host_force = nullptr;  // device-visible pinned host word (may be null)
     const uint32_t* host_abort = nullptr;  // rounds <= this epoch are abandoned (may be null)
     uint32_t* err_out = nullptr;           // device-visible word the round's error word is copied to
+    // device-visible pinned word the round's last workgroup sets to the round epoch once every
+    // workgroup is done (a completion HINT for the host: it still confirms with the event)
+    uint32_t* done_out = nullptr;
     int32_t* counts_host = nullptr;        // device-visible pinned copy of `counts`, written at round end
     // the rank's scratch for split chunks (zeroed per membership; split_scratch_bytes(P));
     // null: one workgroup per chunk

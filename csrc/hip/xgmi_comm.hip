@@ -156,13 +156,13 @@ template <class E>
 __device__ __forceinline__ void push_to_peers(const CommArgs& a, int P, int r, int64_t slot_off, const char* src,
                                               int64_t len) {
   const int64_t npk = len / E::ELEMS;
-  const Pack16* s = reinterpret_cast<const Pack16*>(src);
+  const __amdgpu_buffer_rsrc_t rs = slab_rsrc(src);
   int64_t i = threadIdx.x;
   constexpr int U = 2;
   for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
     Pack16 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = s[i + u * kCommThreads];
+    for (int u = 0; u < U; ++u) v[u] = ld16_nt(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
     for (int k = 0; k < P; ++k) {
       if (k == r) continue;
       const __amdgpu_buffer_rsrc_t rd = slab_rsrc(a.base[k] + slot_off);
@@ -171,7 +171,7 @@ __device__ __forceinline__ void push_to_peers(const CommArgs& a, int P, int r, i
     }
   }
   for (; i < npk; i += kCommThreads) {
-    const Pack16 v = s[i];
+    const Pack16 v = ld16_nt(rs, static_cast<uint32_t>(i * 16));
     for (int k = 0; k < P; ++k)
       if (k != r) st16_wt(slab_rsrc(a.base[k] + slot_off), static_cast<uint32_t>(i * 16), v);
   }
@@ -247,7 +247,7 @@ __device__ __forceinline__ void copy_slab_fwd(char* out, char* next_slab, const 
   for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
     Pack16 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = ld16_sc1(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
+    for (int u = 0; u < U; ++u) v[u] = ld16_nt(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
 #pragma unroll
     for (int u = 0; u < U; ++u) st16_wt(ro, static_cast<uint32_t>((i + u * kCommThreads) * 16), v[u]);
     if (fwd) {
@@ -256,13 +256,13 @@ __device__ __forceinline__ void copy_slab_fwd(char* out, char* next_slab, const 
     }
   }
   for (; i < npk; i += kCommThreads) {
-    const Pack16 v = ld16_sc1(rs, static_cast<uint32_t>(i * 16));
+    const Pack16 v = ld16_nt(rs, static_cast<uint32_t>(i * 16));
     st16_wt(ro, static_cast<uint32_t>(i * 16), v);
     if (fwd) st16_wt(rn, static_cast<uint32_t>(i * 16), v);
   }
   const int64_t t = npk * E::ELEMS + threadIdx.x;
   if (t < len) {
-    const float x = ld_scalar_sc1<E>(rs, t);
+    const float x = ld_scalar_nt<E>(rs, t);
     st_scalar_wt<E>(ro, t, x);
     if (fwd) st_scalar_wt<E>(rn, t, x);
   }
@@ -291,10 +291,10 @@ __device__ __forceinline__ void ring_hop(const char* partial, const char* in, ch
     for (int u = 0; u < U; ++u) {
       if (u >= nu) break;
       const int64_t i = i0 + u * kCommThreads;
-      xv[u] = ld16_sc1(ri, static_cast<uint32_t>(i * 16));
+      xv[u] = ld16_nt(ri, static_cast<uint32_t>(i * 16));
       if (has_p) {
 #pragma unroll
-        for (int h = 0; h < NP; ++h) pv[u][h] = ld16_sc1(rp, static_cast<uint32_t>((i * NP + h) * 16));
+        for (int h = 0; h < NP; ++h) pv[u][h] = ld16_nt(rp, static_cast<uint32_t>((i * NP + h) * 16));
       }
     }
 #pragma unroll
@@ -331,9 +331,9 @@ __device__ __forceinline__ void ring_hop(const char* partial, const char* in, ch
   for (; i < npk; i += kCommThreads) step(i, 1);
   const int64_t t = npk * E::ELEMS + threadIdx.x;
   if (t < len) {  // ragged tail: one element per lane
-    float acc = (has_p ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rp, static_cast<int>(t * 4), 0, kAuxSc1))
+    float acc = (has_p ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rp, static_cast<int>(t * 4), 0, kAuxNt))
                        : 0.f) +
-                ld_scalar_sc1<E>(ri, t);
+                ld_scalar_nt<E>(ri, t);
     if (fwd_f32 != nullptr) {
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc), rf, static_cast<int>(t * 4), 0, kAuxWt);
     } else {
@@ -1060,6 +1060,13 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
       ceil_div(static_cast<int64_t>(a.nch) * a.sub, gx) > kThresholdSnapChunks)
     throw std::invalid_argument("round: more than " + std::to_string(kThresholdSnapChunks) +
                                 " chunks per workgroup at thresholds < 1 (the arrival-order snapshot)");
+  // unsplit: scatter `sgroup` consecutive chunks per unit so that the (P - 1) x groups units
+  // fit the grid once (at most 64: one flag lane each)
+  a.sgroup = 1;
+  if (a.sub <= 1 && W > 1) {
+    const int per = std::max(1, gx / (W - 1));  // groups per destination block
+    a.sgroup = static_cast<int>(std::min<int64_t>(64, std::max<int64_t>(1, ceil_div(a.nch, per))));
+  }
   if (ceil_div(static_cast<int64_t>(W - 1) * a.nch * a.sub, gx) > kThresholdGatherUnits)
     throw std::invalid_argument("allreduce_threshold: more than " + std::to_string(kThresholdGatherUnits) +
                                 " gather units per workgroup (too many chunks for the grid)");
@@ -1102,6 +1109,7 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
     a.hforce = spec->host_force;
     a.habort = spec->host_abort;
     a.err_out = spec->err_out;
+    a.done_out = spec->done_out;
     a.counts_host = counts != nullptr ? spec->counts_host : nullptr;
   }
   a.delay_rank = -1;

@@ -53,6 +53,7 @@ struct CommArgs {
   const uint32_t* hforce;
   const uint32_t* habort;  // pinned host word: rounds <= this epoch are abandoned (threshold kernel)
   uint32_t* err_out;  // optional: the round's error word, written by the last workgroup (pinned host)
+  uint32_t* done_out;  // optional: set to the epoch by the last workgroup after its release (pinned host)
   // optional: where the last workgroup copies `counts` (P x nch int32, pinned host) once the
   // round is done - every workgroup writes its counts to device memory (`counts`), so no
   // unit waits on a PCIe write acknowledgement
@@ -75,6 +76,7 @@ struct CommArgs {
   // split_dec: 64-bit decision words, [c] own reduce chunk c, [maxch + j * maxch + c] gather
   // unit (j, c); split_ctr: slice counters, [c] reduce, [maxch + j * maxch + c] scatter;
   // split_early: [j * maxch + c] = epoch when gather unit (j, c) was in at launch
+  int sgroup;  // threshold kernel, unsplit chunks: chunks per scatter unit (one copy, one release)
   uint64_t* split_dec;
   uint32_t* split_ctr;
   uint32_t* split_early;
@@ -149,23 +151,23 @@ constexpr int kCopyU = MXAR_COPY_U;
 template <class E>
 __device__ __forceinline__ void copy_to_slab(char* slab_dst, const char* src, int64_t len) {
   const int64_t npk = len / E::ELEMS;
-  const Pack16* s = reinterpret_cast<const Pack16*>(src);
+  const __amdgpu_buffer_rsrc_t rs = slab_rsrc(src);  // the input stream: nt loads (device_common.h)
   const __amdgpu_buffer_rsrc_t rd = slab_rsrc(slab_dst);
   int64_t i = threadIdx.x;
   constexpr int U = kCopyU;
   for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
     Pack16 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = s[i + u * kCommThreads];
+    for (int u = 0; u < U; ++u) v[u] = ld16_nt(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
 #pragma unroll
     for (int u = 0; u < U; ++u) st16_wt(rd, static_cast<uint32_t>((i + u * kCommThreads) * 16), v[u]);
   }
-  for (; i < npk; i += kCommThreads) st16_wt(rd, static_cast<uint32_t>(i * 16), s[i]);
+  for (; i < npk; i += kCommThreads) st16_wt(rd, static_cast<uint32_t>(i * 16), ld16_nt(rs, static_cast<uint32_t>(i * 16)));
   const int64_t t = npk * E::ELEMS + threadIdx.x;
   if (t < len) copy_scalar_wt<E>(rd, src, t);
 }
 
-// Copy len elements out of a (fine-grained) slab with sc1 loads - after the caller's
+// Copy len elements out of a (fine-grained) slab with nt loads - after the caller's
 // acquire - 4 packs in flight per lane.
 template <class E>
 __device__ __forceinline__ void copy_from_slab(char* dst, const char* slab_src, int64_t len) {
@@ -177,17 +179,17 @@ __device__ __forceinline__ void copy_from_slab(char* dst, const char* slab_src, 
   for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
     Pack16 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = ld16_sc1(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
+    for (int u = 0; u < U; ++u) v[u] = ld16_nt(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
 #pragma unroll
     for (int u = 0; u < U; ++u) st16_wt(rd, static_cast<uint32_t>((i + u * kCommThreads) * 16), v[u]);
   }
-  for (; i < npk; i += kCommThreads) st16_wt(rd, static_cast<uint32_t>(i * 16), ld16_sc1(rs, static_cast<uint32_t>(i * 16)));
+  for (; i < npk; i += kCommThreads) st16_wt(rd, static_cast<uint32_t>(i * 16), ld16_nt(rs, static_cast<uint32_t>(i * 16)));
   const int64_t t = npk * E::ELEMS + threadIdx.x;
-  if (t < len) st_scalar_wt<E>(rd, t, ld_scalar_sc1<E>(rs, t));
+  if (t < len) st_scalar_wt<E>(rd, t, ld_scalar_nt<E>(rs, t));
 }
 
 // Reduction sources: source s is at slab0 + s * stride, except source `own` (if >= 0),
-// which is the rank's own input. Every source is read with sc1 buffer loads through a
+// which is the rank's own input. Every source is read with nt buffer loads through a
 // descriptor chosen by a scalar select, so the P loads of a pack issue back to back
 // with no per-source branch (and the own input is simply L1-bypassing).
 struct RedSrc {
@@ -220,7 +222,7 @@ __device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, in
 #pragma unroll
       for (int s = 0; s < PT; ++s)
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[s][u] = ld16_sc1(rs[s], static_cast<uint32_t>((i + u * kCommThreads) * 16));
+        for (int u = 0; u < U; ++u) v[s][u] = ld16_nt(rs[s], static_cast<uint32_t>((i + u * kCommThreads) * 16));
       Acc<E> acc[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) acc[u].zero();
@@ -252,7 +254,7 @@ __device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, in
   for (; i < npk; i += kCommThreads) {
     Acc<E> acc;
     acc.zero();
-    for (int s = 0; s < P; ++s) acc.add(ld16_sc1(src.rsrc(s), static_cast<uint32_t>(i * 16)));
+    for (int s = 0; s < P; ++s) acc.add(ld16_nt(src.rsrc(s), static_cast<uint32_t>(i * 16)));
     if (scale != 1.f) acc.scale(scale);
     const Pack16 o = acc.pack();
     for (int k = 0; k < ndst; ++k) {
@@ -267,7 +269,7 @@ __device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, in
   const int64_t t = npk * E::ELEMS + threadIdx.x;
   if (t < len) {
     float acc = 0.f;
-    for (int s = 0; s < P; ++s) acc += ld_scalar_sc1<E>(src.rsrc(s), t);
+    for (int s = 0; s < P; ++s) acc += ld_scalar_nt<E>(src.rsrc(s), t);
     acc *= scale;
     for (int k = 0; k < ndst; ++k) {
       char* d = dst(k);

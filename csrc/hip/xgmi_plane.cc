@@ -198,7 +198,10 @@ XgmiRoundPlane::~XgmiRoundPlane() {
     std::lock_guard<std::mutex> g(rel_->mu);
     if (!rel_->ptrs.empty()) (void)hipStreamSynchronize(nullptr);
     for (void* q : rel_->ptrs) (void)hipFree(q);
+    for (void* q : rel_->free) (void)hipFree(q);
     rel_->ptrs.clear();
+    rel_->free.clear();
+    rel_->bytes = 0;  // outputs still held by users are freed stream-ordered when dropped
   }
   if (rel_ev_) (void)hipEventDestroy(rel_ev_);
   comm_.reset();
@@ -260,6 +263,71 @@ std::shared_ptr<void> XgmiRoundPlane::buffer(size_t bytes, bool user_visible) {
   });
 }
 
+std::shared_ptr<void> XgmiRoundPlane::out_buffer(size_t bytes, std::shared_ptr<std::atomic<bool>>* exported) {
+  bytes = std::max<size_t>(bytes, 256);
+  void* p = nullptr;
+  {
+    std::lock_guard<std::mutex> g(rel_->mu);
+    if (rel_->bytes == bytes && !rel_->free.empty()) {
+      p = rel_->free.back();
+      rel_->free.pop_back();
+    }
+  }
+  if (p == nullptr) {
+    hip_check(hipMallocAsync(&p, bytes, stream_), "hipMallocAsync(plane output)");
+    st_.pool_grown++;
+  }
+  auto flag = std::make_shared<std::atomic<bool>>(false);
+  *exported = flag;
+  const hipStream_t s = stream_;
+  std::weak_ptr<bool> alive = alive_;
+  std::weak_ptr<ReleaseQ> rq = rel_;
+  const bool ordered = o_.order_release;
+  return std::shared_ptr<void>(p, [s, alive, rq, flag, bytes, ordered](void* q) {
+    auto a = alive.lock();
+    auto r = rq.lock();
+    if (a && *a && r) {
+      std::lock_guard<std::mutex> g(r->mu);
+      if (r->bytes == bytes) {
+        // exported: another stream may still read it - reusable only behind the default
+        // stream (flush_releases at the next launch); otherwise at once, on the plane stream
+        if (ordered && flag->load(std::memory_order_relaxed))
+          r->ptrs.push_back(q);
+        else
+          r->free.push_back(q);
+        return;
+      }
+      // an output of an older layout: freed, stream-ordered behind whoever may still read it
+      (void)hipFreeAsync(q, ordered && flag->load() ? nullptr : s);
+      return;
+    }
+    // the plane is gone: stream-ordered on the default stream - hipFree would wait for every
+    // kernel on the device, e.g. another plane's round spinning on its peers
+    (void)hipFreeAsync(q, nullptr);
+  });
+}
+
+void XgmiRoundPlane::reset_pool(size_t bytes) {
+  bytes = std::max<size_t>(bytes, 256);
+  std::vector<void*> fr, pend;
+  {
+    std::lock_guard<std::mutex> g(rel_->mu);
+    if (rel_->bytes == bytes) return;
+    fr.swap(rel_->free);
+    pend.swap(rel_->ptrs);
+    rel_->bytes = bytes;
+  }
+  for (void* q : fr) (void)hipFreeAsync(q, stream_);
+  for (void* q : pend) (void)hipFreeAsync(q, nullptr);
+  // about 3 outputs are live at once (the round in flight, the one a sink holds, the one
+  // being released): grow the pool now - growing it on the round path costs ~8 ms per
+  // 256 MiB buffer (profiles/round2/sync_probe.md)
+  std::vector<void*> warm(3, nullptr);
+  for (void*& w : warm) hip_check(hipMallocAsync(&w, bytes, stream_), "hipMallocAsync(pool)");
+  std::lock_guard<std::mutex> g(rel_->mu);
+  for (void* w : warm) rel_->free.push_back(w);
+}
+
 void XgmiRoundPlane::flush_releases() {
   std::vector<void*> ptrs;
   {
@@ -267,12 +335,13 @@ void XgmiRoundPlane::flush_releases() {
     ptrs.swap(rel_->ptrs);
   }
   if (ptrs.empty()) return;
-  // one event for every output released since the last launch: the frees (and so the reuse
-  // of those blocks by this launch's allocations) come after everything the default stream
-  // held at this point - e.g. a sink's clone of the round output
+  // one event for every exported output released since the last launch: their reuse by
+  // this and later launches comes after everything the default stream held at this point -
+  // e.g. a sink's clone of the round output
   hip_check(hipEventRecord(rel_ev_, nullptr), "hipEventRecord(release)");
   hip_check(hipStreamWaitEvent(stream_, rel_ev_, 0), "hipStreamWaitEvent(release)");
-  for (void* q : ptrs) (void)hipFreeAsync(q, stream_);
+  std::lock_guard<std::mutex> g(rel_->mu);
+  for (void* q : ptrs) rel_->free.push_back(q);
 }
 
 void XgmiRoundPlane::set_done(DoneFn fn) {
@@ -385,12 +454,7 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
   // Grow the stream-ordered pool now for the rounds' output buffers (an output is released
   // one launch after its sink dropped it, so ~3 are live at once): growing it in the round
   // path costs ~8 ms per 256 MiB buffer (profiles/round2/sync_probe.md) - paid here instead.
-  {
-    const size_t bytes = static_cast<size_t>(cfg.dataSize) * static_cast<size_t>(dtype_size(o_.dtype));
-    void* warm[3] = {nullptr, nullptr, nullptr};
-    for (void*& w : warm) hip_check(hipMallocAsync(&w, std::max<size_t>(bytes, 256), stream_), "hipMallocAsync(warm)");
-    for (void* w : warm) hip_check(hipFreeAsync(w, stream_), "hipFreeAsync(warm)");
-  }
+  reset_pool(static_cast<size_t>(cfg.dataSize) * static_cast<size_t>(dtype_size(o_.dtype)));
   comm_->publish_progress(cfg.roundBase, stream_);
   hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize(publish progress)");
   if (static_cast<size_t>(P) * nch_ + 4 > ring_stride_) throw ProtocolError("xgmi plane: counts ring too small");
@@ -430,7 +494,7 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   rec.epoch = cfg_.epoch;
   rec.cold = cold;
   flush_releases();
-  rec.out = buffer(static_cast<size_t>(n * es), o_.order_release);
+  rec.out = out_buffer(static_cast<size_t>(n * es), &rec.exported);
   {
     std::unique_lock<std::mutex> lk(mu_);
     rec.slot = take_slot(lk);
@@ -467,6 +531,7 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   }
   XgmiComm::RoundSpec spec;
   spec.epoch = epoch_of(round);
+  rec.round_epoch = spec.epoch;
   spec.block = block_;
   spec.chunk = chunk_;
   spec.cold = cold;
@@ -474,6 +539,7 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   spec.host_force = hforce_dev_;
   spec.host_abort = hforce_dev_ + 1;
   spec.err_out = reinterpret_cast<uint32_t*>(slot_dev + ring_stride_ - 1);
+  spec.done_out = reinterpret_cast<uint32_t*>(slot_dev + ring_stride_ - 2);
   spec.counts_host = slot_dev;  // the kernel counts into HBM and copies once, at round end
   if (o_.split) {
     spec.split_scratch = split_mem_;
@@ -543,13 +609,23 @@ void XgmiRoundPlane::completion_loop() {
     hipError_t e;
     {
       TraceScope span("plane", [&] { return std::make_pair("wait r" + std::to_string(rec.round), std::string()); });
-      // poll first: a blocking wait sleeps on an interrupt, whose wake-up adds tens of
-      // microseconds to every round; this thread has nothing else to do meanwhile
+      // Poll first: a blocking wait sleeps on an interrupt, whose wake-up adds tens of
+      // microseconds to every round. The kernel's last workgroup sets the slot's pinned done
+      // word to the round epoch (a plain load of host memory: no runtime call, so this thread
+      // does not contend with the workers' launches for the HIP runtime's locks while the
+      // round runs); the round's event then confirms it before the output is handed on.
       const auto t0 = std::chrono::steady_clock::now();
+      const auto budget = std::chrono::microseconds(o_.spin_us);
+      const volatile uint32_t* done = reinterpret_cast<const volatile uint32_t*>(
+          ring_ + static_cast<size_t>(rec.slot) * ring_stride_ + ring_stride_ - 2);
+      const uint32_t want = static_cast<uint32_t>(rec.round_epoch);
+      while (*done != want && std::chrono::steady_clock::now() - t0 < budget) {
+        for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+      }
       for (;;) {
         e = hipEventQuery(rec.ev);
         if (e != hipErrorNotReady) break;
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(o_.spin_us)) {
+        if (std::chrono::steady_clock::now() - t0 > budget) {
           e = hipEventSynchronize(rec.ev);
           break;
         }
@@ -574,8 +650,12 @@ void XgmiRoundPlane::completion_loop() {
     const uint32_t err = static_cast<uint32_t>(host[ring_stride_ - 1]);
     res.error = (err & ~err_seen_) | (e != hipSuccess ? 0x80000000u : 0u);
     err_seen_ |= err;
-    res.data = std::make_shared<DevicePayload>(rec.out, 0, static_cast<size_t>(cfg_.dataSize), o_.device, nullptr,
-                                               nullptr, static_cast<int>(o_.dtype));
+    {
+      auto dp = std::make_shared<DevicePayload>(rec.out, 0, static_cast<size_t>(cfg_.dataSize), o_.device, nullptr,
+                                                nullptr, static_cast<int>(o_.dtype));
+      dp->set_export_flag(rec.exported);
+      res.data = std::move(dp);
+    }
     rec.input.reset();
     rec.staging.reset();
     {

@@ -25,6 +25,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <map>
@@ -64,6 +65,7 @@ struct XgmiPlaneOptions {
 
 struct XgmiPlaneStats {
   uint64_t launches = 0, cold = 0, forced = 0, bytes = 0, completed = 0, coarsened = 0, peer_maps = 0;
+  uint64_t pool_grown = 0;  // round outputs the pool had to allocate (none after warm-up in steady state)
 };
 
 class XgmiRoundPlane final : public RoundPlane {
@@ -102,6 +104,8 @@ class XgmiRoundPlane final : public RoundPlane {
     int round = 0;
     int64_t epoch = 0;
     std::shared_ptr<void> out, staging;
+    std::shared_ptr<std::atomic<bool>> exported;  // the output's export flag (out_buffer)
+    uint32_t round_epoch = 0;                      // the kernel's round epoch (done word)
     Payload input;
     hipEvent_t ev = nullptr;
     int slot = 0;
@@ -115,6 +119,11 @@ class XgmiRoundPlane final : public RoundPlane {
   // last holder drops it): the launch path never calls a device-synchronising allocator
   // while a peer's kernel may be spinning on this worker's next launch.
   std::shared_ptr<void> buffer(size_t bytes, bool user_visible = false);
+  // A round output from the plane's pool (no allocator call on the round path): released
+  // to the pool directly, or - once exported to another stream (DevicePayload::
+  // mark_exported) - at the next launch behind the default stream (flush_releases).
+  std::shared_ptr<void> out_buffer(size_t bytes, std::shared_ptr<std::atomic<bool>>* exported);
+  void reset_pool(size_t bytes);
   int take_slot(std::unique_lock<std::mutex>& lk);
   void completion_loop();
 
@@ -163,7 +172,9 @@ class XgmiRoundPlane final : public RoundPlane {
   // (work a sink queued on torch's default stream may still read them; see buffer()).
   struct ReleaseQ {
     std::mutex mu;
-    std::vector<void*> ptrs;
+    std::vector<void*> ptrs;  // released after an export: reusable once behind the default stream
+    std::vector<void*> free;  // reusable now (ordered on the plane stream)
+    size_t bytes = 0;         // size of the pooled output buffers
   };
   std::shared_ptr<ReleaseQ> rel_ = std::make_shared<ReleaseQ>();
   hipEvent_t rel_ev_ = nullptr;

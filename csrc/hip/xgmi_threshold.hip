@@ -149,7 +149,7 @@ __device__ __forceinline__ void copy_out(char* dst, const char* slab_src, int64_
   }
   const __amdgpu_buffer_rsrc_t rs = slab_rsrc(slab_src);
   const __amdgpu_buffer_rsrc_t rd = slab_rsrc(dst);
-  for (int64_t t = threadIdx.x; t < len; t += kCommThreads) st_scalar_wt<E>(rd, t, ld_scalar_sc1<E>(rs, t));
+  for (int64_t t = threadIdx.x; t < len; t += kCommThreads) st_scalar_wt<E>(rd, t, ld_scalar_nt<E>(rs, t));
 }
 
 template <class E>
@@ -177,7 +177,7 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
     for (int64_t t = threadIdx.x; t < len; t += kCommThreads) {
       float acc = 0.f;
       for (int s = 0; s < P; ++s)
-        if ((mask >> s) & 1u) acc += ld_scalar_sc1<E>(slab_rsrc(s == r ? own_in : S + s * slot), t);
+        if ((mask >> s) & 1u) acc += ld_scalar_nt<E>(slab_rsrc(s == r ? own_in : S + s * slot), t);
       acc *= scale;
       for (int k = 0; k < P; ++k) {
         if (k == r) {
@@ -201,7 +201,7 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
       const __amdgpu_buffer_rsrc_t rs = slab_rsrc(s == r ? own_in : S + s * slot);
       Pack16 v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = ld16_sc1(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
+      for (int u = 0; u < U; ++u) v[u] = ld16_nt(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
 #pragma unroll
       for (int u = 0; u < U; ++u) acc[u].add(v[u]);
     }
@@ -228,7 +228,7 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
     Acc<E> acc;
     acc.zero();
     for (int s = 0; s < P; ++s)
-      if ((mask >> s) & 1u) acc.add(ld16_sc1(slab_rsrc(s == r ? own_in : S + s * slot), static_cast<uint32_t>(i * 16)));
+      if ((mask >> s) & 1u) acc.add(ld16_nt(slab_rsrc(s == r ? own_in : S + s * slot), static_cast<uint32_t>(i * 16)));
     if (scale != 1.f) acc.scale(scale);
     const Pack16 o = acc.pack();
     for (int k = 0; k < P; ++k) {
@@ -244,7 +244,7 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
   if (t < len) {
     float acc = 0.f;
     for (int s = 0; s < P; ++s)
-      if ((mask >> s) & 1u) acc += ld_scalar_sc1<E>(slab_rsrc(s == r ? own_in : S + s * slot), t);
+      if ((mask >> s) & 1u) acc += ld_scalar_nt<E>(slab_rsrc(s == r ? own_in : S + s * slot), t);
     acc *= scale;
     for (int k = 0; k < P; ++k) {
       char* d = k == r ? own_out : a.base[k] + roff;
@@ -519,20 +519,42 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   const bool void_round = sh_flag != 0;  // abandoned before the exchange: no peer writes
   ps.mark(1);
 
-  // Phase 1 - ScatterBlock into the owners' row slots (a cold or void round sends nothing)
+  // Phase 1 - ScatterBlock into the owners' row slots (a cold or void round sends nothing).
+  // Unsplit chunks travel in groups of `sgroup` consecutive chunks of one destination block:
+  // one contiguous copy and ONE release for the group, then one flag per chunk (each chunk
+  // stays its own arrival for the owner's threshold decision). Small chunks otherwise cost a
+  // fence each and the scatter ran at a quarter of the two-shot's rate (phase stamps,
+  // profiles/round3/README.md).
   if (!cold && !void_round) {
-    for (int u = blockIdx.x; u < nu; u += G) {
-      const int b = u / S;
-      const int c = b / Pm1;
-      const int j = (r + 1 + b % Pm1) % P;
-      const int64_t bstart = static_cast<int64_t>(j) * a.block;
-      const int64_t cstart = static_cast<int64_t>(c) * a.chunk + static_cast<int64_t>(u - b * S) * sub;
-      const int64_t len = clamp_len(clamp_len(clamp_len(a.n - bstart, a.block) - c * a.chunk, a.chunk) -
-                                        (cstart - c * a.chunk),
-                                    sub);
-      if (len > 0) copy_in<E>(a.base[j] + rowS + r * slot + cstart * es, in + (bstart + cstart) * es, len);
-      if (split && !last_slice(&a.split_ctr[a.maxch + static_cast<int64_t>(j) * a.maxch + c], S, &sh_last)) continue;
-      publish_flags([&](int) { return f1(a, j, row * P + r, c); }, 1, epoch, rel);
+    if (split) {
+      for (int u = blockIdx.x; u < nu; u += G) {
+        const int b = u / S;
+        const int c = b / Pm1;
+        const int j = (r + 1 + b % Pm1) % P;
+        const int64_t bstart = static_cast<int64_t>(j) * a.block;
+        const int64_t cstart = static_cast<int64_t>(c) * a.chunk + static_cast<int64_t>(u - b * S) * sub;
+        const int64_t len = clamp_len(clamp_len(clamp_len(a.n - bstart, a.block) - c * a.chunk, a.chunk) -
+                                          (cstart - c * a.chunk),
+                                      sub);
+        if (len > 0) copy_in<E>(a.base[j] + rowS + r * slot + cstart * es, in + (bstart + cstart) * es, len);
+        if (!last_slice(&a.split_ctr[a.maxch + static_cast<int64_t>(j) * a.maxch + c], S, &sh_last)) continue;
+        publish_flags([&](int) { return f1(a, j, row * P + r, c); }, 1, epoch, rel);
+      }
+    } else {
+      const int gs = a.sgroup > 1 ? a.sgroup : 1;
+      const int ngr = (a.nch + gs - 1) / gs;
+      const int nsu = Pm1 * ngr;
+      for (int u = blockIdx.x; u < nsu; u += G) {
+        const int cg = u / Pm1;
+        const int j = (r + 1 + u % Pm1) % P;
+        const int c0 = cg * gs;
+        const int ncg = a.nch - c0 < gs ? a.nch - c0 : gs;
+        const int64_t bstart = static_cast<int64_t>(j) * a.block;
+        const int64_t cstart = static_cast<int64_t>(c0) * a.chunk;
+        const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, static_cast<int64_t>(ncg) * a.chunk);
+        if (len > 0) copy_in<E>(a.base[j] + rowS + r * slot + cstart * es, in + (bstart + cstart) * es, len);
+        publish_flags([&](int i) { return f1(a, j, row * P + r, c0 + i); }, ncg, epoch, rel);
+      }
     }
   }
   ps.mark(6);
@@ -849,8 +871,12 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
       if (a.err_out)  // the protocol plane reads it from pinned memory after the round's event
         __hip_atomic_store(a.err_out, ld_ctl(err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       for (int k = 0; k < P; ++k)
         if (k != r) st_flag(prog(a, k, r), epoch);
+      // the host's completion hint: every workgroup has passed its ticket (the host still
+      // waits for the round's event before it hands the output on)
+      if (a.done_out) st_flag(a.done_out, epoch);
     }
   }
 }

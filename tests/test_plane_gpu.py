@@ -204,21 +204,22 @@ def _host_outputs_gated(P, n, chunk, th, straggler, rounds):
     return outs
 
 
-def test_fine_chunks_keep_reference_semantics():
-    """maxChunkSize below the 1 KiB flag granularity (the reference's default 2-float chunk on
-    a 1 M-float vector: 174 763 chunks per block): the plane keeps one flag, count and
-    threshold decision per reference chunk (min_chunk), so a causal straggler at th = 2/3
-    gives bit-identical outputs and counts to the host WorkerCore
-    (DataBuffer.scala:12,28-29,69-75; AllreduceWorker.scala:56-57)."""
-    P, n, chunk, rounds = 3, 1 << 20, 2, 2
+def fine_chunk_parity(n: int, P: int = 3, chunk: int = 2, rounds: int = 2, log=None) -> dict:
+    """The GPU round engine vs the host WorkerCore with a maxChunkSize far below the 1 KiB
+    flag granularity, a causal straggler and th = 2/3: bit-identical outputs and counts
+    (tools/fine_chunk_parity.py runs it at 1 M floats)."""
     th = 2.0 / 3.0
     straggler = 2
     lvl = C.get_log_level()
     C.set_log_level("ERROR")  # the host run logs every outdated 2-float ReduceBlock
+    t0 = time.perf_counter()
     try:
         host = _host_outputs_gated(P, n, chunk, th, straggler, rounds)
     finally:
         C.set_log_level(lvl)
+    t_host = time.perf_counter() - t0
+    if log:
+        log(f"host WorkerCore: {t_host:.1f} s")
     gate = _Gate(P - 1)
 
     def gated(source):
@@ -233,7 +234,11 @@ def test_fine_chunks_keep_reference_semantics():
                    sources=srcs, timeout_s=60.0,
                    on_output=lambda k, out: gate.sink(out.iteration) if k != straggler else None)
     try:
+        t0 = time.perf_counter()
         job.run(timeout=300)
+        t_gpu = time.perf_counter() - t0
+        if log:
+            log(f"GPU round engine: {t_gpu:.1f} s")
         step, nch = layout(n, P, chunk)
         assert job.planes[0].chunks == nch and job.planes[0].stats.coarsened == 0
         for k in range(P):
@@ -243,11 +248,26 @@ def test_fine_chunks_keep_reference_semantics():
                 assert len(gc) == P * nch
                 assert gc == hc, (k, it, [i for i in range(len(gc)) if gc[i] != hc[i]][:8])
                 np.testing.assert_array_equal(g.float().cpu().numpy(), h, err_msg=f"worker {k} round {it}")
-        # the fast workers completed each round with exactly the two fast blocks
         g, gc = job.outputs[0][0]
-        assert gc[:2 * nch] == [2] * (2 * nch) and not any(gc[2 * nch:])
+        return {"n": n, "P": P, "max_chunk_size": chunk, "chunks_per_block": nch, "rounds": rounds,
+                "th": th, "identical": True, "host_s": round(t_host, 1), "gpu_s": round(t_gpu, 1),
+                "fast_worker_counts_round0": [int(sum(1 for c in gc[j * nch:(j + 1) * nch] if c)) for j in range(P)]}
     finally:
         job.shutdown()
+
+
+def test_fine_chunks_keep_reference_semantics():
+    """maxChunkSize below the 1 KiB flag granularity (the reference's default 2-float chunk,
+    43 691 chunks per block at 256 K floats - tools/fine_chunk_parity.py runs 1 M): the plane
+    keeps one flag, count and threshold decision per reference chunk (min_chunk), so a
+    causal straggler at th = 2/3 gives bit-identical outputs and counts to the host
+    WorkerCore (DataBuffer.scala:12,28-29,69-75; AllreduceWorker.scala:56-57). The fast
+    workers complete each round with exactly the two fast blocks."""
+    # 3 equal blocks of 87 382 floats: (2/3 * 3 * nch) is exactly the two fast blocks, so the
+    # rounds' contents do not depend on which of two simultaneous last arrivals wins
+    r = fine_chunk_parity(3 * 87382)
+    nch = r["chunks_per_block"]
+    assert r["fast_worker_counts_round0"][:2] == [nch, nch] and r["fast_worker_counts_round0"][2] == 0
 
 
 def test_fine_chunks_coarsen_at_threshold_one():
@@ -605,7 +625,11 @@ def test_split_chunks_exact_at_threshold_one(P, n, chunk, dtype):
                     ar = torch.arange(n, dtype=torch.float64)
                     ref = sum((ar + it + 1000.0 * j).to(dtype).double() for j in range(P)).numpy()
                     assert np.all(np.abs(got - ref) <= np.abs(ref) * 2.0 ** -8 + 1e-6), (k, it)
-                assert all(c == P for c in counts), counts
+                # P for every chunk that exists; 0 past the end of a short last block (600001 / 3:
+                # blocks of 3, 3 and 2 chunks), as the host WorkerCore reports it
+                step, nch = layout(n, P, chunk)
+                want = [P if min(step, n - j * step) > c * chunk else 0 for j in range(P) for c in range(nch)]
+                assert list(counts) == want, counts
     finally:
         job.shutdown()
 
