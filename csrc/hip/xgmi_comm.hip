@@ -55,16 +55,22 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
   PhaseStamps ps(a, ps_lds);
 
   // Phase 1 - ScatterBlock: push chunk c of block j to its owner j (rotated dest order,
-  // AllreduceWorker.scala:194-209), so concurrent workgroups load all links.
-  for (int u = blockIdx.x; u < nu; u += G) {
-    const int c = u / Pm1;
+  // AllreduceWorker.scala:194-209), so concurrent workgroups load all links. `sgroup`
+  // consecutive chunks of one destination travel as ONE unit (one contiguous copy, one
+  // release), each chunk keeping its own flag: small chunks pipeline the reduce, grouped
+  // copies keep the scatter at copy speed ("flat" geometry, launch_segment).
+  const int gs = a.sgroup > 1 ? a.sgroup : 1;
+  const int nsu = Pm1 * ((a.nch + gs - 1) / gs);
+  for (int u = blockIdx.x; u < nsu; u += G) {
+    const int c0 = (u / Pm1) * gs;
+    const int ncg = a.nch - c0 < gs ? a.nch - c0 : gs;
     const int j = (r + 1 + u % Pm1) % P;
     const int64_t bstart = static_cast<int64_t>(j) * a.block;
-    const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
-    const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
-    if (len > 0 && unit_in_bounds(a, cstart * es, len * es, c, err))
+    const int64_t cstart = static_cast<int64_t>(c0) * a.chunk;
+    const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, static_cast<int64_t>(ncg) * a.chunk);
+    if (len > 0 && unit_in_bounds(a, cstart * es, len * es, c0 + ncg - 1, err))
       copy_to_slab<E>(a.base[j] + a.off_S + r * slot + cstart * es, in + (bstart + cstart) * es, len);
-    publish_flags([&](int) { return f1(a, j, r, c); }, 1, epoch, rel);
+    publish_flags([&](int i) { return f1(a, j, r, c0 + i); }, ncg, epoch, rel);
   }
 
   ps.mark(1);
@@ -113,20 +119,79 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
   }
 
   ps.mark(3);
-  // Phase 3 - complete: gather the other owners' reduced chunks into the output.
-  for (int u = take(9, blockIdx.x), k3 = 1; u < nu; u = take(9, blockIdx.x + k3 * G), ++k3) {
+  // Phase 3 - complete: gather the other owners' reduced chunks into the output. The
+  // workgroup's units are polled together (wave 0, one lane per unit, up to 64 at a time)
+  // and copied in ARRIVAL order: owners finish their reduces at different times, and a
+  // workgroup waiting on its units one by one idles behind the latest of them while others
+  // are ready (the threshold kernel's gather, which does this, was 13 % faster at 8 x 64 MiB
+  // - profiles/round3/README.md). `dynamic` keeps the counter-driven in-order walk.
+  auto gather_unit = [&](int u) {
     const int c = u / Pm1;
     const int j = (r + 1 + u % Pm1) % P;
     const int64_t bstart = static_cast<int64_t>(j) * a.block;
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, a.chunk);
-    const uint64_t tw = ps.now();
-    wait_flags([&](int q) -> const uint32_t* { return f2(a, r, j, c * a.sub + q); }, a.sub, epoch, deadline, err,
-               ERR_TIMEOUT_REDUCE, acq);
-    ps.add(4, tw);
     ps.count(7);
     if (len > 0 && unit_in_bounds(a, cstart * es, len * es, c, err))
       copy_from_slab<E>(out + (bstart + cstart) * es, a.base[r] + a.off_R + j * slot + cstart * es, len);
+  };
+  if (a.dynamic) {
+    for (int u = take(9, blockIdx.x), k3 = 1; u < nu; u = take(9, blockIdx.x + k3 * G), ++k3) {
+      const int c = u / Pm1;
+      const int j = (r + 1 + u % Pm1) % P;
+      const uint64_t tw = ps.now();
+      wait_flags([&](int q) -> const uint32_t* { return f2(a, r, j, c * a.sub + q); }, a.sub, epoch, deadline, err,
+                 ERR_TIMEOUT_REDUCE, acq);
+      ps.add(4, tw);
+      gather_unit(u);
+    }
+  } else {
+    __shared__ uint64_t arrived;
+    __shared__ int late_s;
+    const int mine = blockIdx.x < static_cast<unsigned>(nu) ? (nu - 1 - static_cast<int>(blockIdx.x)) / G + 1 : 0;
+    for (int w0 = 0; w0 < mine; w0 += 64) {
+      const int wn = mine - w0 < 64 ? mine - w0 : 64;
+      uint64_t pending = wn == 64 ? ~0ull : ((1ull << wn) - 1ull);  // uniform across the workgroup
+      const uint64_t tw = ps.now();
+      while (pending) {
+        if (threadIdx.x < 64) {
+          const int lane = static_cast<int>(threadIdx.x);
+          bool arr = false;
+          if ((pending >> lane) & 1ull) {
+            const int u = static_cast<int>(blockIdx.x) + (w0 + lane) * G;
+            const int c = u / Pm1;
+            const int j = (r + 1 + u % Pm1) % P;
+            arr = true;
+            for (int q = 0; q < a.sub && arr; ++q) arr = reached(ld_flag(f2(a, r, j, c * a.sub + q)), epoch);
+          }
+          const uint64_t m = __ballot(arr);
+          const bool late = m == 0 && wall_ticks() > deadline;
+          if (late && lane == 0) __hip_atomic_fetch_or(err, ERR_TIMEOUT_REDUCE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if (m && acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, once per batch
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0) {
+            arrived = m;
+            late_s = late ? 1 : 0;
+          }
+        }
+        __syncthreads();
+        uint64_t m = arrived & pending;
+        const bool late = late_s != 0;
+        __syncthreads();
+        if (late) break;  // the rest is given up (error word set, no data moved)
+        if (!m) {
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        pending &= ~m;
+        while (m) {
+          const int i = __ffsll(static_cast<long long>(m)) - 1;
+          m &= m - 1;
+          gather_unit(static_cast<int>(blockIdx.x) + (w0 + i) * G);
+        }
+      }
+      ps.add(4, tw);
+    }
   }
   ps.mark(5);
   ps.flush();
@@ -511,22 +576,27 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   alloc_bytes_ = L.alloc_bytes;
   // Automatic dispatch limits (resolve()), measured with P logical ranks in one launch on one
   // MI355X (bench.py latency_vs_size, profiles/round3/README.md): the low-latency one-shot
-  // wins up to 1 MiB at 2 ranks and 256 KiB at 8 (it moves 2x bytes as flag-carrying LL
-  // words, so it loses to the plain kernels as soon as they are bandwidth bound); the
-  // one-shot (one hop, every rank reads all P inputs) wins up to 16 MiB at 2 ranks, where it
-  // moves the same bytes as the two-shot with one hand-off less; at 8 ranks the two-shot
-  // takes over from the low-latency kernel directly. MXAR_LL_AUTO_MAX / MXAR_ONESHOT_MAX
+  // wins up to 1 MiB at 2 ranks, 512 KiB at 4 and 256 KiB at 8 (it moves 2x bytes as
+  // flag-carrying LL words, so it loses to the plain kernels once they are bandwidth bound);
+  // the one-shot (one hop, every rank reads all P inputs) wins up to 16 MiB at 2 ranks, where
+  // it moves the same bytes as the two-shot with one hand-off less, and up to 4 MiB at 4; at
+  // 8 ranks the two-shot takes over from the low-latency kernel directly. MXAR_LL_AUTO_MAX / MXAR_ONESHOT_MAX
   // override (bytes).
   const int64_t mib = int64_t{1} << 20;
   ll_auto_max_ = world_ <= 2 ? mib : world_ <= 4 ? mib / 2 : mib / 4;
   if (const char* e = std::getenv("MXAR_LL_AUTO_MAX")) ll_auto_max_ = std::max<int64_t>(0, std::atoll(e));
-  oneshot_max_ = std::min<int64_t>(slot_bytes_, world_ <= 2 ? 16 * mib : world_ <= 4 ? 2 * mib : mib / 4);
+  oneshot_max_ = std::min<int64_t>(slot_bytes_, world_ <= 2 ? 16 * mib : world_ <= 4 ? 4 * mib : mib / 4);
   if (const char* e = std::getenv("MXAR_ONESHOT_MAX")) oneshot_max_ = std::min<int64_t>(slot_bytes_, std::atoll(e));
   if (grid_ <= 0) grid_ = default_grid(device);
   if (const char* f = std::getenv("MXAR_FENCE")) fence_ = std::atoi(f) & 3;
   if (const char* u = std::getenv("MXAR_TWOSHOT_UNITS")) units_per_wg_ = std::max(1, std::atoi(u));
   if (const char* u = std::getenv("MXAR_TWOSHOT_SUB")) sub_max_ = std::max(1, std::atoi(u));
   if (const char* d = std::getenv("MXAR_TWOSHOT_DYNAMIC")) dynamic_ = std::atoi(d) != 0;
+  if (const char* g = std::getenv("MXAR_TWOSHOT_GEOM")) {
+    const std::string v = g;
+    geom_ = v == "coarse" ? 0 : v == "fine" ? 1 : v == "flat" ? 2 : -1;
+  }
+  if (const char* f = std::getenv("MXAR_TWOSHOT_FLAT_MIN")) flat_min_ = std::max<int64_t>(0, std::atoll(f));
 
   hip_check(hipSetDevice(device_), "hipSetDevice");
   const char* mem = std::getenv("MXAR_SLAB_MEM");
@@ -772,18 +842,33 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
     // arrive in a finer stream, so reduces start earlier and the tail is shorter (4 / 8 ranks
     // x 256 MiB: -6 % / -4 %; at 8-16 MiB blocks it loses 14-20 %). MXAR_TWOSHOT_UNITS /
     // MXAR_TWOSHOT_SUB override.
-    const bool fine = a.block * es >= (int64_t{32} << 20);
-    const int upw = c0.units_per_wg_ > 0 ? c0.units_per_wg_ : fine ? std::max(1, W - 1) : 1;
-    const int sub_max = c0.sub_max_ > 0 ? c0.sub_max_ : fine ? 2 : 64;
-    const int64_t target = W > 1 ? std::max<int64_t>(1, int64_t{gmax} * upw / (W - 1)) : int64_t{gmax} * upw;
-    a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, target), elems));
-    a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
-    int64_t sub = std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(W - 1), a.chunk / min_chunk, 64,
-                                                          c0.maxch_ / a.nch, int64_t{sub_max}}));
-    a.subchunk = round_up(ceil_div(a.chunk, sub), elems);
-    a.sub = static_cast<int>(ceil_div(a.chunk, a.subchunk));
-    const int64_t units = std::max<int64_t>((W - 1) * static_cast<int64_t>(a.nch), static_cast<int64_t>(a.nch) * a.sub);
-    gx = static_cast<int>(std::min<int64_t>(gmax, std::max<int64_t>(1, units)));
+    // "flat" (MXAR_TWOSHOT_GEOM=flat): one chunk per workgroup (one reduce unit each, no
+    // split), the scatter in groups of sgroup chunks per destination - the threshold
+    // kernel's geometry, which beat the two others at large blocks (profiles/round3).
+    const int geom = c0.geom_ >= 0 ? c0.geom_ : (a.block * es >= c0.flat_min_ ? 2 : a.block * es >= (int64_t{32} << 20) ? 1 : 0);
+    if (geom == 2 && W > 1) {
+      a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, gmax), elems));
+      a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
+      a.sub = 1;
+      a.subchunk = a.chunk;
+      gx = static_cast<int>(std::min<int64_t>(gmax, std::max<int64_t>(1, static_cast<int64_t>(W - 1) * a.nch)));
+      const int per = std::max(1, gx / (W - 1));  // scatter groups per destination block
+      a.sgroup = static_cast<int>(std::min<int64_t>(64, std::max<int64_t>(1, ceil_div(a.nch, per))));
+    } else {
+      const bool fine = geom == 1;
+      const int upw = c0.units_per_wg_ > 0 ? c0.units_per_wg_ : fine ? std::max(1, W - 1) : 1;
+      const int sub_max = c0.sub_max_ > 0 ? c0.sub_max_ : fine ? 2 : 64;
+      const int64_t target = W > 1 ? std::max<int64_t>(1, int64_t{gmax} * upw / (W - 1)) : int64_t{gmax} * upw;
+      a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, target), elems));
+      a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
+      int64_t sub = std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(W - 1), a.chunk / min_chunk, 64,
+                                                            c0.maxch_ / a.nch, int64_t{sub_max}}));
+      a.subchunk = round_up(ceil_div(a.chunk, sub), elems);
+      a.sub = static_cast<int>(ceil_div(a.chunk, a.subchunk));
+      const int64_t units =
+          std::max<int64_t>((W - 1) * static_cast<int64_t>(a.nch), static_cast<int64_t>(a.nch) * a.sub);
+      gx = static_cast<int>(std::min<int64_t>(gmax, std::max<int64_t>(1, units)));
+    }
   }
   a.fence = c0.fence_;
   a.scale = scale;

@@ -8,6 +8,7 @@ synthetic inputs, sizes from small to the bench's 256 MiB; prints one JSON row p
 from __future__ import annotations
 
 import argparse
+import resource
 import json
 import os
 import sys
@@ -117,10 +118,17 @@ def main() -> None:
             for p, b in zip(job.planes, bufs):
                 p.set_phase_stamps(b.data_ptr(), job.grid)
         t0 = time.perf_counter()
+        ru0 = resource.getrusage(resource.RUSAGE_SELF)
         try:
             job.run(timeout=max(60.0, 4 * a.timeout))
+            ru1 = resource.getrusage(resource.RUSAGE_SELF)
             st = job.state()
             row["wall_s"] = round(time.perf_counter() - t0, 3)
+            # host CPU the job's threads burned (dispatchers, completion pollers, master), per
+            # round: what the busy-polls cost
+            cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+            row["cpu_us_per_round"] = round(cpu / a.rounds * 1e6, 1)
+            row["cpu_cores_busy"] = round(cpu / max(1e-9, time.perf_counter() - t0), 2)
             s = job.stamps
             if len(s) > 2:
                 per = (s[-1] - s[1]) / (len(s) - 2)
