@@ -16,6 +16,8 @@
 // slot for that chunk.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "xgmi_device.h"
 
 namespace mxar {
@@ -38,7 +40,36 @@ __device__ __forceinline__ float adamw(float g, float* p, float* m, float* v, co
 
 }  // namespace
 
-template <class E, int PT>
+// fp32 state access: plain loads / stores (STREAM = false, the default) or nt loads +
+// write-through stores (STREAM = true, MXAR_ADAM_STREAM=1: the store probe's fastest copy
+// form, profiles/round3/store_probe.json). The state is read and written back at the same
+// addresses, and the streaming form is 1.56x slower (1.00 vs 0.64 ms for the 134 M-parameter
+// step, same box: profiles/round3/adamw_stream_ab.jsonl); the gradients (read once, summed)
+// come in with nt loads either way.
+template <bool STREAM>
+__device__ __forceinline__ float4 ld_state(const float* p, __amdgpu_buffer_rsrc_t r, int64_t i) {
+  if constexpr (STREAM) {
+    const Pack16 v = ld16_nt(r, static_cast<uint32_t>(i * 4));
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+  } else {
+    return *reinterpret_cast<const float4*>(p + i);
+  }
+}
+template <bool STREAM>
+__device__ __forceinline__ void st_state(float* p, __amdgpu_buffer_rsrc_t r, int64_t i, const float4& x) {
+  if constexpr (STREAM) {
+    Pack16 v;
+    v[0] = __float_as_uint(x.x);
+    v[1] = __float_as_uint(x.y);
+    v[2] = __float_as_uint(x.z);
+    v[3] = __float_as_uint(x.w);
+    st16_wt(r, static_cast<uint32_t>(i * 4), v);
+  } else {
+    *reinterpret_cast<float4*>(p + i) = x;
+  }
+}
+
+template <class E, int PT, bool STREAM>
 __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a) {
   constexpr int es = 16 / E::ELEMS;
   constexpr int EL = E::ELEMS;
@@ -92,6 +123,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a)
       float* const sp = mp + cstart;
       float* const sm = m1 + cstart;
       float* const sv = m2 + cstart;
+      const __amdgpu_buffer_rsrc_t rp = slab_rsrc(sp), rm = slab_rsrc(sm), rv = slab_rsrc(sv);
       const int64_t npk = len / EL;
       // U packs per lane per iteration, every load issued before the first use: the
       // persistent grid has only 2 workgroups per CU, so bytes in flight come from ILP
@@ -117,9 +149,9 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a)
           }
 #pragma unroll
           for (int e = 0; e < EL / 4; ++e) {
-            p4[w][e] = *reinterpret_cast<const float4*>(sp + i * EL + 4 * e);
-            m4[w][e] = *reinterpret_cast<const float4*>(sm + i * EL + 4 * e);
-            v4[w][e] = *reinterpret_cast<const float4*>(sv + i * EL + 4 * e);
+            p4[w][e] = ld_state<STREAM>(sp, rp, i * EL + 4 * e);
+            m4[w][e] = ld_state<STREAM>(sm, rm, i * EL + 4 * e);
+            v4[w][e] = ld_state<STREAM>(sv, rv, i * EL + 4 * e);
           }
         }
 #pragma unroll
@@ -132,12 +164,15 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a)
             acc[w].v[4 * e + 1] = adamw(acc[w].v[4 * e + 1] * a.scale, &p4[w][e].y, &m4[w][e].y, &v4[w][e].y, a);
             acc[w].v[4 * e + 2] = adamw(acc[w].v[4 * e + 2] * a.scale, &p4[w][e].z, &m4[w][e].z, &v4[w][e].z, a);
             acc[w].v[4 * e + 3] = adamw(acc[w].v[4 * e + 3] * a.scale, &p4[w][e].w, &m4[w][e].w, &v4[w][e].w, a);
-            *reinterpret_cast<float4*>(sp + i * EL + 4 * e) = p4[w][e];
-            *reinterpret_cast<float4*>(sm + i * EL + 4 * e) = m4[w][e];
-            *reinterpret_cast<float4*>(sv + i * EL + 4 * e) = v4[w][e];
+            st_state<STREAM>(sp, rp, i * EL + 4 * e, p4[w][e]);
+            st_state<STREAM>(sm, rm, i * EL + 4 * e, m4[w][e]);
+            st_state<STREAM>(sv, rv, i * EL + 4 * e, v4[w][e]);
           }
           const Pack16 o = acc[w].pack();
-          st16(own_out + i * 16, o);
+          if constexpr (STREAM)
+            st16_wt(slab_rsrc(own_out), static_cast<uint32_t>(i * 16), o);
+          else
+            st16(own_out + i * 16, o);
           for (int k = 0; k < P; ++k)
             if (k != r) st16_wt(slab_rsrc(a.base[k] + roff), static_cast<uint32_t>(i * 16), o);
         }
@@ -170,20 +205,32 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a)
   finish_launch(ctl, epoch);
 }
 
-void launch_adamw(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {
+template <bool STREAM>
+static void launch_adamw_t(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {
   dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
     using E = decltype(tag);
     // P is a template constant wherever it can be: the reduce then issues every source's
     // load before the first add (the PT = 0 loop waits on each load in turn) - P = 1 is the
     // single-GPU optimizer step
     switch (a.P) {
-      case 1: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 1>), grid, dim3(kCommThreads), 0, s, a); break;
-      case 2: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 2>), grid, dim3(kCommThreads), 0, s, a); break;
-      case 4: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 4>), grid, dim3(kCommThreads), 0, s, a); break;
-      case 8: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 8>), grid, dim3(kCommThreads), 0, s, a); break;
-      default: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 0>), grid, dim3(kCommThreads), 0, s, a); break;
+      case 1: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 1, STREAM>), grid, dim3(kCommThreads), 0, s, a); break;
+      case 2: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 2, STREAM>), grid, dim3(kCommThreads), 0, s, a); break;
+      case 4: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 4, STREAM>), grid, dim3(kCommThreads), 0, s, a); break;
+      case 8: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 8, STREAM>), grid, dim3(kCommThreads), 0, s, a); break;
+      default: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 0, STREAM>), grid, dim3(kCommThreads), 0, s, a); break;
     }
   });
+}
+
+void launch_adamw(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {
+  static const bool stream = [] {
+    const char* e = std::getenv("MXAR_ADAM_STREAM");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
+  if (stream)
+    launch_adamw_t<true>(a, grid, s, dt);
+  else
+    launch_adamw_t<false>(a, grid, s, dt);
 }
 
 }  // namespace mxar

@@ -302,7 +302,7 @@ class XgmiComm {
   bool own_ctl_ = true;            // false: control words owned by the caller
   bool dynamic_ = false;           // two-shot units from a counter (MXAR_TWOSHOT_DYNAMIC)
   int geom_ = -1;                  // two-shot geometry: -1 by block size, 0 coarse, 1 fine, 2 flat (MXAR_TWOSHOT_GEOM)
-  int64_t flat_min_ = int64_t{1} << 62;  // blocks of at least this many bytes use the flat geometry (MXAR_TWOSHOT_FLAT_MIN)
+  int64_t flat_min_ = int64_t{2} << 20;  // blocks of at least this many bytes use the flat geometry (MXAR_TWOSHOT_FLAT_MIN)
   bool launched_ = false;          // a launch has been enqueued (last_stream_ valid)
   hipStream_t last_stream_ = nullptr;
   hipEvent_t switch_ev_ = nullptr;  // recorded on last_stream_ when the stream changes

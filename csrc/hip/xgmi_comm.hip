@@ -842,10 +842,18 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
     // arrive in a finer stream, so reduces start earlier and the tail is shorter (4 / 8 ranks
     // x 256 MiB: -6 % / -4 %; at 8-16 MiB blocks it loses 14-20 %). MXAR_TWOSHOT_UNITS /
     // MXAR_TWOSHOT_SUB override.
-    // "flat" (MXAR_TWOSHOT_GEOM=flat): one chunk per workgroup (one reduce unit each, no
-    // split), the scatter in groups of sgroup chunks per destination - the threshold
-    // kernel's geometry, which beat the two others at large blocks (profiles/round3).
-    const int geom = c0.geom_ >= 0 ? c0.geom_ : (a.block * es >= c0.flat_min_ ? 2 : a.block * es >= (int64_t{32} << 20) ? 1 : 0);
+    // Geometry by block size (same-box A/B over 2 / 4 / 8 logical ranks x 1-256 MiB,
+    // profiles/round3/twoshot_geometry_ab.jsonl; MXAR_TWOSHOT_GEOM=coarse|fine|flat forces one):
+    //   coarse (blocks < 2 MiB): ~one scatter unit per workgroup, each chunk reduced in up to
+    //          P-1 pieces - fewest flag hand-offs, best while the round is latency bound;
+    //   flat   (blocks >= 2 MiB): one chunk per workgroup (one reduce unit each, no split),
+    //          the scatter in groups of `sgroup` chunks per destination (one copy and one
+    //          release per group, a flag per chunk) - small chunks start the reduces early,
+    //          grouped copies keep the scatter at copy speed: -22 % at 8 x 64 MiB, -7 % at
+    //          8 x 256 MiB vs the best of the others, equal at 2 ranks;
+    //   fine   (the round-2 choice for blocks >= 32 MiB): one chunk per workgroup for each of
+    //          the P-1 destinations, reduced in 2 pieces - no longer the default.
+    const int geom = c0.geom_ >= 0 ? c0.geom_ : (a.block * es >= c0.flat_min_ ? 2 : 0);
     if (geom == 2 && W > 1) {
       a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, gmax), elems));
       a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
