@@ -175,10 +175,10 @@ class XgmiCommunicator:
         decides; rank 0's choice is broadcast so every rank dispatches identically - a split
         decision would deadlock). `grids`: extra workgroup counts tried for twoshot / ring at
         sizes >= grid_min_bytes (labels "twoshot@256"); only counts <= the default grid, so
-        every workgroup stays resident. Where the two-shot picks its fine geometry (blocks of
-        >= 32 MiB: world - 1 scatter units per workgroup), the coarse one is tried too
-        ("twoshot~1", "twoshot@256~1"): on one GPU fine wins by 4-6 %, over xGMI links the
-        measured choice decides. Returns one row per size: {bytes, <algo>_p50_us, choice}."""
+        every workgroup stays resident. Where the two-shot picks its flat geometry (blocks of
+        >= 2 MiB: one chunk per workgroup, grouped scatter), the coarse one is tried too
+        ("twoshot~1", "twoshot@256~1": one scatter unit per workgroup): on one GPU flat wins
+        by up to 22 % at 8 ranks, over xGMI links the measured choice decides. Returns one row per size: {bytes, <algo>_p50_us, choice}."""
         import torch.distributed as dist
 
         from ..ops import fill_uniform
@@ -203,7 +203,7 @@ class XgmiCommunicator:
                 labels.append(algo)
                 if algo in ("twoshot", "ring") and size >= grid_min_bytes:
                     labels += [f"{algo}@{g}" for g in extra]
-                if algo == "twoshot" and self.world > 2 and self._default_units == 0 and size // self.world >= (32 << 20):
+                if algo == "twoshot" and self.world > 2 and self._default_units == 0 and size // self.world >= (2 << 20):
                     labels += ["twoshot~1"] + [f"twoshot@{g}~1" for g in extra]
             for algo in labels:
                 if algo == "oneshot" and (size > self.slot_bytes or size > (8 << 20)):

@@ -853,7 +853,9 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
     //          8 x 256 MiB vs the best of the others, equal at 2 ranks;
     //   fine   (the round-2 choice for blocks >= 32 MiB): one chunk per workgroup for each of
     //          the P-1 destinations, reduced in 2 pieces - no longer the default.
-    const int geom = c0.geom_ >= 0 ? c0.geom_ : (a.block * es >= c0.flat_min_ ? 2 : 0);
+    // an explicit units-per-workgroup (MXAR_TWOSHOT_UNITS, tune()'s "~1" labels) selects the
+    // coarse / fine family it parameterises
+    const int geom = c0.geom_ >= 0 ? c0.geom_ : c0.units_per_wg_ > 0 ? 0 : (a.block * es >= c0.flat_min_ ? 2 : 0);
     if (geom == 2 && W > 1) {
       a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, gmax), elems));
       a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
