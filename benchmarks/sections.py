@@ -358,7 +358,8 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
             comm = PairRehearsalComm(reducer.buckets, max(grids))
             reducer.comm = comm
             reducer._raw_ok = True
-            bwd = SyntheticBackward(params, 1024, torch.bfloat16, dev)
+            bwds = {1024: SyntheticBackward(params, 1024, torch.bfloat16, dev)}
+            bwd = bwds[1024]
             grads = [q.grad for q in params]
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 
@@ -382,13 +383,21 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
 
             hi_stream, hi_raw = reducer.stream, reducer._comm_raw
             lo_stream = torch.cuda.Stream(device=dev, priority=0)
-            variants = [(f"grid{g}", g, True, True) for g in grids]
+            variants = [(f"grid{g}", g, True, True, 1024) for g in grids]
             # every bucket after backward (no overlap), and the overlap on a normal-priority
             # comm stream (the GEMMs' dispatches are not pre-empted by the comm queue)
-            variants += [("serial_grid512", 512, False, True), ("grid128_normal_prio", 128, True, False)]
-            for name, grid, ov, hi in variants:
-                cell: dict = {}
+            variants += [("serial_grid512", 512, False, True, 1024), ("grid128_normal_prio", 128, True, False, 1024)]
+            if big:
+                # 1024 tokens make the weight-gradient GEMMs (K = tokens) nearly bandwidth bound,
+                # so a bandwidth-bound allreduce beside them slows them; at a training-size
+                # 8192 tokens per GPU they are compute bound
+                variants += [("tokens8192_grid256", 256, True, True, 8192), ("tokens8192_serial", 512, False, True, 8192)]
+            for name, grid, ov, hi, tokens in variants:
+                cell: dict = {"tokens": tokens}
                 try:
+                    if tokens not in bwds:
+                        bwds[tokens] = SyntheticBackward(params, tokens, torch.bfloat16, dev)
+                    bwd = bwds[tokens]
                     for c in comm.cl.comms:
                         c.grid = grid
                     reducer.overlap = ov
@@ -400,12 +409,12 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                                 fn()
                         per = {"step": [], "compute": [], "bwd_with_comm": [], "bwd_alone": []}
                         for _ in range(steps):  # interleaved: clock drift hits both alike
-                            for name, fn, bkey in (("step", overlap, "bwd_with_comm"), ("compute", compute, "bwd_alone")):
+                            for key, fn, bkey in (("step", overlap, "bwd_with_comm"), ("compute", compute, "bwd_alone")):
                                 torch.cuda.synchronize(dev)
                                 t0 = time.perf_counter()
                                 fn()
                                 torch.cuda.synchronize(dev)
-                                per[name].append((time.perf_counter() - t0) * 1e3)
+                                per[key].append((time.perf_counter() - t0) * 1e3)
                                 per[bkey].append(ev[0].elapsed_time(ev[1]))
                         torch.cuda.synchronize(dev)
                         t0 = time.perf_counter()
@@ -416,7 +425,7 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                     comm.check()
                     med = {k: statistics.median(v) for k, v in per.items()}
                     exposed = med["step"] - med["compute"]
-                    cell = {"step_ms": round(med["step"], 3), "compute_ms": round(med["compute"], 3),
+                    cell = {"tokens": tokens, "step_ms": round(med["step"], 3), "compute_ms": round(med["compute"], 3),
                             "exposed_comm_ms": round(exposed, 3), "comm_only_ms": round(comm_ms, 3),
                             "bwd_ms_with_comm": round(med["bwd_with_comm"], 3),
                             "bwd_ms_alone": round(med["bwd_alone"], 3),
@@ -434,6 +443,7 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
             row["error"] = repr(e)
         finally:
             del params, bwd, reducer, comm
+            bwds = None
             torch.cuda.empty_cache()
         out[model] = row
     return out

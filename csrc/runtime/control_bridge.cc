@@ -253,7 +253,10 @@ void ControlBridge::reap() {  // join readers of clients that went away (mu_ not
     }
   }
   for (auto& c : dead) {  // the fd closes with the last reference
-    if (c->reader.joinable()) c->reader.join();
+    // A reader may still be inside tell() to the master (which can block while the actor
+    // system shuts down): it is never joined, only detached - it holds references to the
+    // bridge and its client, so it finishes safely on its own.
+    if (c->reader.joinable()) c->reader.detach();
     if (c->writer.joinable()) c->writer.join();
   }
 }
@@ -372,7 +375,9 @@ void ControlBridge::stop() {
   }
   for (auto& c : cs) {
     c->kill();
-    join(c->reader);
+    // readers are detached, not joined: one may be blocked in tell() on the very system
+    // whose shutdown is running this stop() (see reap)
+    if (c->reader.joinable()) c->reader.detach();
     join(c->writer);
   }
   if (lfd_ >= 0) ::close(lfd_);

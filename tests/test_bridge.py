@@ -433,3 +433,22 @@ def test_client_churn_while_rounds_publish():
             np.testing.assert_array_equal(outs[k][rounds - 1][0], expected(n, rounds - 1, P).astype(F))
     finally:
         system.shutdown()
+
+
+def test_client_that_never_reads_does_not_stall_the_master():
+    """publish() used to block the master actor in send() once a connected client
+    stopped reading. Events now go through a bounded per-client queue drained by a writer
+    thread: a watcher that never reads its socket is disconnected when its queue overflows
+    (4 MiB), and the job's rounds run at their own pace meanwhile."""
+    import socket
+
+    P, n, chunk, rounds = 2, 8, 2, 3000
+    system, master, port, outs, fin = _job(P, n, chunk, rounds, external=False, name="Stall")
+    lazy = socket.create_connection(("127.0.0.1", port))
+    lazy.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4096)  # and never reads
+    try:
+        assert fin.wait(120), "rounds stalled behind a client that never reads"
+        assert len(outs[0]) == rounds and len(outs[1]) == rounds
+    finally:
+        lazy.close()
+        system.shutdown()

@@ -1,6 +1,7 @@
-bash tools/gpu.sh tests && bash tools/gpu.sh bench --steps 20 --warmup 5 && \
-bash tools/gpu.sh rehearsal 2 4 && \
-timeout -k 10 200 python tools/plane_probe.py --P 8 --sizes 16M 256M --rounds 30 --stamps > gpurun_out/probe_p8.jsonl 2> gpurun_out/probe_p8.err && \
-timeout -k 10 200 python tools/plane_probe.py --P 2 --sizes 256M --units 256 --rounds 30 > gpurun_out/probe_split.jsonl 2>> gpurun_out/probe_split.err && \
-timeout -k 10 200 python tools/plane_probe.py --P 2 --sizes 256M --units 4 --rounds 30 >> gpurun_out/probe_split.jsonl 2>> gpurun_out/probe_split.err && \
-timeout -k 10 200 python tools/plane_probe.py --P 2 --sizes 1M 40 --rounds 200 --stamps > gpurun_out/probe_small_stamps.jsonl 2>> gpurun_out/probe_split.err
+for rep in 1 2; do
+  timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-dp --no-local --no-protocol --no-sizes > gpurun_out/adam_default_$rep.json 2>>gpurun_out/adam.err || exit 1
+  MXAR_ADAM_STREAM=0 timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-dp --no-local --no-protocol --no-sizes > gpurun_out/adam_env0_$rep.json 2>>gpurun_out/adam.err || exit 1
+  timeout -k 10 200 python abtest/prev/tools/bench_adamw.py --ranks 1 2 --mib 256 > gpurun_out/adam_prevtool_$rep.jsonl 2>>gpurun_out/adam.err || exit 1
+  echo "rep $rep ok"
+done && \
+timeout -k 10 600 python bench.py --steps 10 --warmup 3 --no-local --no-protocol > gpurun_out/bench_dp.json 2> gpurun_out/bench_dp.err && echo dp ok
