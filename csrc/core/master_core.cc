@@ -106,6 +106,8 @@ void MasterCore::on_complete(int srcId, int round, int64_t epoch) {
   }
   if (srcId >= 0) {
     MXAR_LOG(INFO, "master", "----Node " << srcId << " completes allreduce round " << round);
+    if (Tracer::get().enabled())
+      trace_instant("master", "complete r" + std::to_string(round), "{\"worker\":" + std::to_string(srcId) + "}");
     stats_.completes++;
     if (round != round_ || (p_.externalRounds && (awaiting_ || !started_))) {
       stats_.stale_completes++;

@@ -84,6 +84,9 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   if (o_.max_lag < 0 || o_.max_lag > 62) throw std::invalid_argument("xgmi plane: max_lag must be in [0, 62]");
   o_.ring = std::max(4, o_.ring);
   if (const char* e = std::getenv("MXAR_PLANE_SPLIT")) o_.split = std::atoi(e) != 0;  // A/B knob
+  // A/B knob: 1 = also record an event per round and confirm completion with it (round 2's
+  // form; ~2-3 us of hipEventRecord on every launch, profiles/round3/api_cost.json)
+  if (const char* e = std::getenv("MXAR_PLANE_EVENTS")) event_confirm_ = std::atoi(e) != 0;
   const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
   flag_gran_ = o_.min_chunk > 0 ? std::min<int64_t>(XgmiComm::min_chunk_bytes(), o_.min_chunk * es)
                                 : XgmiComm::min_chunk_bytes();
@@ -562,7 +565,7 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   }
   std::unique_lock<std::mutex> lk(mu_);
   rec.ev = events_[rec.slot];
-  hip_check(hipEventRecord(rec.ev, stream_), "hipEventRecord(round)");
+  if (event_confirm_) hip_check(hipEventRecord(rec.ev, stream_), "hipEventRecord(round)");
   last_round_ = round;
   st_.launches++;
   if (cold) st_.cold++;
@@ -609,11 +612,16 @@ void XgmiRoundPlane::completion_loop() {
     hipError_t e;
     {
       TraceScope span("plane", [&] { return std::make_pair("wait r" + std::to_string(rec.round), std::string()); });
-      // Poll first: a blocking wait sleeps on an interrupt, whose wake-up adds tens of
-      // microseconds to every round. The kernel's last workgroup sets the slot's pinned done
-      // word to the round epoch (a plain load of host memory: no runtime call, so this thread
-      // does not contend with the workers' launches for the HIP runtime's locks while the
-      // round runs); the round's event then confirms it before the output is handed on.
+      // The kernel's last workgroup sets the slot's pinned done word to the round epoch once
+      // every workgroup drained its stores (output, counts) and passed its ticket
+      // (xgmi_threshold.hip, round end): that word IS the completion. Reading it is a plain
+      // load of host memory - no runtime call, so this thread does not contend with the
+      // workers' launches for the HIP runtime's locks, and no event is recorded per round.
+      // The output's consumers are device work on this GPU, which reads the drained stores
+      // through L2. Poll first (a blocking wait sleeps on an interrupt whose wake-up costs
+      // tens of microseconds), then poll with short sleeps: the kernel bounds its own waits
+      // (timeout_s), so a round that never writes the word is a lost kernel - reported as an
+      // error after twice that long.
       const auto t0 = std::chrono::steady_clock::now();
       const auto budget = std::chrono::microseconds(o_.spin_us);
       const volatile uint32_t* done = reinterpret_cast<const volatile uint32_t*>(
@@ -622,17 +630,32 @@ void XgmiRoundPlane::completion_loop() {
       while (*done != want && std::chrono::steady_clock::now() - t0 < budget) {
         for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
       }
-      for (;;) {
-        e = hipEventQuery(rec.ev);
-        if (e != hipErrorNotReady) break;
-        if (std::chrono::steady_clock::now() - t0 > budget) {
-          e = hipEventSynchronize(rec.ev);
-          break;
+      e = hipSuccess;
+      if (event_confirm_) {
+        for (;;) {
+          e = hipEventQuery(rec.ev);
+          if (e != hipErrorNotReady) break;
+          if (std::chrono::steady_clock::now() - t0 > budget) {
+            e = hipEventSynchronize(rec.ev);
+            break;
+          }
+          std::this_thread::yield();
         }
-        std::this_thread::yield();
+      } else {
+        const auto lost = std::chrono::microseconds(static_cast<int64_t>(2e6 * o_.timeout_s) + 5000000);
+        while (*done != want) {
+          if (std::chrono::steady_clock::now() - t0 > lost) {
+            MXAR_LOG(ERROR, "plane", "round " << rec.round << " never signalled its completion word");
+            e = hipErrorLaunchTimeOut;
+            break;
+          }
+          std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);  // counts / error word after the done word
       }
     }
-    trace_instant("plane", "done r" + std::to_string(rec.round));
+    if (Tracer::get().enabled())
+      trace_instant("plane", "done r" + std::to_string(rec.round), "{\"worker\":" + std::to_string(cfg_.id) + "}");
     RoundResult res;
     res.epoch = rec.epoch;
     res.round = rec.round;

@@ -100,6 +100,7 @@ class XgmiRoundPlane final : public RoundPlane {
   }
 
  private:
+  bool event_confirm_ = false;  // MXAR_PLANE_EVENTS=1: per-round event confirms the done word
   struct Rec {
     int round = 0;
     int64_t epoch = 0;

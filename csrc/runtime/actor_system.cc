@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <thread>
 
 #include "../core/log.h"
 
@@ -9,6 +10,20 @@ namespace mxar {
 
 namespace {
 std::atomic<uint64_t> g_uid{1};
+
+// The dispatcher thread's run-next slot (ActorSystem::lifo_): set while the thread runs an
+// actor turn of `tl_sys`; a cell that turn schedules waits in `tl_next`.
+thread_local ActorSystem* tl_sys = nullptr;
+thread_local bool tl_in_turn = false;
+thread_local std::shared_ptr<ActorCell> tl_next;
+
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#else
+  std::this_thread::yield();
+#endif
+}
 
 // Timed condition-variable waits go through system_clock deadlines: libstdc++ implements
 // steady_clock waits with pthread_cond_clockwait, which ThreadSanitizer (GCC 11) does not
@@ -294,6 +309,9 @@ ActorSystem::ActorSystem(std::string name, Mode mode, int threads, int throughpu
     // wake-up per hop costs more than the hop itself.
     spin_us_ = 50;
     if (const char* e = std::getenv("MXAR_DISPATCH_SPIN_US")) spin_us_ = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("MXAR_DISPATCH_NOTIFY")) notify_always_ = std::string(e) == "always";
+    if (const char* e = std::getenv("MXAR_DISPATCH_LIFO")) lifo_ = std::atoi(e) != 0;
+    if (const char* e = std::getenv("MXAR_DISPATCH_YIELD")) spin_yield_ = std::atoi(e) != 0;
     int n = threads > 0 ? threads : std::max(2u, std::min(8u, std::thread::hardware_concurrency()));
     for (int i = 0; i < n; ++i) threads_.emplace_back([this] { worker_loop(); });
     timer_thread_ = std::thread([this] { timer_loop(); });
@@ -374,12 +392,32 @@ void ActorSystem::remove_cell(const std::string& path) {
 
 void ActorSystem::schedule(const std::shared_ptr<ActorCell>& cell) {
   if (cell->scheduled_.exchange(true)) return;
+  if (lifo_ && tl_in_turn && tl_sys == this) {
+    // scheduled by an actor turn on this dispatcher: run it next here; a cell already in the
+    // slot goes to the run queue (for any idle thread to take)
+    std::shared_ptr<ActorCell> prev = std::move(tl_next);
+    tl_next = cell;
+    if (!prev) return;
+    return enqueue(prev);
+  }
+  enqueue(cell);
+}
+
+void ActorSystem::enqueue(const std::shared_ptr<ActorCell>& cell) {
+  size_t queued;
   {
     std::lock_guard<std::mutex> g(rq_mu_);
     runq_.push_back(cell);
-    runq_len_.store(runq_.size(), std::memory_order_release);
+    queued = runq_.size();
+    runq_len_.store(queued, std::memory_order_release);
   }
-  rq_cv_.notify_one();
+  // A spinning dispatcher takes the cell without a wake-up: the futex syscall of notify_one
+  // would sit on the sender's critical path (every hop of a protocol round). No lost wake-up:
+  // a spinner decrements spinning_ BEFORE it locks rq_mu_ and tests the queue, so either it
+  // sees this push under the lock, or the push came later and this load sees it gone.
+  // (One spinner per queued cell: with fewer, a sleeper is woken so that cells queued
+  // back to back - a Start to every worker - still run in parallel.)
+  if (notify_always_ || static_cast<size_t>(spinning_.load(std::memory_order_seq_cst)) < queued) rq_cv_.notify_one();
 }
 
 void ActorSystem::record_exception(std::exception_ptr e) {
@@ -415,15 +453,29 @@ size_t ActorSystem::run_until_idle(size_t max_messages) {
 }
 
 void ActorSystem::worker_loop() {
+  tl_sys = this;
   while (true) {
     std::shared_ptr<ActorCell> cell;
-    if (spin_us_ > 0 && runq_len_.load(std::memory_order_acquire) == 0) {
-      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us_);
-      while (runq_len_.load(std::memory_order_acquire) == 0 && !shutdown_.load() &&
-             std::chrono::steady_clock::now() < until)
-        std::this_thread::yield();
-    }
-    {
+    if (tl_next) {  // the run-next slot: still counted busy since the turn that filled it
+      cell = std::move(tl_next);
+      tl_next.reset();
+    } else {
+      if (spin_us_ > 0 && runq_len_.load(std::memory_order_acquire) == 0) {
+        // Idle spin: pause-based polling (a hop costs ~0.1 us to notice), yielding the core
+        // every ~32 polls so that an oversubscribed host still runs everyone.
+        spinning_.fetch_add(1, std::memory_order_seq_cst);
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us_);
+        for (unsigned i = 1; runq_len_.load(std::memory_order_acquire) == 0 && !shutdown_.load() &&
+                             std::chrono::steady_clock::now() < until;
+             ++i) {
+          if (spin_yield_ || (i & 31) == 0) {
+            std::this_thread::yield();
+          } else {
+            for (int k = 0; k < 8; ++k) cpu_relax();
+          }
+        }
+        spinning_.fetch_sub(1, std::memory_order_seq_cst);
+      }
       std::unique_lock<std::mutex> lk(rq_mu_);
       rq_cv_.wait(lk, [&] { return shutdown_.load() || !runq_.empty(); });
       if (shutdown_) return;
@@ -432,12 +484,21 @@ void ActorSystem::worker_loop() {
       runq_len_.store(runq_.size(), std::memory_order_release);
       ++busy_;
     }
+    tl_in_turn = true;
     size_t n = cell->process(static_cast<size_t>(throughput_));
+    tl_in_turn = false;
     cell->scheduled_.store(false);
-    // Re-check after clearing the flag: a message may have arrived in between.
+    // Re-check after clearing the flag: a message may have arrived in between (to the run
+    // queue, not the run-next slot: a busy actor must not monopolise this thread).
     if (!cell->stopped() && cell->has_mail()) schedule(cell);
     delivered_.fetch_add(n, std::memory_order_relaxed);
-    {
+    if (tl_next && shutdown_.load()) {
+      // shutting down: the slot's cell goes back to the queue (cleared by shutdown())
+      std::shared_ptr<ActorCell> c = std::move(tl_next);
+      tl_next.reset();
+      enqueue(c);
+    }
+    if (!tl_next) {
       std::lock_guard<std::mutex> g(rq_mu_);
       --busy_;
       if (busy_ == 0 && runq_.empty()) idle_cv_.notify_all();
