@@ -10,7 +10,10 @@
 #include <sys/uio.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 
@@ -59,7 +62,10 @@ bool write_frame(int fd, const void* p, uint32_t n) {
 // Scatter/Reduce burst arrives together), instead of two recv() calls per frame.
 class FrameReader {
  public:
-  explicit FrameReader(int fd) : fd_(fd), buf_(64 << 10) {}
+  // spin_us > 0: before blocking in recv(), poll the socket (non-blocking recv) for up to
+  // spin_us after the previous frame - a protocol round's next Start / Complete arrives within
+  // one round, and a blocked reader's wake-up costs several microseconds per hop
+  explicit FrameReader(int fd, int spin_us = 0) : fd_(fd), buf_(64 << 10), spin_us_(spin_us) {}
   // Next frame's payload (valid until the next call); false at EOF / error / bad length.
   bool next(const uint8_t** p, uint32_t* n) {
     if (!fill(4)) return false;
@@ -82,7 +88,18 @@ class FrameReader {
         head_ = 0;
       }
       if (buf_.size() < need) buf_.resize(need);
-      const ssize_t k = ::recv(fd_, buf_.data() + tail_, buf_.size() - tail_, 0);
+      ssize_t k = -1;
+      if (spin_us_ > 0) {
+        const auto until = last_ + std::chrono::microseconds(spin_us_);
+        do {
+          k = ::recv(fd_, buf_.data() + tail_, buf_.size() - tail_, MSG_DONTWAIT);
+          if (k >= 0 || (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)) break;
+          for (int i = 0; i < 16; ++i) __builtin_ia32_pause();
+        } while (Clock::now() < until);
+      }
+      if (k < 0 && (spin_us_ <= 0 || errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR))
+        k = ::recv(fd_, buf_.data() + tail_, buf_.size() - tail_, 0);
+      last_ = Clock::now();
       if (k == 0) return false;
       if (k < 0) {
         if (errno == EINTR) continue;
@@ -95,7 +112,17 @@ class FrameReader {
   int fd_;
   std::vector<uint8_t> buf_;
   size_t head_ = 0, tail_ = 0;
+  int spin_us_ = 0;
+  Clock::time_point last_ = Clock::now();
 };
+
+int tcp_spin_us() {
+  static const int v = [] {
+    const char* e = std::getenv("MXAR_TCP_SPIN_US");
+    return e ? std::max(0, std::atoi(e)) : 0;
+  }();
+  return v;
+}
 
 int connect_with_timeout(const std::string& host, int port, double timeout_s) {
   addrinfo hints{}, *res = nullptr;
@@ -274,7 +301,7 @@ void ClusterNode::accept_loop() {
 }
 
 void ClusterNode::reader_loop(int fd) {
-  FrameReader in(fd);
+  FrameReader in(fd, tcp_spin_us());
   while (!stopping_.load()) {
     const uint8_t* data = nullptr;
     uint32_t len = 0;

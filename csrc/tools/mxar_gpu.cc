@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 
 #include <memory>
+#include <mutex>
+#include <vector>
 #include <stdexcept>
 #include <string>
 
@@ -19,8 +21,22 @@
 namespace mxar {
 
 
+namespace {
+// Round inputs of the iota source: a few device buffers reused round after round. A buffer
+// comes back when the plane drops the round's input (after the round's completion word), and
+// the next fill of it is ordered behind that round's kernel anyway: fills run on the plane's
+// own stream, so no event and no allocator call sits on the round path.
+struct InputPool {
+  std::mutex mu;
+  std::vector<void*> free;
+  ~InputPool() {
+    for (void* p : free) (void)hipFree(p);
+  }
+};
+}  // namespace
+
 GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag, int grid, double timeout_s,
-                               int64_t min_chunk) {
+                               int64_t min_chunk, bool static_source) {
   XgmiPlaneOptions o;
   o.device = device;
   o.dtype = DType::F32;
@@ -31,20 +47,41 @@ GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag,
   o.timeout_s = timeout_s;
   o.min_chunk = min_chunk;
   GpuWorkerParts p;
-  p.plane = make_xgmi_plane(o);
-  hipStream_t s = nullptr;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
-    throw std::runtime_error("mxar-gpu: cannot create a stream on device " + std::to_string(device));
-  // every round's input: a stream-ordered buffer filled by the fill_iota kernel, released
-  // (stream-ordered) once the plane no longer holds it; the ready event orders the round
-  p.source = [device, size, s](const AllReduceInputRequest& r) {
+  auto plane = make_xgmi_plane(o);
+  p.plane = plane;
+  const hipStream_t s = plane->stream();
+  const size_t bytes = static_cast<size_t>(size) * sizeof(float);
+  if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("mxar-gpu: no device " + std::to_string(device));
+  if (static_source) {
+    // --source static: data[i] = i, filled once - the same buffer every round (the bench's
+    // tensor dataSource; isolates the engine from the per-round fill)
     void* mem = nullptr;
-    if (hipMallocAsync(&mem, static_cast<size_t>(size) * sizeof(float), s) != hipSuccess)
-      throw std::runtime_error("mxar-gpu: hipMallocAsync failed");
+    if (hipMalloc(&mem, bytes) != hipSuccess) throw std::runtime_error("mxar-gpu: hipMalloc failed");
+    launch_fill_iota(mem, size, 0.0, DType::F32, s);
+    std::shared_ptr<void> owner(mem, [](void* q) { (void)hipFree(q); });
+    auto payload = std::make_shared<DevicePayload>(owner, 0, static_cast<size_t>(size), device, s, nullptr, 0);
+    p.source = [payload](const AllReduceInputRequest&) { return AllReduceInput{payload}; };
+    return p;
+  }
+  // the demo source (AllreduceWorker.scala:272-301): data[i] = i + iteration, produced by the
+  // fill_iota kernel on the plane's stream into a pooled buffer
+  auto pool = std::make_shared<InputPool>();
+  p.source = [device, size, s, bytes, pool](const AllReduceInputRequest& r) {
+    void* mem = nullptr;
+    {
+      std::lock_guard<std::mutex> g(pool->mu);
+      if (!pool->free.empty()) {
+        mem = pool->free.back();
+        pool->free.pop_back();
+      }
+    }
+    if (mem == nullptr && hipMalloc(&mem, bytes) != hipSuccess) throw std::runtime_error("mxar-gpu: hipMalloc failed");
     launch_fill_iota(mem, size, static_cast<double>(r.iteration), DType::F32, s);
-    std::shared_ptr<void> owner(mem, [s](void* q) { (void)hipFreeAsync(q, s); });
-    return AllReduceInput{std::make_shared<DevicePayload>(owner, 0, static_cast<size_t>(size), device, s,
-                                                          record_ready(s), 0)};
+    std::shared_ptr<void> owner(mem, [pool](void* q) {
+      std::lock_guard<std::mutex> g(pool->mu);
+      pool->free.push_back(q);
+    });
+    return AllReduceInput{std::make_shared<DevicePayload>(owner, 0, static_cast<size_t>(size), device, s, nullptr, 0)};
   };
   return p;
 }

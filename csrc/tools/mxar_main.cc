@@ -73,6 +73,7 @@ struct Options {
   int max_peers = 8, plane_max_lag = 4, grid = 0;
   double plane_timeout_s = 60.0;
   int64_t min_chunk = 0;  // --min-chunk N: one flag per chunk of >= N elements (0: 1 KiB)
+  bool static_source = false;  // --source static: the same input every round (default iota: i + iteration)
 };
 
 [[noreturn]] void usage(const char* msg) {
@@ -84,7 +85,7 @@ struct Options {
                "master control bridge (docs/BRIDGE.md): --bridge PORT [--external-rounds]\n"
                "       mxar drive [host:]bridgePort [rounds] [--lockstep]   (bridge client)\n"
                "worker on a GPU (mxar-gpu): --device K [--max-peers N --plane-max-lag N --grid N --plane-timeout S\n"
-               "                              --min-chunk N]\n",
+               "                              --min-chunk N --source iota|static]\n",
                msg);
   std::exit(2);
 }
@@ -119,6 +120,11 @@ Options parse(int argc, char** argv) {
     else if (a == "--grid") o.grid = std::stoi(val());
     else if (a == "--plane-timeout") o.plane_timeout_s = std::stod(val());
     else if (a == "--min-chunk") o.min_chunk = std::stoll(val());
+    else if (a == "--source") {
+      const std::string v = val();
+      if (v != "iota" && v != "static") usage("--source must be iota or static");
+      o.static_source = v == "static";
+    }
     else if (a.rfind("--", 0) == 0) usage(("unknown option " + a).c_str());
     else o.positional.push_back(a);
   }
@@ -231,7 +237,7 @@ void set_level(const std::string& l) {
   if (o.device >= 0) {  // the round engine on a GPU: one threshold-kernel launch per round
     if (make_gpu_worker == nullptr) usage("--device needs the GPU build of this executable: mxar-gpu");
     GpuWorkerParts g = make_gpu_worker(o.device, size, o.max_peers, o.plane_max_lag, o.grid, o.plane_timeout_s,
-                                         o.min_chunk);
+                                         o.min_chunk, o.static_source);
     cc.meta = g.plane->descriptor();  // relayed by the master in InitWorkers.planes
     sys->actor_of(std::make_unique<PlaneWorkerActor>(g.source, sink, g.plane), "worker");
   } else {

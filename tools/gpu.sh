@@ -79,22 +79,27 @@ case $task in
     done
     ;;
   native)
+    # NATIVE_SOURCE=iota|static (per-round demo fill, or the same input every round),
+    # NATIVE_GRID (workgroups per worker; 256 = half the GPU each, as in-process planes split it)
     sizes=("$@")
     [ ${#sizes[@]} -eq 0 ] && sizes=(262144 16777216 67108864)
+    src=${NATIVE_SOURCE:-iota}
+    grid=${NATIVE_GRID:-256}
     X=akka_allreduce_1_amd
     for n in "${sizes[@]}"; do
       port=$((20000 + RANDOM % 20000))
       seeds="--seeds mxar.tcp://ClusterSystem@127.0.0.1:$port --loglevel ERROR --quiet"
-      timeout -k 5 150 $X/mxar-gpu worker 0 $n --device 0 --max-peers 2 --plane-timeout 20 $seeds > $O/w0.log 2>&1 &
+      wopt="--device 0 --max-peers 2 --plane-timeout 20 --grid $grid --source $src"
+      timeout -k 5 150 $X/mxar-gpu worker 0 $n $wopt $seeds > $O/w0.log 2>&1 &
       w0=$!
-      timeout -k 5 150 $X/mxar-gpu worker 0 $n --device 0 --max-peers 2 --plane-timeout 20 $seeds > $O/w1.log 2>&1 &
+      timeout -k 5 150 $X/mxar-gpu worker 0 $n $wopt $seeds > $O/w1.log 2>&1 &
       w1=$!
-      timeout -k 10 120 $X/mxar master $port 2 $n $((n / 256)) --th-reduce 1 --th-complete 1 --max-lag 2 \
-        --max-round 399 $seeds > $O/m.log 2>&1
+      timeout -k 10 120 $X/mxar master $port 2 $n $((n > 524288 ? n / 512 : 1024)) --th-reduce 1 --th-complete 1 \
+        --max-lag 1 --max-round 399 $seeds > $O/m.log 2>&1
       rc=$?
       wait $w0; r0=$?
       wait $w1; r1=$?
-      echo "{\"n_f32\": $n, \"master\": $(grep steady $O/m.log || echo null)}" | tee -a $O/native_rates.jsonl
+      echo "{\"n_f32\": $n, \"source\": \"$src\", \"grid\": $grid, \"master\": $(grep steady $O/m.log || echo null)}" | tee -a $O/native_rates.jsonl
       [ $rc -eq 0 ] && [ $r0 -eq 0 ] && [ $r1 -eq 0 ] || { echo "failed rc=$rc,$r0,$r1"; tail -5 $O/*.log; exit 1; }
     done
     ;;
