@@ -391,7 +391,11 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                 # 1024 tokens make the weight-gradient GEMMs (K = tokens) nearly bandwidth bound,
                 # so a bandwidth-bound allreduce beside them slows them; at a training-size
                 # 8192 tokens per GPU they are compute bound
-                variants += [("tokens8192_grid256", 256, True, True, 8192), ("tokens8192_serial", 512, False, True, 8192)]
+                # compute-bound backward: a small comm grid stretches the allreduces over the
+                # backward instead of contending with it at full bandwidth
+                variants += [("tokens8192_grid256", 256, True, True, 8192), ("tokens8192_serial", 512, False, True, 8192),
+                             ("tokens8192_grid32", 32, True, True, 8192), ("tokens8192_grid64", 64, True, True, 8192),
+                             ("tokens8192_grid128", 128, True, True, 8192)]
             for name, grid, ov, hi, tokens in variants:
                 cell: dict = {"tokens": tokens}
                 try:

@@ -477,6 +477,13 @@ void bind_hip(py::module_& m) {
       },
       py::arg("dst"), py::arg("n"), py::arg("offset"), py::arg("dtype"), py::arg("stream") = 0);
   h.def(
+      "clock_probe",
+      [](uintptr_t out, int samples, uint64_t interval_ticks, uintptr_t s) {
+        launch_clock_probe(reinterpret_cast<uint64_t*>(out), samples, interval_ticks, as_stream(s));
+      },
+      py::arg("out"), py::arg("samples"), py::arg("interval_ticks"), py::arg("stream") = 0,
+      "study tool: one wave samples (s_memtime, s_memrealtime) every interval_ticks (100 MHz) into out[2 * samples]");
+  h.def(
       "fill_uniform",
       [](uintptr_t dst, int64_t n, uint64_t seed, DType dt, uintptr_t s) {
         launch_fill_uniform(as_ptr(dst), n, seed, dt, as_stream(s));

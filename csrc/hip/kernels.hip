@@ -235,6 +235,33 @@ void launch_fill_uniform(void* dst, int64_t n, uint64_t seed, DType dt, hipStrea
   hip_check(hipGetLastError(), "fill_uniform launch");
 }
 
+// Clock probe (study tool, tools/overlap_trace.py): ONE wave samples the shader-clock counter
+// (s_memtime, counts core clock cycles - power management moves it) against the constant
+// 100 MHz counter (s_memrealtime) every `interval` ticks, `samples` times, into
+// out[2 * i] / out[2 * i + 1]. Sharing the GPU with other work it reports the core clock
+// that work ran at; it exits after `samples` samples (bounded: samples x interval ticks).
+__global__ __launch_bounds__(64) void clock_probe_kernel(uint64_t* out, int samples, uint64_t interval) {
+  if (threadIdx.x != 0) return;
+  uint64_t next = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < samples; ++i) {
+    uint64_t rt;
+    do {
+      __builtin_amdgcn_s_sleep(2);
+      rt = __builtin_amdgcn_s_memrealtime();
+    } while (rt < next);
+    const uint64_t ct = __builtin_amdgcn_s_memtime();
+    out[2 * i] = ct;
+    out[2 * i + 1] = rt;
+    next = rt + interval;
+  }
+}
+
+void launch_clock_probe(uint64_t* out, int samples, uint64_t interval_ticks, hipStream_t stream) {
+  if (samples <= 0) return;
+  hipLaunchKernelGGL(clock_probe_kernel, dim3(1), dim3(64), 0, stream, out, samples, interval_ticks);
+  hip_check(hipGetLastError(), "clock_probe launch");
+}
+
 // Plain device copy, 16 B per lane (used for the 1-rank allreduce: a kernel keeps the copy
 // in stream order with the kernels around it, with no DMA-engine hand-off).
 // Variants (A/B study, tools/bench_copy.py): UNROLL packs in flight per lane, NT = nontemporal

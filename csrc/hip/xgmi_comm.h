@@ -315,6 +315,7 @@ void launch_reduce_slots(const void* slots, int64_t slot_stride_elems, int nslot
                          float scale, hipStream_t stream);
 // dst[i] = (float)(i + offset) (reference data source AllreduceWorker.scala:285-291)
 void launch_fill_iota(void* dst, int64_t n, double offset, DType dt, hipStream_t stream);
+void launch_clock_probe(uint64_t* out, int samples, uint64_t interval_ticks, hipStream_t stream);
 // dst[i] = uniform(-1, 1) from a counter-based hash of (seed, i)
 void launch_fill_uniform(void* dst, int64_t n, uint64_t seed, DType dt, hipStream_t stream);
 // dst[0:bytes) = src[0:bytes) as a kernel (16-B aligned)

@@ -6,6 +6,10 @@
 // produced by the fill_iota kernel - no Python anywhere in the round path.
 #include <hip/hip_runtime.h>
 
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -50,6 +54,36 @@ GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag,
   auto plane = make_xgmi_plane(o);
   p.plane = plane;
   const hipStream_t s = plane->stream();
+  if (const char* path = std::getenv("MXAR_PLANE_STAMPS")) {
+    // study knob: phase stamps of this worker's round kernels (kPhaseSlots u64 per workgroup,
+    // s_memrealtime - one clock for every process on the GPU), the last round's written as one
+    // JSON line to `path` when the job ends (tools/native_stamps.py)
+    constexpr int64_t kSlots = 2048;
+    uint64_t* buf = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&buf), kSlots * 8 * sizeof(uint64_t)) != hipSuccess ||
+        hipMemset(buf, 0, kSlots * 8 * sizeof(uint64_t)) != hipSuccess)
+      throw std::runtime_error("mxar-gpu: stamps buffer");
+    plane->set_phase_stamps(buf, kSlots);
+    const std::string out = path;
+    p.at_exit = [buf, out, device]() {
+      std::vector<uint64_t> h(kSlots * 8);
+      (void)hipSetDevice(device);
+      if (hipMemcpy(h.data(), buf, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return;
+      if (FILE* f = std::fopen(out.c_str(), "a")) {
+        std::fprintf(f, "{\"pid\": %d, \"stamps\": [", static_cast<int>(getpid()));
+        bool first = true;
+        for (int64_t w = 0; w < kSlots; ++w) {
+          if (h[w * 8] == 0) continue;
+          std::fprintf(f, "%s[", first ? "" : ",");
+          for (int k = 0; k < 8; ++k) std::fprintf(f, "%s%llu", k ? "," : "", static_cast<unsigned long long>(h[w * 8 + k]));
+          std::fprintf(f, "]");
+          first = false;
+        }
+        std::fprintf(f, "]}\n");
+        std::fclose(f);
+      }
+    };
+  }
   const size_t bytes = static_cast<size_t>(size) * sizeof(float);
   if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("mxar-gpu: no device " + std::to_string(device));
   if (static_source) {

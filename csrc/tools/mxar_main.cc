@@ -16,6 +16,7 @@
 //   mxar-gpu worker ... --device K   (the same executable linked with csrc/tools/mxar_gpu.cc)
 //       the worker's rounds run on GPU K: an XgmiRoundPlane under a PlaneWorkerActor, the
 //       source filled on the device. Workers on one node exchange through the xGMI arena.
+#include <functional>
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -234,11 +235,13 @@ void set_level(const std::string& l) {
     }
   };
   ClusterConfig cc;
+  std::function<void()> gpu_at_exit;
   if (o.device >= 0) {  // the round engine on a GPU: one threshold-kernel launch per round
     if (make_gpu_worker == nullptr) usage("--device needs the GPU build of this executable: mxar-gpu");
     GpuWorkerParts g = make_gpu_worker(o.device, size, o.max_peers, o.plane_max_lag, o.grid, o.plane_timeout_s,
                                          o.min_chunk, o.static_source);
     cc.meta = g.plane->descriptor();  // relayed by the master in InitWorkers.planes
+    gpu_at_exit = g.at_exit;
     sys->actor_of(std::make_unique<PlaneWorkerActor>(g.source, sink, g.plane), "worker");
   } else {
     sys->actor_of(std::make_unique<WorkerActor>(src, sink), "worker");
@@ -261,6 +264,7 @@ void set_level(const std::string& l) {
     if (saw_master && !master_up) break;  // the master left: the job is over
     std::this_thread::sleep_for(std::chrono::milliseconds(20));
   }
+  if (gpu_at_exit) gpu_at_exit();
   std::printf("[mxar worker] %d rounds completed\n", rounds.load());
   std::fflush(stdout);
   node->leave();

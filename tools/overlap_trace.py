@@ -65,19 +65,51 @@ def run(a) -> None:
         reducer.wait()
         torch._foreach_add_(params, grads, alpha=-1e-3)
 
+    from akka_allreduce_1_amd._native import C
+
     out = {"model": a.model, "layers": a.layers, "tokens": a.tokens, "grid": a.grid, "buckets": len(reducer.buckets),
            "bucket_bytes": [b.nbytes for b in reducer.buckets][:4]}
+    probe_stream = torch.cuda.Stream(device=dev)
+    interval = 5000  # 50 us at 100 MHz
+
+    def clock_mhz(samples: torch.Tensor, dur_s: float) -> float | None:
+        """Median shader clock over the samples inside the phase's first 90 %."""
+        v = samples.view(-1, 2).cpu().tolist()
+        v = [x for x in v if x[1] > 0]
+        if len(v) < 3:
+            return None
+        t_end = v[0][1] + 0.9 * dur_s * 1e8
+        f = [(v[i + 1][0] - v[i][0]) / (v[i + 1][1] - v[i][1]) * 100.0 for i in range(len(v) - 1)
+             if v[i + 1][1] <= t_end and v[i + 1][1] > v[i][1]]
+        return round(statistics.median(f), 1) if f else None
+
     with torch.no_grad():
-        for fn in (compute, overlap, serial):  # warm-up outside the phases
+        est = {}
+        for name, fn in (("A", compute), ("B", overlap), ("C", serial)):  # warm-up outside the phases
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
             fn()
+            torch.cuda.synchronize()
+            est[name] = time.perf_counter() - t0
         torch.cuda.synchronize()
+        # the idle clock: the probe alone
+        buf = torch.zeros(2 * 200, dtype=torch.int64, device=dev)
+        C.hip.clock_probe(buf.data_ptr(), 200, interval, probe_stream.cuda_stream)
+        torch.cuda.synchronize()
+        out["idle_clock_mhz"] = clock_mhz(buf, 200 * interval / 1e8)
         for name, fn in (("A", compute), ("B", overlap), ("C", serial)):
             time.sleep(0.02)
+            n = int(est[name] * a.reps * 1.2 * 1e8 / interval) + 4
+            buf = torch.zeros(2 * n, dtype=torch.int64, device=dev)
+            C.hip.clock_probe(buf.data_ptr(), n, interval, probe_stream.cuda_stream)
             t0 = time.perf_counter()
             for _ in range(a.reps):
                 fn()
-            torch.cuda.synchronize()
-            out[f"{name}_wall_ms_per_step"] = round((time.perf_counter() - t0) / a.reps * 1e3, 3)
+            torch.cuda.current_stream(dev).synchronize()  # the phase (its comm joined in), not the probe
+            dur = time.perf_counter() - t0
+            probe_stream.synchronize()
+            out[f"{name}_wall_ms_per_step"] = round(dur / a.reps * 1e3, 3)
+            out[f"{name}_clock_mhz"] = clock_mhz(buf, dur)
     comm.check()
     print(json.dumps(out), flush=True)
 
