@@ -75,7 +75,21 @@ struct Options {
   double plane_timeout_s = 60.0;
   int64_t min_chunk = 0;  // --min-chunk N: one flag per chunk of >= N elements (0: 1 KiB)
   bool static_source = false;  // --source static: the same input every round (default iota: i + iteration)
+  int spin_us = -1;  // --spin-us N: dispatcher idle spin + cluster reader socket poll (-1: built-in defaults)
 };
+
+// --spin-us: how long an idle actor dispatcher and a cluster reader keep polling before they
+// sleep. A GPU round leaves every host thread idle for the kernel's duration; past the spin
+// they sleep, and each hop of the next round (Complete, Start: two TCP frames, two actor
+// turns) then pays a wake-up. 500 us covers a 256 MiB round: native 64 MiB rounds 176-198 ->
+// 152-160 us, the in-process engine's time (profiles/round3/native_spin_ab.jsonl). Costs a
+// core per spinning thread while rounds run. An explicit MXAR_* environment variable wins.
+void apply_spin(int us) {
+  if (us < 0) return;
+  const std::string v = std::to_string(us);
+  setenv("MXAR_DISPATCH_SPIN_US", v.c_str(), 0);
+  setenv("MXAR_TCP_SPIN_US", v.c_str(), 0);
+}
 
 [[noreturn]] void usage(const char* msg) {
   std::fprintf(stderr,
@@ -86,7 +100,8 @@ struct Options {
                "master control bridge (docs/BRIDGE.md): --bridge PORT [--external-rounds]\n"
                "       mxar drive [host:]bridgePort [rounds] [--lockstep]   (bridge client)\n"
                "worker on a GPU (mxar-gpu): --device K [--max-peers N --plane-max-lag N --grid N --plane-timeout S\n"
-               "                              --min-chunk N --source iota|static]\n",
+               "                              --min-chunk N --source iota|static]\n"
+               "host threads: --spin-us N (dispatcher + socket polling; GPU workers default 500)\n",
                msg);
   std::exit(2);
 }
@@ -121,6 +136,7 @@ Options parse(int argc, char** argv) {
     else if (a == "--grid") o.grid = std::stoi(val());
     else if (a == "--plane-timeout") o.plane_timeout_s = std::stod(val());
     else if (a == "--min-chunk") o.min_chunk = std::stoll(val());
+    else if (a == "--spin-us") o.spin_us = std::stoi(val());
     else if (a == "--source") {
       const std::string v = val();
       if (v != "iota" && v != "static") usage("--source must be iota or static");
@@ -158,6 +174,7 @@ void set_level(const std::string& l) {
   mp.maxChunkSize = chunk;
   mp.roundTimeoutMs = o.round_timeout_ms;
   mp.externalRounds = o.external_rounds;
+  apply_spin(o.spin_us);
   auto sys = std::make_shared<ActorSystem>("ClusterSystem", ActorSystem::Mode::Threaded, 2);
   std::atomic<int> finished{-1};
   const auto t0 = std::chrono::steady_clock::now();
@@ -215,6 +232,7 @@ void set_level(const std::string& l) {
 [[noreturn]] void run_worker(const Options& o) {
   const int port = pos_int(o, 0, 2553);
   const int size = pos_int(o, 1, 10);
+  apply_spin(o.spin_us >= 0 ? o.spin_us : o.device >= 0 ? 500 : -1);  // a GPU worker polls through its rounds
   auto sys = std::make_shared<ActorSystem>("ClusterSystem", ActorSystem::Mode::Threaded, 2);
   DataSource src = [size](const AllReduceInputRequest& r) {  // AllreduceWorker.scala:285-291
     std::vector<float> v(size);

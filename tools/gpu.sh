@@ -95,7 +95,7 @@ case $task in
       timeout -k 5 150 $X/mxar-gpu worker 0 $n $wopt $seeds > $O/w1.log 2>&1 &
       w1=$!
       timeout -k 10 120 $X/mxar master $port 2 $n $((n > 524288 ? n / 512 : 1024)) --th-reduce 1 --th-complete 1 \
-        --max-lag 1 --max-round 399 $seeds > $O/m.log 2>&1
+        --max-lag 1 --max-round 399 --spin-us ${NATIVE_MASTER_SPIN:-500} $seeds > $O/m.log 2>&1
       rc=$?
       wait $w0; r0=$?
       wait $w1; r1=$?
