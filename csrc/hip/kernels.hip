@@ -36,7 +36,8 @@ static int grid_for(int64_t packs) {
 // P is a template parameter for 2..8 slots so every slot's loads of a tile are issued
 // before the first add (P*U*16 bytes in flight per lane); the sum still runs in peer
 // order 0..P-1. NT bit 0 = nontemporal loads, bit 1 = nontemporal stores (streaming data,
-// no reuse).
+// no reuse), bit 2 = write-through (sc0 sc1) stores - the store probe's fastest copy pairs nt
+// loads with them (tools/store_probe.hip).
 // out may alias one slot row (in-place reduce): every element is read and written by the
 // same lane, loads before the store.
 template <class E, int U, int P, int NT>
@@ -63,7 +64,10 @@ __global__ __launch_bounds__(kThreads) void reduce_slots_static(const char* __re
       for (int p = 0; p < P; ++p) a.add(v[p][u]);
       if (scale != 1.f) a.scale(scale);
       Pack16* d = reinterpret_cast<Pack16*>(out) + base + u * kThreads;
-      if (NT & 2)
+      if (NT & 4)  // sc0 sc1 write-through buffer store (aux 17), offset from the tile's base
+        __builtin_amdgcn_raw_buffer_store_b128(a.pack(), slab_rsrc(out + t * kTile * 16),
+                                               static_cast<int>((threadIdx.x + u * kThreads) * 16), 0, 17);
+      else if (NT & 2)
         __builtin_nontemporal_store(a.pack(), d);
       else
         *d = a.pack();
@@ -170,6 +174,8 @@ static void launch_reduce_typed(int v, int P, const char* s, int64_t stride, cha
       break;
     case 8: launch_static<E, 4, 1>(P, s, stride, o, n, scale, grid(4), st); break;  // NT loads only
     case 9: launch_static<E, 4, 2>(P, s, stride, o, n, scale, grid(4), st); break;  // NT stores only
+    case 10: launch_static<E, 4, 5>(P, s, stride, o, n, scale, grid(4), st); break;  // NT loads, write-through stores
+    case 11: launch_static<E, 8, 5>(P, s, stride, o, n, scale, grid(8), st); break;
     default: launch_static<E, 4, 0>(P, s, stride, o, n, scale, grid(4), st); break;
   }
 }
@@ -321,6 +327,35 @@ __global__ __launch_bounds__(kThreads) void copy_tiles_kernel(const char* __rest
   if (t < bytes) out[t] = in[t];
 }
 
+// Unit variant (round 3, tools/store_probe.hip): every workgroup copies contiguous units of
+// 512 KiB with nt buffer loads (aux 2: the input stream is read once) and sc0 sc1
+// write-through buffer stores (aux 17) - 6.77 TB/s in the store probe against 5.2-5.6 for the
+// plain / nt-store flavours. U packs of 16 B per lane in flight.
+template <int U>
+__global__ __launch_bounds__(kThreads) void copy_units_kernel(const char* __restrict__ in, char* __restrict__ out,
+                                                               int64_t bytes, int64_t unit) {
+  const int64_t nunits = (bytes + unit - 1) / unit;
+  for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+    const char* s = in + u * unit;
+    char* d = out + u * unit;
+    const int64_t len = std::min<int64_t>(unit, bytes - u * unit);
+    const int64_t npk = len / 16;
+    const __amdgpu_buffer_rsrc_t rs = slab_rsrc(s), rd = slab_rsrc(d);
+    int64_t i = threadIdx.x;
+    for (; i + (U - 1) * kThreads < npk; i += U * kThreads) {
+      Pack16 v[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q)
+        v[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>((i + q * kThreads) * 16), 0, 2);
+#pragma unroll
+      for (int q = 0; q < U; ++q)
+        __builtin_amdgcn_raw_buffer_store_b128(v[q], rd, static_cast<int>((i + q * kThreads) * 16), 0, 17);
+    }
+    for (; i < npk; i += kThreads) reinterpret_cast<Pack16*>(d)[i] = reinterpret_cast<const Pack16*>(s)[i];
+    for (int64_t t = npk * 16 + threadIdx.x; t < len; t += kThreads) d[t] = s[t];
+  }
+}
+
 static int g_copy_variant = -1;  // -1: default (see launch_copy)
 
 void set_copy_variant(int v) { g_copy_variant = v; }
@@ -348,6 +383,13 @@ void launch_copy(const void* src, void* dst, int64_t bytes, hipStream_t stream) 
                                stream, s, d, bytes); break;
     case 6: hipLaunchKernelGGL((copy_tiles_kernel<8, false>), dim3(std::min<int64_t>(tiles8, 1024)), dim3(kThreads), 0,
                                stream, s, d, bytes); break;
+    case 7: {
+      const int64_t unit = int64_t{512} << 10;
+      const int64_t units = (bytes + unit - 1) / unit;
+      hipLaunchKernelGGL((copy_units_kernel<8>), dim3(std::min<int64_t>(units, 512)), dim3(kThreads), 0, stream, s, d,
+                         bytes, unit);
+      break;
+    }
     default: hipLaunchKernelGGL((copy_tiles_kernel<4, false>), dim3(tiles4), dim3(kThreads), 0, stream, s, d, bytes);
       break;
   }
