@@ -15,6 +15,13 @@ so this module makes the gradients themselves the flat vectors:
   protocol relies on.
 * `wait()` (end of backward) launches any bucket that never became ready (unused
   parameters), then joins the comm stream into the compute stream.
+* `overlap="auto"`: the first steps try each candidate schedule - buckets beside backward at
+  the communicator's grid, beside backward at 128 workgroups, all after backward - for
+  `tune_steps` steps each, timing first-gradient -> comm joined on the GPU; the ranks agree on
+  the fastest (MAX over ranks of each candidate's best step) and keep it. Sharing the GPU with
+  backward's GEMMs is not free: on one MI355X the serial schedule won at every grid
+  (profiles/round3/README.md, DP overlap at kernel level), while across GPUs the comm is
+  link-bound - the measurement decides, per job.
 
 `comm` is anything with `allreduce_(tensor, op=...)` that runs on the current stream:
 `XgmiCommunicator` (fused xGMI kernels), or `TorchDistComm` (RCCL / gloo; CPU tests).
@@ -92,7 +99,8 @@ class BucketedGradReducer:
     def __init__(self, params: Iterable[torch.nn.Parameter] | torch.nn.Module, comm, *,
                  bucket_bytes: int = 64 << 20, op: str = "avg", overlap: bool = True,
                  first_bucket_bytes: int | None = None, sync: str = "native", event_scope: int = 1,
-                 th_reduce: float = 1.0, th_complete: float = 1.0, rescale: bool = False, algo: str = "auto"):
+                 th_reduce: float = 1.0, th_complete: float = 1.0, rescale: bool = False, algo: str = "auto",
+                 tune_steps: int = 2, schedule_candidates: Sequence[tuple[bool, str]] | None = None):
         """sync: how the comm stream is ordered after backward's gradient writes -
         "native" = reusable HIP events created with `event_scope` (1: device-scope release,
         enough within one GPU; 0: HIP default system-scope), "torch" = torch.cuda events.
@@ -114,7 +122,13 @@ class BucketedGradReducer:
         self.op = op
         self.device = self.params[0].device
         self.on_gpu = self.device.type == "cuda"
-        self.overlap = overlap and self.on_gpu
+        # overlap="auto": schedule tuning (module doc); candidates are (overlap, algo label)
+        self._auto = False
+        self._ev0 = self._ev1 = None
+        self.schedule = ("overlap" if overlap and overlap != "auto" and self.on_gpu else "serial", algo)
+        self.overlap = bool(overlap) and overlap != "auto" and self.on_gpu
+        if overlap == "auto" and self.on_gpu and not self.threshold:
+            self.tune_schedule(tune_steps, schedule_candidates)
         self.stream = comm_stream(self.device) if self.on_gpu else None
         self.sync = sync if self.on_gpu else "none"
         self.buckets = self._build(bucket_bytes, first_bucket_bytes)
@@ -184,6 +198,9 @@ class BucketedGradReducer:
 
     # ------------------------------------------------------------------ hooks
     def _on_grad_ready(self, p: torch.Tensor) -> None:
+        if self._auto and self._ev0 is None:  # first gradient of a tuning step
+            self._ev0 = torch.cuda.Event(enable_timing=True)
+            self._ev0.record()
         b, off, expect = self.slot_of[id(p)]
         g = p.grad
         if g is not None and g.data_ptr() != expect:
@@ -260,6 +277,61 @@ class BucketedGradReducer:
             b.done = None
         self._next = 0
         self.stats["steps"] += 1
+        if self._auto:
+            self._tune_step()
+
+    def tune_schedule(self, tune_steps: int = 2, candidates: Sequence[tuple[bool, str]] | None = None) -> None:
+        """(Re)start schedule tuning: the next len(candidates) x tune_steps steps try each
+        (overlap, algo) candidate; then the fastest (agreed over the ranks) is kept."""
+        if not self.on_gpu or self.threshold:
+            return
+        xgmi = bool(getattr(self.comm, "accepts_stream", False))
+        base = self.schedule[1] if self.schedule else self.algo
+        default = [(True, base), (True, "twoshot@128"), (False, base)] if xgmi else [(True, base), (False, base)]
+        self._cands = list(candidates or default)
+        self._tune_steps = max(1, int(tune_steps))
+        self._times: list[list[float]] = [[] for _ in self._cands]
+        self._step_i = 0
+        self._ev0 = self._ev1 = None
+        self.overlap, self.algo = self._cands[0]
+        self.schedule = None
+        self._auto = True
+
+    def _tune_step(self) -> None:
+        """One step of schedule tuning (overlap="auto"): time it, move to the next candidate,
+        and after the last one agree on the fastest over the ranks and keep it."""
+        if self._ev0 is not None:
+            self._ev1 = torch.cuda.Event(enable_timing=True)
+            self._ev1.record()
+            self._ev1.synchronize()  # tuning steps only: the CPU waits for this step's comm
+            self._times[self._step_i // self._tune_steps].append(self._ev0.elapsed_time(self._ev1))
+        self._ev0 = None
+        self._step_i += 1
+        k = self._step_i // self._tune_steps
+        if k < len(self._cands):
+            self.overlap, self.algo = self._cands[k]
+            return
+        best = torch.tensor([min(t) if t else float("inf") for t in self._times], dtype=torch.float64)
+        try:
+            import torch.distributed as dist
+
+            if dist.is_available() and dist.is_initialized():
+                grp = getattr(self.comm, "cpu_group", None)
+                if grp is not None:  # gloo group of the communicator: a CPU tensor
+                    dist.all_reduce(best, op=dist.ReduceOp.MAX, group=grp)
+                else:
+                    t = best.to(self.device)
+                    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=getattr(self.comm, "group", None))
+                    best = t.cpu()
+        except Exception:  # noqa: BLE001 - no process group: this rank alone decides
+            pass
+        i = int(torch.argmin(best).item())
+        self.overlap, self.algo = self._cands[i]
+        self.schedule = ("overlap" if self.overlap else "serial", self.algo)
+        self.stats["schedule_ms"] = {f"{'overlap' if o else 'serial'}:{a}": round(float(x), 3)
+                                     for (o, a), x in zip(self._cands, best.tolist())}
+        self.stats["schedule"] = f"{self.schedule[0]}:{self.schedule[1]}"
+        self._auto = False
 
     def zero_grad(self) -> None:
         for b in self.buckets:

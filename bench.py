@@ -432,6 +432,20 @@ def dp_step(comm: XgmiCommunicator, model: str, dev) -> dict:
                     overlap()
                 t["step_g128"] = max_over_ranks(timed(overlap, steps, dev), dev) / steps * 1e3
                 reducer.algo = "auto"
+                # every bucket after backward (no overlap)
+                reducer.overlap = False
+                for _ in range(warm):
+                    overlap()
+                t["step_serial"] = max_over_ranks(timed(overlap, steps, dev), dev) / steps * 1e3
+                reducer.overlap = True
+                # the reducer's own choice: one tuning step per candidate schedule, agreed
+                # over the ranks, then the kept schedule timed (ddp.py overlap="auto")
+                reducer.tune_schedule(tune_steps=1)
+                for _ in range(len(reducer._cands)):
+                    overlap()
+                for _ in range(warm):
+                    overlap()
+                t["step_auto"] = max_over_ranks(timed(overlap, steps, dev), dev) / steps * 1e3
         comm.check()
         nbytes = sum(b.nbytes for b in reducer.buckets)
         row = {"params": sum(numel(sh) for _, sh in shapes), "grad_bytes": nbytes, "buckets": len(reducer.buckets),
@@ -446,6 +460,10 @@ def dp_step(comm: XgmiCommunicator, model: str, dev) -> dict:
                            "reducer's host overhead; comm-only time / bandwidth are not measured")
         if "step_g128" in t:
             row["step_ms_twoshot_128wg"] = round(t["step_g128"], 3)
+            row["step_ms_serial"] = round(t["step_serial"], 3)
+            row["step_ms_auto_schedule"] = round(t["step_auto"], 3)
+            row["auto_schedule"] = reducer.stats.get("schedule")
+            row["auto_schedule_tuning_ms"] = reducer.stats.get("schedule_ms")
     except Exception as e:  # noqa: BLE001 - reported, never loses the headline
         row["error"] = repr(e)
     finally:

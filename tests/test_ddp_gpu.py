@@ -31,12 +31,14 @@ def _worker(rank, world, port, q, dtype, mode):
         comm = XgmiCommunicator(device=0, slot_bytes=1 << 20, grid=8, timeout_s=15.0, max_lag=1 if thr else None)
         m, ref = _model(0, dtype), _model(0, dtype)
         red = BucketedGradReducer(m, comm, bucket_bytes=32 << 10, op="avg", rescale=thr,
-                                  algo="auto" if thr else "twoshot@4")
+                                  algo="auto" if thr else "twoshot@4",
+                                  overlap="auto" if mode == "auto" else True, tune_steps=1)
         assert red.threshold == thr
         assert len(red.buckets) >= 3
         g = torch.Generator(device="cuda:0")
         data = [torch.randn(16, 64, device="cuda:0", generator=g.manual_seed(10 + r)).to(dtype) for r in range(world)]
-        for step in range(3):
+        # auto: 3 tuning steps (one per candidate schedule), then the agreed schedule
+        for step in range(6 if mode == "auto" else 3):
             red.zero_grad()
             m(data[rank] * (step + 1)).float().pow(2).mean().backward()
             red.wait()
@@ -52,6 +54,9 @@ def _worker(rank, world, port, q, dtype, mode):
                 tol = (1e-5 if dtype == torch.float32 else 2e-2) * scale
                 err = (p.grad.float() - exp).abs().max().item()
                 assert err <= tol, (step, i, err, tol)
+        if mode == "auto":
+            assert red.schedule is not None and "schedule" in red.stats, red.stats
+            assert len(red.stats["schedule_ms"]) == 3, red.stats
         q.put((rank, True, ""))
     except Exception:  # noqa: BLE001
         import traceback
@@ -61,7 +66,7 @@ def _worker(rank, world, port, q, dtype, mode):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["exact", "threshold"])
+@pytest.mark.parametrize("mode", ["exact", "threshold", "auto"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_ddp_reducer_xgmi_two_processes(dtype, mode):
     from akka_allreduce_1_amd.parallel import free_port
