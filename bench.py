@@ -912,6 +912,10 @@ def main() -> None:
 
             log(rank, "protocol: 40 B / 1 MiB / 64 MiB rounds")
             prot["sizes"] = protocol_sizes(dev)
+            from benchmarks.sections import native_deployment
+
+            log(rank, "protocol: native deployment (mxar master + 2 mxar-gpu processes)")
+            prot["native"] = native_deployment()
         if not cancel():  # the watchdog fired and wrote the line; the process is exiting
             return
         result["protocol"] = prot

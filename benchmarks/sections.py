@@ -299,6 +299,82 @@ def protocol_sizes(dev, cases=((40, torch.float32, 2, 101), (1 << 20, torch.bflo
     return res
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _native_job(n: int, chunk: int, rounds: int, quiet: bool, timeout: float = 60.0) -> tuple[dict | None, list[str]]:
+    """One run of the reference's deployment shape: `mxar master` + 2 `mxar-gpu worker`
+    processes on GPU 0 (static source data[i] = i, 256 workgroups each, host threads polling
+    through the round: --spin-us 500). Returns the master's steady-rate line and the workers'
+    stdout lines."""
+    import json as _json
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "akka_allreduce_1_amd")
+    port = _free_port()
+    seeds = ["--seeds", f"mxar.tcp://ClusterSystem@127.0.0.1:{port}", "--loglevel", "ERROR"]
+    wargs = [os.path.join(exe, "mxar-gpu"), "worker", "0", str(n), "--device", "0", "--max-peers", "2",
+             "--plane-timeout", "20", "--grid", "256", "--source", "static"] + seeds + (["--quiet"] if quiet else [])
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    workers = [subprocess.Popen(wargs, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+               for _ in range(2)]
+    master = None
+    try:
+        master = subprocess.run([os.path.join(exe, "mxar"), "master", str(port), "2", str(n), str(chunk),
+                                 "--th-reduce", "1", "--th-complete", "1", "--max-lag", "1", "--max-round",
+                                 str(rounds - 1), "--spin-us", "500"] + seeds + ["--quiet"],
+                                capture_output=True, text=True, timeout=timeout, env=env)
+        outs = [w.communicate(timeout=timeout)[0] for w in workers]
+    finally:
+        for w in workers:
+            if w.poll() is None:
+                w.kill()
+                w.wait()
+    line = next((ln for ln in master.stdout.splitlines() if "steady_rounds_per_s" in ln), None)
+    return (_json.loads(line) if line else None), [ln for o in outs for ln in o.splitlines()]
+
+
+def native_deployment(cases=((10, 2, 400), (262144, 1024, 400), (16777216, 32768, 400), (67108864, 131072, 200))) -> dict:
+    """The reference's deployment shape on the GPU round engine, Python-free: master + 2 worker
+    PROCESSES sharing GPU 0, arenas IPC-mapped, control over TCP (mxar / mxar-gpu). Per size:
+    a 3-round run printing every worker's output sum and head, checked against the exact f32
+    sum 2 * float(i); then the timed run (mean round interval from the master's barrier
+    stamps). (n, maxChunkSize) = (10, 2) is the reference's default job (AllreduceMaster.scala:
+    111-114)."""
+    import re
+
+    import numpy as np
+
+    res: dict = {"workers": 2, "dtype": "float32", "source": "static data[i] = i (mxar-gpu --source static)",
+                 "host": "--spin-us 500", "grid_per_worker": 256}
+    for n, chunk, rounds in cases:
+        row: dict = {"n_f32": n, "bytes": 4 * n, "max_chunk_size": chunk, "rounds": rounds}
+        try:
+            _, lines = _native_job(n, chunk, 3, quiet=False)
+            exp = float((np.arange(n, dtype=np.float32).astype(np.float64) * 2).sum())
+            sums = [float(m.group(1)) for ln in lines if (m := re.search(r"round \d+ sum (\S+)", ln))]
+            row["validated"] = len(sums) == 6 and all(x == exp for x in sums)
+            if not row["validated"]:
+                row["check"] = {"expected_sum": exp, "seen": sums[:6]}
+            else:
+                st, _ = _native_job(n, chunk, rounds, quiet=True)
+                if st:
+                    row["us_per_round"] = round(1e6 / st["steady_rounds_per_s"], 1)
+                    row["round_interval_p50_us"] = st["round_interval_p50_us"]
+                    row["round_interval_p99_us"] = st["round_interval_p99_us"]
+        except Exception as e:  # noqa: BLE001
+            row["error"] = repr(e)[:300]
+        res[f"{4 * n}B"] = row
+    return res
+
+
 class PairRehearsalComm:
     """A 2-rank data-parallel communicator on ONE GPU for overlap rehearsals: every bucket
     allreduce runs the real 2-rank kernel (LocalCluster, both ranks in one launch) over the
