@@ -141,3 +141,35 @@ def test_native_watchdog_fires_without_the_gil_and_can_be_cancelled():
              "print('survived')\n")
     r = subprocess.run([sys.executable, "-c", code2], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "survived" in r.stdout and "FIRED" not in r.stdout, (r.stdout, r.stderr[-500:])
+
+
+def test_round_breakdown_cuts_rounds_into_hops():
+    """tools/round_breakdown.py: the per-hop intervals of a protocol round from tracer events
+    (synthetic trace: 2 workers, 3 rounds, fixed offsets)."""
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "round_breakdown.py")
+    src = open(path).read()
+    # the module's breakdown() only; skip its GPU-facing imports
+    ns: dict = {}
+    start = src.index("_R = re.compile")
+    end = src.index("def parse_size")
+    exec("import re, statistics\n" + src[start:end], ns)  # noqa: S102 - our own tool's source
+    ev = []
+    for r in range(3):
+        t = 100.0 * r
+        ev.append({"name": f"start r{r}", "ph": "i", "ts": t})
+        for w in range(2):
+            ev += [{"name": f"fetch r{r}", "ph": "X", "ts": t + 2 + w, "dur": 1.0, "args": {"worker": w}},
+                   {"name": f"launch r{r}", "ph": "X", "ts": t + 3 + w, "dur": 4.0, "args": {"worker": w}},
+                   {"name": f"done r{r}", "ph": "i", "ts": t + 40 + w, "args": {"worker": w}},
+                   {"name": f"sink r{r}", "ph": "X", "ts": t + 42 + w, "dur": 1.0, "args": {"worker": w}},
+                   {"name": f"complete r{r}", "ph": "i", "ts": t + 45 + w, "args": {"worker": w}}]
+    out = ns["breakdown"](ev, 2, 0)
+    m = out["median_us"]
+    assert out["rounds"] == 2
+    assert m["round_period"] == 100.0
+    assert m["fetch_launch_host"] == 5.0 and m["launch_to_done"] == 33.0
+    assert m["done_to_sink"] == 2.0 and m["sink"] == 1.0 and m["sink_to_master"] == 2.0
+    assert m["barrier_to_next_start"] == 54.0
+    assert out["span_median_us"]["launch"] == 4.0
