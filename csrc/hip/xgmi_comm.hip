@@ -578,14 +578,15 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   // MI355X (bench.py latency_vs_size, profiles/round3/README.md): the low-latency one-shot
   // wins up to 1 MiB at 2 ranks, 512 KiB at 4 and 256 KiB at 8 (it moves 2x bytes as
   // flag-carrying LL words, so it loses to the plain kernels once they are bandwidth bound);
-  // the one-shot (one hop, every rank reads all P inputs) wins up to 16 MiB at 2 ranks, where
-  // it moves the same bytes as the two-shot with one hand-off less, and up to 4 MiB at 4; at
+  // the one-shot (one hop, every rank reads all P inputs) wins up to 64 MiB at 2 ranks (118 vs
+  // 126 us at 64 MiB), where it moves the same bytes as the two-shot with one hand-off less,
+  // and up to 4 MiB at 4; at
   // 8 ranks the two-shot takes over from the low-latency kernel directly. MXAR_LL_AUTO_MAX / MXAR_ONESHOT_MAX
   // override (bytes).
   const int64_t mib = int64_t{1} << 20;
   ll_auto_max_ = world_ <= 2 ? mib : world_ <= 4 ? mib / 2 : mib / 4;
   if (const char* e = std::getenv("MXAR_LL_AUTO_MAX")) ll_auto_max_ = std::max<int64_t>(0, std::atoll(e));
-  oneshot_max_ = std::min<int64_t>(slot_bytes_, world_ <= 2 ? 16 * mib : world_ <= 4 ? 4 * mib : mib / 4);
+  oneshot_max_ = std::min<int64_t>(slot_bytes_, world_ <= 2 ? 64 * mib : world_ <= 4 ? 4 * mib : mib / 4);
   if (const char* e = std::getenv("MXAR_ONESHOT_MAX")) oneshot_max_ = std::min<int64_t>(slot_bytes_, std::atoll(e));
   if (grid_ <= 0) grid_ = default_grid(device);
   if (const char* f = std::getenv("MXAR_FENCE")) fence_ = std::atoi(f) & 3;
