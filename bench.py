@@ -666,6 +666,8 @@ def main() -> None:
     ap.add_argument("--no-dp", action="store_true", help="skip the ResNet-50 / Llama-3-8B DP-step sections")
     ap.add_argument("--no-local", action="store_true", help="skip the 8-logical-rank section at N = 1")
     ap.add_argument("--no-protocol", action="store_true", help="skip the master/worker protocol-engine section")
+    ap.add_argument("--no-native", action="store_true",
+                    help="skip the native-deployment protocol rounds (child mxar processes; e.g. under a profiler)")
     ap.add_argument("--no-sizes", action="store_true",
                     help="skip the N = 1 size-axis sections (latency_vs_size, reduce_kernel, protocol sizes)")
     ap.add_argument("--protocol-timeout", type=float, default=240.0,
@@ -912,10 +914,11 @@ def main() -> None:
 
             log(rank, "protocol: 40 B / 1 MiB / 64 MiB rounds")
             prot["sizes"] = protocol_sizes(dev)
-            from benchmarks.sections import native_deployment
+            if not args.no_native:
+                from benchmarks.sections import native_deployment
 
-            log(rank, "protocol: native deployment (mxar master + 2 mxar-gpu processes)")
-            prot["native"] = native_deployment()
+                log(rank, "protocol: native deployment (mxar master + 2 mxar-gpu processes)")
+                prot["native"] = native_deployment()
         if not cancel():  # the watchdog fired and wrote the line; the process is exiting
             return
         result["protocol"] = prot

@@ -341,7 +341,8 @@ def _native_job(n: int, chunk: int, rounds: int, quiet: bool, timeout: float = 6
     return (_json.loads(line) if line else None), [ln for o in outs for ln in o.splitlines()]
 
 
-def native_deployment(cases=((10, 2, 400), (262144, 1024, 400), (16777216, 32768, 400), (67108864, 131072, 200))) -> dict:
+def native_deployment(cases=((10, 2, 400), (262144, 1024, 400), (16777216, 32768, 400), (67108864, 131072, 200)),
+                      budget_s: float = 90.0) -> dict:
     """The reference's deployment shape on the GPU round engine, Python-free: master + 2 worker
     PROCESSES sharing GPU 0, arenas IPC-mapped, control over TCP (mxar / mxar-gpu). Per size:
     a 3-round run printing every worker's output sum and head, checked against the exact f32
@@ -354,23 +355,30 @@ def native_deployment(cases=((10, 2, 400), (262144, 1024, 400), (16777216, 32768
 
     res: dict = {"workers": 2, "dtype": "float32", "source": "static data[i] = i (mxar-gpu --source static)",
                  "host": "--spin-us 500", "grid_per_worker": 256}
+    t_end = time.monotonic() + budget_s  # the whole section; a failed size ends it
     for n, chunk, rounds in cases:
         row: dict = {"n_f32": n, "bytes": 4 * n, "max_chunk_size": chunk, "rounds": rounds}
+        left = t_end - time.monotonic()
+        if left < 10:
+            row["error"] = f"skipped: section budget {budget_s:g} s spent"
+            res[f"{4 * n}B"] = row
+            continue
         try:
-            _, lines = _native_job(n, chunk, 3, quiet=False)
+            _, lines = _native_job(n, chunk, 3, quiet=False, timeout=min(30.0, left / 2))
             exp = float((np.arange(n, dtype=np.float32).astype(np.float64) * 2).sum())
             sums = [float(m.group(1)) for ln in lines if (m := re.search(r"round \d+ sum (\S+)", ln))]
             row["validated"] = len(sums) == 6 and all(x == exp for x in sums)
             if not row["validated"]:
                 row["check"] = {"expected_sum": exp, "seen": sums[:6]}
             else:
-                st, _ = _native_job(n, chunk, rounds, quiet=True)
+                st, _ = _native_job(n, chunk, rounds, quiet=True, timeout=min(30.0, max(5.0, t_end - time.monotonic())))
                 if st:
                     row["us_per_round"] = round(1e6 / st["steady_rounds_per_s"], 1)
                     row["round_interval_p50_us"] = st["round_interval_p50_us"]
                     row["round_interval_p99_us"] = st["round_interval_p99_us"]
         except Exception as e:  # noqa: BLE001
             row["error"] = repr(e)[:300]
+            t_end = 0.0  # the shape does not run here (e.g. under a profiler): skip the rest
         res[f"{4 * n}B"] = row
     return res
 

@@ -52,10 +52,13 @@ case $task in
   tests) tests "$@" ;;
   bench) bench "$@" ;;
   prof)
-    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $O/prof -o bench -- python3 bench.py "$@" \
+    # (no native-deployment section: its child processes would run under the profiler too)
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 bench.py --no-native "$@" \
       > $O/prof_bench.json 2> $O/prof_bench.err || { echo "profiled bench failed"; tail -20 $O/prof_bench.err; exit 1; }
     f=$(find $O/prof -name '*kernel_stats.csv' | head -1)
     [ -n "$f" ] && python3 tools/prof_summary.py "${f%_kernel_stats.csv}" "bench.py $*" > $O/prof_summary.md
+    # the raw kernel trace runs to hundreds of MiB (gpurun copies back <= 64 MiB): keep the stats
+    find $O/prof -name '*kernel_trace.csv' -delete
     echo "prof ok"
     ;;
   pmc)
