@@ -227,7 +227,8 @@ class PlaneJob:
 def distributed_plane_job(n: int, source, *, max_chunk_size: int, dtype: torch.dtype, rounds: int,
                           th: float = 1.0, max_lag: int = 1, grid: int = 0, timeout_s: float = 300.0,
                           on_output: Callable | None = None, keep_last: bool = False,
-                          external_client: bool = False, min_chunk: int | None = None) -> dict:
+                          external_client: bool = False, min_chunk: int | None = None,
+                          host_spin_us: int | None = 500) -> dict:
     """One plane worker per torch.distributed rank (one process per GPU), the master on rank 0,
     the reference's cluster shape: workers join rank 0's seed over TCP (127.0.0.1) and
     announce their plane descriptors in the join; the master relays them in InitWorkers and
@@ -238,13 +239,22 @@ def distributed_plane_job(n: int, source, *, max_chunk_size: int, dtype: torch.d
     external_client: the master runs in externalRounds mode with a control bridge and rank 0
     drives the rounds through it as an outside client would (docs/BRIDGE.md, pipelined
     StartAllreduce); "stamps" are then the client's RoundComplete arrival times.
+    host_spin_us: actor dispatchers and cluster readers keep polling this long after their last
+    work before sleeping (MXAR_DISPATCH_SPIN_US / MXAR_TCP_SPIN_US unless already set; the
+    native executables' --spin-us): every TCP hop of a round then lands on a running thread -
+    native 64 MiB rounds 176-198 -> 152-160 us (profiles/round3/native_spin_ab.jsonl).
     Returns (rank 0) {"stamps": round completion times, "state": worker state}."""
+    import os
+
     import torch.distributed as dist
 
     from .parallel.comm import free_port
 
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = torch.cuda.current_device()
+    if host_spin_us is not None and host_spin_us >= 0:  # read when the system / readers start
+        os.environ.setdefault("MXAR_DISPATCH_SPIN_US", str(host_spin_us))
+        os.environ.setdefault("MXAR_TCP_SPIN_US", str(host_spin_us))
     system = C.ActorSystem("ClusterSystem", False)
     if min_chunk is None:  # one flag per reference chunk when maxChunkSize is finer than 1 KiB
         min_chunk = max_chunk_size if max_chunk_size * torch.empty(0, dtype=dtype).element_size() < 1024 else 0

@@ -561,8 +561,11 @@ def protocol_rounds(args, rank: int, world: int, dev) -> dict:
             last = {}
             grid = max(8, 512 // world) if args.share_device else 0
             log(rank, f"protocol: one plane worker per rank, {rounds} rounds of {args.size_mib} MiB")
+            # one GPU per rank: host threads poll through the rounds (--spin-us 500 of the native
+            # executables); ranks sharing one GPU (rehearsal) share the box's few CPUs: no polling
+            spin = None if args.share_device else 500
             res = distributed_plane_job(n, x, max_chunk_size=chunk, dtype=dtype, rounds=rounds,
-                                        grid=grid, keep_last=True, timeout_s=120.0)
+                                        grid=grid, keep_last=True, timeout_s=120.0, host_spin_us=spin)
             if res["last"] is not None and res["last"].iteration == rounds - 1:
                 last["y"] = res["last"].data.clone()
             stamps = res["stamps"]
@@ -599,7 +602,8 @@ def protocol_rounds(args, rank: int, world: int, dev) -> dict:
             if row["validated"]:  # the same job with rounds driven by a control-bridge client on rank 0
                 b: dict = {"driver": "control-bridge client on rank 0, pipelined StartAllreduce (JSON lines over TCP)"}
                 res2 = distributed_plane_job(n, x, max_chunk_size=chunk, dtype=dtype, rounds=rounds, grid=grid,
-                                             keep_last=True, timeout_s=45.0, external_client=True)
+                                             keep_last=True, timeout_s=45.0, external_client=True,
+                                             host_spin_us=spin)
                 ids2 = [None] * world
                 dist.all_gather_object(ids2, res2["state"]["id"])
                 ref2 = torch.zeros(n, device=dev)

@@ -312,6 +312,7 @@ ActorSystem::ActorSystem(std::string name, Mode mode, int threads, int throughpu
     if (const char* e = std::getenv("MXAR_DISPATCH_NOTIFY")) notify_always_ = std::string(e) == "always";
     if (const char* e = std::getenv("MXAR_DISPATCH_LIFO")) lifo_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("MXAR_DISPATCH_YIELD")) spin_yield_ = std::atoi(e) != 0;
+    if (const char* e = std::getenv("MXAR_DISPATCH_SPINNERS")) max_spinners_ = std::max(1, std::atoi(e));
     int n = threads > 0 ? threads : std::max(2u, std::min(8u, std::thread::hardware_concurrency()));
     for (int i = 0; i < n; ++i) threads_.emplace_back([this] { worker_loop(); });
     timer_thread_ = std::thread([this] { timer_loop(); });
@@ -460,18 +461,23 @@ void ActorSystem::worker_loop() {
       cell = std::move(tl_next);
       tl_next.reset();
     } else {
+      // Idle spin, by at most max_spinners_ threads at a time (the rest sleep at once: a cell
+      // queued back to back with another wakes one of them): pause-based polling (a hop costs
+      // ~0.1 us to notice), yielding the core every ~32 polls so that an oversubscribed host
+      // still runs everyone.
+      // (A thread over the cap counts in spinning_ until it decrements, which it does before
+      // it locks rq_mu_ and tests the queue: it takes a cell schedule() did not wake anyone for.)
       if (spin_us_ > 0 && runq_len_.load(std::memory_order_acquire) == 0) {
-        // Idle spin: pause-based polling (a hop costs ~0.1 us to notice), yielding the core
-        // every ~32 polls so that an oversubscribed host still runs everyone.
-        spinning_.fetch_add(1, std::memory_order_seq_cst);
-        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us_);
-        for (unsigned i = 1; runq_len_.load(std::memory_order_acquire) == 0 && !shutdown_.load() &&
-                             std::chrono::steady_clock::now() < until;
-             ++i) {
-          if (spin_yield_ || (i & 31) == 0) {
-            std::this_thread::yield();
-          } else {
-            for (int k = 0; k < 8; ++k) cpu_relax();
+        if (spinning_.fetch_add(1, std::memory_order_seq_cst) < max_spinners_) {
+          const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us_);
+          for (unsigned i = 1; runq_len_.load(std::memory_order_acquire) == 0 && !shutdown_.load() &&
+                               std::chrono::steady_clock::now() < until;
+               ++i) {
+            if (spin_yield_ || (i & 31) == 0) {
+              std::this_thread::yield();
+            } else {
+              for (int k = 0; k < 8; ++k) cpu_relax();
+            }
           }
         }
         spinning_.fetch_sub(1, std::memory_order_seq_cst);

@@ -301,6 +301,7 @@ class ActorSystem {
   // Complete -> master -> Start chain stays on one warm thread (Go's runnext)
   bool lifo_ = true;
   bool spin_yield_ = false;  // MXAR_DISPATCH_YIELD=1: idle spin yields every poll (round-2 form)
+  int max_spinners_ = 2;     // MXAR_DISPATCH_SPINNERS: dispatcher threads spinning at once
   int busy_ = 0;
   std::vector<std::thread> threads_;
   std::atomic<bool> shutdown_{false};
