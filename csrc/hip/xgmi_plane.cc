@@ -88,6 +88,7 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   // A/B knob: 1 = also record an event per round and confirm completion with it (round 2's
   // form; ~2-3 us of hipEventRecord on every launch, profiles/round3/api_cost.json)
   if (const char* e = std::getenv("MXAR_PLANE_EVENTS")) event_confirm_ = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MXAR_PLANE_COARSEN")) coarsen_full_ = std::atoi(e) != 0;  // A/B knob
   const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
   flag_gran_ = o_.min_chunk > 0 ? std::min<int64_t>(XgmiComm::min_chunk_bytes(), o_.min_chunk * es)
                                 : XgmiComm::min_chunk_bytes();
@@ -432,6 +433,31 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
     st_.coarsened++;
     MXAR_LOG(INFO, "plane", "maxChunkSize " << cfg.maxChunkSize << " is finer than the flag table at thresholds 1: "
                                             << "kernel chunks of " << chunk_ << " elements, counts per reference chunk");
+  }
+  // Full thresholds: every contribution and every chunk is taken whatever the chunking, so the
+  // kernel may also run whole multiples of maxChunkSize for speed (counts still reported per
+  // reference chunk). Every kernel chunk costs a flag hand-off and a release per hop, so 2 KiB
+  // chunks spend more time on hand-offs than on bytes: kernel chunks of >= 32 KiB, while
+  // every fourth workgroup still gets a reduce unit. Same-box A/B (plane_probe --units):
+  // 8 workers x 16 MiB, 8 -> 32 KiB chunks 0.350 / 0.358 -> 0.307 / 0.272 ms per round; 2 x 1 MiB,
+  // 2 -> 8 KiB 0.069 / 0.057 -> 0.061 / 0.049 ms. MXAR_PLANE_COARSEN=0 keeps maxChunkSize.
+  if (cfg.thReduce >= 1.f && cfg.thComplete >= 1.f && coarsen_full_) {
+    int gx = o_.grid;
+    if (gx <= 0) {
+      int cus = 256;
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device);
+      gx = 2 * cus;
+      if (const char* g = std::getenv("MXAR_GRID")) gx = std::max(1, std::atoi(g));
+    }
+    const int64_t want = ceil_div(int64_t{32} << 10, chunk_ * es);
+    const int64_t room = std::max<int64_t>(1, nch / std::max(1, gx / 4));
+    const int64_t m = std::min(want, room);
+    if (m > 1) {
+      chunk_ *= m;
+      coarse_ *= static_cast<int>(m);
+      nch = ceil_div(block_, chunk_);
+      if (coarse_ == static_cast<int>(m)) st_.coarsened++;
+    }
   }
   nch_ = static_cast<int>(nch);
   std::vector<char*> bases(P, nullptr);
