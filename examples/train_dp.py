@@ -85,6 +85,8 @@ def main() -> int:
     ap.add_argument("--bucket-mib", type=int, default=4)
     ap.add_argument("--th", type=float, default=1.0, help="thReduce = thComplete of every bucket (GPU, < 1: straggler-tolerant)")
     ap.add_argument("--cpu", action="store_true", help="gloo on the CPU (TorchDistComm)")
+    ap.add_argument("--overlap", choices=["on", "off", "auto"], default="on",
+                    help="buckets beside backward, after it, or measured in the first steps (GPU)")
     args = ap.parse_args()
 
     rank, world, local = init_distributed("gloo" if args.cpu else "nccl")
@@ -96,7 +98,8 @@ def main() -> int:
     else:
         comm = XgmiCommunicator(device=dev, max_lag=1 if args.th < 1.0 else None)
     kw = dict(th_reduce=args.th, th_complete=args.th, rescale=True) if args.th < 1.0 else {}
-    reducer = BucketedGradReducer(model, comm, bucket_bytes=args.bucket_mib << 20, op="avg", **kw)
+    overlap = {"on": True, "off": False, "auto": "auto"}[args.overlap]
+    reducer = BucketedGradReducer(model, comm, bucket_bytes=args.bucket_mib << 20, op="avg", overlap=overlap, **kw)
     opt = torch.optim.AdamW(model.parameters(), lr=args.lr)
     gen = torch.Generator().manual_seed(1000 + rank)
     t0 = time.perf_counter()
@@ -126,7 +129,8 @@ def main() -> int:
     dist.all_reduce(diff, op=dist.ReduceOp.MAX)
     if rank == 0:
         print(f"done: {args.steps} steps in {dt:.2f} s, loss {first:.3f} -> {last:.3f}, "
-              f"replica max diff {diff.item():.3g}", flush=True)
+              f"replica max diff {diff.item():.3g}, schedule {reducer.stats.get('schedule', reducer.schedule)}",
+              flush=True)
     ok = last < first and (diff.item() == 0.0 or args.th < 1.0)
     dist.barrier()
     dist.destroy_process_group()

@@ -45,6 +45,9 @@ def test_train_dp_one_gpu():
     from akka_allreduce_1_amd.parallel.comm import free_port
 
     r = _run(["-m", "torch.distributed.run", "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
-              "--master-port", str(free_port()), "examples/train_dp.py", "--steps", "30"], timeout=300)
+              "--master-port", str(free_port()), "examples/train_dp.py", "--steps", "30", "--overlap", "auto"],
+             timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "replica max diff 0" in r.stdout, r.stdout
+    # the reducer measured its candidate schedules in the first steps and kept one
+    assert "schedule overlap:" in r.stdout or "schedule serial:" in r.stdout, r.stdout
