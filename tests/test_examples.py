@@ -51,3 +51,15 @@ def test_train_dp_one_gpu():
     assert "replica max diff 0" in r.stdout, r.stdout
     # the reducer measured its candidate schedules in the first steps and kept one
     assert "schedule overlap:" in r.stdout or "schedule serial:" in r.stdout, r.stdout
+
+
+@pytest.mark.gpu
+def test_native_gpu_job_two_workers_on_one_gpu():
+    """examples/native_gpu_job.sh: master + 2 `mxar-gpu` worker processes (every worker on GPU 0),
+    64 rounds of 1 M floats; the master finishes every round and both workers exit cleanly."""
+    r = subprocess.run(["bash", "examples/native_gpu_job.sh", "2", str(1 << 20), "4096", "64"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=180,
+                       env=dict(os.environ, SHARE_DEVICE="1", HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert '"rounds": 64' in r.stdout, r.stdout
+    assert r.stdout.count("64 rounds completed") == 2, r.stdout
