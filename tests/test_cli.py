@@ -85,10 +85,12 @@ def test_native_master_and_two_workers(tmp_path):
         port = s.getsockname()[1]
     seed = f"mxar.tcp://ClusterSystem@127.0.0.1:{port}"
     common = ["--seeds", seed, "--loglevel", "ERROR"]
+    # the master polls its host threads through the rounds (--spin-us), worker 0 sleeps at once
     master = subprocess.Popen([exe, "master", str(port), "2", "12", "2", "--th-reduce", "1", "--th-complete", "1",
-                               "--max-round", "15"] + common, stdout=subprocess.PIPE, text=True)
-    workers = [subprocess.Popen([exe, "worker", "0", "12"] + common, stdout=subprocess.PIPE, text=True)
-               for _ in range(2)]
+                               "--max-round", "15", "--spin-us", "200"] + common, stdout=subprocess.PIPE, text=True)
+    workers = [subprocess.Popen([exe, "worker", "0", "12"] + common + (["--spin-us", "0"] if k == 0 else []),
+                                stdout=subprocess.PIPE, text=True)
+               for k in range(2)]
     try:
         mout, _ = master.communicate(timeout=60)
         wouts = [w.communicate(timeout=60)[0] for w in workers]
