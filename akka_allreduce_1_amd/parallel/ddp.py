@@ -280,6 +280,27 @@ class BucketedGradReducer:
         if self._auto:
             self._tune_step()
 
+    def _agree(self, times: Sequence[float]) -> tuple[int, torch.Tensor]:
+        """The schedule every rank keeps: per candidate the MAX over ranks of its best step time
+        (a schedule is as fast as its slowest rank), then the fastest candidate - the same
+        index on every rank (ties: the first)."""
+        best = torch.tensor(list(times), dtype=torch.float64)
+        try:
+            import torch.distributed as dist
+
+            if dist.is_available() and dist.is_initialized():
+                grp = getattr(self.comm, "cpu_group", None)
+                if grp is not None or not self.on_gpu:  # a gloo group: a CPU tensor
+                    dist.all_reduce(best, op=dist.ReduceOp.MAX, group=grp if grp is not None else
+                                    getattr(self.comm, "group", None))
+                else:
+                    t = best.to(self.device)
+                    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=getattr(self.comm, "group", None))
+                    best = t.cpu()
+        except Exception:  # noqa: BLE001 - no process group: this rank alone decides
+            pass
+        return int(torch.argmin(best).item()), best
+
     def tune_schedule(self, tune_steps: int = 2, candidates: Sequence[tuple[bool, str]] | None = None) -> None:
         """(Re)start schedule tuning: the next len(candidates) x tune_steps steps try each
         (overlap, algo) candidate; then the fastest (agreed over the ranks) is kept."""
@@ -311,21 +332,7 @@ class BucketedGradReducer:
         if k < len(self._cands):
             self.overlap, self.algo = self._cands[k]
             return
-        best = torch.tensor([min(t) if t else float("inf") for t in self._times], dtype=torch.float64)
-        try:
-            import torch.distributed as dist
-
-            if dist.is_available() and dist.is_initialized():
-                grp = getattr(self.comm, "cpu_group", None)
-                if grp is not None:  # gloo group of the communicator: a CPU tensor
-                    dist.all_reduce(best, op=dist.ReduceOp.MAX, group=grp)
-                else:
-                    t = best.to(self.device)
-                    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=getattr(self.comm, "group", None))
-                    best = t.cpu()
-        except Exception:  # noqa: BLE001 - no process group: this rank alone decides
-            pass
-        i = int(torch.argmin(best).item())
+        i, best = self._agree([min(t) if t else float("inf") for t in self._times])
         self.overlap, self.algo = self._cands[i]
         self.schedule = ("overlap" if self.overlap else "serial", self.algo)
         self.stats["schedule_ms"] = {f"{'overlap' if o else 'serial'}:{a}": round(float(x), 3)

@@ -63,6 +63,11 @@ def _worker(rank, world, port, q):
         m(data[rank]).sum().backward()
         red2.wait()
         assert torch.all(extra.weight.grad == 0)
+        # schedule agreement (overlap="auto"): a schedule is as fast as its slowest rank, and
+        # every rank keeps the same one - rank 0 alone would pick 0, rank 1 alone 1
+        times = [[1.0, 5.0, 3.0], [4.0, 2.0, 3.0]][rank]
+        i, best = red2._agree(times)
+        assert i == 2 and best.tolist() == [4.0, 5.0, 3.0], (i, best)
         q.put((rank, True, ""))
     except Exception as e:  # noqa: BLE001
         import traceback
