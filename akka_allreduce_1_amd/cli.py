@@ -189,6 +189,12 @@ def worker_main(argv: list[str] | None = None) -> int:
     _common(ap)
     args = ap.parse_args(argv)
     cfg = _load(args)
+    if args.device is not None:
+        # a GPU worker's host threads keep polling through each round (the native mxar-gpu's
+        # --spin-us default): every hop of the next round lands on a running thread
+        spin = str(int(cfg["mxar.host-spin-us"]))
+        os.environ.setdefault("MXAR_DISPATCH_SPIN_US", spin)
+        os.environ.setdefault("MXAR_TCP_SPIN_US", spin)
     system = C.ActorSystem(str(cfg["mxar.system-name"]), False)
     n = args.sourceDataSize
     count = {"n": 0}

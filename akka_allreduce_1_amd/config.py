@@ -60,6 +60,7 @@ DEFAULTS: dict[str, Any] = {
     "mxar.plane.grid": 0,                                      # workgroups per round launch (0: 2 per CU)
     "mxar.plane.timeout": 60.0,                                # seconds a kernel waits for a dead peer
     "mxar.plane.min-chunk": 0,                                 # one flag per chunk of >= this many elements (0: 1 KiB)
+    "mxar.host-spin-us": 500,                                  # GPU worker: dispatchers / TCP readers poll this long
     "mxar.plane.spin-us": 1000,                                # completion thread polls a round this long
     "mxar.metrics.json": "",
     "mxar.trace.json": "",
