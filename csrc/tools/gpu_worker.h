@@ -16,7 +16,7 @@ struct GpuWorkerParts {
 };
 
 GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag, int grid, double timeout_s,
-                               int64_t min_chunk, bool static_source)
+                               int64_t min_chunk, bool static_source, int dtype)
     __attribute__((weak));
 
 }  // namespace mxar

@@ -40,10 +40,12 @@ struct InputPool {
 }  // namespace
 
 GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag, int grid, double timeout_s,
-                               int64_t min_chunk, bool static_source) {
+                               int64_t min_chunk, bool static_source, int dtype) {
+  // dtype: 0 float32 (the reference's element type), 1 bfloat16, 2 float16 - the plane's
+  // element type and the source's (the kernel sums in fp32 and rounds once)
   XgmiPlaneOptions o;
   o.device = device;
-  o.dtype = DType::F32;
+  o.dtype = static_cast<DType>(dtype);
   o.capacity = size;
   o.max_peers = max_peers;
   o.max_lag = max_lag;
@@ -84,23 +86,24 @@ GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag,
       }
     };
   }
-  const size_t bytes = static_cast<size_t>(size) * sizeof(float);
+  const size_t bytes = static_cast<size_t>(size) * dtype_size(o.dtype);
   if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("mxar-gpu: no device " + std::to_string(device));
   if (static_source) {
     // --source static: data[i] = i, filled once - the same buffer every round (the bench's
     // tensor dataSource; isolates the engine from the per-round fill)
     void* mem = nullptr;
     if (hipMalloc(&mem, bytes) != hipSuccess) throw std::runtime_error("mxar-gpu: hipMalloc failed");
-    launch_fill_iota(mem, size, 0.0, DType::F32, s);
+    launch_fill_iota(mem, size, 0.0, o.dtype, s);
     std::shared_ptr<void> owner(mem, [](void* q) { (void)hipFree(q); });
-    auto payload = std::make_shared<DevicePayload>(owner, 0, static_cast<size_t>(size), device, s, nullptr, 0);
+    auto payload = std::make_shared<DevicePayload>(owner, 0, static_cast<size_t>(size), device, s, nullptr, dtype);
     p.source = [payload](const AllReduceInputRequest&) { return AllReduceInput{payload}; };
     return p;
   }
   // the demo source (AllreduceWorker.scala:272-301): data[i] = i + iteration, produced by the
   // fill_iota kernel on the plane's stream into a pooled buffer
   auto pool = std::make_shared<InputPool>();
-  p.source = [device, size, s, bytes, pool](const AllReduceInputRequest& r) {
+  const DType dt = o.dtype;
+  p.source = [device, size, s, bytes, pool, dt, dtype](const AllReduceInputRequest& r) {
     void* mem = nullptr;
     {
       std::lock_guard<std::mutex> g(pool->mu);
@@ -110,12 +113,12 @@ GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag,
       }
     }
     if (mem == nullptr && hipMalloc(&mem, bytes) != hipSuccess) throw std::runtime_error("mxar-gpu: hipMalloc failed");
-    launch_fill_iota(mem, size, static_cast<double>(r.iteration), DType::F32, s);
+    launch_fill_iota(mem, size, static_cast<double>(r.iteration), dt, s);
     std::shared_ptr<void> owner(mem, [pool](void* q) {
       std::lock_guard<std::mutex> g(pool->mu);
       pool->free.push_back(q);
     });
-    return AllReduceInput{std::make_shared<DevicePayload>(owner, 0, static_cast<size_t>(size), device, s, nullptr, 0)};
+    return AllReduceInput{std::make_shared<DevicePayload>(owner, 0, static_cast<size_t>(size), device, s, nullptr, dtype)};
   };
   return p;
 }

@@ -75,6 +75,7 @@ struct Options {
   double plane_timeout_s = 60.0;
   int64_t min_chunk = 0;  // --min-chunk N: one flag per chunk of >= N elements (0: 1 KiB)
   bool static_source = false;  // --source static: the same input every round (default iota: i + iteration)
+  int dtype = 0;     // --dtype fp32|bf16|fp16 (GPU worker element type)
   int spin_us = -1;  // --spin-us N: dispatcher idle spin + cluster reader socket poll (-1: built-in defaults)
 };
 
@@ -100,7 +101,7 @@ void apply_spin(int us) {
                "master control bridge (docs/BRIDGE.md): --bridge PORT [--external-rounds]\n"
                "       mxar drive [host:]bridgePort [rounds] [--lockstep]   (bridge client)\n"
                "worker on a GPU (mxar-gpu): --device K [--max-peers N --plane-max-lag N --grid N --plane-timeout S\n"
-               "                              --min-chunk N --source iota|static]\n"
+               "                              --min-chunk N --source iota|static --dtype fp32|bf16|fp16]\n"
                "host threads: --spin-us N (dispatcher + socket polling; GPU workers default 500)\n",
                msg);
   std::exit(2);
@@ -137,6 +138,11 @@ Options parse(int argc, char** argv) {
     else if (a == "--plane-timeout") o.plane_timeout_s = std::stod(val());
     else if (a == "--min-chunk") o.min_chunk = std::stoll(val());
     else if (a == "--spin-us") o.spin_us = std::stoi(val());
+    else if (a == "--dtype") {
+      const std::string v = val();
+      if (v != "fp32" && v != "bf16" && v != "fp16") usage("--dtype must be fp32, bf16 or fp16");
+      o.dtype = v == "fp32" ? 0 : v == "bf16" ? 1 : 2;
+    }
     else if (a == "--source") {
       const std::string v = val();
       if (v != "iota" && v != "static") usage("--source must be iota or static");
@@ -257,7 +263,7 @@ void set_level(const std::string& l) {
   if (o.device >= 0) {  // the round engine on a GPU: one threshold-kernel launch per round
     if (make_gpu_worker == nullptr) usage("--device needs the GPU build of this executable: mxar-gpu");
     GpuWorkerParts g = make_gpu_worker(o.device, size, o.max_peers, o.plane_max_lag, o.grid, o.plane_timeout_s,
-                                         o.min_chunk, o.static_source);
+                                         o.min_chunk, o.static_source, o.dtype);
     cc.meta = g.plane->descriptor();  // relayed by the master in InitWorkers.planes
     gpu_at_exit = g.at_exit;
     sys->actor_of(std::make_unique<PlaneWorkerActor>(g.source, sink, g.plane), "worker");

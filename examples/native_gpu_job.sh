@@ -6,6 +6,7 @@
 #
 #   examples/native_gpu_job.sh [workers=8] [dataSize=67108864] [maxChunkSize=131072] [rounds=100]
 #   SHARE_DEVICE=1 examples/native_gpu_job.sh 2      # every worker on GPU 0 (one-GPU boxes)
+#   DTYPE=bf16 examples/native_gpu_job.sh             # bf16 rounds (fp32 sums, one rounding)
 #
 # Workers print nothing per round (--quiet); the master prints its steady round rate. Drop
 # --quiet from WOPTS to see every round's output sum, as the reference's demo sink does.
@@ -26,7 +27,8 @@ for k in $(seq 0 $((P - 1))); do
   dev=$k
   [ "${SHARE_DEVICE:-0}" = 1 ] && dev=0
   # --source iota: data[i] = i + round (the reference's demo source); --spin-us defaults to 500
-  "$X/mxar-gpu" worker 0 "$N" --device $dev --max-peers $P --grid $GRID --source iota --quiet $SEEDS &
+  "$X/mxar-gpu" worker 0 "$N" --device $dev --max-peers $P --grid $GRID --source iota --dtype ${DTYPE:-fp32} \
+    --quiet $SEEDS &
   pids+=($!)
 done
 "$X/mxar" master $PORT $P $N $CHUNK --th-reduce 1 --th-complete 1 --max-lag 1 --max-round $((ROUNDS - 1)) \
