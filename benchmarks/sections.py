@@ -20,8 +20,9 @@ same HBM, no xGMI):
                    workgroup budget, reporting the GEMMs' slowdown and the exposed time.
   protocol_sizes   the reference's master / worker round protocol driving the GPU round
                    engine (PlaneJob: StartAllreduce -> one threshold-kernel launch per worker)
-                   at 40 B (the reference's default job: 10 floats, maxChunkSize 2, 101
-                   rounds - AllreduceMaster.scala:105-114), 1 MiB and 64 MiB per worker.
+                   at 40 B (the reference's default job: 10 floats, maxChunkSize 2 -
+                   AllreduceMaster.scala:105-114), 1 MiB and 64 MiB per worker; 2000 / 2000 /
+                   200 rounds, mean and median round interval.
 
 Latency method: the host is put ahead of the GPU (a sleep kernel first), then every call is
 bracketed by device events - so p50 is the device time of one call (kernel launch to kernel
@@ -252,8 +253,8 @@ def reduce_kernel(dev, mib: int = 1024, slots=(2, 4, 8), iters: int = 10) -> dic
     return res
 
 
-def protocol_sizes(dev, cases=((40, torch.float32, 2, 101), (1 << 20, torch.bfloat16, 0, 200),
-                               (64 << 20, torch.bfloat16, 0, 60))) -> dict:
+def protocol_sizes(dev, cases=((40, torch.float32, 2, 2000), (1 << 20, torch.bfloat16, 0, 2000),
+                               (64 << 20, torch.bfloat16, 0, 200))) -> dict:
     """The master / worker protocol on the GPU round engine at several per-worker sizes, two
     workers sharing the GPU (th = 1, maxLag 1). chunk 0 = the bench geometry (about 256 reduce
     units per worker). ms_per_round from the master's native round-barrier stamps after 10
@@ -286,6 +287,9 @@ def protocol_sizes(dev, cases=((40, torch.float32, 2, 101), (1 << 20, torch.bflo
                 row["us_per_round"] = round(per * 1e6, 1)
                 row["rounds_per_s"] = round(1.0 / per, 1)
                 row["algbw_per_worker_GBps"] = round(nbytes / per / 1e9, 3)
+                gaps = sorted(st[i + 1] - st[i] for i in range(warm - 1, len(st) - 1))
+                row["round_interval_p50_us"] = round(gaps[len(gaps) // 2] * 1e6, 1)
+                row["round_interval_p99_us"] = round(gaps[int(0.99 * (len(gaps) - 1))] * 1e6, 1)
             lat = job.system.plane_worker_state(job.workers[0])["round_latency"]
             row["worker_round_latency_p50_us"] = round(lat["p50_ms"] * 1e3, 1)
             o = job.last_output(0)
