@@ -437,6 +437,7 @@ void bind_hip(py::module_& m) {
           },
           py::arg("comms"), py::arg("stream") = 0)
       .def("error", &XgmiComm::error)
+      .def("ctl_words", &XgmiComm::ctl_words)
       .def("clear_error", &XgmiComm::clear_error)
       .def("reset_local", [](XgmiComm& c) {
         py::gil_scoped_release r;

@@ -210,6 +210,9 @@ class XgmiComm {
 
   // Sticky device error word (ORed codes, see device_common.h); 0 = healthy.
   uint32_t error() const;
+  // diagnostics: the control words ([0] launch epoch, [1] ticket, [2] error, [4] threshold
+  // round epoch, ...), read with a blocking copy - for error reports, never on a hot path
+  std::vector<uint32_t> ctl_words() const;
   void clear_error();
   // Zero this rank's flags, LL slots and counters (recovery after CommError; collective use
   // only, with every rank idle - see XgmiCommunicator.reset).

@@ -729,6 +729,13 @@ void XgmiComm::order_group(const std::vector<XgmiComm*>& group, hipStream_t s) {
   for (XgmiComm* c : group) c->order_after_last(s);
 }
 
+std::vector<uint32_t> XgmiComm::ctl_words() const {
+  std::vector<uint32_t> w(16, 0);
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipMemcpy(w.data(), ctl_, w.size() * 4, hipMemcpyDeviceToHost), "hipMemcpy(ctl)");
+  return w;
+}
+
 uint32_t XgmiComm::error() const {
   uint32_t e = 0;
   hip_check(hipSetDevice(device_), "hipSetDevice");

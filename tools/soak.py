@@ -133,6 +133,16 @@ def main() -> None:
             print(f"[soak] {last - t0:.0f}s step {step} errors {len(errors)}", flush=True)
     bad = torch.tensor([float(len(errors))])
     dist.all_reduce(bad)
+    if bad.item() > 0:  # every rank's control words next to the error: epoch agreement across ranks
+        words = [None] * world
+        try:
+            mine = list(comm.native.ctl_words())
+        except Exception as e:  # noqa: BLE001
+            mine = [repr(e)]
+        dist.all_gather_object(words, mine)
+        if rank == 0:
+            print(f"[soak] ctl words per rank ([0] launch epoch, [2] error, [4] threshold epoch): {words}",
+                  file=sys.stderr, flush=True)
     if errors:
         print(f"[soak rank {rank}] " + "; ".join(errors[:5]), file=sys.stderr, flush=True)
     if rank == 0:
