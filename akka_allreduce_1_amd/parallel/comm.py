@@ -34,7 +34,7 @@ class CommError(RuntimeError):
     """A device-side wait timed out (a peer never delivered); the communicator is poisoned."""
 
 
-_ERR_NAMES = {1: "scatter wait timed out", 2: "reduce wait timed out", 4: "barrier timed out", 8: "bad arguments",
+_ERR_NAMES = {1: "scatter wait timed out", 2: "reduce wait timed out", 4: "barrier / slot-reuse wait timed out", 8: "bad arguments",
               16: "a peer stayed more than maxLag rounds behind"}
 
 

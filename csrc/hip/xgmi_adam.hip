@@ -92,6 +92,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a)
   const int nu = (P - 1) * a.nch;
 
   // Phase 1 - gradient ScatterBlock: chunk c of block j to its owner j
+  if (static_cast<int>(blockIdx.x) < nu) entry_guard(a, ctl, r, kHazS, -1, deadline, err);
   for (int u = blockIdx.x; u < nu; u += G) {
     const int c = u / Pm1;
     const int j = (r + 1 + u % Pm1) % P;
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a)
     if (len > 0 && unit_in_bounds(a, cstart * es, len * es, c, err))
       copy_from_slab<E>(param + (bstart + cstart) * es, a.base[r] + a.off_R + j * slot + cstart * es, len);
   }
-  finish_launch(ctl, epoch);
+  finish_launch_done(a, ctl, epoch, r, kHazR);  // peers may still gather from R
 }
 
 template <bool STREAM>

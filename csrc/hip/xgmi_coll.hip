@@ -10,10 +10,11 @@
 //   all_gather     : in[m]    -> out[P][m], out_r[s] = in_s
 //   reduce_scatter : in[P][m] -> out[m],    out_r   = scale * sum_s in_s[r] (fp32, rank order)
 // Phase 1 pushes block j (chunked) into rank j's S (or R) slot with write-through stores and
-// a flag per chunk; phase 2 waits per chunk and copies (or reduces) out of the own slab. The
-// last workgroup of every rank then runs a flag barrier (FB flags): when a launch ends on
-// any rank, every peer has finished reading its slots, so the next launch may overwrite
-// them (the allreduce kernels get the same guarantee from their third phase).
+// a flag per chunk; phase 2 waits per chunk and copies (or reduces) out of the own slab.
+// Slot reuse: phase 1 waits (entry_guard, xgmi_device.h) until the target peers have
+// finished reading the region in an earlier launch, and the last workgroup tells every peer
+// when this launch's slab reads are done (FB words) - no end-of-launch barrier, so a fast
+// rank leaves as soon as its own data is out.
 #include <hip/hip_runtime.h>
 
 #include "xgmi_device.h"
@@ -28,33 +29,6 @@ __device__ __forceinline__ void copy_plain(char* dst, const char* src, int64_t l
   for (int64_t i = threadIdx.x; i < npk; i += kCommThreads) st16(dst + i * 16, ld16(src + i * 16));
   const int64_t t = npk * E::ELEMS + threadIdx.x;
   if (t < len) Scalar<E>::copy(dst, src, t);
-}
-
-// The last workgroup of the rank (ticket) tells every peer that all of this rank's slab
-// reads of the launch are done, waits for the same from every peer, then advances the epoch.
-__device__ __forceinline__ void finish_with_barrier(const CommArgs& a, uint32_t* ctl, uint32_t epoch, int r,
-                                                    uint64_t deadline, uint32_t* err) {
-  __shared__ int last;
-  // The last workgroup's FB flags tell the peers that EVERY workgroup's slab reads of this
-  // launch are done: every wave drains its memory operations before the barrier, so each
-  // ticket follows its workgroup's loads. The ticket is relaxed - nothing is read back after
-  // it, and an acq_rel one was an L2 writeback + invalidate per workgroup (the threshold
-  // kernel's round end measured -5 % at 64-256 MiB without it, profiles/round2/README.md).
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = t == gridDim.x - 1 ? 1 : 0;
-  }
-  __syncthreads();
-  if (!last) return;
-  publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : fb(a, k, r); }, a.P, epoch);
-  wait_flags([&](int s) -> const uint32_t* { return s == r ? nullptr : fb(a, r, s); }, a.P, epoch, deadline, err,
-             ERR_TIMEOUT_BARRIER);
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&ctl[0], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 }  // namespace
@@ -80,7 +54,9 @@ __global__ __launch_bounds__(kCommThreads) void coll_kernel(CommArgs a) {
   const int Pm1 = P > 1 ? P - 1 : 1;
   const int nu = (P - 1) * a.nch;
 
+  constexpr uint32_t region = MODE == 1 ? kHazR : kHazS;
   // Phase 1: push this rank's part for peer j into j's slab (rotated peer order)
+  if (static_cast<int>(blockIdx.x) < nu) entry_guard(a, ctl, r, region, -1, deadline, err);
   for (int u = blockIdx.x; u < nu; u += G) {
     const int c = u / Pm1;
     const int j = (r + 1 + u % Pm1) % P;
@@ -134,7 +110,7 @@ __global__ __launch_bounds__(kCommThreads) void coll_kernel(CommArgs a) {
                           a.base[r] + (MODE == 1 ? a.off_R : a.off_S) + s * slot + cstart * es, len);
     }
   }
-  finish_with_barrier(a, ctl, epoch, r, deadline, err);
+  finish_launch_done(a, ctl, epoch, r, region);
 }
 
 void launch_coll(const CommArgs& a, dim3 grid, hipStream_t s, DType dt, int mode) {

@@ -61,6 +61,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
   // copies keep the scatter at copy speed ("flat" geometry, launch_segment).
   const int gs = a.sgroup > 1 ? a.sgroup : 1;
   const int nsu = Pm1 * ((a.nch + gs - 1) / gs);
+  if (static_cast<int>(blockIdx.x) < nsu) entry_guard(a, ctl, r, kHazS, -1, deadline, err);  // block-uniform
   for (int u = blockIdx.x; u < nsu; u += G) {
     const int c0 = (u / Pm1) * gs;
     const int ncg = a.nch - c0 < gs ? a.nch - c0 : gs;
@@ -206,7 +207,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
       }
     }
   }
-  finish_launch(ctl, epoch);
+  finish_launch_done(a, ctl, epoch, r, kHazR);  // peers may still gather from R
 }
 
 // ---------------------------------------------------------------------------------
@@ -261,6 +262,7 @@ __global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
   const int64_t slot = a.slot_bytes;
   uint32_t* err = &ctl[2];
   const bool rel = a.fence & 1, acq = a.fence & 2;
+  if (static_cast<int>(blockIdx.x) < a.nch) entry_guard(a, ctl, r, kHazS, -1, deadline, err);
   for (int c = blockIdx.x; c < a.nch; c += G) {
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     const int64_t len = clamp_len(a.n - cstart, a.chunk);
@@ -279,7 +281,7 @@ __global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
       reduce_to<E, PT>(P, src, 1, 0, [&](int) -> char* { return o; }, len, a.scale, a.fence & 1);
     }
   }
-  finish_launch(ctl, epoch);
+  finish_launch_done(a, ctl, epoch, r, kHazS);  // peers may still reduce from S
 }
 
 // ---------------------------------------------------------------------------------
@@ -426,6 +428,7 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
   const bool rel = a.fence & 1, acq = a.fence & 2;
   __shared__ uint64_t ps_lds[kPhaseSlots];
   PhaseStamps ps(a, ps_lds);  // ring: [1] = end of the reduce-scatter hops, [2]/[4] = waits in RS / AG
+  if (static_cast<int>(blockIdx.x) < a.nch) entry_guard(a, ctl, r, kHazS | kHazR, nxt, deadline, err);
   for (int c = blockIdx.x; c < a.nch; c += gridDim.x) {
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     auto blen = [&](int b) { return clamp_len(clamp_len(a.n - static_cast<int64_t>(b) * a.block, a.block) - cstart, a.chunk); };
@@ -481,7 +484,7 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
   ps.mark(3);
   ps.mark(5);
   ps.flush();
-  finish_launch(ctl, epoch);
+  finish_launch_done(a, ctl, epoch, r, kHazS | kHazR);  // the next rank may still read both
 }
 
 __global__ __launch_bounds__(kCommThreads) void barrier_kernel(CommArgs a) {

@@ -289,12 +289,11 @@ __device__ __forceinline__ void finish_launch(uint32_t* ctl, uint32_t epoch) {
     // relaxed: only the count matters. The next launch of this communicator is ordered
     // after this one - same stream, or XgmiComm::order_after_last makes the new stream
     // wait - and kernel end publishes ctl[0]; no peer learns anything from this ticket
-    // (slot reuse is guarded by the kernels' own phase flags). An acq_rel at agent scope
-    // would be a `buffer_wbl2` per workgroup, writing back the XCD's dirty L2 lines
+    // (slot reuse is guarded by entry_guard / finish_launch_done below). An acq_rel at agent
+    // scope would be a `buffer_wbl2` per workgroup, writing back the XCD's dirty L2 lines
     // mid-kernel (e.g. AdamW state). Kernels whose last workgroup DOES tell peers that all
-    // reads are done (xgmi_coll.hip FB barrier, xgmi_threshold.hip progress words) drain
-    // every wave (s_waitcnt vmcnt(0)) before their barrier and then take a relaxed ticket
-    // too.
+    // reads are done (finish_launch_done, xgmi_threshold.hip progress words) drain every
+    // wave (s_waitcnt vmcnt(0)) before a relaxed ticket.
     const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == gridDim.x - 1) {
       __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -305,6 +304,77 @@ __device__ __forceinline__ void finish_launch(uint32_t* ctl, uint32_t epoch) {
 
 __device__ __forceinline__ uint32_t launch_epoch(const uint32_t* ctl) {
   return __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+}
+
+// ---------------------------------------------------------------------------------
+// Slot reuse across launches. A launch pushes into its peers' S / R slots in its first
+// phase, before it has heard from those peers in this launch - while a slower peer may
+// still be READING the same slots in the previous launch: a one-shot's reduce of S after
+// the fast rank's next one-shot push, a two-shot's gather of R after the fast rank's next
+// all-gather push, a ring hop into a neighbour that is still forwarding. A kernel whose
+// slot reads can still be pending at peers once it has completed locally records the
+// region(s) in ctl[12] (S) / ctl[13] (R) as its epoch and, from its last workgroup, writes
+// "launch e done" into every peer's FB word once every workgroup's loads have returned.
+// A launch that pushes into a region first waits until the target peers' FB words reached
+// that region's recorded epoch - normally already true, so one local load per peer issued
+// beside the epoch load. Every rank runs the same launch sequence, so the local words name
+// the peers' epochs too. Two-shot chains record only R (their S reads end before any rank
+// can complete) and push S first, so back-to-back two-shot segments never wait here.
+// The low-latency kernel keeps its own parity slots and takes no part; the threshold kernel
+// has its own progress-word gate (xgmi_threshold.hip).
+enum : uint32_t { kHazS = 1u, kHazR = 2u };
+
+__device__ __forceinline__ uint32_t later_epoch(uint32_t x, uint32_t y) {
+  if (x == 0) return y;
+  if (y == 0) return x;
+  return static_cast<int32_t>(y - x) > 0 ? y : x;
+}
+
+// All threads call. `only` >= 0 waits for that peer alone (ring: the only rank it writes).
+__device__ __forceinline__ void entry_guard(const CommArgs& a, const uint32_t* ctl, int r, uint32_t regions,
+                                            int only, uint64_t deadline, uint32_t* err) {
+  if (threadIdx.x < 64) {
+    const int k = static_cast<int>(threadIdx.x);
+    const bool mine = k < a.P && k != r && (only < 0 || k == only);
+    const uint32_t* f = mine ? fb(a, r, k) : nullptr;
+    const uint32_t v = f != nullptr ? ld_flag(f) : 0u;  // issued beside the hazard loads
+    const uint32_t hs = (regions & kHazS) ? __hip_atomic_load(&ctl[12], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    const uint32_t hr = (regions & kHazR) ? __hip_atomic_load(&ctl[13], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    const uint32_t h = later_epoch(hs, hr);
+    bool ok = h == 0 || f == nullptr || reached(v, h);
+    while (!__all(ok)) {
+      __builtin_amdgcn_s_sleep(1);
+      if (!ok) ok = reached(ld_flag(f), h);
+      if (wall_ticks() > deadline) break;
+    }
+    if (!__all(ok) && k == 0) __hip_atomic_fetch_or(err, ERR_TIMEOUT_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // write-after-read: the pushes below issue only after the poll returned - no acquire
+  __syncthreads();
+}
+
+// finish_launch for kernels whose slot reads may outlive their local completion: every wave
+// drains its loads before its ticket; the last workgroup tells every peer "launch `epoch`
+// done" (FB word), records the regions' hazard epoch and advances ctl[0].
+__device__ __forceinline__ void finish_launch_done(const CommArgs& a, uint32_t* ctl, uint32_t epoch, int r,
+                                                   uint32_t regions) {
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x - 1 ? 1 : 0;
+  }
+  __syncthreads();
+  if (!last) return;
+  // no release: the word orders nothing this rank wrote, only that its loads have returned
+  publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : fb(a, k, r); }, a.P, epoch, false);
+  if (threadIdx.x == 0) {
+    if (regions & kHazS) __hip_atomic_store(&ctl[12], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (regions & kHazR) __hip_atomic_store(&ctl[13], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ctl[0], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 
