@@ -359,6 +359,7 @@ void bind_hip(py::module_& m) {
       .def("threshold_chunks", &XgmiComm::threshold_chunks, py::arg("n"), py::arg("dtype"),
            py::arg("ranks_in_launch") = 1)
       .def("set_straggler", &XgmiComm::set_straggler, py::arg("rank"), py::arg("us"))
+      .def("set_read_delay", &XgmiComm::set_read_delay, py::arg("rank"), py::arg("us"))
       .def_property_readonly("threshold_rows", &XgmiComm::threshold_rows)
       .def(
           "barrier",

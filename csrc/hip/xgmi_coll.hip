@@ -68,6 +68,7 @@ __global__ __launch_bounds__(kCommThreads) void coll_kernel(CommArgs a) {
     publish_flags([&](int) { return MODE == 1 ? f2(a, j, r, c) : f1(a, j, r, c); }, 1, epoch, rel);
   }
 
+  read_delay(a, r);
   if constexpr (MODE == 2) {
     // Phase 2 (reduce-scatter): own block r = own input + the P-1 received contributions.
     // Each chunk is reduced in `sub` pieces by different workgroups (as many reduce units as

@@ -177,6 +177,12 @@ class XgmiComm {
     delay_rank_ = rank;
     delay_us_ = us;
   }
+  // Test knob: rank `rank` idles `us` microseconds before the slab-reading phase of every
+  // one-shot / two-shot / collective launch (a slow reader for the slot-reuse guard tests).
+  void set_read_delay(int rank, double us) {
+    rdelay_rank_ = rank;
+    rdelay_us_ = us;
+  }
   // Device-side barrier over all ranks (enqueued on `stream`).
   void barrier(hipStream_t stream);
 
@@ -288,6 +294,8 @@ class XgmiComm {
   int64_t alloc_bytes_ = 0;  // slab_bytes_ padded around the IPC size bug (constructor)
   int delay_rank_ = -1;
   double delay_us_ = 0;
+  int rdelay_rank_ = -1;
+  double rdelay_us_ = 0;
   int64_t oneshot_max_;
   int64_t ll_auto_max_ = 0;  // Auto picks the low-latency one-shot up to this many bytes
   double timeout_s_;
@@ -303,6 +311,7 @@ class XgmiComm {
   bool connected_ = false;
   bool own_slab_ = true;           // false: laid out over a caller's arena
   bool own_ctl_ = true;            // false: control words owned by the caller
+  bool noguard_ = false;           // MXAR_SLOT_GUARD=0 (study / negative control only)
   bool dynamic_ = false;           // two-shot units from a counter (MXAR_TWOSHOT_DYNAMIC)
   int geom_ = -1;                  // two-shot geometry: -1 by block size, 0 coarse, 1 fine, 2 flat (MXAR_TWOSHOT_GEOM)
   int64_t flat_min_ = int64_t{2} << 20;  // blocks of at least this many bytes use the flat geometry (MXAR_TWOSHOT_FLAT_MIN)

@@ -120,6 +120,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
   }
 
   ps.mark(3);
+  read_delay(a, r);
   // Phase 3 - complete: gather the other owners' reduced chunks into the output. The
   // workgroup's units are polled together (wave 0, one lane per unit, up to 64 at a time)
   // and copied in ARRIVAL order: owners finish their reduces at different times, and a
@@ -270,6 +271,7 @@ __global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
       push_to_peers<E>(a, P, r, a.off_S + r * slot + cstart * es, in + cstart * es, len);
     publish_flags([&](int k) { return f1(a, k, r, c); }, P, epoch, rel);
   }
+  read_delay(a, r);
   for (int c = blockIdx.x; c < a.nch; c += G) {
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     const int64_t len = clamp_len(a.n - cstart, a.chunk);
@@ -596,6 +598,7 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   if (const char* u = std::getenv("MXAR_TWOSHOT_UNITS")) units_per_wg_ = std::max(1, std::atoi(u));
   if (const char* u = std::getenv("MXAR_TWOSHOT_SUB")) sub_max_ = std::max(1, std::atoi(u));
   if (const char* d = std::getenv("MXAR_TWOSHOT_DYNAMIC")) dynamic_ = std::atoi(d) != 0;
+  if (const char* g = std::getenv("MXAR_SLOT_GUARD")) noguard_ = std::atoi(g) == 0;
   if (const char* g = std::getenv("MXAR_TWOSHOT_GEOM")) {
     const std::string v = g;
     geom_ = v == "coarse" ? 0 : v == "fine" ? 1 : v == "flat" ? 2 : -1;
@@ -893,6 +896,9 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   }
   a.fence = c0.fence_;
   a.scale = scale;
+  a.rdelay_rank = c0.rdelay_rank_;
+  a.rdelay = c0.rdelay_us_ > 0 ? static_cast<uint64_t>(c0.rdelay_us_ * 100.0) : 0;  // 100 MHz ticks
+  a.noguard = c0.noguard_ ? 1 : 0;
   a.dynamic = c0.dynamic_ ? 1 : 0;
   a.stamps = c0.stamps_;
   if (a.stamps != nullptr && gx * ranks_here > c0.stamp_slots_) a.stamps = nullptr;  // buffer too small: off
@@ -1366,6 +1372,9 @@ void XgmiComm::run_coll(const std::vector<XgmiComm*>& group, Coll op, const std:
     a.timeout = static_cast<uint64_t>(c0.timeout_s_ * 1e8);
     a.fence = c0.fence_;
     a.scale = scale;
+    a.rdelay_rank = c0.rdelay_rank_;
+    a.rdelay = c0.rdelay_us_ > 0 ? static_cast<uint64_t>(c0.rdelay_us_ * 100.0) : 0;
+    a.noguard = c0.noguard_ ? 1 : 0;
     for (int k = 0; k < W; ++k) a.base[k] = c0.peers_[k];
     const int64_t target = std::max<int64_t>(1, gmax / (W - 1));
     a.chunk = std::max(min_chunk, round_up(ceil_div(len, target), elems));

@@ -70,6 +70,11 @@ struct CommArgs {
   uint64_t* stamps;
   uint64_t delay;      // test knob: ticks rank `delay_rank` idles before phase 1
   int delay_rank;
+  // test knob (XgmiComm::set_read_delay): ticks rank `rdelay_rank` idles before the phase that
+  // reads what peers pushed - holds a slow reader inside its launch (slot-reuse tests)
+  uint64_t rdelay;
+  int rdelay_rank;
+  int noguard;  // MXAR_SLOT_GUARD=0: skip entry_guard (A/B of its cost and negative control only)
   int dynamic;  // two-shot: workgroups take reduce / gather units from a counter (ctl[8], ctl[9])
   // threshold kernel with sub > 1 (chunks split into `sub` slices of `subchunk` elements,
   // one workgroup each): the rank's own scratch, zeroed when the membership is configured.
@@ -292,8 +297,8 @@ __device__ __forceinline__ void finish_launch(uint32_t* ctl, uint32_t epoch) {
     // (slot reuse is guarded by entry_guard / finish_launch_done below). An acq_rel at agent
     // scope would be a `buffer_wbl2` per workgroup, writing back the XCD's dirty L2 lines
     // mid-kernel (e.g. AdamW state). Kernels whose last workgroup DOES tell peers that all
-    // reads are done (finish_launch_done, xgmi_threshold.hip progress words) drain every
-    // wave (s_waitcnt vmcnt(0)) before a relaxed ticket.
+    // reads are done take a relaxed ticket too (finish_launch_done: every slab load fed a
+    // store before it; xgmi_threshold.hip progress words: every wave drains first).
     const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == gridDim.x - 1) {
       __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -333,6 +338,7 @@ __device__ __forceinline__ uint32_t later_epoch(uint32_t x, uint32_t y) {
 // All threads call. `only` >= 0 waits for that peer alone (ring: the only rank it writes).
 __device__ __forceinline__ void entry_guard(const CommArgs& a, const uint32_t* ctl, int r, uint32_t regions,
                                             int only, uint64_t deadline, uint32_t* err) {
+  if (a.noguard) return;  // uniform
   if (threadIdx.x < 64) {
     const int k = static_cast<int>(threadIdx.x);
     const bool mine = k < a.P && k != r && (only < 0 || k == only);
@@ -353,13 +359,23 @@ __device__ __forceinline__ void entry_guard(const CommArgs& a, const uint32_t* c
   __syncthreads();
 }
 
-// finish_launch for kernels whose slot reads may outlive their local completion: every wave
-// drains its loads before its ticket; the last workgroup tells every peer "launch `epoch`
-// done" (FB word), records the regions' hazard epoch and advances ctl[0].
+// Slot-reuse test knob: rank `rdelay_rank` idles before its slab reads (one scalar compare).
+__device__ __forceinline__ void read_delay(const CommArgs& a, int r) {
+  if (a.rdelay && r == a.rdelay_rank) {
+    const uint64_t until = wall_ticks() + a.rdelay;
+    while (wall_ticks() < until) __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+// finish_launch for kernels whose slot reads may outlive their local completion: the last
+// workgroup tells every peer "launch `epoch` done" (FB word), records the regions' hazard
+// epoch and advances ctl[0]. No drain: every slab load of a workgroup feeds a store (reduce,
+// copy, forward) issued before this point, so it has returned - the barrier extends that to
+// every wave and the ticket to every workgroup. (A vmcnt(0) drain here also waited for the
+// write-through stores and cost ~0.5 us per launch.)
 __device__ __forceinline__ void finish_launch_done(const CommArgs& a, uint32_t* ctl, uint32_t epoch, int r,
                                                    uint32_t regions) {
   __shared__ int last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -367,8 +383,8 @@ __device__ __forceinline__ void finish_launch_done(const CommArgs& a, uint32_t* 
   }
   __syncthreads();
   if (!last) return;
-  // no release: the word orders nothing this rank wrote, only that its loads have returned
-  publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : fb(a, k, r); }, a.P, epoch, false);
+  const int k = static_cast<int>(threadIdx.x);
+  if (k < a.P && k != r) st_flag(fb(a, k, r), epoch);
   if (threadIdx.x == 0) {
     if (regions & kHazS) __hip_atomic_store(&ctl[12], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (regions & kHazR) __hip_atomic_store(&ctl[13], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

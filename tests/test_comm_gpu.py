@@ -135,6 +135,68 @@ def test_multiprocess_ipc_allreduce(world):
     assert not bad, bad
 
 
+def _slot_reuse_worker(rank, world, port, results):
+    """Rank 1 idles 2 ms before every slab-reading phase; rank 0, which needs nothing more
+    from it once its pushes are in, runs ahead into the next launch and would push into the
+    slots rank 1 is about to read (one-shot S -> one-shot, two-shot R -> all-gather, all-to-all
+    S -> all-to-all) without the entry guard (xgmi_device.h)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.parallel import XgmiCommunicator
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ok, msg = True, ""
+    try:
+        comm = XgmiCommunicator(device=0, slot_bytes=1 << 20, grid=8, timeout_s=15.0)
+        comm.native.set_read_delay(1, 2000.0)
+        n = 8192
+        seq = ["oneshot", "oneshot", "twoshot", "all_gather", "all_to_all", "all_to_all", "oneshot", "twoshot",
+               "all_gather", "all_gather", "reduce_scatter", "oneshot"]
+        for it, op in enumerate(seq * 2):
+            xs = [fill_uniform(torch.empty(n, device=DEV), seed=1000 * it + k) for k in range(world)]
+            m = n // world
+            if op == "all_gather":
+                y, ref = comm.all_gather(xs[rank][:m].clone()), torch.cat([x[:m] for x in xs])
+            elif op == "all_to_all":
+                y, ref = comm.all_to_all(xs[rank]), torch.cat([x[rank * m:(rank + 1) * m] for x in xs])
+            elif op == "reduce_scatter":
+                y, ref = comm.reduce_scatter(xs[rank], op="sum"), _ref(xs)[rank * m:(rank + 1) * m]
+            else:
+                y, ref = comm.allreduce(xs[rank], algo=op), _ref(xs)
+            comm.check()
+            err = (y.float() - ref).abs().max().item()
+            if err > 1e-5:
+                ok, msg = False, f"launch {it} ({op}) rank {rank}: err {err}"
+                break
+        comm.native.set_read_delay(-1, 0.0)
+        comm.barrier()
+        comm.check()
+    except Exception as e:  # report, never hang the parent
+        ok, msg = False, repr(e)
+    results.put((rank, ok, msg))
+    dist.destroy_process_group()
+
+
+def test_multiprocess_slot_reuse_slow_reader():
+    from akka_allreduce_1_amd.parallel import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_slot_reuse_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    bad = [r for r in res if not r[1]]
+    assert not bad, bad
+
+
 def _big_slab_worker(rank, world, port, slot, results):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     import torch.distributed as dist
