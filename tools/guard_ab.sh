@@ -23,7 +23,9 @@ for i in 1 2; do
   timeout -k 10 400 python -u bench.py $ARGS > $O/ab_new_$i.json 2> $O/ab_new_$i.err || { echo "new failed"; exit 1; }
   MXAR_SLOT_GUARD=0 timeout -k 10 400 python -u bench.py $ARGS > $O/ab_noguard_$i.json 2> $O/ab_noguard_$i.err \
     || { echo "noguard failed"; exit 1; }
-  (cd ab_old && timeout -k 10 400 python -u bench.py $ARGS) > $O/ab_old_$i.json 2> $O/ab_old_$i.err \
-    || { echo "old failed"; exit 1; }
+  if [ -d ab_old ]; then
+    (cd ab_old && timeout -k 10 400 python -u bench.py $ARGS) > $O/ab_old_$i.json 2> $O/ab_old_$i.err \
+      || { echo "old failed"; exit 1; }
+  fi
   echo "round $i done"
 done
