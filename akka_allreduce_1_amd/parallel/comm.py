@@ -432,7 +432,18 @@ class XgmiCommunicator:
         torch.cuda.synchronize(self.device)
         e = self.error()
         if e:
-            raise CommError(f"rank {self.rank}: {_describe(e)} (error word {e:#x})")
+            raise CommError(f"rank {self.rank}: {_describe(e)} (error word {e:#x}){self._ctl_note()}")
+
+    def _ctl_note(self) -> str:
+        """The rank's control words for a failure report: the launch epoch (compare it across
+        ranks: every rank runs the same launch sequence), the workgroup ticket (0 between
+        launches) and the epochs of the last launches whose S / R reads peers wait for."""
+        try:
+            w = list(self._c.ctl_words())
+        except Exception:  # noqa: BLE001 - diagnostics must not mask the error
+            return ""
+        note = f"; launch epoch {w[0]}, ticket {w[1]}, reads-done epochs S {w[12]} R {w[13]}"
+        return note + (" - ticket not 0 between launches" if w[1] else "")
 
     def step_adamw(self, grads: torch.Tensor, params: torch.Tensor, state: dict, *, lr: float,
                    betas: tuple[float, float] = (0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
