@@ -11,9 +11,9 @@
 // two launches, the round trip of the reduced gradient through HBM and the serialisation
 // between the three steps; the wire bytes are those of one allreduce.
 //
-// Slot reuse across launches is the two-shot argument: a rank finishes a launch only after
-// it has received every owner's updated chunk, which each owner sends after reading its S
-// slot for that chunk.
+// Slot reuse across launches is the two-shot's: a rank finishes a launch only after it has
+// received every owner's updated chunk, which each owner sends after reading its S slot for
+// that chunk; peers' pending reads of R are covered by entry_guard / finish_launch_done.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -92,7 +92,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a)
   const int nu = (P - 1) * a.nch;
 
   // Phase 1 - gradient ScatterBlock: chunk c of block j to its owner j
-  if (static_cast<int>(blockIdx.x) < nu) entry_guard(a, ctl, r, kHazS, -1, deadline, err);
+  if (static_cast<int>(blockIdx.x) < nu) entry_guard(a, ctl, r, epoch, kHazS, -1, deadline, err);
   for (int u = blockIdx.x; u < nu; u += G) {
     const int c = u / Pm1;
     const int j = (r + 1 + u % Pm1) % P;

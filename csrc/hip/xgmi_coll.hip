@@ -56,7 +56,7 @@ __global__ __launch_bounds__(kCommThreads) void coll_kernel(CommArgs a) {
 
   constexpr uint32_t region = MODE == 1 ? kHazR : kHazS;
   // Phase 1: push this rank's part for peer j into j's slab (rotated peer order)
-  if (static_cast<int>(blockIdx.x) < nu) entry_guard(a, ctl, r, region, -1, deadline, err);
+  if (static_cast<int>(blockIdx.x) < nu) entry_guard(a, ctl, r, epoch, region, -1, deadline, err);
   for (int u = blockIdx.x; u < nu; u += G) {
     const int c = u / Pm1;
     const int j = (r + 1 + u % Pm1) % P;

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
   // copies keep the scatter at copy speed ("flat" geometry, launch_segment).
   const int gs = a.sgroup > 1 ? a.sgroup : 1;
   const int nsu = Pm1 * ((a.nch + gs - 1) / gs);
-  if (static_cast<int>(blockIdx.x) < nsu) entry_guard(a, ctl, r, kHazS, -1, deadline, err);  // block-uniform
+  if (static_cast<int>(blockIdx.x) < nsu) entry_guard(a, ctl, r, epoch, kHazS, -1, deadline, err);  // block-uniform
   for (int u = blockIdx.x; u < nsu; u += G) {
     const int c0 = (u / Pm1) * gs;
     const int ncg = a.nch - c0 < gs ? a.nch - c0 : gs;
@@ -263,12 +263,17 @@ __global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
   const int64_t slot = a.slot_bytes;
   uint32_t* err = &ctl[2];
   const bool rel = a.fence & 1, acq = a.fence & 2;
-  if (static_cast<int>(blockIdx.x) < a.nch) entry_guard(a, ctl, r, kHazS, -1, deadline, err);
+  // slots alternate between the S and R regions by epoch parity: a fast rank's next one-shot
+  // pushes into the region its peers are NOT reading (no guard poll between one-shots)
+  const bool odd = epoch & 1u;
+  const int64_t region_off = odd ? a.off_R : a.off_S;
+  const uint32_t region = odd ? kHazR : kHazS;
+  if (static_cast<int>(blockIdx.x) < a.nch) entry_guard(a, ctl, r, epoch, region, -1, deadline, err);
   for (int c = blockIdx.x; c < a.nch; c += G) {
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     const int64_t len = clamp_len(a.n - cstart, a.chunk);
     if (len > 0 && unit_in_bounds(a, cstart * es, len * es, c, err))
-      push_to_peers<E>(a, P, r, a.off_S + r * slot + cstart * es, in + cstart * es, len);
+      push_to_peers<E>(a, P, r, region_off + r * slot + cstart * es, in + cstart * es, len);
     publish_flags([&](int k) { return f1(a, k, r, c); }, P, epoch, rel);
   }
   read_delay(a, r);
@@ -278,12 +283,12 @@ __global__ __launch_bounds__(kCommThreads) void oneshot_kernel(CommArgs a) {
     wait_flags([&](int s) -> const uint32_t* { return f1(a, r, s, c); }, P, epoch, deadline, err, ERR_TIMEOUT_SCATTER,
                acq);
     if (len > 0 && unit_in_bounds(a, cstart * es, len * es, c, err)) {
-      const RedSrc src{in + cstart * es, a.base[r] + a.off_S + cstart * es, slot, r};
+      const RedSrc src{in + cstart * es, a.base[r] + region_off + cstart * es, slot, r};
       char* o = out + cstart * es;
       reduce_to<E, PT>(P, src, 1, 0, [&](int) -> char* { return o; }, len, a.scale, a.fence & 1);
     }
   }
-  finish_launch_done(a, ctl, epoch, r, kHazS);  // peers may still reduce from S
+  finish_launch_done(a, ctl, epoch, r, region);  // peers may still reduce from this region
 }
 
 // ---------------------------------------------------------------------------------
@@ -430,7 +435,7 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
   const bool rel = a.fence & 1, acq = a.fence & 2;
   __shared__ uint64_t ps_lds[kPhaseSlots];
   PhaseStamps ps(a, ps_lds);  // ring: [1] = end of the reduce-scatter hops, [2]/[4] = waits in RS / AG
-  if (static_cast<int>(blockIdx.x) < a.nch) entry_guard(a, ctl, r, kHazS | kHazR, nxt, deadline, err);
+  if (static_cast<int>(blockIdx.x) < a.nch) entry_guard(a, ctl, r, epoch, kHazS | kHazR, nxt, deadline, err);
   for (int c = blockIdx.x; c < a.nch; c += gridDim.x) {
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
     auto blen = [&](int b) { return clamp_len(clamp_len(a.n - static_cast<int64_t>(b) * a.block, a.block) - cstart, a.chunk); };

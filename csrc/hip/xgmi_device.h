@@ -320,11 +320,12 @@ __device__ __forceinline__ uint32_t launch_epoch(const uint32_t* ctl) {
 // slot reads can still be pending at peers once it has completed locally records the
 // region(s) in ctl[12] (S) / ctl[13] (R) as its epoch and, from its last workgroup, writes
 // "launch e done" into every peer's FB word once every workgroup's loads have returned.
-// A launch that pushes into a region first waits until the target peers' FB words reached
-// that region's recorded epoch - normally already true, so one local load per peer issued
-// beside the epoch load. Every rank runs the same launch sequence, so the local words name
+// A launch that pushes into a region whose reads were left by the PREVIOUS launch first
+// waits until the target peers' FB words reached that epoch (normally already true: one
+// local load per peer). Every rank runs the same launch sequence, so the local words name
 // the peers' epochs too. Two-shot chains record only R (their S reads end before any rank
-// can complete) and push S first, so back-to-back two-shot segments never wait here.
+// can complete) and push S first, and one-shot launches alternate between the S and R
+// regions by epoch parity, so back-to-back two-shot or one-shot launches never poll.
 // The low-latency kernel keeps its own parity slots and takes no part; the threshold kernel
 // has its own progress-word gate (xgmi_threshold.hip).
 enum : uint32_t { kHazS = 1u, kHazR = 2u };
@@ -336,18 +337,23 @@ __device__ __forceinline__ uint32_t later_epoch(uint32_t x, uint32_t y) {
 }
 
 // All threads call. `only` >= 0 waits for that peer alone (ring: the only rank it writes).
-__device__ __forceinline__ void entry_guard(const CommArgs& a, const uint32_t* ctl, int r, uint32_t regions,
-                                            int only, uint64_t deadline, uint32_t* err) {
+// Only the PREVIOUS launch's reads can still be pending: every kernel waits for flags of its
+// own epoch from every peer before it can complete (the ring transitively, through its hops),
+// so a peer whose flags this rank saw in launch e-1 had finished every launch before it
+// (stream order). A hazard older than e-1 costs the two control-word loads (beside the
+// epoch load, same line) and nothing else.
+__device__ __forceinline__ void entry_guard(const CommArgs& a, const uint32_t* ctl, int r, uint32_t epoch,
+                                            uint32_t regions, int only, uint64_t deadline, uint32_t* err) {
   if (a.noguard) return;  // uniform
+  const uint32_t hs = (regions & kHazS) ? __hip_atomic_load(&ctl[12], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+  const uint32_t hr = (regions & kHazR) ? __hip_atomic_load(&ctl[13], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+  const uint32_t h = later_epoch(hs, hr);
+  if (h == 0 || h != epoch - 1u) return;  // uniform: every thread loaded the same words
   if (threadIdx.x < 64) {
     const int k = static_cast<int>(threadIdx.x);
     const bool mine = k < a.P && k != r && (only < 0 || k == only);
     const uint32_t* f = mine ? fb(a, r, k) : nullptr;
-    const uint32_t v = f != nullptr ? ld_flag(f) : 0u;  // issued beside the hazard loads
-    const uint32_t hs = (regions & kHazS) ? __hip_atomic_load(&ctl[12], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    const uint32_t hr = (regions & kHazR) ? __hip_atomic_load(&ctl[13], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    const uint32_t h = later_epoch(hs, hr);
-    bool ok = h == 0 || f == nullptr || reached(v, h);
+    bool ok = f == nullptr || reached(ld_flag(f), h);
     while (!__all(ok)) {
       __builtin_amdgcn_s_sleep(1);
       if (!ok) ok = reached(ld_flag(f), h);
