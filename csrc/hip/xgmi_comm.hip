@@ -425,6 +425,7 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
   const int y = blockIdx.y;
   const int r = a.rank0 + y;
   const int nxt = (r + 1) % P;
+  const int prv = (r + P - 1) % P;
   const char* const in = a.in[y];
   char* const out = a.out[y];
   uint32_t* const ctl = a.ctl[y];
@@ -442,34 +443,34 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
     auto at = [&](int b) { return (static_cast<int64_t>(b) * a.block + cstart) * es; };
     const int64_t pofs = cstart * 4;  // fp32 partial slots
     // every S access of this chunk is fp32 [cstart, cstart + chunk), every R access E-typed
-    const bool inb = unit_in_bounds(a, pofs, clamp_len(a.block - cstart, a.chunk) * 4, c, err);
+    const bool inb = unit_in_bounds(a, pofs, clamp_len(a.block - cstart, a.chunk) * 4, (P - 2) * a.nch + c, err);
     if (!inb) {  // publish every flag this workgroup owes, move no data
-      publish_flags([&](int) { return f1(a, nxt, 0, c); }, 1, epoch, rel);
+      publish_flags([&](int) { return f1(a, nxt, r, c); }, 1, epoch, rel);
       continue;
     }
     // RS step 0: raw own block r, widened to fp32
     {
       const int64_t len = blen(r);
       if (len > 0) ring_hop<E>(nullptr, in + at(r), a.base[nxt] + a.off_S + pofs, nullptr, nullptr, len, 1.f);
-      publish_flags([&](int) { return f1(a, nxt, 0, c); }, 1, epoch, rel);
+      publish_flags([&](int) { return f1(a, nxt, r, c); }, 1, epoch, rel);
     }
     // RS steps 1..P-1 (the last one completes block r+1)
     for (int s = 1; s < P; ++s) {
       const int b = (r - s + P) % P;
       const int64_t len = blen(b);
       const uint64_t tw = ps.now();
-      wait_flags([&](int) -> const uint32_t* { return f1(a, r, s - 1, c); }, 1, epoch, deadline, err,
+      wait_flags([&](int) -> const uint32_t* { return f1(a, r, prv, (s - 1) * a.nch + c); }, 1, epoch, deadline, err,
                  ERR_TIMEOUT_SCATTER, acq);
       ps.add(2, tw);
       ps.count(6);
       const char* part = a.base[r] + a.off_S + (s - 1) * slot + pofs;
       if (s < P - 1) {
         if (len > 0) ring_hop<E>(part, in + at(b), a.base[nxt] + a.off_S + s * slot + pofs, nullptr, nullptr, len, 1.f);
-        publish_flags([&](int) { return f1(a, nxt, s, c); }, 1, epoch, rel);
+        publish_flags([&](int) { return f1(a, nxt, r, s * a.nch + c); }, 1, epoch, rel);
       } else {
         if (len > 0)
           ring_hop<E>(part, in + at(b), nullptr, out + at(b), a.base[nxt] + a.off_R + cstart * es, len, a.scale);
-        publish_flags([&](int) { return f2(a, nxt, 0, c); }, 1, epoch, rel);
+        publish_flags([&](int) { return f2(a, nxt, r, c); }, 1, epoch, rel);
       }
     }
     // AG steps: receive block (r - t), forward unless it is the last hop
@@ -478,14 +479,14 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
       const int b = (r - t + P) % P;
       const int64_t len = blen(b);
       const uint64_t tw = ps.now();
-      wait_flags([&](int) -> const uint32_t* { return f2(a, r, t, c); }, 1, epoch, deadline, err, ERR_TIMEOUT_REDUCE,
-                 acq);
+      wait_flags([&](int) -> const uint32_t* { return f2(a, r, prv, t * a.nch + c); }, 1, epoch, deadline, err,
+                 ERR_TIMEOUT_REDUCE, acq);
       ps.add(4, tw);
       ps.count(7);
       const bool fwd = t < P - 2;
       char* d = fwd ? a.base[nxt] + a.off_R + (t + 1) * slot + cstart * es : nullptr;
       if (len > 0) copy_slab_fwd<E>(out + at(b), d, a.base[r] + a.off_R + t * slot + cstart * es, len);
-      if (fwd) publish_flags([&](int) { return f2(a, nxt, t + 1, c); }, 1, epoch, rel);
+      if (fwd) publish_flags([&](int) { return f2(a, nxt, r, (t + 1) * a.nch + c); }, 1, epoch, rel);
     }
   }
   ps.mark(3);
@@ -844,10 +845,19 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
     a.subchunk = a.chunk;
     gx = static_cast<int>(std::min<int64_t>(gmax, a.nch));
   } else if (kind == Algo::Ring) {
-    // one chunk per workgroup, carried around the whole ring by that workgroup
+    // one chunk per workgroup, carried around the whole ring by that workgroup. Hop flags sit
+    // in the row of the WRITER (the previous rank), one column block per hop: every flag word
+    // has a single writer across all kernels, so epochs never go backwards (a ring's late
+    // forward of launch e-1 landing on a word another rank's all-gather set to e lost that
+    // flag - profiles/round3/README.md); (W - 1) * nch columns must fit the flag row.
     a.block = round_up(ceil_div(n, W), elems);
     a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, gmax), elems));
     a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
+    const int64_t cols = std::max<int64_t>(1, c0.maxch_ / std::max(1, W - 1));
+    if (a.nch > cols) {
+      a.chunk = round_up(ceil_div(a.block, cols), elems);
+      a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
+    }
     a.subchunk = a.chunk;
     gx = static_cast<int>(std::min<int64_t>(gmax, a.nch));
   } else {
@@ -908,7 +918,9 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   a.stamps = c0.stamps_;
   if (a.stamps != nullptr && gx * ranks_here > c0.stamp_slots_) a.stamps = nullptr;  // buffer too small: off
   const int64_t block_bytes = a.block * (kind == Algo::Ring ? 4 : es);  // ring: fp32 partial slots
-  if (kind != Algo::LL && (static_cast<int64_t>(a.nch) * a.sub > c0.maxch_ || block_bytes > c0.slot_bytes_ + 16))
+  const int64_t flag_cols = kind == Algo::Ring ? static_cast<int64_t>(std::max(1, W - 1)) * a.nch
+                                              : static_cast<int64_t>(a.nch) * a.sub;
+  if (kind != Algo::LL && (flag_cols > c0.maxch_ || block_bytes > c0.slot_bytes_ + 16))
     throw std::logic_error("XgmiComm: segment geometry exceeds slab");
   const dim3 grid(gx, ranks_here);
   if (adam != nullptr) {
