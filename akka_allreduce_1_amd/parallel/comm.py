@@ -27,6 +27,7 @@ _H = C.hip
 
 ALGOS = {"auto": _H.Algo.Auto, "twoshot": _H.Algo.TwoShot, "oneshot": _H.Algo.OneShot, "ring": _H.Algo.Ring,
          "ll": _H.Algo.LL}
+LIBRARY_ALGOS = ("rccl", "rsag", "p2p")  # timed for comparison, never picked by tune()
 DEFAULT_SLOT_BYTES = int(os.environ.get("MXAR_SLOT_BYTES", 64 << 20))
 
 
@@ -230,8 +231,14 @@ class XgmiCommunicator:
                 dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
                 row[f"{algo}_p50_us"] = round(t.item() * 1e3, 2)
                 row[f"{algo}_algbw"] = round(size / (t.item() / 1e3) / 1e9, 2)
-                if t.item() < best_t:
+                # library paths are comparison columns: the table only ever holds this
+                # framework's kernels (a split of RCCL vs xGMI is reported, never adopted)
+                if algo not in LIBRARY_ALGOS and t.item() < best_t:
                     best, best_t = algo, t.item()
+            if best is None:  # only library candidates were given: keep the built-in policy
+                best = "auto"
+            if "rccl_p50_us" in row and best != "auto":
+                row["speedup_vs_rccl"] = round(row["rccl_p50_us"] / row[f"{best}_p50_us"], 3)
             choice = [best]
             dist.broadcast_object_list(choice, src=src0, group=self.cpu_group)
             row["choice"] = choice[0]
@@ -242,10 +249,14 @@ class XgmiCommunicator:
         return rows
 
     def _pick(self, nbytes: int) -> str:
+        """The tuned kernel label for a message of `nbytes` ("auto" = built-in size policy).
+        Never a library path: tune() does not adopt them, and a hand-set table entry naming
+        one is ignored here too."""
         for limit, algo in self.table:
             if nbytes <= limit:
-                return algo
-        return self.table[-1][1] if self.table else "auto"
+                return "auto" if algo.split("@")[0] in LIBRARY_ALGOS else algo
+        tail = [a for _, a in self.table if a.split("@")[0] not in LIBRARY_ALGOS]
+        return tail[-1] if tail else "auto"
 
     # ------------------------------------------------------------------ collectives
     def allreduce(self, inp: torch.Tensor, out: torch.Tensor | None = None, *, op: str = "sum",

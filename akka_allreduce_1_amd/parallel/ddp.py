@@ -285,20 +285,19 @@ class BucketedGradReducer:
         (a schedule is as fast as its slowest rank), then the fastest candidate - the same
         index on every rank (ties: the first)."""
         best = torch.tensor(list(times), dtype=torch.float64)
-        try:
-            import torch.distributed as dist
+        import torch.distributed as dist
 
-            if dist.is_available() and dist.is_initialized():
-                grp = getattr(self.comm, "cpu_group", None)
-                if grp is not None or not self.on_gpu:  # a gloo group: a CPU tensor
-                    dist.all_reduce(best, op=dist.ReduceOp.MAX, group=grp if grp is not None else
-                                    getattr(self.comm, "group", None))
-                else:
-                    t = best.to(self.device)
-                    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=getattr(self.comm, "group", None))
-                    best = t.cpu()
-        except Exception:  # noqa: BLE001 - no process group: this rank alone decides
-            pass
+        # Only a job without a process group decides alone. With one, a failing MAX reduce
+        # must raise: ranks keeping different schedules would launch different kernels.
+        if dist.is_available() and dist.is_initialized():
+            grp = getattr(self.comm, "cpu_group", None)
+            if grp is not None or not self.on_gpu:  # a gloo group: a CPU tensor
+                dist.all_reduce(best, op=dist.ReduceOp.MAX, group=grp if grp is not None else
+                                getattr(self.comm, "group", None))
+            else:
+                t = best.to(self.device)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=getattr(self.comm, "group", None))
+                best = t.cpu()
         return int(torch.argmin(best).item()), best
 
     def tune_schedule(self, tune_steps: int = 2, candidates: Sequence[tuple[bool, str]] | None = None) -> None:

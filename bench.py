@@ -281,6 +281,20 @@ def local_ranks(dev, args, P: int = 8) -> dict:
     return row
 
 
+def resolve_auto(comm: XgmiCommunicator, n: int, dtype: torch.dtype) -> str:
+    """Name of the kernel the native size policy (Algo.Auto) runs for n elements."""
+    from akka_allreduce_1_amd._native import C
+
+    names = {int(C.hip.Algo.TwoShot): "twoshot", int(C.hip.Algo.OneShot): "oneshot",
+             int(C.hip.Algo.Ring): "ring", int(C.hip.Algo.LL): "ll"}
+    from akka_allreduce_1_amd.parallel.comm import _KERNEL_DTYPES
+
+    try:
+        return names.get(int(comm._c.resolve(n, _KERNEL_DTYPES[dtype], C.hip.Algo.Auto, 1)), "auto")
+    except Exception:  # noqa: BLE001 - the label only
+        return "auto"
+
+
 def timed_local(fn, steps: int, dev) -> float:
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -359,6 +373,8 @@ def fused_step(comm: XgmiCommunicator, grads: torch.Tensor, params: torch.Tensor
         comm.check()
         row["speedup"] = round(row["unfused_ms"] / row["fused_ms"], 3)
         row["params"] = params.numel()
+        if world == 1:  # bytes per param: bf16 grad in + bf16 param out + fp32 master/m/v in and out
+            row["hbm_TBps"] = round(28 * params.numel() / (row["fused_ms"] / 1e3) / 1e12, 3)
     except Exception as e:  # noqa: BLE001 - reported, never loses the headline
         row["error"] = repr(e)
     return row
@@ -638,6 +654,32 @@ _EMIT_LOCK = threading.Lock()
 _EMITTED = [False]
 
 
+_DETAIL = {"path": None}
+
+
+def write_detail(result: dict) -> str | None:
+    """The full result dict (every section, size and candidate) goes to a side file; the
+    stdout line carries compact summaries and names this file (benchmarks/summary.py)."""
+    path = _DETAIL["path"]
+    if not path:
+        return None
+    try:
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(result, f, indent=1)
+        return path
+    except OSError as e:
+        log(0, f"could not write {path}: {e}")
+        return None
+
+
+def result_line(result: dict) -> str:
+    """ONE JSON line <= summary.LINE_BUDGET bytes, the full dict written to the detail file."""
+    from benchmarks.summary import line
+
+    return line(result, write_detail(result)) + "\n"
+
+
 def emit(rank: int, result: dict) -> bool:
     """Write the ONE result line (rank 0), at most once per process: the dp watchdog and the
     main path may both get here. Returns True for the caller that wrote it."""
@@ -646,9 +688,10 @@ def emit(rank: int, result: dict) -> bool:
             return False
         _EMITTED[0] = True
         if rank == 0:
+            text = result_line(result)
             sys.stdout.flush()
             with os.fdopen(_RESULT_FD, "w") as out:
-                out.write(json.dumps(result) + "\n")
+                out.write(text)
         return True
 
 
@@ -679,12 +722,17 @@ def main() -> None:
     ap.add_argument("--dp-rehearsal", action="store_true", help="with --share-device: run the ResNet-50 DP step too")
     ap.add_argument("--dp-timeout", type=float, default=240.0,
                     help="seconds for the DP-step sections; past it the result line is written without them")
+    ap.add_argument("--detail-out", default=None,
+                    help="side file for the full result dict (default gpurun_out/bench_detail_n<N>.json; '' = none)")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal: every rank on cuda:0 over gloo (RCCL refuses two ranks on one GPU), "
                          "workgroup budget split between the ranks so all spinning workgroups stay resident")
     args = ap.parse_args()
 
     rank, world, local = init_distributed("gloo" if args.share_device else "nccl")
+    if rank == 0:
+        _DETAIL["path"] = (os.path.join("gpurun_out", f"bench_detail_n{world}.json") if args.detail_out is None
+                           else args.detail_out or None)
     if world != args.gpus:
         log(rank, f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
     grid = 0
@@ -745,35 +793,43 @@ def main() -> None:
                 comm.reset()
             except Exception as e:  # noqa: BLE001 - recorded, the run degrades to RCCL
                 engine_ok, reason = False, f"reset after failed validation: {e!r}"
-    ok_algos = {k for k, v in (validated or {}).items() if v["validated"]} | {"rccl", "rsag"}
+    ok_algos = {k for k, v in (validated or {}).items() if v["validated"]}
     sweep = None
     if engine_ok and not args.no_tune and world > 1:  # at world = 1 every candidate is the same copy
-        rccl_algos = () if args.no_rccl else ("rccl", "rsag") if world > 1 else ("rccl",)
-        cands = ("ll", "oneshot", "twoshot", "ring") + (("threshold",) if world > 1 else ()) + rccl_algos
-        sweep = comm.tune(max_bytes=nbytes, dtype=dtype, iters=args.sweep_steps,
-                          candidates=tuple(c for c in cands if c in ok_algos), grids=(128, 256))
+        # RCCL / RS+AG are timed as comparison columns (rccl_p50_us, speedup_vs_rccl per size):
+        # tune() never adopts a library path, so the headline is always this engine's kernel
+        lib = () if args.no_rccl else ("rccl", "rsag")
+        cands = tuple(c for c in ("ll", "oneshot", "twoshot", "ring", "threshold") if c in ok_algos) + lib
+        sweep = comm.tune(max_bytes=nbytes, dtype=dtype, iters=args.sweep_steps, candidates=cands,
+                          grids=(128, 256))
+    status = "ok"
     if engine_ok and args.algo != "rccl":
         algo = args.algo
         chosen = comm._pick(nbytes) if algo == "auto" else algo
+        if world > 1 and chosen == "auto":  # the built-in size policy: name the kernel it runs
+            chosen = resolve_auto(comm, n, dtype)
         # never time an unvalidated kernel ("auto" without a tuned table is the size-default
-        # dispatch, checked by validate() above)
+        # dispatch, checked by validate() above); a failure is reported as such, never
+        # replaced by the library's number
         if world > 1 and chosen.split("@")[0].split("~")[0] not in ok_algos | {"auto"}:
-            log(rank, f"headline algorithm {chosen} failed validation: timing RCCL instead")
-            algo = chosen = "rccl"
+            log(rank, f"headline algorithm {chosen} failed validation")
+            status = f"headline kernel {chosen} failed validation"
         elif world > 1 and sweep is not None:
             # the tuned headline configuration (algorithm, grid, geometry) at the full size
             ok_tuned, err_tuned = validate(comm, n, dtype, dev, rank, world)
             if not ok_tuned:
-                log(rank, f"tuned headline {chosen} failed validation (max err {err_tuned:.3g}): timing RCCL")
+                log(rank, f"tuned headline {chosen} failed validation (max err {err_tuned:.3g})")
                 comm.reset()
-                algo = chosen = "rccl"
+                status = f"tuned headline {chosen} failed validation"
+                algo = chosen = "twoshot"
         if world == 1:  # XgmiComm::run: a 1-rank sum is an out-of-place copy, whatever the algorithm
             chosen = "copy (world=1)"
 
         def step():
             comm.allreduce(x, y, algo=algo)
     else:
-        chosen = "rccl" if engine_ok else "rccl-fallback"
+        chosen = "rccl (--algo rccl)" if engine_ok else "rccl-fallback"
+        status = "ok" if engine_ok else "engine_failed: value is RCCL's, not this framework's"
         step = step_rccl
 
     log(rank, f"headline: {chosen}, {args.warmup} + {args.steps} steps")
@@ -819,7 +875,7 @@ def main() -> None:
         "busbw": round(busbw(algbw, world), 2),
         "validated_max_abs_err": err,
         "engine_ok": engine_ok,
-        "status": "ok",
+        "status": status,
     }
     if world == 1:
         result["value_note"] += ("; world=1: the allreduce is an out-of-place HBM copy (no communication) - "
@@ -835,13 +891,13 @@ def main() -> None:
     if reason:
         result["engine_note"] = reason
 
-    if engine_ok and chosen.partition("@")[0] != "twoshot" and world > 1:
+    if engine_ok and not chosen.startswith("twoshot") and world > 1:
         for _ in range(args.warmup):
             comm.allreduce(x, y, algo="twoshot")
         twall = timed(lambda: comm.allreduce(x, y, algo="twoshot"), args.steps, dev)
         tms = max_over_ranks(twall, dev) / args.steps * 1e3
         result["xgmi_twoshot"] = {"algbw": round(nbytes / (tms / 1e3) / 1e9, 2), "ms_per_step": round(tms, 4)}
-    if not args.no_rccl and chosen not in ("rccl", "rccl-fallback") and world > 1:
+    if not args.no_rccl and not chosen.startswith("rccl") and world > 1:
         # (at world = 1 RCCL's allreduce is a no-op after a copy: nothing to compare)
         for _ in range(args.warmup):
             step_rccl()
@@ -911,7 +967,7 @@ def main() -> None:
                          status="protocol_timeout")
         sys.stdout.flush()
         cancel = C.watchdog_arm(args.protocol_timeout, _RESULT_FD if rank == 0 else -1,
-                                json.dumps(timed_out) + "\n", 3)
+                                result_line(timed_out) if rank == 0 else "\n", 3)
         prot = protocol_rounds(args, rank, world, dev)
         if world == 1 and not args.no_sizes:
             from benchmarks.sections import protocol_sizes
@@ -940,7 +996,8 @@ def main() -> None:
 
         timed_out = dict(result, dp={"error": f"timed out after {args.dp_timeout:g} s"}, status="dp_timeout")
         sys.stdout.flush()
-        cancel = C.watchdog_arm(args.dp_timeout, _RESULT_FD if rank == 0 else -1, json.dumps(timed_out) + "\n", 3)
+        cancel = C.watchdog_arm(args.dp_timeout, _RESULT_FD if rank == 0 else -1,
+                                result_line(timed_out) if rank == 0 else "\n", 3)
         log(rank, "dp: ResNet-50 / Llama-3-8B data-parallel steps")
         dp = {m: dp_step(comm, m, dev) for m in (("resnet50",) if args.share_device else ("resnet50", "llama3_8b"))}
         if world == 1 and not args.share_device and not args.no_sizes:

@@ -601,6 +601,11 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   if (const char* e = std::getenv("MXAR_ONESHOT_MAX")) oneshot_max_ = std::min<int64_t>(slot_bytes_, std::atoll(e));
   if (grid_ <= 0) grid_ = default_grid(device);
   if (const char* f = std::getenv("MXAR_FENCE")) fence_ = std::atoi(f) & 3;
+  // Slab reads are `nt` loads: the acquire after each wait (bit 1) is what orders them after
+  // the peers' flags. Without it a stale line could be read, so clearing it is a study-only
+  // setting that must be asked for explicitly.
+  if (!(fence_ & 2) && !std::getenv("MXAR_STUDY"))
+    throw std::invalid_argument("MXAR_FENCE without bit 1 (acquire) needs MXAR_STUDY=1: slab reads rely on it");
   if (const char* u = std::getenv("MXAR_TWOSHOT_UNITS")) units_per_wg_ = std::max(1, std::atoi(u));
   if (const char* u = std::getenv("MXAR_TWOSHOT_SUB")) sub_max_ = std::max(1, std::atoi(u));
   if (const char* d = std::getenv("MXAR_TWOSHOT_DYNAMIC")) dynamic_ = std::atoi(d) != 0;

@@ -152,18 +152,23 @@ __device__ __forceinline__ void copy_out(char* dst, const char* slab_src, int64_
   for (int64_t t = threadIdx.x; t < len; t += kCommThreads) st_scalar_wt<E>(rd, t, ld_scalar_nt<E>(rs, t));
 }
 
+// Zeros for a given-up chunk of the output. Write-through (sc0 sc1) like every other output
+// store of this kernel when the host takes the round's completion from the done word
+// (`done_out`): the output is then handed on before the kernel ends, so no store may sit in
+// this XCD's L2 waiting for the end-of-kernel writeback.
 template <class E>
 __device__ __forceinline__ void zero_fill(char* dst, int64_t len) {
+  const __amdgpu_buffer_rsrc_t rd = slab_rsrc(dst);
   if (al16(dst)) {
     const int64_t npk = len / E::ELEMS;
     Pack16 z;
     z[0] = z[1] = z[2] = z[3] = 0u;
-    for (int64_t i = threadIdx.x; i < npk; i += kCommThreads) st16(dst + i * 16, z);
+    for (int64_t i = threadIdx.x; i < npk; i += kCommThreads) st16_wt(rd, static_cast<uint32_t>(i * 16), z);
     const int64_t t = npk * E::ELEMS + threadIdx.x;
-    if (t < len) Scalar<E>::store(dst, t, 0.f);
+    if (t < len) st_scalar_wt<E>(rd, t, 0.f);
     return;
   }
-  for (int64_t t = threadIdx.x; t < len; t += kCommThreads) Scalar<E>::store(dst, t, 0.f);
+  for (int64_t t = threadIdx.x; t < len; t += kCommThreads) st_scalar_wt<E>(rd, t, 0.f);
 }
 
 // Sum the sources in `mask` (fixed order s = 0..P-1, fp32), store to the own output (when
@@ -656,7 +661,8 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
     char* own_out = out + (bstart_own + cstart) * es;
     if (len > 0) {
       reduce_masked<E>(a, P, r, mask, in + (bstart_own + cstart) * es, a.base[r] + rowS + cstart * es, slot,
-                       take ? own_out : nullptr, rowR + r * slot + cstart * es, len, a.fence & 1, sc);
+                       take ? own_out : nullptr, rowR + r * slot + cstart * es, len,
+                       (a.fence & 1) || a.done_out != nullptr, sc);
       if (!take) zero_fill<E>(own_out, len);
     }
     // a split chunk is reduced once its last slice is: that workgroup publishes it
@@ -874,8 +880,9 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       for (int k = 0; k < P; ++k)
         if (k != r) st_flag(prog(a, k, r), epoch);
-      // the host's completion hint: every workgroup has passed its ticket (the host still
-      // waits for the round's event before it hands the output on)
+      // the round's completion word: every workgroup has passed its ticket and every output
+      // store was write-through (zero_fill, reduce_masked with wt_out), so the host may hand
+      // the output on at once, before the kernel itself ends (xgmi_plane.cc)
       if (a.done_out) st_flag(a.done_out, epoch);
     }
   }
