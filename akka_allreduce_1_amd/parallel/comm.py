@@ -26,7 +26,7 @@ from .._native import C
 _H = C.hip
 
 ALGOS = {"auto": _H.Algo.Auto, "twoshot": _H.Algo.TwoShot, "oneshot": _H.Algo.OneShot, "ring": _H.Algo.Ring,
-         "ll": _H.Algo.LL}
+         "ll": _H.Algo.LL, "ring_native": _H.Algo.RingNative}
 LIBRARY_ALGOS = ("rccl", "rsag", "p2p")  # timed for comparison, never picked by tune()
 DEFAULT_SLOT_BYTES = int(os.environ.get("MXAR_SLOT_BYTES", 64 << 20))
 
@@ -202,7 +202,7 @@ class XgmiCommunicator:
             labels = []
             for algo in candidates:
                 labels.append(algo)
-                if algo in ("twoshot", "ring") and size >= grid_min_bytes:
+                if algo in ("twoshot", "ring", "ring_native") and size >= grid_min_bytes:
                     labels += [f"{algo}@{g}" for g in extra]
                 if algo == "twoshot" and self.world > 2 and self._default_units == 0 and size // self.world >= (2 << 20):
                     labels += ["twoshot~1"] + [f"twoshot@{g}~1" for g in extra]

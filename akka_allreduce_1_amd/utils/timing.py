@@ -23,6 +23,12 @@ def hbm_bytes(S: int, P: int, algo: str, es: int = 4) -> float:
     """HBM bytes the kernels move when P logical ranks of ONE GPU allreduce S bytes each of an
     `es`-byte element type (every rank's traffic lands in the same HBM; counts checked against
     rocprofv3 PMC FETCH_SIZE / WRITE_SIZE in profiles/pmc_counters.md)."""
+    if algo == "ring_native":
+        # element-type partials: hop 0 reads in + writes B, hops 1..P-2 read partial + in and
+        # write B, the final hop reads 2 B and writes out + fwd, AG hops read B and write out +
+        # fwd (the last one out only)
+        B = S / P
+        return P * B * (6 * P - 4)
     if algo == "ring":
         # per rank, blocks B = S/P: RS hops read in (+ an fp32 partial) and push an fp32 partial
         # (Bp = B * 4 / es: 2 (P - 1) partial transfers), the final hop and the AG hops move

@@ -5,8 +5,9 @@ driver reads only the last stdout line and truncates long lines, so the full dic
 side file (`detail`), and the line holds the headline fields plus compact summaries:
 
   sweep          N > 1: per size class [bytes, chosen xGMI kernel, its p50 us, RCCL p50 us]
-  local_ranks    N = 1: 8 logical ranks in one launch, two-shot / ring [p50 ms, fraction of
-                 the same run's copy roofline]
+  local_ranks    N = 1: 8 logical ranks in one launch, two-shot / ring / element-type-wire
+                 ring [p50 ms, fraction of the same run's copy roofline, (ring) reduce-scatter
+                 wire bytes per rank per hop]
   lat_vs_size    N = 1: per P and size [bytes, best kernel, best p50 us, threshold p50 us]
   reduce_kernel  BASELINE config 2: fraction of the copy roofline per slot count
   protocol_us    the reference's round protocol, us per round per size (in-process, native
@@ -50,10 +51,12 @@ def _sweep(rows: list) -> list:
 
 def _local(lr: dict) -> dict:
     out = {"copy_TBps": lr.get("copy_roofline_TBps")}
-    for algo in ("twoshot", "ring", "ring_bf16"):
+    for algo in ("twoshot", "ring", "ring_native"):
         c = lr.get(algo)
         if isinstance(c, dict) and "p50_ms" in c:
             out[algo] = [c["p50_ms"], c.get("frac_copy_roofline")] + ([] if c.get("validated", True) else ["INVALID"])
+            if "wire_bytes_per_hop" in c:  # reduce-scatter hop bytes per rank (all-gather: the block)
+                out[algo].append(c["wire_bytes_per_hop"][0])
     if "error" in lr:
         out["error"] = str(lr["error"])[:160]
     return out

@@ -280,7 +280,7 @@ void bind_hip(py::module_& m) {
       py::arg("min_chunk") = 0,
       "RoundPlane of the protocol engine on MI355X: an HBM arena exported over IPC, one threshold-kernel launch "
       "per round (csrc/hip/xgmi_plane.h)");
-  py::enum_<Algo>(h, "Algo").value("Auto", Algo::Auto).value("TwoShot", Algo::TwoShot).value("OneShot", Algo::OneShot).value("Ring", Algo::Ring).value("LL", Algo::LL);
+  py::enum_<Algo>(h, "Algo").value("Auto", Algo::Auto).value("TwoShot", Algo::TwoShot).value("OneShot", Algo::OneShot).value("Ring", Algo::Ring).value("LL", Algo::LL).value("RingNative", Algo::RingNative);
   py::enum_<Coll>(h, "Coll")
       .value("AllToAll", Coll::AllToAll)
       .value("AllGather", Coll::AllGather)
@@ -458,6 +458,7 @@ void bind_hip(py::module_& m) {
       .def_property_readonly("stats", &XgmiComm::stats)
       .def_property("fence", &XgmiComm::fence, &XgmiComm::set_fence)
       .def_property("units_per_wg", &XgmiComm::units_per_wg, &XgmiComm::set_units_per_wg)
+      .def_property("ring_depth", &XgmiComm::ring_depth, &XgmiComm::set_ring_depth)
       .def("set_timeout", &XgmiComm::set_timeout)
       .def(
           "set_phase_stamps",

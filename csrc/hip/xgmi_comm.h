@@ -32,7 +32,9 @@ namespace mxar {
 enum class DType : int { F32 = 0, BF16 = 1, F16 = 2 };
 inline size_t dtype_size(DType d) { return d == DType::F32 ? 4 : 2; }
 
-enum class Algo : int { Auto = 0, TwoShot = 1, OneShot = 2, Ring = 3, LL = 4 };
+// Ring: fp32 partials on the reduce-scatter hops (rounded once); RingNative: partials in the
+// element type (half the RS wire bytes for 16-bit types, one rounding per hop).
+enum class Algo : int { Auto = 0, TwoShot = 1, OneShot = 2, Ring = 3, LL = 4, RingNative = 5 };
 
 // The reference's two allreduce phases as collectives of their own (xgmi_coll.hip).
 enum class Coll : int { AllToAll = 0, AllGather = 1, ReduceScatter = 2 };
@@ -248,6 +250,8 @@ class XgmiComm {
   int fence() const { return fence_; }
   int units_per_wg() const { return units_per_wg_; }
   void set_units_per_wg(int u) { units_per_wg_ = u > 0 ? u : 0; }
+  int ring_depth() const { return ring_depth_; }
+  void set_ring_depth(int d) { ring_depth_ = d > 0 ? d : 1; }
   void set_fence(int f) { fence_ = f & 3; }
   // Study knob: per-workgroup phase stamps of the two-shot / ring kernels (xgmi_device.h
   // PhaseStamps) into `buf` (device, >= slots x 8 u64; slots = workgroups x ranks in the
@@ -304,6 +308,7 @@ class XgmiComm {
   int64_t stamp_slots_ = 0;
   int units_per_wg_ = 0;  // two-shot scatter units per workgroup; 0 = by block size (launch_segment)
   int sub_max_ = 0;       // two-shot: most reduce pieces per chunk; 0 = by block size
+  int ring_depth_ = 4;    // ring: chunks per workgroup, walked step-major (MXAR_RING_DEPTH)
   char* slab_ = nullptr;            // own fine-grained slab (flags | S | R | LL)
   uint32_t* ctl_ = nullptr;         // [0] epoch, [1] ticket, [2] sticky error (device memory)
   char* peers_[kMaxRanks] = {};     // slab base of every rank (own included)

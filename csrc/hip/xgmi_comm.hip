@@ -342,20 +342,22 @@ __device__ __forceinline__ void copy_slab_fwd(char* out, char* next_slab, const 
   }
 }
 
-// One ring hop on fp32 partials. `partial` (fp32 slab, null on the first hop) + `in` (element
-// type E) -> either the next fp32 partial (`fwd_f32`, write-through into the next rank's S
-// slot) or, on the final hop, scale x sum rounded once to E into `out` and the next rank's R
-// slot (`fwd_e`). One E pack (16 B) of input per lane per step, E::ELEMS / 4 fp32 packs of
-// partial; two steps in flight per lane.
-template <class E>
-__device__ __forceinline__ void ring_hop(const char* partial, const char* in, char* fwd_f32, char* out, char* fwd_e,
+// One ring hop. `partial` (a WT-typed slab slot, null on the first hop) + `in` (element type
+// E), summed in fp32 -> either the next partial (`fwd_p`, write-through into the next rank's S
+// slot, rounded to WT) or, on the final hop, scale x sum rounded once to E into `out` and the
+// next rank's R slot (`fwd_e`). WT = F32 for a 16-bit E is the exact wire (partials travel
+// in fp32, E::ELEMS / 4 fp32 packs per E pack); WT = E is the element-type wire (half the RS
+// bytes, one extra rounding per intermediate hop). Two steps in flight per lane.
+template <class E, class WT>
+__device__ __forceinline__ void ring_hop(const char* partial, const char* in, char* fwd_p, char* out, char* fwd_e,
                                          int64_t len, float scale) {
-  constexpr int NP = E::ELEMS / 4;  // fp32 packs per E pack
+  constexpr bool wide = WT::ELEMS != E::ELEMS;
+  constexpr int NP = wide ? E::ELEMS / 4 : 1;  // partial packs per E pack
   const int64_t npk = len / E::ELEMS;
   const bool has_p = partial != nullptr;
   const __amdgpu_buffer_rsrc_t rp = slab_rsrc(has_p ? partial : in);
   const __amdgpu_buffer_rsrc_t ri = slab_rsrc(in);
-  const __amdgpu_buffer_rsrc_t rf = slab_rsrc(fwd_f32 != nullptr ? fwd_f32 : in);
+  const __amdgpu_buffer_rsrc_t rf = slab_rsrc(fwd_p != nullptr ? fwd_p : in);
   const __amdgpu_buffer_rsrc_t ro = slab_rsrc(out != nullptr ? out : in);
   const __amdgpu_buffer_rsrc_t re = slab_rsrc(fwd_e != nullptr ? fwd_e : in);
   constexpr int U = 2;
@@ -378,19 +380,27 @@ __device__ __forceinline__ void ring_hop(const char* partial, const char* in, ch
       Acc<E> acc;
       acc.zero();
       if (has_p) {
+        if constexpr (wide) {
 #pragma unroll
-        for (int h = 0; h < NP; ++h)
+          for (int h = 0; h < NP; ++h)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) acc.v[4 * h + q] = __uint_as_float(pv[u][h][q]);
+            for (int q = 0; q < 4; ++q) acc.v[4 * h + q] = __uint_as_float(pv[u][h][q]);
+        } else {
+          acc.add(pv[u][0]);
+        }
       }
       acc.add(xv[u]);
-      if (fwd_f32 != nullptr) {
+      if (fwd_p != nullptr) {
+        if constexpr (wide) {
 #pragma unroll
-        for (int h = 0; h < NP; ++h) {
-          Pack16 o;
+          for (int h = 0; h < NP; ++h) {
+            Pack16 o;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = __float_as_uint(acc.v[4 * h + q]);
-          st16_wt(rf, static_cast<uint32_t>((i * NP + h) * 16), o);
+            for (int q = 0; q < 4; ++q) o[q] = __float_as_uint(acc.v[4 * h + q]);
+            st16_wt(rf, static_cast<uint32_t>((i * NP + h) * 16), o);
+          }
+        } else {
+          st16_wt(rf, static_cast<uint32_t>(i * 16), acc.pack());
         }
       } else {
         if (scale != 1.f) acc.scale(scale);
@@ -405,11 +415,9 @@ __device__ __forceinline__ void ring_hop(const char* partial, const char* in, ch
   for (; i < npk; i += kCommThreads) step(i, 1);
   const int64_t t = npk * E::ELEMS + threadIdx.x;
   if (t < len) {  // ragged tail: one element per lane
-    float acc = (has_p ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rp, static_cast<int>(t * 4), 0, kAuxNt))
-                       : 0.f) +
-                ld_scalar_nt<E>(ri, t);
-    if (fwd_f32 != nullptr) {
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc), rf, static_cast<int>(t * 4), 0, kAuxWt);
+    float acc = (has_p ? ld_scalar_nt<WT>(rp, t) : 0.f) + ld_scalar_nt<E>(ri, t);
+    if (fwd_p != nullptr) {
+      st_scalar_wt<WT>(rf, t, acc);
     } else {
       acc *= scale;
       st_scalar_wt<E>(ro, t, acc);
@@ -418,9 +426,16 @@ __device__ __forceinline__ void ring_hop(const char* partial, const char* in, ch
   }
 }
 
-template <class E>
+// The workgroup's chunks are walked STEP-MAJOR: hop s of every chunk the workgroup owns
+// (c = blockIdx.x + k * G) before hop s + 1 of any. The wait for chunk c at hop s then finds
+// the predecessor's hop s - 1 of c long done (it was issued K - 1 chunks earlier), so flag
+// latency and the ranks' jitter hide behind data movement instead of adding up over the
+// 2 (P - 1) dependent hops of a chunk-major walk (round 3: 0.56 of the copy roofline at
+// 8 logical ranks x 256 MiB bf16). Chunks per workgroup: XgmiComm ring_depth_.
+template <class E, class WT>
 __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
   constexpr int es = 16 / E::ELEMS;
+  constexpr int ws = 16 / WT::ELEMS;  // wire bytes per element of a reduce-scatter partial
   const int P = a.P;
   const int y = blockIdx.y;
   const int r = a.rank0 + y;
@@ -432,60 +447,72 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
   const uint32_t epoch = launch_epoch(ctl);
   const uint64_t deadline = wall_ticks() + a.timeout;
   const int64_t slot = a.slot_bytes;
+  const int G = gridDim.x;
   uint32_t* err = &ctl[2];
   const bool rel = a.fence & 1, acq = a.fence & 2;
   __shared__ uint64_t ps_lds[kPhaseSlots];
   PhaseStamps ps(a, ps_lds);  // ring: [1] = end of the reduce-scatter hops, [2]/[4] = waits in RS / AG
   if (static_cast<int>(blockIdx.x) < a.nch) entry_guard(a, ctl, r, epoch, kHazS | kHazR, nxt, deadline, err);
-  for (int c = blockIdx.x; c < a.nch; c += gridDim.x) {
-    const int64_t cstart = static_cast<int64_t>(c) * a.chunk;
-    auto blen = [&](int b) { return clamp_len(clamp_len(a.n - static_cast<int64_t>(b) * a.block, a.block) - cstart, a.chunk); };
-    auto at = [&](int b) { return (static_cast<int64_t>(b) * a.block + cstart) * es; };
-    const int64_t pofs = cstart * 4;  // fp32 partial slots
-    // every S access of this chunk is fp32 [cstart, cstart + chunk), every R access E-typed
-    const bool inb = unit_in_bounds(a, pofs, clamp_len(a.block - cstart, a.chunk) * 4, (P - 2) * a.nch + c, err);
-    if (!inb) {  // publish every flag this workgroup owes, move no data
-      publish_flags([&](int) { return f1(a, nxt, r, c); }, 1, epoch, rel);
-      continue;
-    }
-    // RS step 0: raw own block r, widened to fp32
-    {
-      const int64_t len = blen(r);
-      if (len > 0) ring_hop<E>(nullptr, in + at(r), a.base[nxt] + a.off_S + pofs, nullptr, nullptr, len, 1.f);
-      publish_flags([&](int) { return f1(a, nxt, r, c); }, 1, epoch, rel);
-    }
-    // RS steps 1..P-1 (the last one completes block r+1)
-    for (int s = 1; s < P; ++s) {
-      const int b = (r - s + P) % P;
-      const int64_t len = blen(b);
+  auto cst = [&](int c) { return static_cast<int64_t>(c) * a.chunk; };
+  auto blen = [&](int b, int c) {
+    return clamp_len(clamp_len(a.n - static_cast<int64_t>(b) * a.block, a.block) - cst(c), a.chunk);
+  };
+  auto at = [&](int b, int c) { return (static_cast<int64_t>(b) * a.block + cst(c)) * es; };
+  // every S access of chunk c is WT-typed [cstart, cstart + chunk), every R access E-typed;
+  // the highest flag column is (P - 2) * nch + c. The geometry is the same on every rank,
+  // so a chunk out of bounds is skipped by all of them (no flag is owed).
+  auto inb = [&](int c) {
+    return unit_in_bounds(a, cst(c) * ws, clamp_len(a.block - cst(c), a.chunk) * ws, (P - 2) * a.nch + c, err);
+  };
+  // RS hop 0: the raw own block r
+  for (int c = blockIdx.x; c < a.nch; c += G) {
+    if (!inb(c)) continue;
+    const int64_t len = blen(r, c);
+    if (len > 0) ring_hop<E, WT>(nullptr, in + at(r, c), a.base[nxt] + a.off_S + cst(c) * ws, nullptr, nullptr, len, 1.f);
+    publish_flags([&](int) { return f1(a, nxt, r, c); }, 1, epoch, rel);
+  }
+  read_delay(a, r);  // slow-reader test knob: hold this rank before its first slab read
+  // RS hops 1..P-1 (the last one completes block r+1 and starts its all-gather)
+  for (int s = 1; s < P; ++s) {
+    const int b = (r - s + P) % P;
+    for (int c = blockIdx.x; c < a.nch; c += G) {
+      if (!inb(c)) continue;
+      const int64_t len = blen(b, c);
       const uint64_t tw = ps.now();
       wait_flags([&](int) -> const uint32_t* { return f1(a, r, prv, (s - 1) * a.nch + c); }, 1, epoch, deadline, err,
                  ERR_TIMEOUT_SCATTER, acq);
       ps.add(2, tw);
       ps.count(6);
-      const char* part = a.base[r] + a.off_S + (s - 1) * slot + pofs;
+      const char* part = a.base[r] + a.off_S + (s - 1) * slot + cst(c) * ws;
       if (s < P - 1) {
-        if (len > 0) ring_hop<E>(part, in + at(b), a.base[nxt] + a.off_S + s * slot + pofs, nullptr, nullptr, len, 1.f);
+        if (len > 0)
+          ring_hop<E, WT>(part, in + at(b, c), a.base[nxt] + a.off_S + s * slot + cst(c) * ws, nullptr, nullptr, len,
+                          1.f);
         publish_flags([&](int) { return f1(a, nxt, r, s * a.nch + c); }, 1, epoch, rel);
       } else {
         if (len > 0)
-          ring_hop<E>(part, in + at(b), nullptr, out + at(b), a.base[nxt] + a.off_R + cstart * es, len, a.scale);
+          ring_hop<E, WT>(part, in + at(b, c), nullptr, out + at(b, c), a.base[nxt] + a.off_R + cst(c) * es, len,
+                          a.scale);
         publish_flags([&](int) { return f2(a, nxt, r, c); }, 1, epoch, rel);
       }
     }
-    // AG steps: receive block (r - t), forward unless it is the last hop
-    ps.mark(1);
-    for (int t = 0; t < P - 1; ++t) {
-      const int b = (r - t + P) % P;
-      const int64_t len = blen(b);
+  }
+  ps.mark(1);
+  read_delay(a, r);  // and before its first all-gather read
+  // AG hops: receive block (r - t), forward unless it is the last hop
+  for (int t = 0; t < P - 1; ++t) {
+    const int b = (r - t + P) % P;
+    const bool fwd = t < P - 2;
+    for (int c = blockIdx.x; c < a.nch; c += G) {
+      if (!inb(c)) continue;
+      const int64_t len = blen(b, c);
       const uint64_t tw = ps.now();
       wait_flags([&](int) -> const uint32_t* { return f2(a, r, prv, t * a.nch + c); }, 1, epoch, deadline, err,
                  ERR_TIMEOUT_REDUCE, acq);
       ps.add(4, tw);
       ps.count(7);
-      const bool fwd = t < P - 2;
-      char* d = fwd ? a.base[nxt] + a.off_R + (t + 1) * slot + cstart * es : nullptr;
-      if (len > 0) copy_slab_fwd<E>(out + at(b), d, a.base[r] + a.off_R + t * slot + cstart * es, len);
+      char* d = fwd ? a.base[nxt] + a.off_R + (t + 1) * slot + cst(c) * es : nullptr;
+      if (len > 0) copy_slab_fwd<E>(out + at(b, c), d, a.base[r] + a.off_R + t * slot + cst(c) * es, len);
       if (fwd) publish_flags([&](int) { return f2(a, nxt, r, (t + 1) * a.nch + c); }, 1, epoch, rel);
     }
   }
@@ -608,6 +635,7 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
     throw std::invalid_argument("MXAR_FENCE without bit 1 (acquire) needs MXAR_STUDY=1: slab reads rely on it");
   if (const char* u = std::getenv("MXAR_TWOSHOT_UNITS")) units_per_wg_ = std::max(1, std::atoi(u));
   if (const char* u = std::getenv("MXAR_TWOSHOT_SUB")) sub_max_ = std::max(1, std::atoi(u));
+  if (const char* d = std::getenv("MXAR_RING_DEPTH")) ring_depth_ = std::max(1, std::atoi(d));
   if (const char* d = std::getenv("MXAR_TWOSHOT_DYNAMIC")) dynamic_ = std::atoi(d) != 0;
   if (const char* g = std::getenv("MXAR_SLOT_GUARD")) noguard_ = std::atoi(g) == 0;
   if (const char* g = std::getenv("MXAR_TWOSHOT_GEOM")) {
@@ -781,8 +809,12 @@ void XgmiComm::reset_local() {
 template <class E>
 static void launch_typed(const CommArgs& a, dim3 grid, hipStream_t s, Algo kind) {
   const dim3 b(kCommThreads);
-  if (kind == Algo::Ring) {
-    hipLaunchKernelGGL(ring_kernel<E>, grid, b, 0, s, a);
+  if (kind == Algo::Ring) {  // exact wire: fp32 partials
+    hipLaunchKernelGGL((ring_kernel<E, F32>), grid, b, 0, s, a);
+    return;
+  }
+  if (kind == Algo::RingNative) {  // element-type wire
+    hipLaunchKernelGGL((ring_kernel<E, E>), grid, b, 0, s, a);
     return;
   }
   const bool oneshot = kind == Algo::OneShot;
@@ -849,14 +881,15 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
     a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(n, a.chunk)));
     a.subchunk = a.chunk;
     gx = static_cast<int>(std::min<int64_t>(gmax, a.nch));
-  } else if (kind == Algo::Ring) {
-    // one chunk per workgroup, carried around the whole ring by that workgroup. Hop flags sit
-    // in the row of the WRITER (the previous rank), one column block per hop: every flag word
-    // has a single writer across all kernels, so epochs never go backwards (a ring's late
-    // forward of launch e-1 landing on a word another rank's all-gather set to e lost that
-    // flag - profiles/round3/README.md); (W - 1) * nch columns must fit the flag row.
+  } else if (kind == Algo::Ring || kind == Algo::RingNative) {
+    // ring_depth chunks per workgroup, walked step-major (ring_kernel). Hop flags sit in the
+    // row of the WRITER (the previous rank), one column block per hop: every flag word has a
+    // single writer across all kernels, so epochs never go backwards (a ring's late forward
+    // of launch e-1 landing on a word another rank's all-gather set to e lost that flag -
+    // profiles/round3/README.md); (W - 1) * nch columns must fit the flag row.
+    const int depth = std::max(1, c0.ring_depth_);
     a.block = round_up(ceil_div(n, W), elems);
-    a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, gmax), elems));
+    a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, int64_t{gmax} * depth), elems));
     a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
     const int64_t cols = std::max<int64_t>(1, c0.maxch_ / std::max(1, W - 1));
     if (a.nch > cols) {
@@ -922,8 +955,9 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   a.dynamic = c0.dynamic_ ? 1 : 0;
   a.stamps = c0.stamps_;
   if (a.stamps != nullptr && gx * ranks_here > c0.stamp_slots_) a.stamps = nullptr;  // buffer too small: off
+  const bool ring = kind == Algo::Ring || kind == Algo::RingNative;
   const int64_t block_bytes = a.block * (kind == Algo::Ring ? 4 : es);  // ring: fp32 partial slots
-  const int64_t flag_cols = kind == Algo::Ring ? static_cast<int64_t>(std::max(1, W - 1)) * a.nch
+  const int64_t flag_cols = ring ? static_cast<int64_t>(std::max(1, W - 1)) * a.nch
                                               : static_cast<int64_t>(a.nch) * a.sub;
   if (kind != Algo::LL && (flag_cols > c0.maxch_ || block_bytes > c0.slot_bytes_ + 16))
     throw std::logic_error("XgmiComm: segment geometry exceeds slab");
@@ -959,7 +993,7 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   for (XgmiComm* c : group) {
     ++c->stats_.launches;
     ++(kind == Algo::LL ? c->stats_.ll
-                        : oneshot ? c->stats_.oneshot : kind == Algo::Ring ? c->stats_.ring : c->stats_.twoshot);
+                        : oneshot ? c->stats_.oneshot : ring ? c->stats_.ring : c->stats_.twoshot);
   }
 }
 
@@ -997,6 +1031,7 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
     return std::make_pair(std::string(ll        ? "ll "
                                       : oneshot ? "oneshot "
                                       : kind == Algo::Ring ? "ring "
+                                      : kind == Algo::RingNative ? "ring_native "
                                                            : "twoshot ") +
                               std::to_string(n * es) + "B",
                           "{\"rank\":" + std::to_string(c0.rank_) + ",\"ranks_in_launch\":" +
@@ -1006,6 +1041,7 @@ void XgmiComm::run(const std::vector<XgmiComm*>& group, const std::vector<const 
   const int64_t seg = ll ? c0.ll_max_ / es
                       : oneshot ? c0.slot_bytes_ / es
                       : kind == Algo::Ring ? c0.world_ * (c0.slot_bytes_ / 4) : c0.world_ * (c0.slot_bytes_ / es);
+  // (RingNative: element-type partials, a block fills a slot like the two-shot's)
   std::vector<const char*> ip(group.size());
   std::vector<char*> op(group.size());
   for (int64_t off = 0; off < n; off += seg) {
@@ -1023,7 +1059,7 @@ Algo XgmiComm::resolve(int64_t n, DType dt, Algo algo, int ranks_in_launch) cons
   const int64_t bytes = n * static_cast<int64_t>(dtype_size(dt));
   if (algo == Algo::LL) return ll_max_ >= 16 ? Algo::LL : Algo::TwoShot;
   if (algo == Algo::OneShot) return bytes <= slot_bytes_ ? Algo::OneShot : Algo::TwoShot;
-  if (algo == Algo::Ring) return Algo::Ring;
+  if (algo == Algo::Ring || algo == Algo::RingNative) return algo;
   if (algo == Algo::TwoShot) return Algo::TwoShot;
   // Auto: low-latency one-shot, then one-shot, then two-shot, with size limits per rank count
   // set in the constructor from the bench's latency table (profiles/round3/README.md)

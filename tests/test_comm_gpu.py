@@ -26,8 +26,12 @@ def _ref(xs):
     return acc
 
 
-def _tol(dtype, P):
-    return 0.0 if dtype == torch.float32 else 1e-2 * P
+def _tol(dtype, P, algo=""):
+    if dtype == torch.float32:
+        return 0.0
+    if algo == "ring_native":  # one rounding per hop of partials |p| <= P: (P - 1) x half an ulp of P
+        return 1e-2 * P * P
+    return 1e-2 * P
 
 
 def _diag(y, ref, xs, rank):
@@ -43,7 +47,7 @@ def _diag(y, ref, xs, rank):
 
 @pytest.mark.parametrize("P", [1, 2, 3, 4])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("algo", ["twoshot", "oneshot", "ring", "ll"])
+@pytest.mark.parametrize("algo", ["twoshot", "oneshot", "ring", "ring_native", "ll"])
 @pytest.mark.parametrize("n", [1, 7, 1000, 65536 + 3, 1 << 20])
 def test_local_cluster_allreduce(P, dtype, algo, n):
     cl = LocalCluster(P, slot_bytes=4 << 20, grid=32, timeout_s=10.0)
@@ -53,7 +57,7 @@ def test_local_cluster_allreduce(P, dtype, algo, n):
     ref = _ref(xs)
     for k, y in enumerate(ys):
         err = (y.float() - ref).abs().max().item() if n else 0.0
-        if err > _tol(dtype, P) + (1e-6 if dtype == torch.float32 else 0):
+        if err > _tol(dtype, P, algo) + (1e-6 if dtype == torch.float32 else 0):
             pytest.fail(f"P={P} {dtype} {algo} n={n} rank {k}: err {err}: {_diag(y, ref, xs, k)}")
 
 
@@ -70,7 +74,7 @@ def test_local_cluster_inplace_and_repeated_epochs():
             assert torch.allclose(y, ref, atol=1e-5)
 
 
-@pytest.mark.parametrize("algo", ["twoshot", "ring", "ll"])
+@pytest.mark.parametrize("algo", ["twoshot", "ring", "ring_native", "ll"])
 def test_local_cluster_segments_larger_than_slab(algo):
     P = 2
     cl = LocalCluster(P, slot_bytes=64 << 10, grid=8, timeout_s=10.0)
