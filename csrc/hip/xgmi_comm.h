@@ -318,6 +318,7 @@ class XgmiComm {
   bool own_ctl_ = true;            // false: control words owned by the caller
   bool noguard_ = false;           // MXAR_SLOT_GUARD=0 (study / negative control only)
   bool dynamic_ = false;           // two-shot units from a counter (MXAR_TWOSHOT_DYNAMIC)
+  bool ring_hop_rows_ = false;     // negative control: the two-writer ring flag layout (MXAR_RING_FLAGS=hop)
   int geom_ = -1;                  // two-shot geometry: -1 by block size, 0 coarse, 1 fine, 2 flat (MXAR_TWOSHOT_GEOM)
   int64_t flat_min_ = int64_t{2} << 20;  // blocks of at least this many bytes use the flat geometry (MXAR_TWOSHOT_FLAT_MIN)
   bool launched_ = false;          // a launch has been enqueued (last_stream_ valid)

@@ -440,7 +440,6 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
   const int y = blockIdx.y;
   const int r = a.rank0 + y;
   const int nxt = (r + 1) % P;
-  const int prv = (r + P - 1) % P;
   const char* const in = a.in[y];
   char* const out = a.out[y];
   uint32_t* const ctl = a.ctl[y];
@@ -458,6 +457,16 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
     return clamp_len(clamp_len(a.n - static_cast<int64_t>(b) * a.block, a.block) - cst(c), a.chunk);
   };
   auto at = [&](int b, int c) { return (static_cast<int64_t>(b) * a.block + cst(c)) * es; };
+  // hop flags: rank k's word for hop h of chunk c, in the row of its only writer (k's
+  // predecessor), one column block per hop. ring_hop_rows = the two-writer layout of round 3
+  // (row = hop), a negative control only.
+  const bool hop_rows = a.ring_hop_rows != 0;
+  auto rs_flag = [&](int k, int h, int c) {
+    return hop_rows ? f1(a, k, h, c) : f1(a, k, (k + P - 1) % P, h * a.nch + c);
+  };
+  auto ag_flag = [&](int k, int h, int c) {
+    return hop_rows ? f2(a, k, h, c) : f2(a, k, (k + P - 1) % P, h * a.nch + c);
+  };
   // every S access of chunk c is WT-typed [cstart, cstart + chunk), every R access E-typed;
   // the highest flag column is (P - 2) * nch + c. The geometry is the same on every rank,
   // so a chunk out of bounds is skipped by all of them (no flag is owed).
@@ -469,7 +478,7 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
     if (!inb(c)) continue;
     const int64_t len = blen(r, c);
     if (len > 0) ring_hop<E, WT>(nullptr, in + at(r, c), a.base[nxt] + a.off_S + cst(c) * ws, nullptr, nullptr, len, 1.f);
-    publish_flags([&](int) { return f1(a, nxt, r, c); }, 1, epoch, rel);
+    publish_flags([&](int) { return rs_flag(nxt, 0, c); }, 1, epoch, rel);
   }
   read_delay(a, r);  // slow-reader test knob: hold this rank before its first slab read
   // RS hops 1..P-1 (the last one completes block r+1 and starts its all-gather)
@@ -479,7 +488,7 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
       if (!inb(c)) continue;
       const int64_t len = blen(b, c);
       const uint64_t tw = ps.now();
-      wait_flags([&](int) -> const uint32_t* { return f1(a, r, prv, (s - 1) * a.nch + c); }, 1, epoch, deadline, err,
+      wait_flags([&](int) -> const uint32_t* { return rs_flag(r, s - 1, c); }, 1, epoch, deadline, err,
                  ERR_TIMEOUT_SCATTER, acq);
       ps.add(2, tw);
       ps.count(6);
@@ -488,12 +497,12 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
         if (len > 0)
           ring_hop<E, WT>(part, in + at(b, c), a.base[nxt] + a.off_S + s * slot + cst(c) * ws, nullptr, nullptr, len,
                           1.f);
-        publish_flags([&](int) { return f1(a, nxt, r, s * a.nch + c); }, 1, epoch, rel);
+        publish_flags([&](int) { return rs_flag(nxt, s, c); }, 1, epoch, rel);
       } else {
         if (len > 0)
           ring_hop<E, WT>(part, in + at(b, c), nullptr, out + at(b, c), a.base[nxt] + a.off_R + cst(c) * es, len,
                           a.scale);
-        publish_flags([&](int) { return f2(a, nxt, r, c); }, 1, epoch, rel);
+        publish_flags([&](int) { return ag_flag(nxt, 0, c); }, 1, epoch, rel);
       }
     }
   }
@@ -507,13 +516,13 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
       if (!inb(c)) continue;
       const int64_t len = blen(b, c);
       const uint64_t tw = ps.now();
-      wait_flags([&](int) -> const uint32_t* { return f2(a, r, prv, t * a.nch + c); }, 1, epoch, deadline, err,
+      wait_flags([&](int) -> const uint32_t* { return ag_flag(r, t, c); }, 1, epoch, deadline, err,
                  ERR_TIMEOUT_REDUCE, acq);
       ps.add(4, tw);
       ps.count(7);
       char* d = fwd ? a.base[nxt] + a.off_R + (t + 1) * slot + cst(c) * es : nullptr;
       if (len > 0) copy_slab_fwd<E>(out + at(b, c), d, a.base[r] + a.off_R + t * slot + cst(c) * es, len);
-      if (fwd) publish_flags([&](int) { return f2(a, nxt, r, (t + 1) * a.nch + c); }, 1, epoch, rel);
+      if (fwd) publish_flags([&](int) { return ag_flag(nxt, t + 1, c); }, 1, epoch, rel);
     }
   }
   ps.mark(3);
@@ -637,6 +646,13 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   if (const char* u = std::getenv("MXAR_TWOSHOT_SUB")) sub_max_ = std::max(1, std::atoi(u));
   if (const char* d = std::getenv("MXAR_RING_DEPTH")) ring_depth_ = std::max(1, std::atoi(d));
   if (const char* d = std::getenv("MXAR_TWOSHOT_DYNAMIC")) dynamic_ = std::atoi(d) != 0;
+  if (const char* f = std::getenv("MXAR_RING_FLAGS")) {
+    // the round-3 layout whose flag words had two writers (ring hop rows vs other kernels'
+    // writer rows): kept only as the negative control of tests/test_comm_gpu.py
+    ring_hop_rows_ = std::string(f) == "hop";
+    if (ring_hop_rows_ && !std::getenv("MXAR_STUDY"))
+      throw std::invalid_argument("MXAR_RING_FLAGS=hop is a known-broken layout: set MXAR_STUDY=1 to use it");
+  }
   if (const char* g = std::getenv("MXAR_SLOT_GUARD")) noguard_ = std::atoi(g) == 0;
   if (const char* g = std::getenv("MXAR_TWOSHOT_GEOM")) {
     const std::string v = g;
@@ -953,6 +969,7 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   a.rdelay = c0.rdelay_us_ > 0 ? static_cast<uint64_t>(c0.rdelay_us_ * 100.0) : 0;  // 100 MHz ticks
   a.noguard = c0.noguard_ ? 1 : 0;
   a.dynamic = c0.dynamic_ ? 1 : 0;
+  a.ring_hop_rows = c0.ring_hop_rows_ ? 1 : 0;
   a.stamps = c0.stamps_;
   if (a.stamps != nullptr && gx * ranks_here > c0.stamp_slots_) a.stamps = nullptr;  // buffer too small: off
   const bool ring = kind == Algo::Ring || kind == Algo::RingNative;

@@ -139,12 +139,24 @@ def test_multiprocess_ipc_allreduce(world):
     assert not bad, bad
 
 
-def _slot_reuse_worker(rank, world, port, results):
-    """Rank 1 idles 2 ms before every slab-reading phase; rank 0, which needs nothing more
-    from it once its pushes are in, runs ahead into the next launch and would push into the
-    slots rank 1 is about to read (one-shot S -> one-shot, two-shot R -> all-gather, all-to-all
-    S -> all-to-all) without the entry guard (xgmi_device.h)."""
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+_SLOW_READER_SEQ = {
+    # one-shot S -> one-shot, two-shot R -> all-gather, all-to-all S -> all-to-all
+    "mixed": ["oneshot", "oneshot", "twoshot", "all_gather", "all_to_all", "all_to_all", "oneshot", "twoshot",
+              "all_gather", "all_gather", "reduce_scatter", "oneshot"],
+    # the ring's hop flags next to the other kernels' writer-row flags (round-3 collision)
+    "ring": ["ring", "all_gather", "ring", "twoshot", "ring_native", "all_gather", "ring", "ring", "all_gather",
+             "oneshot", "ring", "reduce_scatter", "ring_native", "twoshot"],
+}
+
+
+def _slot_reuse_worker(rank, world, port, results, slow=1, seq="mixed", env=None):
+    """Rank `slow` idles 2 ms before every slab-reading phase; a rank that needs nothing more
+    from it once its pushes are in runs ahead into the next launch and would push into the
+    slots the slow rank is about to read without the entry guard (xgmi_device.h). In a ring of
+    >= 3 ranks the slow rank's late forwards also land after a peer's next launch has begun:
+    with the round-3 flag layout (row = hop) such a late ring flag overwrote a newer
+    all-gather flag of another writer (profiles/round3/soak8_run4_ring_flag_collision.log)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0", **(env or {}))
     import torch.distributed as dist
 
     from akka_allreduce_1_amd.parallel import XgmiCommunicator
@@ -153,12 +165,10 @@ def _slot_reuse_worker(rank, world, port, results):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ok, msg = True, ""
     try:
-        comm = XgmiCommunicator(device=0, slot_bytes=1 << 20, grid=8, timeout_s=15.0)
-        comm.native.set_read_delay(1, 2000.0)
-        n = 8192
-        seq = ["oneshot", "oneshot", "twoshot", "all_gather", "all_to_all", "all_to_all", "oneshot", "twoshot",
-               "all_gather", "all_gather", "reduce_scatter", "oneshot"]
-        for it, op in enumerate(seq * 2):
+        comm = XgmiCommunicator(device=0, slot_bytes=1 << 20, grid=8, timeout_s=5.0)
+        comm.native.set_read_delay(slow, 2000.0)
+        n = 8192 * world
+        for it, op in enumerate(_SLOW_READER_SEQ[seq] * 2):
             xs = [fill_uniform(torch.empty(n, device=DEV), seed=1000 * it + k) for k in range(world)]
             m = n // world
             if op == "all_gather":
@@ -183,21 +193,26 @@ def _slot_reuse_worker(rank, world, port, results):
     dist.destroy_process_group()
 
 
-def test_multiprocess_slot_reuse_slow_reader():
+def _run_slow_reader(world, slow, seq, env=None):
     from akka_allreduce_1_amd.parallel import free_port
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_slot_reuse_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_slot_reuse_worker, args=(r, world, port, q, slow, seq, env)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=240) for _ in range(2)]
+    res = [q.get(timeout=240) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         if p.is_alive():
             p.kill()
-    bad = [r for r in res if not r[1]]
+    return [r for r in res if not r[1]]
+
+
+@pytest.mark.parametrize("world,slow,seq", [(2, 1, "mixed"), (3, 2, "ring"), (4, 3, "ring"), (3, 1, "mixed")])
+def test_multiprocess_slot_reuse_slow_reader(world, slow, seq):
+    bad = _run_slow_reader(world, slow, seq)
     assert not bad, bad
 
 
