@@ -351,7 +351,7 @@ def native_deployment(cases=((10, 2, 400), (262144, 1024, 400), (16777216, 32768
     PROCESSES sharing GPU 0, arenas IPC-mapped, control over TCP (mxar / mxar-gpu). Per size:
     a 3-round run printing every worker's output sum and head, checked against the exact f32
     sum 2 * float(i); then the timed run (mean round interval from the master's barrier
-    stamps). (n, maxChunkSize) = (10, 2) is the reference's default job (AllreduceMaster.scala:
+    stamps), whose own last round each worker checks the same way (`validated_timed`). (n, maxChunkSize) = (10, 2) is the reference's default job (AllreduceMaster.scala:
     111-114)."""
     import re
 
@@ -375,7 +375,14 @@ def native_deployment(cases=((10, 2, 400), (262144, 1024, 400), (16777216, 32768
             if not row["validated"]:
                 row["check"] = {"expected_sum": exp, "seen": sums[:6]}
             else:
-                st, _ = _native_job(n, chunk, rounds, quiet=True, timeout=min(30.0, max(5.0, t_end - time.monotonic())))
+                st, tl = _native_job(n, chunk, rounds, quiet=True, timeout=min(30.0, max(5.0, t_end - time.monotonic())))
+                # the timed run itself: each worker keeps its newest output and checks its sum at exit
+                last = [(int(m.group(1)), float(m.group(2))) for ln in tl
+                        if (m := re.search(r"last round (\d+) sum (\S+)", ln))]
+                row["validated_timed"] = len(last) == 2 and all(r == rounds - 1 and x == exp for r, x in last)
+                row["validated"] = row["validated"] and row["validated_timed"]
+                if not row["validated_timed"]:
+                    row["check_timed"] = {"expected": [rounds - 1, exp], "seen": last}
                 if st:
                     row["us_per_round"] = round(1e6 / st["steady_rounds_per_s"], 1)
                     row["round_interval_p50_us"] = st["round_interval_p50_us"]

@@ -31,7 +31,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <numeric>
+#include <optional>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -247,8 +249,16 @@ void set_level(const std::string& l) {
   };
   std::atomic<int> rounds{0};
   const bool quiet = o.quiet;
-  DataSink sink = [&rounds, quiet](const AllReduceOutput& out) {  // AllreduceWorker.scala:295-297
+  // quiet: the newest output is kept (a reference, no copy) and checked once at the end, so a
+  // timed run reports the sum of its own last round (benchmarks/sections.py native_deployment)
+  std::mutex last_mu;
+  std::optional<AllReduceOutput> last;
+  DataSink sink = [&rounds, quiet, &last_mu, &last](const AllReduceOutput& out) {  // AllreduceWorker.scala:295-297
     rounds++;
+    if (quiet) {
+      std::lock_guard<std::mutex> g(last_mu);
+      if (!last || out.iteration >= last->iteration) last = out;
+    }
     if (!quiet) {  // quiet: no copy back of a device output either
       const std::vector<float> d = out.data->to_host();
       const double sum = std::accumulate(d.begin(), d.end(), 0.0);
@@ -289,6 +299,15 @@ void set_level(const std::string& l) {
     std::this_thread::sleep_for(std::chrono::milliseconds(20));
   }
   if (gpu_at_exit) gpu_at_exit();
+  {
+    std::lock_guard<std::mutex> g(last_mu);
+    if (last) {
+      const std::vector<float> d = last->data->to_host();
+      const double sum = std::accumulate(d.begin(), d.end(), 0.0);
+      std::printf("[mxar worker] last round %d sum %.1f\n", last->iteration, sum);
+      last.reset();
+    }
+  }
   std::printf("[mxar worker] %d rounds completed\n", rounds.load());
   std::fflush(stdout);
   node->leave();
