@@ -211,7 +211,7 @@ __device__ __forceinline__ void st16(void* p, const Pack16& v) { *static_cast<Pa
 // 1, on by default) is what makes the peers' xGMI stores visible, not the load flavour. As a
 // streaming hint it also keeps one-pass streams from displacing each other in L2: a copy of
 // 256 MiB with nt loads + write-through stores runs 6.77 TB/s vs 5.18 with sc1 or plain loads
-// (tools/store_probe.hip, profiles/round3/store_probe.json), into fine-grained and coarse
+// (a one-off store probe, removed in round 4 - git history - profiles/round3/store_probe.json), into fine-grained and coarse
 // memory alike. Every slab read AND every read of a kernel's own input stream uses it.
 // Descriptor built from wave-uniform values only (cdna_hip_programming.md T8/T20).
 // ---------------------------------------------------------------------------------

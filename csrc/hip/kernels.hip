@@ -37,7 +37,7 @@ static int grid_for(int64_t packs) {
 // before the first add (P*U*16 bytes in flight per lane); the sum still runs in peer
 // order 0..P-1. NT bit 0 = nontemporal loads, bit 1 = nontemporal stores (streaming data,
 // no reuse), bit 2 = write-through (sc0 sc1) stores - the store probe's fastest copy pairs nt
-// loads with them (tools/store_probe.hip).
+// loads with them (round-3 store probe, profiles/round3/store_probe.json).
 // out may alias one slot row (in-place reduce): every element is read and written by the
 // same lane, loads before the store.
 template <class E, int U, int P, int NT>
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(kThreads) void copy_tiles_kernel(const char* __rest
   if (t < bytes) out[t] = in[t];
 }
 
-// Unit variant (round 3, tools/store_probe.hip): every workgroup copies contiguous units of
+// Unit variant (round 3 store probe, profiles/round3/store_probe.json): every workgroup copies contiguous units of
 // 512 KiB with nt buffer loads (aux 2: the input stream is read once) and sc0 sc1
 // write-through buffer stores (aux 17) - 6.77 TB/s in the store probe against 5.2-5.6 for the
 // plain / nt-store flavours. U packs of 16 B per lane in flight.

@@ -34,7 +34,9 @@ def main() -> None:
     ap.add_argument("--ranks", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--sizes", nargs="+", default=["64K", "1M", "16M", "64M", "256M"])
     ap.add_argument("--algos", nargs="+", default=["twoshot", "oneshot"])
-    ap.add_argument("--fence", type=int, nargs="+", default=[2])
+    ap.add_argument("--fence", type=int, nargs="+", default=[3])
+    ap.add_argument("--ring-depth", type=int, nargs="+", default=[0],
+                    help="ring chunks per workgroup to sweep (0 = the communicator's default)")
     ap.add_argument("--grid", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--dtype", default="bf16")
@@ -74,9 +76,12 @@ def main() -> None:
             for algo in args.algos:
                 if (algo == "oneshot" and S > slot) or (algo == "ll" and S > cl.comms[0].ll_max_bytes):
                     continue
-                for fence in args.fence:
+                variants = [(f, d) for f in args.fence for d in (args.ring_depth if algo.startswith("ring") else [0])]
+                for fence, depth in variants:
                     for c in cl.comms:
                         c.fence = fence
+                        if depth:
+                            c.ring_depth = depth
                     if algo in ("all_to_all", "reduce_scatter", "all_gather"):
                         ins = [t[:n // P].contiguous() for t in xs] if algo == "all_gather" else xs
                         outs = [torch.empty(n // P if algo == "reduce_scatter" else n, dtype=dtype, device=dev)
@@ -109,13 +114,13 @@ def main() -> None:
                     ts = [a.elapsed_time(b) for a, b in ev]
                     p50 = percentile(ts, 50)
                     row = {"P": P, "bytes": S, "algo": algo, "fence": fence, "p50_us": round(p50 * 1e3, 1),
-                           "min_us": round(min(ts) * 1e3, 1), "hbm_TBps": round(hbm_bytes(S, P, algo) / p50 / 1e9, 2),
-                           "max_err": err}
+                           "min_us": round(min(ts) * 1e3, 1),
+                           "hbm_TBps": round(hbm_bytes(S, P, algo, es) / p50 / 1e9, 2), "max_err": err}
+                    if depth:
+                        row["ring_depth"] = depth
                     rows.append(row)
                     print(json.dumps(row), flush=True)
             del xs, ys, ref
-        for c in cl.comms:
-            c.fence = 2
         del cl
         torch.cuda.empty_cache()
     if args.out:
