@@ -260,7 +260,8 @@ def local_ranks(dev, args, P: int = 8) -> dict:
         row["copy_roofline_TBps"] = round(copy_tbps, 3)
         del a, b
         a = b = None
-        cl = LocalCluster(P, slot_bytes=-(-S // P) + (1 << 20), grid=512, timeout_s=10.0)
+        # slots of 2 blocks: the exact-wire ring's fp32 partials of a bf16 block fit one launch
+        cl = LocalCluster(P, slot_bytes=2 * -(-S // P) + (1 << 20), grid=512, timeout_s=10.0)
         xs = [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=500 + k) for k in range(P)]
         ys = [torch.empty_like(t) for t in xs]
         ref = torch.zeros(n, device=dev)

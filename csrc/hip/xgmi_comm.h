@@ -308,7 +308,8 @@ class XgmiComm {
   int64_t stamp_slots_ = 0;
   int units_per_wg_ = 0;  // two-shot scatter units per workgroup; 0 = by block size (launch_segment)
   int sub_max_ = 0;       // two-shot: most reduce pieces per chunk; 0 = by block size
-  int ring_depth_ = 4;    // ring: chunks per workgroup, walked step-major (MXAR_RING_DEPTH)
+  int ring_depth_ = 1;    // ring: chunks per workgroup, walked step-major (MXAR_RING_DEPTH)
+  int ring_grid_ = 256;   // ring: workgroups per launch on this device, all ranks of it (MXAR_RING_GRID)
   char* slab_ = nullptr;            // own fine-grained slab (flags | S | R | LL)
   uint32_t* ctl_ = nullptr;         // [0] epoch, [1] ticket, [2] sticky error (device memory)
   char* peers_[kMaxRanks] = {};     // slab base of every rank (own included)

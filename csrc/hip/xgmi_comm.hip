@@ -645,6 +645,7 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   if (const char* u = std::getenv("MXAR_TWOSHOT_UNITS")) units_per_wg_ = std::max(1, std::atoi(u));
   if (const char* u = std::getenv("MXAR_TWOSHOT_SUB")) sub_max_ = std::max(1, std::atoi(u));
   if (const char* d = std::getenv("MXAR_RING_DEPTH")) ring_depth_ = std::max(1, std::atoi(d));
+  if (const char* g = std::getenv("MXAR_RING_GRID")) ring_grid_ = std::max(1, std::atoi(g));
   if (const char* d = std::getenv("MXAR_TWOSHOT_DYNAMIC")) dynamic_ = std::atoi(d) != 0;
   if (const char* f = std::getenv("MXAR_RING_FLAGS")) {
     // the round-3 layout whose flag words had two writers (ring hop rows vs other kernels'
@@ -903,9 +904,15 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
     // single writer across all kernels, so epochs never go backwards (a ring's late forward
     // of launch e-1 landing on a word another rank's all-gather set to e lost that flag -
     // profiles/round3/README.md); (W - 1) * nch columns must fit the flag row.
+    // Every hop of every workgroup pays a system-scope release and acquire, and those
+    // serialise in the XCD's L2 when hundreds of workgroups fence at once: at 8 logical ranks
+    // x 256 MiB the ring ran fastest with 256 workgroups in all (one per CU) and one chunk
+    // per workgroup - more chunks per workgroup only multiply the fences (ring_grid sweep,
+    // profiles/round4/README.md). MXAR_RING_GRID / MXAR_RING_DEPTH override.
     const int depth = std::max(1, c0.ring_depth_);
+    const int gring = std::max(1, std::min(gmax, c0.ring_grid_ / ranks_here));
     a.block = round_up(ceil_div(n, W), elems);
-    a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, int64_t{gmax} * depth), elems));
+    a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, int64_t{gring} * depth), elems));
     a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
     const int64_t cols = std::max<int64_t>(1, c0.maxch_ / std::max(1, W - 1));
     if (a.nch > cols) {
@@ -913,7 +920,7 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
       a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
     }
     a.subchunk = a.chunk;
-    gx = static_cast<int>(std::min<int64_t>(gmax, a.nch));
+    gx = static_cast<int>(std::min<int64_t>(gring, a.nch));
   } else {
     // ~one scatter unit and one gather unit per workgroup: every unit pays one fence, so
     // units are as large as the parallelism allows. The reduce phase splits each chunk
