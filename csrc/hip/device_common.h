@@ -164,6 +164,46 @@ struct Acc<F16> {
   }
 };
 
+// fp32 accumulation of one 8-byte unit (low-latency kernels: xgmi_ll.hip, threshold LL rounds) (2 fp32 or 4 bf16/fp16 elements)
+template <class E>
+struct Acc8;
+template <>
+struct Acc8<F32> {
+  float v[2] = {0.f, 0.f};
+  __device__ __forceinline__ void add(uint2 d) {
+    v[0] += __uint_as_float(d.x);
+    v[1] += __uint_as_float(d.y);
+  }
+  __device__ __forceinline__ uint2 pack(float s) const { return make_uint2(__float_as_uint(v[0] * s), __float_as_uint(v[1] * s)); }
+};
+template <>
+struct Acc8<BF16> {
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  __device__ __forceinline__ void add(uint2 d) {
+    v[0] += bf16_to_f32(d.x & 0xFFFFu);
+    v[1] += bf16_to_f32(d.x >> 16);
+    v[2] += bf16_to_f32(d.y & 0xFFFFu);
+    v[3] += bf16_to_f32(d.y >> 16);
+  }
+  __device__ __forceinline__ uint2 pack(float s) const {
+    return make_uint2(pack_bf16x2(v[0] * s, v[1] * s), pack_bf16x2(v[2] * s, v[3] * s));
+  }
+};
+template <>
+struct Acc8<F16> {
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  __device__ __forceinline__ void add(uint2 d) {
+    v[0] += f16_to_f32(d.x & 0xFFFFu);
+    v[1] += f16_to_f32(d.x >> 16);
+    v[2] += f16_to_f32(d.y & 0xFFFFu);
+    v[3] += f16_to_f32(d.y >> 16);
+  }
+  __device__ __forceinline__ uint2 pack(float s) const {
+    return make_uint2(pack_f16x2(v[0] * s, v[1] * s), pack_f16x2(v[2] * s, v[3] * s));
+  }
+};
+
+
 // Scalar element access for ragged tails (< one pack).
 template <typename E>
 struct Scalar;

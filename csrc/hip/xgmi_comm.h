@@ -251,6 +251,8 @@ class XgmiComm {
   int units_per_wg() const { return units_per_wg_; }
   void set_units_per_wg(int u) { units_per_wg_ = u > 0 ? u : 0; }
   int ring_depth() const { return ring_depth_; }
+  int64_t threshold_ll_max() const { return thr_ll_max_; }
+  void set_threshold_ll_max(int64_t b) { thr_ll_max_ = b > 0 ? b : 0; }
   void set_ring_depth(int d) { ring_depth_ = d > 0 ? d : 1; }
   void set_fence(int f) { fence_ = f & 3; }
   // Study knob: per-workgroup phase stamps of the two-shot / ring kernels (xgmi_device.h
@@ -309,7 +311,8 @@ class XgmiComm {
   int units_per_wg_ = 0;  // two-shot scatter units per workgroup; 0 = by block size (launch_segment)
   int sub_max_ = 0;       // two-shot: most reduce pieces per chunk; 0 = by block size
   int ring_depth_ = 1;    // ring: chunks per workgroup, walked step-major (MXAR_RING_DEPTH)
-  int ring_grid_ = 256;   // ring: workgroups per launch on this device, all ranks of it (MXAR_RING_GRID)
+  int ring_grid_ = 256;
+  int64_t thr_ll_max_ = 64 * 1024;  // threshold rounds up to this many bytes per rank run low-latency (MXAR_THRESHOLD_LL_MAX)   // ring: workgroups per launch on this device, all ranks of it (MXAR_RING_GRID)
   char* slab_ = nullptr;            // own fine-grained slab (flags | S | R | LL)
   uint32_t* ctl_ = nullptr;         // [0] epoch, [1] ticket, [2] sticky error (device memory)
   char* peers_[kMaxRanks] = {};     // slab base of every rank (own included)

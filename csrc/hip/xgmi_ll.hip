@@ -48,45 +48,6 @@ __device__ __forceinline__ void store_unit(char* p, int64_t i, int64_t nbytes, u
   for (int k = 0; k < 4 && off + 2 * k < nbytes; ++k) h[k] = static_cast<uint16_t>(w[k >> 1] >> (16 * (k & 1)));
 }
 
-// fp32 accumulation of one 8-byte unit (2 fp32 or 4 bf16/fp16 elements)
-template <class E>
-struct Acc8;
-template <>
-struct Acc8<F32> {
-  float v[2] = {0.f, 0.f};
-  __device__ __forceinline__ void add(uint2 d) {
-    v[0] += __uint_as_float(d.x);
-    v[1] += __uint_as_float(d.y);
-  }
-  __device__ __forceinline__ uint2 pack(float s) const { return make_uint2(__float_as_uint(v[0] * s), __float_as_uint(v[1] * s)); }
-};
-template <>
-struct Acc8<BF16> {
-  float v[4] = {0.f, 0.f, 0.f, 0.f};
-  __device__ __forceinline__ void add(uint2 d) {
-    v[0] += bf16_to_f32(d.x & 0xFFFFu);
-    v[1] += bf16_to_f32(d.x >> 16);
-    v[2] += bf16_to_f32(d.y & 0xFFFFu);
-    v[3] += bf16_to_f32(d.y >> 16);
-  }
-  __device__ __forceinline__ uint2 pack(float s) const {
-    return make_uint2(pack_bf16x2(v[0] * s, v[1] * s), pack_bf16x2(v[2] * s, v[3] * s));
-  }
-};
-template <>
-struct Acc8<F16> {
-  float v[4] = {0.f, 0.f, 0.f, 0.f};
-  __device__ __forceinline__ void add(uint2 d) {
-    v[0] += f16_to_f32(d.x & 0xFFFFu);
-    v[1] += f16_to_f32(d.x >> 16);
-    v[2] += f16_to_f32(d.y & 0xFFFFu);
-    v[3] += f16_to_f32(d.y >> 16);
-  }
-  __device__ __forceinline__ uint2 pack(float s) const {
-    return make_uint2(pack_f16x2(v[0] * s, v[1] * s), pack_f16x2(v[2] * s, v[3] * s));
-  }
-};
-
 }  // namespace
 
 template <class E>
