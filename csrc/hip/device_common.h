@@ -375,6 +375,9 @@ __device__ __forceinline__ bool wait_flags(FlagAddr addr, int nflags, uint32_t e
   __shared__ int ok_s;
   if (threadIdx.x < 64) {
     const uint32_t* f = threadIdx.x < static_cast<unsigned>(nflags) ? addr(static_cast<int>(threadIdx.x)) : nullptr;
+    // nothing to wait for (a 1-rank launch, the own contribution only): no acquire either -
+    // its L2 invalidate would order nothing (and can write back other workgroups' dirty lines)
+    if (!__any(f != nullptr)) acquire = false;
     bool ok = (f == nullptr) || reached(ld_flag(f), epoch);
     while (!__all(ok)) {
       __builtin_amdgcn_s_sleep(1);

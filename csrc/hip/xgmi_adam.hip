@@ -46,18 +46,24 @@ __device__ __forceinline__ float adamw(float g, float* p, float* m, float* v, co
 // addresses, and the streaming form is 1.56x slower (1.00 vs 0.64 ms for the 134 M-parameter
 // step, same box: profiles/round3/adamw_stream_ab.jsonl); the gradients (read once, summed)
 // come in with nt loads either way.
-template <bool STREAM>
+// MODE 0 (default): plain state loads and stores. MODE 1 (MXAR_ADAM_STREAM=1): nt loads +
+// write-through stores (the store probe's fastest copy form, profiles/round3/store_probe.json)
+// - the state is read and written back at the same addresses, and that form was 1.56x slower
+// (1.00 vs 0.64 ms for the 134 M-parameter step, same box: profiles/round3/README.md).
+// MODE 2 (MXAR_ADAM_STREAM=2): nt loads, plain stores. The gradients (read once, summed) come
+// in with nt loads in every mode.
+template <int MODE>
 __device__ __forceinline__ float4 ld_state(const float* p, __amdgpu_buffer_rsrc_t r, int64_t i) {
-  if constexpr (STREAM) {
+  if constexpr (MODE != 0) {
     const Pack16 v = ld16_nt(r, static_cast<uint32_t>(i * 4));
     return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
   } else {
     return *reinterpret_cast<const float4*>(p + i);
   }
 }
-template <bool STREAM>
+template <int MODE>
 __device__ __forceinline__ void st_state(float* p, __amdgpu_buffer_rsrc_t r, int64_t i, const float4& x) {
-  if constexpr (STREAM) {
+  if constexpr (MODE == 1) {
     Pack16 v;
     v[0] = __float_as_uint(x.x);
     v[1] = __float_as_uint(x.y);
@@ -69,7 +75,7 @@ __device__ __forceinline__ void st_state(float* p, __amdgpu_buffer_rsrc_t r, int
   }
 }
 
-template <class E, int PT, bool STREAM>
+template <class E, int PT, int STREAM, int U>
 __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a) {
   constexpr int es = 16 / E::ELEMS;
   constexpr int EL = E::ELEMS;
@@ -128,7 +134,6 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a)
       const int64_t npk = len / EL;
       // U packs per lane per iteration, every load issued before the first use: the
       // persistent grid has only 2 workgroups per CU, so bytes in flight come from ILP
-      constexpr int U = 2;
       for (int64_t i0 = threadIdx.x; i0 < npk; i0 += U * kCommThreads) {
         Acc<E> acc[U];
         float4 p4[U][EL / 4], m4[U][EL / 4], v4[U][EL / 4];
@@ -170,7 +175,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a)
             st_state<STREAM>(sv, rv, i * EL + 4 * e, v4[w][e]);
           }
           const Pack16 o = acc[w].pack();
-          if constexpr (STREAM)
+          if constexpr (STREAM == 1)
             st16_wt(slab_rsrc(own_out), static_cast<uint32_t>(i * 16), o);
           else
             st16(own_out + i * 16, o);
@@ -206,7 +211,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a)
   finish_launch_done(a, ctl, epoch, r, kHazR);  // peers may still gather from R
 }
 
-template <bool STREAM>
+template <int STREAM, int U>
 static void launch_adamw_t(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {
   dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
     using E = decltype(tag);
@@ -214,24 +219,35 @@ static void launch_adamw_t(const CommArgs& a, dim3 grid, hipStream_t s, DType dt
     // load before the first add (the PT = 0 loop waits on each load in turn) - P = 1 is the
     // single-GPU optimizer step
     switch (a.P) {
-      case 1: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 1, STREAM>), grid, dim3(kCommThreads), 0, s, a); break;
-      case 2: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 2, STREAM>), grid, dim3(kCommThreads), 0, s, a); break;
-      case 4: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 4, STREAM>), grid, dim3(kCommThreads), 0, s, a); break;
-      case 8: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 8, STREAM>), grid, dim3(kCommThreads), 0, s, a); break;
-      default: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 0, STREAM>), grid, dim3(kCommThreads), 0, s, a); break;
+      case 1: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 1, STREAM, U>), grid, dim3(kCommThreads), 0, s, a); break;
+      case 2: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 2, STREAM, U>), grid, dim3(kCommThreads), 0, s, a); break;
+      case 4: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 4, STREAM, U>), grid, dim3(kCommThreads), 0, s, a); break;
+      case 8: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 8, STREAM, U>), grid, dim3(kCommThreads), 0, s, a); break;
+      default: hipLaunchKernelGGL((twoshot_adamw_kernel<E, 0, STREAM, U>), grid, dim3(kCommThreads), 0, s, a); break;
     }
   });
 }
 
 void launch_adamw(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {
-  static const bool stream = [] {
+  // study knobs: MXAR_ADAM_STREAM (state access form, above), MXAR_ADAM_U (packs per lane)
+  static const int mode = [] {
     const char* e = std::getenv("MXAR_ADAM_STREAM");
-    return e != nullptr && std::atoi(e) != 0;
+    return e != nullptr ? std::atoi(e) : 0;
   }();
-  if (stream)
-    launch_adamw_t<true>(a, grid, s, dt);
+  static const int u = [] {
+    const char* e = std::getenv("MXAR_ADAM_U");
+    return e != nullptr ? std::atoi(e) : 2;
+  }();
+  if (mode == 1)
+    launch_adamw_t<1, 2>(a, grid, s, dt);
+  else if (mode == 2)
+    launch_adamw_t<2, 2>(a, grid, s, dt);
+  else if (u == 1)
+    launch_adamw_t<0, 1>(a, grid, s, dt);
+  else if (u == 4)
+    launch_adamw_t<0, 4>(a, grid, s, dt);
   else
-    launch_adamw_t<false>(a, grid, s, dt);
+    launch_adamw_t<0, 2>(a, grid, s, dt);
 }
 
 }  // namespace mxar

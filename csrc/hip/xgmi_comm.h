@@ -312,7 +312,11 @@ class XgmiComm {
   int sub_max_ = 0;       // two-shot: most reduce pieces per chunk; 0 = by block size
   int ring_depth_ = 1;    // ring: chunks per workgroup, walked step-major (MXAR_RING_DEPTH)
   int ring_grid_ = 256;
-  int64_t thr_ll_max_ = 64 * 1024;  // threshold rounds up to this many bytes per rank run low-latency (MXAR_THRESHOLD_LL_MAX)   // ring: workgroups per launch on this device, all ranks of it (MXAR_RING_GRID)
+  // Threshold rounds up to this many bytes per rank run low-latency (MXAR_THRESHOLD_LL_MAX).
+  // Off by default: measured slower than the fenced hand-offs (8 logical ranks x 4 KiB:
+  // 22 vs 13 us per round; the peers' unfenced write-through units became visible ~5 us after
+  // their flags - profiles/round4/README.md).
+  int64_t thr_ll_max_ = 0;   // ring: workgroups per launch on this device, all ranks of it (MXAR_RING_GRID)
   char* slab_ = nullptr;            // own fine-grained slab (flags | S | R | LL)
   uint32_t* ctl_ = nullptr;         // [0] epoch, [1] ticket, [2] sticky error (device memory)
   char* peers_[kMaxRanks] = {};     // slab base of every rank (own included)

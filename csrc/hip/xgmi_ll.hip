@@ -90,21 +90,37 @@ __global__ __launch_bounds__(kCommThreads) void oneshot_ll_kernel(CommArgs a) {
 
   // reduce: own unit from the input, peers' units from the own slab once their epochs show
   bool late = false;
+  // The peers' units of a batch of B sources are loaded together (one load latency per
+  // batch instead of one per source), then each is re-polled only if its epoch is not in yet;
+  // the sum keeps the fixed order s = 0..P-1.
+  constexpr int B = 8;
   for (int64_t i = first; i < units; i += stride) {
     Acc8<E> acc;
-    for (int s = 0; s < P; ++s) {
-      if (s == r) {
-        acc.add(load_unit(in, i, nbytes));
-        continue;
+    for (int s0 = 0; s0 < P; s0 += B) {
+      Pack16 v[B];
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        const int s = s0 + b;
+        if (s < P && s != r)
+          v[b] = __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc(slot(r, s)), static_cast<int>(i * 16), 0, kAuxSys);
       }
-      const __amdgpu_buffer_rsrc_t rs = slab_rsrc(slot(r, s));
-      Pack16 v = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(i * 16), 0, kAuxSys);
-      while ((v[1] != epoch || v[3] != epoch) && !late) {
-        __builtin_amdgcn_s_sleep(1);
-        v = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(i * 16), 0, kAuxSys);
-        if (wall_ticks() > deadline) late = true;
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        const int s = s0 + b;
+        if (s >= P) continue;
+        if (s == r) {
+          acc.add(load_unit(in, i, nbytes));
+          continue;
+        }
+        const __amdgpu_buffer_rsrc_t rs = slab_rsrc(slot(r, s));
+        Pack16 w = v[b];
+        while ((w[1] != epoch || w[3] != epoch) && !late) {
+          __builtin_amdgcn_s_sleep(1);
+          w = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(i * 16), 0, kAuxSys);
+          if (wall_ticks() > deadline) late = true;
+        }
+        if (w[1] == epoch && w[3] == epoch) acc.add(make_uint2(w[0], w[2]));
       }
-      if (v[1] == epoch && v[3] == epoch) acc.add(make_uint2(v[0], v[2]));
     }
     store_unit(out, i, nbytes, acc.pack(a.scale));
   }

@@ -246,14 +246,31 @@ __device__ __forceinline__ void ll_reduce(const CommArgs& a, int P, int r, uint3
   constexpr int es = 16 / E::ELEMS;
   const int64_t nb = len * es, units = (nb + 7) / 8;
   bool late = false;
+  constexpr int B = 8;  // contributions in flight per lane: one load latency per batch, not per source
   for (int64_t i = threadIdx.x; i < units; i += kCommThreads) {
     Acc8<E> acc;
-    for (int s = 0; s < P; ++s) {
-      if (!((mask >> s) & 1u)) continue;
-      if (s == r)
-        acc.add(ld_payload8(own_in, i * 8, nb));
-      else
-        acc.add(ll_wait(slab_rsrc(a.base[r] + s_chunk + s * slot), i, epoch, deadline, &late));
+    for (int s0 = 0; s0 < P; s0 += B) {
+      Pack16 v[B];
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        const int s = s0 + b;
+        if (s < P && s != r && ((mask >> s) & 1u))
+          v[b] = __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc(a.base[r] + s_chunk + s * slot),
+                                                       static_cast<int>(i * 16), 0, kAuxSysLd);
+      }
+#pragma unroll
+      for (int b = 0; b < B; ++b) {  // fixed order s = 0..P-1
+        const int s = s0 + b;
+        if (s >= P || !((mask >> s) & 1u)) continue;
+        if (s == r) {
+          acc.add(ld_payload8(own_in, i * 8, nb));
+        } else {
+          uint2 d = make_uint2(v[b][0], v[b][2]);
+          if (v[b][1] != epoch || v[b][3] != epoch)
+            d = ll_wait(slab_rsrc(a.base[r] + s_chunk + s * slot), i, epoch, deadline, &late);
+          acc.add(d);
+        }
+      }
     }
     const uint2 o = acc.pack(scale);
     if (own_out != nullptr) st_payload8_wt(own_out, i * 8, nb, o);
@@ -275,26 +292,27 @@ __device__ __forceinline__ void ll_reduce(const CommArgs& a, int P, int r, uint3
   }
   if (late) __hip_atomic_fetch_or(err, ERR_TIMEOUT_SCATTER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// Copy a reduced LL chunk to the output; with `count`, lane 0 also returns the chunk's
+// count unit (loaded next to the payload, not after it).
 template <class E>
-__device__ __forceinline__ void ll_copy_out(char* dst, const char* src_chunk, int64_t len, uint32_t epoch,
-                                            uint64_t deadline, uint32_t* err) {
+__device__ __forceinline__ int32_t ll_copy_out(char* dst, const char* src_chunk, int64_t len, uint32_t epoch,
+                                               uint64_t deadline, uint32_t* err, bool count) {
   constexpr int es = 16 / E::ELEMS;
   const int64_t nb = len * es, units = (nb + 7) / 8;
   const __amdgpu_buffer_rsrc_t rs = slab_rsrc(src_chunk);
   bool late = false;
+  const bool lane0 = count && threadIdx.x == 0;
+  Pack16 cv;
+  if (lane0) cv = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(units * 16), 0, kAuxSysLd);
   for (int64_t i = threadIdx.x; i < units; i += kCommThreads) st_payload8_wt(dst, i * 8, nb, ll_wait(rs, i, epoch, deadline, &late));
+  int32_t cnt = 0;
+  if (lane0) {
+    uint2 d = make_uint2(cv[0], cv[2]);
+    if (cv[1] != epoch || cv[3] != epoch) d = ll_wait(rs, units, epoch, deadline, &late);
+    cnt = late ? 0 : static_cast<int32_t>(d.x);
+  }
   if (late) __hip_atomic_fetch_or(err, ERR_TIMEOUT_REDUCE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-// The count unit of a reduced LL chunk of `len` elements (one lane).
-template <class E>
-__device__ __forceinline__ int32_t ll_count(const char* src_chunk, int64_t len, uint32_t epoch, uint64_t deadline,
-                                            uint32_t* err) {
-  constexpr int es = 16 / E::ELEMS;
-  const int64_t units = (len * es + 7) / 8;
-  bool late = false;
-  const uint2 v = ll_wait(slab_rsrc(src_chunk), units, epoch, deadline, &late);
-  if (late) __hip_atomic_fetch_or(err, ERR_TIMEOUT_REDUCE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  return late ? 0 : static_cast<int32_t>(v.x);
+  return cnt;
 }
 
 // Sum the sources in `mask` (fixed order s = 0..P-1, fp32), store to the own output (when
@@ -478,7 +496,8 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   __shared__ uint32_t s0[kMaxSnapChunks];
   __shared__ uint64_t ps_lds[kPhaseSlots];
   // phase stamps (threshold layout): [0] start, [1] snapshot + lag gate done, [2] ticks
-  // waiting for contributions, [3] scatter + reduce done, [4] ticks waiting in the gather,
+  // waiting for contributions + reduce bodies, [3] scatter + reduce done, [4] ticks waiting
+  // in the gather + gather copies,
   // [5] end, [6] scatter done, [7] units gathered
   PhaseStamps ps(a, ps_lds);
   const int P = a.P;
@@ -792,6 +811,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+    const uint64_t t_body = ps.now();  // stamp [2] also holds the reduce body (loads, stores, publish)
     const uint32_t mask = sh_mask;
     const bool take = sh_flag != 0;
     const int cnt = __popc(mask);
@@ -820,6 +840,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
     }
     publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : f2(a, k, row * P + r, c); }, P, epoch,
                   rel && !ll);
+    ps.add(2, t_body);
   }
 
   ps.mark(3);
@@ -888,17 +909,10 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
           }
           if (!adopt) {
             if (counts) {
-              int32_t cv = 0;
-              if (take && ll) {
-                const int64_t lenc = clamp_len(clamp_len(a.n - static_cast<int64_t>(j) * a.block, a.block) -
-                                                   static_cast<int64_t>(c) * a.chunk,
-                                               a.chunk);
-                cv = ll_count<E>(a.base[r] + rowR + j * slot + static_cast<int64_t>(c) * a.ll_cstride, lenc, epoch,
-                                 deadline, err);
-              } else if (take) {
-                cv = static_cast<int32_t>(ld_flag(f2c(a, r, row * P + j, c)));
-              }
-              put_count(counts + static_cast<int64_t>(j) * a.nch + c, cv);
+              // an LL chunk's count travels with its payload: stored after the copy below
+              if (!(take && ll))
+                put_count(counts + static_cast<int64_t>(j) * a.nch + c,
+                          take ? static_cast<int32_t>(ld_flag(f2c(a, r, row * P + j, c))) : 0);
             }
             if (split) dec_publish(dec, epoch, take != 0, 0u);
           }
@@ -912,15 +926,19 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
         const int64_t len = clamp_len(clamp_len(clamp_len(a.n - bstart, a.block) - c * a.chunk, a.chunk) -
                                           (cstart - c * a.chunk),
                                       sub);
+        const uint64_t t_copy = ps.now();  // stamp [4] also holds the gather copies
         if (len > 0) {
-          if (take && ll)
-            ll_copy_out<E>(out + (bstart + cstart) * es, a.base[r] + rowR + j * slot + static_cast<int64_t>(c) * a.ll_cstride,
-                           len, epoch, deadline, err);
-          else if (take)
+          if (take && ll) {
+            const int32_t cv = ll_copy_out<E>(out + (bstart + cstart) * es,
+                                              a.base[r] + rowR + j * slot + static_cast<int64_t>(c) * a.ll_cstride, len,
+                                              epoch, deadline, err, counts != nullptr);
+            if (counts != nullptr && threadIdx.x == 0) put_count(counts + static_cast<int64_t>(j) * a.nch + c, cv);
+          } else if (take)
             copy_out<E>(out + (bstart + cstart) * es, a.base[r] + rowR + j * slot + cstart * es, len);
           else
             zero_fill<E>(out + (bstart + cstart) * es, len);
         }
+        ps.add(4, t_copy);
         progressed = true;
         ps.count(7);
         __syncthreads();

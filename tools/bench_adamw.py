@@ -41,13 +41,15 @@ def main() -> None:
     ap.add_argument("--ranks", type=int, nargs="+", default=[2, 8])
     ap.add_argument("--mib", type=int, default=64, help="bf16 parameter bytes per rank")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--fused-only", action="store_true", help="time the fused launch only (PMC runs)")
+    ap.add_argument("--grid", type=int, default=512)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     dt = torch.bfloat16
     n = (args.mib << 20) // 2
     hp = dict(lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01)
     for P in args.ranks:
-        cl = LocalCluster(P, slot_bytes=-(-(args.mib << 20) // P) + (1 << 20), grid=512, timeout_s=20.0)
+        cl = LocalCluster(P, slot_bytes=-(-(args.mib << 20) // P) + (1 << 20), grid=args.grid, timeout_s=20.0)
         b = cl.comms[0].block_elems(n, dtype_code(dt))
         grads = [fill_uniform(torch.empty(n, dtype=dt, device=dev), seed=k) for k in range(P)]
         params = [fill_uniform(torch.empty(n, dtype=dt, device=dev), seed=99) for _ in range(P)]
@@ -74,10 +76,13 @@ def main() -> None:
                 shard_p[k].copy_(masters[k].detach())
             cl.collective("all_gather", shard_p, params)
 
-        row = {"P": P, "param_MiB_per_rank": args.mib, "unfused_ms": round(timeit(unfused, args.iters), 3),
-               "fused_ms": round(timeit(fused, args.iters), 3)}
+        row = {"P": P, "grid": args.grid, "param_MiB_per_rank": args.mib, "fused_ms": round(timeit(fused, args.iters), 4)}
+        if P == 1:  # bytes per param: bf16 grad in + bf16 param out + fp32 master / m / v in and out
+            row["hbm_TBps"] = round(28 * n / (row["fused_ms"] / 1e3) / 1e12, 3)
+        if not args.fused_only:
+            row["unfused_ms"] = round(timeit(unfused, args.iters), 3)
+            row["speedup"] = round(row["unfused_ms"] / row["fused_ms"], 2)
         cl.check()
-        row["speedup"] = round(row["unfused_ms"] / row["fused_ms"], 2)
         print(json.dumps(row), flush=True)
         del cl, grads, params, states, shard_g, masters, opts, shard_p
         torch.cuda.empty_cache()

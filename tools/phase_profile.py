@@ -35,13 +35,14 @@ def main() -> None:
     ap.add_argument("--P", type=int, default=8)
     ap.add_argument("--mib", type=int, default=256)
     ap.add_argument("--algos", nargs="+", default=["twoshot", "ring"])
+    ap.add_argument("--kib", type=int, default=0, help="bytes per rank in KiB (overrides --mib)")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--grid", type=int, default=512)
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     dtype = torch.bfloat16
-    S = a.mib << 20
+    S = (a.kib << 10) if a.kib else (a.mib << 20)
     n = S // 2
     # a lag ring for the threshold kernel (its stamps: [1] lag gate done, [3] reduce done,
     # [6] scatter done - see xgmi_threshold.hip)
