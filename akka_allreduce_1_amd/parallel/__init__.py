@@ -4,3 +4,4 @@ from .ddp import BucketedGradReducer, TorchDistComm, bucket_sizes  # noqa: F401,
 from .hierarchical import HierarchicalCommunicator  # noqa: F401,E402
 from .p2p import P2PCommunicator, block_bounds, reduce_rows  # noqa: F401,E402
 from .zero import ShardedDataParallel  # noqa: F401,E402
+from .sdma import LocalSdmaCluster, SdmaCommunicator  # noqa: F401,E402

@@ -1,0 +1,131 @@
+"""Bucket allreduce with the cross-rank copies on the SDMA copy engines (csrc/hip/sdma_comm.h).
+
+The CU kernels of `XgmiCommunicator` move every byte with spinning workgroups; beside
+backward's GEMMs those workgroups are CUs the GEMMs do not get (profiles/round3/README.md:
+GEMMs 1.48x slower, comm 1.70x). Here the reference's ScatterBlock and ReduceBlock transfers
+(AllreduceWorker.scala:194-238; SURVEY §2.4 K2, "hipMemcpyPeerAsync writes the source slice
+directly into the owner's scatter slot") run on the copy engines; CUs only reduce the own
+block and gather the peers' reduced blocks locally, in small grids.
+
+`SdmaCommunicator`   one process per GPU (torch.distributed group), handles over gloo
+`LocalSdmaCluster`   P logical ranks in ONE process on one GPU (rehearsal / tests); each rank
+                     has its own stream and its own SDMA engines
+"""
+from __future__ import annotations
+
+from typing import Sequence
+
+import torch
+
+from .._native import C
+from .comm import CommError, _KERNEL_DTYPES, _current_stream, _describe
+
+_H = C.hip
+
+
+class SdmaCommunicator:
+    """Allreduce of the ranks of a torch.distributed group with SDMA cross-rank copies."""
+
+    accepts_stream = True
+
+    def __init__(self, group=None, *, device: torch.device | int | None = None, slot_bytes: int = 64 << 20,
+                 grid: int = 32, engines_per_peer: int = 2, timeout_s: float = 20.0, cpu_group=None):
+        import torch.distributed as dist
+
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        if cpu_group is None:
+            cpu_group = group if dist.get_backend(group) == "gloo" else dist.new_group(
+                ranks=None if group is None else dist.get_process_group_ranks(group), backend="gloo")
+        self.cpu_group = cpu_group
+        c, h, err = None, None, ""
+        try:
+            c = _H.SdmaComm(self.rank, self.world, self.device.index, slot_bytes, grid, engines_per_peer, timeout_s)
+            h = c.handle()
+        except Exception as e:  # noqa: BLE001 - every rank learns of it below
+            err = f"rank {self.rank}: {e}"
+        hs: list = [None] * self.world
+        dist.all_gather_object(hs, (h, err), group=cpu_group)
+        errs = [e for _, e in hs if e]
+        if errs:
+            raise CommError("SdmaCommunicator setup failed: " + "; ".join(errs))
+        try:
+            c.connect([x for x, _ in hs])
+        except Exception as e:  # noqa: BLE001
+            err = f"rank {self.rank}: {e}"
+        st: list = [None] * self.world
+        dist.all_gather_object(st, err, group=cpu_group)
+        errs = [e for e in st if e]
+        if errs:
+            raise CommError("SdmaCommunicator connect failed: " + "; ".join(errs))
+        self._c = c
+        self._dev = self.device.index
+
+    def allreduce(self, inp: torch.Tensor, out: torch.Tensor | None = None, *, op: str = "sum", algo: str = "sdma",
+                  stream: int | None = None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty_like(inp)
+        if op not in ("sum", "avg"):
+            raise ValueError(f"unsupported op {op!r}")
+        code = _KERNEL_DTYPES.get(inp.dtype)
+        if code is None or not (inp.is_contiguous() and out.is_contiguous()) or out.numel() != inp.numel():
+            raise ValueError("SDMA allreduce: contiguous fp32 / bf16 / fp16 tensors of equal size")
+        self._c.allreduce(inp.data_ptr(), out.data_ptr(), inp.numel(), code,
+                          _current_stream(self._dev) if stream is None else stream,
+                          1.0 / self.world if op == "avg" else 1.0)
+        return out
+
+    def allreduce_(self, t: torch.Tensor, *, op: str = "sum", algo: str = "sdma", stream: int | None = None):
+        return self.allreduce(t, t, op=op, stream=stream)
+
+    @property
+    def native(self):
+        return self._c
+
+    def check(self) -> None:
+        e = self._c.error()
+        if e:
+            raise CommError(f"SDMA allreduce rank {self.rank}: {_describe(e)}")
+
+
+class LocalSdmaCluster:
+    """P logical ranks of the SDMA allreduce in one process on one GPU. Rank k's work runs on
+    stream k (its flag waits hold that stream, not the caller's); the caller's stream waits
+    for all of them."""
+
+    def __init__(self, world: int, *, slot_bytes: int = 16 << 20, grid: int = 32, engines_per_peer: int = 1,
+                 timeout_s: float = 10.0, device: int | None = None):
+        dev = torch.cuda.current_device() if device is None else device
+        self.world = world
+        self.device = torch.device("cuda", dev)
+        self.comms = [_H.SdmaComm(k, world, dev, slot_bytes, grid, engines_per_peer, timeout_s) for k in range(world)]
+        for c in self.comms:
+            c.connect_local(self.comms)
+        self.streams = [torch.cuda.Stream(device=self.device) for _ in range(world)]
+
+    def allreduce(self, inputs: Sequence[torch.Tensor], outputs: Sequence[torch.Tensor] | None = None, *,
+                  op: str = "sum", stream: int | None = None) -> list[torch.Tensor]:
+        if len(inputs) != self.world:
+            raise ValueError("one input per logical rank")
+        outputs = list(outputs) if outputs is not None else [torch.empty_like(x) for x in inputs]
+        code = _KERNEL_DTYPES[inputs[0].dtype]
+        caller = torch.cuda.current_stream(self.device) if stream is None else torch.cuda.ExternalStream(
+            stream, device=self.device)
+        scale = 1.0 / self.world if op == "avg" else 1.0
+        for k, c in enumerate(self.comms):
+            s = self.streams[k]
+            s.wait_stream(caller)
+            c.allreduce(inputs[k].data_ptr(), outputs[k].data_ptr(), inputs[k].numel(), code, s.cuda_stream, scale)
+        for s in self.streams:
+            caller.wait_stream(s)
+        return outputs
+
+    def check(self) -> None:
+        for c in self.comms:
+            e = c.error()
+            if e:
+                raise CommError(f"SDMA allreduce rank {c.rank}: {_describe(e)}")

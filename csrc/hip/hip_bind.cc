@@ -11,6 +11,7 @@
 
 #include "../bindings/py_common.h"
 #include "device_plane.h"
+#include "sdma_comm.h"
 #include "xgmi_comm.h"
 #include "xgmi_plane.h"
 
@@ -308,6 +309,40 @@ void bind_hip(py::module_& m) {
       .def_readwrite("weight_decay", &AdamW::weight_decay)
       .def_readwrite("step", &AdamW::step);
 
+  py::class_<SdmaComm>(h, "SdmaComm")
+      .def(py::init<int, int, int, int64_t, int, int, double>(), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::arg("slot_bytes"), py::arg("grid") = 32, py::arg("engines_per_peer") = 2, py::arg("timeout_s") = 20.0)
+      .def("handle", [](const SdmaComm& c) { return py::bytes(c.handle()); })
+      .def("connect", [](SdmaComm& c, const std::vector<py::bytes>& hs) {
+        std::vector<std::string> v;
+        for (auto& b : hs) v.emplace_back(static_cast<std::string>(b));
+        c.connect(v);
+      })
+      .def("connect_local", &SdmaComm::connect_local)
+      .def("allreduce",
+           [](SdmaComm& c, uintptr_t in, uintptr_t out, int64_t n, DType dt, uintptr_t stream, float scale) {
+             py::gil_scoped_release r;
+             c.allreduce(reinterpret_cast<const void*>(in), reinterpret_cast<void*>(out), n, dt,
+                         reinterpret_cast<hipStream_t>(stream), scale);
+           },
+           py::arg("inp"), py::arg("out"), py::arg("n"), py::arg("dtype"), py::arg("stream") = 0, py::arg("scale") = 1.0f,
+           "out = scale x sum over ranks of inp; cross-rank copies on the SDMA engines (sdma_comm.h)")
+      .def("error", &SdmaComm::error)
+      .def("clear_error", &SdmaComm::clear_error)
+      .def_property("grid", &SdmaComm::grid, &SdmaComm::set_grid)
+      .def_property_readonly("engines", &SdmaComm::engines)
+      .def_property_readonly("slot_bytes", &SdmaComm::slot_bytes)
+      .def_property_readonly("rank", &SdmaComm::rank)
+      .def_property_readonly("world", &SdmaComm::world)
+      .def_property_readonly("stats", [](const SdmaComm& c) {
+        const SdmaStats& s = c.stats();
+        py::dict d;
+        d["calls"] = s.calls;
+        d["copies"] = s.copies;
+        d["bytes"] = s.bytes;
+        d["host_waits"] = s.host_waits;
+        return d;
+      });
   py::class_<XgmiComm>(h, "XgmiComm")
       .def(py::init<int, int, int, int64_t, int, double, int>(), py::arg("rank"), py::arg("world"), py::arg("device"),
            py::arg("slot_bytes"), py::arg("grid") = 0, py::arg("timeout_s") = 20.0, py::arg("threshold_rows") = 0)

@@ -1,0 +1,91 @@
+// SdmaComm: a bucket allreduce whose cross-rank data movement runs on the copy engines
+// (SDMA), not on CU workgroups - the MI355X-native form of SURVEY §2.4 K2's
+// "hipMemcpyPeerAsync writes the source slice into the owner's scatter slot", for DP buckets
+// that run beside backward's GEMMs (BASELINE config 5). Same direct two-shot as XgmiComm
+// (the reference's ScatterBlock / ReduceBlock, AllreduceWorker.scala:194-238):
+//
+//   phase 1  ScatterBlock   block j of the input -> rank j's SD slot [r]: one SDMA copy per
+//                           peer (split over `engines_per_peer` engines), then a 4-byte SDMA
+//                           copy of the epoch into rank j's FS[r] flag (ordered after the
+//                           data by an HSA completion-signal dependency)
+//   reduce                  a small-grid kernel (grid_ workgroups) sums the own block from
+//                           the input and the P-1 SD slots once every FS flag shows the epoch
+//   phase 2  ReduceBlock    the reduced own block -> every peer's RD slot [r] + FR flag (SDMA)
+//   gather                  a small-grid kernel copies the peers' RD slots into the output
+//
+// Stream ordering without the host: HIP's hipMemcpyAsync runs device-to-device copies as
+// blit KERNELS (profiles/round4/README.md, tools/sdma_probe.cc), so the copies are submitted
+// with hsa_amd_memory_async_copy_on_engine(force_copy_on_sdma). Each call's copies are
+// queued at call time but depend on an HSA signal that a one-lane kernel on the caller's
+// stream releases (after a system-scope release event, so the engines read what earlier
+// kernels wrote); the engines themselves wait on it. Flag waits are one-wave kernels with a
+// wall-clock deadline (error word, never a hang). SD / RD slots are double-buffered by the
+// call epoch's parity: a rank can be at most one call ahead of any peer still reading.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "xgmi_comm.h"
+
+namespace mxar {
+
+struct SdmaStats {
+  uint64_t calls = 0, copies = 0, bytes = 0, host_waits = 0;
+};
+
+class SdmaComm {
+ public:
+  // slot_bytes: capacity of one SD / RD slot (one block of one peer); calls reduce up to
+  // world * slot_bytes bytes (larger tensors are processed in segments).
+  SdmaComm(int rank, int world, int device, int64_t slot_bytes, int grid = 32, int engines_per_peer = 2,
+           double timeout_s = 20.0);
+  ~SdmaComm();
+  SdmaComm(const SdmaComm&) = delete;
+  SdmaComm& operator=(const SdmaComm&) = delete;
+
+  // IPC handle of the slab + the device's PCI location (peers map the slab and pick the
+  // SDMA engines towards this GPU from it).
+  std::string handle() const;
+  void connect(const std::vector<std::string>& handles);
+  // ranks of ONE process (the one-GPU rehearsal): slabs shared directly
+  void connect_local(const std::vector<SdmaComm*>& comms);
+
+  // out = scale * sum over ranks of in (out may alias in), enqueued on `stream`.
+  void allreduce(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, float scale = 1.f);
+
+  uint32_t error() const;
+  void clear_error();
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  int grid() const { return grid_; }
+  void set_grid(int g) { grid_ = g > 0 ? g : 1; }
+  int engines() const { return static_cast<int>(local_engines_.size()); }
+  int64_t slot_bytes() const { return slot_bytes_; }
+  const SdmaStats& stats() const { return st_; }
+
+ private:
+  struct Impl;
+  void segment(const char* in, char* out, int64_t n, DType dt, hipStream_t stream, float scale);
+  int rank_, world_, device_;
+  int64_t slot_bytes_;
+  int grid_;
+  int epp_;
+  double timeout_s_;
+  char* slab_ = nullptr;
+  int64_t slab_bytes_ = 0;
+  uint32_t* err_ = nullptr;  // device error word
+  std::vector<char*> peers_;
+  std::vector<bool> opened_;
+  std::vector<uint32_t> local_engines_;
+  uint64_t epoch_ = 0;
+  bool connected_ = false;
+  SdmaStats st_;
+  std::unique_ptr<Impl> impl_;
+};
+
+}  // namespace mxar

@@ -1,0 +1,431 @@
+// SdmaComm (sdma_comm.h): bucket allreduce with the cross-rank traffic on the SDMA copy
+// engines. Host side: HSA agents / engines, the per-call signal ring and the SDMA
+// submissions. Device side: the signal release, the bounded flag wait, and the small-grid
+// reduce and gather kernels.
+#include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "sdma_comm.h"
+#include "xgmi_device.h"
+
+namespace mxar {
+
+namespace {
+
+constexpr int kSlots = 16;              // calls in flight at most (signal / epoch-word ring)
+constexpr int64_t kFlagBytes = 64 * 1024;
+constexpr int kFrWord = 64;             // FR flags start at word 64 (FS at word 0)
+
+void hsa_check(hsa_status_t s, const char* what) {
+  if (s != HSA_STATUS_SUCCESS) {
+    const char* m = nullptr;
+    hsa_status_string(s, &m);
+    throw std::runtime_error(std::string("HSA error in ") + what + ": " + (m ? m : "?"));
+  }
+}
+
+int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+int64_t hclamp(int64_t avail, int64_t cap) { return avail <= 0 ? 0 : (avail < cap ? avail : cap); }
+int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// PCI location of a HIP device / an HSA agent: (domain << 32) | bdf
+uint64_t hip_location(int device) {
+  int bus = 0, dev = 0, dom = 0;
+  (void)hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device);
+  (void)hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device);
+  (void)hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device);
+  return (static_cast<uint64_t>(dom) << 32) | static_cast<uint64_t>((bus << 8) | (dev << 3));
+}
+
+struct AgentSearch {
+  uint64_t want = 0;
+  hsa_agent_t found{0};
+  hsa_agent_t cpu{0};
+};
+
+hsa_status_t agent_cb(hsa_agent_t a, void* data) {
+  auto* s = static_cast<AgentSearch*>(data);
+  hsa_device_type_t t;
+  hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
+  if (t == HSA_DEVICE_TYPE_CPU && s->cpu.handle == 0) s->cpu = a;
+  if (t != HSA_DEVICE_TYPE_GPU) return HSA_STATUS_SUCCESS;
+  uint32_t bdf = 0, dom = 0;
+  hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf);
+  hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &dom);
+  const uint64_t loc = (static_cast<uint64_t>(dom) << 32) | (bdf & ~0x7u);
+  if (loc == s->want) s->found = a;
+  return HSA_STATUS_SUCCESS;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------------
+__global__ void sdma_release_kernel(int64_t* sig) {
+  if (threadIdx.x == 0) __hip_atomic_store(sig, int64_t{0}, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One wave: lane k < nflags (k != skip) waits for flags[k] >= epoch, bounded by the deadline.
+__global__ __launch_bounds__(64) void sdma_wait_kernel(const uint32_t* flags, int nflags, int skip, uint32_t epoch,
+                                                       uint64_t timeout, uint32_t* err) {
+  const int k = static_cast<int>(threadIdx.x);
+  const uint64_t deadline = wall_ticks() + timeout;
+  const uint32_t* f = (k < nflags && k != skip) ? flags + k : nullptr;
+  bool ok = f == nullptr || reached(ld_flag(f), epoch);
+  while (!__all(ok)) {
+    __builtin_amdgcn_s_sleep(2);
+    if (!ok) ok = reached(ld_flag(f), epoch);
+    if (wall_ticks() > deadline) break;
+  }
+  if (!__all(ok) && k == 0) __hip_atomic_fetch_or(err, ERR_TIMEOUT_SCATTER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Own block = scale x (own input + the P-1 SD slots), fixed order s = 0..P-1, fp32; written
+// through (the engines read it from memory for phase 2). Workgroup b takes piece b.
+template <class E>
+__global__ __launch_bounds__(kCommThreads) void sdma_reduce_kernel(const char* in_own, const char* sd, int64_t slot,
+                                                                   int P, int r, char* out_own, int64_t len,
+                                                                   int64_t piece, float scale) {
+  constexpr int es = 16 / E::ELEMS;
+  // the engines wrote SD: drop any stale line of an earlier call from this CU's caches
+  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  __syncthreads();
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * piece;
+  const int64_t l = clamp_len(len - b0, piece);
+  if (l <= 0) return;
+  const RedSrc src{in_own + b0 * es, sd + b0 * es, slot, r};
+  reduce_to<E, 0>(P, src, 1, 0, [&](int) -> char* { return out_own + b0 * es; }, l, scale, true);
+}
+
+// out[block s] = RD slot s for every s != r (blockIdx.y = s). Plain-memory consumers follow
+// on this stream: the stores go through to memory.
+template <class E>
+__global__ __launch_bounds__(kCommThreads) void sdma_gather_kernel(char* out, const char* rd, int64_t slot, int r,
+                                                                   int64_t n, int64_t block, int64_t piece) {
+  constexpr int es = 16 / E::ELEMS;
+  const int s = static_cast<int>(blockIdx.y);
+  if (s == r) return;
+  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  __syncthreads();
+  const int64_t blen = clamp_len(n - static_cast<int64_t>(s) * block, block);
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * piece;
+  const int64_t l = clamp_len(blen - b0, piece);
+  if (l <= 0) return;
+  copy_from_slab<E>(out + (static_cast<int64_t>(s) * block + b0) * es, rd + s * slot + b0 * es, l);
+}
+
+// ---------------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------------
+struct SdmaComm::Impl {
+  hsa_agent_t own{0}, cpu{0};
+  std::vector<hsa_agent_t> peer_agent;
+  std::vector<std::vector<hsa_amd_sdma_engine_id_t>> peer_engines;  // engines towards peer k
+  struct Slot {
+    hsa_signal_t start{0}, mid{0}, sc{0}, scf{0}, gd{0}, gdf{0};
+    int64_t* start_p = nullptr;
+    int64_t* mid_p = nullptr;
+    bool used = false;
+  };
+  Slot slots[kSlots];
+  uint32_t* words = nullptr;  // pinned epoch words, one per slot (the flag copies' source)
+  hipEvent_t sysrel = nullptr;
+  bool hsa_up = false;
+};
+
+SdmaComm::SdmaComm(int rank, int world, int device, int64_t slot_bytes, int grid, int engines_per_peer,
+                   double timeout_s)
+    : rank_(rank), world_(world), device_(device), slot_bytes_(rup(std::max<int64_t>(slot_bytes, 4096), 4096)),
+      grid_(std::max(1, grid)), epp_(std::max(1, engines_per_peer)), timeout_s_(timeout_s),
+      impl_(std::make_unique<Impl>()) {
+  if (world < 1 || world > 32 || rank < 0 || rank >= world) throw std::invalid_argument("SdmaComm: bad rank / world");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hsa_check(hsa_init(), "hsa_init");
+  impl_->hsa_up = true;
+  AgentSearch s;
+  s.want = hip_location(device_);
+  hsa_check(hsa_iterate_agents(agent_cb, &s), "hsa_iterate_agents");
+  if (s.found.handle == 0) throw std::runtime_error("SdmaComm: no HSA agent at the HIP device's PCI location");
+  impl_->own = s.found;
+  impl_->cpu = s.cpu;
+  uint32_t mask = 0;
+  hsa_check(hsa_amd_memory_copy_engine_status(impl_->own, impl_->own, &mask), "copy_engine_status");
+  for (int b = 0; b < 32; ++b)
+    if (mask & (1u << b)) local_engines_.push_back(1u << b);
+  if (local_engines_.empty()) throw std::runtime_error("SdmaComm: the device reports no SDMA engine");
+
+  slab_bytes_ = XgmiComm::ipc_safe_bytes(kFlagBytes + 4 * static_cast<int64_t>(world_) * slot_bytes_);
+  hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&slab_), slab_bytes_, hipDeviceMallocFinegrained),
+            "hipExtMallocWithFlags(sdma slab)");
+  hip_check(hipMemset(slab_, 0, kFlagBytes), "hipMemset(sdma flags)");
+  hip_check(hipMalloc(reinterpret_cast<void**>(&err_), 64), "hipMalloc(err)");
+  hip_check(hipMemset(err_, 0, 64), "hipMemset(err)");
+  hip_check(hipHostMalloc(reinterpret_cast<void**>(&impl_->words), kSlots * 64, hipHostMallocCoherent),
+            "hipHostMalloc(epoch words)");
+  std::memset(impl_->words, 0, kSlots * 64);
+  hip_check(hipEventCreateWithFlags(&impl_->sysrel, hipEventDisableTiming | hipEventReleaseToSystem),
+            "hipEventCreate(release to system)");
+  for (auto& sl : impl_->slots) {
+    hsa_check(hsa_amd_signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_IPC, &sl.start), "signal(start)");
+    hsa_check(hsa_amd_signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_IPC, &sl.mid), "signal(mid)");
+    for (hsa_signal_t* x : {&sl.sc, &sl.scf, &sl.gd, &sl.gdf}) hsa_check(hsa_signal_create(0, 0, nullptr, x), "signal");
+    volatile hsa_signal_value_t* p = nullptr;
+    hsa_check(hsa_amd_signal_value_pointer(sl.start, &p), "signal_value_pointer(start)");
+    sl.start_p = const_cast<int64_t*>(reinterpret_cast<volatile int64_t*>(p));
+    hsa_check(hsa_amd_signal_value_pointer(sl.mid, &p), "signal_value_pointer(mid)");
+    sl.mid_p = const_cast<int64_t*>(reinterpret_cast<volatile int64_t*>(p));
+  }
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  peers_.assign(world_, nullptr);
+  opened_.assign(world_, false);
+  peers_[rank_] = slab_;
+}
+
+SdmaComm::~SdmaComm() {
+  (void)hipSetDevice(device_);
+  (void)hipDeviceSynchronize();
+  if (impl_) {
+    // no copy of ours may still target a peer slab we are about to unmap
+    for (auto& sl : impl_->slots)
+      for (hsa_signal_t x : {sl.sc, sl.scf, sl.gd, sl.gdf})
+        if (x.handle) (void)hsa_signal_wait_scacquire(x, HSA_SIGNAL_CONDITION_EQ, 0, 2000000000ull, HSA_WAIT_STATE_BLOCKED);
+    for (auto& sl : impl_->slots)
+      for (hsa_signal_t x : {sl.start, sl.mid, sl.sc, sl.scf, sl.gd, sl.gdf})
+        if (x.handle) hsa_signal_destroy(x);
+    if (impl_->sysrel) (void)hipEventDestroy(impl_->sysrel);
+    if (impl_->words) (void)hipHostFree(impl_->words);
+  }
+  for (int k = 0; k < world_; ++k)
+    if (opened_[k] && peers_[k]) (void)hipIpcCloseMemHandle(peers_[k]);
+  if (err_) (void)hipFree(err_);
+  if (slab_) (void)hipFree(slab_);
+  if (impl_ && impl_->hsa_up) hsa_shut_down();
+}
+
+std::string SdmaComm::handle() const {
+  hipIpcMemHandle_t h;
+  hip_check(hipIpcGetMemHandle(&h, slab_), "hipIpcGetMemHandle(sdma slab)");
+  const uint64_t loc = hip_location(device_);
+  std::string out(reinterpret_cast<const char*>(&h), sizeof(h));
+  out.append(reinterpret_cast<const char*>(&loc), sizeof(loc));
+  return out;
+}
+
+static std::vector<hsa_amd_sdma_engine_id_t> pick_engines(hsa_agent_t dst, hsa_agent_t src, int k, int epp,
+                                                          const std::vector<uint32_t>& allowed) {
+  uint32_t mask = 0;
+  if (hsa_amd_memory_copy_engine_status(dst, src, &mask) != HSA_STATUS_SUCCESS) mask = 0;
+  std::vector<uint32_t> avail;
+  for (uint32_t e : allowed)
+    if (mask & e) avail.push_back(e);
+  if (avail.empty()) avail = allowed;  // peer direction unknown to the query: the local engines
+  std::vector<hsa_amd_sdma_engine_id_t> out;
+  for (int p = 0; p < epp; ++p)
+    out.push_back(static_cast<hsa_amd_sdma_engine_id_t>(avail[(static_cast<size_t>(k) * epp + p) % avail.size()]));
+  return out;
+}
+
+void SdmaComm::connect(const std::vector<std::string>& handles) {
+  if (static_cast<int>(handles.size()) != world_) throw std::invalid_argument("SdmaComm.connect: one handle per rank");
+  impl_->peer_agent.assign(world_, impl_->own);
+  impl_->peer_engines.assign(world_, {});
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  for (int k = 0; k < world_; ++k) {
+    if (k == rank_) continue;
+    const std::string& h = handles[k];
+    if (h.size() != sizeof(hipIpcMemHandle_t) + 8) throw std::invalid_argument("SdmaComm.connect: bad handle");
+    hipIpcMemHandle_t ih;
+    std::memcpy(&ih, h.data(), sizeof(ih));
+    uint64_t loc = 0;
+    std::memcpy(&loc, h.data() + sizeof(ih), 8);
+    void* p = nullptr;
+    hip_check(hipIpcOpenMemHandle(&p, ih, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(sdma slab)");
+    peers_[k] = static_cast<char*>(p);
+    opened_[k] = true;
+    AgentSearch s;
+    s.want = loc;
+    hsa_check(hsa_iterate_agents(agent_cb, &s), "hsa_iterate_agents");
+    if (s.found.handle != 0) impl_->peer_agent[k] = s.found;
+    impl_->peer_engines[k] = pick_engines(impl_->peer_agent[k], impl_->own, k, epp_, local_engines_);
+  }
+  connected_ = true;
+}
+
+void SdmaComm::connect_local(const std::vector<SdmaComm*>& comms) {
+  if (static_cast<int>(comms.size()) != world_) throw std::invalid_argument("SdmaComm.connect_local: one comm per rank");
+  // Ranks of one process share its SDMA queues (one per engine): a rank's phase-2 copies
+  // wait in an engine queue for its own reduce, which needs the peers' phase-1 copies - so
+  // each local rank gets engines of its own (no copy of a peer ever queues behind them).
+  const int nloc = world_;
+  std::vector<uint32_t> mine;
+  for (size_t i = 0; i < local_engines_.size(); ++i)
+    if (static_cast<int>(i % nloc) == rank_) mine.push_back(local_engines_[i]);
+  if (mine.empty()) throw std::runtime_error("SdmaComm.connect_local: fewer SDMA engines than local ranks");
+  local_engines_ = mine;
+  impl_->peer_agent.assign(world_, impl_->own);
+  impl_->peer_engines.assign(world_, {});
+  for (int k = 0; k < world_; ++k) {
+    if (comms[k]->slot_bytes_ != slot_bytes_ || comms[k]->device_ != device_)
+      throw std::invalid_argument("SdmaComm.connect_local: slab geometry / device differs");
+    peers_[k] = comms[k]->slab_;
+    if (k != rank_) impl_->peer_engines[k] = pick_engines(impl_->own, impl_->own, k, epp_, local_engines_);
+  }
+  connected_ = true;
+}
+
+uint32_t SdmaComm::error() const {
+  uint32_t e = 0;
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipMemcpy(&e, err_, 4, hipMemcpyDeviceToHost), "hipMemcpy(err)");
+  return e;
+}
+
+void SdmaComm::clear_error() {
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipMemset(err_, 0, 4), "hipMemset(err)");
+}
+
+void SdmaComm::allreduce(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, float scale) {
+  if (!connected_) throw std::runtime_error("SdmaComm: connect() first");
+  if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15)
+    throw std::invalid_argument("SdmaComm: buffers must be 16-byte aligned");
+  if (n <= 0) return;
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  const int64_t es = static_cast<int64_t>(dtype_size(dt));
+  const int64_t seg = world_ * (slot_bytes_ / es);
+  for (int64_t off = 0; off < n; off += seg)
+    segment(static_cast<const char*>(in) + off * es, static_cast<char*>(out) + off * es, std::min(seg, n - off), dt,
+            stream, scale);
+}
+
+void SdmaComm::segment(const char* in, char* out, int64_t n, DType dt, hipStream_t stream, float scale) {
+  Impl& m = *impl_;
+  const int W = world_, r = rank_;
+  const int64_t es = static_cast<int64_t>(dtype_size(dt));
+  const int64_t elems = 16 / es;
+  const uint64_t e64 = ++epoch_;
+  const uint32_t e = static_cast<uint32_t>(e64);
+  const int par = static_cast<int>(e64 & 1u);
+  Impl::Slot& sl = m.slots[e64 % kSlots];
+  // the slot's previous call: every copy it submitted has completed (the host is at most
+  // kSlots calls ahead of the engines; a peer that stopped turns into an error here)
+  if (sl.used) {
+    for (hsa_signal_t x : {sl.sc, sl.scf, sl.gd, sl.gdf}) {
+      if (hsa_signal_load_scacquire(x) == 0) continue;
+      ++st_.host_waits;
+      const uint64_t ns = static_cast<uint64_t>(timeout_s_ * 1e9);
+      if (hsa_signal_wait_scacquire(x, HSA_SIGNAL_CONDITION_EQ, 0, ns, HSA_WAIT_STATE_BLOCKED) != 0)
+        throw std::runtime_error("SdmaComm: copies of an earlier call did not complete (peer gone?)");
+    }
+  }
+  sl.used = true;
+  const int64_t block = rup(cdiv(n, W), elems);
+  auto blen = [&](int j) { return hclamp(n - static_cast<int64_t>(j) * block, block); };
+  if (block * es > slot_bytes_) throw std::logic_error("SdmaComm: segment exceeds the slot");
+  // split of one block over epp engines, 4 KiB aligned pieces
+  auto parts = [&](int64_t bytes, int p, int64_t* off, int64_t* len) {
+    const int64_t piece = rup(cdiv(bytes, epp_), 4096);
+    *off = std::min<int64_t>(bytes, p * piece);
+    *len = std::min<int64_t>(bytes - *off, piece);
+  };
+  int n1 = 0, n2 = 0;
+  for (int j = 0; j < W; ++j) {
+    if (j == r) continue;
+    for (int p = 0; p < epp_; ++p) {
+      int64_t o, l;
+      parts(blen(j) * es, p, &o, &l);
+      n1 += l > 0;
+      parts(blen(r) * es, p, &o, &l);
+      n2 += l > 0;
+    }
+  }
+  m.words[(e64 % kSlots) * 16] = e;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  hsa_signal_store_relaxed(sl.start, 1);
+  hsa_signal_store_relaxed(sl.mid, 1);
+  hsa_signal_store_relaxed(sl.sc, n1);
+  hsa_signal_store_relaxed(sl.scf, W - 1);
+  hsa_signal_store_relaxed(sl.gd, n2);
+  hsa_signal_store_relaxed(sl.gdf, W - 1);
+  uint32_t* word = m.words + (e64 % kSlots) * 16;
+  const int64_t off_SD = kFlagBytes, off_RD = kFlagBytes + 2 * static_cast<int64_t>(W) * slot_bytes_;
+  auto copy = [&](void* dst, hsa_agent_t da, const void* src, hsa_agent_t sa, int64_t bytes, int ndep,
+                  const hsa_signal_t* deps, hsa_signal_t done, hsa_amd_sdma_engine_id_t eng) {
+    hsa_check(hsa_amd_memory_async_copy_on_engine(dst, da, src, sa, static_cast<size_t>(bytes), ndep, deps, done, eng,
+                                                  true),
+              "hsa_amd_memory_async_copy_on_engine");
+    ++st_.copies;
+    st_.bytes += static_cast<uint64_t>(bytes);
+  };
+  // phase 1: block j -> rank j's SD[par][r], then its FS[r] flag
+  for (int j = 0; j < W; ++j) {
+    if (j == r) continue;
+    for (int p = 0; p < epp_; ++p) {
+      int64_t o, l;
+      parts(blen(j) * es, p, &o, &l);
+      if (l > 0)
+        copy(peers_[j] + off_SD + (static_cast<int64_t>(par) * W + r) * slot_bytes_ + o, m.peer_agent[j],
+             in + static_cast<int64_t>(j) * block * es + o, m.own, l, 1, &sl.start, sl.sc, m.peer_engines[j][p]);
+    }
+  }
+  const hsa_signal_t dep1[2] = {sl.start, sl.sc};
+  for (int j = 0; j < W; ++j)
+    if (j != r)
+      copy(peers_[j] + r * 4, m.peer_agent[j], word, m.cpu, 4, 2, dep1, sl.scf, m.peer_engines[j][0]);
+  // phase 2: the reduced own block -> every peer's RD[par][r], then its FR[r] flag
+  for (int k = 0; k < W; ++k) {
+    if (k == r) continue;
+    for (int p = 0; p < epp_; ++p) {
+      int64_t o, l;
+      parts(blen(r) * es, p, &o, &l);
+      if (l > 0)
+        copy(peers_[k] + off_RD + (static_cast<int64_t>(par) * W + r) * slot_bytes_ + o, m.peer_agent[k],
+             out + static_cast<int64_t>(r) * block * es + o, m.own, l, 1, &sl.mid, sl.gd, m.peer_engines[k][p]);
+    }
+  }
+  const hsa_signal_t dep2[2] = {sl.mid, sl.gd};
+  for (int k = 0; k < W; ++k)
+    if (k != r)
+      copy(peers_[k] + (kFrWord + r) * 4, m.peer_agent[k], word, m.cpu, 4, 2, dep2, sl.gdf, m.peer_engines[k][0]);
+
+  // the stream: release phase 1 once the input is in memory, wait, reduce, release phase 2,
+  // wait, gather
+  const uint64_t ticks = static_cast<uint64_t>(timeout_s_ * 1e8);
+  hip_check(hipEventRecord(m.sysrel, stream), "hipEventRecord(release to system)");
+  hipLaunchKernelGGL(sdma_release_kernel, dim3(1), dim3(64), 0, stream, sl.start_p);
+  hipLaunchKernelGGL(sdma_wait_kernel, dim3(1), dim3(64), 0, stream, reinterpret_cast<const uint32_t*>(slab_), W, r, e,
+                     ticks, err_);
+  const int64_t rl = blen(r);
+  const int64_t piece = std::max<int64_t>(elems, rup(cdiv(rl, grid_), elems));
+  const int g1 = static_cast<int>(std::max<int64_t>(1, cdiv(rl, piece)));
+  const char* sd = slab_ + off_SD + static_cast<int64_t>(par) * W * slot_bytes_;
+  dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
+    using E = decltype(tag);
+    hipLaunchKernelGGL(sdma_reduce_kernel<E>, dim3(g1), dim3(kCommThreads), 0, stream,
+                       in + static_cast<int64_t>(r) * block * es, sd, slot_bytes_, W, r,
+                       out + static_cast<int64_t>(r) * block * es, rl, piece, scale);
+  });
+  hipLaunchKernelGGL(sdma_release_kernel, dim3(1), dim3(64), 0, stream, sl.mid_p);
+  hipLaunchKernelGGL(sdma_wait_kernel, dim3(1), dim3(64), 0, stream,
+                     reinterpret_cast<const uint32_t*>(slab_) + kFrWord, W, r, e, ticks, err_);
+  const int64_t gpiece = std::max<int64_t>(elems, rup(cdiv(block, std::max(1, grid_ / std::max(1, W - 1))), elems));
+  const int g2 = static_cast<int>(std::max<int64_t>(1, cdiv(block, gpiece)));
+  const char* rd = slab_ + off_RD + static_cast<int64_t>(par) * W * slot_bytes_;
+  dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
+    using E = decltype(tag);
+    hipLaunchKernelGGL(sdma_gather_kernel<E>, dim3(g2, W), dim3(kCommThreads), 0, stream, out, rd, slot_bytes_, r, n,
+                       block, gpiece);
+  });
+  hip_check(hipGetLastError(), "sdma kernels");
+  ++st_.calls;
+}
+
+}  // namespace mxar

@@ -109,7 +109,7 @@ def build(jobs: int | None = None, clean: bool = False, debug: bool = False, san
     if todo or not out.exists() or out.stat().st_mtime < max(o.stat().st_mtime for o in objs):
         cmd = [str(ROCM / "bin" / "hipcc"), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(out)]
         cmd += [str(o) for o in objs]
-        cmd += [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM / 'lib'}", "-lpthread"]
+        cmd += [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lhsa-runtime64", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM / 'lib'}", "-lpthread"]
         if sanitize:
             cmd += [f"-fsanitize={sanitize}"]
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -164,7 +164,7 @@ def _build_gpu_exe(bdir: Path, debug: bool, verbose: bool) -> None:
     if exe.exists() and exe.stat().st_mtime >= max(o.stat().st_mtime for o in objs):
         return
     cmd = [str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-o", str(exe)] + [str(o) for o in objs]
-    cmd += [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM / 'lib'}", "-lpthread"]
+    cmd += [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lhsa-runtime64", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM / 'lib'}", "-lpthread"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
