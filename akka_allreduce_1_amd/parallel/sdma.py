@@ -93,9 +93,9 @@ class SdmaCommunicator:
 
 
 class LocalSdmaCluster:
-    """P logical ranks of the SDMA allreduce in one process on one GPU. Rank k's work runs on
-    stream k (its flag waits hold that stream, not the caller's); the caller's stream waits
-    for all of them."""
+    """P logical ranks of the SDMA allreduce in one process on one GPU, all on the caller's
+    stream in one interleaved schedule (SdmaComm::allreduce_local): every wait only needs
+    releases queued before it, so no rank's wait can hold up a peer's progress."""
 
     def __init__(self, world: int, *, slot_bytes: int = 16 << 20, grid: int = 32, engines_per_peer: int = 1,
                  timeout_s: float = 10.0, device: int | None = None):
@@ -105,27 +105,25 @@ class LocalSdmaCluster:
         self.comms = [_H.SdmaComm(k, world, dev, slot_bytes, grid, engines_per_peer, timeout_s) for k in range(world)]
         for c in self.comms:
             c.connect_local(self.comms)
-        self.streams = [torch.cuda.Stream(device=self.device) for _ in range(world)]
 
     def allreduce(self, inputs: Sequence[torch.Tensor], outputs: Sequence[torch.Tensor] | None = None, *,
                   op: str = "sum", stream: int | None = None) -> list[torch.Tensor]:
         if len(inputs) != self.world:
             raise ValueError("one input per logical rank")
         outputs = list(outputs) if outputs is not None else [torch.empty_like(x) for x in inputs]
-        code = _KERNEL_DTYPES[inputs[0].dtype]
-        caller = torch.cuda.current_stream(self.device) if stream is None else torch.cuda.ExternalStream(
-            stream, device=self.device)
-        scale = 1.0 / self.world if op == "avg" else 1.0
-        for k, c in enumerate(self.comms):
-            s = self.streams[k]
-            s.wait_stream(caller)
-            c.allreduce(inputs[k].data_ptr(), outputs[k].data_ptr(), inputs[k].numel(), code, s.cuda_stream, scale)
-        for s in self.streams:
-            caller.wait_stream(s)
+        n = inputs[0].numel()
+        for x, y in zip(inputs, outputs):
+            if x.numel() != n or y.numel() != n or x.dtype != inputs[0].dtype or y.dtype != x.dtype:
+                raise ValueError("all ranks must pass the same shape and dtype")
+        _H.SdmaComm.allreduce_local(self.comms, [x.data_ptr() for x in inputs], [y.data_ptr() for y in outputs], n,
+                                    _KERNEL_DTYPES[inputs[0].dtype],
+                                    _current_stream(self.device.index) if stream is None else stream,
+                                    1.0 / self.world if op == "avg" else 1.0)
         return outputs
 
     def check(self) -> None:
         for c in self.comms:
             e = c.error()
             if e:
-                raise CommError(f"SDMA allreduce rank {c.rank}: {_describe(e)}")
+                state = " || ".join(x.debug_state() for x in self.comms)
+                raise CommError(f"SDMA allreduce rank {c.rank}: {_describe(e)}; state: {state}")

@@ -309,6 +309,7 @@ void bind_hip(py::module_& m) {
       .def_readwrite("weight_decay", &AdamW::weight_decay)
       .def_readwrite("step", &AdamW::step);
 
+  h.def("sdma_diagnose", &sdma_diagnose, py::arg("device") = 0);
   py::class_<SdmaComm>(h, "SdmaComm")
       .def(py::init<int, int, int, int64_t, int, int, double>(), py::arg("rank"), py::arg("world"), py::arg("device"),
            py::arg("slot_bytes"), py::arg("grid") = 32, py::arg("engines_per_peer") = 2, py::arg("timeout_s") = 20.0)
@@ -327,8 +328,22 @@ void bind_hip(py::module_& m) {
            },
            py::arg("inp"), py::arg("out"), py::arg("n"), py::arg("dtype"), py::arg("stream") = 0, py::arg("scale") = 1.0f,
            "out = scale x sum over ranks of inp; cross-rank copies on the SDMA engines (sdma_comm.h)")
+      .def_static(
+          "allreduce_local",
+          [](const std::vector<SdmaComm*>& comms, const std::vector<uintptr_t>& ins, const std::vector<uintptr_t>& outs,
+             int64_t n, DType dt, uintptr_t stream, float scale) {
+            std::vector<const void*> i(ins.size());
+            std::vector<void*> o(outs.size());
+            for (size_t k = 0; k < ins.size(); ++k) i[k] = reinterpret_cast<const void*>(ins[k]);
+            for (size_t k = 0; k < outs.size(); ++k) o[k] = reinterpret_cast<void*>(outs[k]);
+            py::gil_scoped_release r;
+            SdmaComm::allreduce_local(comms, i, o, n, dt, reinterpret_cast<hipStream_t>(stream), scale);
+          },
+          py::arg("comms"), py::arg("inputs"), py::arg("outputs"), py::arg("n"), py::arg("dtype"), py::arg("stream") = 0,
+          py::arg("scale") = 1.0f)
       .def("error", &SdmaComm::error)
       .def("clear_error", &SdmaComm::clear_error)
+      .def("debug_state", &SdmaComm::debug_state)
       .def_property("grid", &SdmaComm::grid, &SdmaComm::set_grid)
       .def_property_readonly("engines", &SdmaComm::engines)
       .def_property_readonly("slot_bytes", &SdmaComm::slot_bytes)

@@ -57,9 +57,14 @@ class SdmaComm {
 
   // out = scale * sum over ranks of in (out may alias in), enqueued on `stream`.
   void allreduce(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, float scale = 1.f);
+  // every rank of this process (connect_local) in one stream-ordered schedule
+  static void allreduce_local(const std::vector<SdmaComm*>& comms, const std::vector<const void*>& ins,
+                              const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream,
+                              float scale = 1.f);
 
   uint32_t error() const;
   void clear_error();
+  std::string debug_state() const;  // signals of the calls in flight, flag words (bring-up)
   int rank() const { return rank_; }
   int world() const { return world_; }
   int grid() const { return grid_; }
@@ -70,7 +75,18 @@ class SdmaComm {
 
  private:
   struct Impl;
-  void segment(const char* in, char* out, int64_t n, DType dt, hipStream_t stream, float scale);
+  struct Plan {
+    const char* in = nullptr;
+    char* out = nullptr;
+    int64_t n = 0, block = 0;
+    DType dt = DType::F32;
+    uint32_t epoch = 0;
+    int par = 0, slot = 0;
+  };
+  // one segment: wait for the slot, arm its signals, queue both phases' copies (host)
+  Plan plan(const char* in, char* out, int64_t n, DType dt);
+  void enqueue_reduce(const Plan& pl, hipStream_t stream, float scale);
+  void enqueue_gather(const Plan& pl, hipStream_t stream);
   int rank_, world_, device_;
   int64_t slot_bytes_;
   int grid_;
@@ -87,5 +103,8 @@ class SdmaComm {
   SdmaStats st_;
   std::unique_ptr<Impl> impl_;
 };
+
+// HSA view of the machine (agents, PCI locations, SDMA engine masks): bring-up diagnostics
+std::string sdma_diagnose(int device);
 
 }  // namespace mxar

@@ -125,6 +125,53 @@ __global__ __launch_bounds__(kCommThreads) void sdma_gather_kernel(char* out, co
 // ---------------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------------
+std::string sdma_diagnose(int device) {
+  std::string out;
+  hip_check(hipSetDevice(device), "hipSetDevice");
+  hsa_status_t st = hsa_init();
+  out += "hsa_init=" + std::to_string(static_cast<int>(st));
+  const uint64_t want = hip_location(device);
+  out += " want=" + std::to_string(want);
+  struct Ctx {
+    std::string* out;
+  } ctx{&out};
+  hsa_iterate_agents(
+      [](hsa_agent_t a, void* d) -> hsa_status_t {
+        auto* c = static_cast<Ctx*>(d);
+        hsa_device_type_t t;
+        hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
+        uint32_t bdf = 0, dom = 0, mask = 0;
+        hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf);
+        hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &dom);
+        hsa_status_t s = HSA_STATUS_SUCCESS;
+        uint32_t m2 = 0;
+        if (t == HSA_DEVICE_TYPE_GPU) s = hsa_amd_memory_copy_engine_status(a, a, &mask);
+        *c->out += " | gpu<-gpu status=" + std::to_string(static_cast<int>(s)) + " mask=" + std::to_string(mask);
+        if (t == HSA_DEVICE_TYPE_GPU) {
+          hsa_agent_t cpu{0};
+          hsa_iterate_agents(
+              [](hsa_agent_t x, void* d) -> hsa_status_t {
+                hsa_device_type_t tt;
+                hsa_agent_get_info(x, HSA_AGENT_INFO_DEVICE, &tt);
+                if (tt == HSA_DEVICE_TYPE_CPU && static_cast<hsa_agent_t*>(d)->handle == 0) *static_cast<hsa_agent_t*>(d) = x;
+                return HSA_STATUS_SUCCESS;
+              },
+              &cpu);
+          s = hsa_amd_memory_copy_engine_status(a, cpu, &m2);
+          *c->out += " gpu<-cpu status=" + std::to_string(static_cast<int>(s)) + " mask=" + std::to_string(m2);
+          s = hsa_amd_memory_copy_engine_status(cpu, a, &m2);
+          *c->out += " cpu<-gpu status=" + std::to_string(static_cast<int>(s)) + " mask=" + std::to_string(m2);
+        }
+        *c->out += " | agent type=" + std::to_string(static_cast<int>(t)) + " bdf=" + std::to_string(bdf) +
+                   " dom=" + std::to_string(dom) + " status=" + std::to_string(static_cast<int>(s)) +
+                   " mask=" + std::to_string(mask);
+        return HSA_STATUS_SUCCESS;
+      },
+      &ctx);
+  if (st == HSA_STATUS_SUCCESS) hsa_shut_down();
+  return out;
+}
+
 struct SdmaComm::Impl {
   hsa_agent_t own{0}, cpu{0};
   std::vector<hsa_agent_t> peer_agent;
@@ -156,8 +203,17 @@ SdmaComm::SdmaComm(int rank, int world, int device, int64_t slot_bytes, int grid
   if (s.found.handle == 0) throw std::runtime_error("SdmaComm: no HSA agent at the HIP device's PCI location");
   impl_->own = s.found;
   impl_->cpu = s.cpu;
-  uint32_t mask = 0;
-  hsa_check(hsa_amd_memory_copy_engine_status(impl_->own, impl_->own, &mask), "copy_engine_status");
+  // The device's SDMA engines. The ROCm 7.0 runtime torch ships answers the same-agent query
+  // with HSA_STATUS_ERROR_INVALID_AGENT (7.2 answers it); the host <-> device directions name
+  // the same engines there.
+  uint32_t mask = 0, m2 = 0;
+  if (hsa_amd_memory_copy_engine_status(impl_->own, impl_->own, &mask) != HSA_STATUS_SUCCESS) {
+    mask = 0;
+    if (impl_->cpu.handle != 0) {
+      if (hsa_amd_memory_copy_engine_status(impl_->own, impl_->cpu, &m2) == HSA_STATUS_SUCCESS) mask |= m2;
+      if (hsa_amd_memory_copy_engine_status(impl_->cpu, impl_->own, &m2) == HSA_STATUS_SUCCESS) mask |= m2;
+    }
+  }
   for (int b = 0; b < 32; ++b)
     if (mask & (1u << b)) local_engines_.push_back(1u << b);
   if (local_engines_.empty()) throw std::runtime_error("SdmaComm: the device reports no SDMA engine");
@@ -281,6 +337,33 @@ void SdmaComm::connect_local(const std::vector<SdmaComm*>& comms) {
   connected_ = true;
 }
 
+std::string SdmaComm::debug_state() const {
+  std::string out = "epoch=" + std::to_string(epoch_) + " engines=";
+  for (uint32_t e : local_engines_) out += std::to_string(e) + ",";
+  for (int k = 0; k < world_; ++k) {
+    out += " peer" + std::to_string(k) + "_engines=";
+    if (k < static_cast<int>(impl_->peer_engines.size()))
+      for (auto e : impl_->peer_engines[k]) out += std::to_string(static_cast<uint32_t>(e)) + ",";
+  }
+  for (int i = 0; i < kSlots; ++i) {
+    const Impl::Slot& sl = impl_->slots[i];
+    if (!sl.used) continue;
+    out += " | slot" + std::to_string(i) + " start=" + std::to_string(hsa_signal_load_relaxed(sl.start)) +
+           " mid=" + std::to_string(hsa_signal_load_relaxed(sl.mid)) +
+           " sc=" + std::to_string(hsa_signal_load_relaxed(sl.sc)) +
+           " scf=" + std::to_string(hsa_signal_load_relaxed(sl.scf)) +
+           " gd=" + std::to_string(hsa_signal_load_relaxed(sl.gd)) +
+           " gdf=" + std::to_string(hsa_signal_load_relaxed(sl.gdf));
+  }
+  std::vector<uint32_t> f(128, 0);
+  (void)hipMemcpy(f.data(), slab_, f.size() * 4, hipMemcpyDeviceToHost);
+  out += " | FS=";
+  for (int k = 0; k < world_; ++k) out += std::to_string(f[k]) + ",";
+  out += " FR=";
+  for (int k = 0; k < world_; ++k) out += std::to_string(f[kFrWord + k]) + ",";
+  return out;
+}
+
 uint32_t SdmaComm::error() const {
   uint32_t e = 0;
   hip_check(hipSetDevice(device_), "hipSetDevice");
@@ -294,27 +377,62 @@ void SdmaComm::clear_error() {
 }
 
 void SdmaComm::allreduce(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, float scale) {
-  if (!connected_) throw std::runtime_error("SdmaComm: connect() first");
-  if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15)
-    throw std::invalid_argument("SdmaComm: buffers must be 16-byte aligned");
-  if (n <= 0) return;
-  hip_check(hipSetDevice(device_), "hipSetDevice");
-  const int64_t es = static_cast<int64_t>(dtype_size(dt));
-  const int64_t seg = world_ * (slot_bytes_ / es);
-  for (int64_t off = 0; off < n; off += seg)
-    segment(static_cast<const char*>(in) + off * es, static_cast<char*>(out) + off * es, std::min(seg, n - off), dt,
-            stream, scale);
+  allreduce_local({this}, {in}, {out}, n, dt, stream, scale);
 }
 
-void SdmaComm::segment(const char* in, char* out, int64_t n, DType dt, hipStream_t stream, float scale) {
+// The ranks of one process on one stream: for each segment every rank's copies are queued
+// first, then the stream releases every rank's phase 1, then runs every rank's wait + reduce
+// + phase-2 release, then every rank's wait + gather. Each wait only needs releases queued
+// before it on the same stream, so one stream carries all local ranks (a wait holding a
+// hardware queue never blocks a peer's release behind it).
+void SdmaComm::allreduce_local(const std::vector<SdmaComm*>& comms, const std::vector<const void*>& ins,
+                               const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, float scale) {
+  if (comms.empty() || ins.size() != comms.size() || outs.size() != comms.size())
+    throw std::invalid_argument("SdmaComm: one input and one output per local rank");
+  SdmaComm& c0 = *comms[0];
+  for (size_t y = 0; y < comms.size(); ++y) {
+    const SdmaComm& c = *comms[y];
+    if (!c.connected_) throw std::runtime_error("SdmaComm: connect() first");
+    if (c.device_ != c0.device_ || c.world_ != c0.world_ || c.slot_bytes_ != c0.slot_bytes_)
+      throw std::invalid_argument("SdmaComm: local ranks must share device, world and slot size");
+    if ((reinterpret_cast<uintptr_t>(ins[y]) | reinterpret_cast<uintptr_t>(outs[y])) & 15)
+      throw std::invalid_argument("SdmaComm: buffers must be 16-byte aligned");
+  }
+  if (n <= 0) return;
+  hip_check(hipSetDevice(c0.device_), "hipSetDevice");
+  const int64_t es = static_cast<int64_t>(dtype_size(dt));
+  const int64_t seg = c0.world_ * (c0.slot_bytes_ / es);
+  std::vector<Plan> plans(comms.size());
+  for (int64_t off = 0; off < n; off += seg) {
+    const int64_t len = std::min(seg, n - off);
+    for (size_t y = 0; y < comms.size(); ++y)
+      plans[y] = comms[y]->plan(static_cast<const char*>(ins[y]) + off * es, static_cast<char*>(outs[y]) + off * es,
+                                len, dt);
+    hip_check(hipEventRecord(c0.impl_->sysrel, stream), "hipEventRecord(release to system)");
+    for (size_t y = 0; y < comms.size(); ++y)
+      hipLaunchKernelGGL(sdma_release_kernel, dim3(1), dim3(64), 0, stream,
+                         comms[y]->impl_->slots[plans[y].slot].start_p);
+    for (size_t y = 0; y < comms.size(); ++y) comms[y]->enqueue_reduce(plans[y], stream, scale);
+    for (size_t y = 0; y < comms.size(); ++y) comms[y]->enqueue_gather(plans[y], stream);
+    hip_check(hipGetLastError(), "sdma kernels");
+  }
+}
+
+SdmaComm::Plan SdmaComm::plan(const char* in, char* out, int64_t n, DType dt) {
   Impl& m = *impl_;
   const int W = world_, r = rank_;
   const int64_t es = static_cast<int64_t>(dtype_size(dt));
   const int64_t elems = 16 / es;
+  Plan pl;
+  pl.in = in;
+  pl.out = out;
+  pl.n = n;
+  pl.dt = dt;
   const uint64_t e64 = ++epoch_;
-  const uint32_t e = static_cast<uint32_t>(e64);
-  const int par = static_cast<int>(e64 & 1u);
-  Impl::Slot& sl = m.slots[e64 % kSlots];
+  pl.epoch = static_cast<uint32_t>(e64);
+  pl.par = static_cast<int>(e64 & 1u);
+  pl.slot = static_cast<int>(e64 % kSlots);
+  Impl::Slot& sl = m.slots[pl.slot];
   // the slot's previous call: every copy it submitted has completed (the host is at most
   // kSlots calls ahead of the engines; a peer that stopped turns into an error here)
   if (sl.used) {
@@ -327,7 +445,8 @@ void SdmaComm::segment(const char* in, char* out, int64_t n, DType dt, hipStream
     }
   }
   sl.used = true;
-  const int64_t block = rup(cdiv(n, W), elems);
+  pl.block = rup(cdiv(n, W), elems);
+  const int64_t block = pl.block;
   auto blen = [&](int j) { return hclamp(n - static_cast<int64_t>(j) * block, block); };
   if (block * es > slot_bytes_) throw std::logic_error("SdmaComm: segment exceeds the slot");
   // split of one block over epp engines, 4 KiB aligned pieces
@@ -347,7 +466,8 @@ void SdmaComm::segment(const char* in, char* out, int64_t n, DType dt, hipStream
       n2 += l > 0;
     }
   }
-  m.words[(e64 % kSlots) * 16] = e;
+  uint32_t* word = m.words + static_cast<int64_t>(pl.slot) * 16;
+  *word = pl.epoch;
   std::atomic_thread_fence(std::memory_order_seq_cst);
   hsa_signal_store_relaxed(sl.start, 1);
   hsa_signal_store_relaxed(sl.mid, 1);
@@ -355,7 +475,6 @@ void SdmaComm::segment(const char* in, char* out, int64_t n, DType dt, hipStream
   hsa_signal_store_relaxed(sl.scf, W - 1);
   hsa_signal_store_relaxed(sl.gd, n2);
   hsa_signal_store_relaxed(sl.gdf, W - 1);
-  uint32_t* word = m.words + (e64 % kSlots) * 16;
   const int64_t off_SD = kFlagBytes, off_RD = kFlagBytes + 2 * static_cast<int64_t>(W) * slot_bytes_;
   auto copy = [&](void* dst, hsa_agent_t da, const void* src, hsa_agent_t sa, int64_t bytes, int ndep,
                   const hsa_signal_t* deps, hsa_signal_t done, hsa_amd_sdma_engine_id_t eng) {
@@ -365,6 +484,7 @@ void SdmaComm::segment(const char* in, char* out, int64_t n, DType dt, hipStream
     ++st_.copies;
     st_.bytes += static_cast<uint64_t>(bytes);
   };
+  const int par = pl.par;
   // phase 1: block j -> rank j's SD[par][r], then its FS[r] flag
   for (int j = 0; j < W; ++j) {
     if (j == r) continue;
@@ -378,8 +498,7 @@ void SdmaComm::segment(const char* in, char* out, int64_t n, DType dt, hipStream
   }
   const hsa_signal_t dep1[2] = {sl.start, sl.sc};
   for (int j = 0; j < W; ++j)
-    if (j != r)
-      copy(peers_[j] + r * 4, m.peer_agent[j], word, m.cpu, 4, 2, dep1, sl.scf, m.peer_engines[j][0]);
+    if (j != r) copy(peers_[j] + r * 4, m.peer_agent[j], word, m.cpu, 4, 2, dep1, sl.scf, m.peer_engines[j][0]);
   // phase 2: the reduced own block -> every peer's RD[par][r], then its FR[r] flag
   for (int k = 0; k < W; ++k) {
     if (k == r) continue;
@@ -395,37 +514,50 @@ void SdmaComm::segment(const char* in, char* out, int64_t n, DType dt, hipStream
   for (int k = 0; k < W; ++k)
     if (k != r)
       copy(peers_[k] + (kFrWord + r) * 4, m.peer_agent[k], word, m.cpu, 4, 2, dep2, sl.gdf, m.peer_engines[k][0]);
+  ++st_.calls;
+  return pl;
+}
 
-  // the stream: release phase 1 once the input is in memory, wait, reduce, release phase 2,
-  // wait, gather
+// wait for every peer's phase-1 flag, reduce the own block, release phase 2
+void SdmaComm::enqueue_reduce(const Plan& pl, hipStream_t stream, float scale) {
+  const int W = world_, r = rank_;
+  const int64_t es = static_cast<int64_t>(dtype_size(pl.dt));
+  const int64_t elems = 16 / es;
   const uint64_t ticks = static_cast<uint64_t>(timeout_s_ * 1e8);
-  hip_check(hipEventRecord(m.sysrel, stream), "hipEventRecord(release to system)");
-  hipLaunchKernelGGL(sdma_release_kernel, dim3(1), dim3(64), 0, stream, sl.start_p);
-  hipLaunchKernelGGL(sdma_wait_kernel, dim3(1), dim3(64), 0, stream, reinterpret_cast<const uint32_t*>(slab_), W, r, e,
-                     ticks, err_);
-  const int64_t rl = blen(r);
+  hipLaunchKernelGGL(sdma_wait_kernel, dim3(1), dim3(64), 0, stream, reinterpret_cast<const uint32_t*>(slab_), W, r,
+                     pl.epoch, ticks, err_);
+  const int64_t rl = hclamp(pl.n - static_cast<int64_t>(r) * pl.block, pl.block);
   const int64_t piece = std::max<int64_t>(elems, rup(cdiv(rl, grid_), elems));
   const int g1 = static_cast<int>(std::max<int64_t>(1, cdiv(rl, piece)));
-  const char* sd = slab_ + off_SD + static_cast<int64_t>(par) * W * slot_bytes_;
-  dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
-    using E = decltype(tag);
-    hipLaunchKernelGGL(sdma_reduce_kernel<E>, dim3(g1), dim3(kCommThreads), 0, stream,
-                       in + static_cast<int64_t>(r) * block * es, sd, slot_bytes_, W, r,
-                       out + static_cast<int64_t>(r) * block * es, rl, piece, scale);
-  });
-  hipLaunchKernelGGL(sdma_release_kernel, dim3(1), dim3(64), 0, stream, sl.mid_p);
+  const char* sd = slab_ + kFlagBytes + static_cast<int64_t>(pl.par) * W * slot_bytes_;
+  if (rl > 0)
+    dispatch_dtype(static_cast<int>(pl.dt), [&](auto tag) {
+      using E = decltype(tag);
+      hipLaunchKernelGGL(sdma_reduce_kernel<E>, dim3(g1), dim3(kCommThreads), 0, stream,
+                         pl.in + static_cast<int64_t>(r) * pl.block * es, sd, slot_bytes_, W, r,
+                         pl.out + static_cast<int64_t>(r) * pl.block * es, rl, piece, scale);
+    });
+  hipLaunchKernelGGL(sdma_release_kernel, dim3(1), dim3(64), 0, stream, impl_->slots[pl.slot].mid_p);
+}
+
+// wait for every peer's reduced block, copy them into the output
+void SdmaComm::enqueue_gather(const Plan& pl, hipStream_t stream) {
+  const int W = world_, r = rank_;
+  const int64_t es = static_cast<int64_t>(dtype_size(pl.dt));
+  const int64_t elems = 16 / es;
+  const uint64_t ticks = static_cast<uint64_t>(timeout_s_ * 1e8);
   hipLaunchKernelGGL(sdma_wait_kernel, dim3(1), dim3(64), 0, stream,
-                     reinterpret_cast<const uint32_t*>(slab_) + kFrWord, W, r, e, ticks, err_);
-  const int64_t gpiece = std::max<int64_t>(elems, rup(cdiv(block, std::max(1, grid_ / std::max(1, W - 1))), elems));
-  const int g2 = static_cast<int>(std::max<int64_t>(1, cdiv(block, gpiece)));
-  const char* rd = slab_ + off_RD + static_cast<int64_t>(par) * W * slot_bytes_;
-  dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
+                     reinterpret_cast<const uint32_t*>(slab_) + kFrWord, W, r, pl.epoch, ticks, err_);
+  if (W < 2) return;
+  const int64_t gpiece = std::max<int64_t>(elems, rup(cdiv(pl.block, std::max(1, grid_ / (W - 1))), elems));
+  const int g2 = static_cast<int>(std::max<int64_t>(1, cdiv(pl.block, gpiece)));
+  const char* rd = slab_ + kFlagBytes + 2 * static_cast<int64_t>(W) * slot_bytes_ +
+                   static_cast<int64_t>(pl.par) * W * slot_bytes_;
+  dispatch_dtype(static_cast<int>(pl.dt), [&](auto tag) {
     using E = decltype(tag);
-    hipLaunchKernelGGL(sdma_gather_kernel<E>, dim3(g2, W), dim3(kCommThreads), 0, stream, out, rd, slot_bytes_, r, n,
-                       block, gpiece);
+    hipLaunchKernelGGL(sdma_gather_kernel<E>, dim3(g2, W), dim3(kCommThreads), 0, stream, pl.out, rd, slot_bytes_, r,
+                       pl.n, pl.block, gpiece);
   });
-  hip_check(hipGetLastError(), "sdma kernels");
-  ++st_.calls;
 }
 
 }  // namespace mxar
