@@ -157,6 +157,19 @@ class XgmiCommunicator:
         self._dev = self.device.index
         self._launch: dict[str, tuple] = {}  # algo label -> (native Algo, grid)
         self._p2p = None
+        self._sdma = None
+
+    @property
+    def sdma(self):
+        """The same ranks' SDMA allreduce (parallel/sdma.py: cross-rank copies on the copy
+        engines), created on first use - collectively: every rank must reach it together
+        (BucketedGradReducer.tune_schedule does)."""
+        if self._sdma is None:
+            from .sdma import SdmaCommunicator
+
+            self._sdma = SdmaCommunicator(self.group, device=self.device, slot_bytes=self.slot_bytes,
+                                          cpu_group=self.cpu_group)
+        return self._sdma
 
     @property
     def p2p(self):
@@ -291,6 +304,8 @@ class XgmiCommunicator:
             self._c.allreduce(inp.data_ptr(), out.data_ptr(), inp.numel(), code,
                               _current_stream(self._dev) if stream is None else stream, kind,
                               1.0 / self.world if op == "avg" else 1.0)
+        elif algo == "sdma":  # copy-engine transfers (parallel/sdma.py); the mean fused into its reduce
+            return self.sdma.allreduce(inp, out, op=op, stream=stream)
         elif algo == "threshold" and self._threshold_fits(inp):
             # the straggler-tolerant kernel at th = 1 is an exact allreduce with its own
             # geometry (one chunk per workgroup, round-robin gather); a tune() candidate

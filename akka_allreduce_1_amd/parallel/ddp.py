@@ -308,6 +308,14 @@ class BucketedGradReducer:
         xgmi = bool(getattr(self.comm, "accepts_stream", False))
         base = self.schedule[1] if self.schedule else self.algo
         default = [(True, base), (True, "twoshot@128"), (False, base)] if xgmi else [(True, base), (False, base)]
+        if xgmi and getattr(self.comm, "world", 1) > 1 and hasattr(self.comm, "sdma") and candidates is None:
+            # the copy-engine allreduce leaves the CUs to backward's GEMMs; created here, on
+            # every rank at the same step (its construction is collective)
+            try:
+                self.comm.sdma
+                default.append((True, "sdma"))
+            except Exception:  # noqa: BLE001 - no SDMA engines: the CU schedules only
+                pass
         self._cands = list(candidates or default)
         self._tune_steps = max(1, int(tune_steps))
         self._times: list[list[float]] = [[] for _ in self._cands]

@@ -461,6 +461,14 @@ def dp_step(comm: XgmiCommunicator, model: str, dev) -> dict:
                 for _ in range(warm):
                     overlap()
                 t["step_g128"] = max_over_ranks(timed(overlap, steps, dev), dev) / steps * 1e3
+                # the copy-engine allreduce (parallel/sdma.py): xGMI transfers off the CUs
+                try:
+                    reducer.algo = "sdma"
+                    for _ in range(warm):
+                        overlap()
+                    t["step_sdma"] = max_over_ranks(timed(overlap, steps, dev), dev) / steps * 1e3
+                except Exception as e:  # noqa: BLE001 - recorded, the other schedules still run
+                    t["sdma_error"] = repr(e)
                 reducer.algo = "auto"
                 # every bucket after backward (no overlap)
                 reducer.overlap = False
@@ -488,6 +496,10 @@ def dp_step(comm: XgmiCommunicator, model: str, dev) -> dict:
         else:  # an average over one rank is the identity: no kernel runs, nothing to rate
             row["note"] = ("world=1: the allreduce is the identity (no launch), so exposed_comm_ms is the "
                            "reducer's host overhead; comm-only time / bandwidth are not measured")
+        if "step_sdma" in t:
+            row["step_ms_sdma"] = round(t["step_sdma"], 3)
+        if "sdma_error" in t:
+            row["sdma_error"] = t["sdma_error"][:200]
         if "step_g128" in t:
             row["step_ms_twoshot_128wg"] = round(t["step_g128"], 3)
             row["step_ms_serial"] = round(t["step_serial"], 3)

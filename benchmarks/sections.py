@@ -394,6 +394,31 @@ def native_deployment(cases=((10, 2, 400), (262144, 1024, 400), (16777216, 32768
     return res
 
 
+class PairSdmaRehearsalComm:
+    """PairRehearsalComm with the SDMA allreduce (parallel/sdma.py): the two logical ranks'
+    cross-rank copies run on copy engines, only the small-grid reduce and gather on CUs. It
+    shares the CU pair's synthetic peer gradients."""
+
+    accepts_stream = True
+    world = 2
+
+    def __init__(self, buckets, peer: dict, grid: int = 32):
+        from akka_allreduce_1_amd.parallel import LocalSdmaCluster
+
+        big = max(b.nbytes for b in buckets)
+        self.cl = LocalSdmaCluster(2, slot_bytes=-(-big // 2) + (1 << 20), grid=grid, engines_per_peer=2,
+                                   timeout_s=20.0)
+        self.peer = peer
+
+    def allreduce_(self, t: torch.Tensor, *, op: str = "sum", algo: str = "auto", stream: int | None = None):
+        x1, y1 = self.peer[t.data_ptr()]
+        self.cl.allreduce([t, x1], [t, y1], op=op, stream=stream)
+        return t
+
+    def check(self):
+        self.cl.check()
+
+
 class PairRehearsalComm:
     """A 2-rank data-parallel communicator on ONE GPU for overlap rehearsals: every bucket
     allreduce runs the real 2-rank kernel (LocalCluster, both ranks in one launch) over the
@@ -482,6 +507,14 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
             # every bucket after backward (no overlap), and the overlap on a normal-priority
             # comm stream (the GEMMs' dispatches are not pre-empted by the comm queue)
             variants += [("serial_grid512", 512, False, True, 1024), ("grid128_normal_prio", 128, True, False, 1024)]
+            # the copy-engine allreduce: cross-rank copies on SDMA engines, reduce / gather on
+            # a small grid (the comm's CU footprint)
+            cu_comm, sdma_comm = comm, None
+            try:
+                sdma_comm = PairSdmaRehearsalComm(reducer.buckets, comm.peer)
+                variants += [("sdma_grid16", 16, True, True, 1024), ("sdma_grid64", 64, True, True, 1024)]
+            except Exception as e:  # noqa: BLE001 - no SDMA engines here: CU variants only
+                row["sdma_error"] = repr(e)
             if big:
                 # 1024 tokens make the weight-gradient GEMMs (K = tokens) nearly bandwidth bound,
                 # so a bandwidth-bound allreduce beside them slows them; at a training-size
@@ -497,6 +530,8 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                     if tokens not in bwds:
                         bwds[tokens] = SyntheticBackward(params, tokens, torch.bfloat16, dev)
                     bwd = bwds[tokens]
+                    comm = sdma_comm if name.startswith("sdma") else cu_comm
+                    reducer.comm = comm
                     for c in comm.cl.comms:
                         c.grid = grid
                     reducer.overlap = ov
@@ -534,14 +569,19 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                     cell["error"] = repr(e)
                 row[name] = cell
             reducer.overlap, reducer.stream, reducer._comm_raw = True, hi_stream, hi_raw
-            ok = {g: c for g, c in row.items() if "step_ms" in c}
+            comm = cu_comm
+            ok = {g: c for g, c in row.items() if isinstance(c, dict) and "step_ms" in c}
             if ok:
                 row["best"] = min(ok, key=lambda g: ok[g]["step_ms"])
+            sd = {g: c for g, c in ok.items() if g.startswith("sdma")}
+            if sd:  # the copy-engine candidate's best cell, next to the CU grids'
+                row["sdma"] = dict(sd[min(sd, key=lambda g: sd[g]["step_ms"])], variant=min(sd, key=lambda g: sd[g]["step_ms"]))
             row["buckets"] = f"{len(reducer.buckets)} ({'64 MiB first, 1 GiB after' if big else '25 MiB'})"
         except Exception as e:  # noqa: BLE001
             row["error"] = repr(e)
         finally:
             del params, bwd, reducer, comm
+            cu_comm = sdma_comm = None
             bwds = None
             torch.cuda.empty_cache()
         out[model] = row

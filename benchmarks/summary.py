@@ -117,6 +117,8 @@ def _dp(dp: dict) -> tuple[dict, dict]:
                 out[m] = [r["step_ms"], r.get("compute_ms"), r.get("exposed_comm_ms")]
                 if "step_ms_auto_schedule" in r:
                     out[m].append(r["step_ms_auto_schedule"])
+                if "step_ms_sdma" in r:
+                    out[m].append({"sdma": r["step_ms_sdma"]})
             elif "error" in r:
                 out[m] = str(r["error"])[:120]
     o = dp.get("overlap_rehearsal") or {}
