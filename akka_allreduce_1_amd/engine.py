@@ -61,10 +61,11 @@ class PlaneJob:
     """Master + P plane workers in one process (threaded actor system).
 
     Workers sharing a GPU run their round kernels concurrently on separate high-priority
-    streams; HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by
+    streams. HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by
     default), and a kernel queued behind a peer's spinning round kernel in the same queue
-    never starts. Set GPU_MAX_HW_QUEUES >= 2 * (workers per GPU) + 4 before HIP initialises
-    (bench.py and tools/plane_probe.py do) when several workers share one GPU."""
+    would never start: each plane therefore probes its stream against the other planes'
+    and the default stream when it is created and takes one on a queue of its own
+    (csrc/hip/xgmi_plane.cc, independent_plane_stream) - no environment setting needed."""
 
     def __init__(self, P: int, data_size: int, *, max_chunk_size: int, th_allreduce: float = 1.0,
                  th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 1, max_round: int = 10,
@@ -107,12 +108,6 @@ class PlaneJob:
             share = max(self.devices.count(d) for d in set(self.devices))
             if grid <= 0:  # workers sharing a GPU split its workgroups so every kernel stays resident
                 grid = max(8, 512 // share)
-            queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
-            if share > 1 and queues < 2 * share + 4:
-                warnings.warn(f"{share} plane workers share a GPU in this process with GPU_MAX_HW_QUEUES={queues}: "
-                              f"a round kernel queued behind a peer's in a shared hardware queue waits out its "
-                              f"deadline; set GPU_MAX_HW_QUEUES >= {2 * share + 4} before HIP initialises",
-                              RuntimeWarning, stacklevel=2)
         self.grid = grid
         self.system = C.ActorSystem("ClusterSystem", False)
         self.finished = threading.Event()

@@ -51,12 +51,8 @@ if "--share-device" in sys.argv:
     # co-resident (measured: 46.7 ms vs 3.1 ms per 256 MiB step at 8 ranks). One queue per
     # process keeps every rank's kernel on the device at once. Set before HIP initialises.
     os.environ["GPU_MAX_HW_QUEUES"] = "1"
-else:
-    # The N = 1 protocol section hosts two plane workers in this process; with RCCL's and
-    # torch's streams, 4 hardware queues (HIP's default) make streams share queues, and work
-    # queued behind a spinning round kernel in a shared queue stalls until its timeout.
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:  # raise, never lower (GPU boxes export 4)
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# (The N = 1 protocol section hosts two plane workers in this process: each plane probes its
+# stream onto a hardware queue of its own, csrc/hip/xgmi_plane.cc - no queue-count setting.)
 
 # Library banners (RCCL's version block, gloo's "connected to N peer ranks") are written to
 # fd 1 from native code; keep stdout for the ONE result line: fd 1 -> stderr for the whole

@@ -452,4 +452,39 @@ void launch_bucket_copy(const uint64_t* dev_table, int count, void* bucket, DTyp
   hip_check(hipGetLastError(), "bucket_copy launch");
 }
 
+// ---------------------------------------------------------------------------------
+// Hardware-queue independence probe. HIP deals a process's streams onto a few hardware
+// queues (GPU_MAX_HW_QUEUES, 4 on the boxes); two streams on one queue run their kernels in
+// order. A persistent round kernel that spins waiting for a co-located peer's kernel must
+// not share a queue with it. The probe: a spinning kernel on `a` waits (bounded) for a flag
+// a kernel on `b` sets - it only returns "seen" when b's kernel could run while a's spun.
+// ---------------------------------------------------------------------------------
+__global__ void queue_probe_spin(int* flag, int* seen, uint64_t ticks) {
+  if (threadIdx.x != 0) return;
+  const uint64_t deadline = __builtin_amdgcn_s_memrealtime() + ticks;
+  int v = 0;
+  while ((v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) == 0 &&
+         __builtin_amdgcn_s_memrealtime() < deadline)
+    __builtin_amdgcn_s_sleep(4);
+  __hip_atomic_store(seen, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void queue_probe_set(int* flag) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+bool streams_independent(hipStream_t a, hipStream_t b, double timeout_ms) {
+  int* mem = nullptr;
+  hip_check(hipMalloc(reinterpret_cast<void**>(&mem), 64), "hipMalloc(queue probe)");
+  hip_check(hipMemset(mem, 0, 64), "hipMemset(queue probe)");
+  hipLaunchKernelGGL(queue_probe_spin, dim3(1), dim3(64), 0, a, mem, mem + 16,
+                     static_cast<uint64_t>(timeout_ms * 1e5));  // s_memrealtime: 100 MHz
+  hipLaunchKernelGGL(queue_probe_set, dim3(1), dim3(64), 0, b, mem);
+  hip_check(hipStreamSynchronize(a), "hipStreamSynchronize(queue probe)");
+  hip_check(hipStreamSynchronize(b), "hipStreamSynchronize(queue probe)");
+  int seen = 0;
+  hip_check(hipMemcpy(&seen, mem + 16, 4, hipMemcpyDeviceToHost), "hipMemcpy(queue probe)");
+  hip_check(hipFree(mem), "hipFree(queue probe)");
+  return seen != 0;
+}
+
 }  // namespace mxar

@@ -346,6 +346,9 @@ void launch_clock_probe(uint64_t* out, int samples, uint64_t interval_ticks, hip
 void launch_fill_uniform(void* dst, int64_t n, uint64_t seed, DType dt, hipStream_t stream);
 // dst[0:bytes) = src[0:bytes) as a kernel (16-B aligned)
 void launch_copy(const void* src, void* dst, int64_t bytes, hipStream_t stream);
+// true when a kernel on `b` runs while a kernel on `a` spins (the streams sit on different
+// hardware queues); kernels.hip
+bool streams_independent(hipStream_t a, hipStream_t b, double timeout_ms = 50.0);
 void set_copy_variant(int v);  // study knob: 0..3, -1 default
 void set_reduce_variant(int v);  // study knob: 0 runtime-P loop, 1..4 static-P (U, NT), -1 default
 // dst (dt_out) = src (dt_in), n elements

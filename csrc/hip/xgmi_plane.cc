@@ -25,6 +25,57 @@ namespace {
 // Arenas of this process by id: a worker cannot open its own process's IPC handles, so
 // in-process peers (several workers of one process on one GPU) are found here.
 std::mutex g_arena_mu;
+
+// The process's live plane streams per device. A new plane's stream must sit on a hardware
+// queue of its own: co-located planes' round kernels spin waiting for each other, and a
+// kernel queued behind a peer's spinning kernel in a shared queue waits out its deadline.
+// HIP deals streams onto GPU_MAX_HW_QUEUES queues (4 on the boxes) round-robin, so the
+// candidate is probed against every live plane stream and the legacy default stream
+// (streams_independent, kernels.hip) and replaced until one is independent of all of them.
+std::mutex g_stream_mu;
+std::vector<std::pair<int, hipStream_t>> g_plane_streams;
+
+hipStream_t independent_plane_stream(int device, int priority, bool* probed_ok) {
+  std::lock_guard<std::mutex> g(g_stream_mu);
+  if (const char* q = std::getenv("GPU_MAX_HW_QUEUES"); q != nullptr && std::atoi(q) == 1) {
+    // one queue per process (the multi-process one-GPU rehearsal, one plane per process):
+    // nothing to choose from
+    hipStream_t s = nullptr;
+    hip_check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority), "hipStreamCreate(plane)");
+    g_plane_streams.emplace_back(device, s);
+    *probed_ok = false;
+    return s;
+  }
+  std::vector<hipStream_t> rejected;  // kept alive while probing: HIP would deal the same queue again
+  hipStream_t s = nullptr;
+  bool ok = false;
+  for (int attempt = 0; attempt < 16 && !ok; ++attempt) {
+    hip_check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority), "hipStreamCreate(plane)");
+    ok = streams_independent(s, nullptr);
+    for (const auto& e : g_plane_streams)
+      if (ok && e.first == device) ok = streams_independent(e.second, s) && streams_independent(s, e.second);
+    if (!ok) rejected.push_back(s);
+  }
+  for (hipStream_t r : rejected)
+    if (r != s || !ok) (void)hipStreamDestroy(r);
+  if (!ok) {  // no independent queue left: keep the last candidate, say so
+    hip_check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority), "hipStreamCreate(plane)");
+    std::fprintf(stderr,
+                 "[mxar] WARNING: no hardware queue independent of the other plane streams on device %d; "
+                 "co-located round kernels may wait out their deadline (raise GPU_MAX_HW_QUEUES)\n",
+                 device);
+  }
+  g_plane_streams.emplace_back(device, s);
+  *probed_ok = ok;
+  return s;
+}
+
+void forget_plane_stream(hipStream_t s) {
+  std::lock_guard<std::mutex> g(g_stream_mu);
+  g_plane_streams.erase(std::remove_if(g_plane_streams.begin(), g_plane_streams.end(),
+                                       [&](const std::pair<int, hipStream_t>& e) { return e.second == s; }),
+                        g_plane_streams.end());
+}
 std::map<uint64_t, char*> g_arenas;
 
 std::string to_hex(const std::string& b) {
@@ -156,8 +207,8 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
   // Many planes in one process (workers sharing a GPU) may instead want normal priority:
   // normal-priority streams are dealt round-robin over GPU_MAX_HW_QUEUES queues.
-  hip_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, o_.high_priority ? hi : lo),
-            "hipStreamCreate(plane)");
+  bool independent = false;
+  stream_ = independent_plane_stream(o_.device, o_.high_priority ? hi : lo, &independent);
   // keep freed round buffers in the device's default pool instead of returning them to the
   // driver at every synchronisation (the next round reuses them)
   hipMemPool_t mp = nullptr;
@@ -221,7 +272,10 @@ XgmiRoundPlane::~XgmiRoundPlane() {
   if (ctl_mem_) (void)hipFree(ctl_mem_);
   if (split_mem_) (void)hipFree(split_mem_);
   if (hforce_) (void)hipHostFree(hforce_);
-  if (stream_) (void)hipStreamDestroy(stream_);
+  if (stream_) {
+    forget_plane_stream(stream_);
+    (void)hipStreamDestroy(stream_);
+  }
   if (arena_) (void)hipFree(arena_);
 }
 
