@@ -308,7 +308,8 @@ class BucketedGradReducer:
         xgmi = bool(getattr(self.comm, "accepts_stream", False))
         base = self.schedule[1] if self.schedule else self.algo
         default = [(True, base), (True, "twoshot@128"), (False, base)] if xgmi else [(True, base), (False, base)]
-        if xgmi and getattr(self.comm, "world", 1) > 1 and hasattr(self.comm, "sdma") and candidates is None:
+        if xgmi and getattr(self.comm, "world", 1) > 1 and getattr(type(self.comm), "sdma", None) is not None \
+                and candidates is None:
             # the copy-engine allreduce leaves the CUs to backward's GEMMs; created here, on
             # every rank at the same step (its construction is collective)
             try:
