@@ -474,8 +474,8 @@ __global__ void queue_probe_set(int* flag) {
 
 bool streams_independent(hipStream_t a, hipStream_t b, double timeout_ms) {
   int* mem = nullptr;
-  hip_check(hipMalloc(reinterpret_cast<void**>(&mem), 64), "hipMalloc(queue probe)");
-  hip_check(hipMemset(mem, 0, 64), "hipMemset(queue probe)");
+  hip_check(hipMalloc(reinterpret_cast<void**>(&mem), 128), "hipMalloc(queue probe)");
+  hip_check(hipMemset(mem, 0, 128), "hipMemset(queue probe)");
   hipLaunchKernelGGL(queue_probe_spin, dim3(1), dim3(64), 0, a, mem, mem + 16,
                      static_cast<uint64_t>(timeout_ms * 1e5));  // s_memrealtime: 100 MHz
   hipLaunchKernelGGL(queue_probe_set, dim3(1), dim3(64), 0, b, mem);
