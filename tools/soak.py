@@ -41,7 +41,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from akka_allreduce_1_amd.ops import fill_uniform  # noqa: E402
 from akka_allreduce_1_amd.parallel.comm import CommError, XgmiCommunicator, init_distributed  # noqa: E402
 
-OPS = ["ll", "oneshot", "twoshot", "ring", "threshold", "auto", "all_gather", "reduce_scatter", "all_to_all"]
+OPS = ["ll", "oneshot", "twoshot", "ring", "ring_native", "threshold", "auto", "all_gather", "reduce_scatter",
+       "all_to_all"]
 DTYPES = {"fp32": (torch.float32, 1e-5), "bf16": (torch.bfloat16, 2.0 ** -7), "fp16": (torch.float16, 2.0 ** -10)}
 
 
@@ -111,10 +112,11 @@ def main() -> None:
                     out = comm.allreduce_threshold(x, x if inplace else None).float()
                 else:
                     out = comm.allreduce(x, x if inplace else None, op="sum", algo=op).float()
-                # the ring (and `auto`, which may pick it) rounds the partial sum to the wire dtype at
-                # each of its P-2 intermediate hops: each rounding <= rtol/2 * sum_k |x_k|
+                # the element-type-wire ring rounds the partial sum to the wire dtype at each of its
+                # P-2 intermediate hops: each rounding <= rtol/2 * sum_k |x_k| (the exact-wire ring and
+                # `auto` keep the bound too, as they did when the ring's partials were element-typed)
                 tol = 1e-4 * world + rtol * ref.abs()
-                if op in ("ring", "auto"):
+                if op in ("ring", "ring_native", "auto"):
                     tol = tol + 0.5 * rtol * max(world - 2, 0) * torch.stack([xk.float().abs() for xk in xs]).sum(0)
                 err = (out - ref).abs()
                 ok = bool((err <= tol).all())
