@@ -157,13 +157,19 @@ def _slot_reuse_worker(rank, world, port, results, slow=1, seq="mixed", env=None
     with the round-3 flag layout (row = hop) such a late ring flag overwrote a newer
     all-gather flag of another writer (profiles/round3/soak8_run4_ring_flag_collision.log)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0", **(env or {}))
+    import datetime
+
     import torch.distributed as dist
 
     from akka_allreduce_1_amd.parallel import XgmiCommunicator
 
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     ok, msg = True, ""
+    try:  # a lost rendezvous (the port taken meanwhile) must fail fast, not hang the parent
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    except Exception as e:  # noqa: BLE001
+        results.put((rank, False, f"rendezvous: {e!r}"))
+        return
     try:
         comm = XgmiCommunicator(device=0, slot_bytes=1 << 20, grid=8, timeout_s=5.0)
         comm.native.set_read_delay(slow, 2000.0)
@@ -202,11 +208,14 @@ def _run_slow_reader(world, slow, seq, env=None):
     procs = [ctx.Process(target=_slot_reuse_worker, args=(r, world, port, q, slow, seq, env)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=240) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-        if p.is_alive():
-            p.kill()
+    res = []
+    try:
+        res = [q.get(timeout=150) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
     return [r for r in res if not r[1]]
 
 

@@ -37,6 +37,7 @@ def main() -> None:
     for name, env, world, slow, seq in cases:
         if only and name not in only:
             continue
+        print(f"[negative_controls] {name} world={world} ...", file=sys.stderr, flush=True)
         bad = _run_slow_reader(world, slow, seq, env)
         print(json.dumps({"case": name, "env": env, "world": world, "slow_rank": slow, "seq": seq,
                           "failed_ranks": len(bad), "first_failure": bad[0][2][:300] if bad else None}), flush=True)
