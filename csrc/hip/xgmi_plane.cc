@@ -30,8 +30,9 @@ std::mutex g_arena_mu;
 // queue of its own: co-located planes' round kernels spin waiting for each other, and a
 // kernel queued behind a peer's spinning kernel in a shared queue waits out its deadline.
 // HIP deals streams onto GPU_MAX_HW_QUEUES queues (4 on the boxes) round-robin, so the
-// candidate is probed against every live plane stream and the legacy default stream
-// (streams_independent, kernels.hip) and replaced until one is independent of all of them.
+// candidate is probed against every idle live plane stream (streams_independent,
+// kernels.hip) and replaced until one is independent of all of them; the high priority
+// keeps plane streams off the default stream's queue.
 std::mutex g_stream_mu;
 std::vector<std::pair<int, hipStream_t>> g_plane_streams;
 
@@ -51,9 +52,13 @@ hipStream_t independent_plane_stream(int device, int priority, bool* probed_ok) 
   bool ok = false;
   for (int attempt = 0; attempt < 16 && !ok; ++attempt) {
     hip_check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority), "hipStreamCreate(plane)");
-    ok = streams_independent(s, nullptr);
+    // Only IDLE plane streams are probed: a busy one may hold a round kernel that waits for
+    // this very worker (a replacement joining a running job), and a probe queued behind it
+    // would wait out that round's deadline.
+    ok = true;
     for (const auto& e : g_plane_streams)
-      if (ok && e.first == device) ok = streams_independent(e.second, s) && streams_independent(s, e.second);
+      if (ok && e.first == device && hipStreamQuery(e.second) == hipSuccess)
+        ok = streams_independent(e.second, s) && streams_independent(s, e.second);
     if (!ok) rejected.push_back(s);
   }
   for (hipStream_t r : rejected)

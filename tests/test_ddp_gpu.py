@@ -56,7 +56,8 @@ def _worker(rank, world, port, q, dtype, mode):
                 assert err <= tol, (step, i, err, tol)
         if mode == "auto":
             assert red.schedule is not None and "schedule" in red.stats, red.stats
-            assert len(red.stats["schedule_ms"]) == 3, red.stats
+            # communicator grid, 128 workgroups, serial, and the copy-engine (SDMA) allreduce
+            assert len(red.stats["schedule_ms"]) == 4 and "overlap:sdma" in red.stats["schedule_ms"], red.stats
         q.put((rank, True, ""))
     except Exception:  # noqa: BLE001
         import traceback
