@@ -406,8 +406,7 @@ class PairSdmaRehearsalComm:
         from akka_allreduce_1_amd.parallel import LocalSdmaCluster
 
         big = max(b.nbytes for b in buckets)
-        self.cl = LocalSdmaCluster(2, slot_bytes=-(-big // 2) + (1 << 20), grid=grid, engines_per_peer=2,
-                                   timeout_s=20.0)
+        self.cl = LocalSdmaCluster(2, slot_bytes=-(-big // 2) + (1 << 20), grid=grid, timeout_s=20.0)
         self.peer = peer
 
     def allreduce_(self, t: torch.Tensor, *, op: str = "sum", algo: str = "auto", stream: int | None = None):

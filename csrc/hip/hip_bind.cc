@@ -312,7 +312,7 @@ void bind_hip(py::module_& m) {
   h.def("sdma_diagnose", &sdma_diagnose, py::arg("device") = 0);
   py::class_<SdmaComm>(h, "SdmaComm")
       .def(py::init<int, int, int, int64_t, int, int, double>(), py::arg("rank"), py::arg("world"), py::arg("device"),
-           py::arg("slot_bytes"), py::arg("grid") = 32, py::arg("engines_per_peer") = 2, py::arg("timeout_s") = 20.0)
+           py::arg("slot_bytes"), py::arg("grid") = 32, py::arg("engines_per_peer") = 0, py::arg("timeout_s") = 20.0)
       .def("handle", [](const SdmaComm& c) { return py::bytes(c.handle()); })
       .def("connect", [](SdmaComm& c, const std::vector<py::bytes>& hs) {
         std::vector<std::string> v;
@@ -346,6 +346,7 @@ void bind_hip(py::module_& m) {
       .def("debug_state", &SdmaComm::debug_state)
       .def_property("grid", &SdmaComm::grid, &SdmaComm::set_grid)
       .def_property_readonly("engines", &SdmaComm::engines)
+      .def_property_readonly("engines_per_peer", &SdmaComm::engines_per_peer)
       .def_property_readonly("slot_bytes", &SdmaComm::slot_bytes)
       .def_property_readonly("rank", &SdmaComm::rank)
       .def_property_readonly("world", &SdmaComm::world)

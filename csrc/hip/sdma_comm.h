@@ -42,7 +42,9 @@ class SdmaComm {
  public:
   // slot_bytes: capacity of one SD / RD slot (one block of one peer); calls reduce up to
   // world * slot_bytes bytes (larger tensors are processed in segments).
-  SdmaComm(int rank, int world, int device, int64_t slot_bytes, int grid = 32, int engines_per_peer = 2,
+  // engines_per_peer: SDMA engines one peer's block is split over; 0 = the device's engines
+  // (this rank's share of them with connect_local) spread over the world - 1 peers
+  SdmaComm(int rank, int world, int device, int64_t slot_bytes, int grid = 32, int engines_per_peer = 0,
            double timeout_s = 20.0);
   ~SdmaComm();
   SdmaComm(const SdmaComm&) = delete;
@@ -70,6 +72,7 @@ class SdmaComm {
   int grid() const { return grid_; }
   void set_grid(int g) { grid_ = g > 0 ? g : 1; }
   int engines() const { return static_cast<int>(local_engines_.size()); }
+  int engines_per_peer() const { return epp_; }
   int64_t slot_bytes() const { return slot_bytes_; }
   const SdmaStats& stats() const { return st_; }
 

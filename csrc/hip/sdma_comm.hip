@@ -191,7 +191,7 @@ struct SdmaComm::Impl {
 SdmaComm::SdmaComm(int rank, int world, int device, int64_t slot_bytes, int grid, int engines_per_peer,
                    double timeout_s)
     : rank_(rank), world_(world), device_(device), slot_bytes_(rup(std::max<int64_t>(slot_bytes, 4096), 4096)),
-      grid_(std::max(1, grid)), epp_(std::max(1, engines_per_peer)), timeout_s_(timeout_s),
+      grid_(std::max(1, grid)), epp_(std::max(0, engines_per_peer)), timeout_s_(timeout_s),
       impl_(std::make_unique<Impl>()) {
   if (world < 1 || world > 32 || rank < 0 || rank >= world) throw std::invalid_argument("SdmaComm: bad rank / world");
   hip_check(hipSetDevice(device_), "hipSetDevice");
@@ -293,6 +293,8 @@ void SdmaComm::connect(const std::vector<std::string>& handles) {
   if (static_cast<int>(handles.size()) != world_) throw std::invalid_argument("SdmaComm.connect: one handle per rank");
   impl_->peer_agent.assign(world_, impl_->own);
   impl_->peer_engines.assign(world_, {});
+  if (epp_ == 0)  // auto: the device's engines spread over the peers
+    epp_ = std::max(1, static_cast<int>(local_engines_.size()) / std::max(1, world_ - 1));
   hip_check(hipSetDevice(device_), "hipSetDevice");
   for (int k = 0; k < world_; ++k) {
     if (k == rank_) continue;
@@ -326,6 +328,7 @@ void SdmaComm::connect_local(const std::vector<SdmaComm*>& comms) {
     if (static_cast<int>(i % nloc) == rank_) mine.push_back(local_engines_[i]);
   if (mine.empty()) throw std::runtime_error("SdmaComm.connect_local: fewer SDMA engines than local ranks");
   local_engines_ = mine;
+  if (epp_ == 0) epp_ = std::max(1, static_cast<int>(local_engines_.size()) / std::max(1, world_ - 1));
   impl_->peer_agent.assign(world_, impl_->own);
   impl_->peer_engines.assign(world_, {});
   for (int k = 0; k < world_; ++k) {
