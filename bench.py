@@ -981,6 +981,10 @@ def main() -> None:
             result["latency_vs_size"] = latency_vs_size(dev, dtype, max_bytes=nbytes)
             log(rank, "reduce_kernel: BASELINE config 2 (1 GiB fp32, P = 2 / 4 / 8)")
             result["reduce_kernel"] = reduce_kernel(dev)
+            from benchmarks.sections import sdma_local
+
+            log(rank, "sdma_local: the copy-engine allreduce, 2 / 8 logical ranks")
+            result["sdma_local"] = sdma_local(dev, dtype, nbytes)
     if engine_ok and not args.no_protocol:
         # the reference's master/worker round protocol driving the GPU engine, under the same
         # native watchdog as the dp section: a stuck round never costs the result line

@@ -394,6 +394,45 @@ def native_deployment(cases=((10, 2, 400), (262144, 1024, 400), (16777216, 32768
     return res
 
 
+def sdma_local(dev, dtype: torch.dtype = torch.bfloat16, nbytes: int = 256 << 20, ranks=(2, 8), iters: int = 10) -> dict:
+    """The copy-engine allreduce (parallel/sdma.py) with P logical ranks on this GPU: p50 per
+    call and algbw, validated against fp32 first. All transfers are same-device engine copies
+    here (the engines' xGMI rate is unmeasured on one GPU)."""
+    from akka_allreduce_1_amd.parallel import LocalSdmaCluster
+
+    es = torch.empty(0, dtype=dtype).element_size()
+    n = nbytes // es
+    out: dict = {"bytes_per_rank": nbytes, "dtype": str(dtype).replace("torch.", "")}
+    for P in ranks:
+        row: dict = {}
+        cl = xs = ys = None
+        try:
+            cl = LocalSdmaCluster(P, slot_bytes=-(-nbytes // P) + (1 << 20), grid=32, timeout_s=20.0)
+            xs = [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=900 + k) for k in range(P)]
+            ys = [torch.empty_like(x) for x in xs]
+            ref = torch.zeros(n, device=dev)
+            for x in xs:
+                ref += x.float()
+            cl.allreduce(xs, ys)
+            torch.cuda.synchronize(dev)
+            cl.check()
+            ok, err, _ = rounding_check(ys, ref, dtype, P)
+            del ref
+            row.update(validated=ok, max_abs_err=err, engines_per_peer=cl.comms[0].engines_per_peer,
+                       engines_per_rank=cl.comms[0].engines)
+            ts = device_times(lambda: cl.allreduce(xs, ys), iters, dev)
+            cl.check()
+            p50 = percentile(ts, 50)
+            row.update(p50_ms=round(p50, 4), algbw_GBps=round(nbytes / (p50 / 1e3) / 1e9, 1))
+        except Exception as e:  # noqa: BLE001
+            row["error"] = repr(e)[:300]
+        finally:
+            del cl, xs, ys
+            torch.cuda.empty_cache()
+        out[f"P{P}"] = row
+    return out
+
+
 class PairSdmaRehearsalComm:
     """PairRehearsalComm with the SDMA allreduce (parallel/sdma.py): the two logical ranks'
     cross-rank copies run on copy engines, only the small-grid reduce and gather on CUs. It

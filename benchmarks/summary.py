@@ -30,7 +30,7 @@ HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per
                  "busbw", "engine_ok", "status")
 
 # least important first: dropped in this order if the line is still over budget
-_DROP_ORDER = ("lat_vs_size", "collectives", "sweep", "dp_overlap", "protocol_us", "dp", "reduce_kernel",
+_DROP_ORDER = ("lat_vs_size", "collectives", "sweep", "dp_overlap", "sdma_local", "protocol_us", "dp", "reduce_kernel",
                "validation_failed", "engine_note", "adamw", "local_ranks", "threshold", "rccl")
 
 # library paths: timed next to the kernels as comparison columns, never the headline
@@ -172,6 +172,11 @@ def compact(result: dict, detail_path: str | None = None) -> dict:
         out["reduce_kernel"] = {"copy_TBps": rk.get("copy_roofline_TBps"),
                                 **{P: rk[P].get("frac_copy_roofline") for P in ("P2", "P4", "P8")
                                    if isinstance(rk.get(P), dict)}}
+    sd = result.get("sdma_local")
+    if isinstance(sd, dict):  # copy-engine allreduce, [p50 ms, algbw GB/s] per logical rank count
+        out["sdma_local"] = {P: ([sd[P].get("p50_ms"), sd[P].get("algbw_GBps")] if "p50_ms" in sd[P]
+                                 else str(sd[P].get("error"))[:80])
+                             for P in ("P2", "P8") if isinstance(sd.get(P), dict)}
     if isinstance(result.get("protocol"), dict):
         out["protocol_us"] = _protocol(result["protocol"])
     if isinstance(result.get("dp"), dict):
