@@ -73,6 +73,27 @@ def comm_stream(device) -> "torch.cuda.Stream":
 
 
 def free_port() -> int:
+    """A bindable port BELOW the kernel's ephemeral range. A port the kernel hands out for
+    bind(0) is also what gloo's own pair connections draw from, so a rendezvous on it can
+    lose the port to another job's connection before the store listens (EADDRINUSE)."""
+    import random
+
+    lo = 20000
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            eph = int(f.read().split()[0])
+    except (OSError, ValueError, IndexError):
+        eph = 32768
+    hi = max(lo + 1000, eph - 1)
+    rng = random.Random()
+    for _ in range(64):
+        port = rng.randrange(lo, hi)
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            try:
+                s.bind(("127.0.0.1", port))
+            except OSError:
+                continue
+            return port
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
