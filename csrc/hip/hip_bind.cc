@@ -237,6 +237,9 @@ void bind_hip(py::module_& m) {
       .def_readonly("completed", &XgmiPlaneStats::completed)
       .def_readonly("coarsened", &XgmiPlaneStats::coarsened)
       .def_readonly("pool_grown", &XgmiPlaneStats::pool_grown)
+      .def_readonly("resident_rounds", &XgmiPlaneStats::resident_rounds)
+      .def_readonly("resident_launches", &XgmiPlaneStats::resident_launches)
+      .def_readonly("resident_parks", &XgmiPlaneStats::resident_parks)
       .def_readonly("peer_maps", &XgmiPlaneStats::peer_maps);
   py::class_<XgmiRoundPlane, RoundPlane, std::shared_ptr<XgmiRoundPlane>>(h, "XgmiRoundPlane")
       .def_property_readonly("stats", &XgmiRoundPlane::stats)

@@ -25,6 +25,7 @@
 
 #include <cstdint>
 #include <string>
+#include <memory>
 #include <vector>
 
 namespace mxar {
@@ -58,6 +59,22 @@ constexpr int kMaxRanks = 16;
 constexpr int kThresholdGatherUnits = 4096;
 constexpr int kThresholdSnapChunks = 2048;
 constexpr int kCommThreads = 256;
+
+// Resident rounds (xgmi_threshold.hip threshold_resident_kernel; xgmi_plane.cc): the host
+// posts each round as one 64-B entry of a door ring in pinned host memory, the sequence word
+// written last; a kernel that stays on the GPU between rounds runs them.
+struct ResidentDoor {
+  uint64_t in, out, counts, counts_host, err_out, done_out;  // device-visible addresses
+  uint32_t epoch;
+  int32_t cmd;  // kResRound / kResCold / kResStop
+  uint32_t seq;
+  uint32_t pad;
+};
+constexpr int kResidentDoors = 64;
+enum : int32_t { kResRound = 0, kResCold = 1, kResStop = 2 };
+// host state words the kernel writes: [0] kResRunning / kResExiting / kResExited, [1] the
+// last entry it consumed (its door slot may be reused)
+enum : uint32_t { kResRunning = 0, kResExiting = 1, kResExited = 2 };
 
 struct CommStats {
   uint64_t calls = 0, launches = 0, bytes = 0, oneshot = 0, twoshot = 0, ring = 0, threshold = 0, ll = 0, coll = 0,
@@ -168,6 +185,21 @@ class XgmiComm {
     return static_cast<size_t>(maxch) * (static_cast<size_t>(P + 1) * 12 + static_cast<size_t>(P) * 4);
   }
   int64_t max_chunks() const { return maxch_; }
+  // Resident rounds: round()'s geometry for n elements computed once (plan_resident; grid 0
+  // = the round does not fit a resident kernel: chunks split over workgroups, or more than
+  // `max_grid` workgroups), and a kernel on `stream` that runs the rounds posted to `door`
+  // from entry `seq` on (launch_resident; hstate / dm: the state words above, and 32 device
+  // words of scratch). Per-round operands come from the entries, not from `spec`.
+  struct ResidentPlan {
+    std::shared_ptr<void> args;  // the kernel's CommArgs
+    int grid = 0;
+    DType dt = DType::F32;
+    int64_t n = 0;
+  };
+  ResidentPlan plan_resident(int64_t n, DType dt, float th_reduce, float th_complete, const RoundSpec& spec,
+                             int max_grid) const;
+  void launch_resident(const ResidentPlan& p, const ResidentDoor* door, uint32_t* hstate, uint32_t* dm,
+                       uint32_t seq, uint32_t gen, uint64_t idle_ticks, hipStream_t stream);
   void round(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, float th_reduce, float th_complete,
              int32_t* counts, const RoundSpec& spec, float scale = 1.f);
   // Workgroups a round launch of `nch` chunks per block uses (counts / geometry checks).
@@ -288,6 +320,10 @@ class XgmiComm {
 
   static void run_coll(const std::vector<XgmiComm*>& group, Coll op, const std::vector<const void*>& ins,
                        const std::vector<void*>& outs, int64_t m, DType dt, hipStream_t stream, float scale);
+  // run_threshold's launch arguments and grid (no launch); false: nothing to do (n <= 0)
+  static bool threshold_args(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
+                             const std::vector<void*>& outs, int64_t n, DType dt, float thr, float thc,
+                             int32_t* counts, float scale, bool rescale, const RoundSpec* spec, void* args, int* gx);
   static void run_threshold(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
                             const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, float thr,
                             float thc, int32_t* counts, float scale, bool rescale, const RoundSpec* spec = nullptr);

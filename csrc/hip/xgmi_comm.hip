@@ -1193,9 +1193,10 @@ int XgmiComm::threshold_chunks(int64_t n, DType dt, int ranks_in_launch) const {
   return nch;
 }
 
-void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
-                             const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, float thr,
-                             float thc, int32_t* counts, float scale, bool rescale, const RoundSpec* spec) {
+bool XgmiComm::threshold_args(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
+                              const std::vector<void*>& outs, int64_t n, DType dt, float thr, float thc,
+                              int32_t* counts, float scale, bool rescale, const RoundSpec* spec, void* args,
+                              int* gx_out) {
   if (group.empty() || ins.size() != group.size() || outs.size() != group.size())
     throw std::invalid_argument("XgmiComm: one input and one output per rank");
   const XgmiComm& c0 = *group[0];
@@ -1212,12 +1213,12 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
     throw std::invalid_argument("allreduce_threshold: construct the comm with threshold_rows = maxLag + 1 >= 1");
   if (!(thr >= 0.f && thr <= 1.f && thc >= 0.f && thc <= 1.f))
     throw std::invalid_argument("allreduce_threshold: thresholds must be in [0, 1]");
-  if (n <= 0) return;
+  if (n <= 0) return false;
   const int W = c0.world_;
   if (W > 32) throw std::invalid_argument("allreduce_threshold: at most 32 ranks");
   const int64_t es = static_cast<int64_t>(dtype_size(dt));
   const int ranks_here = static_cast<int>(group.size());
-  CommArgs a;
+  CommArgs& a = *static_cast<CommArgs*>(args);
   std::memset(&a, 0, sizeof(a));
   for (size_t y = 0; y < group.size(); ++y) {
     a.in[y] = static_cast<const char*>(ins[y]);
@@ -1335,6 +1336,19 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
   for (int k = 0; k < W; ++k) a.base[k] = c0.peers_[k];
   a.stamps = c0.stamps_;
   if (a.stamps != nullptr && gx * ranks_here > c0.stamp_slots_) a.stamps = nullptr;  // buffer too small: off
+  *gx_out = gx;
+  return true;
+}
+
+void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vector<const void*>& ins,
+                             const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, float thr,
+                             float thc, int32_t* counts, float scale, bool rescale, const RoundSpec* spec) {
+  CommArgs a;
+  int gx = 1;
+  if (!threshold_args(group, ins, outs, n, dt, thr, thc, counts, scale, rescale, spec, &a, &gx)) return;
+  const XgmiComm& c0 = *group[0];
+  const int64_t es = static_cast<int64_t>(dtype_size(dt));
+  const int ranks_here = static_cast<int>(group.size());
   hip_check(hipSetDevice(c0.device_), "hipSetDevice");
   TraceScope span("xgmi", [&] {
     return std::make_pair("threshold " + std::to_string(n * es) + "B",
@@ -1350,6 +1364,35 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
     ++c->stats_.threshold;
     c->stats_.bytes += n * es;
   }
+}
+
+XgmiComm::ResidentPlan XgmiComm::plan_resident(int64_t n, DType dt, float th_reduce, float th_complete,
+                                               const RoundSpec& spec, int max_grid) const {
+  ResidentPlan p;
+  auto a = std::make_shared<CommArgs>();
+  int gx = 0;
+  XgmiComm* self = const_cast<XgmiComm*>(this);
+  if (!threshold_args({self}, {nullptr}, {nullptr}, n, dt, th_reduce, th_complete, nullptr, 1.f, false, &spec,
+                      a.get(), &gx))
+    return p;
+  if (a->sub > 1 || gx > max_grid || a->delay_rank >= 0) return p;  // split chunks / big rounds / test knobs
+  a->stamps = nullptr;
+  p.args = a;
+  p.grid = gx;
+  p.dt = dt;
+  p.n = n;
+  return p;
+}
+
+void XgmiComm::launch_resident(const ResidentPlan& p, const ResidentDoor* door, uint32_t* hstate, uint32_t* dm,
+                               uint32_t seq, uint32_t gen, uint64_t idle_ticks, hipStream_t stream) {
+  if (!p.args || p.grid <= 0) throw std::invalid_argument("launch_resident: no resident plan");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  order_after_last(stream);
+  launch_threshold_resident(*static_cast<const CommArgs*>(p.args.get()), p.grid, stream, p.dt, door, hstate, dm, seq, gen,
+                            idle_ticks);
+  hip_check(hipGetLastError(), "resident threshold launch");
+  ++stats_.launches;
 }
 
 void XgmiComm::publish_progress(uint32_t value, hipStream_t stream) {

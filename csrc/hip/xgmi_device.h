@@ -408,6 +408,9 @@ __device__ __forceinline__ void finish_launch_done(const CommArgs& a, uint32_t* 
 
 // Host entry of the threshold kernel (xgmi_threshold.hip).
 void launch_threshold(const CommArgs& a, dim3 grid, hipStream_t s, DType dt);
+// Resident rounds (xgmi_threshold.hip; XgmiComm::launch_resident).
+void launch_threshold_resident(const CommArgs& a, int grid, hipStream_t s, DType dt, const ResidentDoor* door,
+                               uint32_t* hstate, uint32_t* dm, uint32_t seq, uint32_t gen, uint64_t idle_ticks);
 // Progress words = value in every peer's slab (xgmi_threshold.hip; XgmiComm::publish_progress).
 void launch_publish_progress(const CommArgs& a, uint32_t value, hipStream_t s);
 // Host entry of the low-latency one-shot (xgmi_ll.hip).

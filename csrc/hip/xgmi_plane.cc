@@ -145,6 +145,8 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   // form; ~2-3 us of hipEventRecord on every launch, profiles/round3/api_cost.json)
   if (const char* e = std::getenv("MXAR_PLANE_EVENTS")) event_confirm_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("MXAR_PLANE_COARSEN")) coarsen_full_ = std::atoi(e) != 0;  // A/B knob
+  if (const char* e = std::getenv("MXAR_PLANE_RESIDENT")) o_.resident_max = std::atoll(e);
+  if (const char* e = std::getenv("MXAR_PLANE_RESIDENT_IDLE_US")) o_.resident_idle_us = std::atof(e);
   const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
   flag_gran_ = o_.min_chunk > 0 ? std::min<int64_t>(XgmiComm::min_chunk_bytes(), o_.min_chunk * es)
                                 : XgmiComm::min_chunk_bytes();
@@ -193,6 +195,15 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&ring_dev_), ring_, 0), "hipHostGetDevicePointer(ring)");
   hip_check(hipMalloc(reinterpret_cast<void**>(&cnt_vram_), ring_stride_ * 4 * o_.ring), "hipMalloc(plane counts)");
   hip_check(hipMalloc(reinterpret_cast<void**>(&ctl_mem_), 256), "hipMalloc(plane ctl)");
+  hip_check(hipHostMalloc(reinterpret_cast<void**>(&door_), sizeof(ResidentDoor) * kResidentDoors + 64,
+                          hipHostMallocCoherent | hipHostMallocMapped),
+            "hipHostMalloc(resident door)");
+  std::memset(door_, 0, sizeof(ResidentDoor) * kResidentDoors + 64);
+  hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&door_dev_), door_, 0), "hipHostGetDevicePointer(door)");
+  rstate_ = reinterpret_cast<volatile uint32_t*>(door_ + kResidentDoors);
+  rstate_dev_ = reinterpret_cast<uint32_t*>(door_dev_ + kResidentDoors);
+  hip_check(hipMalloc(reinterpret_cast<void**>(&rdm_), 256), "hipMalloc(resident words)");
+  hip_check(hipMemset(rdm_, 0, 256), "hipMemset(resident words)");
   hip_check(hipMemset(ctl_mem_, 0, 256), "hipMemset(plane ctl)");
   // split-chunk scratch (decision words, slice counters; XgmiComm::RoundSpec::split_scratch)
   hip_check(hipMalloc(&split_mem_, split_bytes_), "hipMalloc(plane split scratch)");
@@ -245,6 +256,7 @@ XgmiRoundPlane::~XgmiRoundPlane() {
   try {
     abort(0x7fffffff);
     drain();
+    park_resident();
   } catch (...) {
   }
   {
@@ -265,6 +277,11 @@ XgmiRoundPlane::~XgmiRoundPlane() {
     rel_->bytes = 0;  // outputs still held by users are freed stream-ordered when dropped
   }
   if (rel_ev_) (void)hipEventDestroy(rel_ev_);
+  for (auto& [ev, v] : rel_pend_) {
+    (void)hipEventDestroy(ev);
+    for (void* q : v) (void)hipFree(q);
+  }
+  for (hipEvent_t ev : rel_spare_) (void)hipEventDestroy(ev);
   comm_.reset();
   for (auto& [h, p] : mapped_) (void)hipIpcCloseMemHandle(p);
   {
@@ -277,6 +294,8 @@ XgmiRoundPlane::~XgmiRoundPlane() {
   if (ctl_mem_) (void)hipFree(ctl_mem_);
   if (split_mem_) (void)hipFree(split_mem_);
   if (hforce_) (void)hipHostFree(hforce_);
+  if (door_) (void)hipHostFree(door_);
+  if (rdm_) (void)hipFree(rdm_);
   if (stream_) {
     forget_plane_stream(stream_);
     (void)hipStreamDestroy(stream_);
@@ -398,6 +417,13 @@ void XgmiRoundPlane::flush_releases() {
     std::lock_guard<std::mutex> g(rel_->mu);
     ptrs.swap(rel_->ptrs);
   }
+  // releases parked by resident rounds: their events were recorded on the default stream
+  // before the one below, so its wait covers them
+  for (auto& [ev, v] : rel_pend_) {
+    ptrs.insert(ptrs.end(), v.begin(), v.end());
+    rel_spare_.push_back(ev);
+  }
+  rel_pend_.clear();
   if (ptrs.empty()) return;
   // one event for every exported output released since the last launch: their reuse by
   // this and later launches comes after everything the default stream held at this point -
@@ -461,6 +487,9 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
     abort(last_round_);
     drain();
   }
+  park_resident();  // the stream work below must not queue behind it
+  rplan_tried_ = false;
+  rplan_ = XgmiComm::ResidentPlan();
   hip_check(hipSetDevice(o_.device), "hipSetDevice");
   const int P = cfg.peers;
   const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
@@ -571,10 +600,206 @@ int XgmiRoundPlane::take_slot(std::unique_lock<std::mutex>& lk) {
   return s;
 }
 
+bool XgmiRoundPlane::post_door(const ResidentDoor& e) {
+  const uint32_t seq = res_seq_++;
+  // the door slot is free once the kernel consumed the entry kResidentDoors before this one
+  // (rounds in flight are bounded by the ring's slots, so this does not wait in practice)
+  const auto t0 = std::chrono::steady_clock::now();
+  while (static_cast<int32_t>(seq - static_cast<uint32_t>(kResidentDoors) - rstate_[1]) > 0 &&
+         rstate_[0] != kResExited) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::duration<double>(2 * o_.timeout_s + 5))
+      throw ProtocolError("xgmi plane: the resident round kernel stopped taking rounds");
+    __builtin_ia32_pause();
+  }
+  ResidentDoor* d = door_ + seq % kResidentDoors;
+  d->in = e.in;
+  d->out = e.out;
+  d->counts = e.counts;
+  d->counts_host = e.counts_host;
+  d->err_out = e.err_out;
+  d->done_out = e.done_out;
+  d->epoch = e.epoch;
+  d->cmd = e.cmd;
+  __atomic_store_n(&d->seq, seq, __ATOMIC_RELEASE);  // the kernel reads the operands after the sequence word
+  // Dekker hand-off with the kernel's idle exit (xgmi_threshold.hip, resident_door): the
+  // entry is visible before the state word is read
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  uint32_t st = rstate_[0];
+  while (st == kResExiting) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::duration<double>(2 * o_.timeout_s + 5))
+      throw ProtocolError("xgmi plane: the resident round kernel neither took nor refused a round");
+    __builtin_ia32_pause();
+    st = rstate_[0];
+  }
+  return st != kResExited;
+}
+
+void XgmiRoundPlane::park_resident() {
+  if (!res_on_) return;
+  res_on_ = false;
+  st_.resident_parks++;
+  ResidentDoor e{};
+  e.cmd = kResStop;
+  if (!post_door(e)) return;  // it had left already
+  const auto t0 = std::chrono::steady_clock::now();
+  while (rstate_[0] != kResExited) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::duration<double>(2 * o_.timeout_s + 5)) {
+      MXAR_LOG(ERROR, "plane", "resident round kernel did not stop");
+      return;
+    }
+    std::this_thread::yield();
+  }
+}
+
+std::shared_ptr<void> XgmiRoundPlane::resident_out(size_t bytes, std::shared_ptr<std::atomic<bool>>* exported) {
+  bytes = std::max<size_t>(bytes, 256);
+  std::vector<void*> ptrs;
+  {
+    std::lock_guard<std::mutex> g(rel_->mu);
+    if (rel_->bytes != bytes) return nullptr;
+    ptrs.swap(rel_->ptrs);
+  }
+  if (!ptrs.empty()) {  // exported outputs: reusable behind what the default stream holds now
+    hipEvent_t ev = nullptr;
+    if (!rel_spare_.empty()) {
+      ev = rel_spare_.back();
+      rel_spare_.pop_back();
+    } else {
+      hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate(release)");
+    }
+    hip_check(hipEventRecord(ev, nullptr), "hipEventRecord(release)");
+    rel_pend_.emplace_back(ev, std::move(ptrs));
+  }
+  while (!rel_pend_.empty() && hipEventQuery(rel_pend_.front().first) == hipSuccess) {
+    std::lock_guard<std::mutex> g(rel_->mu);
+    for (void* q : rel_pend_.front().second) rel_->free.push_back(q);
+    rel_spare_.push_back(rel_pend_.front().first);
+    rel_pend_.pop_front();
+  }
+  (void)hipGetLastError();
+  bool grow = false;
+  {
+    std::lock_guard<std::mutex> g(rel_->mu);
+    grow = rel_->free.empty();
+    if (grow) {
+      void* p = nullptr;
+      hip_check(hipMalloc(&p, bytes), "hipMalloc(plane output)");
+      rel_->free.push_back(p);
+      st_.pool_grown++;
+    }
+  }
+  return out_buffer(bytes, exported);
+}
+
+bool XgmiRoundPlane::launch_resident(int round, const Payload& input, bool cold) {
+  if (o_.resident_max <= 0 || event_confirm_ || o_.ring > kResidentDoors) return false;
+  const int64_t n = cfg_.dataSize;
+  const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
+  if (n * es > o_.resident_max) return false;
+  const void* in_ptr = nullptr;
+  if (!cold) {
+    // only inputs the kernel can read now: device memory of this GPU, the plane's dtype, its
+    // producer finished (the launch path orders the rest on the plane stream)
+    auto* dp = input ? dynamic_cast<const DevicePayload*>(input.get()) : nullptr;
+    if (dp == nullptr || static_cast<int64_t>(dp->size()) != n || dp->device() != o_.device ||
+        dp->dtype() != static_cast<int>(o_.dtype))
+      return false;
+    // a producer still running (e.g. the demo source's fill kernel) gets a short host wait:
+    // a few microseconds for a round this small, cheaper than leaving the resident kernel
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      hipError_t q = hipSuccess;
+      if (dp->ready()) q = hipEventQuery(static_cast<hipEvent_t>(dp->ready().get()));
+      else if (dp->stream() && dp->stream() != stream_) q = hipStreamQuery(dp->stream());
+      if (q == hipSuccess) break;
+      (void)hipGetLastError();
+      if (q != hipErrorNotReady || std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) return false;
+      for (int i = 0; i < 16; ++i) __builtin_ia32_pause();
+    }
+    in_ptr = dp->bytes();
+  }
+  XgmiComm::RoundSpec spec;
+  spec.block = block_;
+  spec.chunk = chunk_;
+  spec.order_ref = o_.order_ref;
+  spec.host_force = hforce_dev_;
+  spec.host_abort = hforce_dev_ + 1;
+  if (!rplan_tried_) {
+    rplan_tried_ = true;
+    rplan_ = comm_->plan_resident(n, o_.dtype, cfg_.thReduce, cfg_.thComplete, spec, 16);
+  }
+  if (rplan_.grid <= 0) return false;
+  Rec rec;
+  rec.out = resident_out(static_cast<size_t>(n * es), &rec.exported);
+  if (!rec.out) return false;
+  rec.round = round;
+  rec.epoch = cfg_.epoch;
+  rec.cold = cold;
+  rec.round_epoch = epoch_of(round);
+  if (!cold) rec.input = input;  // held until the round completed
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    rec.slot = take_slot(lk);
+  }
+  int32_t* slot_dev = ring_dev_ + static_cast<size_t>(rec.slot) * ring_stride_;
+  ResidentDoor e{};
+  e.in = reinterpret_cast<uint64_t>(cold ? rec.out.get() : in_ptr);
+  e.out = reinterpret_cast<uint64_t>(rec.out.get());
+  e.counts = reinterpret_cast<uint64_t>(cnt_vram_ + static_cast<size_t>(rec.slot) * ring_stride_);
+  e.counts_host = reinterpret_cast<uint64_t>(slot_dev);
+  e.err_out = reinterpret_cast<uint64_t>(slot_dev + ring_stride_ - 1);
+  e.done_out = reinterpret_cast<uint64_t>(slot_dev + ring_stride_ - 2);
+  e.epoch = rec.round_epoch;
+  e.cmd = cold ? kResCold : kResRound;
+  {
+    TraceScope span("plane", [&] {
+      return std::make_pair(std::string(cold ? "resident cold round " : "resident round ") + std::to_string(round),
+                            "{\"worker\":" + std::to_string(cfg_.id) + ",\"bytes\":" + std::to_string(n * es) + "}");
+    });
+    const uint32_t seq = res_seq_;
+    bool taken = res_on_ && post_door(e);
+    if (!taken) {
+      // no kernel (first resident round, or it left after an idle spell): launch one that
+      // starts at this entry
+      if (!res_on_) {
+        ResidentDoor* d = door_ + seq % kResidentDoors;
+        *d = e;
+        __atomic_store_n(&d->seq, seq, __ATOMIC_RELEASE);
+        res_seq_ = seq + 1;
+      }
+      rstate_[1] = seq - 1u;
+      rstate_[0] = kResRunning;
+      __atomic_thread_fence(__ATOMIC_SEQ_CST);
+      try {
+        comm_->launch_resident(rplan_, door_dev_, rstate_dev_, rdm_, seq, ++res_gen_,
+                               static_cast<uint64_t>(o_.resident_idle_us * 100.0), stream_);
+      } catch (...) {
+        std::lock_guard<std::mutex> g(mu_);
+        free_slots_.push_back(rec.slot);
+        throw;
+      }
+      res_on_ = true;
+      st_.resident_launches++;
+    }
+  }
+  std::unique_lock<std::mutex> lk(mu_);
+  last_round_ = round;
+  st_.launches++;
+  st_.resident_rounds++;
+  if (cold) st_.cold++;
+  st_.bytes += static_cast<uint64_t>(n * es);
+  q_.push_back(std::move(rec));
+  lk.unlock();
+  cv_.notify_all();
+  return true;
+}
+
 void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   if (!configured_) throw ProtocolError("xgmi plane: launch before configure (InitWorkers)");
   if (round != last_round_ + 1) throw ProtocolError("xgmi plane: rounds must be launched in order");
   hip_check(hipSetDevice(o_.device), "hipSetDevice");
+  if (launch_resident(round, input, cold)) return;
+  park_resident();
   const int64_t n = cfg_.dataSize;
   const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
   const int dcode = static_cast<int>(o_.dtype);

@@ -61,11 +61,18 @@ struct XgmiPlaneOptions {
   // maxChunkSize runs at thresholds 1 with chunks coarsened to the flag granularity (counts
   // reported per reference chunk), and is refused at thresholds < 1 (ProtocolError).
   int64_t min_chunk = 0;
+  // Resident rounds (XgmiComm::launch_resident): rounds of at most this many bytes are posted
+  // to a kernel that stays on the plane stream between rounds instead of one launch each
+  // (0 = off; MXAR_PLANE_RESIDENT). The kernel leaves after `resident_idle_us` without a
+  // round (MXAR_PLANE_RESIDENT_IDLE_US) and is launched again by the next one.
+  int64_t resident_max = 64 << 10;
+  double resident_idle_us = 1000.0;
 };
 
 struct XgmiPlaneStats {
   uint64_t launches = 0, cold = 0, forced = 0, bytes = 0, completed = 0, coarsened = 0, peer_maps = 0;
   uint64_t pool_grown = 0;  // round outputs the pool had to allocate (none after warm-up in steady state)
+  uint64_t resident_rounds = 0, resident_launches = 0, resident_parks = 0;
 };
 
 class XgmiRoundPlane final : public RoundPlane {
@@ -128,6 +135,14 @@ class XgmiRoundPlane final : public RoundPlane {
   void reset_pool(size_t bytes);
   int take_slot(std::unique_lock<std::mutex>& lk);
   void completion_loop();
+  // Resident rounds: post the round to the resident kernel (launching it if none runs);
+  // false = the round needs the launch path (park_resident first).
+  bool launch_resident(int round, const Payload& input, bool cold);
+  // Writes door entry res_seq_ and hands it to the kernel; false = the kernel had exited
+  // before it took the entry (nothing runs it).
+  bool post_door(const ResidentDoor& e);
+  // Stops the resident kernel (a STOP entry behind the posted rounds) and waits for it to leave.
+  void park_resident();
 
   XgmiPlaneOptions o_;
   char* arena_ = nullptr;
@@ -182,6 +197,24 @@ class XgmiRoundPlane final : public RoundPlane {
   hipEvent_t rel_ev_ = nullptr;
   void flush_releases();
   std::shared_ptr<bool> alive_ = std::make_shared<bool>(true);
+  // resident rounds
+  ResidentDoor* door_ = nullptr;       // pinned door ring (kResidentDoors entries)
+  ResidentDoor* door_dev_ = nullptr;   // its device-visible address
+  volatile uint32_t* rstate_ = nullptr;  // pinned: [0] kernel state, [1] last entry it consumed
+  uint32_t* rstate_dev_ = nullptr;
+  uint32_t* rdm_ = nullptr;            // the kernel's device words
+  XgmiComm::ResidentPlan rplan_;
+  bool rplan_tried_ = false;
+  bool res_on_ = false;                // a resident kernel was launched and may still run
+  uint32_t res_seq_ = 1;               // next door entry
+  uint32_t res_gen_ = 0;               // resident kernel launches
+  // exported outputs released while a resident kernel holds the plane stream: reusable once
+  // an event recorded on the default stream behind them has completed (host query)
+  std::deque<std::pair<hipEvent_t, std::vector<void*>>> rel_pend_;
+  std::vector<hipEvent_t> rel_spare_;
+  // a pooled round output for a resident round (grown with hipMalloc: nothing may queue on
+  // the plane stream behind the resident kernel)
+  std::shared_ptr<void> resident_out(size_t bytes, std::shared_ptr<std::atomic<bool>>* exported);
 };
 
 std::shared_ptr<XgmiRoundPlane> make_xgmi_plane(const XgmiPlaneOptions& o);

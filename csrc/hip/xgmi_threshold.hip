@@ -483,8 +483,22 @@ __device__ __forceinline__ void put_count(int32_t* p, int32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The per-round operands of threshold_round: a launch's own (CommArgs, threshold_kernel) or
+// the ones a resident kernel read from the host's door (threshold_resident_kernel).
+struct RoundVars {
+  const char* in;
+  char* out;
+  int32_t* counts;
+  int32_t* counts_host;
+  uint32_t* err_out;
+  uint32_t* done_out;
+  uint32_t epoch;  // 0: ctl[4] + 1
+  int cold;
+};
+
+// One round of rank a.rank0 + blockIdx.y by the whole grid.
 template <class E>
-__global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
+__device__ __forceinline__ void threshold_round(const CommArgs& a, const RoundVars& rv) {
   constexpr int es = 16 / E::ELEMS;
   __shared__ uint32_t sh_mask;
   __shared__ int sh_flag;
@@ -503,11 +517,11 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   const int P = a.P;
   const int y = blockIdx.y;
   const int r = a.rank0 + y;
-  const char* const in = a.in[y];
-  char* const out = a.out[y];
+  const char* const in = rv.in;
+  char* const out = rv.out;
   uint32_t* const ctl = a.ctl[y];
   // threshold rounds count separately (ctl[4]); the protocol engine passes its round epochs
-  const uint32_t epoch = a.epoch_set ? a.epoch_set : ld_ctl(&ctl[4]) + 1u;
+  const uint32_t epoch = rv.epoch ? rv.epoch : ld_ctl(&ctl[4]) + 1u;
   const int row = 1 + static_cast<int>(epoch % static_cast<uint32_t>(a.trows));
   const int G = gridDim.x;
   const int64_t slot = a.slot_bytes;
@@ -516,8 +530,8 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   uint32_t* err = &ctl[2];
   const bool rel = a.fence & 1, acq = a.fence & 2;
   const int Pm1 = P > 1 ? P - 1 : 1;
-  int32_t* const counts = a.counts ? a.counts + static_cast<int64_t>(y) * P * a.nch : nullptr;
-  const bool cold = a.cold != 0;
+  int32_t* const counts = rv.counts ? rv.counts + static_cast<int64_t>(y) * P * a.nch : nullptr;
+  const bool cold = rv.cold != 0;
   const bool ref = a.order_ref != 0;
   // Full thresholds (thReduce = thComplete = 1): every contribution and every chunk is taken
   // whatever the arrival order, so neither the launch snapshot (a grid-wide barrier) nor the
@@ -827,7 +841,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
     } else if (len > 0) {
       reduce_masked<E>(a, P, r, mask, in + (bstart_own + cstart) * es, a.base[r] + rowS + cstart * es, slot,
                        take ? own_out : nullptr, rowR + r * slot + cstart * es, len,
-                       (a.fence & 1) || a.done_out != nullptr, sc);
+                       (a.fence & 1) || rv.done_out != nullptr, sc);
       if (!take) zero_fill<E>(own_out, len);
     }
     // a split chunk is reduced once its last slice is: that workgroup publishes it
@@ -1035,9 +1049,9 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   }
   __syncthreads();
   const bool last = sh_flag != 0;
-  if (last && counts != nullptr && a.counts_host != nullptr) {
+  if (last && counts != nullptr && rv.counts_host != nullptr) {
     // every workgroup's counts are visible here (sc1 stores drained before their tickets)
-    int32_t* dst = a.counts_host + static_cast<int64_t>(y) * P * a.nch;
+    int32_t* dst = rv.counts_host + static_cast<int64_t>(y) * P * a.nch;
     for (int64_t i = threadIdx.x; i < static_cast<int64_t>(P) * a.nch; i += kCommThreads)
       __hip_atomic_store(dst + i, __hip_atomic_load(counts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1050,9 +1064,12 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
       __hip_atomic_store(&ctl[5], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&ctl[6], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&ctl[7], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // a resident kernel's workgroups start the next round once ctl[4] names this one: the
+      // resets land first
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(&ctl[4], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (a.err_out)  // the protocol plane reads it from pinned memory after the round's event
-        __hip_atomic_store(a.err_out, ld_ctl(err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (rv.err_out)  // the protocol plane reads it from pinned memory after the round's event
+        __hip_atomic_store(rv.err_out, ld_ctl(err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       for (int k = 0; k < P; ++k)
@@ -1060,8 +1077,150 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
       // the round's completion word: every workgroup has passed its ticket and every output
       // store was write-through (zero_fill, reduce_masked with wt_out), so the host may hand
       // the output on at once, before the kernel itself ends (xgmi_plane.cc)
-      if (a.done_out) st_flag(a.done_out, epoch);
+      if (rv.done_out) st_flag(rv.done_out, epoch);
     }
+  }
+}
+
+template <class E>
+__global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
+  const int y = blockIdx.y;
+  const RoundVars rv{a.in[y], a.out[y], a.counts, a.counts_host, a.err_out, a.done_out, a.epoch_set, a.cold};
+  threshold_round<E>(a, rv);
+}
+
+// ---------------------------------------------------------------------------------
+// Resident rounds (XgmiComm::launch_resident, xgmi_plane.cc). A protocol round of a few KiB
+// is mostly launch: the host's launch call, the dispatch, and the skew between the
+// workers' kernels, each of which then waits for the other's scatter. A resident kernel
+// stays on the GPU between rounds: workgroup 0 (the leader) polls the host's door ring
+// (pinned host memory, one 64-B entry per round, the sequence word written last) and hands
+// each entry to the other workgroups through device words (`dm`); every workgroup then runs
+// the same threshold_round a launch would, and waits for the round's last workgroup to
+// reset the round counters (ctl[4] = epoch) before the next entry.
+//
+// Exit: a STOP entry, or no entry for `idle` ticks. The idle exit cannot lose an entry the
+// host posts meanwhile: the leader writes EXITING to the host state word, fences, and reads
+// the door once more (the host writes the entry, fences, then reads the state word - one
+// side sees the other's write): an entry found then is taken (state back to RUNNING);
+// otherwise the state becomes EXITED and the host launches a new kernel for that entry.
+// dm words: [0..1] go = (launch generation << 32) | entry sequence, [2] command, [4..15] the
+// entry's pointers, [16] epoch. The generation keeps a relaunched kernel's workgroups from
+// taking the previous kernel's last go (its idle exit) for theirs.
+constexpr uint32_t kDmGo = 0, kDmCmd = 2, kDmPtr = 4, kDmEpoch = 16;
+
+__device__ __forceinline__ uint32_t sys_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t sys_ld64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void dm_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Leader, one lane: the command of entry `seq` (its operands copied into dm), or STOP.
+__device__ uint32_t resident_door(const ResidentDoor* door, uint32_t* hstate, uint32_t* dm, uint32_t seq,
+                                  uint32_t gen, uint64_t idle) {
+  const ResidentDoor* d = door + seq % kResidentDoors;
+  const uint64_t t0 = wall_ticks();
+  uint32_t cmd = kResStop;
+  bool taken = true;
+  for (;;) {
+    if (sys_ld(&d->seq) == seq) {
+      cmd = sys_ld(reinterpret_cast<const uint32_t*>(&d->cmd));
+      break;
+    }
+    if (wall_ticks() - t0 > idle) {
+      sys_st(&hstate[0], kResExiting);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (sys_ld(&d->seq) == seq) {
+        sys_st(&hstate[0], kResRunning);
+        cmd = sys_ld(reinterpret_cast<const uint32_t*>(&d->cmd));
+        break;
+      }
+      cmd = kResStop;
+      taken = false;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  if (cmd != kResStop) {
+    const uint64_t* f = &d->in;
+    for (int i = 0; i < 6; ++i) {
+      const uint64_t v = sys_ld64(f + i);
+      dm_st(&dm[kDmPtr + 2 * i], static_cast<uint32_t>(v));
+      dm_st(&dm[kDmPtr + 2 * i + 1], static_cast<uint32_t>(v >> 32));
+    }
+    dm_st(&dm[kDmEpoch], sys_ld(&d->epoch));
+  }
+  dm_st(&dm[kDmCmd], cmd);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(&dm[kDmGo]), (static_cast<uint64_t>(gen) << 32) | seq,
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (taken) sys_st(&hstate[1], seq);  // the entry is copied: the host may reuse its door slot
+  if (cmd == kResStop) sys_st(&hstate[0], kResExited);
+  return cmd;
+}
+
+template <class E>
+__global__ __launch_bounds__(kCommThreads) void threshold_resident_kernel(CommArgs a, const ResidentDoor* door,
+                                                                         uint32_t* hstate, uint32_t* dm,
+                                                                         uint32_t seq, uint32_t gen, uint64_t idle) {
+  __shared__ uint32_t sh_cmd;
+  __shared__ uint64_t sh_ptr[6];
+  __shared__ uint32_t sh_epoch;
+  uint32_t* const ctl = a.ctl[0];
+  for (;; ++seq) {
+    if (threadIdx.x == 0) {
+      uint32_t cmd = kResStop;
+      if (blockIdx.x == 0) {
+        cmd = resident_door(door, hstate, dm, seq, gen, idle);
+      } else {
+        // the leader answers within `idle` plus one round (each bounded by a.timeout)
+        const uint64_t until = wall_ticks() + idle + 2 * a.timeout + 100000000ull;
+        for (;;) {
+          if (__hip_atomic_load(reinterpret_cast<uint64_t*>(&dm[kDmGo]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+              ((static_cast<uint64_t>(gen) << 32) | seq)) {
+            cmd = ld_ctl(&dm[kDmCmd]);
+            break;
+          }
+          if (wall_ticks() > until) {
+            __hip_atomic_fetch_or(&ctl[2], ERR_TIMEOUT_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      if (cmd != kResStop) {
+        for (int i = 0; i < 6; ++i)
+          sh_ptr[i] = static_cast<uint64_t>(ld_ctl(&dm[kDmPtr + 2 * i])) |
+                      (static_cast<uint64_t>(ld_ctl(&dm[kDmPtr + 2 * i + 1])) << 32);
+        sh_epoch = ld_ctl(&dm[kDmEpoch]);
+        // the round's input was written by kernels that finished before the host posted it:
+        // drop what this XCD's caches hold of earlier rounds
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      }
+      sh_cmd = cmd;
+    }
+    __syncthreads();
+    const uint32_t cmd = sh_cmd;
+    if (cmd == kResStop) break;
+    const RoundVars rv{reinterpret_cast<const char*>(sh_ptr[0]), reinterpret_cast<char*>(sh_ptr[1]),
+                       reinterpret_cast<int32_t*>(sh_ptr[2]),    reinterpret_cast<int32_t*>(sh_ptr[3]),
+                       reinterpret_cast<uint32_t*>(sh_ptr[4]),   reinterpret_cast<uint32_t*>(sh_ptr[5]),
+                       sh_epoch,                                 cmd == kResCold ? 1 : 0};
+    __syncthreads();
+    threshold_round<E>(a, rv);
+    if (threadIdx.x == 0) {  // the round's counters are reset before any workgroup starts the next
+      const uint64_t until = wall_ticks() + a.timeout + 100000000ull;
+      while (ld_ctl(&ctl[4]) != rv.epoch && wall_ticks() < until) __builtin_amdgcn_s_sleep(1);
+    }
+    __syncthreads();
   }
 }
 
@@ -1078,6 +1237,14 @@ __global__ __launch_bounds__(64) void publish_progress_kernel(CommArgs a, uint32
 
 void launch_publish_progress(const CommArgs& a, uint32_t value, hipStream_t s) {
   hipLaunchKernelGGL(publish_progress_kernel, dim3(1), dim3(64), 0, s, a, value);
+}
+
+void launch_threshold_resident(const CommArgs& a, int grid, hipStream_t s, DType dt, const ResidentDoor* door,
+                               uint32_t* hstate, uint32_t* dm, uint32_t seq, uint32_t gen, uint64_t idle_ticks) {
+  dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
+    hipLaunchKernelGGL(threshold_resident_kernel<decltype(tag)>, dim3(grid), dim3(kCommThreads), 0, s, a, door,
+                       hstate, dm, seq, gen, idle_ticks);
+  });
 }
 
 void launch_threshold(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {

@@ -814,3 +814,109 @@ def test_distributed_plane_job_master_and_bridge_driven():
     for rank, out in res:
         assert [o[:2] for o in out] == [(False, True), (True, True)], (rank, out)
         assert all(o[2] == 8 for o in out), (rank, out)
+
+
+# ---------------------------------------------------------------------------------------
+# Resident rounds (xgmi_plane.cc launch_resident, xgmi_threshold.hip threshold_resident_kernel):
+# rounds of <= 64 KiB are posted to a kernel that stays on the plane stream between rounds.
+
+def _job_with_env(env, **kw):
+    """A PlaneJob whose planes see `env` (read when a plane is built)."""
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return PlaneJob(**kw)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("P,n,chunk,dtype", [(2, 10, 2, torch.float32), (3, 4096, 512, torch.bfloat16),
+                                             (4, 16384, 1024, torch.float32)])
+def test_resident_rounds_match_launched_rounds(P, n, chunk, dtype):
+    """The same job with resident rounds (default) and with one launch per round
+    (MXAR_PLANE_RESIDENT=0): identical outputs and counts, exact sums, and the resident job
+    ran its rounds on the resident kernel."""
+    rounds = 41
+    got = {}
+    for mode, env in (("resident", {}), ("launched", {"MXAR_PLANE_RESIDENT": "0"})):
+        job = _job_with_env(env, P=P, data_size=n, max_chunk_size=chunk, max_lag=1, max_round=rounds - 1,
+                            dtype=dtype, timeout_s=20.0)
+        try:
+            job.run(timeout=120)
+            assert job.rounds["n"] == rounds
+            for k in range(P):
+                st = job.system.plane_worker_state(job.workers[k])
+                assert st["stats"]["plane_errors"] == 0 and st["stats"]["rounds_completed"] == rounds, st
+            res = [p.stats.resident_rounds for p in job.planes]
+            if mode == "resident":
+                assert all(r >= 0.8 * rounds for r in res), res
+            else:
+                assert res == [0] * P
+            got[mode] = [[(job.outputs[k][it][0].float().cpu().numpy(), list(job.outputs[k][it][1]))
+                          for it in range(rounds)] for k in range(P)]
+        finally:
+            job.shutdown()
+    for k in range(P):
+        for it in range(rounds):
+            a, ca = got["resident"][k][it]
+            b, cb = got["launched"][k][it]
+            np.testing.assert_array_equal(a, b, err_msg=f"worker {k} round {it}")
+            assert ca == cb == [P] * len(ca)
+            if dtype == torch.float32:
+                np.testing.assert_array_equal(a, expected(n, it, range(P)))
+
+
+def test_resident_kernel_leaves_when_idle_and_comes_back():
+    """Sources slower than the resident kernel's idle budget (1 ms): the kernel leaves between
+    rounds and the next round launches it again - every round still exact."""
+    P, n, chunk, rounds = 2, 1000, 100, 9
+
+    def slow(k):
+        def src(req):
+            time.sleep(0.005)
+            x = torch.arange(n, dtype=torch.float32, device=DEV) + (req.iteration + 1000.0 * k)
+            torch.cuda.current_stream(DEV).synchronize()
+            return x
+        return src
+
+    job = PlaneJob(P, n, max_chunk_size=chunk, max_lag=1, max_round=rounds - 1, timeout_s=20.0,
+                   sources=[slow(k) for k in range(P)])
+    try:
+        job.run(timeout=120)
+        assert job.rounds["n"] == rounds
+        for k in range(P):
+            for it in range(rounds):
+                np.testing.assert_array_equal(job.outputs[k][it][0].cpu().numpy(), expected(n, it, range(P)))
+        st = [p.stats for p in job.planes]
+        assert all(s.resident_rounds == rounds for s in st), [s.resident_rounds for s in st]
+        assert all(s.resident_launches >= 2 for s in st), [s.resident_launches for s in st]
+    finally:
+        job.shutdown()
+
+
+def test_resident_rounds_with_released_outputs():
+    """Outputs handed to the sink as tensors and dropped every round go back to the pool
+    behind the default stream (an event per batch, no plane-stream work): sums stay exact
+    and the pool stops growing."""
+    P, n, chunk, rounds = 2, 2048, 256, 60
+    sums = [dict() for _ in range(P)]
+
+    def on_output(k, out):
+        sums[k][out.iteration] = float(out.data.double().sum().item())
+
+    job = PlaneJob(P, n, max_chunk_size=chunk, max_lag=1, max_round=rounds - 1, timeout_s=20.0,
+                   keep_outputs=False, on_output=on_output)
+    try:
+        job.run(timeout=120)
+        for k in range(P):
+            for it in range(rounds):
+                assert sums[k][it] == float(expected(n, it, range(P)).sum()), (k, it)
+        st = [p.stats for p in job.planes]
+        assert all(s.resident_rounds >= 0.8 * rounds for s in st), [s.resident_rounds for s in st]
+        assert all(s.pool_grown <= 8 for s in st), [s.pool_grown for s in st]
+    finally:
+        job.shutdown()
