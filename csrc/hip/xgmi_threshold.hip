@@ -1104,116 +1104,110 @@ __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
 // the door once more (the host writes the entry, fences, then reads the state word - one
 // side sees the other's write): an entry found then is taken (state back to RUNNING);
 // otherwise the state becomes EXITED and the host launches a new kernel for that entry.
-// dm words: [0..1] go = (launch generation << 32) | entry sequence, [2] command, [4..15] the
-// entry's pointers, [16] epoch. The generation keeps a relaunched kernel's workgroups from
-// taking the previous kernel's last go (its idle exit) for theirs.
-constexpr uint32_t kDmGo = 0, kDmCmd = 2, kDmPtr = 4, kDmEpoch = 16;
+// dm (device, 64-bit words): [0] go = (launch generation << 32) | entry sequence, [2..9] the
+// entry's 8 words (word 6 = epoch | cmd << 32). The generation keeps a relaunched kernel's
+// workgroups from taking the previous kernel's last go (its idle exit) for theirs. Every
+// hand-off moves the 64-B entry as ONE load / store instruction of 8 lanes: a host-memory
+// read is a PCIe round trip of microseconds, and reading the fields one by one cost more
+// than the launch the resident kernel saves (profiles/round4/README.md).
+constexpr int kDmGo = 0, kDmEntry = 2;
 
 __device__ __forceinline__ uint32_t sys_ld(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint64_t sys_ld64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void sys_st(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ void dm_st(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
-// Leader, one lane: the command of entry `seq` (its operands copied into dm), or STOP.
-__device__ uint32_t resident_door(const ResidentDoor* door, uint32_t* hstate, uint32_t* dm, uint32_t seq,
+// Leader wave (workgroup 0, wave 0): waits for entry `seq`, copies it into dm and publishes
+// go. Returns the entry's word 6 (epoch | cmd << 32) in every lane; cmd kResStop = leave.
+__device__ uint64_t resident_door(const ResidentDoor* door, uint32_t* hstate, uint64_t* dm, uint32_t seq,
                                   uint32_t gen, uint64_t idle) {
+  const int lane = static_cast<int>(threadIdx.x);
   const ResidentDoor* d = door + seq % kResidentDoors;
-  const uint64_t t0 = wall_ticks();
-  uint32_t cmd = kResStop;
-  bool taken = true;
-  for (;;) {
-    if (sys_ld(&d->seq) == seq) {
-      cmd = sys_ld(reinterpret_cast<const uint32_t*>(&d->cmd));
-      break;
-    }
-    if (wall_ticks() - t0 > idle) {
-      sys_st(&hstate[0], kResExiting);
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (sys_ld(&d->seq) == seq) {
-        sys_st(&hstate[0], kResRunning);
-        cmd = sys_ld(reinterpret_cast<const uint32_t*>(&d->cmd));
+  int found = 1;
+  if (lane == 0) {
+    const uint64_t t0 = wall_ticks();
+    for (;;) {
+      if (sys_ld(&d->seq) == seq) break;
+      if (wall_ticks() - t0 > idle) {
+        sys_st(&hstate[0], kResExiting);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (sys_ld(&d->seq) == seq) {
+          sys_st(&hstate[0], kResRunning);
+        } else {
+          found = 0;
+        }
         break;
       }
-      cmd = kResStop;
-      taken = false;
-      break;
+      __builtin_amdgcn_s_sleep(2);
     }
-    __builtin_amdgcn_s_sleep(2);
   }
-  if (cmd != kResStop) {
-    const uint64_t* f = &d->in;
-    for (int i = 0; i < 6; ++i) {
-      const uint64_t v = sys_ld64(f + i);
-      dm_st(&dm[kDmPtr + 2 * i], static_cast<uint32_t>(v));
-      dm_st(&dm[kDmPtr + 2 * i + 1], static_cast<uint32_t>(v >> 32));
-    }
-    dm_st(&dm[kDmEpoch], sys_ld(&d->epoch));
-  }
-  dm_st(&dm[kDmCmd], cmd);
+  found = __shfl(found, 0);
+  uint64_t w = 0;
+  if (found && lane < 8)  // the whole entry, one instruction (seq is already there: written last)
+    w = __hip_atomic_load(reinterpret_cast<const uint64_t*>(d) + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  uint64_t w6 = __shfl(w, 6);
+  if (!found) w6 = static_cast<uint64_t>(static_cast<uint32_t>(kResStop)) << 32;
+  if (found && lane < 8)
+    __hip_atomic_store(&dm[kDmEntry + lane], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else if (!found && lane == 6)
+    __hip_atomic_store(&dm[kDmEntry + 6], w6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __hip_atomic_store(reinterpret_cast<uint64_t*>(&dm[kDmGo]), (static_cast<uint64_t>(gen) << 32) | seq,
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (taken) sys_st(&hstate[1], seq);  // the entry is copied: the host may reuse its door slot
-  if (cmd == kResStop) sys_st(&hstate[0], kResExited);
-  return cmd;
+  if (lane == 0) {
+    __hip_atomic_store(&dm[kDmGo], (static_cast<uint64_t>(gen) << 32) | seq, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    if (found) sys_st(&hstate[1], seq);  // the entry is copied: the host may reuse its door slot
+    if (static_cast<uint32_t>(w6 >> 32) == static_cast<uint32_t>(kResStop)) sys_st(&hstate[0], kResExited);
+  }
+  return w6;
 }
 
 template <class E>
 __global__ __launch_bounds__(kCommThreads) void threshold_resident_kernel(CommArgs a, const ResidentDoor* door,
-                                                                         uint32_t* hstate, uint32_t* dm,
+                                                                         uint32_t* hstate, uint64_t* dm,
                                                                          uint32_t seq, uint32_t gen, uint64_t idle) {
-  __shared__ uint32_t sh_cmd;
-  __shared__ uint64_t sh_ptr[6];
-  __shared__ uint32_t sh_epoch;
+  __shared__ uint64_t sh_ent[8];
   uint32_t* const ctl = a.ctl[0];
   for (;; ++seq) {
-    if (threadIdx.x == 0) {
-      uint32_t cmd = kResStop;
+    if (threadIdx.x < 64) {
+      const int lane = static_cast<int>(threadIdx.x);
+      uint64_t w = 0;
+      bool ok = true;
       if (blockIdx.x == 0) {
-        cmd = resident_door(door, hstate, dm, seq, gen, idle);
+        (void)resident_door(door, hstate, dm, seq, gen, idle);
+        if (lane < 8) w = __hip_atomic_load(&dm[kDmEntry + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         // the leader answers within `idle` plus one round (each bounded by a.timeout)
-        const uint64_t until = wall_ticks() + idle + 2 * a.timeout + 100000000ull;
-        for (;;) {
-          if (__hip_atomic_load(reinterpret_cast<uint64_t*>(&dm[kDmGo]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-              ((static_cast<uint64_t>(gen) << 32) | seq)) {
-            cmd = ld_ctl(&dm[kDmCmd]);
-            break;
+        const uint64_t want = (static_cast<uint64_t>(gen) << 32) | seq;
+        if (lane == 0) {
+          const uint64_t until = wall_ticks() + idle + 2 * a.timeout + 100000000ull;
+          while (__hip_atomic_load(&dm[kDmGo], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+            if (wall_ticks() > until) {
+              __hip_atomic_fetch_or(&ctl[2], ERR_TIMEOUT_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              ok = false;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
           }
-          if (wall_ticks() > until) {
-            __hip_atomic_fetch_or(&ctl[2], ERR_TIMEOUT_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
         }
+        ok = __shfl(ok ? 1 : 0, 0) != 0;
+        if (ok && lane < 8) w = __hip_atomic_load(&dm[kDmEntry + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!ok && lane == 6) w = static_cast<uint64_t>(static_cast<uint32_t>(kResStop)) << 32;
       }
-      if (cmd != kResStop) {
-        for (int i = 0; i < 6; ++i)
-          sh_ptr[i] = static_cast<uint64_t>(ld_ctl(&dm[kDmPtr + 2 * i])) |
-                      (static_cast<uint64_t>(ld_ctl(&dm[kDmPtr + 2 * i + 1])) << 32);
-        sh_epoch = ld_ctl(&dm[kDmEpoch]);
-        // the round's input was written by kernels that finished before the host posted it:
-        // drop what this XCD's caches hold of earlier rounds
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-      }
-      sh_cmd = cmd;
+      if (lane < 8) sh_ent[lane] = w;
+      // the round's input was written by kernels that finished before the host posted it:
+      // drop what this XCD's caches hold of earlier rounds
+      if (lane == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     }
     __syncthreads();
-    const uint32_t cmd = sh_cmd;
-    if (cmd == kResStop) break;
-    const RoundVars rv{reinterpret_cast<const char*>(sh_ptr[0]), reinterpret_cast<char*>(sh_ptr[1]),
-                       reinterpret_cast<int32_t*>(sh_ptr[2]),    reinterpret_cast<int32_t*>(sh_ptr[3]),
-                       reinterpret_cast<uint32_t*>(sh_ptr[4]),   reinterpret_cast<uint32_t*>(sh_ptr[5]),
-                       sh_epoch,                                 cmd == kResCold ? 1 : 0};
+    const uint32_t cmd = static_cast<uint32_t>(sh_ent[6] >> 32);
+    if (cmd == static_cast<uint32_t>(kResStop)) break;  // uniform
+    const RoundVars rv{reinterpret_cast<const char*>(sh_ent[0]), reinterpret_cast<char*>(sh_ent[1]),
+                       reinterpret_cast<int32_t*>(sh_ent[2]),    reinterpret_cast<int32_t*>(sh_ent[3]),
+                       reinterpret_cast<uint32_t*>(sh_ent[4]),   reinterpret_cast<uint32_t*>(sh_ent[5]),
+                       static_cast<uint32_t>(sh_ent[6]),         cmd == static_cast<uint32_t>(kResCold) ? 1 : 0};
     __syncthreads();
     threshold_round<E>(a, rv);
     if (threadIdx.x == 0) {  // the round's counters are reset before any workgroup starts the next
@@ -1243,7 +1237,7 @@ void launch_threshold_resident(const CommArgs& a, int grid, hipStream_t s, DType
                                uint32_t* hstate, uint32_t* dm, uint32_t seq, uint32_t gen, uint64_t idle_ticks) {
   dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
     hipLaunchKernelGGL(threshold_resident_kernel<decltype(tag)>, dim3(grid), dim3(kCommThreads), 0, s, a, door,
-                       hstate, dm, seq, gen, idle_ticks);
+                       hstate, reinterpret_cast<uint64_t*>(dm), seq, gen, idle_ticks);
   });
 }
 
