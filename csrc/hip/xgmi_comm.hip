@@ -1376,7 +1376,6 @@ XgmiComm::ResidentPlan XgmiComm::plan_resident(int64_t n, DType dt, float th_red
                       a.get(), &gx))
     return p;
   if (a->sub > 1 || gx > max_grid || a->delay_rank >= 0) return p;  // split chunks / big rounds / test knobs
-  a->stamps = nullptr;
   p.args = a;
   p.grid = gx;
   p.dt = dt;

@@ -149,9 +149,13 @@ def main() -> None:
             o = job.last_output(k)
             ok = ok and o is not None and torch.equal(o.data, ref)
         row["validated"] = ok
-        ph = phase_summary([b.view(-1, 8).cpu() for b in bufs])
-        row["kernel_last_round_us"] = {f"w{p['worker']}": round(p["end_max"] - p["start_first"], 1) for p in ph
-                                       if "end_max" in p}
+        try:
+            ph = phase_summary([b.view(-1, 8).cpu() for b in bufs])
+            row["kernel_last_round_us"] = {f"w{p['worker']}": round(p["end_max"] - p["start_first"], 1) for p in ph
+                                           if "end_max" in p}
+        except ValueError:  # no stamps written (e.g. a plane without a stamp buffer)
+            row["kernel_last_round_us"] = None
+        row["resident_rounds"] = [p.stats.resident_rounds for p in job.planes]
         tr = json.loads(C.trace.dump_json())
         row["traced"] = not a.no_trace
         if not a.no_trace:
