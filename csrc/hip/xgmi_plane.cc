@@ -539,7 +539,12 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
     }
     const int64_t want = ceil_div(int64_t{32} << 10, chunk_ * es);
     const int64_t room = std::max<int64_t>(1, nch / std::max(1, gx / 4));
-    const int64_t m = std::min(want, room);
+    int64_t m = std::min(want, room);
+    // a block of at most 32 KiB is ONE kernel chunk: one hand-off per peer instead of one per
+    // chunk - each hand-off is a release, a flag and a wait on the round's critical path, and
+    // below 32 KiB there are no bytes to spread over more workgroups (the reference's
+    // default job, 10 floats in 2-float chunks: 3 chunks per block -> 1)
+    if (block_ * es <= (int64_t{32} << 10)) m = nch;
     if (m > 1) {
       chunk_ *= m;
       coarse_ *= static_cast<int>(m);

@@ -153,6 +153,7 @@ def main() -> None:
             ph = phase_summary([b.view(-1, 8).cpu() for b in bufs])
             row["kernel_last_round_us"] = {f"w{p['worker']}": round(p["end_max"] - p["start_first"], 1) for p in ph
                                            if "end_max" in p}
+            row["kernel_phases"] = ph
         except ValueError:  # no stamps written (e.g. a plane without a stamp buffer)
             row["kernel_last_round_us"] = None
         row["resident_rounds"] = [p.stats.resident_rounds for p in job.planes]
