@@ -113,6 +113,20 @@ struct HostPoll {
   }
 };
 
+// The slab's FORCE words (a peer waiting at its lag gate for this rank) are polled at most
+// every 5 us, the first time at once: checked on every spin they doubled the period of the
+// flag polls beside them (two dependent loads per iteration), and a catch-up noticed a few
+// microseconds later costs nothing.
+struct SlabPoll {
+  uint64_t next = 0;
+  __device__ __forceinline__ bool due() {
+    const uint64_t t = wall_ticks();
+    if (t < next) return false;
+    next = t + 500;
+    return true;
+  }
+};
+
 // The first k set bits of `mask` in the order start, start+1, ... (mod P): the reference's
 // rotated peer order (AllreduceWorker.scala:196) as the tie-break among simultaneous arrivals.
 __device__ __forceinline__ uint32_t first_k(uint32_t mask, int k, int start, int P) {
@@ -494,11 +508,16 @@ struct RoundVars {
   uint32_t* done_out;
   uint32_t epoch;  // 0: ctl[4] + 1
   int cold;
+  // the lag gate is known open: every peer finished round epoch - trows (a resident kernel
+  // whose previous round gathered every peer's chunks of epoch - 1, threshold_resident_kernel)
+  int gate_open;
 };
 
 // One round of rank a.rank0 + blockIdx.y by the whole grid.
+// Returns true when this workgroup's round took every peer's reduced chunk it gathers, with
+// nothing forced, cold or given up (the resident kernel's lag-gate shortcut).
 template <class E>
-__device__ __forceinline__ void threshold_round(const CommArgs& a, const RoundVars& rv) {
+__device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVars& rv) {
   constexpr int es = 16 / E::ELEMS;
   __shared__ uint32_t sh_mask;
   __shared__ int sh_flag;
@@ -558,6 +577,8 @@ __device__ __forceinline__ void threshold_round(const CommArgs& a, const RoundVa
   };
   const int nwords = (mine + 63) / 64;
   HostPoll hp;
+  SlabPoll sp;
+  bool clean = !cold;
 
   if (a.delay && r == a.delay_rank) {  // straggler simulation (tests)
     const uint64_t until = wall_ticks() + a.delay;
@@ -649,7 +670,7 @@ __device__ __forceinline__ void threshold_round(const CommArgs& a, const RoundVa
     const int k = static_cast<int>(threadIdx.x);
     const uint32_t target = epoch - static_cast<uint32_t>(a.trows);
     const uint32_t* f = (k < P && k != r) ? prog(a, r, k) : nullptr;
-    bool ok = f == nullptr || reached(ld_flag(f), target);
+    bool ok = rv.gate_open != 0 || f == nullptr || reached(ld_flag(f), target);
     bool asked = false, aborted = false;
     while (!__all(ok)) {
       if (!ok && !asked && blockIdx.x == 0) {
@@ -682,6 +703,7 @@ __device__ __forceinline__ void threshold_round(const CommArgs& a, const RoundVa
   }
   __syncthreads();
   const bool void_round = sh_flag != 0;  // abandoned before the exchange: no peer writes
+  if (void_round) clean = false;
   ps.mark(1);
 
   // Phase 1 - ScatterBlock into the owners' row slots (a cold or void round sends nothing).
@@ -778,7 +800,8 @@ __device__ __forceinline__ void threshold_round(const CommArgs& a, const RoundVa
           if (static_cast<int>(__popc(mask)) >= a.min_reduce || (mask | own) == (own | others)) break;
           // another slice of this chunk decided (or is deciding): adopt its decision
           if (split && __any(s == 0 && dec_this_epoch(dec_load(dec), epoch))) break;
-          if (wave_forced(a, r, epoch, hp.due())) {
+          const bool host = hp.due();
+          if ((host || sp.due()) && wave_forced(a, r, epoch, host)) {
             forced = true;
             break;
           }
@@ -797,6 +820,7 @@ __device__ __forceinline__ void threshold_round(const CommArgs& a, const RoundVa
         }
       }
       if (threadIdx.x == 0) {
+        if (forced || timed_out) clean = false;
         if (timed_out) __hip_atomic_fetch_or(err, ERR_TIMEOUT_SCATTER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         uint64_t d = 0;
         if (split && !dec_claim(dec, epoch, deadline, err, &d)) {  // adopt the chunk's decision
@@ -962,7 +986,7 @@ __device__ __forceinline__ void threshold_round(const CommArgs& a, const RoundVa
     if (progressed) continue;
     if (threadIdx.x < 64) {
       int give = 0;
-      const uint32_t done = ld_ctl(&ctl[3]);
+      const uint32_t done = full ? 0u : ld_ctl(&ctl[3]);  // full rounds: only a force gives up
       if (ref)
         give = (etotal >= static_cast<uint32_t>(a.min_complete) ||
                 etotal + done >= static_cast<uint32_t>(a.min_complete))
@@ -970,7 +994,11 @@ __device__ __forceinline__ void threshold_round(const CommArgs& a, const RoundVa
                    : 0;
       else
         give = done >= static_cast<uint32_t>(a.min_complete) ? 1 : 0;
-      if (!give && (cold || void_round || wave_forced(a, r, epoch, hp.due()))) give = 1;
+      if (!give && (cold || void_round)) give = 1;
+      if (!give) {
+        const bool host = hp.due();
+        if ((host || sp.due()) && wave_forced(a, r, epoch, host)) give = 1;
+      }
       if (!give && wall_ticks() > deadline) {
         if (threadIdx.x == 0)
           __hip_atomic_fetch_or(err, ERR_TIMEOUT_REDUCE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -987,6 +1015,7 @@ __device__ __forceinline__ void threshold_round(const CommArgs& a, const RoundVa
     ps.add(4, tw);
   }
   if (gave_up) {
+    clean = false;
     for (int w = 0; w < nwords; ++w) {
       uint64_t m = pend[w];
       while (m) {
@@ -1044,7 +1073,8 @@ __device__ __forceinline__ void threshold_round(const CommArgs& a, const RoundVa
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t t = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // one workgroup: it is the last (no ticket - a device-scope atomic's round trip)
+    const uint32_t t = G == 1 ? 0u : __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sh_flag = t == static_cast<uint32_t>(G) - 1 ? 1 : 0;
   }
   __syncthreads();
@@ -1080,13 +1110,14 @@ __device__ __forceinline__ void threshold_round(const CommArgs& a, const RoundVa
       if (rv.done_out) st_flag(rv.done_out, epoch);
     }
   }
+  return clean;
 }
 
 template <class E>
 __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   const int y = blockIdx.y;
-  const RoundVars rv{a.in[y], a.out[y], a.counts, a.counts_host, a.err_out, a.done_out, a.epoch_set, a.cold};
-  threshold_round<E>(a, rv);
+  const RoundVars rv{a.in[y], a.out[y], a.counts, a.counts_host, a.err_out, a.done_out, a.epoch_set, a.cold, 0};
+  (void)threshold_round<E>(a, rv);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1169,7 +1200,15 @@ __global__ __launch_bounds__(kCommThreads) void threshold_resident_kernel(CommAr
                                                                          uint32_t* hstate, uint64_t* dm,
                                                                          uint32_t seq, uint32_t gen, uint64_t idle) {
   __shared__ uint64_t sh_ent[8];
+  __shared__ int sh_clean;
   uint32_t* const ctl = a.ctl[0];
+  // the lag gate of round e is open when this single workgroup's round e - 1 gathered every
+  // peer's chunks of e - 1: a peer publishes round e - 1 only after it finished round e - 2
+  // (its rounds run in order) and published its progress before that, so with trows >= 2
+  // every peer is past e - trows. (More workgroups: a peer's workgroup may start e - 1 before
+  // its last workgroup of e - 2 published progress.)
+  uint32_t prev_epoch = 0;
+  bool prev_clean = false;
   for (;; ++seq) {
     if (threadIdx.x < 64) {
       const int lane = static_cast<int>(threadIdx.x);
@@ -1207,9 +1246,16 @@ __global__ __launch_bounds__(kCommThreads) void threshold_resident_kernel(CommAr
     const RoundVars rv{reinterpret_cast<const char*>(sh_ent[0]), reinterpret_cast<char*>(sh_ent[1]),
                        reinterpret_cast<int32_t*>(sh_ent[2]),    reinterpret_cast<int32_t*>(sh_ent[3]),
                        reinterpret_cast<uint32_t*>(sh_ent[4]),   reinterpret_cast<uint32_t*>(sh_ent[5]),
-                       static_cast<uint32_t>(sh_ent[6]),         cmd == static_cast<uint32_t>(kResCold) ? 1 : 0};
+                       static_cast<uint32_t>(sh_ent[6]),         cmd == static_cast<uint32_t>(kResCold) ? 1 : 0,
+                       (prev_clean && gridDim.x == 1 && a.trows >= 2 && static_cast<uint32_t>(sh_ent[6]) == prev_epoch + 1u)
+                           ? 1
+                           : 0};
     __syncthreads();
-    threshold_round<E>(a, rv);
+    const bool clean = threshold_round<E>(a, rv);
+    if (threadIdx.x == 0) sh_clean = clean ? 1 : 0;
+    __syncthreads();
+    prev_clean = sh_clean != 0;
+    prev_epoch = rv.epoch;
     if (threadIdx.x == 0) {  // the round's counters are reset before any workgroup starts the next
       const uint64_t until = wall_ticks() + a.timeout + 100000000ull;
       while (ld_ctl(&ctl[4]) != rv.epoch && wall_ticks() < until) __builtin_amdgcn_s_sleep(1);
