@@ -263,6 +263,7 @@ XgmiRoundPlane::~XgmiRoundPlane() {
     std::lock_guard<std::mutex> g(mu_);
     stop_ = true;
   }
+  stop_flag_.store(true);
   cv_.notify_all();
   if (th_.joinable()) th_.join();
   (void)hipSetDevice(o_.device);
@@ -794,8 +795,11 @@ bool XgmiRoundPlane::launch_resident(int round, const Payload& input, bool cold)
   if (cold) st_.cold++;
   st_.bytes += static_cast<uint64_t>(n * es);
   q_.push_back(std::move(rec));
+  q_len_.fetch_add(1, std::memory_order_release);
   lk.unlock();
-  cv_.notify_all();
+  // the completion thread is polling for it unless it went to sleep (a futex wake costs the
+  // launch path microseconds)
+  if (comp_sleeping_.load(std::memory_order_seq_cst)) cv_.notify_all();
   return true;
 }
 
@@ -887,8 +891,11 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   if (cold) st_.cold++;
   st_.bytes += static_cast<uint64_t>(n * es);
   q_.push_back(std::move(rec));
+  q_len_.fetch_add(1, std::memory_order_release);
   lk.unlock();
-  cv_.notify_all();
+  // the completion thread is polling for it unless it went to sleep (a futex wake costs the
+  // launch path microseconds)
+  if (comp_sleeping_.load(std::memory_order_seq_cst)) cv_.notify_all();
 }
 
 void XgmiRoundPlane::force(int round) {
@@ -924,8 +931,20 @@ void XgmiRoundPlane::completion_loop() {
   for (;;) {
     Rec rec;
     {
+      // the next round is usually launched within microseconds: poll for it (the spin budget)
+      // before sleeping on the condition variable
+      const auto t_idle = std::chrono::steady_clock::now();
+      const auto idle_budget = std::chrono::microseconds(o_.spin_us);
+      for (unsigned i = 0; q_len_.load(std::memory_order_acquire) == 0; ++i) {
+        if ((i & 63) == 0 && (stop_flag_.load(std::memory_order_relaxed) ||
+                              std::chrono::steady_clock::now() - t_idle > idle_budget))
+          break;
+        __builtin_ia32_pause();
+      }
       std::unique_lock<std::mutex> lk(mu_);
+      comp_sleeping_.store(true, std::memory_order_seq_cst);
       cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      comp_sleeping_.store(false, std::memory_order_relaxed);
       if (q_.empty()) return;
       rec = q_.front();  // stays queued until its callback ran (drain waits for that)
     }
@@ -1009,6 +1028,7 @@ void XgmiRoundPlane::completion_loop() {
       std::lock_guard<std::mutex> g(mu_);
       free_slots_.push_back(rec.slot);
       q_.pop_front();
+      q_len_.fetch_sub(1, std::memory_order_relaxed);
       st_.completed++;
     }
     cv_idle_.notify_all();

@@ -177,6 +177,9 @@ class XgmiRoundPlane final : public RoundPlane {
   std::mutex mu_;
   std::condition_variable cv_, cv_idle_;
   std::deque<Rec> q_;
+  std::atomic<int> q_len_{0};              // q_.size(), polled without the lock by the completion thread
+  std::atomic<bool> comp_sleeping_{false};  // the completion thread waits on cv_ (launch must notify)
+  std::atomic<bool> stop_flag_{false};
   bool stop_ = false;
   std::vector<hipEvent_t> events_;
   std::mutex done_mu_;

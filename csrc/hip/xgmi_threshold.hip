@@ -105,12 +105,12 @@ __device__ __forceinline__ bool wave_forced(const CommArgs& a, int r, uint32_t e
 // learning of it within 100 us is enough.
 struct HostPoll {
   uint64_t next = wall_ticks() + 10000;
-  __device__ __forceinline__ bool due() {
-    const uint64_t t = wall_ticks();
+  __device__ __forceinline__ bool due(uint64_t t) {
     if (t < next) return false;
     next = t + 10000;
     return true;
   }
+  __device__ __forceinline__ bool due() { return due(wall_ticks()); }
 };
 
 // The slab's FORCE words (a peer waiting at its lag gate for this rank) are polled at most
@@ -119,8 +119,7 @@ struct HostPoll {
 // microseconds later costs nothing.
 struct SlabPoll {
   uint64_t next = 0;
-  __device__ __forceinline__ bool due() {
-    const uint64_t t = wall_ticks();
+  __device__ __forceinline__ bool due(uint64_t t) {
     if (t < next) return false;
     next = t + 500;
     return true;
@@ -579,6 +578,14 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   HostPoll hp;
   SlabPoll sp;
   bool clean = !cold;
+  // One workgroup: its counts go to the pinned host copy as they are decided (posted writes,
+  // drained by the round-end release) instead of being read back from HBM at the end.
+  int32_t* const counts_direct =
+      (G == 1 && counts != nullptr && rv.counts_host != nullptr) ? rv.counts_host + static_cast<int64_t>(y) * P * a.nch : nullptr;
+  auto cput = [&](int64_t i, int32_t v) {
+    put_count(counts + i, v);
+    if (counts_direct != nullptr) __hip_atomic_store(counts_direct + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  };
 
   if (a.delay && r == a.delay_rank) {  // straggler simulation (tests)
     const uint64_t until = wall_ticks() + a.delay;
@@ -666,11 +673,13 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   // runs. Only a laggard that never runs again (a dead process) turns into ERR_TIMEOUT_LAG -
   // unless the engine abandons the round meanwhile (host abort word: re-initialisation or
   // shutdown): an abandoned round that has not passed its gate writes nothing anywhere.
-  if (threadIdx.x < 64) {
+  if (rv.gate_open) {
+    if (threadIdx.x == 0) sh_flag = 0;
+  } else if (threadIdx.x < 64) {
     const int k = static_cast<int>(threadIdx.x);
     const uint32_t target = epoch - static_cast<uint32_t>(a.trows);
     const uint32_t* f = (k < P && k != r) ? prog(a, r, k) : nullptr;
-    bool ok = rv.gate_open != 0 || f == nullptr || reached(ld_flag(f), target);
+    bool ok = f == nullptr || reached(ld_flag(f), target);
     bool asked = false, aborted = false;
     while (!__all(ok)) {
       if (!ok && !asked && blockIdx.x == 0) {
@@ -772,7 +781,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     uint64_t* const dec = split ? &a.split_dec[c] : nullptr;
     if (void_round) {  // nothing reduced, nothing sent
       if (len > 0) zero_fill<E>(out + (bstart_own + cstart) * es, len);
-      if (threadIdx.x == 0 && counts) put_count(counts + static_cast<int64_t>(r) * a.nch + c, 0);
+      if (threadIdx.x == 0 && counts) cput(static_cast<int64_t>(r) * a.nch + c, 0);
       continue;
     }
     if (threadIdx.x < 64) {
@@ -800,15 +809,17 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
           if (static_cast<int>(__popc(mask)) >= a.min_reduce || (mask | own) == (own | others)) break;
           // another slice of this chunk decided (or is deciding): adopt its decision
           if (split && __any(s == 0 && dec_this_epoch(dec_load(dec), epoch))) break;
-          const bool host = hp.due();
-          if ((host || sp.due()) && wave_forced(a, r, epoch, host)) {
+          // one clock read per spin: s_memrealtime is a scalar memory round trip
+          const uint64_t now = wall_ticks();
+          const bool host = hp.due(now);
+          if ((host || sp.due(now)) && wave_forced(a, r, epoch, host)) {
             forced = true;
             break;
           }
           __builtin_amdgcn_s_sleep(1);
           if (!in_ && f != nullptr) in_ = reached(ld_flag(f), epoch);
           present = static_cast<uint32_t>(__ballot(in_)) & others;
-          if (wall_ticks() > deadline) {
+          if (now > deadline) {
             timed_out = true;
             break;
           }
@@ -873,7 +884,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     if (threadIdx.x < static_cast<unsigned>(P) && static_cast<int>(threadIdx.x) != r)
       st_flag(f2c(a, static_cast<int>(threadIdx.x), row * P + r, c), static_cast<uint32_t>(cnt));
     if (threadIdx.x == 0) {
-      if (counts) put_count(counts + static_cast<int64_t>(r) * a.nch + c, take ? cnt : 0);
+      if (counts) cput(static_cast<int64_t>(r) * a.nch + c, take ? cnt : 0);
       if (!ref && tickets && blen_own - static_cast<int64_t>(c) * a.chunk > 0) add_ctl(&ctl[3], 1u);
     }
     publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : f2(a, k, row * P + r, c); }, P, epoch,
@@ -949,7 +960,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
             if (counts) {
               // an LL chunk's count travels with its payload: stored after the copy below
               if (!(take && ll))
-                put_count(counts + static_cast<int64_t>(j) * a.nch + c,
+                cput(static_cast<int64_t>(j) * a.nch + c,
                           take ? static_cast<int32_t>(ld_flag(f2c(a, r, row * P + j, c))) : 0);
             }
             if (split) dec_publish(dec, epoch, take != 0, 0u);
@@ -970,7 +981,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
             const int32_t cv = ll_copy_out<E>(out + (bstart + cstart) * es,
                                               a.base[r] + rowR + j * slot + static_cast<int64_t>(c) * a.ll_cstride, len,
                                               epoch, deadline, err, counts != nullptr);
-            if (counts != nullptr && threadIdx.x == 0) put_count(counts + static_cast<int64_t>(j) * a.nch + c, cv);
+            if (counts != nullptr && threadIdx.x == 0) cput(static_cast<int64_t>(j) * a.nch + c, cv);
           } else if (take)
             copy_out<E>(out + (bstart + cstart) * es, a.base[r] + rowR + j * slot + cstart * es, len);
           else
@@ -995,11 +1006,12 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       else
         give = done >= static_cast<uint32_t>(a.min_complete) ? 1 : 0;
       if (!give && (cold || void_round)) give = 1;
+      const uint64_t now = wall_ticks();
       if (!give) {
-        const bool host = hp.due();
-        if ((host || sp.due()) && wave_forced(a, r, epoch, host)) give = 1;
+        const bool host = hp.due(now);
+        if ((host || sp.due(now)) && wave_forced(a, r, epoch, host)) give = 1;
       }
-      if (!give && wall_ticks() > deadline) {
+      if (!give && now > deadline) {
         if (threadIdx.x == 0)
           __hip_atomic_fetch_or(err, ERR_TIMEOUT_REDUCE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         give = 1;
@@ -1036,7 +1048,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
           if (threadIdx.x == 0) {
             uint64_t d = 0;
             if (dec_claim(dec, epoch, deadline, err, &d)) {
-              if (counts) put_count(counts + static_cast<int64_t>(j) * a.nch + c, 0);
+              if (counts) cput(static_cast<int64_t>(j) * a.nch + c, 0);
               dec_publish(dec, epoch, false, 0u);
               sh_flag = 0;
             } else {
@@ -1048,7 +1060,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
           take = sh_flag != 0;
           __syncthreads();
         } else if (threadIdx.x == 0 && counts) {
-          put_count(counts + static_cast<int64_t>(j) * a.nch + c, 0);
+          cput(static_cast<int64_t>(j) * a.nch + c, 0);
         }
         if (len > 0) {
           if (take)
@@ -1079,7 +1091,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   }
   __syncthreads();
   const bool last = sh_flag != 0;
-  if (last && counts != nullptr && rv.counts_host != nullptr) {
+  if (last && counts != nullptr && rv.counts_host != nullptr && counts_direct == nullptr) {
     // every workgroup's counts are visible here (sc1 stores drained before their tickets)
     int32_t* dst = rv.counts_host + static_cast<int64_t>(y) * P * a.nch;
     for (int64_t i = threadIdx.x; i < static_cast<int64_t>(P) * a.nch; i += kCommThreads)
@@ -1189,7 +1201,6 @@ __device__ uint64_t resident_door(const ResidentDoor* door, uint32_t* hstate, ui
   if (lane == 0) {
     __hip_atomic_store(&dm[kDmGo], (static_cast<uint64_t>(gen) << 32) | seq, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
-    if (found) sys_st(&hstate[1], seq);  // the entry is copied: the host may reuse its door slot
     if (static_cast<uint32_t>(w6 >> 32) == static_cast<uint32_t>(kResStop)) sys_st(&hstate[0], kResExited);
   }
   return w6;
@@ -1253,6 +1264,9 @@ __global__ __launch_bounds__(kCommThreads) void threshold_resident_kernel(CommAr
     __syncthreads();
     const bool clean = threshold_round<E>(a, rv);
     if (threadIdx.x == 0) sh_clean = clean ? 1 : 0;
+    // the entry is consumed: the host may reuse its door slot (a PCIe write, kept off the
+    // round's critical path - every release waits for the writes before it)
+    if (blockIdx.x == 0 && threadIdx.x == 0) sys_st(&hstate[1], seq);
     __syncthreads();
     prev_clean = sh_clean != 0;
     prev_epoch = rv.epoch;
