@@ -999,17 +999,40 @@ void XgmiRoundPlane::completion_loop() {
     res.epoch = rec.epoch;
     res.round = rec.round;
     res.cold = rec.cold;
-    const int32_t* host = ring_ + static_cast<size_t>(rec.slot) * ring_stride_;
+    const volatile int32_t* host = ring_ + static_cast<size_t>(rec.slot) * ring_stride_;
     const size_t nc = static_cast<size_t>(cfg_.peers) * nch_;
+    // The kernel writes the counts and the error word after its last release, each tagged
+    // with the round epoch (xgmi_threshold.hip host_tag), so they may land after the done
+    // word: wait for every tag (PCIe writes in flight: microseconds at most).
+    const uint32_t tag = static_cast<uint32_t>(rec.round_epoch) & 0xffffffu;
+    auto tagged = [&](size_t i) { return (static_cast<uint32_t>(host[i]) >> 8) == tag; };
+    if (e == hipSuccess) {
+      const auto t_tag = std::chrono::steady_clock::now();
+      for (size_t i = 0; i < nc || !tagged(ring_stride_ - 1);) {
+        if (i < nc && tagged(i)) {
+          ++i;
+          continue;
+        }
+        if (std::chrono::steady_clock::now() - t_tag > std::chrono::seconds(1)) {
+          MXAR_LOG(ERROR, "plane", "round " << rec.round << ": counts / error word never arrived");
+          e = hipErrorLaunchTimeOut;
+          break;
+        }
+        __builtin_ia32_pause();
+      }
+      std::atomic_thread_fence(std::memory_order_acquire);
+    }
+    auto cnt = [&](size_t i) { return static_cast<int32_t>(static_cast<uint32_t>(host[i]) & 0xffu); };
     if (coarse_ == 1) {
-      res.count.assign(host, host + nc);
+      res.count.resize(nc);
+      for (size_t i = 0; i < nc; ++i) res.count[i] = cnt(i);
     } else {  // coarsened at thresholds 1: every reference chunk of a kernel chunk shares its count
       res.count.resize(static_cast<size_t>(cfg_.peers) * nch_ref_);
       for (int j = 0; j < cfg_.peers; ++j)
         for (int c = 0; c < nch_ref_; ++c)
-          res.count[static_cast<size_t>(j) * nch_ref_ + c] = host[static_cast<size_t>(j) * nch_ + c / coarse_];
+          res.count[static_cast<size_t>(j) * nch_ref_ + c] = cnt(static_cast<size_t>(j) * nch_ + c / coarse_);
     }
-    const uint32_t err = static_cast<uint32_t>(host[ring_stride_ - 1]);
+    const uint32_t err = static_cast<uint32_t>(host[ring_stride_ - 1]) & 0xffu;
     res.error = (err & ~err_seen_) | (e != hipSuccess ? 0x80000000u : 0u);
     err_seen_ |= err;
     {

@@ -492,6 +492,10 @@ __device__ __forceinline__ bool last_slice(uint32_t* ctr, int S, int* sh) {
 
 // A per-chunk count: a `sc1` store (leaves this XCD's L2), read back by the round's last
 // workgroup with `sc1` loads after the ticket count - no release / acquire needed.
+// A host word of round `epoch` (xgmi_plane.cc reads them): value in the low 8 bits (counts
+// <= 32, error bits < 256), the epoch's low 24 bits above.
+__device__ __forceinline__ uint32_t host_tag(uint32_t epoch, uint32_t v) { return (epoch << 8) | (v & 0xffu); }
+
 __device__ __forceinline__ void put_count(int32_t* p, int32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -578,13 +582,13 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   HostPoll hp;
   SlabPoll sp;
   bool clean = !cold;
-  // One workgroup: its counts go to the pinned host copy as they are decided (posted writes,
-  // drained by the round-end release) instead of being read back from HBM at the end.
-  int32_t* const counts_direct =
-      (G == 1 && counts != nullptr && rv.counts_host != nullptr) ? rv.counts_host + static_cast<int64_t>(y) * P * a.nch : nullptr;
+  // One workgroup (then nch = 1, P <= 2): it also keeps its counts in LDS, so the round end
+  // does not read them back from HBM.
+  __shared__ int32_t sh_cnt[2];
+  const bool counts_lds = G == 1 && P <= 2 && a.nch == 1;
   auto cput = [&](int64_t i, int32_t v) {
     put_count(counts + i, v);
-    if (counts_direct != nullptr) __hip_atomic_store(counts_direct + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (counts_lds) sh_cnt[i] = v;
   };
 
   if (a.delay && r == a.delay_rank) {  // straggler simulation (tests)
@@ -1091,14 +1095,6 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   }
   __syncthreads();
   const bool last = sh_flag != 0;
-  if (last && counts != nullptr && rv.counts_host != nullptr && counts_direct == nullptr) {
-    // every workgroup's counts are visible here (sc1 stores drained before their tickets)
-    int32_t* dst = rv.counts_host + static_cast<int64_t>(y) * P * a.nch;
-    for (int64_t i = threadIdx.x; i < static_cast<int64_t>(P) * a.nch; i += kCommThreads)
-      __hip_atomic_store(dst + i, __hip_atomic_load(counts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __syncthreads();
-  }
   if (threadIdx.x == 0) {
     if (last) {
       __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1110,15 +1106,30 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       // resets land first
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(&ctl[4], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (rv.err_out)  // the protocol plane reads it from pinned memory after the round's event
-        __hip_atomic_store(rv.err_out, ld_ctl(err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  if (last) {
+    // Host words AFTER the release, each tagged with the round epoch (host_tag): the host
+    // takes them once the done word and every tag name the round, so no fence waits for
+    // their PCIe write acknowledgements (a release before the done word did, on the round's
+    // critical path). The counts: every workgroup's sc1 stores drained before its ticket.
+    if (counts != nullptr && rv.counts_host != nullptr) {
+      int32_t* dst = rv.counts_host + static_cast<int64_t>(y) * P * a.nch;
+      for (int64_t i = threadIdx.x; i < static_cast<int64_t>(P) * a.nch; i += kCommThreads) {
+        const int32_t v = counts_lds ? sh_cnt[i] : __hip_atomic_load(counts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(dst + i, static_cast<int32_t>(host_tag(epoch, static_cast<uint32_t>(v))), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    if (threadIdx.x == 0) {
+      if (rv.err_out) __hip_atomic_store(rv.err_out, host_tag(epoch, ld_ctl(err)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       for (int k = 0; k < P; ++k)
         if (k != r) st_flag(prog(a, k, r), epoch);
       // the round's completion word: every workgroup has passed its ticket and every output
-      // store was write-through (zero_fill, reduce_masked with wt_out), so the host may hand
-      // the output on at once, before the kernel itself ends (xgmi_plane.cc)
+      // store was write-through (zero_fill, reduce_masked with wt_out) before the release
+      // above, so the host may hand the output on at once, before the kernel itself ends
       if (rv.done_out) st_flag(rv.done_out, epoch);
     }
   }
