@@ -1086,6 +1086,9 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   // is relaxed (an acq_rel one was an L2 writeback + invalidate per workgroup on the round's
   // tail): the only data the last workgroup reads back are the counts, stored `sc1`
   // (put_count) before the drain and loaded `sc1` - the guide's fence-free hand-off form.
+  // the error word, loaded before the drain so its latency hides behind it (one workgroup:
+  // nobody else can raise it later; with more, the last one reads it again after its ticket)
+  const uint32_t errv = (threadIdx.x == 0 && rv.err_out != nullptr) ? ld_ctl(err) : 0u;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1097,14 +1100,18 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   const bool last = sh_flag != 0;
   if (threadIdx.x == 0) {
     if (last) {
-      __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ctl[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ctl[5], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ctl[6], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ctl[7], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // a resident kernel's workgroups start the next round once ctl[4] names this one: the
-      // resets land first
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // one workgroup at full thresholds touched none of the round counters (no ticket, no
+      // completion count, no snapshot): nothing to reset, and no other workgroup waits on ctl[4]
+      if (!(G == 1 && full)) {
+        __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctl[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctl[5], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctl[6], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctl[7], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // a resident kernel's workgroups start the next round once ctl[4] names this one: the
+        // resets land first
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       __hip_atomic_store(&ctl[4], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1124,7 +1131,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       }
     }
     if (threadIdx.x == 0) {
-      if (rv.err_out) __hip_atomic_store(rv.err_out, host_tag(epoch, ld_ctl(err)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (rv.err_out) __hip_atomic_store(rv.err_out, host_tag(epoch, G == 1 ? errv : ld_ctl(err)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       for (int k = 0; k < P; ++k)
         if (k != r) st_flag(prog(a, k, r), epoch);
       // the round's completion word: every workgroup has passed its ticket and every output
