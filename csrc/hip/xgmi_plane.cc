@@ -676,13 +676,17 @@ std::shared_ptr<void> XgmiRoundPlane::resident_out(size_t bytes, std::shared_ptr
     hip_check(hipEventRecord(ev, nullptr), "hipEventRecord(release)");
     rel_pend_.emplace_back(ev, std::move(ptrs));
   }
-  while (!rel_pend_.empty() && hipEventQuery(rel_pend_.front().first) == hipSuccess) {
+  while (!rel_pend_.empty()) {
+    const hipError_t q = hipEventQuery(rel_pend_.front().first);
+    if (q != hipSuccess) {
+      (void)hipGetLastError();  // hipErrorNotReady is sticky-free, but keep the error state clean
+      break;
+    }
     std::lock_guard<std::mutex> g(rel_->mu);
-    for (void* q : rel_pend_.front().second) rel_->free.push_back(q);
+    for (void* p : rel_pend_.front().second) rel_->free.push_back(p);
     rel_spare_.push_back(rel_pend_.front().first);
     rel_pend_.pop_front();
   }
-  (void)hipGetLastError();
   bool grow = false;
   {
     std::lock_guard<std::mutex> g(rel_->mu);
