@@ -19,6 +19,11 @@
 //     (roundBase + r - startRound + 1), per-chunk counts and the error word copied to
 //     pinned host memory, a completion event; a completion thread hands each finished
 //     round to the worker in launch order.
+//   * resident rounds (<= 64 KiB, XgmiPlaneOptions::resident_max): instead of one launch per
+//     round, the round is written to a pinned door ring that a resident threshold kernel
+//     polls (XgmiComm::launch_resident); the kernel leaves after an idle spell or when the
+//     plane needs its stream (re-initialisation, an input that must be staged on the stream)
+//     and the next round launches it again. Same round semantics, same done word.
 //   * force (catch-up): raises a pinned host word the kernel polls; rounds <= it complete
 //     with what has arrived. Peers ahead by more than maxLag force us through our slab.
 #pragma once
