@@ -711,8 +711,10 @@ bool XgmiRoundPlane::launch_resident(int round, const Payload& input, bool cold)
     // only inputs the kernel can read now: device memory of this GPU, the plane's dtype, its
     // producer finished (the launch path orders the rest on the plane stream)
     auto* dp = input ? dynamic_cast<const DevicePayload*>(input.get()) : nullptr;
+    // (a producer on the plane stream itself may be queued behind the resident kernel: that
+    // input takes the launch path, which orders it on the stream)
     if (dp == nullptr || static_cast<int64_t>(dp->size()) != n || dp->device() != o_.device ||
-        dp->dtype() != static_cast<int>(o_.dtype))
+        dp->dtype() != static_cast<int>(o_.dtype) || dp->stream() == stream_)
       return false;
     // a producer still running (e.g. the demo source's fill kernel) gets a short host wait:
     // a few microseconds for a round this small, cheaper than leaving the resident kernel

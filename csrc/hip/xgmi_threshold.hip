@@ -337,9 +337,20 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
   const bool vec = al16(own_in) && al16(S) && (own_out == nullptr || al16(own_out)) && (roff & 15) == 0;
   if (!vec) {
     for (int64_t t = threadIdx.x; t < len; t += kCommThreads) {
+      // every source's load issues before the first add (one memory latency per 8 sources,
+      // not one per source); the fixed order s = 0..P-1 keeps the sum bit-exact (+0.f for a
+      // source outside the mask is an identity: acc starts at +0 and is never -0)
       float acc = 0.f;
-      for (int s = 0; s < P; ++s)
-        if ((mask >> s) & 1u) acc += ld_scalar_nt<E>(slab_rsrc(s == r ? own_in : S + s * slot), t);
+      for (int s0 = 0; s0 < P; s0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int s = s0 + q;
+          v[q] = (s < P && ((mask >> s) & 1u)) ? ld_scalar_nt<E>(slab_rsrc(s == r ? own_in : S + s * slot), t) : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc += v[q];
+      }
       acc *= scale;
       for (int k = 0; k < P; ++k) {
         if (k == r) {
@@ -1102,7 +1113,8 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     if (last) {
       // one workgroup at full thresholds touched none of the round counters (no ticket, no
       // completion count, no snapshot): nothing to reset, and no other workgroup waits on ctl[4]
-      if (!(G == 1 && full)) {
+      const bool solo = G == 1 && full;
+      if (!solo) {
         __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&ctl[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&ctl[5], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1111,10 +1123,13 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         // a resident kernel's workgroups start the next round once ctl[4] names this one: the
         // resets land first
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&ctl[4], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      __hip_atomic_store(&ctl[4], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // solo: only this thread reads ctl[4] (the resident loop), so the store need not be
+      // drained by the release above
+      if (solo) __hip_atomic_store(&ctl[4], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if (last) {
@@ -1181,9 +1196,10 @@ __device__ __forceinline__ void sys_st(uint32_t* p, uint32_t v) {
 }
 
 // Leader wave (workgroup 0, wave 0): waits for entry `seq`, copies it into dm and publishes
-// go. Returns the entry's word 6 (epoch | cmd << 32) in every lane; cmd kResStop = leave.
+// go (more than one workgroup). Returns the lane's entry word (lanes < 8; word 6 = epoch |
+// cmd << 32, cmd kResStop = leave).
 __device__ uint64_t resident_door(const ResidentDoor* door, uint32_t* hstate, uint64_t* dm, uint32_t seq,
-                                  uint32_t gen, uint64_t idle) {
+                                  uint32_t gen, uint64_t idle, bool broadcast) {
   const int lane = static_cast<int>(threadIdx.x);
   const ResidentDoor* d = door + seq % kResidentDoors;
   int found = 1;
@@ -1211,17 +1227,17 @@ __device__ uint64_t resident_door(const ResidentDoor* door, uint32_t* hstate, ui
     w = __hip_atomic_load(reinterpret_cast<const uint64_t*>(d) + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   uint64_t w6 = __shfl(w, 6);
   if (!found) w6 = static_cast<uint64_t>(static_cast<uint32_t>(kResStop)) << 32;
-  if (found && lane < 8)
-    __hip_atomic_store(&dm[kDmEntry + lane], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else if (!found && lane == 6)
-    __hip_atomic_store(&dm[kDmEntry + 6], w6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) {
-    __hip_atomic_store(&dm[kDmGo], (static_cast<uint64_t>(gen) << 32) | seq, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    if (static_cast<uint32_t>(w6 >> 32) == static_cast<uint32_t>(kResStop)) sys_st(&hstate[0], kResExited);
+  if (!found && lane == 6) w = w6;
+  if (broadcast) {
+    if (lane < 8 && (found || lane == 6))
+      __hip_atomic_store(&dm[kDmEntry + lane], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+      __hip_atomic_store(&dm[kDmGo], (static_cast<uint64_t>(gen) << 32) | seq, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
-  return w6;
+  if (lane == 0 && static_cast<uint32_t>(w6 >> 32) == static_cast<uint32_t>(kResStop)) sys_st(&hstate[0], kResExited);
+  return w;
 }
 
 template <class E>
@@ -1244,8 +1260,8 @@ __global__ __launch_bounds__(kCommThreads) void threshold_resident_kernel(CommAr
       uint64_t w = 0;
       bool ok = true;
       if (blockIdx.x == 0) {
-        (void)resident_door(door, hstate, dm, seq, gen, idle);
-        if (lane < 8) w = __hip_atomic_load(&dm[kDmEntry + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // one workgroup: the entry straight from the door (no device hand-off)
+        w = resident_door(door, hstate, dm, seq, gen, idle, gridDim.x > 1);
       } else {
         // the leader answers within `idle` plus one round (each bounded by a.timeout)
         const uint64_t want = (static_cast<uint64_t>(gen) << 32) | seq;

@@ -27,9 +27,11 @@ namespace mxar {
 
 namespace {
 // Round inputs of the iota source: a few device buffers reused round after round. A buffer
-// comes back when the plane drops the round's input (after the round's completion word), and
-// the next fill of it is ordered behind that round's kernel anyway: fills run on the plane's
-// own stream, so no event and no allocator call sits on the round path.
+// comes back when the plane drops the round's input (after the round's completion word: the
+// kernel has read it), so its next fill cannot overwrite data a round still reads. Fills run
+// on a stream of the source's own, not the plane's: a small round's kernel stays resident on
+// the plane stream between rounds (xgmi_plane.cc launch_resident), and a fill queued behind
+// it would not run until it left; the plane waits for the fill's stream instead.
 struct InputPool {
   std::mutex mu;
   std::vector<void*> free;
@@ -55,7 +57,10 @@ GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag,
   GpuWorkerParts p;
   auto plane = make_xgmi_plane(o);
   p.plane = plane;
-  const hipStream_t s = plane->stream();
+  hipStream_t s = nullptr;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+    throw std::runtime_error("mxar-gpu: no stream on device " + std::to_string(device));
+  auto src_stream = std::shared_ptr<void>(s, [](void* q) { (void)hipStreamDestroy(static_cast<hipStream_t>(q)); });
   if (const char* path = std::getenv("MXAR_PLANE_STAMPS")) {
     // study knob: phase stamps of this worker's round kernels (kPhaseSlots u64 per workgroup,
     // s_memrealtime - one clock for every process on the GPU), the last round's written as one
@@ -94,8 +99,9 @@ GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag,
     void* mem = nullptr;
     if (hipMalloc(&mem, bytes) != hipSuccess) throw std::runtime_error("mxar-gpu: hipMalloc failed");
     launch_fill_iota(mem, size, 0.0, o.dtype, s);
+    if (hipStreamSynchronize(s) != hipSuccess) throw std::runtime_error("mxar-gpu: source fill failed");
     std::shared_ptr<void> owner(mem, [](void* q) { (void)hipFree(q); });
-    auto payload = std::make_shared<DevicePayload>(owner, 0, static_cast<size_t>(size), device, s, nullptr, dtype);
+    auto payload = std::make_shared<DevicePayload>(owner, 0, static_cast<size_t>(size), device, nullptr, nullptr, dtype);
     p.source = [payload](const AllReduceInputRequest&) { return AllReduceInput{payload}; };
     return p;
   }
@@ -103,7 +109,7 @@ GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag,
   // fill_iota kernel on the plane's stream into a pooled buffer
   auto pool = std::make_shared<InputPool>();
   const DType dt = o.dtype;
-  p.source = [device, size, s, bytes, pool, dt, dtype](const AllReduceInputRequest& r) {
+  p.source = [device, size, s, src_stream, bytes, pool, dt, dtype](const AllReduceInputRequest& r) {
     void* mem = nullptr;
     {
       std::lock_guard<std::mutex> g(pool->mu);
