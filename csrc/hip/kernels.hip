@@ -9,6 +9,9 @@
 // Grids are grid-stride, capped at 8 workgroups per CU (cdna_hip_programming.md Guideline 11).
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
+
 #include <algorithm>
 
 #include "device_common.h"
@@ -473,17 +476,25 @@ __global__ void queue_probe_set(int* flag) {
 }
 
 bool streams_independent(hipStream_t a, hipStream_t b, double timeout_ms) {
-  int* mem = nullptr;
-  hip_check(hipMalloc(reinterpret_cast<void**>(&mem), 128), "hipMalloc(queue probe)");
-  hip_check(hipMemset(mem, 0, 128), "hipMemset(queue probe)");
+  // one probe word pair per device, allocated once: hipFree would synchronise the device,
+  // i.e. wait for every kernel on it (another plane's round, a resident kernel)
+  static std::mutex mu;
+  static std::map<int, int*> words;
+  int dev = 0;
+  hip_check(hipGetDevice(&dev), "hipGetDevice(queue probe)");
+  std::lock_guard<std::mutex> g(mu);
+  int*& mem = words[dev];
+  if (mem == nullptr) hip_check(hipMalloc(reinterpret_cast<void**>(&mem), 128), "hipMalloc(queue probe)");
+  hip_check(hipMemsetAsync(mem, 0, 128, a), "hipMemsetAsync(queue probe)");
+  hip_check(hipStreamSynchronize(a), "hipStreamSynchronize(queue probe)");
   hipLaunchKernelGGL(queue_probe_spin, dim3(1), dim3(64), 0, a, mem, mem + 16,
                      static_cast<uint64_t>(timeout_ms * 1e5));  // s_memrealtime: 100 MHz
   hipLaunchKernelGGL(queue_probe_set, dim3(1), dim3(64), 0, b, mem);
   hip_check(hipStreamSynchronize(a), "hipStreamSynchronize(queue probe)");
   hip_check(hipStreamSynchronize(b), "hipStreamSynchronize(queue probe)");
   int seen = 0;
-  hip_check(hipMemcpy(&seen, mem + 16, 4, hipMemcpyDeviceToHost), "hipMemcpy(queue probe)");
-  hip_check(hipFree(mem), "hipFree(queue probe)");
+  hip_check(hipMemcpyAsync(&seen, mem + 16, 4, hipMemcpyDeviceToHost, a), "hipMemcpyAsync(queue probe)");
+  hip_check(hipStreamSynchronize(a), "hipStreamSynchronize(queue probe)");
   return seen != 0;
 }
 

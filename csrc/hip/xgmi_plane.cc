@@ -50,7 +50,10 @@ hipStream_t independent_plane_stream(int device, int priority, bool* probed_ok) 
   std::vector<hipStream_t> rejected;  // kept alive while probing: HIP would deal the same queue again
   hipStream_t s = nullptr;
   bool ok = false;
-  for (int attempt = 0; attempt < 16 && !ok; ++attempt) {
+  // HIP deals new streams onto its queues by its own policy (long-lived streams of other
+  // users weigh in), so a queue can take many candidates to come round: up to 64
+  int tried = 0;
+  for (int attempt = 0; attempt < 64 && !ok; ++attempt, ++tried) {
     hip_check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority), "hipStreamCreate(plane)");
     // Only IDLE plane streams are probed: a busy one may hold a round kernel that waits for
     // this very worker (a replacement joining a running job), and a probe queued behind it
@@ -58,7 +61,7 @@ hipStream_t independent_plane_stream(int device, int priority, bool* probed_ok) 
     ok = true;
     for (const auto& e : g_plane_streams)
       if (ok && e.first == device && hipStreamQuery(e.second) == hipSuccess)
-        ok = streams_independent(e.second, s) && streams_independent(s, e.second);
+        ok = streams_independent(e.second, s, 20.0) && streams_independent(s, e.second, 20.0);
     if (!ok) rejected.push_back(s);
   }
   for (hipStream_t r : rejected)
@@ -66,9 +69,10 @@ hipStream_t independent_plane_stream(int device, int priority, bool* probed_ok) 
   if (!ok) {  // no independent queue left: keep the last candidate, say so
     hip_check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority), "hipStreamCreate(plane)");
     std::fprintf(stderr,
-                 "[mxar] WARNING: no hardware queue independent of the other plane streams on device %d; "
-                 "co-located round kernels may wait out their deadline (raise GPU_MAX_HW_QUEUES)\n",
-                 device);
+                 "[mxar] WARNING: no hardware queue independent of the other %d plane streams on device %d "
+                 "after %d candidates; co-located round kernels may wait out their deadline (raise "
+                 "GPU_MAX_HW_QUEUES)\n",
+                 static_cast<int>(g_plane_streams.size()), device, tried);
   }
   g_plane_streams.emplace_back(device, s);
   *probed_ok = ok;
