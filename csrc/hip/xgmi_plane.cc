@@ -48,6 +48,23 @@ hipStream_t independent_plane_stream(int device, int priority, bool* probed_ok) 
     return s;
   }
   std::vector<hipStream_t> rejected;  // kept alive while probing: HIP would deal the same queue again
+  // Only IDLE plane streams are probed: a busy one may hold a round kernel that waits for
+  // this very worker (a replacement joining a running job), and a probe queued behind it
+  // would wait out that round's deadline. A busy one (a round in flight, or a resident kernel
+  // in its idle spell) is given up to 20 ms to go idle, so a job whose rounds leave gaps is
+  // probed too.
+  std::vector<hipStream_t> idle;
+  for (const auto& e : g_plane_streams) {
+    if (e.first != device) continue;
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t q = hipStreamQuery(e.second);
+    while (q == hipErrorNotReady && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(20)) {
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+      q = hipStreamQuery(e.second);
+    }
+    (void)hipGetLastError();
+    if (q == hipSuccess) idle.push_back(e.second);
+  }
   hipStream_t s = nullptr;
   bool ok = false;
   // HIP deals new streams onto its queues by its own policy (long-lived streams of other
@@ -55,13 +72,9 @@ hipStream_t independent_plane_stream(int device, int priority, bool* probed_ok) 
   int tried = 0;
   for (int attempt = 0; attempt < 64 && !ok; ++attempt, ++tried) {
     hip_check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority), "hipStreamCreate(plane)");
-    // Only IDLE plane streams are probed: a busy one may hold a round kernel that waits for
-    // this very worker (a replacement joining a running job), and a probe queued behind it
-    // would wait out that round's deadline.
     ok = true;
-    for (const auto& e : g_plane_streams)
-      if (ok && e.first == device && hipStreamQuery(e.second) == hipSuccess)
-        ok = streams_independent(e.second, s, 20.0) && streams_independent(s, e.second, 20.0);
+    for (hipStream_t p : idle)
+      if (ok) ok = streams_independent(p, s, 20.0) && streams_independent(s, p, 20.0);
     if (!ok) rejected.push_back(s);
   }
   for (hipStream_t r : rejected)

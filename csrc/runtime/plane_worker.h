@@ -41,6 +41,10 @@ class PlaneWorkerActor final : public Actor {
   PlaneWorkerActor(DataSource source, DataSink sink, std::shared_ptr<RoundPlane> plane);
   ~PlaneWorkerActor() override;
   void receive(Envelope& env, ActorContext& ctx) override;
+  // a stopped worker (PoisonPill, downed) abandons its rounds in flight at once: its round
+  // kernel would otherwise wait out its deadline for peers that moved on without it, holding
+  // its hardware queue (and a resident kernel) meanwhile
+  void post_stop(ActorContext&) override { plane_->abort(0x7fffffff); }
   std::string kind() const override { return "plane-worker"; }
 
   int id() const { return id_; }
