@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Randomised soak of the protocol round engine (PlaneJob: master + P plane workers on one GPU),
+resident rounds included: every job draws P, size (both sides of the resident-round limit),
+maxChunkSize, dtype, maxLag, round count and a source kind (per-round iota fill, a static
+tensor, a slow source whose gaps make the resident kernel leave and come back), runs at
+thresholds 1 and checks EVERY round's output of every worker against the exact sum. One JSON
+line per job; the first failing job ends the soak (its line says why).
+
+    python tools/plane_soak.py --seconds 240 --seed 1 > gpurun_out/plane_soak.jsonl
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=240.0)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--max-jobs", type=int, default=10_000)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+
+    from akka_allreduce_1_amd.engine import PlaneJob, iota_source
+
+    dev = torch.device("cuda", 0)
+    rng = random.Random(args.seed)
+    t_end = time.monotonic() + args.seconds
+    totals = {"jobs": 0, "rounds": 0, "resident_rounds": 0, "resident_launches": 0}
+    for j in range(args.max_jobs):
+        if time.monotonic() > t_end:
+            break
+        P = rng.choice([2, 2, 3, 4])
+        n = rng.choice([10, 37, 1000, 4096, 16384, 30000, 100_000, 300_000])
+        chunk = max(1, rng.choice([2, 64, 512, 1024, 4096, n]))
+        dtype = rng.choice([torch.float32, torch.float32, torch.bfloat16])
+        lag = rng.choice([0, 1, 2])
+        rounds = rng.randint(5, 60)
+        kind = rng.choice(["iota", "iota", "static", "slow"])
+        es = 4 if dtype == torch.float32 else 2
+        cfg = {"job": j, "P": P, "n": n, "chunk": chunk, "dtype": str(dtype).replace("torch.", ""), "max_lag": lag,
+               "rounds": rounds, "source": kind, "resident_eligible": n * es <= 65536}
+        if kind == "static":
+            stat = [(torch.arange(n, dtype=torch.float64) + 1000.0 * k).to(dtype).to(dev) for k in range(P)]
+            sources = stat
+        elif kind == "slow":
+            def slow(k, d=rng.uniform(0.0005, 0.003)):
+                base = iota_source(n, dev, dtype, 1000.0 * k)
+
+                def f(req):
+                    time.sleep(d)
+                    return base(req)
+                return f
+            sources = [slow(k) for k in range(P)]
+        else:
+            sources = [iota_source(n, dev, dtype, 1000.0 * k) for k in range(P)]
+        row = dict(cfg)
+        job = None
+        t0 = time.perf_counter()
+        try:
+            job = PlaneJob(P, n, max_chunk_size=chunk, max_lag=lag, max_round=rounds - 1, dtype=dtype, timeout_s=20.0,
+                           sources=sources)
+            job.run(timeout=120)
+            ar = torch.arange(n, dtype=torch.float64)
+            bad = None
+            for it in range(rounds):
+                if kind == "static":
+                    parts = [(ar + 1000.0 * k).to(dtype).double() for k in range(P)]
+                else:
+                    parts = [(ar + it + 1000.0 * k).to(dtype).double() for k in range(P)]
+                ref = sum(parts).numpy()
+                for k in range(P):
+                    data, counts = job.outputs[k][it]
+                    got = data.double().cpu().numpy()
+                    tol = 0.0 if dtype == torch.float32 else 2.0 ** -8
+                    if not np.all(np.abs(got - ref) <= np.abs(ref) * tol) or any(c != P for c in counts):
+                        bad = {"worker": k, "round": it, "max_err": float(np.max(np.abs(got - ref))),
+                               "counts_ok": all(c == P for c in counts)}
+                        break
+                if bad:
+                    break
+            st = [p.stats for p in job.planes]
+            errs = sum(job.system.plane_worker_state(w)["stats"]["plane_errors"] for w in job.workers)
+            row.update(ok=bad is None and errs == 0, plane_errors=errs, first_bad=bad,
+                       resident_rounds=sum(s.resident_rounds for s in st),
+                       resident_launches=sum(s.resident_launches for s in st),
+                       resident_parks=sum(s.resident_parks for s in st), wall_s=round(time.perf_counter() - t0, 3))
+            totals["jobs"] += 1
+            totals["rounds"] += rounds * P
+            totals["resident_rounds"] += row["resident_rounds"]
+            totals["resident_launches"] += row["resident_launches"]
+        except Exception as e:  # noqa: BLE001
+            row.update(ok=False, error=repr(e)[:600])
+        finally:
+            if job is not None:
+                job.shutdown()
+        print(json.dumps(row), flush=True)
+        if not row.get("ok"):
+            break
+    print(json.dumps({"summary": totals, "seed": args.seed}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
