@@ -88,12 +88,12 @@ def main() -> None:
                         break
                 if bad:
                     break
-            st = [p.stats for p in job.planes]
+            # plain ints: a stats object keeps its plane (and the plane's hardware queue) alive
+            res = [(p.stats.resident_rounds, p.stats.resident_launches, p.stats.resident_parks) for p in job.planes]
             errs = sum(job.system.plane_worker_state(w)["stats"]["plane_errors"] for w in job.workers)
             row.update(ok=bad is None and errs == 0, plane_errors=errs, first_bad=bad,
-                       resident_rounds=sum(s.resident_rounds for s in st),
-                       resident_launches=sum(s.resident_launches for s in st),
-                       resident_parks=sum(s.resident_parks for s in st), wall_s=round(time.perf_counter() - t0, 3))
+                       resident_rounds=sum(r[0] for r in res), resident_launches=sum(r[1] for r in res),
+                       resident_parks=sum(r[2] for r in res), wall_s=round(time.perf_counter() - t0, 3))
             totals["jobs"] += 1
             totals["rounds"] += rounds * P
             totals["resident_rounds"] += row["resident_rounds"]
@@ -106,6 +106,8 @@ def main() -> None:
         print(json.dumps(row), flush=True)
         if not row.get("ok"):
             break
+        job = None
+        sources = None
     print(json.dumps({"summary": totals, "seed": args.seed}), flush=True)
 
 
