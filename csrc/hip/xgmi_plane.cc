@@ -162,6 +162,8 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   // form; ~2-3 us of hipEventRecord on every launch, profiles/round3/api_cost.json)
   if (const char* e = std::getenv("MXAR_PLANE_EVENTS")) event_confirm_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("MXAR_PLANE_COARSEN")) coarsen_full_ = std::atoi(e) != 0;  // A/B knob
+  if (const char* q = std::getenv("GPU_MAX_HW_QUEUES"); q != nullptr && std::atoi(q) == 1)
+    o_.resident_max = 0;  // one hardware queue per process: a resident kernel would hold it for every stream
   if (const char* e = std::getenv("MXAR_PLANE_RESIDENT")) o_.resident_max = std::atoll(e);
   if (const char* e = std::getenv("MXAR_PLANE_RESIDENT_IDLE_US")) o_.resident_idle_us = std::atof(e);
   const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
