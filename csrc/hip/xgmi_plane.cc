@@ -788,7 +788,14 @@ bool XgmiRoundPlane::launch_resident(int round, const Payload& input, bool cold)
                             "{\"worker\":" + std::to_string(cfg_.id) + ",\"bytes\":" + std::to_string(n * es) + "}");
     });
     const uint32_t seq = res_seq_;
-    bool taken = res_on_ && post_door(e);
+    bool taken = false;
+    try {
+      taken = res_on_ && post_door(e);
+    } catch (...) {
+      std::lock_guard<std::mutex> g(mu_);
+      free_slots_.push_back(rec.slot);
+      throw;
+    }
     if (!taken) {
       // no kernel (first resident round, or it left after an idle spell): launch one that
       // starts at this entry

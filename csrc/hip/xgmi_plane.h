@@ -106,6 +106,8 @@ class XgmiRoundPlane final : public RoundPlane {
   // Phase-stamp buffer for this plane's round kernels (study knob, XgmiComm::set_phase_stamps);
   // kept across re-initialisations. Call between rounds.
   void set_phase_stamps(uint64_t* buf, int64_t slots) {
+    park_resident();  // a resident kernel holds the old launch arguments
+    rplan_tried_ = false;
     stamps_ = buf;
     stamp_slots_ = buf ? slots : 0;
     if (comm_) comm_->set_phase_stamps(stamps_, stamp_slots_);
