@@ -13,6 +13,7 @@ block and gather the peers' reduced blocks locally, in small grids.
 """
 from __future__ import annotations
 
+import os
 from typing import Sequence
 
 import torch
@@ -53,6 +54,14 @@ class SdmaCommunicator:
         errs = [e for _, e in hs if e]
         if errs:
             raise CommError("SdmaCommunicator setup failed: " + "; ".join(errs))
+        # Engine copies into ANOTHER GPU's memory have not run on a multi-GPU node yet (the
+        # rehearsals put every rank on one GPU): until they have, they are opt-in - a fault
+        # there would take the process down rather than raise. Every rank sees the same
+        # handles, so every rank decides the same way. (handle = IPC handle + 8-B PCI location)
+        locs = {bytes(x)[-8:] for x, _ in hs}
+        if len(locs) > 1 and os.environ.get("MXAR_SDMA_XDEV", "0") != "1":
+            raise CommError("SdmaCommunicator across GPUs is opt-in until validated on a multi-GPU node "
+                            "(MXAR_SDMA_XDEV=1)")
         try:
             c.connect([x for x, _ in hs])
         except Exception as e:  # noqa: BLE001
