@@ -68,9 +68,22 @@ struct ResidentDoor {
   uint32_t epoch;
   int32_t cmd;  // kResRound / kResCold / kResStop
   uint32_t seq;
-  uint32_t pad;
+  uint32_t check;  // door_check(entry): the kernel reads the whole entry in one 64-B load and
+                   // takes it only when the check matches (no second read after the sequence word)
 };
 constexpr int kResidentDoors = 64;
+// A mix of the entry's words and its sequence number (host and device compute the same).
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline uint32_t door_check(const uint32_t* w14, uint32_t seq) {
+  uint32_t h = seq * 0x9E3779B1u + 0x7F4A7C15u;
+  for (int i = 0; i < 14; ++i) {
+    h = (h ^ w14[i]) * 0x85EBCA6Bu;
+    h ^= h >> 13;
+  }
+  return h ^ (h >> 16);
+}
 enum : int32_t { kResRound = 0, kResCold = 1, kResStop = 2 };
 // host state words the kernel writes: [0] kResRunning / kResExiting / kResExited, [1] the
 // last entry it consumed (its door slot may be reused)

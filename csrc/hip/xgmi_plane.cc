@@ -645,7 +645,8 @@ bool XgmiRoundPlane::post_door(const ResidentDoor& e) {
   d->done_out = e.done_out;
   d->epoch = e.epoch;
   d->cmd = e.cmd;
-  __atomic_store_n(&d->seq, seq, __ATOMIC_RELEASE);  // the kernel reads the operands after the sequence word
+  d->check = door_check(reinterpret_cast<const uint32_t*>(&e), seq);
+  __atomic_store_n(&d->seq, seq, __ATOMIC_RELEASE);  // sequence word last
   // Dekker hand-off with the kernel's idle exit (xgmi_threshold.hip, resident_door): the
   // entry is visible before the state word is read
   __atomic_thread_fence(__ATOMIC_SEQ_CST);
@@ -802,6 +803,7 @@ bool XgmiRoundPlane::launch_resident(int round, const Payload& input, bool cold)
       if (!res_on_) {
         ResidentDoor* d = door_ + seq % kResidentDoors;
         *d = e;
+        d->check = door_check(reinterpret_cast<const uint32_t*>(&e), seq);
         __atomic_store_n(&d->seq, seq, __ATOMIC_RELEASE);
         res_seq_ = seq + 1;
       }

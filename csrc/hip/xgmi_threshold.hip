@@ -1202,29 +1202,44 @@ __device__ uint64_t resident_door(const ResidentDoor* door, uint32_t* hstate, ui
                                   uint32_t gen, uint64_t idle, bool broadcast) {
   const int lane = static_cast<int>(threadIdx.x);
   const ResidentDoor* d = door + seq % kResidentDoors;
-  int found = 1;
-  if (lane == 0) {
-    const uint64_t t0 = wall_ticks();
-    for (;;) {
-      if (sys_ld(&d->seq) == seq) break;
-      if (wall_ticks() - t0 > idle) {
+  const uint64_t* dw = reinterpret_cast<const uint64_t*>(d);
+  // Every poll reads the whole 64-B entry (lanes 0-7, one instruction: one PCIe round trip);
+  // the entry is taken when its sequence word is `seq` and its check word matches the other
+  // words - a read that caught the host mid-write fails the check and is simply repeated.
+  auto poll = [&](uint64_t* w) -> bool {
+    *w = lane < 8 ? __hip_atomic_load(dw + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+    uint32_t v[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint64_t x = __shfl(*w, i);
+      v[2 * i] = static_cast<uint32_t>(x);
+      v[2 * i + 1] = static_cast<uint32_t>(x >> 32);
+    }
+    return v[14] == seq && v[15] == door_check(v, seq);
+  };
+  uint64_t w = 0;
+  bool found = true;
+  const uint64_t t0 = wall_ticks();
+  for (;;) {
+    if (poll(&w)) break;
+    if (wall_ticks() - t0 > idle) {
+      if (lane == 0) {
         sys_st(&hstate[0], kResExiting);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (sys_ld(&d->seq) == seq) {
-          sys_st(&hstate[0], kResRunning);
-        } else {
-          found = 0;
-        }
-        break;
       }
-      __builtin_amdgcn_s_sleep(2);
+      // the host may have posted the entry meanwhile: one more (checked) read decides
+      found = false;
+      for (int i = 0; i < 4 && !found; ++i) found = poll(&w);
+      if (!found && __shfl(static_cast<uint32_t>(__shfl(w, 7)), 0) == seq) {
+        // the sequence word is there but the reads kept catching a write: wait for it
+        while (!found) found = poll(&w);
+      }
+      if (lane == 0) sys_st(&hstate[0], found ? kResRunning : kResExited);
+      break;
     }
+    __builtin_amdgcn_s_sleep(2);
   }
-  found = __shfl(found, 0);
-  uint64_t w = 0;
-  if (found && lane < 8)  // the whole entry, one instruction (seq is already there: written last)
-    w = __hip_atomic_load(reinterpret_cast<const uint64_t*>(d) + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   uint64_t w6 = __shfl(w, 6);
   if (!found) w6 = static_cast<uint64_t>(static_cast<uint32_t>(kResStop)) << 32;
   if (!found && lane == 6) w = w6;
@@ -1236,7 +1251,8 @@ __device__ uint64_t resident_door(const ResidentDoor* door, uint32_t* hstate, ui
       __hip_atomic_store(&dm[kDmGo], (static_cast<uint64_t>(gen) << 32) | seq, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (lane == 0 && static_cast<uint32_t>(w6 >> 32) == static_cast<uint32_t>(kResStop)) sys_st(&hstate[0], kResExited);
+  if (lane == 0 && found && static_cast<uint32_t>(w6 >> 32) == static_cast<uint32_t>(kResStop))
+    sys_st(&hstate[0], kResExited);
   return w;
 }
 
