@@ -1,0 +1,149 @@
+// Roofline of the fused AdamW step's memory pattern (xgmi_adam.hip at world 1): per parameter
+// read bf16 grad + fp32 master / m / v, write fp32 master / m / v + bf16 param = 28 B, eight
+// streams, no communication. A plain streaming kernel with the same streams and a trivial
+// update, so the fused kernel's TB/s can be set against what the pattern itself reaches.
+//   mode 0: plain loads / stores
+//   mode 1: nontemporal loads / stores (__builtin_nontemporal_*)
+//   mode 2: plain loads, nontemporal stores
+// Output: one JSON line per (mode, grid): ms per step, HBM TB/s at 28 B/param; plus a 2-stream
+// copy of the same byte count for the copy roofline.
+//   hipcc --offload-arch=gfx950 -O3 -o tools/adam_stream_probe.bin tools/adam_stream_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#define CHECK(x)                                                                   \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                 \
+      return 1;                                                                    \
+    }                                                                              \
+  } while (0)
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+
+template <int MODE>
+__device__ __forceinline__ f4 ldf(const f4* p) {
+  if constexpr (MODE == 1) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <int MODE>
+__device__ __forceinline__ u4 ldu(const u4* p) {
+  if constexpr (MODE == 1) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <int MODE>
+__device__ __forceinline__ void stf(f4* p, f4 v) {
+  if constexpr (MODE >= 1) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+template <int MODE>
+__device__ __forceinline__ void stu(u4* p, u4 v) {
+  if constexpr (MODE >= 1) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+__device__ __forceinline__ float bf(uint32_t h) { return __uint_as_float(h << 16); }
+__device__ __forceinline__ uint32_t tobf(float f) { return __float_as_uint(f) >> 16; }
+
+// one unit = 8 parameters: 16 B of bf16 grad, 2 x 16 B of each fp32 array, 16 B of bf16 param
+template <int MODE>
+__global__ __launch_bounds__(256) void adam_like(const u4* g, f4* p, f4* m, f4* v, u4* w, int64_t units, float lr) {
+  for (int64_t u = blockIdx.x * 256 + threadIdx.x; u < units; u += static_cast<int64_t>(gridDim.x) * 256) {
+    const u4 gg = ldu<MODE>(g + u);
+    f4 p0 = ldf<MODE>(p + 2 * u), p1 = ldf<MODE>(p + 2 * u + 1);
+    f4 m0 = ldf<MODE>(m + 2 * u), m1 = ldf<MODE>(m + 2 * u + 1);
+    f4 v0 = ldf<MODE>(v + 2 * u), v1 = ldf<MODE>(v + 2 * u + 1);
+    float gf[8];
+    for (int i = 0; i < 4; ++i) {
+      gf[2 * i] = bf(gg[i] & 0xffffu);
+      gf[2 * i + 1] = bf(gg[i] >> 16);
+    }
+    u4 out;
+    for (int i = 0; i < 4; ++i) {
+      const float ga = gf[i], gb = gf[4 + i];
+      m0[i] = 0.9f * m0[i] + 0.1f * ga;
+      m1[i] = 0.9f * m1[i] + 0.1f * gb;
+      v0[i] = 0.999f * v0[i] + 0.001f * ga * ga;
+      v1[i] = 0.999f * v1[i] + 0.001f * gb * gb;
+      p0[i] -= lr * m0[i] * __frsqrt_rn(v0[i] + 1e-8f);
+      p1[i] -= lr * m1[i] * __frsqrt_rn(v1[i] + 1e-8f);
+    }
+    for (int i = 0; i < 2; ++i) out[i] = tobf(p0[2 * i]) | (tobf(p0[2 * i + 1]) << 16);
+    for (int i = 0; i < 2; ++i) out[2 + i] = tobf(p1[2 * i]) | (tobf(p1[2 * i + 1]) << 16);
+    stf<MODE>(p + 2 * u, p0);
+    stf<MODE>(p + 2 * u + 1, p1);
+    stf<MODE>(m + 2 * u, m0);
+    stf<MODE>(m + 2 * u + 1, m1);
+    stf<MODE>(v + 2 * u, v0);
+    stf<MODE>(v + 2 * u + 1, v1);
+    stu<MODE>(w + u, out);
+  }
+}
+
+__global__ __launch_bounds__(256) void copy4(const f4* a, f4* b, int64_t n4) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += static_cast<int64_t>(gridDim.x) * 256) b[i] = a[i];
+}
+
+template <int MODE>
+int run(int grid, const u4* g, f4* p, f4* m, f4* v, u4* w, int64_t units, hipEvent_t e0, hipEvent_t e1) {
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(adam_like<MODE>, dim3(grid), dim3(256), 0, 0, g, p, m, v, w, units, 1e-6f);
+  CHECK(hipDeviceSynchronize());
+  const int it = 20;
+  CHECK(hipEventRecord(e0, 0));
+  for (int i = 0; i < it; ++i) hipLaunchKernelGGL(adam_like<MODE>, dim3(grid), dim3(256), 0, 0, g, p, m, v, w, units, 1e-6f);
+  CHECK(hipEventRecord(e1, 0));
+  CHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= it;
+  const double bytes = 28.0 * 8.0 * static_cast<double>(units);
+  std::printf("{\"kernel\": \"adam_like\", \"mode\": %d, \"grid\": %d, \"params\": %lld, \"ms\": %.4f, \"TBps\": %.3f}\n", MODE,
+              grid, static_cast<long long>(units * 8), ms, bytes / (ms * 1e-3) / 1e12);
+  return 0;
+}
+
+int main() {
+  const int64_t params = int64_t{134217728};
+  const int64_t units = params / 8;
+  u4 *g = nullptr, *w = nullptr;
+  f4 *p = nullptr, *m = nullptr, *v = nullptr;
+  CHECK(hipMalloc(&g, params * 2));
+  CHECK(hipMalloc(&w, params * 2));
+  CHECK(hipMalloc(&p, params * 4));
+  CHECK(hipMalloc(&m, params * 4));
+  CHECK(hipMalloc(&v, params * 4));
+  CHECK(hipMemset(g, 0x3c, params * 2));
+  CHECK(hipMemset(p, 0, params * 4));
+  CHECK(hipMemset(m, 0, params * 4));
+  CHECK(hipMemset(v, 0, params * 4));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  for (int grid : {1024, 2048, 4096, 8192}) {
+    if (run<0>(grid, g, p, m, v, w, units, e0, e1) || run<1>(grid, g, p, m, v, w, units, e0, e1) ||
+        run<2>(grid, g, p, m, v, w, units, e0, e1))
+      return 1;
+  }
+  // copy roofline: the fp32 master array into v (4 B/param read + 4 B/param written)
+  {
+    const int64_t n4 = params / 4;  // f4 elements of one fp32 array
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(copy4, dim3(4096), dim3(256), 0, 0, p, v, n4);
+    CHECK(hipDeviceSynchronize());
+    const int it = 20;
+    CHECK(hipEventRecord(e0, 0));
+    for (int i = 0; i < it; ++i) hipLaunchKernelGGL(copy4, dim3(4096), dim3(256), 0, 0, p, v, n4);
+    CHECK(hipEventRecord(e1, 0));
+    CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= it;
+    const double bytes = 2.0 * 16.0 * static_cast<double>(n4);
+    std::printf("{\"kernel\": \"copy\", \"bytes_moved\": %.0f, \"ms\": %.4f, \"TBps\": %.3f}\n", bytes, ms,
+                bytes / (ms * 1e-3) / 1e12);
+  }
+  return 0;
+}
