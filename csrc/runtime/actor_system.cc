@@ -313,7 +313,6 @@ ActorSystem::ActorSystem(std::string name, Mode mode, int threads, int throughpu
     if (const char* e = std::getenv("MXAR_DISPATCH_LIFO")) lifo_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("MXAR_DISPATCH_YIELD")) spin_yield_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("MXAR_DISPATCH_SPINNERS")) max_spinners_ = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("MXAR_DISPATCH_INLINE")) inline_ok_ = std::atoi(e) != 0;
     int n = threads > 0 ? threads : std::max(2u, std::min(8u, std::thread::hardware_concurrency()));
     for (int i = 0; i < n; ++i) threads_.emplace_back([this] { worker_loop(); });
     timer_thread_ = std::thread([this] { timer_loop(); });
@@ -403,38 +402,6 @@ void ActorSystem::schedule(const std::shared_ptr<ActorCell>& cell) {
     return enqueue(prev);
   }
   enqueue(cell);
-}
-
-bool ActorSystem::tell_inline(const ActorRef& to, Message msg, ActorRef sender) {
-  auto* lr = dynamic_cast<LocalActorRef*>(to.get());
-  std::shared_ptr<ActorCell> c = lr != nullptr ? lr->cell() : nullptr;
-  if (!c || c->stopped() || mode_ != Mode::Threaded || !inline_ok_ || tl_sys == this || shutdown_.load()) {
-    if (to) to->tell(std::move(msg), std::move(sender));
-    return false;
-  }
-  // counted before the push, as enqueue() does: a dispatcher releasing the cell sees it
-  const bool alone = c->pending_.fetch_add(1) == 0;
-  c->mailbox_.push(Envelope{std::move(msg), std::move(sender)});
-  if (!alone || c->scheduled_.exchange(true)) {
-    // other mail first (its order is kept by the normal path), or a dispatcher holds the
-    // cell and will find this message when it releases it
-    if (!alone) schedule(c);
-    return false;
-  }
-  {
-    std::lock_guard<std::mutex> g(rq_mu_);
-    ++busy_;  // await_idle() counts this turn like a dispatcher's
-  }
-  const size_t n = c->process(1);
-  c->scheduled_.store(false);
-  if (!c->stopped() && c->has_mail()) schedule(c);
-  delivered_.fetch_add(n, std::memory_order_relaxed);
-  {
-    std::lock_guard<std::mutex> g(rq_mu_);
-    --busy_;
-    if (busy_ == 0 && runq_.empty()) idle_cv_.notify_all();
-  }
-  return true;
 }
 
 void ActorSystem::enqueue(const std::shared_ptr<ActorCell>& cell) {

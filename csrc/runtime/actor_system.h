@@ -223,14 +223,6 @@ class ActorSystem {
   ActorRef dead_letters() const { return dead_letters_; }
   ActorRef lookup(const std::string& path);
   void stop(const ActorRef& ref);
-  // Delivers `msg` to a local actor and, when its mailbox held nothing else and no dispatcher
-  // holds it, runs that one message on the CALLING thread (a foreign thread - a plane's
-  // completion thread) instead of waking a dispatcher for it: one thread hop less per
-  // protocol round. Otherwise (other mail queued, a dispatcher turn in progress, a remote or
-  // stopped target, a dispatcher thread calling) it is an ordinary tell. Only for messages
-  // whose handler never waits on the calling thread's own work. MXAR_DISPATCH_INLINE=0: off.
-  // Returns true when it ran inline.
-  bool tell_inline(const ActorRef& to, Message msg, ActorRef sender = nullptr);
 
   // Deterministic mode: run until no actor has mail (or max_messages processed).
   // Rethrows the first exception an actor raised while processing.
@@ -309,7 +301,6 @@ class ActorSystem {
   // Complete -> master -> Start chain stays on one warm thread (Go's runnext)
   bool lifo_ = true;
   bool spin_yield_ = false;  // MXAR_DISPATCH_YIELD=1: idle spin yields every poll (round-2 form)
-  bool inline_ok_ = true;    // MXAR_DISPATCH_INLINE=0: tell_inline never runs inline
   int max_spinners_ = 2;     // MXAR_DISPATCH_SPINNERS: dispatcher threads spinning at once
   int busy_ = 0;
   std::vector<std::thread> threads_;

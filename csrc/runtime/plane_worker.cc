@@ -27,18 +27,15 @@ void PlaneWorkerActor::receive(Envelope& env, ActorContext& ctx) {
   if (!self_) {
     self_ = ctx.self();
     // the plane's completion thread posts each finished round to this worker's mailbox
-    // - run inline on that thread when the worker is idle (ActorSystem::tell_inline: on_done
-    // only sinks the output and tells the master, it never waits on the plane)
     std::weak_ptr<ActorRefBase> weak = self_;
-    ActorSystem* sys = &ctx.system();
-    plane_->set_done([weak, sys](RoundResult&& r) {
+    plane_->set_done([weak](RoundResult&& r) {
       if (auto s = weak.lock()) {
         PlaneRoundDone d;
         d.epoch = r.epoch;
         d.output = AllReduceOutput{std::move(r.data), std::move(r.count), r.round};
         d.error = r.error;
         d.cold = r.cold;
-        sys->tell_inline(s, Message(std::move(d)), nullptr);
+        s->tell(Message(std::move(d)), nullptr);
       }
     });
   }
