@@ -361,6 +361,12 @@ class XgmiComm {
   int sub_max_ = 0;       // two-shot: most reduce pieces per chunk; 0 = by block size
   int ring_depth_ = 1;    // ring: chunks per workgroup, walked step-major (MXAR_RING_DEPTH)
   int ring_grid_ = 256;
+  // The device-default grid, and whether a launch at the default grid sizes it by its bytes
+  // (launch_grid; MXAR_SIZE_GRID=0: always the full grid). An explicit grid (set_grid(g),
+  // tune()'s "algo@g" labels) is always used as given.
+  int default_grid_ = 0;
+  bool size_grid_ = true;
+  int launch_grid(int64_t bytes_in_launch) const;
   // Threshold rounds up to this many bytes per rank run low-latency (MXAR_THRESHOLD_LL_MAX).
   // Off by default: measured slower than the fenced hand-offs (8 logical ranks x 4 KiB:
   // 22 vs 13 us per round; the peers' unfenced write-through units became visible ~5 us after

@@ -635,7 +635,9 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   if (const char* e = std::getenv("MXAR_LL_AUTO_MAX")) ll_auto_max_ = std::max<int64_t>(0, std::atoll(e));
   oneshot_max_ = std::min<int64_t>(slot_bytes_, world_ <= 2 ? 64 * mib : world_ <= 4 ? 4 * mib : mib / 4);
   if (const char* e = std::getenv("MXAR_ONESHOT_MAX")) oneshot_max_ = std::min<int64_t>(slot_bytes_, std::atoll(e));
-  if (grid_ <= 0) grid_ = default_grid(device);
+  default_grid_ = default_grid(device);
+  if (grid_ <= 0) grid_ = default_grid_;
+  if (const char* e = std::getenv("MXAR_SIZE_GRID")) size_grid_ = std::atoi(e) != 0;
   if (const char* f = std::getenv("MXAR_FENCE")) fence_ = std::atoi(f) & 3;
   // Slab reads are `nt` loads: the acquire after each wait (bit 1) is what orders them after
   // the peers' flags. Without it a stale line could be read, so clearing it is a study-only
@@ -765,7 +767,20 @@ void XgmiComm::connect_ptrs(const std::vector<char*>& bases) {
   connected_ = true;
 }
 
-void XgmiComm::set_grid(int g) { grid_ = g > 0 ? g : default_grid(device_); }
+void XgmiComm::set_grid(int g) { grid_ = g > 0 ? g : default_grid_; }
+
+int XgmiComm::launch_grid(int64_t bytes) const {
+  // Workgroups for a two-shot / one-shot launch moving `bytes` of input (all ranks of the
+  // launch). Every unit of work pays flag hand-offs and system-scope fences, and hundreds of
+  // workgroups fencing at once serialise in the L2: below ~512 MiB per launch the full grid
+  // is slower than ~one workgroup per 64 KiB, capped at 256 (8 / 2 logical ranks x 256 KiB -
+  // 16 MiB, grid 64 - 1024: 1 MiB x 8 ranks 35.8 -> 21.7 us, 4 MiB 64.9 -> 46.2 us, 16 MiB
+  // 174.6 -> 149.4 us; profiles/round4/README.md section 9). At the default grid only.
+  if (!size_grid_ || grid_ != default_grid_) return grid_;
+  if (bytes >= (int64_t{512} << 20)) return grid_;
+  const int64_t g = std::max<int64_t>(64, std::min<int64_t>(256, bytes / (int64_t{64} << 10)));
+  return static_cast<int>(std::min<int64_t>(grid_, g));
+}
 
 static bool capturing(hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
@@ -894,7 +909,10 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   for (int k = 0; k < W; ++k) a.base[k] = c0.peers_[k];
   const int64_t min_chunk = min_chunk_bytes() / es;
   const int ranks_here = static_cast<int>(group.size());
-  const int gmax = std::max(1, c0.grid_ / ranks_here);  // all workgroups of the launch stay resident
+  // all workgroups of the launch stay resident; plain two-shot / one-shot launches size the
+  // grid by their bytes (launch_grid), the fused AdamW step keeps the full grid
+  const bool sized = adam_state == nullptr && (kind == Algo::TwoShot || oneshot);
+  const int gmax = std::max(1, (sized ? c0.launch_grid(n * es * ranks_here) : c0.grid_) / ranks_here);
   int gx;
   a.sub = 1;
   a.off_LL = c0.off_LL_;
