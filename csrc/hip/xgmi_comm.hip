@@ -769,16 +769,20 @@ void XgmiComm::connect_ptrs(const std::vector<char*>& bases) {
 
 void XgmiComm::set_grid(int g) { grid_ = g > 0 ? g : default_grid_; }
 
-int XgmiComm::launch_grid(int64_t bytes) const {
+int XgmiComm::launch_grid(int64_t bytes, bool oneshot) const {
   // Workgroups for a two-shot / one-shot launch moving `bytes` of input (all ranks of the
   // launch). Every unit of work pays flag hand-offs and system-scope fences, and hundreds of
-  // workgroups fencing at once serialise in the L2: below ~512 MiB per launch the full grid
-  // is slower than ~one workgroup per 64 KiB, capped at 256 (8 / 2 logical ranks x 256 KiB -
-  // 16 MiB, grid 64 - 1024: 1 MiB x 8 ranks 35.8 -> 21.7 us, 4 MiB 64.9 -> 46.2 us, 16 MiB
-  // 174.6 -> 149.4 us; profiles/round4/README.md section 9). At the default grid only.
+  // workgroups fencing at once serialise in the L2, so below ~512 MiB per launch the full
+  // grid loses to ~one workgroup per 64 KiB (8 / 4 / 2 logical ranks x 64 KiB - 256 MiB, same
+  // box: two-shot 1 MiB x 8 ranks 36.6 -> 21.9 us, 16 MiB x 4 ranks 95.4 -> 67.8 us, 64 MiB x 2
+  // ranks 132 -> 101 us, 256 MiB unchanged; profiles/round4/README.md section 9):
+  //   two-shot: one workgroup per 64 KiB, 64..256, the full grid from 512 MiB;
+  //   one-shot: every rank reads all P inputs, so one per 64 KiB of P x bytes, 64..full grid.
+  // At the default grid only: an explicit grid is used as given.
   if (!size_grid_ || grid_ != default_grid_) return grid_;
-  if (bytes >= (int64_t{512} << 20)) return grid_;
-  const int64_t g = std::max<int64_t>(64, std::min<int64_t>(256, bytes / (int64_t{64} << 10)));
+  if (oneshot) bytes *= std::max(1, world_);
+  else if (bytes >= (int64_t{512} << 20)) return grid_;
+  const int64_t g = std::max<int64_t>(64, std::min<int64_t>(oneshot ? grid_ : 256, bytes / (int64_t{64} << 10)));
   return static_cast<int>(std::min<int64_t>(grid_, g));
 }
 
@@ -912,7 +916,7 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   // all workgroups of the launch stay resident; plain two-shot / one-shot launches size the
   // grid by their bytes (launch_grid), the fused AdamW step keeps the full grid
   const bool sized = adam_state == nullptr && (kind == Algo::TwoShot || oneshot);
-  const int gmax = std::max(1, (sized ? c0.launch_grid(n * es * ranks_here) : c0.grid_) / ranks_here);
+  const int gmax = std::max(1, (sized ? c0.launch_grid(n * es * ranks_here, oneshot) : c0.grid_) / ranks_here);
   int gx;
   a.sub = 1;
   a.off_LL = c0.off_LL_;
