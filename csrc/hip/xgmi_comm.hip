@@ -622,18 +622,19 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   slab_bytes_ = L.slab_bytes;
   alloc_bytes_ = L.alloc_bytes;
   // Automatic dispatch limits (resolve()), measured with P logical ranks in one launch on one
-  // MI355X (bench.py latency_vs_size, profiles/round3/README.md): the low-latency one-shot
-  // wins up to 1 MiB at 2 ranks, 512 KiB at 4 and 256 KiB at 8 (it moves 2x bytes as
-  // flag-carrying LL words, so it loses to the plain kernels once they are bandwidth bound);
-  // the one-shot (one hop, every rank reads all P inputs) wins up to 64 MiB at 2 ranks (118 vs
-  // 126 us at 64 MiB), where it moves the same bytes as the two-shot with one hand-off less,
-  // and up to 4 MiB at 4; at
-  // 8 ranks the two-shot takes over from the low-latency kernel directly. MXAR_LL_AUTO_MAX / MXAR_ONESHOT_MAX
-  // override (bytes).
+  // MI355X (bench.py latency_vs_size; round 4, with launch-size grids, profiles/round4/README.md
+  // section 9): the low-latency one-shot wins up to 512 KiB at 2 and 4 ranks and 256 KiB at 8
+  // (it moves 2x bytes as flag-carrying LL words, so it loses to the plain kernels once they
+  // are bandwidth bound: 2 ranks x 1 MiB ll 15.8 vs one-shot 12.1 us); the one-shot (one hop,
+  // every rank reads all P inputs) up to 8 MiB at 2 ranks and 2 MiB at 4 (2 x 16 MiB: two-shot
+  // 37.4 vs one-shot 42.1 us; 4 x 4 MiB: 32.3 vs 39.4 us); at 8 ranks the two-shot takes over
+  // from the low-latency kernel directly. Across GPUs the one-shot reads every peer's whole
+  // buffer over its link, so the two-shot's crossover comes no later there.
+  // MXAR_LL_AUTO_MAX / MXAR_ONESHOT_MAX override (bytes).
   const int64_t mib = int64_t{1} << 20;
-  ll_auto_max_ = world_ <= 2 ? mib : world_ <= 4 ? mib / 2 : mib / 4;
+  ll_auto_max_ = world_ <= 4 ? mib / 2 : mib / 4;
   if (const char* e = std::getenv("MXAR_LL_AUTO_MAX")) ll_auto_max_ = std::max<int64_t>(0, std::atoll(e));
-  oneshot_max_ = std::min<int64_t>(slot_bytes_, world_ <= 2 ? 64 * mib : world_ <= 4 ? 4 * mib : mib / 4);
+  oneshot_max_ = std::min<int64_t>(slot_bytes_, world_ <= 2 ? 8 * mib : world_ <= 4 ? 2 * mib : mib / 4);
   if (const char* e = std::getenv("MXAR_ONESHOT_MAX")) oneshot_max_ = std::min<int64_t>(slot_bytes_, std::atoll(e));
   default_grid_ = default_grid(device);
   if (grid_ <= 0) grid_ = default_grid_;
