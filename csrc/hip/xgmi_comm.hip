@@ -1543,7 +1543,22 @@ void XgmiComm::run_coll(const std::vector<XgmiComm*>& group, Coll op, const std:
     a.rdelay = c0.rdelay_us_ > 0 ? static_cast<uint64_t>(c0.rdelay_us_ * 100.0) : 0;
     a.noguard = c0.noguard_ ? 1 : 0;
     for (int k = 0; k < W; ++k) a.base[k] = c0.peers_[k];
-    const int64_t target = std::max<int64_t>(1, gmax / (W - 1));
+    // launch-size grid as for the two-shot (launch_grid), over P x block bytes per rank: a
+    // block goes to every peer (all-gather) or P blocks come in (all-to-all, reduce-scatter).
+    // 8 / 2 logical ranks x 128 KiB - 8 MiB blocks, grid 64 - 512 (coll_grid_sweep.jsonl):
+    // 8 x 512 KiB all-gather 58.4 -> 50.1 us, all-to-all 50.7 -> 41.2, reduce-scatter 44.9 ->
+    // 35.4; the full grid pays off from 512 MiB (all-gather, all-to-all) / not yet at 512 MiB
+    // for the reduce-scatter (8 x 8 MiB: 331 us full vs 284 us at 256).
+    int gcap = gmax;
+    if (c0.size_grid_ && c0.grid_ == c0.default_grid_) {
+      const int64_t bytes = static_cast<int64_t>(ranks_here) * W * len * es;
+      const int64_t full_at = op == Coll::ReduceScatter ? (int64_t{1} << 30) : (int64_t{512} << 20);
+      if (bytes < full_at) {
+        const int64_t g = std::min<int64_t>(c0.grid_, std::max<int64_t>(64, std::min<int64_t>(256, bytes / (int64_t{64} << 10))));
+        gcap = std::max(1, static_cast<int>(g) / ranks_here);
+      }
+    }
+    const int64_t target = std::max<int64_t>(1, gcap / (W - 1));
     a.chunk = std::max(min_chunk, round_up(ceil_div(len, target), elems));
     a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(len, a.chunk)));
     a.subchunk = a.chunk;
@@ -1554,7 +1569,7 @@ void XgmiComm::run_coll(const std::vector<XgmiComm*>& group, Coll op, const std:
       a.sub = static_cast<int>(ceil_div(a.chunk, a.subchunk));
     }
     if (a.nch > c0.maxch_) throw std::logic_error("XgmiComm: collective geometry exceeds the flag table");
-    const int gx = static_cast<int>(std::min<int64_t>(gmax, std::max<int64_t>(1, (W - 1) * int64_t{a.nch})));
+    const int gx = static_cast<int>(std::min<int64_t>(gcap, std::max<int64_t>(1, (W - 1) * int64_t{a.nch})));
     launch_coll(a, dim3(gx, ranks_here), stream, dt, static_cast<int>(op));
     hip_check(hipGetLastError(), "collective launch");
     for (XgmiComm* c : group) {

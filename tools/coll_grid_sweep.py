@@ -20,6 +20,12 @@ H = C.hip
 
 
 def main() -> None:
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--grids", type=int, nargs="+", default=[64, 128, 256, 512],
+                    help="device workgroup budgets (512 = the default grid: launch-size grids apply)")
+    args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     ops = {"all_to_all": H.Coll.AllToAll, "all_gather": H.Coll.AllGather, "reduce_scatter": H.Coll.ReduceScatter}
@@ -35,7 +41,7 @@ def main() -> None:
                 out_blocks = 1 if name == "reduce_scatter" else P
                 ins = [torch.randn(in_blocks * m, device=dev).to(torch.bfloat16) for _ in range(P)]
                 outs = [torch.empty(out_blocks * m, dtype=torch.bfloat16, device=dev) for _ in range(P)]
-                for g in (64, 128, 256, 512):
+                for g in args.grids:
                     for c in comms:
                         c.grid = g
                     call = lambda: H.XgmiComm.collective_local(comms, op, [x.data_ptr() for x in ins],  # noqa: E731
