@@ -1192,7 +1192,8 @@ void XgmiComm::geometry_threshold(int64_t n, DType dt, int ranks_here, int64_t* 
   const int64_t es = static_cast<int64_t>(dtype_size(dt));
   const int64_t elems = 16 / es;
   const int64_t min_chunk = min_chunk_bytes() / es;
-  const int gmax = std::max(1, grid_ / std::max(1, ranks_here));
+  // launch-size grid as for the two-shot (launch_grid; at the default grid only)
+  const int gmax = std::max(1, launch_grid(n * es * std::max(1, ranks_here), false) / std::max(1, ranks_here));
   *block = round_up(ceil_div(n, world_), elems);
   // one reduce unit (a chunk: one threshold decision) per workgroup; phase 1/3 get P-1 each,
   // spread over up to (P - 1) x nch workgroups when the chunks are few (small tensors)
