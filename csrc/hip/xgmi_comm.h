@@ -366,7 +366,7 @@ class XgmiComm {
   // tune()'s "algo@g" labels) is always used as given.
   int default_grid_ = 0;
   bool size_grid_ = true;
-  int launch_grid(int64_t bytes_in_launch, bool oneshot) const;
+  int launch_grid(int64_t bytes_in_launch, bool oneshot, int64_t full_at = int64_t{512} << 20) const;
   // Threshold rounds up to this many bytes per rank run low-latency (MXAR_THRESHOLD_LL_MAX).
   // Off by default: measured slower than the fenced hand-offs (8 logical ranks x 4 KiB:
   // 22 vs 13 us per round; the peers' unfenced write-through units became visible ~5 us after

@@ -770,19 +770,20 @@ void XgmiComm::connect_ptrs(const std::vector<char*>& bases) {
 
 void XgmiComm::set_grid(int g) { grid_ = g > 0 ? g : default_grid_; }
 
-int XgmiComm::launch_grid(int64_t bytes, bool oneshot) const {
+int XgmiComm::launch_grid(int64_t bytes, bool oneshot, int64_t full_at) const {
   // Workgroups for a two-shot / one-shot launch moving `bytes` of input (all ranks of the
   // launch). Every unit of work pays flag hand-offs and system-scope fences, and hundreds of
   // workgroups fencing at once serialise in the L2, so below ~512 MiB per launch the full
   // grid loses to ~one workgroup per 64 KiB (8 / 4 / 2 logical ranks x 64 KiB - 256 MiB, same
   // box: two-shot 1 MiB x 8 ranks 36.6 -> 21.9 us, 16 MiB x 4 ranks 95.4 -> 67.8 us, 64 MiB x 2
   // ranks 132 -> 101 us, 256 MiB unchanged; profiles/round4/README.md section 9):
-  //   two-shot: one workgroup per 64 KiB, 64..256, the full grid from 512 MiB;
+  //   two-shot: one workgroup per 64 KiB, 64..256, the full grid from `full_at` (512 MiB;
+  //             the threshold kernel: 256 MiB - 4 x 64 MiB 288 us full vs 307 us sized);
   //   one-shot: every rank reads all P inputs, so one per 64 KiB of P x bytes, 64..full grid.
   // At the default grid only: an explicit grid is used as given.
   if (!size_grid_ || grid_ != default_grid_) return grid_;
   if (oneshot) bytes *= std::max(1, world_);
-  else if (bytes >= (int64_t{512} << 20)) return grid_;
+  else if (bytes >= full_at) return grid_;
   const int64_t g = std::max<int64_t>(64, std::min<int64_t>(oneshot ? grid_ : 256, bytes / (int64_t{64} << 10)));
   return static_cast<int>(std::min<int64_t>(grid_, g));
 }
@@ -1193,7 +1194,8 @@ void XgmiComm::geometry_threshold(int64_t n, DType dt, int ranks_here, int64_t* 
   const int64_t elems = 16 / es;
   const int64_t min_chunk = min_chunk_bytes() / es;
   // launch-size grid as for the two-shot (launch_grid; at the default grid only)
-  const int gmax = std::max(1, launch_grid(n * es * std::max(1, ranks_here), false) / std::max(1, ranks_here));
+  const int gmax =
+      std::max(1, launch_grid(n * es * std::max(1, ranks_here), false, int64_t{256} << 20) / std::max(1, ranks_here));
   *block = round_up(ceil_div(n, world_), elems);
   // one reduce unit (a chunk: one threshold decision) per workgroup; phase 1/3 get P-1 each,
   // spread over up to (P - 1) x nch workgroups when the chunks are few (small tensors)
