@@ -198,6 +198,7 @@ class XgmiComm {
     return static_cast<size_t>(maxch) * (static_cast<size_t>(P + 1) * 12 + static_cast<size_t>(P) * 4);
   }
   int64_t max_chunks() const { return maxch_; }
+  uintptr_t slab_address() const { return reinterpret_cast<uintptr_t>(slab_); }  // study: placement
   // Resident rounds: round()'s geometry for n elements computed once (plan_resident; grid 0
   // = the round does not fit a resident kernel: chunks split over workgroups, or more than
   // `max_grid` workgroups), and a kernel on `stream` that runs the rounds posted to `door`
