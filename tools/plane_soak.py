@@ -26,6 +26,8 @@ def main() -> None:
     ap.add_argument("--seconds", type=float, default=240.0)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--max-jobs", type=int, default=10_000)
+    ap.add_argument("--threshold-frac", type=float, default=0.0,
+                    help="share of jobs at thresholds < 1 with a straggler (checked for consistency)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -36,9 +38,79 @@ def main() -> None:
     rng = random.Random(args.seed)
     t_end = time.monotonic() + args.seconds
     totals = {"jobs": 0, "rounds": 0, "resident_rounds": 0, "resident_launches": 0}
+    def subset_ok(v, lo, hi, it, cnt, P):
+        """v[lo:hi] is the sum of `cnt` distinct workers' iota data of round `it`."""
+        i = np.arange(lo, hi, dtype=np.float64)
+        s_ = (v[lo:hi].astype(np.float64) - cnt * (i + it)) / 1000.0
+        return bool(np.allclose(s_, s_[0], atol=1e-3)) and abs(s_[0] - round(s_[0])) <= 1e-3
+
     for j in range(args.max_jobs):
         if time.monotonic() > t_end:
             break
+        if rng.random() < args.threshold_frac:
+            # thresholds < 1 with a straggler: every chunk must be the sum of `count` distinct
+            # workers (zeros at count 0) - the reference's partial rounds and catch-up
+            P = rng.choice([3, 4])
+            n = rng.choice([1000, 4096, 30000])
+            chunk = rng.choice([64, 256, 1000])
+            th = rng.choice([0.5, 2.0 / 3.0, 0.75])
+            lag = rng.choice([1, 2])
+            rounds = rng.randint(10, 40)
+            slow_k, delay = rng.randrange(P), rng.uniform(0.001, 0.005)
+            row = {"job": j, "P": P, "n": n, "chunk": chunk, "dtype": "float32", "max_lag": lag, "rounds": rounds,
+                   "source": f"straggler {slow_k}", "th": round(th, 3), "resident_eligible": n * 4 <= 65536}
+
+            def src(k):
+                base = iota_source(n, dev, torch.float32, 1000.0 * k)
+                if k != slow_k:
+                    return base
+
+                def f(req):
+                    time.sleep(delay)
+                    return base(req)
+                return f
+            job = None
+            t0 = time.perf_counter()
+            try:
+                job = PlaneJob(P, n, max_chunk_size=chunk, th_reduce=th, th_complete=th, max_lag=lag,
+                               max_round=rounds - 1, timeout_s=20.0, sources=[src(k) for k in range(P)])
+                job.run(timeout=120)
+                step = -(-n // P)
+                nch = -(-step // chunk)
+                bad = None
+                for k in range(P):
+                    for it, (data, counts) in job.outputs[k].items():
+                        v = data.float().cpu().numpy()
+                        for jb in range(P):
+                            for c in range(nch):
+                                lo, hi = jb * step + c * chunk, min(n, jb * step + min(step, (c + 1) * chunk))
+                                if lo >= hi:
+                                    continue
+                                cnt = counts[jb * nch + c]
+                                ok = (0 <= cnt <= P) and ((cnt == 0 and not np.any(v[lo:hi])) or
+                                                          (cnt > 0 and subset_ok(v, lo, hi, it, cnt, P)))
+                                if not ok and bad is None:
+                                    bad = {"worker": k, "round": it, "block": jb, "chunk": c, "count": cnt}
+                errs = sum(job.system.plane_worker_state(w)["stats"]["plane_errors"] for w in job.workers)
+                res = [(p.stats.resident_rounds, p.stats.resident_launches) for p in job.planes]
+                row.update(ok=bad is None and errs == 0, plane_errors=errs, first_bad=bad,
+                           resident_rounds=sum(r[0] for r in res), resident_launches=sum(r[1] for r in res),
+                           wall_s=round(time.perf_counter() - t0, 3))
+                totals["jobs"] += 1
+                totals["rounds"] += sum(len(job.outputs[k]) for k in range(P))
+                totals["resident_rounds"] += row["resident_rounds"]
+                totals["resident_launches"] += row["resident_launches"]
+                totals["threshold_jobs"] = totals.get("threshold_jobs", 0) + 1
+            except Exception as e:  # noqa: BLE001
+                row.update(ok=False, error=repr(e)[:600])
+            finally:
+                if job is not None:
+                    job.shutdown()
+            print(json.dumps(row), flush=True)
+            job = None
+            if not row.get("ok"):
+                break
+            continue
         P = rng.choice([2, 2, 3, 4])
         n = rng.choice([10, 37, 1000, 4096, 16384, 30000, 100_000, 300_000])
         chunk = max(1, rng.choice([2, 64, 512, 1024, 4096, n]))
