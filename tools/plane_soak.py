@@ -3,7 +3,9 @@
 resident rounds included: every job draws P, size (both sides of the resident-round limit),
 maxChunkSize, dtype, maxLag, round count and a source kind (per-round iota fill, a static
 tensor, a slow source whose gaps make the resident kernel leave and come back), runs at
-thresholds 1 and checks EVERY round's output of every worker against the exact sum. One JSON
+thresholds 1 and checks EVERY round's output of every worker against the exact sum. With
+--threshold-frac a share of the jobs runs at thresholds < 1 with a straggler instead, each
+chunk checked to be the sum of exactly `count` distinct workers (zeros at count 0). One JSON
 line per job; the first failing job ends the soak (its line says why).
 
     python tools/plane_soak.py --seconds 240 --seed 1 > gpurun_out/plane_soak.jsonl
