@@ -37,12 +37,12 @@ __device__ __forceinline__ u4 ldu(const u4* p) {
 }
 template <int MODE>
 __device__ __forceinline__ void stf(f4* p, f4 v) {
-  if constexpr (MODE >= 1) __builtin_nontemporal_store(v, p);
+  if constexpr (MODE == 1 || MODE == 2) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
 template <int MODE>
 __device__ __forceinline__ void stu(u4* p, u4 v) {
-  if constexpr (MODE >= 1) __builtin_nontemporal_store(v, p);
+  if constexpr (MODE == 1 || MODE == 2) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
 
@@ -50,9 +50,18 @@ __device__ __forceinline__ float bf(uint32_t h) { return __uint_as_float(h << 16
 __device__ __forceinline__ uint32_t tobf(float f) { return __float_as_uint(f) >> 16; }
 
 // one unit = 8 parameters: 16 B of bf16 grad, 2 x 16 B of each fp32 array, 16 B of bf16 param
+// MODE 3: plain access, but each workgroup walks ONE contiguous range of the arrays (blocked)
+// instead of the grid-stride interleave: fewer concurrently open DRAM pages per stream
 template <int MODE>
 __global__ __launch_bounds__(256) void adam_like(const u4* g, f4* p, f4* m, f4* v, u4* w, int64_t units, float lr) {
-  for (int64_t u = blockIdx.x * 256 + threadIdx.x; u < units; u += static_cast<int64_t>(gridDim.x) * 256) {
+  int64_t u0 = blockIdx.x * 256 + threadIdx.x, stride = static_cast<int64_t>(gridDim.x) * 256, u1 = units;
+  if constexpr (MODE == 3) {
+    const int64_t per = (units + gridDim.x - 1) / gridDim.x;
+    u0 = blockIdx.x * per + threadIdx.x;
+    u1 = units < (blockIdx.x + 1) * per ? units : (blockIdx.x + 1) * per;
+    stride = 256;
+  }
+  for (int64_t u = u0; u < u1; u += stride) {
     const u4 gg = ldu<MODE>(g + u);
     f4 p0 = ldf<MODE>(p + 2 * u), p1 = ldf<MODE>(p + 2 * u + 1);
     f4 m0 = ldf<MODE>(m + 2 * u), m1 = ldf<MODE>(m + 2 * u + 1);
@@ -127,6 +136,9 @@ int main() {
     if (run<0>(grid, g, p, m, v, w, units, e0, e1) || run<1>(grid, g, p, m, v, w, units, e0, e1) ||
         run<2>(grid, g, p, m, v, w, units, e0, e1))
       return 1;
+  }
+  for (int grid : {256, 512, 1024, 2048}) {
+    if (run<3>(grid, g, p, m, v, w, units, e0, e1)) return 1;
   }
   // copy roofline: the fp32 master array into v (4 B/param read + 4 B/param written)
   {
