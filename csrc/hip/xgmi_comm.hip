@@ -916,9 +916,14 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   const int64_t min_chunk = min_chunk_bytes() / es;
   const int ranks_here = static_cast<int>(group.size());
   // all workgroups of the launch stay resident; plain two-shot / one-shot launches size the
-  // grid by their bytes (launch_grid), the fused AdamW step keeps the full grid
+  // grid by their bytes (launch_grid); the fused AdamW step (8 streams per element) runs best
+  // at 256 workgroups per device (134 M params: 0.745 vs 0.762 ms at 512, same box, twice;
+  // profiles/round4/README.md section 5), at the default grid
   const bool sized = adam_state == nullptr && (kind == Algo::TwoShot || oneshot);
-  const int gmax = std::max(1, (sized ? c0.launch_grid(n * es * ranks_here, oneshot) : c0.grid_) / ranks_here);
+  const int gdev = sized ? c0.launch_grid(n * es * ranks_here, oneshot)
+                   : (adam_state != nullptr && c0.size_grid_ && c0.grid_ == c0.default_grid_) ? std::min(c0.grid_, 256)
+                                                                                            : c0.grid_;
+  const int gmax = std::max(1, gdev / ranks_here);
   int gx;
   a.sub = 1;
   a.off_LL = c0.off_LL_;
