@@ -79,13 +79,21 @@ hipStream_t independent_plane_stream(int device, int priority, bool* probed_ok) 
   }
   for (hipStream_t r : rejected)
     if (r != s || !ok) (void)hipStreamDestroy(r);
-  if (!ok) {  // no independent queue left: keep the last candidate, say so
+  if (!ok) {
+    // No independent queue left: a round kernel of this plane would queue behind a co-located
+    // plane's round kernel that waits for it, and every round would wait out its deadline. Say
+    // so now rather than hang (MXAR_PLANE_SHARED_QUEUE_OK=1 keeps the last candidate anyway).
+    const char* e = std::getenv("MXAR_PLANE_SHARED_QUEUE_OK");
+    if (e == nullptr || std::atoi(e) == 0) {
+      throw std::runtime_error(
+          "xgmi plane: no hardware queue independent of the " + std::to_string(g_plane_streams.size()) +
+          " other plane streams on device " + std::to_string(device) + " after " + std::to_string(tried) +
+          " candidates: co-located plane workers need one queue each (GPU_MAX_HW_QUEUES; or one process per "
+          "worker)");
+    }
     hip_check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority), "hipStreamCreate(plane)");
-    std::fprintf(stderr,
-                 "[mxar] WARNING: no hardware queue independent of the other %d plane streams on device %d "
-                 "after %d candidates; co-located round kernels may wait out their deadline (raise "
-                 "GPU_MAX_HW_QUEUES)\n",
-                 static_cast<int>(g_plane_streams.size()), device, tried);
+    std::fprintf(stderr, "[mxar] WARNING: plane stream shares a hardware queue with another plane (device %d)\n",
+                 device);
   }
   g_plane_streams.emplace_back(device, s);
   *probed_ok = ok;
@@ -243,7 +251,21 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   // Many planes in one process (workers sharing a GPU) may instead want normal priority:
   // normal-priority streams are dealt round-robin over GPU_MAX_HW_QUEUES queues.
   bool independent = false;
-  stream_ = independent_plane_stream(o_.device, o_.high_priority ? hi : lo, &independent);
+  try {
+    stream_ = independent_plane_stream(o_.device, o_.high_priority ? hi : lo, &independent);
+  } catch (...) {  // no queue for this plane: release what the constructor allocated so far
+    for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+    if (rel_ev_) (void)hipEventDestroy(rel_ev_);
+    (void)hipFree(split_mem_);
+    (void)hipFree(rdm_);
+    (void)hipFree(ctl_mem_);
+    (void)hipFree(cnt_vram_);
+    (void)hipHostFree(ring_);
+    (void)hipHostFree(door_);
+    (void)hipHostFree(hforce_);
+    (void)hipFree(arena_);
+    throw;
+  }
   // keep freed round buffers in the device's default pool instead of returning them to the
   // driver at every synchronisation (the next round reuses them)
   hipMemPool_t mp = nullptr;

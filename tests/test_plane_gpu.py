@@ -920,3 +920,20 @@ def test_resident_rounds_with_released_outputs():
         assert all(s.pool_grown <= 8 for s in st), [s.pool_grown for s in st]
     finally:
         job.shutdown()
+
+
+def test_co_located_planes_beyond_the_hardware_queues_fail_loudly():
+    """Co-located plane workers need one hardware queue each (a round kernel queued behind a
+    peer's spinning round kernel would wait out its deadline every round): once the process
+    has no independent queue left, building another plane raises at once instead of hanging
+    the job's rounds (xgmi_plane.cc independent_plane_stream)."""
+    queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    planes = []
+    try:
+        with pytest.raises(RuntimeError, match="hardware queue"):
+            for _ in range(3 * queues):
+                planes.append(C.hip.xgmi_plane(0, C.hip.DType.F32, 1024, max_peers=2, max_lag=1, grid=8,
+                                               timeout_s=5.0))
+        assert 1 <= len(planes) <= queues, len(planes)
+    finally:
+        planes.clear()
