@@ -227,6 +227,9 @@ void bind_hip(py::module_& m) {
   h.def("device_plane", &make_device_plane, py::arg("device") = 0,
         "DataPlane whose slabs and payloads live in HBM of `device` (worker protocol on the GPU)");
 
+  h.def("size_grid_rule", &size_grid_rule, py::arg("bytes"), py::arg("grid"), py::arg("world"), py::arg("oneshot"),
+        py::arg("full_at") = int64_t{512} << 20, py::arg("cap") = 256,
+        "workgroups a default-grid launch of `bytes` (all ranks of the launch) uses (XgmiComm::launch_grid)");
   py::enum_<DType>(h, "DType").value("F32", DType::F32).value("BF16", DType::BF16).value("F16", DType::F16);
 
   py::class_<XgmiPlaneStats>(h, "XgmiPlaneStats")

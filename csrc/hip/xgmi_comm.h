@@ -89,6 +89,20 @@ enum : int32_t { kResRound = 0, kResCold = 1, kResStop = 2 };
 // last entry it consumed (its door slot may be reused)
 enum : uint32_t { kResRunning = 0, kResExiting = 1, kResExited = 2 };
 
+// The launch-size grid rule (XgmiComm::launch_grid; profiles/round4/README.md section 9):
+// workgroups for a launch moving `bytes` of input over all its ranks at device grid `grid`.
+// Two-shot style: one per 64 KiB, 64..`cap`, the full grid from `full_at`; one-shot: every
+// rank reads all `world` inputs, so one per 64 KiB of world x bytes, 64..the full grid.
+inline int size_grid_rule(int64_t bytes, int grid, int world, bool oneshot, int64_t full_at = int64_t{512} << 20,
+                          int64_t cap = 256) {
+  if (oneshot) bytes *= (world > 1 ? world : 1);
+  else if (bytes >= full_at) return grid;
+  int64_t g = bytes / (int64_t{64} << 10);
+  const int64_t hi = oneshot ? grid : cap;
+  g = g < 64 ? 64 : (g > hi ? hi : g);
+  return static_cast<int>(g < grid ? g : grid);
+}
+
 struct CommStats {
   uint64_t calls = 0, launches = 0, bytes = 0, oneshot = 0, twoshot = 0, ring = 0, threshold = 0, ll = 0, coll = 0,
            adamw = 0, stream_switches = 0;

@@ -782,10 +782,7 @@ int XgmiComm::launch_grid(int64_t bytes, bool oneshot, int64_t full_at) const {
   //   one-shot: every rank reads all P inputs, so one per 64 KiB of P x bytes, 64..full grid.
   // At the default grid only: an explicit grid is used as given.
   if (!size_grid_ || grid_ != default_grid_) return grid_;
-  if (oneshot) bytes *= std::max(1, world_);
-  else if (bytes >= full_at) return grid_;
-  const int64_t g = std::max<int64_t>(64, std::min<int64_t>(oneshot ? grid_ : 256, bytes / (int64_t{64} << 10)));
-  return static_cast<int>(std::min<int64_t>(grid_, g));
+  return size_grid_rule(bytes, grid_, world_, oneshot, full_at);
 }
 
 static bool capturing(hipStream_t s) {
@@ -1561,10 +1558,7 @@ void XgmiComm::run_coll(const std::vector<XgmiComm*>& group, Coll op, const std:
     if (c0.size_grid_ && c0.grid_ == c0.default_grid_) {
       const int64_t bytes = static_cast<int64_t>(ranks_here) * W * len * es;
       const int64_t full_at = op == Coll::ReduceScatter ? (int64_t{1} << 30) : (int64_t{512} << 20);
-      if (bytes < full_at) {
-        const int64_t g = std::min<int64_t>(c0.grid_, std::max<int64_t>(64, std::min<int64_t>(256, bytes / (int64_t{64} << 10))));
-        gcap = std::max(1, static_cast<int>(g) / ranks_here);
-      }
+      if (bytes < full_at) gcap = std::max(1, size_grid_rule(bytes, c0.grid_, W, false, full_at) / ranks_here);
     }
     const int64_t target = std::max<int64_t>(1, gcap / (W - 1));
     a.chunk = std::max(min_chunk, round_up(ceil_div(len, target), elems));

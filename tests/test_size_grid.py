@@ -1,0 +1,36 @@
+"""The launch-size grid rule (csrc/hip/xgmi_comm.h size_grid_rule, XgmiComm::launch_grid) on
+the CPU: the workgroup counts the measured table in profiles/round4/README.md section 9 asks
+for (grid sweep: 8 logical ranks x 1 MiB best at 128, x 4 MiB / 16 MiB at 256, 256 MiB at the
+full grid; one-shot over P x bytes)."""
+from akka_allreduce_1_amd._native import C
+
+R = C.hip.size_grid_rule
+KiB, MiB = 1 << 10, 1 << 20
+
+
+def test_two_shot_one_workgroup_per_64_kib_between_64_and_256():
+    assert R(8 * 256 * KiB, 512, 8, False) == 64      # 2 MiB in the launch: the floor
+    assert R(8 * MiB, 512, 8, False) == 128           # 8 ranks x 1 MiB
+    assert R(32 * MiB, 512, 8, False) == 256          # 8 x 4 MiB: the cap
+    assert R(128 * MiB, 512, 8, False) == 256         # 8 x 16 MiB
+    assert R(2 * MiB, 512, 2, False) == 64            # 2 x 1 MiB
+    assert R(8 * MiB, 512, 2, False) == 128           # 2 x 4 MiB
+
+
+def test_full_grid_from_the_limit():
+    assert R(512 * MiB, 512, 2, False) == 512         # 2 x 256 MiB
+    assert R(2048 * MiB, 512, 8, False) == 512        # 8 x 256 MiB
+    assert R(256 * MiB, 512, 4, False, 256 * MiB) == 512   # threshold kernel: full from 256 MiB
+    assert R(256 * MiB, 512, 4, False) == 256
+
+
+def test_one_shot_counts_every_input_and_may_use_the_full_grid():
+    assert R(2 * 256 * KiB, 512, 2, True) == 64       # 2 x (2 x 256 KiB) = 1 MiB
+    assert R(2 * 4 * MiB, 512, 2, True) == 256        # 2 x 8 MiB = 16 MiB
+    assert R(8 * MiB, 512, 8, True) == 512            # 8 x 8 MiB = 64 MiB: the full grid
+
+
+def test_never_above_the_device_grid():
+    assert R(64 * MiB, 128, 8, False) == 128
+    assert R(64 * MiB, 32, 8, True) == 32
+    assert R(1 * KiB, 32, 2, False) == 32
