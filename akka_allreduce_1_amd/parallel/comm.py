@@ -174,9 +174,11 @@ class XgmiCommunicator:
         self.table: list[tuple[int, str]] = []  # (max bytes, algo) from tune(); empty = built-in policy
         self._default_grid = self._c.grid
         self._grid = self._c.grid
+        self._default_sized = bool(self._c.size_grid)  # launch-size grids (MXAR_SIZE_GRID)
+        self._sized = self._default_sized
         self._default_units = self._units = self._c.units_per_wg  # MXAR_TWOSHOT_UNITS or 0 (by size)
         self._dev = self.device.index
-        self._launch: dict[str, tuple] = {}  # algo label -> (native Algo, grid)
+        self._launch: dict[str, tuple] = {}  # algo label -> (native Algo, grid, units, launch-size grid)
         self._p2p = None
         self._sdma = None
 
@@ -238,6 +240,10 @@ class XgmiCommunicator:
                 labels.append(algo)
                 if algo in ("twoshot", "ring", "ring_native") and size >= grid_min_bytes:
                     labels += [f"{algo}@{g}" for g in extra]
+                    if algo == "twoshot" and grids and self._default_sized:
+                        # the default grid sizes itself by the launch's bytes; the full grid too,
+                        # so a link-bound xGMI launch can still pick it
+                        labels.append("twoshot@full")
                 if algo == "twoshot" and self.world > 2 and self._default_units == 0 and size // self.world >= (2 << 20):
                     labels += ["twoshot~1"] + [f"twoshot@{g}~1" for g in extra]
             for algo in labels:
@@ -315,10 +321,13 @@ class XgmiCommunicator:
         code = _KERNEL_DTYPES.get(inp.dtype)
         launch = self._launch.get(algo) if code is not None else None
         if launch is not None:  # the mean is fused into the kernel (scale applied to the fp32 sum)
-            kind, grid, units = launch
+            kind, grid, units, sized = launch
             if self._grid != grid:
                 self._c.grid = grid
                 self._grid = grid
+            if self._sized != sized:  # "algo@full": the full grid at every size
+                self._c.size_grid = sized
+                self._sized = sized
             if self._units != units:  # two-shot geometry: scatter units per workgroup (0 = by size)
                 self._c.units_per_wg = units
                 self._units = units
@@ -348,13 +357,16 @@ class XgmiCommunicator:
         else:
             # "twoshot@256": workgroup count chosen by tune(); "twoshot@256~1": and one scatter
             # unit per workgroup (coarse chunks) instead of the size-based geometry
+            # "twoshot@full": the default grid without launch-size sizing
             label, _, u = algo.partition("~")
             name, _, g = label.partition("@")
             if name == "threshold":  # no lag ring, or too large for one launch
                 return self.allreduce(inp, out, op=op, algo="twoshot", stream=stream)
             if name not in ALGOS:
                 raise ValueError(f"unknown algo {algo!r}")
-            self._launch[algo] = (ALGOS[name], int(g) if g else self._default_grid, int(u) if u else self._default_units)
+            full = g == "full"
+            self._launch[algo] = (ALGOS[name], int(g) if g and not full else self._default_grid,
+                                  int(u) if u else self._default_units, self._default_sized and not full)
             return self.allreduce(inp, out, op=op, algo=algo, stream=stream)
         return out
 
@@ -506,6 +518,9 @@ class XgmiCommunicator:
         if self._grid != g:
             self._c.grid = g
             self._grid = g
+        if self._sized != self._default_sized:  # an "@full" label must not leak in here
+            self._c.size_grid = self._default_sized
+            self._sized = self._default_sized
         if self._units != self._default_units:  # a tuned "~1" two-shot label must not leak in here
             self._c.units_per_wg = self._default_units
             self._units = self._default_units

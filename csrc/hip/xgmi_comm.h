@@ -213,6 +213,9 @@ class XgmiComm {
   }
   int64_t max_chunks() const { return maxch_; }
   uintptr_t slab_address() const { return reinterpret_cast<uintptr_t>(slab_); }  // study: placement
+  // Launch-size grids at the default grid (launch_grid); false: the full grid ("algo@full").
+  bool size_grid() const { return size_grid_; }
+  void set_size_grid(bool on) { size_grid_ = on; }
   // Resident rounds: round()'s geometry for n elements computed once (plan_resident; grid 0
   // = the round does not fit a resident kernel: chunks split over workgroups, or more than
   // `max_grid` workgroups), and a kernel on `stream` that runs the rounds posted to `door`

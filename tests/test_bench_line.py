@@ -33,7 +33,7 @@ def _n8_shape(base: dict) -> dict:
                             "speedup_vs_rccl": 1.244} for k in ("all_to_all", "all_gather", "reduce_scatter")}
     sweep = []
     size = 4096
-    labels = ["ll", "oneshot", "twoshot", "twoshot@128", "twoshot@256", "twoshot~1", "twoshot@128~1",
+    labels = ["ll", "oneshot", "twoshot", "twoshot@128", "twoshot@256", "twoshot@full", "twoshot~1", "twoshot@128~1",
               "twoshot@256~1", "ring", "ring@128", "ring@256", "threshold", "rccl", "rsag"]
     while size <= 256 << 20:
         row = {"bytes": size}

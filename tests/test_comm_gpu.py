@@ -103,7 +103,8 @@ def _mp_worker(rank, world, port, results):
             # "~1": the coarse two-shot geometry the tuner tries on large blocks (one scatter
             # unit per workgroup), then the default geometry again
             for n, algo in ((100_003, "twoshot"), (5_000, "oneshot"), (1 << 20, "auto"), (3_333, "ll"),
-                            (300_001, "ll"), (100_003, "twoshot~1"), (1 << 20, "twoshot@4~1"), (1 << 20, "twoshot")):
+                            (300_001, "ll"), (100_003, "twoshot~1"), (1 << 20, "twoshot@4~1"), (1 << 20, "twoshot"),
+                            (1 << 20, "twoshot@full"), (100_003, "twoshot")):
                 xs = [fill_uniform(torch.empty(n, dtype=dtype, device=DEV), seed=k) for k in range(world)]
                 y = comm.allreduce(xs[rank], algo=algo)
                 comm.check()
