@@ -772,9 +772,10 @@ void XgmiComm::set_grid(int g) { grid_ = g > 0 ? g : default_grid_; }
 
 int XgmiComm::launch_grid(int64_t bytes, bool oneshot, int64_t full_at) const {
   // Workgroups for a two-shot / one-shot launch moving `bytes` of input (all ranks of the
-  // launch). Every unit of work pays flag hand-offs and system-scope fences, and hundreds of
-  // workgroups fencing at once serialise in the L2, so below ~512 MiB per launch the full
-  // grid loses to ~one workgroup per 64 KiB (8 / 4 / 2 logical ranks x 64 KiB - 256 MiB, same
+  // launch). Every unit of work pays flag hand-offs and fenced stores without adding bytes
+  // (PMC: 4x the workgroups at 8 x 1 MiB cost 8x the wait cycles, with no extra L2
+  // write-back / invalidate operations), so below ~512 MiB per launch the full grid loses
+  // to ~one workgroup per 64 KiB (8 / 4 / 2 logical ranks x 64 KiB - 256 MiB, same
   // box: two-shot 1 MiB x 8 ranks 36.6 -> 21.9 us, 16 MiB x 4 ranks 95.4 -> 67.8 us, 64 MiB x 2
   // ranks 132 -> 101 us, 256 MiB unchanged; profiles/round4/README.md section 9):
   //   two-shot: one workgroup per 64 KiB, 64..256, the full grid from `full_at` (512 MiB;
