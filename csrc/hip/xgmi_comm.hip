@@ -949,7 +949,14 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
     // per workgroup - more chunks per workgroup only multiply the fences (ring_grid sweep,
     // profiles/round4/README.md). MXAR_RING_GRID / MXAR_RING_DEPTH override.
     const int depth = std::max(1, c0.ring_depth_);
-    const int gring = std::max(1, std::min(gmax, c0.ring_grid_ / ranks_here));
+    // and at the default grid, one workgroup per 32 KiB of the per-rank bytes, 64..ring_grid:
+    // every hop of every workgroup is a dependent hand-off (8 / 2 logical ranks, ring_native
+    // p50 at ring grid 64 / 128 / 256 / 512: 8 x 1 MiB 51 / 62 / 99 / 162 us, 8 x 4 MiB 108 / 96
+    // / 136 / 250 us, 2 x 16 MiB 72 / 48 / 39 / 46 us; profiles/round4/ring_grid_mid.jsonl)
+    int ring_dev = c0.ring_grid_;
+    if (c0.size_grid_ && c0.grid_ == c0.default_grid_)
+      ring_dev = static_cast<int>(std::min<int64_t>(c0.ring_grid_, std::max<int64_t>(64, n * es / (int64_t{32} << 10))));
+    const int gring = std::max(1, std::min(gmax, ring_dev / ranks_here));
     a.block = round_up(ceil_div(n, W), elems);
     a.chunk = std::max(min_chunk, round_up(ceil_div(a.block, int64_t{gring} * depth), elems));
     a.nch = static_cast<int>(std::max<int64_t>(1, ceil_div(a.block, a.chunk)));
