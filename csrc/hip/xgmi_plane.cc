@@ -780,7 +780,11 @@ bool XgmiRoundPlane::launch_resident(int round, const Payload& input, bool cold)
   spec.host_abort = hforce_dev_ + 1;
   if (!rplan_tried_) {
     rplan_tried_ = true;
-    rplan_ = comm_->plan_resident(n, o_.dtype, cfg_.thReduce, cfg_.thComplete, spec, 16);
+    static const int kResGrid = [] {
+      const char* e = std::getenv("MXAR_PLANE_RESIDENT_GRID");
+      return e ? std::max(1, std::min(256, std::atoi(e))) : 64;
+    }();
+    rplan_ = comm_->plan_resident(n, o_.dtype, cfg_.thReduce, cfg_.thComplete, spec, kResGrid);
   }
   if (rplan_.grid <= 0) return false;
   Rec rec;

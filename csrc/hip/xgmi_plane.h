@@ -19,7 +19,7 @@
 //     (roundBase + r - startRound + 1), per-chunk counts and the error word copied to
 //     pinned host memory, a completion event; a completion thread hands each finished
 //     round to the worker in launch order.
-//   * resident rounds (<= 64 KiB, XgmiPlaneOptions::resident_max): instead of one launch per
+//   * resident rounds (<= 4 MiB, XgmiPlaneOptions::resident_max): instead of one launch per
 //     round, the round is written to a pinned door ring that a resident threshold kernel
 //     polls (XgmiComm::launch_resident); the kernel leaves after an idle spell or when the
 //     plane needs its stream (re-initialisation, an input that must be staged on the stream)
@@ -69,8 +69,11 @@ struct XgmiPlaneOptions {
   // Resident rounds (XgmiComm::launch_resident): rounds of at most this many bytes are posted
   // to a kernel that stays on the plane stream between rounds instead of one launch each
   // (0 = off; MXAR_PLANE_RESIDENT). The kernel leaves after `resident_idle_us` without a
-  // round (MXAR_PLANE_RESIDENT_IDLE_US) and is launched again by the next one.
-  int64_t resident_max = 64 << 10;
+  // round (MXAR_PLANE_RESIDENT_IDLE_US) and is launched again by the next one. Rounds whose
+  // geometry needs more than 64 workgroups (MXAR_PLANE_RESIDENT_GRID) or split chunks are
+  // launched. 2 workers, th 1, bench geometry: 256 KiB 38-47 -> 32-34 us, 1 MiB 44-45 ->
+  // 34-40, 4 MiB 46-52 -> 42-47 per round (profiles/round4/resident_grid_ab.jsonl).
+  int64_t resident_max = 4 << 20;
   double resident_idle_us = 1000.0;
 };
 

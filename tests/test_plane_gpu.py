@@ -818,7 +818,8 @@ def test_distributed_plane_job_master_and_bridge_driven():
 
 # ---------------------------------------------------------------------------------------
 # Resident rounds (xgmi_plane.cc launch_resident, xgmi_threshold.hip threshold_resident_kernel):
-# rounds of <= 64 KiB are posted to a kernel that stays on the plane stream between rounds.
+# rounds of <= 4 MiB (up to 64 workgroups) are posted to a kernel that stays on the plane
+# stream between rounds.
 
 def _job_with_env(env, **kw):
     """A PlaneJob whose planes see `env` (read when a plane is built)."""
@@ -835,7 +836,8 @@ def _job_with_env(env, **kw):
 
 
 @pytest.mark.parametrize("P,n,chunk,dtype", [(2, 10, 2, torch.float32), (3, 4096, 512, torch.bfloat16),
-                                             (4, 16384, 1024, torch.float32)])
+                                             (4, 16384, 1024, torch.float32), (2, 262144, 1024, torch.float32),
+                                             (2, 1 << 20, 4096, torch.bfloat16)])
 def test_resident_rounds_match_launched_rounds(P, n, chunk, dtype):
     """The same job with resident rounds (default) and with one launch per round
     (MXAR_PLANE_RESIDENT=0): identical outputs and counts, exact sums, and the resident job

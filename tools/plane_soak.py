@@ -60,7 +60,7 @@ def main() -> None:
             rounds = rng.randint(10, 40)
             slow_k, delay = rng.randrange(P), rng.uniform(0.001, 0.005)
             row = {"job": j, "P": P, "n": n, "chunk": chunk, "dtype": "float32", "max_lag": lag, "rounds": rounds,
-                   "source": f"straggler {slow_k}", "th": round(th, 3), "resident_eligible": n * 4 <= 65536}
+                   "source": f"straggler {slow_k}", "th": round(th, 3), "resident_eligible": n * 4 <= 4 << 20}
 
             def src(k):
                 base = iota_source(n, dev, torch.float32, 1000.0 * k)
@@ -122,7 +122,7 @@ def main() -> None:
         kind = rng.choice(["iota", "iota", "static", "slow"])
         es = 4 if dtype == torch.float32 else 2
         cfg = {"job": j, "P": P, "n": n, "chunk": chunk, "dtype": str(dtype).replace("torch.", ""), "max_lag": lag,
-               "rounds": rounds, "source": kind, "resident_eligible": n * es <= 65536}
+               "rounds": rounds, "source": kind, "resident_eligible": n * es <= 4 << 20}
         if kind == "static":
             stat = [(torch.arange(n, dtype=torch.float64) + 1000.0 * k).to(dtype).to(dev) for k in range(P)]
             sources = stat
