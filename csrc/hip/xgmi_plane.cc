@@ -174,6 +174,8 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
     o_.resident_max = 0;  // one hardware queue per process: a resident kernel would hold it for every stream
   if (const char* e = std::getenv("MXAR_PLANE_RESIDENT")) o_.resident_max = std::atoll(e);
   if (const char* e = std::getenv("MXAR_PLANE_RESIDENT_IDLE_US")) o_.resident_idle_us = std::atof(e);
+  if (const char* e = std::getenv("MXAR_PLANE_RESIDENT_GRID")) o_.resident_grid = std::atoi(e);
+  o_.resident_grid = std::max(1, std::min(256, o_.resident_grid));
   const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
   flag_gran_ = o_.min_chunk > 0 ? std::min<int64_t>(XgmiComm::min_chunk_bytes(), o_.min_chunk * es)
                                 : XgmiComm::min_chunk_bytes();
@@ -780,11 +782,7 @@ bool XgmiRoundPlane::launch_resident(int round, const Payload& input, bool cold)
   spec.host_abort = hforce_dev_ + 1;
   if (!rplan_tried_) {
     rplan_tried_ = true;
-    static const int kResGrid = [] {
-      const char* e = std::getenv("MXAR_PLANE_RESIDENT_GRID");
-      return e ? std::max(1, std::min(256, std::atoi(e))) : 64;
-    }();
-    rplan_ = comm_->plan_resident(n, o_.dtype, cfg_.thReduce, cfg_.thComplete, spec, kResGrid);
+    rplan_ = comm_->plan_resident(n, o_.dtype, cfg_.thReduce, cfg_.thComplete, spec, o_.resident_grid);
   }
   if (rplan_.grid <= 0) return false;
   Rec rec;

@@ -74,6 +74,7 @@ struct XgmiPlaneOptions {
   // launched. 2 workers, th 1, bench geometry: 256 KiB 38-47 -> 32-34 us, 1 MiB 44-45 ->
   // 34-40, 4 MiB 46-52 -> 42-47 per round (profiles/round4/resident_grid_ab.jsonl).
   int64_t resident_max = 4 << 20;
+  int resident_grid = 64;
   double resident_idle_us = 1000.0;
 };
 
