@@ -28,6 +28,11 @@ _H = C.hip
 ALGOS = {"auto": _H.Algo.Auto, "twoshot": _H.Algo.TwoShot, "oneshot": _H.Algo.OneShot, "ring": _H.Algo.Ring,
          "ll": _H.Algo.LL, "ring_native": _H.Algo.RingNative}
 LIBRARY_ALGOS = ("rccl", "rsag", "p2p")  # timed for comparison, never picked by tune()
+# kernels that round more than once (ring_native: every reduce-scatter hop's partial is rounded
+# to the element type): timed by tune() as comparison columns but adopted only with
+# exact_only=False - by default every tuned choice sums in fp32 and rounds once, as precise as
+# the reference's fp32 sums
+LOSSY_ALGOS = ("ring_native",)
 DEFAULT_SLOT_BYTES = int(os.environ.get("MXAR_SLOT_BYTES", 64 << 20))
 
 
@@ -206,7 +211,7 @@ class XgmiCommunicator:
     # ------------------------------------------------------------------ tuning
     def tune(self, max_bytes: int = 256 << 20, dtype: torch.dtype = torch.bfloat16, iters: int = 10,
              candidates: Sequence[str] = ("oneshot", "twoshot", "rccl"), min_bytes: int = 4 << 10,
-             grids: Sequence[int] = (), grid_min_bytes: int = 1 << 20) -> list[dict]:
+             grids: Sequence[int] = (), grid_min_bytes: int = 1 << 20, exact_only: bool = True) -> list[dict]:
         """Measure p50 latency of every algorithm per power-of-4 size class in
         [min_bytes, max_bytes] and keep the fastest per class (the slowest rank's p50
         decides; rank 0's choice is broadcast so every rank dispatches identically - a split
@@ -215,7 +220,9 @@ class XgmiCommunicator:
         every workgroup stays resident. Where the two-shot picks its flat geometry (blocks of
         >= 2 MiB: one chunk per workgroup, grouped scatter), the coarse one is tried too
         ("twoshot~1", "twoshot@256~1": one scatter unit per workgroup): on one GPU flat wins
-        by up to 22 % at 8 ranks, over xGMI links the measured choice decides. Returns one row per size: {bytes, <algo>_p50_us, choice}."""
+        by up to 22 % at 8 ranks, over xGMI links the measured choice decides. `exact_only`: the
+        per-hop-rounded kernels (LOSSY_ALGOS) are timed but never adopted. Returns one row per
+        size: {bytes, <algo>_p50_us, choice}."""
         import torch.distributed as dist
 
         from ..ops import fill_uniform
@@ -273,7 +280,9 @@ class XgmiCommunicator:
                 row[f"{algo}_algbw"] = round(size / (t.item() / 1e3) / 1e9, 2)
                 # library paths are comparison columns: the table only ever holds this
                 # framework's kernels (a split of RCCL vs xGMI is reported, never adopted)
-                if algo not in LIBRARY_ALGOS and t.item() < best_t:
+                base = algo.split("@")[0].split("~")[0]
+                if (algo not in LIBRARY_ALGOS and not (exact_only and base in LOSSY_ALGOS)
+                        and t.item() < best_t):
                     best, best_t = algo, t.item()
             if best is None:  # only library candidates were given: keep the built-in policy
                 best = "auto"

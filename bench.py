@@ -67,7 +67,8 @@ import torch.distributed as dist  # noqa: E402
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from akka_allreduce_1_amd.ops import fill_uniform  # noqa: E402
-from akka_allreduce_1_amd.parallel.comm import CommError, XgmiCommunicator, init_distributed  # noqa: E402
+from akka_allreduce_1_amd.parallel.comm import LOSSY_ALGOS, CommError, XgmiCommunicator, init_distributed  # noqa: E402
+from benchmarks.summary import headline_guard  # noqa: E402
 from akka_allreduce_1_amd.utils.timing import busbw, percentile  # noqa: E402
 
 BASELINE_VALUE = None  # the reference publishes no numbers
@@ -735,6 +736,7 @@ def main() -> None:
     ap.add_argument("--no-fused-step", action="store_true", help="skip the fused reduce-scatter + AdamW + all-gather timing")
     ap.add_argument("--no-dp", action="store_true", help="skip the ResNet-50 / Llama-3-8B DP-step sections")
     ap.add_argument("--no-local", action="store_true", help="skip the 8-logical-rank section at N = 1")
+    ap.add_argument("--no-links", action="store_true", help="skip the xGMI bring-up probes at N > 1")
     ap.add_argument("--no-protocol", action="store_true", help="skip the master/worker protocol-engine section")
     ap.add_argument("--no-native", action="store_true",
                     help="skip the native-deployment protocol rounds (child mxar processes; e.g. under a profiler)")
@@ -817,6 +819,22 @@ def main() -> None:
             except Exception as e:  # noqa: BLE001 - recorded, the run degrades to RCCL
                 engine_ok, reason = False, f"reset after failed validation: {e!r}"
     ok_algos = {k for k, v in (validated or {}).items() if v["validated"]}
+    links = None
+    if engine_ok and world > 1 and not args.no_links:
+        # the xGMI bring-up pack, before anything else is timed: per-link push rate, all-peer
+        # fan-out rate and flag hand-off latency on the engine's own store path
+        # (akka_allreduce_1_amd/utils/links.py), so a slow first multi-GPU run is attributable
+        from akka_allreduce_1_amd.utils.links import probe_links
+
+        log(rank, "xgmi_links: per-link push rates, fan-out, flag latency")
+        try:
+            links = probe_links(comm, nbytes=min(nbytes, 64 << 20))
+        except Exception as e:  # noqa: BLE001 - recorded, never loses the headline
+            links = {"error": repr(e)}
+            try:
+                comm.reset()
+            except Exception as e2:  # noqa: BLE001
+                engine_ok, reason = False, f"reset after link probe failure: {e2!r}"
     sweep = None
     if engine_ok and not args.no_tune and world > 1:  # at world = 1 every candidate is the same copy
         # RCCL / RS+AG are timed as comparison columns (rccl_p50_us, speedup_vs_rccl per size):
@@ -834,6 +852,13 @@ def main() -> None:
         # never time an unvalidated kernel ("auto" without a tuned table is the size-default
         # dispatch, checked by validate() above); a failure is reported as such, never
         # replaced by the library's number
+        # a per-hop-rounded kernel or a library path is never the automatic headline (lower
+        # precision than the reference's fp32 sums / not this engine): tune(exact_only=True)
+        # never adopts one, a hand-set table entry is replaced here and said so
+        guarded, note = headline_guard(chosen, args.algo, world)
+        if note:
+            log(rank, note)
+            status, algo, chosen = note, guarded, guarded
         if world > 1 and chosen.split("@")[0].split("~")[0] not in ok_algos | {"auto"}:
             log(rank, f"headline algorithm {chosen} failed validation")
             status = f"headline kernel {chosen} failed validation"
@@ -893,6 +918,8 @@ def main() -> None:
             "parallelism": f"dp{world}" + (" (rehearsal: all ranks on one GPU)" if args.share_device else ""),
             "tensor_bytes": nbytes,
             "algo": chosen,
+            "wire": ("element type per hop (rounded P-1 times)" if chosen.split("@")[0] in LOSSY_ALGOS
+                     else "fp32 accumulation, rounded once" if args.dtype == "bf16" else "fp32"),
         },
         "p50_ms": round(p50, 4),
         "busbw": round(busbw(algbw, world), 2),
@@ -913,6 +940,8 @@ def main() -> None:
             result["topology"] = {"error": repr(e)}
     if reason:
         result["engine_note"] = reason
+    if links is not None:
+        result["xgmi_links"] = links
 
     if engine_ok and not chosen.startswith("twoshot") and world > 1:
         for _ in range(args.warmup):

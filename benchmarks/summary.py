@@ -14,6 +14,10 @@ side file (`detail`), and the line holds the headline fields plus compact summar
                  deployment, control-bridge), plus whether the timed rounds were validated
   adamw          fused reduce-scatter + AdamW + all-gather: ms and HBM TB/s
   dp             BASELINE configs 4 / 5: [step ms, compute-only ms, exposed ms]
+  xgmi_links     N > 1: the bring-up pack (akka_allreduce_1_amd/utils/links.py) - single-peer
+                 push GB/s [min, median, max], all-peer push GB/s per rank [min, max], fan-out
+                 ratio (all-peer / single-peer, 7 links ideal = 7), one-way flag hand-off us
+                 [bare min, bare max, fenced max]; never dropped before the headline sections
 
 `line()` guarantees the encoded line stays under LINE_BUDGET bytes: if a summary section
 still overflows (e.g. a future section grows), sections are dropped in a fixed order and
@@ -30,11 +34,23 @@ HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per
                  "busbw", "engine_ok", "status")
 
 # least important first: dropped in this order if the line is still over budget
-_DROP_ORDER = ("lat_vs_size", "collectives", "sweep", "dp_overlap", "sdma_local", "protocol_us", "dp", "reduce_kernel",
-               "validation_failed", "engine_note", "adamw", "local_ranks", "threshold", "rccl")
+_DROP_ORDER = ("lat_vs_size", "collectives", "sweep", "dp_overlap", "sdma_local", "sdma", "protocol_us", "dp",
+               "reduce_kernel", "validation_failed", "engine_note", "adamw", "local_ranks", "threshold", "rccl",
+               "xgmi_links")
 
 # library paths: timed next to the kernels as comparison columns, never the headline
 LIBRARY_ALGOS = ("rccl", "rsag", "p2p")
+# per-hop-rounded kernels (parallel/comm.py LOSSY_ALGOS): never the automatic headline
+LOSSY_ALGOS = ("ring_native",)
+
+
+def headline_guard(chosen: str, requested: str, world: int) -> tuple[str, str | None]:
+    """The kernel the headline times: an automatic choice that is a library path or rounds
+    per hop becomes the two-shot (with a status note); an explicit --algo is kept."""
+    base = chosen.split("@")[0].split("~")[0]
+    if world > 1 and requested == "auto" and (base in LOSSY_ALGOS or base in LIBRARY_ALGOS):
+        return "twoshot", f"{chosen} is not a once-rounded engine kernel; headline is the two-shot"
+    return chosen, None
 
 
 def _r(x, nd=3):
@@ -133,6 +149,19 @@ def _dp(dp: dict) -> tuple[dict, dict]:
     return out, ovl
 
 
+def _links(x: dict) -> dict:
+    if not isinstance(x, dict) or "error" in x:
+        return {"error": str(x.get("error", x))[:160] if isinstance(x, dict) else "?"}
+    lat = x.get("flag_us") or {}
+    bare = [v for v in lat.get("bare") or [] if v is not None]
+    fen = [v for v in lat.get("fenced") or [] if v is not None]
+    allr = x.get("all_GBps") or []
+    return {"single_GBps": x.get("single_GBps_min_med_max"),
+            "all_GBps": [min(allr), max(allr)] if allr else None,
+            "ratio": x.get("fanout_ratio"),
+            "flag_us": [min(bare) if bare else None, max(bare) if bare else None, max(fen) if fen else None]}
+
+
 def compact(result: dict, detail_path: str | None = None) -> dict:
     """The short line: headline fields + compact summaries of every section."""
     out = {k: result[k] for k in HEADLINE_KEYS if k in result}
@@ -147,6 +176,8 @@ def compact(result: dict, detail_path: str | None = None) -> dict:
     if "rccl" in result:
         out["rccl"] = {"algbw": result["rccl"].get("algbw"), "p50_ms": result["rccl"].get("p50_ms")}
         out["speedup_vs_rccl"] = result.get("speedup_vs_rccl")
+    if "xgmi_links" in result:
+        out["xgmi_links"] = _links(result["xgmi_links"])
     if "xgmi_twoshot" in result:
         out["twoshot_algbw"] = result["xgmi_twoshot"].get("algbw")
     t = result.get("xgmi_threshold")

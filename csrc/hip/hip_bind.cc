@@ -496,6 +496,23 @@ void bind_hip(py::module_& m) {
             XgmiComm::barrier_group(comms, as_stream(stream));
           },
           py::arg("comms"), py::arg("stream") = 0)
+      .def_property_readonly("probe_max_bytes", &XgmiComm::probe_max_bytes)
+      .def(
+          "probe_push",
+          [](XgmiComm& c, uintptr_t src, int64_t bytes, uint32_t mask, int grid, uintptr_t stream) {
+            py::gil_scoped_release r;
+            c.probe_push(as_cptr(src), bytes, mask, grid, as_stream(stream));
+          },
+          py::arg("src"), py::arg("bytes"), py::arg("peer_mask"), py::arg("grid"), py::arg("stream") = 0,
+          "bring-up probe: write-through push into the S slot of every peer in peer_mask (no flags)")
+      .def(
+          "probe_pingpong",
+          [](XgmiComm& c, int peer, int iters, uint32_t nonce, bool fenced, uintptr_t out, uintptr_t stream) {
+            py::gil_scoped_release r;
+            c.probe_pingpong(peer, iters, nonce, fenced, reinterpret_cast<uint64_t*>(out), as_stream(stream));
+          },
+          py::arg("peer"), py::arg("iters"), py::arg("nonce"), py::arg("fenced"), py::arg("out"),
+          py::arg("stream") = 0, "bring-up probe: flag round trips with peer; the leader writes ticks to out[0]")
       .def("error", &XgmiComm::error)
       .def("ctl_words", &XgmiComm::ctl_words)
       .def("clear_error", &XgmiComm::clear_error)

@@ -477,7 +477,7 @@ SdmaComm::Plan SdmaComm::plan(const char* in, char* out, int64_t n, DType dt) {
   hsa_signal_store_relaxed(sl.sc, n1);
   hsa_signal_store_relaxed(sl.scf, W - 1);
   hsa_signal_store_relaxed(sl.gd, n2);
-  hsa_signal_store_relaxed(sl.gdf, W - 1);
+  hsa_signal_store_relaxed(sl.gdf, W > 1 ? W : 0);  // W - 1 peer flags + the own "phase 2 sent" flag
   const int64_t off_SD = kFlagBytes, off_RD = kFlagBytes + 2 * static_cast<int64_t>(W) * slot_bytes_;
   auto copy = [&](void* dst, hsa_agent_t da, const void* src, hsa_agent_t sa, int64_t bytes, int ndep,
                   const hsa_signal_t* deps, hsa_signal_t done, hsa_amd_sdma_engine_id_t eng) {
@@ -517,6 +517,13 @@ SdmaComm::Plan SdmaComm::plan(const char* in, char* out, int64_t n, DType dt) {
   for (int k = 0; k < W; ++k)
     if (k != r)
       copy(peers_[k] + (kFrWord + r) * 4, m.peer_agent[k], word, m.cpu, 4, 2, dep2, sl.gdf, m.peer_engines[k][0]);
+  // and the own FR[r] word once every phase-2 copy has completed: the engines read the own
+  // block of `out` for them, so the call may not count as done (and the caller may not write
+  // `out`) before they are - enqueue_gather waits for this word with the peers' 
+  if (W > 1) {
+    const int k0 = (r + 1) % W;
+    copy(slab_ + (kFrWord + r) * 4, m.own, word, m.cpu, 4, 2, dep2, sl.gdf, m.peer_engines[k0][0]);
+  }
   ++st_.calls;
   return pl;
 }
@@ -549,8 +556,9 @@ void SdmaComm::enqueue_gather(const Plan& pl, hipStream_t stream) {
   const int64_t es = static_cast<int64_t>(dtype_size(pl.dt));
   const int64_t elems = 16 / es;
   const uint64_t ticks = static_cast<uint64_t>(timeout_s_ * 1e8);
+  // every peer's reduced block AND the own phase-2 copies (FR[r], written behind them)
   hipLaunchKernelGGL(sdma_wait_kernel, dim3(1), dim3(64), 0, stream,
-                     reinterpret_cast<const uint32_t*>(slab_) + kFrWord, W, r, pl.epoch, ticks, err_);
+                     reinterpret_cast<const uint32_t*>(slab_) + kFrWord, W, W > 1 ? -1 : r, pl.epoch, ticks, err_);
   if (W < 2) return;
   const int64_t gpiece = std::max<int64_t>(elems, rup(cdiv(pl.block, std::max(1, grid_ / (W - 1))), elems));
   const int g2 = static_cast<int>(std::max<int64_t>(1, cdiv(pl.block, gpiece)));

@@ -251,6 +251,17 @@ class XgmiComm {
   // Device-side barrier over all ranks (enqueued on `stream`).
   void barrier(hipStream_t stream);
 
+  // xGMI bring-up probes (xgmi_probe.hip; bench.py `xgmi_links`), for collective quiet points
+  // only (every rank idle). probe_push: `bytes` of `src` written through into the S slot (row
+  // 0, column rank()) of every peer in `peer_mask`, one launch, `grid` workgroups per peer -
+  // the scatter's store path, no flags. probe_pingpong: `iters` flag round trips with `peer`
+  // (both ranks call it concurrently with the same iters / nonce; the lower rank leads and
+  // writes the elapsed 100 MHz ticks to out[0], 0 on timeout); `fenced` adds the kernels'
+  // release / acquire around each hand-off.
+  int64_t probe_max_bytes() const;
+  void probe_push(const void* src, int64_t bytes, uint32_t peer_mask, int grid, hipStream_t stream);
+  void probe_pingpong(int peer, int iters, uint32_t nonce, bool fenced, uint64_t* out, hipStream_t stream);
+
   // Fused data-parallel step (xgmi_adam.hip): grads [n] of every rank are reduce-scattered
   // (x scale, fp32), the owner applies AdamW to its shard state, and the updated parameters
   // are all-gathered into `params` [n] (identical on every rank). One launch; n * dtype must

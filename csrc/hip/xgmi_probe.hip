@@ -1,0 +1,113 @@
+// xGMI bring-up probes (bench.py `xgmi_links`; XgmiComm::probe_push / probe_pingpong).
+//
+// The reference's whole data plane is the all-peer fan-out: every worker scatters a chunk to
+// every other worker (AllreduceWorker.scala:194-209) and broadcasts every reduced chunk to
+// all of them (:230-238). On an 8 x MI355X node that is 7 xGMI links per GPU driven at once.
+// Before the first multi-GPU allreduce is timed, these probes measure what those links give
+// THIS store path - the two-shot's own write-through `st16_wt` pushes into a peer's
+// fine-grained slab and its relaxed system-scope flag store + poll - so a slow or failing
+// first 8-GPU run says whether the links, the flag hand-off or the kernels are at fault:
+//   * probe_push: raw push rate into one peer, or into every peer at once (gridDim.y = peers);
+//   * probe_pingpong: flag round trip between two ranks, relaxed (the wire) and with the
+//     kernels' release / acquire fences (the production hand-off).
+// Neither touches a flag word or a control word of the collectives: the push lands in the
+// S slot the two-shot's scatter writes (row 0, column = this rank) and the ping-pong words
+// sit at the end of that slot, past any probe payload. Callers run them between collective
+// quiet points (every rank idle, barriers around), which bench.py does.
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+
+#include "xgmi_device.h"
+
+namespace mxar {
+
+namespace {
+
+struct ProbeArgs {
+  const char* src;
+  char* dst[kMaxRanks];
+  int64_t bytes;  // per destination, a multiple of 16
+};
+
+// Workgroup x of row y copies its contiguous piece of src into dst[y] (16 B per lane, nt
+// loads, write-through stores: copy_to_slab, the scatter's copy loop).
+__global__ __launch_bounds__(kCommThreads) void probe_push_kernel(ProbeArgs a) {
+  const int64_t npk = a.bytes / 16;
+  const int64_t per = (npk + gridDim.x - 1) / gridDim.x;
+  const int64_t p0 = static_cast<int64_t>(blockIdx.x) * per;
+  const int64_t len = clamp_len(npk - p0, per);
+  if (len > 0) copy_to_slab<F32>(a.dst[blockIdx.y] + p0 * 16, a.src + p0 * 16, len * F32::ELEMS);
+}
+
+// One lane per side. Token i of this probe = nonce << 16 | i (the words may hold any older
+// value, never one of these tokens unless the nonce repeats). Leader: store, then wait for the
+// echo; echo: wait, then store back. `fenced`: the kernels' hand-off (system release before the
+// store, system acquire after the wait) instead of the bare relaxed store / poll.
+__global__ void probe_pingpong_kernel(uint32_t* mine, uint32_t* theirs, int leader, int iters, uint32_t nonce,
+                                      int fenced, uint64_t timeout, uint64_t* out, uint32_t* err) {
+  if (threadIdx.x != 0) return;
+  const uint64_t deadline = wall_ticks() + timeout;
+  bool ok = true;
+  const uint64_t t0 = wall_ticks();
+  for (int i = 1; i <= iters && ok; ++i) {
+    const uint32_t tok = (nonce << 16) | static_cast<uint32_t>(i);
+    if (leader) {
+      if (fenced) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      st_flag(theirs, tok);
+    }
+    while (ld_flag(mine) != tok) {
+      if (wall_ticks() > deadline) {
+        ok = false;
+        break;
+      }
+    }
+    if (fenced) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (!leader && ok) {
+      if (fenced) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      st_flag(theirs, tok);
+    }
+  }
+  const uint64_t t1 = wall_ticks();
+  if (!ok) __hip_atomic_fetch_or(err, ERR_TIMEOUT_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  out[0] = ok ? t1 - t0 : 0;
+}
+
+}  // namespace
+
+int64_t XgmiComm::probe_max_bytes() const { return slot_bytes_ - 4096; }
+
+void XgmiComm::probe_push(const void* src, int64_t bytes, uint32_t peer_mask, int grid, hipStream_t stream) {
+  if (!connected_) throw std::runtime_error("XgmiComm.probe_push: connect() first");
+  if (bytes <= 0 || bytes % 16 || bytes > probe_max_bytes() || (reinterpret_cast<uintptr_t>(src) & 15))
+    throw std::invalid_argument("XgmiComm.probe_push: bytes must be a positive multiple of 16 <= probe_max_bytes() "
+                                "and src 16-byte aligned");
+  ProbeArgs a{};
+  a.src = static_cast<const char*>(src);
+  a.bytes = bytes;
+  int np = 0;
+  for (int k = 0; k < world_; ++k)
+    if (k != rank_ && (peer_mask >> k) & 1u) a.dst[np++] = peers_[k] + off_S_ + static_cast<int64_t>(rank_) * slot_stride_;
+  if (np == 0) return;
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  order_after_last(stream);
+  const int gx = std::max(1, grid);
+  hipLaunchKernelGGL(probe_push_kernel, dim3(gx, np), dim3(kCommThreads), 0, stream, a);
+  hip_check(hipGetLastError(), "probe_push launch");
+}
+
+void XgmiComm::probe_pingpong(int peer, int iters, uint32_t nonce, bool fenced, uint64_t* out, hipStream_t stream) {
+  if (!connected_) throw std::runtime_error("XgmiComm.probe_pingpong: connect() first");
+  if (peer < 0 || peer >= world_ || peer == rank_ || iters < 1 || iters > 65535)
+    throw std::invalid_argument("XgmiComm.probe_pingpong: bad peer or iters (1..65535)");
+  const int64_t word = slot_bytes_ - 64;  // past any probe_push payload (probe_max_bytes)
+  uint32_t* mine = reinterpret_cast<uint32_t*>(slab_ + off_S_ + static_cast<int64_t>(peer) * slot_stride_ + word);
+  uint32_t* theirs = reinterpret_cast<uint32_t*>(peers_[peer] + off_S_ + static_cast<int64_t>(rank_) * slot_stride_ + word);
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  order_after_last(stream);
+  hipLaunchKernelGGL(probe_pingpong_kernel, dim3(1), dim3(64), 0, stream, mine, theirs, rank_ < peer ? 1 : 0, iters,
+                     nonce & 0xFFFFu, fenced ? 1 : 0, static_cast<uint64_t>(timeout_s_ * 1e8), out, ctl_ + 2);
+  hip_check(hipGetLastError(), "probe_pingpong launch");
+}
+
+}  // namespace mxar

@@ -123,3 +123,97 @@ def test_tuner_table_never_yields_a_library_path():
         assert c._pick(nbytes).split("@")[0] not in LIBRARY_ALGOS
     c.table = [(256 << 20, "twoshot@256")]
     assert c._pick(1 << 30) == "twoshot@256"
+
+
+def _links(P: int = 8) -> dict:
+    """An N = 8 xgmi_links section (akka_allreduce_1_amd/utils/links.py) at its widest."""
+    return {"bytes": 67108864, "reps": 5, "grid_per_peer": 64, "store": "st16_wt (two-shot scatter path)",
+            "push_GBps": [[0.0 if k == r else 123.45 for k in range(P)] for r in range(P)],
+            "all_GBps": [812.34] * P, "single_GBps_min_med_max": [101.23, 123.45, 131.11], "fanout_ratio": 6.58,
+            "flag_us": {"bare": [None] + [1.234] * (P - 1), "fenced": [None] + [1.567] * (P - 1)}}
+
+
+def test_n8_line_carries_the_link_pack():
+    r = _n8_shape(_full_n1())
+    r["xgmi_links"] = _links()
+    s = line(r, "gpurun_out/bench_detail_n8.json")
+    assert len(s.encode()) <= LINE_BUDGET
+    d = json.loads(s)
+    assert "dropped" not in d
+    assert d["xgmi_links"] == {"single_GBps": [101.23, 123.45, 131.11], "all_GBps": [812.34, 812.34],
+                               "ratio": 6.58, "flag_us": [1.234, 1.234, 1.567]}
+    assert d["config"]["algo"].split("@")[0].split("~")[0] not in ("ring_native", "rccl", "rsag")
+
+
+def test_link_pack_outlives_every_other_section():
+    r = _n8_shape(_full_n1())
+    r["xgmi_links"] = _links()
+    r["engine_note"] = "e" * 5000
+    r["latency_vs_size"]["P8"] = r["latency_vs_size"]["P8"] * 60
+    r["sweep"] = r["sweep"] * 10
+    d = json.loads(line(r))
+    assert "xgmi_links" in d and "lat_vs_size" in d["dropped"]
+
+
+def test_headline_guard_keeps_lossy_and_library_paths_out():
+    from akka_allreduce_1_amd.parallel import comm
+    from benchmarks.summary import LOSSY_ALGOS, headline_guard
+
+    assert tuple(comm.LOSSY_ALGOS) == LOSSY_ALGOS and tuple(comm.LIBRARY_ALGOS) == LIBRARY_ALGOS
+    for auto_pick in ("ring_native", "ring_native@128", "rccl", "rsag"):
+        algo, note = headline_guard(auto_pick, "auto", 8)
+        assert algo == "twoshot" and note
+    for ok in ("twoshot@256~1", "ring", "oneshot", "ll", "auto"):
+        assert headline_guard(ok, "auto", 8) == (ok, None)
+    assert headline_guard("ring_native", "ring_native", 8) == ("ring_native", None)  # explicit --algo
+
+
+def test_tuner_never_adopts_a_lossy_kernel(monkeypatch):
+    """tune() times ring_native as a comparison column but, with exact_only (the default),
+    keeps a once-rounded kernel as the choice even when ring_native is fastest."""
+    import torch
+
+    from akka_allreduce_1_amd.parallel.comm import XgmiCommunicator
+
+    import torch.distributed as dist
+
+    c = object.__new__(XgmiCommunicator)
+    c.rank, c.world, c.device, c.slot_bytes, c.cpu_group, c.group = 0, 8, torch.device("cpu"), 64 << 20, None, None
+    c._default_grid, c._default_sized, c._default_units = 512, True, 0
+
+    class _C:
+        ll_max_bytes = 512 << 10
+        threshold_rows = 0
+
+    c._c = _C()
+    speed = {"twoshot": 2.0, "ring_native": 1.0, "oneshot": 3.0}
+    cur = {}
+
+    def fake_allreduce(a, b, algo="auto", **kw):
+        cur["algo"] = algo
+
+    class _Ev:
+        def __init__(self, enable_timing=True):
+            pass
+
+        def record(self):
+            self.algo = cur.get("algo")
+
+        def elapsed_time(self, other):
+            return speed.get(other.algo.split("@")[0], 9.0)
+
+    c.allreduce = fake_allreduce
+    c.check = lambda: None
+    monkeypatch.setattr(torch.cuda, "Event", _Ev)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    monkeypatch.setattr(dist, "all_reduce", lambda *a, **k: None)
+    monkeypatch.setattr(dist, "broadcast_object_list", lambda *a, **k: None)
+    monkeypatch.setattr(dist, "get_backend", lambda *a, **k: "gloo")
+    import akka_allreduce_1_amd.ops as ops
+
+    monkeypatch.setattr(ops, "fill_uniform", lambda t, seed=0: t)
+    rows = c.tune(max_bytes=64 << 10, min_bytes=16 << 10, candidates=("twoshot", "ring_native"), iters=2)
+    assert all(r["choice"] == "twoshot" for r in rows) and all("ring_native_p50_us" in r for r in rows)
+    rows = c.tune(max_bytes=64 << 10, min_bytes=16 << 10, candidates=("twoshot", "ring_native"), iters=2,
+                  exact_only=False)
+    assert all(r["choice"] == "ring_native" for r in rows)

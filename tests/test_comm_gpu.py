@@ -462,3 +462,67 @@ def test_reset_recovers_after_a_missed_collective():
             p.kill()
     bad = [r for r in res if not r[1]]
     assert not bad, bad
+
+
+def _links_worker(rank, world, port, results):
+    """The xGMI bring-up pack (utils/links.py) between processes sharing the GPU: every probe
+    returns rates and latencies, and the collectives around it still validate (the probes
+    touch no flag or control word)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import datetime
+
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.parallel import XgmiCommunicator
+    from akka_allreduce_1_amd.utils.links import probe_links
+
+    torch.cuda.set_device(0)
+    ok, msg, info = True, "", None
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
+    try:
+        comm = XgmiCommunicator(device=0, slot_bytes=8 << 20, grid=8, timeout_s=10.0)
+        n = 100_003
+        xs = [fill_uniform(torch.empty(n, device=DEV), seed=k) for k in range(world)]
+        y0 = comm.allreduce(xs[rank], algo="twoshot")
+        info = probe_links(comm, nbytes=4 << 20, reps=2, iters=200, grid=4)
+        y1 = comm.allreduce(xs[rank], algo="twoshot")
+        y2 = comm.allreduce(xs[rank], algo="oneshot")
+        comm.check()
+        for y in (y0, y1, y2):
+            err = (y - _ref(xs)).abs().max().item()
+            if err > 1e-5:
+                ok, msg = False, f"err {err} after the probe"
+        singles = [v for i, row in enumerate(info["push_GBps"]) for k, v in enumerate(row) if k != i]
+        if not (len(info["all_GBps"]) == world and min(singles) > 0 and min(info["all_GBps"]) > 0):
+            ok, msg = False, f"rates {info}"
+        lat = info["flag_us"]
+        if rank == 0 and not all(lat[m][k] and lat[m][k] > 0 for m in ("bare", "fenced") for k in range(1, world)):
+            ok, msg = False, f"latencies {lat}"
+    except Exception as e:  # noqa: BLE001 - report, never hang the parent
+        ok, msg = False, repr(e)
+    results.put((rank, ok, msg, info if rank == 0 else None))
+    dist.destroy_process_group()
+
+
+def test_multiprocess_link_probes():
+    from akka_allreduce_1_amd.parallel import free_port
+
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_links_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = []
+    try:
+        res = [q.get(timeout=150) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    bad = [r[:3] for r in res if not r[1]]
+    assert not bad, bad
+    info = next(r[3] for r in res if r[0] == 0)
+    print("link probes:", info["single_GBps_min_med_max"], info["all_GBps"], info["flag_us"])
