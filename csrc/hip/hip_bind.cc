@@ -240,6 +240,7 @@ void bind_hip(py::module_& m) {
       .def_readonly("completed", &XgmiPlaneStats::completed)
       .def_readonly("coarsened", &XgmiPlaneStats::coarsened)
       .def_readonly("pool_grown", &XgmiPlaneStats::pool_grown)
+      .def_readonly("resident_pool_misses", &XgmiPlaneStats::resident_pool_misses)
       .def_readonly("resident_rounds", &XgmiPlaneStats::resident_rounds)
       .def_readonly("resident_launches", &XgmiPlaneStats::resident_launches)
       .def_readonly("resident_parks", &XgmiPlaneStats::resident_parks)

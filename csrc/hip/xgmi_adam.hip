@@ -14,6 +14,7 @@
 // Slot reuse across launches is the two-shot's: a rank finishes a launch only after it has
 // received every owner's updated chunk, which each owner sends after reading its S slot for
 // that chunk; peers' pending reads of R are covered by entry_guard / finish_launch_done.
+#include "../core/env.h"
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -231,11 +232,11 @@ static void launch_adamw_t(const CommArgs& a, dim3 grid, hipStream_t s, DType dt
 void launch_adamw(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {
   // study knobs: MXAR_ADAM_STREAM (state access form, above), MXAR_ADAM_U (packs per lane)
   static const int mode = [] {
-    const char* e = std::getenv("MXAR_ADAM_STREAM");
+    const char* e = study_env("MXAR_ADAM_STREAM");
     return e != nullptr ? std::atoi(e) : 0;
   }();
   static const int u = [] {
-    const char* e = std::getenv("MXAR_ADAM_U");
+    const char* e = study_env("MXAR_ADAM_U");
     return e != nullptr ? std::atoi(e) : 2;
   }();
   if (mode == 1)

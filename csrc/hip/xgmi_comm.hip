@@ -9,6 +9,7 @@
 //   [R : P slots x slot_bytes]   R_k[j] = reduced block j, pushed by its owner j
 // Flags hold the epoch of the launch that wrote them; epochs come from a device counter
 // so launches replay correctly under hipGraph capture.
+#include "../core/env.h"
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -576,7 +577,7 @@ XgmiComm::Layout XgmiComm::layout(int world, int64_t slot_bytes, int threshold_r
   // no gain for the reduce kernel (benchmarks/bench_reduce.py --pad-kib, profiles/reduce_kernel.md),
   // so the knob stays for study.
   int64_t pad = 0;
-  if (const char* e = std::getenv("MXAR_SLOT_PAD")) pad = round_up(std::max<int64_t>(0, std::atoll(e)), 4096);
+  if (const char* e = study_env("MXAR_SLOT_PAD")) pad = round_up(std::max<int64_t>(0, std::atoll(e)), 4096);
   L.slot_stride = L.slot_bytes + pad;
   L.off_R = L.off_S + rows * world * L.slot_stride;
   // low-latency one-shot slots: [2 parities][P sources] x ll_slot (two 8-B LL words per
@@ -597,7 +598,7 @@ XgmiComm::Layout XgmiComm::layout(int world, int64_t slot_bytes, int threshold_r
 }
 
 int64_t XgmiComm::ipc_safe_bytes(int64_t bytes) {
-  if ((bytes & (int64_t{1} << 31)) && !std::getenv("MXAR_IPC_NO_PAD")) return round_up(bytes, int64_t{1} << 32);
+  if ((bytes & (int64_t{1} << 31)) && !study_env("MXAR_IPC_NO_PAD")) return round_up(bytes, int64_t{1} << 32);
   return bytes;
 }
 
@@ -639,41 +640,39 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   default_grid_ = default_grid(device);
   if (grid_ <= 0) grid_ = default_grid_;
   if (const char* e = std::getenv("MXAR_SIZE_GRID")) size_grid_ = std::atoi(e) != 0;
-  if (const char* f = std::getenv("MXAR_FENCE")) fence_ = std::atoi(f) & 3;
+  if (const char* f = study_env("MXAR_FENCE")) fence_ = std::atoi(f) & 3;
   // Slab reads are `nt` loads: the acquire after each wait (bit 1) is what orders them after
   // the peers' flags. Without it a stale line could be read, so clearing it is a study-only
   // setting that must be asked for explicitly.
-  if (!(fence_ & 2) && !std::getenv("MXAR_STUDY"))
-    throw std::invalid_argument("MXAR_FENCE without bit 1 (acquire) needs MXAR_STUDY=1: slab reads rely on it");
-  if (const char* u = std::getenv("MXAR_TWOSHOT_UNITS")) units_per_wg_ = std::max(1, std::atoi(u));
-  if (const char* u = std::getenv("MXAR_TWOSHOT_SUB")) sub_max_ = std::max(1, std::atoi(u));
-  if (const char* d = std::getenv("MXAR_RING_DEPTH")) ring_depth_ = std::max(1, std::atoi(d));
+  if (const char* u = study_env("MXAR_TWOSHOT_UNITS")) units_per_wg_ = std::max(1, std::atoi(u));
+  if (const char* u = study_env("MXAR_TWOSHOT_SUB")) sub_max_ = std::max(1, std::atoi(u));
+  if (const char* d = study_env("MXAR_RING_DEPTH")) ring_depth_ = std::max(1, std::atoi(d));
   if (const char* g = std::getenv("MXAR_RING_GRID")) ring_grid_ = std::max(1, std::atoi(g));
   if (const char* t = std::getenv("MXAR_THRESHOLD_LL_MAX")) thr_ll_max_ = std::max<int64_t>(0, std::atoll(t));
-  if (const char* d = std::getenv("MXAR_TWOSHOT_DYNAMIC")) dynamic_ = std::atoi(d) != 0;
-  if (const char* f = std::getenv("MXAR_RING_FLAGS")) {
+  if (const char* d = study_env("MXAR_TWOSHOT_DYNAMIC")) dynamic_ = std::atoi(d) != 0;
+  if (const char* f = study_env("MXAR_RING_FLAGS")) {
     // the round-3 layout whose flag words had two writers (ring hop rows vs other kernels'
     // writer rows): kept only as the negative control of tests/test_comm_gpu.py
     ring_hop_rows_ = std::string(f) == "hop";
-    if (ring_hop_rows_ && !std::getenv("MXAR_STUDY"))
-      throw std::invalid_argument("MXAR_RING_FLAGS=hop is a known-broken layout: set MXAR_STUDY=1 to use it");
   }
-  if (const char* g = std::getenv("MXAR_SLOT_GUARD")) noguard_ = std::atoi(g) == 0;
-  if (const char* g = std::getenv("MXAR_TWOSHOT_GEOM")) {
+  if (const char* g = study_env("MXAR_SLOT_GUARD")) noguard_ = std::atoi(g) == 0;
+  // A/B of the threshold kernel's lag-gate shortcut
+  if (const char* g = study_env("MXAR_GATE_SHORTCUT")) no_gate_shortcut_ = std::atoi(g) == 0;
+  if (const char* g = study_env("MXAR_TWOSHOT_GEOM")) {
     const std::string v = g;
     geom_ = v == "coarse" ? 0 : v == "fine" ? 1 : v == "flat" ? 2 : -1;
   }
-  if (const char* f = std::getenv("MXAR_TWOSHOT_FLAT_MIN")) flat_min_ = std::max<int64_t>(0, std::atoll(f));
+  if (const char* f = study_env("MXAR_TWOSHOT_FLAT_MIN")) flat_min_ = std::max<int64_t>(0, std::atoll(f));
 
   hip_check(hipSetDevice(device_), "hipSetDevice");
-  const char* mem = std::getenv("MXAR_SLAB_MEM");
+  const char* mem = study_env("MXAR_SLAB_MEM");
   const std::string kind = mem ? mem : "fine";
   // study knobs that trade away correctness guarantees: say so once per communicator
-  if (fence_ != 3 || kind != "fine" || std::getenv("MXAR_IPC_NO_PAD"))
+  if (fence_ != 3 || kind != "fine" || (study_mode() && std::getenv("MXAR_IPC_NO_PAD")))
     std::fprintf(stderr,
                  "[mxar] WARNING rank %d: study settings active (MXAR_FENCE=%d, MXAR_SLAB_MEM=%s%s); "
                  "results may be wrong - use the defaults in production\n",
-                 rank_, fence_, kind.c_str(), std::getenv("MXAR_IPC_NO_PAD") ? ", MXAR_IPC_NO_PAD" : "");
+                 rank_, fence_, kind.c_str(), (study_mode() && std::getenv("MXAR_IPC_NO_PAD")) ? ", MXAR_IPC_NO_PAD" : "");
   if (external_slab != nullptr) {
     // An arena owned by the caller (xgmi_plane.cc): allocated fine-grained and zeroed ONCE,
     // exported before any peer knew it, and laid out again on every re-initialisation. Its
@@ -1352,6 +1351,11 @@ bool XgmiComm::threshold_args(const std::vector<XgmiComm*>& group, const std::ve
                              : std::max(1, f32_threshold_count(thc, static_cast<int>(total)));
   }
   a.full = (a.min_reduce >= W && thc >= 1.f) ? 1 : 0;
+  // the lag-gate shortcut (xgmi_threshold.hip): rows for two rounds in flight, and a clean
+  // round proves something about EVERY peer - each block holds a chunk, or nothing but a
+  // complete round counts as clean (full thresholds)
+  a.gate_shortcut = (c0.rows_ - 1 >= 2 && (a.full || n > static_cast<int64_t>(W - 1) * a.block) &&
+                     !c0.no_gate_shortcut_) ? 1 : 0;
   a.counts = counts;
   if (spec != nullptr) {
     a.epoch_set = spec->epoch;

@@ -88,6 +88,11 @@ struct CommArgs {
   // unit (j, c); split_ctr: slice counters, [c] reduce, [maxch + j * maxch + c] scatter;
   // split_early: [j * maxch + c] = epoch when gather unit (j, c) was in at launch
   int sgroup;  // threshold kernel, unsplit chunks: chunks per scatter unit (one copy, one release)
+  // threshold kernel: the lag gate of round e may be taken as open when this rank's round e - 1
+  // was clean (it gathered every peer's reduced chunk of e - 1, so every peer had finished
+  // e - 2). Set by the host when that proof holds: trows >= 2 and every rank's block holds at
+  // least one chunk or the thresholds are full (XgmiComm::threshold_args).
+  int gate_shortcut;
   uint64_t* split_dec;
   uint32_t* split_ctr;
   uint32_t* split_early;
@@ -262,19 +267,49 @@ __device__ __forceinline__ void reduce_to(int P, const RedSrc& src, int ndst, in
       }
     }
   }
-  for (; i < npk; i += kCommThreads) {
-    Acc<E> acc;
-    acc.zero();
-    for (int s = 0; s < P; ++s) acc.add(ld16_nt(src.rsrc(s), static_cast<uint32_t>(i * 16)));
-    if (scale != 1.f) acc.scale(scale);
-    const Pack16 o = acc.pack();
+  // runtime P (and the tail of a static-P launch): the sources' packs load in batches of 8
+  // before their adds (one memory latency per batch, not one per source); a source past P
+  // loads nothing and adds +0, exact (acc starts at +0 and is never -0)
+  auto store_all = [&](int64_t at, const Pack16& o) {
     for (int k = 0; k < ndst; ++k) {
       char* d = dst(k);
       if (d == nullptr) continue;
       if (k == own_dst && !wt_out)
-        st16(d + i * 16, o);
+        st16(d + at * 16, o);
       else
-        st16_wt(slab_rsrc(d), static_cast<uint32_t>(i * 16), o);
+        st16_wt(slab_rsrc(d), static_cast<uint32_t>(at * 16), o);
+    }
+  };
+  for (; i < npk; i += U * kCommThreads) {
+    const int nu = i + kCommThreads < npk ? 2 : 1;
+    Acc<E> acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u].zero();
+    for (int s0 = 0; s0 < P; s0 += 8) {
+      Pack16 v[8][U];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int s = s0 + q;
+        const __amdgpu_buffer_rsrc_t rs = src.rsrc(s < P ? s : 0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (s < P && u < nu) {
+            v[q][u] = ld16_nt(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
+          } else {
+            v[q][u][0] = v[q][u][1] = v[q][u][2] = v[q][u][3] = 0u;
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u].add(v[q][u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u >= nu) break;
+      if (scale != 1.f) acc[u].scale(scale);
+      store_all(i + u * kCommThreads, acc[u].pack());
     }
   }
   const int64_t t = npk * E::ELEMS + threadIdx.x;

@@ -1,3 +1,4 @@
+#include "../core/env.h"
 #include "xgmi_plane.h"
 
 #include <sys/prctl.h>
@@ -83,7 +84,7 @@ hipStream_t independent_plane_stream(int device, int priority, bool* probed_ok) 
     // No independent queue left: a round kernel of this plane would queue behind a co-located
     // plane's round kernel that waits for it, and every round would wait out its deadline. Say
     // so now rather than hang (MXAR_PLANE_SHARED_QUEUE_OK=1 keeps the last candidate anyway).
-    const char* e = std::getenv("MXAR_PLANE_SHARED_QUEUE_OK");
+    const char* e = study_env("MXAR_PLANE_SHARED_QUEUE_OK");
     if (e == nullptr || std::atoi(e) == 0) {
       throw std::runtime_error(
           "xgmi plane: no hardware queue independent of the " + std::to_string(g_plane_streams.size()) +
@@ -168,8 +169,8 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   if (const char* e = std::getenv("MXAR_PLANE_SPLIT")) o_.split = std::atoi(e) != 0;  // A/B knob
   // A/B knob: 1 = also record an event per round and confirm completion with it (round 2's
   // form; ~2-3 us of hipEventRecord on every launch, profiles/round3/api_cost.json)
-  if (const char* e = std::getenv("MXAR_PLANE_EVENTS")) event_confirm_ = std::atoi(e) != 0;
-  if (const char* e = std::getenv("MXAR_PLANE_COARSEN")) coarsen_full_ = std::atoi(e) != 0;  // A/B knob
+  if (const char* e = study_env("MXAR_PLANE_EVENTS")) event_confirm_ = std::atoi(e) != 0;
+  if (const char* e = study_env("MXAR_PLANE_COARSEN")) coarsen_full_ = std::atoi(e) != 0;  // A/B knob
   if (const char* q = std::getenv("GPU_MAX_HW_QUEUES"); q != nullptr && std::atoi(q) == 1)
     o_.resident_max = 0;  // one hardware queue per process: a resident kernel would hold it for every stream
   if (const char* e = std::getenv("MXAR_PLANE_RESIDENT")) o_.resident_max = std::atoll(e);
@@ -344,6 +345,7 @@ XgmiRoundPlane::~XgmiRoundPlane() {
     forget_plane_stream(stream_);
     (void)hipStreamDestroy(stream_);
   }
+  if (alloc_stream_) (void)hipStreamDestroy(alloc_stream_);
   if (arena_) (void)hipFree(arena_);
 }
 
@@ -360,7 +362,7 @@ std::shared_ptr<void> XgmiRoundPlane::buffer(size_t bytes, bool user_visible) {
   // the same block from the pool and overwrite it under that work.
   std::weak_ptr<ReleaseQ> rq = rel_;
   static const bool via_event = [] {
-    const char* e = std::getenv("MXAR_PLANE_RELEASE");
+    const char* e = study_env("MXAR_PLANE_RELEASE");
     return e != nullptr && std::string(e) == "event";
   }();
   return std::shared_ptr<void>(p, [s, alive, user_visible, rq](void* q) {
@@ -449,7 +451,10 @@ void XgmiRoundPlane::reset_pool(size_t bytes) {
   // about 3 outputs are live at once (the round in flight, the one a sink holds, the one
   // being released): grow the pool now - growing it on the round path costs ~8 ms per
   // 256 MiB buffer (profiles/round2/sync_probe.md)
-  std::vector<void*> warm(3, nullptr);
+  // (resident-size rounds - every round then draws from this pool, see resident_out - keep
+  // more: a sink holding a few outputs must not push rounds off the resident kernel)
+  const bool resident_size = o_.resident_max > 0 && static_cast<int64_t>(bytes) <= o_.resident_max;
+  std::vector<void*> warm(resident_size ? 8 : 3, nullptr);
   for (void*& w : warm) hip_check(hipMallocAsync(&w, bytes, stream_), "hipMallocAsync(pool)");
   std::lock_guard<std::mutex> g(rel_->mu);
   for (void* w : warm) rel_->free.push_back(w);
@@ -731,15 +736,35 @@ std::shared_ptr<void> XgmiRoundPlane::resident_out(size_t bytes, std::shared_ptr
     rel_spare_.push_back(rel_pend_.front().first);
     rel_pend_.pop_front();
   }
-  bool grow = false;
+  bool empty = false;
   {
     std::lock_guard<std::mutex> g(rel_->mu);
-    grow = rel_->free.empty();
-    if (grow) {
-      void* p = nullptr;
-      hip_check(hipMalloc(&p, bytes), "hipMalloc(plane output)");
-      rel_->free.push_back(p);
-      st_.pool_grown++;
+    empty = rel_->free.empty();
+  }
+  if (empty) {
+    // Grow the pool with pool memory (hipMallocAsync) on the plane's idle allocation stream:
+    // the kernel already running on the plane stream may use it once that stream has passed
+    // the allocation - never a plain hipMalloc, whose later hipFreeAsync would fall back to a
+    // device-wide synchronous free (the hazard for co-located planes' spinning kernels; ADVICE
+    // r4). If the allocation stream does not get there within 100 us (it shares a hardware
+    // queue with busy work), this round takes the launch path instead - no host wait on
+    // another plane's kernel. reset_pool pre-grows resident-size pools, so this is rare.
+    void* p = nullptr;
+    if (alloc_stream_ == nullptr)
+      hip_check(hipStreamCreateWithFlags(&alloc_stream_, hipStreamNonBlocking), "hipStreamCreate(plane alloc)");
+    hip_check(hipMallocAsync(&p, bytes, alloc_stream_), "hipMallocAsync(plane output)");
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t q;
+    while ((q = hipStreamQuery(alloc_stream_)) == hipErrorNotReady &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(100))
+      __builtin_ia32_pause();
+    (void)hipGetLastError();
+    std::lock_guard<std::mutex> g(rel_->mu);
+    rel_->free.push_back(p);  // usable by the launch path in any case (stream-ordered after it)
+    st_.pool_grown++;
+    if (q != hipSuccess) {
+      st_.resident_pool_misses++;
+      return nullptr;
     }
   }
   return out_buffer(bytes, exported);

@@ -81,6 +81,7 @@ struct XgmiPlaneOptions {
 struct XgmiPlaneStats {
   uint64_t launches = 0, cold = 0, forced = 0, bytes = 0, completed = 0, coarsened = 0, peer_maps = 0;
   uint64_t pool_grown = 0;  // round outputs the pool had to allocate (none after warm-up in steady state)
+  uint64_t resident_pool_misses = 0;  // resident-size rounds launched instead: pool growth not ready in time
   uint64_t resident_rounds = 0, resident_launches = 0, resident_parks = 0;
 };
 
@@ -165,6 +166,7 @@ class XgmiRoundPlane final : public RoundPlane {
   uint32_t* hforce_ = nullptr;      // pinned host words the engine raises: [0] force, [1] abort
   uint32_t* hforce_dev_ = nullptr;  // their device-visible address
   hipStream_t stream_ = nullptr;
+  hipStream_t alloc_stream_ = nullptr;  // idle stream for resident-round output growth (resident_out)
   std::unique_ptr<XgmiComm> comm_;
   std::map<std::string, char*> mapped_;  // peer IPC handle -> mapping (kept across epochs)
   PlaneConfig cfg_;

@@ -41,6 +41,8 @@
 //                host WorkerCore for the same arrival order.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "xgmi_device.h"
 
 namespace mxar {
@@ -104,7 +106,8 @@ __device__ __forceinline__ bool wave_forced(const CommArgs& a, int r, uint32_t e
 // rounds themselves (same-box A/B, profiles/round2/README.md). A forced round is exceptional;
 // learning of it within 100 us is enough.
 struct HostPoll {
-  uint64_t next = wall_ticks() + 10000;
+  uint64_t next;
+  __device__ __forceinline__ explicit HostPoll(uint64_t now) : next(now + 10000) {}
   __device__ __forceinline__ bool due(uint64_t t) {
     if (t < next) return false;
     next = t + 10000;
@@ -114,11 +117,14 @@ struct HostPoll {
 };
 
 // The slab's FORCE words (a peer waiting at its lag gate for this rank) are polled at most
-// every 5 us, the first time at once: checked on every spin they doubled the period of the
+// every 5 us, the first time 5 us after the round started: checked on every spin they doubled the period of the
 // flag polls beside them (two dependent loads per iteration), and a catch-up noticed a few
 // microseconds later costs nothing.
 struct SlabPoll {
-  uint64_t next = 0;
+  // the first poll 5 us in too: a wait that ends sooner (the common case) never pays the
+  // fine-grained load of P FORCE words on its critical path
+  uint64_t next;
+  __device__ __forceinline__ explicit SlabPoll(uint64_t now) : next(now + 500) {}
   __device__ __forceinline__ bool due(uint64_t t) {
     if (t < next) return false;
     next = t + 500;
@@ -362,22 +368,52 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
     }
     return;
   }
+  // Every source's pack is loaded before the first add: a batch of B sources x U packs issues
+  // back to back (one memory latency per batch, not one per source - the per-source
+  // load-then-add loop cost ~1 us of fine-grained-memory latency per peer at small rounds).
+  // B = 2 / 4 / 8 by P, so small P carries no idle batch slots. Sources outside the mask load
+  // nothing and add +0, which is exact (acc starts at +0 and is never -0), so the fixed order
+  // s = 0..P-1 keeps the sum bit-exact.
   const int64_t npk = len / E::ELEMS;
   constexpr int U = 2;
+  auto sum_batched = [&](auto bt, int64_t i0, int nu, Acc<E>* acc) {
+    constexpr int B = decltype(bt)::value;
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u].zero();
+    for (int s0 = 0; s0 < P; s0 += B) {
+      Pack16 v[B][U];
+#pragma unroll
+      for (int q = 0; q < B; ++q) {
+        const int s = s0 + q;
+        const bool on = s < P && ((mask >> s) & 1u);
+        const __amdgpu_buffer_rsrc_t rs = slab_rsrc(s == r ? own_in : S + (on ? s : 0) * slot);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (on && u < nu) {
+            v[q][u] = ld16_nt(rs, static_cast<uint32_t>((i0 + u * kCommThreads) * 16));
+          } else {
+            v[q][u][0] = v[q][u][1] = v[q][u][2] = v[q][u][3] = 0u;
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < B; ++q)
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u].add(v[q][u]);
+    }
+  };
+  auto sum_packs = [&](int64_t i0, int nu, Acc<E>* acc) {
+    if (P <= 2)
+      sum_batched(std::integral_constant<int, 2>{}, i0, nu, acc);
+    else if (P <= 4)
+      sum_batched(std::integral_constant<int, 4>{}, i0, nu, acc);
+    else
+      sum_batched(std::integral_constant<int, 8>{}, i0, nu, acc);
+  };
   int64_t i = threadIdx.x;
   for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
     Acc<E> acc[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) acc[u].zero();
-    for (int s = 0; s < P; ++s) {
-      if (!((mask >> s) & 1u)) continue;
-      const __amdgpu_buffer_rsrc_t rs = slab_rsrc(s == r ? own_in : S + s * slot);
-      Pack16 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = ld16_nt(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
-#pragma unroll
-      for (int u = 0; u < U; ++u) acc[u].add(v[u]);
-    }
+    sum_packs(i, U, acc);
     Pack16 o[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -398,10 +434,9 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
     }
   }
   for (; i < npk; i += kCommThreads) {
-    Acc<E> acc;
-    acc.zero();
-    for (int s = 0; s < P; ++s)
-      if ((mask >> s) & 1u) acc.add(ld16_nt(slab_rsrc(s == r ? own_in : S + s * slot), static_cast<uint32_t>(i * 16)));
+    Acc<E> accs[U];
+    sum_packs(i, 1, accs);
+    Acc<E>& acc = accs[0];
     if (scale != 1.f) acc.scale(scale);
     const Pack16 o = acc.pack();
     for (int k = 0; k < P; ++k) {
@@ -525,6 +560,9 @@ struct RoundVars {
   // the lag gate is known open: every peer finished round epoch - trows (a resident kernel
   // whose previous round gathered every peer's chunks of epoch - 1, threshold_resident_kernel)
   int gate_open;
+  // run by a resident kernel: its workgroups start the next round once ctl[4] names this
+  // one, so the round end orders its counter resets before that store
+  int resident;
 };
 
 // One round of rank a.rank0 + blockIdx.y by the whole grid.
@@ -553,7 +591,10 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   const char* const in = rv.in;
   char* const out = rv.out;
   uint32_t* const ctl = a.ctl[y];
-  // threshold rounds count separately (ctl[4]); the protocol engine passes its round epochs
+  // threshold rounds count separately (ctl[4]); the protocol engine passes its round epochs.
+  // ctl[14] = the last round of this rank that was clean (every workgroup gathered every
+  // peer's reduced chunks): loaded beside ctl[4], same line, no extra latency
+  const uint32_t clean_prev = rv.epoch ? 0u : ld_ctl(&ctl[14]);
   const uint32_t epoch = rv.epoch ? rv.epoch : ld_ctl(&ctl[4]) + 1u;
   const int row = 1 + static_cast<int>(epoch % static_cast<uint32_t>(a.trows));
   const int G = gridDim.x;
@@ -590,8 +631,10 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
                      a.chunk) > 0;
   };
   const int nwords = (mine + 63) / 64;
-  HostPoll hp;
-  SlabPoll sp;
+  // ONE clock read for the round's prologue (each s_memrealtime is a scalar-memory round trip)
+  const uint64_t t_start = wall_ticks();
+  HostPoll hp(t_start);
+  SlabPoll sp(t_start);
   bool clean = !cold;
   // One workgroup (then nch = 1, P <= 2): it also keeps its counts in LDS, so the round end
   // does not read them back from HBM.
@@ -602,11 +645,12 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     if (counts_lds) sh_cnt[i] = v;
   };
 
+  uint64_t deadline = t_start + a.timeout;
   if (a.delay && r == a.delay_rank) {  // straggler simulation (tests)
     const uint64_t until = wall_ticks() + a.delay;
     while (wall_ticks() < until) __builtin_amdgcn_s_sleep(8);
+    deadline = wall_ticks() + a.timeout;
   }
-  const uint64_t deadline = wall_ticks() + a.timeout;
 
   // Reference order: what had arrived when the round started (S0 per own chunk, R0 for the
   // round) comes before the own scatter. One grid-wide count of R0 (every workgroup is
@@ -688,7 +732,17 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   // runs. Only a laggard that never runs again (a dead process) turns into ERR_TIMEOUT_LAG -
   // unless the engine abandons the round meanwhile (host abort word: re-initialisation or
   // shutdown): an abandoned round that has not passed its gate writes nothing anywhere.
-  if (rv.gate_open) {
+  // Shortcut (a.gate_shortcut, trows >= 2): this rank's round e - 1 was clean - every peer
+  // published its reduced chunks of e - 1, which it does only after its round e - 2 ended
+  // (rounds of a rank run in order; a launched round's kernel starts after the previous one
+  // ended, a resident workgroup after its previous round's last workgroup), so every peer is
+  // past e - 2 >= e - trows: P fine-grained progress-word loads (~2 us at 4 KiB rounds,
+  // profiles/round4/README.md section 4) are skipped. The resident kernel proves it itself
+  // (rv.gate_open); a launched round reads ctl[14], written by its predecessor's last
+  // workgroup when every workgroup of that round was clean.
+  const bool gate_open = a.gate_shortcut &&
+                         (rv.gate_open || (rv.epoch == 0 && clean_prev != 0u && clean_prev == epoch - 1u));
+  if (gate_open) {
     if (threadIdx.x == 0) sh_flag = 0;
   } else if (threadIdx.x < 64) {
     const int k = static_cast<int>(threadIdx.x);
@@ -919,6 +973,9 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   }
   __syncthreads();
   bool gave_up = false;
+  // full thresholds, unsplit, no counts: a gathered unit needs no decision (no ticket, no
+  // count, no slice agreement) - no workgroup barrier per unit
+  const bool fastg = !split && !tickets && counts == nullptr;
   for (;;) {
     bool any = false, progressed = false;
     for (int w = 0; w < nwords; ++w) {
@@ -950,6 +1007,11 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         const int c = b / Pm1;
         const int j = (r + 1 + b % Pm1) % P;
         uint64_t* const dec = split ? &a.split_dec[a.maxch + static_cast<int64_t>(j) * a.maxch + c] : nullptr;
+        bool take;
+        if (fastg) {  // nothing to decide: every thread knows the unit is taken if it exists
+          take = exists(j, c);
+          if (threadIdx.x == 0) pend[w] &= ~(1ull << i);
+        } else {
         if (threadIdx.x == 0) {
           int take = 1;
           uint64_t d = 0;
@@ -984,7 +1046,8 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
           pend[w] &= ~(1ull << i);
         }
         __syncthreads();
-        const bool take = sh_flag != 0;
+        take = sh_flag != 0;
+        }
         const int64_t bstart = static_cast<int64_t>(j) * a.block;
         const int64_t cstart = static_cast<int64_t>(c) * a.chunk + static_cast<int64_t>(u - b * S) * sub;
         const int64_t len = clamp_len(clamp_len(clamp_len(a.n - bstart, a.block) - c * a.chunk, a.chunk) -
@@ -1005,8 +1068,9 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         ps.add(4, t_copy);
         progressed = true;
         ps.count(7);
-        __syncthreads();
+        if (!fastg) __syncthreads();  // sh_flag is reused by the next unit
       }
+      if (fastg) __syncthreads();  // thread 0's pend[] updates before anyone reads pend[] again
     }
     if (!any) break;
     if (progressed) continue;
@@ -1100,33 +1164,53 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   // the error word, loaded before the drain so its latency hides behind it (one workgroup:
   // nobody else can raise it later; with more, the last one reads it again after its ticket)
   const uint32_t errv = (threadIdx.x == 0 && rv.err_out != nullptr) ? ld_ctl(err) : 0u;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // The drain makes every workgroup's output / count stores complete before the ticket: only
+  // the host hand-off needs that (the done word, the counts copied to pinned memory). The
+  // progress words promise the peers that this rank's READS of the row are done, and every
+  // load of a round feeds a store or a branch that issued before this point - a launched round
+  // without host words skips the store-acknowledgement wait on its tail.
+  if (rv.done_out != nullptr || rv.counts_host != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  bool all_clean = clean;
   if (threadIdx.x == 0) {
-    // one workgroup: it is the last (no ticket - a device-scope atomic's round trip)
-    const uint32_t t = G == 1 ? 0u : __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sh_flag = t == static_cast<uint32_t>(G) - 1 ? 1 : 0;
+    // one workgroup: it is the last (no ticket - a device-scope atomic's round trip). The
+    // ticket's high half counts the clean workgroups (one atomic for both)
+    const uint32_t inc = 1u + (clean ? 0x10000u : 0u);
+    const uint32_t t = G == 1 ? 0u : __hip_atomic_fetch_add(&ctl[1], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool is_last = (t & 0xffffu) == static_cast<uint32_t>(G) - 1;
+    sh_flag = is_last ? ((t >> 16) + (clean ? 1u : 0u) == static_cast<uint32_t>(G) ? 3 : 1) : 0;
   }
   __syncthreads();
   const bool last = sh_flag != 0;
+  all_clean = sh_flag == 3;
   if (threadIdx.x == 0) {
     if (last) {
       // one workgroup at full thresholds touched none of the round counters (no ticket, no
       // completion count, no snapshot): nothing to reset, and no other workgroup waits on ctl[4]
       const bool solo = G == 1 && full;
+      // the next launched round's lag-gate shortcut (self-counted epochs only)
+      if (rv.epoch == 0)
+        __hip_atomic_store(&ctl[14], all_clean ? epoch : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!solo) {
         __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ctl[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ctl[5], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ctl[6], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ctl[7], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!full) {  // full thresholds touch no ticket, snapshot or early-arrival counter
+          __hip_atomic_store(&ctl[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&ctl[5], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&ctl[6], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&ctl[7], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         // a resident kernel's workgroups start the next round once ctl[4] names this one: the
-        // resets land first
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // resets land first (a launched round's successor is ordered by the kernel boundary)
+        if (rv.resident) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(&ctl[4], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // the host words below follow every store of the round; a launched round without host
+      // words tells only its peers (progress: reads done, no release needed) and its successor
+      // (kernel boundary)
+      if (rv.resident || rv.done_out != nullptr || rv.err_out != nullptr || rv.counts_host != nullptr) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       // solo: only this thread reads ctl[4] (the resident loop), so the store need not be
       // drained by the release above
       if (solo) __hip_atomic_store(&ctl[4], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1161,7 +1245,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
 template <class E>
 __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   const int y = blockIdx.y;
-  const RoundVars rv{a.in[y], a.out[y], a.counts, a.counts_host, a.err_out, a.done_out, a.epoch_set, a.cold, 0};
+  const RoundVars rv{a.in[y], a.out[y], a.counts, a.counts_host, a.err_out, a.done_out, a.epoch_set, a.cold, 0, 0};
   (void)threshold_round<E>(a, rv);
 }
 
@@ -1310,7 +1394,8 @@ __global__ __launch_bounds__(kCommThreads) void threshold_resident_kernel(CommAr
                        static_cast<uint32_t>(sh_ent[6]),         cmd == static_cast<uint32_t>(kResCold) ? 1 : 0,
                        (prev_clean && gridDim.x == 1 && a.trows >= 2 && static_cast<uint32_t>(sh_ent[6]) == prev_epoch + 1u)
                            ? 1
-                           : 0};
+                           : 0,
+                       1};
     __syncthreads();
     const bool clean = threshold_round<E>(a, rv);
     if (threadIdx.x == 0) sh_clean = clean ? 1 : 0;

@@ -1,3 +1,4 @@
+#include "../core/env.h"
 #include "actor_system.h"
 
 #include <algorithm>
@@ -309,10 +310,10 @@ ActorSystem::ActorSystem(std::string name, Mode mode, int threads, int throughpu
     // wake-up per hop costs more than the hop itself.
     spin_us_ = 50;
     if (const char* e = std::getenv("MXAR_DISPATCH_SPIN_US")) spin_us_ = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("MXAR_DISPATCH_NOTIFY")) notify_always_ = std::string(e) == "always";
-    if (const char* e = std::getenv("MXAR_DISPATCH_LIFO")) lifo_ = std::atoi(e) != 0;
-    if (const char* e = std::getenv("MXAR_DISPATCH_YIELD")) spin_yield_ = std::atoi(e) != 0;
-    if (const char* e = std::getenv("MXAR_DISPATCH_SPINNERS")) max_spinners_ = std::max(1, std::atoi(e));
+    if (const char* e = study_env("MXAR_DISPATCH_NOTIFY")) notify_always_ = std::string(e) == "always";
+    if (const char* e = study_env("MXAR_DISPATCH_LIFO")) lifo_ = std::atoi(e) != 0;
+    if (const char* e = study_env("MXAR_DISPATCH_YIELD")) spin_yield_ = std::atoi(e) != 0;
+    if (const char* e = study_env("MXAR_DISPATCH_SPINNERS")) max_spinners_ = std::max(1, std::atoi(e));
     int n = threads > 0 ? threads : std::max(2u, std::min(8u, std::thread::hardware_concurrency()));
     for (int i = 0; i < n; ++i) threads_.emplace_back([this] { worker_loop(); });
     timer_thread_ = std::thread([this] { timer_loop(); });

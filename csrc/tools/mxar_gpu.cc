@@ -4,6 +4,7 @@
 // worker (AllreduceWorker.scala:272-301) with its rounds on GPU k: an XgmiRoundPlane
 // (csrc/hip/xgmi_plane.h) under a PlaneWorkerActor, the demo source data[i] = i + iteration
 // produced by the fill_iota kernel - no Python anywhere in the round path.
+#include "../core/env.h"
 #include <hip/hip_runtime.h>
 
 #include <unistd.h>
@@ -61,7 +62,7 @@ GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag,
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
     throw std::runtime_error("mxar-gpu: no stream on device " + std::to_string(device));
   auto src_stream = std::shared_ptr<void>(s, [](void* q) { (void)hipStreamDestroy(static_cast<hipStream_t>(q)); });
-  if (const char* path = std::getenv("MXAR_PLANE_STAMPS")) {
+  if (const char* path = study_env("MXAR_PLANE_STAMPS")) {
     // study knob: phase stamps of this worker's round kernels (kPhaseSlots u64 per workgroup,
     // s_memrealtime - one clock for every process on the GPU), the last round's written as one
     // JSON line to `path` when the job ends (tools/native_stamps.py)

@@ -103,3 +103,62 @@ def test_multiprocess_sdma_allreduce(world):
             p.kill()
     bad = [r for r in res if not r[1]]
     assert not bad, bad
+
+
+
+def _reuse_worker(rank, world, port, results):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.parallel import SdmaCommunicator
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ok, msg = True, ""
+    try:
+        n = 24 << 20  # 48 MiB bf16 per rank: ~24 MiB engine copies per peer and phase, one engine each
+        comm = SdmaCommunicator(device=0, slot_bytes=(2 * n) // world + (1 << 20), grid=64, engines_per_peer=1,
+                                timeout_s=15.0)
+        xs = [fill_uniform(torch.empty(n, dtype=torch.bfloat16, device=DEV), seed=70 + k) for k in range(world)]
+        ref = _ref(xs)
+        for it in range(6):
+            y = comm.allreduce(xs[rank])
+            snap = y.clone()  # stream-ordered after the call
+            y.fill_(float("nan"))  # the caller reuses `out` at once: the peers must not see it
+            torch.cuda.synchronize()
+            comm.check()
+            err = (snap.float() - ref).abs().max().item()
+            if not err <= _tol(torch.bfloat16, world):
+                ok, msg = False, f"it {it}: err {err}"
+                break
+            dist.barrier()
+    except Exception as e:  # noqa: BLE001 - report, never hang the parent
+        ok, msg = False, repr(e)
+    results.put((rank, ok, msg))
+    dist.destroy_process_group()
+
+
+def test_multiprocess_sdma_output_reusable_right_after_the_call():
+    """The engines read each rank's reduced block out of `out` for the peers (phase 2): the
+    call must not count as done on the caller's stream before those copies are.
+    Every rank overwrites its output with NaN right after each call; the peers' results must
+    still be the sums."""
+    from akka_allreduce_1_amd.parallel import free_port
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_reuse_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = []
+    try:
+        res = [q.get(timeout=180) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    bad = [r for r in res if not r[1]]
+    assert not bad, bad

@@ -31,7 +31,7 @@ def main() -> None:
         ("ring_hop_rows", {"MXAR_RING_FLAGS": "hop", "MXAR_STUDY": "1"}, 3, 2, "ring"),
         ("protected", {}, 4, 3, "ring"),
         ("ring_hop_rows", {"MXAR_RING_FLAGS": "hop", "MXAR_STUDY": "1"}, 4, 3, "ring"),
-        ("no_guard", {"MXAR_SLOT_GUARD": "0"}, 3, 2, "ring"),
+        ("no_guard", {"MXAR_SLOT_GUARD": "0", "MXAR_STUDY": "1"}, 3, 2, "ring"),
     ]
     only = set(sys.argv[1:])
     for name, env, world, slow, seq in cases:
