@@ -320,8 +320,9 @@ def _native_job(n: int, chunk: int, rounds: int, quiet: bool, timeout: float = 6
     import os
     import subprocess
 
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    exe = os.path.join(root, "akka_allreduce_1_amd")
+    import akka_allreduce_1_amd
+
+    exe = os.path.dirname(os.path.abspath(akka_allreduce_1_amd.__file__))  # the imported package's executables
     port = _free_port()
     seeds = ["--seeds", f"mxar.tcp://ClusterSystem@127.0.0.1:{port}", "--loglevel", "ERROR"]
     wargs = [os.path.join(exe, "mxar-gpu"), "worker", "0", str(n), "--device", "0", "--max-peers", "2",

@@ -89,15 +89,30 @@ __device__ __forceinline__ bool host_forced(const CommArgs& a, uint32_t epoch, b
 // Wave 0 only: is round `epoch` forced? Lane s < P reads FORCE[s] of the own slab (peer s
 // waits at its lag gate for this rank); lane 63 reads the engine's pinned host words when
 // `host` (a PCIe read: callers rate-limit it). Wave-uniform.
-__device__ __forceinline__ bool wave_forced(const CommArgs& a, int r, uint32_t epoch, bool host) {
+// (out of line - see copy_in below; it takes plain values, not the kernel's CommArgs, which an
+// out-of-line callee would have copied to scratch)
+__device__ __attribute__((noinline)) bool wave_forced_words(const uint32_t* own_force, int P, int r, uint32_t epoch,
+                                                            const uint32_t* hforce, const uint32_t* habort) {
   const int s = static_cast<int>(threadIdx.x);
   bool f = false;
-  if (s < a.P && s != r) f = reached(ld_flag(forcew(a, r, s)), epoch);
-  if (host && s == 63) {
-    bool ab;
-    f = host_forced(a, epoch, &ab);
+  if (s < P && s != r) f = reached(ld_flag(own_force + s), epoch);
+  if (hforce != nullptr && s == 63) {
+    uint32_t fw, aw = epoch - 1u;
+    if (habort == hforce + 1) {
+      const uint64_t w = __hip_atomic_load(reinterpret_cast<const uint64_t*>(hforce), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+      fw = static_cast<uint32_t>(w);
+      aw = static_cast<uint32_t>(w >> 32);
+    } else {
+      fw = __hip_atomic_load(const_cast<uint32_t*>(hforce), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (habort != nullptr) aw = __hip_atomic_load(const_cast<uint32_t*>(habort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    f = reached(aw, epoch) || reached(fw, epoch);
   }
   return __any(f);
+}
+__device__ __forceinline__ bool wave_forced(const CommArgs& a, int r, uint32_t epoch, bool host) {
+  return wave_forced_words(forcew(a, r, 0), a.P, r, epoch, host ? a.hforce : nullptr, a.habort);
 }
 
 // Host-word polls at most every 100 us per workgroup, the first one 100 us after the kernel
@@ -150,25 +165,37 @@ __device__ __forceinline__ bool al16(const void* p) { return (reinterpret_cast<u
 
 // Protocol geometry (maxChunkSize elements, reference block ranges) need not be 16-B
 // aligned: such a unit takes an element-wise path (wave-uniform branch).
+// Code size matters for the small rounds: a round's code is fetched into the instruction
+// cache of every CU it lands on, from L2, on the round's critical path (the full-threshold
+// kernel went 19.3 -> 16.5 us at 8 logical ranks x 4 KiB when its code shrank from 51 to 26 KB,
+// profiles/round5/README.md). Paths a round rarely takes - element-wise copies of unaligned
+// protocol geometry, zero fills of given-up chunks, FORCE polls - are out-of-line functions, so
+// the hot path stays dense.
 template <class E>
-__device__ __forceinline__ void copy_in(char* slab_dst, const char* src, int64_t len) {
-  if (al16(slab_dst) && al16(src)) {
-    copy_to_slab<E>(slab_dst, src, len);
-    return;
-  }
+__device__ __attribute__((noinline)) void copy_in_scalar(char* slab_dst, const char* src, int64_t len) {
   const __amdgpu_buffer_rsrc_t rd = slab_rsrc(slab_dst);
   for (int64_t t = threadIdx.x; t < len; t += kCommThreads) copy_scalar_wt<E>(rd, src, t);
 }
+template <class E>
+__device__ __forceinline__ void copy_in(char* slab_dst, const char* src, int64_t len) {
+  if (al16(slab_dst) && al16(src))
+    copy_to_slab<E>(slab_dst, src, len);
+  else
+    copy_in_scalar<E>(slab_dst, src, len);
+}
 
 template <class E>
-__device__ __forceinline__ void copy_out(char* dst, const char* slab_src, int64_t len) {
-  if (al16(dst) && al16(slab_src)) {
-    copy_from_slab<E>(dst, slab_src, len);
-    return;
-  }
+__device__ __attribute__((noinline)) void copy_out_scalar(char* dst, const char* slab_src, int64_t len) {
   const __amdgpu_buffer_rsrc_t rs = slab_rsrc(slab_src);
   const __amdgpu_buffer_rsrc_t rd = slab_rsrc(dst);
   for (int64_t t = threadIdx.x; t < len; t += kCommThreads) st_scalar_wt<E>(rd, t, ld_scalar_nt<E>(rs, t));
+}
+template <class E>
+__device__ __forceinline__ void copy_out(char* dst, const char* slab_src, int64_t len) {
+  if (al16(dst) && al16(slab_src))
+    copy_from_slab<E>(dst, slab_src, len);
+  else
+    copy_out_scalar<E>(dst, slab_src, len);
 }
 
 // Zeros for a given-up chunk of the output. Write-through (sc0 sc1) like every other output
@@ -176,7 +203,7 @@ __device__ __forceinline__ void copy_out(char* dst, const char* slab_src, int64_
 // (`done_out`): the output is then handed on before the kernel ends, so no store may sit in
 // this XCD's L2 waiting for the end-of-kernel writeback.
 template <class E>
-__device__ __forceinline__ void zero_fill(char* dst, int64_t len) {
+__device__ __attribute__((noinline)) void zero_fill(char* dst, int64_t len) {
   const __amdgpu_buffer_rsrc_t rd = slab_rsrc(dst);
   if (al16(dst)) {
     const int64_t npk = len / E::ELEMS;
@@ -334,6 +361,38 @@ __device__ __forceinline__ int32_t ll_copy_out(char* dst, const char* src_chunk,
   return cnt;
 }
 
+// reduce_masked for unaligned protocol geometry: element by element (inline: an out-of-line
+// function taking the kernel's CommArgs would copy them to scratch)
+template <class E>
+__device__ __forceinline__ void reduce_masked_scalar(const CommArgs& a, int P, int r, uint32_t mask,
+                                                             const char* own_in, const char* S, int64_t slot,
+                                                             char* own_out, int64_t roff, int64_t len, float scale) {
+  for (int64_t t = threadIdx.x; t < len; t += kCommThreads) {
+    // every source's load issues before the first add (one memory latency per 8 sources,
+    // not one per source); the fixed order s = 0..P-1 keeps the sum bit-exact (+0.f for a
+    // source outside the mask is an identity: acc starts at +0 and is never -0)
+    float acc = 0.f;
+    for (int s0 = 0; s0 < P; s0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int s = s0 + q;
+        v[q] = (s < P && ((mask >> s) & 1u)) ? ld_scalar_nt<E>(slab_rsrc(s == r ? own_in : S + s * slot), t) : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc += v[q];
+    }
+    acc *= scale;
+    for (int k = 0; k < P; ++k) {
+      if (k == r) {
+        if (own_out != nullptr) st_scalar_wt<E>(slab_rsrc(own_out), t, acc);
+      } else {
+        st_scalar_wt<E>(slab_rsrc(a.base[k] + roff), t, acc);
+      }
+    }
+  }
+}
+
 // Sum the sources in `mask` (fixed order s = 0..P-1, fp32), store to the own output (when
 // own_out != nullptr) and to every peer's R slot. Source r is the rank's own input.
 template <class E>
@@ -342,36 +401,13 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
                                               int64_t len, bool wt_out, float scale) {
   const bool vec = al16(own_in) && al16(S) && (own_out == nullptr || al16(own_out)) && (roff & 15) == 0;
   if (!vec) {
-    for (int64_t t = threadIdx.x; t < len; t += kCommThreads) {
-      // every source's load issues before the first add (one memory latency per 8 sources,
-      // not one per source); the fixed order s = 0..P-1 keeps the sum bit-exact (+0.f for a
-      // source outside the mask is an identity: acc starts at +0 and is never -0)
-      float acc = 0.f;
-      for (int s0 = 0; s0 < P; s0 += 8) {
-        float v[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int s = s0 + q;
-          v[q] = (s < P && ((mask >> s) & 1u)) ? ld_scalar_nt<E>(slab_rsrc(s == r ? own_in : S + s * slot), t) : 0.f;
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) acc += v[q];
-      }
-      acc *= scale;
-      for (int k = 0; k < P; ++k) {
-        if (k == r) {
-          if (own_out != nullptr) st_scalar_wt<E>(slab_rsrc(own_out), t, acc);
-        } else {
-          st_scalar_wt<E>(slab_rsrc(a.base[k] + roff), t, acc);
-        }
-      }
-    }
+    reduce_masked_scalar<E>(a, P, r, mask, own_in, S, slot, own_out, roff, len, scale);
     return;
   }
   // Every source's pack is loaded before the first add: a batch of B sources x U packs issues
   // back to back (one memory latency per batch, not one per source - the per-source
   // load-then-add loop cost ~1 us of fine-grained-memory latency per peer at small rounds).
-  // B = 2 / 4 / 8 by P, so small P carries no idle batch slots. Sources outside the mask load
+  // Sources outside the mask (or past P) load
   // nothing and add +0, which is exact (acc starts at +0 and is never -0), so the fixed order
   // s = 0..P-1 keeps the sum bit-exact.
   const int64_t npk = len / E::ELEMS;
@@ -402,18 +438,18 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
         for (int u = 0; u < U; ++u) acc[u].add(v[q][u]);
     }
   };
+  // (2 or 4 sources: a batch of 4; more: batches of 8 - two instantiations only, one call site
+  // each, so the kernel's code stays small enough to fetch quickly on a cold CU)
   auto sum_packs = [&](int64_t i0, int nu, Acc<E>* acc) {
-    if (P <= 2)
-      sum_batched(std::integral_constant<int, 2>{}, i0, nu, acc);
-    else if (P <= 4)
+    if (P <= 4)
       sum_batched(std::integral_constant<int, 4>{}, i0, nu, acc);
     else
       sum_batched(std::integral_constant<int, 8>{}, i0, nu, acc);
   };
-  int64_t i = threadIdx.x;
-  for (; i + (U - 1) * kCommThreads < npk; i += U * kCommThreads) {
+  for (int64_t i = threadIdx.x; i < npk; i += U * kCommThreads) {
+    const int nu = i + kCommThreads < npk ? U : 1;
     Acc<E> acc[U];
-    sum_packs(i, U, acc);
+    sum_packs(i, nu, acc);
     Pack16 o[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -423,29 +459,15 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
     for (int k = 0; k < P; ++k) {
       char* d = k == r ? own_out : a.base[k] + roff;
       if (d == nullptr) continue;
-      if (k == r && !wt_out) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) st16(d + (i + u * kCommThreads) * 16, o[u]);
-      } else {
-        const __amdgpu_buffer_rsrc_t rd = slab_rsrc(d);
-#pragma unroll
-        for (int u = 0; u < U; ++u) st16_wt(rd, static_cast<uint32_t>((i + u * kCommThreads) * 16), o[u]);
+      for (int u = 0; u < U; ++u) {
+        if (u >= nu) break;
+        const int64_t at = i + u * kCommThreads;
+        if (k == r && !wt_out)
+          st16(d + at * 16, o[u]);
+        else
+          st16_wt(slab_rsrc(d), static_cast<uint32_t>(at * 16), o[u]);
       }
-    }
-  }
-  for (; i < npk; i += kCommThreads) {
-    Acc<E> accs[U];
-    sum_packs(i, 1, accs);
-    Acc<E>& acc = accs[0];
-    if (scale != 1.f) acc.scale(scale);
-    const Pack16 o = acc.pack();
-    for (int k = 0; k < P; ++k) {
-      char* d = k == r ? own_out : a.base[k] + roff;
-      if (d == nullptr) continue;
-      if (k == r && !wt_out)
-        st16(d + i * 16, o);
-      else
-        st16_wt(slab_rsrc(d), static_cast<uint32_t>(i * 16), o);
     }
   }
   const int64_t t = npk * E::ELEMS + threadIdx.x;
@@ -568,7 +590,12 @@ struct RoundVars {
 // One round of rank a.rank0 + blockIdx.y by the whole grid.
 // Returns true when this workgroup's round took every peer's reduced chunk it gathers, with
 // nothing forced, cold or given up (the resident kernel's lag-gate shortcut).
-template <class E>
+// FULL: a compile-time full-threshold round (thReduce = thComplete = 1, unsplit chunks, no
+// LL units - the DP communicator's exact lag-tolerant allreduce and most protocol rounds).
+// Snapshot, tickets, split-chunk agreement and the LL unit paths fold away: less than half
+// the code of the general kernel, whose instruction fetch a small round otherwise pays from
+// L2 on every cold CU (51 KB of code vs 21 KB for the 8-rank two-shot).
+template <class E, bool FULL>
 __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVars& rv) {
   constexpr int es = 16 / E::ELEMS;
   __shared__ uint32_t sh_mask;
@@ -611,13 +638,13 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   // whatever the arrival order, so neither the launch snapshot (a grid-wide barrier) nor the
   // output tickets (one device-scope atomic per unit) change the result: both are skipped.
   // Forced rounds still exclude their own force-reduced chunks (reference order).
-  const bool full = a.full != 0;
-  const bool ll = a.ll != 0;  // low-latency round: {payload, epoch} units, no fences (host: unsplit only)
+  const bool full = FULL || a.full != 0;
+  const bool ll = !FULL && a.ll != 0;  // low-latency round: {payload, epoch} units, no fences (host: unsplit only)
   const bool snap = ref && !cold && !full;  // cold rounds are forced from the start: no snapshot
   const bool tickets = !full;
   // work units: S slices per chunk (S = 1: a unit is a chunk). Scatter / gather unit
   // u = ((c * (P-1) + peer) * S + slice); reduce unit v = c * S + slice.
-  const int S = a.sub > 1 ? a.sub : 1;
+  const int S = (!FULL && a.sub > 1) ? a.sub : 1;
   const bool split = S > 1;
   const int nu = (P - 1) * a.nch * S;
   const int nr = a.nch * S;
@@ -1242,11 +1269,11 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   return clean;
 }
 
-template <class E>
+template <class E, bool FULL>
 __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   const int y = blockIdx.y;
   const RoundVars rv{a.in[y], a.out[y], a.counts, a.counts_host, a.err_out, a.done_out, a.epoch_set, a.cold, 0, 0};
-  (void)threshold_round<E>(a, rv);
+  (void)threshold_round<E, FULL>(a, rv);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1340,7 +1367,7 @@ __device__ uint64_t resident_door(const ResidentDoor* door, uint32_t* hstate, ui
   return w;
 }
 
-template <class E>
+template <class E, bool FULL>
 __global__ __launch_bounds__(kCommThreads) void threshold_resident_kernel(CommArgs a, const ResidentDoor* door,
                                                                          uint32_t* hstate, uint64_t* dm,
                                                                          uint32_t seq, uint32_t gen, uint64_t idle) {
@@ -1397,7 +1424,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_resident_kernel(CommAr
                            : 0,
                        1};
     __syncthreads();
-    const bool clean = threshold_round<E>(a, rv);
+    const bool clean = threshold_round<E, FULL>(a, rv);
     if (threadIdx.x == 0) sh_clean = clean ? 1 : 0;
     // the entry is consumed: the host may reuse its door slot (a PCIe write, kept off the
     // round's critical path - every release waits for the writes before it)
@@ -1424,6 +1451,9 @@ __global__ __launch_bounds__(64) void publish_progress_kernel(CommArgs a, uint32
   }
 }
 
+// the compile-time full-threshold kernel applies (threshold_round FULL)
+static bool full_fast(const CommArgs& a) { return a.full != 0 && a.sub <= 1 && a.ll == 0; }
+
 void launch_publish_progress(const CommArgs& a, uint32_t value, hipStream_t s) {
   hipLaunchKernelGGL(publish_progress_kernel, dim3(1), dim3(64), 0, s, a, value);
 }
@@ -1431,14 +1461,23 @@ void launch_publish_progress(const CommArgs& a, uint32_t value, hipStream_t s) {
 void launch_threshold_resident(const CommArgs& a, int grid, hipStream_t s, DType dt, const ResidentDoor* door,
                                uint32_t* hstate, uint32_t* dm, uint32_t seq, uint32_t gen, uint64_t idle_ticks) {
   dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
-    hipLaunchKernelGGL(threshold_resident_kernel<decltype(tag)>, dim3(grid), dim3(kCommThreads), 0, s, a, door,
-                       hstate, reinterpret_cast<uint64_t*>(dm), seq, gen, idle_ticks);
+    using E = decltype(tag);
+    if (full_fast(a))
+      hipLaunchKernelGGL((threshold_resident_kernel<E, true>), dim3(grid), dim3(kCommThreads), 0, s, a, door, hstate,
+                         reinterpret_cast<uint64_t*>(dm), seq, gen, idle_ticks);
+    else
+      hipLaunchKernelGGL((threshold_resident_kernel<E, false>), dim3(grid), dim3(kCommThreads), 0, s, a, door, hstate,
+                         reinterpret_cast<uint64_t*>(dm), seq, gen, idle_ticks);
   });
 }
 
 void launch_threshold(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {
   dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
-    hipLaunchKernelGGL(threshold_kernel<decltype(tag)>, grid, dim3(kCommThreads), 0, s, a);
+    using E = decltype(tag);
+    if (full_fast(a))
+      hipLaunchKernelGGL((threshold_kernel<E, true>), grid, dim3(kCommThreads), 0, s, a);
+    else
+      hipLaunchKernelGGL((threshold_kernel<E, false>), grid, dim3(kCommThreads), 0, s, a);
   });
 }
 
