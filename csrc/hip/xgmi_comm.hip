@@ -349,7 +349,7 @@ __device__ __forceinline__ void copy_slab_fwd(char* out, char* next_slab, const 
 // next rank's R slot (`fwd_e`). WT = F32 for a 16-bit E is the exact wire (partials travel
 // in fp32, E::ELEMS / 4 fp32 packs per E pack); WT = E is the element-type wire (half the RS
 // bytes, one extra rounding per intermediate hop). Two steps in flight per lane.
-template <class E, class WT>
+template <class E, class WT, int U>
 __device__ __forceinline__ void ring_hop(const char* partial, const char* in, char* fwd_p, char* out, char* fwd_e,
                                          int64_t len, float scale) {
   constexpr bool wide = WT::ELEMS != E::ELEMS;
@@ -361,7 +361,21 @@ __device__ __forceinline__ void ring_hop(const char* partial, const char* in, ch
   const __amdgpu_buffer_rsrc_t rf = slab_rsrc(fwd_p != nullptr ? fwd_p : in);
   const __amdgpu_buffer_rsrc_t ro = slab_rsrc(out != nullptr ? out : in);
   const __amdgpu_buffer_rsrc_t re = slab_rsrc(fwd_e != nullptr ? fwd_e : in);
-  constexpr int U = 2;
+  // fp32 partial packs (wide wire) are laid out in planes of kCommThreads packs: for each run
+  // of 256 E packs, NP planes of 256 fp32 packs - so every load / store instruction of a wave
+  // covers 1 KiB of consecutive bytes (pack h of lane l at plane h, slot l). The plain layout
+  // (lane l's NP packs side by side) gave each instruction every other 16 B of 2 KiB: twice
+  // the lines per instruction, each half written. The last, short run is packed the same way
+  // with `rows` slots per plane, so a chunk's partial stays inside its len x 4 bytes. Writer
+  // and reader of a hop run this same function over the same len: the layout is private to
+  // the ring's S slots.
+  auto poff = [&](int64_t i, int h) -> uint32_t {
+    const int64_t run = i / kCommThreads;
+    const int64_t lane = i - run * kCommThreads;
+    const int64_t left = npk - run * kCommThreads;
+    const int64_t rows = left < kCommThreads ? left : kCommThreads;
+    return static_cast<uint32_t>((run * kCommThreads * NP + h * rows + lane) * 16);
+  };
   auto step = [&](int64_t i0, int nu) {
     Pack16 xv[U], pv[U][NP];
 #pragma unroll
@@ -371,7 +385,7 @@ __device__ __forceinline__ void ring_hop(const char* partial, const char* in, ch
       xv[u] = ld16_nt(ri, static_cast<uint32_t>(i * 16));
       if (has_p) {
 #pragma unroll
-        for (int h = 0; h < NP; ++h) pv[u][h] = ld16_nt(rp, static_cast<uint32_t>((i * NP + h) * 16));
+        for (int h = 0; h < NP; ++h) pv[u][h] = ld16_nt(rp, wide ? poff(i, h) : static_cast<uint32_t>(i * 16));
       }
     }
 #pragma unroll
@@ -398,7 +412,7 @@ __device__ __forceinline__ void ring_hop(const char* partial, const char* in, ch
             Pack16 o;
 #pragma unroll
             for (int q = 0; q < 4; ++q) o[q] = __float_as_uint(acc.v[4 * h + q]);
-            st16_wt(rf, static_cast<uint32_t>((i * NP + h) * 16), o);
+            st16_wt(rf, poff(i, h), o);
           }
         } else {
           st16_wt(rf, static_cast<uint32_t>(i * 16), acc.pack());
@@ -433,7 +447,7 @@ __device__ __forceinline__ void ring_hop(const char* partial, const char* in, ch
 // latency and the ranks' jitter hide behind data movement instead of adding up over the
 // 2 (P - 1) dependent hops of a chunk-major walk (round 3: 0.56 of the copy roofline at
 // 8 logical ranks x 256 MiB bf16). Chunks per workgroup: XgmiComm ring_depth_.
-template <class E, class WT>
+template <class E, class WT, int U>
 __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
   constexpr int es = 16 / E::ELEMS;
   constexpr int ws = 16 / WT::ELEMS;  // wire bytes per element of a reduce-scatter partial
@@ -478,7 +492,7 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
   for (int c = blockIdx.x; c < a.nch; c += G) {
     if (!inb(c)) continue;
     const int64_t len = blen(r, c);
-    if (len > 0) ring_hop<E, WT>(nullptr, in + at(r, c), a.base[nxt] + a.off_S + cst(c) * ws, nullptr, nullptr, len, 1.f);
+    if (len > 0) ring_hop<E, WT, U>(nullptr, in + at(r, c), a.base[nxt] + a.off_S + cst(c) * ws, nullptr, nullptr, len, 1.f);
     publish_flags([&](int) { return rs_flag(nxt, 0, c); }, 1, epoch, rel);
   }
   read_delay(a, r);  // slow-reader test knob: hold this rank before its first slab read
@@ -496,12 +510,12 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
       const char* part = a.base[r] + a.off_S + (s - 1) * slot + cst(c) * ws;
       if (s < P - 1) {
         if (len > 0)
-          ring_hop<E, WT>(part, in + at(b, c), a.base[nxt] + a.off_S + s * slot + cst(c) * ws, nullptr, nullptr, len,
+          ring_hop<E, WT, U>(part, in + at(b, c), a.base[nxt] + a.off_S + s * slot + cst(c) * ws, nullptr, nullptr, len,
                           1.f);
         publish_flags([&](int) { return rs_flag(nxt, s, c); }, 1, epoch, rel);
       } else {
         if (len > 0)
-          ring_hop<E, WT>(part, in + at(b, c), nullptr, out + at(b, c), a.base[nxt] + a.off_R + cst(c) * es, len,
+          ring_hop<E, WT, U>(part, in + at(b, c), nullptr, out + at(b, c), a.base[nxt] + a.off_R + cst(c) * es, len,
                           a.scale);
         publish_flags([&](int) { return ag_flag(nxt, 0, c); }, 1, epoch, rel);
       }
@@ -856,12 +870,13 @@ void XgmiComm::reset_local() {
 template <class E>
 static void launch_typed(const CommArgs& a, dim3 grid, hipStream_t s, Algo kind) {
   const dim3 b(kCommThreads);
+  // two packs in flight per lane and hop: 4 and 8 measured no faster (profiles/round5/ring_packs_in_flight_ab.jsonl)
   if (kind == Algo::Ring) {  // exact wire: fp32 partials
-    hipLaunchKernelGGL((ring_kernel<E, F32>), grid, b, 0, s, a);
+    hipLaunchKernelGGL((ring_kernel<E, F32, 2>), grid, b, 0, s, a);
     return;
   }
   if (kind == Algo::RingNative) {  // element-type wire
-    hipLaunchKernelGGL((ring_kernel<E, E>), grid, b, 0, s, a);
+    hipLaunchKernelGGL((ring_kernel<E, E, 2>), grid, b, 0, s, a);
     return;
   }
   const bool oneshot = kind == Algo::OneShot;

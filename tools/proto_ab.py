@@ -15,7 +15,7 @@ import torch
 
 if not os.environ.get("PYTHONPATH"):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path.insert(1, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.append(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from benchmarks.sections import native_deployment, protocol_sizes  # noqa: E402
 
