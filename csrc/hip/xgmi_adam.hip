@@ -133,6 +133,80 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_adamw_kernel(CommArgs a)
       float* const sv = m2 + cstart;
       const __amdgpu_buffer_rsrc_t rp = slab_rsrc(sp), rm = slab_rsrc(sm), rv = slab_rsrc(sv);
       const int64_t npk = len / EL;
+      if constexpr (STREAM == 3 && EL == 8) {
+        // Run-contiguous halves (16-bit parameters, the default): lane l of a run of 256 packs
+        // takes elements [4l, 4l + 4) of each half of the run's 2048 elements, so every fp32
+        // state load / store instruction of a wave covers 1 KiB of consecutive bytes and every
+        // 16-bit one 512 B. (One 16-B parameter pack per lane made each fp32 state access hit
+        // every other 16 B of 2 KiB: half-written lines, 15.3 B written per parameter instead
+        // of 14 - profiles/round4/README.md section 5.) The last, short run is split the same
+        // way with `rows` lanes per half. Scatter and gather stay plain contiguous copies.
+        auto eoff = [&](int64_t i, int h) -> int64_t {
+          const int64_t run = i / kCommThreads;
+          const int64_t l = i - run * kCommThreads;
+          const int64_t left = npk - run * kCommThreads;
+          const int64_t rows = left < kCommThreads ? left : kCommThreads;
+          return run * kCommThreads * EL + h * rows * 4 + l * 4;
+        };
+        for (int64_t i0 = threadIdx.x; i0 < npk; i0 += U * kCommThreads) {
+          Acc8<E> acc[U][2];
+          float4 p4[U][2], m4[U][2], v4[U][2];
+          bool live[U];
+#pragma unroll
+          for (int w = 0; w < U; ++w) {
+            const int64_t i = i0 + w * kCommThreads;
+            live[w] = i < npk;
+            if (!live[w]) continue;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int64_t e0 = eoff(i, h);
+              if constexpr (PT > 0) {
+                uint2 g[PT];
+#pragma unroll
+                for (int s = 0; s < PT; ++s) {
+                  const auto v = __builtin_amdgcn_raw_buffer_load_b64(src.rsrc(s), static_cast<int>(e0 * 2), 0, kAuxNt);
+                  g[s] = make_uint2(v[0], v[1]);
+                }
+#pragma unroll
+                for (int s = 0; s < PT; ++s) acc[w][h].add(g[s]);
+              } else {
+                for (int s = 0; s < P; ++s) {
+                  const auto v = __builtin_amdgcn_raw_buffer_load_b64(src.rsrc(s), static_cast<int>(e0 * 2), 0, kAuxNt);
+                  acc[w][h].add(make_uint2(v[0], v[1]));
+                }
+              }
+              p4[w][h] = *reinterpret_cast<const float4*>(sp + e0);
+              m4[w][h] = *reinterpret_cast<const float4*>(sm + e0);
+              v4[w][h] = *reinterpret_cast<const float4*>(sv + e0);
+            }
+          }
+#pragma unroll
+          for (int w = 0; w < U; ++w) {
+            if (!live[w]) continue;
+            const int64_t i = i0 + w * kCommThreads;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int64_t e0 = eoff(i, h);
+              Acc8<E>& ac = acc[w][h];
+              ac.v[0] = adamw(ac.v[0] * a.scale, &p4[w][h].x, &m4[w][h].x, &v4[w][h].x, a);
+              ac.v[1] = adamw(ac.v[1] * a.scale, &p4[w][h].y, &m4[w][h].y, &v4[w][h].y, a);
+              ac.v[2] = adamw(ac.v[2] * a.scale, &p4[w][h].z, &m4[w][h].z, &v4[w][h].z, a);
+              ac.v[3] = adamw(ac.v[3] * a.scale, &p4[w][h].w, &m4[w][h].w, &v4[w][h].w, a);
+              *reinterpret_cast<float4*>(sp + e0) = p4[w][h];
+              *reinterpret_cast<float4*>(sm + e0) = m4[w][h];
+              *reinterpret_cast<float4*>(sv + e0) = v4[w][h];
+              const uint2 o = ac.pack(1.f);
+              *reinterpret_cast<uint2*>(own_out + e0 * 2) = o;
+              typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+              const u32x2 ov = {o.x, o.y};
+              for (int k = 0; k < P; ++k)
+                if (k != r)
+                  __builtin_amdgcn_raw_buffer_store_b64(ov, slab_rsrc(a.base[k] + roff), static_cast<int>(e0 * 2), 0,
+                                                        kAuxWt);
+            }
+          }
+        }
+      } else
       // U packs per lane per iteration, every load issued before the first use: the
       // persistent grid has only 2 workgroups per CU, so bytes in flight come from ILP
       for (int64_t i0 = threadIdx.x; i0 < npk; i0 += U * kCommThreads) {
@@ -233,13 +307,15 @@ void launch_adamw(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {
   // study knobs: MXAR_ADAM_STREAM (state access form, above), MXAR_ADAM_U (packs per lane)
   static const int mode = [] {
     const char* e = study_env("MXAR_ADAM_STREAM");
-    return e != nullptr ? std::atoi(e) : 0;
+    return e != nullptr ? std::atoi(e) : -1;
   }();
   static const int u = [] {
     const char* e = study_env("MXAR_ADAM_U");
     return e != nullptr ? std::atoi(e) : 2;
   }();
-  if (mode == 1)
+  if (mode == 3 || (mode < 0 && dt != DType::F32))
+    launch_adamw_t<3, 2>(a, grid, s, dt);  // 16-bit parameters: run-contiguous halves (default)
+  else if (mode == 1)
     launch_adamw_t<1, 2>(a, grid, s, dt);
   else if (mode == 2)
     launch_adamw_t<2, 2>(a, grid, s, dt);

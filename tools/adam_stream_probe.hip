@@ -93,6 +93,34 @@ __global__ __launch_bounds__(256) void adam_like(const u4* g, f4* p, f4* m, f4* 
   }
 }
 
+// MODE 4: the same 28 B/param, lane-contiguous: unit u = 8 parameters as two halves of 4, at
+// element offsets [4l, 4l + 4) of each 1024-parameter half of a 256-lane run (the fused
+// kernel's default layout since round 5), so every fp32 access of a wave is 1 KiB of
+// consecutive bytes and every bf16 one 512 B. Modes 0-3 give each lane 32 consecutive fp32
+// bytes, so each 16-B instruction touches every other 16 B of 2 KiB.
+__global__ __launch_bounds__(256) void adam_like_halves(const uint2* g, f4* p, f4* m, f4* v, uint2* w, int64_t units,
+                                                         float lr) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  for (int64_t u = blockIdx.x * 256 + threadIdx.x; u < units; u += stride) {
+    const int64_t run = u / 256, l = u - run * 256;
+    for (int h = 0; h < 2; ++h) {
+      const int64_t q = run * 512 + h * 256 + l;  // index in units of 4 parameters
+      const uint2 gg = g[q];
+      f4 p0 = p[q], m0 = m[q], v0 = v[q];
+      const float gf[4] = {bf(gg.x & 0xffffu), bf(gg.x >> 16), bf(gg.y & 0xffffu), bf(gg.y >> 16)};
+      for (int i = 0; i < 4; ++i) {
+        m0[i] = 0.9f * m0[i] + 0.1f * gf[i];
+        v0[i] = 0.999f * v0[i] + 0.001f * gf[i] * gf[i];
+        p0[i] -= lr * m0[i] * __frsqrt_rn(v0[i] + 1e-8f);
+      }
+      p[q] = p0;
+      m[q] = m0;
+      v[q] = v0;
+      w[q] = make_uint2(tobf(p0[0]) | (tobf(p0[1]) << 16), tobf(p0[2]) | (tobf(p0[3]) << 16));
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void copy4(const f4* a, f4* b, int64_t n4) {
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += static_cast<int64_t>(gridDim.x) * 256) b[i] = a[i];
 }
@@ -139,6 +167,25 @@ int main() {
   }
   for (int grid : {256, 512, 1024, 2048}) {
     if (run<3>(grid, g, p, m, v, w, units, e0, e1)) return 1;
+  }
+  for (int grid : {1024, 2048, 4096, 8192}) {  // MODE 4: lane-contiguous halves
+    for (int i = 0; i < 3; ++i)
+      hipLaunchKernelGGL(adam_like_halves, dim3(grid), dim3(256), 0, 0, reinterpret_cast<const uint2*>(g), p, m, v,
+                         reinterpret_cast<uint2*>(w), units, 1e-6f);
+    CHECK(hipDeviceSynchronize());
+    const int it = 20;
+    CHECK(hipEventRecord(e0, 0));
+    for (int i = 0; i < it; ++i)
+      hipLaunchKernelGGL(adam_like_halves, dim3(grid), dim3(256), 0, 0, reinterpret_cast<const uint2*>(g), p, m, v,
+                         reinterpret_cast<uint2*>(w), units, 1e-6f);
+    CHECK(hipEventRecord(e1, 0));
+    CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= it;
+    const double bytes = 28.0 * 8.0 * static_cast<double>(units);
+    std::printf("{\"kernel\": \"adam_like\", \"mode\": 4, \"grid\": %d, \"params\": %lld, \"ms\": %.4f, \"TBps\": %.3f}\n",
+                grid, static_cast<long long>(units * 8), ms, bytes / (ms * 1e-3) / 1e12);
   }
   // copy roofline: the fp32 master array into v (4 B/param read + 4 B/param written)
   {
