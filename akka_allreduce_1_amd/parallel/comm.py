@@ -186,6 +186,7 @@ class XgmiCommunicator:
         self._launch: dict[str, tuple] = {}  # algo label -> (native Algo, grid, units, launch-size grid)
         self._p2p = None
         self._sdma = None
+        self._sdma_error: CommError | None = None
 
     @property
     def sdma(self):
@@ -193,10 +194,16 @@ class XgmiCommunicator:
         engines), created on first use - collectively: every rank must reach it together
         (BucketedGradReducer.tune_schedule does)."""
         if self._sdma is None:
+            if self._sdma_error is not None:  # failed before on every rank: not tried again
+                raise self._sdma_error
             from .sdma import SdmaCommunicator
 
-            self._sdma = SdmaCommunicator(self.group, device=self.device, slot_bytes=self.slot_bytes,
-                                          cpu_group=self.cpu_group)
+            try:
+                self._sdma = SdmaCommunicator(self.group, device=self.device, slot_bytes=self.slot_bytes,
+                                              cpu_group=self.cpu_group)
+            except CommError as e:  # collective: every rank raised the same
+                self._sdma_error = e
+                raise
         return self._sdma
 
     @property

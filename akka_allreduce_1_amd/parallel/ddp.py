@@ -15,8 +15,12 @@ so this module makes the gradients themselves the flat vectors:
   protocol relies on.
 * `wait()` (end of backward) launches any bucket that never became ready (unused
   parameters), then joins the comm stream into the compute stream.
+* CU-sliced schedules: an algo label `cuN:<algo>` (e.g. "cu32:twoshot@64") runs the bucket
+  allreduces on a comm stream whose kernels may use only N of the GPU's CUs
+  (hipExtStreamCreateWithCUMask, spread over every XCD): the collective then occupies a fixed
+  slice of the GPU instead of a workgroup on every CU beside backward's GEMMs.
 * `overlap="auto"`: the first steps try each candidate schedule - buckets beside backward at
-  the communicator's grid, beside backward at 128 workgroups, all after backward - for
+  the communicator's grid, beside backward at 128 workgroups, on a 32-CU slice, all after backward - for
   `tune_steps` steps each, timing first-gradient -> comm joined on the GPU; the ranks agree on
   the fastest (MAX over ranks of each candidate's best step) and keep it. Sharing the GPU with
   backward's GEMMs is not free: on one MI355X the serial schedule won at every grid
@@ -108,6 +112,8 @@ class BucketedGradReducer:
         algo: the communicator's algorithm label per bucket, e.g. "twoshot@128": a bucket
         reduced while backward still runs competes with it for CUs, and fewer persistent
         workgroups leave more of the GPU to the GEMMs (default: the tuned / built-in choice)."""
+        self._masked: dict[int, tuple[int, object]] = {}  # CUs -> (raw masked stream, torch ExternalStream)
+        self._cus = 0
         self.algo = algo
         self.threshold = th_reduce < 1.0 or th_complete < 1.0 or rescale
         self.th = (float(th_reduce), float(th_complete), bool(rescale))
@@ -157,11 +163,47 @@ class BucketedGradReducer:
         self._cur_stream = _current_stream
         self._dev_index = self.device.index if self.on_gpu else -1
         self._comm_raw = self.stream.cuda_stream if self.stream is not None else None
+        self._base_stream = (self.stream, self._comm_raw)
+        self._set_algo(self.label)  # a "cuN:" schedule chosen before the streams existed
         # communicators that take a raw `stream=` argument (XgmiCommunicator) skip the context
         self._raw_ok = self.on_gpu and bool(getattr(comm, "accepts_stream", False))
         self._next = 0
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad_ready) for p in self.params]
         self.stats = {"steps": 0, "buckets_launched": 0, "bytes": 0}
+
+    # ------------------------------------------------------------------ CU slices
+    def _set_algo(self, label: str) -> None:
+        """Adopt an algo label: "cuN:<algo>" = <algo> on a comm stream restricted to N CUs."""
+        cus, algo = 0, label
+        if isinstance(label, str) and label.startswith("cu") and ":" in label:
+            head, algo = label.split(":", 1)
+            cus = int(head[2:])
+        self.algo = algo
+        if not self.on_gpu or getattr(self, "_base_stream", None) is None:
+            self._cus = cus
+            return
+        if cus == self._cus and (cus == 0 or cus in self._masked):
+            return
+        if cus:
+            if cus not in self._masked:
+                from .._native import C
+
+                raw = C.hip.stream_create_cu_mask(self.device.index, cus)
+                self._masked[cus] = (raw, torch.cuda.ExternalStream(raw, device=self.device))
+            raw, ext = self._masked[cus]
+            prev_raw = self._comm_raw
+            self.stream, self._comm_raw = ext, raw
+            # buckets of the previous stream finish first (the communicator also orders its
+            # launches across streams, XgmiComm::order_after_last)
+            if prev_raw is not None and prev_raw != raw:
+                self.stream.wait_stream(torch.cuda.ExternalStream(prev_raw, device=self.device))
+        else:
+            self.stream, self._comm_raw = self._base_stream
+        self._cus = cus
+
+    @property
+    def label(self) -> str:
+        return f"cu{self._cus}:{self.algo}" if self._cus else self.algo
 
     # ------------------------------------------------------------------ layout
     def _build(self, bucket_bytes: int, first_bucket_bytes: int | None) -> list[GradBucket]:
@@ -306,8 +348,9 @@ class BucketedGradReducer:
         if not self.on_gpu or self.threshold:
             return
         xgmi = bool(getattr(self.comm, "accepts_stream", False))
-        base = self.schedule[1] if self.schedule else self.algo
-        default = [(True, base), (True, "twoshot@128"), (False, base)] if xgmi else [(True, base), (False, base)]
+        base = self.schedule[1] if self.schedule else self.label
+        default = ([(True, base), (True, "twoshot@128"), (True, "cu32:twoshot@64"), (False, base)] if xgmi
+                   else [(True, base), (False, base)])
         if xgmi and getattr(self.comm, "world", 1) > 1 and getattr(type(self.comm), "sdma", None) is not None \
                 and candidates is None:
             # the copy-engine allreduce leaves the CUs to backward's GEMMs; created here, on
@@ -322,7 +365,8 @@ class BucketedGradReducer:
         self._times: list[list[float]] = [[] for _ in self._cands]
         self._step_i = 0
         self._ev0 = self._ev1 = None
-        self.overlap, self.algo = self._cands[0]
+        self.overlap = self._cands[0][0]
+        self._set_algo(self._cands[0][1])
         self.schedule = None
         self._auto = True
 
@@ -338,11 +382,13 @@ class BucketedGradReducer:
         self._step_i += 1
         k = self._step_i // self._tune_steps
         if k < len(self._cands):
-            self.overlap, self.algo = self._cands[k]
+            self.overlap = self._cands[k][0]
+            self._set_algo(self._cands[k][1])
             return
         i, best = self._agree([min(t) if t else float("inf") for t in self._times])
-        self.overlap, self.algo = self._cands[i]
-        self.schedule = ("overlap" if self.overlap else "serial", self.algo)
+        self.overlap = self._cands[i][0]
+        self._set_algo(self._cands[i][1])
+        self.schedule = ("overlap" if self.overlap else "serial", self.label)
         self.stats["schedule_ms"] = {f"{'overlap' if o else 'serial'}:{a}": round(float(x), 3)
                                      for (o, a), x in zip(self._cands, best.tolist())}
         self.stats["schedule"] = f"{self.schedule[0]}:{self.schedule[1]}"
@@ -359,6 +405,14 @@ class BucketedGradReducer:
             except Exception:  # noqa: BLE001 - interpreter shutdown
                 pass
         self._events = []
+        for raw, _ in getattr(self, "_masked", {}).values():
+            try:
+                from .._native import C
+
+                C.hip.stream_destroy(raw)
+            except Exception:  # noqa: BLE001 - interpreter shutdown
+                pass
+        self._masked = {}
 
     def remove_hooks(self) -> None:
         for h in self._hooks:

@@ -24,13 +24,30 @@ from .comm import CommError, _KERNEL_DTYPES, _current_stream, _describe
 _H = C.hip
 
 
+_XDEV_VALIDATED = [False]
+
+
+def mark_xdev_validated() -> None:
+    """Allow SDMA copies across GPUs in this process: called once a cross-GPU SDMA allreduce of
+    the same job has been validated where a fault could not take the caller down (bench.py
+    runs it in child processes first, `benchmarks/sdma_xdev.py`)."""
+    _XDEV_VALIDATED[0] = True
+
+
+def xdev_allowed() -> bool:
+    return _XDEV_VALIDATED[0] or os.environ.get("MXAR_SDMA_XDEV", "0") == "1"
+
+
 class SdmaCommunicator:
     """Allreduce of the ranks of a torch.distributed group with SDMA cross-rank copies."""
 
     accepts_stream = True
 
     def __init__(self, group=None, *, device: torch.device | int | None = None, slot_bytes: int = 64 << 20,
-                 grid: int = 32, engines_per_peer: int = 0, timeout_s: float = 20.0, cpu_group=None):
+                 grid: int = 32, engines_per_peer: int = 0, timeout_s: float = 20.0, cpu_group=None,
+                 validate: bool = True):
+        """validate: one small allreduce checked against the exact sum on every rank before the
+        communicator is handed out (collective; a wrong result raises CommError everywhere)."""
         import torch.distributed as dist
 
         self.group = group
@@ -43,6 +60,16 @@ class SdmaCommunicator:
             cpu_group = group if dist.get_backend(group) == "gloo" else dist.new_group(
                 ranks=None if group is None else dist.get_process_group_ranks(group), backend="gloo")
         self.cpu_group = cpu_group
+        # Engine copies into ANOTHER GPU's memory: allowed once validated for this job in a
+        # process a fault cannot take down (mark_xdev_validated), or with MXAR_SDMA_XDEV=1.
+        # Decided from the ranks' PCI locations BEFORE anything is allocated; every rank sees
+        # the same locations, so every rank decides the same way.
+        locs: list = [None] * self.world
+        dist.all_gather_object(locs, int(_H.pci_location(self.device.index)), group=cpu_group)
+        self.cross_gpu = len(set(locs)) > 1
+        if self.cross_gpu and not xdev_allowed():
+            raise CommError("SdmaCommunicator across GPUs needs a validated run first "
+                            "(mark_xdev_validated / benchmarks/sdma_xdev.py) or MXAR_SDMA_XDEV=1")
         c, h, err = None, None, ""
         try:
             c = _H.SdmaComm(self.rank, self.world, self.device.index, slot_bytes, grid, engines_per_peer, timeout_s)
@@ -54,14 +81,6 @@ class SdmaCommunicator:
         errs = [e for _, e in hs if e]
         if errs:
             raise CommError("SdmaCommunicator setup failed: " + "; ".join(errs))
-        # Engine copies into ANOTHER GPU's memory have not run on a multi-GPU node yet (the
-        # rehearsals put every rank on one GPU): until they have, they are opt-in - a fault
-        # there would take the process down rather than raise. Every rank sees the same
-        # handles, so every rank decides the same way. (handle = IPC handle + 8-B PCI location)
-        locs = {bytes(x)[-8:] for x, _ in hs}
-        if len(locs) > 1 and os.environ.get("MXAR_SDMA_XDEV", "0") != "1":
-            raise CommError("SdmaCommunicator across GPUs is opt-in until validated on a multi-GPU node "
-                            "(MXAR_SDMA_XDEV=1)")
         try:
             c.connect([x for x, _ in hs])
         except Exception as e:  # noqa: BLE001
@@ -73,6 +92,36 @@ class SdmaCommunicator:
             raise CommError("SdmaCommunicator connect failed: " + "; ".join(errs))
         self._c = c
         self._dev = self.device.index
+        if validate:
+            self.validate()
+
+    def validate(self, n: int = 1 << 20 | 12345) -> float:
+        """One allreduce of n fp32 elements against the exact sum (every rank regenerates every
+        rank's input from its seed); collective. Returns the max error, raises CommError on
+        any rank's failure."""
+        import torch.distributed as dist
+
+        from ..ops import fill_uniform
+
+        err, msg = float("inf"), ""
+        try:
+            xs = [fill_uniform(torch.empty(n, device=self.device), seed=4242 + k) for k in range(self.world)]
+            ref = torch.zeros(n, device=self.device)
+            for x in xs:
+                ref += x
+            y = self.allreduce(xs[self.rank])
+            torch.cuda.synchronize(self.device)
+            self.check()
+            err = (y - ref).abs().max().item()
+        except Exception as e:  # noqa: BLE001 - every rank learns of it below
+            msg = repr(e)
+        ok = err <= 1e-5 * self.world
+        res: list = [None] * self.world
+        dist.all_gather_object(res, (ok, err, msg), group=self.cpu_group)
+        bad = [(k, r) for k, r in enumerate(res) if not r[0]]
+        if bad:
+            raise CommError(f"SdmaCommunicator validation failed: {bad}")
+        return max(r[1] for r in res)
 
     def allreduce(self, inp: torch.Tensor, out: torch.Tensor | None = None, *, op: str = "sum", algo: str = "sdma",
                   stream: int | None = None) -> torch.Tensor:

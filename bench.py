@@ -737,6 +737,7 @@ def main() -> None:
     ap.add_argument("--no-dp", action="store_true", help="skip the ResNet-50 / Llama-3-8B DP-step sections")
     ap.add_argument("--no-local", action="store_true", help="skip the 8-logical-rank section at N = 1")
     ap.add_argument("--no-links", action="store_true", help="skip the xGMI bring-up probes at N > 1")
+    ap.add_argument("--no-sdma", action="store_true", help="skip the copy-engine allreduce section at N > 1")
     ap.add_argument("--no-protocol", action="store_true", help="skip the master/worker protocol-engine section")
     ap.add_argument("--no-native", action="store_true",
                     help="skip the native-deployment protocol rounds (child mxar processes; e.g. under a profiler)")
@@ -996,6 +997,29 @@ def main() -> None:
     if engine_ok and not args.no_fused_step:
         log(rank, "fused AdamW step")
         result["fused_adamw_step"] = fused_step(comm, x, y, world, rank, args, dev)
+    if engine_ok and world > 1 and not args.no_sdma:
+        # the copy-engine allreduce across the GPUs, first in child processes (a fault there
+        # cannot cost this line); validated on every rank -> the DP tuner may use it too
+        from akka_allreduce_1_amd.parallel.comm import free_port
+        from akka_allreduce_1_amd.parallel.sdma import mark_xdev_validated
+        from benchmarks.sdma_xdev import run_children
+
+        log(rank, "sdma: copy-engine allreduce across the ranks (child processes)")
+        port = [free_port() if rank == 0 else 0]
+        dist.broadcast_object_list(port, src=0)
+        torch.cuda.synchronize(dev)
+        mine = run_children(rank, world, local, port[0], mib=args.size_mib)
+        rows = [None] * world
+        dist.all_gather_object(rows, mine)
+        ok = all(r.get("validated") for r in rows)
+        p50 = [r.get("p50_ms") for r in rows if r.get("p50_ms") is not None]
+        result["sdma"] = {"validated": ok, "cross_gpu": bool(rows[0].get("cross_gpu")),
+                          "p50_ms": max(p50) if len(p50) == world else None,
+                          "algbw": round(nbytes / (max(p50) / 1e3) / 1e9, 2) if len(p50) == world else None,
+                          "max_abs_err": max((r.get("max_abs_err") or 0.0) for r in rows),
+                          "errors": [r.get("error") for r in rows if r.get("error")][:2]}
+        if ok:
+            mark_xdev_validated()
     if sweep is not None:
         result["sweep"] = sweep
     if engine_ok and world == 1 and not args.share_device and not args.no_local:

@@ -546,6 +546,10 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
             # every bucket after backward (no overlap), and the overlap on a normal-priority
             # comm stream (the GEMMs' dispatches are not pre-empted by the comm queue)
             variants += [("serial_grid512", 512, False, True, 1024), ("grid128_normal_prio", 128, True, False, 1024)]
+            # CU-sliced comm streams (hipExtStreamCreateWithCUMask; ddp.py "cuN:" schedules): the
+            # bucket kernels may use only N of the 256 CUs, two workgroups per CU of the slice
+            variants += [("cu16_grid32", 32, True, True, 1024), ("cu32_grid64", 64, True, True, 1024),
+                         ("cu64_grid128", 128, True, True, 1024)]
             # the copy-engine allreduce: cross-rank copies on SDMA engines, reduce / gather on
             # a small grid (the comm's CU footprint)
             cu_comm, sdma_comm = comm, None
@@ -576,6 +580,11 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                     reducer.overlap = ov
                     reducer.stream = hi_stream if hi else lo_stream
                     reducer._comm_raw = hi_raw if hi else lo_stream.cuda_stream
+                    reducer._cus = 0
+                    if name.startswith("cu"):
+                        reducer._cus = -1  # force the switch onto the masked stream
+                        reducer._set_algo(f"{name.split('_')[0]}:auto")
+                        cell["cus"] = reducer._cus
                     with torch.no_grad():
                         for fn in (overlap, compute, comm_only):
                             for _ in range(warm):
@@ -607,11 +616,16 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                 except Exception as e:  # noqa: BLE001
                     cell["error"] = repr(e)
                 row[name] = cell
-            reducer.overlap, reducer.stream, reducer._comm_raw = True, hi_stream, hi_raw
+            reducer.overlap, reducer.stream, reducer._comm_raw, reducer._cus = True, hi_stream, hi_raw, 0
+            reducer.algo = "auto"
             comm = cu_comm
             ok = {g: c for g, c in row.items() if isinstance(c, dict) and "step_ms" in c}
             if ok:
                 row["best"] = min(ok, key=lambda g: ok[g]["step_ms"])
+            cu = {g: c for g, c in ok.items() if g.startswith("cu")}
+            if cu:  # the CU-sliced candidate's best cell
+                g = min(cu, key=lambda k: cu[k]["step_ms"])
+                row["cu_slice"] = dict(cu[g], variant=g)
             sd = {g: c for g, c in ok.items() if g.startswith("sdma")}
             if sd:  # the copy-engine candidate's best cell, next to the CU grids'
                 row["sdma"] = dict(sd[min(sd, key=lambda g: sd[g]["step_ms"])], variant=min(sd, key=lambda g: sd[g]["step_ms"]))

@@ -14,6 +14,8 @@ side file (`detail`), and the line holds the headline fields plus compact summar
                  deployment, control-bridge), plus whether the timed rounds were validated
   adamw          fused reduce-scatter + AdamW + all-gather: ms and HBM TB/s
   dp             BASELINE configs 4 / 5: [step ms, compute-only ms, exposed ms]
+  sdma           N > 1: the copy-engine allreduce across the GPUs, validated in child processes
+                 first [ok, p50 ms, algbw GB/s] (benchmarks/sdma_xdev.py)
   xgmi_links     N > 1: the bring-up pack (akka_allreduce_1_amd/utils/links.py) - single-peer
                  push GB/s [min, median, max], all-peer push GB/s per rank [min, max], fan-out
                  ratio (all-peer / single-peer, 7 links ideal = 7), one-way flag hand-off us
@@ -146,6 +148,12 @@ def _dp(dp: dict) -> tuple[dict, dict]:
             sd = r.get("sdma")
             if isinstance(sd, dict) and "step_ms" in sd:
                 ovl[m + "_sdma"] = [sd.get("step_ms"), sd.get("exposed_comm_ms"), sd.get("gemm_slowdown")]
+            cu = r.get("cu_slice")
+            if isinstance(cu, dict) and "step_ms" in cu:
+                ovl[m + "_cu"] = [cu.get("variant"), cu.get("step_ms"), cu.get("exposed_comm_ms"), cu.get("gemm_slowdown")]
+            se = r.get("serial_grid512")
+            if isinstance(se, dict) and "step_ms" in se:
+                ovl[m + "_serial"] = [se.get("step_ms"), se.get("gemm_slowdown")]
     return out, ovl
 
 
@@ -203,6 +211,11 @@ def compact(result: dict, detail_path: str | None = None) -> dict:
         out["reduce_kernel"] = {"copy_TBps": rk.get("copy_roofline_TBps"),
                                 **{P: rk[P].get("frac_copy_roofline") for P in ("P2", "P4", "P8")
                                    if isinstance(rk.get(P), dict)}}
+    x = result.get("sdma")
+    if isinstance(x, dict):  # N > 1: the copy-engine allreduce across the GPUs (child processes)
+        out["sdma"] = {"ok": x.get("validated"), "ms": x.get("p50_ms"), "algbw": x.get("algbw")}
+        if x.get("errors"):
+            out["sdma"]["error"] = str(x["errors"][0])[:100]
     sd = result.get("sdma_local")
     if isinstance(sd, dict):  # copy-engine allreduce, [p50 ms, algbw GB/s] per logical rank count
         out["sdma_local"] = {P: ([sd[P].get("p50_ms"), sd[P].get("algbw_GBps")] if "p50_ms" in sd[P]

@@ -317,6 +317,7 @@ void bind_hip(py::module_& m) {
       .def_readwrite("step", &AdamW::step);
 
   h.def("sdma_diagnose", &sdma_diagnose, py::arg("device") = 0);
+  h.def("pci_location", &pci_location, py::arg("device"));
   py::class_<SdmaComm>(h, "SdmaComm")
       .def(py::init<int, int, int, int64_t, int, int, double>(), py::arg("rank"), py::arg("world"), py::arg("device"),
            py::arg("slot_bytes"), py::arg("grid") = 32, py::arg("engines_per_peer") = 0, py::arg("timeout_s") = 20.0)
@@ -610,6 +611,28 @@ void bind_hip(py::module_& m) {
   h.def("stream_wait_event", [](uintptr_t s, uintptr_t e) {
     hip_check(hipStreamWaitEvent(as_stream(s), reinterpret_cast<hipEvent_t>(e), 0), "hipStreamWaitEvent");
   });
+  // A stream whose kernels run only on `cus` of the device's CUs, spread evenly over the CU
+  // numbering (every XCD gets its share): a collective overlapped with compute then occupies
+  // a fixed slice of the GPU instead of a workgroup on every CU (ddp.py `cuN:` schedules).
+  h.def(
+      "stream_create_cu_mask",
+      [](int device, int cus) {
+        hip_check(hipSetDevice(device), "hipSetDevice");
+        int total = 0;
+        hip_check(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, device), "CU count");
+        if (cus < 1 || cus > total) throw std::invalid_argument("stream_create_cu_mask: cus must be in [1, CU count]");
+        std::vector<uint32_t> mask(static_cast<size_t>((total + 31) / 32), 0u);
+        for (int i = 0; i < cus; ++i) {
+          const int cu = static_cast<int>(static_cast<int64_t>(i) * total / cus);
+          mask[static_cast<size_t>(cu / 32)] |= 1u << (cu % 32);
+        }
+        hipStream_t st = nullptr;
+        hip_check(hipExtStreamCreateWithCUMask(&st, static_cast<uint32_t>(mask.size()), mask.data()),
+                  "hipExtStreamCreateWithCUMask");
+        return reinterpret_cast<uintptr_t>(st);
+      },
+      py::arg("device"), py::arg("cus"));
+  h.def("stream_destroy", [](uintptr_t s) { (void)hipStreamDestroy(reinterpret_cast<hipStream_t>(s)); });
   h.def("device_count", [] {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) n = 0;

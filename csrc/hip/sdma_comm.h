@@ -109,5 +109,8 @@ class SdmaComm {
 
 // HSA view of the machine (agents, PCI locations, SDMA engine masks): bring-up diagnostics
 std::string sdma_diagnose(int device);
+// PCI location of a HIP device ((domain << 32) | bdf): which GPU a rank's SDMA slab lives on,
+// known before anything is allocated (SdmaCommunicator's cross-GPU check).
+uint64_t pci_location(int device);
 
 }  // namespace mxar

@@ -125,6 +125,8 @@ __global__ __launch_bounds__(kCommThreads) void sdma_gather_kernel(char* out, co
 // ---------------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------------
+uint64_t pci_location(int device) { return hip_location(device); }
+
 std::string sdma_diagnose(int device) {
   std::string out;
   hip_check(hipSetDevice(device), "hipSetDevice");

@@ -51,6 +51,8 @@ def _n8_shape(base: dict) -> dict:
                           auto_schedule_tuning_ms=[123.4, 123.4, 123.4])
     r["protocol"] = dict(r["protocol"], worker_ids=list(range(8)),
                          bridge={"driver": "x" * 80, "validated": True, "ms_per_round": 0.4326})
+    r["sdma"] = {"validated": True, "cross_gpu": True, "p50_ms": 1.2345, "algbw": 217.45, "max_abs_err": 0.0312,
+                 "errors": []}
     r["topology"] = {"devices_visible": 8, "ranks": 8, "peer_access": [[1] * 8] * 8,
                      "link_type": [["xgmi"] * 8] * 8, "hops": [[1] * 8] * 8}
     return r
@@ -143,6 +145,7 @@ def test_n8_line_carries_the_link_pack():
     assert d["xgmi_links"] == {"single_GBps": [101.23, 123.45, 131.11], "all_GBps": [812.34, 812.34],
                                "ratio": 6.58, "flag_us": [1.234, 1.234, 1.567]}
     assert d["config"]["algo"].split("@")[0].split("~")[0] not in ("ring_native", "rccl", "rsag")
+    assert d["sdma"] == {"ok": True, "ms": 1.2345, "algbw": 217.45}
 
 
 def test_link_pack_outlives_every_other_section():

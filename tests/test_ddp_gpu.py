@@ -37,8 +37,8 @@ def _worker(rank, world, port, q, dtype, mode):
         assert len(red.buckets) >= 3
         g = torch.Generator(device="cuda:0")
         data = [torch.randn(16, 64, device="cuda:0", generator=g.manual_seed(10 + r)).to(dtype) for r in range(world)]
-        # auto: 3 tuning steps (one per candidate schedule), then the agreed schedule
-        for step in range(6 if mode == "auto" else 3):
+        # auto: 5 tuning steps (one per candidate schedule), then the agreed schedule
+        for step in range(7 if mode == "auto" else 3):
             red.zero_grad()
             m(data[rank] * (step + 1)).float().pow(2).mean().backward()
             red.wait()
@@ -56,8 +56,10 @@ def _worker(rank, world, port, q, dtype, mode):
                 assert err <= tol, (step, i, err, tol)
         if mode == "auto":
             assert red.schedule is not None and "schedule" in red.stats, red.stats
-            # communicator grid, 128 workgroups, serial, and the copy-engine (SDMA) allreduce
-            assert len(red.stats["schedule_ms"]) == 4 and "overlap:sdma" in red.stats["schedule_ms"], red.stats
+            # communicator grid, 128 workgroups, a 32-CU slice, serial, and the copy-engine (SDMA)
+            # allreduce
+            sm = red.stats["schedule_ms"]
+            assert len(sm) == 5 and "overlap:sdma" in sm and "overlap:cu32:twoshot@64" in sm, red.stats
         q.put((rank, True, ""))
     except Exception:  # noqa: BLE001
         import traceback

@@ -162,3 +162,27 @@ def test_multiprocess_sdma_output_reusable_right_after_the_call():
                 p.kill()
     bad = [r for r in res if not r[1]]
     assert not bad, bad
+
+
+def test_sdma_xdev_children_validate():
+    """bench.py's N > 1 copy-engine section (benchmarks/sdma_xdev.py): one child process per
+    rank, a gloo group of their own, validated against the exact sum and timed. Two 'ranks'
+    share this GPU here (the same path a multi-GPU node takes, same-device copies)."""
+    import threading
+
+    from akka_allreduce_1_amd.parallel import free_port
+    from benchmarks.sdma_xdev import run_children
+
+    port = free_port()
+    rows = [None, None]
+
+    def go(r):
+        rows[r] = run_children(r, 2, 0, port, mib=16, timeout=120.0)
+
+    th = [threading.Thread(target=go, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert all(r and r.get("validated") for r in rows), rows
+    assert all(r.get("p50_ms", 0) > 0 for r in rows), rows
