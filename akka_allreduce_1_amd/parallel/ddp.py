@@ -18,7 +18,9 @@ so this module makes the gradients themselves the flat vectors:
 * CU-sliced schedules: an algo label `cuN:<algo>` (e.g. "cu32:twoshot@64") runs the bucket
   allreduces on a comm stream whose kernels may use only N of the GPU's CUs
   (hipExtStreamCreateWithCUMask, spread over every XCD): the collective then occupies a fixed
-  slice of the GPU instead of a workgroup on every CU beside backward's GEMMs.
+  slice of the GPU instead of a workgroup on every CU beside backward's GEMMs. With the
+  training step on `compute_stream_excluding(device, N)` the split is complete: GEMMs on the
+  other CUs only, none of their tiles beside a spinning comm workgroup.
 * `overlap="auto"`: the first steps try each candidate schedule - buckets beside backward at
   the communicator's grid, beside backward at 128 workgroups, on a 32-CU slice, all after backward - for
   `tune_steps` steps each, timing first-gradient -> comm joined on the GPU; the ranks agree on
@@ -46,6 +48,19 @@ import torch
 from .comm import comm_stream
 
 _ALIGN_BYTES = 16
+
+
+def compute_stream_excluding(device, cus: int) -> "torch.cuda.ExternalStream":
+    """A stream on every CU of `device` except the `cus` CUs a "cuN:" comm schedule uses (the
+    same spread-out selection, csrc/hip/hip_bind.cc stream_create_cu_mask): run forward and
+    backward under `with torch.cuda.stream(s):` and the GEMMs never share a CU with the
+    overlapped collective - a GEMM otherwise waits for its slowest tile, and a tile on a CU
+    beside a spinning comm workgroup is slow. The stream lives as long as the process."""
+    from .._native import C
+
+    dev = torch.device(device)
+    raw = C.hip.stream_create_cu_mask(dev.index if dev.index is not None else torch.cuda.current_device(), cus, True)
+    return torch.cuda.ExternalStream(raw, device=dev)
 
 
 class TorchDistComm:

@@ -31,6 +31,7 @@ rate of back-to-back calls is reported next to it (`wall_us`).
 """
 from __future__ import annotations
 
+import contextlib
 import statistics
 import time
 
@@ -522,12 +523,18 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
             grads = [q.grad for q in params]
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 
+            cstream = {"s": None}  # the masked compute stream of a CU-split variant
+
             def overlap():
-                ev[0].record()
-                bwd.run(reducer)
-                ev[1].record()
-                reducer.wait()
-                torch._foreach_add_(params, grads, alpha=-1e-3)
+                ctx = torch.cuda.stream(cstream["s"]) if cstream["s"] is not None else contextlib.nullcontext()
+                with ctx:
+                    ev[0].record()
+                    bwd.run(reducer)
+                    ev[1].record()
+                    reducer.wait()
+                    torch._foreach_add_(params, grads, alpha=-1e-3)
+                if cstream["s"] is not None:
+                    torch.cuda.current_stream(dev).wait_stream(cstream["s"])
 
             def compute():
                 ev[0].record()
@@ -541,6 +548,7 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                 torch.cuda.current_stream(dev).wait_stream(reducer.stream)
 
             hi_stream, hi_raw = reducer.stream, reducer._comm_raw
+            splits: dict = {}
             lo_stream = torch.cuda.Stream(device=dev, priority=0)
             variants = [(f"grid{g}", g, True, True, 1024) for g in grids]
             # every bucket after backward (no overlap), and the overlap on a normal-priority
@@ -550,6 +558,9 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
             # bucket kernels may use only N of the 256 CUs, two workgroups per CU of the slice
             variants += [("cu16_grid32", 32, True, True, 1024), ("cu32_grid64", 64, True, True, 1024),
                          ("cu64_grid128", 128, True, True, 1024)]
+            # and the complete split: backward on every OTHER CU (ddp.compute_stream_excluding),
+            # so no GEMM tile shares a CU with a spinning comm workgroup
+            variants += [("split32_grid64", 64, True, True, 1024), ("split64_grid128", 128, True, True, 1024)]
             # the copy-engine allreduce: cross-rank copies on SDMA engines, reduce / gather on
             # a small grid (the comm's CU footprint)
             cu_comm, sdma_comm = comm, None
@@ -566,7 +577,9 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                 # backward instead of contending with it at full bandwidth
                 variants += [("tokens8192_grid256", 256, True, True, 8192), ("tokens8192_serial", 512, False, True, 8192),
                              ("tokens8192_grid32", 32, True, True, 8192), ("tokens8192_grid64", 64, True, True, 8192),
-                             ("tokens8192_grid128", 128, True, True, 8192)]
+                             ("tokens8192_grid128", 128, True, True, 8192),
+                             ("split16_tokens8192", 32, True, True, 8192), ("split32_tokens8192", 64, True, True, 8192),
+                             ("split64_tokens8192", 128, True, True, 8192)]
             for name, grid, ov, hi, tokens in variants:
                 cell: dict = {"tokens": tokens}
                 try:
@@ -581,10 +594,18 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                     reducer.stream = hi_stream if hi else lo_stream
                     reducer._comm_raw = hi_raw if hi else lo_stream.cuda_stream
                     reducer._cus = 0
-                    if name.startswith("cu"):
+                    cstream["s"] = None
+                    if name.startswith("cu") or name.startswith("split"):
+                        ncu = int(name.split("_")[0].replace("split", "").replace("cu", ""))
                         reducer._cus = -1  # force the switch onto the masked stream
-                        reducer._set_algo(f"{name.split('_')[0]}:auto")
+                        reducer._set_algo(f"cu{ncu}:auto")
                         cell["cus"] = reducer._cus
+                        if name.startswith("split"):
+                            if ncu not in splits:
+                                from akka_allreduce_1_amd.parallel import compute_stream_excluding
+
+                                splits[ncu] = compute_stream_excluding(dev, ncu)
+                            cstream["s"] = splits[ncu]
                     with torch.no_grad():
                         for fn in (overlap, compute, comm_only):
                             for _ in range(warm):
@@ -618,11 +639,12 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                 row[name] = cell
             reducer.overlap, reducer.stream, reducer._comm_raw, reducer._cus = True, hi_stream, hi_raw, 0
             reducer.algo = "auto"
+            cstream["s"] = None
             comm = cu_comm
             ok = {g: c for g, c in row.items() if isinstance(c, dict) and "step_ms" in c}
             if ok:
                 row["best"] = min(ok, key=lambda g: ok[g]["step_ms"])
-            cu = {g: c for g, c in ok.items() if g.startswith("cu")}
+            cu = {g: c for g, c in ok.items() if g.startswith("cu") or g.startswith("split")}
             if cu:  # the CU-sliced candidate's best cell
                 g = min(cu, key=lambda k: cu[k]["step_ms"])
                 row["cu_slice"] = dict(cu[g], variant=g)

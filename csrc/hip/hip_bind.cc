@@ -614,9 +614,11 @@ void bind_hip(py::module_& m) {
   // A stream whose kernels run only on `cus` of the device's CUs, spread evenly over the CU
   // numbering (every XCD gets its share): a collective overlapped with compute then occupies
   // a fixed slice of the GPU instead of a workgroup on every CU (ddp.py `cuN:` schedules).
+  // exclude=True gives the complement - the compute stream of a CU split (ddp.py
+  // compute_stream_excluding), whose GEMM tiles then never share a CU with the collective.
   h.def(
       "stream_create_cu_mask",
-      [](int device, int cus) {
+      [](int device, int cus, bool exclude) {
         hip_check(hipSetDevice(device), "hipSetDevice");
         int total = 0;
         hip_check(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, device), "CU count");
@@ -626,12 +628,16 @@ void bind_hip(py::module_& m) {
           const int cu = static_cast<int>(static_cast<int64_t>(i) * total / cus);
           mask[static_cast<size_t>(cu / 32)] |= 1u << (cu % 32);
         }
+        if (exclude) {  // every CU BUT those: the compute side of a CU split
+          for (int cu = 0; cu < total; ++cu) mask[static_cast<size_t>(cu / 32)] ^= 1u << (cu % 32);
+        }
         hipStream_t st = nullptr;
         hip_check(hipExtStreamCreateWithCUMask(&st, static_cast<uint32_t>(mask.size()), mask.data()),
                   "hipExtStreamCreateWithCUMask");
         return reinterpret_cast<uintptr_t>(st);
       },
-      py::arg("device"), py::arg("cus"));
+      py::arg("device"), py::arg("cus"), py::arg("exclude") = false,
+      "stream on `cus` CUs spread over the device (exclude=True: on every CU but those)");
   h.def("stream_destroy", [](uintptr_t s) { (void)hipStreamDestroy(reinterpret_cast<hipStream_t>(s)); });
   h.def("device_count", [] {
     int n = 0;
