@@ -419,6 +419,7 @@ void bind_hip(py::module_& m) {
            py::arg("ranks_in_launch") = 1)
       .def("set_straggler", &XgmiComm::set_straggler, py::arg("rank"), py::arg("us"))
       .def("set_read_delay", &XgmiComm::set_read_delay, py::arg("rank"), py::arg("us"))
+      .def("set_forward_delay", &XgmiComm::set_forward_delay, py::arg("rank"), py::arg("us"))
       .def_property_readonly("threshold_rows", &XgmiComm::threshold_rows)
       .def_property_readonly("slab_address", &XgmiComm::slab_address)
       .def_property("size_grid", &XgmiComm::size_grid, &XgmiComm::set_size_grid)

@@ -248,6 +248,12 @@ class XgmiComm {
     rdelay_rank_ = rank;
     rdelay_us_ = us;
   }
+  // Test knob: rank `rank` idles `us` microseconds before the ring's last all-gather forward
+  // of every ring launch (its late flag races the next kernel's flags: flag-ownership test).
+  void set_forward_delay(int rank, double us) {
+    fdelay_rank_ = rank;
+    fdelay_us_ = us;
+  }
   // Device-side barrier over all ranks (enqueued on `stream`).
   void barrier(hipStream_t stream);
 
@@ -380,6 +386,8 @@ class XgmiComm {
   double delay_us_ = 0;
   int rdelay_rank_ = -1;
   double rdelay_us_ = 0;
+  int fdelay_rank_ = -1;
+  double fdelay_us_ = 0;
   int64_t oneshot_max_;
   int64_t ll_auto_max_ = 0;  // Auto picks the low-latency one-shot up to this many bytes
   double timeout_s_;

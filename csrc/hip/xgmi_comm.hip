@@ -535,6 +535,7 @@ __global__ __launch_bounds__(kCommThreads) void ring_kernel(CommArgs a) {
                  ERR_TIMEOUT_REDUCE, acq);
       ps.add(4, tw);
       ps.count(7);
+      if (fwd && t == P - 3) forward_delay(a, r);  // test knob: the last forward comes late
       char* d = fwd ? a.base[nxt] + a.off_R + (t + 1) * slot + cst(c) * es : nullptr;
       if (len > 0) copy_slab_fwd<E>(out + at(b, c), d, a.base[r] + a.off_R + t * slot + cst(c) * es, len);
       if (fwd) publish_flags([&](int) { return ag_flag(nxt, t + 1, c); }, 1, epoch, rel);
@@ -1034,6 +1035,8 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   a.scale = scale;
   a.rdelay_rank = c0.rdelay_rank_;
   a.rdelay = c0.rdelay_us_ > 0 ? static_cast<uint64_t>(c0.rdelay_us_ * 100.0) : 0;  // 100 MHz ticks
+  a.fdelay_rank = c0.fdelay_rank_;
+  a.fdelay = c0.fdelay_us_ > 0 ? static_cast<uint64_t>(c0.fdelay_us_ * 100.0) : 0;
   a.noguard = c0.noguard_ ? 1 : 0;
   a.dynamic = c0.dynamic_ ? 1 : 0;
   a.ring_hop_rows = c0.ring_hop_rows_ ? 1 : 0;

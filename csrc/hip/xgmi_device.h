@@ -79,6 +79,11 @@ struct CommArgs {
   // reads what peers pushed - holds a slow reader inside its launch (slot-reuse tests)
   uint64_t rdelay;
   int rdelay_rank;
+  // test knob (XgmiComm::set_forward_delay): ticks rank `fdelay_rank` idles before the ring's
+  // LAST all-gather forward (its late flag then races the next kernel's flags - the flag
+  // ownership test, tests/test_comm_gpu.py)
+  uint64_t fdelay;
+  int fdelay_rank;
   int noguard;  // MXAR_SLOT_GUARD=0: skip entry_guard (A/B of its cost and negative control only)
   int dynamic;  // two-shot: workgroups take reduce / gather units from a counter (ctl[8], ctl[9])
   int ring_hop_rows;  // study only (MXAR_RING_FLAGS=hop): the pre-fix ring flag layout, row = hop index
@@ -404,6 +409,14 @@ __device__ __forceinline__ void entry_guard(const CommArgs& a, const uint32_t* c
   }
   // write-after-read: the pushes below issue only after the poll returned - no acquire
   __syncthreads();
+}
+
+// Flag-ownership test knob: rank `fdelay_rank` idles before the ring's last forward.
+__device__ __forceinline__ void forward_delay(const CommArgs& a, int r) {
+  if (a.fdelay && r == a.fdelay_rank) {
+    const uint64_t until = wall_ticks() + a.fdelay;
+    while (wall_ticks() < until) __builtin_amdgcn_s_sleep(8);
+  }
 }
 
 // Slot-reuse test knob: rank `rdelay_rank` idles before its slab reads (one scalar compare).

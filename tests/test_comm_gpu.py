@@ -526,3 +526,79 @@ def test_multiprocess_link_probes():
     assert not bad, bad
     info = next(r[3] for r in res if r[0] == 0)
     print("link probes:", info["single_GBps_min_med_max"], info["all_GBps"], info["flag_us"])
+
+
+def _flag_owner_worker(rank, world, port, results, env=None):
+    """Flag ownership, deterministically (verdict r4 #8): rank 2 of 3 holds its ring's LAST
+    all-gather forward (the flag into rank 0's slab) for 3 ms. Rank 1 needs nothing more from
+    rank 2, finishes the ring and starts an all_gather, whose flag into rank 0 is, in the
+    round-3 layout (MXAR_RING_FLAGS=hop: ring flag row = hop index 1), the SAME word as rank 2's
+    late ring flag - rank 0 then takes rank 1's newer epoch for rank 2's data (stale ring
+    output), or rank 2's late store overwrites rank 1's newer epoch (the all_gather times out).
+    In the shipped layout every flag word has one writer and both results are exact."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0", **(env or {}))
+    import datetime
+
+    import torch.distributed as dist
+
+    from akka_allreduce_1_amd.parallel import XgmiCommunicator
+
+    torch.cuda.set_device(0)
+    ok, msg = True, ""
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    except Exception as e:  # noqa: BLE001
+        results.put((rank, False, f"rendezvous: {e!r}"))
+        return
+    try:
+        comm = XgmiCommunicator(device=0, slot_bytes=1 << 20, grid=8, timeout_s=4.0)
+        comm.native.set_forward_delay(2, 3000.0)
+        n = 8192 * world
+        m = n // world
+        for it in range(4):
+            xs = [fill_uniform(torch.empty(n, device=DEV), seed=300 * it + k) for k in range(world)]
+            y = comm.allreduce(xs[rank], algo="ring")
+            comm.check()
+            err = (y - _ref(xs)).abs().max().item()
+            if err > 1e-5:
+                ok, msg = False, f"iteration {it} ring rank {rank}: err {err}"
+                break
+            y2 = comm.all_gather(xs[rank][:m].clone())
+            comm.check()
+            err = (y2 - torch.cat([x[:m] for x in xs])).abs().max().item()
+            if err > 1e-6:
+                ok, msg = False, f"iteration {it} all_gather rank {rank}: err {err}"
+                break
+        comm.native.set_forward_delay(-1, 0.0)
+        comm.barrier()
+        comm.check()
+    except Exception as e:  # report, never hang the parent
+        ok, msg = False, repr(e)[:300]
+    results.put((rank, ok, msg))
+    dist.destroy_process_group()
+
+
+def _run_flag_owner(env=None):
+    from akka_allreduce_1_amd.parallel import free_port
+
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_flag_owner_worker, args=(r, world, port, q, env)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = []
+    try:
+        res = [q.get(timeout=150) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    return [r for r in res if not r[1]]
+
+
+def test_ring_flag_ownership_late_forward():
+    bad = _run_flag_owner()
+    assert not bad, bad

@@ -7,6 +7,9 @@ must FAIL, or the test is not testing it.
                  words had two writers (the ring's predecessor and another kernel's owner)
   no_guard       MXAR_SLOT_GUARD=0 - no entry guard: a fast rank's next launch may push into
                  slots a slow reader has not read yet
+  late_forward   test_ring_flag_ownership_late_forward (rank 2's last ring forward held 3 ms,
+                 rank 1's all_gather flag on the same word in the hop layout): protected and
+                 with MXAR_RING_FLAGS=hop - the deterministic control of the flag ownership
 
 Each case prints one JSON line {case, world, seq, failed_ranks, first_failure}; the
 protected runs (no env) are printed too, as the positive side of the A/B.
@@ -24,7 +27,7 @@ sys.path.insert(0, ROOT)
 
 
 def main() -> None:
-    from tests.test_comm_gpu import _run_slow_reader
+    from tests.test_comm_gpu import _run_flag_owner, _run_slow_reader
 
     cases = [
         ("protected", {}, 3, 2, "ring"),
@@ -34,6 +37,17 @@ def main() -> None:
         ("no_guard", {"MXAR_SLOT_GUARD": "0", "MXAR_STUDY": "1"}, 3, 2, "ring"),
     ]
     only = set(sys.argv[1:])
+    for name, env in (("late_forward_protected", {}),
+                      ("late_forward_ring_hop_rows", {"MXAR_RING_FLAGS": "hop", "MXAR_STUDY": "1"}),
+                      ("late_forward_no_guard", {"MXAR_SLOT_GUARD": "0", "MXAR_STUDY": "1"}),
+                      ("late_forward_hop_rows_no_guard", {"MXAR_RING_FLAGS": "hop", "MXAR_SLOT_GUARD": "0",
+                                                          "MXAR_STUDY": "1"})):
+        if only and name not in only:
+            continue
+        print(f"[negative_controls] {name} ...", file=sys.stderr, flush=True)
+        bad = _run_flag_owner(env)
+        print(json.dumps({"case": name, "env": env, "world": 3, "failed_ranks": len(bad),
+                          "first_failure": bad[0][2][:300] if bad else None}), flush=True)
     for name, env, world, slow, seq in cases:
         if only and name not in only:
             continue
