@@ -60,12 +60,14 @@ def host_iota_source(n: int, offset: float = 0.0) -> Callable:
 class PlaneJob:
     """Master + P plane workers in one process (threaded actor system).
 
-    Workers sharing a GPU run their round kernels concurrently on separate high-priority
-    streams. HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by
-    default), and a kernel queued behind a peer's spinning round kernel in the same queue
-    would never start: each plane therefore probes its stream against the other planes'
-    and the default stream when it is created and takes one on a queue of its own
-    (csrc/hip/xgmi_plane.cc, independent_plane_stream) - no environment setting needed."""
+    Workers sharing a GPU form a plane group (csrc/hip/xgmi_plane.cc PlaneGroup): ONE
+    resident kernel runs every round of every one of them, a slice of workgroups per worker
+    fed from that worker's own door ring (xgmi_threshold.hip
+    threshold_group_resident_kernel). Each worker's rounds still run on their own schedule (a
+    straggler's slice lags while the others run ahead), and no round can wait in a hardware
+    queue behind a co-located peer's spinning round, so any number of workers (<= 16 per GPU)
+    runs at the boxes' GPU_MAX_HW_QUEUES = 4 - the reference hosts any number of worker
+    actors in one ActorSystem (AllreduceSpec.scala:746-755)."""
 
     def __init__(self, P: int, data_size: int, *, max_chunk_size: int, th_allreduce: float = 1.0,
                  th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 1, max_round: int = 10,
@@ -175,7 +177,10 @@ class PlaneJob:
         t0 = time.perf_counter()
         self.start()
         if not self.finished.wait(timeout):
-            raise TimeoutError(f"plane job did not finish in {timeout} s: {self.state()}")
+            planes = [p.debug_state() for p in self.planes if hasattr(p, "debug_state")]
+            msg = f"plane job did not finish in {timeout} s: {self.state()} planes: {planes}"
+            print(msg, file=__import__("sys").stderr, flush=True)  # before any teardown that may block
+            raise TimeoutError(msg)
         for p in self.planes:  # the last round's sinks run after the master's last barrier
             p.drain()
         self.system.await_idle(10.0)
@@ -307,7 +312,8 @@ def distributed_plane_job(n: int, source, *, max_chunk_size: int, dtype: torch.d
     system.await_idle(5.0)
     stamps = (client_stamps if external_client else system.master_round_stamps(master)) if master is not None else []
     out = {"ok": bool(ok[0]), "stamps": stamps, "state": system.plane_worker_state(worker),
-           "plane": {"launches": plane.stats.launches, "chunk_elems": plane.chunk_elems, "chunks": plane.chunks},
+           "plane": {"launches": plane.stats.launches, "chunk_elems": plane.chunk_elems, "chunks": plane.chunks,
+                     "resident_rounds": plane.stats.resident_rounds},
            "last": last.last() if last is not None else None}
     dist.barrier()
     node.leave()

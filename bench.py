@@ -51,8 +51,8 @@ if "--share-device" in sys.argv:
     # co-resident (measured: 46.7 ms vs 3.1 ms per 256 MiB step at 8 ranks). One queue per
     # process keeps every rank's kernel on the device at once. Set before HIP initialises.
     os.environ["GPU_MAX_HW_QUEUES"] = "1"
-# (The N = 1 protocol section hosts two plane workers in this process: each plane probes its
-# stream onto a hardware queue of its own, csrc/hip/xgmi_plane.cc - no queue-count setting.)
+# (The N = 1 protocol section hosts two plane workers in this process: their rounds share one
+# group kernel, csrc/hip/xgmi_plane.cc PlaneGroup - no queue-count setting.)
 
 # Library banners (RCCL's version block, gloo's "connected to N peer ranks") are written to
 # fd 1 from native code; keep stdout for the ONE result line: fd 1 -> stderr for the whole

@@ -244,9 +244,14 @@ void bind_hip(py::module_& m) {
       .def_readonly("resident_rounds", &XgmiPlaneStats::resident_rounds)
       .def_readonly("resident_launches", &XgmiPlaneStats::resident_launches)
       .def_readonly("resident_parks", &XgmiPlaneStats::resident_parks)
+      .def_readonly("group_rounds", &XgmiPlaneStats::group_rounds)
+      .def_readonly("group_launches", &XgmiPlaneStats::group_launches)
+      .def_readonly("group_size", &XgmiPlaneStats::group_size)
       .def_readonly("peer_maps", &XgmiPlaneStats::peer_maps);
   py::class_<XgmiRoundPlane, RoundPlane, std::shared_ptr<XgmiRoundPlane>>(h, "XgmiRoundPlane")
       .def_property_readonly("stats", &XgmiRoundPlane::stats)
+      .def("debug_state", &XgmiRoundPlane::debug_state,
+           "diagnostics: door / resident / group words, the device go word and control words (JSON)")
       .def_property_readonly("arena_bytes", &XgmiRoundPlane::arena_bytes)
       .def_property_readonly("chunk_elems", &XgmiRoundPlane::chunk_elems)
       .def_property_readonly("block_elems", &XgmiRoundPlane::block_elems)

@@ -89,6 +89,19 @@ enum : int32_t { kResRound = 0, kResCold = 1, kResStop = 2 };
 // last entry it consumed (its door slot may be reused)
 enum : uint32_t { kResRunning = 0, kResExiting = 1, kResExited = 2 };
 
+// Group resident rounds (xgmi_threshold.hip threshold_group_resident_kernel; xgmi_plane.cc
+// PlaneGroup): the co-located workers of one job share ONE resident kernel, a slice of
+// workgroups per worker, each fed from that worker's own door ring by a dispatcher wave.
+struct GroupResidentMember {
+  const ResidentDoor* door;  // the worker's pinned door ring (device-visible address)
+  uint32_t* hstate;          // its pinned words: [1] the last entry consumed
+  uint64_t* dm;              // its device words: [0] go, [2..9] the entry handed to its slice
+  const uint32_t* hforce;    // its pinned force / abort words
+  const uint32_t* habort;
+  uint32_t seq0;             // the first entry this launch takes
+  int rank;
+};
+
 // The launch-size grid rule (XgmiComm::launch_grid; profiles/round4/README.md section 9):
 // workgroups for a launch moving `bytes` of input over all its ranks at device grid `grid`.
 // Two-shot style: one per 64 KiB, 64..`cap`, the full grid from `full_at`; one-shot: every
@@ -233,6 +246,13 @@ class XgmiComm {
                        uint32_t seq, uint32_t gen, uint64_t idle_ticks, hipStream_t stream);
   void round(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, float th_reduce, float th_complete,
              int32_t* counts, const RoundSpec& spec, float scale = 1.f);
+  // A plane group's resident kernel (xgmi_threshold.hip threshold_group_resident_kernel): ONE
+  // launch serves the co-located workers `comms` (their plan_resident plans, one geometry),
+  // members[k] = worker k's door, words and first entry; gstate: the group's pinned state
+  // word, gdm: 8 device words of the group.
+  static void launch_group_resident(const std::vector<XgmiComm*>& comms, const std::vector<const ResidentPlan*>& plans,
+                                    const std::vector<GroupResidentMember>& members, uint32_t* gstate, uint64_t* gdm,
+                                    uint32_t gen, uint64_t idle_ticks, hipStream_t stream);
   // Workgroups a round launch of `nch` chunks per block uses (counts / geometry checks).
   int round_grid(int nch) const;
   // Chunks per block the threshold kernel uses for n elements (size of `counts` = P * this).

@@ -1473,6 +1473,57 @@ void XgmiComm::round(const void* in, void* out, int64_t n, DType dt, hipStream_t
   run_threshold({this}, {in}, {out}, n, dt, stream, th_reduce, th_complete, counts, scale, false, &spec);
 }
 
+// Two rounds of co-located workers may share a launch: the same geometry, thresholds and slabs.
+static bool same_round_shape(const CommArgs& b, const CommArgs& a0) {
+  bool same = b.n == a0.n && b.block == a0.block && b.chunk == a0.chunk && b.subchunk == a0.subchunk &&
+              b.nch == a0.nch && b.sub == a0.sub && b.sgroup == a0.sgroup && b.P == a0.P && b.rows == a0.rows &&
+              b.ll == a0.ll && b.ll_cstride == a0.ll_cstride && b.full == a0.full && b.min_reduce == a0.min_reduce &&
+              b.min_complete == a0.min_complete && b.maxch == a0.maxch && b.off_S == a0.off_S && b.off_R == a0.off_R &&
+              b.slot_bytes == a0.slot_bytes && b.order_ref == a0.order_ref && b.fence == a0.fence &&
+              b.gate_shortcut == a0.gate_shortcut && b.scale == a0.scale && b.rescale == a0.rescale &&
+              b.timeout == a0.timeout;
+  for (int k = 0; same && k < a0.P; ++k) same = b.base[k] == a0.base[k];
+  return same;
+}
+
+void XgmiComm::launch_group_resident(const std::vector<XgmiComm*>& comms, const std::vector<const ResidentPlan*>& plans,
+                                     const std::vector<GroupResidentMember>& members, uint32_t* gstate, uint64_t* gdm,
+                                     uint32_t gen, uint64_t idle_ticks, hipStream_t stream) {
+  const int Y = static_cast<int>(plans.size());
+  if (Y < 1 || Y > kMaxRanks || comms.size() != plans.size() || members.size() != plans.size())
+    throw std::invalid_argument("launch_group_resident: one communicator, plan and member per worker, at most " +
+                                std::to_string(kMaxRanks));
+  for (const ResidentPlan* p : plans)
+    if (p == nullptr || !p->args || p->grid <= 0) throw std::invalid_argument("launch_group_resident: no resident plan");
+  const ResidentPlan& p0 = *plans[0];
+  const CommArgs& a0 = *static_cast<const CommArgs*>(p0.args.get());
+  CommArgs a = a0;
+  GroupResArgs g;
+  std::memset(&g, 0, sizeof(g));
+  for (int y = 0; y < Y; ++y) {
+    const ResidentPlan& p = *plans[y];
+    const CommArgs& b = *static_cast<const CommArgs*>(p.args.get());
+    if (p.grid != p0.grid || p.dt != p0.dt || p.n != p0.n || comms[y]->device_ != comms[0]->device_ ||
+        !same_round_shape(b, a0))
+      throw std::invalid_argument("launch_group_resident: the workers' rounds must share geometry and slabs");
+    a.ctl[y] = comms[y]->ctl_;
+    g.m[y] = members[y];
+    g.m[y].rank = comms[y]->rank_;
+  }
+  a.stamps = nullptr;
+  a.delay_rank = -1;
+  g.gstate = gstate;
+  g.gdm = gdm;
+  g.idle = idle_ticks;
+  g.gen = gen;
+  g.Y = Y;
+  hip_check(hipSetDevice(comms[0]->device_), "hipSetDevice");
+  order_group(comms, stream);
+  launch_threshold_group_resident(a, g, p0.grid, stream, p0.dt);
+  hip_check(hipGetLastError(), "group resident threshold launch");
+  for (XgmiComm* c : comms) ++c->stats_.launches;
+}
+
 void XgmiComm::allreduce_threshold(const void* in, void* out, int64_t n, DType dt, hipStream_t stream,
                                    float th_reduce, float th_complete, int32_t* counts, float scale, bool rescale) {
   run_threshold({this}, {in}, {out}, n, dt, stream, th_reduce, th_complete, counts, scale, rescale);

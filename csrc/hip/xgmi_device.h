@@ -103,6 +103,18 @@ struct CommArgs {
   uint32_t* split_early;
 };
 
+// A plane group's resident kernel (threshold_group_resident_kernel): y = 0 is the dispatcher
+// row, y = 1 + k worker k's slice.
+struct GroupResArgs {
+  GroupResidentMember m[kMaxRanks];
+  uint32_t* gstate;  // pinned: [0] kResRunning / kResExiting / kResExited (the group's kernel)
+  uint64_t* gdm;     // device: [0] the dispatcher's heartbeat (100 MHz ticks)
+  uint64_t idle;     // ticks without a round before the kernel leaves
+  uint32_t gen;      // launch generation (the go words of a relaunched kernel differ)
+  int Y;             // workers
+};
+static_assert(sizeof(CommArgs) + sizeof(GroupResArgs) <= 4096, "threshold_group_resident_kernel arguments exceed 4 KiB");
+
 // Phase stamps of one workgroup (100 MHz s_memrealtime ticks): [0] start, [1] scatter done,
 // [2] ticks spent waiting in the reduce phase, [3] reduce phase done, [4] ticks spent
 // waiting in the gather phase, [5] end, [6] units reduced, [7] units gathered. Thread 0
@@ -456,6 +468,8 @@ __device__ __forceinline__ void finish_launch_done(const CommArgs& a, uint32_t* 
 
 // Host entry of the threshold kernel (xgmi_threshold.hip).
 void launch_threshold(const CommArgs& a, dim3 grid, hipStream_t s, DType dt);
+// A plane group's resident kernel: dim3(grid, workers + 1) (xgmi_threshold.hip).
+void launch_threshold_group_resident(const CommArgs& a, const GroupResArgs& g, int grid, hipStream_t s, DType dt);
 // Resident rounds (xgmi_threshold.hip; XgmiComm::launch_resident).
 void launch_threshold_resident(const CommArgs& a, int grid, hipStream_t s, DType dt, const ResidentDoor* door,
                                uint32_t* hstate, uint32_t* dm, uint32_t seq, uint32_t gen, uint64_t idle_ticks);

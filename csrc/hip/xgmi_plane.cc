@@ -27,86 +27,35 @@ namespace {
 // in-process peers (several workers of one process on one GPU) are found here.
 std::mutex g_arena_mu;
 
-// The process's live plane streams per device. A new plane's stream must sit on a hardware
-// queue of its own: co-located planes' round kernels spin waiting for each other, and a
-// kernel queued behind a peer's spinning kernel in a shared queue waits out its deadline.
-// HIP deals streams onto GPU_MAX_HW_QUEUES queues (4 on the boxes) round-robin, so the
-// candidate is probed against every idle live plane stream (streams_independent,
-// kernels.hip) and replaced until one is independent of all of them; the high priority
-// keeps plane streams off the default stream's queue.
-std::mutex g_stream_mu;
-std::vector<std::pair<int, hipStream_t>> g_plane_streams;
+// Resident kernel generations, process-wide: a plane's device words (go = gen << 32 | seq)
+// serve its own resident kernels and its group's in turn, and a kernel must never take a go
+// that an earlier kernel of either kind wrote for the same entry (its STOP at an idle exit).
+std::atomic<uint32_t> g_res_gen{0};
 
-hipStream_t independent_plane_stream(int device, int priority, bool* probed_ok) {
-  std::lock_guard<std::mutex> g(g_stream_mu);
-  if (const char* q = std::getenv("GPU_MAX_HW_QUEUES"); q != nullptr && std::atoi(q) == 1) {
-    // one queue per process (the multi-process one-GPU rehearsal, one plane per process):
-    // nothing to choose from
-    hipStream_t s = nullptr;
-    hip_check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority), "hipStreamCreate(plane)");
-    g_plane_streams.emplace_back(device, s);
-    *probed_ok = false;
-    return s;
+// Pinned state words of plane groups (64 B each) from blocks that are never freed: freeing
+// pinned memory may synchronise the device while a co-located kernel spins.
+std::mutex g_gword_mu;
+std::vector<uint32_t*> g_gword_free;
+
+uint32_t* take_group_word() {
+  std::lock_guard<std::mutex> g(g_gword_mu);
+  if (g_gword_free.empty()) {
+    uint32_t* blk = nullptr;
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&blk), 64 * 256, hipHostMallocCoherent | hipHostMallocMapped),
+              "hipHostMalloc(group words)");
+    std::memset(blk, 0, 64 * 256);
+    for (int i = 255; i >= 0; --i) g_gword_free.push_back(blk + 16 * i);
   }
-  std::vector<hipStream_t> rejected;  // kept alive while probing: HIP would deal the same queue again
-  // Only IDLE plane streams are probed: a busy one may hold a round kernel that waits for
-  // this very worker (a replacement joining a running job), and a probe queued behind it
-  // would wait out that round's deadline. A busy one (a round in flight, or a resident kernel
-  // in its idle spell) is given up to 20 ms to go idle, so a job whose rounds leave gaps is
-  // probed too.
-  std::vector<hipStream_t> idle;
-  for (const auto& e : g_plane_streams) {
-    if (e.first != device) continue;
-    const auto t0 = std::chrono::steady_clock::now();
-    hipError_t q = hipStreamQuery(e.second);
-    while (q == hipErrorNotReady && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(20)) {
-      std::this_thread::sleep_for(std::chrono::microseconds(100));
-      q = hipStreamQuery(e.second);
-    }
-    (void)hipGetLastError();
-    if (q == hipSuccess) idle.push_back(e.second);
-  }
-  hipStream_t s = nullptr;
-  bool ok = false;
-  // HIP deals new streams onto its queues by its own policy (long-lived streams of other
-  // users weigh in), so a queue can take many candidates to come round: up to 64
-  int tried = 0;
-  for (int attempt = 0; attempt < 64 && !ok; ++attempt, ++tried) {
-    hip_check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority), "hipStreamCreate(plane)");
-    ok = true;
-    for (hipStream_t p : idle)
-      if (ok) ok = streams_independent(p, s, 20.0) && streams_independent(s, p, 20.0);
-    if (!ok) rejected.push_back(s);
-  }
-  for (hipStream_t r : rejected)
-    if (r != s || !ok) (void)hipStreamDestroy(r);
-  if (!ok) {
-    // No independent queue left: a round kernel of this plane would queue behind a co-located
-    // plane's round kernel that waits for it, and every round would wait out its deadline. Say
-    // so now rather than hang (MXAR_PLANE_SHARED_QUEUE_OK=1 keeps the last candidate anyway).
-    const char* e = study_env("MXAR_PLANE_SHARED_QUEUE_OK");
-    if (e == nullptr || std::atoi(e) == 0) {
-      throw std::runtime_error(
-          "xgmi plane: no hardware queue independent of the " + std::to_string(g_plane_streams.size()) +
-          " other plane streams on device " + std::to_string(device) + " after " + std::to_string(tried) +
-          " candidates: co-located plane workers need one queue each (GPU_MAX_HW_QUEUES; or one process per "
-          "worker)");
-    }
-    hip_check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority), "hipStreamCreate(plane)");
-    std::fprintf(stderr, "[mxar] WARNING: plane stream shares a hardware queue with another plane (device %d)\n",
-                 device);
-  }
-  g_plane_streams.emplace_back(device, s);
-  *probed_ok = ok;
-  return s;
+  uint32_t* w = g_gword_free.back();
+  g_gword_free.pop_back();
+  return w;
 }
 
-void forget_plane_stream(hipStream_t s) {
-  std::lock_guard<std::mutex> g(g_stream_mu);
-  g_plane_streams.erase(std::remove_if(g_plane_streams.begin(), g_plane_streams.end(),
-                                       [&](const std::pair<int, hipStream_t>& e) { return e.second == s; }),
-                        g_plane_streams.end());
+void give_group_word(uint32_t* w) {
+  std::lock_guard<std::mutex> g(g_gword_mu);
+  g_gword_free.push_back(w);
 }
+
 std::map<uint64_t, char*> g_arenas;
 
 std::string to_hex(const std::string& b) {
@@ -158,6 +107,125 @@ Desc parse_desc(const std::string& s) {
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+}  // namespace
+
+// The co-located workers of one membership (this process, this GPU, one InitWorkers epoch):
+// ONE resident kernel runs all their rounds, worker k's on its own slice of workgroups, fed
+// from k's door ring (xgmi_threshold.hip threshold_group_resident_kernel). Found by key
+// (device, the workers' arena ids in rank order, the membership epoch), so every worker of
+// the membership joins the same group and a new membership forms a new one. The kernel runs
+// while any worker has rounds; it leaves after an idle spell (the dispatcher decides for the
+// whole group) and the next post launches it again. It is launched only once every worker has
+// joined (its slices need every worker's words) - except for rounds being abandoned.
+struct PlaneGroup {
+  enum : int { kPending = 0, kJoined = 1, kLeft = 2 };
+  std::string key;
+  int device = 0;
+  std::vector<int> state;                 // per worker
+  std::vector<XgmiRoundPlane*> planes;    // joined workers
+  std::vector<char> in_kernel;            // served by the kernel launched last
+  uint32_t* gword = nullptr;              // pinned: [0] the kernel's state (kResRunning / ...)
+  uint32_t* gword_dev = nullptr;
+  uint64_t* gdm = nullptr;                // device words: [0] the dispatcher's heartbeat
+  hipStream_t stream = nullptr;
+  bool launched = false;                  // a kernel was launched (gword[0] says whether it left)
+  std::mutex mu;
+
+  PlaneGroup(std::string k, int dev, int workers, bool high_priority) : key(std::move(k)), device(dev) {
+    state.assign(static_cast<size_t>(workers), kPending);
+    planes.assign(static_cast<size_t>(workers), nullptr);
+    in_kernel.assign(static_cast<size_t>(workers), 0);
+    hip_check(hipSetDevice(device), "hipSetDevice");
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    hip_check(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, high_priority ? hi : lo),
+              "hipStreamCreate(plane group)");
+    gword = take_group_word();
+    reinterpret_cast<volatile uint32_t*>(gword)[0] = kResExited;
+    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&gword_dev), gword, 0), "hipHostGetDevicePointer(group)");
+    hip_check(hipMallocAsync(reinterpret_cast<void**>(&gdm), 64, stream), "hipMallocAsync(group words)");
+    hip_check(hipMemsetAsync(gdm, 0, 64, stream), "hipMemsetAsync(group words)");
+    hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize(group)");
+  }
+  ~PlaneGroup() {
+    // every worker left: the dispatcher saw each one's STOP (or no kernel ran)
+    const volatile uint32_t* g = gword;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (launched && g[0] != kResExited && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10))
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    (void)hipSetDevice(device);
+    (void)hipFreeAsync(gdm, stream);
+    (void)hipStreamDestroy(stream);
+    if (!launched || g[0] == kResExited) give_group_word(gword);  // else leaked: a kernel may still write it
+  }
+  volatile uint32_t* state_word() const { return gword; }
+  bool kernel_left() const { return !launched || reinterpret_cast<volatile uint32_t*>(gword)[0] == kResExited; }
+
+  // Launches a kernel for every joined worker (mu held; no kernel running).
+  void launch_locked(XgmiRoundPlane* by) {
+    std::vector<XgmiComm*> comms;
+    std::vector<const XgmiComm::ResidentPlan*> plans;
+    std::vector<GroupResidentMember> mem;
+    double idle_us = 1000.0;
+    for (size_t k = 0; k < planes.size(); ++k) {
+      in_kernel[k] = 0;
+      if (state[k] != kJoined) continue;
+      XgmiRoundPlane* p = planes[k];
+      comms.push_back(p->comm_.get());
+      plans.push_back(&p->gplan_);
+      GroupResidentMember m{};
+      m.door = p->door_dev_;
+      m.hstate = p->rstate_dev_;
+      m.dm = reinterpret_cast<uint64_t*>(p->rdm_);
+      m.hforce = p->hforce_dev_;
+      m.habort = p->hforce_dev_ + 1;
+      m.seq0 = p->rstate_[1] + 1u;  // its first entry not consumed yet
+      mem.push_back(m);
+      in_kernel[k] = 1;
+      idle_us = p->o_.resident_idle_us;
+    }
+    if (comms.empty()) return;
+    reinterpret_cast<volatile uint32_t*>(gword)[0] = kResRunning;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    try {
+      XgmiComm::launch_group_resident(comms, plans, mem, gword_dev, gdm, g_res_gen.fetch_add(1) + 1u,
+                                      static_cast<uint64_t>(idle_us * 100.0), stream);
+    } catch (...) {
+      reinterpret_cast<volatile uint32_t*>(gword)[0] = kResExited;
+      std::fill(in_kernel.begin(), in_kernel.end(), 0);
+      throw;
+    }
+    launched = true;
+    by->st_.group_launches++;
+  }
+
+  // Worker k posted an entry: make sure a kernel takes it. A kernel launched before k joined
+  // does not serve k: wait for it to leave (bounded), then launch one that does. With workers
+  // still to join, the last of them launches it - unless `partial` (k's rounds are being
+  // abandoned: they must run now, without the missing worker).
+  void ensure(XgmiRoundPlane* by, int k, bool partial, double timeout_s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      {
+        std::lock_guard<std::mutex> g(mu);
+        if (kernel_left()) {
+          const bool waiting = std::find(state.begin(), state.end(), kPending) != state.end();
+          if (waiting && !partial) return;
+          launch_locked(by);
+          return;
+        }
+        if (in_kernel[static_cast<size_t>(k)]) return;  // running (or deciding to leave: it re-reads the doors)
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::duration<double>(2 * timeout_s + 5))
+        throw ProtocolError("xgmi plane group: a kernel without this worker never left");
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  }
+};
+
+namespace {
+std::mutex g_group_mu;
+std::map<std::string, std::weak_ptr<PlaneGroup>> g_groups;
 }  // namespace
 
 XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
@@ -248,15 +316,12 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   // plane's persistent round kernels never sit in the same hardware queue as the default
   // stream (a marker or kernel queued behind a spinning round in a shared queue would wait
   // for that round - a deadlock when the round waits for a peer fed by that work; seen in
-  // a kernel trace with two workers in one process).
+  // a kernel trace with two workers in one process). Co-located workers of one job do not
+  // need queues of their own: their rounds share one group kernel (PlaneGroup).
   int lo = 0, hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-  // Many planes in one process (workers sharing a GPU) may instead want normal priority:
-  // normal-priority streams are dealt round-robin over GPU_MAX_HW_QUEUES queues.
-  bool independent = false;
-  try {
-    stream_ = independent_plane_stream(o_.device, o_.high_priority ? hi : lo, &independent);
-  } catch (...) {  // no queue for this plane: release what the constructor allocated so far
+  const hipError_t se = hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, o_.high_priority ? hi : lo);
+  if (se != hipSuccess) {  // release what the constructor allocated so far
     for (hipEvent_t e : events_) (void)hipEventDestroy(e);
     if (rel_ev_) (void)hipEventDestroy(rel_ev_);
     (void)hipFree(split_mem_);
@@ -267,7 +332,7 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
     (void)hipHostFree(door_);
     (void)hipHostFree(hforce_);
     (void)hipFree(arena_);
-    throw;
+    hip_check(se, "hipStreamCreate(plane)");
   }
   // keep freed round buffers in the device's default pool instead of returning them to the
   // driver at every synchronisation (the next round reuses them)
@@ -300,6 +365,7 @@ XgmiRoundPlane::~XgmiRoundPlane() {
   try {
     abort(0x7fffffff);
     drain();
+    leave_group();
     park_resident();
   } catch (...) {
   }
@@ -341,10 +407,7 @@ XgmiRoundPlane::~XgmiRoundPlane() {
   if (hforce_) (void)hipHostFree(hforce_);
   if (door_) (void)hipHostFree(door_);
   if (rdm_) (void)hipFree(rdm_);
-  if (stream_) {
-    forget_plane_stream(stream_);
-    (void)hipStreamDestroy(stream_);
-  }
+  if (stream_) (void)hipStreamDestroy(stream_);
   if (alloc_stream_) (void)hipStreamDestroy(alloc_stream_);
   if (arena_) (void)hipFree(arena_);
 }
@@ -453,7 +516,7 @@ void XgmiRoundPlane::reset_pool(size_t bytes) {
   // 256 MiB buffer (profiles/round2/sync_probe.md)
   // (resident-size rounds - every round then draws from this pool, see resident_out - keep
   // more: a sink holding a few outputs must not push rounds off the resident kernel)
-  const bool resident_size = o_.resident_max > 0 && static_cast<int64_t>(bytes) <= o_.resident_max;
+  const bool resident_size = grouped_ || (o_.resident_max > 0 && static_cast<int64_t>(bytes) <= o_.resident_max);
   std::vector<void*> warm(resident_size ? 8 : 3, nullptr);
   for (void*& w : warm) hip_check(hipMallocAsync(&w, bytes, stream_), "hipMallocAsync(pool)");
   std::lock_guard<std::mutex> g(rel_->mu);
@@ -536,6 +599,7 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
     abort(last_round_);
     drain();
   }
+  leave_group();
   park_resident();  // the stream work below must not queue behind it
   rplan_tried_ = false;
   rplan_ = XgmiComm::ResidentPlan();
@@ -626,6 +690,7 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
   // Grow the stream-ordered pool now for the rounds' output buffers (an output is released
   // one launch after its sink dropped it, so ~3 are live at once): growing it in the round
   // path costs ~8 ms per 256 MiB buffer (profiles/round2/sync_probe.md) - paid here instead.
+  grouped_ = colocated(cfg).size() > 1;  // every round then draws its output from the pool
   reset_pool(static_cast<size_t>(cfg.dataSize) * static_cast<size_t>(dtype_size(o_.dtype)));
   comm_->publish_progress(cfg.roundBase, stream_);
   hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize(publish progress)");
@@ -641,10 +706,250 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
   configured_ = true;
   last_round_ = cfg.startRound - 1;
   err_seen_ = 0;
+  if (grouped_) join_group(cfg);
   MXAR_LOG(INFO, "plane", "xgmi plane: worker " << cfg.id << " of " << P << ", block " << block_ << ", chunk "
                                                 << chunk_ << " x " << nch_ << " (" << nch_ref_
                                                 << " reference chunks), rows " << cfg.maxLag + 1
                                                 << ", round epochs from " << cfg.roundBase + 1);
+}
+
+std::vector<std::pair<int, uint64_t>> XgmiRoundPlane::colocated(const PlaneConfig& cfg) const {
+  std::vector<std::pair<int, uint64_t>> v;
+  for (int k = 0; k < cfg.peers; ++k) {
+    auto it = cfg.descriptors.find(k);
+    if (it == cfg.descriptors.end() || it->second.empty()) continue;
+    const Desc d = parse_desc(it->second);
+    if (d.pid == static_cast<long>(getpid()) && d.device == o_.device) v.emplace_back(k, d.id);
+  }
+  return v;
+}
+
+void XgmiRoundPlane::join_group(const PlaneConfig& cfg) {
+  const auto mates = colocated(cfg);
+  const int Y = static_cast<int>(mates.size());
+  if (Y > kMaxRanks)
+    throw ProtocolError("xgmi plane: at most " + std::to_string(kMaxRanks) + " workers of a job per process and GPU");
+  if (const char* q = std::getenv("GPU_MAX_HW_QUEUES"); q != nullptr && std::atoi(q) == 1)
+    throw ProtocolError("xgmi plane: co-located workers need GPU_MAX_HW_QUEUES >= 2 (their group kernel holds a "
+                        "hardware queue while the inputs are produced on another)");
+  // the group kernel's geometry: round()'s for this membership, every chunk one workgroup's
+  XgmiComm::RoundSpec spec;
+  spec.block = block_;
+  spec.chunk = chunk_;
+  spec.order_ref = o_.order_ref;
+  spec.host_force = hforce_dev_;
+  spec.host_abort = hforce_dev_ + 1;
+  gplan_ = comm_->plan_resident(cfg.dataSize, o_.dtype, cfg.thReduce, cfg.thComplete, spec, 1 << 20);
+  if (gplan_.grid <= 0) throw ProtocolError("xgmi plane: this membership's rounds do not fit the group kernel");
+  // every slice's workgroups must be resident at once (they wait for each other's rounds):
+  // two workgroups per CU over the workers, the PlaneJob default (grid = 512 / workers)
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device);
+  if (static_cast<int64_t>(Y) * gplan_.grid > 2 * static_cast<int64_t>(cus))
+    throw ProtocolError("xgmi plane: " + std::to_string(Y) + " co-located workers x " + std::to_string(gplan_.grid) +
+                        " workgroups exceed the " + std::to_string(2 * cus) +
+                        " a group kernel keeps resident: build the planes with grid <= " + std::to_string(2 * cus / Y));
+  std::ostringstream key;
+  key << "dev" << o_.device << " e" << cfg.epoch;
+  int idx = -1;
+  for (int i = 0; i < Y; ++i) {
+    key << ' ' << mates[i].second;
+    if (mates[i].first == cfg.id) idx = i;
+  }
+  if (idx < 0) throw ProtocolError("xgmi plane: this worker is not among its own co-located workers");
+  std::shared_ptr<PlaneGroup> g;
+  {
+    std::lock_guard<std::mutex> lk(g_group_mu);
+    for (auto it = g_groups.begin(); it != g_groups.end();) it = it->second.expired() ? g_groups.erase(it) : std::next(it);
+    auto& w = g_groups[key.str()];
+    g = w.lock();
+    if (!g) {
+      g = std::make_shared<PlaneGroup>(key.str(), o_.device, Y, o_.high_priority);
+      w = g;
+    }
+  }
+  rstate_[1] = res_seq_ - 1u;  // every entry before res_seq_ was taken (or dropped) before
+  std::lock_guard<std::mutex> lk(g->mu);
+  if (g->state[static_cast<size_t>(idx)] != PlaneGroup::kPending)
+    throw ProtocolError("xgmi plane: two workers of one membership claim the same group slot");
+  g->planes[static_cast<size_t>(idx)] = this;
+  g->state[static_cast<size_t>(idx)] = PlaneGroup::kJoined;
+  group_ = g;
+  gidx_ = idx;
+  st_.group_size = Y;
+  // the last worker to join starts the kernel: the others' first rounds may be posted already
+  if (std::find(g->state.begin(), g->state.end(), PlaneGroup::kPending) == g->state.end() && g->kernel_left())
+    g->launch_locked(this);
+}
+
+void XgmiRoundPlane::leave_group() {
+  if (!group_) return;
+  std::shared_ptr<PlaneGroup> g = group_;
+  bool serving = false;
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    serving = g->in_kernel[static_cast<size_t>(gidx_)] != 0 && !g->kernel_left();
+  }
+  if (serving) {
+    // a STOP entry ends this worker's slice; the kernel goes on for the others (or leaves
+    // when this was the last)
+    ResidentDoor e{};
+    e.cmd = kResStop;
+    const uint32_t seq = res_seq_;
+    if (post_door(e, g->state_word())) {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (static_cast<int32_t>(rstate_[1] - seq) < 0 && !g->kernel_left()) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::duration<double>(2 * o_.timeout_s + 5)) {
+          MXAR_LOG(ERROR, "plane", "the group kernel did not take this worker's STOP");
+          break;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+      }
+    }
+  }
+  rstate_[1] = res_seq_ - 1u;  // entries no kernel took are dropped
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->state[static_cast<size_t>(gidx_)] = PlaneGroup::kLeft;
+    g->planes[static_cast<size_t>(gidx_)] = nullptr;
+    g->in_kernel[static_cast<size_t>(gidx_)] = 0;
+  }
+  group_.reset();
+  gidx_ = -1;
+  gplan_ = XgmiComm::ResidentPlan();
+  st_.group_size = 0;
+}
+
+void XgmiRoundPlane::launch_group(int round, const Payload& input, bool cold) {
+  const int64_t n = cfg_.dataSize;
+  const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
+  const int dcode = static_cast<int>(o_.dtype);
+  Rec rec;
+  rec.round = round;
+  rec.epoch = cfg_.epoch;
+  rec.cold = cold;
+  rec.round_epoch = epoch_of(round);
+  const void* in_ptr = nullptr;
+  if (!cold) {
+    if (!input || static_cast<int64_t>(input->size()) != n) throw ProtocolError("xgmi plane: input must hold dataSize elements");
+    auto* dp = dynamic_cast<const DevicePayload*>(input.get());
+    if (dp != nullptr && dp->device() == o_.device && dp->dtype() == dcode) {
+      // no stream orders the group kernel after the producer: the host waits for it (normal-
+      // priority streams: never queued behind the group kernel's high-priority queue)
+      if (dp->ready())
+        hip_check(hipEventSynchronize(static_cast<hipEvent_t>(dp->ready().get())), "hipEventSynchronize(input)");
+      else if (dp->stream() && dp->stream() != stream_)
+        hip_check(hipStreamSynchronize(dp->stream()), "hipStreamSynchronize(input)");
+      in_ptr = dp->bytes();
+      rec.input = input;  // held until the round completed
+    } else {
+      // staged on the side stream (normal priority) and waited for: a host payload, another
+      // device's, or another dtype
+      if (alloc_stream_ == nullptr)
+        hip_check(hipStreamCreateWithFlags(&alloc_stream_, hipStreamNonBlocking), "hipStreamCreate(plane side)");
+      const hipStream_t ss = alloc_stream_;
+      auto side_buf = [&](size_t bytes) {
+        void* p = nullptr;
+        hip_check(hipMallocAsync(&p, std::max<size_t>(bytes, 256), ss), "hipMallocAsync(plane staging)");
+        return std::shared_ptr<void>(p, [ss](void* q) { (void)hipFreeAsync(q, ss); });
+      };
+      void* src = nullptr;
+      DType sdt = DType::F32;
+      std::shared_ptr<void> up;
+      if (dp != nullptr && dp->device() == o_.device) {
+        if (dp->ready()) hip_check(hipStreamWaitEvent(ss, static_cast<hipEvent_t>(dp->ready().get()), 0), "hipStreamWaitEvent");
+        else if (dp->stream()) hip_check(hipStreamSynchronize(dp->stream()), "hipStreamSynchronize(input)");
+        src = const_cast<void*>(dp->bytes());
+        sdt = static_cast<DType>(dp->dtype());
+        rec.input = input;
+      } else {
+        const std::vector<float> h = input->to_host();
+        up = side_buf(static_cast<size_t>(n * 4));
+        hip_check(hipMemcpyAsync(up.get(), h.data(), n * 4, hipMemcpyHostToDevice, ss), "hipMemcpyAsync H2D");
+        hip_check(hipStreamSynchronize(ss), "hipStreamSynchronize(upload)");  // h is pageable and local
+        src = up.get();
+      }
+      if (sdt == o_.dtype && up) {
+        rec.staging = up;
+      } else {
+        rec.staging = side_buf(static_cast<size_t>(n * es));
+        launch_cast(src, sdt, rec.staging.get(), o_.dtype, n, ss);
+      }
+      hip_check(hipStreamSynchronize(ss), "hipStreamSynchronize(staging)");
+      in_ptr = rec.staging.get();
+    }
+  }
+  rec.out = resident_out(static_cast<size_t>(n * es), &rec.exported, true);
+  if (!rec.out) throw ProtocolError("xgmi plane: no round output buffer for the group kernel");
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    rec.slot = take_slot(lk);
+  }
+  int32_t* slot_dev = ring_dev_ + static_cast<size_t>(rec.slot) * ring_stride_;
+  ResidentDoor e{};
+  e.in = reinterpret_cast<uint64_t>(cold ? rec.out.get() : in_ptr);
+  e.out = reinterpret_cast<uint64_t>(rec.out.get());
+  e.counts = reinterpret_cast<uint64_t>(cnt_vram_ + static_cast<size_t>(rec.slot) * ring_stride_);
+  e.counts_host = reinterpret_cast<uint64_t>(slot_dev);
+  e.err_out = reinterpret_cast<uint64_t>(slot_dev + ring_stride_ - 1);
+  e.done_out = reinterpret_cast<uint64_t>(slot_dev + ring_stride_ - 2);
+  e.epoch = rec.round_epoch;
+  e.cmd = cold ? kResCold : kResRound;
+  try {
+    TraceScope span("plane", [&] {
+      return std::make_pair(std::string(cold ? "group cold round " : "group round ") + std::to_string(round),
+                            "{\"worker\":" + std::to_string(cfg_.id) + ",\"bytes\":" + std::to_string(n * es) + "}");
+    });
+    bool taken = post_door(e, group_->state_word());
+    {
+      std::lock_guard<std::mutex> lk(group_->mu);
+      taken = taken && group_->in_kernel[static_cast<size_t>(gidx_)] != 0;
+    }
+    if (!taken) group_->ensure(this, gidx_, false, o_.timeout_s);
+  } catch (...) {
+    std::lock_guard<std::mutex> g(mu_);
+    free_slots_.push_back(rec.slot);
+    throw;
+  }
+  std::unique_lock<std::mutex> lk(mu_);
+  last_round_ = round;
+  st_.launches++;
+  st_.group_rounds++;
+  if (cold) st_.cold++;
+  st_.bytes += static_cast<uint64_t>(n * es);
+  q_.push_back(std::move(rec));
+  q_len_.fetch_add(1, std::memory_order_release);
+  lk.unlock();
+  if (comp_sleeping_.load(std::memory_order_seq_cst)) cv_.notify_all();
+}
+
+std::string XgmiRoundPlane::debug_state() const {
+  std::ostringstream os;
+  os << "{\"res_seq\":" << res_seq_ << ",\"consumed\":" << rstate_[1] << ",\"solo_state\":" << rstate_[0]
+     << ",\"res_on\":" << (res_on_ ? 1 : 0) << ",\"last_round\":" << last_round_ << ",\"queued\":" << q_len_.load();
+  if (res_seq_ > 1) {
+    const ResidentDoor* d = door_ + (res_seq_ - 1u) % kResidentDoors;
+    os << ",\"door_last\":{\"seq\":" << d->seq << ",\"cmd\":" << d->cmd << ",\"epoch\":" << d->epoch << "}";
+  }
+  if (group_) {
+    os << ",\"group\":{\"idx\":" << gidx_ << ",\"state\":" << group_->state_word()[0]
+       << ",\"launched\":" << (group_->launched ? 1 : 0)
+       << ",\"in_kernel\":" << static_cast<int>(group_->in_kernel[static_cast<size_t>(gidx_)]) << "}";
+    uint64_t hb = 0;
+    (void)hipMemcpy(&hb, group_->gdm, 8, hipMemcpyDeviceToHost);
+    os << ",\"heartbeat\":" << hb;
+  }
+  uint64_t dm[10] = {};
+  (void)hipMemcpy(dm, rdm_, sizeof(dm), hipMemcpyDeviceToHost);
+  os << ",\"go\":[" << (dm[0] >> 32) << "," << (dm[0] & 0xffffffffu) << "],\"dm_epoch_cmd\":[" << (dm[8] & 0xffffffffu)
+     << "," << (dm[8] >> 32) << "]";
+  uint32_t ctl[16] = {};
+  (void)hipMemcpy(ctl, ctl_mem_, sizeof(ctl), hipMemcpyDeviceToHost);
+  os << ",\"ctl\":[";
+  for (int i = 0; i < 16; ++i) os << (i ? "," : "") << ctl[i];
+  os << "]}";
+  (void)hipGetLastError();
+  return os.str();
 }
 
 int XgmiRoundPlane::take_slot(std::unique_lock<std::mutex>& lk) {
@@ -654,13 +959,14 @@ int XgmiRoundPlane::take_slot(std::unique_lock<std::mutex>& lk) {
   return s;
 }
 
-bool XgmiRoundPlane::post_door(const ResidentDoor& e) {
+bool XgmiRoundPlane::post_door(const ResidentDoor& e, const volatile uint32_t* state) {
+  const volatile uint32_t* sw = state != nullptr ? state : rstate_;
   const uint32_t seq = res_seq_++;
   // the door slot is free once the kernel consumed the entry kResidentDoors before this one
   // (rounds in flight are bounded by the ring's slots, so this does not wait in practice)
   const auto t0 = std::chrono::steady_clock::now();
   while (static_cast<int32_t>(seq - static_cast<uint32_t>(kResidentDoors) - rstate_[1]) > 0 &&
-         rstate_[0] != kResExited) {
+         sw[0] != kResExited) {
     if (std::chrono::steady_clock::now() - t0 > std::chrono::duration<double>(2 * o_.timeout_s + 5))
       throw ProtocolError("xgmi plane: the resident round kernel stopped taking rounds");
     __builtin_ia32_pause();
@@ -679,12 +985,12 @@ bool XgmiRoundPlane::post_door(const ResidentDoor& e) {
   // Dekker hand-off with the kernel's idle exit (xgmi_threshold.hip, resident_door): the
   // entry is visible before the state word is read
   __atomic_thread_fence(__ATOMIC_SEQ_CST);
-  uint32_t st = rstate_[0];
+  uint32_t st = sw[0];
   while (st == kResExiting) {
     if (std::chrono::steady_clock::now() - t0 > std::chrono::duration<double>(2 * o_.timeout_s + 5))
       throw ProtocolError("xgmi plane: the resident round kernel neither took nor refused a round");
     __builtin_ia32_pause();
-    st = rstate_[0];
+    st = sw[0];
   }
   return st != kResExited;
 }
@@ -706,7 +1012,8 @@ void XgmiRoundPlane::park_resident() {
   }
 }
 
-std::shared_ptr<void> XgmiRoundPlane::resident_out(size_t bytes, std::shared_ptr<std::atomic<bool>>* exported) {
+std::shared_ptr<void> XgmiRoundPlane::resident_out(size_t bytes, std::shared_ptr<std::atomic<bool>>* exported,
+                                                    bool wait) {
   bytes = std::max<size_t>(bytes, 256);
   std::vector<void*> ptrs;
   {
@@ -759,6 +1066,9 @@ std::shared_ptr<void> XgmiRoundPlane::resident_out(size_t bytes, std::shared_ptr
            std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(100))
       __builtin_ia32_pause();
     (void)hipGetLastError();
+    // a grouped worker has no launch path: it waits (the allocation stream has normal
+    // priority, never behind the group kernel's queue)
+    if (q == hipErrorNotReady && wait) q = hipStreamSynchronize(alloc_stream_);
     std::lock_guard<std::mutex> g(rel_->mu);
     rel_->free.push_back(p);  // usable by the launch path in any case (stream-ordered after it)
     st_.pool_grown++;
@@ -860,7 +1170,7 @@ bool XgmiRoundPlane::launch_resident(int round, const Payload& input, bool cold)
       rstate_[0] = kResRunning;
       __atomic_thread_fence(__ATOMIC_SEQ_CST);
       try {
-        comm_->launch_resident(rplan_, door_dev_, rstate_dev_, rdm_, seq, ++res_gen_,
+        comm_->launch_resident(rplan_, door_dev_, rstate_dev_, rdm_, seq, g_res_gen.fetch_add(1) + 1u,
                                static_cast<uint64_t>(o_.resident_idle_us * 100.0), stream_);
       } catch (...) {
         std::lock_guard<std::mutex> g(mu_);
@@ -890,6 +1200,10 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   if (!configured_) throw ProtocolError("xgmi plane: launch before configure (InitWorkers)");
   if (round != last_round_ + 1) throw ProtocolError("xgmi plane: rounds must be launched in order");
   hip_check(hipSetDevice(o_.device), "hipSetDevice");
+  if (group_) {
+    launch_group(round, input, cold);
+    return;
+  }
   if (launch_resident(round, input, cold)) return;
   park_resident();
   const int64_t n = cfg_.dataSize;
@@ -999,6 +1313,15 @@ void XgmiRoundPlane::abort(int round) {
   const uint32_t e = epoch_of(r);
   volatile uint32_t* w = hforce_ + 1;
   if (static_cast<int32_t>(e - *w) > 0) *w = e;  // the kernel polls it at its lag gate
+  // a grouped worker's posted rounds must run to be abandoned: with a co-located worker still
+  // to join, no group kernel may be running - start one without it
+  if (group_ && static_cast<int32_t>(res_seq_ - 1u - rstate_[1]) > 0) {
+    try {
+      group_->ensure(this, gidx_, true, o_.timeout_s);
+    } catch (const std::exception& ex) {
+      MXAR_LOG(ERROR, "plane", "abandoning rounds: " << ex.what());
+    }
+  }
 }
 
 void XgmiRoundPlane::drain() {

@@ -26,6 +26,13 @@
 //     and the next round launches it again. Same round semantics, same done word.
 //   * force (catch-up): raises a pinned host word the kernel polls; rounds <= it complete
 //     with what has arrived. Peers ahead by more than maxLag force us through our slab.
+//   * co-located workers (several workers of one job in this process on this GPU, e.g. a
+//     PlaneJob): they form a PlaneGroup and every round of every one of them runs in ONE
+//     resident kernel, a slice of workgroups per worker fed from that worker's door
+//     (xgmi_threshold.hip threshold_group_resident_kernel). Each worker's rounds still run on
+//     their own schedule (a straggler's slice lags, the others run ahead), and no worker's
+//     round can wait in a hardware queue behind a co-located peer's spinning round - any number
+//     of workers at any GPU_MAX_HW_QUEUES (>= 2).
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -83,7 +90,12 @@ struct XgmiPlaneStats {
   uint64_t pool_grown = 0;  // round outputs the pool had to allocate (none after warm-up in steady state)
   uint64_t resident_pool_misses = 0;  // resident-size rounds launched instead: pool growth not ready in time
   uint64_t resident_rounds = 0, resident_launches = 0, resident_parks = 0;
+  uint64_t group_rounds = 0;   // rounds run by the co-located workers' group kernel
+  uint64_t group_launches = 0;  // group kernels this worker launched
+  int group_size = 0;          // co-located workers in the current membership (0: none / alone)
 };
+
+struct PlaneGroup;
 
 class XgmiRoundPlane final : public RoundPlane {
  public:
@@ -108,6 +120,9 @@ class XgmiRoundPlane final : public RoundPlane {
   int64_t chunk_elems() const { return chunk_; }
   int64_t block_elems() const { return block_; }
   XgmiComm* comm() const { return comm_.get(); }
+  // Diagnostics (blocking copies of device words - never on a hot path): the door / resident
+  // words, the group's state, the device go word and control words.
+  std::string debug_state() const;
   // Phase-stamp buffer for this plane's round kernels (study knob, XgmiComm::set_phase_stamps);
   // kept across re-initialisations. Call between rounds.
   void set_phase_stamps(uint64_t* buf, int64_t slots) {
@@ -151,10 +166,24 @@ class XgmiRoundPlane final : public RoundPlane {
   // false = the round needs the launch path (park_resident first).
   bool launch_resident(int round, const Payload& input, bool cold);
   // Writes door entry res_seq_ and hands it to the kernel; false = the kernel had exited
-  // before it took the entry (nothing runs it).
-  bool post_door(const ResidentDoor& e);
+  // before it took the entry (nothing runs it). state: the kernel's state word (the group's
+  // for a grouped worker; null = this plane's own).
+  bool post_door(const ResidentDoor& e, const volatile uint32_t* state = nullptr);
   // Stops the resident kernel (a STOP entry behind the posted rounds) and waits for it to leave.
   void park_resident();
+  // Co-located workers (PlaneGroup): join the group of this membership (configure), post a
+  // round to the group kernel (every round of a grouped worker), leave the group (a STOP entry
+  // for this worker's slice; configure / destruction).
+  void join_group(const PlaneConfig& cfg);
+  void launch_group(int round, const Payload& input, bool cold);
+  void leave_group();
+  friend struct PlaneGroup;
+  // the workers of this membership in this process on this device: (rank, arena id)
+  std::vector<std::pair<int, uint64_t>> colocated(const PlaneConfig& cfg) const;
+  bool grouped_ = false;  // this membership has co-located workers (configure)
+  std::shared_ptr<PlaneGroup> group_;
+  int gidx_ = -1;                      // this worker's index in the group
+  XgmiComm::ResidentPlan gplan_;       // the group kernel's geometry for this membership
 
   XgmiPlaneOptions o_;
   char* arena_ = nullptr;
@@ -223,14 +252,14 @@ class XgmiRoundPlane final : public RoundPlane {
   bool rplan_tried_ = false;
   bool res_on_ = false;                // a resident kernel was launched and may still run
   uint32_t res_seq_ = 1;               // next door entry
-  uint32_t res_gen_ = 0;               // resident kernel launches
   // exported outputs released while a resident kernel holds the plane stream: reusable once
   // an event recorded on the default stream behind them has completed (host query)
   std::deque<std::pair<hipEvent_t, std::vector<void*>>> rel_pend_;
   std::vector<hipEvent_t> rel_spare_;
   // a pooled round output for a resident round (grown with hipMalloc: nothing may queue on
   // the plane stream behind the resident kernel)
-  std::shared_ptr<void> resident_out(size_t bytes, std::shared_ptr<std::atomic<bool>>* exported);
+  // (wait: a grouped worker has no launch path - it waits for the pool's growth)
+  std::shared_ptr<void> resident_out(size_t bytes, std::shared_ptr<std::atomic<bool>>* exported, bool wait = false);
 };
 
 std::shared_ptr<XgmiRoundPlane> make_xgmi_plane(const XgmiPlaneOptions& o);

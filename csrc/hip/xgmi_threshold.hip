@@ -68,19 +68,20 @@ __device__ __forceinline__ uint32_t* forcew(const CommArgs& a, int k, int s) {
 // The engine's pinned host words, [0] force and [1] abort: ONE PCIe read when they are
 // adjacent (the plane's layout). Returns "forced" (an abandoned round is forced too) and
 // sets *aborted.
-__device__ __forceinline__ bool host_forced(const CommArgs& a, uint32_t epoch, bool* aborted) {
+__device__ __forceinline__ bool host_forced(const uint32_t* hforce, const uint32_t* habort, uint32_t epoch,
+                                            bool* aborted) {
   *aborted = false;
-  if (a.hforce == nullptr) return false;
+  if (hforce == nullptr) return false;
   uint32_t fw, aw = epoch - 1u;
-  if (a.habort == a.hforce + 1) {
-    const uint64_t w = __hip_atomic_load(reinterpret_cast<const uint64_t*>(a.hforce), __ATOMIC_RELAXED,
+  if (habort == hforce + 1) {
+    const uint64_t w = __hip_atomic_load(reinterpret_cast<const uint64_t*>(hforce), __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_SYSTEM);
     fw = static_cast<uint32_t>(w);
     aw = static_cast<uint32_t>(w >> 32);
   } else {
-    fw = __hip_atomic_load(const_cast<uint32_t*>(a.hforce), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (a.habort != nullptr)
-      aw = __hip_atomic_load(const_cast<uint32_t*>(a.habort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    fw = __hip_atomic_load(const_cast<uint32_t*>(hforce), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (habort != nullptr)
+      aw = __hip_atomic_load(const_cast<uint32_t*>(habort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   *aborted = reached(aw, epoch);
   return *aborted || reached(fw, epoch);
@@ -111,8 +112,9 @@ __device__ __attribute__((noinline)) bool wave_forced_words(const uint32_t* own_
   }
   return __any(f);
 }
-__device__ __forceinline__ bool wave_forced(const CommArgs& a, int r, uint32_t epoch, bool host) {
-  return wave_forced_words(forcew(a, r, 0), a.P, r, epoch, host ? a.hforce : nullptr, a.habort);
+__device__ __forceinline__ bool wave_forced(const CommArgs& a, const uint32_t* hforce, const uint32_t* habort, int r,
+                                            uint32_t epoch, bool host) {
+  return wave_forced_words(forcew(a, r, 0), a.P, r, epoch, host ? hforce : nullptr, habort);
 }
 
 // Host-word polls at most every 100 us per workgroup, the first one 100 us after the kernel
@@ -570,11 +572,14 @@ __device__ __forceinline__ void put_count(int32_t* p, int32_t v) {
 
 // The per-round operands of threshold_round: a launch's own (CommArgs, threshold_kernel) or
 // the ones a resident kernel read from the host's door (threshold_resident_kernel).
+// The rank's own words come with them too (its control words, pinned host words and split
+// scratch): a plane group's resident kernel (threshold_group_resident_kernel) runs several
+// workers' rounds, each with its own set, under one CommArgs of shared geometry.
 struct RoundVars {
   const char* in;
   char* out;
-  int32_t* counts;
-  int32_t* counts_host;
+  int32_t* counts;       // this rank's [P][nch] (already offset)
+  int32_t* counts_host;  // this rank's pinned copy (already offset)
   uint32_t* err_out;
   uint32_t* done_out;
   uint32_t epoch;  // 0: ctl[4] + 1
@@ -585,7 +590,24 @@ struct RoundVars {
   // run by a resident kernel: its workgroups start the next round once ctl[4] names this
   // one, so the round end orders its counter resets before that store
   int resident;
+  int rank;
+  uint32_t* ctl;
+  const uint32_t* hforce;
+  const uint32_t* habort;
+  uint64_t* split_dec;
+  uint32_t* split_ctr;
+  uint32_t* split_early;
 };
+
+// A launch's own round of rank a.rank0 + y (threshold_kernel; the resident kernel: y = 0).
+__device__ __forceinline__ RoundVars launch_vars(const CommArgs& a, int y, const char* in, char* out, int32_t* counts,
+                                                 int32_t* counts_host, uint32_t* err_out, uint32_t* done_out,
+                                                 uint32_t epoch, int cold, int gate_open, int resident) {
+  const int64_t cy = static_cast<int64_t>(y) * a.P * a.nch;
+  return RoundVars{in, out, counts ? counts + cy : nullptr, counts_host ? counts_host + cy : nullptr, err_out, done_out,
+                   epoch, cold, gate_open, resident, a.rank0 + y, a.ctl[y], a.hforce, a.habort, a.split_dec,
+                   a.split_ctr, a.split_early};
+}
 
 // One round of rank a.rank0 + blockIdx.y by the whole grid.
 // Returns true when this workgroup's round took every peer's reduced chunk it gathers, with
@@ -613,11 +635,10 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   // [5] end, [6] scatter done, [7] units gathered
   PhaseStamps ps(a, ps_lds);
   const int P = a.P;
-  const int y = blockIdx.y;
-  const int r = a.rank0 + y;
+  const int r = rv.rank;
   const char* const in = rv.in;
   char* const out = rv.out;
-  uint32_t* const ctl = a.ctl[y];
+  uint32_t* const ctl = rv.ctl;
   // threshold rounds count separately (ctl[4]); the protocol engine passes its round epochs.
   // ctl[14] = the last round of this rank that was clean (every workgroup gathered every
   // peer's reduced chunks): loaded beside ctl[4], same line, no extra latency
@@ -631,7 +652,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   uint32_t* err = &ctl[2];
   const bool rel = a.fence & 1, acq = a.fence & 2;
   const int Pm1 = P > 1 ? P - 1 : 1;
-  int32_t* const counts = rv.counts ? rv.counts + static_cast<int64_t>(y) * P * a.nch : nullptr;
+  int32_t* const counts = rv.counts;
   const bool cold = rv.cold != 0;
   const bool ref = a.order_ref != 0;
   // Full thresholds (thReduce = thComplete = 1): every contribution and every chunk is taken
@@ -705,7 +726,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
           arr = exists(j, c) && reached(ld_flag(f2(a, r, row * P + j, c)), epoch);
           first = u - b * S == 0;  // a split chunk's early arrival is decided by its slice 0
           if (split && first && arr)
-            __hip_atomic_store(&a.split_early[static_cast<int64_t>(j) * a.maxch + c], epoch, __ATOMIC_RELAXED,
+            __hip_atomic_store(&rv.split_early[static_cast<int64_t>(j) * a.maxch + c], epoch, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
         const uint64_t m = __ballot(arr);
@@ -740,7 +761,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
             const int b = (static_cast<int>(blockIdx.x) + idx * G) / S;
             const int c = b / Pm1;
             const int j = (r + 1 + b % Pm1) % P;
-            arr = ld_ctl(&a.split_early[static_cast<int64_t>(j) * a.maxch + c]) == epoch;
+            arr = ld_ctl(&rv.split_early[static_cast<int64_t>(j) * a.maxch + c]) == epoch;
           }
           const uint64_t m = __ballot(arr);
           if (lane == 0) early[w] = m;
@@ -784,9 +805,9 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       }
       __builtin_amdgcn_s_sleep(2);
       if (!ok) ok = reached(ld_flag(f), target);
-      if (a.habort != nullptr && hp.due()) {
+      if (rv.habort != nullptr && hp.due()) {
         bool ab = false;
-        if (k == 0) (void)host_forced(a, epoch, &ab);
+        if (k == 0) (void)host_forced(rv.hforce, rv.habort, epoch, &ab);
         if (__any(ab)) {
           aborted = true;
           break;
@@ -829,7 +850,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
                                           (cstart - c * a.chunk),
                                       sub);
         if (len > 0) copy_in<E>(a.base[j] + rowS + r * slot + cstart * es, in + (bstart + cstart) * es, len);
-        if (!last_slice(&a.split_ctr[a.maxch + static_cast<int64_t>(j) * a.maxch + c], S, &sh_last)) continue;
+        if (!last_slice(&rv.split_ctr[a.maxch + static_cast<int64_t>(j) * a.maxch + c], S, &sh_last)) continue;
         publish_flags([&](int) { return f1(a, j, row * P + r, c); }, 1, epoch, rel);
       }
     } else {
@@ -874,7 +895,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     // this workgroup's slice of chunk c (the whole chunk when S = 1)
     const int64_t cstart = static_cast<int64_t>(c) * a.chunk + static_cast<int64_t>(v - c * S) * sub;
     const int64_t len = clamp_len(clamp_len(blen_own - c * a.chunk, a.chunk) - (cstart - c * a.chunk), sub);
-    uint64_t* const dec = split ? &a.split_dec[c] : nullptr;
+    uint64_t* const dec = split ? &rv.split_dec[c] : nullptr;
     if (void_round) {  // nothing reduced, nothing sent
       if (len > 0) zero_fill<E>(out + (bstart_own + cstart) * es, len);
       if (threadIdx.x == 0 && counts) cput(static_cast<int64_t>(r) * a.nch + c, 0);
@@ -908,7 +929,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
           // one clock read per spin: s_memrealtime is a scalar memory round trip
           const uint64_t now = wall_ticks();
           const bool host = hp.due(now);
-          if ((host || sp.due(now)) && wave_forced(a, r, epoch, host)) {
+          if ((host || sp.due(now)) && wave_forced(a, rv.hforce, rv.habort, r, epoch, host)) {
             forced = true;
             break;
           }
@@ -976,7 +997,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       if (!take) zero_fill<E>(own_out, len);
     }
     // a split chunk is reduced once its last slice is: that workgroup publishes it
-    if (split && !last_slice(&a.split_ctr[c], S, &sh_last)) continue;
+    if (split && !last_slice(&rv.split_ctr[c], S, &sh_last)) continue;
     if (threadIdx.x < static_cast<unsigned>(P) && static_cast<int>(threadIdx.x) != r)
       st_flag(f2c(a, static_cast<int>(threadIdx.x), row * P + r, c), static_cast<uint32_t>(cnt));
     if (threadIdx.x == 0) {
@@ -1033,7 +1054,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         const int b = u / S;
         const int c = b / Pm1;
         const int j = (r + 1 + b % Pm1) % P;
-        uint64_t* const dec = split ? &a.split_dec[a.maxch + static_cast<int64_t>(j) * a.maxch + c] : nullptr;
+        uint64_t* const dec = split ? &rv.split_dec[a.maxch + static_cast<int64_t>(j) * a.maxch + c] : nullptr;
         bool take;
         if (fastg) {  // nothing to decide: every thread knows the unit is taken if it exists
           take = exists(j, c);
@@ -1115,7 +1136,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       const uint64_t now = wall_ticks();
       if (!give) {
         const bool host = hp.due(now);
-        if ((host || sp.due(now)) && wave_forced(a, r, epoch, host)) give = 1;
+        if ((host || sp.due(now)) && wave_forced(a, rv.hforce, rv.habort, r, epoch, host)) give = 1;
       }
       if (!give && now > deadline) {
         if (threadIdx.x == 0)
@@ -1150,7 +1171,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
                                       sub);
         bool take = false;
         if (split) {  // give the unit up, unless another slice of it already took it
-          uint64_t* const dec = &a.split_dec[a.maxch + static_cast<int64_t>(j) * a.maxch + c];
+          uint64_t* const dec = &rv.split_dec[a.maxch + static_cast<int64_t>(j) * a.maxch + c];
           if (threadIdx.x == 0) {
             uint64_t d = 0;
             if (dec_claim(dec, epoch, deadline, err, &d)) {
@@ -1249,7 +1270,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     // their PCIe write acknowledgements (a release before the done word did, on the round's
     // critical path). The counts: every workgroup's sc1 stores drained before its ticket.
     if (counts != nullptr && rv.counts_host != nullptr) {
-      int32_t* dst = rv.counts_host + static_cast<int64_t>(y) * P * a.nch;
+      int32_t* dst = rv.counts_host;
       for (int64_t i = threadIdx.x; i < static_cast<int64_t>(P) * a.nch; i += kCommThreads) {
         const int32_t v = counts_lds ? sh_cnt[i] : __hip_atomic_load(counts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(dst + i, static_cast<int32_t>(host_tag(epoch, static_cast<uint32_t>(v))), __ATOMIC_RELAXED,
@@ -1272,7 +1293,8 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
 template <class E, bool FULL>
 __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   const int y = blockIdx.y;
-  const RoundVars rv{a.in[y], a.out[y], a.counts, a.counts_host, a.err_out, a.done_out, a.epoch_set, a.cold, 0, 0};
+  const RoundVars rv =
+      launch_vars(a, y, a.in[y], a.out[y], a.counts, a.counts_host, a.err_out, a.done_out, a.epoch_set, a.cold, 0, 0);
   (void)threshold_round<E, FULL>(a, rv);
 }
 
@@ -1415,14 +1437,13 @@ __global__ __launch_bounds__(kCommThreads) void threshold_resident_kernel(CommAr
     __syncthreads();
     const uint32_t cmd = static_cast<uint32_t>(sh_ent[6] >> 32);
     if (cmd == static_cast<uint32_t>(kResStop)) break;  // uniform
-    const RoundVars rv{reinterpret_cast<const char*>(sh_ent[0]), reinterpret_cast<char*>(sh_ent[1]),
-                       reinterpret_cast<int32_t*>(sh_ent[2]),    reinterpret_cast<int32_t*>(sh_ent[3]),
-                       reinterpret_cast<uint32_t*>(sh_ent[4]),   reinterpret_cast<uint32_t*>(sh_ent[5]),
-                       static_cast<uint32_t>(sh_ent[6]),         cmd == static_cast<uint32_t>(kResCold) ? 1 : 0,
-                       (prev_clean && gridDim.x == 1 && a.trows >= 2 && static_cast<uint32_t>(sh_ent[6]) == prev_epoch + 1u)
-                           ? 1
-                           : 0,
-                       1};
+    const RoundVars rv = launch_vars(
+        a, 0, reinterpret_cast<const char*>(sh_ent[0]), reinterpret_cast<char*>(sh_ent[1]),
+        reinterpret_cast<int32_t*>(sh_ent[2]), reinterpret_cast<int32_t*>(sh_ent[3]),
+        reinterpret_cast<uint32_t*>(sh_ent[4]), reinterpret_cast<uint32_t*>(sh_ent[5]), static_cast<uint32_t>(sh_ent[6]),
+        cmd == static_cast<uint32_t>(kResCold) ? 1 : 0,
+        (prev_clean && gridDim.x == 1 && a.trows >= 2 && static_cast<uint32_t>(sh_ent[6]) == prev_epoch + 1u) ? 1 : 0,
+        1);
     __syncthreads();
     const bool clean = threshold_round<E, FULL>(a, rv);
     if (threadIdx.x == 0) sh_clean = clean ? 1 : 0;
@@ -1435,6 +1456,281 @@ __global__ __launch_bounds__(kCommThreads) void threshold_resident_kernel(CommAr
     if (threadIdx.x == 0) {  // the round's counters are reset before any workgroup starts the next
       const uint64_t until = wall_ticks() + a.timeout + 100000000ull;
       while (ld_ctl(&ctl[4]) != rv.epoch && wall_ticks() < until) __builtin_amdgcn_s_sleep(1);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Group resident rounds (xgmi_plane.cc PlaneGroup). Co-located workers of one job (one
+// process, one GPU) run their rounds in ONE resident kernel: worker k's slice is grid row
+// y = 1 + k and runs k's rounds one after another, exactly as threshold_resident_kernel runs
+// one worker's; the slices never wait for each other's turn, so a straggler's slice lags
+// while the others run ahead (the protocol's bounded staleness), and no slice can sit in a
+// hardware queue behind a co-located peer's spinning round - however many workers share the
+// GPU and however few hardware queues the process has (GPU_MAX_HW_QUEUES).
+//
+// Row 0, workgroup 0, wave 0 is the dispatcher. It alone reads the doors: lanes 8j..8j+7
+// read worker j's next 64-B entry (and worker 8 + j's in a second load), so ONE load polls up
+// to eight doors. A found entry goes to the worker's slice through its device words (entry,
+// then go = gen << 32 | seq) once the slice's previous round ended (its ctl[4] names that
+// round's epoch: every workgroup of the slice has read the previous entry), and the door slot
+// is released at once (hstate[1]). A STOP entry (the worker leaves the group) ends its slice.
+//
+// Exit: only the dispatcher decides it, for the whole group - no worker's rounds may be left
+// to a kernel queued behind this one. After `idle` ticks with no entry and no round running
+// it writes EXITING to the group's state word, fences, and polls every door once more (the
+// hosts write an entry, fence, then read the state word): an entry found keeps the kernel
+// (RUNNING); otherwise every slice gets STOP and the state becomes EXITED, and the next post
+// launches a new kernel. Slices wait for go without a deadline of their own while the
+// dispatcher's heartbeat (gdm[0]) advances.
+__device__ __forceinline__ void group_dispatch(const CommArgs& a, const GroupResArgs& g) {
+  const int lane = static_cast<int>(threadIdx.x);
+  const int Y = g.Y;
+  const int w = lane & 7;
+  // lane-held state: lanes 8j..8j+7 poll worker j (bank 0) and worker 8 + j (bank 1); lane k
+  // keeps worker k's control words, its running round's epoch and whether it left
+  const uint64_t* dp0 = nullptr;
+  const uint64_t* dp1 = nullptr;
+  uint32_t nx0 = 0, nx1 = 0;
+  uint32_t* myctl = nullptr;
+  for (int y = 0; y < Y; ++y) {  // uniform: scalar loads of the arguments
+    if ((lane >> 3) == (y & 7)) {
+      if (y < 8) {
+        dp0 = reinterpret_cast<const uint64_t*>(g.m[y].door);
+        nx0 = g.m[y].seq0;
+      } else {
+        dp1 = reinterpret_cast<const uint64_t*>(g.m[y].door);
+        nx1 = g.m[y].seq0;
+      }
+    }
+    if (lane == y) myctl = a.ctl[y];
+  }
+  uint32_t run_epoch = 0;
+  bool busy = false, gone = lane >= Y;
+  const uint64_t hb_every = 50000;  // 0.5 ms
+  uint64_t t_act = wall_ticks(), t_hb = 0;
+  auto poll = [&](uint64_t* v0, uint64_t* v1) {
+    *v0 = dp0 != nullptr ? __hip_atomic_load(dp0 + static_cast<uint64_t>(nx0 % kResidentDoors) * 8 + w,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                         : 0ull;
+    *v1 = (Y > 8 && dp1 != nullptr) ? __hip_atomic_load(dp1 + static_cast<uint64_t>(nx1 % kResidentDoors) * 8 + w,
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                    : 0ull;
+  };
+  // worker y's entry in (v0, v1): 1 = a whole entry, 2 = its sequence word only (a read that
+  // caught the host mid-write), 0 = nothing. Uniform.
+  auto entry_of = [&](int y, uint64_t v0, uint64_t v1, uint32_t* e) -> int {
+    const uint64_t v = y < 8 ? v0 : v1;
+    const int base = (y & 7) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint64_t x = __shfl(v, base + i);
+      e[2 * i] = static_cast<uint32_t>(x);
+      e[2 * i + 1] = static_cast<uint32_t>(x >> 32);
+    }
+    const uint32_t seq = static_cast<uint32_t>(__shfl(static_cast<int>(y < 8 ? nx0 : nx1), base));
+    if (e[14] != seq) return 0;
+    return e[15] == door_check(e, seq) ? 1 : 2;
+  };
+  auto go = [&](int y, uint32_t seq) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // explicit: the compiler drops the fence's own wait when it can prove nothing in flight
+    // (MI355X_MICROARCH.md, compiler hazard), and the go word must not overtake the entry
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+      __hip_atomic_store(&g.m[y].dm[kDmGo], (static_cast<uint64_t>(g.gen) << 32) | seq, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  };
+  for (;;) {
+    const uint64_t now = wall_ticks();
+    if (now - t_hb > hb_every) {
+      if (lane == 0) __hip_atomic_store(&g.gdm[0], now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t_hb = now;
+    }
+    if (busy) busy = ld_ctl(&myctl[4]) != run_epoch;  // the slice's round ended
+    uint64_t v0, v1;
+    poll(&v0, &v1);
+    bool pending = false;
+    for (int y = 0; y < Y; ++y) {
+      if (__shfl(gone ? 1 : 0, y) != 0) continue;
+      uint32_t e[16];
+      const int st = entry_of(y, v0, v1, e);
+      if (st == 0) continue;
+      pending = true;
+      if (st != 1 || __shfl(busy ? 1 : 0, y) != 0) continue;  // taken once whole / once the slice is free
+      const uint32_t seq = e[14];
+      const uint64_t word = __shfl(y < 8 ? v0 : v1, (y & 7) * 8 + w);
+      if (lane < 8)
+        __hip_atomic_store(&g.m[y].dm[kDmEntry + lane], word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      go(y, seq);
+      if (lane == 0) sys_st(&g.m[y].hstate[1], seq);  // the door slot is free
+      if (static_cast<int32_t>(e[13]) == kResStop) {
+        if (lane == y) gone = true;
+      } else if (lane == y) {
+        busy = true;
+        run_epoch = e[12];
+      }
+      if ((lane >> 3) == (y & 7)) {
+        if (y < 8)
+          ++nx0;
+        else
+          ++nx1;
+      }
+      t_act = now;
+    }
+    if (__all(gone)) {  // every worker left: nothing more to serve
+      if (lane == 0) {  // after every consumed-entry word (the hosts read them once EXITED)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        sys_st(&g.gstate[0], kResExited);
+      }
+      return;
+    }
+    if (!pending && !__any(busy) && wall_ticks() - t_act > g.idle) {
+      if (lane == 0) {
+        sys_st(&g.gstate[0], kResExiting);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      bool found = false;
+      for (int i = 0; i < 4 && !found; ++i) {
+        poll(&v0, &v1);
+        for (int y = 0; y < Y && !found; ++y) {
+          if (__shfl(gone ? 1 : 0, y) != 0) continue;
+          uint32_t e[16];
+          found = entry_of(y, v0, v1, e) != 0;
+        }
+      }
+      if (found) {  // posted meanwhile: keep serving
+        if (lane == 0) sys_st(&g.gstate[0], kResRunning);
+        t_act = wall_ticks();
+        continue;
+      }
+      for (int y = 0; y < Y; ++y) {  // every slice still here leaves
+        if (__shfl(gone ? 1 : 0, y) != 0) continue;
+        const uint32_t seq = static_cast<uint32_t>(__shfl(static_cast<int>(y < 8 ? nx0 : nx1), (y & 7) * 8));
+        // word 6: STOP; word 7: the entry's sequence number (slices check it)
+        if (lane == 6 || lane == 7)
+          __hip_atomic_store(&g.m[y].dm[kDmEntry + lane],
+                             lane == 6 ? static_cast<uint64_t>(static_cast<uint32_t>(kResStop)) << 32 : seq,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        go(y, seq);
+      }
+      if (lane == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        sys_st(&g.gstate[0], kResExited);
+      }
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+template <class E, bool FULL>
+__global__ __launch_bounds__(kCommThreads) void threshold_group_resident_kernel(CommArgs a, GroupResArgs g) {
+  if (blockIdx.y == 0) {  // the dispatcher row: one wave works, the rest leave at once
+    if (blockIdx.x == 0 && threadIdx.x < 64) group_dispatch(a, g);
+    return;
+  }
+  const int y = static_cast<int>(blockIdx.y) - 1;
+  const GroupResidentMember& m = g.m[y];
+  uint32_t* const ctl = a.ctl[y];
+  __shared__ uint64_t sh_ent[8];
+  __shared__ int sh_clean;
+  uint32_t prev_epoch = 0;
+  bool prev_clean = false;
+  const uint64_t lost = 2 * a.timeout + 100000000ull;  // the dispatcher's heartbeat stopped this long ago
+  for (uint32_t seq = m.seq0;; ++seq) {
+    if (threadIdx.x < 64) {
+      const int lane = static_cast<int>(threadIdx.x);
+      uint64_t w = 0;
+      bool ok = true;
+      if (lane == 0) {
+        const uint64_t want = (static_cast<uint64_t>(g.gen) << 32) | seq;
+        // the heartbeat is judged by THIS workgroup's clock only: it counts as stopped when its
+        // value has not changed for `lost` local ticks (realtime counters of different XCDs are
+        // not comparable - a dispatcher clock a little ahead made `now - hb` wrap)
+        uint64_t hb_seen = __hip_atomic_load(&g.gdm[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t hb_at = wall_ticks();
+        for (;;) {
+          const uint64_t cur = __hip_atomic_load(&m.dm[kDmGo], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (cur == want) break;
+          // a newer kernel's go (generations only grow): this kernel's dispatcher has left and
+          // its STOP was overwritten - leave too
+          if (static_cast<int32_t>(static_cast<uint32_t>(cur >> 32) - g.gen) > 0) {
+            ok = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+          const uint64_t hb = __hip_atomic_load(&g.gdm[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint64_t now = wall_ticks();
+          if (hb != hb_seen) {
+            hb_seen = hb;
+            hb_at = now;
+          } else if (now - hb_at > lost) {
+            __hip_atomic_fetch_or(&ctl[2], ERR_TIMEOUT_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            ok = false;
+            break;
+          }
+        }
+      }
+      ok = __shfl(ok ? 1 : 0, 0) != 0;
+      if (ok) {
+        // The entry names its own sequence number (word 7): an entry read that does not is
+        // stale (an older entry's line) - counted in ctl[15] and read again after an acquire.
+        for (uint32_t tries = 0;; ++tries) {
+          if (lane < 8) w = __hip_atomic_load(&m.dm[kDmEntry + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (static_cast<uint32_t>(__shfl(w, 7)) == seq) break;
+          if (lane == 0) {
+            __hip_atomic_fetch_add(&ctl[15], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          }
+          if (tries > (1u << 20)) {  // never seen: leave (the host reports the error word)
+            if (lane == 0)
+              __hip_atomic_fetch_or(&ctl[2], ERR_TIMEOUT_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            ok = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      if (!ok && lane == 6) w = static_cast<uint64_t>(static_cast<uint32_t>(kResStop)) << 32;
+      if (lane < 8) sh_ent[lane] = w;
+      // the round's input was written by kernels that finished before the host posted it
+      if (lane == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    }
+    __syncthreads();
+    const uint32_t cmd = static_cast<uint32_t>(sh_ent[6] >> 32);
+    if (cmd == static_cast<uint32_t>(kResStop)) break;  // uniform
+    const uint32_t epoch = static_cast<uint32_t>(sh_ent[6]);
+    const RoundVars rv{reinterpret_cast<const char*>(sh_ent[0]),
+                       reinterpret_cast<char*>(sh_ent[1]),
+                       reinterpret_cast<int32_t*>(sh_ent[2]),
+                       reinterpret_cast<int32_t*>(sh_ent[3]),
+                       reinterpret_cast<uint32_t*>(sh_ent[4]),
+                       reinterpret_cast<uint32_t*>(sh_ent[5]),
+                       epoch,
+                       cmd == static_cast<uint32_t>(kResCold) ? 1 : 0,
+                       (prev_clean && gridDim.x == 1 && a.trows >= 2 && epoch == prev_epoch + 1u) ? 1 : 0,
+                       1,
+                       m.rank,
+                       ctl,
+                       m.hforce,
+                       m.habort,
+                       nullptr,
+                       nullptr,
+                       nullptr};
+    __syncthreads();
+    const bool clean = threshold_round<E, FULL>(a, rv);
+    if (threadIdx.x == 0) sh_clean = clean ? 1 : 0;
+    __syncthreads();
+    prev_clean = sh_clean != 0;
+    prev_epoch = epoch;
+    if (threadIdx.x == 0) {  // the round's counters are reset before any workgroup starts the next
+      const uint64_t until = wall_ticks() + a.timeout + 100000000ull;
+      while (ld_ctl(&ctl[4]) != epoch && wall_ticks() < until) __builtin_amdgcn_s_sleep(1);
     }
     __syncthreads();
   }
@@ -1478,6 +1774,17 @@ void launch_threshold(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {
       hipLaunchKernelGGL((threshold_kernel<E, true>), grid, dim3(kCommThreads), 0, s, a);
     else
       hipLaunchKernelGGL((threshold_kernel<E, false>), grid, dim3(kCommThreads), 0, s, a);
+  });
+}
+
+void launch_threshold_group_resident(const CommArgs& a, const GroupResArgs& g, int grid, hipStream_t s, DType dt) {
+  const dim3 gd(static_cast<unsigned>(grid), static_cast<unsigned>(g.Y + 1));
+  dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
+    using E = decltype(tag);
+    if (full_fast(a))
+      hipLaunchKernelGGL((threshold_group_resident_kernel<E, true>), gd, dim3(kCommThreads), 0, s, a, g);
+    else
+      hipLaunchKernelGGL((threshold_group_resident_kernel<E, false>), gd, dim3(kCommThreads), 0, s, a, g);
   });
 }
 

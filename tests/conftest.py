@@ -10,9 +10,9 @@ if str(ROOT) not in sys.path:
 
 os.environ.setdefault("MXAR_LOGLEVEL", "ERROR")
 
-# Several plane workers share this process (and the GPU) in the round-engine tests; each
-# plane probes its stream onto a hardware queue of its own (csrc/hip/xgmi_plane.cc), so the
-# suite runs at the box's GPU_MAX_HW_QUEUES (4) - it does not raise it.
+# Several plane workers share this process (and the GPU) in the round-engine tests; their
+# rounds run in one group kernel (csrc/hip/xgmi_plane.cc PlaneGroup), so the suite runs at the
+# box's GPU_MAX_HW_QUEUES (4) - it does not raise it.
 
 
 def pytest_configure(config):
