@@ -1533,10 +1533,10 @@ __device__ __forceinline__ void group_dispatch(const CommArgs& a, const GroupRes
     if (e[14] != seq) return 0;
     return e[15] == door_check(e, seq) ? 1 : 2;
   };
+  // The entry words are 8-B agent-scope atomic stores (write-through, sc1) and the slices read
+  // them with 8-B agent-scope loads: draining them before the go store is the whole release
+  // (MI355X_MICROARCH.md, valid forms: 8-B agent atomics both sides) - no L2 write-back.
   auto go = [&](int y, uint32_t seq) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    // explicit: the compiler drops the fence's own wait when it can prove nothing in flight
-    // (MI355X_MICROARCH.md, compiler hazard), and the go word must not overtake the entry
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
       __hip_atomic_store(&g.m[y].dm[kDmGo], (static_cast<uint64_t>(g.gen) << 32) | seq, __ATOMIC_RELAXED,
@@ -1548,9 +1548,9 @@ __device__ __forceinline__ void group_dispatch(const CommArgs& a, const GroupRes
       if (lane == 0) __hip_atomic_store(&g.gdm[0], now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       t_hb = now;
     }
-    if (busy) busy = ld_ctl(&myctl[4]) != run_epoch;  // the slice's round ended
     uint64_t v0, v1;
-    poll(&v0, &v1);
+    poll(&v0, &v1);  // (the PCIe reads first: the control-word read below overlaps them)
+    if (busy) busy = ld_ctl(&myctl[4]) != run_epoch;  // the slice's round ended
     bool pending = false;
     for (int y = 0; y < Y; ++y) {
       if (__shfl(gone ? 1 : 0, y) != 0) continue;
@@ -1647,23 +1647,33 @@ __global__ __launch_bounds__(kCommThreads) void threshold_group_resident_kernel(
       const int lane = static_cast<int>(threadIdx.x);
       uint64_t w = 0;
       bool ok = true;
-      if (lane == 0) {
-        const uint64_t want = (static_cast<uint64_t>(g.gen) << 32) | seq;
-        // the heartbeat is judged by THIS workgroup's clock only: it counts as stopped when its
-        // value has not changed for `lost` local ticks (realtime counters of different XCDs are
-        // not comparable - a dispatcher clock a little ahead made `now - hb` wrap)
-        uint64_t hb_seen = __hip_atomic_load(&g.gdm[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint64_t hb_at = wall_ticks();
-        for (;;) {
-          const uint64_t cur = __hip_atomic_load(&m.dm[kDmGo], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (cur == want) break;
-          // a newer kernel's go (generations only grow): this kernel's dispatcher has left and
-          // its STOP was overwritten - leave too
-          if (static_cast<int32_t>(static_cast<uint32_t>(cur >> 32) - g.gen) > 0) {
-            ok = false;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
+      // ONE load per poll: lanes 0-7 the entry, lane 8 the go word (the same 128-B line). The
+      // entry is taken when go names this kernel's generation and entry `seq`, and the entry
+      // names `seq` itself (word 7): a read that caught an older entry is simply repeated.
+      const uint64_t want = (static_cast<uint64_t>(g.gen) << 32) | seq;
+      // the heartbeat is judged by THIS workgroup's clock only: it counts as stopped when its
+      // value has not changed for `lost` local ticks (realtime counters of different XCDs are
+      // not comparable - a dispatcher clock a little ahead made `now - hb` wrap)
+      uint64_t hb_seen = lane == 0 ? __hip_atomic_load(&g.gdm[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+      uint64_t hb_at = wall_ticks();
+      for (;;) {
+        const uint64_t x = lane < 8    ? __hip_atomic_load(&m.dm[kDmEntry + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : lane == 8 ? __hip_atomic_load(&m.dm[kDmGo], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                       : 0ull;
+        const uint64_t cur = __shfl(x, 8);
+        if (cur == want && static_cast<uint32_t>(__shfl(x, 7)) == seq) {
+          w = x;
+          break;
+        }
+        // a newer kernel's go (generations only grow): this kernel's dispatcher has left and
+        // its STOP was overwritten - leave too
+        if (static_cast<int32_t>(static_cast<uint32_t>(cur >> 32) - g.gen) > 0) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        int lost_now = 0;
+        if (lane == 0) {
           const uint64_t hb = __hip_atomic_load(&g.gdm[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           const uint64_t now = wall_ticks();
           if (hb != hb_seen) {
@@ -1671,29 +1681,12 @@ __global__ __launch_bounds__(kCommThreads) void threshold_group_resident_kernel(
             hb_at = now;
           } else if (now - hb_at > lost) {
             __hip_atomic_fetch_or(&ctl[2], ERR_TIMEOUT_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            ok = false;
-            break;
+            lost_now = 1;
           }
         }
-      }
-      ok = __shfl(ok ? 1 : 0, 0) != 0;
-      if (ok) {
-        // The entry names its own sequence number (word 7): an entry read that does not is
-        // stale (an older entry's line) - counted in ctl[15] and read again after an acquire.
-        for (uint32_t tries = 0;; ++tries) {
-          if (lane < 8) w = __hip_atomic_load(&m.dm[kDmEntry + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (static_cast<uint32_t>(__shfl(w, 7)) == seq) break;
-          if (lane == 0) {
-            __hip_atomic_fetch_add(&ctl[15], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          }
-          if (tries > (1u << 20)) {  // never seen: leave (the host reports the error word)
-            if (lane == 0)
-              __hip_atomic_fetch_or(&ctl[2], ERR_TIMEOUT_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            ok = false;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
+        if (__shfl(lost_now, 0) != 0) {
+          ok = false;
+          break;
         }
       }
       if (!ok && lane == 6) w = static_cast<uint64_t>(static_cast<uint32_t>(kResStop)) << 32;
