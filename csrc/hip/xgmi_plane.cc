@@ -835,11 +835,26 @@ void XgmiRoundPlane::launch_group(int round, const Payload& input, bool cold) {
     auto* dp = dynamic_cast<const DevicePayload*>(input.get());
     if (dp != nullptr && dp->device() == o_.device && dp->dtype() == dcode) {
       // no stream orders the group kernel after the producer: the host waits for it (normal-
-      // priority streams: never queued behind the group kernel's high-priority queue)
-      if (dp->ready())
-        hip_check(hipEventSynchronize(static_cast<hipEvent_t>(dp->ready().get())), "hipEventSynchronize(input)");
-      else if (dp->stream() && dp->stream() != stream_)
-        hip_check(hipStreamSynchronize(dp->stream()), "hipStreamSynchronize(input)");
+      // priority streams: never queued behind the group kernel's high-priority queue). A query
+      // first: a finished producer - the usual case - costs no blocking runtime call
+      if (dp->ready()) {
+        const hipEvent_t ev = static_cast<hipEvent_t>(dp->ready().get());
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipErrorNotReady) {
+          (void)hipGetLastError();
+          hip_check(hipEventSynchronize(ev), "hipEventSynchronize(input)");
+        } else {
+          hip_check(q, "hipEventQuery(input)");
+        }
+      } else if (dp->stream() && dp->stream() != stream_) {
+        const hipError_t q = hipStreamQuery(dp->stream());
+        if (q == hipErrorNotReady) {
+          (void)hipGetLastError();
+          hip_check(hipStreamSynchronize(dp->stream()), "hipStreamSynchronize(input)");
+        } else {
+          hip_check(q, "hipStreamQuery(input)");
+        }
+      }
       in_ptr = dp->bytes();
       rec.input = input;  // held until the round completed
     } else {

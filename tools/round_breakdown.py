@@ -27,17 +27,6 @@ import statistics
 import sys
 
 
-def _workers_from_argv() -> int:
-    for i, t in enumerate(sys.argv):
-        if t == "--P" and i + 1 < len(sys.argv):
-            return int(sys.argv[i + 1])
-    return 2
-
-
-_need = min(32, max(8, 2 * _workers_from_argv() + 4))
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _need:  # raise, never lower
-    os.environ["GPU_MAX_HW_QUEUES"] = str(_need)
-
 import torch  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
