@@ -98,6 +98,7 @@ struct GroupResidentMember {
   uint64_t* dm;              // its device words: [0] go, [2..9] the entry handed to its slice
   const uint32_t* hforce;    // its pinned force / abort words
   const uint32_t* habort;
+  uint64_t* stamps;          // its phase-stamp buffer (study knob; null = off)
   uint32_t seq0;             // the first entry this launch takes
   int rank;
 };

@@ -1509,6 +1509,7 @@ void XgmiComm::launch_group_resident(const std::vector<XgmiComm*>& comms, const 
     a.ctl[y] = comms[y]->ctl_;
     g.m[y] = members[y];
     g.m[y].rank = comms[y]->rank_;
+    g.m[y].stamps = comms[y]->stamp_slots_ >= p0.grid ? comms[y]->stamps_ : nullptr;  // study knob
   }
   a.stamps = nullptr;
   a.delay_rank = -1;

@@ -123,9 +123,13 @@ constexpr int kPhaseSlots = 8;
 struct PhaseStamps {
   uint64_t* out;  // this workgroup's slots in the buffer, or null (uniform)
   uint64_t* lds;  // kPhaseSlots u64 of LDS (thread 0 updates them)
-  __device__ __forceinline__ PhaseStamps(const CommArgs& a, uint64_t* sh) : lds(sh) {
-    out = a.stamps == nullptr ? nullptr
-                              : a.stamps + (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * kPhaseSlots;
+  __device__ __forceinline__ PhaseStamps(const CommArgs& a, uint64_t* sh)
+      : PhaseStamps(a.stamps == nullptr
+                        ? nullptr
+                        : a.stamps + (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * kPhaseSlots,
+                    sh) {}
+  // this workgroup's slots given (a plane group's slice: its worker's own buffer)
+  __device__ __forceinline__ PhaseStamps(uint64_t* slots, uint64_t* sh) : out(slots), lds(sh) {
     if (out != nullptr && threadIdx.x == 0) {
       for (int i = 0; i < kPhaseSlots; ++i) lds[i] = 0;
       lds[0] = wall_ticks();

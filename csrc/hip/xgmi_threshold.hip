@@ -597,6 +597,7 @@ struct RoundVars {
   uint64_t* split_dec;
   uint32_t* split_ctr;
   uint32_t* split_early;
+  uint64_t* stamps;  // this workgroup's phase-stamp slots (null = off)
 };
 
 // A launch's own round of rank a.rank0 + y (threshold_kernel; the resident kernel: y = 0).
@@ -606,7 +607,10 @@ __device__ __forceinline__ RoundVars launch_vars(const CommArgs& a, int y, const
   const int64_t cy = static_cast<int64_t>(y) * a.P * a.nch;
   return RoundVars{in, out, counts ? counts + cy : nullptr, counts_host ? counts_host + cy : nullptr, err_out, done_out,
                    epoch, cold, gate_open, resident, a.rank0 + y, a.ctl[y], a.hforce, a.habort, a.split_dec,
-                   a.split_ctr, a.split_early};
+                   a.split_ctr, a.split_early,
+                   a.stamps == nullptr
+                       ? nullptr
+                       : a.stamps + (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * kPhaseSlots};
 }
 
 // One round of rank a.rank0 + blockIdx.y by the whole grid.
@@ -633,7 +637,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   // waiting for contributions + reduce bodies, [3] scatter + reduce done, [4] ticks waiting
   // in the gather + gather copies,
   // [5] end, [6] scatter done, [7] units gathered
-  PhaseStamps ps(a, ps_lds);
+  PhaseStamps ps(rv.stamps, ps_lds);
   const int P = a.P;
   const int r = rv.rank;
   const char* const in = rv.in;
@@ -1714,7 +1718,8 @@ __global__ __launch_bounds__(kCommThreads) void threshold_group_resident_kernel(
                        m.habort,
                        nullptr,
                        nullptr,
-                       nullptr};
+                       nullptr,
+                       m.stamps == nullptr ? nullptr : m.stamps + static_cast<int64_t>(blockIdx.x) * kPhaseSlots};
     __syncthreads();
     const bool clean = threshold_round<E, FULL>(a, rv);
     if (threadIdx.x == 0) sh_clean = clean ? 1 : 0;
