@@ -99,6 +99,9 @@ struct GroupResidentMember {
   const uint32_t* hforce;    // its pinned force / abort words
   const uint32_t* habort;
   uint64_t* stamps;          // its phase-stamp buffer (study knob; null = off)
+  uint64_t* split_dec;       // its split-chunk scratch (RoundSpec::split_scratch; null = unsplit)
+  uint32_t* split_ctr;
+  uint32_t* split_early;
   uint32_t seq0;             // the first entry this launch takes
   int rank;
 };
@@ -241,8 +244,10 @@ class XgmiComm {
     DType dt = DType::F32;
     int64_t n = 0;
   };
+  // allow_split: a plane group's kernel also runs geometries that split their chunks (a lone
+  // worker launches those)
   ResidentPlan plan_resident(int64_t n, DType dt, float th_reduce, float th_complete, const RoundSpec& spec,
-                             int max_grid) const;
+                             int max_grid, bool allow_split = false) const;
   void launch_resident(const ResidentPlan& p, const ResidentDoor* door, uint32_t* hstate, uint32_t* dm,
                        uint32_t seq, uint32_t gen, uint64_t idle_ticks, hipStream_t stream);
   void round(const void* in, void* out, int64_t n, DType dt, hipStream_t stream, float th_reduce, float th_complete,

@@ -1425,7 +1425,7 @@ void XgmiComm::run_threshold(const std::vector<XgmiComm*>& group, const std::vec
 }
 
 XgmiComm::ResidentPlan XgmiComm::plan_resident(int64_t n, DType dt, float th_reduce, float th_complete,
-                                               const RoundSpec& spec, int max_grid) const {
+                                               const RoundSpec& spec, int max_grid, bool allow_split) const {
   ResidentPlan p;
   auto a = std::make_shared<CommArgs>();
   int gx = 0;
@@ -1433,7 +1433,9 @@ XgmiComm::ResidentPlan XgmiComm::plan_resident(int64_t n, DType dt, float th_red
   if (!threshold_args({self}, {nullptr}, {nullptr}, n, dt, th_reduce, th_complete, nullptr, 1.f, false, &spec,
                       a.get(), &gx))
     return p;
-  if (a->sub > 1 || gx > max_grid || a->delay_rank >= 0) return p;  // split chunks / big rounds / test knobs
+  // split chunks (the spec carried split scratch and the geometry used it) run on the launch
+  // path of a lone worker; a plane group's kernel runs them
+  if ((a->sub > 1 && !allow_split) || gx > max_grid || a->delay_rank >= 0) return p;  // big rounds / test knobs
   p.args = a;
   p.grid = gx;
   p.dt = dt;
@@ -1510,6 +1512,9 @@ void XgmiComm::launch_group_resident(const std::vector<XgmiComm*>& comms, const 
     g.m[y] = members[y];
     g.m[y].rank = comms[y]->rank_;
     g.m[y].stamps = comms[y]->stamp_slots_ >= p0.grid ? comms[y]->stamps_ : nullptr;  // study knob
+    g.m[y].split_dec = b.split_dec;  // each worker's own scratch (its plan's spec)
+    g.m[y].split_ctr = b.split_ctr;
+    g.m[y].split_early = b.split_early;
   }
   a.stamps = nullptr;
   a.delay_rank = -1;

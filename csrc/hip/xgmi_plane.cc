@@ -739,7 +739,11 @@ void XgmiRoundPlane::join_group(const PlaneConfig& cfg) {
   spec.order_ref = o_.order_ref;
   spec.host_force = hforce_dev_;
   spec.host_abort = hforce_dev_ + 1;
-  gplan_ = comm_->plan_resident(cfg.dataSize, o_.dtype, cfg.thReduce, cfg.thComplete, spec, 1 << 20);
+  if (o_.split) {  // few large chunks: slices over several workgroups, as the launch path does
+    spec.split_scratch = split_mem_;
+    spec.split_bytes = split_bytes_;
+  }
+  gplan_ = comm_->plan_resident(cfg.dataSize, o_.dtype, cfg.thReduce, cfg.thComplete, spec, 1 << 20, true);
   if (gplan_.grid <= 0) throw ProtocolError("xgmi plane: this membership's rounds do not fit the group kernel");
   // every slice's workgroups must be resident at once (they wait for each other's rounds):
   // two workgroups per CU over the workers, the PlaneJob default (grid = 512 / workers)
@@ -1130,6 +1134,10 @@ bool XgmiRoundPlane::launch_resident(int round, const Payload& input, bool cold)
   spec.order_ref = o_.order_ref;
   spec.host_force = hforce_dev_;
   spec.host_abort = hforce_dev_ + 1;
+  if (o_.split) {  // a geometry that splits its chunks takes the launch path (plan_resident)
+    spec.split_scratch = split_mem_;
+    spec.split_bytes = split_bytes_;
+  }
   if (!rplan_tried_) {
     rplan_tried_ = true;
     rplan_ = comm_->plan_resident(n, o_.dtype, cfg_.thReduce, cfg_.thComplete, spec, o_.resident_grid);

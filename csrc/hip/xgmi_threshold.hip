@@ -1716,9 +1716,9 @@ __global__ __launch_bounds__(kCommThreads) void threshold_group_resident_kernel(
                        ctl,
                        m.hforce,
                        m.habort,
-                       nullptr,
-                       nullptr,
-                       nullptr,
+                       m.split_dec,
+                       m.split_ctr,
+                       m.split_early,
                        m.stamps == nullptr ? nullptr : m.stamps + static_cast<int64_t>(blockIdx.x) * kPhaseSlots};
     __syncthreads();
     const bool clean = threshold_round<E, FULL>(a, rv);
