@@ -997,7 +997,11 @@ def main() -> None:
     if engine_ok and not args.no_fused_step:
         log(rank, "fused AdamW step")
         result["fused_adamw_step"] = fused_step(comm, x, y, world, rank, args, dev)
-    if engine_ok and world > 1 and not args.no_sdma:
+    if engine_ok and world > 1 and not args.no_sdma and args.share_device and 2 * world > 12:
+        # every rank's child would open the one shared GPU too: 2 x world processes on it,
+        # past what a rehearsal box admits (16) - on a node it is 2 per GPU
+        result["sdma"] = {"skipped": "share-device rehearsal with more than 6 ranks (2 processes per rank on one GPU)"}
+    elif engine_ok and world > 1 and not args.no_sdma:
         # the copy-engine allreduce across the GPUs, first in child processes (a fault there
         # cannot cost this line); validated on every rank -> the DP tuner may use it too
         from akka_allreduce_1_amd.parallel.comm import free_port

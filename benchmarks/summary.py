@@ -212,7 +212,9 @@ def compact(result: dict, detail_path: str | None = None) -> dict:
                                 **{P: rk[P].get("frac_copy_roofline") for P in ("P2", "P4", "P8")
                                    if isinstance(rk.get(P), dict)}}
     x = result.get("sdma")
-    if isinstance(x, dict):  # N > 1: the copy-engine allreduce across the GPUs (child processes)
+    if isinstance(x, dict) and "skipped" in x:
+        out["sdma"] = {"skipped": str(x["skipped"])[:60]}
+    elif isinstance(x, dict):  # N > 1: the copy-engine allreduce across the GPUs (child processes)
         out["sdma"] = {"ok": x.get("validated"), "ms": x.get("p50_ms"), "algbw": x.get("algbw")}
         if x.get("errors"):
             out["sdma"]["error"] = str(x["errors"][0])[:100]
