@@ -40,6 +40,7 @@ delays nobody: its late contributions are left out of this step's sums, and with
 """
 from __future__ import annotations
 
+import atexit
 from dataclasses import dataclass, field
 from typing import Iterable, Sequence
 
@@ -49,6 +50,39 @@ from .comm import comm_stream
 
 _ALIGN_BYTES = 16
 
+# CU-masked streams this module created and still holds. Those alive at interpreter exit are
+# destroyed then, while the HIP runtime is still whole: a masked stream left to the runtime's
+# own teardown crashed the process at exit under rocprofv3's library (exit status 139).
+_LIVE_MASKED: set[int] = set()
+_ATEXIT = [False]
+
+
+def _masked_stream(device_index: int, cus: int, exclude: bool) -> int:
+    from .._native import C
+
+    raw = C.hip.stream_create_cu_mask(device_index, cus, exclude)
+    if not _ATEXIT[0]:
+        atexit.register(_destroy_live_masked)
+        _ATEXIT[0] = True
+    _LIVE_MASKED.add(raw)
+    return raw
+
+
+def _release_masked(raw: int) -> None:
+    if raw in _LIVE_MASKED:
+        _LIVE_MASKED.discard(raw)
+        from .._native import C
+
+        C.hip.stream_destroy(raw)
+
+
+def _destroy_live_masked() -> None:
+    for raw in list(_LIVE_MASKED):
+        try:
+            _release_masked(raw)
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
 
 def compute_stream_excluding(device, cus: int) -> "torch.cuda.ExternalStream":
     """A stream on every CU of `device` except the `cus` CUs a "cuN:" comm schedule uses (the
@@ -56,10 +90,8 @@ def compute_stream_excluding(device, cus: int) -> "torch.cuda.ExternalStream":
     backward under `with torch.cuda.stream(s):` and the GEMMs never share a CU with the
     overlapped collective - a GEMM otherwise waits for its slowest tile, and a tile on a CU
     beside a spinning comm workgroup is slow. The stream lives as long as the process."""
-    from .._native import C
-
     dev = torch.device(device)
-    raw = C.hip.stream_create_cu_mask(dev.index if dev.index is not None else torch.cuda.current_device(), cus, True)
+    raw = _masked_stream(dev.index if dev.index is not None else torch.cuda.current_device(), cus, True)
     return torch.cuda.ExternalStream(raw, device=dev)
 
 
@@ -201,9 +233,7 @@ class BucketedGradReducer:
             return
         if cus:
             if cus not in self._masked:
-                from .._native import C
-
-                raw = C.hip.stream_create_cu_mask(self.device.index, cus)
+                raw = _masked_stream(self.device.index, cus, False)
                 self._masked[cus] = (raw, torch.cuda.ExternalStream(raw, device=self.device))
             raw, ext = self._masked[cus]
             prev_raw = self._comm_raw
@@ -422,9 +452,7 @@ class BucketedGradReducer:
         self._events = []
         for raw, _ in getattr(self, "_masked", {}).values():
             try:
-                from .._native import C
-
-                C.hip.stream_destroy(raw)
+                _release_masked(raw)
             except Exception:  # noqa: BLE001 - interpreter shutdown
                 pass
         self._masked = {}
