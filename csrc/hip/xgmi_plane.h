@@ -73,7 +73,8 @@ struct XgmiPlaneOptions {
   // maxChunkSize runs at thresholds 1 with chunks coarsened to the flag granularity (counts
   // reported per reference chunk), and is refused at thresholds < 1 (ProtocolError).
   int64_t min_chunk = 0;
-  // Resident rounds (XgmiComm::launch_resident): rounds of at most this many bytes are posted
+  // Resident rounds of a lone worker (XgmiComm::launch_resident; co-located workers run every
+  // round on their group kernel instead): rounds of at most this many bytes are posted
   // to a kernel that stays on the plane stream between rounds instead of one launch each
   // (0 = off; MXAR_PLANE_RESIDENT). The kernel leaves after `resident_idle_us` without a
   // round (MXAR_PLANE_RESIDENT_IDLE_US) and is launched again by the next one. Rounds whose
