@@ -89,7 +89,7 @@ def _lat(lvs: dict) -> dict:
         rows = []
         for c in cells:
             best = c.get("best")
-            th = c.get("threshold_ll") or c.get("threshold") or {}
+            th = c.get("threshold") or {}
             rows.append([c.get("bytes"), best, (c.get(best) or {}).get("p50_us"), th.get("p50_us")])
         out[P] = rows
         if lvs.get(f"{P}_all_validated") is False:

@@ -543,7 +543,6 @@ void bind_hip(py::module_& m) {
       .def_property("fence", &XgmiComm::fence, &XgmiComm::set_fence)
       .def_property("units_per_wg", &XgmiComm::units_per_wg, &XgmiComm::set_units_per_wg)
       .def_property("ring_depth", &XgmiComm::ring_depth, &XgmiComm::set_ring_depth)
-      .def_property("threshold_ll_max", &XgmiComm::threshold_ll_max, &XgmiComm::set_threshold_ll_max)
       .def("set_timeout", &XgmiComm::set_timeout)
       .def(
           "set_phase_stamps",

@@ -357,8 +357,6 @@ class XgmiComm {
   int units_per_wg() const { return units_per_wg_; }
   void set_units_per_wg(int u) { units_per_wg_ = u > 0 ? u : 0; }
   int ring_depth() const { return ring_depth_; }
-  int64_t threshold_ll_max() const { return thr_ll_max_; }
-  void set_threshold_ll_max(int64_t b) { thr_ll_max_ = b > 0 ? b : 0; }
   void set_ring_depth(int d) { ring_depth_ = d > 0 ? d : 1; }
   void set_fence(int f) { fence_ = f & 3; }
   // Study knob: per-workgroup phase stamps of the two-shot / ring kernels (xgmi_device.h
@@ -430,11 +428,6 @@ class XgmiComm {
   int default_grid_ = 0;
   bool size_grid_ = true;
   int launch_grid(int64_t bytes_in_launch, bool oneshot, int64_t full_at = int64_t{512} << 20) const;
-  // Threshold rounds up to this many bytes per rank run low-latency (MXAR_THRESHOLD_LL_MAX).
-  // Off by default: measured slower than the fenced hand-offs (8 logical ranks x 4 KiB:
-  // 22 vs 13 us per round; the peers' unfenced write-through units became visible ~5 us after
-  // their flags - profiles/round4/README.md).
-  int64_t thr_ll_max_ = 0;   // ring: workgroups per launch on this device, all ranks of it (MXAR_RING_GRID)
   char* slab_ = nullptr;            // own fine-grained slab (flags | S | R | LL)
   uint32_t* ctl_ = nullptr;         // [0] epoch, [1] ticket, [2] sticky error (device memory)
   char* peers_[kMaxRanks] = {};     // slab base of every rank (own included)

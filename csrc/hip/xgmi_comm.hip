@@ -663,7 +663,6 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   if (const char* u = study_env("MXAR_TWOSHOT_SUB")) sub_max_ = std::max(1, std::atoi(u));
   if (const char* d = study_env("MXAR_RING_DEPTH")) ring_depth_ = std::max(1, std::atoi(d));
   if (const char* g = std::getenv("MXAR_RING_GRID")) ring_grid_ = std::max(1, std::atoi(g));
-  if (const char* t = std::getenv("MXAR_THRESHOLD_LL_MAX")) thr_ll_max_ = std::max<int64_t>(0, std::atoll(t));
   if (const char* d = study_env("MXAR_TWOSHOT_DYNAMIC")) dynamic_ = std::atoi(d) != 0;
   if (const char* f = study_env("MXAR_RING_FLAGS")) {
     // the round-3 layout whose flag words had two writers (ring hop rows vs other kernels'
@@ -853,17 +852,6 @@ void XgmiComm::reset_local() {
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
   hip_check(hipMemset(slab_, 0, off_S_), "hipMemset(flags)");
   hip_check(hipMemset(slab_ + off_LL_, 0, 2 * world_ * ll_slot_), "hipMemset(ll)");
-  if (rows_ > 1) {
-    // Threshold rows hold low-latency rounds' {payload, epoch} units (xgmi_threshold.hip):
-    // the epochs restart below, so a stale unit must not carry one of the coming epochs. LL
-    // rounds only use the head of each slot (<= 2 x thr_ll_max_ / world + count units).
-    const int64_t head = std::min<int64_t>(slot_bytes_, 4 * std::max<int64_t>(thr_ll_max_, 64 * 1024));
-    const int64_t nslots = static_cast<int64_t>(rows_ - 1) * world_;
-    hip_check(hipMemset2D(slab_ + off_S_ + static_cast<int64_t>(world_) * slot_stride_, slot_stride_, 0, head, nslots),
-              "hipMemset2D(threshold S rows)");
-    hip_check(hipMemset2D(slab_ + off_R_ + static_cast<int64_t>(world_) * slot_stride_, slot_stride_, 0, head, nslots),
-              "hipMemset2D(threshold R rows)");
-  }
   hip_check(hipMemset(ctl_, 0, 256), "hipMemset(ctl)");
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
 }
@@ -1327,14 +1315,6 @@ bool XgmiComm::threshold_args(const std::vector<XgmiComm*>& group, const std::ve
     const int per = std::max(1, gx / (W - 1));  // groups per destination block
     a.sgroup = static_cast<int>(std::min<int64_t>(64, std::max<int64_t>(1, ceil_div(a.nch, per))));
   }
-  // Low-latency round (xgmi_threshold.hip, a.ll): small unsplit rounds move {payload, epoch}
-  // units with no fence per hand-off; a chunk takes (its 8-B units + a count unit) x 16 B of a
-  // slot, so the LL layout needs about twice the block
-  {
-    const int64_t upc = ceil_div(a.chunk * es, 8);
-    a.ll_cstride = (upc + 1) * 16;
-    a.ll = (a.sub <= 1 && n * es <= c0.thr_ll_max_ && a.nch * a.ll_cstride <= c0.slot_bytes_) ? 1 : 0;
-  }
   if (ceil_div(static_cast<int64_t>(W - 1) * a.nch * a.sub, gx) > kThresholdGatherUnits)
     throw std::invalid_argument("allreduce_threshold: more than " + std::to_string(kThresholdGatherUnits) +
                                 " gather units per workgroup (too many chunks for the grid)");
@@ -1479,7 +1459,7 @@ void XgmiComm::round(const void* in, void* out, int64_t n, DType dt, hipStream_t
 static bool same_round_shape(const CommArgs& b, const CommArgs& a0) {
   bool same = b.n == a0.n && b.block == a0.block && b.chunk == a0.chunk && b.subchunk == a0.subchunk &&
               b.nch == a0.nch && b.sub == a0.sub && b.sgroup == a0.sgroup && b.P == a0.P && b.rows == a0.rows &&
-              b.ll == a0.ll && b.ll_cstride == a0.ll_cstride && b.full == a0.full && b.min_reduce == a0.min_reduce &&
+              b.full == a0.full && b.min_reduce == a0.min_reduce &&
               b.min_complete == a0.min_complete && b.maxch == a0.maxch && b.off_S == a0.off_S && b.off_R == a0.off_R &&
               b.slot_bytes == a0.slot_bytes && b.order_ref == a0.order_ref && b.fence == a0.fence &&
               b.gate_shortcut == a0.gate_shortcut && b.scale == a0.scale && b.rescale == a0.rescale &&

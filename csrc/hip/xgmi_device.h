@@ -60,11 +60,6 @@ struct CommArgs {
   int32_t* counts_host;
   // low-latency one-shot (xgmi_ll.hip): slots [parity][src] of ll_slot bytes at off_LL
   int64_t off_LL, ll_slot;
-  // threshold kernel, low-latency rounds (xgmi_threshold.hip): S / R slot chunks carry
-  // {payload, epoch} words - no release / acquire fence per hand-off; chunk c sits at
-  // c * ll_cstride bytes of a slot (its payload units, then one {count, epoch} unit)
-  int ll;
-  int64_t ll_cstride;
   // fused reduce-scatter + AdamW + all-gather (xgmi_adam.hip): per rank fp32 shard state
   float* opt_p[kMaxRanks];
   float* opt_m[kMaxRanks];

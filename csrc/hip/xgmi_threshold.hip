@@ -219,150 +219,6 @@ __device__ __attribute__((noinline)) void zero_fill(char* dst, int64_t len) {
   for (int64_t t = threadIdx.x; t < len; t += kCommThreads) st_scalar_wt<E>(rd, t, 0.f);
 }
 
-// ---------------------------------------------------------------------------------
-// Low-latency rounds (a.ll, small rounds, unsplit chunks). The scatter contributions and
-// the reduced chunks travel as 16-B stores of two {payload u32, epoch u32} words, as the LL
-// one-shot does (xgmi_ll.hip): an aligned 8-B word is delivered whole, so a reader that
-// sees this round's epoch in a word has that word's payload. The per-chunk flags still
-// carry ARRIVAL (the threshold decisions - first min_reduce contributions, tickets, forced
-// rounds - are unchanged and read only flags), but no release fence precedes them and no
-// acquire follows them: a flag may become visible before its data, and the reader then
-// waits word by word for the epoch. A reduced chunk's count travels as one more
-// {count, epoch} unit behind its payload. Chunk c of a slot sits at c * a.ll_cstride.
-// ---------------------------------------------------------------------------------
-constexpr int kAuxSysLd = 17;  // sc0 | sc1 loads: system-coherent, see the peers' xGMI stores
-
-// 8 payload bytes at byte offset `off` of [p, p + nbytes) (zero past the end). The protocol's
-// chunks need not be 8-B aligned (maxChunkSize elements of 2 or 4 bytes): element-wise then.
-__device__ __forceinline__ uint2 ld_payload8(const char* p, int64_t off, int64_t nbytes) {
-  const char* q = p + off;
-  if (off + 8 <= nbytes && (reinterpret_cast<uintptr_t>(q) & 7) == 0) return *reinterpret_cast<const uint2*>(q);
-  uint32_t w[2] = {0u, 0u};
-  const uint16_t* h = reinterpret_cast<const uint16_t*>(q);
-  for (int k = 0; k < 4 && off + 2 * k < nbytes; ++k) w[k >> 1] |= static_cast<uint32_t>(h[k]) << (16 * (k & 1));
-  return make_uint2(w[0], w[1]);
-}
-// Write-through store of 8 payload bytes (the output is handed on at the round's done word).
-__device__ __forceinline__ void st_payload8_wt(char* p, int64_t off, int64_t nbytes, uint2 v) {
-  char* q = p + off;
-  if (off + 8 <= nbytes && (reinterpret_cast<uintptr_t>(q) & 7) == 0) {
-    const __amdgpu_buffer_rsrc_t rd = slab_rsrc(q);
-    __builtin_amdgcn_raw_buffer_store_b32(v.x, rd, 0, 0, kAuxWt);
-    __builtin_amdgcn_raw_buffer_store_b32(v.y, rd, 4, 0, kAuxWt);
-    return;
-  }
-  const __amdgpu_buffer_rsrc_t rd = slab_rsrc(q);
-  const uint32_t w[2] = {v.x, v.y};
-  for (int k = 0; k < 4 && off + 2 * k < nbytes; ++k)
-    __builtin_amdgcn_raw_buffer_store_b16(static_cast<unsigned short>(w[k >> 1] >> (16 * (k & 1))), rd, 2 * k, 0,
-                                          kAuxWt);
-}
-// Unit i of an LL chunk once it holds this round's epoch (bounded: *late on the deadline).
-__device__ __forceinline__ uint2 ll_wait(__amdgpu_buffer_rsrc_t rs, int64_t i, uint32_t epoch, uint64_t deadline,
-                                         bool* late) {
-  Pack16 v = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(i * 16), 0, kAuxSysLd);
-  while ((v[1] != epoch || v[3] != epoch) && !*late) {
-    __builtin_amdgcn_s_sleep(1);
-    v = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(i * 16), 0, kAuxSysLd);
-    if (wall_ticks() > deadline) *late = true;
-  }
-  return make_uint2(v[0], v[2]);
-}
-template <class E>
-__device__ __forceinline__ void ll_push(char* dst, const char* src, int64_t len, uint32_t epoch) {
-  constexpr int es = 16 / E::ELEMS;
-  const int64_t nb = len * es, units = (nb + 7) / 8;
-  const __amdgpu_buffer_rsrc_t rd = slab_rsrc(dst);
-  for (int64_t i = threadIdx.x; i < units; i += kCommThreads) {
-    const uint2 d = ld_payload8(src, i * 8, nb);
-    Pack16 v;
-    v[0] = d.x;
-    v[1] = epoch;
-    v[2] = d.y;
-    v[3] = epoch;
-    st16_wt(rd, static_cast<uint32_t>(i * 16), v);
-  }
-}
-// reduce_masked for an LL round: contributions s != r from the own S row (LL units at
-// s_chunk + s * slot), the own from the input; the sum (fixed order s = 0..P-1, fp32) to the
-// own output (when own_out) and as LL units + a {count, epoch} unit into every peer's R slot.
-template <class E>
-__device__ __forceinline__ void ll_reduce(const CommArgs& a, int P, int r, uint32_t mask, const char* own_in,
-                                          int64_t s_chunk, int64_t slot, char* own_out, int64_t roff, int64_t len,
-                                          float scale, uint32_t epoch, uint32_t cnt, uint64_t deadline,
-                                          uint32_t* err) {
-  constexpr int es = 16 / E::ELEMS;
-  const int64_t nb = len * es, units = (nb + 7) / 8;
-  bool late = false;
-  constexpr int B = 8;  // contributions in flight per lane: one load latency per batch, not per source
-  for (int64_t i = threadIdx.x; i < units; i += kCommThreads) {
-    Acc8<E> acc;
-    for (int s0 = 0; s0 < P; s0 += B) {
-      Pack16 v[B];
-#pragma unroll
-      for (int b = 0; b < B; ++b) {
-        const int s = s0 + b;
-        if (s < P && s != r && ((mask >> s) & 1u))
-          v[b] = __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc(a.base[r] + s_chunk + s * slot),
-                                                       static_cast<int>(i * 16), 0, kAuxSysLd);
-      }
-#pragma unroll
-      for (int b = 0; b < B; ++b) {  // fixed order s = 0..P-1
-        const int s = s0 + b;
-        if (s >= P || !((mask >> s) & 1u)) continue;
-        if (s == r) {
-          acc.add(ld_payload8(own_in, i * 8, nb));
-        } else {
-          uint2 d = make_uint2(v[b][0], v[b][2]);
-          if (v[b][1] != epoch || v[b][3] != epoch)
-            d = ll_wait(slab_rsrc(a.base[r] + s_chunk + s * slot), i, epoch, deadline, &late);
-          acc.add(d);
-        }
-      }
-    }
-    const uint2 o = acc.pack(scale);
-    if (own_out != nullptr) st_payload8_wt(own_out, i * 8, nb, o);
-    Pack16 v;
-    v[0] = o.x;
-    v[1] = epoch;
-    v[2] = o.y;
-    v[3] = epoch;
-    for (int k = 0; k < P; ++k)
-      if (k != r) st16_wt(slab_rsrc(a.base[k] + roff), static_cast<uint32_t>(i * 16), v);
-  }
-  if (static_cast<int>(threadIdx.x) < P && static_cast<int>(threadIdx.x) != r) {
-    Pack16 v;
-    v[0] = cnt;
-    v[1] = epoch;
-    v[2] = cnt;
-    v[3] = epoch;
-    st16_wt(slab_rsrc(a.base[threadIdx.x] + roff), static_cast<uint32_t>(units * 16), v);
-  }
-  if (late) __hip_atomic_fetch_or(err, ERR_TIMEOUT_SCATTER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-// Copy a reduced LL chunk to the output; with `count`, lane 0 also returns the chunk's
-// count unit (loaded next to the payload, not after it).
-template <class E>
-__device__ __forceinline__ int32_t ll_copy_out(char* dst, const char* src_chunk, int64_t len, uint32_t epoch,
-                                               uint64_t deadline, uint32_t* err, bool count) {
-  constexpr int es = 16 / E::ELEMS;
-  const int64_t nb = len * es, units = (nb + 7) / 8;
-  const __amdgpu_buffer_rsrc_t rs = slab_rsrc(src_chunk);
-  bool late = false;
-  const bool lane0 = count && threadIdx.x == 0;
-  Pack16 cv;
-  if (lane0) cv = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(units * 16), 0, kAuxSysLd);
-  for (int64_t i = threadIdx.x; i < units; i += kCommThreads) st_payload8_wt(dst, i * 8, nb, ll_wait(rs, i, epoch, deadline, &late));
-  int32_t cnt = 0;
-  if (lane0) {
-    uint2 d = make_uint2(cv[0], cv[2]);
-    if (cv[1] != epoch || cv[3] != epoch) d = ll_wait(rs, units, epoch, deadline, &late);
-    cnt = late ? 0 : static_cast<int32_t>(d.x);
-  }
-  if (late) __hip_atomic_fetch_or(err, ERR_TIMEOUT_REDUCE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  return cnt;
-}
-
 // reduce_masked for unaligned protocol geometry: element by element (inline: an out-of-line
 // function taking the kernel's CommArgs would copy them to scratch)
 template <class E>
@@ -616,9 +472,9 @@ __device__ __forceinline__ RoundVars launch_vars(const CommArgs& a, int y, const
 // One round of rank a.rank0 + blockIdx.y by the whole grid.
 // Returns true when this workgroup's round took every peer's reduced chunk it gathers, with
 // nothing forced, cold or given up (the resident kernel's lag-gate shortcut).
-// FULL: a compile-time full-threshold round (thReduce = thComplete = 1, unsplit chunks, no
-// LL units - the DP communicator's exact lag-tolerant allreduce and most protocol rounds).
-// Snapshot, tickets, split-chunk agreement and the LL unit paths fold away: less than half
+// FULL: a compile-time full-threshold round (thReduce = thComplete = 1, unsplit chunks - the
+// DP communicator's exact lag-tolerant allreduce and most protocol rounds).
+// Snapshot, tickets and split-chunk agreement fold away: less than half
 // the code of the general kernel, whose instruction fetch a small round otherwise pays from
 // L2 on every cold CU (51 KB of code vs 21 KB for the 8-rank two-shot).
 template <class E, bool FULL>
@@ -664,7 +520,6 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   // output tickets (one device-scope atomic per unit) change the result: both are skipped.
   // Forced rounds still exclude their own force-reduced chunks (reference order).
   const bool full = FULL || a.full != 0;
-  const bool ll = !FULL && a.ll != 0;  // low-latency round: {payload, epoch} units, no fences (host: unsplit only)
   const bool snap = ref && !cold && !full;  // cold rounds are forced from the start: no snapshot
   const bool tickets = !full;
   // work units: S slices per chunk (S = 1: a unit is a chunk). Scatter / gather unit
@@ -869,17 +724,6 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         const int64_t bstart = static_cast<int64_t>(j) * a.block;
         const int64_t cstart = static_cast<int64_t>(c0) * a.chunk;
         const int64_t len = clamp_len(clamp_len(a.n - bstart, a.block) - cstart, static_cast<int64_t>(ncg) * a.chunk);
-        if (ll) {
-          const int64_t blen = clamp_len(a.n - bstart, a.block);
-          for (int i = 0; i < ncg; ++i) {
-            const int64_t cl = clamp_len(blen - static_cast<int64_t>(c0 + i) * a.chunk, a.chunk);
-            if (cl > 0)
-              ll_push<E>(a.base[j] + rowS + r * slot + static_cast<int64_t>(c0 + i) * a.ll_cstride,
-                         in + (bstart + static_cast<int64_t>(c0 + i) * a.chunk) * es, cl, epoch);
-          }
-          publish_flags([&](int i) { return f1(a, j, row * P + r, c0 + i); }, ncg, epoch, false);
-          continue;
-        }
         if (len > 0) copy_in<E>(a.base[j] + rowS + r * slot + cstart * es, in + (bstart + cstart) * es, len);
         publish_flags([&](int i) { return f1(a, j, row * P + r, c0 + i); }, ncg, epoch, rel);
       }
@@ -977,7 +821,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
           }
         }
       }
-      if (acq && !ll) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      if (acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
@@ -987,14 +831,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     const int cnt = __popc(mask);
     const float sc = (a.rescale && cnt > 0) ? a.scale * static_cast<float>(P) / static_cast<float>(cnt) : a.scale;
     char* own_out = out + (bstart_own + cstart) * es;
-    if (ll) {
-      if (len > 0) {
-        ll_reduce<E>(a, P, r, mask, in + (bstart_own + cstart) * es, rowS + static_cast<int64_t>(c) * a.ll_cstride, slot,
-                     take ? own_out : nullptr, rowR + r * slot + static_cast<int64_t>(c) * a.ll_cstride, len, sc,
-                     epoch, static_cast<uint32_t>(cnt), deadline, err);
-        if (!take) zero_fill<E>(own_out, len);
-      }
-    } else if (len > 0) {
+    if (len > 0) {
       reduce_masked<E>(a, P, r, mask, in + (bstart_own + cstart) * es, a.base[r] + rowS + cstart * es, slot,
                        take ? own_out : nullptr, rowR + r * slot + cstart * es, len,
                        (a.fence & 1) || rv.done_out != nullptr, sc);
@@ -1008,8 +845,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       if (counts) cput(static_cast<int64_t>(r) * a.nch + c, take ? cnt : 0);
       if (!ref && tickets && blen_own - static_cast<int64_t>(c) * a.chunk > 0) add_ctl(&ctl[3], 1u);
     }
-    publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : f2(a, k, row * P + r, c); }, P, epoch,
-                  rel && !ll);
+    publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : f2(a, k, row * P + r, c); }, P, epoch, rel);
     ps.add(2, t_body);
   }
 
@@ -1044,7 +880,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         }
         const uint64_t m = __ballot(arr);
         if (threadIdx.x == 0) sh_arr = m;
-        if (m && acq && !ll) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        if (m && acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
@@ -1086,12 +922,8 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
             add_ctl(&ctl[3], 1u);
           }
           if (!adopt) {
-            if (counts) {
-              // an LL chunk's count travels with its payload: stored after the copy below
-              if (!(take && ll))
-                cput(static_cast<int64_t>(j) * a.nch + c,
-                          take ? static_cast<int32_t>(ld_flag(f2c(a, r, row * P + j, c))) : 0);
-            }
+            if (counts)
+              cput(static_cast<int64_t>(j) * a.nch + c, take ? static_cast<int32_t>(ld_flag(f2c(a, r, row * P + j, c))) : 0);
             if (split) dec_publish(dec, epoch, take != 0, 0u);
           }
           sh_flag = take;
@@ -1107,12 +939,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
                                       sub);
         const uint64_t t_copy = ps.now();  // stamp [4] also holds the gather copies
         if (len > 0) {
-          if (take && ll) {
-            const int32_t cv = ll_copy_out<E>(out + (bstart + cstart) * es,
-                                              a.base[r] + rowR + j * slot + static_cast<int64_t>(c) * a.ll_cstride, len,
-                                              epoch, deadline, err, counts != nullptr);
-            if (counts != nullptr && threadIdx.x == 0) cput(static_cast<int64_t>(j) * a.nch + c, cv);
-          } else if (take)
+          if (take)
             copy_out<E>(out + (bstart + cstart) * es, a.base[r] + rowR + j * slot + cstart * es, len);
           else
             zero_fill<E>(out + (bstart + cstart) * es, len);
@@ -1746,7 +1573,7 @@ __global__ __launch_bounds__(64) void publish_progress_kernel(CommArgs a, uint32
 }
 
 // the compile-time full-threshold kernel applies (threshold_round FULL)
-static bool full_fast(const CommArgs& a) { return a.full != 0 && a.sub <= 1 && a.ll == 0; }
+static bool full_fast(const CommArgs& a) { return a.full != 0 && a.sub <= 1; }
 
 void launch_publish_progress(const CommArgs& a, uint32_t value, hipStream_t s) {
   hipLaunchKernelGGL(publish_progress_kernel, dim3(1), dim3(64), 0, s, a, value);

@@ -41,20 +41,11 @@ def _blocks(n, P, nch, dtype):
     return block, chunk
 
 
-def _low_latency(cl, on):
-    """Opt the cluster's threshold rounds into the low-latency ({payload, epoch} unit) form."""
-    if on:
-        for c in cl.comms:
-            c.threshold_ll_max = 1 << 20
-
-
-@pytest.mark.parametrize("ll", [False, True])
 @pytest.mark.parametrize("P", [2, 4, 8])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("max_lag", [0, 2])
-def test_threshold_one_is_exact(P, dtype, max_lag, ll):
+def test_threshold_one_is_exact(P, dtype, max_lag):
     cl = LocalCluster(P, slot_bytes=1 << 20, grid=64, timeout_s=10.0, max_lag=max_lag)
-    _low_latency(cl, ll)
     for it in range(4):  # cycles through the lag-ring rows
         n = [100_003, 4096, 777][it % 3]
         xs = [fill_uniform(torch.empty(n, dtype=dtype, device=DEV), seed=31 * it + k) for k in range(P)]
@@ -68,12 +59,10 @@ def test_threshold_one_is_exact(P, dtype, max_lag, ll):
     assert cl.comms[0].stats.threshold == 4
 
 
-@pytest.mark.parametrize("ll", [False, True])
 @pytest.mark.parametrize("P", [3, 4])
-def test_straggler_is_left_out_and_its_block_given_up(P, ll):
+def test_straggler_is_left_out_and_its_block_given_up(P):
     slow = P - 1
     cl = LocalCluster(P, slot_bytes=1 << 20, grid=32, timeout_s=10.0, max_lag=0)
-    _low_latency(cl, ll)
     cl.comms[0].set_straggler(slow, 5000.0)  # 5 ms idle at the start of the slow rank
     th = (P - 1) / P
     n = 50_001
