@@ -774,7 +774,10 @@ void XgmiRoundPlane::join_group(const PlaneConfig& cfg) {
   }
   rstate_[1] = res_seq_ - 1u;  // every entry before res_seq_ was taken (or dropped) before
   std::lock_guard<std::mutex> lk(g->mu);
-  if (g->state[static_cast<size_t>(idx)] != PlaneGroup::kPending)
+  // (a worker that left this membership's group may join it again - the same InitWorkers
+  // delivered twice; a kernel launched meanwhile does not serve it and leaves before one that
+  // does is launched, PlaneGroup::ensure)
+  if (g->state[static_cast<size_t>(idx)] == PlaneGroup::kJoined && g->planes[static_cast<size_t>(idx)] != this)
     throw ProtocolError("xgmi plane: two workers of one membership claim the same group slot");
   g->planes[static_cast<size_t>(idx)] = this;
   g->state[static_cast<size_t>(idx)] = PlaneGroup::kJoined;
