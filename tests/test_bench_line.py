@@ -148,6 +148,16 @@ def test_n8_line_carries_the_link_pack():
     assert d["sdma"] == {"ok": True, "ms": 1.2345, "algbw": 217.45}
 
 
+def test_skipped_sdma_section_says_why():
+    """A share-device rehearsal past 6 ranks skips the SDMA child section (2 processes per rank on
+    one GPU); the line carries the reason instead of an empty or failed result."""
+    r = _n8_shape(_full_n1())
+    r["sdma"] = {"skipped": "share-device rehearsal with more than 6 ranks (2 processes per rank on one GPU)"}
+    d = json.loads(line(r))
+    assert d["sdma"]["skipped"].startswith("share-device rehearsal")
+    assert len(json.dumps(d)) <= LINE_BUDGET
+
+
 def test_link_pack_outlives_every_other_section():
     r = _n8_shape(_full_n1())
     r["xgmi_links"] = _links()
