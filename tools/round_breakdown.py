@@ -106,6 +106,7 @@ def main() -> None:
     ap.add_argument("--spin-us", type=int, default=1000)
     ap.add_argument("--trace-out", default=None, help="also write the Chrome trace here")
     ap.add_argument("--no-trace", action="store_true", help="round time only, without the tracer's own cost")
+    ap.add_argument("--stamps-out", default=None, help="also write the last round's raw per-workgroup stamps here")
     a = ap.parse_args()
     from akka_allreduce_1_amd._native import C
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -143,6 +144,9 @@ def main() -> None:
             row["kernel_last_round_us"] = {f"w{p['worker']}": round(p["end_max"] - p["start_first"], 1) for p in ph
                                            if "end_max" in p}
             row["kernel_phases"] = ph
+            if a.stamps_out:
+                with open(a.stamps_out, "w") as f:
+                    json.dump([b.view(-1, 8).cpu().tolist() for b in bufs], f)
         except ValueError:  # no stamps written (e.g. a plane without a stamp buffer)
             row["kernel_last_round_us"] = None
         row["resident_rounds"] = [p.stats.resident_rounds for p in job.planes]
