@@ -34,6 +34,18 @@ from .ops.kernels import dtype_code
 _HUBS = itertools.count()
 
 
+def default_plane_grid(device: int, share: int) -> int:
+    """Workgroups per round kernel of a plane worker when `share` workers run on `device`.
+
+    One worker per GPU: 2 per CU (the plane's own default). Co-located workers split
+    the CUs: together they run about one workgroup per CU, so every worker's kernel stays
+    resident beside the others. The plane also coarsens full-threshold rounds to one chunk
+    per workgroup. 2 workers x 128 workgroups beat 2 x 256 by 8-30 % per round at
+    16-256 MiB (profiles/round5/protocol_grid_chunk.jsonl)."""
+    cus = torch.cuda.get_device_properties(device).multi_processor_count if torch.cuda.is_available() else 256
+    return 2 * cus if share <= 1 else max(8, cus // share)
+
+
 def iota_source(n: int, device: torch.device, dtype: torch.dtype, offset: float = 0.0) -> Callable:
     """The reference's demo dataSource (AllreduceWorker.scala:285-291), data[i] = i + iteration
     (+ offset), produced on the GPU by the fill_iota kernel on torch's current stream."""
@@ -108,8 +120,8 @@ class PlaneJob:
             raise ValueError("one device per worker")
         if plane == "xgmi":
             share = max(self.devices.count(d) for d in set(self.devices))
-            if grid <= 0:  # workers sharing a GPU split its workgroups so every kernel stays resident
-                grid = max(8, 512 // share)
+            if grid <= 0:
+                grid = default_plane_grid(self.devices[0], share)
         self.grid = grid
         self.system = C.ActorSystem("ClusterSystem", False)
         self.finished = threading.Event()

@@ -652,7 +652,11 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
     }
     const int64_t want = ceil_div(int64_t{32} << 10, chunk_ * es);
     const int64_t room = std::max<int64_t>(1, nch / std::max(1, gx / 4));
-    int64_t m = std::min(want, room);
+    // ...and at most one kernel chunk per workgroup: a workgroup that reduces two chunks pays
+    // the second chunk's hand-offs after the first one's, on the round's critical path. 2
+    // co-located workers x 128 workgroups, bf16 (profiles/round5/protocol_grid_chunk.jsonl):
+    // 64 MiB 159-164 -> 145-149 us per round, 16 MiB 86-95 -> 74-75, 256 MiB 441-474 -> 426-454
+    int64_t m = std::max(std::min(want, room), ceil_div(nch, std::max(1, gx)));
     // a block of at most 32 KiB is ONE kernel chunk: one hand-off per peer instead of one per
     // chunk - each hand-off is a release, a flag and a wait on the round's critical path, and
     // below 32 KiB there are no bytes to spread over more workgroups (the reference's

@@ -71,6 +71,14 @@ def main() -> None:
             st = buf.view(-1, SLOTS).cpu()
             used = st[st[:, 0] > 0]
             t0 = int(used[:, 0].min())
+            # slot = blockIdx.y * gridDim.x + blockIdx.x = the linear workgroup id, which the
+            # dispatcher deals round-robin over the 8 XCDs: XCD = slot % 8
+            idx = torch.nonzero(st[:, 0] > 0).flatten()
+            by_xcd = {}
+            for x in range(8):
+                sel = used[(idx % 8) == x]
+                if len(sel):
+                    by_xcd[x] = round(float((sel[:, 5] - sel[:, 0]).double().median()) / 100.0, 1)
             us = lambda v: float(v) / 100.0  # noqa: E731 - 100 MHz ticks -> us
             rows.append({
                 "span_us": us(int(used[:, 5].max()) - t0),
@@ -82,11 +90,13 @@ def main() -> None:
                 "stamp6": [us(int(x) - t0) if algo == "threshold" else float(x) for x in used[:, 6]],
                 "end_us": [us(int(x) - t0) for x in used[:, 5]],
                 "workgroups": int(used.shape[0]),
+                "span_by_xcd_us": by_xcd,
             })
         cl.check()
         span = [r["span_us"] for r in rows]
         best = rows[span.index(sorted(span)[len(span) // 2])]  # the median launch
-        summ = {"span_us": stats(span), "start_skew_us": best["start_skew_us"], "workgroups": best["workgroups"]}
+        summ = {"span_us": stats(span), "start_skew_us": best["start_skew_us"], "workgroups": best["workgroups"],
+                "span_by_xcd_us": best["span_by_xcd_us"]}
         for k in ("scatter_end_us", "reduce_wait_us", "reduce_end_us", "gather_wait_us", "end_us", "stamp6"):
             summ[k] = stats(best[k])
         summ["hbm_TBps_at_span_p50"] = round(hbm_bytes(S, a.P, "twoshot" if algo == "threshold" else algo, 2) / (summ["span_us"]["p50"] * 1e-6) / 1e12, 3)

@@ -106,6 +106,8 @@ def main() -> None:
     ap.add_argument("--spin-us", type=int, default=1000)
     ap.add_argument("--trace-out", default=None, help="also write the Chrome trace here")
     ap.add_argument("--no-trace", action="store_true", help="round time only, without the tracer's own cost")
+    ap.add_argument("--grid", type=int, default=0, help="workgroups per worker (0: PlaneJob's default)")
+    ap.add_argument("--no-split", action="store_true", help="PlaneJob(split=False): one workgroup per chunk")
     ap.add_argument("--stamps-out", default=None, help="also write the last round's raw per-workgroup stamps here")
     a = ap.parse_args()
     from akka_allreduce_1_amd._native import C
@@ -120,14 +122,15 @@ def main() -> None:
     xs = [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=k) for k in range(a.P)]
     ref = sum(x.float() for x in xs).to(dtype)
     job = PlaneJob(a.P, n, max_chunk_size=a.chunk or 1024, dtype=dtype, max_round=a.rounds - 1, timeout_s=10.0,
-                   spin_us=a.spin_us, sources=xs, keep_outputs=False, keep_last=True)
+                   spin_us=a.spin_us, sources=xs, keep_outputs=False, keep_last=True, split=not a.no_split,
+                   grid=a.grid)
     bufs = [torch.zeros(job.grid * 8, dtype=torch.int64, device=dev) for _ in job.planes]
     for p, b in zip(job.planes, bufs):
         p.set_phase_stamps(b.data_ptr(), job.grid)
     C.trace.clear()
     C.trace.enable(not a.no_trace)
     row = {"P": a.P, "bytes": S, "dtype": a.dtype, "max_chunk_size": a.chunk or 1024, "rounds": a.rounds,
-           "spin_us": a.spin_us, "dispatch_spin_us": os.environ.get("MXAR_DISPATCH_SPIN_US", "default")}
+           "spin_us": a.spin_us, "split": not a.no_split, "grid": job.grid, "dispatch_spin_us": os.environ.get("MXAR_DISPATCH_SPIN_US", "default")}
     try:
         job.run(timeout=120.0)
         C.trace.enable(False)
