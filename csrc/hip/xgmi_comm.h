@@ -261,6 +261,8 @@ class XgmiComm {
                                     uint32_t gen, uint64_t idle_ticks, hipStream_t stream);
   // Workgroups a round launch of `nch` chunks per block uses (counts / geometry checks).
   int round_grid(int nch) const;
+  // Workgroups per rank at most when several ranks share one launch (default grid only).
+  int shared_launch_cap(int ranks_here) const;
   // Chunks per block the threshold kernel uses for n elements (size of `counts` = P * this).
   int threshold_chunks(int64_t n, DType dt, int ranks_in_launch = 1) const;
   // Test knob: rank `rank` idles `us` microseconds at the start of each threshold launch.

@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <stdexcept>
 #include <string>
 
@@ -799,6 +800,15 @@ int XgmiComm::launch_grid(int64_t bytes, bool oneshot, int64_t full_at) const {
   return size_grid_rule(bytes, grid_, world_, oneshot, full_at);
 }
 
+int XgmiComm::shared_launch_cap(int ranks_here) const {
+  // Several logical ranks in one launch (one GPU): at most a quarter of the default grid - half
+  // the CUs - per rank at the default grid. 2 ranks x 256 MiB bf16 two-shot 426-436 -> 389-395
+  // us, threshold 432-440 -> 411-414; 4 x 128 MiB 128 per rank beats 64; 8 x 256 MiB equal
+  // (profiles/round5/local_launch_grid.jsonl). One rank per GPU keeps launch_grid's rule.
+  if (ranks_here <= 1 || !size_grid_ || grid_ != default_grid_) return std::numeric_limits<int>::max();
+  return std::max(1, default_grid_ / 4);
+}
+
 static bool capturing(hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
@@ -924,7 +934,8 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   const int gdev = sized ? c0.launch_grid(n * es * ranks_here, oneshot)
                    : (adam_state != nullptr && c0.size_grid_ && c0.grid_ == c0.default_grid_) ? std::min(c0.grid_, 256)
                                                                                             : c0.grid_;
-  const int gmax = std::max(1, gdev / ranks_here);
+  const int gmax = std::min(std::max(1, gdev / ranks_here), kind == Algo::TwoShot ? c0.shared_launch_cap(ranks_here)
+                                                                                  : std::numeric_limits<int>::max());
   int gx;
   a.sub = 1;
   a.off_LL = c0.off_LL_;
@@ -1210,7 +1221,8 @@ void XgmiComm::geometry_threshold(int64_t n, DType dt, int ranks_here, int64_t* 
   const int64_t min_chunk = min_chunk_bytes() / es;
   // launch-size grid as for the two-shot (launch_grid; at the default grid only)
   const int gmax =
-      std::max(1, launch_grid(n * es * std::max(1, ranks_here), false, int64_t{256} << 20) / std::max(1, ranks_here));
+      std::min(std::max(1, launch_grid(n * es * std::max(1, ranks_here), false, int64_t{256} << 20) / std::max(1, ranks_here)),
+               shared_launch_cap(ranks_here));
   *block = round_up(ceil_div(n, world_), elems);
   // one reduce unit (a chunk: one threshold decision) per workgroup; phase 1/3 get P-1 each,
   // spread over up to (P - 1) x nch workgroups when the chunks are few (small tensors)
