@@ -39,7 +39,7 @@ def default_plane_grid(device: int, share: int) -> int:
 
     One worker per GPU: 2 per CU (the plane's own default). Co-located workers split
     the CUs: together they run about one workgroup per CU, so every worker's kernel stays
-    resident beside the others. The plane also coarsens full-threshold rounds to one chunk
+    resident beside the others. Their planes also coarsen full-threshold rounds to one chunk
     per workgroup. 2 workers x 128 workgroups beat 2 x 256 by 8-30 % per round at
     16-256 MiB (profiles/round5/protocol_grid_chunk.jsonl)."""
     cus = torch.cuda.get_device_properties(device).multi_processor_count if torch.cuda.is_available() else 256

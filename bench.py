@@ -558,7 +558,7 @@ def protocol_rounds(args, rank: int, world: int, dev) -> dict:
     worker per GPU process, master on rank 0, control over TCP, data over xGMI.
     rounds_per_s / ms_per_round come from the master's round-barrier stamps after the
     warm-up rounds; algbw = buffer bytes / ms_per_round."""
-    from akka_allreduce_1_amd.engine import PlaneJob, default_plane_grid, distributed_plane_job
+    from akka_allreduce_1_amd.engine import PlaneJob, distributed_plane_job
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     es = 2 if dtype == torch.bfloat16 else 4
@@ -598,7 +598,9 @@ def protocol_rounds(args, rank: int, world: int, dev) -> dict:
         else:
             x = fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=700 + rank)
             last = {}
-            grid = default_plane_grid(dev.index, world) if args.share_device else 0
+            # ranks sharing one GPU (rehearsal): separate kernels, one per process, together two
+            # workgroups per CU (profiles/round5/rehearsal_grid.jsonl: 8 processes x 32 lose to x 64)
+            grid = (args.plane_grid or max(8, 512 // world)) if args.share_device else 0
             log(rank, f"protocol: one plane worker per rank, {rounds} rounds of {args.size_mib} MiB")
             # one GPU per rank: host threads poll through the rounds (--spin-us 500 of the native
             # executables); ranks sharing one GPU (rehearsal) share the box's few CPUs: no polling
@@ -750,6 +752,8 @@ def main() -> None:
                     help="seconds for the DP-step sections; past it the result line is written without them")
     ap.add_argument("--detail-out", default=None,
                     help="side file for the full result dict (default gpurun_out/bench_detail_n<N>.json; '' = none)")
+    ap.add_argument("--plane-grid", type=int, default=0,
+                    help="with --share-device: workgroups per protocol worker (0: 512 / ranks)")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal: every rank on cuda:0 over gloo (RCCL refuses two ranks on one GPU), "
                          "workgroup budget split between the ranks so all spinning workgroups stay resident")

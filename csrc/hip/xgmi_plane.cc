@@ -239,6 +239,7 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   // form; ~2-3 us of hipEventRecord on every launch, profiles/round3/api_cost.json)
   if (const char* e = study_env("MXAR_PLANE_EVENTS")) event_confirm_ = std::atoi(e) != 0;
   if (const char* e = study_env("MXAR_PLANE_COARSEN")) coarsen_full_ = std::atoi(e) != 0;  // A/B knob
+  if (const char* e = study_env("MXAR_PLANE_WG_CHUNKS")) wg_chunks_ = std::max(0, std::atoi(e));  // A/B knob
   if (const char* q = std::getenv("GPU_MAX_HW_QUEUES"); q != nullptr && std::atoi(q) == 1)
     o_.resident_max = 0;  // one hardware queue per process: a resident kernel would hold it for every stream
   if (const char* e = std::getenv("MXAR_PLANE_RESIDENT")) o_.resident_max = std::atoll(e);
@@ -652,11 +653,16 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
     }
     const int64_t want = ceil_div(int64_t{32} << 10, chunk_ * es);
     const int64_t room = std::max<int64_t>(1, nch / std::max(1, gx / 4));
-    // ...and at most one kernel chunk per workgroup: a workgroup that reduces two chunks pays
-    // the second chunk's hand-offs after the first one's, on the round's critical path. 2
-    // co-located workers x 128 workgroups, bf16 (profiles/round5/protocol_grid_chunk.jsonl):
-    // 64 MiB 159-164 -> 145-149 us per round, 16 MiB 86-95 -> 74-75, 256 MiB 441-474 -> 426-454
-    int64_t m = std::max(std::min(want, room), ceil_div(nch, std::max(1, gx)));
+    // ...and, for workers sharing one group kernel, at most one kernel chunk per workgroup: a
+    // workgroup that reduces two chunks pays the second chunk's hand-offs after the first
+    // one's, on the round's critical path. 2 co-located workers x 128 workgroups, bf16
+    // (profiles/round5/protocol_grid_chunk.jsonl): 64 MiB 159-164 -> 145-149 us per round,
+    // 16 MiB 86-95 -> 74-75, 256 MiB 441-474 -> 426-454. A worker alone in its process keeps
+    // the finer chunks: 8 such processes sharing one GPU did not gain from it (noisy,
+    // rehearsal_grid.jsonl), and over xGMI it is unmeasured.
+    int64_t m = std::min(want, room);
+    if (wg_chunks_ > 0 && colocated(cfg).size() > 1)
+      m = std::max(m, ceil_div(nch, static_cast<int64_t>(std::max(1, gx)) * wg_chunks_));
     // a block of at most 32 KiB is ONE kernel chunk: one hand-off per peer instead of one per
     // chunk - each hand-off is a release, a flag and a wait on the round's critical path, and
     // below 32 KiB there are no bytes to spread over more workgroups (the reference's

@@ -1,19 +1,14 @@
-# ad-hoc GPU run: default-grid LocalCluster launches after the shared-launch cap
+# ad-hoc GPU run: final settings - 2 co-located workers (group kernel) and the 8-process rehearsal protocol
 set -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
 mkdir -p gpurun_out
-out=gpurun_out/shared_cap.jsonl
-rm -f $out
-for rep in 0 1; do
-  for cfg in 2:256 2:128 4:128 4:256 8:256 2:64; do
-    IFS=: read P mib <<< "$cfg"
-    timeout -k 10 120 python -u tools/phase_profile.py --P $P --mib $mib --grid 512 --algos twoshot threshold --iters 8 > /tmp/o.jsonl 2>/dev/null || exit 1
-    python3 -c "
-import json
-for l in open('/tmp/o.jsonl'):
-    d=json.loads(l)
-    for k,v in d.items(): print(json.dumps({'rep':$rep,'P':$P,'mib':$mib,'grid':'default','algo':k,'span_p50':v['span_us']['p50'],'wgs':v['workgroups'],'TBps':v['hbm_TBps_at_span_p50']}))
-" >> $out
-  done
+for cfg in 64M:65536 16M:16384; do
+  IFS=: read size c <<< "$cfg"
+  timeout -k 10 120 python -u tools/round_breakdown.py --P 2 --size $size --dtype bf16 --chunk $c --rounds 200 --no-trace > /tmp/o.json 2>/dev/null || exit 1
+  python3 -c "import json;d=json.load(open('/tmp/o.json'));print(json.dumps({'size':'$size','grid':d.get('grid'),'ms':d.get('ms_per_round'),'ok':d.get('validated')}))"
 done
-cat $out
+skip="--no-dp --no-tune --no-rccl --no-threshold --no-collectives --no-fused-step --no-links --no-sdma --no-native --no-sizes"
+timeout -k 10 300 python -u -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+    --master-port $((29700 + RANDOM % 200)) bench.py --gpus 8 --share-device --steps 10 --warmup 3 $skip \
+    > /tmp/r.json 2> gpurun_out/rg_final.err || exit 1
+python3 -c "import json;d=json.load(open('/tmp/r.json'));print(json.dumps({'rehearsal8':d.get('protocol_us'),'value':d.get('value')}))"
