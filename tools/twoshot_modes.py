@@ -74,6 +74,9 @@ def main():
     ap.add_argument("--mib", type=int, default=256)
     ap.add_argument("--P", type=int, default=8)
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--staggers", default="0",
+                    help="comma list of byte offsets: rank k's input / output start k x offset past a "
+                         "multiple of the buffer size inside one allocation (each row tries every one)")
     ap.add_argument("--vary", choices=["both", "io", "slabs"], default="both",
                     help="what is allocated anew per row: everything, only the rank buffers (one "
                          "cluster kept), or only the cluster's slabs (one set of rank buffers kept)")
@@ -99,31 +102,41 @@ def main():
         del x, y
         if k == 0 or a.vary != "io":
             cl = LocalCluster(P, slot_bytes=2 * -(-S // P) + (1 << 20), grid=512, timeout_s=10.0)
-        if k == 0 or a.vary != "slabs":
-            # the previous row's buffers stay alive while these are taken: new pages, not reused ones
-            xs2 = [fill_uniform(torch.empty(n, dtype=torch.bfloat16, device=dev), seed=500 + j) for j in range(P)]
-            ys2 = [torch.empty_like(t) for t in xs2]
-            keep = (xs, ys) if k else None  # noqa: F841 - held until the next row
-            xs, ys = xs2, ys2
+        staggers = [int(v) for v in a.staggers.split(",")]
+        for stg in staggers:
+            if k == 0 or a.vary != "slabs" or len(staggers) > 1:
+                # the previous row's buffers stay alive while these are taken: new pages, not reused ones
+                if stg == 0:
+                    xs2 = [fill_uniform(torch.empty(n, dtype=torch.bfloat16, device=dev), seed=500 + j) for j in range(P)]
+                    ys2 = [torch.empty_like(t) for t in xs2]
+                else:  # one allocation per side, rank j at j x (S + stg) bytes (stg a multiple of 16)
+                    bx = torch.empty(P * (S + stg), dtype=torch.uint8, device=dev)
+                    by = torch.empty_like(bx)
+                    xs2 = [fill_uniform(bx[j * (S + stg):j * (S + stg) + S].view(torch.bfloat16), seed=500 + j)
+                           for j in range(P)]
+                    ys2 = [by[j * (S + stg):j * (S + stg) + S].view(torch.bfloat16) for j in range(P)]
+                keep = (xs, ys) if k else None  # noqa: F841 - held until the next row
+                xs, ys = xs2, ys2
 
-        def ts():
-            cl.allreduce(xs, ys, algo="twoshot")
+            def ts():
+                cl.allreduce(xs, ys, algo="twoshot")
 
-        for _ in range(3):
-            ts()
-        cl.check()
-        tms, tmhz = times(ts, a.iters, dev, probe)
-        cl.check()
-        c50, t50 = pct(cms, 50), pct(tms, 50)
-        copy_tbps = 2 * S / (c50 / 1e3) / 1e12
-        # two-shot HBM bytes, utils.timing.hbm_bytes: P inputs read + P outputs written + slabs
-        from akka_allreduce_1_amd.utils.timing import hbm_bytes
-        tbps = hbm_bytes(S, P, "twoshot", 2) / (t50 / 1e3) / 1e12
-        print(json.dumps({"row": k, "vary": a.vary, "copy_ms": [round(pct(cms, 10), 4), round(c50, 4), round(pct(cms, 90), 4)],
-                          "copy_TBps": round(copy_tbps, 3), "copy_core_MHz": cmhz,
-                          "twoshot_ms": [round(pct(tms, 10), 4), round(t50, 4), round(pct(tms, 90), 4)],
-                          "twoshot_TBps": round(tbps, 3), "frac_copy": round(tbps / copy_tbps, 3),
-                          "twoshot_core_MHz": tmhz}), flush=True)
+            for _ in range(3):
+                ts()
+            cl.check()
+            tms, tmhz = times(ts, a.iters, dev, probe)
+            cl.check()
+            c50, t50 = pct(cms, 50), pct(tms, 50)
+            copy_tbps = 2 * S / (c50 / 1e3) / 1e12
+            # two-shot HBM bytes, utils.timing.hbm_bytes: P inputs read + P outputs written + slabs
+            from akka_allreduce_1_amd.utils.timing import hbm_bytes
+            tbps = hbm_bytes(S, P, "twoshot", 2) / (t50 / 1e3) / 1e12
+            print(json.dumps({"row": k, "vary": a.vary, "stagger": stg,
+                              "copy_ms": [round(pct(cms, 10), 4), round(c50, 4), round(pct(cms, 90), 4)],
+                              "copy_TBps": round(copy_tbps, 3), "copy_core_MHz": cmhz,
+                              "twoshot_ms": [round(pct(tms, 10), 4), round(t50, 4), round(pct(tms, 90), 4)],
+                              "twoshot_TBps": round(tbps, 3), "frac_copy": round(tbps / copy_tbps, 3),
+                              "twoshot_core_MHz": tmhz}), flush=True)
         if a.vary == "both":
             del cl, xs, ys
             cl = xs = ys = None
