@@ -314,8 +314,8 @@ def _free_port() -> int:
 
 def _native_job(n: int, chunk: int, rounds: int, quiet: bool, timeout: float = 60.0) -> tuple[dict | None, list[str]]:
     """One run of the reference's deployment shape: `mxar master` + 2 `mxar-gpu worker`
-    processes on GPU 0 (static source data[i] = i, 128 workgroups each - together one per CU,
-    engine.default_plane_grid - host threads polling
+    processes on GPU 0 (static source data[i] = i, 256 workgroups each - separate kernels:
+    profiles/round5/native_grid_ab.jsonl, 128 each is no faster - host threads polling
     through the round: --spin-us 500). Returns the master's steady-rate line and the workers'
     stdout lines."""
     import json as _json
@@ -328,7 +328,7 @@ def _native_job(n: int, chunk: int, rounds: int, quiet: bool, timeout: float = 6
     port = _free_port()
     seeds = ["--seeds", f"mxar.tcp://ClusterSystem@127.0.0.1:{port}", "--loglevel", "ERROR"]
     wargs = [os.path.join(exe, "mxar-gpu"), "worker", "0", str(n), "--device", "0", "--max-peers", "2",
-             "--plane-timeout", "20", "--grid", "128", "--source", "static"] + seeds + (["--quiet"] if quiet else [])
+             "--plane-timeout", "20", "--grid", "256", "--source", "static"] + seeds + (["--quiet"] if quiet else [])
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     workers = [subprocess.Popen(wargs, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
                for _ in range(2)]
@@ -361,7 +361,7 @@ def native_deployment(cases=((10, 2, 400), (262144, 1024, 400), (16777216, 32768
     import numpy as np
 
     res: dict = {"workers": 2, "dtype": "float32", "source": "static data[i] = i (mxar-gpu --source static)",
-                 "host": "--spin-us 500", "grid_per_worker": 128}
+                 "host": "--spin-us 500", "grid_per_worker": 256}
     t_end = time.monotonic() + budget_s  # the whole section; a failed size ends it
     for n, chunk, rounds in cases:
         row: dict = {"n_f32": n, "bytes": 4 * n, "max_chunk_size": chunk, "rounds": rounds}

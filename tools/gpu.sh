@@ -87,11 +87,11 @@ case $task in
     ;;
   native)
     # NATIVE_SOURCE=iota|static (per-round demo fill, or the same input every round),
-    # NATIVE_GRID (workgroups per worker; 128 = one per CU for the two, as in-process planes split it)
+    # NATIVE_GRID (workgroups per worker; 256 = half the GPU each: separate kernels, one per process)
     sizes=("$@")
     [ ${#sizes[@]} -eq 0 ] && sizes=(262144 16777216 67108864)
     src=${NATIVE_SOURCE:-iota}
-    grid=${NATIVE_GRID:-128}
+    grid=${NATIVE_GRID:-256}
     X=akka_allreduce_1_amd
     for n in "${sizes[@]}"; do
       port=$((20000 + RANDOM % 20000))
