@@ -227,6 +227,8 @@ void bind_hip(py::module_& m) {
   h.def("device_plane", &make_device_plane, py::arg("device") = 0,
         "DataPlane whose slabs and payloads live in HBM of `device` (worker protocol on the GPU)");
 
+  h.def("shared_launch_rule", &shared_launch_rule, py::arg("ranks_here"), py::arg("default_grid"),
+        "workgroups per rank at most when several logical ranks share one default-grid launch (0: no cap)");
   h.def("size_grid_rule", &size_grid_rule, py::arg("bytes"), py::arg("grid"), py::arg("world"), py::arg("oneshot"),
         py::arg("full_at") = int64_t{512} << 20, py::arg("cap") = 256,
         "workgroups a default-grid launch of `bytes` (all ranks of the launch) uses (XgmiComm::launch_grid)");

@@ -120,6 +120,12 @@ inline int size_grid_rule(int64_t bytes, int grid, int world, bool oneshot, int6
   return static_cast<int>(g < grid ? g : grid);
 }
 
+// Workgroups per rank at most when `ranks_here` logical ranks share one launch at the default
+// grid (XgmiComm::shared_launch_cap): a quarter of that grid, half the CUs. 0 = no cap.
+inline int shared_launch_rule(int ranks_here, int default_grid) {
+  return ranks_here <= 1 ? 0 : (default_grid / 4 > 1 ? default_grid / 4 : 1);
+}
+
 struct CommStats {
   uint64_t calls = 0, launches = 0, bytes = 0, oneshot = 0, twoshot = 0, ring = 0, threshold = 0, ll = 0, coll = 0,
            adamw = 0, stream_switches = 0;

@@ -805,8 +805,9 @@ int XgmiComm::shared_launch_cap(int ranks_here) const {
   // the CUs - per rank at the default grid. 2 ranks x 256 MiB bf16 two-shot 426-436 -> 389-395
   // us, threshold 432-440 -> 411-414; 4 x 128 MiB 128 per rank beats 64; 8 x 256 MiB equal
   // (profiles/round5/local_launch_grid.jsonl). One rank per GPU keeps launch_grid's rule.
-  if (ranks_here <= 1 || !size_grid_ || grid_ != default_grid_) return std::numeric_limits<int>::max();
-  return std::max(1, default_grid_ / 4);
+  const int cap = shared_launch_rule(ranks_here, default_grid_);
+  if (cap <= 0 || !size_grid_ || grid_ != default_grid_) return std::numeric_limits<int>::max();
+  return cap;
 }
 
 static bool capturing(hipStream_t s) {

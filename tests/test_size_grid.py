@@ -34,3 +34,26 @@ def test_never_above_the_device_grid():
     assert R(64 * MiB, 128, 8, False) == 128
     assert R(64 * MiB, 32, 8, True) == 32
     assert R(1 * KiB, 32, 2, False) == 32
+
+
+def test_shared_launches_cap_each_rank_at_half_the_cus():
+    """Several logical ranks in one launch: at most 128 workgroups per rank at the default
+    grid of 512 (profiles/round5/README.md section 13: 2 x 256 MiB two-shot 426-436 -> 389-395
+    us; 4 ranks at 128 beat 64; 8 ranks indifferent)."""
+    S = C.hip.shared_launch_rule
+    assert S(1, 512) == 0                      # a rank alone on its GPU: launch_grid's rule
+    assert S(2, 512) == 128
+    assert S(8, 512) == 128                    # 512 / 8 = 64 is below the cap anyway
+    assert min(R(512 * MiB, 512, 2, False) // 2, S(2, 512)) == 128
+
+
+def test_co_located_plane_workers_share_the_cus():
+    """engine.default_plane_grid: co-located workers together run about one workgroup per
+    CU; a worker alone on its GPU keeps two per CU (section 12)."""
+    from akka_allreduce_1_amd.engine import default_plane_grid
+
+    cus = 256  # no GPU here: the MI355X count
+    assert default_plane_grid(0, 1) == 2 * cus
+    assert default_plane_grid(0, 2) == cus // 2
+    assert default_plane_grid(0, 8) == cus // 8
+    assert default_plane_grid(0, 64) == 8      # never below 8
