@@ -89,7 +89,8 @@ class PlaneJob:
                  max_peers: int | None = None, high_priority: bool = True, order_release: bool = True,
                  plane: str = "xgmi", hub: str | None = None, spin_us: int = 1000, reinit_on_loss: bool = False,
                  split: bool = True, keep_last: bool = False, bridge_port: int | None = None,
-                 external_rounds: bool = False, min_chunk: int | None = None):
+                 external_rounds: bool = False, min_chunk: int | None = None, lag_wait_us: float | None = None,
+                 record: bool = False):
         """plane: "xgmi" (one threshold-kernel launch per round on the GPUs in `devices`) or
         "loopback" (host memory, no GPU: csrc/runtime/loopback_plane.h; `hub` names the
         workers' shared hub, default a fresh one; dtype float32, devices ignored).
@@ -104,7 +105,12 @@ class PlaneJob:
         min_chunk: the planes keep one flag / count / threshold decision per chunk of at least
         this many elements (xgmi_plane.h); default: max_chunk_size whenever it is finer than the
         1 KiB flag granularity, so every reference chunk is decided on its own (the reference's
-        DataBuffer semantics at any maxChunkSize)."""
+        DataBuffer semantics at any maxChunkSize).
+        lag_wait_us: a round waits at most this long at its lag gate for a peer still in the
+        round that last used its row, then runs without it (XgmiPlaneOptions::lag_wait_us; the
+        straggler mode at thresholds < 1). None: wait for the peer (bounded buffers).
+        record: with keep_last, the native sinks also keep every round's sink time and count
+        totals (`sink_stamps(k)`, `count_stats(k)`)."""
         self.P = P
         self.n = data_size
         self.dtype = dtype
@@ -141,7 +147,8 @@ class PlaneJob:
             self.planes = [C.hip.xgmi_plane(d, dtype_code(dtype), data_size, max_peers=max_peers or P,
                                             max_lag=max_lag, grid=grid, timeout_s=timeout_s, order_ref=order_ref,
                                             high_priority=high_priority, order_release=order_release,
-                                            spin_us=spin_us, split=split, min_chunk=min_chunk)
+                                            spin_us=spin_us, split=split, min_chunk=min_chunk,
+                                            lag_wait_us=-1.0 if lag_wait_us is None else float(lag_wait_us))
                            for d in self.devices]
             if sources is None:
                 sources = [iota_source(data_size, torch.device("cuda", d), dtype, 1000.0 * k)
@@ -152,7 +159,7 @@ class PlaneJob:
                         for src in sources]
         self.keep_last = keep_last
         self._final_stamps: list[float] | None = None
-        self._last = [C.last_output_sink() for _ in range(P)] if keep_last else None
+        self._last = [C.last_output_sink(record) for _ in range(P)] if keep_last else None
 
         def fin(r):
             self.rounds["n"] = r
@@ -216,6 +223,14 @@ class PlaneJob:
         if self._last is None:
             raise RuntimeError("PlaneJob(keep_last=True) keeps the last output")
         return self._last[k].last()
+
+    def sink_stamps(self, k: int) -> list[tuple[int, float]]:
+        """keep_last + record: worker k's (iteration, perf_counter seconds) per completed round."""
+        return self._last[k].stamps()
+
+    def count_stats(self, k: int) -> dict:
+        """keep_last + record: worker k's per-chunk count totals over every round."""
+        return self._last[k].count_stats()
 
     def state(self) -> dict:
         return {"master": self.system.master_state(self.master),

@@ -22,17 +22,12 @@ from typing import Sequence
 import torch
 
 from .._native import C
+from ..algos import LIBRARY_ALGOS, LOSSY_ALGOS  # noqa: F401 - one definition (algos.py)
 
 _H = C.hip
 
 ALGOS = {"auto": _H.Algo.Auto, "twoshot": _H.Algo.TwoShot, "oneshot": _H.Algo.OneShot, "ring": _H.Algo.Ring,
          "ll": _H.Algo.LL, "ring_native": _H.Algo.RingNative}
-LIBRARY_ALGOS = ("rccl", "rsag", "p2p")  # timed for comparison, never picked by tune()
-# kernels that round more than once (ring_native: every reduce-scatter hop's partial is rounded
-# to the element type): timed by tune() as comparison columns but adopted only with
-# exact_only=False - by default every tuned choice sums in fp32 and rounds once, as precise as
-# the reference's fp32 sums
-LOSSY_ALGOS = ("ring_native",)
 DEFAULT_SLOT_BYTES = int(os.environ.get("MXAR_SLOT_BYTES", 64 << 20))
 
 

@@ -9,10 +9,10 @@ buffer across 8xMI355X over xGMI"), one process per GPU.
 One "step" = one out-of-place allreduce of the buffer through the framework's engine
 (the fused xGMI two-shot kernel, csrc/hip/xgmi_comm.hip). The result is validated against
 an fp32 reference before timing. RCCL (`torch.distributed` nccl backend) is timed on the
-same buffer for comparison. Rank 0 prints ONE JSON line. Per-rank algbw = buffer bytes / time
-of the slowest rank (nccl-tests convention, reported as `algbw_per_rank`); `value` is the
-whole-job aggregate the driver contract asks for = N x per-rank algbw (gradient bytes reduced
-per second by the job). At N=1 an allreduce is an out-of-place copy, so the N=1 point is an
+same buffer for comparison. Rank 0 prints ONE JSON line. `value` = algbw = buffer bytes / time
+of the slowest rank (nccl-tests convention: the job reduces S bytes per step, whatever N), the
+figure RCCL's algbw column and BASELINE's metric use; `algbw_sum_over_ranks` = N x algbw is
+kept under its own key. At N=1 an allreduce is an out-of-place copy, so the N=1 point is an
 HBM copy rate, not a communication rate (`algo` says "copy (world=1)" and the tuner is
 skipped); the `local_ranks` section then times the allreduce kernels themselves with 8
 logical ranks in one launch on the GPU. Data: synthetic uniform(-1, 1) gradients.
@@ -26,6 +26,11 @@ tuner's size sweep vs RCCL, the straggler-tolerant kernel, all-to-all / all-gath
 reduce-scatter, the fused sharded AdamW step, and `dp` = BASELINE configs 4 and 5 (one
 data-parallel step of the ResNet-50 and full Llama-3-8B gradient sets with a GEMM-backed
 synthetic backward overlapped with the bucketed reducer).
+
+At N = 1 straggler tolerance is timed (`stragglers`, benchmarks/stragglers.py): the
+reference's default job at its own thresholds (in process and native), and P = 4 workers with
+one dataSource delayed 0 / 0.2 / 2 ms per round at th 0.75, maxLag 1 / 2, 40 B / 1 MiB / 64 MiB
+(fast workers' round period vs no straggler, forced / cold rounds, counts, validated outputs).
 
 At N = 1 the metric's size axis is timed too (benchmarks/sections.py): `latency_vs_size`
 (p50 latency + algbw of every kernel and of `auto`, 8 / 4 / 2 logical ranks in one launch,
@@ -745,6 +750,9 @@ def main() -> None:
                     help="skip the native-deployment protocol rounds (child mxar processes; e.g. under a profiler)")
     ap.add_argument("--no-sizes", action="store_true",
                     help="skip the N = 1 size-axis sections (latency_vs_size, reduce_kernel, protocol sizes)")
+    ap.add_argument("--no-stragglers", action="store_true",
+                    help="skip the straggler-tolerance section at N = 1 (benchmarks/stragglers.py)")
+    ap.add_argument("--stragglers-budget", type=float, default=90.0, help="seconds for the straggler section")
     ap.add_argument("--protocol-timeout", type=float, default=240.0,
                     help="native watchdog over the protocol section (s); the result line is written either way")
     ap.add_argument("--dp-rehearsal", action="store_true", help="with --share-device: run the ResNet-50 DP step too")
@@ -903,9 +911,11 @@ def main() -> None:
 
     result = {
         "metric": "allreduce_algbw",
-        "value": round(algbw * world, 2),
-        "value_note": "aggregate over ranks = n_gpus x algbw_per_rank",
+        "value": round(algbw, 2),
+        "value_note": ("nccl-tests algbw = buffer bytes / time of the slowest rank (the job reduces S bytes per "
+                       "step); algbw_sum_over_ranks = n_gpus x algbw"),
         "algbw_per_rank": round(algbw, 2),
+        "algbw_sum_over_ranks": round(algbw * world, 2),
         "unit": "GB/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -913,7 +923,7 @@ def main() -> None:
         "ms_per_step": round(ms, 4),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": None if BASELINE_VALUE is None else round(algbw * world / BASELINE_VALUE, 3),
+        "vs_baseline": None if BASELINE_VALUE is None else round(algbw / BASELINE_VALUE, 3),
         "dtype": args.dtype,
         "data": "synthetic uniform(-1,1) gradient buffer per rank",
         "config": {
@@ -1070,6 +1080,22 @@ def main() -> None:
         if not cancel():  # the watchdog fired and wrote the line; the process is exiting
             return
         result["protocol"] = prot
+    if engine_ok and world == 1 and not args.share_device and not args.no_stragglers:
+        # straggler tolerance, timed (the reference's thresholds / maxLag with one slow worker),
+        # under its own native watchdog: a stuck round never costs the result line
+        from akka_allreduce_1_amd._native import C
+        from benchmarks.stragglers import section as straggler_section
+
+        timed_out = dict(result, stragglers={"error": f"timed out after {2 * args.stragglers_budget:g} s"},
+                         status="stragglers_timeout")
+        sys.stdout.flush()
+        cancel = C.watchdog_arm(2 * args.stragglers_budget + 60, _RESULT_FD if rank == 0 else -1,
+                                result_line(timed_out) if rank == 0 else "\n", 3)
+        log(rank, "stragglers: reference default job, P = 4 straggler sweep, native 2-process shape")
+        strag = straggler_section(dev, budget_s=args.stragglers_budget)
+        if not cancel():
+            return
+        result["stragglers"] = strag
     if engine_ok and not args.no_dp and (not args.share_device or args.dp_rehearsal):
         # configs 4 / 5 (full Llama-3-8B: 32 GB of params + grads per rank). Not in the
         # one-GPU rehearsal: there every rank's spinning comm kernel shares the device with the

@@ -12,6 +12,10 @@ side file (`detail`), and the line holds the headline fields plus compact summar
   reduce_kernel  BASELINE config 2: fraction of the copy roofline per slot count
   protocol_us    the reference's round protocol, us per round per size (in-process, native
                  deployment, control-bridge), plus whether the timed rounds were validated
+  stragglers     straggler tolerance (benchmarks/stragglers.py compact): the reference's default
+                 job us per round [in process, native]; per size and maxLag [no-straggler period
+                 us, ratio with a 0.2 ms straggler, ratio at 2 ms, p99 us at 2 ms, straggler lag];
+                 the waiting gate's ratio at 2 ms; the 2-process native shape; validated
   adamw          fused reduce-scatter + AdamW + all-gather: ms and HBM TB/s
   dp             BASELINE configs 4 / 5: [step ms, compute-only ms, exposed ms]
   sdma           N > 1: the copy-engine allreduce across the GPUs, validated in child processes
@@ -33,17 +37,15 @@ LINE_BUDGET = 4000  # bytes, newline excluded; the driver contract is "one JSON 
 
 HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "p50_ms",
                  "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "algbw_per_rank",
-                 "busbw", "engine_ok", "status")
+                 "algbw_sum_over_ranks", "busbw", "engine_ok", "status")
 
 # least important first: dropped in this order if the line is still over budget
 _DROP_ORDER = ("lat_vs_size", "collectives", "sweep", "dp_overlap", "sdma_local", "sdma", "protocol_us", "dp",
+               "stragglers",
                "reduce_kernel", "validation_failed", "engine_note", "adamw", "local_ranks", "threshold", "rccl",
                "xgmi_links")
 
-# library paths: timed next to the kernels as comparison columns, never the headline
-LIBRARY_ALGOS = ("rccl", "rsag", "p2p")
-# per-hop-rounded kernels (parallel/comm.py LOSSY_ALGOS): never the automatic headline
-LOSSY_ALGOS = ("ring_native",)
+from akka_allreduce_1_amd.algos import LIBRARY_ALGOS, LOSSY_ALGOS  # noqa: E402,F401 - one definition
 
 
 def headline_guard(chosen: str, requested: str, world: int) -> tuple[str, str | None]:
@@ -225,6 +227,11 @@ def compact(result: dict, detail_path: str | None = None) -> dict:
                              for P in ("P2", "P8") if isinstance(sd.get(P), dict)}
     if isinstance(result.get("protocol"), dict):
         out["protocol_us"] = _protocol(result["protocol"])
+    if isinstance(result.get("stragglers"), dict):
+        from benchmarks.stragglers import compact as _strag
+
+        sg = result["stragglers"]
+        out["stragglers"] = _strag(sg) if "error" not in sg else {"error": str(sg["error"])[:160]}
     if isinstance(result.get("dp"), dict):
         dp, ovl = _dp(result["dp"])
         if dp:

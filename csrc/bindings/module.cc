@@ -434,16 +434,41 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("rounds", [](NativeSink& k) {
         std::lock_guard<std::mutex> g(k.keep->mu);
         return k.keep->rounds;
-      });
-  m.def("last_output_sink", [] {
+      })
+      .def("stamps", [](NativeSink& k) {
+        std::lock_guard<std::mutex> g(k.keep->mu);
+        return k.keep->stamps;
+      }, "record=True: [(iteration, time.perf_counter()-compatible seconds at the sink)] per round")
+      .def("count_stats", [](NativeSink& k) {
+        std::lock_guard<std::mutex> g(k.keep->mu);
+        py::dict d;
+        d["sum"] = k.keep->count_sum;
+        d["n"] = k.keep->count_n;
+        d["zero"] = k.keep->count_zero;
+        return d;
+      }, "record=True: totals over every round's per-chunk counts (sum, entries, zero entries)");
+  m.def("last_output_sink", [](bool record) {
     auto keep = std::make_shared<LastOutput>();
+    keep->record = record;
     return NativeSink{[keep](const AllReduceOutput& o) {
+                        const double t =
+                            std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
                         std::lock_guard<std::mutex> g(keep->mu);
                         keep->out = o;  // holds the round output's buffer until the next round
                         keep->rounds++;
+                        if (keep->record) {
+                          if (keep->stamps.size() < (size_t{1} << 22)) keep->stamps.emplace_back(o.iteration, t);
+                          for (int c : o.count) {
+                            keep->count_sum += static_cast<uint64_t>(c > 0 ? c : 0);
+                            keep->count_zero += c == 0 ? 1 : 0;
+                          }
+                          keep->count_n += o.count.size();
+                        }
                       },
                       keep};
-  }, "dataSink keeping only the newest round output, without the GIL (plane workers)");
+  }, py::arg("record") = false,
+        "dataSink keeping only the newest round output, without the GIL (plane workers); record: per-round "
+        "sink stamps and count totals too");
 
   // ---------------------------------------------------------------- core helpers
   m.def("f32_threshold_count", &f32_threshold_count, py::arg("threshold"), py::arg("peers"));
@@ -589,6 +614,12 @@ PYBIND11_MODULE(_C, m) {
           }, py::arg("source"), py::arg("sink") = py::none(), py::arg("plane"), py::arg("name") = "",
           "Round-granular worker (csrc/runtime/plane_worker.h): the reference protocol with one plane launch "
           "per round; announce plane.descriptor as the member's meta (MemberUp / ClusterConfig.meta)")
+      .def("plane_worker_rounds", [](ActorSystem&, ActorRef ref) {
+        // (round, maxRound, launched): plain words read without stopping the worker - a
+        // sampling probe (the straggler bench's lag), unlike plane_worker_state's statistics
+        auto* w = plane_worker_of(ref);
+        return std::make_tuple(w->round(), w->max_round(), w->launched());
+      }, "(round, maxRound, launched) of a plane worker, safe to sample while it runs")
       .def("plane_worker_state", [](ActorSystem&, ActorRef ref) {
         auto* w = plane_worker_of(ref);
         py::dict d;
@@ -602,7 +633,7 @@ PYBIND11_MODULE(_C, m) {
         py::dict st;
 #define F(x) st[#x] = s.x
         F(start_in); F(rounds_launched); F(cold_rounds); F(forced_completions); F(rounds_completed);
-        F(complete_out); F(stale_dropped); F(stashed); F(plane_errors); F(inits);
+        F(complete_out); F(stale_dropped); F(stashed); F(plane_errors); F(inits); F(starts_coalesced);
 #undef F
         d["stats"] = st;
         const RoundLatency lat = w->round_latency();

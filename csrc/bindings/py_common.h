@@ -57,6 +57,12 @@ struct LastOutput {
   std::mutex mu;
   std::optional<AllReduceOutput> out;
   uint64_t rounds = 0;
+  // record = true: every round's (iteration, steady-clock seconds at the sink) and its
+  // per-chunk counts folded into totals (the straggler bench's per-worker round period and
+  // mean count, without Python on the round path)
+  bool record = false;
+  std::vector<std::pair<int, double>> stamps;
+  uint64_t count_sum = 0, count_n = 0, count_zero = 0;
 };
 struct NativeSink {
   DataSink fn;

@@ -2,6 +2,7 @@
 // addresses (torch `tensor.data_ptr()`) and streams as `torch.cuda.Stream.cuda_stream`,
 // so the native module does not link against libtorch; torch is imported first and its
 // bundled libamdhip64 (same SONAME) is the one HIP runtime of the process.
+#include "../core/delay.h"
 #include <hip/hip_runtime_api.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -178,7 +179,7 @@ Payload py_to_device_payload_typed(const py::handle& obj) {
 // the same buffer, ordered after the work queued on the stream that was torch's current
 // stream at creation (an event only if that stream is busy, as the per-round import does).
 // That stream must outlive the source (torch's default / current streams do).
-NativeSource tensor_source(py::object obj) {
+NativeSource tensor_source(py::object obj, double delay_us) {
   const TorchRefs& T = torch_refs();
   if (!py::isinstance(obj, T.tensor_type) || !obj.attr("is_cuda").cast<bool>())
     throw py::type_error("tensor_source needs a GPU tensor");
@@ -195,7 +196,8 @@ NativeSource tensor_source(py::object obj) {
   auto holder = std::make_shared<PyCallable>(obj);  // keeps the tensor alive; released with the GIL
   std::shared_ptr<void> mem(holder, reinterpret_cast<void*>(ptr));
   const hipStream_t ps = reinterpret_cast<hipStream_t>(cs);
-  return NativeSource{[mem, n, dev, code, ps](const AllReduceInputRequest&) -> AllReduceInput {
+  return NativeSource{[mem, n, dev, code, ps, delay_us](const AllReduceInputRequest&) -> AllReduceInput {
+    precise_delay_us(delay_us);  // a straggling source (0: none)
     ReadyEvent ready = hipStreamQuery(ps) == hipSuccess ? nullptr : record_ready(ps);
     (void)hipGetLastError();
     return AllReduceInput{std::make_shared<DevicePayload>(mem, 0, n, dev, nullptr, std::move(ready), code)};
@@ -210,8 +212,9 @@ void bind_hip(py::module_& m) {
   py::module_ h = m.def_submodule("hip", "HIP/CDNA4 data plane (gfx950)");
   register_device_payload_hooks(&device_payload_to_py, &py_to_device_payload);
   register_typed_payload_hook(&py_to_device_payload_typed);
-  h.def("tensor_source", &tensor_source, py::arg("tensor"),
-        "dataSource for a plane worker: the same GPU tensor every round, no Python (GIL) per round");
+  h.def("tensor_source", &tensor_source, py::arg("tensor"), py::arg("delay_us") = 0.0,
+        "dataSource for a plane worker: the same GPU tensor every round, no Python (GIL) per round; "
+        "delay_us: each fetch first waits this long on the worker's thread (a straggler)");
 
   py::class_<DevicePlane, DataPlane, std::shared_ptr<DevicePlane>>(h, "DevicePlane")
       .def_property_readonly("device", &DevicePlane::device)
@@ -271,7 +274,8 @@ void bind_hip(py::module_& m) {
   h.def(
       "xgmi_plane",
       [](int device, DType dtype, int64_t capacity, int max_peers, int max_lag, int grid, double timeout_s,
-         bool order_ref, bool high_priority, bool order_release, int spin_us, bool split, int64_t min_chunk) {
+         bool order_ref, bool high_priority, bool order_release, int spin_us, bool split, int64_t min_chunk,
+         double lag_wait_us) {
         XgmiPlaneOptions o;
         o.device = device;
         o.dtype = dtype;
@@ -286,13 +290,14 @@ void bind_hip(py::module_& m) {
         o.spin_us = spin_us;
         o.split = split;
         o.min_chunk = min_chunk;
+        o.lag_wait_us = lag_wait_us;
         py::gil_scoped_release r;
         return make_xgmi_plane(o);
       },
       py::arg("device") = 0, py::arg("dtype") = DType::F32, py::arg("capacity"), py::arg("max_peers") = 8,
       py::arg("max_lag") = 4, py::arg("grid") = 0, py::arg("timeout_s") = 60.0, py::arg("order_ref") = true,
       py::arg("high_priority") = true, py::arg("order_release") = true, py::arg("spin_us") = 1000, py::arg("split") = true,
-      py::arg("min_chunk") = 0,
+      py::arg("min_chunk") = 0, py::arg("lag_wait_us") = -1.0,
       "RoundPlane of the protocol engine on MI355X: an HBM arena exported over IPC, one threshold-kernel launch "
       "per round (csrc/hip/xgmi_plane.h)");
   py::enum_<Algo>(h, "Algo").value("Auto", Algo::Auto).value("TwoShot", Algo::TwoShot).value("OneShot", Algo::OneShot).value("Ring", Algo::Ring).value("LL", Algo::LL).value("RingNative", Algo::RingNative);

@@ -199,20 +199,24 @@ void launch_reduce_slots(const void* slots, int64_t slot_stride_elems, int nslot
 }
 
 template <class E>
-__global__ __launch_bounds__(kThreads) void fill_iota_kernel(char* out, int64_t n, double offset) {
+__global__ __launch_bounds__(kThreads) void fill_affine_kernel(char* out, int64_t n, double slope, double offset) {
   const int64_t step = static_cast<int64_t>(gridDim.x) * kThreads;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n; i += step)
-    Scalar<E>::store(out, i, static_cast<float>(static_cast<double>(i) + offset));
+    Scalar<E>::store(out, i, static_cast<float>(slope * static_cast<double>(i) + offset));
 }
 
-void launch_fill_iota(void* dst, int64_t n, double offset, DType dt, hipStream_t stream) {
+void launch_fill_affine(void* dst, int64_t n, double slope, double offset, DType dt, hipStream_t stream) {
   if (n <= 0) return;
   const int g = grid_for(n);
   dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
-    hipLaunchKernelGGL(fill_iota_kernel<decltype(tag)>, dim3(g), dim3(kThreads), 0, stream, static_cast<char*>(dst), n,
-                       offset);
+    hipLaunchKernelGGL(fill_affine_kernel<decltype(tag)>, dim3(g), dim3(kThreads), 0, stream, static_cast<char*>(dst),
+                       n, slope, offset);
   });
-  hip_check(hipGetLastError(), "fill_iota launch");
+  hip_check(hipGetLastError(), "fill_affine launch");
+}
+
+void launch_fill_iota(void* dst, int64_t n, double offset, DType dt, hipStream_t stream) {
+  launch_fill_affine(dst, n, 1.0, offset, dt, stream);
 }
 
 __device__ __forceinline__ uint32_t hash32(uint64_t x) {

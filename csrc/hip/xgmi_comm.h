@@ -229,6 +229,10 @@ class XgmiComm {
     // null: one workgroup per chunk
     void* split_scratch = nullptr;
     size_t split_bytes = 0;
+    // lag skip (CommArgs::lag_skip): wait at most this long at the lag gate for a peer, then
+    // skip it for the round; < 0 = wait for it. Taken only where it is safe and useful: unsplit
+    // chunks and thresholds that let a round complete without one peer.
+    double lag_wait_us = -1.0;
   };
   // Scratch a round of P ranks needs to split its chunks over several workgroups.
   static size_t split_scratch_bytes(int P, int64_t maxch) {
@@ -461,6 +465,8 @@ void launch_reduce_slots(const void* slots, int64_t slot_stride_elems, int nslot
                          float scale, hipStream_t stream);
 // dst[i] = (float)(i + offset) (reference data source AllreduceWorker.scala:285-291)
 void launch_fill_iota(void* dst, int64_t n, double offset, DType dt, hipStream_t stream);
+// dst[i] = slope * i + offset (iota: slope 1; a constant: slope 0)
+void launch_fill_affine(void* dst, int64_t n, double slope, double offset, DType dt, hipStream_t stream);
 void launch_clock_probe(uint64_t* out, int samples, uint64_t interval_ticks, hipStream_t stream);
 // dst[i] = uniform(-1, 1) from a counter-based hash of (seed, i)
 void launch_fill_uniform(void* dst, int64_t n, uint64_t seed, DType dt, hipStream_t stream);

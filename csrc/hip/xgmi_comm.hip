@@ -1349,8 +1349,8 @@ bool XgmiComm::threshold_args(const std::vector<XgmiComm*>& group, const std::ve
   // thComplete: the reference's (th * P * nch) when every block has nch chunks; with a short
   // last block (uneven blocks) the chunks that exist, as the host WorkerCore
   // counts them (worker_core.cc) - the kernel never counts a chunk past a block's end
+  int64_t total = 0;  // chunks that exist in the round
   {
-    int64_t total = 0;
     bool uniform = true;
     for (int j = 0; j < W; ++j) {
       const int64_t bl = std::max<int64_t>(0, std::min<int64_t>(a.block, n - static_cast<int64_t>(j) * a.block));
@@ -1377,6 +1377,14 @@ bool XgmiComm::threshold_args(const std::vector<XgmiComm*>& group, const std::ve
     a.err_out = spec->err_out;
     a.done_out = spec->done_out;
     a.counts_host = counts != nullptr ? spec->counts_host : nullptr;
+    // lag skip: unsplit chunks (a split chunk's slices publish one flag between them, so they
+    // would have to agree on the skip) and thresholds under which a round can complete
+    // without one peer - its contribution (min_reduce < P) and its block's chunks
+    // (min_complete within the other blocks' chunks)
+    if (spec->lag_wait_us >= 0.0 && a.sub <= 1 && W >= 2 && a.min_reduce < W && a.min_complete <= total - a.nch) {
+      a.lag_skip = 1;
+      a.lag_wait = static_cast<uint64_t>(spec->lag_wait_us * 100.0);  // s_memrealtime: 100 MHz
+    }
   }
   a.delay_rank = -1;
   for (XgmiComm* c : group)

@@ -93,6 +93,14 @@ struct CommArgs {
   // e - 2). Set by the host when that proof holds: trows >= 2 and every rank's block holds at
   // least one chunk or the thresholds are full (XgmiComm::threshold_args).
   int gate_shortcut;
+  // threshold kernel, protocol rounds with thresholds that tolerate a missing peer (unsplit
+  // chunks only): a peer still inside the round that last used this round's row after
+  // `lag_wait` ticks at the lag gate is SKIPPED for the round - nothing is written into its
+  // slab (its FORCE request still is), so a straggler never holds the fast ranks back. The
+  // laggard's late writes land in its own slots of our slab under older epochs, which no
+  // round of ours takes (xgmi_threshold.hip, lag gate). 0 = wait (the bounded-buffer gate).
+  int lag_skip;
+  uint64_t lag_wait;
   uint64_t* split_dec;
   uint32_t* split_ctr;
   uint32_t* split_early;

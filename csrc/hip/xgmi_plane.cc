@@ -748,6 +748,7 @@ void XgmiRoundPlane::join_group(const PlaneConfig& cfg) {
   spec.chunk = chunk_;
   spec.order_ref = o_.order_ref;
   spec.host_force = hforce_dev_;
+  spec.lag_wait_us = o_.lag_wait_us;
   spec.host_abort = hforce_dev_ + 1;
   if (o_.split) {  // few large chunks: slices over several workgroups, as the launch path does
     spec.split_scratch = split_mem_;
@@ -1146,6 +1147,7 @@ bool XgmiRoundPlane::launch_resident(int round, const Payload& input, bool cold)
   spec.chunk = chunk_;
   spec.order_ref = o_.order_ref;
   spec.host_force = hforce_dev_;
+  spec.lag_wait_us = o_.lag_wait_us;
   spec.host_abort = hforce_dev_ + 1;
   if (o_.split) {  // a geometry that splits its chunks takes the launch path (plan_resident)
     spec.split_scratch = split_mem_;
@@ -1293,6 +1295,7 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   spec.cold = cold;
   spec.order_ref = o_.order_ref;
   spec.host_force = hforce_dev_;
+  spec.lag_wait_us = o_.lag_wait_us;
   spec.host_abort = hforce_dev_ + 1;
   spec.err_out = reinterpret_cast<uint32_t*>(slot_dev + ring_stride_ - 1);
   spec.done_out = reinterpret_cast<uint32_t*>(slot_dev + ring_stride_ - 2);

@@ -82,6 +82,12 @@ struct XgmiPlaneOptions {
   // launched. 2 workers, th 1, bench geometry: 256 KiB 38-47 -> 32-34 us, 1 MiB 44-45 ->
   // 34-40, 4 MiB 46-52 -> 42-47 per round (profiles/round4/resident_grid_ab.jsonl).
   int64_t resident_max = 4 << 20;
+  // Lag skip (XgmiComm::RoundSpec::lag_wait_us): a round waits at most this long at its lag
+  // gate for a peer still inside the round that last used the row, then runs without it
+  // (writes nothing to it, forces it). < 0: wait for the peer - a straggler then holds every
+  // fast worker within maxLag + 1 rounds of itself (bounded buffers). Applies only where
+  // the thresholds let a round complete without one peer.
+  double lag_wait_us = -1.0;
   int resident_grid = 64;
   double resident_idle_us = 1000.0;
 };

@@ -224,7 +224,8 @@ __device__ __attribute__((noinline)) void zero_fill(char* dst, int64_t len) {
 template <class E>
 __device__ __forceinline__ void reduce_masked_scalar(const CommArgs& a, int P, int r, uint32_t mask,
                                                              const char* own_in, const char* S, int64_t slot,
-                                                             char* own_out, int64_t roff, int64_t len, float scale) {
+                                                             char* own_out, int64_t roff, int64_t len, float scale,
+                                                             uint32_t skip) {
   for (int64_t t = threadIdx.x; t < len; t += kCommThreads) {
     // every source's load issues before the first add (one memory latency per 8 sources,
     // not one per source); the fixed order s = 0..P-1 keeps the sum bit-exact (+0.f for a
@@ -244,7 +245,7 @@ __device__ __forceinline__ void reduce_masked_scalar(const CommArgs& a, int P, i
     for (int k = 0; k < P; ++k) {
       if (k == r) {
         if (own_out != nullptr) st_scalar_wt<E>(slab_rsrc(own_out), t, acc);
-      } else {
+      } else if (!((skip >> k) & 1u)) {
         st_scalar_wt<E>(slab_rsrc(a.base[k] + roff), t, acc);
       }
     }
@@ -252,14 +253,15 @@ __device__ __forceinline__ void reduce_masked_scalar(const CommArgs& a, int P, i
 }
 
 // Sum the sources in `mask` (fixed order s = 0..P-1, fp32), store to the own output (when
-// own_out != nullptr) and to every peer's R slot. Source r is the rank's own input.
+// own_out != nullptr) and to the R slot of every peer not in `skip` (lagging peers, lag skip).
+// Source r is the rank's own input.
 template <class E>
 __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, uint32_t mask, const char* own_in,
                                               const char* S, int64_t slot, char* own_out, int64_t roff,
-                                              int64_t len, bool wt_out, float scale) {
+                                              int64_t len, bool wt_out, float scale, uint32_t skip) {
   const bool vec = al16(own_in) && al16(S) && (own_out == nullptr || al16(own_out)) && (roff & 15) == 0;
   if (!vec) {
-    reduce_masked_scalar<E>(a, P, r, mask, own_in, S, slot, own_out, roff, len, scale);
+    reduce_masked_scalar<E>(a, P, r, mask, own_in, S, slot, own_out, roff, len, scale, skip);
     return;
   }
   // Every source's pack is loaded before the first add: a batch of B sources x U packs issues
@@ -315,7 +317,7 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
       o[u] = acc[u].pack();
     }
     for (int k = 0; k < P; ++k) {
-      char* d = k == r ? own_out : a.base[k] + roff;
+      char* d = k == r ? own_out : ((skip >> k) & 1u) ? nullptr : a.base[k] + roff;
       if (d == nullptr) continue;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -335,7 +337,7 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
       if ((mask >> s) & 1u) acc += ld_scalar_nt<E>(slab_rsrc(s == r ? own_in : S + s * slot), t);
     acc *= scale;
     for (int k = 0; k < P; ++k) {
-      char* d = k == r ? own_out : a.base[k] + roff;
+      char* d = k == r ? own_out : ((skip >> k) & 1u) ? nullptr : a.base[k] + roff;
       if (d == nullptr) continue;
       if (k == r && !wt_out)
         Scalar<E>::store(d, t, acc);
@@ -647,21 +649,36 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   // profiles/round4/README.md section 4) are skipped. The resident kernel proves it itself
   // (rv.gate_open); a launched round reads ctl[14], written by its predecessor's last
   // workgroup when every workgroup of that round was clean.
+  // Lag skip (a.lag_skip, unsplit thresholds < 1): a peer still short of the gate after
+  // a.lag_wait ticks is skipped for this round - its FORCE request is written, nothing else of
+  // this round goes into its slab (scatter units, reduced chunks, counts). The reference's
+  // fast workers never wait for a straggler either: their messages queue in its mailbox and
+  // come out outdated (AllreduceWorker.scala:113-114,137-138). Each workgroup decides for its
+  // own units, and both outcomes are safe: a peer that reached the gate may be written, one
+  // that did not is not; the laggard's own late writes go to its slots of our slab with an
+  // older epoch, which no later round of ours takes, and its rounds in order mean its newer
+  // data always follows its older data.
+  __shared__ uint32_t sh_skip;
   const bool gate_open = a.gate_shortcut &&
                          (rv.gate_open || (rv.epoch == 0 && clean_prev != 0u && clean_prev == epoch - 1u));
   if (gate_open) {
-    if (threadIdx.x == 0) sh_flag = 0;
+    if (threadIdx.x == 0) {
+      sh_flag = 0;
+      sh_skip = 0;
+    }
   } else if (threadIdx.x < 64) {
     const int k = static_cast<int>(threadIdx.x);
     const uint32_t target = epoch - static_cast<uint32_t>(a.trows);
     const uint32_t* f = (k < P && k != r) ? prog(a, r, k) : nullptr;
     bool ok = f == nullptr || reached(ld_flag(f), target);
     bool asked = false, aborted = false;
+    const uint64_t skip_at = a.lag_skip ? t_start + a.lag_wait : ~0ull;
     while (!__all(ok)) {
       if (!ok && !asked && blockIdx.x == 0) {
         st_flag(forcew(a, k, r), target);
         asked = true;
       }
+      if (wall_ticks() >= skip_at) break;  // scalar clock: the whole wave leaves together
       __builtin_amdgcn_s_sleep(2);
       if (!ok) ok = reached(ld_flag(f), target);
       if (rv.habort != nullptr && hp.due()) {
@@ -677,7 +694,11 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         break;
       }
     }
-    if (k == 0) sh_flag = aborted ? 1 : 0;
+    const uint32_t lag = static_cast<uint32_t>(__ballot(!ok));
+    if (k == 0) {
+      sh_flag = aborted ? 1 : 0;
+      sh_skip = a.lag_skip ? lag : 0u;
+    }
     // No acquire here: the gate orders this round's STORES into the peers' rows after the
     // peers' reads of those rows (write-after-read - the progress word was published after
     // them, and our stores issue only once the poll has returned: the wait below + the
@@ -689,6 +710,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   __syncthreads();
   const bool void_round = sh_flag != 0;  // abandoned before the exchange: no peer writes
   if (void_round) clean = false;
+  const uint32_t skip = sh_skip;  // peers this workgroup writes nothing to (lag skip)
   ps.mark(1);
 
   // Phase 1 - ScatterBlock into the owners' row slots (a cold or void round sends nothing).
@@ -719,6 +741,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       for (int u = blockIdx.x; u < nsu; u += G) {
         const int cg = u / Pm1;
         const int j = (r + 1 + u % Pm1) % P;
+        if ((skip >> j) & 1u) continue;  // a lagging owner: uniform per workgroup (LDS)
         const int c0 = cg * gs;
         const int ncg = a.nch - c0 < gs ? a.nch - c0 : gs;
         const int64_t bstart = static_cast<int64_t>(j) * a.block;
@@ -834,18 +857,19 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     if (len > 0) {
       reduce_masked<E>(a, P, r, mask, in + (bstart_own + cstart) * es, a.base[r] + rowS + cstart * es, slot,
                        take ? own_out : nullptr, rowR + r * slot + cstart * es, len,
-                       (a.fence & 1) || rv.done_out != nullptr, sc);
+                       (a.fence & 1) || rv.done_out != nullptr, sc, skip);
       if (!take) zero_fill<E>(own_out, len);
     }
     // a split chunk is reduced once its last slice is: that workgroup publishes it
     if (split && !last_slice(&rv.split_ctr[c], S, &sh_last)) continue;
-    if (threadIdx.x < static_cast<unsigned>(P) && static_cast<int>(threadIdx.x) != r)
+    if (threadIdx.x < static_cast<unsigned>(P) && static_cast<int>(threadIdx.x) != r && !((skip >> threadIdx.x) & 1u))
       st_flag(f2c(a, static_cast<int>(threadIdx.x), row * P + r, c), static_cast<uint32_t>(cnt));
     if (threadIdx.x == 0) {
       if (counts) cput(static_cast<int64_t>(r) * a.nch + c, take ? cnt : 0);
       if (!ref && tickets && blen_own - static_cast<int64_t>(c) * a.chunk > 0) add_ctl(&ctl[3], 1u);
     }
-    publish_flags([&](int k) -> uint32_t* { return k == r ? nullptr : f2(a, k, row * P + r, c); }, P, epoch, rel);
+    publish_flags([&](int k) -> uint32_t* { return (k == r || ((skip >> k) & 1u)) ? nullptr : f2(a, k, row * P + r, c); },
+                  P, epoch, rel);
     ps.add(2, t_body);
   }
 

@@ -226,6 +226,7 @@ void ActorCell::enqueue(Envelope env) {
   // count first (seq_cst), then push, then try to schedule: a dispatcher that clears
   // scheduled_ and then reads pending_ sees this message whenever our schedule() lost
   pending_.fetch_add(1);
+  actor_->on_enqueue(env.msg);
   mailbox_.push(std::move(env));
   sys_->schedule(shared_from_this());
 }

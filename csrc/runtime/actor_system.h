@@ -67,6 +67,10 @@ class Actor {
   virtual void receive(Envelope& env, ActorContext& ctx) = 0;
   virtual void post_stop(ActorContext&) {}
   virtual std::string kind() const { return "actor"; }
+  // Called on the SENDER's thread as a message is enqueued (before the push): a hint an actor
+  // may record with atomics only (it may run concurrently with receive()). PlaneWorkerActor
+  // notes the newest StartAllreduce in its mailbox here.
+  virtual void on_enqueue(const Message&) {}
 };
 
 class ActorContext {

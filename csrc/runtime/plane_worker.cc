@@ -97,11 +97,30 @@ void PlaneWorkerActor::on_init(const InitWorkers& m, ActorContext&) {
                                                           << ", maxLag = " << m.maxLag);
 }
 
+void PlaneWorkerActor::on_enqueue(const Message& m) {
+  const auto* st = std::get_if<StartAllreduce>(&m);
+  if (st == nullptr || st->round < 0) return;
+  const uint64_t v = (static_cast<uint64_t>(static_cast<uint32_t>(st->epoch)) << 32) | static_cast<uint32_t>(st->round);
+  uint64_t cur = announced_.load(std::memory_order_relaxed);
+  while (v > cur && !announced_.compare_exchange_weak(cur, v, std::memory_order_relaxed)) {
+  }
+}
+
 // StartAllreduce (AllreduceWorker.scala:84-104)
 void PlaneWorkerActor::on_start(const StartAllreduce& m) {
   stats_.start_in++;
   MXAR_LOG(INFO, "worker", "----Start allreduce round " << m.round);
   maxRound_ = std::max(maxRound_, m.round);
+  // a newer StartAllreduce of this epoch already waits in the mailbox: take its round now (it
+  // is a no-op when its turn comes), so a worker slower than the master catches up in one step
+  const uint64_t ann = announced_.load(std::memory_order_relaxed);
+  if (static_cast<uint32_t>(ann >> 32) == static_cast<uint32_t>(cfg_.epoch)) {
+    const int newest = static_cast<int>(static_cast<uint32_t>(ann));
+    if (newest > maxRound_) {
+      stats_.starts_coalesced += static_cast<uint64_t>(newest - maxRound_);
+      maxRound_ = newest;
+    }
+  }
   const int target = maxRound_ - cfg_.maxLag;  // every round < target must complete now
   if (round_ < target) {
     // forced catch-up (:91-97): rounds in flight stop waiting, rounds never started are
@@ -158,6 +177,7 @@ void PlaneWorkerActor::on_done(PlaneRoundDone& d) {
   }
   if (auto it = t0_.find(r); it != t0_.end()) {
     const double ms = (Tracer::now_ns() - it->second) / 1e6;
+    std::lock_guard<std::mutex> g(lat_mu_);
     if (lat_ms_.size() < 4096)
       lat_ms_.push_back(ms);
     else
@@ -186,9 +206,13 @@ void PlaneWorkerActor::on_done(PlaneRoundDone& d) {
 
 RoundLatency PlaneWorkerActor::round_latency() const {
   RoundLatency r;
-  r.count = lat_count_;
-  if (lat_ms_.empty()) return r;
-  std::vector<double> v = lat_ms_;
+  std::vector<double> v;
+  {
+    std::lock_guard<std::mutex> g(lat_mu_);
+    r.count = lat_count_;
+    v = lat_ms_;
+  }
+  if (v.empty()) return r;
   std::sort(v.begin(), v.end());
   auto q = [&](double p) { return v[std::min(v.size() - 1, static_cast<size_t>(p * (v.size() - 1) + 0.5))]; };
   r.p50_ms = q(0.5);

@@ -19,8 +19,10 @@
 // stashed and older ones dropped (Q2).
 #pragma once
 
+#include <atomic>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <set>
 #include <vector>
 
@@ -34,6 +36,8 @@ namespace mxar {
 struct PlaneWorkerStats {
   uint64_t start_in = 0, rounds_launched = 0, cold_rounds = 0, forced_completions = 0, rounds_completed = 0;
   uint64_t complete_out = 0, stale_dropped = 0, stashed = 0, plane_errors = 0, inits = 0;
+  // rounds a StartAllreduce jumped ahead to because a newer one was already in the mailbox
+  uint64_t starts_coalesced = 0;
 };
 
 class PlaneWorkerActor final : public Actor {
@@ -45,6 +49,11 @@ class PlaneWorkerActor final : public Actor {
   // kernel would otherwise wait out its deadline for peers that moved on without it, holding
   // its hardware queue (and a resident kernel) meanwhile
   void post_stop(ActorContext&) override { plane_->abort(0x7fffffff); }
+  // The newest StartAllreduce enqueued (epoch, round): a worker that fell behind its mailbox
+  // (a slow dataSource) catches up to it at once instead of fetching every queued round -
+  // the GPU analogue of the reference's future-round message making a laggard StartAllreduce
+  // (AllreduceWorker.scala:123-126), which on the device is the peers' FORCE word.
+  void on_enqueue(const Message& m) override;
   std::string kind() const override { return "plane-worker"; }
 
   int id() const { return id_; }
@@ -52,6 +61,7 @@ class PlaneWorkerActor final : public Actor {
   int max_round() const { return maxRound_; }
   int launched() const { return launched_; }
   int64_t epoch() const { return cfg_.epoch; }
+  int peers() const { return cfg_.peers; }
   bool initialized() const { return id_ >= 0; }
   const PlaneWorkerStats& stats() const { return stats_; }
   RoundLatency round_latency() const;
@@ -71,7 +81,9 @@ class PlaneWorkerActor final : public Actor {
   int id_ = -1;
   int round_ = -1, maxRound_ = -1, launched_ = -1;
   std::set<int> completed_;
+  std::atomic<uint64_t> announced_{0};  // (epoch low 32 bits << 32) | round of the newest Start enqueued
   std::map<int, uint64_t> t0_;
+  mutable std::mutex lat_mu_;  // lat_ms_: round_latency() may be called from another thread
   std::vector<double> lat_ms_;
   size_t lat_pos_ = 0;
   uint64_t lat_count_ = 0;

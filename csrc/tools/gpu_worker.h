@@ -15,8 +15,18 @@ struct GpuWorkerParts {
   std::function<void()> at_exit;      // after the job (MXAR_PLANE_STAMPS: write the last round's stamps)
 };
 
-GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag, int grid, double timeout_s,
-                               int64_t min_chunk, bool static_source, int dtype)
-    __attribute__((weak));
+struct GpuWorkerOptions {
+  int device = 0, size = 10, max_peers = 8, max_lag = 4, grid = 0;
+  double timeout_s = 60.0;
+  int64_t min_chunk = 0;
+  bool static_source = false;  // the same buffer every round (data[i] = i, or source_value)
+  bool has_value = false;      // --source-value V: a static source holding V everywhere
+  double source_value = 0.0;
+  double source_delay_us = 0.0;  // --source-delay-us D: every fetch waits D us first (a straggler)
+  double lag_wait_us = -1.0;     // --lag-wait-us W: XgmiPlaneOptions::lag_wait_us
+  int dtype = 0;
+};
+
+GpuWorkerParts make_gpu_worker(const GpuWorkerOptions& g) __attribute__((weak));
 
 }  // namespace mxar

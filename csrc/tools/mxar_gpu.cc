@@ -4,6 +4,7 @@
 // worker (AllreduceWorker.scala:272-301) with its rounds on GPU k: an XgmiRoundPlane
 // (csrc/hip/xgmi_plane.h) under a PlaneWorkerActor, the demo source data[i] = i + iteration
 // produced by the fill_iota kernel - no Python anywhere in the round path.
+#include "../core/delay.h"
 #include "../core/env.h"
 #include <hip/hip_runtime.h>
 
@@ -42,10 +43,15 @@ struct InputPool {
 };
 }  // namespace
 
-GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag, int grid, double timeout_s,
-                               int64_t min_chunk, bool static_source, int dtype) {
+GpuWorkerParts make_gpu_worker(const GpuWorkerOptions& g) {
   // dtype: 0 float32 (the reference's element type), 1 bfloat16, 2 float16 - the plane's
   // element type and the source's (the kernel sums in fp32 and rounds once)
+  const int device = g.device, size = g.size, max_peers = g.max_peers, max_lag = g.max_lag, grid = g.grid;
+  const double timeout_s = g.timeout_s;
+  const int64_t min_chunk = g.min_chunk;
+  const bool static_source = g.static_source || g.has_value;
+  const int dtype = g.dtype;
+  const double delay_us = g.source_delay_us;
   XgmiPlaneOptions o;
   o.device = device;
   o.dtype = static_cast<DType>(dtype);
@@ -55,6 +61,7 @@ GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag,
   o.grid = grid;
   o.timeout_s = timeout_s;
   o.min_chunk = min_chunk;
+  o.lag_wait_us = g.lag_wait_us;
   GpuWorkerParts p;
   auto plane = make_xgmi_plane(o);
   p.plane = plane;
@@ -99,18 +106,25 @@ GpuWorkerParts make_gpu_worker(int device, int size, int max_peers, int max_lag,
     // tensor dataSource; isolates the engine from the per-round fill)
     void* mem = nullptr;
     if (hipMalloc(&mem, bytes) != hipSuccess) throw std::runtime_error("mxar-gpu: hipMalloc failed");
-    launch_fill_iota(mem, size, 0.0, o.dtype, s);
+    if (g.has_value)
+      launch_fill_affine(mem, size, 0.0, g.source_value, o.dtype, s);
+    else
+      launch_fill_iota(mem, size, 0.0, o.dtype, s);
     if (hipStreamSynchronize(s) != hipSuccess) throw std::runtime_error("mxar-gpu: source fill failed");
     std::shared_ptr<void> owner(mem, [](void* q) { (void)hipFree(q); });
     auto payload = std::make_shared<DevicePayload>(owner, 0, static_cast<size_t>(size), device, nullptr, nullptr, dtype);
-    p.source = [payload](const AllReduceInputRequest&) { return AllReduceInput{payload}; };
+    p.source = [payload, delay_us](const AllReduceInputRequest&) {
+      precise_delay_us(delay_us);
+      return AllReduceInput{payload};
+    };
     return p;
   }
   // the demo source (AllreduceWorker.scala:272-301): data[i] = i + iteration, produced by the
   // fill_iota kernel on the plane's stream into a pooled buffer
   auto pool = std::make_shared<InputPool>();
   const DType dt = o.dtype;
-  p.source = [device, size, s, src_stream, bytes, pool, dt, dtype](const AllReduceInputRequest& r) {
+  p.source = [device, size, s, src_stream, bytes, pool, dt, dtype, delay_us](const AllReduceInputRequest& r) {
+    precise_delay_us(delay_us);
     void* mem = nullptr;
     {
       std::lock_guard<std::mutex> g(pool->mu);

@@ -41,6 +41,7 @@
 
 #include "../cluster/cluster_node.h"
 #include "../core/log.h"
+#include "../core/output_check.h"
 #include "../runtime/allreduce_actors.h"
 #include "../runtime/plane_worker.h"
 #include "gpu_worker.h"
@@ -79,6 +80,11 @@ struct Options {
   bool static_source = false;  // --source static: the same input every round (default iota: i + iteration)
   int dtype = 0;     // --dtype fp32|bf16|fp16 (GPU worker element type)
   int spin_us = -1;  // --spin-us N: dispatcher idle spin + cluster reader socket poll (-1: built-in defaults)
+  bool has_value = false;    // --source-value V: static source, V everywhere (the straggler bench: 1, 2, 4, ...)
+  double source_value = 0.0;
+  double source_delay_us = 0.0;  // --source-delay-us D: every fetch waits D us (a straggling dataSource)
+  double lag_wait_us = -1.0;     // --lag-wait-us W: a round waits at most W us for a lagging peer
+  int check_chunk = 0;           // --check-chunk C: check the last output (power-of-two sources, maxChunkSize C)
 };
 
 // --spin-us: how long an idle actor dispatcher and a cluster reader keep polling before they
@@ -103,7 +109,8 @@ void apply_spin(int us) {
                "master control bridge (docs/BRIDGE.md): --bridge PORT [--external-rounds]\n"
                "       mxar drive [host:]bridgePort [rounds] [--lockstep]   (bridge client)\n"
                "worker on a GPU (mxar-gpu): --device K [--max-peers N --plane-max-lag N --grid N --plane-timeout S\n"
-               "                              --min-chunk N --source iota|static --dtype fp32|bf16|fp16]\n"
+               "                              --min-chunk N --source iota|static --dtype fp32|bf16|fp16\n"
+               "                              --source-value V --source-delay-us D --lag-wait-us W --check-chunk C]\n"
                "host threads: --spin-us N (dispatcher + socket polling; GPU workers default 500)\n",
                msg);
   std::exit(2);
@@ -150,6 +157,13 @@ Options parse(int argc, char** argv) {
       if (v != "iota" && v != "static") usage("--source must be iota or static");
       o.static_source = v == "static";
     }
+    else if (a == "--source-value") {
+      o.has_value = true;
+      o.source_value = std::stod(val());
+    }
+    else if (a == "--source-delay-us") o.source_delay_us = std::stod(val());
+    else if (a == "--lag-wait-us") o.lag_wait_us = std::stod(val());
+    else if (a == "--check-chunk") o.check_chunk = std::stoi(val());
     else if (a.rfind("--", 0) == 0) usage(("unknown option " + a).c_str());
     else o.positional.push_back(a);
   }
@@ -237,6 +251,20 @@ void set_level(const std::string& l) {
   exit_now(finished.load() >= 0 ? 0 : 1);
 }
 
+const PlaneWorkerActor* plane_actor(const ActorRef& ref) {
+  auto* l = dynamic_cast<LocalActorRef*>(ref.get());
+  auto c = l ? l->cell() : nullptr;
+  return c ? dynamic_cast<const PlaneWorkerActor*>(c->actor()) : nullptr;
+}
+int plane_worker_peers(const ActorRef& ref) {
+  const PlaneWorkerActor* w = plane_actor(ref);
+  return w ? w->peers() : 0;
+}
+PlaneWorkerStats plane_worker_stats(const ActorRef& ref) {
+  const PlaneWorkerActor* w = plane_actor(ref);
+  return w ? w->stats() : PlaneWorkerStats{};
+}
+
 [[noreturn]] void run_worker(const Options& o) {
   const int port = pos_int(o, 0, 2553);
   const int size = pos_int(o, 1, 10);
@@ -250,14 +278,25 @@ void set_level(const std::string& l) {
   std::atomic<int> rounds{0};
   const bool quiet = o.quiet;
   // quiet: the newest output is kept (a reference, no copy) and checked once at the end, so a
-  // timed run reports the sum of its own last round (benchmarks/sections.py native_deployment)
+  // timed run reports the sum of its own last round (benchmarks/sections.py native_deployment);
+  // every round's sink time and count totals are kept for the summary line
   std::mutex last_mu;
   std::optional<AllReduceOutput> last;
-  DataSink sink = [&rounds, quiet, &last_mu, &last](const AllReduceOutput& out) {  // AllreduceWorker.scala:295-297
+  std::vector<double> sink_t;
+  uint64_t count_sum = 0, count_n = 0, count_zero = 0;
+  DataSink sink = [&rounds, quiet, &last_mu, &last, &sink_t, &count_sum, &count_n,
+                   &count_zero](const AllReduceOutput& out) {  // AllreduceWorker.scala:295-297
     rounds++;
     if (quiet) {
+      const double t = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
       std::lock_guard<std::mutex> g(last_mu);
       if (!last || out.iteration >= last->iteration) last = out;
+      if (sink_t.size() < (size_t{1} << 22)) sink_t.push_back(t);
+      for (int c : out.count) {
+        count_sum += static_cast<uint64_t>(c > 0 ? c : 0);
+        count_zero += c == 0 ? 1 : 0;
+      }
+      count_n += out.count.size();
     }
     if (!quiet) {  // quiet: no copy back of a device output either
       const std::vector<float> d = out.data->to_host();
@@ -270,13 +309,27 @@ void set_level(const std::string& l) {
   };
   ClusterConfig cc;
   std::function<void()> gpu_at_exit;
+  ActorRef plane_worker;
   if (o.device >= 0) {  // the round engine on a GPU: one threshold-kernel launch per round
     if (make_gpu_worker == nullptr) usage("--device needs the GPU build of this executable: mxar-gpu");
-    GpuWorkerParts g = make_gpu_worker(o.device, size, o.max_peers, o.plane_max_lag, o.grid, o.plane_timeout_s,
-                                         o.min_chunk, o.static_source, o.dtype);
+    GpuWorkerOptions go;
+    go.device = o.device;
+    go.size = size;
+    go.max_peers = o.max_peers;
+    go.max_lag = o.plane_max_lag;
+    go.grid = o.grid;
+    go.timeout_s = o.plane_timeout_s;
+    go.min_chunk = o.min_chunk;
+    go.static_source = o.static_source;
+    go.has_value = o.has_value;
+    go.source_value = o.source_value;
+    go.source_delay_us = o.source_delay_us;
+    go.lag_wait_us = o.lag_wait_us;
+    go.dtype = o.dtype;
+    GpuWorkerParts g = make_gpu_worker(go);
     cc.meta = g.plane->descriptor();  // relayed by the master in InitWorkers.planes
     gpu_at_exit = g.at_exit;
-    sys->actor_of(std::make_unique<PlaneWorkerActor>(g.source, sink, g.plane), "worker");
+    plane_worker = sys->actor_of(std::make_unique<PlaneWorkerActor>(g.source, sink, g.plane), "worker");
   } else {
     sys->actor_of(std::make_unique<WorkerActor>(src, sink), "worker");
   }
@@ -301,11 +354,44 @@ void set_level(const std::string& l) {
   if (gpu_at_exit) gpu_at_exit();
   {
     std::lock_guard<std::mutex> g(last_mu);
+    std::string check = "null";
+    int last_round = -1;
     if (last) {
       const std::vector<float> d = last->data->to_host();
       const double sum = std::accumulate(d.begin(), d.end(), 0.0);
       std::printf("[mxar worker] last round %d sum %.1f\n", last->iteration, sum);
+      last_round = last->iteration;
+      if (o.check_chunk > 0 && !last->count.empty()) {
+        const int peers = plane_worker ? plane_worker_peers(plane_worker) : 0;
+        const OutputCheck c = check_power_of_two_output(d, last->count, peers, o.check_chunk);
+        check = c.ok ? "true" : "false";
+        if (!c.ok)
+          std::printf("[mxar worker] check failed: %lld of %lld chunks\n", static_cast<long long>(c.bad_chunks),
+                      static_cast<long long>(c.chunks));
+      }
       last.reset();
+    }
+    if (quiet && sink_t.size() > 4) {
+      // the worker's own round period: intervals between consecutive sink calls, the first
+      // tenth left out (warm-up)
+      std::vector<double> iv;
+      for (size_t i = std::max<size_t>(1, sink_t.size() / 10); i < sink_t.size(); ++i)
+        iv.push_back((sink_t[i] - sink_t[i - 1]) * 1e6);
+      std::sort(iv.begin(), iv.end());
+      double mean = 0;
+      for (double x : iv) mean += x;
+      mean /= static_cast<double>(iv.size());
+      PlaneWorkerStats ps{};
+      if (plane_worker) ps = plane_worker_stats(plane_worker);
+      std::printf("{\"worker_summary\": {\"rounds\": %zu, \"last_round\": %d, \"period_p50_us\": %.2f, "
+                  "\"period_p99_us\": %.2f, \"period_mean_us\": %.2f, \"count_mean\": %.4f, \"count_zero_frac\": %.4f, "
+                  "\"forced\": %llu, \"cold\": %llu, \"coalesced\": %llu, \"plane_errors\": %llu, \"validated\": %s}}\n",
+                  sink_t.size(), last_round, iv[iv.size() / 2], iv[std::min(iv.size() - 1, iv.size() * 99 / 100)], mean,
+                  count_n ? static_cast<double>(count_sum) / static_cast<double>(count_n) : 0.0,
+                  count_n ? static_cast<double>(count_zero) / static_cast<double>(count_n) : 0.0,
+                  static_cast<unsigned long long>(ps.forced_completions), static_cast<unsigned long long>(ps.cold_rounds),
+                  static_cast<unsigned long long>(ps.starts_coalesced), static_cast<unsigned long long>(ps.plane_errors),
+                  check.c_str());
     }
   }
   std::printf("[mxar worker] %d rounds completed\n", rounds.load());

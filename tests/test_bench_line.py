@@ -22,7 +22,7 @@ def _n8_shape(base: dict) -> dict:
     """Every section an N = 8 run adds (sweep, collectives, rccl, threshold, dp with the
     schedule variants), with the widest values they can carry."""
     r = copy.deepcopy(base)
-    r.update(n_gpus=8, value=4321.12, algbw_per_rank=540.14, busbw=945.25)
+    r.update(n_gpus=8, value=540.14, algbw_per_rank=540.14, algbw_sum_over_ranks=4321.12, busbw=945.25)
     r["config"] = dict(r["config"], algo="twoshot@256~1", parallelism="dp8", global_batch=8)
     r["rccl"] = {"algbw": 401.23, "ms_per_step": 0.6691, "p50_ms": 0.6654, "note": "copy + in-place dist.all_reduce"}
     r["speedup_vs_rccl"] = 1.346
@@ -93,6 +93,8 @@ def test_n8_summaries():
     d = json.loads(line(_n8_shape(_full_n1())))
     assert len(d["sweep"]) == 9 and d["sweep"][0] == [4096, "twoshot@256~1", 123456.78, 123456.78]
     assert d["speedup_vs_rccl"] == 1.346 and d["rccl"]["algbw"] == 401.23
+    # the headline is the nccl-tests algbw (S / t), the N-sum under its own key
+    assert d["value"] == d["algbw_per_rank"] == 540.14 and d["algbw_sum_over_ranks"] == 4321.12
     assert set(d["collectives"]) == {"all_to_all", "all_gather", "reduce_scatter"}
 
 
@@ -172,7 +174,7 @@ def test_headline_guard_keeps_lossy_and_library_paths_out():
     from akka_allreduce_1_amd.parallel import comm
     from benchmarks.summary import LOSSY_ALGOS, headline_guard
 
-    assert tuple(comm.LOSSY_ALGOS) == LOSSY_ALGOS and tuple(comm.LIBRARY_ALGOS) == LIBRARY_ALGOS
+    assert comm.LOSSY_ALGOS is LOSSY_ALGOS and comm.LIBRARY_ALGOS is LIBRARY_ALGOS  # one definition
     for auto_pick in ("ring_native", "ring_native@128", "rccl", "rsag"):
         algo, note = headline_guard(auto_pick, "auto", 8)
         assert algo == "twoshot" and note
