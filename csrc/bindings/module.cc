@@ -23,6 +23,7 @@
 #include "../runtime/allreduce_actors.h"
 #include "../runtime/fault_injector.h"
 #include "../runtime/loopback_plane.h"
+#include "../runtime/plane_geometry.h"
 #include "../runtime/plane_worker.h"
 #include "py_common.h"
 
@@ -469,6 +470,31 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("record") = false,
         "dataSink keeping only the newest round output, without the GIL (plane workers); record: per-round "
         "sink stamps and count totals too");
+
+  m.def("plane_geometry",
+        [](int peers, int dataSize, int maxChunkSize, float thReduce, float thComplete,
+           std::map<int, std::string> descriptors, int64_t flag_maxch, int64_t es) {
+          PlaneConfig c;
+          c.peers = peers;
+          c.dataSize = dataSize;
+          c.maxChunkSize = maxChunkSize;
+          c.thReduce = thReduce;
+          c.thComplete = thComplete;
+          c.descriptors = std::move(descriptors);
+          const PlaneGeometry g = plane_geometry(c, flag_maxch, es);
+          py::dict d;
+          d["block"] = g.block;
+          d["chunk"] = g.chunk;
+          d["nch"] = g.nch;
+          d["nch_ref"] = g.nch_ref;
+          d["coarse"] = g.coarse;
+          d["colocation"] = g.colocation;
+          d["grid"] = g.grid;
+          return d;
+        },
+        py::arg("peers"), py::arg("dataSize"), py::arg("maxChunkSize"), py::arg("thReduce"), py::arg("thComplete"),
+        py::arg("descriptors"), py::arg("flag_maxch") = 1 << 20, py::arg("es") = 4,
+        "The kernel geometry every worker of a membership derives from InitWorkers (csrc/runtime/plane_geometry.h)");
 
   // ---------------------------------------------------------------- core helpers
   m.def("f32_threshold_count", &f32_threshold_count, py::arg("threshold"), py::arg("peers"));

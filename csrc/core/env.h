@@ -6,6 +6,9 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
+#include <set>
+#include <string>
 
 namespace mxar {
 
@@ -17,12 +20,17 @@ inline bool study_mode() {
   return on;
 }
 
-// The study knob `name`, or nullptr outside study mode (a set knob is then reported once).
+// The study knob `name`, or nullptr outside study mode (a set knob is then reported once per
+// process, however many communicators or planes read it).
 inline const char* study_env(const char* name) {
   const char* v = std::getenv(name);
   if (v == nullptr) return nullptr;
   if (study_mode()) return v;
-  std::fprintf(stderr, "[mxar] %s ignored: study knob, needs MXAR_STUDY=1 (docs/TUNING.md)\n", name);
+  static std::mutex mu;
+  static std::set<std::string> reported;
+  std::lock_guard<std::mutex> g(mu);
+  if (reported.insert(name).second)
+    std::fprintf(stderr, "[mxar] %s ignored: study knob, needs MXAR_STUDY=1 (docs/TUNING.md)\n", name);
   return nullptr;
 }
 

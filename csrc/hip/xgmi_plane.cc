@@ -1,6 +1,8 @@
 #include "../core/env.h"
 #include "xgmi_plane.h"
 
+#include "../runtime/plane_geometry.h"
+
 #include <sys/prctl.h>
 #include <unistd.h>
 
@@ -10,6 +12,7 @@
 #include <cstdlib>
 #include <chrono>
 #include <cstring>
+#include <functional>
 #include <random>
 #include <sstream>
 #include <string>
@@ -68,39 +71,10 @@ std::string to_hex(const std::string& b) {
   return s;
 }
 
-std::string from_hex(const std::string& h) {
-  if (h.size() % 2) throw ProtocolError("plane descriptor: odd hex length");
-  std::string b(h.size() / 2, '\0');
-  for (size_t i = 0; i < b.size(); ++i) b[i] = static_cast<char>(std::stoi(h.substr(2 * i, 2), nullptr, 16));
-  return b;
-}
-
-struct Desc {
-  long pid = 0;
-  int device = 0;
-  int64_t bytes = 0;
-  uint64_t id = 0;
-  std::string handle;
-};
-
-// "xgmi1 pid=<pid> dev=<device> bytes=<arena bytes> id=<arena id> h=<hex IPC handle>"
-Desc parse_desc(const std::string& s) {
-  std::istringstream is(s);
-  std::string tag;
-  is >> tag;
-  if (tag != "xgmi1") throw ProtocolError("not an xGMI plane descriptor: '" + s.substr(0, 40) + "'");
-  Desc d;
-  std::string kv;
-  while (is >> kv) {
-    const size_t eq = kv.find('=');
-    if (eq == std::string::npos) continue;
-    const std::string k = kv.substr(0, eq), v = kv.substr(eq + 1);
-    if (k == "pid") d.pid = std::stol(v);
-    else if (k == "dev") d.device = std::stoi(v);
-    else if (k == "bytes") d.bytes = std::stoll(v);
-    else if (k == "id") d.id = std::stoull(v);
-    else if (k == "h") d.handle = from_hex(v);
-  }
+// "xgmi1 pid=<pid> dev=<device> bytes=<arena bytes> id=<arena id> grid=<G> wgc=<cap>
+// coarsen=<0|1> h=<hex IPC handle>" (csrc/runtime/plane_geometry.h); the IPC handle is required
+PlaneDesc parse_desc(const std::string& s) {
+  PlaneDesc d = parse_plane_desc(s);
   if (d.handle.size() != sizeof(hipIpcMemHandle_t)) throw ProtocolError("plane descriptor without an IPC handle");
   return d;
 }
@@ -129,6 +103,10 @@ struct PlaneGroup {
   uint64_t* gdm = nullptr;                // device words: [0] the dispatcher's heartbeat
   hipStream_t stream = nullptr;
   bool launched = false;                  // a kernel was launched (gword[0] says whether it left)
+  // memory of workers whose STOP the kernel never took (XgmiRoundPlane::leave_group): the
+  // kernel may still poll their doors and words, so it is freed only once the kernel is
+  // known to have exited - or never (leaked) if it did not
+  std::vector<std::function<void()>> orphans;
   std::mutex mu;
 
   PlaneGroup(std::string k, int dev, int workers, bool high_priority) : key(std::move(k)), device(dev) {
@@ -154,9 +132,17 @@ struct PlaneGroup {
     while (launched && g[0] != kResExited && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10))
       std::this_thread::sleep_for(std::chrono::microseconds(50));
     (void)hipSetDevice(device);
+    const bool exited = !launched || g[0] == kResExited;
+    if (exited) {
+      (void)hipStreamSynchronize(stream);
+      for (auto& f : orphans) f();
+    } else if (!orphans.empty()) {
+      MXAR_LOG(ERROR, "plane", "group kernel still running at teardown: " << orphans.size()
+                                                                            << " workers' round memory leaked");
+    }
     (void)hipFreeAsync(gdm, stream);
     (void)hipStreamDestroy(stream);
-    if (!launched || g[0] == kResExited) give_group_word(gword);  // else leaked: a kernel may still write it
+    if (exited) give_group_word(gword);  // else leaked: a kernel may still write it
   }
   volatile uint32_t* state_word() const { return gword; }
   bool kernel_left() const { return !launched || reinterpret_cast<volatile uint32_t*>(gword)[0] == kResExited; }
@@ -353,8 +339,18 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
     g_arenas[arena_id_] = arena_;
   }
   std::ostringstream os;
+  // the knobs that shape a round's geometry travel in the descriptor: every worker of a job
+  // derives the same chunking from InitWorkers alone (plane_geometry.h)
+  int eff_grid = o_.grid;
+  if (eff_grid <= 0) {
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device);
+    eff_grid = 2 * cus;
+    if (const char* g = std::getenv("MXAR_GRID")) eff_grid = std::max(1, std::atoi(g));
+  }
   os << "xgmi1 pid=" << static_cast<long>(getpid()) << " dev=" << o_.device << " bytes=" << arena_bytes_
-     << " id=" << arena_id_ << " h=" << to_hex(std::string(reinterpret_cast<const char*>(&h), sizeof(h)));
+     << " id=" << arena_id_ << " grid=" << eff_grid << " wgc=" << wg_chunks_ << " coarsen=" << (coarsen_full_ ? 1 : 0)
+     << " h=" << to_hex(std::string(reinterpret_cast<const char*>(&h), sizeof(h)));
   desc_ = os.str();
   th_ = std::thread([this] { completion_loop(); });
   MXAR_LOG(INFO, "plane", "xgmi plane on device " << o_.device << ": arena " << (arena_bytes_ >> 20) << " MiB for <= "
@@ -553,7 +549,7 @@ void XgmiRoundPlane::set_done(DoneFn fn) {
 }
 
 char* XgmiRoundPlane::map_peer(const std::string& desc) {
-  const Desc d = parse_desc(desc);
+  const PlaneDesc d = parse_desc(desc);
   if (d.pid == static_cast<long>(getpid())) {  // a worker of this process: no IPC
     std::lock_guard<std::mutex> g(g_arena_mu);
     auto it = g_arenas.find(d.id);
@@ -601,80 +597,31 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
     drain();
   }
   leave_group();
+  if (orphaned_) {
+    configured_ = false;
+    throw ProtocolError("xgmi plane: the group kernel never released this worker (its STOP was not taken); "
+                        "the plane cannot be configured again");
+  }
   park_resident();  // the stream work below must not queue behind it
   rplan_tried_ = false;
   rplan_ = XgmiComm::ResidentPlan();
   hip_check(hipSetDevice(o_.device), "hipSetDevice");
   const int P = cfg.peers;
   const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
-  // the reference's geometry: blocks of step = ceil(N / P) (float32 division,
-  // AllreduceWorker.scala:211-214), chunks of maxChunkSize elements (:56-57)
-  block_ = static_cast<int64_t>(f32_ceil_div(cfg.dataSize, P));
-  chunk_ = cfg.maxChunkSize;
-  int64_t nch = std::max<int64_t>(1, ceil_div(block_, chunk_));
-  const int64_t slot = std::max<int64_t>(block_ * es, 16);
+  const int64_t slot = std::max<int64_t>(static_cast<int64_t>(f32_ceil_div(cfg.dataSize, P)) * es, 16);
   const XgmiComm::Layout L = XgmiComm::layout(P, slot, cfg.maxLag + 1, flag_bytes_, flag_gran_);
   if (L.slab_bytes > arena_bytes_) throw ProtocolError("xgmi plane arena too small for this membership");
-  nch_ref_ = static_cast<int>(nch);
-  coarse_ = 1;
-  if (nch > L.maxch) {
-    // More reference chunks than the flag table holds (maxChunkSize below the plane's flag
-    // granularity). At thresholds 1 every contribution and every chunk is taken whatever the
-    // granularity, so the kernel runs whole multiples of maxChunkSize and the counts are
-    // reported per reference chunk. Below 1 the threshold decisions ARE per reference chunk
-    // (DataBuffer.scala:28-29,69-75): coarser units would change which data a round keeps.
-    if (cfg.thReduce < 1.f || cfg.thComplete < 1.f)
-      throw ProtocolError("maxChunkSize " + std::to_string(cfg.maxChunkSize) + " at thReduce " +
-                          std::to_string(cfg.thReduce) + " / thComplete " + std::to_string(cfg.thComplete) +
-                          " needs one flag per chunk: build the plane with min_chunk <= " +
-                          std::to_string(cfg.maxChunkSize) + " (PlaneJob(min_chunk=...), mxar.plane.min_chunk)");
-    const int64_t m = ceil_div(nch, L.maxch);
-    chunk_ *= m;
-    coarse_ = static_cast<int>(m);
-    nch = ceil_div(block_, chunk_);
-    st_.coarsened++;
+  // the round geometry from InitWorkers alone: every worker of the job computes the same one
+  const PlaneGeometry geo = plane_geometry(cfg, L.maxch, es);
+  block_ = geo.block;
+  chunk_ = geo.chunk;
+  nch_ref_ = geo.nch_ref;
+  coarse_ = geo.coarse;
+  const int64_t nch = geo.nch;
+  if (geo.coarse > 1) st_.coarsened++;
+  if (geo.coarsened_for_flags)
     MXAR_LOG(INFO, "plane", "maxChunkSize " << cfg.maxChunkSize << " is finer than the flag table at thresholds 1: "
                                             << "kernel chunks of " << chunk_ << " elements, counts per reference chunk");
-  }
-  // Full thresholds: every contribution and every chunk is taken whatever the chunking, so the
-  // kernel may also run whole multiples of maxChunkSize for speed (counts still reported per
-  // reference chunk). Every kernel chunk costs a flag hand-off and a release per hop, so 2 KiB
-  // chunks spend more time on hand-offs than on bytes: kernel chunks of >= 32 KiB, while
-  // every fourth workgroup still gets a reduce unit. Same-box A/B (plane_probe --units):
-  // 8 workers x 16 MiB, 8 -> 32 KiB chunks 0.350 / 0.358 -> 0.307 / 0.272 ms per round; 2 x 1 MiB,
-  // 2 -> 8 KiB 0.069 / 0.057 -> 0.061 / 0.049 ms. MXAR_PLANE_COARSEN=0 keeps maxChunkSize.
-  if (cfg.thReduce >= 1.f && cfg.thComplete >= 1.f && coarsen_full_) {
-    int gx = o_.grid;
-    if (gx <= 0) {
-      int cus = 256;
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device);
-      gx = 2 * cus;
-      if (const char* g = std::getenv("MXAR_GRID")) gx = std::max(1, std::atoi(g));
-    }
-    const int64_t want = ceil_div(int64_t{32} << 10, chunk_ * es);
-    const int64_t room = std::max<int64_t>(1, nch / std::max(1, gx / 4));
-    // ...and, for workers sharing one group kernel, at most one kernel chunk per workgroup: a
-    // workgroup that reduces two chunks pays the second chunk's hand-offs after the first
-    // one's, on the round's critical path. 2 co-located workers x 128 workgroups, bf16
-    // (profiles/round5/protocol_grid_chunk.jsonl): 64 MiB 159-164 -> 145-149 us per round,
-    // 16 MiB 86-95 -> 74-75, 256 MiB 441-474 -> 426-454. A worker alone in its process keeps
-    // the finer chunks: 8 such processes sharing one GPU did not gain from it (noisy,
-    // rehearsal_grid.jsonl), and over xGMI it is unmeasured.
-    int64_t m = std::min(want, room);
-    if (wg_chunks_ > 0 && colocated(cfg).size() > 1)
-      m = std::max(m, ceil_div(nch, static_cast<int64_t>(std::max(1, gx)) * wg_chunks_));
-    // a block of at most 32 KiB is ONE kernel chunk: one hand-off per peer instead of one per
-    // chunk - each hand-off is a release, a flag and a wait on the round's critical path, and
-    // below 32 KiB there are no bytes to spread over more workgroups (the reference's
-    // default job, 10 floats in 2-float chunks: 3 chunks per block -> 1)
-    if (block_ * es <= (int64_t{32} << 10)) m = nch;
-    if (m > 1) {
-      chunk_ *= m;
-      coarse_ *= static_cast<int>(m);
-      nch = ceil_div(block_, chunk_);
-      if (coarse_ == static_cast<int>(m)) st_.coarsened++;
-    }
-  }
   nch_ = static_cast<int>(nch);
   std::vector<char*> bases(P, nullptr);
   for (int k = 0; k < P; ++k) {
@@ -728,7 +675,7 @@ std::vector<std::pair<int, uint64_t>> XgmiRoundPlane::colocated(const PlaneConfi
   for (int k = 0; k < cfg.peers; ++k) {
     auto it = cfg.descriptors.find(k);
     if (it == cfg.descriptors.end() || it->second.empty()) continue;
-    const Desc d = parse_desc(it->second);
+    const PlaneDesc d = parse_desc(it->second);
     if (d.pid == static_cast<long>(getpid()) && d.device == o_.device) v.emplace_back(k, d.id);
   }
   return v;
@@ -808,6 +755,7 @@ void XgmiRoundPlane::leave_group() {
     std::lock_guard<std::mutex> lk(g->mu);
     serving = g->in_kernel[static_cast<size_t>(gidx_)] != 0 && !g->kernel_left();
   }
+  bool lost = false;
   if (serving) {
     // a STOP entry ends this worker's slice; the kernel goes on for the others (or leaves
     // when this was the last)
@@ -819,11 +767,38 @@ void XgmiRoundPlane::leave_group() {
       while (static_cast<int32_t>(rstate_[1] - seq) < 0 && !g->kernel_left()) {
         if (std::chrono::steady_clock::now() - t0 > std::chrono::duration<double>(2 * o_.timeout_s + 5)) {
           MXAR_LOG(ERROR, "plane", "the group kernel did not take this worker's STOP");
+          lost = true;
           break;
         }
         std::this_thread::sleep_for(std::chrono::microseconds(20));
       }
     }
+  }
+  if (lost) {
+    // The kernel may still serve this worker's slice: its door, device words, force / abort
+    // words, counts, control words, split scratch and arena stay allocated until the group
+    // sees the kernel exit (PlaneGroup::orphans), never freed under a running kernel
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->orphans.push_back([door = door_, rdm = rdm_, hforce = hforce_, ctl = ctl_mem_, split = split_mem_,
+                          cnt = cnt_vram_, ring = ring_, arena = arena_] {
+      (void)hipHostFree(door);
+      (void)hipHostFree(hforce);
+      (void)hipHostFree(ring);
+      (void)hipFree(rdm);
+      (void)hipFree(ctl);
+      (void)hipFree(split);
+      (void)hipFree(cnt);
+      (void)hipFree(arena);
+    });
+    door_ = nullptr;
+    rdm_ = nullptr;
+    hforce_ = nullptr;
+    ctl_mem_ = nullptr;
+    split_mem_ = nullptr;
+    cnt_vram_ = nullptr;
+    ring_ = nullptr;
+    arena_ = nullptr;
+    orphaned_ = true;
   }
   rstate_[1] = res_seq_ - 1u;  // entries no kernel took are dropped
   {
@@ -1236,6 +1211,7 @@ bool XgmiRoundPlane::launch_resident(int round, const Payload& input, bool cold)
 
 void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   if (!configured_) throw ProtocolError("xgmi plane: launch before configure (InitWorkers)");
+  if (orphaned_) throw ProtocolError("xgmi plane: its round memory was handed to a group kernel that never left");
   if (round != last_round_ + 1) throw ProtocolError("xgmi plane: rounds must be launched in order");
   hip_check(hipSetDevice(o_.device), "hipSetDevice");
   if (group_) {

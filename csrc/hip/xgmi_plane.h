@@ -189,6 +189,9 @@ class XgmiRoundPlane final : public RoundPlane {
   // the workers of this membership in this process on this device: (rank, arena id)
   std::vector<std::pair<int, uint64_t>> colocated(const PlaneConfig& cfg) const;
   bool grouped_ = false;  // this membership has co-located workers (configure)
+  // the group kernel never took this worker's STOP: its round memory went to the group
+  // (PlaneGroup::orphans) and the plane can run no further round
+  bool orphaned_ = false;
   std::shared_ptr<PlaneGroup> group_;
   int gidx_ = -1;                      // this worker's index in the group
   XgmiComm::ResidentPlan gplan_;       // the group kernel's geometry for this membership
