@@ -14,9 +14,9 @@ times that on the GPU round engine (PlaneWorkerActor + XgmiRoundPlane):
 * `sweep`: P = 4 co-located workers (one group kernel), thReduce = thComplete = thAllreduce
   = 0.75, maxLag 1 and 2, one worker's dataSource delayed by 0 / 0.2 / 2 ms per round
   (native tensor source, csrc/hip/hip_bind.cc tensor_source(delay_us)), rounds of 40 B /
-  1 MiB / 64 MiB per worker. Lag skip on (lag_wait_us 0): a fast round never waits at its lag
-  gate for the straggler (xgmi_threshold.hip). One 2 ms case with the waiting gate shows what
-  bounded buffers cost without it.
+  1 MiB / 64 MiB per worker. Lag skip on: a fast round waits at most lag_wait_us at its lag
+  gate for the straggler, then runs without it and forces it (xgmi_threshold.hip; sticky while
+  it lags). One 2 ms case with the waiting gate shows what bounded buffers cost without it.
 * `native`: the deployment shape, 2 worker processes (P = 2: thReduce 0.75 -> 1 of 2,
   thComplete and thAllreduce 0.5, so the fast worker can finish on its own block), one of
   them delayed.
@@ -95,10 +95,10 @@ def inproc_case(dev, P: int, nbytes: int, dtype, chunk: int, max_lag: int, delay
     bufs = [torch.full((n,), float(1 << k), dtype=dtype, device=dev) for k in range(P)]
     srcs = [C.hip.tensor_source(b, delay_us=delay_us if k == slow else 0.0) for k, b in enumerate(bufs)]
     torch.cuda.synchronize(dev)
-    row: dict = {"delay_us": delay_us, "max_lag": max_lag, "rounds": rounds}
+    row: dict = {"delay_us": delay_us, "max_lag": max_lag, "rounds": rounds, "lag_wait_us": lag_wait_us}
     job = PlaneJob(P, n, max_chunk_size=chunk, th_allreduce=th_all, th_reduce=th, th_complete=th, max_lag=max_lag,
                    max_round=rounds - 1, dtype=dtype, sources=srcs, keep_outputs=False, keep_last=True, record=True,
-                   timeout_s=20.0, lag_wait_us=lag_wait_us)
+                   timeout_s=8.0, lag_wait_us=lag_wait_us)
     fast = [k for k in range(P) if k != slow]
     strag = slow if 0 <= slow < P else None
     try:
@@ -165,8 +165,12 @@ SIZES = ((40, torch.float32, 1500), (1 << 20, torch.bfloat16, 1200), (64 << 20, 
 
 
 def sweep(dev, P: int = 4, lags=(1, 2), delays=(0.0, 200.0, 2000.0), sizes=SIZES, budget_s: float = 60.0) -> dict:
-    """The straggler sweep (module docstring). ratio = fast period (mean) / no-straggler period."""
-    out: dict = {"workers": P, "th": 0.75, "th_allreduce": 0.75, "straggler": 1, "lag_wait_us": 0.0,
+    """The straggler sweep (module docstring). ratio = fast period (mean) / no-straggler period.
+    Lag-skip policy: a peer still short of the lag gate after lag_wait_us is skipped (sticky
+    while it lags). The no-straggler case waits up to 5 ms (momentary lateness is waited
+    for); the straggler cases use lag_wait = 2 x that case's mean round period (>= 100 us)."""
+    out: dict = {"workers": P, "th": 0.75, "th_allreduce": 0.75, "straggler": 1,
+                 "lag_wait_us": "d0: 5000; stragglers: max(100, 2 x the d0 mean period)",
                  "sources": "worker k: 2^k everywhere (tensor sources; the straggler's delayed natively)"}
     t_end = time.monotonic() + budget_s
     for nbytes, dtype, rounds in sizes:
@@ -179,7 +183,8 @@ def sweep(dev, P: int = 4, lags=(1, 2), delays=(0.0, 200.0, 2000.0), sizes=SIZES
                 if time.monotonic() > t_end:
                     cell[f"lag{lag}_d{int(d)}"] = {"error": f"skipped: section budget {budget_s:g} s spent"}
                     continue
-                r = inproc_case(dev, P, nbytes, dtype, chunk, lag, d, rounds)
+                wait = 5000.0 if d == 0.0 else max(100.0, 2.0 * (base or 50.0))
+                r = inproc_case(dev, P, nbytes, dtype, chunk, lag, d, rounds, lag_wait_us=round(wait, 1))
                 if d == 0.0:
                     base = r.get("fast_period_mean_us")
                 elif base and r.get("fast_period_mean_us"):
@@ -191,6 +196,7 @@ def sweep(dev, P: int = 4, lags=(1, 2), delays=(0.0, 200.0, 2000.0), sizes=SIZES
         nb, dt, rounds = sizes[min(1, len(sizes) - 1)]
         _, chunk = _geometry(nb, dt, P)
         r = inproc_case(dev, P, nb, dt, chunk, 1, delays[-1], max(60, rounds // 20), lag_wait_us=None)
+        r["policy"] = "waiting lag gate (no skip): bounded buffers hold the fast workers within maxLag + 1 rounds"
         base = ((out.get(f"{nb}B") or {}).get("lag1_d0") or {}).get("fast_period_mean_us")
         if base and r.get("fast_period_mean_us"):
             r["ratio_vs_no_straggler"] = round(r["fast_period_mean_us"] / base, 3)
@@ -290,7 +296,7 @@ def native_cases(delays=(0.0, 2000.0), sizes=((10, 2, 1500), (262144, 1024, 1200
     """The 2-process deployment with a straggler (module docstring): worker 0 fast, worker 1
     delayed; fp32 sources 1 / 2."""
     out: dict = {"workers": 2, "th_reduce": 0.75, "th_complete": 0.5, "th_allreduce": 0.5, "max_lag": 1,
-                 "lag_wait_us": 0.0, "dtype": "float32"}
+                 "lag_wait_us": "d0: 5000; straggler: max(100, 2 x the d0 mean period)", "dtype": "float32"}
     t_end = time.monotonic() + budget_s
     for n, chunk, rounds in sizes:
         cell: dict = {"max_chunk_size": chunk}
@@ -300,8 +306,10 @@ def native_cases(delays=(0.0, 2000.0), sizes=((10, 2, 1500), (262144, 1024, 1200
                 cell[f"d{int(d)}"] = {"error": "skipped: section budget spent"}
                 continue
             try:
+                wait = 5000.0 if d == 0.0 else max(100.0, 2.0 * (base or 50.0))
                 r = native_job(n, chunk, rounds, th_reduce=0.75, th_complete=0.5, th_all=0.5, delay_us=d,
-                               timeout=min(60.0, max(10.0, t_end - time.monotonic())))
+                               lag_wait_us=round(wait, 1), timeout=min(60.0, max(15.0, t_end - time.monotonic())))
+                r["lag_wait_us"] = round(wait, 1)
                 f = r["workers"][0] if r.get("workers") else {}
                 r["fast_period_p50_us"] = f.get("period_p50_us")
                 r["fast_period_mean_us"] = f.get("period_mean_us")

@@ -66,6 +66,8 @@ class FrameReader {
   // spin_us after the previous frame - a protocol round's next Start / Complete arrives within
   // one round, and a blocked reader's wake-up costs several microseconds per hop
   explicit FrameReader(int fd, int spin_us = 0) : fd_(fd), buf_(64 << 10), spin_us_(spin_us) {}
+  // From now on the frames come from this ring (the socket only tells when the peer is gone).
+  void use_ring(ShmRing* r) { ring_ = r; }
   // Next frame's payload (valid until the next call); false at EOF / error / bad length.
   bool next(const uint8_t** p, uint32_t* n) {
     if (!fill(4)) return false;
@@ -88,6 +90,10 @@ class FrameReader {
         head_ = 0;
       }
       if (buf_.size() < need) buf_.resize(need);
+      if (ring_ != nullptr) {
+        if (!fill_ring()) return false;
+        continue;
+      }
       ssize_t k = -1;
       if (spin_us_ > 0) {
         const auto until = last_ + std::chrono::microseconds(spin_us_);
@@ -109,12 +115,47 @@ class FrameReader {
     }
     return true;
   }
+  // Ring mode: poll the ring for the spin budget after the last frame, then sleep on its futex
+  // in 20 ms slices, checking between them whether the peer closed the socket.
+  bool fill_ring() {
+    const auto until = last_ + std::chrono::microseconds(spin_us_);
+    for (;;) {
+      const size_t k = ring_->read(buf_.data() + tail_, buf_.size() - tail_);
+      if (k > 0) {
+        tail_ += k;
+        last_ = Clock::now();
+        return true;
+      }
+      if (Clock::now() < until) {
+        for (int i = 0; i < 16; ++i) __builtin_ia32_pause();
+        continue;
+      }
+      if (ring_->wait(20)) continue;
+      pollfd pfd{fd_, POLLIN | POLLRDHUP, 0};
+      if (::poll(&pfd, 1, 0) != 0) {  // the peer closed (nothing else travels on the socket now)
+        if (pfd.revents & (POLLHUP | POLLRDHUP | POLLERR | POLLNVAL)) return !ring_->empty() ? true : false;
+        char c;
+        if (::recv(fd_, &c, 1, MSG_DONTWAIT | MSG_PEEK) == 0) return false;
+      }
+    }
+  }
   int fd_;
   std::vector<uint8_t> buf_;
   size_t head_ = 0, tail_ = 0;
   int spin_us_ = 0;
   Clock::time_point last_ = Clock::now();
+  ShmRing* ring_ = nullptr;
 };
+
+// Same-host fast path (shm_ring.h): on unless MXAR_SHM=0; ring bytes per connection.
+bool shm_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("MXAR_SHM");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
+}
+constexpr size_t kShmRingBytes = size_t{1} << 20;
 
 int tcp_spin_us() {
   static const int v = [] {
@@ -302,6 +343,8 @@ void ClusterNode::accept_loop() {
 
 void ClusterNode::reader_loop(int fd) {
   FrameReader in(fd, tcp_spin_us());
+  std::string peer;                  // the connecting node (its Hello)
+  std::unique_ptr<ShmRing> offered;  // its ring, mapped at ShmOffer, read from ShmSwitch on
   while (!stopping_.load()) {
     const uint8_t* data = nullptr;
     uint32_t len = 0;
@@ -312,6 +355,28 @@ void ClusterNode::reader_loop(int fd) {
       stats_.bytes_in += len + 4;
     }
     try {
+      const auto kind = static_cast<FrameKind>(data[0]);
+      if (kind == FrameKind::Hello || kind == FrameKind::ShmOffer || kind == FrameKind::ShmSwitch) {
+        Reader r(data, len);
+        (void)r.u8();
+        if (kind == FrameKind::Hello) {
+          peer = r.str();
+        } else if (kind == FrameKind::ShmOffer) {
+          const std::string name = r.str();
+          offered = shm_enabled() ? ShmRing::open(name) : nullptr;
+          Writer ack;  // over OUR connection to the offerer: it switches only on a good ack
+          ack.u8(static_cast<uint8_t>(FrameKind::ShmAck));
+          ack.str(address_);
+          ack.str(name);
+          ack.u8(offered ? 1 : 0);
+          if (peer.empty() || !send_frame(peer, ack.bytes())) offered.reset();
+        } else if (offered) {  // ShmSwitch: every later frame of this peer is in the ring
+          in.use_ring(offered.get());
+          std::lock_guard<std::mutex> g(stats_mu_);
+          ++stats_.shm_links_in;
+        }
+        continue;
+      }
       handle_frame(data, len);
     } catch (const std::exception& e) {
       std::lock_guard<std::mutex> g(stats_mu_);
@@ -357,10 +422,36 @@ bool ClusterNode::send_frame(const std::string& address, const std::vector<uint8
         c->fd = -1;
         continue;
       }
-      std::lock_guard<std::mutex> gs(stats_mu_);
-      ++stats_.connects;
+      {
+        std::lock_guard<std::mutex> gs(stats_mu_);
+        ++stats_.connects;
+      }
+      c->ring.reset();
+      c->ring_live = false;
+      c->ring_tried = false;
+    }
+    if (!c->ring_tried && shm_enabled() && same_host(address)) {
+      // offer a ring; frames keep going over TCP until the peer's ShmAck (on_shm_ack)
+      c->ring_tried = true;
+      c->ring = ShmRing::create(kShmRingBytes);
+      if (c->ring) {
+        Writer offer;
+        offer.u8(static_cast<uint8_t>(FrameKind::ShmOffer));
+        offer.str(c->ring->name());
+        if (!write_frame(c->fd, offer.bytes().data(), static_cast<uint32_t>(offer.bytes().size()))) c->ring.reset();
+      }
     }
     const uint32_t len = static_cast<uint32_t>(payload.size());
+    if (c->ring_live) {
+      const uint32_t l = len;
+      if (c->ring->write(&l, 4, &stopping_) && c->ring->write(payload.data(), len, &stopping_)) {
+        std::lock_guard<std::mutex> gs(stats_mu_);
+        ++stats_.frames_out;
+        stats_.bytes_out += len + 4;
+        return true;
+      }
+      return false;
+    }
     if (write_frame(c->fd, payload.data(), len)) {
       std::lock_guard<std::mutex> gs(stats_mu_);
       ++stats_.frames_out;
@@ -387,6 +478,42 @@ void ClusterNode::close_connection(const std::string& address) {
   std::lock_guard<std::mutex> g(c->mu);
   if (c->fd >= 0) ::close(c->fd);
   c->fd = -1;
+  c->ring.reset();
+  c->ring_live = false;
+}
+
+bool ClusterNode::same_host(const std::string& address) const {
+  try {
+    const std::string h = parse_address(address).first;
+    return h == "127.0.0.1" || h == "localhost" || h == cfg_.host;
+  } catch (const std::exception&) {
+    return false;
+  }
+}
+
+void ClusterNode::on_shm_ack(const std::string& from, const std::string& name, bool ok) {
+  std::shared_ptr<OutConn> c;
+  {
+    std::lock_guard<std::mutex> g(conn_mu_);
+    auto it = conns_.find(from);
+    if (it == conns_.end()) return;
+    c = it->second;
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->ring || c->ring->name() != name || c->ring_live || c->fd < 0) return;
+  if (!ok) {  // the peer could not map it: stay on TCP
+    c->ring.reset();
+    return;
+  }
+  Writer sw;  // the last frame on the socket: the peer's reader switches to the ring behind it
+  sw.u8(static_cast<uint8_t>(FrameKind::ShmSwitch));
+  if (!write_frame(c->fd, sw.bytes().data(), static_cast<uint32_t>(sw.bytes().size()))) {
+    c->ring.reset();
+    return;
+  }
+  c->ring_live = true;
+  std::lock_guard<std::mutex> gs(stats_mu_);
+  ++stats_.shm_links_out;
 }
 
 void ClusterNode::broadcast(const std::vector<uint8_t>& payload, const std::string& except) {
@@ -584,6 +711,12 @@ void ClusterNode::handle_frame(const uint8_t* p, size_t n) {
     case FrameKind::Hello:
       (void)r.str();
       break;
+    case FrameKind::ShmAck: {
+      const std::string from = r.str();
+      const std::string name = r.str();
+      on_shm_ack(from, name, r.u8() != 0);
+      break;
+    }
     case FrameKind::Envelope: {
       const std::string sender = r.str();
       const std::string path = r.str();

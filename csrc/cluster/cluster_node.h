@@ -34,6 +34,7 @@
 
 #include "../runtime/actor_system.h"
 #include "codec.h"
+#include "shm_ring.h"
 
 namespace mxar {
 
@@ -56,6 +57,7 @@ struct ClusterStats {
   uint64_t frames_out = 0, frames_in = 0, bytes_out = 0, bytes_in = 0;
   uint64_t connects = 0, connect_failures = 0, send_failures = 0, undeliverable = 0, decode_errors = 0;
   uint64_t members_up = 0, members_removed = 0, heartbeats_in = 0;
+  uint64_t shm_links_out = 0, shm_links_in = 0;  // same-host connections on the shared-memory ring
 };
 
 class ClusterNode;
@@ -125,7 +127,14 @@ class ClusterNode : public std::enable_shared_from_this<ClusterNode>, public Ref
   struct OutConn {
     int fd = -1;
     std::mutex mu;
+    // same-host fast path: the ring offered on this connection (ShmOffer), live once the peer
+    // acked it and ShmSwitch went out - every later frame goes through the ring
+    std::unique_ptr<ShmRing> ring;
+    bool ring_live = false;
+    bool ring_tried = false;
   };
+  bool same_host(const std::string& address) const;
+  void on_shm_ack(const std::string& from, const std::string& name, bool ok);
 
   std::weak_ptr<ActorSystem> sys_;
   ClusterConfig cfg_;

@@ -26,6 +26,11 @@ enum class FrameKind : uint8_t {
   MemberEvent = 5,  // {event, member}
   Heartbeat = 6,    // {from address, seq}
   Leave = 7,        // {address}
+  // same-host fast path (shm_ring.h): the connecting node offers a ring, the peer maps it and
+  // acks over its own connection, the offerer sends ShmSwitch over TCP and the ring from then on
+  ShmOffer = 8,     // {ring name}
+  ShmAck = 9,       // {acker address, ring name, ok}
+  ShmSwitch = 10,   // {}
 };
 
 enum class MemberStatus : uint8_t { Joining = 0, Up = 1, Leaving = 2, Down = 3, Removed = 4 };

@@ -673,6 +673,7 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   if (const char* g = study_env("MXAR_SLOT_GUARD")) noguard_ = std::atoi(g) == 0;
   // A/B of the threshold kernel's lag-gate shortcut
   if (const char* g = study_env("MXAR_GATE_SHORTCUT")) no_gate_shortcut_ = std::atoi(g) == 0;
+  if (const char* g = study_env("MXAR_TH_ONESHOT_MAX")) th_oneshot_max_ = std::max<int64_t>(0, std::atoll(g));
   if (const char* g = study_env("MXAR_TWOSHOT_GEOM")) {
     const std::string v = g;
     geom_ = v == "coarse" ? 0 : v == "fine" ? 1 : v == "flat" ? 2 : -1;
@@ -1367,6 +1368,16 @@ bool XgmiComm::threshold_args(const std::vector<XgmiComm*>& group, const std::ve
   // complete round counts as clean (full thresholds)
   a.gate_shortcut = (c0.rows_ - 1 >= 2 && (a.full || n > static_cast<int64_t>(W - 1) * a.block) &&
                      !c0.no_gate_shortcut_) ? 1 : 0;
+  // the one-shot body (xgmi_threshold.hip): full thresholds, unsplit, a small round whose chunk
+  // boundaries fall on 4-B words (a low-latency word is 4 payload bytes) and whose
+  // LL-encoded input (two bytes of slot per byte) fits one S slot
+  {
+    const int64_t nbytes = n * es;
+    a.oneshot = (a.full && a.sub <= 1 && W <= kMaxRanks && nbytes <= c0.th_oneshot_max_ && nbytes % 4 == 0 &&
+                 (a.block * es) % 4 == 0 && (a.chunk * es) % 4 == 0 && 2 * round_up(nbytes, 8) <= c0.slot_bytes_)
+                    ? 1
+                    : 0;
+  }
   a.counts = counts;
   if (spec != nullptr) {
     a.epoch_set = spec->epoch;

@@ -101,6 +101,9 @@ struct CommArgs {
   // round of ours takes (xgmi_threshold.hip, lag gate). 0 = wait (the bounded-buffer gate).
   int lag_skip;
   uint64_t lag_wait;
+  // threshold kernel, full thresholds: the one-shot body (xgmi_threshold.hip) - every rank
+  // pushes its whole input as low-latency units and reduces every chunk itself (small rounds)
+  int oneshot;
   uint64_t* split_dec;
   uint32_t* split_ctr;
   uint32_t* split_early;

@@ -64,6 +64,11 @@ __device__ __forceinline__ uint32_t* f2c(const CommArgs& a, int k, int rs, int c
 __device__ __forceinline__ uint32_t* forcew(const CommArgs& a, int k, int s) {
   return reinterpret_cast<uint32_t*>(a.base[k]) + static_cast<int64_t>(3 * a.rows * a.P) * a.maxch + 2 * a.P + s;
 }
+// FORCE requests only ever move forward (a later, lower request must not un-force a round):
+// an atomic max on the peer's word, over xGMI on fine-grained memory.
+__device__ __forceinline__ void force_max(uint32_t* w, uint32_t v) {
+  __hip_atomic_fetch_max(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // The engine's pinned host words, [0] force and [1] abort: ONE PCIe read when they are
 // adjacent (the plane's layout). Returns "forced" (an abandoned round is forced too) and
@@ -428,6 +433,23 @@ __device__ __forceinline__ void put_count(int32_t* p, int32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// One-shot body (CommArgs::oneshot): the low-latency unit of xgmi_ll.hip - a 16-B store of two
+// {4 payload bytes, tag} words, each delivered whole - tagged per round epoch. The tag mixes the
+// epoch so that stale data in a slot (an older round's units, or plain two-shot data of a
+// round of another size) matches it with probability 2^-64 per unit; never 0 (a fresh slab).
+__device__ __forceinline__ uint32_t ll_tag(uint32_t epoch) {
+  const uint32_t t = (epoch * 0x9E3779B1u) ^ 0x7F4A7C15u;
+  return t ? t : 1u;
+}
+typedef unsigned int U32x2 __attribute__((ext_vector_type(2)));
+constexpr int kAuxSysLd = 17;  // sc0 | sc1: loads that see the peers' xGMI stores in HBM
+// 8 bytes of a byte range at unit i (zero past its end; the range is a whole number of 4-B words)
+__device__ __forceinline__ uint2 load_unit8(const char* p, int64_t i, int64_t nbytes) {
+  const int64_t off = i * 8;
+  if (off + 8 <= nbytes) return *reinterpret_cast<const uint2*>(p + off);
+  return make_uint2(off + 4 <= nbytes ? *reinterpret_cast<const uint32_t*>(p + off) : 0u, 0u);
+}
+
 // The per-round operands of threshold_round: a launch's own (CommArgs, threshold_kernel) or
 // the ones a resident kernel read from the host's door (threshold_resident_kernel).
 // The rank's own words come with them too (its control words, pinned host words and split
@@ -479,7 +501,8 @@ __device__ __forceinline__ RoundVars launch_vars(const CommArgs& a, int y, const
 // Snapshot, tickets and split-chunk agreement fold away: less than half
 // the code of the general kernel, whose instruction fetch a small round otherwise pays from
 // L2 on every cold CU (51 KB of code vs 21 KB for the 8-rank two-shot).
-template <class E, bool FULL>
+// ONESHOT: the one-shot body of a small full-threshold round (CommArgs::oneshot, below).
+template <class E, bool FULL, bool ONESHOT = false>
 __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVars& rv) {
   constexpr int es = 16 / E::ELEMS;
   __shared__ uint32_t sh_mask;
@@ -672,13 +695,18 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     const uint32_t* f = (k < P && k != r) ? prog(a, r, k) : nullptr;
     bool ok = f == nullptr || reached(ld_flag(f), target);
     bool asked = false, aborted = false;
-    const uint64_t skip_at = a.lag_skip ? t_start + a.lag_wait : ~0ull;
-    while (!__all(ok)) {
+    // lag skip: a peer this rank skipped last round (ctl[15], sticky while it lags) is skipped
+    // at once; any other after lag_wait - a peer momentarily late is waited for
+    const uint64_t skip_at =
+        !a.lag_skip ? ~0ull : t_start + (((ld_ctl(&ctl[15]) >> (k & 31)) & 1u) ? 0ull : a.lag_wait);
+    bool give = false;
+    while (!__all(ok || give)) {
       if (!ok && !asked && blockIdx.x == 0) {
-        st_flag(forcew(a, k, r), target);
+        force_max(forcew(a, k, r), target);
         asked = true;
       }
-      if (wall_ticks() >= skip_at) break;  // scalar clock: the whole wave leaves together
+      give = !ok && wall_ticks() >= skip_at;
+      if (__all(ok || give)) break;
       __builtin_amdgcn_s_sleep(2);
       if (!ok) ok = reached(ld_flag(f), target);
       if (rv.habort != nullptr && hp.due()) {
@@ -694,10 +722,19 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         break;
       }
     }
-    const uint32_t lag = static_cast<uint32_t>(__ballot(!ok));
+    const uint32_t lag = a.lag_skip ? static_cast<uint32_t>(__ballot(!ok)) : 0u;
+    // a skipped peer gets nothing of this round, so its round `epoch` can only end forced:
+    // force it now (up to this round), not only up to epoch - trows - it then completes its
+    // stale rounds at once with what it has and is back at the gate in time, instead of
+    // waiting trows rounds for the force and staying skipped (a one-off late peer would
+    // otherwise turn into a permanent laggard). The sticky hint skips it at once next round.
+    if (a.lag_skip && blockIdx.x == 0) {
+      if ((lag >> k) & 1u) force_max(forcew(a, k, r), epoch);
+      if (k == 0) __hip_atomic_store(&ctl[15], lag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (k == 0) {
       sh_flag = aborted ? 1 : 0;
-      sh_skip = a.lag_skip ? lag : 0u;
+      sh_skip = lag;
     }
     // No acquire here: the gate orders this round's STORES into the peers' rows after the
     // peers' reads of those rows (write-after-read - the progress word was published after
@@ -713,6 +750,148 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   const uint32_t skip = sh_skip;  // peers this workgroup writes nothing to (lag skip)
   ps.mark(1);
 
+  if constexpr (ONESHOT) {
+    // One-shot body (a.oneshot: full thresholds, unsplit, at most a few KiB per rank, chunk
+    // boundaries on 4-B words, the LL-encoded input fits a slot): every rank pushes its WHOLE
+    // input into its S slot of this row in every peer's slab as low-latency units (the tag is
+    // the flag: no release, no flag store), then reduces EVERY chunk itself once each source's
+    // words carry this round's tag. One xGMI hop and no fenced hand-off, where the two-shot
+    // body below takes five on the round's critical path (scatter -> flag -> reduce ->
+    // broadcast -> flag -> gather); same sums (fixed order s = 0..P-1 in fp32, one rounding)
+    // and counts (P per chunk). The lag gate above guards the row exactly as for the two-shot:
+    // a peer still reading its slot of this row (epoch - trows) is never overwritten. A chunk
+    // that is forced, cold or timed out sums exactly the sources whose every word of the chunk
+    // arrived, and reports that count - the two-shot's "reduce what has arrived".
+    const uint32_t tag = ll_tag(epoch);
+    const int64_t nbytes = a.n * es;
+    const int64_t units = (nbytes + 7) / 8;
+    const int64_t gstride = static_cast<int64_t>(G) * kCommThreads;
+    if (!cold && !void_round) {
+      for (int64_t i = static_cast<int64_t>(blockIdx.x) * kCommThreads + threadIdx.x; i < units; i += gstride) {
+        const uint2 d = load_unit8(in, i, nbytes);
+        Pack16 v;
+        v[0] = d.x;
+        v[1] = tag;
+        v[2] = d.y;
+        v[3] = tag;
+        for (int k = 0; k < P; ++k)
+          if (k != r) st16_wt(slab_rsrc(a.base[k] + rowS + static_cast<int64_t>(r) * slot), static_cast<uint32_t>(i * 16), v);
+      }
+    }
+    ps.mark(6);
+    const char* const mine_s = a.base[r] + rowS;  // source s's units at mine_s + s * slot
+    const __amdgpu_buffer_rsrc_t ro = slab_rsrc(out);
+    __shared__ uint32_t sh_miss;
+    const int nq = P * a.nch;
+    for (int q = blockIdx.x; q < nq; q += G) {
+      const int j = q / a.nch;
+      const int c = q - j * a.nch;
+      const int64_t blen = clamp_len(a.n - static_cast<int64_t>(j) * a.block, a.block);
+      const int64_t clen = clamp_len(blen - static_cast<int64_t>(c) * a.chunk, a.chunk);
+      if (clen <= 0) {  // past the end of a short last block: not a chunk of the round
+        if (threadIdx.x == 0 && counts) cput(static_cast<int64_t>(q), 0);
+        continue;
+      }
+      const int64_t b0 = (static_cast<int64_t>(j) * a.block + static_cast<int64_t>(c) * a.chunk) * es;
+      const int64_t b1 = b0 + clen * es;
+      const int64_t u0 = b0 / 8, u1 = (b1 + 7) / 8;
+      if (threadIdx.x == 0) sh_miss = 0u;
+      __syncthreads();
+      // a forced / timed-out wave stops waiting; a cold round waits for nothing
+      bool stop = cold || void_round;
+      uint32_t miss = 0;
+      for (int64_t ub = u0; ub < u1; ub += kCommThreads) {
+        const int64_t u = ub + threadIdx.x;
+        const bool act = u < u1;
+        const bool h0 = act && u * 8 >= b0 && u * 8 < b1;          // low word in this chunk
+        const bool h1 = act && u * 8 + 4 >= b0 && u * 8 + 4 < b1;  // high word in this chunk
+        Pack16 v[kMaxRanks];
+        uint32_t want = 0;  // sources whose words of this unit are not in yet
+#pragma unroll
+        for (int s = 0; s < kMaxRanks; ++s) {
+          if (s < P && s != r && act) {
+            v[s] = __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc(mine_s + static_cast<int64_t>(s) * slot),
+                                                          static_cast<int>(u * 16), 0, kAuxSysLd);
+            want |= 1u << s;
+          }
+        }
+        auto in_now = [&](const Pack16& w) { return (!h0 || w[1] == tag) && (!h1 || w[3] == tag); };
+#pragma unroll
+        for (int s = 0; s < kMaxRanks; ++s)
+          if (((want >> s) & 1u) && in_now(v[s])) want &= ~(1u << s);
+        const uint64_t tw = ps.now();
+        while (__any(want != 0) && !stop) {
+          __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+          for (int s = 0; s < kMaxRanks; ++s) {
+            if ((want >> s) & 1u) {
+              v[s] = __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc(mine_s + static_cast<int64_t>(s) * slot),
+                                                            static_cast<int>(u * 16), 0, kAuxSysLd);
+              if (in_now(v[s])) want &= ~(1u << s);
+            }
+          }
+          const uint64_t now = wall_ticks();
+          const bool host = hp.due(now);
+          if ((host || sp.due(now)) && wave_forced(a, rv.hforce, rv.habort, r, epoch, host)) stop = true;
+          if (now > deadline) {
+            if ((threadIdx.x & 63) == 0)
+              __hip_atomic_fetch_or(err, ERR_TIMEOUT_SCATTER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            stop = true;
+          }
+        }
+        ps.add(2, tw);
+        miss |= want;
+        if (act && want == 0u && !cold) {  // every source in: the sum, in rank order
+          Acc8<E> acc;
+#pragma unroll
+          for (int s = 0; s < kMaxRanks; ++s) {
+            if (s >= P) continue;
+            acc.add(s == r ? load_unit8(in, u, nbytes) : make_uint2(v[s][0], v[s][2]));
+          }
+          const uint2 o = acc.pack(a.scale);
+          if (h0 && h1)
+            __builtin_amdgcn_raw_buffer_store_b64(U32x2{o.x, o.y}, ro, static_cast<int>(u * 8), 0, kAuxWt);
+          else if (h0)
+            __builtin_amdgcn_raw_buffer_store_b32(o.x, ro, static_cast<int>(u * 8), 0, kAuxWt);
+          else if (h1)
+            __builtin_amdgcn_raw_buffer_store_b32(o.y, ro, static_cast<int>(u * 8 + 4), 0, kAuxWt);
+        }
+      }
+      if (miss) atomicOr(&sh_miss, miss);
+      __syncthreads();
+      const uint32_t missing = sh_miss;
+      const bool partial = missing != 0u || cold || void_round;
+      uint32_t mask = (P >= 32 ? 0xffffffffu : ((1u << P) - 1u)) & ~missing;
+      if (cold) mask &= ~(1u << r);
+      if (void_round) mask = 0u;  // abandoned before the exchange: zeros, count 0 (as the two-shot)
+      if (partial) {
+        // forced / cold / timed out: the sources whose every word of the chunk arrived (arrival
+        // within a round is final), the same mask for every word of the chunk
+        clean = false;
+        for (int64_t u = u0 + threadIdx.x; u < u1; u += kCommThreads) {
+          const bool h0 = u * 8 >= b0 && u * 8 < b1;
+          const bool h1 = u * 8 + 4 >= b0 && u * 8 + 4 < b1;
+          Acc8<E> acc;
+          for (int s = 0; s < P; ++s) {
+            if (!((mask >> s) & 1u)) continue;
+            if (s == r) {
+              acc.add(load_unit8(in, u, nbytes));
+            } else {
+              const Pack16 w = __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc(mine_s + static_cast<int64_t>(s) * slot),
+                                                                     static_cast<int>(u * 16), 0, kAuxSysLd);
+              acc.add(make_uint2(w[0], w[2]));
+            }
+          }
+          const uint2 o = acc.pack(a.scale);
+          if (h0) __builtin_amdgcn_raw_buffer_store_b32(o.x, ro, static_cast<int>(u * 8), 0, kAuxWt);
+          if (h1) __builtin_amdgcn_raw_buffer_store_b32(o.y, ro, static_cast<int>(u * 8 + 4), 0, kAuxWt);
+        }
+      }
+      if (threadIdx.x == 0 && counts) cput(static_cast<int64_t>(j) * a.nch + c, __popc(mask));
+      __syncthreads();  // sh_miss is reused by the next chunk
+    }
+    ps.mark(3);
+  } else {
   // Phase 1 - ScatterBlock into the owners' row slots (a cold or void round sends nothing).
   // Unsplit chunks travel in groups of `sgroup` consecutive chunks of one destination block:
   // one contiguous copy and ONE release for the group, then one flag per chunk (each chunk
@@ -1054,6 +1233,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     }
   }
 
+  }  // two-shot body
   ps.mark(5);
   ps.flush();
 
@@ -1145,12 +1325,12 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   return clean;
 }
 
-template <class E, bool FULL>
+template <class E, bool FULL, bool ONESHOT>
 __global__ __launch_bounds__(kCommThreads) void threshold_kernel(CommArgs a) {
   const int y = blockIdx.y;
   const RoundVars rv =
       launch_vars(a, y, a.in[y], a.out[y], a.counts, a.counts_host, a.err_out, a.done_out, a.epoch_set, a.cold, 0, 0);
-  (void)threshold_round<E, FULL>(a, rv);
+  (void)threshold_round<E, FULL, ONESHOT>(a, rv);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1244,7 +1424,7 @@ __device__ uint64_t resident_door(const ResidentDoor* door, uint32_t* hstate, ui
   return w;
 }
 
-template <class E, bool FULL>
+template <class E, bool FULL, bool ONESHOT>
 __global__ __launch_bounds__(kCommThreads) void threshold_resident_kernel(CommArgs a, const ResidentDoor* door,
                                                                          uint32_t* hstate, uint64_t* dm,
                                                                          uint32_t seq, uint32_t gen, uint64_t idle) {
@@ -1300,7 +1480,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_resident_kernel(CommAr
         (prev_clean && gridDim.x == 1 && a.trows >= 2 && static_cast<uint32_t>(sh_ent[6]) == prev_epoch + 1u) ? 1 : 0,
         1);
     __syncthreads();
-    const bool clean = threshold_round<E, FULL>(a, rv);
+    const bool clean = threshold_round<E, FULL, ONESHOT>(a, rv);
     if (threadIdx.x == 0) sh_clean = clean ? 1 : 0;
     // the entry is consumed: the host may reuse its door slot (a PCIe write, kept off the
     // round's critical path - every release waits for the writes before it)
@@ -1483,7 +1663,7 @@ __device__ __forceinline__ void group_dispatch(const CommArgs& a, const GroupRes
   }
 }
 
-template <class E, bool FULL>
+template <class E, bool FULL, bool ONESHOT>
 __global__ __launch_bounds__(kCommThreads) void threshold_group_resident_kernel(CommArgs a, GroupResArgs g) {
   if (blockIdx.y == 0) {  // the dispatcher row: one wave works, the rest leave at once
     if (blockIdx.x == 0 && threadIdx.x < 64) group_dispatch(a, g);
@@ -1572,7 +1752,7 @@ __global__ __launch_bounds__(kCommThreads) void threshold_group_resident_kernel(
                        m.split_early,
                        m.stamps == nullptr ? nullptr : m.stamps + static_cast<int64_t>(blockIdx.x) * kPhaseSlots};
     __syncthreads();
-    const bool clean = threshold_round<E, FULL>(a, rv);
+    const bool clean = threshold_round<E, FULL, ONESHOT>(a, rv);
     if (threadIdx.x == 0) sh_clean = clean ? 1 : 0;
     __syncthreads();
     prev_clean = sh_clean != 0;
@@ -1596,8 +1776,9 @@ __global__ __launch_bounds__(64) void publish_progress_kernel(CommArgs a, uint32
   }
 }
 
-// the compile-time full-threshold kernel applies (threshold_round FULL)
+// the compile-time full-threshold kernel applies (threshold_round FULL), with its one-shot body
 static bool full_fast(const CommArgs& a) { return a.full != 0 && a.sub <= 1; }
+static bool full_oneshot(const CommArgs& a) { return full_fast(a) && a.oneshot != 0; }
 
 void launch_publish_progress(const CommArgs& a, uint32_t value, hipStream_t s) {
   hipLaunchKernelGGL(publish_progress_kernel, dim3(1), dim3(64), 0, s, a, value);
@@ -1607,22 +1788,27 @@ void launch_threshold_resident(const CommArgs& a, int grid, hipStream_t s, DType
                                uint32_t* hstate, uint32_t* dm, uint32_t seq, uint32_t gen, uint64_t idle_ticks) {
   dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
     using E = decltype(tag);
-    if (full_fast(a))
-      hipLaunchKernelGGL((threshold_resident_kernel<E, true>), dim3(grid), dim3(kCommThreads), 0, s, a, door, hstate,
-                         reinterpret_cast<uint64_t*>(dm), seq, gen, idle_ticks);
+    if (full_oneshot(a))
+      hipLaunchKernelGGL((threshold_resident_kernel<E, true, true>), dim3(grid), dim3(kCommThreads), 0, s, a, door,
+                         hstate, reinterpret_cast<uint64_t*>(dm), seq, gen, idle_ticks);
+    else if (full_fast(a))
+      hipLaunchKernelGGL((threshold_resident_kernel<E, true, false>), dim3(grid), dim3(kCommThreads), 0, s, a, door,
+                         hstate, reinterpret_cast<uint64_t*>(dm), seq, gen, idle_ticks);
     else
-      hipLaunchKernelGGL((threshold_resident_kernel<E, false>), dim3(grid), dim3(kCommThreads), 0, s, a, door, hstate,
-                         reinterpret_cast<uint64_t*>(dm), seq, gen, idle_ticks);
+      hipLaunchKernelGGL((threshold_resident_kernel<E, false, false>), dim3(grid), dim3(kCommThreads), 0, s, a, door,
+                         hstate, reinterpret_cast<uint64_t*>(dm), seq, gen, idle_ticks);
   });
 }
 
 void launch_threshold(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {
   dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
     using E = decltype(tag);
-    if (full_fast(a))
-      hipLaunchKernelGGL((threshold_kernel<E, true>), grid, dim3(kCommThreads), 0, s, a);
+    if (full_oneshot(a))
+      hipLaunchKernelGGL((threshold_kernel<E, true, true>), grid, dim3(kCommThreads), 0, s, a);
+    else if (full_fast(a))
+      hipLaunchKernelGGL((threshold_kernel<E, true, false>), grid, dim3(kCommThreads), 0, s, a);
     else
-      hipLaunchKernelGGL((threshold_kernel<E, false>), grid, dim3(kCommThreads), 0, s, a);
+      hipLaunchKernelGGL((threshold_kernel<E, false, false>), grid, dim3(kCommThreads), 0, s, a);
   });
 }
 
@@ -1630,10 +1816,12 @@ void launch_threshold_group_resident(const CommArgs& a, const GroupResArgs& g, i
   const dim3 gd(static_cast<unsigned>(grid), static_cast<unsigned>(g.Y + 1));
   dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
     using E = decltype(tag);
-    if (full_fast(a))
-      hipLaunchKernelGGL((threshold_group_resident_kernel<E, true>), gd, dim3(kCommThreads), 0, s, a, g);
+    if (full_oneshot(a))
+      hipLaunchKernelGGL((threshold_group_resident_kernel<E, true, true>), gd, dim3(kCommThreads), 0, s, a, g);
+    else if (full_fast(a))
+      hipLaunchKernelGGL((threshold_group_resident_kernel<E, true, false>), gd, dim3(kCommThreads), 0, s, a, g);
     else
-      hipLaunchKernelGGL((threshold_group_resident_kernel<E, false>), gd, dim3(kCommThreads), 0, s, a, g);
+      hipLaunchKernelGGL((threshold_group_resident_kernel<E, false, false>), gd, dim3(kCommThreads), 0, s, a, g);
   });
 }
 

@@ -24,7 +24,7 @@ def test_every_round_consistent_with_a_2ms_straggler():
     srcs = [C.hip.tensor_source(b, delay_us=2000.0 if k == slow else 0.0) for k, b in enumerate(bufs)]
     torch.cuda.synchronize()
     job = PlaneJob(P, n, max_chunk_size=chunk, th_allreduce=0.75, th_reduce=0.75, th_complete=0.75, max_lag=1,
-                   max_round=rounds - 1, sources=srcs, timeout_s=20.0, lag_wait_us=0.0)
+                   max_round=rounds - 1, sources=srcs, timeout_s=20.0, lag_wait_us=100.0)
     try:
         job.start()
         assert job.finished.wait(60), job.state()
@@ -49,8 +49,47 @@ def test_fast_workers_keep_their_rate():
     """40 B rounds (the reference's 2-float chunks): the fast workers' mean round period with a
     2 ms straggler stays within 1.5x of the no-straggler period (the bench's target is 1.25x;
     the test leaves room for a loaded box)."""
-    base = inproc_case(DEV, 4, 40, torch.float32, 2, 1, 0.0, 800)
-    slow = inproc_case(DEV, 4, 40, torch.float32, 2, 1, 2000.0, 800)
+    base = inproc_case(DEV, 4, 40, torch.float32, 2, 1, 0.0, 800, lag_wait_us=5000.0)
+    slow = inproc_case(DEV, 4, 40, torch.float32, 2, 1, 2000.0, 800, lag_wait_us=100.0)
     assert base.get("validated") and slow.get("validated"), (base, slow)
     assert slow["fast_period_mean_us"] <= 1.5 * base["fast_period_mean_us"], (base, slow)
     assert slow["straggler_coalesced"] > 0, slow
+
+
+def test_oneshot_forced_rounds_sum_what_arrived():
+    """Full thresholds at 12 KB per worker run the threshold kernel's one-shot body (every rank
+    reduces every chunk itself). A worker stalled in round 0 is forced along by the master's
+    round deadline (AllreduceSpec.scala:535-559, T13): the fast workers' forced rounds hold
+    exactly the sources whose words arrived - count 2 in EVERY chunk, the stalled worker's
+    block included (the two-shot body would report its block as 0: its owner reduced nothing)
+    - and every output chunk equals the sum its count names."""
+    import time
+
+    P, n, chunk, rounds = 3, 3000, 500, 8
+    bufs = [torch.full((n,), float(1 << k), device=DEV) for k in range(P)]
+    srcs = [C.hip.tensor_source(b) for b in bufs]
+    base = srcs[2]
+
+    def stall(req):
+        if req.iteration == 0:
+            time.sleep(1.5)
+        return base(req)
+
+    srcs[2] = stall
+    job = PlaneJob(P, n, max_chunk_size=chunk, th_reduce=1.0, th_complete=1.0, max_lag=1, max_round=rounds - 1,
+                   sources=srcs, round_timeout_ms=250, timeout_s=30.0)
+    try:
+        job.run(timeout=120)
+        st = job.state()
+        for k, w in enumerate(st["workers"]):
+            assert w["stats"]["plane_errors"] == 0, (k, w)
+            assert w["round"] == rounds, (k, w)
+        for k in range(P):
+            for it, (data, counts) in job.outputs[k].items():
+                assert pow2_check(data, counts, P, n, chunk), (k, it, counts)
+        data, counts = job.outputs[0][0]  # forced: the two fast workers' inputs in every chunk
+        assert counts == [2] * len(counts), counts
+        data, counts = job.outputs[0][rounds - 1]  # the straggler caught up: exact again
+        assert counts == [P] * len(counts), counts
+    finally:
+        job.shutdown()
