@@ -698,7 +698,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     // lag skip: a peer this rank skipped last round (ctl[15], sticky while it lags) is skipped
     // at once; any other after lag_wait - a peer momentarily late is waited for
     const uint64_t skip_at =
-        !a.lag_skip ? ~0ull : t_start + (((ld_ctl(&ctl[15]) >> (k & 31)) & 1u) ? 0ull : a.lag_wait);
+        !a.lag_skip ? ~0ull : t_start + ((k < 32 && ((ld_ctl(&ctl[15]) >> k) & 1u)) ? 0ull : a.lag_wait);
     bool give = false;
     while (!__all(ok || give)) {
       if (!ok && !asked && blockIdx.x == 0) {
@@ -729,7 +729,9 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     // waiting trows rounds for the force and staying skipped (a one-off late peer would
     // otherwise turn into a permanent laggard). The sticky hint skips it at once next round.
     if (a.lag_skip && blockIdx.x == 0) {
-      if ((lag >> k) & 1u) force_max(forcew(a, k, r), epoch);
+      // (k < P first: a 32-bit shift by k >= 32 wraps on the hardware - lane 32 + j would
+      // alias peer j and write through base[32 + j], past the peer table)
+      if (k < P && ((lag >> k) & 1u)) force_max(forcew(a, k, r), epoch);
       if (k == 0) __hip_atomic_store(&ctl[15], lag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (k == 0) {
