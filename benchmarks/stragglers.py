@@ -35,6 +35,7 @@ import json
 import os
 import statistics
 import subprocess
+import sys
 import time
 
 import torch
@@ -147,6 +148,8 @@ def inproc_case(dev, P: int, nbytes: int, dtype, chunk: int, max_lag: int, delay
     finally:
         job.shutdown()
         del bufs, srcs
+    print(f"[stragglers] P={P} {nbytes} B lag={max_lag} delay={delay_us:g} us: "
+          f"{row.get('fast_period_mean_us')} us/round validated={row.get('validated')}", file=sys.stderr, flush=True)
     return row
 
 

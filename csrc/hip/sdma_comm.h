@@ -14,7 +14,7 @@
 //   gather                  a small-grid kernel copies the peers' RD slots into the output
 //
 // Stream ordering without the host: HIP's hipMemcpyAsync runs device-to-device copies as
-// blit KERNELS (profiles/round4/README.md, tools/sdma_probe.cc), so the copies are submitted
+// blit KERNELS (profiles/round4/README.md, tools/sdma_probe.cc in git history), so the copies are submitted
 // with hsa_amd_memory_async_copy_on_engine(force_copy_on_sdma). Each call's copies are
 // queued at call time but depend on an HSA signal that a one-lane kernel on the caller's
 // stream releases (after a system-scope release event, so the engines read what earlier

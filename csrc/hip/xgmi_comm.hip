@@ -606,7 +606,7 @@ XgmiComm::Layout XgmiComm::layout(int world, int64_t slot_bytes, int threshold_r
   L.slab_bytes = L.off_LL + 2 * world * L.ll_slot;
   // Allocation size: on this ROCm stack hipIpcOpenMemHandle of an allocation whose size has
   // bit 31 set (2-4 GiB, 6-8 GiB, ...) never returns in the importing process, while the
-  // sizes around it map and reduce correctly (measured with tools/ipc_size_probe.py: 1.97,
+  // sizes around it map and reduce correctly (measured with tools/ipc_size_probe.py, in git history: 1.97,
   // 4.05, 4.33 GiB fine; 2.03-3.9 GiB hang). Such slabs are padded up to the next multiple of
   // 4 GiB - at most 2 GiB of the 288 GB of HBM. MXAR_IPC_NO_PAD=1 disables it (probing).
   L.alloc_bytes = ipc_safe_bytes(L.slab_bytes);

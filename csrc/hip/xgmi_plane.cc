@@ -220,7 +220,7 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
     throw std::invalid_argument("xgmi plane: max_peers must be in [1, 16]");
   if (o_.max_lag < 0 || o_.max_lag > 62) throw std::invalid_argument("xgmi plane: max_lag must be in [0, 62]");
   o_.ring = std::max(4, o_.ring);
-  if (const char* e = std::getenv("MXAR_PLANE_SPLIT")) o_.split = std::atoi(e) != 0;  // A/B knob
+  if (const char* e = study_env("MXAR_PLANE_SPLIT")) o_.split = std::atoi(e) != 0;  // A/B knob
   // A/B knob: 1 = also record an event per round and confirm completion with it (round 2's
   // form; ~2-3 us of hipEventRecord on every launch, profiles/round3/api_cost.json)
   if (const char* e = study_env("MXAR_PLANE_EVENTS")) event_confirm_ = std::atoi(e) != 0;

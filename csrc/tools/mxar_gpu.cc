@@ -72,7 +72,7 @@ GpuWorkerParts make_gpu_worker(const GpuWorkerOptions& g) {
   if (const char* path = study_env("MXAR_PLANE_STAMPS")) {
     // study knob: phase stamps of this worker's round kernels (kPhaseSlots u64 per workgroup,
     // s_memrealtime - one clock for every process on the GPU), the last round's written as one
-    // JSON line to `path` when the job ends (tools/native_stamps.py)
+    // JSON line to `path` when the job ends (tools/phase_profile.py reads the same layout)
     constexpr int64_t kSlots = 2048;
     uint64_t* buf = nullptr;
     if (hipMalloc(reinterpret_cast<void**>(&buf), kSlots * 8 * sizeof(uint64_t)) != hipSuccess ||

@@ -252,3 +252,26 @@ def test_comm_stream_has_priority_over_compute():
 
     s = comm_stream(torch.device("cuda", 0))
     assert s.priority < torch.cuda.current_stream(0).priority
+
+
+def test_process_with_cu_masked_streams_exits_cleanly():
+    """A process that made CU-masked streams (compute_stream_excluding, the "cuN:" schedules)
+    and ran work on them exits with status 0: the streams still alive at interpreter exit are
+    destroyed by an atexit hook while the HIP runtime is whole (ddp.py _destroy_live_masked; a
+    masked stream left to the runtime's own teardown once ended the process with SIGSEGV)."""
+    import subprocess
+    import sys
+
+    code = (
+        "import torch\n"
+        "from akka_allreduce_1_amd.parallel.ddp import compute_stream_excluding\n"
+        "s = compute_stream_excluding('cuda:0', 32)\n"
+        "with torch.cuda.stream(s):\n"
+        "    a = torch.randn(1024, 1024, device='cuda:0'); b = (a @ a).sum()\n"
+        "torch.cuda.synchronize(); print('ok', float(b) == float(b))\n"
+    )
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=root,
+                       env=dict(os.environ, PYTHONPATH=root))
+    assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
+    assert "ok True" in r.stdout

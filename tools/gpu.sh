@@ -60,7 +60,7 @@ case $task in
     # the raw kernel trace runs to hundreds of MiB (gpurun copies back <= 64 MiB): keep the stats
     find $O/prof -name '*kernel_trace.csv' -delete
     [ -n "$f" ] || { echo "profiled bench failed (rc=$rc, no stats)"; tail -20 $O/prof_bench.err; exit 1; }
-    python3 tools/prof_summary.py "${f%_kernel_stats.csv}" "bench.py $*" > $O/prof_summary.md
+    python3 tools/prof.py csv "${f%_kernel_stats.csv}" "bench.py $*" > $O/prof_summary.md
     # a non-zero status after the profiler wrote its stats (e.g. a crash in process teardown
     # under the profiler's library) is reported, the stats are kept
     echo "prof ok (bench rc=$rc)"
