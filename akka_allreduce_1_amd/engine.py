@@ -41,9 +41,15 @@ def default_plane_grid(device: int, share: int) -> int:
     the CUs: together they run about one workgroup per CU, so every worker's kernel stays
     resident beside the others. Their planes also coarsen full-threshold rounds to one chunk
     per workgroup. 2 workers x 128 workgroups beat 2 x 256 by 8-30 % per round at
-    16-256 MiB (profiles/round5/protocol_grid_chunk.jsonl)."""
+    16-256 MiB (profiles/round5/protocol_grid_chunk.jsonl). Co-located workers also fit what
+    the device's residency budget has left (csrc/hip/residency.h: every spinning kernel of
+    the process reserves its workgroups; a second job shares the device with the first)."""
     cus = torch.cuda.get_device_properties(device).multi_processor_count if torch.cuda.is_available() else 256
-    return 2 * cus if share <= 1 else max(8, cus // share)
+    if share <= 1:
+        return 2 * cus
+    st = C.hip.residency_state(device)
+    free = st["capacity"] - st["used"]
+    return max(0, min(max(8, cus // share), (free - 1) // share))
 
 
 def iota_source(n: int, device: torch.device, dtype: torch.dtype, offset: float = 0.0) -> Callable:
@@ -124,10 +130,23 @@ class PlaneJob:
             self.devices = list(devices) if devices is not None else [torch.cuda.current_device()] * P
         if len(self.devices) != P:
             raise ValueError("one device per worker")
+        self._residency = []
         if plane == "xgmi":
             share = max(self.devices.count(d) for d in set(self.devices))
             if grid <= 0:
-                grid = default_plane_grid(self.devices[0], share)
+                grid = min(default_plane_grid(d, self.devices.count(d)) for d in set(self.devices))
+            # co-located workers' group kernels spin: reserve their workgroups (+ the
+            # dispatcher wave) in the device budget now, so a job that cannot fit beside what
+            # already runs fails HERE, loudly, not as round timeouts (csrc/hip/residency.h)
+            for d in sorted(set(self.devices)):
+                k = self.devices.count(d)
+                if k > 1:
+                    if grid < 8:
+                        st = C.hip.residency_state(d)
+                        raise RuntimeError(f"residency budget: {k} co-located workers on device {d} need >= 8 "
+                                           f"workgroups each; {st['capacity'] - st['used']} of {st['capacity']} "
+                                           f"free (held: {st['holders']})")
+                    self._residency.append(C.hip.residency_reserve(d, k * grid + 1, f"PlaneJob {k} workers x {grid}"))
         self.grid = grid
         self.system = C.ActorSystem("ClusterSystem", False)
         self.finished = threading.Event()
@@ -148,7 +167,8 @@ class PlaneJob:
                                             max_lag=max_lag, grid=grid, timeout_s=timeout_s, order_ref=order_ref,
                                             high_priority=high_priority, order_release=order_release,
                                             spin_us=spin_us, split=split, min_chunk=min_chunk,
-                                            lag_wait_us=-1.0 if lag_wait_us is None else float(lag_wait_us))
+                                            lag_wait_us=-1.0 if lag_wait_us is None else float(lag_wait_us),
+                                            residency_external=self.devices.count(d) > 1)
                            for d in self.devices]
             if sources is None:
                 sources = [iota_source(data_size, torch.device("cuda", d), dtype, 1000.0 * k)
@@ -249,6 +269,9 @@ class PlaneJob:
         self.planes = []
         self.workers = []
         gc.collect()
+        for t in self._residency:  # after the planes (and their group kernels) are gone
+            t.release()
+        self._residency = []
 
 
 def distributed_plane_job(n: int, source, *, max_chunk_size: int, dtype: torch.dtype, rounds: int,

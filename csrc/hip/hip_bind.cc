@@ -15,6 +15,7 @@
 #include "sdma_comm.h"
 #include "xgmi_comm.h"
 #include "xgmi_plane.h"
+#include "residency.h"
 
 namespace py = pybind11;
 
@@ -216,6 +217,25 @@ void bind_hip(py::module_& m) {
         "dataSource for a plane worker: the same GPU tensor every round, no Python (GIL) per round; "
         "delay_us: each fetch first waits this long on the worker's thread (a straggler)");
 
+  // the device budget of spinning workgroups (residency.h)
+  struct ResidencyToken {
+    std::shared_ptr<void> t;
+  };
+  py::class_<ResidencyToken>(h, "ResidencyToken").def("release", [](ResidencyToken& k) { k.t.reset(); });
+  h.def("residency_reserve",
+        [](int device, int wgs, const std::string& who) { return ResidencyToken{Residency::get().reserve(device, wgs, who)}; },
+        py::arg("device"), py::arg("wgs"), py::arg("who"),
+        "reserve spinning workgroups on a device (released with the token); raises with the budget named");
+  h.def("residency_state", [](int device) {
+    py::dict d;
+    d["capacity"] = Residency::get().capacity(device);
+    d["used"] = Residency::get().used(device);
+    py::list hs;
+    for (const ResidencyHolder& x : Residency::get().holders(device)) hs.append(py::make_tuple(x.who, x.wgs));
+    d["holders"] = hs;
+    return d;
+  }, py::arg("device"));
+
   py::class_<DevicePlane, DataPlane, std::shared_ptr<DevicePlane>>(h, "DevicePlane")
       .def_property_readonly("device", &DevicePlane::device)
       .def("synchronize", [](DevicePlane& p) {
@@ -275,7 +295,7 @@ void bind_hip(py::module_& m) {
       "xgmi_plane",
       [](int device, DType dtype, int64_t capacity, int max_peers, int max_lag, int grid, double timeout_s,
          bool order_ref, bool high_priority, bool order_release, int spin_us, bool split, int64_t min_chunk,
-         double lag_wait_us) {
+         double lag_wait_us, bool residency_external) {
         XgmiPlaneOptions o;
         o.device = device;
         o.dtype = dtype;
@@ -291,13 +311,14 @@ void bind_hip(py::module_& m) {
         o.split = split;
         o.min_chunk = min_chunk;
         o.lag_wait_us = lag_wait_us;
+        o.residency_external = residency_external;
         py::gil_scoped_release r;
         return make_xgmi_plane(o);
       },
       py::arg("device") = 0, py::arg("dtype") = DType::F32, py::arg("capacity"), py::arg("max_peers") = 8,
       py::arg("max_lag") = 4, py::arg("grid") = 0, py::arg("timeout_s") = 60.0, py::arg("order_ref") = true,
       py::arg("high_priority") = true, py::arg("order_release") = true, py::arg("spin_us") = 1000, py::arg("split") = true,
-      py::arg("min_chunk") = 0, py::arg("lag_wait_us") = -1.0,
+      py::arg("min_chunk") = 0, py::arg("lag_wait_us") = -1.0, py::arg("residency_external") = false,
       "RoundPlane of the protocol engine on MI355X: an HBM arena exported over IPC, one threshold-kernel launch "
       "per round (csrc/hip/xgmi_plane.h)");
   py::enum_<Algo>(h, "Algo").value("Auto", Algo::Auto).value("TwoShot", Algo::TwoShot).value("OneShot", Algo::OneShot).value("Ring", Algo::Ring).value("LL", Algo::LL).value("RingNative", Algo::RingNative);

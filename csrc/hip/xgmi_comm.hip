@@ -1377,6 +1377,12 @@ bool XgmiComm::threshold_args(const std::vector<XgmiComm*>& group, const std::ve
                  (a.block * es) % 4 == 0 && (a.chunk * es) % 4 == 0 && 2 * round_up(nbytes, 8) <= c0.slot_bytes_)
                     ? 1
                     : 0;
+    // one chunk per workgroup: the body reduces every chunk of the round (P x nch), and a
+    // workgroup with two of them polls and sums them one after the other
+    if (a.oneshot) {
+      const int cap = ranks_here > 1 ? std::max(1, c0.shared_launch_cap(ranks_here)) : c0.grid_;
+      gx = std::max(gx, static_cast<int>(std::min<int64_t>(cap, static_cast<int64_t>(W) * a.nch)));
+    }
   }
   a.counts = counts;
   if (spec != nullptr) {

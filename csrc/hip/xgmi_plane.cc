@@ -2,6 +2,7 @@
 #include "xgmi_plane.h"
 
 #include "../runtime/plane_geometry.h"
+#include "residency.h"
 
 #include <sys/prctl.h>
 #include <unistd.h>
@@ -107,6 +108,7 @@ struct PlaneGroup {
   // kernel may still poll their doors and words, so it is freed only once the kernel is
   // known to have exited - or never (leaked) if it did not
   std::vector<std::function<void()>> orphans;
+  std::shared_ptr<void> residency;  // the group kernel's workgroups in the device budget (residency.h)
   std::mutex mu;
 
   PlaneGroup(std::string k, int dev, int workers, bool high_priority) : key(std::move(k)), device(dev) {
@@ -605,6 +607,7 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
   park_resident();  // the stream work below must not queue behind it
   rplan_tried_ = false;
   rplan_ = XgmiComm::ResidentPlan();
+  res_token_.reset();
   hip_check(hipSetDevice(o_.device), "hipSetDevice");
   const int P = cfg.peers;
   const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
@@ -704,13 +707,13 @@ void XgmiRoundPlane::join_group(const PlaneConfig& cfg) {
   gplan_ = comm_->plan_resident(cfg.dataSize, o_.dtype, cfg.thReduce, cfg.thComplete, spec, 1 << 20, true);
   if (gplan_.grid <= 0) throw ProtocolError("xgmi plane: this membership's rounds do not fit the group kernel");
   // every slice's workgroups must be resident at once (they wait for each other's rounds):
-  // two workgroups per CU over the workers, the PlaneJob default (grid = 512 / workers)
-  int cus = 256;
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device);
-  if (static_cast<int64_t>(Y) * gplan_.grid > 2 * static_cast<int64_t>(cus))
+  // two workgroups per CU over the workers, the PlaneJob default (grid = 512 / workers) - and
+  // together with every other spinning kernel of this process on the device (residency.h)
+  const int cap = Residency::get().capacity(o_.device);
+  if (static_cast<int64_t>(Y) * gplan_.grid + 1 > cap)
     throw ProtocolError("xgmi plane: " + std::to_string(Y) + " co-located workers x " + std::to_string(gplan_.grid) +
-                        " workgroups exceed the " + std::to_string(2 * cus) +
-                        " a group kernel keeps resident: build the planes with grid <= " + std::to_string(2 * cus / Y));
+                        " workgroups exceed the " + std::to_string(cap) +
+                        " a group kernel keeps resident: build the planes with grid <= " + std::to_string((cap - 1) / Y));
   std::ostringstream key;
   key << "dev" << o_.device << " e" << cfg.epoch;
   int idx = -1;
@@ -726,7 +729,10 @@ void XgmiRoundPlane::join_group(const PlaneConfig& cfg) {
     auto& w = g_groups[key.str()];
     g = w.lock();
     if (!g) {
-      g = std::make_shared<PlaneGroup>(key.str(), o_.device, Y, o_.high_priority);
+      auto fresh = std::make_shared<PlaneGroup>(key.str(), o_.device, Y, o_.high_priority);
+      if (!o_.residency_external)  // the dispatcher wave + every slice (throws with the budget named)
+        fresh->residency = Residency::get().reserve(o_.device, Y * gplan_.grid + 1, "plane group " + key.str());
+      g = fresh;
       w = g;
     }
   }
@@ -1131,6 +1137,13 @@ bool XgmiRoundPlane::launch_resident(int round, const Payload& input, bool cold)
   if (!rplan_tried_) {
     rplan_tried_ = true;
     rplan_ = comm_->plan_resident(n, o_.dtype, cfg_.thReduce, cfg_.thComplete, spec, o_.resident_grid);
+    // an optional resident kernel: without room in the device budget the rounds are launched
+    res_token_.reset();
+    if (rplan_.grid > 0) {
+      res_token_ = Residency::get().try_reserve(o_.device, rplan_.grid,
+                                                "resident kernel of worker " + std::to_string(cfg_.id));
+      if (!res_token_) rplan_ = XgmiComm::ResidentPlan();
+    }
   }
   if (rplan_.grid <= 0) return false;
   Rec rec;

@@ -88,6 +88,10 @@ struct XgmiPlaneOptions {
   // fast worker within maxLag + 1 rounds of itself (bounded buffers). Applies only where
   // the thresholds let a round complete without one peer.
   double lag_wait_us = -1.0;
+  // The owner reserved this plane's group-kernel workgroups in the device residency budget
+  // (residency.h) already - PlaneJob does, for all its co-located planes at once, so a job that
+  // cannot fit fails at construction. false: the group reserves them itself when it forms.
+  bool residency_external = false;
   int resident_grid = 64;
   double resident_idle_us = 1000.0;
 };
@@ -261,6 +265,7 @@ class XgmiRoundPlane final : public RoundPlane {
   uint32_t* rdm_ = nullptr;            // the kernel's device words
   XgmiComm::ResidentPlan rplan_;
   bool rplan_tried_ = false;
+  std::shared_ptr<void> res_token_;    // the resident kernel's share of the residency budget
   bool res_on_ = false;                // a resident kernel was launched and may still run
   uint32_t res_seq_ = 1;               // next door entry
   // exported outputs released while a resident kernel holds the plane stream: reusable once

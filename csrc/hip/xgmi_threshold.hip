@@ -732,7 +732,13 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       // (k < P first: a 32-bit shift by k >= 32 wraps on the hardware - lane 32 + j would
       // alias peer j and write through base[32 + j], past the peer table)
       if (k < P && ((lag >> k) & 1u)) force_max(forcew(a, k, r), epoch);
-      if (k == 0) __hip_atomic_store(&ctl[15], lag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // the sticky hint keeps a skipped peer until it has caught up with the round before
+      // this one (hysteresis): a straggler hovering at the gate target would otherwise be
+      // waited for lag_wait every other round
+      const bool caught_up = f == nullptr || reached(ld_flag(f), epoch - 1u);
+      const uint32_t up = static_cast<uint32_t>(__ballot(caught_up));
+      const uint32_t hint = ld_ctl(&ctl[15]);
+      if (k == 0) __hip_atomic_store(&ctl[15], (hint & ~up) | lag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (k == 0) {
       sh_flag = aborted ? 1 : 0;
@@ -859,9 +865,14 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
             __builtin_amdgcn_raw_buffer_store_b32(o.y, ro, static_cast<int>(u * 8 + 4), 0, kAuxWt);
         }
       }
-      if (miss) atomicOr(&sh_miss, miss);
-      __syncthreads();
-      const uint32_t missing = sh_miss;
+      // the common case (every word of every source in) costs one barrier-with-reduction; only
+      // a forced / cold / timed-out chunk gathers which sources it misses
+      const bool any_miss = __syncthreads_or(miss != 0u) != 0;
+      if (any_miss) {
+        if (miss) atomicOr(&sh_miss, miss);
+        __syncthreads();
+      }
+      const uint32_t missing = any_miss ? sh_miss : 0u;
       const bool partial = missing != 0u || cold || void_round;
       uint32_t mask = (P >= 32 ? 0xffffffffu : ((1u << P) - 1u)) & ~missing;
       if (cold) mask &= ~(1u << r);

@@ -1013,3 +1013,56 @@ def test_co_located_planes_construct_beyond_the_hardware_queues():
               for _ in range(3 * queues)]
     assert len({p.descriptor for p in planes}) == 3 * queues
     planes.clear()
+
+
+def test_two_jobs_share_the_device_budget_and_a_third_fails_loudly():
+    """Two 4-worker PlaneJobs in ONE process, rounds interleaved, with a GEMM loop on a third
+    stream: each job's group kernel reserved its workgroups in the device budget
+    (csrc/hip/residency.h), the second took what the first left, every round of both is exact.
+    A third job cannot fit and fails at construction with the budget named - never as round
+    timeouts on the device."""
+    import threading
+
+    P, n, chunk, rounds = 4, 40000, 1000, 40
+    jobs = []
+    try:
+        for j in range(2):
+            srcs = [iota_source(n, DEV, torch.float32, 1000.0 * k + 10.0 * j) for k in range(P)]
+            jobs.append(PlaneJob(P, n, max_chunk_size=chunk, max_round=rounds - 1, sources=srcs, timeout_s=20.0))
+        st = C.hip.residency_state(0)
+        assert st["used"] <= st["capacity"], st
+        with pytest.raises(RuntimeError, match="residency budget"):
+            PlaneJob(P, n, max_chunk_size=chunk, max_round=1, timeout_s=5.0)
+        stop = threading.Event()
+
+        def gemms():  # a third stream keeps the CUs busy with work that does not spin
+            s = torch.cuda.Stream()
+            a = torch.randn(2048, 2048, device=DEV)
+            with torch.cuda.stream(s):
+                while not stop.is_set():
+                    a = torch.tanh(a @ a * 1e-3)
+                    s.synchronize()
+
+        th = threading.Thread(target=gemms)
+        th.start()
+        try:
+            for job in jobs:
+                job.start()
+            for job in jobs:
+                assert job.finished.wait(120), job.state()
+        finally:
+            stop.set()
+            th.join()
+        for j, job in enumerate(jobs):
+            for p in job.planes:
+                p.drain()
+            for k in range(P):
+                for it in (0, rounds // 2, rounds - 1):
+                    data, counts = job.outputs[k][it]
+                    exp = sum(np.arange(n, dtype=np.float64) + it + 1000.0 * q + 10.0 * j for q in range(P))
+                    np.testing.assert_array_equal(data.float().cpu().numpy(), exp, err_msg=f"job {j} worker {k} round {it}")
+                    assert all(c == P for c in counts)
+    finally:
+        for job in jobs:
+            job.shutdown()
+    assert C.hip.residency_state(0)["used"] == 0

@@ -56,4 +56,17 @@ def test_co_located_plane_workers_share_the_cus():
     assert default_plane_grid(0, 1) == 2 * cus
     assert default_plane_grid(0, 2) == cus // 2
     assert default_plane_grid(0, 8) == cus // 8
-    assert default_plane_grid(0, 64) == 8      # never below 8
+    assert default_plane_grid(0, 16) == 16
+    # the device residency budget (2 x CUs spinning workgroups, csrc/hip/residency.h) caps it:
+    # 64 co-located workers x 8 + the dispatcher wave would not fit
+    assert default_plane_grid(0, 64) == (2 * cus - 1) // 64
+    from akka_allreduce_1_amd._native import C
+
+    tok = C.hip.residency_reserve(0, 300, "another job")
+    try:
+        assert default_plane_grid(0, 4) == (2 * cus - 300 - 1) // 4  # what the first job left
+        with __import__("pytest").raises(RuntimeError, match="residency budget"):
+            C.hip.residency_reserve(0, 2 * cus, "too big")
+    finally:
+        tok.release()
+    assert C.hip.residency_state(0)["used"] == 0
