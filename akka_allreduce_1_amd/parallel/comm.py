@@ -590,7 +590,17 @@ class LocalCluster:
     """
 
     def __init__(self, world: int, devices: Sequence[int] | None = None, *, slot_bytes: int = 16 << 20,
-                 grid: int = 32, timeout_s: float = 10.0, max_lag: int | None = None):
+                 grid: int = 32, timeout_s: float = 10.0, max_lag: int | None = None, placement_tries: int = 1,
+                 placement_bytes: int = 0, placement_dtype: torch.dtype = torch.bfloat16,
+                 placement_min_frac: float = 0.95):
+        """placement_tries > 1 (one device only): time one two-shot of `placement_bytes` per
+        rank against the copy roofline and, while it runs below `placement_min_frac` of it,
+        build the slabs anew on other physical pages (the earlier ones are held until the
+        choice is made), up to that many times; the fastest placement is kept
+        (`placement` reports the tries and fractions). The two-shot's speed at 8 x 256 MiB
+        depends on where the driver puts the slab and buffer pages, by up to 17 %
+        (profiles/round5/README.md section 10). The timing buffers are freed into torch's
+        cache, so buffers of the same size allocated next reuse the pages that were timed."""
         if devices is None:
             devices = [torch.cuda.current_device()] * world
         if len(devices) != world:
@@ -598,16 +608,75 @@ class LocalCluster:
         self.world = world
         self.devices = [torch.device("cuda", d) for d in devices]
         rows = 0 if max_lag is None else max_lag + 1  # threshold lag ring (allreduce_threshold)
-        self.comms = [_H.XgmiComm(k, world, self.devices[k].index, slot_bytes, grid, timeout_s, rows)
-                      for k in range(world)]
-        for c in self.comms:
-            c.connect_local(self.comms)
+
+        def build():
+            comms = [_H.XgmiComm(k, world, self.devices[k].index, slot_bytes, grid, timeout_s, rows)
+                     for k in range(world)]
+            for c in comms:
+                c.connect_local(comms)
+            return comms
+
+        self.comms = build()
+        self.placement: dict = {"tries": 1}
+        if placement_tries > 1 and len(set(self.devices)) == 1 and world > 1:
+            self._place(build, placement_tries, placement_bytes or world * (slot_bytes // 2), placement_dtype,
+                        placement_min_frac)
         self.groups: list[list[int]] = []
         for k in range(world):
             if self.groups and self.devices[self.groups[-1][-1]] == self.devices[k]:
                 self.groups[-1].append(k)
             else:
                 self.groups.append([k])
+
+    def _place(self, build, tries: int, nbytes: int, dtype: torch.dtype, min_frac: float) -> None:
+        from ..ops import fill_uniform
+        from ..utils.timing import hbm_bytes
+
+        dev = self.devices[0]
+        es = torch.empty(0, dtype=dtype).element_size()
+        n = max(1, nbytes // es)
+        S = n * es
+        stream = _current_stream(dev.index)
+        # the order a caller's rank buffers are usually taken in: inputs, then outputs
+        xs = [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=900 + k) for k in range(self.world)]
+        ys = [torch.empty_like(t) for t in xs]
+        code = _dtype_code(dtype)
+
+        def timed_ms(fn, iters: int = 7, warm: int = 2, q: float = 0.5) -> float:
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+            for _ in range(warm):
+                fn()
+            for a, b in ev:
+                a.record()
+                fn()
+                b.record()
+            torch.cuda.synchronize(dev)
+            return sorted(a.elapsed_time(b) for a, b in ev)[int(q * (iters - 1))]
+
+        # the roofline: the copy kernel's best of 20 (its first calls run up to 10 % slow, which
+        # would flatter every placement)
+        copy_ms = timed_ms(lambda: C.hip.copy(xs[0].data_ptr(), ys[0].data_ptr(), S, stream), 20, 5, 0.0)
+        roof = hbm_bytes(S, self.world, "twoshot", es) / (2 * S / copy_ms)  # ms at the copy's rate
+        held, fracs = [], []
+        comms = self.comms
+        for t in range(tries):
+            if t:
+                comms = build()  # the earlier slabs are still held: these land on other pages
+            ms = timed_ms(lambda: _H.XgmiComm.allreduce_local(
+                comms, [x.data_ptr() for x in xs], [y.data_ptr() for y in ys], n, code, stream, ALGOS["twoshot"], 1.0))
+            errs = [c.error() for c in comms]
+            if any(errs):
+                raise CommError("placement probe: " + "; ".join(f"rank {k}: {_describe(e)}"
+                                                               for k, e in enumerate(errs) if e))
+            held.append(comms)
+            fracs.append(round(roof / ms, 3))
+            if fracs[-1] >= min_frac:
+                break
+        keep = max(range(len(fracs)), key=lambda i: fracs[i])
+        self.comms = held[keep]
+        del held, comms, xs, ys  # the other placements' slabs are freed here
+        self.placement = {"tries": len(fracs), "frac_copy_roofline": fracs, "kept": keep,
+                          "bytes_per_rank": S, "copy_ms": round(copy_ms, 4)}
 
     def _check(self, inputs, outputs) -> list[torch.Tensor]:
         if len(inputs) != self.world:

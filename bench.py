@@ -263,7 +263,11 @@ def local_ranks(dev, args, P: int = 8) -> dict:
         del a, b
         a = b = None
         # slots of 2 blocks: the exact-wire ring's fp32 partials of a bf16 block fit one launch
-        cl = LocalCluster(P, slot_bytes=2 * -(-S // P) + (1 << 20), grid=512, timeout_s=10.0)
+        # placement: up to 6 slab placements, timed on buffers of the rank buffers' size (torch's
+        # cache hands the same pages to the xs / ys below), the fastest kept
+        cl = LocalCluster(P, slot_bytes=2 * -(-S // P) + (1 << 20), grid=512, timeout_s=10.0, placement_tries=6,
+                          placement_bytes=S, placement_dtype=dtype)
+        row["placement"] = cl.placement
         xs = [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=500 + k) for k in range(P)]
         ys = [torch.empty_like(t) for t in xs]
         ref = torch.zeros(n, device=dev)
@@ -1115,11 +1119,12 @@ def main() -> None:
         log(rank, "dp: ResNet-50 / Llama-3-8B data-parallel steps")
         dp = {m: dp_step(comm, m, dev) for m in (("resnet50",) if args.share_device else ("resnet50", "llama3_8b"))}
         if world == 1 and not args.share_device and not args.no_sizes:
-            # the same steps with REAL comm kernels beside the GEMMs (2 logical ranks per
-            # bucket launch), swept over the reducer's workgroup budget
+            # the same steps with REAL comm kernels beside the GEMMs (one rank of an 8-GPU
+            # two-shot per bucket, run alone: a real rank's per-GPU HBM bytes), serial vs
+            # overlapped vs CU slices vs paced grids
             from benchmarks.sections import dp_overlap
 
-            log(rank, "dp.overlap_rehearsal: 2-logical-rank bucket allreduces beside backward")
+            log(rank, "dp.overlap_rehearsal: one rank of an 8-GPU two-shot per bucket beside backward")
             dp["overlap_rehearsal"] = dp_overlap(dev)
         if not cancel():  # the watchdog fired and wrote the line; the process is exiting
             return

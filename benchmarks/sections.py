@@ -13,11 +13,11 @@ same HBM, no xGMI):
   reduce_kernel    BASELINE config 2: the reduce_slots kernel over P = 2 / 4 / 8 slots of a
                    1 GiB fp32 buffer (the worker's `reduce`, AllreduceWorker.scala:240-251),
                    TB/s of HBM traffic and the fraction of the same-run copy roofline.
-  dp_overlap       BASELINE config 5's overlap on one GPU with REAL communication: the
-                   bucketed reducer's buckets go through a 2-logical-rank allreduce (this
-                   rank's bucket + a synthetic peer gradient, one launch, on the comm stream)
-                   while the synthetic backward's GEMMs run; swept over the reducer's
-                   workgroup budget, reporting the GEMMs' slowdown and the exposed time.
+  dp_overlap       BASELINE config 5's overlap on one GPU with REAL communication: every
+                   bucket goes through ONE rank of an 8-GPU two-shot run alone (peers' flags
+                   pre-armed; the same per-GPU HBM bytes as a real rank) on the comm stream
+                   while the synthetic backward's GEMMs run; serial vs overlapped vs CU
+                   slices vs paced (small-grid) comm, the GEMMs' slowdown and the exposed time.
   protocol_sizes   the reference's master / worker round protocol driving the GPU round
                    engine (PlaneJob: StartAllreduce -> one threshold-kernel launch per worker)
                    at 40 B (the reference's default job: 10 floats, maxChunkSize 2 -
@@ -436,28 +436,56 @@ def sdma_local(dev, dtype: torch.dtype = torch.bfloat16, nbytes: int = 256 << 20
     return out
 
 
-class PairSdmaRehearsalComm:
-    """PairRehearsalComm with the SDMA allreduce (parallel/sdma.py): the two logical ranks'
-    cross-rank copies run on copy engines, only the small-grid reduce and gather on CUs. It
-    shares the CU pair's synthetic peer gradients."""
+class SoloRehearsalComm:
+    """ONE rank of an N-rank (default 8) direct two-shot, run alone on this GPU: the N - 1 peers
+    are communicators whose slabs live here but which never launch, and this rank's slab has
+    every flag a peer would write pre-armed (XgmiComm.arm_solo_rehearsal), so its kernel runs
+    the real two-shot without waiting. It reads its input, pushes the N - 1 foreign blocks into
+    the peers' S slots, reduces its own block from the input and its own S slots (the synthetic
+    peers' contributions: zeros), pushes the sum into the peers' R slots and gathers its own R
+    slots (never written: the other blocks of the output come back as zeros). Every byte lands in this GPU's HBM, and per bucket of S bytes it moves reads
+    (1 + 2 (N - 1) / N) S and writes (1 + 2 (N - 1) / N) S: exactly the per-GPU HBM traffic of a
+    real N-GPU two-shot, where the outgoing pushes land on the peers and the peers' pushes land
+    here (`hbm_bytes`). What it cannot model is the xGMI time: the pushes run at HBM speed, so
+    the small-grid variants of dp_overlap pace it towards the link-bound duration."""
 
     accepts_stream = True
-    world = 2
 
-    def __init__(self, buckets, peer: dict, grid: int = 32):
-        from akka_allreduce_1_amd.parallel import LocalSdmaCluster
+    def __init__(self, buckets, world: int = 8, grid: int = 512):
+        from akka_allreduce_1_amd._native import C
 
+        self.H = C.hip
         big = max(b.nbytes for b in buckets)
-        self.cl = LocalSdmaCluster(2, slot_bytes=-(-big // 2) + (1 << 20), grid=grid, timeout_s=20.0)
-        self.peer = peer
+        dev = torch.cuda.current_device()
+        self.world = world
+        slot = -(-big // world) + (1 << 20)
+        self.comms = [self.H.XgmiComm(k, world, dev, slot, grid, 20.0, 0) for k in range(world)]
+        for c in self.comms:
+            c.connect_local(self.comms)
+        self.comms[0].arm_solo_rehearsal()
+        self.cl = self  # dp_overlap sets `cl.comms[*].grid`
+        self.bytes_moved = 0
+
+    @staticmethod
+    def hbm_bytes(S: int, world: int = 8) -> int:
+        """Per-GPU HBM bytes of one rank of a real `world`-GPU two-shot of S bytes: reads of
+        the input, the S slots and the R slots; writes of the own output block, the peers'
+        incoming S and R pushes and the gathered output."""
+        return int(2 * (S + 2 * S * (world - 1) / world))
 
     def allreduce_(self, t: torch.Tensor, *, op: str = "sum", algo: str = "auto", stream: int | None = None):
-        x1, y1 = self.peer[t.data_ptr()]
-        self.cl.allreduce([t, x1], [t, y1], op=op, stream=stream)
+        from akka_allreduce_1_amd.parallel.comm import _dtype_code
+
+        s = torch.cuda.current_stream(t.device).cuda_stream if stream is None else stream
+        self.comms[0].allreduce(t.data_ptr(), t.data_ptr(), t.numel(), _dtype_code(t.dtype), s,
+                                self.H.Algo.TwoShot, 1.0 / self.world if op == "avg" else 1.0)
         return t
 
     def check(self):
-        self.cl.check()
+        torch.cuda.synchronize()
+        e = self.comms[0].error()
+        if e:
+            raise RuntimeError(f"solo rehearsal: error word {e:#x}")
 
 
 class PairRehearsalComm:
@@ -491,20 +519,25 @@ class PairRehearsalComm:
         self.cl.check()
 
 
-def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 512)) -> dict:
-    """BASELINE config 5 (and 4) rehearsed on one GPU with real comm kernels beside the GEMMs:
-    per reducer grid (workgroups of one bucket launch, both logical ranks), the step
-    (backward + overlapped bucket allreduces + SGD update), the compute-only step, the
-    backward's own time with comm running beside it (up to the last GEMM on the compute
-    stream) vs without it (gemm_slowdown), and the comm-only time of every bucket."""
+def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 512), world: int = 8,
+               link_GBps: float = 153.6) -> dict:
+    """BASELINE config 5 (and 4) rehearsed on one GPU with a byte-faithful comm beside the
+    GEMMs: every bucket allreduce is ONE rank of a `world`-GPU two-shot (SoloRehearsalComm),
+    so the comm moves exactly one rank's per-GPU HBM bytes of the N = 8 job (reported as
+    hbm_bytes_per_rank). Per variant: the step (backward + overlapped bucket allreduces + SGD
+    update), the compute-only step, the backward's own time with the comm beside it vs without
+    (gemm_slowdown) and the comm-only time. The comm pushes at HBM speed, not xGMI speed: the
+    grid variants pace it (comm_GBps, against xgmi_floor_ms = the link-bound time of the same
+    buckets at `link_GBps` per link and direction), serial runs every bucket after backward,
+    and the cu / split variants confine the comm (and the backward) to CU slices."""
     from akka_allreduce_1_amd.models.grad_sets import gradient_shapes
     from akka_allreduce_1_amd.parallel import BucketedGradReducer
     from benchmarks.bench_dp import SyntheticBackward
 
-    out: dict = {"method": "2 logical ranks in one launch per bucket (this rank's bucket + a synthetic peer) "
-                           "on the reducer's comm stream; medians of interleaved steps",
-                 "note": "both ranks' comm traffic lands on this GPU: about 2x the HBM traffic of one rank "
-                         "of a real 2-GPU job (upper bound on contention); no xGMI"}
+    out: dict = {"method": f"one rank of a {world}-GPU two-shot per bucket, run alone (peers' flags pre-armed, "
+                           "pushes into local peer slabs) on the reducer's comm stream; medians of interleaved steps",
+                 "note": "per-GPU HBM bytes equal a real N-GPU rank's; the pushes run at HBM rather than xGMI speed "
+                         "(grid variants pace them)"}
     for model in models:
         row: dict = {}
         params = bwd = reducer = comm = None
@@ -514,11 +547,14 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
             big = model == "llama3_8b"
             steps, warm = (5, 1) if big else (15, 3)
             kw = dict(bucket_bytes=1 << 30, first_bucket_bytes=64 << 20) if big else dict(bucket_bytes=25 << 20)
-            reducer = BucketedGradReducer(params, _Placeholder(), op="avg", **kw)
+            reducer = BucketedGradReducer(params, _Placeholder(world), op="avg", **kw)
             reducer.remove_hooks()  # the synthetic backward calls the hook itself
-            comm = PairRehearsalComm(reducer.buckets, max(grids))
+            comm = SoloRehearsalComm(reducer.buckets, world, max(grids))
             reducer.comm = comm
             reducer._raw_ok = True
+            sizes = [b.nbytes for b in reducer.buckets]
+            row["hbm_bytes_per_rank"] = sum(SoloRehearsalComm.hbm_bytes(S, world) for S in sizes)
+            row["xgmi_floor_ms"] = round(sum(2 * (S / world) / (link_GBps * 1e9) for S in sizes) * 1e3, 3)
             bwds = {1024: SyntheticBackward(params, 1024, torch.bfloat16, dev)}
             bwd = bwds[1024]
             grads = [q.grad for q in params]
@@ -562,20 +598,11 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
             # and the complete split: backward on every OTHER CU (ddp.compute_stream_excluding),
             # so no GEMM tile shares a CU with a spinning comm workgroup
             variants += [("split32_grid64", 64, True, True, 1024), ("split64_grid128", 128, True, True, 1024)]
-            # the copy-engine allreduce: cross-rank copies on SDMA engines, reduce / gather on
-            # a small grid (the comm's CU footprint)
-            cu_comm, sdma_comm = comm, None
-            try:
-                sdma_comm = PairSdmaRehearsalComm(reducer.buckets, comm.peer)
-                variants += [("sdma_grid16", 16, True, True, 1024), ("sdma_grid64", 64, True, True, 1024)]
-            except Exception as e:  # noqa: BLE001 - no SDMA engines here: CU variants only
-                row["sdma_error"] = repr(e)
             if big:
                 # 1024 tokens make the weight-gradient GEMMs (K = tokens) nearly bandwidth bound,
                 # so a bandwidth-bound allreduce beside them slows them; at a training-size
-                # 8192 tokens per GPU they are compute bound
-                # compute-bound backward: a small comm grid stretches the allreduces over the
-                # backward instead of contending with it at full bandwidth
+                # 8192 tokens per GPU they are compute bound, and a small comm grid stretches
+                # the allreduces over the backward instead of contending at full bandwidth
                 variants += [("tokens8192_grid256", 256, True, True, 8192), ("tokens8192_serial", 512, False, True, 8192),
                              ("tokens8192_grid32", 32, True, True, 8192), ("tokens8192_grid64", 64, True, True, 8192),
                              ("tokens8192_grid128", 128, True, True, 8192),
@@ -587,8 +614,6 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                     if tokens not in bwds:
                         bwds[tokens] = SyntheticBackward(params, tokens, torch.bfloat16, dev)
                     bwd = bwds[tokens]
-                    comm = sdma_comm if name.startswith("sdma") else cu_comm
-                    reducer.comm = comm
                     for c in comm.cl.comms:
                         c.grid = grid
                     reducer.overlap = ov
@@ -634,14 +659,14 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                             "bwd_ms_with_comm": round(med["bwd_with_comm"], 3),
                             "bwd_ms_alone": round(med["bwd_alone"], 3),
                             "gemm_slowdown": round(med["bwd_with_comm"] / med["bwd_alone"], 3),
-                            "hidden_frac": round(max(0.0, 1 - exposed / comm_ms), 3)}
+                            "hidden_frac": round(max(0.0, 1 - exposed / comm_ms), 3),
+                            "comm_GBps": round(row["hbm_bytes_per_rank"] / (comm_ms * 1e6), 1)}
                 except Exception as e:  # noqa: BLE001
                     cell["error"] = repr(e)
                 row[name] = cell
             reducer.overlap, reducer.stream, reducer._comm_raw, reducer._cus = True, hi_stream, hi_raw, 0
             reducer.algo = "auto"
             cstream["s"] = None
-            comm = cu_comm
             ok = {g: c for g, c in row.items() if isinstance(c, dict) and "step_ms" in c}
             if ok:
                 row["best"] = min(ok, key=lambda g: ok[g]["step_ms"])
@@ -649,15 +674,19 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
             if cu:  # the CU-sliced candidate's best cell
                 g = min(cu, key=lambda k: cu[k]["step_ms"])
                 row["cu_slice"] = dict(cu[g], variant=g)
-            sd = {g: c for g, c in ok.items() if g.startswith("sdma")}
-            if sd:  # the copy-engine candidate's best cell, next to the CU grids'
-                row["sdma"] = dict(sd[min(sd, key=lambda g: sd[g]["step_ms"])], variant=min(sd, key=lambda g: sd[g]["step_ms"]))
+            ser = {g: c for g, c in ok.items() if "serial" in g}
+            for tag, pre in (("tokens1024", "grid"), ("tokens8192", "tokens8192_grid")):
+                s_ = [c for g, c in ser.items() if (c["tokens"] == 8192) == (tag == "tokens8192")]
+                ov_ = {g: c for g, c in ok.items() if g.startswith(pre) or (g.startswith("split") and
+                                                                            (c["tokens"] == 8192) == (tag == "tokens8192"))}
+                if s_ and ov_:  # the best overlapped cell against serial, per token count
+                    g = min(ov_, key=lambda k: ov_[k]["step_ms"])
+                    row[f"overlap_vs_serial_{tag}"] = [g, round(ov_[g]["step_ms"] / s_[0]["step_ms"], 3)]
             row["buckets"] = f"{len(reducer.buckets)} ({'64 MiB first, 1 GiB after' if big else '25 MiB'})"
         except Exception as e:  # noqa: BLE001
             row["error"] = repr(e)
         finally:
             del params, bwd, reducer, comm
-            cu_comm = sdma_comm = None
             bwds = None
             torch.cuda.empty_cache()
         out[model] = row
@@ -666,7 +695,9 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
 
 class _Placeholder:
     """Stands in for the communicator while the reducer lays out its buckets (the rehearsal
-    communicator needs the bucket buffers to build its peer gradients)."""
+    communicator needs the bucket buffers to size its slabs)."""
 
-    world = 2
     accepts_stream = True
+
+    def __init__(self, world: int = 2):
+        self.world = world

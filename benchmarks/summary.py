@@ -71,6 +71,9 @@ def _sweep(rows: list) -> list:
 
 def _local(lr: dict) -> dict:
     out = {"copy_TBps": lr.get("copy_roofline_TBps")}
+    pl = lr.get("placement")
+    if isinstance(pl, dict) and pl.get("frac_copy_roofline"):  # slab placements tried, their fractions
+        out["placement"] = pl["frac_copy_roofline"]
     for algo in ("twoshot", "ring", "ring_native"):
         c = lr.get(algo)
         if isinstance(c, dict) and "p50_ms" in c:
@@ -147,9 +150,8 @@ def _dp(dp: dict) -> tuple[dict, dict]:
         if isinstance(r, dict) and isinstance(r.get("best"), str) and isinstance(r.get(r["best"]), dict):
             b = r[r["best"]]
             ovl[m] = [r["best"], b.get("step_ms"), b.get("exposed_comm_ms"), b.get("gemm_slowdown")]
-            sd = r.get("sdma")
-            if isinstance(sd, dict) and "step_ms" in sd:
-                ovl[m + "_sdma"] = [sd.get("step_ms"), sd.get("exposed_comm_ms"), sd.get("gemm_slowdown")]
+            if "overlap_vs_serial_tokens8192" in r or "overlap_vs_serial_tokens1024" in r:
+                ovl[m + "_vs_serial"] = r.get("overlap_vs_serial_tokens8192") or r.get("overlap_vs_serial_tokens1024")
             cu = r.get("cu_slice")
             if isinstance(cu, dict) and "step_ms" in cu:
                 ovl[m + "_cu"] = [cu.get("variant"), cu.get("step_ms"), cu.get("exposed_comm_ms"), cu.get("gemm_slowdown")]

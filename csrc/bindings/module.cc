@@ -10,6 +10,8 @@
 #include <atomic>
 #include <condition_variable>
 #include <thread>
+#include <execinfo.h>
+#include <signal.h>
 #include <unistd.h>
 #include <optional>
 #include <sstream>
@@ -497,6 +499,31 @@ PYBIND11_MODULE(_C, m) {
         "The kernel geometry every worker of a membership derives from InitWorkers (csrc/runtime/plane_geometry.h)");
 
   // ---------------------------------------------------------------- core helpers
+  // bring-up aid (no debugger on the GPU boxes): a native SIGSEGV / SIGBUS prints the faulting
+  // thread's native frames to stderr, then the previous handler (Python's faulthandler) runs
+  m.def("install_native_backtrace", [] {
+    static struct sigaction prev_segv, prev_bus;
+    struct sigaction sa {};
+    sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
+    sa.sa_sigaction = [](int sig, siginfo_t* info, void* ctx) {
+      void* frames[64];
+      const int n = backtrace(frames, 64);
+      const char head[] = "\n[native backtrace]\n";
+      (void)!write(2, head, sizeof(head) - 1);
+      backtrace_symbols_fd(frames, n, 2);
+      struct sigaction& prev = sig == SIGSEGV ? prev_segv : prev_bus;
+      if (prev.sa_flags & SA_SIGINFO) {
+        if (prev.sa_sigaction) prev.sa_sigaction(sig, info, ctx);
+      } else if (prev.sa_handler != SIG_DFL && prev.sa_handler != SIG_IGN && prev.sa_handler) {
+        prev.sa_handler(sig);
+      }
+      signal(sig, SIG_DFL);
+      raise(sig);
+    };
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGSEGV, &sa, &prev_segv);
+    sigaction(SIGBUS, &sa, &prev_bus);
+  });
   m.def("f32_threshold_count", &f32_threshold_count, py::arg("threshold"), py::arg("peers"));
   m.def("f32_threshold_chunks", &f32_threshold_chunks, py::arg("threshold"), py::arg("peers"), py::arg("numChunks"));
   m.def("f32_ceil_div", &f32_ceil_div);

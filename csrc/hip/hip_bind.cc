@@ -386,6 +386,8 @@ void bind_hip(py::module_& m) {
       .def("clear_error", &SdmaComm::clear_error)
       .def("debug_state", &SdmaComm::debug_state)
       .def_property("grid", &SdmaComm::grid, &SdmaComm::set_grid)
+      .def_property("pieces", &SdmaComm::pieces, &SdmaComm::set_pieces,
+                    "pipeline pieces per block (0 = one per 8 MiB of the block, 2..8)")
       .def_property_readonly("engines", &SdmaComm::engines)
       .def_property_readonly("engines_per_peer", &SdmaComm::engines_per_peer)
       .def_property_readonly("slot_bytes", &SdmaComm::slot_bytes)
@@ -556,6 +558,10 @@ void bind_hip(py::module_& m) {
         py::gil_scoped_release r;
         c.reset_local();
       })
+      .def("arm_solo_rehearsal", [](XgmiComm& c) {
+        py::gil_scoped_release r;
+        c.arm_solo_rehearsal();
+      }, "one-rank traffic rehearsal only: peers' flags into this slab read as reached (xgmi_comm.h)")
       .def_property_readonly("rank", &XgmiComm::rank)
       .def_property_readonly("world", &XgmiComm::world)
       .def_property_readonly("device", &XgmiComm::device)

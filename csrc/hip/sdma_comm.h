@@ -4,14 +4,18 @@
 // that run beside backward's GEMMs (BASELINE config 5). Same direct two-shot as XgmiComm
 // (the reference's ScatterBlock / ReduceBlock, AllreduceWorker.scala:194-238):
 //
-//   phase 1  ScatterBlock   block j of the input -> rank j's SD slot [r]: one SDMA copy per
-//                           peer (split over `engines_per_peer` engines), then a 4-byte SDMA
-//                           copy of the epoch into rank j's FS[r] flag (ordered after the
-//                           data by an HSA completion-signal dependency)
-//   reduce                  a small-grid kernel (grid_ workgroups) sums the own block from
-//                           the input and the P-1 SD slots once every FS flag shows the epoch
-//   phase 2  ReduceBlock    the reduced own block -> every peer's RD slot [r] + FR flag (SDMA)
-//   gather                  a small-grid kernel copies the peers' RD slots into the output
+//   phase 1  ScatterBlock   block j of the input -> rank j's SD slot [r], in K pipeline
+//                           pieces: piece k is split over the `engines_per_peer` engines,
+//                           and a 4-byte SDMA copy of the epoch into rank j's FS[r][k] flag
+//                           follows its parts (HSA completion-signal dependencies)
+//   reduce                  ONE small-grid kernel (grid_ workgroups, every local rank) walks
+//                           the pieces in order: wait for FS[*][k], sum piece k of the own
+//                           block from the input and the P-1 SD slots, and the piece's last
+//                           workgroup releases the signal its phase-2 copies wait on - so
+//                           the engines copy piece k + 1 while the CUs reduce piece k
+//   phase 2  ReduceBlock    reduced piece k -> every peer's RD slot [r] + FR[r][k] (SDMA)
+//   gather                  ONE small-grid kernel copies each peer's RD piece into the
+//                           output as soon as its FR flag shows the epoch
 //
 // Stream ordering without the host: HIP's hipMemcpyAsync runs device-to-device copies as
 // blit KERNELS (profiles/round4/README.md, tools/sdma_probe.cc in git history), so the copies are submitted
@@ -33,6 +37,9 @@
 #include "xgmi_comm.h"
 
 namespace mxar {
+
+constexpr int kSdmaMaxPieces = 8;  // pipeline pieces per block at most
+constexpr int kSdmaMaxLocal = 8;   // local ranks one reduce / gather launch serves
 
 struct SdmaStats {
   uint64_t calls = 0, copies = 0, bytes = 0, host_waits = 0;
@@ -71,6 +78,9 @@ class SdmaComm {
   int world() const { return world_; }
   int grid() const { return grid_; }
   void set_grid(int g) { grid_ = g > 0 ? g : 1; }
+  // pipeline pieces per block (0 = by size: one per 8 MiB of the block, 2..kSdmaMaxPieces)
+  int pieces() const { return pieces_; }
+  void set_pieces(int k) { pieces_ = k < 0 ? 0 : k; }
   int engines() const { return static_cast<int>(local_engines_.size()); }
   int engines_per_peer() const { return epp_; }
   int64_t slot_bytes() const { return slot_bytes_; }
@@ -81,19 +91,20 @@ class SdmaComm {
   struct Plan {
     const char* in = nullptr;
     char* out = nullptr;
-    int64_t n = 0, block = 0;
+    int64_t n = 0, block = 0, pe = 0;  // pe: elements per pipeline piece
+    int K = 1;                         // pipeline pieces of a block
     DType dt = DType::F32;
     uint32_t epoch = 0;
     int par = 0, slot = 0;
   };
   // one segment: wait for the slot, arm its signals, queue both phases' copies (host)
   Plan plan(const char* in, char* out, int64_t n, DType dt);
-  void enqueue_reduce(const Plan& pl, hipStream_t stream, float scale);
-  void enqueue_gather(const Plan& pl, hipStream_t stream);
   int rank_, world_, device_;
   int64_t slot_bytes_;
   int grid_;
   int epp_;
+  int pieces_ = 0;
+  uint32_t* cnt_ = nullptr;  // device: per-piece workgroup tickets of the reduce kernel
   double timeout_s_;
   char* slab_ = nullptr;
   int64_t slab_bytes_ = 0;

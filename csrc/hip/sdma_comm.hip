@@ -21,7 +21,9 @@ namespace {
 
 constexpr int kSlots = 16;              // calls in flight at most (signal / epoch-word ring)
 constexpr int64_t kFlagBytes = 64 * 1024;
-constexpr int kFrWord = 64;             // FR flags start at word 64 (FS at word 0)
+// flag words: FS[s][k] at s * kSdmaMaxPieces + k, FR[s][k] at kFrWord + s * kSdmaMaxPieces + k
+constexpr int kFrWord = 32 * kSdmaMaxPieces;
+constexpr int64_t kPieceBytes = int64_t{8} << 20;  // auto pieces: one per 8 MiB of the block
 
 void hsa_check(hsa_status_t s, const char* what) {
   if (s != HSA_STATUS_SUCCESS) {
@@ -31,9 +33,9 @@ void hsa_check(hsa_status_t s, const char* what) {
   }
 }
 
-int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+__host__ __device__ inline int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 int64_t hclamp(int64_t avail, int64_t cap) { return avail <= 0 ? 0 : (avail < cap ? avail : cap); }
-int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+__host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // PCI location of a HIP device / an HSA agent: (domain << 32) | bdf
 uint64_t hip_location(int device) {
@@ -73,53 +75,97 @@ __global__ void sdma_release_kernel(int64_t* sig) {
   if (threadIdx.x == 0) __hip_atomic_store(sig, int64_t{0}, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// One wave: lane k < nflags (k != skip) waits for flags[k] >= epoch, bounded by the deadline.
-__global__ __launch_bounds__(64) void sdma_wait_kernel(const uint32_t* flags, int nflags, int skip, uint32_t epoch,
-                                                       uint64_t timeout, uint32_t* err) {
-  const int k = static_cast<int>(threadIdx.x);
-  const uint64_t deadline = wall_ticks() + timeout;
-  const uint32_t* f = (k < nflags && k != skip) ? flags + k : nullptr;
-  bool ok = f == nullptr || reached(ld_flag(f), epoch);
-  while (!__all(ok)) {
-    __builtin_amdgcn_s_sleep(2);
-    if (!ok) ok = reached(ld_flag(f), epoch);
-    if (wall_ticks() > deadline) break;
+// One launch of the pipelined reduce / gather for the local ranks of a call (blockIdx.y).
+struct SdmaRankArgs {
+  const char* in;         // the rank's input (whole tensor segment)
+  char* out;              // its output
+  const char* sd;         // its SD slots of this call's parity (slot s at s * slot)
+  const char* rd;         // its RD slots of this call's parity
+  const uint32_t* flags;  // its flag words (FS at 0, FR at kFrWord)
+  int64_t* mid[kSdmaMaxPieces];  // phase-2 release signal of each piece (value pointer)
+  uint32_t* cnt;          // per-piece workgroup tickets (device, zero between launches)
+  uint32_t* err;
+  uint32_t epoch;
+  int r;
+};
+struct SdmaLaunch {
+  SdmaRankArgs y[kSdmaMaxLocal];
+  int64_t n, block, pe, slot;  // elements (slot: bytes)
+  uint64_t timeout;            // 100 MHz ticks
+  int W, K;
+  float scale;
+};
+
+__device__ __forceinline__ int64_t sdma_blen(const SdmaLaunch& L, int s) {
+  return clamp_len(L.n - static_cast<int64_t>(s) * L.block, L.block);
+}
+
+// Own block = scale x (own input + the P-1 SD slots), fixed order s = 0..P-1, fp32, written
+// through (the engines read it from memory for phase 2), piece by piece: piece k is reduced
+// once every peer's FS[s][k] shows the epoch, and its last workgroup releases mid[k] - the
+// signal the engines' phase-2 copies of piece k wait on. No workgroup waits for another.
+template <class E>
+__global__ __launch_bounds__(kCommThreads) void sdma_reduce_kernel(SdmaLaunch L) {
+  constexpr int es = 16 / E::ELEMS;
+  const SdmaRankArgs& a = L.y[blockIdx.y];
+  const int G = static_cast<int>(gridDim.x);
+  const uint64_t deadline = wall_ticks() + L.timeout;
+  const int64_t rl = sdma_blen(L, a.r);
+  const int64_t own0 = static_cast<int64_t>(a.r) * L.block;
+  for (int k = 0; k < L.K; ++k) {
+    const int64_t p0 = static_cast<int64_t>(k) * L.pe;
+    const int64_t lk = clamp_len(rl - p0, L.pe);
+    if (lk <= 0) break;  // uniform
+    wait_flags([&](int s) -> const uint32_t* { return s == a.r ? nullptr : a.flags + s * kSdmaMaxPieces + k; }, L.W,
+               a.epoch, deadline, a.err, ERR_TIMEOUT_SCATTER);
+    const int64_t sub = rup(cdiv(lk, G), E::ELEMS);
+    const int64_t b0 = static_cast<int64_t>(blockIdx.x) * sub;
+    const int64_t l = clamp_len(lk - b0, sub);
+    if (l > 0) {
+      const RedSrc src{a.in + (own0 + p0 + b0) * es, a.sd + (p0 + b0) * es, L.slot, a.r};
+      char* dst = a.out + (own0 + p0 + b0) * es;
+      reduce_to<E, 0>(L.W, src, 1, 0, [&](int) -> char* { return dst; }, l, L.scale, true);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the engines read the piece
+      const uint32_t t = __hip_atomic_fetch_add(&a.cnt[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == static_cast<uint32_t>(G - 1)) {
+        __hip_atomic_store(&a.cnt[k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.mid[k], int64_t{0}, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
-  if (!__all(ok) && k == 0) __hip_atomic_fetch_or(err, ERR_TIMEOUT_SCATTER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Own block = scale x (own input + the P-1 SD slots), fixed order s = 0..P-1, fp32; written
-// through (the engines read it from memory for phase 2). Workgroup b takes piece b.
+// out[block s, piece k] = RD slot s piece k for every s != r, piece by piece as the FR[s][k]
+// flags arrive (and the own FR[r][k]: the engines have finished READING the own block's
+// piece k for phase 2, so the call is complete for the stream). Plain-memory consumers
+// follow on this stream: the stores go through to memory.
 template <class E>
-__global__ __launch_bounds__(kCommThreads) void sdma_reduce_kernel(const char* in_own, const char* sd, int64_t slot,
-                                                                   int P, int r, char* out_own, int64_t len,
-                                                                   int64_t piece, float scale) {
+__global__ __launch_bounds__(kCommThreads) void sdma_gather_kernel(SdmaLaunch L) {
   constexpr int es = 16 / E::ELEMS;
-  // the engines wrote SD: drop any stale line of an earlier call from this CU's caches
-  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  __syncthreads();
-  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * piece;
-  const int64_t l = clamp_len(len - b0, piece);
-  if (l <= 0) return;
-  const RedSrc src{in_own + b0 * es, sd + b0 * es, slot, r};
-  reduce_to<E, 0>(P, src, 1, 0, [&](int) -> char* { return out_own + b0 * es; }, l, scale, true);
-}
-
-// out[block s] = RD slot s for every s != r (blockIdx.y = s). Plain-memory consumers follow
-// on this stream: the stores go through to memory.
-template <class E>
-__global__ __launch_bounds__(kCommThreads) void sdma_gather_kernel(char* out, const char* rd, int64_t slot, int r,
-                                                                   int64_t n, int64_t block, int64_t piece) {
-  constexpr int es = 16 / E::ELEMS;
-  const int s = static_cast<int>(blockIdx.y);
-  if (s == r) return;
-  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  __syncthreads();
-  const int64_t blen = clamp_len(n - static_cast<int64_t>(s) * block, block);
-  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * piece;
-  const int64_t l = clamp_len(blen - b0, piece);
-  if (l <= 0) return;
-  copy_from_slab<E>(out + (static_cast<int64_t>(s) * block + b0) * es, rd + s * slot + b0 * es, l);
+  const SdmaRankArgs& a = L.y[blockIdx.y];
+  const int G = static_cast<int>(gridDim.x);
+  const uint64_t deadline = wall_ticks() + L.timeout;
+  for (int k = 0; k < L.K; ++k) {
+    const int64_t p0 = static_cast<int64_t>(k) * L.pe;
+    if (p0 >= L.block) break;  // uniform
+    wait_flags([&](int s) -> const uint32_t* {
+                 return sdma_blen(L, s) > p0 ? a.flags + kFrWord + s * kSdmaMaxPieces + k : nullptr;
+               },
+               L.W, a.epoch, deadline, a.err, ERR_TIMEOUT_REDUCE);
+    const int64_t sub = rup(cdiv(L.pe, G), E::ELEMS);
+    const int64_t b0 = static_cast<int64_t>(blockIdx.x) * sub;
+    for (int s = 0; s < L.W; ++s) {
+      if (s == a.r) continue;
+      const int64_t l = clamp_len(clamp_len(sdma_blen(L, s) - p0, L.pe) - b0, sub);
+      if (l > 0)
+        copy_from_slab<E>(a.out + (static_cast<int64_t>(s) * L.block + p0 + b0) * es,
+                          a.rd + s * L.slot + (p0 + b0) * es, l);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -179,11 +225,25 @@ struct SdmaComm::Impl {
   std::vector<hsa_agent_t> peer_agent;
   std::vector<std::vector<hsa_amd_sdma_engine_id_t>> peer_engines;  // engines towards peer k
   struct Slot {
-    hsa_signal_t start{0}, mid{0}, sc{0}, scf{0}, gd{0}, gdf{0};
+    hsa_signal_t start{0}, scf{0}, gdf{0};
+    hsa_signal_t mid[kSdmaMaxPieces]{};
     int64_t* start_p = nullptr;
-    int64_t* mid_p = nullptr;
+    int64_t* mid_p[kSdmaMaxPieces]{};
+    // completion of a piece's data parts: phase 1 per peer ([j * K + k]), phase 2 over every
+    // peer ([k]: the own FR flag needs them all, and a copy with one dependency is the form the
+    // engines are known to take), armed to the part count - every part's completion
+    // decrements it, the piece's flag copies wait for 0. Memory-only signals (the host never waits on them, so
+    // no interrupt events - KFD has few), grown on demand.
+    std::vector<hsa_signal_t> c1, c2;
     bool used = false;
   };
+  static void grow(std::vector<hsa_signal_t>& v, size_t need) {
+    while (v.size() < need) {
+      hsa_signal_t x{0};
+      hsa_check(hsa_amd_signal_create(0, 0, nullptr, HSA_AMD_SIGNAL_AMD_GPU_ONLY, &x), "signal(piece)");
+      v.push_back(x);
+    }
+  }
   Slot slots[kSlots];
   uint32_t* words = nullptr;  // pinned epoch words, one per slot (the flag copies' source)
   hipEvent_t sysrel = nullptr;
@@ -231,15 +291,19 @@ SdmaComm::SdmaComm(int rank, int world, int device, int64_t slot_bytes, int grid
   std::memset(impl_->words, 0, kSlots * 64);
   hip_check(hipEventCreateWithFlags(&impl_->sysrel, hipEventDisableTiming | hipEventReleaseToSystem),
             "hipEventCreate(release to system)");
+  hip_check(hipMalloc(reinterpret_cast<void**>(&cnt_), kSdmaMaxPieces * 4), "hipMalloc(piece tickets)");
+  hip_check(hipMemset(cnt_, 0, kSdmaMaxPieces * 4), "hipMemset(piece tickets)");
   for (auto& sl : impl_->slots) {
-    hsa_check(hsa_amd_signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_IPC, &sl.start), "signal(start)");
-    hsa_check(hsa_amd_signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_IPC, &sl.mid), "signal(mid)");
-    for (hsa_signal_t* x : {&sl.sc, &sl.scf, &sl.gd, &sl.gdf}) hsa_check(hsa_signal_create(0, 0, nullptr, x), "signal");
     volatile hsa_signal_value_t* p = nullptr;
+    hsa_check(hsa_amd_signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_IPC, &sl.start), "signal(start)");
     hsa_check(hsa_amd_signal_value_pointer(sl.start, &p), "signal_value_pointer(start)");
     sl.start_p = const_cast<int64_t*>(reinterpret_cast<volatile int64_t*>(p));
-    hsa_check(hsa_amd_signal_value_pointer(sl.mid, &p), "signal_value_pointer(mid)");
-    sl.mid_p = const_cast<int64_t*>(reinterpret_cast<volatile int64_t*>(p));
+    for (int k = 0; k < kSdmaMaxPieces; ++k) {
+      hsa_check(hsa_amd_signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_IPC, &sl.mid[k]), "signal(mid)");
+      hsa_check(hsa_amd_signal_value_pointer(sl.mid[k], &p), "signal_value_pointer(mid)");
+      sl.mid_p[k] = const_cast<int64_t*>(reinterpret_cast<volatile int64_t*>(p));
+    }
+    for (hsa_signal_t* x : {&sl.scf, &sl.gdf}) hsa_check(hsa_signal_create(0, 0, nullptr, x), "signal");
   }
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
   peers_.assign(world_, nullptr);
@@ -252,18 +316,25 @@ SdmaComm::~SdmaComm() {
   (void)hipDeviceSynchronize();
   if (impl_) {
     // no copy of ours may still target a peer slab we are about to unmap
+    // (every data part precedes a flag copy counted in scf / gdf)
     for (auto& sl : impl_->slots)
-      for (hsa_signal_t x : {sl.sc, sl.scf, sl.gd, sl.gdf})
+      for (hsa_signal_t x : {sl.scf, sl.gdf})
         if (x.handle) (void)hsa_signal_wait_scacquire(x, HSA_SIGNAL_CONDITION_EQ, 0, 2000000000ull, HSA_WAIT_STATE_BLOCKED);
-    for (auto& sl : impl_->slots)
-      for (hsa_signal_t x : {sl.start, sl.mid, sl.sc, sl.scf, sl.gd, sl.gdf})
+    for (auto& sl : impl_->slots) {
+      for (hsa_signal_t x : {sl.start, sl.scf, sl.gdf})
         if (x.handle) hsa_signal_destroy(x);
+      for (hsa_signal_t x : sl.mid)
+        if (x.handle) hsa_signal_destroy(x);
+      for (auto* v : {&sl.c1, &sl.c2})
+        for (hsa_signal_t x : *v) hsa_signal_destroy(x);
+    }
     if (impl_->sysrel) (void)hipEventDestroy(impl_->sysrel);
     if (impl_->words) (void)hipHostFree(impl_->words);
   }
   for (int k = 0; k < world_; ++k)
     if (opened_[k] && peers_[k]) (void)hipIpcCloseMemHandle(peers_[k]);
   if (err_) (void)hipFree(err_);
+  if (cnt_) (void)hipFree(cnt_);
   if (slab_) (void)hipFree(slab_);
   if (impl_ && impl_->hsa_up) hsa_shut_down();
 }
@@ -354,18 +425,21 @@ std::string SdmaComm::debug_state() const {
     const Impl::Slot& sl = impl_->slots[i];
     if (!sl.used) continue;
     out += " | slot" + std::to_string(i) + " start=" + std::to_string(hsa_signal_load_relaxed(sl.start)) +
-           " mid=" + std::to_string(hsa_signal_load_relaxed(sl.mid)) +
-           " sc=" + std::to_string(hsa_signal_load_relaxed(sl.sc)) +
-           " scf=" + std::to_string(hsa_signal_load_relaxed(sl.scf)) +
-           " gd=" + std::to_string(hsa_signal_load_relaxed(sl.gd)) +
+           " mid=";
+    for (hsa_signal_t x : sl.mid) out += std::to_string(hsa_signal_load_relaxed(x)) + ",";
+    out += " scf=" + std::to_string(hsa_signal_load_relaxed(sl.scf)) +
            " gdf=" + std::to_string(hsa_signal_load_relaxed(sl.gdf));
   }
-  std::vector<uint32_t> f(128, 0);
+  std::vector<uint32_t> f(2 * kFrWord, 0);
   (void)hipMemcpy(f.data(), slab_, f.size() * 4, hipMemcpyDeviceToHost);
-  out += " | FS=";
-  for (int k = 0; k < world_; ++k) out += std::to_string(f[k]) + ",";
-  out += " FR=";
-  for (int k = 0; k < world_; ++k) out += std::to_string(f[kFrWord + k]) + ",";
+  for (const char* what : {"FS", "FR"}) {
+    const int base = what[1] == 'S' ? 0 : kFrWord;
+    out += std::string(" | ") + what + "[rank][piece]=";
+    for (int k = 0; k < world_; ++k) {
+      for (int q = 0; q < kSdmaMaxPieces; ++q) out += std::to_string(f[base + k * kSdmaMaxPieces + q]) + ",";
+      out += ";";
+    }
+  }
   return out;
 }
 
@@ -386,10 +460,9 @@ void SdmaComm::allreduce(const void* in, void* out, int64_t n, DType dt, hipStre
 }
 
 // The ranks of one process on one stream: for each segment every rank's copies are queued
-// first, then the stream releases every rank's phase 1, then runs every rank's wait + reduce
-// + phase-2 release, then every rank's wait + gather. Each wait only needs releases queued
-// before it on the same stream, so one stream carries all local ranks (a wait holding a
-// hardware queue never blocks a peer's release behind it).
+// first, then the stream releases every rank's phase 1, then ONE pipelined reduce launch for
+// every local rank (blockIdx.y) and ONE pipelined gather launch. Each wait inside them only
+// needs copies released before the launch, so one stream carries all local ranks.
 void SdmaComm::allreduce_local(const std::vector<SdmaComm*>& comms, const std::vector<const void*>& ins,
                                const std::vector<void*>& outs, int64_t n, DType dt, hipStream_t stream, float scale) {
   if (comms.empty() || ins.size() != comms.size() || outs.size() != comms.size())
@@ -398,8 +471,9 @@ void SdmaComm::allreduce_local(const std::vector<SdmaComm*>& comms, const std::v
   for (size_t y = 0; y < comms.size(); ++y) {
     const SdmaComm& c = *comms[y];
     if (!c.connected_) throw std::runtime_error("SdmaComm: connect() first");
-    if (c.device_ != c0.device_ || c.world_ != c0.world_ || c.slot_bytes_ != c0.slot_bytes_)
-      throw std::invalid_argument("SdmaComm: local ranks must share device, world and slot size");
+    if (c.device_ != c0.device_ || c.world_ != c0.world_ || c.slot_bytes_ != c0.slot_bytes_ ||
+        c.pieces_ != c0.pieces_ || c.grid_ != c0.grid_)
+      throw std::invalid_argument("SdmaComm: local ranks must share device, world, slot size, pieces and grid");
     if ((reinterpret_cast<uintptr_t>(ins[y]) | reinterpret_cast<uintptr_t>(outs[y])) & 15)
       throw std::invalid_argument("SdmaComm: buffers must be 16-byte aligned");
   }
@@ -407,6 +481,7 @@ void SdmaComm::allreduce_local(const std::vector<SdmaComm*>& comms, const std::v
   hip_check(hipSetDevice(c0.device_), "hipSetDevice");
   const int64_t es = static_cast<int64_t>(dtype_size(dt));
   const int64_t seg = c0.world_ * (c0.slot_bytes_ / es);
+  const int W = c0.world_;
   std::vector<Plan> plans(comms.size());
   for (int64_t off = 0; off < n; off += seg) {
     const int64_t len = std::min(seg, n - off);
@@ -417,8 +492,39 @@ void SdmaComm::allreduce_local(const std::vector<SdmaComm*>& comms, const std::v
     for (size_t y = 0; y < comms.size(); ++y)
       hipLaunchKernelGGL(sdma_release_kernel, dim3(1), dim3(64), 0, stream,
                          comms[y]->impl_->slots[plans[y].slot].start_p);
-    for (size_t y = 0; y < comms.size(); ++y) comms[y]->enqueue_reduce(plans[y], stream, scale);
-    for (size_t y = 0; y < comms.size(); ++y) comms[y]->enqueue_gather(plans[y], stream);
+    for (size_t y0 = 0; y0 < comms.size(); y0 += kSdmaMaxLocal) {
+      const size_t ny = std::min<size_t>(kSdmaMaxLocal, comms.size() - y0);
+      SdmaLaunch L{};
+      L.n = len;
+      L.block = plans[y0].block;
+      L.pe = plans[y0].pe;
+      L.K = plans[y0].K;
+      L.slot = c0.slot_bytes_;
+      L.W = W;
+      L.scale = scale;
+      L.timeout = static_cast<uint64_t>(c0.timeout_s_ * 1e8);
+      for (size_t i = 0; i < ny; ++i) {
+        SdmaComm& c = *comms[y0 + i];
+        const Plan& pl = plans[y0 + i];
+        SdmaRankArgs& a = L.y[i];
+        a.in = pl.in;
+        a.out = pl.out;
+        a.sd = c.slab_ + kFlagBytes + static_cast<int64_t>(pl.par) * W * c.slot_bytes_;
+        a.rd = c.slab_ + kFlagBytes + (2 + static_cast<int64_t>(pl.par)) * W * c.slot_bytes_;
+        a.flags = reinterpret_cast<const uint32_t*>(c.slab_);
+        for (int k = 0; k < kSdmaMaxPieces; ++k) a.mid[k] = c.impl_->slots[pl.slot].mid_p[k];
+        a.cnt = c.cnt_;
+        a.err = c.err_;
+        a.epoch = pl.epoch;
+        a.r = c.rank_;
+      }
+      dispatch_dtype(static_cast<int>(dt), [&](auto tag) {
+        using E = decltype(tag);
+        hipLaunchKernelGGL(sdma_reduce_kernel<E>, dim3(c0.grid_, ny), dim3(kCommThreads), 0, stream, L);
+        if (W > 1)  // one rank: the reduce wrote the whole (scaled) output
+          hipLaunchKernelGGL(sdma_gather_kernel<E>, dim3(c0.grid_, ny), dim3(kCommThreads), 0, stream, L);
+      });
+    }
     hip_check(hipGetLastError(), "sdma kernels");
   }
 }
@@ -441,7 +547,7 @@ SdmaComm::Plan SdmaComm::plan(const char* in, char* out, int64_t n, DType dt) {
   // the slot's previous call: every copy it submitted has completed (the host is at most
   // kSlots calls ahead of the engines; a peer that stopped turns into an error here)
   if (sl.used) {
-    for (hsa_signal_t x : {sl.sc, sl.scf, sl.gd, sl.gdf}) {
+    for (hsa_signal_t x : {sl.scf, sl.gdf}) {  // every part precedes a flag counted here
       if (hsa_signal_load_scacquire(x) == 0) continue;
       ++st_.host_waits;
       const uint64_t ns = static_cast<uint64_t>(timeout_s_ * 1e9);
@@ -452,34 +558,47 @@ SdmaComm::Plan SdmaComm::plan(const char* in, char* out, int64_t n, DType dt) {
   sl.used = true;
   pl.block = rup(cdiv(n, W), elems);
   const int64_t block = pl.block;
-  auto blen = [&](int j) { return hclamp(n - static_cast<int64_t>(j) * block, block); };
   if (block * es > slot_bytes_) throw std::logic_error("SdmaComm: segment exceeds the slot");
-  // split of one block over epp engines, 4 KiB aligned pieces
-  auto parts = [&](int64_t bytes, int p, int64_t* off, int64_t* len) {
-    const int64_t piece = rup(cdiv(bytes, epp_), 4096);
-    *off = std::min<int64_t>(bytes, p * piece);
-    *len = std::min<int64_t>(bytes - *off, piece);
+  auto blen = [&](int j) { return hclamp(n - static_cast<int64_t>(j) * block, block); };
+  // pipeline pieces: 4 KiB aligned, the same on every rank (they derive it from n and W alone)
+  const int want = pieces_ > 0 ? std::min(pieces_, kSdmaMaxPieces)
+                               : static_cast<int>(std::clamp<int64_t>(cdiv(block * es, kPieceBytes), 2, kSdmaMaxPieces));
+  pl.pe = rup(cdiv(block, want), std::max<int64_t>(elems, 4096 / es));
+  pl.K = static_cast<int>(std::max<int64_t>(1, cdiv(block, pl.pe)));
+  const int K = pl.K;
+  auto kn = [&](int j) { return static_cast<int>(cdiv(blen(j), pl.pe)); };  // pieces holding data
+  auto plen = [&](int j, int k) { return hclamp(blen(j) - static_cast<int64_t>(k) * pl.pe, pl.pe); };
+  // part p of a piece of `bytes` (over the epp engines), 4 KiB aligned
+  auto part = [&](int64_t bytes, int p, int64_t* off, int64_t* len) {
+    const int64_t sz = rup(cdiv(bytes, epp_), 4096);
+    *off = std::min<int64_t>(bytes, p * sz);
+    *len = std::min<int64_t>(bytes - *off, sz);
   };
-  int n1 = 0, n2 = 0;
-  for (int j = 0; j < W; ++j) {
-    if (j == r) continue;
+  auto nparts = [&](int j, int k) {
+    int c = 0;
     for (int p = 0; p < epp_; ++p) {
       int64_t o, l;
-      parts(blen(j) * es, p, &o, &l);
-      n1 += l > 0;
-      parts(blen(r) * es, p, &o, &l);
-      n2 += l > 0;
+      part(plen(j, k) * es, p, &o, &l);
+      c += l > 0;
     }
+    return c;
+  };
+  Impl::grow(sl.c1, static_cast<size_t>(W) * K);
+  Impl::grow(sl.c2, static_cast<size_t>(K));
+  for (int k = 0; k < K; ++k) {
+    for (int j = 0; j < W; ++j) hsa_signal_store_relaxed(sl.c1[static_cast<size_t>(j) * K + k], j == r ? 0 : nparts(j, k));
+    hsa_signal_store_relaxed(sl.c2[static_cast<size_t>(k)], (W - 1) * nparts(r, k));
   }
+  int nflag1 = 0;
+  for (int j = 0; j < W; ++j)
+    if (j != r) nflag1 += kn(j);
   uint32_t* word = m.words + static_cast<int64_t>(pl.slot) * 16;
   *word = pl.epoch;
   std::atomic_thread_fence(std::memory_order_seq_cst);
   hsa_signal_store_relaxed(sl.start, 1);
-  hsa_signal_store_relaxed(sl.mid, 1);
-  hsa_signal_store_relaxed(sl.sc, n1);
-  hsa_signal_store_relaxed(sl.scf, W - 1);
-  hsa_signal_store_relaxed(sl.gd, n2);
-  hsa_signal_store_relaxed(sl.gdf, W > 1 ? W : 0);  // W - 1 peer flags + the own "phase 2 sent" flag
+  for (int k = 0; k < kSdmaMaxPieces; ++k) hsa_signal_store_relaxed(sl.mid[k], 1);
+  hsa_signal_store_relaxed(sl.scf, nflag1);
+  hsa_signal_store_relaxed(sl.gdf, W > 1 ? W * kn(r) : 0);  // W - 1 peer flags + the own flag per piece
   const int64_t off_SD = kFlagBytes, off_RD = kFlagBytes + 2 * static_cast<int64_t>(W) * slot_bytes_;
   auto copy = [&](void* dst, hsa_agent_t da, const void* src, hsa_agent_t sa, int64_t bytes, int ndep,
                   const hsa_signal_t* deps, hsa_signal_t done, hsa_amd_sdma_engine_id_t eng) {
@@ -490,87 +609,57 @@ SdmaComm::Plan SdmaComm::plan(const char* in, char* out, int64_t n, DType dt) {
     st_.bytes += static_cast<uint64_t>(bytes);
   };
   const int par = pl.par;
-  // phase 1: block j -> rank j's SD[par][r], then its FS[r] flag
-  for (int j = 0; j < W; ++j) {
-    if (j == r) continue;
-    for (int p = 0; p < epp_; ++p) {
-      int64_t o, l;
-      parts(blen(j) * es, p, &o, &l);
-      if (l > 0)
-        copy(peers_[j] + off_SD + (static_cast<int64_t>(par) * W + r) * slot_bytes_ + o, m.peer_agent[j],
-             in + static_cast<int64_t>(j) * block * es + o, m.own, l, 1, &sl.start, sl.sc, m.peer_engines[j][p]);
+  // phase 1, piece by piece: piece k of block j -> rank j's SD[par][r], then its FS[r][k]
+  for (int k = 0; k < K; ++k)
+    for (int j = 0; j < W; ++j) {
+      if (j == r || k >= kn(j)) continue;
+      const hsa_signal_t done = sl.c1[static_cast<size_t>(j) * K + k];
+      int last = 0;
+      for (int p = 0; p < epp_; ++p) {
+        int64_t o, l;
+        part(plen(j, k) * es, p, &o, &l);
+        if (l <= 0) continue;
+        const int64_t at = static_cast<int64_t>(k) * pl.pe * es + o;
+        copy(peers_[j] + off_SD + (static_cast<int64_t>(par) * W + r) * slot_bytes_ + at, m.peer_agent[j],
+             in + static_cast<int64_t>(j) * block * es + at, m.own, l, 1, &sl.start, done, m.peer_engines[j][p]);
+        last = p;
+      }
+      copy(peers_[j] + (r * kSdmaMaxPieces + k) * 4, m.peer_agent[j], word, m.cpu, 4, 1, &done, sl.scf,
+           m.peer_engines[j][last]);
     }
-  }
-  const hsa_signal_t dep1[2] = {sl.start, sl.sc};
-  for (int j = 0; j < W; ++j)
-    if (j != r) copy(peers_[j] + r * 4, m.peer_agent[j], word, m.cpu, 4, 2, dep1, sl.scf, m.peer_engines[j][0]);
-  // phase 2: the reduced own block -> every peer's RD[par][r], then its FR[r] flag
-  for (int k = 0; k < W; ++k) {
-    if (k == r) continue;
-    for (int p = 0; p < epp_; ++p) {
-      int64_t o, l;
-      parts(blen(r) * es, p, &o, &l);
-      if (l > 0)
-        copy(peers_[k] + off_RD + (static_cast<int64_t>(par) * W + r) * slot_bytes_ + o, m.peer_agent[k],
-             out + static_cast<int64_t>(r) * block * es + o, m.own, l, 1, &sl.mid, sl.gd, m.peer_engines[k][p]);
+  // phase 2, piece by piece: reduced piece k of the own block -> every peer's RD[par][r], then
+  // its FR[r][k]; each part waits for mid[k] (released by the reduce kernel's last workgroup of
+  // the piece)
+  // (every part of the piece is queued before any of its flags: a flag waits in its engine's
+  // queue for ALL the piece's parts, so none of them may be queued behind it)
+  for (int k = 0; k < kn(r); ++k) {
+    const hsa_signal_t done = sl.c2[static_cast<size_t>(k)];
+    for (int q = 0; q < W; ++q) {
+      if (q == r) continue;
+      for (int p = 0; p < epp_; ++p) {
+        int64_t o, l;
+        part(plen(r, k) * es, p, &o, &l);
+        if (l <= 0) continue;
+        const int64_t at = static_cast<int64_t>(k) * pl.pe * es + o;
+        copy(peers_[q] + off_RD + (static_cast<int64_t>(par) * W + r) * slot_bytes_ + at, m.peer_agent[q],
+             out + static_cast<int64_t>(r) * block * es + at, m.own, l, 1, &sl.mid[k], done, m.peer_engines[q][p]);
+      }
     }
-  }
-  const hsa_signal_t dep2[2] = {sl.mid, sl.gd};
-  for (int k = 0; k < W; ++k)
-    if (k != r)
-      copy(peers_[k] + (kFrWord + r) * 4, m.peer_agent[k], word, m.cpu, 4, 2, dep2, sl.gdf, m.peer_engines[k][0]);
-  // and the own FR[r] word once every phase-2 copy has completed: the engines read the own
-  // block of `out` for them, so the call may not count as done (and the caller may not write
-  // `out`) before they are - enqueue_gather waits for this word with the peers' 
-  if (W > 1) {
-    const int k0 = (r + 1) % W;
-    copy(slab_ + (kFrWord + r) * 4, m.own, word, m.cpu, 4, 2, dep2, sl.gdf, m.peer_engines[k0][0]);
+    for (int q = 0; q < W; ++q)
+      if (q != r)
+        copy(peers_[q] + (kFrWord + r * kSdmaMaxPieces + k) * 4, m.peer_agent[q], word, m.cpu, 4, 1, &done, sl.gdf,
+             m.peer_engines[q][0]);
+    // and the own FR[r][k] once every phase-2 part of the piece has completed: the engines
+    // read the own block of `out` for them, so the call may not count as done (and the
+    // caller may not write `out`) before they are - the gather kernel waits for this word
+    // with the peers' 
+    if (W < 2) break;
+    const int q0 = (r + 1) % W;
+    copy(slab_ + (kFrWord + r * kSdmaMaxPieces + k) * 4, m.own, word, m.cpu, 4, 1, &done, sl.gdf,
+         m.peer_engines[q0][0]);
   }
   ++st_.calls;
   return pl;
-}
-
-// wait for every peer's phase-1 flag, reduce the own block, release phase 2
-void SdmaComm::enqueue_reduce(const Plan& pl, hipStream_t stream, float scale) {
-  const int W = world_, r = rank_;
-  const int64_t es = static_cast<int64_t>(dtype_size(pl.dt));
-  const int64_t elems = 16 / es;
-  const uint64_t ticks = static_cast<uint64_t>(timeout_s_ * 1e8);
-  hipLaunchKernelGGL(sdma_wait_kernel, dim3(1), dim3(64), 0, stream, reinterpret_cast<const uint32_t*>(slab_), W, r,
-                     pl.epoch, ticks, err_);
-  const int64_t rl = hclamp(pl.n - static_cast<int64_t>(r) * pl.block, pl.block);
-  const int64_t piece = std::max<int64_t>(elems, rup(cdiv(rl, grid_), elems));
-  const int g1 = static_cast<int>(std::max<int64_t>(1, cdiv(rl, piece)));
-  const char* sd = slab_ + kFlagBytes + static_cast<int64_t>(pl.par) * W * slot_bytes_;
-  if (rl > 0)
-    dispatch_dtype(static_cast<int>(pl.dt), [&](auto tag) {
-      using E = decltype(tag);
-      hipLaunchKernelGGL(sdma_reduce_kernel<E>, dim3(g1), dim3(kCommThreads), 0, stream,
-                         pl.in + static_cast<int64_t>(r) * pl.block * es, sd, slot_bytes_, W, r,
-                         pl.out + static_cast<int64_t>(r) * pl.block * es, rl, piece, scale);
-    });
-  hipLaunchKernelGGL(sdma_release_kernel, dim3(1), dim3(64), 0, stream, impl_->slots[pl.slot].mid_p);
-}
-
-// wait for every peer's reduced block, copy them into the output
-void SdmaComm::enqueue_gather(const Plan& pl, hipStream_t stream) {
-  const int W = world_, r = rank_;
-  const int64_t es = static_cast<int64_t>(dtype_size(pl.dt));
-  const int64_t elems = 16 / es;
-  const uint64_t ticks = static_cast<uint64_t>(timeout_s_ * 1e8);
-  // every peer's reduced block AND the own phase-2 copies (FR[r], written behind them)
-  hipLaunchKernelGGL(sdma_wait_kernel, dim3(1), dim3(64), 0, stream,
-                     reinterpret_cast<const uint32_t*>(slab_) + kFrWord, W, W > 1 ? -1 : r, pl.epoch, ticks, err_);
-  if (W < 2) return;
-  const int64_t gpiece = std::max<int64_t>(elems, rup(cdiv(pl.block, std::max(1, grid_ / (W - 1))), elems));
-  const int g2 = static_cast<int>(std::max<int64_t>(1, cdiv(pl.block, gpiece)));
-  const char* rd = slab_ + kFlagBytes + 2 * static_cast<int64_t>(W) * slot_bytes_ +
-                   static_cast<int64_t>(pl.par) * W * slot_bytes_;
-  dispatch_dtype(static_cast<int>(pl.dt), [&](auto tag) {
-    using E = decltype(tag);
-    hipLaunchKernelGGL(sdma_gather_kernel<E>, dim3(g2, W), dim3(kCommThreads), 0, stream, pl.out, rd, slot_bytes_, r,
-                       pl.n, pl.block, gpiece);
-  });
 }
 
 }  // namespace mxar

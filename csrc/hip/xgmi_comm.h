@@ -343,6 +343,12 @@ class XgmiComm {
   // Zero this rank's flags, LL slots and counters (recovery after CommError; collective use
   // only, with every rank idle - see XgmiCommunicator.reset).
   void reset_local();
+  // One-rank traffic rehearsal (benchmarks/sections.py dp_overlap): mark every flag word peers
+  // would write into THIS rank's slab as reached for the next 2^30 epochs, so this rank's
+  // two-shot runs alone - reading its input, pushing into the (local, never launched) peers'
+  // slots, reducing its own S slots and gathering its own R slots - and moves exactly one
+  // rank's HBM bytes of a real P-rank two-shot without waiting. Never for real collectives.
+  void arm_solo_rehearsal();
 
   int rank() const { return rank_; }
   int threshold_rows() const { return rows_ - 1; }

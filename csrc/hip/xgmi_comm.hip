@@ -868,6 +868,16 @@ void XgmiComm::reset_local() {
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
 }
 
+void XgmiComm::arm_solo_rehearsal() {
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  hip_check(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(slab_), 0x40000000u, static_cast<size_t>(off_S_ / 4)),
+            "hipMemsetD32(flags)");
+  // the synthetic peers' contributions in the S / R slots: zeros (the sums stay the input)
+  hip_check(hipMemset(slab_ + off_S_, 0, static_cast<size_t>(slab_bytes_ - off_S_)), "hipMemset(slots)");
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+}
+
 template <class E>
 static void launch_typed(const CommArgs& a, dim3 grid, hipStream_t s, Algo kind) {
   const dim3 b(kCommThreads);
@@ -1377,11 +1387,14 @@ bool XgmiComm::threshold_args(const std::vector<XgmiComm*>& group, const std::ve
                  (a.block * es) % 4 == 0 && (a.chunk * es) % 4 == 0 && 2 * round_up(nbytes, 8) <= c0.slot_bytes_)
                     ? 1
                     : 0;
-    // one chunk per workgroup: the body reduces every chunk of the round (P x nch), and a
-    // workgroup with two of them polls and sums them one after the other
+    // the body reduces every chunk of the round (P x nch): as many chunks per workgroup as fit
+    // its fast pass (one 8-B unit per thread, xgmi_threshold.hip), so the fewest workgroups
+    // start (their start skew is on the round's critical path) and none walks chunks serially
     if (a.oneshot) {
       const int cap = ranks_here > 1 ? std::max(1, c0.shared_launch_cap(ranks_here)) : c0.grid_;
-      gx = std::max(gx, static_cast<int>(std::min<int64_t>(cap, static_cast<int64_t>(W) * a.nch)));
+      const int64_t upc = ceil_div(a.chunk * es, 8) + 1;  // units of one chunk at most
+      const int64_t cpw = std::max<int64_t>(1, kCommThreads / upc);
+      gx = static_cast<int>(std::min<int64_t>(cap, ceil_div(static_cast<int64_t>(W) * a.nch, cpw)));
     }
   }
   a.counts = counts;

@@ -594,17 +594,26 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
   // the previous epoch's rounds are abandoned before the arena is laid out again (their
   // results would be dropped as an older epoch; a round still at its lag gate must not
   // wait for a peer that left the membership)
+  struct StageReset {
+    std::atomic<int>& s;
+    ~StageReset() { s.store(0); }
+  } stage_reset{cfg_stage_};
   if (configured_) {
+    cfg_stage_.store(1);
     abort(last_round_);
+    cfg_stage_.store(2);
     drain();
   }
+  cfg_stage_.store(3);
   leave_group();
   if (orphaned_) {
     configured_ = false;
     throw ProtocolError("xgmi plane: the group kernel never released this worker (its STOP was not taken); "
                         "the plane cannot be configured again");
   }
+  cfg_stage_.store(4);
   park_resident();  // the stream work below must not queue behind it
+  cfg_stage_.store(5);
   rplan_tried_ = false;
   rplan_ = XgmiComm::ResidentPlan();
   res_token_.reset();
@@ -632,6 +641,7 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
     if (it == cfg.descriptors.end() || it->second.empty()) throw ProtocolError("InitWorkers.planes misses worker " + std::to_string(k));
     bases[k] = k == cfg.id ? arena_ : map_peer(it->second);
   }
+  cfg_stage_.store(6);
   comm_.reset();
   // No device-synchronising call from here on: a peer's round kernel of the new epoch may
   // already spin waiting for this worker (its lag gate opens on the progress published
@@ -666,6 +676,7 @@ void XgmiRoundPlane::configure(const PlaneConfig& cfg) {
   configured_ = true;
   last_round_ = cfg.startRound - 1;
   err_seen_ = 0;
+  cfg_stage_.store(7);
   if (grouped_) join_group(cfg);
   MXAR_LOG(INFO, "plane", "xgmi plane: worker " << cfg.id << " of " << P << ", block " << block_ << ", chunk "
                                                 << chunk_ << " x " << nch_ << " (" << nch_ref_
@@ -940,7 +951,8 @@ void XgmiRoundPlane::launch_group(int round, const Payload& input, bool cold) {
 std::string XgmiRoundPlane::debug_state() const {
   std::ostringstream os;
   os << "{\"res_seq\":" << res_seq_ << ",\"consumed\":" << rstate_[1] << ",\"solo_state\":" << rstate_[0]
-     << ",\"res_on\":" << (res_on_ ? 1 : 0) << ",\"last_round\":" << last_round_ << ",\"queued\":" << q_len_.load();
+     << ",\"res_on\":" << (res_on_ ? 1 : 0) << ",\"last_round\":" << last_round_ << ",\"queued\":" << q_len_.load()
+     << ",\"configure_stage\":" << cfg_stage_.load();
   if (res_seq_ > 1) {
     const ResidentDoor* d = door_ + (res_seq_ - 1u) % kResidentDoors;
     os << ",\"door_last\":{\"seq\":" << d->seq << ",\"cmd\":" << d->cmd << ",\"epoch\":" << d->epoch << "}";

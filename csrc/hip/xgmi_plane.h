@@ -196,6 +196,10 @@ class XgmiRoundPlane final : public RoundPlane {
   // the group kernel never took this worker's STOP: its round memory went to the group
   // (PlaneGroup::orphans) and the plane can run no further round
   bool orphaned_ = false;
+  // where configure() is (debug_state): 0 idle, 1 abandoning the old epoch's rounds, 2 draining
+  // them, 3 leaving the old group, 4 parking a solo kernel, 5 mapping peers, 6 the new
+  // communicator and published progress, 7 joining the new group
+  std::atomic<int> cfg_stage_{0};
   std::shared_ptr<PlaneGroup> group_;
   int gidx_ = -1;                      // this worker's index in the group
   XgmiComm::ResidentPlan gplan_;       // the group kernel's geometry for this membership

@@ -791,7 +791,107 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     const __amdgpu_buffer_rsrc_t ro = slab_rsrc(out);
     __shared__ uint32_t sh_miss;
     const int nq = P * a.nch;
-    for (int q = blockIdx.x; q < nq; q += G) {
+    auto chunk_span = [&](int q, int64_t* b0, int64_t* b1) -> bool {  // bytes of chunk q (false: none)
+      const int j = q / a.nch;
+      const int c = q - j * a.nch;
+      const int64_t blen = clamp_len(a.n - static_cast<int64_t>(j) * a.block, a.block);
+      const int64_t clen = clamp_len(blen - static_cast<int64_t>(c) * a.chunk, a.chunk);
+      *b0 = (static_cast<int64_t>(j) * a.block + static_cast<int64_t>(c) * a.chunk) * es;
+      *b1 = *b0 + clen * es;
+      return clen > 0;
+    };
+    auto poll_unit = [&](int64_t u, bool act, bool h0, bool h1, Pack16* v, bool& stop) -> uint32_t {
+      uint32_t want = 0;  // sources whose words of this unit are not in yet
+#pragma unroll
+      for (int s = 0; s < kMaxRanks; ++s) {
+        if (s < P && s != r && act) {
+          v[s] = __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc(mine_s + static_cast<int64_t>(s) * slot),
+                                                        static_cast<int>(u * 16), 0, kAuxSysLd);
+          want |= 1u << s;
+        }
+      }
+      auto in_now = [&](const Pack16& w) { return (!h0 || w[1] == tag) && (!h1 || w[3] == tag); };
+#pragma unroll
+      for (int s = 0; s < kMaxRanks; ++s)
+        if (((want >> s) & 1u) && in_now(v[s])) want &= ~(1u << s);
+      const uint64_t tw = ps.now();
+      while (__any(want != 0) && !stop) {
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int s = 0; s < kMaxRanks; ++s) {
+          if ((want >> s) & 1u) {
+            v[s] = __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc(mine_s + static_cast<int64_t>(s) * slot),
+                                                          static_cast<int>(u * 16), 0, kAuxSysLd);
+            if (in_now(v[s])) want &= ~(1u << s);
+          }
+        }
+        const uint64_t now = wall_ticks();
+        const bool host = hp.due(now);
+        if ((host || sp.due(now)) && wave_forced(a, rv.hforce, rv.habort, r, epoch, host)) stop = true;
+        if (now > deadline) {
+          if ((threadIdx.x & 63) == 0)
+            __hip_atomic_fetch_or(err, ERR_TIMEOUT_SCATTER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          stop = true;
+        }
+      }
+      ps.add(2, tw);
+      return want;
+    };
+    auto sum_unit = [&](int64_t u, bool h0, bool h1, const Pack16* v) {  // every source in, rank order
+      Acc8<E> acc;
+#pragma unroll
+      for (int s = 0; s < kMaxRanks; ++s) {
+        if (s >= P) continue;
+        acc.add(s == r ? load_unit8(in, u, nbytes) : make_uint2(v[s][0], v[s][2]));
+      }
+      const uint2 o = acc.pack(a.scale);
+      if (h0 && h1)
+        __builtin_amdgcn_raw_buffer_store_b64(U32x2{o.x, o.y}, ro, static_cast<int>(u * 8), 0, kAuxWt);
+      else if (h0)
+        __builtin_amdgcn_raw_buffer_store_b32(o.x, ro, static_cast<int>(u * 8), 0, kAuxWt);
+      else if (h1)
+        __builtin_amdgcn_raw_buffer_store_b32(o.y, ro, static_cast<int>(u * 8 + 4), 0, kAuxWt);
+    };
+    // Fast pass: every unit of every chunk this workgroup owns at once, one per thread (the host
+    // sizes the grid for it), all sources' loads in flight together - one load round trip after
+    // the data lands, where a chunk-by-chunk walk pays one per chunk. It completes when every
+    // word of every source arrives (the common case at full thresholds); a forced / cold /
+    // void / timed-out pass falls through to the chunk-by-chunk body (arrival within a round is
+    // final: it reads the slots again and reduces what arrived).
+    bool done_fast = false;
+    if (!cold && !void_round) {
+      int64_t tot = 0, my_u = -1, my_b0 = 0, my_b1 = 0;
+      for (int q = blockIdx.x; q < nq; q += G) {
+        int64_t b0, b1;
+        if (!chunk_span(q, &b0, &b1)) continue;
+        const int64_t u0 = b0 / 8, u1 = (b1 + 7) / 8;
+        const int64_t t = static_cast<int64_t>(threadIdx.x) - tot;
+        if (t >= 0 && t < u1 - u0) {
+          my_u = u0 + t;
+          my_b0 = b0;
+          my_b1 = b1;
+        }
+        tot += u1 - u0;
+      }
+      if (tot <= kCommThreads) {  // uniform
+        const bool act = my_u >= 0;
+        const bool h0 = act && my_u * 8 >= my_b0 && my_u * 8 < my_b1;
+        const bool h1 = act && my_u * 8 + 4 >= my_b0 && my_u * 8 + 4 < my_b1;
+        Pack16 v[kMaxRanks];
+        bool stop = false;
+        const uint32_t want = poll_unit(my_u, act, h0, h1, v, stop);
+        if (__syncthreads_or(want != 0u) == 0) {
+          if (act) sum_unit(my_u, h0, h1, v);
+          if (counts)
+            for (int q = blockIdx.x + static_cast<int>(threadIdx.x) * G; q < nq; q += G * kCommThreads) {
+              int64_t b0, b1;
+              cput(static_cast<int64_t>(q), chunk_span(q, &b0, &b1) ? P : 0);
+            }
+          done_fast = true;
+        }
+      }
+    }
+    for (int q = blockIdx.x; q < nq && !done_fast; q += G) {
       const int j = q / a.nch;
       const int c = q - j * a.nch;
       const int64_t blen = clamp_len(a.n - static_cast<int64_t>(j) * a.block, a.block);
@@ -814,56 +914,9 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         const bool h0 = act && u * 8 >= b0 && u * 8 < b1;          // low word in this chunk
         const bool h1 = act && u * 8 + 4 >= b0 && u * 8 + 4 < b1;  // high word in this chunk
         Pack16 v[kMaxRanks];
-        uint32_t want = 0;  // sources whose words of this unit are not in yet
-#pragma unroll
-        for (int s = 0; s < kMaxRanks; ++s) {
-          if (s < P && s != r && act) {
-            v[s] = __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc(mine_s + static_cast<int64_t>(s) * slot),
-                                                          static_cast<int>(u * 16), 0, kAuxSysLd);
-            want |= 1u << s;
-          }
-        }
-        auto in_now = [&](const Pack16& w) { return (!h0 || w[1] == tag) && (!h1 || w[3] == tag); };
-#pragma unroll
-        for (int s = 0; s < kMaxRanks; ++s)
-          if (((want >> s) & 1u) && in_now(v[s])) want &= ~(1u << s);
-        const uint64_t tw = ps.now();
-        while (__any(want != 0) && !stop) {
-          __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-          for (int s = 0; s < kMaxRanks; ++s) {
-            if ((want >> s) & 1u) {
-              v[s] = __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc(mine_s + static_cast<int64_t>(s) * slot),
-                                                            static_cast<int>(u * 16), 0, kAuxSysLd);
-              if (in_now(v[s])) want &= ~(1u << s);
-            }
-          }
-          const uint64_t now = wall_ticks();
-          const bool host = hp.due(now);
-          if ((host || sp.due(now)) && wave_forced(a, rv.hforce, rv.habort, r, epoch, host)) stop = true;
-          if (now > deadline) {
-            if ((threadIdx.x & 63) == 0)
-              __hip_atomic_fetch_or(err, ERR_TIMEOUT_SCATTER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            stop = true;
-          }
-        }
-        ps.add(2, tw);
+        const uint32_t want = poll_unit(u, act, h0, h1, v, stop);
         miss |= want;
-        if (act && want == 0u && !cold) {  // every source in: the sum, in rank order
-          Acc8<E> acc;
-#pragma unroll
-          for (int s = 0; s < kMaxRanks; ++s) {
-            if (s >= P) continue;
-            acc.add(s == r ? load_unit8(in, u, nbytes) : make_uint2(v[s][0], v[s][2]));
-          }
-          const uint2 o = acc.pack(a.scale);
-          if (h0 && h1)
-            __builtin_amdgcn_raw_buffer_store_b64(U32x2{o.x, o.y}, ro, static_cast<int>(u * 8), 0, kAuxWt);
-          else if (h0)
-            __builtin_amdgcn_raw_buffer_store_b32(o.x, ro, static_cast<int>(u * 8), 0, kAuxWt);
-          else if (h1)
-            __builtin_amdgcn_raw_buffer_store_b32(o.y, ro, static_cast<int>(u * 8 + 4), 0, kAuxWt);
-        }
+        if (act && want == 0u && !cold) sum_unit(u, h0, h1, v);
       }
       // the common case (every word of every source in) costs one barrier-with-reduction; only
       // a forced / cold / timed-out chunk gathers which sources it misses

@@ -18,6 +18,17 @@ os.environ.setdefault("MXAR_LOGLEVEL", "ERROR")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device); run via gpurun")
     config.addinivalue_line("markers", "slow: multi-process or long-running test")
+    # a native crash prints its C++ frames before Python's faulthandler dump (no debugger on
+    # the GPU boxes)
+    try:
+        import faulthandler
+
+        faulthandler.enable()
+        from akka_allreduce_1_amd._native import C as _C
+
+        _C.install_native_backtrace()
+    except Exception:  # noqa: BLE001 - a diagnostic only
+        pass
 
 
 def gpu_available() -> bool:

@@ -67,13 +67,12 @@ def test_oneshot_forced_rounds_sum_what_arrived():
 
     P, n, chunk, rounds = 3, 3000, 500, 8
     bufs = [torch.full((n,), float(1 << k), device=DEV) for k in range(P)]
-    srcs = [C.hip.tensor_source(b) for b in bufs]
-    base = srcs[2]
+    srcs = [lambda req, b=b: b for b in bufs]  # Python sources: the stall below is one too
 
     def stall(req):
         if req.iteration == 0:
             time.sleep(1.5)
-        return base(req)
+        return bufs[2]
 
     srcs[2] = stall
     job = PlaneJob(P, n, max_chunk_size=chunk, th_reduce=1.0, th_complete=1.0, max_lag=1, max_round=rounds - 1,

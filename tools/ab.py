@@ -166,14 +166,20 @@ def exp_sdma(a) -> None:
     for rep in range(a.reps):
         for g in [int(x) for x in a.grids.split(",")]:
             cl = LocalSdmaCluster(P, slot_bytes=-(-nbytes // P) + (1 << 20), grid=g, timeout_s=20.0)
-            cl.allreduce(xs, ys)
-            torch.cuda.synchronize(dev)
-            cl.check()
-            ok, err, _ = rounding_check(ys, ref, dtype, P)
-            p50 = percentile(device_times(lambda: cl.allreduce(xs, ys), a.iters, dev), 50)
-            cl.check()
-            _emit({"exp": "sdma", "tag": a.tag, "rep": rep, "P": P, "mib": a.mib, "grid": g, "validated": ok,
-                   "max_abs_err": err, "p50_ms": round(p50, 4), "algbw_GBps": round(nbytes / (p50 / 1e3) / 1e9, 1)})
+            for k in [int(x) for x in a.pieces.split(",")]:
+                for c in cl.comms:
+                    c.pieces = k
+                for y in ys:
+                    y.fill_(float("nan"))
+                cl.allreduce(xs, ys)
+                torch.cuda.synchronize(dev)
+                cl.check()
+                ok, err, _ = rounding_check(ys, ref, dtype, P)
+                p50 = percentile(device_times(lambda: cl.allreduce(xs, ys), a.iters, dev), 50)
+                cl.check()
+                _emit({"exp": "sdma", "tag": a.tag, "rep": rep, "P": P, "mib": a.mib, "grid": g, "pieces": k,
+                       "validated": ok, "max_abs_err": err, "p50_ms": round(p50, 4),
+                       "algbw_GBps": round(nbytes / (p50 / 1e3) / 1e9, 1)})
             del cl
             torch.cuda.empty_cache()
 
@@ -265,6 +271,7 @@ def main() -> None:
     p.add_argument("--P", type=int, default=2)
     p.add_argument("--mib", type=int, default=256)
     p.add_argument("--grids", default="32,128,256,512")
+    p.add_argument("--pieces", default="0", help="pipeline pieces per block (0 = by size)")
     p.add_argument("--reps", type=int, default=2)
     p.add_argument("--iters", type=int, default=10)
     p = sub.add_parser("grid")

@@ -74,6 +74,8 @@ def main():
     ap.add_argument("--mib", type=int, default=256)
     ap.add_argument("--P", type=int, default=8)
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--placement-tries", type=int, default=1,
+                    help="LocalCluster placement_tries: slab placements timed at construction (fastest kept)")
     ap.add_argument("--staggers", default="0",
                     help="comma list of byte offsets: rank k's input / output start k x offset past a "
                          "multiple of the buffer size inside one allocation (each row tries every one)")
@@ -101,7 +103,8 @@ def main():
         cms, cmhz = times(cp, a.iters, dev, probe)
         del x, y
         if k == 0 or a.vary != "io":
-            cl = LocalCluster(P, slot_bytes=2 * -(-S // P) + (1 << 20), grid=512, timeout_s=10.0)
+            cl = LocalCluster(P, slot_bytes=2 * -(-S // P) + (1 << 20), grid=512, timeout_s=10.0,
+                              placement_tries=a.placement_tries, placement_bytes=S)
         staggers = [int(v) for v in a.staggers.split(",")]
         for stg in staggers:
             if k == 0 or a.vary != "slabs" or len(staggers) > 1:
@@ -136,7 +139,7 @@ def main():
                               "copy_TBps": round(copy_tbps, 3), "copy_core_MHz": cmhz,
                               "twoshot_ms": [round(pct(tms, 10), 4), round(t50, 4), round(pct(tms, 90), 4)],
                               "twoshot_TBps": round(tbps, 3), "frac_copy": round(tbps / copy_tbps, 3),
-                              "twoshot_core_MHz": tmhz}), flush=True)
+                              "twoshot_core_MHz": tmhz, "placement": cl.placement}), flush=True)
         if a.vary == "both":
             del cl, xs, ys
             cl = xs = ys = None
