@@ -44,7 +44,7 @@ class SdmaCommunicator:
     accepts_stream = True
 
     def __init__(self, group=None, *, device: torch.device | int | None = None, slot_bytes: int = 64 << 20,
-                 grid: int = 32, engines_per_peer: int = 0, timeout_s: float = 20.0, cpu_group=None,
+                 grid: int = 128, engines_per_peer: int = 0, timeout_s: float = 20.0, cpu_group=None,
                  validate: bool = True):
         """validate: one small allreduce checked against the exact sum on every rank before the
         communicator is handed out (collective; a wrong result raises CommError everywhere)."""
@@ -155,7 +155,7 @@ class LocalSdmaCluster:
     stream in one interleaved schedule (SdmaComm::allreduce_local): every wait only needs
     releases queued before it, so no rank's wait can hold up a peer's progress."""
 
-    def __init__(self, world: int, *, slot_bytes: int = 16 << 20, grid: int = 32, engines_per_peer: int = 0,
+    def __init__(self, world: int, *, slot_bytes: int = 16 << 20, grid: int = 128, engines_per_peer: int = 0,
                  timeout_s: float = 10.0, device: int | None = None):
         dev = torch.cuda.current_device() if device is None else device
         self.world = world

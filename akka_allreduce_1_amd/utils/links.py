@@ -11,6 +11,11 @@ GPU at once. The probes (csrc/hip/xgmi_probe.hip) use the two-shot's exact store
                    d = k - r (a permutation: each GPU sends on one link and receives on one);
   all_GBps[r]      rank r pushing the same bytes into all peers at once (the fan-out);
   fanout_ratio     all_GBps / mean single-peer rate (7 links ideal: 7.0);
+  coarse / pull    the same single-peer and all-peer rates for two other paths a two-shot
+                   could take: plain stores into the peer's COARSE-grained memory with one
+                   system release per workgroup (`coarse`), and remote LOADS of the peer's
+                   fine-grained slab (`pull`) - which store path and memory kind the links
+                   serve best is then read off the first 8-GPU run;
   flag_us[k]       one-way flag hand-off rank 0 <-> k, bare (relaxed store + poll) and with
                    the kernels' release / acquire fences.
 
@@ -41,35 +46,48 @@ def probe_links(comm, nbytes: int = 64 << 20, reps: int = 5, iters: int = 2000, 
     g = grid or 64
     src = torch.empty(nbytes // 2, dtype=torch.bfloat16, device=dev).uniform_(-1, 1)
     stream = torch.cuda.current_stream(dev)
-    out: dict = {"bytes": nbytes, "reps": reps, "grid_per_peer": g, "store": "st16_wt (two-shot scatter path)"}
+    out: dict = {"bytes": nbytes, "reps": reps, "grid_per_peer": g, "store": "st16_wt (two-shot scatter path)",
+                 "coarse_store": "plain st16 + system release per workgroup", "pull_load": "remote system-coherent ld16"}
 
-    def timed_push(mask: int) -> float:
-        c.probe_push(src.data_ptr(), nbytes, mask, g, stream.cuda_stream)  # warm-up
+    def timed_push(mask: int, mode: int = 0) -> float:
+        c.probe_push(src.data_ptr(), nbytes, mask, g, stream.cuda_stream, mode)  # warm-up
         _barrier(comm)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(reps):
-            c.probe_push(src.data_ptr(), nbytes, mask, g, stream.cuda_stream)
+            c.probe_push(src.data_ptr(), nbytes, mask, g, stream.cuda_stream, mode)
         e1.record(stream)
         torch.cuda.synchronize(dev)
         return e0.elapsed_time(e1) / 1e3 / reps  # s per launch
 
-    # one peer at a time, every rank with the same shift d: rates[d] = this rank -> (r + d) % P
-    mine = [0.0] * P
-    for d in range(1, P):
-        k = (r + d) % P
-        s = timed_push(1 << k)
-        mine[k] = round(nbytes / s / 1e9, 2)
-    s = timed_push(((1 << P) - 1) & ~(1 << r))
-    all_rate = round((P - 1) * nbytes / s / 1e9, 2)
-    rows: list = [None] * P
-    dist.all_gather_object(rows, (mine, all_rate), group=comm.cpu_group)
+    def rates(mode: int):
+        # one peer at a time, every rank with the same shift d: mine[k] = this rank <-> (r + d) % P
+        mine = [0.0] * P
+        for d in range(1, P):
+            k = (r + d) % P
+            mine[k] = round(nbytes / timed_push(1 << k, mode) / 1e9, 2)
+        all_rate = round((P - 1) * nbytes / timed_push(((1 << P) - 1) & ~(1 << r), mode) / 1e9, 2)
+        rows: list = [None] * P
+        dist.all_gather_object(rows, (mine, all_rate), group=comm.cpu_group)
+        singles = [v for i, row in enumerate(rows) for k, v in enumerate(row[0]) if k != i]
+        return rows, singles
+
+    rows, singles = rates(0)
     out["push_GBps"] = [row[0] for row in rows]
     out["all_GBps"] = [row[1] for row in rows]
-    singles = [v for i, row in enumerate(rows) for k, v in enumerate(row[0]) if k != i]
     mean_single = sum(singles) / len(singles) if singles else 0.0
     out["single_GBps_min_med_max"] = [min(singles), sorted(singles)[len(singles) // 2], max(singles)]
     out["fanout_ratio"] = round(min(out["all_GBps"]) / mean_single, 2) if mean_single else None
+    # the coarse-grained push and the pull: [single-peer min, median, max], [all-peer min, max]
+    handles: list = [None] * P
+    dist.all_gather_object(handles, c.probe_coarse_handle(), group=comm.cpu_group)
+    c.probe_coarse_connect(handles)
+    _barrier(comm)
+    for mode, key in ((1, "coarse"), (2, "pull")):
+        rows_m, singles_m = rates(mode)
+        alls = [row[1] for row in rows_m]
+        out[key] = {"single_GBps_min_med_max": [min(singles_m), sorted(singles_m)[len(singles_m) // 2], max(singles_m)],
+                    "all_GBps_min_max": [min(alls), max(alls)]}
 
     # flag hand-off rank 0 <-> k (others idle between barriers)
     # (the token nonce is the same on both sides: a per-communicator call count, so a word

@@ -410,7 +410,7 @@ def sdma_local(dev, dtype: torch.dtype = torch.bfloat16, nbytes: int = 256 << 20
         row: dict = {}
         cl = xs = ys = None
         try:
-            cl = LocalSdmaCluster(P, slot_bytes=-(-nbytes // P) + (1 << 20), grid=512, timeout_s=20.0)
+            cl = LocalSdmaCluster(P, slot_bytes=-(-nbytes // P) + (1 << 20), grid=128, timeout_s=20.0)
             xs = [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=900 + k) for k in range(P)]
             ys = [torch.empty_like(x) for x in xs]
             ref = torch.zeros(n, device=dev)

@@ -23,7 +23,8 @@ side file (`detail`), and the line holds the headline fields plus compact summar
   xgmi_links     N > 1: the bring-up pack (akka_allreduce_1_amd/utils/links.py) - single-peer
                  push GB/s [min, median, max], all-peer push GB/s per rank [min, max], fan-out
                  ratio (all-peer / single-peer, 7 links ideal = 7), one-way flag hand-off us
-                 [bare min, bare max, fenced max]; never dropped before the headline sections
+                 [bare min, bare max, fenced max], coarse-grained push and pull [single-peer
+                 median, all-peer min] GB/s; never dropped before the headline sections
 
 `line()` guarantees the encoded line stays under LINE_BUDGET bytes: if a summary section
 still overflows (e.g. a future section grows), sections are dropped in a fixed order and
@@ -171,7 +172,10 @@ def _links(x: dict) -> dict:
     return {"single_GBps": x.get("single_GBps_min_med_max"),
             "all_GBps": [min(allr), max(allr)] if allr else None,
             "ratio": x.get("fanout_ratio"),
-            "flag_us": [min(bare) if bare else None, max(bare) if bare else None, max(fen) if fen else None]}
+            "flag_us": [min(bare) if bare else None, max(bare) if bare else None, max(fen) if fen else None],
+            # the coarse-grained push and the pull: [single median, all-peer min]
+            **{k: [x[k]["single_GBps_min_med_max"][1], x[k]["all_GBps_min_max"][0]]
+               for k in ("coarse", "pull") if isinstance(x.get(k), dict)}}
 
 
 def compact(result: dict, detail_path: str | None = None) -> dict:

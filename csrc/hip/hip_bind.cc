@@ -387,7 +387,7 @@ void bind_hip(py::module_& m) {
       .def("debug_state", &SdmaComm::debug_state)
       .def_property("grid", &SdmaComm::grid, &SdmaComm::set_grid)
       .def_property("pieces", &SdmaComm::pieces, &SdmaComm::set_pieces,
-                    "pipeline pieces per block (0 = one per 8 MiB of the block, 2..8)")
+                    "pipeline pieces per block (0 = one per 64 MiB of the block, 2..8)")
       .def_property_readonly("engines", &SdmaComm::engines)
       .def_property_readonly("engines_per_peer", &SdmaComm::engines_per_peer)
       .def_property_readonly("slot_bytes", &SdmaComm::slot_bytes)
@@ -537,12 +537,20 @@ void bind_hip(py::module_& m) {
       .def_property_readonly("probe_max_bytes", &XgmiComm::probe_max_bytes)
       .def(
           "probe_push",
-          [](XgmiComm& c, uintptr_t src, int64_t bytes, uint32_t mask, int grid, uintptr_t stream) {
+          [](XgmiComm& c, uintptr_t src, int64_t bytes, uint32_t mask, int grid, uintptr_t stream, int mode) {
             py::gil_scoped_release r;
-            c.probe_push(as_cptr(src), bytes, mask, grid, as_stream(stream));
+            c.probe_push(as_cptr(src), bytes, mask, grid, as_stream(stream), mode);
           },
           py::arg("src"), py::arg("bytes"), py::arg("peer_mask"), py::arg("grid"), py::arg("stream") = 0,
-          "bring-up probe: write-through push into the S slot of every peer in peer_mask (no flags)")
+          py::arg("mode") = 0,
+          "bring-up probe (no flags), every peer in peer_mask: mode 0 write-through push into its S slot, 1 plain "
+          "stores into its coarse-grained probe buffer + a system release, 2 pull (remote loads of its S slot)")
+      .def("probe_coarse_handle", [](XgmiComm& c) { return py::bytes(c.probe_coarse_handle()); })
+      .def("probe_coarse_connect", [](XgmiComm& c, const std::vector<py::bytes>& hs) {
+        std::vector<std::string> v;
+        for (auto& b : hs) v.emplace_back(static_cast<std::string>(b));
+        c.probe_coarse_connect(v);
+      })
       .def(
           "probe_pingpong",
           [](XgmiComm& c, int peer, int iters, uint32_t nonce, bool fenced, uintptr_t out, uintptr_t stream) {

@@ -78,7 +78,8 @@ class SdmaComm {
   int world() const { return world_; }
   int grid() const { return grid_; }
   void set_grid(int g) { grid_ = g > 0 ? g : 1; }
-  // pipeline pieces per block (0 = by size: one per 8 MiB of the block, 2..kSdmaMaxPieces)
+  // pipeline pieces per block (0 = by size: one per 64 MiB of the block, 2..kSdmaMaxPieces;
+  // profiles/round6/sdma_pipe_*.jsonl: 2 pieces at 32-128 MiB blocks, grid 128)
   int pieces() const { return pieces_; }
   void set_pieces(int k) { pieces_ = k < 0 ? 0 : k; }
   int engines() const { return static_cast<int>(local_engines_.size()); }

@@ -8,6 +8,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <map>
+#include <mutex>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -23,7 +25,7 @@ constexpr int kSlots = 16;              // calls in flight at most (signal / epo
 constexpr int64_t kFlagBytes = 64 * 1024;
 // flag words: FS[s][k] at s * kSdmaMaxPieces + k, FR[s][k] at kFrWord + s * kSdmaMaxPieces + k
 constexpr int kFrWord = 32 * kSdmaMaxPieces;
-constexpr int64_t kPieceBytes = int64_t{8} << 20;  // auto pieces: one per 8 MiB of the block
+constexpr int64_t kPieceBytes = int64_t{64} << 20;  // auto pieces: one per 64 MiB of the block (2..8)
 
 void hsa_check(hsa_status_t s, const char* what) {
   if (s != HSA_STATUS_SUCCESS) {
@@ -64,6 +66,27 @@ hsa_status_t agent_cb(hsa_agent_t a, void* data) {
   const uint64_t loc = (static_cast<uint64_t>(dom) << 32) | (bdf & ~0x7u);
   if (loc == s->want) s->found = a;
   return HSA_STATUS_SUCCESS;
+}
+
+// The engines towards `dst` from `src`, first answer per (dst, src) kept for the process.
+uint32_t cached_engine_status(hsa_agent_t dst, hsa_agent_t src) {
+  static std::mutex mu;
+  static std::map<std::pair<uint64_t, uint64_t>, uint32_t> seen;
+  std::lock_guard<std::mutex> g(mu);
+  const auto key = std::make_pair(dst.handle, src.handle);
+  auto it = seen.find(key);
+  if (it != seen.end()) return it->second;
+  uint32_t m = 0;
+  if (hsa_amd_memory_copy_engine_status(dst, src, &m) != HSA_STATUS_SUCCESS) m = 0;
+  seen[key] = m;
+  return m;
+}
+
+uint32_t engine_mask(int device, hsa_agent_t own, hsa_agent_t cpu) {
+  (void)device;
+  uint32_t mask = cached_engine_status(own, own);
+  if (mask == 0 && cpu.handle != 0) mask = cached_engine_status(own, cpu) | cached_engine_status(cpu, own);
+  return mask;
 }
 
 }  // namespace
@@ -267,15 +290,11 @@ SdmaComm::SdmaComm(int rank, int world, int device, int64_t slot_bytes, int grid
   impl_->cpu = s.cpu;
   // The device's SDMA engines. The ROCm 7.0 runtime torch ships answers the same-agent query
   // with HSA_STATUS_ERROR_INVALID_AGENT (7.2 answers it); the host <-> device directions name
-  // the same engines there.
-  uint32_t mask = 0, m2 = 0;
-  if (hsa_amd_memory_copy_engine_status(impl_->own, impl_->own, &mask) != HSA_STATUS_SUCCESS) {
-    mask = 0;
-    if (impl_->cpu.handle != 0) {
-      if (hsa_amd_memory_copy_engine_status(impl_->own, impl_->cpu, &m2) == HSA_STATUS_SUCCESS) mask |= m2;
-      if (hsa_amd_memory_copy_engine_status(impl_->cpu, impl_->own, &m2) == HSA_STATUS_SUCCESS) mask |= m2;
-    }
-  }
+  // the same engines there. The query reports the engines FREE at the time: engines whose
+  // queues an earlier communicator of this process opened drop out of it (a second
+  // LocalSdmaCluster then ran on about half the engines, 1.44 vs 0.87 ms at 2 x 256 MiB,
+  // profiles/round6/README.md) - so the first answer per device is kept for the process.
+  uint32_t mask = engine_mask(device_, impl_->own, impl_->cpu);
   for (int b = 0; b < 32; ++b)
     if (mask & (1u << b)) local_engines_.push_back(1u << b);
   if (local_engines_.empty()) throw std::runtime_error("SdmaComm: the device reports no SDMA engine");
@@ -350,8 +369,7 @@ std::string SdmaComm::handle() const {
 
 static std::vector<hsa_amd_sdma_engine_id_t> pick_engines(hsa_agent_t dst, hsa_agent_t src, int k, int epp,
                                                           const std::vector<uint32_t>& allowed) {
-  uint32_t mask = 0;
-  if (hsa_amd_memory_copy_engine_status(dst, src, &mask) != HSA_STATUS_SUCCESS) mask = 0;
+  const uint32_t mask = cached_engine_status(dst, src);
   std::vector<uint32_t> avail;
   for (uint32_t e : allowed)
     if (mask & e) avail.push_back(e);

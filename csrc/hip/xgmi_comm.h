@@ -54,6 +54,9 @@ struct AdamShard {
 };
 
 constexpr int kMaxRanks = 16;
+// threshold kernel one-shot body: ranks at most (its per-source registers; larger memberships
+// take the two-shot body)
+constexpr int kOneshotRanks = 8;
 // Threshold kernel: gather units (chunk x peer) one workgroup may own (its pending bitmap in
 // LDS), and reduce chunks per workgroup with a launch snapshot (reference arrival order).
 constexpr int kThresholdGatherUnits = 4096;
@@ -302,8 +305,16 @@ class XgmiComm {
   // (both ranks call it concurrently with the same iters / nonce; the lower rank leads and
   // writes the elapsed 100 MHz ticks to out[0], 0 on timeout); `fenced` adds the kernels'
   // release / acquire around each hand-off.
+  // mode 0: the write-through pushes above; 1: plain stores into the peers' COARSE-grained
+  // probe buffers (probe_coarse_handle / probe_coarse_connect) and one system release per
+  // workgroup at the end - the other memory kind and store path a two-shot could use; 2: PULL,
+  // this rank loading the peers' S slots (fine-grained, remote loads) into `src` (scratch).
   int64_t probe_max_bytes() const;
-  void probe_push(const void* src, int64_t bytes, uint32_t peer_mask, int grid, hipStream_t stream);
+  void probe_push(const void* src, int64_t bytes, uint32_t peer_mask, int grid, hipStream_t stream, int mode = 0);
+  // the coarse-grained probe buffer (probe_max_bytes, allocated on the first call): IPC handle
+  // for the peers, and the peers' handles (collective, like connect)
+  std::string probe_coarse_handle();
+  void probe_coarse_connect(const std::vector<std::string>& handles);
   void probe_pingpong(int peer, int iters, uint32_t nonce, bool fenced, uint64_t* out, hipStream_t stream);
 
   // Fused data-parallel step (xgmi_adam.hip): grads [n] of every rank are reduce-scattered
@@ -421,6 +432,8 @@ class XgmiComm {
                           int* gx) const;
 
   int rank_, world_, device_, grid_, rows_;
+  char* probe_coarse_ = nullptr;  // this rank's coarse-grained probe buffer (xgmi_probe.hip)
+  std::vector<char*> probe_peers_;  // the peers' coarse probe buffers, IPC-mapped
   int64_t slot_bytes_, slot_stride_, maxch_, off_S_, off_R_, off_B_, slab_bytes_;
   int64_t ll_max_ = 0, ll_slot_ = 0, off_LL_ = 0;
   int64_t alloc_bytes_ = 0;  // slab_bytes_ padded around the IPC size bug (constructor)

@@ -725,6 +725,9 @@ XgmiComm::~XgmiComm() {
   if (switch_ev_) (void)hipEventDestroy(switch_ev_);
   for (int k = 0; k < world_; ++k)
     if (ipc_opened_[k] && peers_[k]) (void)hipIpcCloseMemHandle(peers_[k]);
+  for (int k = 0; k < static_cast<int>(probe_peers_.size()); ++k)
+    if (k != rank_ && probe_peers_[k]) (void)hipIpcCloseMemHandle(probe_peers_[k]);
+  if (probe_coarse_) (void)hipFree(probe_coarse_);
   if (slab_ && own_slab_) (void)hipFree(slab_);
   if (ctl_ && own_ctl_) (void)hipFree(ctl_);
 }
@@ -1383,7 +1386,7 @@ bool XgmiComm::threshold_args(const std::vector<XgmiComm*>& group, const std::ve
   // LL-encoded input (two bytes of slot per byte) fits one S slot
   {
     const int64_t nbytes = n * es;
-    a.oneshot = (a.full && a.sub <= 1 && W <= kMaxRanks && nbytes <= c0.th_oneshot_max_ && nbytes % 4 == 0 &&
+    a.oneshot = (a.full && a.sub <= 1 && W <= kOneshotRanks && nbytes <= c0.th_oneshot_max_ && nbytes % 4 == 0 &&
                  (a.block * es) % 4 == 0 && (a.chunk * es) % 4 == 0 && 2 * round_up(nbytes, 8) <= c0.slot_bytes_)
                     ? 1
                     : 0;
@@ -1392,7 +1395,7 @@ bool XgmiComm::threshold_args(const std::vector<XgmiComm*>& group, const std::ve
     // start (their start skew is on the round's critical path) and none walks chunks serially
     if (a.oneshot) {
       const int cap = ranks_here > 1 ? std::max(1, c0.shared_launch_cap(ranks_here)) : c0.grid_;
-      const int64_t upc = ceil_div(a.chunk * es, 8) + 1;  // units of one chunk at most
+      const int64_t upc = ceil_div(std::min(a.chunk, a.block) * es, 8) + 1;  // units of one chunk at most
       const int64_t cpw = std::max<int64_t>(1, kCommThreads / upc);
       gx = static_cast<int>(std::min<int64_t>(cap, ceil_div(static_cast<int64_t>(W) * a.nch, cpw)));
     }

@@ -92,6 +92,10 @@ int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // while any worker has rounds; it leaves after an idle spell (the dispatcher decides for the
 // whole group) and the next post launches it again. It is launched only once every worker has
 // joined (its slices need every worker's words) - except for rounds being abandoned.
+// where the last group teardown of this process is (debug_state while a configure leaves a
+// group): 1 waiting for the kernel to leave, 2 synchronising its stream, 3 freeing orphans, 0 done
+std::atomic<int> g_group_teardown{0};
+
 struct PlaneGroup {
   enum : int { kPending = 0, kJoined = 1, kLeft = 2 };
   std::string key;
@@ -130,13 +134,16 @@ struct PlaneGroup {
   ~PlaneGroup() {
     // every worker left: the dispatcher saw each one's STOP (or no kernel ran)
     const volatile uint32_t* g = gword;
+    g_group_teardown.store(1);
     const auto t0 = std::chrono::steady_clock::now();
     while (launched && g[0] != kResExited && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10))
       std::this_thread::sleep_for(std::chrono::microseconds(50));
     (void)hipSetDevice(device);
     const bool exited = !launched || g[0] == kResExited;
     if (exited) {
+      g_group_teardown.store(2);
       (void)hipStreamSynchronize(stream);
+      g_group_teardown.store(3);
       for (auto& f : orphans) f();
     } else if (!orphans.empty()) {
       MXAR_LOG(ERROR, "plane", "group kernel still running at teardown: " << orphans.size()
@@ -145,6 +152,7 @@ struct PlaneGroup {
     (void)hipFreeAsync(gdm, stream);
     (void)hipStreamDestroy(stream);
     if (exited) give_group_word(gword);  // else leaked: a kernel may still write it
+    g_group_teardown.store(0);
   }
   volatile uint32_t* state_word() const { return gword; }
   bool kernel_left() const { return !launched || reinterpret_cast<volatile uint32_t*>(gword)[0] == kResExited; }
@@ -767,6 +775,7 @@ void XgmiRoundPlane::join_group(const PlaneConfig& cfg) {
 void XgmiRoundPlane::leave_group() {
   if (!group_) return;
   std::shared_ptr<PlaneGroup> g = group_;
+  cfg_stage_.store(31);  // leave_group: 31 deciding, 32 waiting for the STOP, 33 leaving, 34 group released
   bool serving = false;
   {
     std::lock_guard<std::mutex> lk(g->mu);
@@ -779,6 +788,7 @@ void XgmiRoundPlane::leave_group() {
     ResidentDoor e{};
     e.cmd = kResStop;
     const uint32_t seq = res_seq_;
+    cfg_stage_.store(32);
     if (post_door(e, g->state_word())) {
       const auto t0 = std::chrono::steady_clock::now();
       while (static_cast<int32_t>(rstate_[1] - seq) < 0 && !g->kernel_left()) {
@@ -818,6 +828,7 @@ void XgmiRoundPlane::leave_group() {
     orphaned_ = true;
   }
   rstate_[1] = res_seq_ - 1u;  // entries no kernel took are dropped
+  cfg_stage_.store(33);
   {
     std::lock_guard<std::mutex> lk(g->mu);
     g->state[static_cast<size_t>(gidx_)] = PlaneGroup::kLeft;
@@ -825,6 +836,9 @@ void XgmiRoundPlane::leave_group() {
     g->in_kernel[static_cast<size_t>(gidx_)] = 0;
   }
   group_.reset();
+  cfg_stage_.store(34);
+  g.reset();  // the last worker out tears the group down here (waits for its kernel to leave)
+  cfg_stage_.store(35);
   gidx_ = -1;
   gplan_ = XgmiComm::ResidentPlan();
   st_.group_size = 0;
@@ -952,7 +966,7 @@ std::string XgmiRoundPlane::debug_state() const {
   std::ostringstream os;
   os << "{\"res_seq\":" << res_seq_ << ",\"consumed\":" << rstate_[1] << ",\"solo_state\":" << rstate_[0]
      << ",\"res_on\":" << (res_on_ ? 1 : 0) << ",\"last_round\":" << last_round_ << ",\"queued\":" << q_len_.load()
-     << ",\"configure_stage\":" << cfg_stage_.load();
+     << ",\"configure_stage\":" << cfg_stage_.load() << ",\"group_teardown\":" << g_group_teardown.load();
   if (res_seq_ > 1) {
     const ResidentDoor* d = door_ + (res_seq_ - 1u) % kResidentDoors;
     os << ",\"door_last\":{\"seq\":" << d->seq << ",\"cmd\":" << d->cmd << ",\"epoch\":" << d->epoch << "}";

@@ -197,8 +197,8 @@ class XgmiRoundPlane final : public RoundPlane {
   // (PlaneGroup::orphans) and the plane can run no further round
   bool orphaned_ = false;
   // where configure() is (debug_state): 0 idle, 1 abandoning the old epoch's rounds, 2 draining
-  // them, 3 leaving the old group, 4 parking a solo kernel, 5 mapping peers, 6 the new
-  // communicator and published progress, 7 joining the new group
+  // them, 3 leaving the old group (31-35: leave_group's steps), 4 parking a solo kernel, 5
+  // mapping peers, 6 the new communicator and published progress, 7 joining the new group
   std::atomic<int> cfg_stage_{0};
   std::shared_ptr<PlaneGroup> group_;
   int gidx_ = -1;                      // this worker's index in the group

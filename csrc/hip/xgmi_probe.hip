@@ -16,7 +16,10 @@
 // quiet points (every rank idle, barriers around), which bench.py does.
 #include <hip/hip_runtime.h>
 
+#include <cstring>
 #include <stdexcept>
+#include <string>
+#include <vector>
 
 #include "xgmi_device.h"
 
@@ -26,18 +29,42 @@ namespace {
 
 struct ProbeArgs {
   const char* src;
-  char* dst[kMaxRanks];
-  int64_t bytes;  // per destination, a multiple of 16
+  char* dst[kMaxRanks];  // per row y: the peer's slot (mode 0, 2) or coarse buffer (mode 1)
+  int64_t bytes;         // per destination, a multiple of 16
 };
 
-// Workgroup x of row y copies its contiguous piece of src into dst[y] (16 B per lane, nt
-// loads, write-through stores: copy_to_slab, the scatter's copy loop).
+// Workgroup x of row y moves its contiguous piece between src and dst[y], 16 B per lane:
+//   MODE 0  src -> peer slab: nt loads, write-through stores (copy_to_slab, the scatter's loop)
+//   MODE 1  src -> peer coarse buffer: plain loads and stores (4 in flight per lane), then one
+//           system-scope release per workgroup (its dirty lines written back to the peer)
+//   MODE 2  peer slab -> src: remote loads (system-coherent: fine-grained memory is not
+//           cached), plain local stores
+template <int MODE>
 __global__ __launch_bounds__(kCommThreads) void probe_push_kernel(ProbeArgs a) {
   const int64_t npk = a.bytes / 16;
   const int64_t per = (npk + gridDim.x - 1) / gridDim.x;
   const int64_t p0 = static_cast<int64_t>(blockIdx.x) * per;
   const int64_t len = clamp_len(npk - p0, per);
-  if (len > 0) copy_to_slab<F32>(a.dst[blockIdx.y] + p0 * 16, a.src + p0 * 16, len * F32::ELEMS);
+  if constexpr (MODE == 0) {
+    if (len > 0) copy_to_slab<F32>(a.dst[blockIdx.y] + p0 * 16, a.src + p0 * 16, len * F32::ELEMS);
+  } else {
+    const uint4* s = reinterpret_cast<const uint4*>(MODE == 1 ? a.src : a.dst[blockIdx.y]) + p0;
+    uint4* d = reinterpret_cast<uint4*>(MODE == 1 ? a.dst[blockIdx.y] : const_cast<char*>(a.src)) + p0;
+    constexpr int U = 4;
+    int64_t i = threadIdx.x;
+    for (; i + (U - 1) * kCommThreads < len; i += U * kCommThreads) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = s[i + u * kCommThreads];
+#pragma unroll
+      for (int u = 0; u < U; ++u) d[i + u * kCommThreads] = v[u];
+    }
+    for (; i < len; i += kCommThreads) d[i] = s[i];
+    if constexpr (MODE == 1) {
+      __syncthreads();
+      if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    }
+  }
 }
 
 // One lane per side. Token i of this probe = nonce << 16 | i (the words may hold any older
@@ -77,23 +104,59 @@ __global__ void probe_pingpong_kernel(uint32_t* mine, uint32_t* theirs, int lead
 
 int64_t XgmiComm::probe_max_bytes() const { return slot_bytes_ - 4096; }
 
-void XgmiComm::probe_push(const void* src, int64_t bytes, uint32_t peer_mask, int grid, hipStream_t stream) {
+void XgmiComm::probe_push(const void* src, int64_t bytes, uint32_t peer_mask, int grid, hipStream_t stream, int mode) {
   if (!connected_) throw std::runtime_error("XgmiComm.probe_push: connect() first");
   if (bytes <= 0 || bytes % 16 || bytes > probe_max_bytes() || (reinterpret_cast<uintptr_t>(src) & 15))
     throw std::invalid_argument("XgmiComm.probe_push: bytes must be a positive multiple of 16 <= probe_max_bytes() "
                                 "and src 16-byte aligned");
+  if (mode < 0 || mode > 2) throw std::invalid_argument("XgmiComm.probe_push: mode 0 (push), 1 (coarse push), 2 (pull)");
+  if (mode == 1 && static_cast<int>(probe_peers_.size()) != world_)
+    throw std::runtime_error("XgmiComm.probe_push(mode=1): probe_coarse_connect() first");
   ProbeArgs a{};
   a.src = static_cast<const char*>(src);
   a.bytes = bytes;
   int np = 0;
   for (int k = 0; k < world_; ++k)
-    if (k != rank_ && (peer_mask >> k) & 1u) a.dst[np++] = peers_[k] + off_S_ + static_cast<int64_t>(rank_) * slot_stride_;
+    if (k != rank_ && (peer_mask >> k) & 1u)
+      a.dst[np++] = mode == 1 ? probe_peers_[k] : peers_[k] + off_S_ + static_cast<int64_t>(rank_) * slot_stride_;
   if (np == 0) return;
   hip_check(hipSetDevice(device_), "hipSetDevice");
   order_after_last(stream);
-  const int gx = std::max(1, grid);
-  hipLaunchKernelGGL(probe_push_kernel, dim3(gx, np), dim3(kCommThreads), 0, stream, a);
+  const dim3 g(std::max(1, grid), np), b(kCommThreads);
+  if (mode == 0) hipLaunchKernelGGL(probe_push_kernel<0>, g, b, 0, stream, a);
+  if (mode == 1) hipLaunchKernelGGL(probe_push_kernel<1>, g, b, 0, stream, a);
+  if (mode == 2) hipLaunchKernelGGL(probe_push_kernel<2>, g, b, 0, stream, a);
   hip_check(hipGetLastError(), "probe_push launch");
+}
+
+std::string XgmiComm::probe_coarse_handle() {
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  if (probe_coarse_ == nullptr)
+    hip_check(hipMalloc(reinterpret_cast<void**>(&probe_coarse_), ipc_safe_bytes(probe_max_bytes())),
+              "hipMalloc(coarse probe buffer)");
+  hipIpcMemHandle_t h;
+  hip_check(hipIpcGetMemHandle(&h, probe_coarse_), "hipIpcGetMemHandle(coarse probe buffer)");
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void XgmiComm::probe_coarse_connect(const std::vector<std::string>& handles) {
+  if (static_cast<int>(handles.size()) != world_) throw std::invalid_argument("probe_coarse_connect: one handle per rank");
+  if (probe_coarse_ == nullptr) throw std::runtime_error("probe_coarse_connect: probe_coarse_handle() first");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  if (!probe_peers_.empty()) return;  // mapped by an earlier probe
+  probe_peers_.assign(world_, nullptr);
+  for (int k = 0; k < world_; ++k) {
+    if (k == rank_) {
+      probe_peers_[k] = probe_coarse_;
+      continue;
+    }
+    if (handles[k].size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("probe_coarse_connect: bad handle");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handles[k].data(), sizeof(h));
+    void* p = nullptr;
+    hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(coarse probe buffer)");
+    probe_peers_[k] = static_cast<char*>(p);
+  }
 }
 
 void XgmiComm::probe_pingpong(int peer, int iters, uint32_t nonce, bool fenced, uint64_t* out, hipStream_t stream) {

@@ -99,7 +99,10 @@ __device__ __forceinline__ bool host_forced(const uint32_t* hforce, const uint32
 // out-of-line callee would have copied to scratch)
 __device__ __attribute__((noinline)) bool wave_forced_words(const uint32_t* own_force, int P, int r, uint32_t epoch,
                                                             const uint32_t* hforce, const uint32_t* habort) {
-  const int s = static_cast<int>(threadIdx.x);
+  // lane, not thread: every wave of a one-shot workgroup polls (xgmi_threshold.hip one-shot
+  // body); with threadIdx.x only wave 0 could ever see a force and the others waited for the
+  // deadline
+  const int s = static_cast<int>(threadIdx.x & 63u);
   bool f = false;
   if (s < P && s != r) f = reached(ld_flag(own_force + s), epoch);
   if (hforce != nullptr && s == 63) {
@@ -772,6 +775,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     // arrived, and reports that count - the two-shot's "reduce what has arrived".
     const uint32_t tag = ll_tag(epoch);
     const int64_t nbytes = a.n * es;
+    static_assert(kOneshotRanks <= kMaxRanks, "one-shot sources beyond the peer table");
     const int64_t units = (nbytes + 7) / 8;
     const int64_t gstride = static_cast<int64_t>(G) * kCommThreads;
     if (!cold && !void_round) {
@@ -791,7 +795,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     const __amdgpu_buffer_rsrc_t ro = slab_rsrc(out);
     __shared__ uint32_t sh_miss;
     const int nq = P * a.nch;
-    auto chunk_span = [&](int q, int64_t* b0, int64_t* b1) -> bool {  // bytes of chunk q (false: none)
+    auto chunk_span = [&](int q, int64_t* b0, int64_t* b1) __attribute__((always_inline)) -> bool {  // bytes of chunk q (false: none)
       const int j = q / a.nch;
       const int c = q - j * a.nch;
       const int64_t blen = clamp_len(a.n - static_cast<int64_t>(j) * a.block, a.block);
@@ -800,10 +804,10 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       *b1 = *b0 + clen * es;
       return clen > 0;
     };
-    auto poll_unit = [&](int64_t u, bool act, bool h0, bool h1, Pack16* v, bool& stop) -> uint32_t {
+    auto poll_unit = [&](int64_t u, bool act, bool h0, bool h1, Pack16* v, bool& stop) __attribute__((always_inline)) -> uint32_t {
       uint32_t want = 0;  // sources whose words of this unit are not in yet
 #pragma unroll
-      for (int s = 0; s < kMaxRanks; ++s) {
+      for (int s = 0; s < kOneshotRanks; ++s) {
         if (s < P && s != r && act) {
           v[s] = __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc(mine_s + static_cast<int64_t>(s) * slot),
                                                         static_cast<int>(u * 16), 0, kAuxSysLd);
@@ -812,13 +816,13 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       }
       auto in_now = [&](const Pack16& w) { return (!h0 || w[1] == tag) && (!h1 || w[3] == tag); };
 #pragma unroll
-      for (int s = 0; s < kMaxRanks; ++s)
+      for (int s = 0; s < kOneshotRanks; ++s)
         if (((want >> s) & 1u) && in_now(v[s])) want &= ~(1u << s);
       const uint64_t tw = ps.now();
       while (__any(want != 0) && !stop) {
         __builtin_amdgcn_s_sleep(1);
 #pragma unroll
-        for (int s = 0; s < kMaxRanks; ++s) {
+        for (int s = 0; s < kOneshotRanks; ++s) {
           if ((want >> s) & 1u) {
             v[s] = __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc(mine_s + static_cast<int64_t>(s) * slot),
                                                           static_cast<int>(u * 16), 0, kAuxSysLd);
@@ -827,7 +831,9 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         }
         const uint64_t now = wall_ticks();
         const bool host = hp.due(now);
-        if ((host || sp.due(now)) && wave_forced(a, rv.hforce, rv.habort, r, epoch, host)) stop = true;
+        const bool slab = sp.due(now);  // both polls advance unconditionally: a short-circuit
+                                        // picked one of them by address (a scratch round trip)
+        if ((host || slab) && wave_forced(a, rv.hforce, rv.habort, r, epoch, host)) stop = true;
         if (now > deadline) {
           if ((threadIdx.x & 63) == 0)
             __hip_atomic_fetch_or(err, ERR_TIMEOUT_SCATTER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -837,10 +843,10 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       ps.add(2, tw);
       return want;
     };
-    auto sum_unit = [&](int64_t u, bool h0, bool h1, const Pack16* v) {  // every source in, rank order
+    auto sum_unit = [&](int64_t u, bool h0, bool h1, const Pack16* v) __attribute__((always_inline)) {  // every source in, rank order
       Acc8<E> acc;
 #pragma unroll
-      for (int s = 0; s < kMaxRanks; ++s) {
+      for (int s = 0; s < kOneshotRanks; ++s) {
         if (s >= P) continue;
         acc.add(s == r ? load_unit8(in, u, nbytes) : make_uint2(v[s][0], v[s][2]));
       }
@@ -877,7 +883,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         const bool act = my_u >= 0;
         const bool h0 = act && my_u * 8 >= my_b0 && my_u * 8 < my_b1;
         const bool h1 = act && my_u * 8 + 4 >= my_b0 && my_u * 8 + 4 < my_b1;
-        Pack16 v[kMaxRanks];
+        Pack16 v[kOneshotRanks];
         bool stop = false;
         const uint32_t want = poll_unit(my_u, act, h0, h1, v, stop);
         if (__syncthreads_or(want != 0u) == 0) {
@@ -913,7 +919,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         const bool act = u < u1;
         const bool h0 = act && u * 8 >= b0 && u * 8 < b1;          // low word in this chunk
         const bool h1 = act && u * 8 + 4 >= b0 && u * 8 + 4 < b1;  // high word in this chunk
-        Pack16 v[kMaxRanks];
+        Pack16 v[kOneshotRanks];
         const uint32_t want = poll_unit(u, act, h0, h1, v, stop);
         miss |= want;
         if (act && want == 0u && !cold) sum_unit(u, h0, h1, v);
@@ -1045,7 +1051,8 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
           // one clock read per spin: s_memrealtime is a scalar memory round trip
           const uint64_t now = wall_ticks();
           const bool host = hp.due(now);
-          if ((host || sp.due(now)) && wave_forced(a, rv.hforce, rv.habort, r, epoch, host)) {
+          const bool slab = sp.due(now);
+          if ((host || slab) && wave_forced(a, rv.hforce, rv.habort, r, epoch, host)) {
             forced = true;
             break;
           }
@@ -1236,7 +1243,8 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       const uint64_t now = wall_ticks();
       if (!give) {
         const bool host = hp.due(now);
-        if ((host || sp.due(now)) && wave_forced(a, rv.hforce, rv.habort, r, epoch, host)) give = 1;
+        const bool slab = sp.due(now);
+        if ((host || slab) && wave_forced(a, rv.hforce, rv.habort, r, epoch, host)) give = 1;
       }
       if (!give && now > deadline) {
         if (threadIdx.x == 0)

@@ -134,7 +134,9 @@ def _links(P: int = 8) -> dict:
     return {"bytes": 67108864, "reps": 5, "grid_per_peer": 64, "store": "st16_wt (two-shot scatter path)",
             "push_GBps": [[0.0 if k == r else 123.45 for k in range(P)] for r in range(P)],
             "all_GBps": [812.34] * P, "single_GBps_min_med_max": [101.23, 123.45, 131.11], "fanout_ratio": 6.58,
-            "flag_us": {"bare": [None] + [1.234] * (P - 1), "fenced": [None] + [1.567] * (P - 1)}}
+            "flag_us": {"bare": [None] + [1.234] * (P - 1), "fenced": [None] + [1.567] * (P - 1)},
+            "coarse": {"single_GBps_min_med_max": [90.12, 111.11, 120.5], "all_GBps_min_max": [700.25, 760.5]},
+            "pull": {"single_GBps_min_med_max": [60.12, 70.75, 80.5], "all_GBps_min_max": [400.25, 420.5]}}
 
 
 def test_n8_line_carries_the_link_pack():
@@ -145,7 +147,8 @@ def test_n8_line_carries_the_link_pack():
     d = json.loads(s)
     assert "dropped" not in d
     assert d["xgmi_links"] == {"single_GBps": [101.23, 123.45, 131.11], "all_GBps": [812.34, 812.34],
-                               "ratio": 6.58, "flag_us": [1.234, 1.234, 1.567]}
+                               "ratio": 6.58, "flag_us": [1.234, 1.234, 1.567], "coarse": [111.11, 700.25],
+                               "pull": [70.75, 400.25]}
     assert d["config"]["algo"].split("@")[0].split("~")[0] not in ("ring_native", "rccl", "rsag")
     assert d["sdma"] == {"ok": True, "ms": 1.2345, "algbw": 217.45}
 

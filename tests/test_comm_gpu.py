@@ -495,6 +495,10 @@ def _links_worker(rank, world, port, results):
         singles = [v for i, row in enumerate(info["push_GBps"]) for k, v in enumerate(row) if k != i]
         if not (len(info["all_GBps"]) == world and min(singles) > 0 and min(info["all_GBps"]) > 0):
             ok, msg = False, f"rates {info}"
+        for key in ("coarse", "pull"):  # the coarse-grained push and the pull ran and moved bytes
+            m = info.get(key) or {}
+            if not (min(m.get("single_GBps_min_med_max") or [0]) > 0 and min(m.get("all_GBps_min_max") or [0]) > 0):
+                ok, msg = False, f"{key} rates {info}"
         lat = info["flag_us"]
         if rank == 0 and not all(lat[m][k] and lat[m][k] > 0 for m in ("bare", "fenced") for k in range(1, world)):
             ok, msg = False, f"latencies {lat}"
@@ -602,3 +606,26 @@ def _run_flag_owner(env=None):
 def test_ring_flag_ownership_late_forward():
     bad = _run_flag_owner()
     assert not bad, bad
+
+
+def test_solo_rehearsal_comm_runs_one_rank_of_an_8_rank_two_shot():
+    """benchmarks/sections.py SoloRehearsalComm (the DP-overlap rehearsal's comm): rank 0 of an
+    8-rank two-shot runs alone with its peers' flags pre-armed - it never waits, and since the
+    synthetic peers contribute zeros and never reduce, the own block keeps the input and the
+    gathered blocks read zeros. Repeated calls (epochs advance) keep doing exactly that."""
+    from benchmarks.sections import SoloRehearsalComm
+
+    class _B:
+        def __init__(self, t):
+            self.buffer, self.nbytes = t, t.numel() * t.element_size()
+
+    n = (3 << 20) + 40  # bf16 elements: blocks of ceil(n / 8) rounded to 16 B
+    t = torch.ones(n, dtype=torch.bfloat16, device=DEV)
+    comm = SoloRehearsalComm([_B(t)], 8, 64)
+    blk = -(-(-(-n // 8)) // 8) * 8
+    for _ in range(3):
+        t.fill_(1.0)
+        comm.allreduce_(t, op="sum")
+        comm.check()
+        assert bool((t[:blk] == 1).all()) and bool((t[blk:] == 0).all())
+    assert SoloRehearsalComm.hbm_bytes(1 << 30, 8) == int(2 * ((1 << 30) + 2 * (1 << 30) * 7 / 8))

@@ -59,6 +59,27 @@ def test_local_sdma_inplace_mean_and_many_calls():
     assert cl.comms[0].stats["calls"] >= 40
 
 
+@pytest.mark.parametrize("pieces", [1, 3, 8])
+def test_local_sdma_pipeline_pieces(pieces):
+    """The pipelined schedule (sdma_comm.hip): each block in `pieces` pieces - reduce of piece k
+    beside the engines' copies of k + 1, phase 2 and the gather per piece - including pieces
+    that end inside a short last block and blocks with fewer pieces than the others."""
+    from akka_allreduce_1_amd.parallel import LocalSdmaCluster
+
+    P = 3
+    cl = LocalSdmaCluster(P, slot_bytes=4 << 20, grid=16)
+    for c in cl.comms:
+        c.pieces = pieces
+    for n in (2_500_003, 1_000_000, 12_289):
+        xs = [fill_uniform(torch.empty(n, dtype=torch.bfloat16, device=DEV), seed=n + k) for k in range(P)]
+        ys = cl.allreduce(xs)
+        torch.cuda.synchronize()
+        cl.check()
+        ref = _ref(xs)
+        for y in ys:
+            assert (y.float() - ref).abs().max().item() <= _tol(torch.bfloat16, P)
+
+
 def _mp_worker(rank, world, port, results):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     import torch.distributed as dist

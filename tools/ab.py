@@ -178,6 +178,7 @@ def exp_sdma(a) -> None:
                 p50 = percentile(device_times(lambda: cl.allreduce(xs, ys), a.iters, dev), 50)
                 cl.check()
                 _emit({"exp": "sdma", "tag": a.tag, "rep": rep, "P": P, "mib": a.mib, "grid": g, "pieces": k,
+                       "engines": cl.comms[0].engines, "engines_per_peer": cl.comms[0].engines_per_peer,
                        "validated": ok, "max_abs_err": err, "p50_ms": round(p50, 4),
                        "algbw_GBps": round(nbytes / (p50 / 1e3) / 1e9, 1)})
             del cl
