@@ -389,3 +389,18 @@ def compact(s: dict) -> dict:
         out["native2"] = nrow
     out["validated"] = all(x is True for x in ok if x is not None) and any(x is not None for x in ok)
     return out
+
+
+if __name__ == "__main__":
+    # the section on its own: python -m benchmarks.stragglers [--budget S] > full.json
+    import argparse
+    import json
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--budget", type=float, default=100.0)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    s = section(dev, a.budget)
+    print(json.dumps(s), flush=True)
+    print(json.dumps({"compact": compact(s)}), flush=True)

@@ -780,6 +780,12 @@ void XgmiRoundPlane::leave_group() {
   {
     std::lock_guard<std::mutex> lk(g->mu);
     serving = g->in_kernel[static_cast<size_t>(gidx_)] != 0 && !g->kernel_left();
+    // from here on no kernel launched for the group serves this worker: a co-located worker's
+    // post could otherwise relaunch the group kernel between the running kernel taking our
+    // STOP and our leaving, with a slice that then took this worker's NEXT membership's rounds
+    // from its door (an old-membership kernel running a new-membership round until the
+    // deadline; profiles/round6/README.md section 5)
+    g->state[static_cast<size_t>(gidx_)] = PlaneGroup::kLeft;
   }
   bool lost = false;
   if (serving) {

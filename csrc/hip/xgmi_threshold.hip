@@ -778,7 +778,45 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     static_assert(kOneshotRanks <= kMaxRanks, "one-shot sources beyond the peer table");
     const int64_t units = (nbytes + 7) / 8;
     const int64_t gstride = static_cast<int64_t>(G) * kCommThreads;
-    if (!cold && !void_round) {
+    const int nq = P * a.nch;
+    auto chunk_span = [&](int q, int64_t* b0, int64_t* b1) __attribute__((always_inline)) -> bool {  // bytes of chunk q (false: none)
+      const int j = q / a.nch;
+      const int c = q - j * a.nch;
+      const int64_t blen = clamp_len(a.n - static_cast<int64_t>(j) * a.block, a.block);
+      const int64_t clen = clamp_len(blen - static_cast<int64_t>(c) * a.chunk, a.chunk);
+      *b0 = (static_cast<int64_t>(j) * a.block + static_cast<int64_t>(c) * a.chunk) * es;
+      *b1 = *b0 + clen * es;
+      return clen > 0;
+    };
+    // the fast pass's mapping (below): thread t of this workgroup owns flat unit t of the
+    // workgroup's chunks q = blockIdx.x + i * G
+    int64_t tot = 0, my_u = -1, my_b0 = 0, my_b1 = 0;
+    for (int q = blockIdx.x; q < nq; q += G) {
+      int64_t b0, b1;
+      if (!chunk_span(q, &b0, &b1)) continue;
+      const int64_t u0 = b0 / 8, u1 = (b1 + 7) / 8;
+      const int64_t t = static_cast<int64_t>(threadIdx.x) - tot;
+      if (t >= 0 && t < u1 - u0) {
+        my_u = u0 + t;
+        my_b0 = b0;
+        my_b1 = b1;
+      }
+      tot += u1 - u0;
+    }
+    const bool fast = !cold && !void_round && tot <= kCommThreads;  // uniform
+    uint2 own_unit = make_uint2(0u, 0u);
+    if (fast) {
+      // each thread pushes the unit it will sum: the workgroups' chunks together cover the
+      // input (a unit shared by two chunks goes twice, identical), and the own word is loaded
+      // once for both
+      if (my_u >= 0) {
+        own_unit = load_unit8(in, my_u, nbytes);
+        const Pack16 v{own_unit.x, tag, own_unit.y, tag};
+        for (int k = 0; k < P; ++k)
+          if (k != r)
+            st16_wt(slab_rsrc(a.base[k] + rowS + static_cast<int64_t>(r) * slot), static_cast<uint32_t>(my_u * 16), v);
+      }
+    } else if (!cold && !void_round) {
       for (int64_t i = static_cast<int64_t>(blockIdx.x) * kCommThreads + threadIdx.x; i < units; i += gstride) {
         const uint2 d = load_unit8(in, i, nbytes);
         Pack16 v;
@@ -794,16 +832,6 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     const char* const mine_s = a.base[r] + rowS;  // source s's units at mine_s + s * slot
     const __amdgpu_buffer_rsrc_t ro = slab_rsrc(out);
     __shared__ uint32_t sh_miss;
-    const int nq = P * a.nch;
-    auto chunk_span = [&](int q, int64_t* b0, int64_t* b1) __attribute__((always_inline)) -> bool {  // bytes of chunk q (false: none)
-      const int j = q / a.nch;
-      const int c = q - j * a.nch;
-      const int64_t blen = clamp_len(a.n - static_cast<int64_t>(j) * a.block, a.block);
-      const int64_t clen = clamp_len(blen - static_cast<int64_t>(c) * a.chunk, a.chunk);
-      *b0 = (static_cast<int64_t>(j) * a.block + static_cast<int64_t>(c) * a.chunk) * es;
-      *b1 = *b0 + clen * es;
-      return clen > 0;
-    };
     auto poll_unit = [&](int64_t u, bool act, bool h0, bool h1, Pack16* v, bool& stop) __attribute__((always_inline)) -> uint32_t {
       uint32_t want = 0;  // sources whose words of this unit are not in yet
 #pragma unroll
@@ -821,14 +849,16 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       const uint64_t tw = ps.now();
       while (__any(want != 0) && !stop) {
         __builtin_amdgcn_s_sleep(1);
+        // every missing source's load in flight first, then the tag checks: a check right after
+        // each load waited for it before the next was issued (one memory round trip per source)
 #pragma unroll
-        for (int s = 0; s < kOneshotRanks; ++s) {
-          if ((want >> s) & 1u) {
+        for (int s = 0; s < kOneshotRanks; ++s)
+          if ((want >> s) & 1u)
             v[s] = __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc(mine_s + static_cast<int64_t>(s) * slot),
                                                           static_cast<int>(u * 16), 0, kAuxSysLd);
-            if (in_now(v[s])) want &= ~(1u << s);
-          }
-        }
+#pragma unroll
+        for (int s = 0; s < kOneshotRanks; ++s)
+          if (((want >> s) & 1u) && in_now(v[s])) want &= ~(1u << s);
         const uint64_t now = wall_ticks();
         const bool host = hp.due(now);
         const bool slab = sp.due(now);  // both polls advance unconditionally: a short-circuit
@@ -843,12 +873,13 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       ps.add(2, tw);
       return want;
     };
-    auto sum_unit = [&](int64_t u, bool h0, bool h1, const Pack16* v) __attribute__((always_inline)) {  // every source in, rank order
+    // every source in: the sum in rank order (`own`: this rank's unit, already loaded)
+    auto sum_unit = [&](int64_t u, bool h0, bool h1, const Pack16* v, const uint2* own) __attribute__((always_inline)) {
       Acc8<E> acc;
 #pragma unroll
       for (int s = 0; s < kOneshotRanks; ++s) {
         if (s >= P) continue;
-        acc.add(s == r ? load_unit8(in, u, nbytes) : make_uint2(v[s][0], v[s][2]));
+        acc.add(s == r ? (own != nullptr ? *own : load_unit8(in, u, nbytes)) : make_uint2(v[s][0], v[s][2]));
       }
       const uint2 o = acc.pack(a.scale);
       if (h0 && h1)
@@ -865,21 +896,8 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     // void / timed-out pass falls through to the chunk-by-chunk body (arrival within a round is
     // final: it reads the slots again and reduces what arrived).
     bool done_fast = false;
-    if (!cold && !void_round) {
-      int64_t tot = 0, my_u = -1, my_b0 = 0, my_b1 = 0;
-      for (int q = blockIdx.x; q < nq; q += G) {
-        int64_t b0, b1;
-        if (!chunk_span(q, &b0, &b1)) continue;
-        const int64_t u0 = b0 / 8, u1 = (b1 + 7) / 8;
-        const int64_t t = static_cast<int64_t>(threadIdx.x) - tot;
-        if (t >= 0 && t < u1 - u0) {
-          my_u = u0 + t;
-          my_b0 = b0;
-          my_b1 = b1;
-        }
-        tot += u1 - u0;
-      }
-      if (tot <= kCommThreads) {  // uniform
+    if (fast) {
+      {
         const bool act = my_u >= 0;
         const bool h0 = act && my_u * 8 >= my_b0 && my_u * 8 < my_b1;
         const bool h1 = act && my_u * 8 + 4 >= my_b0 && my_u * 8 + 4 < my_b1;
@@ -887,7 +905,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         bool stop = false;
         const uint32_t want = poll_unit(my_u, act, h0, h1, v, stop);
         if (__syncthreads_or(want != 0u) == 0) {
-          if (act) sum_unit(my_u, h0, h1, v);
+          if (act) sum_unit(my_u, h0, h1, v, &own_unit);
           if (counts)
             for (int q = blockIdx.x + static_cast<int>(threadIdx.x) * G; q < nq; q += G * kCommThreads) {
               int64_t b0, b1;
@@ -922,7 +940,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         Pack16 v[kOneshotRanks];
         const uint32_t want = poll_unit(u, act, h0, h1, v, stop);
         miss |= want;
-        if (act && want == 0u && !cold) sum_unit(u, h0, h1, v);
+        if (act && want == 0u && !cold) sum_unit(u, h0, h1, v, nullptr);
       }
       // the common case (every word of every source in) costs one barrier-with-reduction; only
       // a forced / cold / timed-out chunk gathers which sources it misses
