@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import contextlib
 import statistics
+import sys
 import time
 
 import torch
@@ -610,6 +611,7 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                              ("split64_tokens8192", 128, True, True, 8192)]
             for name, grid, ov, hi, tokens in variants:
                 cell: dict = {"tokens": tokens}
+                print(f"[dp_overlap] {model} {name}", file=sys.stderr, flush=True)  # progress (a long section)
                 try:
                     if tokens not in bwds:
                         bwds[tokens] = SyntheticBackward(params, tokens, torch.bfloat16, dev)

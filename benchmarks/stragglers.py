@@ -274,7 +274,15 @@ def native_job(n: int, chunk: int, rounds: int, *, th_reduce: float, th_complete
                             str(th_complete), "--max-lag", str(max_lag), "--max-round", str(rounds - 1),
                             "--spin-us", "500"] + seeds + ["--quiet"],
                            capture_output=True, text=True, timeout=timeout, env=env)
-        outs = [w.communicate(timeout=timeout)[0] for w in workers]
+        outs = []
+        for k, w in enumerate(workers):
+            try:
+                outs.append(w.communicate(timeout=timeout)[0])
+            except subprocess.TimeoutExpired:  # keep what it printed: the bench records why
+                w.kill()
+                tail = (w.communicate()[0] or "")[-600:]
+                row["hung_worker"] = {"id": k, "output_tail": tail, "master_tail": (m.stdout or "")[-300:]}
+                outs.append(tail)
     finally:
         for w in workers:
             if w.poll() is None:

@@ -120,6 +120,9 @@ __device__ __attribute__((noinline)) bool wave_forced_words(const uint32_t* own_
   }
   return __any(f);
 }
+// lag skip: on-time rounds in a row after which a skipped peer is waited for again
+constexpr uint32_t kHintRounds = 16;
+
 __device__ __forceinline__ bool wave_forced(const CommArgs& a, const uint32_t* hforce, const uint32_t* habort, int r,
                                             uint32_t epoch, bool host) {
   return wave_forced_words(forcew(a, r, 0), a.P, r, epoch, host ? hforce : nullptr, habort);
@@ -735,12 +738,24 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       // (k < P first: a 32-bit shift by k >= 32 wraps on the hardware - lane 32 + j would
       // alias peer j and write through base[32 + j], past the peer table)
       if (k < P && ((lag >> k) & 1u)) force_max(forcew(a, k, r), epoch);
-      // the sticky hint keeps a skipped peer until it has caught up with the round before
-      // this one (hysteresis): a straggler hovering at the gate target would otherwise be
-      // waited for lag_wait every other round
-      const bool caught_up = f == nullptr || reached(ld_flag(f), epoch - 1u);
-      const uint32_t up = static_cast<uint32_t>(__ballot(caught_up));
+      // The sticky hint keeps a skipped peer until it has been at the gate on time for
+      // kHintRounds rounds in a row (ctl[16 + k] counts them; a skip restarts the count). A
+      // straggler that catches up in bursts - forced and cold rounds complete at once - is at
+      // the gate now and then; clearing the hint on each such round made the fast ranks wait
+      // lag_wait for it every few rounds (4.5x their period with a 0.2 ms straggler at 40 B,
+      // profiles/round6/README.md section 6).
       const uint32_t hint = ld_ctl(&ctl[15]);
+      const bool lagged = k < P && ((lag >> k) & 1u);
+      bool clear = false;
+      if (k < P && k != r && (lagged || (k < 32 && ((hint >> k) & 1u)))) {
+        uint32_t streak = lagged ? 0u : ld_ctl(&ctl[16 + k]) + 1u;
+        if (streak >= kHintRounds) {
+          clear = true;
+          streak = 0u;
+        }
+        __hip_atomic_store(&ctl[16 + k], streak, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const uint32_t up = static_cast<uint32_t>(__ballot(clear));
       if (k == 0) __hip_atomic_store(&ctl[15], (hint & ~up) | lag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (k == 0) {
