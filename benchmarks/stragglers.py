@@ -119,10 +119,21 @@ def inproc_case(dev, P: int, nbytes: int, dtype, chunk: int, max_lag: int, delay
         st = job.state()
         warm = max(10, rounds // 10)
         iv = [x for k in fast for x in _period(job.sink_stamps(k), warm)]
+        # where the long fast periods are: (worker, round ending it, us) for the 4 longest
+        # above 4 x the median (a stall's position says what it waited for)
+        med = statistics.median(iv) if iv else 0.0
+        longest = []
+        for k in fast:
+            st_k = sorted((r, t) for r, t in job.sink_stamps(k) if r >= warm)
+            longest += [(k, b[0], round((b[1] - a[1]) * 1e6, 1)) for a, b in zip(st_k, st_k[1:])
+                        if (b[1] - a[1]) * 1e6 > 4 * med]
+        if longest:
+            row["long_periods"] = sorted(longest, key=lambda x: -x[2])[:4]
         ws = st["workers"]
         cs = [job.count_stats(k) for k in fast]
         row.update({
-            "fast_period_p50_us": _q(iv, 0.5), "fast_period_p99_us": _q(iv, 0.99),
+            "fast_period_p10_us": _q(iv, 0.1), "fast_period_p50_us": _q(iv, 0.5), "fast_period_p90_us": _q(iv, 0.9),
+            "fast_period_p99_us": _q(iv, 0.99),
             "fast_period_mean_us": round(statistics.fmean(iv), 2) if iv else None,
             "master_rounds": st["master"].get("round"), "wall_s": round(wall, 3),
             "fast_count_mean": round(sum(c["sum"] for c in cs) / max(1, sum(c["n"] for c in cs)), 4),

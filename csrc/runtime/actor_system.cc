@@ -273,6 +273,16 @@ size_t ActorCell::process(size_t n) {
       do_stop();
       break;
     }
+    // A cell this turn put in the run-next slot waits for the turn to end. When the turn goes
+    // on (more mail), it goes to the run queue for an idle thread instead: a straggling worker
+    // whose handler blocks in its dataSource for 2 ms per message held the master - scheduled
+    // by the worker's CompleteAllreduce - for two or three such messages, stalling every fast
+    // worker's round with it (profiles/round6/README.md section 6).
+    if (tl_next && tl_sys == sys_ && done < n && pending_.load() > 0) {
+      std::shared_ptr<ActorCell> next = std::move(tl_next);
+      tl_next.reset();
+      sys_->enqueue(next);
+    }
   }
   return done;
 }
