@@ -687,6 +687,37 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   // that did not is not; the laggard's own late writes go to its slots of our slab with an
   // older epoch, which no later round of ours takes, and its rounds in order mean its newer
   // data always follows its older data.
+  // One-shot body: this thread's unit of the fast pass and its input word, loaded BEFORE the
+  // lag gate so the input load overlaps the gate's progress-word loads (both are latency)
+  [[maybe_unused]] int64_t tot = 0, my_u = -1, my_b0 = 0, my_b1 = 0;
+  [[maybe_unused]] uint2 own_unit = make_uint2(0u, 0u);
+  if constexpr (ONESHOT) {
+    const int nq = P * a.nch;
+    auto chunk_span = [&](int q, int64_t* b0, int64_t* b1) __attribute__((always_inline)) -> bool {  // bytes of chunk q (false: none)
+      const int j = q / a.nch;
+      const int c = q - j * a.nch;
+      const int64_t blen = clamp_len(a.n - static_cast<int64_t>(j) * a.block, a.block);
+      const int64_t clen = clamp_len(blen - static_cast<int64_t>(c) * a.chunk, a.chunk);
+      *b0 = (static_cast<int64_t>(j) * a.block + static_cast<int64_t>(c) * a.chunk) * es;
+      *b1 = *b0 + clen * es;
+      return clen > 0;
+    };
+    // the fast pass's mapping (below): thread t of this workgroup owns flat unit t of the
+    // workgroup's chunks q = blockIdx.x + i * G
+    for (int q = blockIdx.x; q < nq; q += G) {
+      int64_t b0, b1;
+      if (!chunk_span(q, &b0, &b1)) continue;
+      const int64_t u0 = b0 / 8, u1 = (b1 + 7) / 8;
+      const int64_t t = static_cast<int64_t>(threadIdx.x) - tot;
+      if (t >= 0 && t < u1 - u0) {
+        my_u = u0 + t;
+        my_b0 = b0;
+        my_b1 = b1;
+      }
+      tot += u1 - u0;
+    }
+    if (!cold && tot <= kCommThreads && my_u >= 0) own_unit = load_unit8(in, my_u, a.n * es);
+  }
   __shared__ uint32_t sh_skip;
   const bool gate_open = a.gate_shortcut &&
                          (rv.gate_open || (rv.epoch == 0 && clean_prev != 0u && clean_prev == epoch - 1u));
@@ -794,7 +825,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
     const int64_t units = (nbytes + 7) / 8;
     const int64_t gstride = static_cast<int64_t>(G) * kCommThreads;
     const int nq = P * a.nch;
-    auto chunk_span = [&](int q, int64_t* b0, int64_t* b1) __attribute__((always_inline)) -> bool {  // bytes of chunk q (false: none)
+    auto chunk_span = [&](int q, int64_t* b0, int64_t* b1) __attribute__((always_inline)) -> bool {
       const int j = q / a.nch;
       const int c = q - j * a.nch;
       const int64_t blen = clamp_len(a.n - static_cast<int64_t>(j) * a.block, a.block);
@@ -803,29 +834,11 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       *b1 = *b0 + clen * es;
       return clen > 0;
     };
-    // the fast pass's mapping (below): thread t of this workgroup owns flat unit t of the
-    // workgroup's chunks q = blockIdx.x + i * G
-    int64_t tot = 0, my_u = -1, my_b0 = 0, my_b1 = 0;
-    for (int q = blockIdx.x; q < nq; q += G) {
-      int64_t b0, b1;
-      if (!chunk_span(q, &b0, &b1)) continue;
-      const int64_t u0 = b0 / 8, u1 = (b1 + 7) / 8;
-      const int64_t t = static_cast<int64_t>(threadIdx.x) - tot;
-      if (t >= 0 && t < u1 - u0) {
-        my_u = u0 + t;
-        my_b0 = b0;
-        my_b1 = b1;
-      }
-      tot += u1 - u0;
-    }
     const bool fast = !cold && !void_round && tot <= kCommThreads;  // uniform
-    uint2 own_unit = make_uint2(0u, 0u);
     if (fast) {
-      // each thread pushes the unit it will sum: the workgroups' chunks together cover the
-      // input (a unit shared by two chunks goes twice, identical), and the own word is loaded
-      // once for both
+      // each thread pushes the unit it will sum (loaded before the gate): the workgroups'
+      // chunks together cover the input (a unit shared by two chunks goes twice, identical)
       if (my_u >= 0) {
-        own_unit = load_unit8(in, my_u, nbytes);
         const Pack16 v{own_unit.x, tag, own_unit.y, tag};
         for (int k = 0; k < P; ++k)
           if (k != r)

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Why the one-GPU DP overlap rehearsal loses to the serial schedule (bench dp.overlap_rehearsal):
-a kernel-level look, run under rocprofv3 --kernel-trace.
+a kernel-level look, run under rocprofv3 --kernel-trace (and `--contention`: the memory-system
+counters of one GEMM beside the comm, for PMC passes). The comm is one rank of an 8-GPU
+two-shot (benchmarks/sections.py SoloRehearsalComm: a real rank's per-GPU HBM bytes).
 
 Three phases, separated by idle gaps of 20 ms that the analysis splits on:
   A  compute only: the synthetic backward (weight-gradient GEMMs) + SGD update
@@ -33,15 +35,15 @@ def run(a) -> None:
     from akka_allreduce_1_amd.models.grad_sets import gradient_shapes, llama3_8b_shapes
     from akka_allreduce_1_amd.parallel import BucketedGradReducer
     from benchmarks.bench_dp import SyntheticBackward
-    from benchmarks.sections import PairRehearsalComm, _Placeholder
+    from benchmarks.sections import SoloRehearsalComm, _Placeholder
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     shapes = llama3_8b_shapes(a.layers) if a.model == "llama3_8b" else gradient_shapes(a.model)
     params = [torch.nn.Parameter(torch.zeros(sh, dtype=torch.bfloat16, device=dev)) for _, sh in shapes]
-    reducer = BucketedGradReducer(params, _Placeholder(), op="avg", bucket_bytes=a.bucket_mib << 20)
+    reducer = BucketedGradReducer(params, _Placeholder(8), op="avg", bucket_bytes=a.bucket_mib << 20)
     reducer.remove_hooks()
-    comm = PairRehearsalComm(reducer.buckets, max(a.grid, 8))
+    comm = SoloRehearsalComm(reducer.buckets, 8, max(a.grid, 8))  # one rank of an 8-GPU two-shot
     for c in comm.cl.comms:
         c.grid = a.grid
     reducer.comm = comm
@@ -114,6 +116,100 @@ def run(a) -> None:
     print(json.dumps(out), flush=True)
 
 
+def contention(a) -> None:
+    """The memory-system side of the overlap loss, for a PMC pass: the weight-gradient GEMM of
+    a Llama-3-8B MLP projection (dW[4096 x 14336] = X^T dY, K = `--tokens`) alone (phase A),
+    then beside a continuous one-rank 8-GPU two-shot of 1 GiB buckets on a side stream at the
+    full grid (phase B) and at a paced grid of 32 (phase C). Phases are separated by a sleep
+    kernel (the `spin_kernel` marker `--analyze-pmc` splits on). The TCC counters are
+    device-wide: during a GEMM of phase B they count the comm's traffic too.
+
+        tools/gpu.sh pmc "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES" python tools/overlap_trace.py --contention
+        python tools/overlap_trace.py --analyze-pmc gpurun_out/pmc_GRBM_GUI_ACTIVE/run_counter_collection.csv
+    """
+    import torch
+
+    from benchmarks.sections import SoloRehearsalComm
+
+    class _B:
+        def __init__(self, t):
+            self.buffer, self.nbytes = t, t.numel() * t.element_size()
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    x = torch.randn(a.tokens, 4096, dtype=torch.bfloat16, device=dev)
+    dy = torch.randn(a.tokens, 14336, dtype=torch.bfloat16, device=dev)
+    dw = torch.empty(4096, 14336, dtype=torch.bfloat16, device=dev)
+    bucket = torch.zeros((1 << 30) // 2, dtype=torch.bfloat16, device=dev)
+    comm = SoloRehearsalComm([_B(bucket)], 8, 512)
+    side = torch.cuda.Stream(device=dev, priority=-1)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    out: dict = {"tokens": a.tokens, "gemm": "dW[4096 x 14336] = X^T dY (bf16)"}
+
+    def gemms(n: int) -> float:
+        ev[0].record()
+        for _ in range(n):
+            torch.matmul(x.t(), dy, out=dw)
+        ev[1].record()
+        torch.cuda.synchronize(dev)
+        return ev[0].elapsed_time(ev[1]) / n
+
+    gemms(5)
+    for phase, grid in (("A", 0), ("B", 512), ("C", 32)):
+        torch.cuda._sleep(2_000_000)  # the phase marker (spin_kernel)
+        torch.cuda.synchronize(dev)
+        if grid:
+            for c in comm.comms:
+                c.grid = grid
+            with torch.cuda.stream(side):  # enough comm to cover the GEMMs
+                for _ in range(a.comm_calls if grid == 512 else max(2, a.comm_calls // 3)):
+                    comm.allreduce_(bucket, op="avg", stream=side.cuda_stream)
+        out[f"{phase}_gemm_ms"] = round(gemms(a.gemms), 4)
+        torch.cuda.synchronize(dev)
+    comm.check()
+    print(json.dumps(out), flush=True)
+
+
+def analyze_pmc(path: str) -> dict:
+    """Per phase (split on spin_kernel dispatches): medians of the GEMM dispatches' counters."""
+    rows: dict = {}
+    for r in csv.DictReader(open(path)):
+        d = rows.setdefault(int(r["Dispatch_Id"]), {"name": r["Kernel_Name"],
+                                                     "us": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3})
+        d[r["Counter_Name"]] = float(r["Counter_Value"])
+    phase, per = -1, {}
+    for i in sorted(rows):
+        n = rows[i]["name"]
+        if "spin_kernel" in n:
+            phase += 1
+            continue
+        low = n.lower()
+        if phase >= 0 and ("gemm" in low or "cijk" in low):
+            per.setdefault("ABC"[min(phase, 2)], []).append(rows[i])
+    res = {}
+    for ph, ds in per.items():
+        cs = [k for k in ds[0] if k not in ("name",)]
+        med = {k: statistics.median(d[k] for d in ds if k in d) for k in cs}
+        cell = {"gemms": len(ds), "us": round(med["us"], 1)}
+        cyc = med.get("GRBM_GUI_ACTIVE")
+        for k, v in med.items():
+            if k != "us":
+                cell[k] = v
+        if cyc and "SQ_VALU_MFMA_BUSY_CYCLES" in med:  # per CU-cycle: 256 CUs x GUI cycles / 8 XCDs
+            cell["mfma_busy_frac"] = round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (256 * cyc / 8), 4)
+        if "TCC_HIT_sum" in med and "TCC_MISS_sum" in med:
+            cell["l2_hit"] = round(med["TCC_HIT_sum"] / max(1.0, med["TCC_HIT_sum"] + med["TCC_MISS_sum"]), 4)
+        if "TCC_EA0_RDREQ_sum" in med and "TCC_EA0_WRREQ_sum" in med:  # 64-B requests (device-wide)
+            cell["hbm_TBps_device"] = round((med["TCC_EA0_RDREQ_sum"] + med["TCC_EA0_WRREQ_sum"]) * 64 /
+                                            (med["us"] * 1e-6) / 1e12, 3)
+        if "TCP_TCC_READ_REQ_LATENCY_sum" in med and med.get("TCP_TCC_READ_REQ_sum"):
+            cell["l1_to_l2_read_latency_cycles"] = round(med["TCP_TCC_READ_REQ_LATENCY_sum"] / med["TCP_TCC_READ_REQ_sum"], 1)
+        if "TCC_EA0_RDREQ_LEVEL_sum" in med and med.get("TCC_EA0_RDREQ_sum"):
+            cell["ea_read_cycles_in_flight"] = round(med["TCC_EA0_RDREQ_LEVEL_sum"] / med["TCC_EA0_RDREQ_sum"], 1)
+        res[ph] = cell
+    return res
+
+
 def analyze(prefix: str, reps: int) -> dict:
     paths = glob.glob(prefix + "_kernel_trace.csv") or glob.glob(os.path.join(prefix, "**", "*kernel_trace.csv"),
                                                                     recursive=True)
@@ -169,8 +265,16 @@ def main() -> None:
     ap.add_argument("--grid", type=int, default=256, help="workgroups per bucket launch (both logical ranks)")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--analyze", default=None, help="kernel-trace prefix (or directory) to analyse instead of running")
+    ap.add_argument("--contention", action="store_true", help="the GEMM-beside-comm probe for PMC passes")
+    ap.add_argument("--gemms", type=int, default=30)
+    ap.add_argument("--comm-calls", type=int, default=24)
+    ap.add_argument("--analyze-pmc", default=None, help="a PMC pass's counter_collection.csv of --contention")
     a = ap.parse_args()
-    if a.analyze:
+    if a.analyze_pmc:
+        print(json.dumps(analyze_pmc(a.analyze_pmc)))
+    elif a.contention:
+        contention(a)
+    elif a.analyze:
         print(json.dumps(analyze(a.analyze, a.reps), indent=1))
     else:
         run(a)
