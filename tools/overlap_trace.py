@@ -195,8 +195,8 @@ def analyze_pmc(path: str) -> dict:
         for k, v in med.items():
             if k != "us":
                 cell[k] = v
-        if cyc and "SQ_VALU_MFMA_BUSY_CYCLES" in med:  # per CU-cycle: 256 CUs x GUI cycles / 8 XCDs
-            cell["mfma_busy_frac"] = round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (256 * cyc / 8), 4)
+        if cyc and "SQ_VALU_MFMA_BUSY_CYCLES" in med:  # per SIMD-cycle: 1024 SIMDs x GUI cycles / 8 XCDs
+            cell["mfma_busy_frac"] = round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * cyc / 8), 4)
         if "TCC_HIT_sum" in med and "TCC_MISS_sum" in med:
             cell["l2_hit"] = round(med["TCC_HIT_sum"] / max(1.0, med["TCC_HIT_sum"] + med["TCC_MISS_sum"]), 4)
         if "TCC_EA0_RDREQ_sum" in med and "TCC_EA0_WRREQ_sum" in med:  # 64-B requests (device-wide)
