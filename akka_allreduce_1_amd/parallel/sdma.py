@@ -156,60 +156,13 @@ class LocalSdmaCluster:
     releases queued before it, so no rank's wait can hold up a peer's progress."""
 
     def __init__(self, world: int, *, slot_bytes: int = 16 << 20, grid: int = 128, engines_per_peer: int = 0,
-                 timeout_s: float = 10.0, device: int | None = None, placement_tries: int = 1,
-                 placement_bytes: int = 0):
-        """placement_tries > 1: the engines' rate for one set of slabs is bimodal (about 1.7x
-        between modes, profiles/round6/README.md section 3); time one allreduce of
-        `placement_bytes` per rank on each of that many slab sets (the earlier ones held while
-        the next is built) and keep the fastest (`placement` reports the times)."""
+                 timeout_s: float = 10.0, device: int | None = None):
         dev = torch.cuda.current_device() if device is None else device
         self.world = world
         self.device = torch.device("cuda", dev)
-
-        def build():
-            comms = [_H.SdmaComm(k, world, dev, slot_bytes, grid, engines_per_peer, timeout_s) for k in range(world)]
-            for c in comms:
-                c.connect_local(comms)
-            return comms
-
-        self.comms = build()
-        self.placement: dict = {"tries": 1}
-        if placement_tries > 1 and world > 1:
-            self._place(build, placement_tries, placement_bytes or world * (slot_bytes // 2))
-
-    def _place(self, build, tries: int, nbytes: int) -> None:
-        n = max(8, nbytes // 2)
-        xs = [torch.ones(n, dtype=torch.bfloat16, device=self.device) for _ in range(self.world)]
-        ys = [torch.empty_like(x) for x in xs]
-        stream = _current_stream(self.device.index)
-
-        def timed(comms) -> float:
-            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
-            run = lambda: _H.SdmaComm.allreduce_local(comms, [x.data_ptr() for x in xs],  # noqa: E731
-                                                      [y.data_ptr() for y in ys], n, _KERNEL_DTYPES[torch.bfloat16],
-                                                      stream, 1.0)
-            for _ in range(3):
-                run()
-            for a, b in ev:
-                a.record()
-                run()
-                b.record()
-            torch.cuda.synchronize(self.device)
-            return sorted(a.elapsed_time(b) for a, b in ev)[2]
-
-        held, times = [self.comms], [timed(self.comms)]
-        for _ in range(tries - 1):
-            held.append(build())
-            times.append(timed(held[-1]))
-        keep = min(range(len(times)), key=lambda i: times[i])
-        self.comms = held[keep]
-        for i, cs in enumerate(held):
-            if i != keep:
-                for c in cs:
-                    if c.error():
-                        raise CommError(f"SDMA placement probe: {_describe(c.error())}")
-        del held, xs, ys
-        self.placement = {"tries": len(times), "ms": [round(t, 4) for t in times], "kept": keep, "bytes_per_rank": 2 * n}
+        self.comms = [_H.SdmaComm(k, world, dev, slot_bytes, grid, engines_per_peer, timeout_s) for k in range(world)]
+        for c in self.comms:
+            c.connect_local(self.comms)
 
     def allreduce(self, inputs: Sequence[torch.Tensor], outputs: Sequence[torch.Tensor] | None = None, *,
                   op: str = "sum", stream: int | None = None) -> list[torch.Tensor]:

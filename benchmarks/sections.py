@@ -411,8 +411,7 @@ def sdma_local(dev, dtype: torch.dtype = torch.bfloat16, nbytes: int = 256 << 20
         row: dict = {}
         cl = xs = ys = None
         try:
-            cl = LocalSdmaCluster(P, slot_bytes=-(-nbytes // P) + (1 << 20), grid=128, timeout_s=20.0,
-                                  placement_tries=3, placement_bytes=nbytes)
+            cl = LocalSdmaCluster(P, slot_bytes=-(-nbytes // P) + (1 << 20), grid=128, timeout_s=20.0)
             xs = [fill_uniform(torch.empty(n, dtype=dtype, device=dev), seed=900 + k) for k in range(P)]
             ys = [torch.empty_like(x) for x in xs]
             ref = torch.zeros(n, device=dev)
@@ -424,7 +423,7 @@ def sdma_local(dev, dtype: torch.dtype = torch.bfloat16, nbytes: int = 256 << 20
             ok, err, _ = rounding_check(ys, ref, dtype, P)
             del ref
             row.update(validated=ok, max_abs_err=err, engines_per_peer=cl.comms[0].engines_per_peer,
-                       engines_per_rank=cl.comms[0].engines, placement=cl.placement)
+                       engines_per_rank=cl.comms[0].engines)
             for _ in range(10):  # the engines' rate is bimodal run to run (profiles/round6 section 3): warm up
                 cl.allreduce(xs, ys)
             ts = device_times(lambda: cl.allreduce(xs, ys), iters, dev)
