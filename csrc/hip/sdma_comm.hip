@@ -290,10 +290,8 @@ SdmaComm::SdmaComm(int rank, int world, int device, int64_t slot_bytes, int grid
   impl_->cpu = s.cpu;
   // The device's SDMA engines. The ROCm 7.0 runtime torch ships answers the same-agent query
   // with HSA_STATUS_ERROR_INVALID_AGENT (7.2 answers it); the host <-> device directions name
-  // the same engines there. The query reports the engines FREE at the time: engines whose
-  // queues an earlier communicator of this process opened drop out of it (a second
-  // LocalSdmaCluster then ran on about half the engines, 1.44 vs 0.87 ms at 2 x 256 MiB,
-  // profiles/round6/README.md) - so the first answer per device is kept for the process.
+  // the same engines there. The first answer per (dst, src) agent pair is kept for the
+  // process, so every communicator of it picks its engines from the same mask.
   uint32_t mask = engine_mask(device_, impl_->own, impl_->cpu);
   for (int b = 0; b < 32; ++b)
     if (mask & (1u << b)) local_engines_.push_back(1u << b);
