@@ -10,11 +10,21 @@ from akka_allreduce_1_amd._native import C
 from akka_allreduce_1_amd.protocol import AllReduceInput, MemberUp
 
 
+DONE_AT = [0.0]  # perf_counter() at which the last run_cluster's master finished
+
+
 def run_cluster(P, N, chunk, thA, thR, thC, lag, rounds, data=None, wrap=None, stop_after=None, timeout=30):
     """Master + P workers; returns ({k: {iteration: (data, counts)}}, master_state, worker_states)."""
+    import time
+
     system = C.ActorSystem("ClusterSystem", False)
     done = threading.Event()
-    master = system.master(P, thA, thR, thC, lag, N, rounds - 1, chunk, on_finished=lambda r: done.set())
+
+    def finished(r):
+        DONE_AT[0] = time.perf_counter()
+        done.set()
+
+    master = system.master(P, thA, thR, thC, lag, N, rounds - 1, chunk, on_finished=finished)
     outs = {k: {} for k in range(P)}
     lock = threading.Lock()
     data = data or (lambda k, it: (np.arange(N, dtype=np.float32) + it) * (k + 1))
@@ -188,3 +198,32 @@ def test_master_round_deadline_advances_past_a_hung_worker():
     system.shutdown()
     assert st["round_timeouts"] >= 1
     assert all(len(outs[k]) == rounds for k in (0, 1))
+
+
+def test_blocking_straggler_does_not_hold_the_master():
+    """A worker whose dataSource blocks (10 ms per round) must not slow the rounds the fast
+    worker drives at thAllreduce 0.5. Its CompleteAllreduce schedules the master on the
+    straggler's dispatcher thread (the run-next slot); while the straggler's turn goes on with
+    more blocking messages the master must run elsewhere (csrc/runtime/actor_system.cc), not
+    wait for the turn to end - that held every round of the job behind up to 64 blocking
+    messages (profiles/round6/README.md section 6)."""
+    import time
+
+
+    def timed(delay):
+        def data(k, it):
+            if k == 1 and delay:
+                time.sleep(delay)
+            return np.arange(10, dtype=np.float32) + it
+
+        t0 = time.perf_counter()
+        outs, mstate, _ = run_cluster(2, 10, 2, 0.5, 0.5, 0.5, 1, 3000, data=data, timeout=60)
+        assert mstate["round"] >= 2999, mstate
+        return DONE_AT[0] - t0, outs  # to the master's last round (the backlog drains after)
+
+    base, _ = timed(0.0)
+    wall, outs = timed(0.01)
+    assert len(outs[0]) >= 2900  # the fast worker completed (nearly) every round itself
+    assert 0 < len(outs[1]) < 2900  # the straggler completed some rounds during the job (its
+    # CompleteAllreduce is what scheduled the master on its thread)
+    assert wall < 3 * base + 0.25, (wall, base)

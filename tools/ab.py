@@ -95,7 +95,9 @@ def exp_protocol(a) -> None:
     dev = torch.device("cuda", 0)
     for rep in range(a.reps):
         p = protocol_sizes(dev, cases=((40, torch.float32, 2, 2000), (1 << 20, torch.bfloat16, 0, 2000)))
-        row = {"exp": "protocol", "tag": a.tag, "rep": rep,
+        import akka_allreduce_1_amd
+
+        row = {"exp": "protocol", "tag": a.tag, "rep": rep, "pkg": os.path.dirname(akka_allreduce_1_amd.__file__),
                "inproc_us": {k: v.get("us_per_round") for k, v in p.items() if isinstance(v, dict) and "us_per_round" in v},
                "inproc_ok": all(v.get("validated") for v in p.values() if isinstance(v, dict) and "validated" in v)}
         if a.native:
