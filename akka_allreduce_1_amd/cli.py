@@ -101,10 +101,14 @@ def master_main(argv: list[str] | None = None) -> int:
                     help="serve the control bridge (JSON lines, docs/BRIDGE.md) on PORT (0 = any free port)")
     ap.add_argument("--external-rounds", action="store_true",
                     help="bridge clients drive the rounds with StartAllreduce (the master only inits workers)")
+    ap.add_argument("--akka-port", type=int, default=None, metavar="PORT",
+                    help="serve the master as akka.tcp://<system>@host:PORT/user/master (docs/AKKA_WIRE.md)")
     _common(ap)
     args = ap.parse_args(argv)
     if args.bridge is not None:
         args.set.append(f"mxar.bridge.port={args.bridge}")
+    if args.akka_port is not None:
+        args.set.append(f"mxar.akka.port={args.akka_port}")
     if args.external_rounds:
         args.set.append("mxar.bridge.external-rounds=true")
     cfg = _load(args)
@@ -146,11 +150,19 @@ def master_main(argv: list[str] | None = None) -> int:
                            startRound=start_round, on_round=on_round,
                            roundTimeoutMs=int(float(cfg["mxar.allreduce.round-timeout"]) * 1000),
                            externalRounds=bool(cfg["mxar.bridge.external-rounds"]),
-                           bridgePort=int(cfg["mxar.bridge.port"]), bridgeHost=str(cfg["mxar.bridge.host"]))
+                           bridgePort=max(int(cfg["mxar.bridge.port"]), 0 if int(cfg["mxar.akka.port"]) >= 0 else -1),
+                           bridgeHost=str(cfg["mxar.bridge.host"]))
     bridge_port = system.master_bridge_port(master)
     if bridge_port >= 0:
         print(f"[mxar-master] control bridge on {cfg['mxar.bridge.host']}:{bridge_port}"
               f"{' (external rounds)' if cfg['mxar.bridge.external-rounds'] else ''}", flush=True)
+    if int(cfg["mxar.akka.port"]) >= 0:  # a front-end of the bridge (csrc/runtime/akka_endpoint.h)
+        akka_ep = C.akka.start_endpoint(master, port=int(cfg["mxar.akka.port"]), host=str(cfg["mxar.bridge.host"]),
+                                        system=str(cfg["mxar.system-name"]), package=str(cfg["mxar.akka.package"]),
+                                        suid_start=int(cfg["mxar.akka.suid.start-allreduce"]),
+                                        suid_complete=int(cfg["mxar.akka.suid.complete-allreduce"]),
+                                        cookie=str(cfg["mxar.akka.cookie"]))
+        print(f"[mxar-master] akka.tcp endpoint {akka_ep.address} serves {akka_ep.master_path}", flush=True)
     node = C.ClusterNode.start(system, _cluster_cfg(cfg, args.port, ["master"]))
     node.subscribe(master)
     reg = _observe(args, cfg, {"role": "master", "address": node.address})

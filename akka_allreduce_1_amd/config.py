@@ -46,6 +46,11 @@ DEFAULTS: dict[str, Any] = {
     "mxar.bridge.port": -1,                                    # control bridge TCP port (-1 off, 0 any free port)
     "mxar.bridge.host": "127.0.0.1",                           # control bridge listen address
     "mxar.bridge.external-rounds": False,                      # bridge clients drive the rounds (StartAllreduce)
+    "mxar.akka.port": -1,                                      # akka.tcp endpoint of the master (-1 off; docs/AKKA_WIRE.md)
+    "mxar.akka.package": "sample.cluster.allreduce",           # package of the message classes (AllreduceMessage.scala:1)
+    "mxar.akka.cookie": "",                                    # akka.remote.require-cookie (empty: none)
+    "mxar.akka.suid.start-allreduce": 0,                       # serialVersionUID overrides (0: scalac 2.12 model)
+    "mxar.akka.suid.complete-allreduce": 0,
     "mxar.allreduce.round-timeout": 0.0,                       # seconds; 0 = off
     "mxar.engine.device": "cpu",                               # cpu | cuda[:i]
     "mxar.engine.algo": "auto",                                # auto | twoshot | oneshot | rccl

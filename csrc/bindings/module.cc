@@ -35,6 +35,7 @@ using namespace mxar;
 namespace mxar {
 void bind_cluster(py::module_& m);  // csrc/bindings/cluster_bind.cc
 void bind_hip(py::module_& m);      // csrc/hip/hip_bind.cc
+void bind_akka(py::module_& m);     // csrc/bindings/akka_bind.cc
 }  // namespace mxar
 
 namespace mxar {
@@ -873,4 +874,5 @@ PYBIND11_MODULE(_C, m) {
 
   bind_cluster(m);
   bind_hip(m);
+  bind_akka(m);
 }

@@ -17,6 +17,10 @@ namespace mxar {
 struct OutputCheck {
   bool ok = true;
   int64_t chunks = 0, bad_chunks = 0, count_sum = 0;
+  // the first bad chunk: block, chunk, its count, the value at its first element and the
+  // number of distinct values in it
+  int first_block = -1, first_chunk = -1, first_count = 0, first_distinct = 0;
+  float first_value = 0.f;
 };
 
 inline OutputCheck check_power_of_two_output(const std::vector<float>& data, const std::vector<int>& count,
@@ -42,6 +46,13 @@ inline OutputCheck check_power_of_two_output(const std::vector<float>& data, con
                   __builtin_popcountll(static_cast<uint64_t>(v)) == cnt;
       for (int i = lo + 1; good && i < hi; ++i) good = data[i] == v;
       if (!good) {
+        if (r.bad_chunks == 0) {
+          r.first_block = j, r.first_chunk = c, r.first_count = cnt, r.first_value = v;
+          std::vector<float> seen;
+          for (int i = lo; i < hi && seen.size() < 8; ++i)
+            if (std::find(seen.begin(), seen.end(), data[i]) == seen.end()) seen.push_back(data[i]);
+          r.first_distinct = static_cast<int>(seen.size());
+        }
         ++r.bad_chunks;
         r.ok = false;
       }

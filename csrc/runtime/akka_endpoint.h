@@ -1,0 +1,124 @@
+// Akka classic-remoting front-end of the control bridge: an Akka 2.5 client (akka.tcp, Java
+// serialization - the reference's own stack, build.sbt:3, application.conf:5-9) drives the
+// rounds with the reference's messages instead of JSON lines (VERDICT
+// round 5 "Akka wire compatibility").
+//
+// The endpoint listens as the actor system `akka.tcp://<system>@<host>:<port>` and serves one
+// actor, `/user/<master>` (AllreduceMaster.scala:132: name "master"):
+//   client -> endpoint
+//     association handshake (ASSOCIATE both ways), transport heartbeats
+//     StartAllreduce(round)   to /user/master, by ActorRef or ActorSelection (Java serializer)
+//                             -> the bridge's StartAllreduce; the sender becomes a subscriber
+//     Identify(id)            (resolveOne / actorSelection ? Identify) -> ActorIdentity(id,
+//                             Some(master)) for /user/master, ActorIdentity(id, None) otherwise
+//     remote-watcher Heartbeat -> HeartbeatRsp(uid) (context.watch(master) keeps working)
+//     sequenced system messages (Watch, ...) are acknowledged and otherwise ignored
+//   endpoint -> subscribers
+//     CompleteAllreduce(srcId, round) for every worker completion the master sees - the
+//     messages AllreduceMaster.scala:58-67 counts (AllreduceWorker.scala:246-251 sends them)
+// Payloads never cross it (docs/BRIDGE.md). Cluster membership gossip is not spoken: workers
+// join the engine's own cluster, the Akka client only drives and observes rounds.
+//
+// Threads: one acceptor; per association a reader and a writer with a bounded outbound
+// queue (a client that stops reading is dropped, the master never blocks on it). The
+// writer also sends the transport heartbeat. Every thread holds a strong reference to the
+// endpoint; stop() (the bridge's stop hooks call it) ends them.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../cluster/akka_wire.h"
+#include "control_bridge.h"
+
+namespace mxar {
+
+class AkkaEndpoint : public std::enable_shared_from_this<AkkaEndpoint> {
+ public:
+  struct Options {
+    std::string host = "127.0.0.1";
+    int port = 0;                                      // 0 = any free port
+    std::string system = "ClusterSystem";              // AllreduceMaster.scala:125
+    std::string master = "master";                     // AllreduceMaster.scala:132
+    std::string package = "sample.cluster.allreduce";  // AllreduceMessage.scala:1
+    int64_t suid_start = 0;     // serialVersionUID overrides (0 = scalac 2.12 model)
+    int64_t suid_complete = 0;
+    double heartbeat_s = 1.0;   // transport heartbeat period
+    std::string cookie;         // akka.remote.require-cookie: non-empty = required
+  };
+  struct Stats {
+    uint64_t associations = 0, frames_in = 0, frames_out = 0, starts = 0, completes_sent = 0,
+             identifies = 0, watcher_heartbeats = 0, system_messages = 0, unsupported = 0,
+             suid_mismatches = 0, rejected = 0;
+    int64_t client_suid_start = 0;  // the SUID the last client's StartAllreduce carried
+  };
+
+  static std::shared_ptr<AkkaEndpoint> start(std::shared_ptr<ControlBridge> bridge, Options o);
+  ~AkkaEndpoint();
+  AkkaEndpoint(const AkkaEndpoint&) = delete;
+  AkkaEndpoint& operator=(const AkkaEndpoint&) = delete;
+
+  int port() const { return port_; }
+  std::string address() const;      // akka.tcp://System@host:port
+  std::string master_path() const;   // .../user/master#uid (what ActorIdentity returns)
+  int64_t suid_start() const { return suid_start_; }
+  int64_t suid_complete() const { return suid_complete_; }
+  Stats stats() const;
+  size_t associations() const;
+  void stop();
+
+ private:
+  struct Assoc {
+    ~Assoc();
+    int fd = -1;
+    uint64_t tap = 0;
+    std::mutex wmu;
+    std::condition_variable wcv;
+    std::deque<std::string> out;
+    size_t queued = 0;
+    std::thread reader, writer;
+    std::atomic<bool> dead{false};
+    akka::Address remote;
+    uint64_t remote_uid = 0;
+    std::mutex smu;
+    std::vector<std::string> subscribers;  // actor paths that sent StartAllreduce
+    void kill();
+  };
+
+  AkkaEndpoint() = default;
+  void accept_loop(std::shared_ptr<AkkaEndpoint> self);
+  void read_loop(std::shared_ptr<AkkaEndpoint> self, std::shared_ptr<Assoc> a);
+  void write_loop(std::shared_ptr<AkkaEndpoint> self, std::shared_ptr<Assoc> a);
+  bool send_pdu(Assoc& a, const std::string& pdu);
+  void send_message(Assoc& a, const std::string& recipient, const akka::SerializedMsg& m);
+  void on_envelope(Assoc& a, const akka::Envelope& e);
+  void deliver(Assoc& a, std::vector<std::string> elems, const akka::SerializedMsg& m, const std::string& sender);
+  void on_line(Assoc& a, const std::string& line);
+  void reap();
+  void warn_once(const std::string& key, const std::string& what);
+
+  Options opt_;
+  std::shared_ptr<ControlBridge> bridge_;
+  int lfd_ = -1;
+  int wake_[2] = {-1, -1};
+  int port_ = 0;
+  uint64_t uid_ = 0;
+  int64_t suid_start_ = 0, suid_complete_ = 0;
+  std::atomic<bool> stop_{false};
+  std::thread acceptor_;
+  mutable std::mutex mu_;
+  std::vector<std::shared_ptr<Assoc>> assocs_;
+  std::vector<std::string> warned_;
+  std::atomic<uint64_t> n_assoc_{0}, n_in_{0}, n_out_{0}, n_start_{0}, n_complete_{0}, n_identify_{0},
+      n_rh_{0}, n_sys_{0}, n_unsup_{0}, n_suid_{0}, n_rej_{0};
+  std::atomic<int64_t> client_suid_{0};
+};
+
+}  // namespace mxar

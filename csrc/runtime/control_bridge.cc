@@ -222,21 +222,60 @@ void ControlBridge::write_loop(std::shared_ptr<ControlBridge> self, std::shared_
 
 void ControlBridge::publish(const std::string& line) {
   std::vector<std::shared_ptr<Client>> cs;
+  std::vector<Tap> ts;
   {
     std::lock_guard<std::mutex> g(mu_);
     cs = clients_;
+    for (auto& t : taps_) ts.push_back(t.second);
   }
   for (auto& c : cs) write_line(*c, line);
+  for (auto& t : ts) t(line);
 }
 
 void ControlBridge::reply(uint64_t client, const std::string& line) {
   std::shared_ptr<Client> c;
+  Tap tap;
   {
     std::lock_guard<std::mutex> g(mu_);
     for (auto& x : clients_)
       if (x->id == client) c = x;
+    for (auto& t : taps_)
+      if (t.first == client) tap = t.second;
   }
   if (c) write_line(*c, line);
+  if (tap) tap(line);
+}
+
+uint64_t ControlBridge::add_tap(Tap tap) {
+  std::lock_guard<std::mutex> g(mu_);
+  const uint64_t id = next_id_++;  // shares the client id space: replies find it by id
+  taps_.emplace_back(id, std::move(tap));
+  return id;
+}
+
+void ControlBridge::remove_tap(uint64_t id) {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto it = taps_.begin(); it != taps_.end(); ++it)
+    if (it->first == id) {
+      taps_.erase(it);
+      return;
+    }
+}
+
+bool ControlBridge::submit(const BridgeCommand& cmd) {
+  ActorRef m;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    m = master_;
+  }
+  if (!m) return false;
+  m->tell(Message(cmd), nullptr);
+  return true;
+}
+
+void ControlBridge::on_stop(std::function<void()> hook) {
+  std::lock_guard<std::mutex> g(mu_);
+  stop_hooks_.push_back(std::move(hook));
 }
 
 void ControlBridge::reap() {  // join readers of clients that went away (mu_ not held)
@@ -354,6 +393,12 @@ void ControlBridge::read_loop(std::shared_ptr<ControlBridge> self, std::shared_p
 
 void ControlBridge::stop() {
   if (stop_.exchange(true)) return;
+  std::vector<std::function<void()>> hooks;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    hooks.swap(stop_hooks_);
+  }
+  for (auto& h : hooks) h();
   if (wake_[1] >= 0) {
     char x = 1;
     (void)!::write(wake_[1], &x, 1);
@@ -371,6 +416,7 @@ void ControlBridge::stop() {
   {
     std::lock_guard<std::mutex> g(mu_);
     cs.swap(clients_);
+    taps_.clear();
     master_ = nullptr;
   }
   for (auto& c : cs) {

@@ -1,11 +1,11 @@
 // Control bridge: the master's round protocol over a language-neutral line protocol.
 //
-// SURVEY §7.5 item 3 ("existing Akka client can drive it"): real Akka wire compatibility
-// would mean Akka classic remoting plus Java serialization, i.e. a JVM on
-// the control path. Instead the bridge carries the reference's CONTROL messages with the
-// reference's names and field names as JSON lines over TCP, so a JVM client needs only a
-// socket and a JSON printer (examples/akka_bridge/BridgeDriver.scala). Payloads never
-// cross it: data stays on the workers' planes (HBM / xGMI).
+// SURVEY §7.5 item 3 ("existing Akka client can drive it"): the bridge carries the
+// reference's CONTROL messages with the reference's names and field names as JSON lines over
+// TCP, so any client needs only a socket and a JSON printer
+// (examples/akka_bridge/BridgeDriver.scala). An Akka client that speaks only akka.tcp uses
+// the bridge's Akka front-end instead (csrc/runtime/akka_endpoint.h, docs/AKKA_WIRE.md).
+// Payloads never cross either: data stays on the workers' planes (HBM / xGMI).
 //
 // The client plays the round driver of AllreduceMaster.scala:58-67,91-97; the master
 // (MasterParams.externalRounds) keeps membership, dense ids and InitWorkers (:38-56,84-89).
@@ -40,6 +40,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -73,6 +74,15 @@ class ControlBridge : public std::enable_shared_from_this<ControlBridge> {
   // Remember the latest InitWorkers line for clients that connect later.
   void set_init_line(std::string line);
   size_t clients() const;
+  // In-process front-ends (csrc/runtime/akka_endpoint.h) speak other wire formats: a tap gets
+  // every event line and the replies addressed to its id (it must not block), submit()
+  // forwards a command as a client's would (false without a master). on_stop() hooks run in
+  // stop(), before the clients are dropped.
+  using Tap = std::function<void(const std::string& line)>;
+  uint64_t add_tap(Tap tap);
+  void remove_tap(uint64_t id);
+  bool submit(const BridgeCommand& cmd);
+  void on_stop(std::function<void()> hook);
   // Outbound queue cap per client (bytes, default kMaxQueuedBytes); tests lower it.
   void set_max_queued_bytes(size_t b) { max_queued_.store(b); }
   void stop();
@@ -114,6 +124,8 @@ class ControlBridge : public std::enable_shared_from_this<ControlBridge> {
   ActorRef master_;
   std::string master_path_;
   std::string init_line_;
+  std::vector<std::pair<uint64_t, Tap>> taps_;
+  std::vector<std::function<void()>> stop_hooks_;
 };
 
 }  // namespace mxar

@@ -42,6 +42,7 @@
 #include "../cluster/cluster_node.h"
 #include "../core/log.h"
 #include "../core/output_check.h"
+#include "../runtime/akka_endpoint.h"
 #include "../runtime/allreduce_actors.h"
 #include "../runtime/plane_worker.h"
 #include "gpu_worker.h"
@@ -69,6 +70,9 @@ struct Options {
   float th_allreduce = 1.f, th_reduce = 0.9f, th_complete = 0.8f;  // AllreduceMaster.scala:105-107
   int bridge_port = -1;                 // --bridge PORT (control bridge, docs/BRIDGE.md)
   bool external_rounds = false;         // --external-rounds
+  int akka_port = -1;                   // --akka-port PORT (akka.tcp endpoint, docs/AKKA_WIRE.md)
+  std::string akka_package = "sample.cluster.allreduce", akka_cookie;
+  int64_t akka_suid_start = 0, akka_suid_complete = 0;
   bool lockstep = false;                // drive: start the next round only after the barrier
   int max_lag = 1, max_round = 100, round_timeout_ms = 0;          // :108-109
   std::string loglevel = "INFO";
@@ -107,6 +111,8 @@ void apply_spin(int us) {
                "options: --host H --seeds a[,b] --th-allreduce F --th-reduce F --th-complete F --max-lag N\n"
                "         --max-round N --round-timeout-ms N --loglevel L --quiet\n"
                "master control bridge (docs/BRIDGE.md): --bridge PORT [--external-rounds]\n"
+               "master akka.tcp endpoint (docs/AKKA_WIRE.md): --akka-port PORT [--akka-package P --akka-cookie C\n"
+               "                              --akka-suid-start N --akka-suid-complete N]\n"
                "       mxar drive [host:]bridgePort [rounds] [--lockstep]   (bridge client)\n"
                "worker on a GPU (mxar-gpu): --device K [--max-peers N --plane-max-lag N --grid N --plane-timeout S\n"
                "                              --min-chunk N --source iota|static --dtype fp32|bf16|fp16\n"
@@ -137,6 +143,11 @@ Options parse(int argc, char** argv) {
     else if (a == "--round-timeout-ms") o.round_timeout_ms = std::stoi(val());
     else if (a == "--bridge") o.bridge_port = std::stoi(val());
     else if (a == "--external-rounds") o.external_rounds = true;
+    else if (a == "--akka-port") o.akka_port = std::stoi(val());
+    else if (a == "--akka-package") o.akka_package = val();
+    else if (a == "--akka-cookie") o.akka_cookie = val();
+    else if (a == "--akka-suid-start") o.akka_suid_start = std::stoll(val());
+    else if (a == "--akka-suid-complete") o.akka_suid_complete = std::stoll(val());
     else if (a == "--lockstep") o.lockstep = true;
     else if (a == "--loglevel") o.loglevel = val();
     else if (a == "--quiet") o.quiet = true;
@@ -207,15 +218,28 @@ void set_level(const std::string& l) {
   };
   auto master_actor = std::make_unique<MasterActor>(mp, [&](int rounds) { finished = rounds; }, on_round);
   std::shared_ptr<ControlBridge> bridge;
-  if (o.bridge_port >= 0) {
-    bridge = ControlBridge::start(o.host, o.bridge_port);
+  if (o.bridge_port >= 0 || o.akka_port >= 0) {  // the akka.tcp endpoint is a front-end of the bridge
+    bridge = ControlBridge::start(o.host, o.bridge_port >= 0 ? o.bridge_port : 0);
     master_actor->set_bridge(bridge);
   }
   ActorRef master = sys->actor_of(std::move(master_actor), "master");
+  std::shared_ptr<AkkaEndpoint> akka_ep;
   if (bridge) {
     bridge->attach(master, master->path());
     std::printf("[mxar master] control bridge on %s:%d%s\n", o.host.c_str(), bridge->port(),
                 o.external_rounds ? " (external rounds)" : "");
+    if (o.akka_port >= 0) {
+      AkkaEndpoint::Options ao;
+      ao.host = o.host;
+      ao.port = o.akka_port;
+      ao.package = o.akka_package;
+      ao.cookie = o.akka_cookie;
+      ao.suid_start = o.akka_suid_start;
+      ao.suid_complete = o.akka_suid_complete;
+      akka_ep = AkkaEndpoint::start(bridge, ao);
+      std::printf("[mxar master] akka.tcp endpoint %s serves %s\n", akka_ep->address().c_str(),
+                  akka_ep->master_path().c_str());
+    }
   }
   ClusterConfig cc;
   cc.host = o.host;
@@ -246,6 +270,7 @@ void set_level(const std::string& l) {
   std::fflush(stdout);
   node->leave();
   std::this_thread::sleep_for(std::chrono::milliseconds(200));  // let the Leave / Removed frames go out
+  if (akka_ep) akka_ep->stop();  // DISASSOCIATE_SHUTTING_DOWN to its clients
   node->shutdown();
   sys->shutdown();
   exit_now(finished.load() >= 0 ? 0 : 1);
@@ -354,7 +379,7 @@ PlaneWorkerStats plane_worker_stats(const ActorRef& ref) {
   if (gpu_at_exit) gpu_at_exit();
   {
     std::lock_guard<std::mutex> g(last_mu);
-    std::string check = "null";
+    std::string check = "null", check_detail = "null";
     int last_round = -1;
     if (last) {
       const std::vector<float> d = last->data->to_host();
@@ -365,9 +390,17 @@ PlaneWorkerStats plane_worker_stats(const ActorRef& ref) {
         const int peers = plane_worker ? plane_worker_peers(plane_worker) : 0;
         const OutputCheck c = check_power_of_two_output(d, last->count, peers, o.check_chunk);
         check = c.ok ? "true" : "false";
-        if (!c.ok)
+        if (!c.ok) {
           std::printf("[mxar worker] check failed: %lld of %lld chunks\n", static_cast<long long>(c.bad_chunks),
                       static_cast<long long>(c.chunks));
+          char b[256];
+          std::snprintf(b, sizeof(b),
+                        "{\"bad_chunks\": %lld, \"chunks\": %lld, \"peers\": %d, \"block\": %d, \"chunk\": %d, "
+                        "\"count\": %d, \"value\": %g, \"distinct\": %d}",
+                        static_cast<long long>(c.bad_chunks), static_cast<long long>(c.chunks), peers, c.first_block,
+                        c.first_chunk, c.first_count, static_cast<double>(c.first_value), c.first_distinct);
+          check_detail = b;
+        }
       }
       last.reset();
     }
@@ -385,13 +418,14 @@ PlaneWorkerStats plane_worker_stats(const ActorRef& ref) {
       if (plane_worker) ps = plane_worker_stats(plane_worker);
       std::printf("{\"worker_summary\": {\"rounds\": %zu, \"last_round\": %d, \"period_p50_us\": %.2f, "
                   "\"period_p99_us\": %.2f, \"period_mean_us\": %.2f, \"count_mean\": %.4f, \"count_zero_frac\": %.4f, "
-                  "\"forced\": %llu, \"cold\": %llu, \"coalesced\": %llu, \"plane_errors\": %llu, \"validated\": %s}}\n",
+                  "\"forced\": %llu, \"cold\": %llu, \"coalesced\": %llu, \"plane_errors\": %llu, \"validated\": %s, "
+                  "\"check_detail\": %s}}\n",
                   sink_t.size(), last_round, iv[iv.size() / 2], iv[std::min(iv.size() - 1, iv.size() * 99 / 100)], mean,
                   count_n ? static_cast<double>(count_sum) / static_cast<double>(count_n) : 0.0,
                   count_n ? static_cast<double>(count_zero) / static_cast<double>(count_n) : 0.0,
                   static_cast<unsigned long long>(ps.forced_completions), static_cast<unsigned long long>(ps.cold_rounds),
                   static_cast<unsigned long long>(ps.starts_coalesced), static_cast<unsigned long long>(ps.plane_errors),
-                  check.c_str());
+                  check.c_str(), check_detail.c_str());
     }
   }
   std::printf("[mxar worker] %d rounds completed\n", rounds.load());
