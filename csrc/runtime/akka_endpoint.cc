@@ -224,7 +224,11 @@ void AkkaEndpoint::write_loop(std::shared_ptr<AkkaEndpoint> self, std::shared_pt
   for (;;) {
     {
       std::unique_lock<std::mutex> g(a->wmu);
-      a->wcv.wait_until(g, next_hb, [&] { return !a->out.empty() || a->dead.load(); });
+      // a system_clock deadline: pthread_cond_timedwait (a steady_clock wait_until becomes
+      // pthread_cond_clockwait, which this toolchain's ThreadSanitizer does not intercept)
+      const auto left = next_hb - std::chrono::steady_clock::now();
+      a->wcv.wait_until(g, std::chrono::system_clock::now() + left,
+                        [&] { return !a->out.empty() || a->dead.load(); });
       if (a->dead.load()) return;
       buf.clear();
       size_t frames = 0;

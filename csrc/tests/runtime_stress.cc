@@ -23,6 +23,7 @@
 #include "../cluster/cluster_node.h"
 #include "../core/log.h"
 #include "../runtime/allreduce_actors.h"
+#include "../runtime/akka_endpoint.h"
 #include "../runtime/control_bridge.h"
 #include "../runtime/fault_injector.h"
 #include "../runtime/loopback_plane.h"
@@ -404,6 +405,155 @@ static int run_mailbox(int producers, int per) {
   return 0;
 }
 
+// The akka.tcp front-end (csrc/runtime/akka_endpoint.h): a driver associates and runs every
+// round with Java-serialized StartAllreduce by ActorSelection, counting CompleteAllreduce;
+// churn threads associate and vanish, send garbage or a frame without a handshake; the
+// system shuts down with the driver still associated (the endpoint's stop hook) - the
+// endpoint's acceptor / reader / writer threads and the bridge's taps under the sanitizer.
+static int run_akka(int P, int N, int C, int rounds) {
+  auto sys = std::make_shared<ActorSystem>("ClusterSystem", ActorSystem::Mode::Threaded, 4);
+  std::atomic<bool> done{false};
+  MasterParams mp{P, 1.f, 1.f, 1.f, 1, N, rounds - 1, C, false};
+  mp.externalRounds = true;
+  auto actor = std::make_unique<MasterActor>(mp, [&](int) { done = true; });
+  auto bridge = ControlBridge::start("127.0.0.1", 0);
+  actor->set_bridge(bridge);
+  ActorRef master = sys->actor_of(std::move(actor), "master");
+  bridge->attach(master, master->path());
+  AkkaEndpoint::Options ao;
+  ao.heartbeat_s = 0.002;  // heartbeats race the replies on every writer
+  auto ep = AkkaEndpoint::start(bridge, ao);
+  const int port = ep->port();
+  for (int k = 0; k < P; ++k) {
+    DataSource src = [N](const AllReduceInputRequest& r) {
+      std::vector<float> v(N, static_cast<float>(r.iteration));
+      return AllReduceInput{make_host_payload(std::move(v))};
+    };
+    ActorRef w = sys->actor_of(std::make_unique<WorkerActor>(src, [](const AllReduceOutput&) {}),
+                               "worker" + std::to_string(k));
+    master->tell(MemberUp{w, "worker", ""}, nullptr);
+  }
+  auto send_frame = [](int fd, const std::string& pdu) {
+    std::string f(4, '\0');
+    for (int k = 0; k < 4; ++k) f[static_cast<size_t>(k)] = static_cast<char>(pdu.size() >> (24 - 8 * k));
+    f += pdu;
+    (void)!::send(fd, f.data(), f.size(), MSG_NOSIGNAL);
+  };
+  auto read_frame = [](int fd, std::string& body) {
+    char h[4];
+    size_t got = 0;
+    while (got < 4) {
+      ssize_t n = ::recv(fd, h + got, 4 - got, 0);
+      if (n <= 0) return false;
+      got += static_cast<size_t>(n);
+    }
+    size_t len = 0;
+    for (char c : h) len = len << 8 | static_cast<uint8_t>(c);
+    body.resize(len);
+    got = 0;
+    while (got < len) {
+      ssize_t n = ::recv(fd, body.data() + got, len - got, 0);
+      if (n <= 0) return false;
+      got += static_cast<size_t>(n);
+    }
+    return true;
+  };
+  akka::Address me;
+  me.system = "Driver";
+  me.host = "127.0.0.1";
+  me.port = 1;
+  std::atomic<bool> stop_churn{false};
+  std::vector<std::thread> churn;
+  for (int t = 0; t < 3; ++t)
+    churn.emplace_back([&, t] {
+      for (int i = 0; !stop_churn.load(); ++i) {
+        int fd = connect_to(port);
+        if (fd < 0) continue;
+        if ((i + t) % 3 == 0) {
+          send_frame(fd, akka::encode_associate(me, 7, ""));
+          std::string b;
+          (void)read_frame(fd, b);
+        } else if ((i + t) % 3 == 1) {
+          send_frame(fd, akka::encode_payload_pdu("x"));
+        } else {
+          (void)!::send(fd, "\xff\xff\xff\xff", 4, MSG_NOSIGNAL);
+        }
+        ::close(fd);
+      }
+    });
+  std::string err;
+  int completed = 0;
+  int fd = -1;
+  for (int i = 0; i < 100 && fd < 0; ++i) fd = connect_to(port);
+  send_frame(fd, akka::encode_associate(me, 42, ""));
+  const std::string self = me.str() + "/user/driver";
+  auto start = [&](int r) {
+    akka::JavaObject o;
+    o.class_name = "sample.cluster.allreduce.StartAllreduce";
+    o.suid = ep->suid_start();
+    o.fields = {{'I', "round", r, 0.0}};
+    akka::SerializedMsg inner;
+    inner.serializer = akka::kJavaSerializer;
+    inner.bytes = akka::java_serialize(o);
+    akka::Envelope e;
+    e.has_envelope = true;
+    e.recipient = ep->address() + "/";
+    e.msg.serializer = akka::kContainerSerializer;
+    e.msg.bytes = akka::encode_selection(inner, {{1, "user"}, {1, "master"}}, false);
+    e.has_sender = true;
+    e.sender = self;
+    send_frame(fd, akka::encode_payload_pdu(akka::encode_container(e)));
+  };
+  std::string body;
+  int seen = 0;
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(60);
+  start(0);
+  while (completed < rounds && std::chrono::steady_clock::now() < deadline) {
+    if (!read_frame(fd, body)) {
+      err = "driver association closed";
+      break;
+    }
+    akka::Pdu pdu;
+    akka::Envelope env;
+    akka::JavaObject o;
+    if (!akka::decode_pdu(body, pdu)) {
+      err = "undecodable PDU";
+      break;
+    }
+    if (!pdu.is_payload || !akka::decode_container(pdu.payload, env) || !env.has_envelope) continue;
+    if (env.recipient != self || !akka::java_deserialize(env.msg.bytes, o) || o.fields.size() != 2) {
+      err = "unexpected message to " + env.recipient;
+      break;
+    }
+    const int round = static_cast<int>(o.fields[0].i);  // fields in stream order: round, srcId
+    if (round != completed) continue;
+    if (++seen == P) {
+      seen = 0;
+      if (++completed < rounds) start(completed);
+    }
+  }
+  stop_churn = true;
+  for (auto& t : churn) t.join();
+  const bool ok = err.empty() && completed == rounds && wait_until([&] { return done.load(); }, 30);
+  const auto st = ep->stats();
+  sys->await_idle(std::chrono::milliseconds(5000));
+  sys->shutdown();  // the master's bridge stop runs the endpoint's stop: the driver is told
+  std::string bye;
+  akka::Pdu last;
+  bool told = false;
+  while (read_frame(fd, bye))
+    if (akka::decode_pdu(bye, last) && !last.is_payload && last.command == akka::kShuttingDown) told = true;
+  ::close(fd);
+  bridge.reset();
+  ep.reset();
+  if (!ok || !told || st.starts != static_cast<uint64_t>(rounds)) {
+    std::fprintf(stderr, "akka-driven job failed: %s (rounds %d, starts %llu, shutdown notice %d)\n", err.c_str(),
+                 completed, static_cast<unsigned long long>(st.starts), told);
+    return 1;
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   Logger::get().set_level(LogLevel::ERROR);
   const std::string only = argc > 1 ? argv[1] : "";
@@ -415,6 +565,7 @@ int main(int argc, char** argv) {
   if (rc == 0 && (only.empty() || only == "plane")) rc = run_plane(3, 41, 4, 40);
   if (rc == 0 && (only.empty() || only == "bridge")) rc = run_bridge(3, 23, 4, 60);
   if (rc == 0 && (only.empty() || only == "bridge_teardown")) rc = run_bridge_teardown(3, 23, 4, 400);
+  if (rc == 0 && (only.empty() || only == "akka")) rc = run_akka(3, 23, 4, 60);
   std::printf(rc == 0 ? "runtime_stress: OK\n" : "runtime_stress: FAILED\n");
   return rc;
 }
