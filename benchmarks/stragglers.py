@@ -283,6 +283,11 @@ def native_job(n: int, chunk: int, rounds: int, *, th_reduce: float, th_complete
         m = subprocess.run([os.path.join(exe, "mxar"), "master", str(port), "2", str(n), str(chunk),
                             "--th-allreduce", str(th_all), "--th-reduce", str(th_reduce), "--th-complete",
                             str(th_complete), "--max-lag", str(max_lag), "--max-round", str(rounds - 1),
+                            # both workers before the first init: below thAllreduce = 1 the
+                            # reference starts with the first worker up and restarts the job at
+                            # round 0 when the second joins (a lone-worker epoch, or a job that
+                            # ends before the second worker ever joins)
+                            "--init-workers", "2",
                             "--spin-us", "500"] + seeds + ["--quiet"],
                            capture_output=True, text=True, timeout=timeout, env=env)
         outs = []

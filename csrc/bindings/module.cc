@@ -617,10 +617,10 @@ PYBIND11_MODULE(_C, m) {
                         int maxLag, int dataSize, int maxRound, int maxChunkSize, bool liveBarrier,
                         py::object on_finished, std::string name, int startRound, py::object on_round,
                         int roundTimeoutMs, bool reinitOnLoss, bool resumeOnJoin, bool externalRounds,
-                        int bridgePort, std::string bridgeHost) {
+                        int bridgePort, std::string bridgeHost, int initWorkers) {
             MasterParams p{totalWorkers, thAllreduce, thReduce, thComplete, maxLag, dataSize, maxRound,
                            maxChunkSize, liveBarrier, startRound, roundTimeoutMs, reinitOnLoss, resumeOnJoin,
-                           externalRounds};
+                           externalRounds, initWorkers};
             MasterActor::RoundCallback rcb;
             if (!on_round.is_none()) {
               auto h = std::make_shared<PyCallable>(std::move(on_round));
@@ -651,7 +651,7 @@ PYBIND11_MODULE(_C, m) {
           py::arg("liveBarrier") = false, py::arg("on_finished") = py::none(), py::arg("name") = "master",
           py::arg("startRound") = 0, py::arg("on_round") = py::none(), py::arg("roundTimeoutMs") = 0,
           py::arg("reinitOnLoss") = false, py::arg("resumeOnJoin") = false, py::arg("externalRounds") = false,
-          py::arg("bridgePort") = -1, py::arg("bridgeHost") = "127.0.0.1",
+          py::arg("bridgePort") = -1, py::arg("bridgeHost") = "127.0.0.1", py::arg("initWorkers") = 0,
           "bridgePort >= 0 starts a control bridge (csrc/runtime/control_bridge.h; 0 = any free port, see "
           "master_bridge_port); externalRounds makes its clients drive the rounds")
       .def("master_bridge_port", [](ActorSystem&, ActorRef ref) {

@@ -25,7 +25,9 @@ void MasterCore::on_member_up(int handle) {
     if (!external_idle()) start_allreduce();
     return;
   }
-  if (static_cast<int>(workers_.size()) >= f32_threshold_count(p_.thAllreduce, p_.totalWorkers)) {
+  const int need = round_ < 0 ? std::max(p_.initWorkers, f32_threshold_count(p_.thAllreduce, p_.totalWorkers))
+                              : f32_threshold_count(p_.thAllreduce, p_.totalWorkers);
+  if (static_cast<int>(workers_.size()) >= need) {
     MXAR_LOG(INFO, "master", "----" << workers_.size() << " (out of " << p_.totalWorkers << ") workers are up");
     init_workers();
     round_ = std::max(0, p_.startRound);

@@ -51,6 +51,11 @@ struct MasterParams {
   // client plays AllreduceMaster.scala:58-67,91-97 while this master keeps membership,
   // ids and InitWorkers.
   bool externalRounds = false;
+  // Extension: the FIRST initialisation waits for at least this many registered workers
+  // (0: the reference's totalWorkers * thAllreduce, AllreduceMaster.scala:42). Below
+  // thAllreduce = 1 the reference starts the job with the first workers up and restarts it
+  // at round 0 when the next one joins; a deployment that knows its size asks for it here.
+  int initWorkers = 0;
 };
 
 class MasterEffects {

@@ -75,6 +75,7 @@ struct Options {
   int64_t akka_suid_start = 0, akka_suid_complete = 0;
   bool lockstep = false;                // drive: start the next round only after the barrier
   int max_lag = 1, max_round = 100, round_timeout_ms = 0;          // :108-109
+  int init_workers = 0;  // --init-workers N: the first init waits for N workers (MasterParams.initWorkers)
   std::string loglevel = "INFO";
   bool quiet = false;
   int device = -1;  // worker: >= 0 runs the rounds on this GPU (mxar-gpu)
@@ -109,7 +110,7 @@ void apply_spin(int us) {
                "%s\nusage: mxar master [port totalWorkers dataSize maxChunkSize] [options]\n"
                "       mxar worker [port sourceDataSize] [options]\n"
                "options: --host H --seeds a[,b] --th-allreduce F --th-reduce F --th-complete F --max-lag N\n"
-               "         --max-round N --round-timeout-ms N --loglevel L --quiet\n"
+               "         --max-round N --round-timeout-ms N --init-workers N --loglevel L --quiet\n"
                "master control bridge (docs/BRIDGE.md): --bridge PORT [--external-rounds]\n"
                "master akka.tcp endpoint (docs/AKKA_WIRE.md): --akka-port PORT [--akka-package P --akka-cookie C\n"
                "                              --akka-suid-start N --akka-suid-complete N]\n"
@@ -141,6 +142,7 @@ Options parse(int argc, char** argv) {
     else if (a == "--max-lag") o.max_lag = std::stoi(val());
     else if (a == "--max-round") o.max_round = std::stoi(val());
     else if (a == "--round-timeout-ms") o.round_timeout_ms = std::stoi(val());
+    else if (a == "--init-workers") o.init_workers = std::stoi(val());
     else if (a == "--bridge") o.bridge_port = std::stoi(val());
     else if (a == "--external-rounds") o.external_rounds = true;
     else if (a == "--akka-port") o.akka_port = std::stoi(val());
@@ -207,6 +209,7 @@ void set_level(const std::string& l) {
   mp.maxChunkSize = chunk;
   mp.roundTimeoutMs = o.round_timeout_ms;
   mp.externalRounds = o.external_rounds;
+  mp.initWorkers = o.init_workers;
   apply_spin(o.spin_us);
   auto sys = std::make_shared<ActorSystem>("ClusterSystem", ActorSystem::Mode::Threaded, 2);
   std::atomic<int> finished{-1};

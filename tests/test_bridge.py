@@ -452,3 +452,39 @@ def test_client_that_never_reads_does_not_stall_the_master():
     finally:
         lazy.close()
         system.shutdown()
+
+
+@pytest.mark.parametrize("init_workers", [0, 2])
+def test_init_workers_waits_for_the_whole_membership(init_workers):
+    """MasterParams.initWorkers: below thAllreduce = 1 the reference initialises with the first
+    workers up (AllreduceMaster.scala:42) and restarts at round 0 when the next one joins;
+    initWorkers = N makes the first init wait for N workers."""
+    n, chunk, rounds = 8, 2, 6
+    system = C.ActorSystem(f"InitW{init_workers}", False)
+    fin = threading.Event()
+    outs = [dict(), dict()]
+
+    def sink(k):
+        return lambda out: outs[k].__setitem__(out.iteration, list(out.count))
+
+    try:
+        master = system.master(2, 0.5, 1.0, 1.0, 1, n, rounds - 1, chunk, on_finished=lambda r: fin.set(),
+                               initWorkers=init_workers)
+        w0 = system.worker(lambda req: AllReduceInput(host_iota_source(n, 0.0)(req)), sink(0), "w0")
+        master.tell(MemberUp(w0, "worker", ""), None)
+        time.sleep(0.3)
+        if init_workers == 2:
+            assert not outs[0] and not fin.is_set()  # nothing runs with one of two workers
+        else:
+            assert outs[0]  # the reference: the lone worker's job already ran
+        w1 = system.worker(lambda req: AllReduceInput(host_iota_source(n, 1000.0)(req)), sink(1), "w1")
+        master.tell(MemberUp(w1, "worker", ""), None)
+        if init_workers == 2:
+            assert fin.wait(10)
+            deadline = time.time() + 5
+            while time.time() < deadline and len(outs[1]) < rounds:
+                time.sleep(0.01)
+            assert sorted(outs[1]) == list(range(rounds))
+            assert all(c == [2] * len(c) for c in outs[1].values())
+    finally:
+        system.shutdown()
