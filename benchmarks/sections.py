@@ -611,7 +611,12 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                              ("tokens8192_grid128", 128, True, True, 8192),
                              ("split16_tokens8192", 32, True, True, 8192), ("split32_tokens8192", 64, True, True, 8192),
                              ("split64_tokens8192", 128, True, True, 8192)]
-            for name, grid, ov, hi, tokens in variants:
+            # ResNet-50's steps are ~2 ms: a clock or power excursion during one variant's
+            # window moves its step AND compute medians (a 4.7 ms serial step beside 2.3 ms
+            # ones, BENCH of round 6), so every variant runs twice and keeps the pass with the
+            # lower compute median; Llama-3-8B's 30-160 ms steps average such excursions out
+            passes = 1 if big else 2
+            for name, grid, ov, hi, tokens in [v for v in variants for _ in range(passes)]:
                 cell: dict = {"tokens": tokens}
                 print(f"[dp_overlap] {model} {name}", file=sys.stderr, flush=True)  # progress (a long section)
                 try:
@@ -667,7 +672,9 @@ def dp_overlap(dev, models=("resnet50", "llama3_8b"), grids=(32, 64, 128, 256, 5
                             "comm_GBps": round(row["hbm_bytes_per_rank"] / (comm_ms * 1e6), 1)}
                 except Exception as e:  # noqa: BLE001
                     cell["error"] = repr(e)
-                row[name] = cell
+                prev = row.get(name)
+                if prev is None or "step_ms" not in prev or ("step_ms" in cell and cell["compute_ms"] < prev["compute_ms"]):
+                    row[name] = cell
             reducer.overlap, reducer.stream, reducer._comm_raw, reducer._cus = True, hi_stream, hi_raw, 0
             reducer.algo = "auto"
             cstream["s"] = None
