@@ -16,6 +16,9 @@ experiments (every cell validated against an fp32 sum before it is timed):
   ring       8 logical ranks x 256 MiB: fp32-wire ring, element-type ring, two-shot, p50 and
              fraction of the same process's copy roofline
   sdma       the copy-engine allreduce at several reduce grids (--grids)
+  sdma-remap the copy-engine allreduce before / after its input (x), output (y) or both
+             were freed, the cache emptied and re-allocated at the same addresses, and with
+             the input staged through a buffer allocated first (--mode x|y|both)
   grid       protocol rounds (2 workers, th = 1) at several per-worker workgroup budgets
   coll-grid  all-gather / reduce-scatter / all-to-all over device workgroup budgets
 
@@ -187,6 +190,53 @@ def exp_sdma(a) -> None:
             torch.cuda.empty_cache()
 
 
+def exp_sdma_remap(a) -> None:
+    import torch
+
+    from akka_allreduce_1_amd.ops import fill_uniform
+    from akka_allreduce_1_amd.parallel import LocalSdmaCluster
+    from akka_allreduce_1_amd.utils.timing import percentile
+    from benchmarks.sections import device_times
+
+    dev = torch.device("cuda", 0)
+    P, nbytes = a.P, a.mib << 20
+    n = nbytes // 2
+
+    def bufs(seed):
+        xs = [fill_uniform(torch.empty(n, dtype=torch.bfloat16, device=dev), seed=seed + k) for k in range(P)]
+        return xs, [torch.empty_like(x) for x in xs]
+
+    cl = LocalSdmaCluster(P, slot_bytes=-(-nbytes // P) + (1 << 20), grid=128, timeout_s=20.0)
+    stage = [torch.empty(n, dtype=torch.bfloat16, device=dev) for _ in range(P)]
+
+    def t(fn, tag, xs):
+        for _ in range(3):
+            fn()
+        ts = device_times(fn, a.iters, dev)
+        cl.check()
+        _emit({"exp": "sdma-remap", "tag": a.tag, "mode": a.mode, "P": P, "case": tag,
+               "x": hex(xs[0].data_ptr()), "p50_ms": round(percentile(ts, 50), 4)})
+
+    xs, ys = bufs(0)
+    t(lambda: cl.allreduce(xs, ys), "first", xs)
+    if a.mode in ("x", "both"):
+        del xs
+        torch.cuda.empty_cache()
+        xs, _ = bufs(10)
+    if a.mode in ("y", "both"):
+        del ys
+        torch.cuda.empty_cache()
+        ys = [torch.empty_like(x) for x in xs]
+    t(lambda: cl.allreduce(xs, ys), "remapped", xs)
+
+    def staged():
+        for s_, x in zip(stage, xs):
+            s_.copy_(x)
+        cl.allreduce(stage, ys)
+
+    t(staged, "staged_input", xs)
+
+
 def exp_grid(a) -> None:
     import torch
 
@@ -277,6 +327,11 @@ def main() -> None:
     p.add_argument("--pieces", default="0", help="pipeline pieces per block (0 = by size)")
     p.add_argument("--reps", type=int, default=2)
     p.add_argument("--iters", type=int, default=10)
+    p = sub.add_parser("sdma-remap")
+    p.add_argument("--P", type=int, default=2)
+    p.add_argument("--mib", type=int, default=256)
+    p.add_argument("--mode", default="both", choices=["x", "y", "both"])
+    p.add_argument("--iters", type=int, default=10)
     p = sub.add_parser("grid")
     p.add_argument("--grids", default="64,128,256")
     p = sub.add_parser("coll-grid")
@@ -285,7 +340,7 @@ def main() -> None:
         s.add_argument("--tag", default="")
     a = ap.parse_args()
     _setup(a.env)
-    {"threshold": exp_threshold, "protocol": exp_protocol, "ring": exp_ring, "sdma": exp_sdma, "grid": exp_grid,
+    {"threshold": exp_threshold, "protocol": exp_protocol, "ring": exp_ring, "sdma": exp_sdma, "sdma-remap": exp_sdma_remap, "grid": exp_grid,
      "coll-grid": exp_coll_grid}[a.exp](a)
 
 
