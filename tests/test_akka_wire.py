@@ -379,3 +379,55 @@ def test_cli_master_serves_akka(tmp_path):
             if p.poll() is None:
                 p.kill()
                 p.wait()
+
+
+def test_python_cli_master_serves_akka():
+    """`python -m akka_allreduce_1_amd master ... --akka-port P --external-rounds` with two
+    Python worker processes: the Akka client drives every round (exact thresholds)."""
+    import subprocess
+    import sys
+
+    from akka_allreduce_1_amd.parallel.comm import free_port
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port, aport = free_port(), free_port()
+    common = ["--set", f"mxar.cluster.seed-nodes=mxar.tcp://ClusterSystem@127.0.0.1:{port}",
+              "--set", "mxar.loglevel=WARNING"]
+    exact = ["--set", "mxar.allreduce.th-reduce=1.0", "--set", "mxar.allreduce.th-complete=1.0",
+             "--set", "mxar.allreduce.max-round=3"]
+    env = dict(os.environ, PYTHONPATH=root)
+    py = [sys.executable, "-m", "akka_allreduce_1_amd"]
+    m = subprocess.Popen(py + ["master", str(port), "2", "10", "2", "--akka-port", str(aport), "--external-rounds"]
+                         + common + exact, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    ws = [subprocess.Popen(py + ["worker", "0", "10"] + common, env=env, stdout=subprocess.DEVNULL,
+                           stderr=subprocess.DEVNULL) for _ in range(2)]
+    try:
+        deadline = time.time() + 60
+        cl = None
+        while cl is None and time.time() < deadline:
+            try:
+                cl = ar.AkkaClient("127.0.0.1", aport, timeout=10)
+            except OSError:
+                time.sleep(0.2)
+        assert cl is not None
+        with cl:
+            for r in range(4):
+                while True:  # a start before the workers are initialised is refused: retry
+                    cl.start_allreduce(r)
+                    try:
+                        seen = set()
+                        while len(seen) < 2:
+                            s, rr, _, _ = cl.complete_allreduce(timeout=2 if r == 0 and not seen else 20)
+                            if rr == r:
+                                seen.add(s)
+                        break
+                    except TimeoutError:
+                        assert r == 0 and time.time() < deadline
+        out, _ = m.communicate(timeout=30)
+        assert m.returncode == 0, out
+        assert "akka.tcp endpoint" in out and "finished 4 rounds" in out, out
+    finally:
+        for p in [m] + ws:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
