@@ -238,11 +238,12 @@ void AkkaEndpoint::write_loop(std::shared_ptr<AkkaEndpoint> self, std::shared_pt
         ++frames;
       }
       a->queued = 0;
+      a->inflight = true;
       n_out_ += frames;
     }
     const auto now = std::chrono::steady_clock::now();
     if (now >= next_hb) {  // transport failure detector (akka.remote.transport-failure-detector)
-      buf += hb;
+      if (a->open.load()) buf += hb;  // never ahead of our ASSOCIATE reply
       next_hb = now + std::chrono::duration_cast<std::chrono::nanoseconds>(period);
     }
     size_t off = 0;
@@ -255,6 +256,7 @@ void AkkaEndpoint::write_loop(std::shared_ptr<AkkaEndpoint> self, std::shared_pt
       }
       off += static_cast<size_t>(n);
     }
+    a->inflight = false;
   }
 }
 
@@ -275,6 +277,9 @@ void AkkaEndpoint::accept_loop(std::shared_ptr<AkkaEndpoint> self) {
       std::lock_guard<std::mutex> g(mu_);
       assocs_.push_back(a);
     }
+    // both threads start here (stop() joins the writer: it must never be assigned later
+    // by another thread)
+    a->writer = std::thread([self, a] { self->write_loop(self, a); });
     a->reader = std::thread([self, a] { self->read_loop(self, a); });
   }
 }
@@ -319,14 +324,15 @@ void AkkaEndpoint::read_loop(std::shared_ptr<AkkaEndpoint> self, std::shared_ptr
       me.host = opt_.host;
       me.port = static_cast<uint32_t>(port_);
       send_pdu(*a, akka::encode_associate(me, uid_, opt_.cookie));
+      a->open = true;
       std::weak_ptr<AkkaEndpoint> we = self;
       std::weak_ptr<Assoc> wa = a;
-      a->tap = bridge_->add_tap([we, wa](const std::string& line) {
-        auto e = we.lock();
-        auto x = wa.lock();
-        if (e && x) e->on_line(*x, line);
-      });
-      a->writer = std::thread([self, a] { self->write_loop(self, a); });
+      if (!stop_.load())  // (after stop() the bridge drops every tap anyway)
+        a->tap = bridge_->add_tap([we, wa](const std::string& line) {
+          auto e = we.lock();
+          auto x = wa.lock();
+          if (e && x) e->on_line(*x, line);
+        });
       open = true;
       ++n_assoc_;
       MXAR_LOG(INFO, "akka", "----associated with " << a->remote.str() << " (uid " << a->remote_uid << ")");
@@ -345,7 +351,7 @@ void AkkaEndpoint::read_loop(std::shared_ptr<AkkaEndpoint> self, std::shared_ptr
     }
     if (env.has_envelope) on_envelope(*a, env);
   }
-  if (a->tap) bridge_->remove_tap(a->tap);
+  if (const uint64_t t = a->tap.exchange(0)) bridge_->remove_tap(t);
   a->kill();
 }
 
@@ -466,7 +472,7 @@ void AkkaEndpoint::deliver(Assoc& a, std::vector<std::string> elems, const akka:
   BridgeCommand cmd;
   cmd.kind = BridgeCommand::Start;
   cmd.round = static_cast<int>(o.fields[0].i);
-  cmd.client = a.tap;
+  cmd.client = a.tap.load();
   if (cmd.round < 0 || !bridge_->submit(cmd)) warn_once("start", "StartAllreduce refused (negative round or no master)");
 }
 
@@ -532,12 +538,24 @@ void AkkaEndpoint::stop() {
     std::lock_guard<std::mutex> g(mu_);
     as.swap(assocs_);
   }
-  const std::string bye = frame(akka::encode_control(akka::kShuttingDown));
-  for (auto& a : as) {
-    if (a->tap && bridge_) bridge_->remove_tap(a->tap);
-    if (a->writer.joinable() && !a->dead.load()) {  // best effort: tell the client we are going down
-      (void)::send(a->fd, bye.data(), bye.size(), MSG_NOSIGNAL | MSG_DONTWAIT);
+  const std::string bye = akka::encode_control(akka::kShuttingDown);
+  for (auto& a : as)  // best effort: tell every client we are going down (through its writer)
+    if (const uint64_t t = a->tap.exchange(0)) {
+      bridge_->remove_tap(t);
+      if (a->open.load()) send_pdu(*a, bye);
     }
+  const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(200);
+  for (auto& a : as)
+    for (;;) {
+      bool drained;
+      {
+        std::lock_guard<std::mutex> g(a->wmu);
+        drained = a->out.empty() && !a->inflight.load();
+      }
+      if (drained || a->dead.load() || std::chrono::steady_clock::now() > until) break;
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+  for (auto& a : as) {
     a->kill();
     if (a->reader.joinable()) a->reader.detach();
     join(a->writer);

@@ -78,7 +78,9 @@ class AkkaEndpoint : public std::enable_shared_from_this<AkkaEndpoint> {
   struct Assoc {
     ~Assoc();
     int fd = -1;
-    uint64_t tap = 0;
+    std::atomic<uint64_t> tap{0};     // the bridge tap (set by the reader after the handshake)
+    std::atomic<bool> open{false};    // handshake done: the writer sends heartbeats
+    std::atomic<bool> inflight{false};  // the writer holds taken frames not yet sent
     std::mutex wmu;
     std::condition_variable wcv;
     std::deque<std::string> out;
