@@ -350,6 +350,8 @@ void bind_hip(py::module_& m) {
       .def_readwrite("step", &AdamW::step);
 
   h.def("sdma_diagnose", &sdma_diagnose, py::arg("device") = 0);
+  h.def("sdma_copy_probe", &sdma_copy_probe, py::arg("device"), py::arg("dst"), py::arg("src"), py::arg("bytes"),
+        py::arg("engine") = 0, py::arg("iters") = 10, py::arg("nengines") = 1, py::call_guard<py::gil_scoped_release>());
   h.def("pci_location", &pci_location, py::arg("device"));
   py::class_<SdmaComm>(h, "SdmaComm")
       .def(py::init<int, int, int, int64_t, int, int, double>(), py::arg("rank"), py::arg("world"), py::arg("device"),

@@ -121,6 +121,9 @@ class SdmaComm {
 
 // HSA view of the machine (agents, PCI locations, SDMA engine masks): bring-up diagnostics
 std::string sdma_diagnose(int device);
+// ms per engine copy of `bytes` (src -> dst on `device`, engine index into its mask)
+double sdma_copy_probe(int device, uint64_t dst, uint64_t src, int64_t bytes, int engine, int iters,
+                       int nengines = 1);
 // PCI location of a HIP device ((domain << 32) | bdf): which GPU a rank's SDMA slab lives on,
 // known before anything is allocated (SdmaCommunicator's cross-GPU check).
 uint64_t pci_location(int device);

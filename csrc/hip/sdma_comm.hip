@@ -15,6 +15,8 @@
 #include <string>
 
 #include "sdma_comm.h"
+
+#include <chrono>
 #include "xgmi_device.h"
 
 namespace mxar {
@@ -90,6 +92,52 @@ uint32_t engine_mask(int device, hsa_agent_t own, hsa_agent_t cpu) {
 }
 
 }  // namespace
+
+// Engine copies of `bytes` from src to dst on this device, split over `nengines` engines
+// (from index `engine` of the device's mask) running at once, `iters` times back to back;
+// ms per copy by the host clock. The probe behind profiles/round6 section 3 (which
+// buffers, and how many engines at once, the engines are slow on).
+double sdma_copy_probe(int device, uint64_t dst, uint64_t src, int64_t bytes, int engine, int iters, int nengines) {
+  hip_check(hipSetDevice(device), "hipSetDevice");
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  hsa_check(hsa_init(), "hsa_init");
+  AgentSearch s;
+  s.want = hip_location(device);
+  hsa_check(hsa_iterate_agents(agent_cb, &s), "hsa_iterate_agents");
+  if (s.found.handle == 0) throw std::runtime_error("sdma_copy_probe: no HSA agent for the device");
+  const uint32_t mask = engine_mask(device, s.found, s.cpu);
+  std::vector<uint32_t> engines;
+  for (int b = 0; b < 32; ++b)
+    if (mask & (1u << b)) engines.push_back(1u << b);
+  if (engines.empty()) throw std::runtime_error("sdma_copy_probe: no SDMA engine");
+  const int ne = std::max(1, nengines);
+  const int64_t part = rup(cdiv(bytes, ne), 4096);
+  hsa_signal_t done;
+  hsa_check(hsa_signal_create(1, 0, nullptr, &done), "signal");
+  auto one = [&] {
+    int parts = 0;
+    for (int e = 0; e < ne; ++e) parts += std::min<int64_t>(bytes, e * part) < bytes;
+    hsa_signal_store_relaxed(done, parts);
+    for (int e = 0; e < ne; ++e) {
+      const int64_t off = std::min<int64_t>(bytes, e * part), len = std::min<int64_t>(bytes - off, part);
+      if (len <= 0) continue;
+      const auto eng = static_cast<hsa_amd_sdma_engine_id_t>(engines[static_cast<size_t>(engine + e) % engines.size()]);
+      hsa_check(hsa_amd_memory_async_copy_on_engine(reinterpret_cast<void*>(dst + off), s.found,
+                                                    reinterpret_cast<const void*>(src + off), s.found,
+                                                    static_cast<size_t>(len), 0, nullptr, done, eng, true),
+                "hsa_amd_memory_async_copy_on_engine");
+    }
+    if (hsa_signal_wait_scacquire(done, HSA_SIGNAL_CONDITION_EQ, 0, 10'000'000'000ull, HSA_WAIT_STATE_ACTIVE) != 0)
+      throw std::runtime_error("sdma_copy_probe: copy did not complete");
+  };
+  one();  // warm
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < iters; ++i) one();
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / iters;
+  hsa_signal_destroy(done);
+  hsa_shut_down();
+  return ms;
+}
 
 // ---------------------------------------------------------------------------------
 // Kernels
