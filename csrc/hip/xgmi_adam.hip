@@ -304,14 +304,11 @@ static void launch_adamw_t(const CommArgs& a, dim3 grid, hipStream_t s, DType dt
 }
 
 void launch_adamw(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {
-  // study knobs: MXAR_ADAM_STREAM (state access form, above), MXAR_ADAM_U (packs per lane)
+  // study knob MXAR_ADAM_STREAM (state access form, above); two packs per lane in flight (1
+  // and 4 measured no better - their knob was removed in round 6)
   static const int mode = [] {
     const char* e = study_env("MXAR_ADAM_STREAM");
     return e != nullptr ? std::atoi(e) : -1;
-  }();
-  static const int u = [] {
-    const char* e = study_env("MXAR_ADAM_U");
-    return e != nullptr ? std::atoi(e) : 2;
   }();
   if (mode == 3 || (mode < 0 && dt != DType::F32))
     launch_adamw_t<3, 2>(a, grid, s, dt);  // 16-bit parameters: run-contiguous halves (default)
@@ -319,10 +316,6 @@ void launch_adamw(const CommArgs& a, dim3 grid, hipStream_t s, DType dt) {
     launch_adamw_t<1, 2>(a, grid, s, dt);
   else if (mode == 2)
     launch_adamw_t<2, 2>(a, grid, s, dt);
-  else if (u == 1)
-    launch_adamw_t<0, 1>(a, grid, s, dt);
-  else if (u == 4)
-    launch_adamw_t<0, 4>(a, grid, s, dt);
   else
     launch_adamw_t<0, 2>(a, grid, s, dt);
 }

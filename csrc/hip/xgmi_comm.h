@@ -471,7 +471,6 @@ class XgmiComm {
   // full-threshold rounds of at most this many bytes per rank run the one-shot body
   // (xgmi_threshold.hip; MXAR_STUDY=1 MXAR_TH_ONESHOT_MAX=bytes, 0 = off)
   int64_t th_oneshot_max_ = 32 << 10;
-  bool dynamic_ = false;           // two-shot units from a counter (MXAR_TWOSHOT_DYNAMIC)
   bool ring_hop_rows_ = false;     // negative control: the two-writer ring flag layout (MXAR_RING_FLAGS=hop)
   int geom_ = -1;                  // two-shot geometry: -1 by block size, 0 coarse, 1 fine, 2 flat (MXAR_TWOSHOT_GEOM)
   int64_t flat_min_ = int64_t{2} << 20;  // blocks of at least this many bytes use the flat geometry (MXAR_TWOSHOT_FLAT_MIN)

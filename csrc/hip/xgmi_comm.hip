@@ -80,24 +80,13 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
   // Phase 2 - reduce own block once all P contributions of a chunk have arrived
   // (thReduce = 1), then ReduceBlock-broadcast the sum into every rank's R slot. A chunk
   // is reduced in `sub` pieces by different workgroups so that phase 2 has as many
-  // units as phases 1 and 3 (each piece pays one acquire and one release).
-  // `dynamic`: units are taken in order from a per-rank counter instead of the static
-  // blockIdx stride, so a workgroup whose units' contributions arrive late does not hold
-  // back units another workgroup could already reduce (the counters are reset by the
-  // last workgroup of the launch).
+  // units as phases 1 and 3 (each piece pays one acquire and one release). Units go to
+  // workgroups by a static blockIdx stride (a counter-driven walk measured +1 % at 8 logical
+  // ranks and slower at 2 - profiles/round4 - and was removed in round 6).
   const int64_t bstart_own = static_cast<int64_t>(r) * a.block;
   const int64_t blen_own = clamp_len(a.n - bstart_own, a.block);
   const int nu2 = a.nch * a.sub;
-  __shared__ int next_unit;
-  auto take = [&](int slot, int u_static) -> int {
-    if (!a.dynamic) return u_static;
-    __syncthreads();
-    if (threadIdx.x == 0)
-      next_unit = static_cast<int>(__hip_atomic_fetch_add(&ctl[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    __syncthreads();
-    return next_unit;
-  };
-  for (int u = take(8, blockIdx.x), k2 = 1; u < nu2; u = take(8, blockIdx.x + k2 * G), ++k2) {
+  for (int u = blockIdx.x; u < nu2; u += G) {
     const int c = u / a.sub;
     const int q = u % a.sub;
     const int64_t cbeg = static_cast<int64_t>(c) * a.chunk;
@@ -128,7 +117,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
   // and copied in ARRIVAL order: owners finish their reduces at different times, and a
   // workgroup waiting on its units one by one idles behind the latest of them while others
   // are ready (the threshold kernel's gather, which does this, was 13 % faster at 8 x 64 MiB
-  // - profiles/round3/README.md). `dynamic` keeps the counter-driven in-order walk.
+  // - profiles/round3/README.md).
   auto gather_unit = [&](int u) {
     const int c = u / Pm1;
     const int j = (r + 1 + u % Pm1) % P;
@@ -139,17 +128,7 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
     if (len > 0 && unit_in_bounds(a, cstart * es, len * es, c, err))
       copy_from_slab<E>(out + (bstart + cstart) * es, a.base[r] + a.off_R + j * slot + cstart * es, len);
   };
-  if (a.dynamic) {
-    for (int u = take(9, blockIdx.x), k3 = 1; u < nu; u = take(9, blockIdx.x + k3 * G), ++k3) {
-      const int c = u / Pm1;
-      const int j = (r + 1 + u % Pm1) % P;
-      const uint64_t tw = ps.now();
-      wait_flags([&](int q) -> const uint32_t* { return f2(a, r, j, c * a.sub + q); }, a.sub, epoch, deadline, err,
-                 ERR_TIMEOUT_REDUCE, acq);
-      ps.add(4, tw);
-      gather_unit(u);
-    }
-  } else {
+  {
     __shared__ uint64_t arrived;
     __shared__ int late_s;
     const int mine = blockIdx.x < static_cast<unsigned>(nu) ? (nu - 1 - static_cast<int>(blockIdx.x)) / G + 1 : 0;
@@ -199,17 +178,6 @@ __global__ __launch_bounds__(kCommThreads) void twoshot_kernel(CommArgs a) {
   }
   ps.mark(5);
   ps.flush();
-  if (a.dynamic) {  // the last workgroup resets the unit counters for the next launch
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint32_t t = __hip_atomic_fetch_add(&ctl[10], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t == gridDim.x - 1) {
-        __hip_atomic_store(&ctl[8], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ctl[9], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ctl[10], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
   finish_launch_done(a, ctl, epoch, r, kHazR);  // peers may still gather from R
 }
 
@@ -588,13 +556,11 @@ XgmiComm::Layout XgmiComm::layout(int world, int64_t slot_bytes, int threshold_r
   L.slot_bytes = round_up(std::max<int64_t>(slot_bytes, 64 * 1024), 64 * 1024);
   L.maxch = ceil_div(L.slot_bytes, flag_gran);
   L.off_S = round_up(std::max(flag_bytes(world, slot_bytes, threshold_rows, flag_gran), min_flag_bytes), 64 * 1024);
-  // Slots sit slot_stride = capacity + MXAR_SLOT_PAD bytes apart (default 0). A pad takes the
-  // P slots a reduce reads at one offset off a power-of-two spacing; an A/B on one box showed
-  // no gain for the reduce kernel (benchmarks/bench_reduce.py --pad-kib, profiles/reduce_kernel.md),
-  // so the knob stays for study.
-  int64_t pad = 0;
-  if (const char* e = study_env("MXAR_SLOT_PAD")) pad = round_up(std::max<int64_t>(0, std::atoll(e)), 4096);
-  L.slot_stride = L.slot_bytes + pad;
+  // Slots sit back to back (slot_stride = capacity). A pad that takes the P slots a reduce
+  // reads off a power-of-two spacing showed no gain for the reduce kernel
+  // (benchmarks/bench_reduce.py --pad-kib, profiles/reduce_kernel.md); its study knob was
+  // removed in round 6.
+  L.slot_stride = L.slot_bytes;
   L.off_R = L.off_S + rows * world * L.slot_stride;
   // low-latency one-shot slots: [2 parities][P sources] x ll_slot (two 8-B LL words per
   // 16-B store: ll_slot = 2 x payload)
@@ -608,13 +574,13 @@ XgmiComm::Layout XgmiComm::layout(int world, int64_t slot_bytes, int threshold_r
   // bit 31 set (2-4 GiB, 6-8 GiB, ...) never returns in the importing process, while the
   // sizes around it map and reduce correctly (measured with tools/ipc_size_probe.py, in git history: 1.97,
   // 4.05, 4.33 GiB fine; 2.03-3.9 GiB hang). Such slabs are padded up to the next multiple of
-  // 4 GiB - at most 2 GiB of the 288 GB of HBM. MXAR_IPC_NO_PAD=1 disables it (probing).
+  // 4 GiB - at most 2 GiB of the 288 GB of HBM.
   L.alloc_bytes = ipc_safe_bytes(L.slab_bytes);
   return L;
 }
 
 int64_t XgmiComm::ipc_safe_bytes(int64_t bytes) {
-  if ((bytes & (int64_t{1} << 31)) && !study_env("MXAR_IPC_NO_PAD")) return round_up(bytes, int64_t{1} << 32);
+  if (bytes & (int64_t{1} << 31)) return round_up(bytes, int64_t{1} << 32);
   return bytes;
 }
 
@@ -664,7 +630,6 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   if (const char* u = study_env("MXAR_TWOSHOT_SUB")) sub_max_ = std::max(1, std::atoi(u));
   if (const char* d = study_env("MXAR_RING_DEPTH")) ring_depth_ = std::max(1, std::atoi(d));
   if (const char* g = std::getenv("MXAR_RING_GRID")) ring_grid_ = std::max(1, std::atoi(g));
-  if (const char* d = study_env("MXAR_TWOSHOT_DYNAMIC")) dynamic_ = std::atoi(d) != 0;
   if (const char* f = study_env("MXAR_RING_FLAGS")) {
     // the round-3 layout whose flag words had two writers (ring hop rows vs other kernels'
     // writer rows): kept only as the negative control of tests/test_comm_gpu.py
@@ -684,11 +649,11 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t slot_bytes, int grid
   const char* mem = study_env("MXAR_SLAB_MEM");
   const std::string kind = mem ? mem : "fine";
   // study knobs that trade away correctness guarantees: say so once per communicator
-  if (fence_ != 3 || kind != "fine" || (study_mode() && std::getenv("MXAR_IPC_NO_PAD")))
+  if (fence_ != 3 || kind != "fine")
     std::fprintf(stderr,
-                 "[mxar] WARNING rank %d: study settings active (MXAR_FENCE=%d, MXAR_SLAB_MEM=%s%s); "
+                 "[mxar] WARNING rank %d: study settings active (MXAR_FENCE=%d, MXAR_SLAB_MEM=%s); "
                  "results may be wrong - use the defaults in production\n",
-                 rank_, fence_, kind.c_str(), (study_mode() && std::getenv("MXAR_IPC_NO_PAD")) ? ", MXAR_IPC_NO_PAD" : "");
+                 rank_, fence_, kind.c_str());
   if (external_slab != nullptr) {
     // An arena owned by the caller (xgmi_plane.cc): allocated fine-grained and zeroed ONCE,
     // exported before any peer knew it, and laid out again on every re-initialisation. Its
@@ -1052,7 +1017,6 @@ void XgmiComm::launch_segment(const std::vector<XgmiComm*>& group, const char* c
   a.fdelay_rank = c0.fdelay_rank_;
   a.fdelay = c0.fdelay_us_ > 0 ? static_cast<uint64_t>(c0.fdelay_us_ * 100.0) : 0;
   a.noguard = c0.noguard_ ? 1 : 0;
-  a.dynamic = c0.dynamic_ ? 1 : 0;
   a.ring_hop_rows = c0.ring_hop_rows_ ? 1 : 0;
   a.stamps = c0.stamps_;
   if (a.stamps != nullptr && gx * ranks_here > c0.stamp_slots_) a.stamps = nullptr;  // buffer too small: off

@@ -80,7 +80,6 @@ struct CommArgs {
   uint64_t fdelay;
   int fdelay_rank;
   int noguard;  // MXAR_SLOT_GUARD=0: skip entry_guard (A/B of its cost and negative control only)
-  int dynamic;  // two-shot: workgroups take reduce / gather units from a counter (ctl[8], ctl[9])
   int ring_hop_rows;  // study only (MXAR_RING_FLAGS=hop): the pre-fix ring flag layout, row = hop index
   // threshold kernel with sub > 1 (chunks split into `sub` slices of `subchunk` elements,
   // one workgroup each): the rank's own scratch, zeroed when the membership is configured.

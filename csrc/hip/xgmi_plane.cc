@@ -231,9 +231,6 @@ XgmiRoundPlane::XgmiRoundPlane(const XgmiPlaneOptions& o) : o_(o) {
   if (o_.max_lag < 0 || o_.max_lag > 62) throw std::invalid_argument("xgmi plane: max_lag must be in [0, 62]");
   o_.ring = std::max(4, o_.ring);
   if (const char* e = study_env("MXAR_PLANE_SPLIT")) o_.split = std::atoi(e) != 0;  // A/B knob
-  // A/B knob: 1 = also record an event per round and confirm completion with it (round 2's
-  // form; ~2-3 us of hipEventRecord on every launch, profiles/round3/api_cost.json)
-  if (const char* e = study_env("MXAR_PLANE_EVENTS")) event_confirm_ = std::atoi(e) != 0;
   if (const char* e = study_env("MXAR_PLANE_COARSEN")) coarsen_full_ = std::atoi(e) != 0;  // A/B knob
   if (const char* e = study_env("MXAR_PLANE_WG_CHUNKS")) wg_chunks_ = std::max(0, std::atoi(e));  // A/B knob
   if (const char* q = std::getenv("GPU_MAX_HW_QUEUES"); q != nullptr && std::atoi(q) == 1)
@@ -1127,7 +1124,7 @@ std::shared_ptr<void> XgmiRoundPlane::resident_out(size_t bytes, std::shared_ptr
 }
 
 bool XgmiRoundPlane::launch_resident(int round, const Payload& input, bool cold) {
-  if (o_.resident_max <= 0 || event_confirm_ || o_.ring > kResidentDoors) return false;
+  if (o_.resident_max <= 0 || o_.ring > kResidentDoors) return false;
   const int64_t n = cfg_.dataSize;
   const int64_t es = static_cast<int64_t>(dtype_size(o_.dtype));
   if (n * es > o_.resident_max) return false;
@@ -1342,7 +1339,6 @@ void XgmiRoundPlane::launch(int round, const Payload& input, bool cold) {
   }
   std::unique_lock<std::mutex> lk(mu_);
   rec.ev = events_[rec.slot];
-  if (event_confirm_) hip_check(hipEventRecord(rec.ev, stream_), "hipEventRecord(round)");
   last_round_ = round;
   st_.launches++;
   if (cold) st_.cold++;
@@ -1436,17 +1432,8 @@ void XgmiRoundPlane::completion_loop() {
         for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
       }
       e = hipSuccess;
-      if (event_confirm_) {
-        for (;;) {
-          e = hipEventQuery(rec.ev);
-          if (e != hipErrorNotReady) break;
-          if (std::chrono::steady_clock::now() - t0 > budget) {
-            e = hipEventSynchronize(rec.ev);
-            break;
-          }
-          std::this_thread::yield();
-        }
-      } else {
+      {  // (round 2 confirmed with a per-round event: +2-3 us of hipEventRecord per launch,
+         // profiles/round3/api_cost.json; the pinned done word replaced it)
         const auto lost = std::chrono::microseconds(static_cast<int64_t>(2e6 * o_.timeout_s) + 5000000);
         while (*done != want) {
           if (std::chrono::steady_clock::now() - t0 > lost) {

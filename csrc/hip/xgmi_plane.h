@@ -145,7 +145,6 @@ class XgmiRoundPlane final : public RoundPlane {
   }
 
  private:
-  bool event_confirm_ = false;  // MXAR_PLANE_EVENTS=1: per-round event confirms the done word
   bool coarsen_full_ = true;    // MXAR_PLANE_COARSEN=0: kernel chunks = maxChunkSize at thresholds 1
   int wg_chunks_ = 1;           // at thresholds 1: kernel chunks per workgroup at most (0: no cap)
   struct Rec {

@@ -321,9 +321,7 @@ ActorSystem::ActorSystem(std::string name, Mode mode, int threads, int throughpu
     // wake-up per hop costs more than the hop itself.
     spin_us_ = 50;
     if (const char* e = std::getenv("MXAR_DISPATCH_SPIN_US")) spin_us_ = std::max(0, std::atoi(e));
-    if (const char* e = study_env("MXAR_DISPATCH_NOTIFY")) notify_always_ = std::string(e) == "always";
     if (const char* e = study_env("MXAR_DISPATCH_LIFO")) lifo_ = std::atoi(e) != 0;
-    if (const char* e = study_env("MXAR_DISPATCH_YIELD")) spin_yield_ = std::atoi(e) != 0;
     if (const char* e = study_env("MXAR_DISPATCH_SPINNERS")) max_spinners_ = std::max(1, std::atoi(e));
     int n = threads > 0 ? threads : std::max(2u, std::min(8u, std::thread::hardware_concurrency()));
     for (int i = 0; i < n; ++i) threads_.emplace_back([this] { worker_loop(); });
@@ -430,7 +428,7 @@ void ActorSystem::enqueue(const std::shared_ptr<ActorCell>& cell) {
   // sees this push under the lock, or the push came later and this load sees it gone.
   // (One spinner per queued cell: with fewer, a sleeper is woken so that cells queued
   // back to back - a Start to every worker - still run in parallel.)
-  if (notify_always_ || static_cast<size_t>(spinning_.load(std::memory_order_seq_cst)) < queued) rq_cv_.notify_one();
+  if (static_cast<size_t>(spinning_.load(std::memory_order_seq_cst)) < queued) rq_cv_.notify_one();
 }
 
 void ActorSystem::record_exception(std::exception_ptr e) {
@@ -485,7 +483,7 @@ void ActorSystem::worker_loop() {
           for (unsigned i = 1; runq_len_.load(std::memory_order_acquire) == 0 && !shutdown_.load() &&
                                std::chrono::steady_clock::now() < until;
                ++i) {
-            if (spin_yield_ || (i & 31) == 0) {
+            if ((i & 31) == 0) {
               std::this_thread::yield();
             } else {
               for (int k = 0; k < 8; ++k) cpu_relax();

@@ -297,14 +297,12 @@ class ActorSystem {
   std::atomic<size_t> runq_len_{0};  // runq_.size(), readable without rq_mu_ (idle spin)
   int spin_us_ = 0;                  // idle dispatcher threads poll this long before sleeping
   // dispatcher threads in their idle spin: schedule() skips the condition variable's futex
-  // wake while one of them will see the run queue anyway (MXAR_DISPATCH_NOTIFY=always: never)
+  // wake while one of them will see the run queue anyway
   std::atomic<int> spinning_{0};
-  bool notify_always_ = false;
   // run-next slot (MXAR_DISPATCH_LIFO, default on): a cell scheduled by an actor turn on a
   // dispatcher thread runs next on THAT thread, without a run-queue hop - a protocol round's
   // Complete -> master -> Start chain stays on one warm thread (Go's runnext)
   bool lifo_ = true;
-  bool spin_yield_ = false;  // MXAR_DISPATCH_YIELD=1: idle spin yields every poll (round-2 form)
   int max_spinners_ = 2;     // MXAR_DISPATCH_SPINNERS: dispatcher threads spinning at once
   int busy_ = 0;
   std::vector<std::thread> threads_;
