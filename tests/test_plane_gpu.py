@@ -764,6 +764,51 @@ def test_bridge_client_drives_gpu_rounds():
         job.shutdown()
 
 
+def test_akka_client_drives_gpu_rounds():
+    """The north star's "an existing Akka client can drive it" on the GPU engine: an Akka 2.5
+    client (akka_allreduce_1_amd/akka_remote.py) associates with the master's akka.tcp
+    endpoint (docs/AKKA_WIRE.md), resolves /user/master with Identify, sends Java-serialized
+    StartAllreduce(r) and counts CompleteAllreduce(srcId, r) as AllreduceMaster.scala:58-67
+    does; the plane workers run one threshold-kernel launch per round, every output exact."""
+    from akka_allreduce_1_amd import akka_remote as ar
+
+    P, n, chunk, rounds = 2, 10007, 333, 10
+    job = PlaneJob(P, n, max_chunk_size=chunk, max_round=rounds - 1, timeout_s=20.0, bridge_port=0,
+                   external_rounds=True)
+    try:
+        job.start()
+        ep = C.akka.start_endpoint(job.master)
+        with ar.AkkaClient("127.0.0.1", ep.port) as cl:
+            ref = cl.identify(["user", "master"])
+            assert ref == ep.master_path
+            for r in range(rounds):
+                deadline = time.time() + 20
+                while True:  # a start before the workers' InitWorkers is refused: retry
+                    cl.start_allreduce(r, to=ref)
+                    try:
+                        seen = set()
+                        while len(seen) < P:
+                            src, rr, cls, suid = cl.complete_allreduce(timeout=2 if r == 0 and not seen else 20)
+                            assert cls.endswith(".CompleteAllreduce") and suid == ep.suid_complete
+                            if rr == r:
+                                seen.add(src)
+                        break
+                    except TimeoutError:
+                        assert r == 0 and time.time() < deadline
+        assert job.finished.wait(10)
+        for p in job.planes:
+            p.drain()
+        job.system.await_idle(10.0)
+        for k in range(P):
+            for it in range(rounds):
+                data, counts = job.outputs[k][it]
+                np.testing.assert_array_equal(data.float().cpu().numpy(), expected(n, it, range(P)))
+                assert all(c == P for c in counts)
+        assert ep.stats()["suid_mismatches"] == 0
+    finally:
+        job.shutdown()
+
+
 def _dist_job_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     import torch.distributed as dist
