@@ -282,65 +282,70 @@ __device__ __forceinline__ void reduce_masked(const CommArgs& a, int P, int r, u
   // nothing and add +0, which is exact (acc starts at +0 and is never -0), so the fixed order
   // s = 0..P-1 keeps the sum bit-exact.
   const int64_t npk = len / E::ELEMS;
-  constexpr int U = 2;
-  auto sum_batched = [&](auto bt, int64_t i0, int nu, Acc<E>* acc) {
+  // Batches of B sources x U packs per lane: 2 sources x 8 (16 packs in flight), 3-4 x 2 and
+  // more x 2 in batches of 8. Three instantiations, one call site each, so the kernel's code
+  // stays small enough to fetch quickly on a cold CU. At 2 ranks the former 4 x 2 form kept
+  // only 4 packs of real sources in flight and its reduce phase ran at ~4.5 TB/s against the
+  // two-shot's 5.6 (phase stamps); 4 x 4 at 4 ranks measured 2 % slower than 4 x 2 at 64 MiB
+  // (same-box A/B, profiles/round6 section 11).
+  auto run = [&](auto bt) {
     constexpr int B = decltype(bt)::value;
+    constexpr int U = B == 2 ? 8 : 2;
+    for (int64_t i = threadIdx.x; i < npk; i += U * kCommThreads) {
+      const int64_t left = (npk - i + kCommThreads - 1) / kCommThreads;
+      const int nu = left < U ? static_cast<int>(left) : U;
+      Acc<E> acc[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc[u].zero();
-    for (int s0 = 0; s0 < P; s0 += B) {
-      Pack16 v[B][U];
+      for (int u = 0; u < U; ++u) acc[u].zero();
+      for (int s0 = 0; s0 < P; s0 += B) {
+        Pack16 v[B][U];
 #pragma unroll
-      for (int q = 0; q < B; ++q) {
-        const int s = s0 + q;
-        const bool on = s < P && ((mask >> s) & 1u);
-        const __amdgpu_buffer_rsrc_t rs = slab_rsrc(s == r ? own_in : S + (on ? s : 0) * slot);
+        for (int q = 0; q < B; ++q) {
+          const int s = s0 + q;
+          const bool on = s < P && ((mask >> s) & 1u);
+          const __amdgpu_buffer_rsrc_t rs = slab_rsrc(s == r ? own_in : S + (on ? s : 0) * slot);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if (on && u < nu) {
+              v[q][u] = ld16_nt(rs, static_cast<uint32_t>((i + u * kCommThreads) * 16));
+            } else {
+              v[q][u][0] = v[q][u][1] = v[q][u][2] = v[q][u][3] = 0u;
+            }
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+#pragma unroll
+          for (int u = 0; u < U; ++u) acc[u].add(v[q][u]);
+      }
+      Pack16 o[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (scale != 1.f) acc[u].scale(scale);
+        o[u] = acc[u].pack();
+      }
+      for (int k = 0; k < P; ++k) {
+        char* d = k == r ? own_out : ((skip >> k) & 1u) ? nullptr : a.base[k] + roff;
+        if (d == nullptr) continue;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          if (on && u < nu) {
-            v[q][u] = ld16_nt(rs, static_cast<uint32_t>((i0 + u * kCommThreads) * 16));
-          } else {
-            v[q][u][0] = v[q][u][1] = v[q][u][2] = v[q][u][3] = 0u;
+          if (u < nu) {
+            const int64_t at = i + u * kCommThreads;
+            if (k == r && !wt_out)
+              st16(d + at * 16, o[u]);
+            else
+              st16_wt(slab_rsrc(d), static_cast<uint32_t>(at * 16), o[u]);
           }
         }
       }
-#pragma unroll
-      for (int q = 0; q < B; ++q)
-#pragma unroll
-        for (int u = 0; u < U; ++u) acc[u].add(v[q][u]);
     }
   };
-  // (2 or 4 sources: a batch of 4; more: batches of 8 - two instantiations only, one call site
-  // each, so the kernel's code stays small enough to fetch quickly on a cold CU)
-  auto sum_packs = [&](int64_t i0, int nu, Acc<E>* acc) {
-    if (P <= 4)
-      sum_batched(std::integral_constant<int, 4>{}, i0, nu, acc);
-    else
-      sum_batched(std::integral_constant<int, 8>{}, i0, nu, acc);
-  };
-  for (int64_t i = threadIdx.x; i < npk; i += U * kCommThreads) {
-    const int nu = i + kCommThreads < npk ? U : 1;
-    Acc<E> acc[U];
-    sum_packs(i, nu, acc);
-    Pack16 o[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (scale != 1.f) acc[u].scale(scale);
-      o[u] = acc[u].pack();
-    }
-    for (int k = 0; k < P; ++k) {
-      char* d = k == r ? own_out : ((skip >> k) & 1u) ? nullptr : a.base[k] + roff;
-      if (d == nullptr) continue;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (u >= nu) break;
-        const int64_t at = i + u * kCommThreads;
-        if (k == r && !wt_out)
-          st16(d + at * 16, o[u]);
-        else
-          st16_wt(slab_rsrc(d), static_cast<uint32_t>(at * 16), o[u]);
-      }
-    }
-  }
+  if (P <= 2)
+    run(std::integral_constant<int, 2>{});
+  else if (P <= 4)
+    run(std::integral_constant<int, 4>{});
+  else
+    run(std::integral_constant<int, 8>{});
   const int64_t t = npk * E::ELEMS + threadIdx.x;
   if (t < len) {
     float acc = 0.f;
