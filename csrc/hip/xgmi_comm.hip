@@ -1198,9 +1198,14 @@ void XgmiComm::geometry_threshold(int64_t n, DType dt, int ranks_here, int64_t* 
   const int64_t es = static_cast<int64_t>(dtype_size(dt));
   const int64_t elems = 16 / es;
   const int64_t min_chunk = min_chunk_bytes() / es;
-  // launch-size grid as for the two-shot (launch_grid; at the default grid only)
+  // launch-size grid as for the two-shot (launch_grid; at the default grid only). The full
+  // grid from 256 MiB per launch for one rank per device (round 4: 4 x 64 MiB 288 us full vs
+  // 307 us sized); several logical ranks in one launch take it from 512 MiB like the two-shot
+  // since round 6 (one reduce chunk per workgroup, 2 x 8 reduce batches): 4 x 64 MiB 271 ->
+  // 248 us, 4 x 256 MiB 1066 -> 1040 us sized (profiles/round6 section 11)
+  const int64_t full_at = ranks_here > 1 ? int64_t{512} << 20 : int64_t{256} << 20;
   const int gmax =
-      std::min(std::max(1, launch_grid(n * es * std::max(1, ranks_here), false, int64_t{256} << 20) / std::max(1, ranks_here)),
+      std::min(std::max(1, launch_grid(n * es * std::max(1, ranks_here), false, full_at) / std::max(1, ranks_here)),
                shared_launch_cap(ranks_here));
   *block = round_up(ceil_div(n, world_), elems);
   // one reduce unit (a chunk: one threshold decision) per workgroup; phase 1/3 get P-1 each,
