@@ -1191,6 +1191,12 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   // full thresholds, unsplit, no counts: a gathered unit needs no decision (no ticket, no
   // count, no slice agreement) - no workgroup barrier per unit
   const bool fastg = !split && !tickets && counts == nullptr;
+  // full thresholds, unsplit, with counts: still no decision, and the owners' count words of
+  // the arrived units are loaded by the polling wave (one lane per unit, after the acquire)
+  // instead of one dependent load plus two workgroup barriers per unit in thread 0 - at 8 x 1
+  // MiB that serial walk was most of the gather (profiles/round6 section 13)
+  const bool batchc = !split && !tickets && counts != nullptr;
+  __shared__ uint32_t sh_gcnt[64];
   for (;;) {
     bool any = false, progressed = false;
     for (int w = 0; w < nwords; ++w) {
@@ -1199,15 +1205,17 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       if (threadIdx.x < 64) {
         const int idx = w * 64 + static_cast<int>(threadIdx.x);
         bool arr = false;
+        int cj = 0, cc = 0;
         if ((pend[w] >> threadIdx.x) & 1ull) {
           const int b = (static_cast<int>(blockIdx.x) + idx * G) / S;
-          const int c = b / Pm1;
-          const int j = (r + 1 + b % Pm1) % P;
-          arr = reached(ld_flag(f2(a, r, row * P + j, c)), epoch);
+          cc = b / Pm1;
+          cj = (r + 1 + b % Pm1) % P;
+          arr = reached(ld_flag(f2(a, r, row * P + cj, cc)), epoch);
         }
         const uint64_t m = __ballot(arr);
         if (threadIdx.x == 0) sh_arr = m;
         if (m && acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        if (batchc && arr) sh_gcnt[threadIdx.x] = ld_flag(f2c(a, r, row * P + cj, cc));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
@@ -1226,6 +1234,12 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         if (fastg) {  // nothing to decide: every thread knows the unit is taken if it exists
           take = exists(j, c);
           if (threadIdx.x == 0) pend[w] &= ~(1ull << i);
+        } else if (batchc) {  // the same, and the count the polling wave loaded
+          take = exists(j, c);
+          if (threadIdx.x == 0) {
+            cput(static_cast<int64_t>(j) * a.nch + c, take ? static_cast<int32_t>(sh_gcnt[i]) : 0);
+            pend[w] &= ~(1ull << i);
+          }
         } else {
         if (threadIdx.x == 0) {
           int take = 1;
@@ -1274,9 +1288,10 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
         ps.add(4, t_copy);
         progressed = true;
         ps.count(7);
-        if (!fastg) __syncthreads();  // sh_flag is reused by the next unit
+        if (!fastg && !batchc) __syncthreads();  // sh_flag is reused by the next unit
       }
-      if (fastg) __syncthreads();  // thread 0's pend[] updates before anyone reads pend[] again
+      // thread 0's pend[] updates before anyone reads pend[] again (and sh_gcnt is refilled)
+      if (fastg || batchc) __syncthreads();
     }
     if (!any) break;
     if (progressed) continue;
