@@ -1197,6 +1197,7 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
   // MiB that serial walk was most of the gather (profiles/round6 section 13)
   const bool batchc = !split && !tickets && counts != nullptr;
   __shared__ uint32_t sh_gcnt[64];
+  uint32_t idle = 0;  // passes since the last arrival (uniform over the workgroup)
   for (;;) {
     bool any = false, progressed = false;
     for (int w = 0; w < nwords; ++w) {
@@ -1294,7 +1295,17 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
       if (fastg || batchc) __syncthreads();
     }
     if (!any) break;
-    if (progressed) continue;
+    if (progressed) {
+      idle = 0;
+      continue;
+    }
+    // a full round gives up only on a force (or its deadline): between arrivals the wave
+    // re-polls 7 times of 8 without the give-up block (a clock read, the host / slab force
+    // polls and two workgroup barriers per pass delayed the next arrival's copy)
+    if (full && !cold && !void_round && (++idle & 7) != 0) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
     if (threadIdx.x < 64) {
       int give = 0;
       const uint32_t done = full ? 0u : ld_ctl(&ctl[3]);  // full rounds: only a force gives up
