@@ -1366,7 +1366,15 @@ bool XgmiComm::threshold_args(const std::vector<XgmiComm*>& group, const std::ve
       const int cap = ranks_here > 1 ? std::max(1, c0.shared_launch_cap(ranks_here)) : c0.grid_;
       const int64_t upc = ceil_div(std::min(a.chunk, a.block) * es, 8) + 1;  // units of one chunk at most
       const int64_t cpw = std::max<int64_t>(1, kCommThreads / upc);
-      gx = static_cast<int>(std::min<int64_t>(cap, ceil_div(static_cast<int64_t>(W) * a.nch, cpw)));
+      const int64_t need = ceil_div(static_cast<int64_t>(W) * a.nch, cpw);
+      // only where every workgroup's chunks fit its fast pass (one unit per thread): a grid too
+      // small for that (a small default grid, a CU-limited communicator) or chunks of more than
+      // kCommThreads units take the two-shot body - the one-shot body's chunk-by-chunk form
+      // timed out there (MXAR_GRID=64, 8 x 128 KiB; profiles/round6 section 12)
+      if (need > cap || upc > kCommThreads)
+        a.oneshot = 0;
+      else
+        gx = static_cast<int>(need);
     }
   }
   a.counts = counts;

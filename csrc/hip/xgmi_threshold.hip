@@ -850,15 +850,25 @@ __device__ __forceinline__ bool threshold_round(const CommArgs& a, const RoundVa
             st16_wt(slab_rsrc(a.base[k] + rowS + static_cast<int64_t>(r) * slot), static_cast<uint32_t>(my_u * 16), v);
       }
     } else if (!cold && !void_round) {
-      for (int64_t i = static_cast<int64_t>(blockIdx.x) * kCommThreads + threadIdx.x; i < units; i += gstride) {
-        const uint2 d = load_unit8(in, i, nbytes);
-        Pack16 v;
-        v[0] = d.x;
-        v[1] = tag;
-        v[2] = d.y;
-        v[3] = tag;
-        for (int k = 0; k < P; ++k)
-          if (k != r) st16_wt(slab_rsrc(a.base[k] + rowS + static_cast<int64_t>(r) * slot), static_cast<uint32_t>(i * 16), v);
+      // the units of this workgroup's OWN chunks, as the fast pass does: `fast` is uniform per
+      // workgroup, not over the grid (a workgroup with more chunks may exceed the fast pass
+      // while the others do not), so a grid-stride walk here left the units whose stride owner
+      // took the fast pass unpushed - their chunks waited out the deadline (MXAR_GRID=64, 8 x
+      // 128 KiB; the 2- and 4-process stress tests at 64 KiB, profiles/round6 section 12)
+      for (int q = blockIdx.x; q < nq; q += G) {
+        int64_t b0, b1;
+        if (!chunk_span(q, &b0, &b1)) continue;
+        const int64_t u1 = (b1 + 7) / 8;
+        for (int64_t i = b0 / 8 + threadIdx.x; i < u1; i += kCommThreads) {
+          const uint2 d = load_unit8(in, i, nbytes);
+          Pack16 v;
+          v[0] = d.x;
+          v[1] = tag;
+          v[2] = d.y;
+          v[3] = tag;
+          for (int k = 0; k < P; ++k)
+            if (k != r) st16_wt(slab_rsrc(a.base[k] + rowS + static_cast<int64_t>(r) * slot), static_cast<uint32_t>(i * 16), v);
+        }
       }
     }
     ps.mark(6);

@@ -215,3 +215,39 @@ def test_threshold_needs_a_lag_ring():
     xs = [torch.zeros(1024, device=DEV) for _ in range(2)]
     with pytest.raises(Exception, match="threshold_rows"):
         cl.allreduce_threshold(xs)
+
+
+_ONESHOT_GRID_CHILD = r"""
+import torch
+from akka_allreduce_1_amd.ops import fill_uniform
+from akka_allreduce_1_amd.parallel import LocalCluster
+dev = torch.device("cuda", 0)
+P, n = 8, 64 * 1024  # 128 KiB bf16 per rank
+cl = LocalCluster(P, slot_bytes=(1 << 20), grid=64, timeout_s=5.0, max_lag=1)
+xs = [fill_uniform(torch.empty(n, dtype=torch.bfloat16, device=dev), seed=k) for k in range(P)]
+ys = [torch.empty_like(x) for x in xs]
+ref = sum(x.float() for x in xs)
+for _ in range(3):
+    cl.allreduce_threshold(xs, ys, counts=False)
+    torch.cuda.synchronize()
+    cl.check()
+    err = max((y.float() - ref).abs().max().item() for y in ys)
+    assert err <= ref.abs().max().item() * 2 ** -7, err
+print("ok")
+"""
+
+
+def test_oneshot_body_workgroups_past_the_fast_pass():
+    """The threshold kernel's one-shot body where the grid is too small for every workgroup's
+    fast pass (default grid 64, 8 x 128 KiB, the body allowed up to 256 KiB): its chunk-by-chunk
+    form timed out there, so the host now takes the two-shot body for such geometries - the
+    rounds must complete exact (profiles/round6 section 12). A child process, so the
+    construction-time knobs apply to it alone."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, MXAR_GRID="64", MXAR_STUDY="1", MXAR_TH_ONESHOT_MAX=str(256 << 10))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _ONESHOT_GRID_CHILD], env=env, cwd=root, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
