@@ -1367,11 +1367,12 @@ bool XgmiComm::threshold_args(const std::vector<XgmiComm*>& group, const std::ve
       const int64_t upc = ceil_div(std::min(a.chunk, a.block) * es, 8) + 1;  // units of one chunk at most
       const int64_t cpw = std::max<int64_t>(1, kCommThreads / upc);
       const int64_t need = ceil_div(static_cast<int64_t>(W) * a.nch, cpw);
-      // only where every workgroup's chunks fit its fast pass (one unit per thread): a grid too
-      // small for that (a small default grid, a CU-limited communicator) or chunks of more than
-      // kCommThreads units take the two-shot body - the one-shot body's chunk-by-chunk form
-      // timed out there (MXAR_GRID=64, 8 x 128 KiB; profiles/round6 section 12)
-      if (need > cap || upc > kCommThreads)
+      // only where the grid holds a workgroup for each of those groups: a grid too small for
+      // that (a small default grid, a shared launch's cap) left workgroups walking several
+      // chunks chunk by chunk, which timed out (MXAR_GRID=64, 8 x 128 KiB; profiles/round6
+      // section 12). One chunk of more than kCommThreads units per workgroup stays one-shot
+      // (every workgroup walks its one chunk: the plane's coarsened forced rounds, T13).
+      if (need > cap)
         a.oneshot = 0;
       else
         gx = static_cast<int>(need);
