@@ -469,11 +469,11 @@ class XgmiComm {
   bool noguard_ = false;           // MXAR_SLOT_GUARD=0 (study / negative control only)
   bool no_gate_shortcut_ = false;  // MXAR_STUDY=1 MXAR_GATE_SHORTCUT=0: threshold lag gate always polled (A/B)
   // full-threshold rounds of at most this many bytes per rank run the one-shot body
-  // (xgmi_threshold.hip; MXAR_STUDY=1 MXAR_TH_ONESHOT_MAX=bytes, 0 = off). 32 KiB: larger
-  // bodies measured 1.1-1.8x faster at 64-256 KiB in one launch, but the 2- and 4-process
-  // stress tests (tests/test_ddp_gpu.py, test_coll_gpu.py random operations) failed with them
-  // at 64 KiB - wrong sums and a scatter timeout, cause open (profiles/round6 section 12)
-  int64_t th_oneshot_max_ = 32 << 10;
+  // (xgmi_threshold.hip; MXAR_STUDY=1 MXAR_TH_ONESHOT_MAX=bytes, 0 = off): 1.1-1.8x faster
+  // than the two-shot body at 64-256 KiB (profiles/round6 section 12). The multi-process
+  // failures of a first 256 KiB default came from workgroups past the fast pass; the host now
+  // sizes the grid for it or takes the two-shot body (threshold_args)
+  int64_t th_oneshot_max_ = 256 << 10;
   bool ring_hop_rows_ = false;     // negative control: the two-writer ring flag layout (MXAR_RING_FLAGS=hop)
   int geom_ = -1;                  // two-shot geometry: -1 by block size, 0 coarse, 1 fine, 2 flat (MXAR_TWOSHOT_GEOM)
   int64_t flat_min_ = int64_t{2} << 20;  // blocks of at least this many bytes use the flat geometry (MXAR_TWOSHOT_FLAT_MIN)

@@ -251,3 +251,23 @@ def test_oneshot_body_workgroups_past_the_fast_pass():
     r = subprocess.run([sys.executable, "-c", _ONESHOT_GRID_CHILD], env=env, cwd=root, capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_threshold_body_transitions_round_to_round():
+    """Threshold rounds whose body changes from call to call on ONE cluster: one-shot (16 KiB,
+    64 KiB), one-shot or two-shot by the grid guard (256 KiB at grid 64: 8 ranks share the
+    launch), two-shot (512 KiB), then one-shot again - the rows, tags and flags each body leaves
+    behind must not leak into the next (profiles/round6 section 12). Every round exact."""
+    P = 8
+    cl = LocalCluster(P, slot_bytes=1 << 20, grid=64, timeout_s=5.0, max_lag=1)
+    for rep, S in enumerate([16 << 10, 64 << 10, 256 << 10, 512 << 10, 64 << 10, 16 << 10]):
+        n = S // 2
+        xs = [fill_uniform(torch.empty(n, dtype=torch.bfloat16, device=DEV), seed=k + 31 * rep) for k in range(P)]
+        ys = [torch.empty_like(x) for x in xs]
+        ref = sum(x.float() for x in xs)
+        for _ in range(3):
+            cl.allreduce_threshold(xs, ys, counts=False)
+            torch.cuda.synchronize()
+            cl.check()
+            err = max((y.float() - ref).abs().max().item() for y in ys)
+            assert err <= ref.abs().max().item() * 2 ** -7, (S, err)
